@@ -1,0 +1,399 @@
+// pybind11 module `_gpuexp`: the Python control plane drives the C++ data plane through
+// this surface.  Python never runs on the sample or scrape path.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cmath>
+
+#include "gpuexp/backends.h"
+#include "gpuexp/client.h"
+#include "gpuexp/engine.h"
+#include "gpuexp/exposition.h"
+#include "gpuexp/gpu_metrics.h"
+#include "gpuexp/procs.h"
+#include "gpuexp/snapshot.h"
+
+namespace py = pybind11;
+using namespace gpuexp;
+
+void register_kernels(py::module_& m);  // kernels_bindings.cc (HIP workload kernels)
+
+namespace {
+
+py::dict cgroup_dict(const CgroupInfo& c, bool ok) {
+  py::dict d;
+  d["kube"] = ok && c.kube;
+  d["pod_uid"] = c.pod_uid;
+  d["container_id"] = c.container_id;
+  d["runtime"] = c.runtime;
+  d["qos"] = c.qos;
+  d["path"] = c.path;
+  return d;
+}
+
+py::dict device_dict(const DeviceInfo& d) {
+  py::dict o;
+  o["index"] = d.index;
+  o["uuid"] = d.uuid;
+  o["bdf"] = d.bdf;
+  o["name"] = d.name;
+  o["kfd_gpu_id"] = d.kfd_gpu_id;
+  o["render_minor"] = d.render_minor;
+  o["hip_id"] = d.hip_id;
+  o["vram_total"] = d.vram_total;
+  o["num_xcc"] = d.num_xcc;
+  o["num_cu"] = d.num_cu;
+  py::list peers;
+  for (int l = 0; l < kMaxXgmiLinks; ++l) peers.append(d.xgmi_peer_bdf[l]);
+  o["xgmi_peers"] = peers;
+  return o;
+}
+
+py::dict sample_dict(const DeviceSample& s) {
+  py::dict o;
+  o["ok"] = s.ok;
+  o["error"] = s.error;
+  o["gfx_activity"] = s.gfx_activity;
+  o["umc_activity"] = s.umc_activity;
+  o["vram_used"] = s.vram_used;
+  o["power_w"] = s.power_w;
+  o["energy_acc"] = s.energy_acc;
+  o["temp_hotspot"] = s.temp_hotspot;
+  o["temp_mem"] = s.temp_mem;
+  o["temp_vrsoc"] = s.temp_vrsoc;
+  o["clk_gfx"] = s.clk_gfx;
+  o["clk_soc"] = s.clk_soc;
+  o["clk_mem"] = s.clk_mem;
+  o["num_xgmi_links"] = s.num_xgmi_links;
+  py::list rd, wr, up;
+  for (int l = 0; l < kMaxXgmiLinks; ++l) {
+    rd.append(s.xgmi_read_kb[l]);
+    wr.append(s.xgmi_write_kb[l]);
+    up.append(s.xgmi_link_up[l]);
+  }
+  o["xgmi_read_kb"] = rd;
+  o["xgmi_write_kb"] = wr;
+  o["xgmi_link_up"] = up;
+  o["pcie_width"] = s.pcie_width;
+  o["pcie_speed_gts"] = s.pcie_speed_gts;
+  o["pcie_bw_inst"] = s.pcie_bw_inst;
+  o["fw_ts_10ns"] = s.fw_ts_10ns;
+  o["accumulation_counter"] = s.accumulation_counter;
+  o["res_ppt"] = s.res_ppt;
+  o["vram_max_bw_gbs"] = s.vram_max_bw_gbs;
+  py::list busy;
+  for (int c = 0; c < kMaxXcc; ++c) busy.append(s.gfx_busy_acc[c]);
+  o["gfx_busy_acc"] = busy;
+  return o;
+}
+
+ProcSample proc_from_dict(const py::dict& d) {
+  ProcSample p;
+  p.pid = d["pid"].cast<int>();
+  p.vram_bytes = d.contains("vram_bytes") ? d["vram_bytes"].cast<double>() : 0.0;
+  p.cu_occupancy = d.contains("cu_occupancy") ? d["cu_occupancy"].cast<double>() : kNaN;
+  p.sdma_us = d.contains("sdma_us") ? d["sdma_us"].cast<double>() : kNaN;
+  p.name = d.contains("name") ? d["name"].cast<std::string>() : "";
+  return p;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_gpuexp, m) {
+  m.doc() = "MI355X per-pod GPU exporter: native telemetry core";
+
+  m.def("mono_ns", &mono_ns);
+  m.def("set_log_level", [](int lvl) { set_log_level(static_cast<LogLevel>(lvl)); });
+  m.def("format_value", [](double v) {
+    std::string s;
+    append_value(&s, v);
+    return s;
+  });
+  m.def("escape_label_value", [](const std::string& v) {
+    std::string s;
+    append_escaped_label_value(&s, v);
+    return s;
+  });
+  m.def("gzip", [](py::bytes b, int level) {
+    std::string in = b, out;
+    if (!gzip_compress(in, &out, level)) throw std::runtime_error("gzip failed");
+    return py::bytes(out);
+  }, py::arg("data"), py::arg("level") = 1);
+  m.def("parse_cgroup_path", [](const std::string& p) {
+    CgroupInfo c;
+    bool ok = parse_kube_cgroup_path(p, &c);
+    return cgroup_dict(c, ok);
+  });
+  m.def("parse_proc_cgroup", [](const std::string& content) {
+    CgroupInfo c;
+    bool ok = parse_proc_cgroup(content, &c);
+    return cgroup_dict(c, ok);
+  });
+  m.def("decode_gpu_metrics", [](py::bytes blob) -> py::object {
+    std::string b = blob;
+    DeviceSample s;
+    if (!decode_gpu_metrics_v1_8(b.data(), b.size(), &s)) return py::none();
+    s.ok = true;
+    return sample_dict(s);
+  });
+  m.def("gpu_metrics_v1_8_size", []() { return sizeof(GpuMetricsV1_8); });
+  m.def("uuid_from_unique_id", &SysfsBackend::uuid_from_unique_id);
+  m.def("read_backend", [](const std::string& backend, const std::string& host_root, int ndev) {
+    // One-shot enumerate + sample (diagnostics / tests).
+    std::unique_ptr<Backend> b;
+    if (backend == "sysfs") b = std::make_unique<SysfsBackend>(host_root);
+    else if (backend == "amdsmi") b = make_amdsmi_backend(host_root, true, false);
+    else b = std::make_unique<MockBackend>(ndev);
+    std::vector<DeviceInfo> devs;
+    std::string err;
+    py::list out;
+    bool ok;
+    {
+      py::gil_scoped_release rel;
+      ok = b->init(&devs, &err);
+    }
+    if (!ok) throw std::runtime_error(err);
+    for (auto& d : devs) {
+      DeviceSample s;
+      s.host_ns = mono_ns();
+      b->sample(d, &s);
+      py::dict e = device_dict(d);
+      e["sample"] = sample_dict(s);
+      std::vector<ProcSample> procs;
+      py::list pl;
+      if (b->processes(d, &procs))
+        for (auto& p : procs) {
+          py::dict pd;
+          pd["pid"] = p.pid;
+          pd["vram_bytes"] = p.vram_bytes;
+          pd["cu_occupancy"] = p.cu_occupancy;
+          pd["name"] = p.name;
+          pl.append(pd);
+        }
+      e["processes"] = pl;
+      out.append(e);
+    }
+    b->shutdown();
+    return out;
+  }, py::arg("backend"), py::arg("host_root") = "", py::arg("ndev") = 1);
+  m.def("scan_kfd", [](const std::string& host_root, std::vector<uint32_t> gpu_ids, int self_pid) {
+    std::vector<DeviceInfo> devs;
+    for (size_t i = 0; i < gpu_ids.size(); ++i) {
+      DeviceInfo d;
+      d.index = int(i);
+      d.kfd_gpu_id = gpu_ids[i];
+      devs.push_back(d);
+    }
+    KfdProcReader r(host_root, self_pid, true);
+    std::vector<std::vector<ProcSample>> per;
+    r.scan(devs, &per);
+    py::list out;
+    for (auto& l : per) {
+      py::list dl;
+      for (auto& p : l) {
+        py::dict pd;
+        pd["pid"] = p.pid;
+        pd["vram_bytes"] = p.vram_bytes;
+        pd["cu_occupancy"] = p.cu_occupancy;
+        pd["sdma_us"] = p.sdma_us;
+        pd["name"] = p.name;
+        dl.append(pd);
+      }
+      out.append(dl);
+    }
+    return out;
+  }, py::arg("host_root"), py::arg("gpu_ids"), py::arg("self_pid") = -1);
+
+  m.def("scrape_loop", [](const std::string& host, int port, const std::string& path, double hz, int count,
+                          bool gzip, bool keepalive, int timeout_ms, bool keep_last_body) {
+    ScrapeResult r;
+    {
+      py::gil_scoped_release rel;
+      r = scrape_loop(host, port, path, hz, count, gzip, keepalive, timeout_ms, keep_last_body);
+    }
+    py::dict d;
+    d["latency_ns"] = r.latency_ns;
+    d["bytes"] = r.bytes;
+    d["errors"] = r.errors;
+    d["non200"] = r.non200;
+    d["wall_s"] = r.wall_s;
+    d["last_body"] = py::bytes(r.last_body);
+    return d;
+  }, py::arg("host"), py::arg("port"), py::arg("path") = "/metrics", py::arg("hz") = 10.0,
+     py::arg("count") = 100, py::arg("gzip") = false, py::arg("keepalive") = true,
+     py::arg("timeout_ms") = 5000, py::arg("keep_last_body") = false);
+
+  // --- SeriesTable (unit tests of the exposition layer) ---
+  py::enum_<MetricType>(m, "MetricType")
+      .value("gauge", MetricType::kGauge)
+      .value("counter", MetricType::kCounter)
+      .value("histogram", MetricType::kHistogram);
+  py::class_<SeriesTable>(m, "SeriesTable")
+      .def(py::init<>())
+      .def("add_family", [](SeriesTable& t, const std::string& name, const std::string& help, MetricType type,
+                            std::vector<std::string> labels) {
+        return t.add_family(FamilyDef{name, help, type, std::move(labels)});
+      })
+      .def("put", &SeriesTable::put)
+      .def("observe", [](SeriesTable& t, int fid, std::vector<std::string> labels, double v, uint64_t gen,
+                         std::vector<double> bounds) {
+        t.observe(t.upsert(fid, labels), v, gen, bounds);
+      })
+      .def("render", [](SeriesTable& t, uint64_t gen, uint64_t gc_after) {
+        std::string out;
+        t.render(&out, gen, gc_after);
+        return out;
+      }, py::arg("gen"), py::arg("gc_after") = 1)
+      .def("live_series", &SeriesTable::live_series);
+
+  // --- Engine ---
+  py::class_<HttpConfig>(m, "HttpConfig")
+      .def(py::init<>())
+      .def_readwrite("host", &HttpConfig::host)
+      .def_readwrite("port", &HttpConfig::port)
+      .def_readwrite("metrics_path", &HttpConfig::metrics_path)
+      .def_readwrite("threads", &HttpConfig::threads)
+      .def_readwrite("max_conns", &HttpConfig::max_conns)
+      .def_readwrite("idle_timeout_ms", &HttpConfig::idle_timeout_ms)
+      .def_readwrite("enable_gzip", &HttpConfig::enable_gzip);
+
+  py::class_<EngineConfig>(m, "EngineConfig")
+      .def(py::init<>())
+      .def_readwrite("backend", &EngineConfig::backend)
+      .def_readwrite("mock_devices", &EngineConfig::mock_devices)
+      .def_readwrite("host_root", &EngineConfig::host_root)
+      .def_readwrite("interval_s", &EngineConfig::interval_s)
+      .def_readwrite("serve_http", &EngineConfig::serve_http)
+      .def_readwrite("http", &EngineConfig::http)
+      .def_readwrite("series_profile", &EngineConfig::series_profile)
+      .def_readwrite("legacy_families", &EngineConfig::legacy_families)
+      .def_readwrite("pod_attribution", &EngineConfig::pod_attribution)
+      .def_readwrite("infer_device_owner", &EngineConfig::infer_device_owner)
+      .def_readwrite("process_source", &EngineConfig::process_source)
+      .def_readwrite("kfd_cu_occupancy", &EngineConfig::kfd_cu_occupancy)
+      .def_readwrite("exclude_self", &EngineConfig::exclude_self)
+      .def_readwrite("enable_sentinel", &EngineConfig::enable_sentinel)
+      .def_readwrite("sentinel_ring", &EngineConfig::sentinel_ring)
+      .def_readwrite("sentinel_spin", &EngineConfig::sentinel_spin)
+      .def_readwrite("enable_counters", &EngineConfig::enable_counters)
+      .def_readwrite("counters_plugin", &EngineConfig::counters_plugin)
+      .def_readwrite("enable_rccl", &EngineConfig::enable_rccl)
+      .def_readwrite("rccl_dir", &EngineConfig::rccl_dir)
+      .def_readwrite("force_amdsmi_metrics", &EngineConfig::force_amdsmi_metrics)
+      .def_readwrite("gzip_level", &EngineConfig::gzip_level)
+      .def_readwrite("gc_after", &EngineConfig::gc_after)
+      .def_readwrite("device_filter", &EngineConfig::device_filter)
+      .def_readwrite("trace_path", &EngineConfig::trace_path)
+      .def_readwrite("trace_max_events", &EngineConfig::trace_max_events)
+      .def_readwrite("version", &EngineConfig::version);
+
+  py::class_<Engine>(m, "Engine")
+      .def(py::init<const EngineConfig&>())
+      .def("start", [](Engine& e) {
+        std::string err;
+        bool ok;
+        {
+          py::gil_scoped_release rel;
+          ok = e.start(&err);
+        }
+        if (!ok) throw std::runtime_error("engine start failed: " + err);
+      })
+      .def("stop", [](Engine& e) {
+        py::gil_scoped_release rel;
+        e.stop();
+      })
+      .def("tick", [](Engine& e, py::object now_ns) {
+        uint64_t t = now_ns.is_none() ? mono_ns() : now_ns.cast<uint64_t>();
+        py::gil_scoped_release rel;
+        e.tick_now(t);
+      }, py::arg("now_ns") = py::none())
+      .def("snapshot_text", [](Engine& e) {
+        std::string s;
+        {
+          py::gil_scoped_release rel;
+          s = e.snapshot_text();
+        }
+        return s;
+      })
+      .def_property_readonly("http_port", &Engine::http_port)
+      .def("devices", [](Engine& e) {
+        py::list l;
+        for (auto& d : e.devices()) l.append(device_dict(d));
+        return l;
+      })
+      .def("stats", [](Engine& e) {
+        EngineStats s = e.stats();
+        py::dict d;
+        d["ticks"] = s.ticks;
+        d["overruns"] = s.overruns;
+        d["publish_skipped"] = s.publish_skipped;
+        d["last_tick_ns"] = s.last_tick_ns;
+        d["max_tick_ns"] = s.max_tick_ns;
+        d["render_bytes"] = s.render_bytes;
+        d["series"] = s.series;
+        d["device_errors"] = s.device_errors;
+        d["sampler_cpu_ns"] = s.sampler_cpu_ns;
+        py::dict st;
+        for (int k = 0; k < Engine::kStages; ++k) st[Engine::stage_name(k)] = s.stage_ns[k];
+        d["stage_ns"] = st;
+        if (const HttpStats* hs = e.http_stats()) {
+          d["http_requests"] = hs->requests.load();
+          d["http_metrics_requests"] = hs->metrics_requests.load();
+          d["http_gzip_responses"] = hs->gzip_responses.load();
+          d["http_bytes"] = hs->bytes_sent.load();
+          d["http_errors"] = hs->errors.load();
+          d["http_open_conns"] = hs->open_conns.load();
+        }
+        return d;
+      })
+      .def("source_status", &Engine::source_status)
+      .def("set_pods", [](Engine& e, py::list pods) {
+        std::vector<PodMeta> v;
+        for (auto item : pods) {
+          py::dict d = item.cast<py::dict>();
+          PodMeta p;
+          p.uid = d["uid"].cast<std::string>();
+          p.ns = d["namespace"].cast<std::string>();
+          p.name = d["name"].cast<std::string>();
+          if (d.contains("containers"))
+            for (auto kv : d["containers"].cast<py::dict>())
+              p.containers.emplace_back(kv.first.cast<std::string>(), kv.second.cast<std::string>());
+          v.push_back(std::move(p));
+        }
+        e.set_pods(std::move(v));
+      })
+      .def("set_device_owners", [](Engine& e, py::dict owners) {
+        std::vector<std::pair<std::string, DeviceOwner>> v;
+        for (auto kv : owners) {
+          py::dict o = kv.second.cast<py::dict>();
+          DeviceOwner d;
+          d.ns = o.contains("namespace") ? o["namespace"].cast<std::string>() : "";
+          d.pod = o.contains("pod") ? o["pod"].cast<std::string>() : "";
+          d.container = o.contains("container") ? o["container"].cast<std::string>() : "";
+          v.emplace_back(kv.first.cast<std::string>(), d);
+        }
+        e.set_device_owners(std::move(v));
+      })
+      .def("set_pid_cgroup", &Engine::set_pid_cgroup)
+      .def("clear_pid_cgroups", &Engine::clear_pid_cgroups)
+      .def("mock_set_value", [](Engine& e, int dev, const std::string& field, double v) {
+        if (!e.mock()) throw std::runtime_error("not a mock backend");
+        e.mock()->set_value(dev, field, v);
+      })
+      .def("mock_set_processes", [](Engine& e, int dev, py::list procs) {
+        if (!e.mock()) throw std::runtime_error("not a mock backend");
+        std::vector<ProcSample> v;
+        for (auto item : procs) v.push_back(proc_from_dict(item.cast<py::dict>()));
+        e.mock()->set_processes(dev, v);
+      })
+      .def("mock_clear_processes", [](Engine& e) {
+        if (!e.mock()) throw std::runtime_error("not a mock backend");
+        e.mock()->clear_processes();
+      })
+      .def("mock_set_fault", [](Engine& e, int dev, const std::string& fault) {
+        if (!e.mock()) throw std::runtime_error("not a mock backend");
+        e.mock()->set_fault(dev, fault);
+      });
+
+  register_kernels(m);
+}

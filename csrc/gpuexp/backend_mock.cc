@@ -1,0 +1,205 @@
+// Mock GPU backend (BASELINE config 1: "mock-GPU backend on CPU, 1 fake device").
+// Values are smooth deterministic functions of the injected sample time, so tests can
+// assert exact rates; every field can be pinned and faults injected from Python.
+#include <cmath>
+#include <cstdio>
+
+#include "gpuexp/backends.h"
+
+namespace gpuexp {
+
+MockBackend::MockBackend(int num_devices, uint32_t kfd_id_base)
+    : n_(num_devices), kfd_base_(kfd_id_base), scripts_(size_t(num_devices > 0 ? num_devices : 0)) {}
+
+bool MockBackend::init(std::vector<DeviceInfo>* devices, std::string* err) {
+  if (n_ <= 0) {
+    *err = "mock backend needs >= 1 device";
+    return false;
+  }
+  devices->clear();
+  for (int i = 0; i < n_; ++i) {
+    DeviceInfo d;
+    d.index = i;
+    char buf[64];
+    std::snprintf(buf, sizeof(buf), "0000:%02x:00.0", 0x10 + 0x10 * i);
+    d.bdf = buf;
+    std::snprintf(buf, sizeof(buf), "e2ff75a3-0000-1000-80%02x-00000000%04x", i, 0xa000 + i);
+    d.uuid = buf;
+    d.name = "AMD Instinct MI355X (mock)";
+    d.kfd_gpu_id = kfd_base_ + uint32_t(i);
+    d.render_minor = 128 + i;
+    d.card = i;
+    d.hip_id = i;
+    d.vram_total = 309220868096ull;  // measured MI355X mem_info_vram_total
+    d.num_xcc = 8;
+    d.num_cu = 256;
+    // Fully connected 8-GPU OAM mesh: link 0 unsupported, links 1..7 to peers.
+    for (int l = 1; l < kMaxXgmiLinks; ++l) {
+      int peer = (i + l) % 8;
+      std::snprintf(buf, sizeof(buf), "0000:%02x:00.0", 0x10 + 0x10 * peer);
+      d.xgmi_peer_bdf[l] = buf;
+    }
+    devices->push_back(d);
+  }
+  return true;
+}
+
+double MockBackend::get(const Script& s, const char* field, double dflt) const {
+  auto it = s.overrides.find(field);
+  return it == s.overrides.end() ? dflt : it->second;
+}
+
+void MockBackend::sample(const DeviceInfo& dev, DeviceSample* out) {
+  std::lock_guard<std::mutex> lk(mu_);
+  Script& s = scripts_[size_t(dev.index)];
+  uint64_t now = out->host_ns;
+  if (s.fault == "error" || s.fault == "vanish") {
+    out->ok = false;
+    out->error = s.fault == "vanish" ? "device vanished" : "AMDSMI_STATUS_DRM_ERROR (injected)";
+    return;
+  }
+  double dt = s.started && now > s.last_ns ? double(now - s.last_ns) * 1e-9 : 0.0;
+  s.started = true;
+  s.last_ns = now;
+  double t = double(now) * 1e-9;
+  double ph = 0.7 * dev.index;
+
+  out->ok = true;
+  out->fw_ts_10ns = now / 10;
+  out->gfx_activity = get(s, "gfx_activity", std::round(50 + 45 * std::sin(0.5 * t + ph)));
+  out->umc_activity = get(s, "umc_activity", std::round(30 + 25 * std::sin(0.3 * t + ph)));
+  out->vram_total = double(dev.vram_total);
+  out->vram_used = get(s, "vram_used", 297766912.0 + 1e9 * dev.index);
+  out->power_w = get(s, "power_w", std::round(600 + 300 * std::sin(0.2 * t + ph)));
+  out->power_cap_w = get(s, "power_cap_w", 1400);
+  out->temp_hotspot = get(s, "temp_hotspot", std::round(55 + 10 * std::sin(0.1 * t + ph)));
+  out->temp_mem = get(s, "temp_mem", std::round(45 + 5 * std::sin(0.1 * t + ph)));
+  out->temp_vrsoc = get(s, "temp_vrsoc", 41);
+  out->clk_gfx = get(s, "clk_gfx", 2100);
+  out->clk_soc = get(s, "clk_soc", 1000);
+  out->clk_mem = get(s, "clk_mem", 2000);
+  out->pcie_width = 16;
+  out->pcie_speed_gts = 32;
+  out->pcie_bw_inst = get(s, "pcie_bw_gbs", 18);
+  out->pcie_replay = 0;
+  out->vram_max_bw_gbs = 8192;
+
+  // Integrate accumulators with the scripted rates.
+  s.energy_units += out->power_w * dt / 15.259e-6;
+  double rd_rate = get(s, "xgmi_read_rate_kbps", 1000.0);   // per link
+  double wr_rate = get(s, "xgmi_write_rate_kbps", 1000.0);
+  for (int l = 1; l < kMaxXgmiLinks; ++l) {
+    double r = s.xgmi_frac[0][l] + rd_rate * dt, w = s.xgmi_frac[1][l] + wr_rate * dt;
+    s.xgmi_rd_kb[l] += uint64_t(r);
+    s.xgmi_wr_kb[l] += uint64_t(w);
+    s.xgmi_frac[0][l] = r - std::floor(r);
+    s.xgmi_frac[1][l] = w - std::floor(w);
+  }
+  s.accum += dt * 1000.0;  // accumulation counter ticks at 1 kHz in the mock
+  for (int c = 0; c < kMaxXcc; ++c) s.busy_acc[c] += out->gfx_activity * dt * 1000.0;
+  s.res_ppt += get(s, "ppt_residency_percent", 0.0) / 100.0 * dt * 1000.0;
+  s.pcie_acc += out->pcie_bw_inst * dt;
+
+  if (s.fault == "counter_reset") {
+    s.energy_units = 0;
+    for (int l = 0; l < kMaxXgmiLinks; ++l) s.xgmi_rd_kb[l] = s.xgmi_wr_kb[l] = 0;
+    s.fault = "none";
+  } else if (s.fault == "wrap") {
+    for (int l = 0; l < kMaxXgmiLinks; ++l) s.xgmi_rd_kb[l] = ~uint64_t(0) - 100;
+    s.fault = "none";
+  }
+
+  out->energy_valid = true;
+  out->energy_acc = uint64_t(s.energy_units);
+  out->energy_unit_j = 15.259e-6;
+  out->num_xgmi_links = kMaxXgmiLinks;
+  out->xgmi_valid = true;
+  out->xgmi_link_up[0] = kNaN;
+  for (int l = 1; l < kMaxXgmiLinks; ++l) {
+    out->xgmi_read_kb[l] = s.xgmi_rd_kb[l];
+    out->xgmi_write_kb[l] = s.xgmi_wr_kb[l];
+    out->xgmi_link_up[l] = 1;
+  }
+  out->residency_valid = true;
+  out->accumulation_counter = uint64_t(s.accum);
+  out->res_ppt = uint64_t(s.res_ppt);
+  out->pcie_bw_acc = uint64_t(s.pcie_acc);
+  for (int c = 0; c < kMaxXcc; ++c) out->gfx_busy_acc[c] = uint64_t(s.busy_acc[c]);
+}
+
+bool MockBackend::processes(const DeviceInfo& dev, std::vector<ProcSample>* out) {
+  std::lock_guard<std::mutex> lk(mu_);
+  bool any = false;
+  for (auto& s : scripts_) any = any || s.has_procs;
+  if (!any) return false;
+  out->clear();
+  const Script& s = scripts_[size_t(dev.index)];
+  if (s.fault == "error" || s.fault == "vanish") return true;
+  for (auto p : s.procs) {
+    p.device = dev.index;
+    out->push_back(p);
+  }
+  return true;
+}
+
+bool MockBackend::counters(const DeviceInfo& dev, double dt_s, CounterReading* out) {
+  std::lock_guard<std::mutex> lk(mu_);
+  const Script& s = scripts_[size_t(dev.index)];
+  if (s.fault == "error" || s.fault == "vanish") return false;
+  double busy = get(s, "gfx_activity", 50);
+  out->ok = true;
+  out->gui_active_pct = get(s, "gui_active_pct", busy);
+  out->sq_busy_pct = get(s, "sq_busy_pct", busy * 0.95);
+  out->mfma_busy_pct = get(s, "mfma_busy_pct", busy * 0.6);
+  out->waves_per_s = get(s, "waves_per_s", 1e6 * busy);
+  out->lds_active_pct = get(s, "lds_active_pct", busy * 0.3);
+  out->lds_bank_conflict_pct = get(s, "lds_bank_conflict_pct", 1.5);
+  out->hbm_read_bps = get(s, "hbm_read_bps", 4e12 * busy / 100);
+  out->hbm_write_bps = get(s, "hbm_write_bps", 1e12 * busy / 100);
+  (void)dt_s;
+  return true;
+}
+
+bool MockBackend::sentinel(const DeviceInfo& dev, SentinelReading* out) {
+  std::lock_guard<std::mutex> lk(mu_);
+  const Script& s = scripts_[size_t(dev.index)];
+  if (s.fault == "error" || s.fault == "vanish") return false;
+  out->ok = true;
+  out->sclk_hz = get(s, "sentinel_sclk_hz", 2.1e9);
+  out->dispatch_latency_s = get(s, "sentinel_latency_s", 8e-6);
+  out->xcc_id = double(dev.index % 8);
+  out->runs = s.started ? uint64_t(s.accum) : 0;
+  return true;
+}
+
+void MockBackend::set_value(int dev, const std::string& field, double v) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (dev < 0 || dev >= n_) return;
+  if (std::isnan(v))
+    scripts_[size_t(dev)].overrides.erase(field);
+  else
+    scripts_[size_t(dev)].overrides[field] = v;
+}
+
+void MockBackend::set_processes(int dev, const std::vector<ProcSample>& procs) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (dev < 0 || dev >= n_) return;
+  scripts_[size_t(dev)].procs = procs;
+  for (auto& s : scripts_) s.has_procs = true;
+}
+
+void MockBackend::clear_processes() {
+  std::lock_guard<std::mutex> lk(mu_);
+  for (auto& s : scripts_) {
+    s.procs.clear();
+    s.has_procs = false;
+  }
+}
+
+void MockBackend::set_fault(int dev, const std::string& fault) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (dev < 0 || dev >= n_) return;
+  scripts_[size_t(dev)].fault = fault;
+}
+
+}  // namespace gpuexp

@@ -1,0 +1,201 @@
+// sysfs backend: KFD topology for identity, drm sysfs + raw gpu_metrics for telemetry.
+// Every path is prefixed with the host root, so tests build a fake tree (SURVEY.md §4.2
+// "fake sysfs/procfs root") and a DaemonSet mounts the host's /sys read-only.
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstdio>
+#include <cstdlib>
+#include <sstream>
+
+#include "gpuexp/backends.h"
+
+namespace gpuexp {
+
+CachedFile::~CachedFile() { close(); }
+
+CachedFile& CachedFile::operator=(CachedFile&& o) noexcept {
+  close();
+  fd_ = o.fd_;
+  path_ = std::move(o.path_);
+  o.fd_ = -1;
+  return *this;
+}
+
+bool CachedFile::open(const std::string& path) {
+  close();
+  path_ = path;
+  fd_ = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  return fd_ >= 0;
+}
+
+long CachedFile::read(char* buf, size_t cap) {
+  if (fd_ < 0) return -1;
+  return pread_all(fd_, buf, cap);
+}
+
+bool CachedFile::read_u64(uint64_t* v) {
+  char buf[64];
+  long n = read(buf, sizeof(buf) - 1);
+  if (n <= 0) return false;
+  return parse_u64(buf, size_t(n), v);
+}
+
+void CachedFile::close() {
+  if (fd_ >= 0) ::close(fd_);
+  fd_ = -1;
+}
+
+// Parses "key value\n" lines of a KFD topology `properties` file.
+static std::map<std::string, uint64_t> parse_properties(const std::string& text) {
+  std::map<std::string, uint64_t> kv;
+  std::istringstream is(text);
+  std::string k;
+  std::string v;
+  while (is >> k >> v) {
+    uint64_t x = 0;
+    if (parse_u64(v.c_str(), v.size(), &x)) kv[k] = x;
+  }
+  return kv;
+}
+
+std::string SysfsBackend::uuid_from_unique_id(uint64_t unique_id, uint32_t device_id) {
+  // amdsmi format: <b0>ff<devid16>-0000-1000-80<b1>-<b2..b7>, where b0..b7 are the
+  // big-endian bytes of the KFD unique_id (checked against amdsmi on MI355X:
+  // unique_id e296a367fef9a1be, device 0x75a3 -> e2ff75a3-0000-1000-8096-a367fef9a1be).
+  char hex[17];
+  std::snprintf(hex, sizeof(hex), "%016llx", static_cast<unsigned long long>(unique_id));
+  char out[64];
+  std::snprintf(out, sizeof(out), "%.2sff%04x-0000-1000-80%.2s-%.12s", hex, device_id & 0xFFFF,
+                hex + 2, hex + 4);
+  return out;
+}
+
+SysfsBackend::SysfsBackend(std::string host_root) : root_(std::move(host_root)) {
+  if (!root_.empty() && root_.back() == '/') root_.pop_back();
+}
+
+bool SysfsBackend::init(std::vector<DeviceInfo>* devices, std::string* err) {
+  devices->clear();
+  devs_.clear();
+  std::string nodes_dir = root_ + "/sys/class/kfd/kfd/topology/nodes";
+  std::vector<std::string> nodes = list_dir(nodes_dir);
+  std::sort(nodes.begin(), nodes.end(), [](const std::string& a, const std::string& b) {
+    return std::atoi(a.c_str()) < std::atoi(b.c_str());
+  });
+  struct Found {
+    uint64_t bdf_sort;
+    DeviceInfo info;
+  };
+  std::vector<Found> found;
+  for (auto& n : nodes) {
+    uint64_t gpu_id = 0;
+    if (!read_u64_file(nodes_dir + "/" + n + "/gpu_id", &gpu_id) || gpu_id == 0) continue;
+    std::string props;
+    if (!read_small_file(nodes_dir + "/" + n + "/properties", &props)) continue;
+    auto kv = parse_properties(props);
+    DeviceInfo d;
+    d.kfd_gpu_id = uint32_t(gpu_id);
+    uint64_t loc = kv["location_id"], dom = kv["domain"];
+    char bdf[32];
+    std::snprintf(bdf, sizeof(bdf), "%04llx:%02llx:%02llx.%llx", (unsigned long long)dom,
+                  (unsigned long long)((loc >> 8) & 0xFF), (unsigned long long)((loc >> 3) & 0x1F),
+                  (unsigned long long)(loc & 0x7));
+    d.bdf = bdf;
+    d.render_minor = int(kv.count("drm_render_minor") ? kv["drm_render_minor"] : 0);
+    d.num_xcc = uint32_t(kv["num_xcc"]);
+    uint64_t cus = kv["simd_count"] && kv["simd_per_cu"] ? kv["simd_count"] / kv["simd_per_cu"] : 0;
+    d.num_cu = uint32_t(cus);
+    d.uuid = uuid_from_unique_id(kv["unique_id"], uint32_t(kv["device_id"]));
+    std::string name;
+    if (read_small_file(nodes_dir + "/" + n + "/name", &name)) d.name = trim(name);
+    found.push_back({(dom << 16) | (loc & 0xFFFF), d});
+  }
+  // Stable exporter index order = PCI order (what HIP/amdsmi enumerate by default).
+  std::sort(found.begin(), found.end(),
+            [](const Found& a, const Found& b) { return a.bdf_sort < b.bdf_sort; });
+  for (size_t i = 0; i < found.size(); ++i) {
+    DeviceInfo d = found[i].info;
+    d.index = int(i);
+    d.hip_id = int(i);
+    auto dev = std::make_unique<Dev>();
+    dev->dev_dir = root_ + "/sys/class/drm/renderD" + std::to_string(d.render_minor) + "/device";
+    uint64_t total = 0;
+    if (read_u64_file(dev->dev_dir + "/mem_info_vram_total", &total)) d.vram_total = total;
+    open_dev_files(dev.get());
+    devices->push_back(d);
+    devs_.push_back(std::move(dev));
+  }
+  if (devices->empty()) {
+    *err = "no KFD GPU nodes under " + nodes_dir;
+    return false;
+  }
+  return true;
+}
+
+void SysfsBackend::open_dev_files(Dev* d) {
+  std::string e;
+  d->gm_ok = d->gm.open(d->dev_dir + "/gpu_metrics", &e);
+  d->vram_used.open(d->dev_dir + "/mem_info_vram_used");
+  d->busy.open(d->dev_dir + "/gpu_busy_percent");
+  d->mem_busy.open(d->dev_dir + "/mem_busy_percent");
+  // hwmon: power1_input (uW), temp*_input with labels junction/mem/edge.
+  for (auto& h : list_dir(d->dev_dir + "/hwmon")) {
+    std::string hd = d->dev_dir + "/hwmon/" + h;
+    if (!d->power.open(hd + "/power1_input")) d->power.open(hd + "/power1_average");
+    uint64_t cap = 0;
+    if (read_u64_file(hd + "/power1_cap", &cap)) d->power_cap_w = double(cap) * 1e-6;
+    for (int t = 1; t <= 8; ++t) {
+      std::string label;
+      if (!read_small_file(hd + "/temp" + std::to_string(t) + "_label", &label)) continue;
+      label = trim(label);
+      std::string in = hd + "/temp" + std::to_string(t) + "_input";
+      if (label == "junction" || label == "hotspot") d->temp_hot.open(in);
+      else if (label == "mem") d->temp_mem.open(in);
+      else if (label == "edge") d->temp_edge.open(in);
+    }
+    break;
+  }
+}
+
+void SysfsBackend::sample_fallback(Dev& d, DeviceSample* out) {
+  uint64_t v = 0;
+  if (d.busy.read_u64(&v)) out->gfx_activity = double(v);
+  if (d.mem_busy.read_u64(&v)) out->umc_activity = double(v);
+  if (d.power.read_u64(&v)) out->power_w = double(v) * 1e-6;
+  if (d.temp_hot.read_u64(&v)) out->temp_hotspot = double(v) * 1e-3;
+  if (d.temp_mem.read_u64(&v)) out->temp_mem = double(v) * 1e-3;
+  if (d.temp_edge.read_u64(&v)) out->temp_edge = double(v) * 1e-3;
+}
+
+void SysfsBackend::sample(const DeviceInfo& dev, DeviceSample* out) {
+  Dev& d = *devs_.at(size_t(dev.index));
+  bool any = false;
+  if (d.gm_ok) {
+    if (d.gm.read(out)) {
+      any = true;
+    } else {
+      // The blob can vanish with the device (hot-unplug/reset): retry open once.
+      std::string e;
+      d.gm_ok = d.gm.open(d.dev_dir + "/gpu_metrics", &e) && d.gm.read(out);
+      any = d.gm_ok;
+    }
+  }
+  if (!any) sample_fallback(d, out);
+  uint64_t used = 0;
+  if (d.vram_used.read_u64(&used)) {
+    out->vram_used = double(used);
+    any = true;
+  } else if (d.vram_used.open(d.dev_dir + "/mem_info_vram_used") && d.vram_used.read_u64(&used)) {
+    out->vram_used = double(used);
+    any = true;
+  }
+  out->vram_total = double(dev.vram_total);
+  out->power_cap_w = d.power_cap_w;
+  out->ok = any || !std::isnan(out->gfx_activity) || !std::isnan(out->power_w);
+  if (!out->ok && out->error.empty()) out->error = "no readable telemetry under " + d.dev_dir;
+}
+
+}  // namespace gpuexp

@@ -1,0 +1,150 @@
+// Device identity + per-tick sample model and the backend interface.
+//
+// Reference: NVML DeviceGetCount / DeviceGetHandleByIndex / GetMemoryInfo /
+// GetComputeRunningProcesses, re-queried every cycle and fatal on any error
+// (/root/reference/main.go:116-138).  Here devices are enumerated ONCE (stable identity:
+// BDF, UUID, KFD gpu_id, render minor), and each tick fills a DeviceSample per GPU;
+// a failing GPU only marks itself down (amd_gpu_up=0) — no other GPU is affected.
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "gpuexp/common.h"
+
+namespace gpuexp {
+
+constexpr int kMaxXgmiLinks = 8;   // AMDSMI_MAX_NUM_XGMI_LINKS (amdsmi.h:118)
+constexpr int kMaxHbm = 4;         // AMDSMI_NUM_HBM_INSTANCES (amdsmi.h:97)
+constexpr int kMaxXcc = 8;         // AMDSMI_MAX_NUM_XCC (amdsmi.h:167)
+
+struct DeviceInfo {
+  int index = 0;              // exporter GPU index == `gpu` label
+  std::string uuid;
+  std::string bdf;            // "0000:72:00.0"
+  std::string name;           // marketing/asic name
+  uint32_t kfd_gpu_id = 0;    // /sys/class/kfd/kfd/proc/<pid>/vram_<gpu_id>
+  int render_minor = -1;      // /dev/dri/renderD<minor>
+  int card = -1;
+  int hip_id = -1;
+  uint64_t vram_total = 0;    // bytes (static)
+  uint32_t num_xcc = 0;
+  uint32_t num_cu = 0;
+  std::string xgmi_peer_bdf[kMaxXgmiLinks];  // from amdsmi_get_link_metrics (once)
+};
+
+// One tick of device telemetry.  NaN = unsupported/unavailable; raw accumulators are
+// kept as integers so deltas are exact across wraps.
+struct DeviceSample {
+  bool ok = false;
+  std::string error;
+  uint64_t host_ns = 0;        // CLOCK_MONOTONIC at read
+  uint64_t fw_ts_10ns = 0;     // PMFW timestamp (10 ns units), 0 = n/a
+
+  double gfx_activity = kNaN;  // %
+  double umc_activity = kNaN;  // %
+  double mm_activity = kNaN;   // %
+  double vram_used = kNaN;     // bytes
+  double vram_total = kNaN;    // bytes
+  double power_w = kNaN;       // current socket power
+  double power_cap_w = kNaN;
+  uint64_t energy_acc = 0;     // raw accumulator
+  double energy_unit_j = 15.259e-6;  // J per unit (amdsmi: 15.259 uJ)
+  bool energy_valid = false;
+
+  // temperatures (C)
+  double temp_hotspot = kNaN, temp_mem = kNaN, temp_edge = kNaN;
+  double temp_vrgfx = kNaN, temp_vrsoc = kNaN, temp_vrmem = kNaN;
+  double temp_hbm[kMaxHbm] = {kNaN, kNaN, kNaN, kNaN};
+
+  // clocks (MHz)
+  double clk_gfx = kNaN, clk_soc = kNaN, clk_mem = kNaN;
+
+  // xGMI accumulators (KB) per link; link_up: 1/0, NaN unsupported
+  int num_xgmi_links = 0;
+  uint64_t xgmi_read_kb[kMaxXgmiLinks] = {};
+  uint64_t xgmi_write_kb[kMaxXgmiLinks] = {};
+  double xgmi_link_up[kMaxXgmiLinks] = {kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN};
+  bool xgmi_valid = false;
+
+  double pcie_bw_inst = kNaN;       // GB/s
+  uint64_t pcie_bw_acc = 0;         // GB/s accumulated
+  double pcie_replay = kNaN;        // count
+  double pcie_width = kNaN, pcie_speed_gts = kNaN;
+
+  // throttle residency accumulators (same units as accumulation_counter)
+  bool residency_valid = false;
+  uint64_t accumulation_counter = 0;
+  uint64_t res_ppt = 0, res_socket_thm = 0, res_vr_thm = 0, res_hbm_thm = 0, res_prochot = 0;
+
+  // per-XCC busy accumulators (for gfx util from counters)
+  uint64_t gfx_busy_acc[kMaxXcc] = {};
+  double vram_max_bw_gbs = kNaN;
+};
+
+// One GPU process observed on one device.
+struct ProcSample {
+  int pid = 0;
+  int device = 0;              // DeviceInfo::index
+  double vram_bytes = 0;
+  double cu_occupancy = kNaN;  // CUs (KFD stats_<id>/cu_occupancy)
+  double sdma_us = kNaN;       // accumulated SDMA usage (us)
+  double gfx_ns = kNaN;        // engine time (amdsmi)
+  std::string name;            // comm
+};
+
+// rocprofiler-sdk device-counting derived values for one GPU over one tick.
+struct CounterReading {
+  bool ok = false;
+  double mfma_busy_pct = kNaN;      // SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE * SIMDs)
+  double sq_busy_pct = kNaN;        // SQ_BUSY_CYCLES / GRBM_GUI_ACTIVE
+  double gui_active_pct = kNaN;     // GRBM_GUI_ACTIVE / GRBM_COUNT
+  double waves_per_s = kNaN;        // SQ_WAVES / dt
+  double lds_active_pct = kNaN;     // SQ_LDS_IDX_ACTIVE / (GUI_ACTIVE * CUs)
+  double lds_bank_conflict_pct = kNaN;  // SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
+  double hbm_read_bps = kNaN;       // TCC_EA0_RDREQ * 64B * 2 (gfx950 half-count) / dt
+  double hbm_write_bps = kNaN;      // TCC_EA0_WRREQ * 64B / dt
+};
+
+// HIP sentinel kernel stamps for one GPU (latest completed run).
+struct SentinelReading {
+  bool ok = false;
+  double sclk_hz = kNaN;              // d(s_memtime)/d(s_memrealtime) * 100 MHz
+  double dispatch_latency_s = kNaN;   // host launch -> first wave running
+  double xcc_id = kNaN;               // XCC the wave landed on
+  uint64_t runs = 0;                  // completed sentinel runs
+};
+
+class Backend {
+ public:
+  virtual ~Backend() = default;
+  virtual const char* name() const = 0;
+  // Enumerates devices once.  Returns false (with *err) if the backend cannot run.
+  virtual bool init(std::vector<DeviceInfo>* devices, std::string* err) = 0;
+  virtual void sample(const DeviceInfo& dev, DeviceSample* out) = 0;
+  // Optional process listing owned by the backend (mock, amdsmi).  Returns false if the
+  // backend has no process source (the engine then uses the KFD sysfs reader).
+  virtual bool processes(const DeviceInfo& dev, std::vector<ProcSample>* out) {
+    (void)dev;
+    (void)out;
+    return false;
+  }
+  // Optional synthetic counter/sentinel sources (the mock backend simulates both so the
+  // CPU-only plumbing config exports the full 64-series/GPU profile).
+  virtual bool counters(const DeviceInfo& dev, double dt_s, CounterReading* out) {
+    (void)dev;
+    (void)dt_s;
+    (void)out;
+    return false;
+  }
+  virtual bool sentinel(const DeviceInfo& dev, SentinelReading* out) {
+    (void)dev;
+    (void)out;
+    return false;
+  }
+  virtual void shutdown() {}
+};
+
+}  // namespace gpuexp

@@ -1,0 +1,829 @@
+#include "gpuexp/engine.h"
+
+#include <sys/eventfd.h>
+#include <sys/poll.h>
+#include <sys/timerfd.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <set>
+
+namespace gpuexp {
+
+namespace {
+
+const std::vector<std::string> kDevLabels = {"gpu", "bdf", "namespace", "pod", "container"};
+
+std::vector<std::string> with(const std::vector<std::string>& base, std::initializer_list<const char*> extra) {
+  std::vector<std::string> v = base;
+  for (auto e : extra) v.emplace_back(e);
+  return v;
+}
+
+std::string lower(std::string s) {
+  std::transform(s.begin(), s.end(), s.begin(), ::tolower);
+  return s;
+}
+
+// Delta of a monotonically increasing hardware accumulator.  Unsigned wrap is accepted
+// when the wrapped delta is plausible; a large backwards jump is a reset (returns false).
+bool acc_delta(uint64_t cur, uint64_t prev, double* d) {
+  uint64_t diff = cur - prev;  // modular
+  if (cur >= prev || diff < (1ull << 62)) {
+    *d = double(diff);
+    return true;
+  }
+  return false;
+}
+
+const std::vector<double>& stage_bounds() {
+  static const std::vector<double> b = {1e-6,  5e-6,  10e-6, 25e-6, 50e-6, 100e-6, 250e-6,
+                                        500e-6, 1e-3, 2.5e-3, 5e-3, 10e-3, 25e-3, 100e-3};
+  return b;
+}
+
+const char* kTempNames[9] = {"hotspot", "mem", "vrsoc", "edge", "vrgfx", "vrmem", "hbm0", "hbm1", "hbm2"};
+const char* kClkNames[3] = {"gfx", "soc", "mem"};
+const char* kThrNames[5] = {"ppt", "socket_thermal", "vr_thermal", "hbm_thermal", "prochot"};
+
+}  // namespace
+
+const char* Engine::stage_name(int i) {
+  static const char* n[kStages] = {"devices", "processes", "attribution", "sentinel",
+                                   "counters", "series", "render", "publish"};
+  return n[i];
+}
+
+Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) { self_pid_ = int(::getpid()); }
+
+Engine::~Engine() { stop(); }
+
+void Engine::define_families() {
+  auto G = MetricType::kGauge;
+  auto C = MetricType::kCounter;
+  auto H = MetricType::kHistogram;
+  auto add = [this](const char* n, const char* h, MetricType t, std::vector<std::string> l) {
+    return table_.add_family(FamilyDef{n, h, t, std::move(l)});
+  };
+  const auto& D = kDevLabels;
+  // --- per-GPU device families (standard profile: 64 series per GPU) ---
+  f_info_ = add("amd_gpu_info", "MI355X device identity (value is always 1)", G,
+                {"gpu", "bdf", "uuid", "name", "kfd_gpu_id", "render_node", "hip_id"});
+  f_up_ = add("amd_gpu_up", "1 if the last telemetry read of this GPU succeeded", G, D);
+  f_gfx_ = add("amd_gpu_gfx_activity_percent", "Average graphics/compute engine activity (PMFW)", G, D);
+  f_umc_ = add("amd_gpu_umc_activity_percent", "Average memory-controller (HBM3E) activity", G, D);
+  f_xcc_ = add("amd_gpu_xcc_busy_percent", "Per-XCD compute busy over the last tick (gfx_busy_acc deltas)", G,
+               with(D, {"xcc"}));
+  f_vram_used_ = add("amd_gpu_vram_used_bytes", "HBM3E VRAM in use", G, D);
+  f_vram_total_ = add("amd_gpu_vram_total_bytes", "HBM3E VRAM capacity", G, D);
+  f_hbm_bw_ = add("amd_gpu_hbm_bandwidth_bytes_per_second",
+                  "HBM bandwidth estimate: UMC activity x max VRAM bandwidth", G, D);
+  f_power_ = add("amd_gpu_power_watts", "Current socket power", G, D);
+  f_power_cap_ = add("amd_gpu_power_cap_watts", "Socket power cap", G, D);
+  f_energy_ = add("amd_gpu_energy_joules_total", "Energy consumed (hardware accumulator)", C, D);
+  f_temp_ = add("amd_gpu_temperature_celsius", "Temperature by sensor", G, with(D, {"sensor"}));
+  f_clk_ = add("amd_gpu_clock_hz", "Current clock frequency by domain", G, with(D, {"clock"}));
+  f_xrd_ = add("amd_gpu_xgmi_read_bytes_total", "xGMI bytes received on a link (hardware accumulator)", C,
+               with(D, {"link", "peer_bdf"}));
+  f_xwr_ = add("amd_gpu_xgmi_write_bytes_total", "xGMI bytes sent on a link (hardware accumulator)", C,
+               with(D, {"link", "peer_bdf"}));
+  f_xrd_rate_ = add("amd_gpu_xgmi_read_bytes_per_second", "xGMI receive rate summed over links", G, D);
+  f_xwr_rate_ = add("amd_gpu_xgmi_write_bytes_per_second", "xGMI transmit rate summed over links", G, D);
+  f_links_up_ = add("amd_gpu_xgmi_links_up", "Number of xGMI links reporting up", G, D);
+  f_pcie_bw_ = add("amd_gpu_pcie_bandwidth_bytes_per_second", "PCIe instantaneous bandwidth", G, D);
+  f_pcie_replay_ = add("amd_gpu_pcie_replay_total", "PCIe replay count", C, D);
+  f_pcie_speed_ = add("amd_gpu_pcie_link_speed_gts", "PCIe link speed (GT/s)", G, D);
+  f_pcie_width_ = add("amd_gpu_pcie_link_width", "PCIe link width (lanes)", G, D);
+  f_thr_ = add("amd_gpu_throttle_residency_percent", "Share of the last tick spent throttled, by reason", G,
+               with(D, {"reason"}));
+  f_nprocs_ = add("amd_gpu_processes", "Processes with a KFD context on this GPU", G, D);
+  f_cu_occ_ = add("amd_gpu_cu_occupancy", "CUs occupied by all processes on this GPU", G, D);
+  f_mfma_ = add("amd_gpu_mfma_busy_percent", "MFMA (matrix core) busy: SQ_VALU_MFMA_BUSY_CYCLES per SIMD", G, D);
+  f_sq_busy_ = add("amd_gpu_sq_busy_percent", "Shader sequencer busy (SQ_BUSY_CYCLES)", G, D);
+  f_gui_ = add("amd_gpu_gui_active_percent", "Graphics pipe active (GRBM_GUI_ACTIVE / GRBM_COUNT)", G, D);
+  f_waves_ = add("amd_gpu_waves_per_second", "Waves dispatched per second (SQ_WAVES)", G, D);
+  f_lds_ = add("amd_gpu_lds_active_percent", "LDS active cycles per CU (SQ_LDS_IDX_ACTIVE)", G, D);
+  f_lds_conf_ = add("amd_gpu_lds_bank_conflict_percent", "LDS bank-conflict cycles / LDS active cycles", G, D);
+  f_hbm_rd_ = add("amd_gpu_hbm_read_bytes_per_second", "HBM read bandwidth (TCC_EA0_RDREQ)", G, D);
+  f_hbm_wr_ = add("amd_gpu_hbm_write_bytes_per_second", "HBM write bandwidth (TCC_EA0_WRREQ)", G, D);
+  f_sen_sclk_ = add("amd_gpu_sentinel_sclk_hz", "Effective shader clock measured by the sentinel kernel", G, D);
+  f_sen_lat_ = add("amd_gpu_sentinel_dispatch_latency_seconds",
+                   "Host launch to first-wave start of the sentinel kernel (queue contention)", G, D);
+  f_sen_xcc_ = add("amd_gpu_sentinel_xcc_id", "XCC the last sentinel wave ran on", G, D);
+  f_sen_runs_ = add("amd_gpu_sentinel_runs_total", "Completed sentinel kernel runs", C, D);
+
+  // --- per-process / per-pod families ---
+  const std::vector<std::string> P = {"gpu", "pid", "comm", "namespace", "pod", "container"};
+  f_proc_vram_ = add("amd_gpu_process_vram_bytes", "VRAM held by a process on a GPU (KFD)", G, P);
+  f_proc_cu_ = add("amd_gpu_process_cu_occupancy", "CUs occupied by a process on a GPU (KFD)", G, P);
+  f_proc_sdma_ = add("amd_gpu_process_sdma_seconds_total", "SDMA engine time used by a process", C, P);
+  if (cfg_.legacy_families) {
+    // Byte-compatible with the reference (/root/reference/main.go:22-35): names, HELP,
+    // label names and order {pid, pod}.  `pid` is the host PID (the reference's intended
+    // meaning; it accidentally exported a slice index, main.go:144).
+    f_legacy_mem_ = add("pod_gpu_memory_usage", "GPU memory used by Kubernetes Pod", G, {"pid", "pod"});
+    f_legacy_perc_ = add("docker_gpu_memory_perc_usage", "GPU memory in percentage used by pod", G,
+                         {"pid", "pod"});
+  }
+  const std::vector<std::string> PO = {"namespace", "pod"};
+  f_pod_vram_ = add("amd_pod_gpu_vram_bytes", "VRAM held by all GPU processes of a pod", G, PO);
+  f_pod_procs_ = add("amd_pod_gpu_processes", "GPU processes of a pod", G, PO);
+  f_pod_gpus_ = add("amd_pod_gpus", "GPUs attributed to a pod", G, PO);
+  f_pod_xrd_ = add("amd_pod_xgmi_read_bytes_per_second", "xGMI receive rate of the pod's GPUs", G, PO);
+  f_pod_xwr_ = add("amd_pod_xgmi_write_bytes_per_second", "xGMI transmit rate of the pod's GPUs", G, PO);
+  f_pod_power_ = add("amd_pod_gpu_power_watts", "Socket power of the pod's GPUs", G, PO);
+  f_pod_gfx_ = add("amd_pod_gpu_gfx_activity_percent", "Mean gfx activity of the pod's GPUs", G, PO);
+  f_rccl_calls_ = add("amd_rccl_collective_calls_total", "RCCL collective/p2p calls by op (rocprofiler-sdk tracer)",
+                      C, {"namespace", "pod", "pid", "op"});
+  f_rccl_bytes_ = add("amd_rccl_collective_bytes_total", "RCCL payload bytes by op (rocprofiler-sdk tracer)", C,
+                      {"namespace", "pod", "pid", "op"});
+
+  // --- exporter self-metrics (own prefix; the reference registry had none, main.go:40) ---
+  f_self_build_ = add("gpuexp_build_info", "Exporter build and backend", G, {"version", "backend"});
+  f_self_ticks_ = add("gpuexp_ticks_total", "Sampler ticks completed", C, {});
+  f_self_stage_ = add("gpuexp_sample_stage_duration_seconds", "Sampler stage duration", H, {"stage"});
+  f_self_scrape_ = add("gpuexp_scrape_duration_seconds", "Server-side /metrics latency (request parsed -> last byte written)",
+                       H, {});
+  f_self_scrapes_ = add("gpuexp_scrapes_total", "Scrapes of the metrics path", C, {});
+  f_self_http_bytes_ = add("gpuexp_http_response_bytes_total", "HTTP response bytes written", C, {});
+  f_self_render_bytes_ = add("gpuexp_render_bytes", "Size of the last rendered exposition", G, {});
+  f_self_series_ = add("gpuexp_series", "Series in the last rendered exposition", G, {});
+  f_self_dev_errors_ = add("gpuexp_device_errors_total", "Failed telemetry reads per GPU", C, {"gpu"});
+  f_self_overruns_ = add("gpuexp_tick_overruns_total", "Ticks skipped because a tick ran past its deadline", C, {});
+  f_self_cpu_ = add("gpuexp_sampler_cpu_seconds_total", "CPU time used by the sampler thread", C, {});
+  f_self_source_up_ = add("gpuexp_source_up", "1 if an optional source is active", G, {"source"});
+}
+
+bool Engine::start(std::string* err) {
+  if (running_.load()) return true;
+  define_families();
+  if (cfg_.backend == "mock") {
+    auto m = std::make_unique<MockBackend>(cfg_.mock_devices);
+    mock_ = m.get();
+    backend_ = std::move(m);
+  } else if (cfg_.backend == "sysfs") {
+    backend_ = std::make_unique<SysfsBackend>(cfg_.host_root);
+  } else if (cfg_.backend == "amdsmi") {
+    backend_ = make_amdsmi_backend(cfg_.host_root, cfg_.process_source == "amdsmi", cfg_.force_amdsmi_metrics);
+  } else {
+    *err = "unknown backend: " + cfg_.backend;
+    return false;
+  }
+  std::vector<DeviceInfo> all;
+  if (!backend_->init(&all, err)) return false;
+  if (!cfg_.device_filter.empty()) {
+    for (auto& d : all)
+      if (std::find(cfg_.device_filter.begin(), cfg_.device_filter.end(), d.index) != cfg_.device_filter.end())
+        devices_.push_back(d);
+    // keep backend indices: DeviceInfo::index addresses the backend's own table
+  } else {
+    devices_ = all;
+  }
+  dstate_.assign(devices_.size(), DevState());
+  kfd_ = std::make_unique<KfdProcReader>(cfg_.host_root, cfg_.exclude_self ? self_pid_ : -1, cfg_.kfd_cu_occupancy);
+  resolver_ = std::make_unique<PidResolver>(cfg_.host_root);
+
+  if (cfg_.enable_sentinel && cfg_.backend != "mock") {
+    sentinel_ = make_hip_sentinel(cfg_.sentinel_ring, cfg_.sentinel_spin);
+    std::string e;
+    if (!sentinel_ || !sentinel_->start(devices_, &e)) {
+      sentinel_status_ = "unavailable: " + e;
+      GPUEXP_LOG(LogLevel::kWarn, "sentinel", sentinel_status_);
+      sentinel_.reset();
+    } else {
+      sentinel_status_ = sentinel_->status();
+    }
+  } else if (cfg_.enable_sentinel) {
+    sentinel_status_ = "mock";
+  }
+  if (cfg_.enable_counters && cfg_.backend != "mock") {
+    counters_ = make_rocprof_counters(cfg_.counters_plugin);
+    std::string e;
+    if (!counters_ || !counters_->start(devices_, &e)) {
+      counters_status_ = "unavailable: " + e;
+      GPUEXP_LOG(LogLevel::kWarn, "counters", counters_status_);
+      counters_.reset();
+    } else {
+      counters_status_ = counters_->status();
+    }
+  } else if (cfg_.enable_counters) {
+    counters_status_ = "mock";
+  }
+  if (cfg_.enable_rccl) rccl_ = make_rccl_source(cfg_.rccl_dir);
+
+  if (!cfg_.trace_path.empty()) {
+    trace_ = std::fopen(cfg_.trace_path.c_str(), "w");
+    if (trace_) {
+      std::fputs("[\n", trace_);
+      trace_t0_ = mono_ns();
+    }
+  }
+  if (cfg_.serve_http) {
+    http_ = std::make_unique<HttpServer>(&store_, cfg_.http);
+    if (!http_->start(err)) {
+      http_.reset();
+      return false;
+    }
+  }
+  running_.store(true);
+  if (cfg_.interval_s > 0) {
+    stop_fd_ = ::eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+    sampler_ = std::thread([this] { run_sampler(); });
+  }
+  return true;
+}
+
+void Engine::stop() {
+  if (!running_.exchange(false)) return;
+  if (stop_fd_ >= 0) {
+    uint64_t one = 1;
+    ssize_t r = ::write(stop_fd_, &one, sizeof(one));
+    (void)r;
+  }
+  if (sampler_.joinable()) sampler_.join();
+  if (stop_fd_ >= 0) ::close(stop_fd_);
+  stop_fd_ = -1;
+  if (http_) http_->stop();
+  if (sentinel_) sentinel_->stop();
+  if (counters_) counters_->stop();
+  if (backend_) backend_->shutdown();
+  if (trace_) {
+    std::fputs("{}]\n", trace_);
+    std::fclose(trace_);
+    trace_ = nullptr;
+  }
+}
+
+void Engine::run_sampler() {
+  int tfd = ::timerfd_create(CLOCK_MONOTONIC, TFD_CLOEXEC);
+  uint64_t period = uint64_t(cfg_.interval_s * 1e9);
+  if (period < 1000000) period = 1000000;  // 1 kHz cap
+  itimerspec its{};
+  its.it_interval.tv_sec = time_t(period / 1000000000ull);
+  its.it_interval.tv_nsec = long(period % 1000000000ull);
+  its.it_value.tv_nsec = 1;  // first tick immediately
+  ::timerfd_settime(tfd, 0, &its, nullptr);
+  pollfd fds[2] = {{tfd, POLLIN, 0}, {stop_fd_, POLLIN, 0}};
+  while (running_.load()) {
+    int n = ::poll(fds, 2, -1);
+    if (n < 0) continue;
+    if (fds[1].revents & POLLIN) break;
+    if (fds[0].revents & POLLIN) {
+      uint64_t expirations = 0;
+      ssize_t r = ::read(tfd, &expirations, sizeof(expirations));
+      if (r != sizeof(expirations)) continue;
+      if (expirations > 1) {
+        std::lock_guard<std::mutex> lk(stats_mu_);
+        stats_.overruns += expirations - 1;
+      }
+      std::lock_guard<std::mutex> lk(tick_mu_);
+      tick_locked(mono_ns());
+    }
+  }
+  ::close(tfd);
+}
+
+void Engine::tick_now(uint64_t now_ns) {
+  std::lock_guard<std::mutex> lk(tick_mu_);
+  tick_locked(now_ns);
+}
+
+void Engine::set_pods(std::vector<PodMeta> pods) {
+  std::lock_guard<std::mutex> lk(ctl_mu_);
+  pending_pods_ = std::move(pods);
+  ctl_dirty_ = true;
+}
+
+void Engine::set_device_owners(std::vector<std::pair<std::string, DeviceOwner>> owners) {
+  std::lock_guard<std::mutex> lk(ctl_mu_);
+  pending_owners_ = std::move(owners);
+  ctl_dirty_ = true;
+}
+
+void Engine::set_pid_cgroup(int pid, const std::string& cgroup_path) {
+  std::lock_guard<std::mutex> lk(ctl_mu_);
+  pending_overrides_.emplace_back(pid, cgroup_path);
+}
+
+void Engine::clear_pid_cgroups() {
+  std::lock_guard<std::mutex> lk(ctl_mu_);
+  pending_overrides_.clear();
+  clear_overrides_ = true;
+}
+
+void Engine::trace_event(const char* name, uint64_t start_ns, uint64_t dur_ns) {
+  if (!trace_ || trace_events_ >= cfg_.trace_max_events) return;
+  ++trace_events_;
+  std::fprintf(trace_, "{\"name\":\"%s\",\"ph\":\"X\",\"ts\":%.3f,\"dur\":%.3f,\"pid\":%d,\"tid\":1},\n", name,
+               double(start_ns - trace_t0_) * 1e-3, double(dur_ns) * 1e-3, self_pid_);
+}
+
+void Engine::dput(DevState& st, int dev, SeriesRef& r, int fid, const std::vector<std::string>& extra,
+                  double v, uint64_t gen) {
+  if (std::isnan(v)) return;
+  if (table_.set(r, v, gen)) return;
+  const DeviceInfo& d = devices_[size_t(dev)];
+  std::vector<std::string> labels = {std::to_string(d.index), d.bdf, st.owner.ns, st.owner.pod,
+                                     st.owner.container};
+  labels.insert(labels.end(), extra.begin(), extra.end());
+  r = table_.upsert(fid, labels);
+  table_.set(r, v, gen);
+}
+
+void Engine::collect_device(int i, uint64_t gen, double dt_s) {
+  DevState& st = dstate_[size_t(i)];
+  const DeviceInfo& d = devices_[size_t(i)];
+  const DeviceSample& c = st.cur;
+  // Owner change -> rebuild every cached handle with the new pod labels.
+  std::string okey = st.owner.ns + "/" + st.owner.pod + "/" + st.owner.container;
+  if (okey != st.owner_key) {
+    DeviceOwner keep = st.owner;
+    DevState fresh;
+    fresh.cur = st.cur;
+    fresh.prev = st.prev;
+    fresh.have_prev = st.have_prev;
+    std::copy(std::begin(st.xgmi_rd_rate), std::end(st.xgmi_rd_rate), std::begin(fresh.xgmi_rd_rate));
+    std::copy(std::begin(st.xgmi_wr_rate), std::end(st.xgmi_wr_rate), std::begin(fresh.xgmi_wr_rate));
+    fresh.rates_valid = st.rates_valid;
+    fresh.errors = st.errors;
+    fresh.err_ref = st.err_ref;
+    fresh.owner = keep;
+    fresh.owner_key = okey;
+    st = fresh;
+  }
+
+  if (!table_.set(st.info, 1, gen)) {
+    st.info = table_.upsert(f_info_, {std::to_string(d.index), d.bdf, d.uuid, d.name, std::to_string(d.kfd_gpu_id),
+                                      d.render_minor >= 0 ? "renderD" + std::to_string(d.render_minor) : "",
+                                      std::to_string(d.hip_id)});
+    table_.set(st.info, 1, gen);
+  }
+  dput(st, i, st.up, f_up_, {}, c.ok ? 1 : 0, gen);
+  if (!table_.set(st.err_ref, double(st.errors), gen)) {
+    st.err_ref = table_.upsert(f_self_dev_errors_, {std::to_string(d.index)});
+    table_.set(st.err_ref, double(st.errors), gen);
+  }
+  if (!c.ok) return;  // a failed GPU exports only up=0 (+ errors); others unaffected
+  bool compact = cfg_.series_profile == "compact";
+
+  dput(st, i, st.gfx, f_gfx_, {}, c.gfx_activity, gen);
+  dput(st, i, st.umc, f_umc_, {}, c.umc_activity, gen);
+  dput(st, i, st.vram_used, f_vram_used_, {}, c.vram_used, gen);
+  dput(st, i, st.vram_total, f_vram_total_, {}, c.vram_total, gen);
+  dput(st, i, st.power, f_power_, {}, c.power_w, gen);
+  dput(st, i, st.power_cap, f_power_cap_, {}, c.power_cap_w, gen);
+  if (c.energy_valid) dput(st, i, st.energy, f_energy_, {}, double(c.energy_acc) * c.energy_unit_j, gen);
+  double temps[9] = {c.temp_hotspot, c.temp_mem, c.temp_vrsoc, c.temp_edge, c.temp_vrgfx, c.temp_vrmem,
+                     c.temp_hbm[0], c.temp_hbm[1], c.temp_hbm[2]};
+  for (int k = 0; k < 9; ++k) dput(st, i, st.temp[k], f_temp_, {kTempNames[k]}, temps[k], gen);
+  double clks[3] = {c.clk_gfx, c.clk_soc, c.clk_mem};
+  for (int k = 0; k < 3; ++k)
+    dput(st, i, st.clk[k], f_clk_, {kClkNames[k]}, std::isnan(clks[k]) ? kNaN : clks[k] * 1e6, gen);
+  if (!std::isnan(c.umc_activity) && !std::isnan(c.vram_max_bw_gbs))
+    dput(st, i, st.hbm_bw, f_hbm_bw_, {}, c.umc_activity / 100.0 * c.vram_max_bw_gbs * 1e9, gen);
+
+  // Rates from hardware accumulators over the PMFW timestamp delta (host time fallback).
+  const DeviceSample& p = st.prev;
+  bool have_prev = st.have_prev && p.ok;
+  double dt_dev = 0;
+  if (have_prev) {
+    if (c.fw_ts_10ns && p.fw_ts_10ns && c.fw_ts_10ns > p.fw_ts_10ns)
+      dt_dev = double(c.fw_ts_10ns - p.fw_ts_10ns) * 1e-8;
+    else if (!(c.fw_ts_10ns && c.fw_ts_10ns == p.fw_ts_10ns) && c.host_ns > p.host_ns)
+      dt_dev = double(c.host_ns - p.host_ns) * 1e-9;
+  }
+  if (c.xgmi_valid) {
+    int links_up = 0;
+    for (int l = 0; l < c.num_xgmi_links; ++l) {
+      if (std::isnan(c.xgmi_link_up[l])) continue;
+      links_up += c.xgmi_link_up[l] > 0;
+      if (compact) continue;
+      std::string ls = std::to_string(l);
+      const std::string& peer = d.xgmi_peer_bdf[l];
+      dput(st, i, st.xrd[l], f_xrd_, {ls, peer}, double(c.xgmi_read_kb[l]) * 1024.0, gen);
+      dput(st, i, st.xwr[l], f_xwr_, {ls, peer}, double(c.xgmi_write_kb[l]) * 1024.0, gen);
+    }
+    dput(st, i, st.links_up, f_links_up_, {}, double(links_up), gen);
+    if (have_prev && p.xgmi_valid && dt_dev > 0) {
+      bool ok = true;
+      for (int l = 0; l < kMaxXgmiLinks; ++l) {
+        double dr, dw;
+        if (!acc_delta(c.xgmi_read_kb[l], p.xgmi_read_kb[l], &dr) ||
+            !acc_delta(c.xgmi_write_kb[l], p.xgmi_write_kb[l], &dw)) {
+          ok = false;  // counter reset: skip one rate sample
+          continue;
+        }
+        st.xgmi_rd_rate[l] = dr * 1024.0 / dt_dev;
+        st.xgmi_wr_rate[l] = dw * 1024.0 / dt_dev;
+      }
+      st.rates_valid = ok || st.rates_valid;
+    }
+    if (st.rates_valid) {
+      double rs = 0, ws = 0;
+      for (int l = 0; l < kMaxXgmiLinks; ++l) {
+        rs += st.xgmi_rd_rate[l];
+        ws += st.xgmi_wr_rate[l];
+      }
+      dput(st, i, st.xrd_rate, f_xrd_rate_, {}, rs, gen);
+      dput(st, i, st.xwr_rate, f_xwr_rate_, {}, ws, gen);
+    }
+  }
+  dput(st, i, st.pcie_bw, f_pcie_bw_, {}, std::isnan(c.pcie_bw_inst) ? kNaN : c.pcie_bw_inst * 1e9, gen);
+  dput(st, i, st.pcie_replay, f_pcie_replay_, {}, c.pcie_replay, gen);
+  dput(st, i, st.pcie_speed, f_pcie_speed_, {}, c.pcie_speed_gts, gen);
+  dput(st, i, st.pcie_width, f_pcie_width_, {}, c.pcie_width, gen);
+
+  if (have_prev && c.residency_valid && p.residency_valid) {
+    double dacc;
+    if (acc_delta(c.accumulation_counter, p.accumulation_counter, &dacc) && dacc > 0) {
+      uint64_t cr[5] = {c.res_ppt, c.res_socket_thm, c.res_vr_thm, c.res_hbm_thm, c.res_prochot};
+      uint64_t pr[5] = {p.res_ppt, p.res_socket_thm, p.res_vr_thm, p.res_hbm_thm, p.res_prochot};
+      for (int k = 0; k < 5; ++k) {
+        double dr;
+        if (acc_delta(cr[k], pr[k], &dr))
+          dput(st, i, st.thr[k], f_thr_, {kThrNames[k]}, std::min(100.0, dr * 100.0 / dacc), gen);
+      }
+      if (!compact) {
+        uint32_t nx = d.num_xcc ? std::min<uint32_t>(d.num_xcc, kMaxXcc) : kMaxXcc;
+        for (uint32_t x = 0; x < nx; ++x) {
+          double db;
+          if (acc_delta(c.gfx_busy_acc[x], p.gfx_busy_acc[x], &db))
+            dput(st, i, st.xcc[x], f_xcc_, {std::to_string(x)}, std::min(100.0, db / dacc), gen);
+        }
+      }
+    }
+  }
+
+  // Optional sources: rocprofiler counters, sentinel (real or mock-simulated).
+  CounterReading cr;
+  bool have_ctr = false;
+  if (counters_) have_ctr = counters_->sample(i, dt_s, &cr) && cr.ok;
+  else if (cfg_.enable_counters) have_ctr = backend_->counters(d, dt_s, &cr) && cr.ok;
+  if (have_ctr) {
+    dput(st, i, st.ctr[0], f_mfma_, {}, cr.mfma_busy_pct, gen);
+    dput(st, i, st.ctr[1], f_sq_busy_, {}, cr.sq_busy_pct, gen);
+    dput(st, i, st.ctr[2], f_gui_, {}, cr.gui_active_pct, gen);
+    dput(st, i, st.ctr[3], f_waves_, {}, cr.waves_per_s, gen);
+    dput(st, i, st.ctr[4], f_lds_, {}, cr.lds_active_pct, gen);
+    dput(st, i, st.ctr[5], f_lds_conf_, {}, cr.lds_bank_conflict_pct, gen);
+    dput(st, i, st.ctr[6], f_hbm_rd_, {}, cr.hbm_read_bps, gen);
+    dput(st, i, st.ctr[7], f_hbm_wr_, {}, cr.hbm_write_bps, gen);
+  }
+  SentinelReading sr;
+  bool have_sen = false;
+  if (sentinel_) have_sen = sentinel_->read(i, &sr) && sr.ok;
+  else if (cfg_.enable_sentinel) have_sen = backend_->sentinel(d, &sr) && sr.ok;
+  if (have_sen) {
+    dput(st, i, st.sen[0], f_sen_sclk_, {}, sr.sclk_hz, gen);
+    dput(st, i, st.sen[1], f_sen_lat_, {}, sr.dispatch_latency_s, gen);
+    dput(st, i, st.sen[2], f_sen_xcc_, {}, sr.xcc_id, gen);
+    dput(st, i, st.sen[3], f_sen_runs_, {}, double(sr.runs), gen);
+  }
+}
+
+void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSample>>& per_dev) {
+  // pid -> attribution, resolved once per tick
+  std::unordered_map<int, ProcAttr> attr;
+  std::vector<int> live;
+  for (auto& lst : per_dev)
+    for (auto& p : lst) {
+      if (attr.count(p.pid)) continue;
+      ProcAttr a;
+      if (cfg_.pod_attribution) {
+        const CgroupInfo* ci = resolver_->resolve(p.pid);
+        if (ci && ci->kube) {
+          a.uid = ci->pod_uid;
+          auto it = pods_by_uid_.find(ci->pod_uid);
+          if (it != pods_by_uid_.end()) {
+            a.ns = it->second.ns;
+            a.pod = it->second.name;
+          } else {
+            a.pod = ci->pod_uid;  // name unknown until the control plane reports it
+          }
+          auto cn = container_names_.find(ci->container_id);
+          if (cn != container_names_.end()) a.container = cn->second;
+        }
+      }
+      attr.emplace(p.pid, a);
+      live.push_back(p.pid);
+    }
+  resolver_->gc(live);
+
+  struct PidAgg {
+    double used = 0, total = 0;
+  };
+  std::map<int, PidAgg> legacy;
+  struct PodAgg {
+    double vram = 0;
+    std::set<int> pids;
+    int gpus = 0;
+    double xrd = 0, xwr = 0, power = 0, gfx = 0;
+    int gfx_n = 0;
+  };
+  std::map<std::pair<std::string, std::string>, PodAgg> pods;
+
+  for (size_t di = 0; di < per_dev.size(); ++di) {
+    const DeviceInfo& d = devices_[di];
+    DevState& st = dstate_[di];
+    double cu_sum = 0;
+    bool cu_any = false;
+    for (auto& p : per_dev[di]) {
+      const ProcAttr& a = attr[p.pid];
+      std::vector<std::string> L = {std::to_string(d.index), std::to_string(p.pid), p.name, a.ns, a.pod, a.container};
+      table_.put(f_proc_vram_, L, p.vram_bytes, gen);
+      if (!std::isnan(p.cu_occupancy)) {
+        table_.put(f_proc_cu_, L, p.cu_occupancy, gen);
+        cu_sum += p.cu_occupancy;
+        cu_any = true;
+      }
+      if (!std::isnan(p.sdma_us)) table_.put(f_proc_sdma_, L, p.sdma_us * 1e-6, gen);
+      if (!a.pod.empty()) {
+        auto& la = legacy[p.pid];
+        la.used += p.vram_bytes;
+        la.total += double(d.vram_total);
+        auto& pa = pods[{a.ns, a.pod}];
+        pa.vram += p.vram_bytes;
+        pa.pids.insert(p.pid);
+      }
+    }
+    if (st.cur.ok) {
+      dput(st, int(di), st.nprocs, f_nprocs_, {}, double(per_dev[di].size()), gen);
+      if (cu_any) dput(st, int(di), st.cu_occ, f_cu_occ_, {}, cu_sum, gen);
+    }
+    if (!st.owner.pod.empty()) {
+      auto& pa = pods[{st.owner.ns, st.owner.pod}];
+      pa.gpus += 1;
+      if (st.cur.ok) {
+        if (st.rates_valid)
+          for (int l = 0; l < kMaxXgmiLinks; ++l) {
+            pa.xrd += st.xgmi_rd_rate[l];
+            pa.xwr += st.xgmi_wr_rate[l];
+          }
+        if (!std::isnan(st.cur.power_w)) pa.power += st.cur.power_w;
+        if (!std::isnan(st.cur.gfx_activity)) {
+          pa.gfx += st.cur.gfx_activity;
+          pa.gfx_n += 1;
+        }
+      }
+    }
+  }
+  if (f_legacy_mem_ >= 0) {
+    // Legacy families: one series per attributed host PID, summed over GPUs (the
+    // reference overwrote per device, last-device-wins, main.go:147-150).
+    for (auto& kv : legacy) {
+      const ProcAttr& a = attr[kv.first];
+      std::vector<std::string> L = {std::to_string(kv.first), a.pod};
+      table_.put(f_legacy_mem_, L, kv.second.used, gen);
+      table_.put(f_legacy_perc_, L, kv.second.total > 0 ? kv.second.used / kv.second.total * 100.0 : 0.0, gen);
+    }
+  }
+  if (cfg_.series_profile == "legacy") return;
+  for (auto& kv : pods) {
+    std::vector<std::string> L = {kv.first.first, kv.first.second};
+    const PodAgg& pa = kv.second;
+    table_.put(f_pod_vram_, L, pa.vram, gen);
+    table_.put(f_pod_procs_, L, double(pa.pids.size()), gen);
+    table_.put(f_pod_gpus_, L, double(pa.gpus), gen);
+    if (pa.gpus > 0) {
+      table_.put(f_pod_xrd_, L, pa.xrd, gen);
+      table_.put(f_pod_xwr_, L, pa.xwr, gen);
+      table_.put(f_pod_power_, L, pa.power, gen);
+      if (pa.gfx_n) table_.put(f_pod_gfx_, L, pa.gfx / pa.gfx_n, gen);
+    }
+  }
+  if (rccl_) {
+    std::vector<RcclTotals> tot;
+    rccl_->poll(&tot);
+    for (auto& t : tot) {
+      ProcAttr a;
+      auto it = attr.find(t.pid);
+      if (it != attr.end()) a = it->second;
+      else if (cfg_.pod_attribution) {
+        const CgroupInfo* ci = resolver_->resolve(t.pid);
+        if (ci && ci->kube) {
+          auto pit = pods_by_uid_.find(ci->pod_uid);
+          if (pit != pods_by_uid_.end()) {
+            a.ns = pit->second.ns;
+            a.pod = pit->second.name;
+          } else {
+            a.pod = ci->pod_uid;
+          }
+        }
+      }
+      std::vector<std::string> L = {a.ns, a.pod, std::to_string(t.pid), t.op};
+      table_.put(f_rccl_calls_, L, double(t.calls), gen);
+      table_.put(f_rccl_bytes_, L, double(t.bytes), gen);
+    }
+  }
+}
+
+void Engine::emit_self(uint64_t gen) {
+  table_.put(f_self_build_, {cfg_.version, backend_->name()}, 1, gen);
+  EngineStats s;
+  {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    s = stats_;
+  }
+  table_.put(f_self_ticks_, {}, double(s.ticks), gen);
+  table_.put(f_self_overruns_, {}, double(s.overruns), gen);
+  table_.put(f_self_render_bytes_, {}, double(s.render_bytes), gen);
+  table_.put(f_self_series_, {}, double(s.series), gen);
+  table_.put(f_self_cpu_, {}, double(s.sampler_cpu_ns) * 1e-9, gen);
+  for (int k = 0; k < kStages; ++k) {
+    if (!self_stage_refs_[k].valid()) self_stage_refs_[k] = table_.upsert(f_self_stage_, {stage_name(k)});
+    if (s.ticks) table_.observe(self_stage_refs_[k], double(last_stage_ns_[k]) * 1e-9, gen, stage_bounds());
+    else table_.touch(self_stage_refs_[k], gen);
+  }
+  if (http_) {
+    const HttpStats& hs = http_->stats();
+    std::vector<uint64_t> counts(HttpStats::kBuckets + 1);
+    for (int b = 0; b <= HttpStats::kBuckets; ++b) counts[size_t(b)] = hs.lat_buckets[b].load(std::memory_order_relaxed);
+    uint64_t cnt = hs.lat_count.load(std::memory_order_relaxed);
+    double sum = double(hs.lat_sum_ns.load(std::memory_order_relaxed)) * 1e-9;
+    table_.set_histogram(table_.upsert(f_self_scrape_, {}), scrape_latency_bounds(), counts, sum, cnt, gen);
+    table_.put(f_self_scrapes_, {}, double(hs.metrics_requests.load(std::memory_order_relaxed)), gen);
+    table_.put(f_self_http_bytes_, {}, double(hs.bytes_sent.load(std::memory_order_relaxed)), gen);
+  }
+  table_.put(f_self_source_up_, {"backend:" + std::string(backend_->name())}, 1, gen);
+  table_.put(f_self_source_up_, {"sentinel"}, (sentinel_ || (cfg_.enable_sentinel && mock_)) ? 1 : 0, gen);
+  table_.put(f_self_source_up_, {"counters"}, (counters_ || (cfg_.enable_counters && mock_)) ? 1 : 0, gen);
+  table_.put(f_self_source_up_, {"rccl"}, rccl_ ? 1 : 0, gen);
+}
+
+void Engine::tick_locked(uint64_t now) {
+  uint64_t cpu0 = thread_cpu_ns();
+  uint64_t gen = ++gen_;
+  double dt_s = last_tick_now_ && now > last_tick_now_ ? double(now - last_tick_now_) * 1e-9 : 0.0;
+  last_tick_now_ = now;
+  uint64_t ts[kStages + 1];
+  ts[0] = mono_ns();
+
+  // Control-plane updates (pushed from Python at low rate).
+  {
+    std::lock_guard<std::mutex> lk(ctl_mu_);
+    if (clear_overrides_) {
+      resolver_->clear_overrides();
+      clear_overrides_ = false;
+    }
+    for (auto& o : pending_overrides_) resolver_->set_override(o.first, o.second);
+    pending_overrides_.clear();
+    if (ctl_dirty_) {
+      pods_by_uid_.clear();
+      container_names_.clear();
+      for (auto& p : pending_pods_) {
+        for (auto& c : p.containers) container_names_[lower(c.first)] = c.second;
+        pods_by_uid_[lower(p.uid)] = p;
+      }
+      owners_.clear();
+      for (auto& o : pending_owners_) owners_[lower(o.first)] = o.second;
+      ctl_dirty_ = false;
+    }
+  }
+
+  // 0: device telemetry
+  uint64_t errs = 0;
+  for (size_t i = 0; i < devices_.size(); ++i) {
+    DevState& st = dstate_[i];
+    if (st.cur.ok) {
+      st.prev = st.cur;
+      st.have_prev = true;
+    }
+    st.cur = DeviceSample();
+    st.cur.host_ns = now;
+    backend_->sample(devices_[i], &st.cur);
+    if (!st.cur.ok) {
+      st.errors += 1;
+      errs += 1;
+    }
+  }
+  ts[1] = mono_ns();
+
+  // 1: processes
+  std::vector<std::vector<ProcSample>> per_dev(devices_.size());
+  if (cfg_.process_source != "none") {
+    bool from_backend = cfg_.process_source != "kfd";
+    if (from_backend)
+      for (size_t i = 0; i < devices_.size(); ++i)
+        if (!backend_->processes(devices_[i], &per_dev[i])) {
+          from_backend = false;
+          break;
+        }
+    if (!from_backend) {
+      kfd_->scan(devices_, &per_dev);
+    } else if (cfg_.exclude_self) {
+      for (auto& l : per_dev)
+        l.erase(std::remove_if(l.begin(), l.end(), [this](const ProcSample& p) { return p.pid == self_pid_; }),
+                l.end());
+    }
+  }
+  ts[2] = mono_ns();
+
+  // 2: device ownership (device plugin map first, then single-pod inference).
+  for (size_t i = 0; i < devices_.size(); ++i) {
+    DevState& st = dstate_[i];
+    const DeviceInfo& d = devices_[i];
+    DeviceOwner own;
+    auto it = owners_.find(lower(d.bdf));
+    if (it == owners_.end()) it = owners_.find(lower(d.uuid));
+    if (it != owners_.end()) {
+      own = it->second;
+    } else if (cfg_.pod_attribution && cfg_.infer_device_owner) {
+      std::set<std::tuple<std::string, std::string, std::string>> seen;
+      for (auto& p : per_dev[i]) {
+        const CgroupInfo* ci = resolver_->resolve(p.pid);
+        if (!ci || !ci->kube) continue;
+        auto pit = pods_by_uid_.find(ci->pod_uid);
+        std::string ns = pit != pods_by_uid_.end() ? pit->second.ns : "";
+        std::string name = pit != pods_by_uid_.end() ? pit->second.name : ci->pod_uid;
+        auto cn = container_names_.find(ci->container_id);
+        seen.emplace(ns, name, cn != container_names_.end() ? cn->second : "");
+      }
+      std::set<std::pair<std::string, std::string>> podset;
+      for (auto& t : seen) podset.emplace(std::get<0>(t), std::get<1>(t));
+      if (podset.size() == 1) {
+        own.ns = podset.begin()->first;
+        own.pod = podset.begin()->second;
+        if (seen.size() == 1) own.container = std::get<2>(*seen.begin());
+      }
+    }
+    st.owner = own;
+  }
+  ts[3] = mono_ns();
+
+  // 3: sentinel (drain previous run, launch next; never blocks on the GPU)
+  if (sentinel_) sentinel_->tick(now);
+  ts[4] = mono_ns();
+  // 4: counters are sampled inside collect_device (per GPU); timed there as part of series
+  ts[5] = mono_ns();
+
+  // 5: series
+  for (size_t i = 0; i < devices_.size(); ++i) {
+    if (cfg_.series_profile != "legacy") collect_device(int(i), gen, dt_s);
+  }
+  emit_processes(gen, per_dev);
+  emit_self(gen);
+  ts[6] = mono_ns();
+
+  // 6: render into a free snapshot slot
+  int slot = store_.begin_write();
+  uint64_t rbytes = 0, nseries = 0;
+  if (slot >= 0) {
+    Snapshot* snap = store_.slot(slot);
+    table_.render(&snap->body, gen, cfg_.gc_after);
+    snap->gen = gen;
+    snap->render_ns = now;
+    rbytes = snap->body.size();
+    nseries = table_.live_series(gen);
+    snap->series = nseries;
+    ts[7] = mono_ns();
+    // 7: gzip (only while clients ask for it) + publish
+    snap->gz.clear();
+    if (http_ && http_->gzip_wanted_ns() && mono_ns() - http_->gzip_wanted_ns() < 60000000000ull)
+      gzip_compress(snap->body, &snap->gz, cfg_.gzip_level);
+    store_.publish(slot);
+    if (http_) http_->set_ready(true);
+  } else {
+    ts[7] = mono_ns();
+  }
+  uint64_t tend = mono_ns();
+  uint64_t stage_dur[kStages] = {ts[1] - ts[0], ts[2] - ts[1], ts[3] - ts[2], ts[4] - ts[3],
+                                 ts[5] - ts[4], ts[6] - ts[5], ts[7] - ts[6], tend - ts[7]};
+  for (int k = 0; k < kStages; ++k) {
+    last_stage_ns_[k] = stage_dur[k];
+    uint64_t start = k == 0 ? ts[0] : (k < kStages - 1 ? ts[k] : ts[7]);
+    trace_event(stage_name(k), start, stage_dur[k]);
+  }
+  {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    stats_.ticks += 1;
+    if (slot < 0) stats_.publish_skipped += 1;
+    stats_.last_tick_ns = tend - ts[0];
+    stats_.max_tick_ns = std::max(stats_.max_tick_ns, stats_.last_tick_ns);
+    if (slot >= 0) {
+      stats_.render_bytes = rbytes;
+      stats_.series = nseries;
+    }
+    stats_.device_errors += errs;
+    for (int k = 0; k < kStages; ++k) stats_.stage_ns[k] = double(stage_dur[k]);
+    stats_.sampler_cpu_ns += thread_cpu_ns() - cpu0;
+  }
+}
+
+std::string Engine::snapshot_text() {
+  auto pin = store_.acquire();
+  return pin ? pin->body : std::string();
+}
+
+EngineStats Engine::stats() {
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  return stats_;
+}
+
+std::string Engine::source_status() {
+  return std::string("backend=") + (backend_ ? backend_->name() : "none") + " sentinel=" + sentinel_status_ +
+         " counters=" + counters_status_ + " rccl=" + (rccl_ ? cfg_.rccl_dir : "disabled");
+}
+
+}  // namespace gpuexp

@@ -1,0 +1,208 @@
+// The telemetry engine: sampler thread + series table + snapshot store + HTTP server.
+//
+// Reference control loop: `for { list pods; kubectl exec ps; NVML loop; Sleep(30s) }`
+// (/root/reference/main.go:74-157), period = 30 s + scan time, crash on any error.
+// Here a timerfd drives a fixed-rate tick (1/10/100 Hz) whose stages never block on the
+// network, and each source fails in isolation (SURVEY.md §5 failure-detection row).
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "gpuexp/backends.h"
+#include "gpuexp/device.h"
+#include "gpuexp/exposition.h"
+#include "gpuexp/http.h"
+#include "gpuexp/procs.h"
+#include "gpuexp/snapshot.h"
+#include "gpuexp/sources.h"
+
+namespace gpuexp {
+
+struct EngineConfig {
+  std::string backend = "mock";        // mock | sysfs | amdsmi
+  int mock_devices = 1;
+  std::string host_root;               // "" == "/"
+  double interval_s = 1.0;             // 0 = manual ticks only (tests)
+  bool serve_http = true;
+  HttpConfig http;
+  std::string series_profile = "standard";  // standard | compact | legacy
+  bool legacy_families = true;         // pod_gpu_memory_usage / docker_gpu_memory_perc_usage
+  bool pod_attribution = true;
+  bool infer_device_owner = true;      // single-pod GPU -> device series carry the pod
+  std::string process_source = "auto";  // auto | kfd | amdsmi | none
+  bool kfd_cu_occupancy = true;
+  bool exclude_self = true;
+  bool enable_sentinel = false;
+  int sentinel_ring = 64;
+  int sentinel_spin = 2000;
+  bool enable_counters = false;
+  std::string counters_plugin;         // path to _gpuexp_rocprof.so
+  bool enable_rccl = false;
+  std::string rccl_dir = "/dev/shm";
+  bool force_amdsmi_metrics = false;
+  int gzip_level = 1;
+  uint64_t gc_after = 1;               // stale series vanish this many ticks after last seen
+  std::vector<int> device_filter;      // empty = all
+  std::string trace_path;              // Chrome trace JSON of sampler stages
+  size_t trace_max_events = 200000;
+  std::string version = "0.1.0";
+};
+
+struct PodMeta {
+  std::string uid;
+  std::string ns;
+  std::string name;
+  std::vector<std::pair<std::string, std::string>> containers;  // (container_id, name)
+};
+
+struct DeviceOwner {
+  std::string ns, pod, container;
+};
+
+struct EngineStats {
+  uint64_t ticks = 0;
+  uint64_t overruns = 0;
+  uint64_t publish_skipped = 0;
+  uint64_t last_tick_ns = 0;
+  uint64_t max_tick_ns = 0;
+  uint64_t render_bytes = 0;
+  uint64_t series = 0;
+  uint64_t device_errors = 0;
+  double stage_ns[8] = {};
+  uint64_t sampler_cpu_ns = 0;
+};
+
+class Engine {
+ public:
+  explicit Engine(const EngineConfig& cfg);
+  ~Engine();
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+
+  bool start(std::string* err);
+  void stop();
+  // One tick with an injected monotonic time (manual mode / tests).
+  void tick_now(uint64_t now_ns);
+
+  SnapshotStore::Pin snapshot() { return store_.acquire(); }
+  std::string snapshot_text();
+  int http_port() const { return http_ ? http_->port() : -1; }
+  const std::vector<DeviceInfo>& devices() const { return devices_; }
+  MockBackend* mock() { return mock_; }
+  EngineStats stats();
+  const HttpStats* http_stats() const { return http_ ? &http_->stats() : nullptr; }
+  std::string source_status();
+
+  // Control-plane inputs (any thread; applied at the next tick).
+  void set_pods(std::vector<PodMeta> pods);
+  void set_device_owners(std::vector<std::pair<std::string, DeviceOwner>> owners);
+  void set_pid_cgroup(int pid, const std::string& cgroup_path);
+  void clear_pid_cgroups();
+
+  static const char* stage_name(int i);
+  static constexpr int kStages = 8;
+
+ private:
+  struct DevState {
+    DeviceSample cur, prev;
+    bool have_prev = false;
+    double xgmi_rd_rate[kMaxXgmiLinks] = {};
+    double xgmi_wr_rate[kMaxXgmiLinks] = {};
+    bool rates_valid = false;
+    DeviceOwner owner;
+    std::string owner_key;  // ns/pod/container the refs were built for
+    // cached series handles (re-upserted on owner change or GC)
+    SeriesRef info, up, gfx, umc, xcc[kMaxXcc], vram_used, vram_total, hbm_bw, power, power_cap,
+        energy, temp[9], clk[3], xrd[kMaxXgmiLinks], xwr[kMaxXgmiLinks], xrd_rate, xwr_rate,
+        links_up, pcie_bw, pcie_replay, pcie_speed, pcie_width, thr[5], nprocs, cu_occ, ctr[8],
+        sen[4];
+    uint64_t errors = 0;
+    SeriesRef err_ref;
+  };
+  struct ProcAttr {
+    std::string ns, pod, container, uid;
+  };
+
+  void define_families();
+  void run_sampler();
+  void tick_locked(uint64_t now_ns);
+  void collect_device(int i, uint64_t gen, double dt_s);
+  void emit_processes(uint64_t gen, const std::vector<std::vector<ProcSample>>& per_dev);
+  void emit_self(uint64_t gen);
+  void trace_event(const char* name, uint64_t start_ns, uint64_t dur_ns);
+  void dput(DevState& st, int dev, SeriesRef& r, int fid, const std::vector<std::string>& extra,
+            double v, uint64_t gen);
+
+  EngineConfig cfg_;
+  std::unique_ptr<Backend> backend_;
+  MockBackend* mock_ = nullptr;
+  std::vector<DeviceInfo> devices_;
+  std::vector<DevState> dstate_;
+  std::unique_ptr<KfdProcReader> kfd_;
+  std::unique_ptr<PidResolver> resolver_;
+  std::unique_ptr<SentinelSource> sentinel_;
+  std::unique_ptr<CounterSource> counters_;
+  std::unique_ptr<RcclSource> rccl_;
+  std::string sentinel_status_ = "disabled", counters_status_ = "disabled";
+
+  SeriesTable table_;
+  SnapshotStore store_;
+  std::unique_ptr<HttpServer> http_;
+  std::string render_buf_;
+
+  std::mutex tick_mu_;
+  std::thread sampler_;
+  std::atomic<bool> running_{false};
+  int stop_fd_ = -1;
+  uint64_t gen_ = 0;
+  uint64_t last_tick_now_ = 0;
+  int self_pid_ = 0;
+
+  // control plane (guarded by ctl_mu_)
+  std::mutex ctl_mu_;
+  bool ctl_dirty_ = false;
+  std::vector<PodMeta> pending_pods_;
+  std::vector<std::pair<std::string, DeviceOwner>> pending_owners_;
+  std::vector<std::pair<int, std::string>> pending_overrides_;
+  bool clear_overrides_ = false;
+  // applied (sampler thread only)
+  std::unordered_map<std::string, PodMeta> pods_by_uid_;
+  std::unordered_map<std::string, std::string> container_names_;  // cid -> name
+  std::unordered_map<std::string, DeviceOwner> owners_;           // lower(bdf|uuid) -> owner
+
+  // stats (guarded by stats_mu_)
+  std::mutex stats_mu_;
+  EngineStats stats_;
+
+  // trace
+  FILE* trace_ = nullptr;
+  size_t trace_events_ = 0;
+  uint64_t trace_t0_ = 0;
+
+  // family ids
+  int f_info_, f_up_, f_gfx_, f_umc_, f_xcc_, f_vram_used_, f_vram_total_, f_hbm_bw_, f_power_,
+      f_power_cap_, f_energy_, f_temp_, f_clk_, f_xrd_, f_xwr_, f_xrd_rate_, f_xwr_rate_,
+      f_links_up_, f_pcie_bw_, f_pcie_replay_, f_pcie_speed_, f_pcie_width_, f_thr_, f_nprocs_,
+      f_cu_occ_, f_mfma_, f_sq_busy_, f_gui_, f_waves_, f_lds_, f_lds_conf_, f_hbm_rd_,
+      f_hbm_wr_, f_sen_sclk_, f_sen_lat_, f_sen_xcc_, f_sen_runs_;
+  int f_proc_vram_, f_proc_cu_, f_proc_sdma_;
+  int f_legacy_mem_ = -1, f_legacy_perc_ = -1;
+  int f_pod_vram_, f_pod_procs_, f_pod_gpus_, f_pod_xrd_, f_pod_xwr_, f_pod_power_, f_pod_gfx_;
+  int f_rccl_calls_, f_rccl_bytes_;
+  int f_self_build_, f_self_ticks_, f_self_stage_, f_self_scrape_, f_self_scrapes_,
+      f_self_http_bytes_, f_self_render_bytes_, f_self_series_, f_self_dev_errors_,
+      f_self_overruns_, f_self_cpu_, f_self_source_up_;
+  SeriesRef self_stage_refs_[kStages];
+  uint64_t last_stage_ns_[kStages] = {};
+};
+
+}  // namespace gpuexp

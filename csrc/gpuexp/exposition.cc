@@ -1,0 +1,323 @@
+#include "gpuexp/exposition.h"
+
+#include <algorithm>
+#include <charconv>
+#include <cmath>
+#include <stdexcept>
+
+namespace gpuexp {
+
+void append_value(std::string* out, double v) {
+  if (std::isnan(v)) {
+    out->append("NaN");
+    return;
+  }
+  if (std::isinf(v)) {
+    out->append(v > 0 ? "+Inf" : "-Inf");
+    return;
+  }
+  char buf[40];
+  // Integral values (bytes, counts, PIDs) print without exponent, like Go's
+  // strconv 'g' for <1e21 only when they are short; Prometheus parses either form.
+  if (v == std::floor(v) && std::fabs(v) < 9007199254740992.0) {
+    auto r = std::to_chars(buf, buf + sizeof(buf), static_cast<long long>(v));
+    out->append(buf, r.ptr);
+    return;
+  }
+  auto r = std::to_chars(buf, buf + sizeof(buf), v);
+  out->append(buf, r.ptr);
+}
+
+void append_escaped_label_value(std::string* out, const std::string& v) {
+  for (char c : v) {
+    switch (c) {
+      case '\\': out->append("\\\\"); break;
+      case '"': out->append("\\\""); break;
+      case '\n': out->append("\\n"); break;
+      default: out->push_back(c);
+    }
+  }
+}
+
+void append_escaped_help(std::string* out, const std::string& v) {
+  for (char c : v) {
+    switch (c) {
+      case '\\': out->append("\\\\"); break;
+      case '\n': out->append("\\n"); break;
+      default: out->push_back(c);
+    }
+  }
+}
+
+static bool name_ok(const std::string& s, bool allow_colon) {
+  if (s.empty()) return false;
+  for (size_t i = 0; i < s.size(); ++i) {
+    char c = s[i];
+    bool alpha = (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || c == '_' ||
+                 (allow_colon && c == ':');
+    bool digit = c >= '0' && c <= '9';
+    if (!(alpha || (i > 0 && digit))) return false;
+  }
+  return true;
+}
+
+bool valid_metric_name(const std::string& s) { return name_ok(s, true); }
+bool valid_label_name(const std::string& s) {
+  return name_ok(s, false) && !(s.size() >= 2 && s[0] == '_' && s[1] == '_');
+}
+
+int SeriesTable::add_family(const FamilyDef& def) {
+  if (!valid_metric_name(def.name)) throw std::invalid_argument("bad metric name: " + def.name);
+  for (auto& l : def.label_names)
+    if (!valid_label_name(l)) throw std::invalid_argument("bad label name: " + l);
+  if (family_id(def.name) >= 0) throw std::invalid_argument("duplicate family: " + def.name);
+  Family f;
+  f.def = def;
+  f.header = "# HELP " + def.name + " ";
+  append_escaped_help(&f.header, def.help);
+  static const char* tn[] = {"gauge", "counter", "histogram"};
+  f.header += "\n# TYPE " + def.name + " " + tn[int(def.type)] + "\n";
+  families_.push_back(std::move(f));
+  int fid = int(families_.size() - 1);
+  render_order_.push_back(fid);
+  std::sort(render_order_.begin(), render_order_.end(), [this](int a, int b) {
+    return families_[size_t(a)].def.name < families_[size_t(b)].def.name;
+  });
+  return fid;
+}
+
+int SeriesTable::family_id(const std::string& name) const {
+  for (size_t i = 0; i < families_.size(); ++i)
+    if (families_[i].def.name == name) return int(i);
+  return -1;
+}
+
+SeriesRef SeriesTable::upsert(int fid, const std::vector<std::string>& values) {
+  Family& fam = families_.at(size_t(fid));
+  if (values.size() != fam.def.label_names.size())
+    throw std::invalid_argument("label arity mismatch for " + fam.def.name);
+  keybuf_.clear();
+  keybuf_.append(reinterpret_cast<const char*>(&fid), sizeof(fid));
+  for (auto& v : values) {
+    keybuf_.append(v);
+    keybuf_.push_back('\0');
+  }
+  auto it = index_.find(keybuf_);
+  if (it != index_.end()) return SeriesRef{it->second, series_[it->second].ver};
+
+  uint32_t idx;
+  if (!free_.empty()) {
+    idx = free_.back();
+    free_.pop_back();
+  } else {
+    idx = uint32_t(series_.size());
+    series_.emplace_back();
+  }
+  Series& s = series_[idx];
+  s.fid = fid;
+  s.ver += 1;
+  s.gen = 0;
+  s.value = 0;
+  s.labels = values;
+  s.key = keybuf_;
+  s.bounds.clear();
+  s.buckets.clear();
+  s.hsum = 0;
+  s.hcount = 0;
+  s.prefix = fam.def.name;
+  if (!values.empty()) {
+    s.prefix.push_back('{');
+    for (size_t i = 0; i < values.size(); ++i) {
+      if (i) s.prefix.push_back(',');
+      s.prefix.append(fam.def.label_names[i]);
+      s.prefix.append("=\"");
+      append_escaped_label_value(&s.prefix, values[i]);
+      s.prefix.push_back('"');
+    }
+    s.prefix.push_back('}');
+  }
+  index_.emplace(s.key, idx);
+  fam.members.push_back(idx);
+  fam.dirty_order = true;
+  return SeriesRef{idx, s.ver};
+}
+
+bool SeriesTable::set(SeriesRef r, double v, uint64_t gen) {
+  if (!r.valid() || r.idx >= series_.size()) return false;
+  Series& s = series_[r.idx];
+  if (s.ver != r.ver || s.fid < 0) return false;
+  s.value = v;
+  s.gen = gen;
+  return true;
+}
+
+bool SeriesTable::touch(SeriesRef r, uint64_t gen) {
+  if (!r.valid() || r.idx >= series_.size()) return false;
+  Series& s = series_[r.idx];
+  if (s.ver != r.ver || s.fid < 0) return false;
+  s.gen = gen;
+  return true;
+}
+
+bool SeriesTable::observe(SeriesRef r, double v, uint64_t gen, const std::vector<double>& bounds) {
+  if (!r.valid() || r.idx >= series_.size()) return false;
+  Series& s = series_[r.idx];
+  if (s.ver != r.ver || s.fid < 0) return false;
+  if (s.bounds.empty()) {
+    s.bounds = bounds;
+    s.buckets.assign(bounds.size(), 0);
+  }
+  // Buckets are stored non-cumulative; rendering accumulates.
+  auto it = std::lower_bound(s.bounds.begin(), s.bounds.end(), v);
+  if (it != s.bounds.end()) s.buckets[size_t(it - s.bounds.begin())] += 1;
+  s.hsum += v;
+  s.hcount += 1;
+  s.gen = gen;
+  return true;
+}
+
+bool SeriesTable::set_histogram(SeriesRef r, const std::vector<double>& bounds,
+                                const std::vector<uint64_t>& counts, double sum, uint64_t count,
+                                uint64_t gen) {
+  if (!r.valid() || r.idx >= series_.size()) return false;
+  Series& s = series_[r.idx];
+  if (s.ver != r.ver || s.fid < 0) return false;
+  s.bounds = bounds;
+  s.buckets.assign(bounds.size(), 0);
+  for (size_t i = 0; i < bounds.size() && i < counts.size(); ++i) s.buckets[i] = counts[i];
+  s.hsum = sum;
+  s.hcount = count;
+  s.gen = gen;
+  return true;
+}
+
+double SeriesTable::value(SeriesRef r) const {
+  if (!r.valid() || r.idx >= series_.size()) return std::nan("");
+  const Series& s = series_[r.idx];
+  if (s.ver != r.ver) return std::nan("");
+  return s.value;
+}
+
+void SeriesTable::free_series(uint32_t idx) {
+  Series& s = series_[idx];
+  index_.erase(s.key);
+  s.fid = -1;
+  s.ver += 1;
+  s.labels.clear();
+  s.prefix.clear();
+  s.key.clear();
+  s.bounds.clear();
+  s.buckets.clear();
+  free_.push_back(idx);
+}
+
+void SeriesTable::sort_members(Family& f) {
+  std::sort(f.members.begin(), f.members.end(), [this](uint32_t a, uint32_t b) {
+    const auto& la = series_[a].labels;
+    const auto& lb = series_[b].labels;
+    for (size_t i = 0; i < la.size(); ++i) {
+      if (la[i] != lb[i]) {
+        // numeric-aware ordering so gpu="10" sorts after gpu="9"
+        bool da = !la[i].empty() && la[i].find_first_not_of("0123456789") == std::string::npos;
+        bool db = !lb[i].empty() && lb[i].find_first_not_of("0123456789") == std::string::npos;
+        if (da && db && la[i].size() != lb[i].size()) return la[i].size() < lb[i].size();
+        return la[i] < lb[i];
+      }
+    }
+    return false;
+  });
+  f.dirty_order = false;
+}
+
+void SeriesTable::render_histogram(std::string* out, const Series& s) const {
+  const Family& fam = families_[size_t(s.fid)];
+  // name_bucket{labels,le="x"} cumulative
+  std::string base = fam.def.name;
+  std::string labels;  // `a="x",b="y"`
+  if (s.prefix.size() > base.size() + 2) labels = s.prefix.substr(base.size() + 1, s.prefix.size() - base.size() - 2);
+  uint64_t cum = 0;
+  for (size_t i = 0; i <= s.bounds.size(); ++i) {
+    out->append(base);
+    out->append("_bucket{");
+    if (!labels.empty()) {
+      out->append(labels);
+      out->push_back(',');
+    }
+    out->append("le=\"");
+    if (i < s.bounds.size()) {
+      cum += s.buckets[i];
+      append_value(out, s.bounds[i]);
+    } else {
+      cum = s.hcount;
+      out->append("+Inf");
+    }
+    out->append("\"} ");
+    append_value(out, double(cum));
+    out->push_back('\n');
+  }
+  const char* sfx[2] = {"_sum", "_count"};
+  for (int k = 0; k < 2; ++k) {
+    out->append(base);
+    out->append(sfx[k]);
+    if (!labels.empty()) {
+      out->push_back('{');
+      out->append(labels);
+      out->push_back('}');
+    }
+    out->push_back(' ');
+    append_value(out, k == 0 ? s.hsum : double(s.hcount));
+    out->push_back('\n');
+  }
+}
+
+void SeriesTable::render(std::string* out, uint64_t gen, uint64_t gc_after) {
+  out->clear();
+  for (int fid : render_order_) {
+    Family& fam = families_[size_t(fid)];
+    // GC pass: drop members that have been stale for longer than gc_after gens.
+    bool any_live = false;
+    size_t w = 0;
+    for (size_t i = 0; i < fam.members.size(); ++i) {
+      uint32_t idx = fam.members[i];
+      Series& s = series_[idx];
+      if (s.gen + gc_after < gen) {
+        free_series(idx);
+        continue;
+      }
+      fam.members[w++] = idx;
+      if (s.gen == gen) any_live = true;
+    }
+    fam.members.resize(w);
+    if (!any_live) continue;
+    if (fam.dirty_order) sort_members(fam);
+    out->append(fam.header);
+    for (uint32_t idx : fam.members) {
+      const Series& s = series_[idx];
+      if (s.gen != gen) continue;
+      if (fam.def.type == MetricType::kHistogram) {
+        render_histogram(out, s);
+        continue;
+      }
+      out->append(s.prefix);
+      out->push_back(' ');
+      append_value(out, s.value);
+      out->push_back('\n');
+    }
+  }
+}
+
+size_t SeriesTable::live_series(uint64_t gen) const {
+  size_t n = 0;
+  for (auto& s : series_)
+    if (s.fid >= 0 && s.gen == gen) ++n;
+  return n;
+}
+
+size_t SeriesTable::live_series_in_family(int fid, uint64_t gen) const {
+  size_t n = 0;
+  for (uint32_t idx : families_[size_t(fid)].members)
+    if (series_[idx].gen == gen) ++n;
+  return n;
+}
+
+}  // namespace gpuexp

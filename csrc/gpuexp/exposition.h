@@ -1,0 +1,112 @@
+// Prometheus text-format 0.0.4 series table + renderer.
+//
+// Reference: two client_golang GaugeVecs registered on a custom registry
+// (/root/reference/main.go:21-36, :40-42) rendered by promhttp on every scrape
+// (main.go:68-70).  Here every series owns a pre-rendered `name{labels} ` prefix that is
+// built once when the label set is interned; a tick only formats numbers, and the
+// result is published as an immutable snapshot that scrapes copy out with writev().
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace gpuexp {
+
+enum class MetricType : uint8_t { kGauge = 0, kCounter = 1, kHistogram = 2 };
+
+struct FamilyDef {
+  std::string name;
+  std::string help;
+  MetricType type = MetricType::kGauge;
+  std::vector<std::string> label_names;
+};
+
+// Versioned handle: a slot freed by GC and reused for another label set bumps its
+// version, so a stale cached handle is detected instead of writing a wrong series.
+struct SeriesRef {
+  uint32_t idx = UINT32_MAX;
+  uint32_t ver = 0;
+  bool valid() const { return idx != UINT32_MAX; }
+};
+
+// Appends `v` in the shortest round-trip form ("NaN", "+Inf", "-Inf" for specials;
+// integers without exponent up to 2^53).
+void append_value(std::string* out, double v);
+void append_escaped_label_value(std::string* out, const std::string& v);
+void append_escaped_help(std::string* out, const std::string& v);
+bool valid_metric_name(const std::string& s);
+bool valid_label_name(const std::string& s);
+
+class SeriesTable {
+ public:
+  // Families render sorted by name (client_golang's Gather order).
+  int add_family(const FamilyDef& def);
+  int family_id(const std::string& name) const;
+  const FamilyDef& family(int fid) const { return families_[size_t(fid)].def; }
+  size_t num_families() const { return families_.size(); }
+
+  // Interns (family, label values) and returns a handle.  Slow path (hashing); callers
+  // cache handles for series that persist across ticks.
+  SeriesRef upsert(int fid, const std::vector<std::string>& values);
+  // Sets a gauge/counter value and marks the series live for generation `gen`.
+  // Returns false if the handle went stale (caller must re-upsert).
+  bool set(SeriesRef r, double v, uint64_t gen);
+  // Histogram observation (cumulative; `bounds` fixed at first use).
+  bool observe(SeriesRef r, double v, uint64_t gen, const std::vector<double>& bounds);
+  // Marks a histogram series live without a new observation.
+  bool touch(SeriesRef r, uint64_t gen);
+  // Replaces a histogram's state wholesale (non-cumulative bucket counts; the last
+  // entry of `counts` is the +Inf overflow and is implied by `count`).
+  bool set_histogram(SeriesRef r, const std::vector<double>& bounds,
+                     const std::vector<uint64_t>& counts, double sum, uint64_t count, uint64_t gen);
+
+  // Convenience: upsert + set.
+  void put(int fid, const std::vector<std::string>& values, double v, uint64_t gen) {
+    set(upsert(fid, values), v, gen);
+  }
+
+  // Renders every series that is live at `gen`.  Series not live for more than
+  // `gc_after` generations are freed (stale-series GC; the reference never Reset() its
+  // vectors, main.go:147-150, so exited PIDs stayed forever).
+  void render(std::string* out, uint64_t gen, uint64_t gc_after = 1);
+
+  size_t live_series(uint64_t gen) const;
+  size_t live_series_in_family(int fid, uint64_t gen) const;
+  double value(SeriesRef r) const;
+
+ private:
+  struct Series {
+    int fid = -1;
+    uint32_t ver = 0;
+    uint64_t gen = 0;  // last generation it was set
+    double value = 0;
+    std::vector<std::string> labels;
+    std::string prefix;       // `name{a="x",b="y"}` (no trailing space)
+    std::string key;          // interning key
+    // histogram state
+    std::vector<double> bounds;
+    std::vector<uint64_t> buckets;
+    double hsum = 0;
+    uint64_t hcount = 0;
+  };
+  struct Family {
+    FamilyDef def;
+    std::string header;              // "# HELP ...\n# TYPE ...\n"
+    std::vector<uint32_t> members;   // sorted by label values
+    bool dirty_order = false;
+  };
+  void free_series(uint32_t idx);
+  void sort_members(Family& f);
+  void render_histogram(std::string* out, const Series& s) const;
+
+  std::vector<Family> families_;
+  std::vector<int> render_order_;  // family ids sorted by name
+  std::vector<Series> series_;
+  std::vector<uint32_t> free_;
+  std::unordered_map<std::string, uint32_t> index_;
+  std::string keybuf_;
+};
+
+}  // namespace gpuexp

@@ -1,0 +1,114 @@
+#include "gpuexp/gpu_metrics.h"
+
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <cstring>
+
+namespace gpuexp {
+
+namespace {
+inline double u16v(uint16_t v) { return v == 0xFFFF ? kNaN : double(v); }
+}  // namespace
+
+bool decode_gpu_metrics_v1_8(const void* blob, size_t len, DeviceSample* out) {
+  if (len < sizeof(GpuMetricsV1_8)) return false;
+  GpuMetricsV1_8 m;
+  std::memcpy(&m, blob, sizeof(m));
+  if (m.header.format_revision != 1 || m.header.content_revision != 8) return false;
+  out->temp_hotspot = u16v(m.temperature_hotspot);
+  out->temp_mem = u16v(m.temperature_mem);
+  out->temp_vrsoc = u16v(m.temperature_vrsoc);
+  out->power_w = u16v(m.curr_socket_power);
+  out->gfx_activity = u16v(m.average_gfx_activity);
+  out->umc_activity = u16v(m.average_umc_activity);
+  out->vram_max_bw_gbs = m.mem_max_bandwidth == ~0ull ? kNaN : double(m.mem_max_bandwidth);
+  out->energy_valid = m.energy_accumulator != ~0ull;
+  out->energy_acc = m.energy_accumulator;
+  out->energy_unit_j = 15.259e-6;
+  out->residency_valid = m.accumulation_counter != 0xFFFFFFFFu;
+  out->accumulation_counter = m.accumulation_counter;
+  out->res_prochot = m.prochot_residency_acc;
+  out->res_ppt = m.ppt_residency_acc;
+  out->res_socket_thm = m.socket_thm_residency_acc;
+  out->res_vr_thm = m.vr_thm_residency_acc;
+  out->res_hbm_thm = m.hbm_thm_residency_acc;
+  out->pcie_width = u16v(m.pcie_link_width);
+  out->pcie_speed_gts = m.pcie_link_speed == 0xFFFF ? kNaN : m.pcie_link_speed / 10.0;
+  out->pcie_bw_acc = m.pcie_bandwidth_acc;
+  out->pcie_bw_inst = m.pcie_bandwidth_inst == ~0ull ? kNaN : double(m.pcie_bandwidth_inst);
+  out->pcie_replay = m.pcie_replay_count_acc == ~0ull ? kNaN : double(m.pcie_replay_count_acc);
+  int nl = 0;
+  for (int l = 0; l < kMaxXgmiLinks; ++l) {
+    out->xgmi_read_kb[l] = m.xgmi_read_data_acc[l] == ~0ull ? 0 : m.xgmi_read_data_acc[l];
+    out->xgmi_write_kb[l] = m.xgmi_write_data_acc[l] == ~0ull ? 0 : m.xgmi_write_data_acc[l];
+    out->xgmi_link_up[l] = m.xgmi_link_status[l] == 0xFFFF ? kNaN : double(m.xgmi_link_status[l] ? 1 : 0);
+    if (m.xgmi_link_status[l] != 0xFFFF) nl = l + 1;
+  }
+  out->num_xgmi_links = nl;
+  out->xgmi_valid = true;
+  out->fw_ts_10ns = m.firmware_timestamp == ~0ull ? 0 : m.firmware_timestamp;
+  // Per-XCC gfx clocks: report the mean of the valid instances.
+  double sum = 0;
+  int n = 0;
+  for (int i = 0; i < 8; ++i)
+    if (m.current_gfxclk[i] != 0xFFFF && m.current_gfxclk[i] != 0) {
+      sum += m.current_gfxclk[i];
+      ++n;
+    }
+  out->clk_gfx = n ? sum / n : kNaN;
+  out->clk_soc = u16v(m.current_socclk[0]);
+  out->clk_mem = u16v(m.current_uclk);
+  for (int c = 0; c < kMaxXcc; ++c) out->gfx_busy_acc[c] = m.xcp_stats[0].gfx_busy_acc[c];
+  return true;
+}
+
+GpuMetricsReader::~GpuMetricsReader() {
+  if (fd_ >= 0) ::close(fd_);
+}
+
+bool GpuMetricsReader::open(const std::string& path, std::string* err) {
+  if (fd_ >= 0) ::close(fd_);
+  path_ = path;
+  fd_ = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd_ < 0) {
+    *err = "open " + path + " failed";
+    return false;
+  }
+  long n = pread_all(fd_, reinterpret_cast<char*>(buf_), sizeof(buf_));
+  if (n < long(sizeof(GpuMetricsHeader))) {
+    *err = "short gpu_metrics read";
+    ::close(fd_);
+    fd_ = -1;
+    return false;
+  }
+  auto* h = reinterpret_cast<const GpuMetricsHeader*>(buf_);
+  fmt_ = h->format_revision;
+  content_ = h->content_revision;
+  if (!(fmt_ == 1 && content_ == 8)) {
+    *err = "unsupported gpu_metrics format " + std::to_string(fmt_) + "." + std::to_string(content_);
+    ::close(fd_);
+    fd_ = -1;
+    return false;
+  }
+  return true;
+}
+
+bool GpuMetricsReader::read(DeviceSample* out) {
+  if (fd_ < 0) {
+    out->error = "gpu_metrics not open";
+    return false;
+  }
+  long n = pread_all(fd_, reinterpret_cast<char*>(buf_), sizeof(buf_));
+  if (n <= 0) {
+    out->error = "gpu_metrics read failed";
+    return false;
+  }
+  if (!decode_gpu_metrics_v1_8(buf_, size_t(n), out)) {
+    out->error = "gpu_metrics decode failed";
+    return false;
+  }
+  return true;
+}
+
+}  // namespace gpuexp

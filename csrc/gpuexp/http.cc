@@ -1,0 +1,431 @@
+#include "gpuexp/http.h"
+
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <sys/uio.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstring>
+#include <unordered_map>
+
+#include "gpuexp/common.h"
+
+namespace gpuexp {
+
+const std::vector<double>& scrape_latency_bounds() {
+  static const std::vector<double> b = {5e-6,  10e-6, 25e-6, 50e-6, 100e-6, 250e-6,
+                                        500e-6, 1e-3,  2.5e-3, 5e-3, 10e-3, 25e-3,
+                                        50e-3, 100e-3, 250e-3, 1.0};
+  return b;
+}
+
+void HttpStats::record_latency(uint64_t ns) {
+  const auto& b = scrape_latency_bounds();
+  double s = double(ns) * 1e-9;
+  int i = 0;
+  while (i < kBuckets && s > b[size_t(i)]) ++i;
+  lat_buckets[i].fetch_add(1, std::memory_order_relaxed);
+  lat_sum_ns.fetch_add(ns, std::memory_order_relaxed);
+  lat_count.fetch_add(1, std::memory_order_relaxed);
+}
+
+namespace {
+
+struct Conn {
+  int fd = -1;
+  std::string in;
+  std::string head;
+  SnapshotStore::Pin pin;
+  const char* body = nullptr;
+  size_t body_len = 0;
+  std::string owned_body;  // small non-snapshot bodies
+  size_t sent = 0;         // bytes of head+body already written
+  bool pending = false;
+  bool close_after = false;
+  bool is_metrics = false;
+  uint64_t last_active_ns = 0;
+  uint64_t req_start_ns = 0;
+};
+
+bool ieq_prefix(const char* a, size_t alen, const char* b) {
+  size_t bl = std::strlen(b);
+  if (alen < bl) return false;
+  for (size_t i = 0; i < bl; ++i) {
+    char x = a[i], y = b[i];
+    if (x >= 'A' && x <= 'Z') x = char(x - 'A' + 'a');
+    if (y >= 'A' && y <= 'Z') y = char(y - 'A' + 'a');
+    if (x != y) return false;
+  }
+  return true;
+}
+
+bool contains_token(const char* s, size_t n, const char* tok) {
+  size_t tl = std::strlen(tok);
+  for (size_t i = 0; i + tl <= n; ++i)
+    if (ieq_prefix(s + i, n - i, tok)) return true;
+  return false;
+}
+
+}  // namespace
+
+struct HttpServer::Worker {
+  int listen_fd = -1;
+  int epfd = -1;
+  int stopfd = -1;
+  std::thread th;
+  std::unordered_map<int, Conn> conns;
+};
+
+HttpServer::HttpServer(SnapshotStore* store, const HttpConfig& cfg) : store_(store), cfg_(cfg) {}
+
+HttpServer::~HttpServer() { stop(); }
+
+static int make_listener(const std::string& host, int port, bool reuseport, std::string* err) {
+  int fd = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+  if (fd < 0) {
+    *err = std::string("socket: ") + std::strerror(errno);
+    return -1;
+  }
+  int one = 1;
+  ::setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  if (reuseport) ::setsockopt(fd, SOL_SOCKET, SO_REUSEPORT, &one, sizeof(one));
+  sockaddr_in addr{};
+  addr.sin_family = AF_INET;
+  addr.sin_port = htons(uint16_t(port));
+  std::string h = host.empty() ? "0.0.0.0" : host;
+  if (::inet_pton(AF_INET, h.c_str(), &addr.sin_addr) != 1) {
+    *err = "bad listen host: " + h;
+    ::close(fd);
+    return -1;
+  }
+  if (::bind(fd, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) < 0) {
+    *err = "bind " + h + ":" + std::to_string(port) + ": " + std::strerror(errno);
+    ::close(fd);
+    return -1;
+  }
+  if (::listen(fd, 1024) < 0) {
+    *err = std::string("listen: ") + std::strerror(errno);
+    ::close(fd);
+    return -1;
+  }
+  return fd;
+}
+
+bool HttpServer::start(std::string* err) {
+  if (running_.load()) return true;
+  int nthreads = std::max(1, cfg_.threads);
+  int port = cfg_.port;
+  for (int t = 0; t < nthreads; ++t) {
+    auto w = std::make_unique<Worker>();
+    w->listen_fd = make_listener(cfg_.host, port, nthreads > 1, err);
+    if (w->listen_fd < 0) {
+      stop();
+      return false;
+    }
+    if (t == 0) {
+      sockaddr_in a{};
+      socklen_t al = sizeof(a);
+      ::getsockname(w->listen_fd, reinterpret_cast<sockaddr*>(&a), &al);
+      bound_port_ = ntohs(a.sin_port);
+      port = bound_port_;
+    }
+    w->epfd = ::epoll_create1(EPOLL_CLOEXEC);
+    w->stopfd = ::eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.fd = w->listen_fd;
+    ::epoll_ctl(w->epfd, EPOLL_CTL_ADD, w->listen_fd, &ev);
+    ev.data.fd = w->stopfd;
+    ::epoll_ctl(w->epfd, EPOLL_CTL_ADD, w->stopfd, &ev);
+    workers_.push_back(std::move(w));
+  }
+  running_.store(true);
+  for (auto& w : workers_) {
+    Worker* wp = w.get();
+    wp->th = std::thread([this, wp] { run(wp); });
+  }
+  return true;
+}
+
+void HttpServer::stop() {
+  for (auto& w : workers_) {
+    if (w->stopfd >= 0) {
+      uint64_t one = 1;
+      ssize_t r = ::write(w->stopfd, &one, sizeof(one));
+      (void)r;
+    }
+  }
+  for (auto& w : workers_) {
+    if (w->th.joinable()) w->th.join();
+    for (auto& kv : w->conns) ::close(kv.first);
+    w->conns.clear();
+    if (w->listen_fd >= 0) ::close(w->listen_fd);
+    if (w->epfd >= 0) ::close(w->epfd);
+    if (w->stopfd >= 0) ::close(w->stopfd);
+  }
+  workers_.clear();
+  running_.store(false);
+}
+
+void HttpServer::run(Worker* w) {
+  constexpr int kMaxEvents = 256;
+  epoll_event events[kMaxEvents];
+  char rbuf[16384];
+  uint64_t last_sweep = mono_ns();
+
+  auto close_conn = [&](int fd) {
+    ::epoll_ctl(w->epfd, EPOLL_CTL_DEL, fd, nullptr);
+    ::close(fd);
+    w->conns.erase(fd);
+    stats_.open_conns.fetch_sub(1, std::memory_order_relaxed);
+  };
+
+  // Writes as much of the pending response as the socket takes.  Returns false if the
+  // connection must be closed.
+  auto flush = [&](Conn& c) -> bool {
+    while (c.pending) {
+      size_t hl = c.head.size();
+      iovec iov[2];
+      int n = 0;
+      if (c.sent < hl) {
+        iov[n].iov_base = const_cast<char*>(c.head.data() + c.sent);
+        iov[n].iov_len = hl - c.sent;
+        ++n;
+        if (c.body_len) {
+          iov[n].iov_base = const_cast<char*>(c.body);
+          iov[n].iov_len = c.body_len;
+          ++n;
+        }
+      } else {
+        size_t off = c.sent - hl;
+        iov[n].iov_base = const_cast<char*>(c.body + off);
+        iov[n].iov_len = c.body_len - off;
+        ++n;
+      }
+      ssize_t wr = ::writev(c.fd, iov, n);
+      if (wr < 0) {
+        if (errno == EINTR) continue;
+        if (errno == EAGAIN || errno == EWOULDBLOCK) {
+          epoll_event ev{};
+          ev.events = EPOLLIN | EPOLLOUT;
+          ev.data.fd = c.fd;
+          ::epoll_ctl(w->epfd, EPOLL_CTL_MOD, c.fd, &ev);
+          return true;
+        }
+        stats_.errors.fetch_add(1, std::memory_order_relaxed);
+        return false;
+      }
+      c.sent += size_t(wr);
+      stats_.bytes_sent.fetch_add(uint64_t(wr), std::memory_order_relaxed);
+      if (c.sent >= hl + c.body_len) {
+        c.pending = false;
+        if (c.is_metrics) stats_.record_latency(mono_ns() - c.req_start_ns);
+        c.pin.release();
+        c.owned_body.clear();
+        c.body = nullptr;
+        c.body_len = 0;
+        epoll_event ev{};
+        ev.events = EPOLLIN;
+        ev.data.fd = c.fd;
+        ::epoll_ctl(w->epfd, EPOLL_CTL_MOD, c.fd, &ev);
+        if (c.close_after) return false;
+      }
+    }
+    return true;
+  };
+
+  auto respond_simple = [&](Conn& c, int code, const char* reason, const std::string& ctype,
+                            std::string body, bool head_only) {
+    c.owned_body = std::move(body);
+    c.head = "HTTP/1.1 " + std::to_string(code) + " " + reason + "\r\nContent-Type: " + ctype +
+             "\r\nContent-Length: " + std::to_string(c.owned_body.size()) + "\r\n" +
+             (c.close_after ? "Connection: close\r\n" : "") + "\r\n";
+    c.body = head_only ? nullptr : c.owned_body.data();
+    c.body_len = head_only ? 0 : c.owned_body.size();
+    c.sent = 0;
+    c.pending = true;
+    c.is_metrics = false;
+  };
+
+  // Parses and answers every complete request in the input buffer (in order; a
+  // pipelined request waits until the previous response is fully written).
+  auto handle_input = [&](Conn& c) -> bool {
+    while (!c.pending) {
+      size_t end = c.in.find("\r\n\r\n");
+      if (end == std::string::npos) {
+        if (c.in.size() > 16384) return false;  // header too large
+        return true;
+      }
+      uint64_t t0 = mono_ns();
+      const char* p = c.in.data();
+      size_t hdr_len = end + 4;
+      size_t le = c.in.find("\r\n");
+      std::string line(p, le);
+      size_t s1 = line.find(' ');
+      size_t s2 = line.find(' ', s1 == std::string::npos ? 0 : s1 + 1);
+      std::string method, target, version;
+      if (s1 != std::string::npos && s2 != std::string::npos) {
+        method = line.substr(0, s1);
+        target = line.substr(s1 + 1, s2 - s1 - 1);
+        version = line.substr(s2 + 1);
+      }
+      bool http10 = version == "HTTP/1.0";
+      bool want_gzip = false, conn_close = http10, conn_keep = false;
+      uint64_t content_len = 0;
+      size_t pos = le + 2;
+      while (pos < end) {
+        size_t nl = c.in.find("\r\n", pos);
+        if (nl == std::string::npos || nl > end) nl = end;
+        const char* h = p + pos;
+        size_t hn = nl - pos;
+        if (ieq_prefix(h, hn, "accept-encoding:")) {
+          want_gzip = contains_token(h + 16, hn - 16, "gzip");
+        } else if (ieq_prefix(h, hn, "connection:")) {
+          if (contains_token(h + 11, hn - 11, "close")) conn_close = true;
+          if (contains_token(h + 11, hn - 11, "keep-alive")) conn_keep = true;
+        } else if (ieq_prefix(h, hn, "content-length:")) {
+          parse_u64(h + 15, hn - 15, &content_len);
+        }
+        pos = nl + 2;
+      }
+      if (content_len > 1 << 20) return false;
+      if (c.in.size() < hdr_len + content_len) return true;  // wait for body
+      c.in.erase(0, hdr_len + size_t(content_len));
+      stats_.requests.fetch_add(1, std::memory_order_relaxed);
+      c.close_after = conn_close && !(http10 && conn_keep);
+      c.req_start_ns = t0;
+
+      size_t q = target.find('?');
+      std::string path = q == std::string::npos ? target : target.substr(0, q);
+      bool is_head = method == "HEAD";
+      if (method.empty()) {
+        c.close_after = true;
+        respond_simple(c, 400, "Bad Request", "text/plain", "bad request\n", false);
+      } else if (method != "GET" && !is_head) {
+        respond_simple(c, 405, "Method Not Allowed", "text/plain", "method not allowed\n", false);
+      } else if (path == cfg_.metrics_path) {
+        stats_.metrics_requests.fetch_add(1, std::memory_order_relaxed);
+        SnapshotStore::Pin pin = store_->acquire();
+        if (!pin) {
+          respond_simple(c, 503, "Service Unavailable", "text/plain", "no sample yet\n", is_head);
+        } else {
+          if (want_gzip && cfg_.enable_gzip) gzip_wanted_ns_.store(t0, std::memory_order_relaxed);
+          bool gz = want_gzip && cfg_.enable_gzip && !pin->gz.empty();
+          const std::string& b = gz ? pin->gz : pin->body;
+          c.head.clear();
+          c.head.append("HTTP/1.1 200 OK\r\nContent-Type: text/plain; version=0.0.4; charset=utf-8\r\n");
+          if (gz) {
+            c.head.append("Content-Encoding: gzip\r\n");
+            stats_.gzip_responses.fetch_add(1, std::memory_order_relaxed);
+          }
+          c.head.append("Content-Length: ");
+          c.head.append(std::to_string(b.size()));
+          c.head.append(c.close_after ? "\r\nConnection: close\r\n\r\n" : "\r\n\r\n");
+          c.body = is_head ? nullptr : b.data();
+          c.body_len = is_head ? 0 : b.size();
+          c.pin = std::move(pin);
+          c.sent = 0;
+          c.pending = true;
+          c.is_metrics = true;
+        }
+      } else if (path == "/healthz") {
+        respond_simple(c, 200, "OK", "text/plain", "ok\n", is_head);
+      } else if (path == "/readyz") {
+        if (ready_.load())
+          respond_simple(c, 200, "OK", "text/plain", "ready\n", is_head);
+        else
+          respond_simple(c, 503, "Service Unavailable", "text/plain", "not ready\n", is_head);
+      } else if (path == "/") {
+        respond_simple(c, 200, "OK", "text/html",
+                       "<html><head><title>MI355X GPU exporter</title></head><body>"
+                       "<h1>MI355X per-pod GPU exporter</h1><p><a href=\"" + cfg_.metrics_path +
+                           "\">Metrics</a></p></body></html>\n",
+                       is_head);
+      } else {
+        respond_simple(c, 404, "Not Found", "text/plain", "not found\n", is_head);
+      }
+      if (!flush(c)) return false;
+    }
+    return true;
+  };
+
+  for (;;) {
+    int n = ::epoll_wait(w->epfd, events, kMaxEvents, 1000);
+    if (n < 0 && errno != EINTR) break;
+    bool stopping = false;
+    for (int i = 0; i < n; ++i) {
+      int fd = events[i].data.fd;
+      if (fd == w->stopfd) {
+        stopping = true;
+        continue;
+      }
+      if (fd == w->listen_fd) {
+        for (;;) {
+          int cfd = ::accept4(w->listen_fd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+          if (cfd < 0) break;
+          if (int(w->conns.size()) >= cfg_.max_conns) {
+            ::close(cfd);
+            stats_.errors.fetch_add(1, std::memory_order_relaxed);
+            continue;
+          }
+          int one = 1;
+          ::setsockopt(cfd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+          Conn& c = w->conns[cfd];
+          c.fd = cfd;
+          c.last_active_ns = mono_ns();
+          epoll_event ev{};
+          ev.events = EPOLLIN;
+          ev.data.fd = cfd;
+          ::epoll_ctl(w->epfd, EPOLL_CTL_ADD, cfd, &ev);
+          stats_.accepted.fetch_add(1, std::memory_order_relaxed);
+          stats_.open_conns.fetch_add(1, std::memory_order_relaxed);
+        }
+        continue;
+      }
+      auto it = w->conns.find(fd);
+      if (it == w->conns.end()) continue;
+      Conn& c = it->second;
+      c.last_active_ns = mono_ns();
+      bool ok = true;
+      if (events[i].events & (EPOLLERR | EPOLLHUP)) ok = false;
+      if (ok && (events[i].events & EPOLLOUT)) ok = flush(c);
+      if (ok && (events[i].events & EPOLLIN)) {
+        for (;;) {
+          ssize_t r = ::read(fd, rbuf, sizeof(rbuf));
+          if (r > 0) {
+            c.in.append(rbuf, size_t(r));
+            if (size_t(r) < sizeof(rbuf)) break;
+            continue;
+          }
+          if (r == 0) ok = false;
+          else if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) ok = false;
+          break;
+        }
+        if (ok || !c.in.empty()) {
+          bool hok = handle_input(c);
+          ok = ok && hok;
+        }
+      }
+      if (!ok) close_conn(fd);
+    }
+    if (stopping) break;
+    uint64_t now = mono_ns();
+    if (now - last_sweep > 1000000000ull) {
+      last_sweep = now;
+      std::vector<int> idle;
+      for (auto& kv : w->conns)
+        if (now - kv.second.last_active_ns > uint64_t(cfg_.idle_timeout_ms) * 1000000ull)
+          idle.push_back(kv.first);
+      for (int fd : idle) close_conn(fd);
+    }
+  }
+}
+
+}  // namespace gpuexp

@@ -1,0 +1,81 @@
+// Minimal epoll HTTP/1.1 server for /metrics, /healthz, /readyz.
+//
+// Reference: `http.Handle("/metrics", promhttp.HandlerFor(reg, ...))` +
+// `ListenAndServe(":8000")` in a goroutine (/root/reference/main.go:67-72), fatal on
+// bind error.  Here: one (or N, SO_REUSEPORT) event-loop thread(s) that never render —
+// a request pins the current snapshot and writev()s pre-built bytes, so scrape latency
+// is O(bytes) and independent of GPU I/O.
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "gpuexp/snapshot.h"
+
+namespace gpuexp {
+
+struct HttpConfig {
+  std::string host = "0.0.0.0";
+  int port = 8000;                     // main.go:71 ":8000"; 0 = ephemeral
+  std::string metrics_path = "/metrics";  // main.go:70
+  int threads = 1;
+  int max_conns = 4096;
+  int idle_timeout_ms = 120000;
+  bool enable_gzip = true;
+};
+
+// Fixed latency buckets (seconds) for gpuexp_scrape_duration_seconds.
+const std::vector<double>& scrape_latency_bounds();
+
+struct HttpStats {
+  static constexpr int kBuckets = 16;
+  std::atomic<uint64_t> requests{0};
+  std::atomic<uint64_t> metrics_requests{0};
+  std::atomic<uint64_t> gzip_responses{0};
+  std::atomic<uint64_t> bytes_sent{0};
+  std::atomic<uint64_t> errors{0};
+  std::atomic<uint64_t> accepted{0};
+  std::atomic<uint64_t> open_conns{0};
+  std::atomic<uint64_t> lat_buckets[kBuckets + 1]{};  // +Inf last, non-cumulative
+  std::atomic<uint64_t> lat_sum_ns{0};
+  std::atomic<uint64_t> lat_count{0};
+  void record_latency(uint64_t ns);
+};
+
+class HttpServer {
+ public:
+  HttpServer(SnapshotStore* store, const HttpConfig& cfg);
+  ~HttpServer();
+  HttpServer(const HttpServer&) = delete;
+  HttpServer& operator=(const HttpServer&) = delete;
+
+  bool start(std::string* err);
+  void stop();
+  int port() const { return bound_port_; }
+  bool running() const { return running_.load(); }
+
+  void set_ready(bool r) { ready_.store(r); }
+  // Last time (mono ns) a client asked for gzip; the sampler pre-compresses while
+  // this is recent so gzip scrapes stay O(bytes) too.
+  uint64_t gzip_wanted_ns() const { return gzip_wanted_ns_.load(std::memory_order_relaxed); }
+  const HttpStats& stats() const { return stats_; }
+
+ private:
+  struct Worker;
+  void run(Worker* w);
+
+  SnapshotStore* store_;
+  HttpConfig cfg_;
+  int bound_port_ = -1;
+  std::atomic<bool> running_{false};
+  std::atomic<bool> ready_{false};
+  std::atomic<uint64_t> gzip_wanted_ns_{0};
+  HttpStats stats_;
+  std::vector<std::unique_ptr<Worker>> workers_;
+};
+
+}  // namespace gpuexp

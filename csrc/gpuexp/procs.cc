@@ -1,0 +1,295 @@
+#include "gpuexp/procs.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <unordered_set>
+
+namespace gpuexp {
+
+KfdProcReader::KfdProcReader(std::string host_root, int self_pid, bool read_cu_occupancy)
+    : root_(std::move(host_root)), self_(self_pid), read_cu_(read_cu_occupancy) {
+  if (!root_.empty() && root_.back() == '/') root_.pop_back();
+}
+
+void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
+                         std::vector<std::vector<ProcSample>>* per_dev) {
+  per_dev->assign(devs.size(), {});
+  ++scan_no_;
+  const std::string base = root_ + "/sys/class/kfd/kfd/proc";
+  char buf[128];
+  for (const std::string& name : list_dir(base)) {
+    int pid = std::atoi(name.c_str());
+    if (pid <= 0 || pid == self_) continue;
+    auto it = pids_.find(pid);
+    if (it == pids_.end()) {
+      // New process: find which of OUR devices it has a KFD context on.
+      Entry e;
+      std::string pdir = base + "/" + name;
+      for (size_t di = 0; di < devs.size(); ++di) {
+        const DeviceInfo& d = devs[di];
+        PerDev pd;
+        pd.dev = int(di);  // position in `devs` (the engine's device order)
+        std::string id = std::to_string(d.kfd_gpu_id);
+        if (!pd.vram.open(pdir + "/vram_" + id)) continue;
+        if (read_cu_) pd.cu.open(pdir + "/stats_" + id + "/cu_occupancy");
+        pd.sdma.open(pdir + "/sdma_" + id);
+        e.devs.push_back(std::move(pd));
+      }
+      std::string comm;
+      if (read_small_file(root_ + "/proc/" + name + "/comm", &comm, 64)) e.comm = trim(comm);
+      it = pids_.emplace(pid, std::move(e)).first;
+    }
+    Entry& e = it->second;
+    e.seen = scan_no_;
+    for (auto& pd : e.devs) {
+      uint64_t v = 0;
+      if (!pd.vram.read_u64(&v)) continue;  // process exiting
+      ProcSample ps;
+      ps.pid = pid;
+      ps.device = pd.dev;
+      ps.vram_bytes = double(v);
+      long n;
+      if (pd.cu.is_open() && (n = pd.cu.read(buf, sizeof(buf) - 1)) > 0 && parse_u64(buf, size_t(n), &v))
+        ps.cu_occupancy = double(v);
+      if (pd.sdma.is_open() && (n = pd.sdma.read(buf, sizeof(buf) - 1)) > 0 && parse_u64(buf, size_t(n), &v))
+        ps.sdma_us = double(v);
+      ps.name = e.comm;
+      (*per_dev)[size_t(pd.dev)].push_back(ps);
+    }
+  }
+  // Forget processes that left the KFD proc directory (closes their fds).
+  for (auto it = pids_.begin(); it != pids_.end();)
+    it = it->second.seen != scan_no_ ? pids_.erase(it) : std::next(it);
+}
+
+// ---------------------------------------------------------------------------------
+// cgroup path parsing
+
+namespace {
+
+bool is_uid_char(char c) {
+  return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F') || c == '-' ||
+         c == '_';
+}
+
+bool is_hex(const std::string& s) {
+  if (s.empty()) return false;
+  for (char c : s)
+    if (!((c >= '0' && c <= '9') || (c >= 'a' && c <= 'f'))) return false;
+  return true;
+}
+
+std::vector<std::string> split_path(const std::string& p) {
+  std::vector<std::string> out;
+  size_t i = 0;
+  while (i <= p.size()) {
+    size_t j = p.find('/', i);
+    if (j == std::string::npos) j = p.size();
+    if (j > i) out.push_back(p.substr(i, j - i));
+    i = j + 1;
+  }
+  return out;
+}
+
+// Finds "pod<36-char uid>" inside a component; returns the dashed uid.
+bool extract_pod_uid(const std::string& comp, std::string* uid) {
+  size_t pos = 0;
+  while ((pos = comp.find("pod", pos)) != std::string::npos) {
+    size_t s = pos + 3;
+    size_t e = s;
+    while (e < comp.size() && is_uid_char(comp[e])) ++e;
+    if (e - s == 36) {
+      std::string u = comp.substr(s, 36);
+      std::replace(u.begin(), u.end(), '_', '-');
+      std::transform(u.begin(), u.end(), u.begin(), ::tolower);
+      // 8-4-4-4-12
+      if (u[8] == '-' && u[13] == '-' && u[18] == '-' && u[23] == '-') {
+        *uid = u;
+        return true;
+      }
+    }
+    pos = s;
+  }
+  return false;
+}
+
+bool strip_prefix(std::string* s, const char* p) {
+  size_t n = std::strlen(p);
+  if (s->compare(0, n, p) == 0) {
+    s->erase(0, n);
+    return true;
+  }
+  return false;
+}
+
+bool strip_suffix(std::string* s, const char* p) {
+  size_t n = std::strlen(p);
+  if (s->size() >= n && s->compare(s->size() - n, n, p) == 0) {
+    s->erase(s->size() - n);
+    return true;
+  }
+  return false;
+}
+
+// Container component forms: cri-containerd-<id>.scope, crio-<id>.scope,
+// docker-<id>.scope, <id> (cgroupfs), ...:cri-containerd:<id>.
+bool extract_container(std::string comp, std::string* id, std::string* runtime) {
+  size_t colon = comp.rfind(':');
+  if (colon != std::string::npos) {
+    std::string rt = comp.substr(0, colon);
+    comp = comp.substr(colon + 1);
+    if (rt.find("containerd") != std::string::npos) *runtime = "containerd";
+    else if (rt.find("crio") != std::string::npos) *runtime = "crio";
+    else if (rt.find("docker") != std::string::npos) *runtime = "docker";
+  }
+  strip_suffix(&comp, ".scope");
+  if (strip_prefix(&comp, "cri-containerd-")) *runtime = "containerd";
+  else if (strip_prefix(&comp, "crio-conmon-")) return false;  // conmon, not a container
+  else if (strip_prefix(&comp, "crio-")) *runtime = "crio";
+  else if (strip_prefix(&comp, "docker-")) *runtime = "docker";
+  else if (strip_prefix(&comp, "containerd-")) *runtime = "containerd";
+  std::transform(comp.begin(), comp.end(), comp.begin(), ::tolower);
+  if (comp.size() >= 12 && is_hex(comp)) {
+    *id = comp;
+    if (runtime->empty()) *runtime = "unknown";
+    return true;
+  }
+  return false;
+}
+
+}  // namespace
+
+bool parse_kube_cgroup_path(const std::string& path, CgroupInfo* out) {
+  *out = CgroupInfo();
+  out->path = path;
+  auto comps = split_path(path);
+  int pod_idx = -1;
+  for (size_t i = 0; i < comps.size(); ++i) {
+    std::string uid;
+    if (comps[i].find("kubepods") != std::string::npos || comps[i].compare(0, 3, "pod") == 0) {
+      if (extract_pod_uid(comps[i], &uid)) {
+        out->pod_uid = uid;
+        pod_idx = int(i);
+      }
+    }
+  }
+  if (pod_idx < 0) return false;
+  out->kube = true;
+  out->qos = "guaranteed";
+  for (int i = 0; i <= pod_idx; ++i) {
+    if (comps[size_t(i)].find("burstable") != std::string::npos) out->qos = "burstable";
+    if (comps[size_t(i)].find("besteffort") != std::string::npos) out->qos = "besteffort";
+  }
+  for (size_t i = size_t(pod_idx) + 1; i < comps.size(); ++i) {
+    std::string id, rt;
+    if (extract_container(comps[i], &id, &rt)) {
+      out->container_id = id;
+      out->runtime = rt;
+      break;
+    }
+  }
+  // Some runtimes put the pod and container in ONE component ("...pod<uid>.slice:cri-containerd:<id>").
+  if (out->container_id.empty()) {
+    std::string id, rt;
+    if (extract_container(comps[size_t(pod_idx)], &id, &rt)) {
+      out->container_id = id;
+      out->runtime = rt;
+    }
+  }
+  return true;
+}
+
+bool parse_proc_cgroup(const std::string& content, CgroupInfo* out) {
+  // Prefer the unified (v2) hierarchy; otherwise any v1 controller line that names a pod.
+  std::string v2;
+  std::vector<std::string> v1;
+  size_t i = 0;
+  while (i < content.size()) {
+    size_t e = content.find('\n', i);
+    if (e == std::string::npos) e = content.size();
+    std::string line = content.substr(i, e - i);
+    i = e + 1;
+    size_t c1 = line.find(':');
+    if (c1 == std::string::npos) continue;
+    size_t c2 = line.find(':', c1 + 1);
+    if (c2 == std::string::npos) continue;
+    std::string hier = line.substr(0, c1), ctrl = line.substr(c1 + 1, c2 - c1 - 1);
+    std::string path = line.substr(c2 + 1);
+    if (hier == "0" && ctrl.empty()) v2 = path;
+    else v1.push_back(path);
+  }
+  if (!v2.empty() && parse_kube_cgroup_path(v2, out)) return true;
+  for (auto& p : v1)
+    if (parse_kube_cgroup_path(p, out)) return true;
+  *out = CgroupInfo();
+  out->path = v2.empty() && !v1.empty() ? v1.front() : v2;
+  return false;
+}
+
+PidResolver::PidResolver(std::string host_root) : root_(std::move(host_root)) {
+  if (!root_.empty() && root_.back() == '/') root_.pop_back();
+}
+
+bool PidResolver::read_starttime(int pid, uint64_t* st) {
+  std::string s;
+  if (!read_small_file(root_ + "/proc/" + std::to_string(pid) + "/stat", &s, 4096)) return false;
+  // Field 22 (starttime), counted after the ")" that ends comm.
+  size_t p = s.rfind(')');
+  if (p == std::string::npos) return false;
+  int field = 2;
+  size_t i = p + 1;
+  while (i < s.size() && field < 22) {
+    while (i < s.size() && s[i] == ' ') ++i;
+    ++field;
+    if (field == 22) break;
+    while (i < s.size() && s[i] != ' ') ++i;
+  }
+  return parse_u64(s.c_str() + i, s.size() - i, st);
+}
+
+const CgroupInfo* PidResolver::resolve(int pid) {
+  auto ov = overrides_.find(pid);
+  if (ov != overrides_.end()) {
+    Entry& e = cache_[pid];
+    if (e.info.path != ov->second || !e.ok) {
+      e.ok = true;
+      parse_kube_cgroup_path(ov->second, &e.info);
+      e.info.path = ov->second;
+    }
+    return &e.info;
+  }
+  uint64_t st = 0;
+  bool have_st = read_starttime(pid, &st);
+  auto it = cache_.find(pid);
+  if (it != cache_.end() && it->second.ok && (!have_st || it->second.starttime == st))
+    return &it->second.info;
+  std::string content;
+  if (!read_small_file(root_ + "/proc/" + std::to_string(pid) + "/cgroup", &content)) {
+    cache_.erase(pid);
+    return nullptr;
+  }
+  Entry& e = cache_[pid];
+  e.starttime = st;
+  e.ok = true;
+  parse_proc_cgroup(content, &e.info);
+  return &e.info;
+}
+
+void PidResolver::set_override(int pid, const std::string& cgroup_path) {
+  overrides_[pid] = cgroup_path;
+  cache_.erase(pid);
+}
+
+void PidResolver::clear_overrides() {
+  for (auto& kv : overrides_) cache_.erase(kv.first);
+  overrides_.clear();
+}
+
+void PidResolver::gc(const std::vector<int>& live_pids) {
+  std::unordered_set<int> live(live_pids.begin(), live_pids.end());
+  for (auto it = cache_.begin(); it != cache_.end();)
+    it = live.count(it->first) ? std::next(it) : cache_.erase(it);
+}
+
+}  // namespace gpuexp

@@ -1,0 +1,85 @@
+// GPU process discovery (KFD sysfs) and PID -> pod attribution (cgroup v2/v1 paths).
+//
+// Reference: NVML GetComputeRunningProcesses (host PIDs, /root/reference/main.go:135)
+// joined against `kubectl exec <pod> -- ps -e -o pid=` output (container-namespace PIDs,
+// main.go:101) with `for pid := range pids` comparing an INDEX to a PID (main.go:144) —
+// broken twice.  Here: host PIDs from /sys/class/kfd/kfd/proc/<pid>/
+// vram_<gpu_id> (exactly the GPUs that process has a KFD context on, measured on the
+// box), then /proc/<pid>/cgroup -> pod UID + container ID, no subprocesses, no exec RBAC.
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "gpuexp/backends.h"
+#include "gpuexp/device.h"
+
+namespace gpuexp {
+
+class KfdProcReader {
+ public:
+  KfdProcReader(std::string host_root, int self_pid, bool read_cu_occupancy);
+  // Fills per_dev[d] with the processes that have a KFD context on device d.
+  void scan(const std::vector<DeviceInfo>& devs, std::vector<std::vector<ProcSample>>* per_dev);
+  size_t tracked() const { return pids_.size(); }
+
+ private:
+  struct PerDev {
+    int dev = -1;
+    CachedFile vram, cu, sdma;
+  };
+  struct Entry {
+    std::vector<PerDev> devs;
+    std::string comm;
+    uint64_t seen = 0;
+  };
+  std::string root_;
+  int self_;
+  bool read_cu_;
+  uint64_t scan_no_ = 0;
+  std::unordered_map<int, Entry> pids_;
+};
+
+struct CgroupInfo {
+  bool kube = false;
+  std::string pod_uid;       // dashed form
+  std::string container_id;  // 64-hex (or runtime-specific)
+  std::string runtime;       // containerd | crio | docker | unknown
+  std::string qos;           // guaranteed | burstable | besteffort
+  std::string path;          // the cgroup path the info came from
+};
+
+// Parses one cgroup path (e.g. "/kubepods.slice/kubepods-burstable.slice/
+// kubepods-burstable-pod<uid_>.slice/cri-containerd-<id>.scope" or
+// "/kubepods/burstable/pod<uid>/<id>").  Returns false if no pod UID is found.
+bool parse_kube_cgroup_path(const std::string& path, CgroupInfo* out);
+// Parses a whole /proc/<pid>/cgroup file (v2 "0::" line preferred; v1 fallbacks).
+bool parse_proc_cgroup(const std::string& content, CgroupInfo* out);
+
+// Caches pid -> CgroupInfo keyed on (pid, starttime) so PID reuse is detected.
+class PidResolver {
+ public:
+  explicit PidResolver(std::string host_root);
+  // Returns nullptr if the PID cannot be read (other PID namespace, exited).
+  const CgroupInfo* resolve(int pid);
+  // Test/bench hook: pretend /proc/<pid>/cgroup contains `cgroup_path`.
+  void set_override(int pid, const std::string& cgroup_path);
+  void clear_overrides();
+  void gc(const std::vector<int>& live_pids);
+
+ private:
+  struct Entry {
+    uint64_t starttime = 0;
+    bool ok = false;
+    CgroupInfo info;
+  };
+  bool read_starttime(int pid, uint64_t* st);
+  std::string root_;
+  std::unordered_map<int, Entry> cache_;
+  std::unordered_map<int, std::string> overrides_;
+};
+
+}  // namespace gpuexp

@@ -1,0 +1,274 @@
+// HIP sentinel: one 64-lane wave per GPU per tick, on the lowest-priority stream, that
+// stamps the shader clock (s_memtime), the 100 MHz reference clock (s_memrealtime) and
+// the XCC/CU it landed on into a pinned, host-coherent ring.  The sampler never
+// synchronizes: it drains completed slots (seq written last, system-scope release) and
+// launches the next run.  Nothing like it exists in the reference (NVML only,
+// /root/reference/main.go:16); SURVEY.md §2.2 / §7.2 step 6.
+//
+// Measures, per tick:
+//   sclk      = d(s_memtime) / d(s_memrealtime) * 100 MHz over a dependent ALU chain
+//               (the in-kernel clock recipe of MI355X_MICROARCH.md "DVFS give-back" (6))
+//   latency   = host launch -> first wave start, both in the HSA system time domain
+//               (GPU ticks converted with hsa_amd_profiling_convert_tick_to_system_domain)
+//   xcc_id    = HW_REG_XCC_ID of the wave (round-robin dispatch is observed, not assumed)
+// Cost: one wave on one CU for a few microseconds per tick (<0.01% of a 256-CU chip).
+#include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "gpuexp/sources.h"
+
+namespace gpuexp {
+
+struct alignas(64) SentinelSlot {
+  uint64_t seq;          // written LAST by the GPU (system-scope release)
+  uint64_t host_launch;  // HSA system timestamp taken just before the launch
+  uint64_t rt0, rt1;     // s_memrealtime at start / end (100 MHz)
+  uint64_t mt0, mt1;     // s_memtime at start / end (shader clock)
+  uint32_t xcc_id;
+  uint32_t hw_id;
+  uint32_t pad[2];
+};
+static_assert(sizeof(SentinelSlot) == 64, "one cache line per slot");
+
+__global__ void __launch_bounds__(64) sentinel_kernel(SentinelSlot* __restrict__ ring, uint32_t slot,
+                                                      uint64_t seq, int spin) {
+  if (threadIdx.x != 0) return;
+  uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t mt0 = __builtin_amdgcn_s_memtime();
+  // Dependent integer chain: the compiler cannot shorten it; its length only sets the
+  // timing window (~spin*8 shader cycles).
+  uint32_t x = uint32_t(seq) | 1u;
+  for (int i = 0; i < spin; ++i) {
+    x = x * 1664525u + 1013904223u;
+    asm volatile("" : "+v"(x));
+  }
+  uint64_t mt1 = __builtin_amdgcn_s_memtime();
+  uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+  uint32_t xcc, hwid;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+  SentinelSlot* s = ring + slot;
+  s->rt0 = rt0;
+  s->rt1 = rt1;
+  s->mt0 = mt0;
+  s->mt1 = mt1;
+  s->xcc_id = xcc;
+  s->hw_id = hwid ^ (x & 0u);  // keep x live without changing hw_id
+  __atomic_thread_fence(__ATOMIC_RELEASE);  // orders the payload before seq (system scope below)
+  __hip_atomic_store(&s->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+namespace {
+
+struct HsaAgentMatch {
+  uint32_t bdfid;
+  uint32_t domain;
+  hsa_agent_t agent;
+  bool found;
+};
+
+hsa_status_t match_agent(hsa_agent_t a, void* data) {
+  auto* m = static_cast<HsaAgentMatch*>(data);
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS || t != HSA_DEVICE_TYPE_GPU)
+    return HSA_STATUS_SUCCESS;
+  uint32_t bdfid = 0, dom = 0;
+  hsa_agent_get_info(a, hsa_agent_info_t(HSA_AMD_AGENT_INFO_BDFID), &bdfid);
+  hsa_agent_get_info(a, hsa_agent_info_t(HSA_AMD_AGENT_INFO_DOMAIN), &dom);
+  if (bdfid == m->bdfid && dom == m->domain) {
+    m->agent = a;
+    m->found = true;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+uint64_t hsa_now() {
+  uint64_t t = 0;
+  hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP, &t);
+  return t;
+}
+
+class HipSentinel : public SentinelSource {
+  struct Reading {
+    bool ok = false;
+    double sclk_hz = 0, latency_s = 0, xcc = 0;
+  };
+  struct Per {
+    int hip = -1;
+    bool ready = false;
+    hipStream_t stream = nullptr;
+    SentinelSlot* ring = nullptr;
+    SentinelSlot* dring = nullptr;
+    hsa_agent_t agent{};
+    bool have_agent = false;
+    uint64_t launched = 0, completed = 0, stalled = 0, errors = 0;
+    Reading last;
+  };
+
+ public:
+  HipSentinel(int ring, int spin) : nslots_(ring < 4 ? 4 : ring), spin_(spin < 16 ? 16 : spin) {}
+  ~HipSentinel() override { stop(); }
+
+  bool start(const std::vector<DeviceInfo>& devs, std::string* err) override {
+    int nhip = 0;
+    if (hipGetDeviceCount(&nhip) != hipSuccess || nhip == 0) {
+      *err = "no HIP devices";
+      return false;
+    }
+    // HIP device order can differ from the exporter's; match by PCI BDF.
+    std::vector<std::string> hip_bdf(static_cast<size_t>(nhip));
+    for (int h = 0; h < nhip; ++h) {
+      char bus[64] = {0};
+      if (hipDeviceGetPCIBusId(bus, sizeof(bus), h) == hipSuccess) {
+        std::string b(bus);
+        for (auto& c : b) c = char(::tolower(c));
+        hip_bdf[size_t(h)] = b;
+      }
+    }
+    hsa_init();  // refcounted; HIP already initialised it
+    uint64_t freq = 0;
+    hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &freq);
+    sys_ns_per_tick_ = freq ? 1e9 / double(freq) : 1.0;
+    per_.resize(devs.size());
+    int ok = 0;
+    for (size_t i = 0; i < devs.size(); ++i) {
+      Per& p = per_[i];
+      std::string want = devs[i].bdf;
+      for (auto& c : want) c = char(::tolower(c));
+      for (int h = 0; h < nhip; ++h)
+        if (hip_bdf[size_t(h)] == want) p.hip = h;
+      if (p.hip < 0) continue;
+      if (hipSetDevice(p.hip) != hipSuccess) continue;
+      int least = 0, greatest = 0;
+      (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+      if (hipStreamCreateWithPriority(&p.stream, hipStreamNonBlocking, least) != hipSuccess) continue;
+      void* mem = nullptr;
+      if (hipHostMalloc(&mem, sizeof(SentinelSlot) * size_t(nslots_), hipHostMallocCoherent | hipHostMallocMapped) !=
+          hipSuccess)
+        continue;
+      p.ring = static_cast<SentinelSlot*>(mem);
+      std::memset(mem, 0, sizeof(SentinelSlot) * size_t(nslots_));
+      void* dptr = nullptr;
+      (void)hipHostGetDevicePointer(&dptr, mem, 0);
+      p.dring = static_cast<SentinelSlot*>(dptr ? dptr : mem);
+      // HSA agent for tick -> system-domain conversion.
+      unsigned bus = 0, dev = 0, fn = 0, dom = 0;
+      if (std::sscanf(want.c_str(), "%x:%x:%x.%x", &dom, &bus, &dev, &fn) == 4) {
+        HsaAgentMatch m{(bus << 8) | (dev << 3) | fn, dom, {}, false};
+        hsa_iterate_agents(match_agent, &m);
+        p.agent = m.agent;
+        p.have_agent = m.found;
+      }
+      p.ready = true;
+      ++ok;
+    }
+    if (!ok) {
+      *err = "no exporter GPU matched a HIP device";
+      return false;
+    }
+    status_ = "hip sentinel on " + std::to_string(ok) + " GPU(s), ring " + std::to_string(nslots_);
+    return true;
+  }
+
+  void tick(uint64_t) override {
+    for (size_t i = 0; i < per_.size(); ++i) {
+      Per& p = per_[i];
+      if (!p.ready) continue;
+      drain(p);
+      // Bound the in-flight window: a saturated queue shows up as latency, not as an
+      // unbounded backlog of sentinel launches.
+      if (p.launched - p.completed >= 4) {
+        p.stalled += 1;
+        continue;
+      }
+      uint64_t seq = p.launched + 1;
+      uint32_t slot = uint32_t(seq % uint64_t(nslots_));
+      SentinelSlot* s = p.ring + slot;
+      __atomic_store_n(&s->seq, 0ull, __ATOMIC_RELAXED);
+      (void)hipSetDevice(p.hip);
+      s->host_launch = hsa_now();
+      hipLaunchKernelGGL(sentinel_kernel, dim3(1), dim3(64), 0, p.stream, p.dring, slot, seq, spin_);
+      if (hipGetLastError() != hipSuccess) {
+        p.errors += 1;
+        continue;
+      }
+      p.launched = seq;
+    }
+  }
+
+  void drain(Per& p) {
+    while (p.completed < p.launched) {
+      uint64_t seq = p.completed + 1;
+      SentinelSlot* s = p.ring + (seq % uint64_t(nslots_));
+      if (__atomic_load_n(&s->seq, __ATOMIC_ACQUIRE) != seq) break;
+      p.completed = seq;
+      double drt = double(s->rt1 - s->rt0);
+      double dmt = double(s->mt1 - s->mt0);
+      Reading r;
+      r.ok = true;
+      r.sclk_hz = drt > 0 ? dmt / drt * 100e6 : std::nan("");
+      r.xcc = double(s->xcc_id & 0xF);
+      r.latency_s = std::nan("");
+      if (p.have_agent) {
+        uint64_t sys = 0;
+        if (hsa_amd_profiling_convert_tick_to_system_domain(p.agent, s->rt0, &sys) == HSA_STATUS_SUCCESS) {
+          double lat = (double(sys) - double(s->host_launch)) * sys_ns_per_tick_ * 1e-9;
+          // A negative value means the GPU tick and s_memrealtime domains disagree; keep
+          // the rest of the reading and drop the latency rather than export garbage.
+          if (lat > -1e-6 && lat < 10.0) r.latency_s = lat < 0 ? 0 : lat;
+        }
+      }
+      p.last = r;
+    }
+  }
+
+  bool read(int dev, SentinelReading* out) override {
+    if (dev < 0 || size_t(dev) >= per_.size() || !per_[size_t(dev)].ready) return false;
+    Per& p = per_[size_t(dev)];
+    if (!p.last.ok) return false;
+    out->ok = true;
+    out->sclk_hz = p.last.sclk_hz;
+    out->dispatch_latency_s = p.last.latency_s;
+    out->xcc_id = p.last.xcc;
+    out->runs = p.completed;
+    return true;
+  }
+
+  void stop() override {
+    for (auto& p : per_) {
+      if (!p.ready) continue;
+      (void)hipSetDevice(p.hip);
+      (void)hipStreamSynchronize(p.stream);  // a sentinel run is microseconds long
+      drain(p);
+      (void)hipStreamDestroy(p.stream);
+      (void)hipHostFree(p.ring);
+      p.ready = false;
+    }
+    per_.clear();
+  }
+
+  std::string status() const override { return status_; }
+
+ private:
+  int nslots_;
+  int spin_;
+  double sys_ns_per_tick_ = 1.0;
+  std::vector<Per> per_;
+  std::string status_ = "not started";
+};
+
+}  // namespace
+
+std::unique_ptr<SentinelSource> make_hip_sentinel(int ring_slots, int spin_iters) {
+  return std::make_unique<HipSentinel>(ring_slots, spin_iters);
+}
+
+}  // namespace gpuexp

@@ -1,0 +1,54 @@
+// Optional per-GPU sources beyond the device backend: the HIP sentinel kernel, the
+// rocprofiler-sdk device-counting plugin, and the RCCL API-trace shared-memory rings.
+// None of these exist in the reference (it had NVML only, /root/reference/main.go:16).
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "gpuexp/device.h"
+
+namespace gpuexp {
+
+class SentinelSource {
+ public:
+  virtual ~SentinelSource() = default;
+  virtual bool start(const std::vector<DeviceInfo>& devs, std::string* err) = 0;
+  // Called once per tick: drains completed runs, then launches the next one.
+  virtual void tick(uint64_t now_ns) = 0;
+  virtual bool read(int dev, SentinelReading* out) = 0;
+  virtual void stop() = 0;
+  virtual std::string status() const = 0;
+};
+// Implemented in sentinel.hip (1 wave, lowest-priority stream, pinned host ring).
+std::unique_ptr<SentinelSource> make_hip_sentinel(int ring_slots, int spin_iters);
+
+class CounterSource {
+ public:
+  virtual ~CounterSource() = default;
+  virtual bool start(const std::vector<DeviceInfo>& devs, std::string* err) = 0;
+  virtual bool sample(int dev, double dt_s, CounterReading* out) = 0;
+  virtual void stop() = 0;
+  virtual std::string status() const = 0;
+};
+// dlopen()s the rocprofiler-sdk plugin (_gpuexp_rocprof.so) next to the core.
+std::unique_ptr<CounterSource> make_rocprof_counters(const std::string& plugin_path);
+
+// One collective call record written by the RCCL tracer tool into a per-process ring.
+struct RcclTotals {
+  int pid = 0;
+  std::string op;     // allreduce, allgather, reducescatter, alltoall, send, recv, broadcast, ...
+  uint64_t calls = 0;
+  uint64_t bytes = 0;
+};
+class RcclSource {
+ public:
+  virtual ~RcclSource() = default;
+  // Drains every ring under `dir` and returns cumulative per-(pid, op) totals.
+  virtual void poll(std::vector<RcclTotals>* out) = 0;
+};
+std::unique_ptr<RcclSource> make_rccl_source(const std::string& dir);
+
+}  // namespace gpuexp

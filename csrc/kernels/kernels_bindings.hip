@@ -1,0 +1,88 @@
+// Python bindings for the HIP workload kernels (raw device pointers + stream handles, so
+// they work with torch tensors via .data_ptr() and without torch at all via gemm_burn).
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+
+#include <chrono>
+#include <stdexcept>
+#include <string>
+
+namespace py = pybind11;
+
+namespace gpuexp {
+bool gemm_shape_ok(int M, int N, int K);
+hipError_t launch_gemm_bf16_tn(const void* A, const void* B, void* C, int M, int N, int K, hipStream_t stream);
+hipError_t launch_fill_bf16(void* p, size_t n, uint32_t seed, hipStream_t stream);
+}  // namespace gpuexp
+
+namespace {
+
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace
+
+void register_kernels(py::module_& m) {
+  m.def("hip_device_count", []() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+  });
+  m.def("gemm_shape_ok", &gpuexp::gemm_shape_ok);
+  m.def("gemm_bf16", [](uintptr_t a, uintptr_t b, uintptr_t c, int M, int N, int K, uintptr_t stream) {
+    if (!gpuexp::gemm_shape_ok(M, N, K))
+      throw std::invalid_argument("gemm_bf16 needs M%128==0, N%128==0, K%64==0");
+    if (!a || !b || !c) throw std::invalid_argument("null pointer");
+    check(gpuexp::launch_gemm_bf16_tn(reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b),
+                                      reinterpret_cast<void*>(c), M, N, K, reinterpret_cast<hipStream_t>(stream)),
+          "gemm_bf16 launch");
+  }, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("stream") = 0,
+     "C[M,N] = A[M,K] @ B[N,K]^T; bf16 row-major, fp32 accumulate (MFMA 16x16x32)");
+  m.def("fill_bf16", [](uintptr_t p, size_t n, uint32_t seed, uintptr_t stream) {
+    check(gpuexp::launch_fill_bf16(reinterpret_cast<void*>(p), n, seed, reinterpret_cast<hipStream_t>(stream)),
+          "fill_bf16 launch");
+  }, py::arg("ptr"), py::arg("n"), py::arg("seed") = 1, py::arg("stream") = 0);
+  m.def("gemm_burn", [](int device, int M, int N, int K, double seconds, int iters_per_sync) {
+    // Torch-free synthetic GEMM pod: keeps one GPU busy for `seconds` and reports the
+    // achieved bf16 TFLOP/s (random operands).
+    if (!gpuexp::gemm_shape_ok(M, N, K)) throw std::invalid_argument("bad GEMM shape");
+    if (seconds <= 0 || seconds > 3600) throw std::invalid_argument("seconds out of range");
+    double tflops = 0;
+    long iters = 0;
+    double elapsed = 0;
+    {
+      py::gil_scoped_release rel;
+      check(hipSetDevice(device), "hipSetDevice");
+      void *a = nullptr, *b = nullptr, *c = nullptr;
+      check(hipMalloc(&a, size_t(M) * K * 2), "hipMalloc A");
+      check(hipMalloc(&b, size_t(N) * K * 2), "hipMalloc B");
+      check(hipMalloc(&c, size_t(M) * N * 2), "hipMalloc C");
+      hipStream_t s;
+      check(hipStreamCreate(&s), "hipStreamCreate");
+      (void)gpuexp::launch_fill_bf16(a, size_t(M) * K, 1, s);
+      (void)gpuexp::launch_fill_bf16(b, size_t(N) * K, 2, s);
+      check(hipStreamSynchronize(s), "fill");
+      auto t0 = std::chrono::steady_clock::now();
+      int per = iters_per_sync > 0 ? iters_per_sync : 8;
+      for (;;) {
+        for (int i = 0; i < per; ++i) (void)gpuexp::launch_gemm_bf16_tn(a, b, c, M, N, K, s);
+        check(hipStreamSynchronize(s), "gemm");
+        iters += per;
+        elapsed = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (elapsed >= seconds) break;
+      }
+      tflops = 2.0 * M * N * double(K) * double(iters) / elapsed / 1e12;
+      (void)hipStreamDestroy(s);
+      (void)hipFree(a);
+      (void)hipFree(b);
+      (void)hipFree(c);
+    }
+    py::dict d;
+    d["tflops"] = tflops;
+    d["iters"] = iters;
+    d["seconds"] = elapsed;
+    return d;
+  }, py::arg("device"), py::arg("M") = 4096, py::arg("N") = 4096, py::arg("K") = 4096, py::arg("seconds") = 1.0,
+     py::arg("iters_per_sync") = 8);
+}

@@ -1,0 +1,217 @@
+"""Exporter configuration: one object, precedence CLI flags > env GPUEXP_* > YAML > defaults.
+
+The reference has no configuration at all — port `:8000` (/root/reference/main.go:71),
+path `/metrics` (main.go:70), interval 30 s (main.go:156), in-cluster auth only
+(main.go:57) and all namespaces (main.go:77) are hard-coded.
+Defaults here keep the reference's listen address and path for compatibility.
+"""
+from __future__ import annotations
+
+import argparse
+import dataclasses
+import os
+from dataclasses import dataclass, field, fields
+from typing import Any, Optional
+
+import yaml
+
+
+@dataclass
+class Config:
+    # exposition
+    listen: str = ":8000"                  # main.go:71
+    path: str = "/metrics"                 # main.go:70
+    http_threads: int = 1
+    gzip: bool = True
+    # sampling
+    interval: float = 1.0                  # seconds; reference: 30 s (main.go:156)
+    backend: str = "auto"                  # auto | amdsmi | sysfs | mock
+    mock_devices: int = 1
+    host_root: str = ""                    # prefix for /sys and /proc (DaemonSet: /host)
+    devices: list = field(default_factory=list)  # exporter GPU indices to export (empty = all)
+    series_profile: str = "standard"       # standard | compact | legacy
+    legacy_families: bool = True           # pod_gpu_memory_usage / docker_gpu_memory_perc_usage
+    process_source: str = "auto"           # auto | kfd | amdsmi | none
+    kfd_cu_occupancy: bool = True
+    gc_after: int = 1
+    # optional sources
+    enable_sentinel: bool = False
+    sentinel_spin: int = 2000
+    enable_counters: bool = False
+    counters_plugin: str = ""
+    enable_rccl: bool = False
+    rccl_dir: str = "/var/run/gpuexp/rccl"
+    # attribution / kubernetes control plane
+    pod_attribution: bool = True
+    infer_device_owner: bool = True
+    node_name: str = ""                    # downward API NODE_NAME
+    kubelet_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"
+    podresources: bool = True
+    gpu_resource_names: list = field(default_factory=lambda: ["amd.com/gpu"])
+    apiserver: str = ""                    # "" = in-cluster (KUBERNETES_SERVICE_HOST) if present
+    apiserver_token_file: str = "/var/run/secrets/kubernetes.io/serviceaccount/token"
+    apiserver_ca_file: str = "/var/run/secrets/kubernetes.io/serviceaccount/ca.crt"
+    pod_logdir: str = "/var/log/pods"      # zero-RBAC fallback: <ns>_<pod>_<uid> directories
+    control_interval: float = 5.0          # seconds between control-plane refreshes
+    control_timeout: float = 3.0           # per-call timeout for gRPC / apiserver
+    # diagnostics
+    log_level: str = "warn"
+    trace: str = ""                        # Chrome trace JSON of sampler stages
+
+    def listen_host_port(self) -> tuple[str, int]:
+        host, _, port = self.listen.rpartition(":")
+        return (host or "0.0.0.0"), int(port)
+
+    def resolved_backend(self) -> str:
+        if self.backend != "auto":
+            return self.backend
+        root = self.host_root or "/"
+        kfd = os.path.join(root, "sys/class/kfd/kfd/topology/nodes")
+        if os.path.isdir(kfd) and (os.path.exists("/dev/kfd") or self.host_root):
+            return "amdsmi" if not self.host_root else "sysfs"
+        return "mock"
+
+    def to_engine_config(self, native) -> Any:
+        ec = native.EngineConfig()
+        ec.backend = self.resolved_backend()
+        ec.mock_devices = int(self.mock_devices)
+        ec.host_root = self.host_root
+        ec.interval_s = float(self.interval)
+        host, port = self.listen_host_port()
+        hc = native.HttpConfig()
+        hc.host = host
+        hc.port = port
+        hc.metrics_path = self.path
+        hc.threads = int(self.http_threads)
+        hc.enable_gzip = bool(self.gzip)
+        ec.http = hc
+        ec.series_profile = self.series_profile
+        ec.legacy_families = bool(self.legacy_families)
+        ec.pod_attribution = bool(self.pod_attribution)
+        ec.infer_device_owner = bool(self.infer_device_owner)
+        ec.process_source = self.process_source
+        ec.kfd_cu_occupancy = bool(self.kfd_cu_occupancy)
+        ec.enable_sentinel = bool(self.enable_sentinel)
+        ec.sentinel_spin = int(self.sentinel_spin)
+        ec.enable_counters = bool(self.enable_counters)
+        if self.counters_plugin:
+            ec.counters_plugin = self.counters_plugin
+        else:
+            from ._native import rocprof_plugin_path
+            ec.counters_plugin = rocprof_plugin_path()
+        ec.enable_rccl = bool(self.enable_rccl)
+        ec.rccl_dir = self.rccl_dir
+        ec.gc_after = int(self.gc_after)
+        ec.device_filter = [int(d) for d in self.devices]
+        ec.trace_path = self.trace
+        from . import __version__
+        ec.version = __version__
+        return ec
+
+
+_BOOL_TRUE = {"1", "true", "yes", "on"}
+_BOOL_FALSE = {"0", "false", "no", "off"}
+
+
+def _coerce(f: dataclasses.Field, raw: Any) -> Any:
+    default = f.default if f.default is not dataclasses.MISSING else f.default_factory()  # type: ignore
+    if isinstance(default, bool):
+        if isinstance(raw, bool):
+            return raw
+        s = str(raw).strip().lower()
+        if s in _BOOL_TRUE:
+            return True
+        if s in _BOOL_FALSE:
+            return False
+        raise ValueError(f"{f.name}: not a boolean: {raw!r}")
+    if isinstance(default, int):
+        return int(raw)
+    if isinstance(default, float):
+        return float(raw)
+    if isinstance(default, list):
+        if isinstance(raw, (list, tuple)):
+            return list(raw)
+        return [x for x in str(raw).split(",") if x != ""]
+    return str(raw)
+
+
+def from_yaml(path: str) -> dict:
+    with open(path) as fh:
+        data = yaml.safe_load(fh) or {}
+    if not isinstance(data, dict):
+        raise ValueError(f"{path}: top level must be a mapping")
+    return data
+
+
+def from_env(env: Optional[dict] = None) -> dict:
+    env = os.environ if env is None else env
+    out = {}
+    for f in fields(Config):
+        key = "GPUEXP_" + f.name.upper()
+        if key in env:
+            out[f.name] = env[key]
+    if "node_name" not in out and env.get("NODE_NAME"):
+        out["node_name"] = env["NODE_NAME"]
+    return out
+
+
+def build_arg_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(prog="gpuexp", description="MI355X per-pod GPU Prometheus exporter")
+    ap.add_argument("--config", help="YAML config file")
+    for f in fields(Config):
+        flag = "--" + f.name.replace("_", "-")
+        default = f.default if f.default is not dataclasses.MISSING else None
+        if isinstance(default, bool):
+            ap.add_argument(flag, dest=f.name, default=None, nargs="?", const="true",
+                            help=f"bool (default {default})")
+        else:
+            ap.add_argument(flag, dest=f.name, default=None, help=f"(default {default!r})")
+    return ap
+
+
+def load_config(argv: Optional[list] = None, env: Optional[dict] = None) -> Config:
+    """Merges defaults < YAML < env < CLI into one validated Config."""
+    ap = build_arg_parser()
+    ns = ap.parse_args(argv)
+    merged: dict = {}
+    if ns.config:
+        merged.update(from_yaml(ns.config))
+    merged.update(from_env(env))
+    for f in fields(Config):
+        v = getattr(ns, f.name, None)
+        if v is not None:
+            merged[f.name] = v
+    return make_config(merged)
+
+
+def make_config(values: dict) -> Config:
+    known = {f.name: f for f in fields(Config)}
+    kwargs = {}
+    for k, v in values.items():
+        k = k.replace("-", "_")
+        if k not in known:
+            raise ValueError(f"unknown config key: {k}")
+        kwargs[k] = _coerce(known[k], v)
+    cfg = Config(**kwargs)
+    validate(cfg)
+    return cfg
+
+
+def validate(cfg: Config) -> None:
+    if cfg.backend not in ("auto", "amdsmi", "sysfs", "mock"):
+        raise ValueError(f"backend must be auto|amdsmi|sysfs|mock, got {cfg.backend}")
+    if cfg.series_profile not in ("standard", "compact", "legacy"):
+        raise ValueError(f"series_profile must be standard|compact|legacy, got {cfg.series_profile}")
+    if cfg.process_source not in ("auto", "kfd", "amdsmi", "none"):
+        raise ValueError(f"process_source must be auto|kfd|amdsmi|none, got {cfg.process_source}")
+    if cfg.interval < 0 or (0 < cfg.interval < 0.001):
+        raise ValueError("interval must be 0 (manual) or >= 1 ms")
+    if not cfg.path.startswith("/"):
+        raise ValueError("path must start with /")
+    _, port = cfg.listen_host_port()
+    if not (0 <= port < 65536):
+        raise ValueError("listen port out of range")
+    if cfg.mock_devices < 1:
+        raise ValueError("mock_devices must be >= 1")
+    if cfg.log_level not in ("debug", "info", "warn", "error", "off"):
+        raise ValueError("log_level must be debug|info|warn|error|off")

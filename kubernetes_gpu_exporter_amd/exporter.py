@@ -1,0 +1,86 @@
+"""Process entry point: wires the native engine to the Kubernetes control plane.
+
+Reference lifecycle (/root/reference/main.go:38-158): register two GaugeVecs, nvml.Init
+(fatal on error), rest.InClusterConfig (panic outside a cluster), start the HTTP
+goroutine, then loop forever; `nvml.Shutdown` is deferred but never runs.
+Here: the native engine owns sampling + serving; a Python control-plane thread refreshes
+pod metadata at low rate; SIGTERM/SIGINT stop both and shut amdsmi/HIP down cleanly.
+"""
+from __future__ import annotations
+
+import logging
+import signal
+import threading
+from typing import Optional
+
+from ._native import load
+from .config import Config
+
+log = logging.getLogger("gpuexp")
+
+_LEVELS = {"debug": 0, "info": 1, "warn": 2, "error": 3, "off": 4}
+
+
+class Exporter:
+    def __init__(self, cfg: Config, control_plane: Optional[object] = None):
+        self.cfg = cfg
+        self.native = load()
+        self.native.set_log_level(_LEVELS[cfg.log_level])
+        self.engine = self.native.Engine(cfg.to_engine_config(self.native))
+        self._control = control_plane
+        self._stop = threading.Event()
+        self._started = False
+
+    # ---- lifecycle ----
+    def start(self) -> "Exporter":
+        self.engine.start()
+        self._started = True
+        if self._control is None and self.cfg.pod_attribution and self.cfg.resolved_backend() != "mock":
+            from .k8s.controlplane import ControlPlane
+            self._control = ControlPlane.from_config(self.cfg)
+        if self._control is not None:
+            self._control.attach(self.engine)
+            self._control.start()
+        return self
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._control is not None:
+            self._control.stop()
+        if self._started:
+            self.engine.stop()
+            self._started = False
+
+    def __enter__(self) -> "Exporter":
+        return self.start()
+
+    def __exit__(self, *exc) -> None:
+        self.stop()
+
+    # ---- accessors ----
+    @property
+    def port(self) -> int:
+        return self.engine.http_port
+
+    def text(self) -> str:
+        return self.engine.snapshot_text()
+
+    def tick(self, now_ns: Optional[int] = None) -> None:
+        self.engine.tick(now_ns)
+
+    def stats(self) -> dict:
+        return self.engine.stats()
+
+    def run_forever(self) -> int:
+        def _handler(signum, frame):
+            log.info("signal %s: shutting down", signum)
+            self._stop.set()
+
+        signal.signal(signal.SIGTERM, _handler)
+        signal.signal(signal.SIGINT, _handler)
+        self.start()
+        log.info("serving %s on %s (%s)", self.cfg.path, self.cfg.listen, self.engine.source_status())
+        while not self._stop.wait(1.0):
+            pass
+        self.stop()
+        return 0

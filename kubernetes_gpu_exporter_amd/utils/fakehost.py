@@ -1,0 +1,167 @@
+"""Fake host roots: a temp tree shaped like an MI355X node's /sys + /proc, for the
+fake-host integration tier.  Layout mirrors what the probe found on the
+GPU box (profiles/probe_host.txt): KFD topology nodes with gpu_id/properties, drm
+renderD<minor>/device with gpu_metrics + mem_info_* + hwmon, KFD per-process
+vram_<gpu_id>/sdma_<gpu_id>/stats_<gpu_id>/cu_occupancy, /proc/<pid>/{cgroup,comm,stat}.
+"""
+from __future__ import annotations
+
+import os
+import struct
+from dataclasses import dataclass, field
+from pathlib import Path
+
+GPU_METRICS_V1_8_SIZE = 3872
+
+
+def encode_gpu_metrics_v1_8(*, hotspot=46, mem=34, vrsoc=41, power=244, gfx=0, umc=0, max_bw=8192,
+                            energy=18067985097658, sysclk=1051434741968776, accum=1051349996,
+                            ppt_res=2146364, pcie_width=16, pcie_speed=320, xgmi_width=16, xgmi_speed=38,
+                            pcie_bw_acc=912039705430, pcie_bw_inst=18, xgmi_rd=None, xgmi_wr=None,
+                            xgmi_status=None, fw_ts=105165583750064, gfxclk=(111,) * 8, socclk=38,
+                            uclk=2000, gfx_busy_acc=(0,) * 8) -> bytes:
+    """Packs a gpu_metrics format-1.8 blob with the field offsets the C++ decoder uses."""
+    xgmi_rd = list(xgmi_rd or [0] * 8)
+    xgmi_wr = list(xgmi_wr or [0] * 8)
+    xgmi_status = list(xgmi_status or [0xFFFF] + [1] * 7)
+    b = bytearray(GPU_METRICS_V1_8_SIZE)
+    struct.pack_into("<HBB", b, 0, GPU_METRICS_V1_8_SIZE, 1, 8)
+    struct.pack_into("<6H", b, 4, hotspot, mem, vrsoc, power, gfx, umc)
+    struct.pack_into("<3Q", b, 16, max_bw, energy, sysclk)
+    struct.pack_into("<7I", b, 40, accum, 0, ppt_res, 0, 0, 0, 0)
+    struct.pack_into("<4H", b, 68, pcie_width, pcie_speed, xgmi_width, xgmi_speed)
+    struct.pack_into("<2I", b, 76, 0, 0)
+    struct.pack_into("<5Q", b, 88, pcie_bw_acc, pcie_bw_inst, 0, 0, 0)
+    struct.pack_into("<2I", b, 128, 0, 0)
+    struct.pack_into("<8Q", b, 136, *xgmi_rd)
+    struct.pack_into("<8Q", b, 200, *xgmi_wr)
+    struct.pack_into("<8H", b, 264, *xgmi_status)
+    struct.pack_into("<Q", b, 288, fw_ts)
+    struct.pack_into("<8H", b, 296, *gfxclk)
+    struct.pack_into("<4H", b, 312, socclk, 0xFFFF, 0xFFFF, 0xFFFF)
+    struct.pack_into("<H", b, 336, uclk)
+    struct.pack_into("<H", b, 338, 1)
+    # xcp_stats[0].gfx_busy_acc at 344 + 120
+    struct.pack_into("<8Q", b, 344 + 120, *gfx_busy_acc)
+    return bytes(b)
+
+
+@dataclass
+class FakeGpu:
+    gpu_id: int
+    location_id: int            # (bus << 8) | (dev << 3) | fn
+    render_minor: int
+    unique_id: int = 0xE296A367FEF9A1BE
+    device_id: int = 0x75A3
+    vram_total: int = 309220868096
+    vram_used: int = 297766912
+    metrics: dict = field(default_factory=dict)
+
+
+class FakeHost:
+    def __init__(self, root: str | os.PathLike):
+        self.root = Path(root)
+        self.gpus: list[FakeGpu] = []
+
+    def _w(self, rel: str, data, mode: str = "w") -> Path:
+        p = self.root / rel
+        p.parent.mkdir(parents=True, exist_ok=True)
+        with open(p, mode) as fh:
+            fh.write(data)
+        return p
+
+    # ---- devices ----
+    def add_gpu(self, node: int, gpu: FakeGpu) -> FakeGpu:
+        nd = f"sys/class/kfd/kfd/topology/nodes/{node}"
+        self._w(f"{nd}/gpu_id", f"{gpu.gpu_id}\n")
+        self._w(f"{nd}/name", "ip discovery\n")
+        props = {"simd_count": 1024, "simd_per_cu": 4, "array_count": 32, "location_id": gpu.location_id,
+                 "domain": 0, "drm_render_minor": gpu.render_minor, "unique_id": gpu.unique_id,
+                 "device_id": gpu.device_id, "num_xcc": 8, "gfx_target_version": 90500,
+                 "max_engine_clk_fcompute": 2400}
+        self._w(f"{nd}/properties", "".join(f"{k} {v}\n" for k, v in props.items()))
+        dev = f"sys/class/drm/renderD{gpu.render_minor}/device"
+        self._w(f"{dev}/mem_info_vram_total", f"{gpu.vram_total}\n")
+        self._w(f"{dev}/mem_info_vram_used", f"{gpu.vram_used}\n")
+        self._w(f"{dev}/gpu_busy_percent", "0\n")
+        self._w(f"{dev}/mem_busy_percent", "0\n")
+        self._w(f"{dev}/hwmon/hwmon0/power1_input", "244000000\n")
+        self._w(f"{dev}/hwmon/hwmon0/power1_cap", "1400000000\n")
+        self._w(f"{dev}/hwmon/hwmon0/temp2_label", "junction\n")
+        self._w(f"{dev}/hwmon/hwmon0/temp2_input", "46000\n")
+        self._w(f"{dev}/hwmon/hwmon0/temp3_label", "mem\n")
+        self._w(f"{dev}/hwmon/hwmon0/temp3_input", "34000\n")
+        self.set_metrics(gpu, **gpu.metrics)
+        self.gpus.append(gpu)
+        return gpu
+
+    def add_cpu_node(self, node: int) -> None:
+        nd = f"sys/class/kfd/kfd/topology/nodes/{node}"
+        self._w(f"{nd}/gpu_id", "0\n")
+        self._w(f"{nd}/properties", "simd_count 0\nlocation_id 0\n")
+
+    def set_metrics(self, gpu: FakeGpu, **kw) -> None:
+        gpu.metrics = kw
+        dev = f"sys/class/drm/renderD{gpu.render_minor}/device"
+        self._w(f"{dev}/gpu_metrics", encode_gpu_metrics_v1_8(**kw), "wb")
+
+    def set_vram_used(self, gpu: FakeGpu, used: int) -> None:
+        self._w(f"sys/class/drm/renderD{gpu.render_minor}/device/mem_info_vram_used", f"{used}\n")
+
+    def remove_gpu_metrics(self, gpu: FakeGpu) -> None:
+        (self.root / f"sys/class/drm/renderD{gpu.render_minor}/device/gpu_metrics").unlink()
+
+    # ---- processes ----
+    def add_process(self, pid: int, cgroup: str, comm: str = "python3", gpus: dict | None = None,
+                    starttime: int = 1000) -> None:
+        """gpus: {gpu_id: (vram_bytes, cu_occupancy)}"""
+        self._w(f"proc/{pid}/cgroup", f"0::{cgroup}\n")
+        self._w(f"proc/{pid}/comm", comm + "\n")
+        fields = ["S"] + ["0"] * 18 + [str(starttime)] + ["0"] * 10
+        self._w(f"proc/{pid}/stat", f"{pid} ({comm}) " + " ".join(fields) + "\n")
+        for gid, (vram, cu) in (gpus or {}).items():
+            self.set_process_gpu(pid, gid, vram, cu)
+
+    def set_process_gpu(self, pid: int, gpu_id: int, vram: int, cu: int = 0, sdma_us: int = 0) -> None:
+        pd = f"sys/class/kfd/kfd/proc/{pid}"
+        self._w(f"{pd}/vram_{gpu_id}", f"{vram}\n")
+        self._w(f"{pd}/sdma_{gpu_id}", f"{sdma_us}\n")
+        self._w(f"{pd}/stats_{gpu_id}/cu_occupancy", f"{cu}\n")
+        self._w(f"{pd}/pasid", "32769\n")
+
+    def remove_process(self, pid: int) -> None:
+        import shutil
+        shutil.rmtree(self.root / f"sys/class/kfd/kfd/proc/{pid}", ignore_errors=True)
+        shutil.rmtree(self.root / f"proc/{pid}", ignore_errors=True)
+
+    def add_pod_logdir(self, namespace: str, pod: str, uid: str, containers=("main",)) -> None:
+        for c in containers:
+            d = self.root / f"var/log/pods/{namespace}_{pod}_{uid}/{c}"
+            d.mkdir(parents=True, exist_ok=True)
+
+
+def kubepods_cgroup(uid: str, container_id: str, qos: str = "burstable", driver: str = "systemd",
+                    runtime: str = "containerd") -> str:
+    """Builds a realistic cgroup-v2 path for a container of pod `uid`."""
+    prefix = {"containerd": "cri-containerd-", "crio": "crio-", "docker": "docker-"}[runtime]
+    if driver == "systemd":
+        u = uid.replace("-", "_")
+        if qos == "guaranteed":
+            return f"/kubepods.slice/kubepods-pod{u}.slice/{prefix}{container_id}.scope"
+        return (f"/kubepods.slice/kubepods-{qos}.slice/kubepods-{qos}-pod{u}.slice/"
+                f"{prefix}{container_id}.scope")
+    if qos == "guaranteed":
+        return f"/kubepods/pod{uid}/{container_id}"
+    return f"/kubepods/{qos}/pod{uid}/{container_id}"
+
+
+def mi355x_node(root, n_gpus: int = 8) -> FakeHost:
+    """An 8-GPU MI355X node (gpu_ids/BDFs shaped like the probe's real values)."""
+    h = FakeHost(root)
+    h.add_cpu_node(0)
+    h.add_cpu_node(1)
+    buses = [0x72, 0x5A, 0x23, 0xD9, 0xF1, 0xA4, 0x8B, 0x0A]
+    for i in range(n_gpus):
+        h.add_gpu(2 + i, FakeGpu(gpu_id=28720 + 17 * i, location_id=buses[i] << 8, render_minor=128 + 8 * i,
+                                 unique_id=0xE296A367FEF9A1BE + i))
+    return h
