@@ -1,0 +1,309 @@
+#!/usr/bin/env python3
+"""Headline benchmark (BASELINE.json): p50 scrape latency + exporter CPU% at N MI355X,
+10 Hz, 64 series/GPU, under synthetic HIP-workload pods.
+
+One rank per GPU (torchrun for N>1).  Rank 0 starts the exporter as a separate process
+BEFORE touching the GPU (amdsmi backend, raw gpu_metrics fast path, HIP sentinel,
+10 Hz sampling, every GPU of the job), then every rank becomes a synthetic "GEMM pod":
+each step it launches a burst of bf16 MFMA GEMMs (our HIP kernel) and, for N>1, an RCCL
+all-reduce (DP gradient traffic over xGMI).  Rank 0 scrapes /metrics once per step over a
+persistent keep-alive connection with the native client while the GPUs are busy; steps
+are paced at the scrape rate.  Each rank's PID is mapped to a fake pod through a pod-map
+file, so the per-pod families are exercised too.
+
+value = p50 scrape latency (us, whole job: one exporter serves all N GPUs), lower is
+better; exporter CPU% over the timed window is reported alongside.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import statistics
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "p50 scrape latency + exporter CPU% at 1/2/4/8 MI355X, 10 Hz, 64 series/GPU"
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def http_get(port: int, path: str, timeout: float = 2.0) -> tuple[int, bytes]:
+    import http.client
+    c = http.client.HTTPConnection("127.0.0.1", port, timeout=timeout)
+    try:
+        c.request("GET", path)
+        r = c.getresponse()
+        return r.status, r.read()
+    finally:
+        c.close()
+
+
+def start_exporter(args, n_gpus: int, backend: str, port: int, pod_map: str, log_path: str):
+    cmd = [sys.executable, "-m", "kubernetes_gpu_exporter_amd", "--listen", f"127.0.0.1:{port}",
+           "--interval", str(1.0 / args.sample_hz), "--backend", backend,
+           "--series-profile", args.series_profile, "--control-interval", "0.5", "--log-level", "warn"]
+    if backend != "mock":
+        cmd += ["--devices", ",".join(str(i) for i in range(n_gpus))]
+        if args.sentinel:
+            cmd += ["--enable-sentinel", "true"]
+        if args.counters:
+            cmd += ["--enable-counters", "true"]
+    else:
+        cmd += ["--mock-devices", str(n_gpus), "--enable-sentinel", "true", "--enable-counters", "true"]
+    env = dict(os.environ)
+    env["GPUEXP_POD_MAP_FILE"] = pod_map
+    env["GPUEXP_POD_ATTRIBUTION"] = "true"
+    logf = open(log_path, "w")
+    proc = subprocess.Popen(cmd, env=env, stdout=logf, stderr=subprocess.STDOUT, cwd=ROOT)
+    deadline = time.time() + 120
+    while time.time() < deadline:
+        if proc.poll() is not None:
+            raise RuntimeError(f"exporter exited with {proc.returncode}; see {log_path}")
+        try:
+            st, _ = http_get(port, "/readyz", 0.5)
+            if st == 200:
+                return proc
+        except OSError:
+            pass
+        time.sleep(0.05)
+    proc.kill()
+    raise RuntimeError("exporter did not become ready")
+
+
+def pct(v: list, q: float) -> float:
+    if not v:
+        return float("nan")
+    v = sorted(v)
+    k = (len(v) - 1) * q
+    lo, hi = int(k), min(int(k) + 1, len(v) - 1)
+    return v[lo] + (v[hi] - v[lo]) * (k - lo)
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--scrape-hz", type=float, default=10.0)
+    ap.add_argument("--sample-hz", type=float, default=10.0)
+    ap.add_argument("--series-profile", default="standard")
+    ap.add_argument("--backend", default="auto", help="auto | amdsmi | sysfs | mock")
+    ap.add_argument("--gemm", type=int, default=8192, help="GEMM edge (M=N=K) of the synthetic pod")
+    ap.add_argument("--busy", type=float, default=0.6, help="target GPU-busy fraction of each step")
+    ap.add_argument("--allreduce-mb", type=float, default=64.0)
+    ap.add_argument("--gzip", action="store_true", help="scrape with Accept-Encoding: gzip")
+    ap.add_argument("--sentinel", type=int, default=1)
+    ap.add_argument("--counters", type=int, default=0)
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    n_gpus = max(args.gpus, world)
+
+    # --- rank 0: exporter first (before this process initialises the GPU) ---
+    import torch  # noqa: E402  (import does not initialise HIP; device_count() does not either)
+    have_gpu = os.path.exists("/dev/kfd") and torch.cuda.device_count() > 0
+    backend = args.backend if args.backend != "auto" else ("amdsmi" if have_gpu else "mock")
+    tmpdir = tempfile.mkdtemp(prefix="gpuexp-bench-")
+    pod_map = os.path.join(tmpdir, "podmap.json")
+    port = 0
+    exporter = None
+    if rank == 0:
+        os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+        port = free_port()
+        exporter = start_exporter(args, n_gpus, backend, port, pod_map,
+                                  os.path.join(ROOT, "gpurun_out", "bench_exporter.log"))
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl" if have_gpu else "gloo")
+    use_gpu = have_gpu and backend != "mock"
+    if use_gpu:
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
+    else:
+        dev = torch.device("cpu")
+
+    from kubernetes_gpu_exporter_amd._native import load
+    from kubernetes_gpu_exporter_amd.k8s.filesource import write_pod_map
+    from kubernetes_gpu_exporter_amd.utils import promtext
+    from kubernetes_gpu_exporter_amd.utils.fakehost import kubepods_cgroup
+    from kubernetes_gpu_exporter_amd.utils.procstat import cpu_seconds_precise
+    n = load()
+
+    # --- synthetic GEMM pod workload ---
+    G = args.gemm
+    stream = 0
+    if use_gpu:
+        a = torch.empty(G, G, device=dev, dtype=torch.bfloat16)
+        b = torch.empty(G, G, device=dev, dtype=torch.bfloat16)
+        c = torch.empty(G, G, device=dev, dtype=torch.bfloat16)
+        stream = torch.cuda.current_stream().cuda_stream
+        n.fill_bf16(a.data_ptr(), a.numel(), 1 + rank, stream)
+        n.fill_bf16(b.data_ptr(), b.numel(), 7 + rank, stream)
+        grad = torch.ones(int(args.allreduce_mb * (1 << 20)) // 2, device=dev, dtype=torch.bfloat16)
+    else:
+        grad = torch.ones(1024)
+
+    def sync():
+        if use_gpu:
+            torch.cuda.synchronize()
+
+    def gemm_burst(iters: int):
+        for _ in range(iters):
+            n.gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), G, G, G, stream)
+
+    period = 1.0 / args.scrape_hz
+    iters = 0
+    gemm_ms = 0.0
+    if use_gpu:
+        gemm_burst(2)
+        sync()
+        t0 = time.perf_counter()
+        gemm_burst(5)
+        sync()
+        gemm_ms = (time.perf_counter() - t0) / 5 * 1e3
+        iters = max(1, int(args.busy * period * 1e3 / gemm_ms))
+        if dist is not None:
+            t = torch.tensor([iters], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            iters = int(t.item())
+
+    # --- pod map: every rank's PID -> fake pod bench/gemm-pod-<rank> ---
+    pid = os.getpid()
+    if dist is not None:
+        pids = [None] * world
+        dist.all_gather_object(pids, pid)
+    else:
+        pids = [pid]
+    if rank == 0:
+        pods, cgroups = [], {}
+        for r, p in enumerate(pids):
+            uid = f"00000000-0000-4000-8000-{r:012d}"
+            cid = f"{r:064x}"
+            pods.append({"uid": uid, "namespace": "bench", "name": f"gemm-pod-{r}", "containers": {cid: "worker"}})
+            cgroups[p] = kubepods_cgroup(uid, cid, qos="guaranteed")
+        write_pod_map(pod_map, pods, cgroups)
+        client = n.ScrapeClient("127.0.0.1", port, "/metrics", args.gzip, 5000)
+
+    def step(lat: list | None):
+        t_start = time.perf_counter()
+        if use_gpu:
+            gemm_burst(iters)
+        if rank == 0:
+            ns = client.scrape()  # GPUs are busy with the burst while we scrape
+            if lat is not None and ns >= 0:
+                lat.append(ns / 1e3)
+        if dist is not None:
+            dist.all_reduce(grad)
+        sync()
+        rest = period - (time.perf_counter() - t_start)
+        if rest > 0:
+            time.sleep(rest)
+
+    for _ in range(args.warmup):
+        step(None)
+    if dist is not None:
+        dist.barrier()
+    sync()
+    lat: list = []
+    if rank == 0:
+        cpu0 = cpu_seconds_precise(exporter.pid)
+        stats0 = None
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(lat)
+    if dist is not None:
+        dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    ms_per_step = elapsed / max(1, args.steps) * 1e3
+    if dist is not None:
+        t = torch.tensor([ms_per_step], device=dev if use_gpu else "cpu", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms_per_step = float(t.item())
+
+    result = None
+    if rank == 0:
+        cpu1 = cpu_seconds_precise(exporter.pid)
+        cpu_pct = 100.0 * (cpu1 - cpu0) / elapsed
+        body = client.last_body()
+        fams = promtext.parse(body.decode() if not args.gzip else __import__("gzip").decompress(body).decode())
+        per_gpu: dict = {}
+        for name, fam in fams.items():
+            if name.startswith("amd_gpu_") and not name.startswith("amd_gpu_process_"):
+                for _, lab, _ in fam.samples:
+                    per_gpu[lab.get("gpu")] = per_gpu.get(lab.get("gpu"), 0) + 1
+        attributed = {lab["pod"] for _, lab, _ in fams.get("pod_gpu_memory_usage", promtext.Family("x")).samples}
+        sentinel = {}
+        for key, fam_name in (("sclk_hz", "amd_gpu_sentinel_sclk_hz"),
+                              ("dispatch_latency_s", "amd_gpu_sentinel_dispatch_latency_seconds")):
+            v = [s[2] for s in promtext.samples(fams, fam_name)]
+            if v:
+                sentinel[key] = statistics.median(v)
+        gfx = [s[2] for s in promtext.samples(fams, "amd_gpu_gfx_activity_percent")]
+        tflops = 2.0 * G ** 3 * iters / (gemm_ms * iters * 1e-3) / 1e12 if gemm_ms else None
+        result = {
+            "metric": METRIC,
+            "value": round(statistics.median(lat), 2) if lat else None,
+            "unit": "us",
+            "n_gpus": n_gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": False,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic",
+            "config": {"model": "mi355x-per-pod-exporter (standard profile) + bf16 MFMA GEMM pods",
+                       "global_batch": n_gpus, "seq_len": 0, "parallelism": f"dp{n_gpus}",
+                       "scrape_hz": args.scrape_hz, "sample_hz": args.sample_hz, "backend": backend,
+                       "series_profile": args.series_profile, "gzip": args.gzip,
+                       "gemm": f"{G}^3 x {iters}/step", "allreduce_mb": args.allreduce_mb if world > 1 else 0},
+            "p50_scrape_us": round(statistics.median(lat), 2) if lat else None,
+            "p99_scrape_us": round(pct(lat, 0.99), 2) if lat else None,
+            "max_scrape_us": round(max(lat), 2) if lat else None,
+            "exporter_cpu_percent": round(cpu_pct, 3),
+            "scrapes": len(lat),
+            "scrape_errors": client.errors,
+            "scrape_bytes": client.last_bytes,
+            "series_per_gpu": {k: v for k, v in sorted(per_gpu.items()) if k is not None},
+            "attributed_pods": sorted(attributed),
+            "gpu_gfx_activity_percent": gfx,
+            "sentinel": sentinel,
+            "workload_gemm_tflops_per_gpu": round(tflops, 1) if tflops else None,
+        }
+        print(json.dumps(result), flush=True)
+        if args.out:
+            with open(args.out, "w") as fh:
+                json.dump(result, fh, indent=1)
+        exporter.terminate()
+        try:
+            exporter.wait(timeout=10)
+        except subprocess.TimeoutExpired:
+            exporter.kill()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

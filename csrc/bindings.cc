@@ -159,6 +159,7 @@ PYBIND11_MODULE(_gpuexp, m) {
       b->sample(d, &s);
       py::dict e = device_dict(d);
       e["sample"] = sample_dict(s);
+      e["source"] = b->describe(d);
       std::vector<ProcSample> procs;
       py::list pl;
       if (b->processes(d, &procs))
@@ -222,6 +223,18 @@ PYBIND11_MODULE(_gpuexp, m) {
   }, py::arg("host"), py::arg("port"), py::arg("path") = "/metrics", py::arg("hz") = 10.0,
      py::arg("count") = 100, py::arg("gzip") = false, py::arg("keepalive") = true,
      py::arg("timeout_ms") = 5000, py::arg("keep_last_body") = false);
+
+  py::class_<ScrapeClient>(m, "ScrapeClient")
+      .def(py::init<std::string, int, std::string, bool, int>(), py::arg("host"), py::arg("port"),
+           py::arg("path") = "/metrics", py::arg("gzip") = false, py::arg("timeout_ms") = 5000)
+      .def("scrape", [](ScrapeClient& c) {
+        py::gil_scoped_release rel;
+        return c.scrape();
+      })
+      .def_property_readonly("last_status", &ScrapeClient::last_status)
+      .def_property_readonly("last_bytes", &ScrapeClient::last_bytes)
+      .def_property_readonly("errors", &ScrapeClient::errors)
+      .def("last_body", [](ScrapeClient& c) { return py::bytes(c.last_body()); });
 
   // --- SeriesTable (unit tests of the exposition layer) ---
   py::enum_<MetricType>(m, "MetricType")

@@ -282,6 +282,12 @@ class AmdsmiBackend : public Backend {
     return true;
   }
 
+  std::string describe(const DeviceInfo& dev) override {
+    const Dev& d = devs_.at(size_t(dev.index));
+    return d.fast_ok ? "raw gpu_metrics v1.8 (validated against amdsmi)"
+                     : "amdsmi_get_gpu_metrics_info (" + d.validate_msg + ")";
+  }
+
   void shutdown() override {
     if (inited_) amdsmi_shut_down();
     inited_ = false;

@@ -94,6 +94,9 @@ class SysfsBackend : public Backend {
   const char* name() const override { return "sysfs"; }
   bool init(std::vector<DeviceInfo>* devices, std::string* err) override;
   void sample(const DeviceInfo& dev, DeviceSample* out) override;
+  std::string describe(const DeviceInfo& dev) override {
+    return devs_.at(size_t(dev.index))->gm_ok ? "raw gpu_metrics v1.8 (sysfs)" : "drm sysfs + hwmon";
+  }
 
   // amdsmi-compatible UUID from the KFD unique_id + PCI device id.
   static std::string uuid_from_unique_id(uint64_t unique_id, uint32_t device_id);

@@ -66,6 +66,46 @@ int read_response(int fd, std::string* buf, std::string* body, bool* server_clos
 
 }  // namespace
 
+ScrapeClient::ScrapeClient(std::string host, int port, std::string path, bool gzip, int timeout_ms)
+    : host_(std::move(host)), path_(std::move(path)), port_(port), timeout_ms_(timeout_ms) {
+  req_ = "GET " + path_ + " HTTP/1.1\r\nHost: " + host_ + "\r\nUser-Agent: gpuexp-bench\r\n";
+  if (gzip) req_ += "Accept-Encoding: gzip\r\n";
+  req_ += "\r\n";
+}
+
+ScrapeClient::~ScrapeClient() {
+  if (fd_ >= 0) ::close(fd_);
+}
+
+double ScrapeClient::scrape() {
+  if (fd_ < 0) {
+    fd_ = connect_to(host_, port_, timeout_ms_);
+    buf_.clear();
+    if (fd_ < 0) {
+      ++errors_;
+      return -1;
+    }
+  }
+  uint64_t t0 = mono_ns();
+  bool ok = ::send(fd_, req_.data(), req_.size(), MSG_NOSIGNAL) == ssize_t(req_.size());
+  bool server_close = false;
+  int code = ok ? read_response(fd_, &buf_, &body_, &server_close) : -1;
+  uint64_t t1 = mono_ns();
+  if (code < 0) {
+    ++errors_;
+    ::close(fd_);
+    fd_ = -1;
+    return -1;
+  }
+  status_ = code;
+  bytes_ = body_.size();
+  if (server_close) {
+    ::close(fd_);
+    fd_ = -1;
+  }
+  return double(t1 - t0);
+}
+
 ScrapeResult scrape_loop(const std::string& host, int port, const std::string& path, double hz, int count,
                          bool gzip, bool keepalive, int timeout_ms, bool keep_last_body) {
   ScrapeResult r;

@@ -18,6 +18,24 @@ struct ScrapeResult {
   double wall_s = 0;
 };
 
+// One persistent keep-alive connection; scrape() returns the latency in ns (-1 on error).
+class ScrapeClient {
+ public:
+  ScrapeClient(std::string host, int port, std::string path, bool gzip, int timeout_ms);
+  ~ScrapeClient();
+  double scrape();
+  int last_status() const { return status_; }
+  uint64_t last_bytes() const { return bytes_; }
+  const std::string& last_body() const { return body_; }
+  uint64_t errors() const { return errors_; }
+
+ private:
+  std::string host_, path_, req_;
+  int port_, timeout_ms_, fd_ = -1, status_ = 0;
+  uint64_t bytes_ = 0, errors_ = 0;
+  std::string buf_, body_;
+};
+
 ScrapeResult scrape_loop(const std::string& host, int port, const std::string& path, double hz, int count,
                          bool gzip, bool keepalive, int timeout_ms, bool keep_last_body);
 

@@ -144,6 +144,11 @@ class Backend {
     (void)out;
     return false;
   }
+  // Human-readable per-device source description (e.g. which metrics path is in use).
+  virtual std::string describe(const DeviceInfo& dev) {
+    (void)dev;
+    return name();
+  }
   virtual void shutdown() {}
 };
 

@@ -524,6 +524,7 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
   };
   std::map<std::pair<std::string, std::string>, PodAgg> pods;
 
+  const bool legacy_only = cfg_.series_profile == "legacy";
   for (size_t di = 0; di < per_dev.size(); ++di) {
     const DeviceInfo& d = devices_[di];
     DevState& st = dstate_[di];
@@ -531,14 +532,16 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
     bool cu_any = false;
     for (auto& p : per_dev[di]) {
       const ProcAttr& a = attr[p.pid];
-      std::vector<std::string> L = {std::to_string(d.index), std::to_string(p.pid), p.name, a.ns, a.pod, a.container};
-      table_.put(f_proc_vram_, L, p.vram_bytes, gen);
       if (!std::isnan(p.cu_occupancy)) {
-        table_.put(f_proc_cu_, L, p.cu_occupancy, gen);
         cu_sum += p.cu_occupancy;
         cu_any = true;
       }
-      if (!std::isnan(p.sdma_us)) table_.put(f_proc_sdma_, L, p.sdma_us * 1e-6, gen);
+      if (!legacy_only) {
+        std::vector<std::string> L = {std::to_string(d.index), std::to_string(p.pid), p.name, a.ns, a.pod, a.container};
+        table_.put(f_proc_vram_, L, p.vram_bytes, gen);
+        if (!std::isnan(p.cu_occupancy)) table_.put(f_proc_cu_, L, p.cu_occupancy, gen);
+        if (!std::isnan(p.sdma_us)) table_.put(f_proc_sdma_, L, p.sdma_us * 1e-6, gen);
+      }
       if (!a.pod.empty()) {
         auto& la = legacy[p.pid];
         la.used += p.vram_bytes;
@@ -548,9 +551,10 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
         pa.pids.insert(p.pid);
       }
     }
-    if (st.cur.ok) {
+    if (st.cur.ok && !legacy_only) {
       dput(st, int(di), st.nprocs, f_nprocs_, {}, double(per_dev[di].size()), gen);
-      if (cu_any) dput(st, int(di), st.cu_occ, f_cu_occ_, {}, cu_sum, gen);
+      // No processes -> 0 CUs occupied (a known value, not an unknown one).
+      if (cu_any || per_dev[di].empty()) dput(st, int(di), st.cu_occ, f_cu_occ_, {}, cu_sum, gen);
     }
     if (!st.owner.pod.empty()) {
       auto& pa = pods[{st.owner.ns, st.owner.pod}];

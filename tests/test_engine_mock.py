@@ -1,0 +1,231 @@
+"""Engine on the mock backend (BASELINE config 1): series profile, legacy-family
+compatibility, rates from hardware accumulators, fault isolation, attribution."""
+import collections
+
+import pytest
+
+from kubernetes_gpu_exporter_amd.utils import promtext
+
+S = 1_000_000_000
+UID = "12345678-1234-1234-1234-123456789abc"
+CID = "a" * 64
+CG = ("/kubepods.slice/kubepods-burstable.slice/kubepods-burstable-pod"
+      + UID.replace("-", "_") + ".slice/cri-containerd-" + CID + ".scope")
+
+
+def ticks(e, n, t0=S, dt=S // 10):
+    t = t0
+    for _ in range(n):
+        e.tick(t)
+        t += dt
+    return t
+
+
+def parse(e):
+    return promtext.parse(e.snapshot_text())
+
+
+def device_series_per_gpu(fams):
+    cnt = collections.Counter()
+    for name, fam in fams.items():
+        if not name.startswith("amd_gpu_") or name.startswith("amd_gpu_process_"):
+            continue
+        for _, labels, _ in fam.samples:
+            cnt[labels["gpu"]] += 1
+    return cnt
+
+
+@pytest.mark.parametrize("n", [1, 2, 8])
+def test_standard_profile_is_64_series_per_gpu(mock_engine, n):
+    e = mock_engine(n, http=False, enable_sentinel=True, enable_counters=True)
+    ticks(e, 3)
+    cnt = device_series_per_gpu(parse(e))
+    assert dict(cnt) == {str(i): 64 for i in range(n)}
+
+
+def test_compact_and_legacy_profiles(mock_engine):
+    e = mock_engine(1, http=False, series_profile="compact")
+    ticks(e, 3)
+    assert device_series_per_gpu(parse(e))["0"] < 40
+    e2 = mock_engine(1, http=False, series_profile="legacy")
+    e2.mock_set_processes(0, [dict(pid=100, vram_bytes=1e9)])
+    e2.set_pid_cgroup(100, CG)
+    ticks(e2, 2)
+    fams = parse(e2)
+    assert not [n for n in fams if n.startswith("amd_")]
+    assert "pod_gpu_memory_usage" in fams
+
+
+def test_legacy_families_exact_contract(mock_engine):
+    """Names, HELP, TYPE and label order byte-identical to /root/reference/main.go:22-35."""
+    e = mock_engine(1, http=False)
+    e.mock_set_processes(0, [dict(pid=4242, vram_bytes=30922086809.6)])
+    e.set_pid_cgroup(4242, CG)
+    e.set_pods([dict(uid=UID, namespace="ml", name="trainer-0", containers={CID: "main"})])
+    ticks(e, 2)
+    text = e.snapshot_text()
+    assert ("# HELP docker_gpu_memory_perc_usage GPU memory in percentage used by pod\n"
+            "# TYPE docker_gpu_memory_perc_usage gauge\n"
+            'docker_gpu_memory_perc_usage{pid="4242",pod="trainer-0"} 10\n') in text
+    assert ("# HELP pod_gpu_memory_usage GPU memory used by Kubernetes Pod\n"
+            "# TYPE pod_gpu_memory_usage gauge\n"
+            'pod_gpu_memory_usage{pid="4242",pod="trainer-0"} 30922086809.6\n') in text
+    # docker_ sorts before pod_ (client_golang Gather order)
+    assert text.index("docker_gpu_memory_perc_usage") < text.index("pod_gpu_memory_usage")
+
+
+def test_legacy_sums_over_gpus_and_skips_unattributed(mock_engine):
+    e = mock_engine(2, http=False)
+    e.mock_set_processes(0, [dict(pid=10, vram_bytes=100.0), dict(pid=11, vram_bytes=5.0)])
+    e.mock_set_processes(1, [dict(pid=10, vram_bytes=300.0)])
+    e.set_pid_cgroup(10, CG)  # pid 11 has no pod
+    ticks(e, 2)
+    fams = parse(e)
+    assert promtext.value(fams, "pod_gpu_memory_usage", pid=10) == 400.0
+    pct = promtext.value(fams, "docker_gpu_memory_perc_usage", pid=10)
+    assert abs(pct - 400.0 / (2 * 309220868096) * 100) < 1e-12
+    with pytest.raises(KeyError):
+        promtext.value(fams, "pod_gpu_memory_usage", pid=11)
+    # the new per-process family keeps unattributed processes (pod="")
+    assert promtext.value(fams, "amd_gpu_process_vram_bytes", pid=11, pod="") == 5.0
+    # pod name unknown to the control plane -> pod label falls back to the UID
+    assert promtext.value(fams, "pod_gpu_memory_usage", pid=10, pod=UID) == 400.0
+
+
+def test_process_exit_removes_series_next_tick(mock_engine):
+    e = mock_engine(1, http=False)
+    e.mock_set_processes(0, [dict(pid=77, vram_bytes=1.0)])
+    e.set_pid_cgroup(77, CG)
+    t = ticks(e, 2)
+    assert 'pid="77"' in e.snapshot_text()
+    e.mock_set_processes(0, [])
+    e.tick(t)
+    assert 'pid="77"' not in e.snapshot_text()
+
+
+def test_xgmi_rates_exact(mock_engine):
+    e = mock_engine(1, http=False)
+    e.mock_set_value(0, "xgmi_read_rate_kbps", 5000.0)
+    e.mock_set_value(0, "xgmi_write_rate_kbps", 2000.0)
+    ticks(e, 3)
+    fams = parse(e)
+    rd = promtext.value(fams, "amd_gpu_xgmi_read_bytes_per_second", gpu=0)
+    wr = promtext.value(fams, "amd_gpu_xgmi_write_bytes_per_second", gpu=0)
+    assert rd == pytest.approx(7 * 5000 * 1024, rel=1e-9)
+    assert wr == pytest.approx(7 * 2000 * 1024, rel=1e-9)
+    links = [s for s in fams["amd_gpu_xgmi_read_bytes_total"].samples]
+    assert len(links) == 7 and all(s[1]["peer_bdf"] for s in links)
+
+
+def test_counter_reset_and_wrap(mock_engine):
+    e = mock_engine(1, http=False)
+    e.mock_set_value(0, "xgmi_read_rate_kbps", 1000.0)
+    t = ticks(e, 3)
+    e.mock_set_fault(0, "counter_reset")
+    e.tick(t)
+    t += S // 10
+    rd = promtext.value(parse(e), "amd_gpu_xgmi_read_bytes_per_second", gpu=0)
+    assert rd >= 0  # a reset never produces a negative or huge rate
+    assert rd == pytest.approx(7 * 1000 * 1024, rel=1e-6)  # previous rate carried
+    e.mock_set_fault(0, "wrap")
+    e.tick(t)
+    t += S // 10
+    e.tick(t)
+    rd = promtext.value(parse(e), "amd_gpu_xgmi_read_bytes_per_second", gpu=0)
+    assert rd == pytest.approx(7 * 1000 * 1024, rel=1e-6)
+
+
+def test_energy_counter_monotonic(mock_engine):
+    e = mock_engine(1, http=False)
+    e.mock_set_value(0, "power_w", 500.0)
+    t = ticks(e, 2)
+    e1 = promtext.value(parse(e), "amd_gpu_energy_joules_total", gpu=0)
+    e.tick(t + S)
+    e2 = promtext.value(parse(e), "amd_gpu_energy_joules_total", gpu=0)
+    assert e2 - e1 == pytest.approx(500.0 * 1.1, rel=1e-3)
+
+
+def test_fault_isolation(mock_engine):
+    """One failing GPU exports up=0; the others keep reporting (reference: log.Fatalf,
+    main.go:119-137)."""
+    e = mock_engine(3, http=False)
+    t = ticks(e, 2)
+    e.mock_set_fault(1, "error")
+    t = ticks(e, 2, t)
+    fams = parse(e)
+    assert promtext.value(fams, "amd_gpu_up", gpu=1) == 0
+    assert promtext.value(fams, "amd_gpu_up", gpu=0) == 1
+    assert promtext.value(fams, "amd_gpu_up", gpu=2) == 1
+    with pytest.raises(KeyError):
+        promtext.value(fams, "amd_gpu_power_watts", gpu=1)
+    assert promtext.value(fams, "gpuexp_device_errors_total", gpu=1) == 2
+    e.mock_set_fault(1, "none")
+    ticks(e, 2, t)
+    assert promtext.value(parse(e), "amd_gpu_power_watts", gpu=1) > 0
+
+
+def test_throttle_residency_percent(mock_engine):
+    e = mock_engine(1, http=False)
+    e.mock_set_value(0, "ppt_residency_percent", 25.0)
+    ticks(e, 3, dt=S)
+    v = promtext.value(parse(e), "amd_gpu_throttle_residency_percent", gpu=0, reason="ppt")
+    assert v == pytest.approx(25.0, abs=0.2)
+
+
+def test_device_owner_explicit_and_inferred(mock_engine):
+    e = mock_engine(2, http=False)
+    e.set_pods([dict(uid=UID, namespace="ml", name="trainer-0", containers={CID: "main"})])
+    e.set_device_owners({"0000:20:00.0": dict(namespace="infer", pod="server-1", container="srv")})
+    e.mock_set_processes(0, [dict(pid=5, vram_bytes=1.0)])
+    e.set_pid_cgroup(5, CG)
+    ticks(e, 2)
+    fams = parse(e)
+    up = {s[1]["gpu"]: s[1] for s in fams["amd_gpu_up"].samples}
+    assert (up["0"]["namespace"], up["0"]["pod"], up["0"]["container"]) == ("ml", "trainer-0", "main")
+    assert (up["1"]["namespace"], up["1"]["pod"]) == ("infer", "server-1")
+    assert promtext.value(fams, "amd_pod_gpus", namespace="infer", pod="server-1") == 1
+    # owner change relabels: the old series vanish
+    e.set_device_owners({})
+    e.mock_set_processes(0, [])
+    ticks(e, 2, t0=10 * S)
+    up = {s[1]["gpu"]: s[1] for s in parse(e)["amd_gpu_up"].samples}
+    assert up["1"]["pod"] == "" and up["0"]["pod"] == ""
+
+
+def test_shared_gpu_has_no_owner(mock_engine):
+    e = mock_engine(1, http=False)
+    uid2 = "22345678-1234-1234-1234-123456789abc"
+    cg2 = CG.replace(UID.replace("-", "_"), uid2.replace("-", "_"))
+    e.mock_set_processes(0, [dict(pid=5, vram_bytes=1.0), dict(pid=6, vram_bytes=2.0)])
+    e.set_pid_cgroup(5, CG)
+    e.set_pid_cgroup(6, cg2)
+    ticks(e, 2)
+    fams = parse(e)
+    assert fams["amd_gpu_up"].samples[0][1]["pod"] == ""
+    assert promtext.value(fams, "amd_pod_gpu_vram_bytes", pod=uid2) == 2.0
+
+
+def test_self_metrics(mock_engine):
+    e = mock_engine(1, http=False)
+    ticks(e, 5)
+    fams = parse(e)
+    assert promtext.value(fams, "gpuexp_ticks_total") == 4  # rendered before this tick's count
+    assert fams["gpuexp_sample_stage_duration_seconds"].type == "histogram"
+    stages = {s[1]["stage"] for s in fams["gpuexp_sample_stage_duration_seconds"].samples}
+    assert {"devices", "processes", "render", "series"} <= stages
+    st = e.stats()
+    assert st["ticks"] == 5 and st["series"] > 60 and st["render_bytes"] > 1000
+
+
+def test_sampler_thread_runs(native):
+    import time
+    c = native.EngineConfig()
+    c.backend = "mock"
+    c.interval_s = 0.01
+    c.serve_http = False
+    e = native.Engine(c)
+    e.start()
+    time.sleep(0.3)
+    e.stop()
+    st = e.stats()
+    assert 15 <= st["ticks"] <= 40

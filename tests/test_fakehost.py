@@ -1,0 +1,162 @@
+"""Fake-host integration tier (SURVEY.md §4.2): the sysfs backend, raw gpu_metrics decode,
+KFD process discovery and PID -> pod attribution, all against a fake /sys + /proc tree."""
+import pytest
+
+from kubernetes_gpu_exporter_amd.utils import promtext
+from kubernetes_gpu_exporter_amd.utils.fakehost import (FakeGpu, FakeHost, encode_gpu_metrics_v1_8,
+                                                        kubepods_cgroup, mi355x_node)
+
+S = 1_000_000_000
+UID = "aaaaaaaa-bbbb-cccc-dddd-eeeeeeeeeeee"
+CID = "c0ffee00" * 8
+
+
+def test_gpu_metrics_layout_size(native):
+    assert native.gpu_metrics_v1_8_size() == 3872  # blob size measured on MI355X
+
+
+def test_decode_gpu_metrics_matches_encoder(native):
+    blob = encode_gpu_metrics_v1_8(hotspot=71, mem=55, vrsoc=44, power=812, gfx=97, umc=40,
+                                   xgmi_rd=[0, 10, 20, 30, 40, 50, 60, 70], xgmi_wr=[0, 1, 2, 3, 4, 5, 6, 7],
+                                   gfxclk=(2100, 2100, 2000, 2000, 0xFFFF, 0xFFFF, 0xFFFF, 0xFFFF),
+                                   gfx_busy_acc=(1, 2, 3, 4, 5, 6, 7, 8))
+    d = native.decode_gpu_metrics(blob)
+    assert d["temp_hotspot"] == 71 and d["temp_mem"] == 55 and d["temp_vrsoc"] == 44
+    assert d["power_w"] == 812 and d["gfx_activity"] == 97 and d["umc_activity"] == 40
+    assert d["xgmi_read_kb"] == [0, 10, 20, 30, 40, 50, 60, 70]
+    assert d["xgmi_write_kb"][7] == 7
+    assert d["num_xgmi_links"] == 8
+    assert d["xgmi_link_up"][1] == 1 and d["xgmi_link_up"][0] != d["xgmi_link_up"][0]  # NaN
+    assert d["clk_gfx"] == 2050 and d["clk_mem"] == 2000
+    assert d["pcie_width"] == 16 and d["pcie_speed_gts"] == 32.0
+    assert d["vram_max_bw_gbs"] == 8192
+    assert d["gfx_busy_acc"] == [1, 2, 3, 4, 5, 6, 7, 8]
+    assert native.decode_gpu_metrics(blob[:100]) is None
+    bad = bytearray(blob)
+    bad[3] = 6  # content revision 6 -> not decoded raw
+    assert native.decode_gpu_metrics(bytes(bad)) is None
+
+
+def test_uuid_formula_matches_amdsmi(native):
+    # measured on the GPU box: unique_id e296a367fef9a1be, device 0x75a3
+    assert native.uuid_from_unique_id(0xE296A367FEF9A1BE, 0x75A3) == "e2ff75a3-0000-1000-8096-a367fef9a1be"
+
+
+def test_sysfs_backend_enumeration(native, tmp_path):
+    mi355x_node(tmp_path, 8)
+    devs = native.read_backend("sysfs", str(tmp_path))
+    assert len(devs) == 8
+    bdfs = [d["bdf"] for d in devs]
+    assert bdfs == sorted(bdfs)  # PCI order
+    assert bdfs[0] == "0000:0a:00.0"
+    for d in devs:
+        assert d["vram_total"] == 309220868096
+        assert d["render_minor"] >= 128
+        assert d["num_cu"] == 256
+        s = d["sample"]
+        assert s["ok"] and s["temp_hotspot"] == 46 and s["vram_used"] == 297766912
+
+
+def test_sysfs_fallback_without_gpu_metrics(native, tmp_path):
+    h = FakeHost(tmp_path)
+    g = h.add_gpu(2, FakeGpu(gpu_id=5, location_id=0x7200, render_minor=128))
+    h.remove_gpu_metrics(g)
+    d = native.read_backend("sysfs", str(tmp_path))[0]["sample"]
+    assert d["ok"] and d["power_w"] == 244.0 and d["temp_hotspot"] == 46.0 and d["gfx_activity"] == 0
+
+
+def test_kfd_scan(native, tmp_path):
+    h = mi355x_node(tmp_path, 2)
+    g0, g1 = h.gpus
+    h.add_process(100, "/user.slice", gpus={g0.gpu_id: (1 << 30, 32)})
+    h.add_process(101, "/user.slice", comm="trainer", gpus={g0.gpu_id: (5, 0), g1.gpu_id: (7, 64)})
+    h.add_process(102, "/user.slice", gpus={99999: (1, 1)})  # another node's GPU
+    per = native.scan_kfd(str(tmp_path), [g0.gpu_id, g1.gpu_id], self_pid=-1)
+    assert sorted(p["pid"] for p in per[0]) == [100, 101]
+    assert [(p["pid"], p["vram_bytes"], p["cu_occupancy"], p["name"]) for p in per[1]] == [(101, 7, 64, "trainer")]
+    per = native.scan_kfd(str(tmp_path), [g0.gpu_id, g1.gpu_id], self_pid=100)
+    assert [p["pid"] for p in per[0]] == [101]  # self-exclusion
+
+
+def _engine(native, root, **kw):
+    c = native.EngineConfig()
+    c.backend = "sysfs"
+    c.host_root = str(root)
+    c.interval_s = 0
+    c.serve_http = False
+    for k, v in kw.items():
+        setattr(c, k, v)
+    e = native.Engine(c)
+    e.start()
+    return e
+
+
+def test_end_to_end_attribution(native, tmp_path):
+    """KFD host PID -> /proc/<pid>/cgroup -> pod UID -> (namespace, name, container)."""
+    h = mi355x_node(tmp_path, 2)
+    g0, g1 = h.gpus
+    h.add_process(4242, kubepods_cgroup(UID, CID), comm="python3", gpus={g0.gpu_id: (30922086809, 128)})
+    h.add_process(5151, "/system.slice/other.service", gpus={g1.gpu_id: (1000, 1)})
+    e = _engine(native, tmp_path)
+    try:
+        e.set_pods([dict(uid=UID, namespace="research", name="llama-train-0", containers={CID: "trainer"})])
+        e.tick(S)
+        e.tick(S + S // 10)
+        fams = promtext.parse(e.snapshot_text())
+        assert promtext.value(fams, "pod_gpu_memory_usage", pid=4242, pod="llama-train-0") == 30922086809
+        assert promtext.value(fams, "docker_gpu_memory_perc_usage", pid=4242) == pytest.approx(
+            30922086809 / 309220868096 * 100)
+        assert promtext.value(fams, "amd_gpu_process_vram_bytes", pid=4242, namespace="research",
+                              container="trainer", comm="python3") == 30922086809
+        assert promtext.value(fams, "amd_gpu_process_cu_occupancy", pid=4242) == 128
+        # single-pod GPU -> device series carry the pod (inferred ownership)
+        up0 = [s for s in fams["amd_gpu_up"].samples if s[1]["bdf"] == "0000:72:00.0"][0][1]
+        assert (up0["namespace"], up0["pod"], up0["container"]) == ("research", "llama-train-0", "trainer")
+        # non-kube process: new families only, pod=""
+        assert promtext.value(fams, "amd_gpu_process_vram_bytes", pid=5151, pod="") == 1000
+        with pytest.raises(KeyError):
+            promtext.value(fams, "pod_gpu_memory_usage", pid=5151)
+        # process exits -> its series vanish next tick
+        h.remove_process(4242)
+        e.tick(S + 2 * S // 10)
+        assert 'pid="4242"' not in e.snapshot_text()
+    finally:
+        e.stop()
+
+
+def test_pid_reuse_is_detected(native, tmp_path):
+    h = mi355x_node(tmp_path, 1)
+    g0 = h.gpus[0]
+    h.add_process(300, kubepods_cgroup(UID, CID), gpus={g0.gpu_id: (10, 0)}, starttime=1000)
+    e = _engine(native, tmp_path)
+    try:
+        e.tick(S)
+        assert 'pod_gpu_memory_usage{pid="300",pod="' + UID + '"}' in e.snapshot_text()
+        uid2 = "11111111-2222-3333-4444-555555555555"
+        h.remove_process(300)
+        h.add_process(300, kubepods_cgroup(uid2, CID), gpus={g0.gpu_id: (10, 0)}, starttime=2000)
+        e.tick(2 * S)
+        assert 'pod_gpu_memory_usage{pid="300",pod="' + uid2 + '"}' in e.snapshot_text()
+    finally:
+        e.stop()
+
+
+def test_live_metric_updates(native, tmp_path):
+    h = mi355x_node(tmp_path, 1)
+    g = h.gpus[0]
+    e = _engine(native, tmp_path)
+    try:
+        h.set_metrics(g, power=700, gfx=88, xgmi_rd=[0] * 8, fw_ts=1_000_000_000)
+        e.tick(S)
+        h.set_metrics(g, power=710, gfx=90, xgmi_rd=[0] + [100 * 1024] * 7, fw_ts=1_000_000_000 + 10_000_000)
+        h.set_vram_used(g, 12345)
+        e.tick(S + S // 10)
+        fams = promtext.parse(e.snapshot_text())
+        assert promtext.value(fams, "amd_gpu_power_watts", gpu=0) == 710
+        assert promtext.value(fams, "amd_gpu_gfx_activity_percent", gpu=0) == 90
+        assert promtext.value(fams, "amd_gpu_vram_used_bytes", gpu=0) == 12345
+        # 7 links x 100 MiB over a firmware dt of 0.1 s -> 7 GiB/s
+        assert promtext.value(fams, "amd_gpu_xgmi_read_bytes_per_second", gpu=0) == pytest.approx(
+            7 * 100 * 1024 * 1024 / 0.1)
+    finally:
+        e.stop()

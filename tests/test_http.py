@@ -1,0 +1,168 @@
+"""HTTP server over real sockets: status codes, keep-alive, pipelining, gzip, HEAD,
+readiness, and snapshot consistency under concurrent scraping at 100 Hz sampling."""
+import gzip
+import http.client
+import socket
+import threading
+import time
+
+import pytest
+
+from kubernetes_gpu_exporter_amd.utils import promtext
+
+
+def req(port, path, method="GET", headers=None):
+    c = http.client.HTTPConnection("127.0.0.1", port, timeout=5)
+    c.request(method, path, headers=headers or {})
+    r = c.getresponse()
+    body = r.read()
+    c.close()
+    return r, body
+
+
+def test_not_ready_before_first_tick(mock_engine):
+    e = mock_engine(1)
+    r, body = req(e.http_port, "/metrics")
+    assert r.status == 503
+    r, _ = req(e.http_port, "/readyz")
+    assert r.status == 503
+    r, body = req(e.http_port, "/healthz")
+    assert r.status == 200 and body == b"ok\n"
+
+
+def test_metrics_endpoint(mock_engine):
+    e = mock_engine(1)
+    e.tick(1_000_000_000)
+    r, body = req(e.http_port, "/metrics")
+    assert r.status == 200
+    assert r.getheader("Content-Type") == "text/plain; version=0.0.4; charset=utf-8"
+    assert body.decode() == e.snapshot_text()
+    promtext.parse(body.decode())
+    r, body = req(e.http_port, "/metrics?x=1")
+    assert r.status == 200
+    r, _ = req(e.http_port, "/readyz")
+    assert r.status == 200
+    r, body = req(e.http_port, "/metrics", method="HEAD")
+    assert r.status == 200 and body == b"" and int(r.getheader("Content-Length")) > 0
+    r, _ = req(e.http_port, "/nope")
+    assert r.status == 404
+    r, _ = req(e.http_port, "/metrics", method="POST")
+    assert r.status == 405
+    r, body = req(e.http_port, "/")
+    assert r.status == 200 and b"/metrics" in body
+
+
+def test_custom_path(mock_engine, native):
+    c = native.HttpConfig()
+    e = mock_engine(1)
+    e.tick(1)
+    # default path; a custom path is exercised through the exporter config test
+    r, _ = req(e.http_port, "/metrics")
+    assert r.status == 200
+
+
+def test_keepalive_and_pipelining(mock_engine):
+    e = mock_engine(1)
+    e.tick(1_000_000_000)
+    s = socket.create_connection(("127.0.0.1", e.http_port))
+    s.sendall(b"GET /metrics HTTP/1.1\r\nHost: x\r\n\r\nGET /healthz HTTP/1.1\r\nHost: x\r\n\r\n"
+              b"GET /metrics HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n")
+    data = b""
+    while True:
+        chunk = s.recv(1 << 16)
+        if not chunk:
+            break
+        data += chunk
+    s.close()
+    assert data.count(b"HTTP/1.1 200 OK") == 3
+    assert b"Connection: close" in data
+
+
+def test_gzip_negotiation(mock_engine):
+    e = mock_engine(1)
+    e.tick(1_000_000_000)
+    r, body = req(e.http_port, "/metrics", headers={"Accept-Encoding": "gzip"})
+    assert r.status == 200 and r.getheader("Content-Encoding") is None  # not yet compressed
+    e.tick(1_100_000_000)  # sampler now pre-compresses each tick
+    r, body = req(e.http_port, "/metrics", headers={"Accept-Encoding": "gzip, deflate"})
+    assert r.getheader("Content-Encoding") == "gzip"
+    assert gzip.decompress(body).decode() == e.snapshot_text()
+    r, body = req(e.http_port, "/metrics")
+    assert r.getheader("Content-Encoding") is None
+
+
+def test_bad_request_closes(mock_engine):
+    e = mock_engine(1)
+    s = socket.create_connection(("127.0.0.1", e.http_port))
+    s.sendall(b"GARBAGE\r\n\r\n")
+    data = s.recv(4096)
+    assert b"400" in data
+    s.close()
+
+
+def test_concurrent_scrapes_see_consistent_snapshots(native):
+    """Sampler at 100 Hz + 4 scraper threads: every body parses and ticks never go back."""
+    c = native.EngineConfig()
+    c.backend = "mock"
+    c.mock_devices = 8
+    c.interval_s = 0.01
+    c.http.host = "127.0.0.1"
+    c.http.port = 0
+    c.http.threads = 2
+    e = native.Engine(c)
+    e.start()
+    try:
+        deadline = time.time() + 5
+        while time.time() < deadline:
+            r, _ = req(e.http_port, "/readyz")
+            if r.status == 200:
+                break
+            time.sleep(0.01)
+        errors = []
+
+        def scraper():
+            conn = http.client.HTTPConnection("127.0.0.1", e.http_port, timeout=5)
+            last = -1
+            for _ in range(60):
+                conn.request("GET", "/metrics")
+                body = conn.getresponse().read().decode()
+                try:
+                    fams = promtext.parse(body)
+                    t = promtext.value(fams, "gpuexp_ticks_total")
+                    if t < last:
+                        errors.append(f"ticks went back {last}->{t}")
+                    last = t
+                    # one consistent tick: all 8 GPUs present in every family we check
+                    assert len(fams["amd_gpu_up"].samples) == 8
+                except Exception as ex:  # noqa: BLE001
+                    errors.append(repr(ex))
+            conn.close()
+
+        th = [threading.Thread(target=scraper) for _ in range(4)]
+        [t.start() for t in th]
+        [t.join() for t in th]
+        assert not errors, errors[:3]
+    finally:
+        e.stop()
+
+
+def test_native_scrape_client(mock_engine, native):
+    e = mock_engine(2)
+    e.tick(1_000_000_000)
+    r = native.scrape_loop("127.0.0.1", e.http_port, "/metrics", hz=0, count=50, keep_last_body=True)
+    assert r["errors"] == 0 and r["non200"] == 0 and len(r["latency_ns"]) == 50
+    assert r["last_body"].decode() == e.snapshot_text()
+    r = native.scrape_loop("127.0.0.1", e.http_port, "/metrics", hz=200, count=20, keepalive=False)
+    assert r["errors"] == 0 and 0.08 < r["wall_s"] < 1.0
+
+
+def test_many_connections(mock_engine):
+    e = mock_engine(1)
+    e.tick(1)
+    socks = [socket.create_connection(("127.0.0.1", e.http_port)) for _ in range(200)]
+    for s in socks:
+        s.sendall(b"GET /healthz HTTP/1.1\r\nHost: x\r\n\r\n")
+    for s in socks:
+        assert s.recv(4096).startswith(b"HTTP/1.1 200")
+        s.close()
+    assert e.stats()["http_requests"] >= 200
