@@ -146,6 +146,8 @@ def main() -> int:
     from kubernetes_gpu_exporter_amd.utils.fakehost import kubepods_cgroup
     from kubernetes_gpu_exporter_amd.utils.procstat import cpu_seconds_precise
     n = load()
+    from kubernetes_gpu_exporter_amd.ops.gemm import kernels
+    kern = kernels() if use_gpu else None
 
     # --- synthetic GEMM pod workload ---
     G = args.gemm
@@ -155,8 +157,8 @@ def main() -> int:
         b = torch.empty(G, G, device=dev, dtype=torch.bfloat16)
         c = torch.empty(G, G, device=dev, dtype=torch.bfloat16)
         stream = torch.cuda.current_stream().cuda_stream
-        n.fill_bf16(a.data_ptr(), a.numel(), 1 + rank, stream)
-        n.fill_bf16(b.data_ptr(), b.numel(), 7 + rank, stream)
+        kern.fill_bf16(a.data_ptr(), a.numel(), 1 + rank, stream)
+        kern.fill_bf16(b.data_ptr(), b.numel(), 7 + rank, stream)
         grad = torch.ones(int(args.allreduce_mb * (1 << 20)) // 2, device=dev, dtype=torch.bfloat16)
     else:
         grad = torch.ones(1024)
@@ -167,7 +169,7 @@ def main() -> int:
 
     def gemm_burst(iters: int):
         for _ in range(iters):
-            n.gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), G, G, G, stream)
+            kern.gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), G, G, G, stream)
 
     period = 1.0 / args.scrape_hz
     iters = 0

@@ -34,7 +34,8 @@ CORE_CC = [
     "gpuexp/backend_amdsmi.cc", "gpuexp/procs.cc", "gpuexp/engine.cc",
     "gpuexp/optional_sources.cc", "gpuexp/client.cc", "bindings.cc",
 ]
-CORE_HIP = ["gpuexp/sentinel.hip", "kernels/gemm_bf16.hip", "kernels/kernels_bindings.hip"]
+SENTINEL_HIP = ["gpuexp/sentinel.hip"]
+KERNELS_HIP = ["kernels/gemm_bf16.hip", "kernels/kernels_bindings.hip"]
 ROCPROF_CC = ["gpuexp/rocprof_plugin.cc"]
 TRACER_CC = ["gpuexp/rccl_tracer.cc"]
 
@@ -89,17 +90,27 @@ def compile_one(src_rel: str, hdr_mtime: float, force: bool, sanitize: str | Non
     return obj
 
 
-def link_module(objs: list[Path], sanitize: str | None) -> Path:
-    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
-    out = PKG / f"_gpuexp{suffix}"
+def _ext(name: str) -> Path:
+    return PKG / f"{name}{sysconfig.get_config_var('EXT_SUFFIX') or '.so'}"
+
+
+def link_core(objs: list[Path], sanitize: str | None) -> Path:
+    """The telemetry core links NO HIP runtime (see sentinel.hip's factory comment)."""
+    out = _ext("_gpuexp")
     tmp = out.with_suffix(".tmp.so")
-    cmd = [str(ROCM / "bin" / "hipcc"), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)]
-    cmd += [str(o) for o in objs]
-    cmd += [f"-L{ROCM / 'lib'}", "-lamd_smi", "-lamdhip64", "-lhsa-runtime64", "-lz", "-ldl", "-lpthread",
-            f"-Wl,-rpath,{ROCM / 'lib'}"]
+    cmd = ["g++", "-shared", "-fPIC", "-o", str(tmp)] + [str(o) for o in objs]
+    cmd += [f"-L{ROCM / 'lib'}", "-lamd_smi", "-lz", "-ldl", "-lpthread", f"-Wl,-rpath,{ROCM / 'lib'}"]
     if sanitize:
         cmd += [f"-fsanitize={sanitize}"]
     _run(cmd)
+    os.replace(tmp, out)
+    return out
+
+
+def link_hip(objs: list[Path], out: Path, libs: list[str]) -> Path:
+    tmp = out.with_suffix(".tmp.so")
+    _run([str(ROCM / "bin" / "hipcc"), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] +
+         [str(o) for o in objs] + [f"-L{ROCM / 'lib'}"] + libs + [f"-Wl,-rpath,{ROCM / 'lib'}"])
     os.replace(tmp, out)
     return out
 
@@ -115,12 +126,17 @@ def link_plain(objs: list[Path], out: Path, libs: list[str]) -> Path:
 def build(force: bool = False, jobs: int = 8, sanitize: str | None = None, verbose: bool = True) -> dict:
     hdr = _hdr_mtime()
     BUILD.mkdir(parents=True, exist_ok=True)
-    srcs = CORE_CC + CORE_HIP
+    srcs = CORE_CC + SENTINEL_HIP + KERNELS_HIP
     extra = [s for s in ROCPROF_CC + TRACER_CC if (CSRC / s).exists()]
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         futs = {s: ex.submit(compile_one, s, hdr, force, sanitize) for s in srcs + extra}
         objs = {s: f.result() for s, f in futs.items()}
-    outputs = {"module": str(link_module([objs[s] for s in srcs], sanitize))}
+    outputs = {
+        "module": str(link_core([objs[s] for s in CORE_CC], sanitize)),
+        "sentinel": str(link_hip([objs[s] for s in SENTINEL_HIP], PKG / "libgpuexp_hip.so",
+                                 ["-lamdhip64", "-lhsa-runtime64"])),
+        "kernels": str(link_hip([objs[s] for s in KERNELS_HIP], _ext("_gpuexp_kernels"), ["-lamdhip64"])),
+    }
     if (CSRC / ROCPROF_CC[0]).exists():
         outputs["rocprof_plugin"] = str(link_plain([objs[ROCPROF_CC[0]]], PKG / "_gpuexp_rocprof.so",
                                                    ["-lrocprofiler-sdk", "-lpthread"]))

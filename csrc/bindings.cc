@@ -16,7 +16,6 @@
 namespace py = pybind11;
 using namespace gpuexp;
 
-void register_kernels(py::module_& m);  // kernels_bindings.cc (HIP workload kernels)
 
 namespace {
 
@@ -408,5 +407,5 @@ PYBIND11_MODULE(_gpuexp, m) {
         e.mock()->set_fault(dev, fault);
       });
 
-  register_kernels(m);
+  m.def("default_rocprof_plugin", &default_rocprof_plugin);
 }

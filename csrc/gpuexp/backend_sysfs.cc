@@ -33,7 +33,7 @@ bool CachedFile::open(const std::string& path) {
 
 long CachedFile::read(char* buf, size_t cap) {
   if (fd_ < 0) return -1;
-  return pread_all(fd_, buf, cap);
+  return pread_once(fd_, buf, cap);
 }
 
 bool CachedFile::read_u64(uint64_t* v) {

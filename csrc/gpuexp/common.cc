@@ -84,6 +84,14 @@ long pread_all(int fd, char* buf, size_t cap) {
   return long(got);
 }
 
+long pread_once(int fd, char* buf, size_t cap) {
+  for (;;) {
+    ssize_t n = ::pread(fd, buf, cap, 0);
+    if (n < 0 && errno == EINTR) continue;
+    return long(n);
+  }
+}
+
 std::string trim(const std::string& s) {
   size_t b = 0, e = s.size();
   while (b < e && (s[b] == ' ' || s[b] == '\n' || s[b] == '\t' || s[b] == '\r')) ++b;

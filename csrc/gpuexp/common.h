@@ -49,6 +49,10 @@ bool read_small_file(const std::string& path, std::string* out, size_t max_bytes
 bool read_u64_file(const std::string& path, uint64_t* v);
 // pread() an already-open fd from offset 0.  Returns bytes read or -1.
 long pread_all(int fd, char* buf, size_t cap);
+// ONE pread() at offset 0.  For sysfs attributes: the kernel renders the whole value
+// (<= PAGE_SIZE) per read, and a second read at EOF renders it AGAIN — for gpu_metrics
+// that is a second SMU table transfer (measured: 410 us/GPU/tick with two reads).
+long pread_once(int fd, char* buf, size_t cap);
 bool parse_u64(const char* s, size_t n, uint64_t* v);
 std::string trim(const std::string& s);
 std::vector<std::string> list_dir(const std::string& path);

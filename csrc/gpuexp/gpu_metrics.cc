@@ -75,7 +75,7 @@ bool GpuMetricsReader::open(const std::string& path, std::string* err) {
     *err = "open " + path + " failed";
     return false;
   }
-  long n = pread_all(fd_, reinterpret_cast<char*>(buf_), sizeof(buf_));
+  long n = pread_once(fd_, reinterpret_cast<char*>(buf_), sizeof(buf_));
   if (n < long(sizeof(GpuMetricsHeader))) {
     *err = "short gpu_metrics read";
     ::close(fd_);
@@ -99,7 +99,7 @@ bool GpuMetricsReader::read(DeviceSample* out) {
     out->error = "gpu_metrics not open";
     return false;
   }
-  long n = pread_all(fd_, reinterpret_cast<char*>(buf_), sizeof(buf_));
+  long n = pread_once(fd_, reinterpret_cast<char*>(buf_), sizeof(buf_));
   if (n <= 0) {
     out->error = "gpu_metrics read failed";
     return false;

@@ -191,7 +191,37 @@ class ShmRcclSource : public RcclSource {
   std::unordered_map<std::string, Mapping> maps_;
 };
 
+// Directory of the core module itself (the HIP/rocprof plugins are installed beside it).
+std::string self_dir() {
+  Dl_info info{};
+  if (::dladdr(reinterpret_cast<void*>(&self_dir), &info) && info.dli_fname) {
+    std::string p(info.dli_fname);
+    size_t s = p.rfind('/');
+    return s == std::string::npos ? std::string(".") : p.substr(0, s);
+  }
+  return ".";
+}
+
 }  // namespace
+
+std::unique_ptr<SentinelSource> make_hip_sentinel(int ring_slots, int spin_iters) {
+  // RTLD_GLOBAL is not needed: the plugin only exports its factory.  If the process has
+  // already loaded a HIP runtime (e.g. torch's bundled one, same SONAME), the plugin's
+  // DT_NEEDED libamdhip64.so.7 binds to it instead of loading a second copy.
+  std::string path = self_dir() + "/libgpuexp_hip.so";
+  void* h = ::dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    const char* e = ::dlerror();
+    GPUEXP_LOG(LogLevel::kWarn, "sentinel", std::string("dlopen ") + path + ": " + (e ? e : "?"));
+    return nullptr;
+  }
+  using factory_t = SentinelSource* (*)(int, int);
+  auto f = reinterpret_cast<factory_t>(::dlsym(h, "gpuexp_make_hip_sentinel"));
+  if (!f) return nullptr;
+  return std::unique_ptr<SentinelSource>(f(ring_slots, spin_iters));
+}
+
+std::string default_rocprof_plugin() { return self_dir() + "/_gpuexp_rocprof.so"; }
 
 std::unique_ptr<CounterSource> make_rocprof_counters(const std::string& plugin_path) {
   return std::make_unique<PluginCounters>(plugin_path);

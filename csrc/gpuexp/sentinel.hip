@@ -267,8 +267,13 @@ class HipSentinel : public SentinelSource {
 
 }  // namespace
 
-std::unique_ptr<SentinelSource> make_hip_sentinel(int ring_slots, int spin_iters) {
-  return std::make_unique<HipSentinel>(ring_slots, spin_iters);
-}
-
 }  // namespace gpuexp
+
+// Factory exported from libgpuexp_hip.so.  The telemetry core dlopen()s this library
+// only when the sentinel is enabled, so the core itself never links a HIP runtime: a
+// process that also imports torch (which bundles its own libamdhip64.so.7) must end up
+// with ONE HIP runtime, not two (measured: two copies -> hipMalloc OOM + exit hang).
+extern "C" __attribute__((visibility("default"))) gpuexp::SentinelSource* gpuexp_make_hip_sentinel(int ring_slots,
+                                                                                                   int spin_iters) {
+  return new gpuexp::HipSentinel(ring_slots, spin_iters);
+}

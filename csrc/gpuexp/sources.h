@@ -22,8 +22,10 @@ class SentinelSource {
   virtual void stop() = 0;
   virtual std::string status() const = 0;
 };
-// Implemented in sentinel.hip (1 wave, lowest-priority stream, pinned host ring).
+// Implemented in sentinel.hip (1 wave, lowest-priority stream, pinned host ring), built
+// as libgpuexp_hip.so and dlopen()ed from beside the core module; nullptr if unavailable.
 std::unique_ptr<SentinelSource> make_hip_sentinel(int ring_slots, int spin_iters);
+std::string default_rocprof_plugin();
 
 class CounterSource {
  public:

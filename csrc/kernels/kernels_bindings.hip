@@ -23,7 +23,10 @@ void check(hipError_t e, const char* what) {
 
 }  // namespace
 
-void register_kernels(py::module_& m) {
+// Separate module from the telemetry core: it links a HIP runtime, so it is imported
+// only AFTER torch (when torch is used) to bind to torch's runtime — see ops/gemm.py.
+PYBIND11_MODULE(_gpuexp_kernels, m) {
+  m.doc() = "HIP/CDNA4 workload kernels (bf16 MFMA GEMM) for synthetic GPU pods";
   m.def("hip_device_count", []() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;

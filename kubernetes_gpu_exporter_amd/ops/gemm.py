@@ -1,0 +1,52 @@
+"""bf16 MFMA GEMM (hand-written HIP for gfx950, csrc/kernels/gemm_bf16.hip) — the
+synthetic "HIP-GEMM pod" workload of BASELINE configs 3-5.
+
+`_gpuexp_kernels` links a HIP runtime.  torch ROCm wheels bundle their own
+libamdhip64.so.7 (same SONAME as /opt/rocm's), so when torch is installed it is imported
+FIRST: the kernels module's DT_NEEDED then binds to torch's already-loaded runtime
+instead of loading a second one into the process.
+"""
+from __future__ import annotations
+
+import importlib
+
+_mod = None
+
+
+def kernels():
+    global _mod
+    if _mod is None:
+        try:
+            import torch  # noqa: F401  (load torch's HIP runtime first)
+        except ImportError:
+            pass
+        _mod = importlib.import_module("kubernetes_gpu_exporter_amd._gpuexp_kernels")
+    return _mod
+
+
+def gemm_bf16(a, b, out=None, stream=None):
+    """out[M,N] = a[M,K] @ b[N,K]^T for contiguous bf16 torch tensors on one GPU.
+    Shapes must satisfy M%128 == N%128 == K%64 == 0 (checked by the native op)."""
+    import torch
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
+        raise TypeError("gemm_bf16 expects bf16 tensors")
+    if a.dim() != 2 or b.dim() != 2 or a.shape[1] != b.shape[1]:
+        raise ValueError(f"shape mismatch {tuple(a.shape)} x {tuple(b.shape)}^T")
+    if not (a.is_contiguous() and b.is_contiguous()):
+        raise ValueError("operands must be contiguous (row-major, K innermost)")
+    if a.device != b.device or a.device.type != "cuda":
+        raise ValueError("operands must be on the same GPU")
+    M, K = a.shape
+    N = b.shape[0]
+    if out is None:
+        out = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
+    elif out.shape != (M, N) or out.dtype != torch.bfloat16 or not out.is_contiguous():
+        raise ValueError("bad output tensor")
+    s = stream if stream is not None else torch.cuda.current_stream(a.device).cuda_stream
+    kernels().gemm_bf16(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, s)
+    return out
+
+
+def gemm_burn(device: int = 0, size: int = 8192, seconds: float = 1.0, iters_per_sync: int = 4) -> dict:
+    """Torch-free GPU load: keeps `device` busy with size^3 GEMMs for `seconds`."""
+    return kernels().gemm_burn(device, size, size, size, seconds, iters_per_sync)

@@ -9,6 +9,12 @@ if ROOT not in sys.path:
 
 
 def pytest_configure(config):
+    # torch bundles its own libamdhip64.so.7; load it before any of our HIP plugins so the
+    # process ends up with one HIP runtime (see csrc/gpuexp/sentinel.hip factory comment).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run on the GPU box)")
     config.addinivalue_line("markers", "slow: takes more than a few seconds")
 

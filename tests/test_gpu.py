@@ -8,6 +8,7 @@ import time
 
 import pytest
 
+from kubernetes_gpu_exporter_amd.ops.gemm import kernels
 from kubernetes_gpu_exporter_amd.utils import promtext
 
 pytestmark = pytest.mark.gpu
@@ -98,7 +99,7 @@ def test_gemm_bf16_numerics(native, on_gpu, M, N, K):
     a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
     b = torch.randn(N, K, device="cuda").to(torch.bfloat16)
     c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    native.gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, torch.cuda.current_stream().cuda_stream)
+    kernels().gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     ref = a.float() @ b.float().T  # fp32 reference of the same op
     err = (c.float() - ref).abs()
@@ -114,18 +115,18 @@ def test_gemm_identity_asymmetric(native, on_gpu):
     a = torch.eye(M, K, device="cuda", dtype=torch.bfloat16)
     b = (torch.arange(N * K, device="cuda", dtype=torch.float32).reshape(N, K) % 97).to(torch.bfloat16)
     c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    native.gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, 0)
+    kernels().gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, 0)
     torch.cuda.synchronize()
     assert torch.equal(c, b.T.contiguous())
 
 
 def test_gemm_rejects_bad_shapes(native):
     with pytest.raises(ValueError):
-        native.gemm_bf16(1, 1, 1, 100, 128, 64, 0)
+        kernels().gemm_bf16(1, 1, 1, 100, 128, 64, 0)
 
 
 def test_gemm_burn_throughput(native):
-    r = native.gemm_burn(0, 4096, 4096, 4096, 1.0, 8)
+    r = kernels().gemm_burn(0, 4096, 4096, 4096, 1.0, 8)
     print("gemm 4096^3 bf16:", r)
     assert r["tflops"] > 100  # sanity: MFMA path, not a scalar fallback
 
@@ -135,8 +136,8 @@ def test_process_discovery_under_workload(native):
     gfx activity rises while it runs."""
     child = subprocess.Popen([sys.executable, "-c",
                               "import sys; sys.path.insert(0, %r);"
-                              "from kubernetes_gpu_exporter_amd._native import load;"
-                              "print(load().gemm_burn(0, 8192, 8192, 8192, 6.0, 4), flush=True)" % ROOT],
+                              "from kubernetes_gpu_exporter_amd.ops.gemm import gemm_burn;"
+                              "print(gemm_burn(0, 8192, 6.0, 4), flush=True)" % ROOT],
                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     e = amdsmi_engine(native)
     try:
