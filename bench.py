@@ -189,6 +189,11 @@ def main() -> int:
 
     # --- pod map: every rank's PID -> fake pod bench/gemm-pod-<rank> ---
     pid = os.getpid()
+    if use_gpu:
+        # KFD names processes by HOST pid; inside a PID namespace (no hostPID) find ours by
+        # a VRAM fingerprint so the exporter can attribute this rank to its fake pod.
+        from kubernetes_gpu_exporter_amd.utils.kfdself import find_own_kfd_pid
+        pid = find_own_kfd_pid(local_rank, salt=rank) or pid
     if dist is not None:
         pids = [None] * world
         dist.all_gather_object(pids, pid)

@@ -15,4 +15,11 @@ def main(argv=None) -> int:
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    rc = main()
+    # The engine is fully stopped (sampler joined, HTTP closed, sentinel drained, amdsmi
+    # shut down).  Skip interpreter/static teardown: HIP and amdsmi runtime destructors
+    # can block process exit, and a DaemonSet pod must terminate within its grace period.
+    sys.stdout.flush()
+    sys.stderr.flush()
+    import os
+    os._exit(rc)

@@ -11,8 +11,13 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     # torch bundles its own libamdhip64.so.7; load it before any of our HIP plugins so the
     # process ends up with one HIP runtime (see csrc/gpuexp/sentinel.hip factory comment).
+    # Also initialise that runtime first when a GPU is present: measured on the box, HIP
+    # initialised by our sentinel before torch (with amdsmi in the same process) makes
+    # the interpreter hang at exit; torch-first is clean (tools/probe_order.sh, D vs E).
     try:
-        import torch  # noqa: F401
+        import torch
+        if torch.cuda.is_available():
+            torch.zeros(1, device="cuda")
     except ImportError:
         pass
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run on the GPU box)")
