@@ -139,7 +139,7 @@ def build(force: bool = False, jobs: int = 8, sanitize: str | None = None, verbo
     }
     if (CSRC / ROCPROF_CC[0]).exists():
         outputs["rocprof_plugin"] = str(link_plain([objs[ROCPROF_CC[0]]], PKG / "_gpuexp_rocprof.so",
-                                                   ["-lrocprofiler-sdk", "-lpthread"]))
+                                                   ["-lrocprofiler-sdk", "-lhsa-runtime64", "-lpthread"]))
     if (CSRC / TRACER_CC[0]).exists():
         outputs["rccl_tracer"] = str(link_plain([objs[TRACER_CC[0]]], PKG / "libgpuexp_rccl_tracer.so",
                                                 ["-lrocprofiler-sdk", "-lpthread"]))

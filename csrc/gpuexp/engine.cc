@@ -185,19 +185,8 @@ bool Engine::start(std::string* err) {
   kfd_ = std::make_unique<KfdProcReader>(cfg_.host_root, cfg_.exclude_self ? self_pid_ : -1, cfg_.kfd_cu_occupancy);
   resolver_ = std::make_unique<PidResolver>(cfg_.host_root);
 
-  if (cfg_.enable_sentinel && cfg_.backend != "mock") {
-    sentinel_ = make_hip_sentinel(cfg_.sentinel_ring, cfg_.sentinel_spin);
-    std::string e;
-    if (!sentinel_ || !sentinel_->start(devices_, &e)) {
-      sentinel_status_ = "unavailable: " + e;
-      GPUEXP_LOG(LogLevel::kWarn, "sentinel", sentinel_status_);
-      sentinel_.reset();
-    } else {
-      sentinel_status_ = sentinel_->status();
-    }
-  } else if (cfg_.enable_sentinel) {
-    sentinel_status_ = "mock";
-  }
+  // Counters first: the rocprofiler tool must register before the HSA runtime loads,
+  // which the sentinel's first HIP call does.
   if (cfg_.enable_counters && cfg_.backend != "mock") {
     counters_ = make_rocprof_counters(cfg_.counters_plugin);
     std::string e;
@@ -210,6 +199,19 @@ bool Engine::start(std::string* err) {
     }
   } else if (cfg_.enable_counters) {
     counters_status_ = "mock";
+  }
+  if (cfg_.enable_sentinel && cfg_.backend != "mock") {
+    sentinel_ = make_hip_sentinel(cfg_.sentinel_ring, cfg_.sentinel_spin);
+    std::string e = "libgpuexp_hip.so not loadable";
+    if (!sentinel_ || !sentinel_->start(devices_, &e)) {
+      sentinel_status_ = "unavailable: " + e;
+      GPUEXP_LOG(LogLevel::kWarn, "sentinel", sentinel_status_);
+      sentinel_.reset();
+    } else {
+      sentinel_status_ = sentinel_->status();
+    }
+  } else if (cfg_.enable_sentinel) {
+    sentinel_status_ = "mock";
   }
   if (cfg_.enable_rccl) rccl_ = make_rccl_source(cfg_.rccl_dir);
 

@@ -1,0 +1,278 @@
+// rocprofiler-sdk device-counting plugin (_gpuexp_rocprof.so), dlopen()ed by the core.
+//
+// BASELINE config 4 asks for MFMA / LDS counters per GPU at 10 Hz.  Shaders cannot read
+// SQ/TCC performance counters (SURVEY.md §7.4 risk 2), so they come from the
+// rocprofiler-sdk agent ("device") counting service: one context per GPU, one counter
+// config that fits a single pass within the gfx950 per-block slot limits
+// (MI355X_MICROARCH.md "rocprofv3 PMC slots": SQ 8, TCC 4, GRBM 2):
+//   SQ   SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT
+//   GRBM GRBM_GUI_ACTIVE GRBM_COUNT
+//   TCC  TCC_BUBBLE TCC_EA0_RDREQ TCC_EA0_WRREQ TCC_EA0_WRREQ_64B
+// Derived per tick from deltas (formulas of counter_defs.yaml for gfx950: MfmaUtil,
+// FETCH_SIZE, WRITE_SIZE, LDS util / bank-conflict ratio).  Counter values read by
+// rocprofiler_sample_device_counting_service accumulate from context start; the plugin
+// keeps the previous reading and treats a decrease as a restart.
+//
+// The tool registers with rocprofiler_force_configure() — it must run before the HSA
+// runtime loads in this process, so the engine starts counters before the HIP sentinel.
+// Any failure (non-root, PMCs owned by another profiler) leaves the engine without
+// counter series; the other sources are unaffected.
+#include <hsa/hsa.h>
+#include <rocprofiler-sdk/registration.h>
+#include <rocprofiler-sdk/rocprofiler.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace {
+
+enum Ctr {
+  kMfma = 0,
+  kSqBusy,
+  kWaves,
+  kLdsActive,
+  kLdsConflict,
+  kGuiActive,
+  kGrbmCount,
+  kTccBubble,
+  kRdReq,
+  kWrReq,
+  kWrReq64,
+  kNumCtr
+};
+const char* kNames[kNumCtr] = {"SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAVES",
+                               "SQ_LDS_IDX_ACTIVE",        "SQ_LDS_BANK_CONFLICT", "GRBM_GUI_ACTIVE",
+                               "GRBM_COUNT",               "TCC_BUBBLE",      "TCC_EA0_RDREQ",
+                               "TCC_EA0_WRREQ",            "TCC_EA0_WRREQ_64B"};
+// GRBM counters are per-XCC copies of one clock: reduce with max; everything else sums.
+bool use_max(int c) { return c == kGuiActive || c == kGrbmCount; }
+
+struct Agent {
+  rocprofiler_agent_id_t id{};
+  int dev = -1;
+  uint32_t simd = 0, cu = 0;
+  rocprofiler_context_id_t ctx{};
+  rocprofiler_counter_config_id_t cfg{};
+  bool have_cfg = false;
+  bool started = false;
+  std::map<uint64_t, int> counter_slot;  // counter id handle -> Ctr
+  std::vector<rocprofiler_counter_record_t> recs;
+  double prev[kNumCtr] = {};
+  bool have_prev = false;
+  std::chrono::steady_clock::time_point prev_t;
+};
+
+std::mutex g_mu;
+std::vector<std::string> g_want_bdfs;
+std::vector<Agent> g_agents;
+std::string g_status = "not initialised";
+std::string g_err;
+bool g_configured = false;
+rocprofiler_client_finalize_t g_fini = nullptr;
+rocprofiler_client_id_t* g_client = nullptr;
+
+std::string lower(std::string s) {
+  for (auto& c : s) c = char(::tolower(c));
+  return s;
+}
+
+void set_profile_cb(rocprofiler_context_id_t ctx, rocprofiler_agent_id_t, rocprofiler_device_counting_agent_cb_t set_config,
+                    void* user) {
+  auto* a = static_cast<Agent*>(user);
+  if (a && a->have_cfg) set_config(ctx, a->cfg);
+}
+
+int tool_init(rocprofiler_client_finalize_t fini, void*) {
+  g_fini = fini;
+  std::vector<rocprofiler_agent_v0_t> agents;
+  auto cb = [](rocprofiler_agent_version_t ver, const void** arr, size_t n, void* ud) -> rocprofiler_status_t {
+    if (ver != ROCPROFILER_AGENT_INFO_VERSION_0) return ROCPROFILER_STATUS_ERROR;
+    auto* v = static_cast<std::vector<rocprofiler_agent_v0_t>*>(ud);
+    for (size_t i = 0; i < n; ++i) {
+      const auto* a = static_cast<const rocprofiler_agent_v0_t*>(arr[i]);
+      if (a->type == ROCPROFILER_AGENT_TYPE_GPU) v->push_back(*a);
+    }
+    return ROCPROFILER_STATUS_SUCCESS;
+  };
+  if (rocprofiler_query_available_agents(ROCPROFILER_AGENT_INFO_VERSION_0, cb, sizeof(rocprofiler_agent_t),
+                                         &agents) != ROCPROFILER_STATUS_SUCCESS) {
+    g_err = "rocprofiler_query_available_agents failed";
+    return -1;
+  }
+  g_agents.resize(g_want_bdfs.size());
+  int matched = 0;
+  for (const auto& a : agents) {
+    char bdf[32];
+    std::snprintf(bdf, sizeof(bdf), "%04x:%02x:%02x.%x", a.domain, (a.location_id >> 8) & 0xFF,
+                  (a.location_id >> 3) & 0x1F, a.location_id & 0x7);
+    for (size_t d = 0; d < g_want_bdfs.size(); ++d) {
+      if (lower(g_want_bdfs[d]) != bdf) continue;
+      Agent& ag = g_agents[d];
+      ag.id = a.id;
+      ag.dev = int(d);
+      ag.simd = a.simd_count;
+      ag.cu = a.cu_count ? a.cu_count : (a.simd_per_cu ? a.simd_count / a.simd_per_cu : 0);
+      if (rocprofiler_create_context(&ag.ctx) != ROCPROFILER_STATUS_SUCCESS) continue;
+      rocprofiler_buffer_id_t nobuf{};  // values come back in the sample call itself
+      if (rocprofiler_configure_device_counting_service(ag.ctx, nobuf, a.id, set_profile_cb, &ag) !=
+          ROCPROFILER_STATUS_SUCCESS) {
+        g_err = "configure_device_counting_service failed for " + std::string(bdf);
+        continue;
+      }
+      ++matched;
+    }
+  }
+  g_configured = matched > 0;
+  if (!matched && g_err.empty()) g_err = "no rocprofiler GPU agent matched the exporter's GPUs";
+  return 0;
+}
+
+void tool_fini(void*) { g_configured = false; }
+
+rocprofiler_tool_configure_result_t* configure(uint32_t, const char*, uint32_t, rocprofiler_client_id_t* id) {
+  id->name = "gpuexp-device-counters";
+  g_client = id;
+  static rocprofiler_tool_configure_result_t cfg{sizeof(rocprofiler_tool_configure_result_t), &tool_init,
+                                                 &tool_fini, nullptr};
+  return &cfg;
+}
+
+// Builds the counter config for an agent, dropping counters the agent lacks.
+bool build_config(Agent& a, std::string* why) {
+  std::vector<rocprofiler_counter_id_t> all;
+  rocprofiler_iterate_agent_supported_counters(
+      a.id,
+      [](rocprofiler_agent_id_t, rocprofiler_counter_id_t* c, size_t n, void* ud) -> rocprofiler_status_t {
+        auto* v = static_cast<std::vector<rocprofiler_counter_id_t>*>(ud);
+        v->insert(v->end(), c, c + n);
+        return ROCPROFILER_STATUS_SUCCESS;
+      },
+      &all);
+  std::vector<rocprofiler_counter_id_t> use;
+  for (auto& c : all) {
+    rocprofiler_counter_info_v0_t info{};
+    if (rocprofiler_query_counter_info(c, ROCPROFILER_COUNTER_INFO_VERSION_0, &info) != ROCPROFILER_STATUS_SUCCESS)
+      continue;
+    for (int k = 0; k < kNumCtr; ++k)
+      if (info.name && std::strcmp(info.name, kNames[k]) == 0) {
+        use.push_back(c);
+        a.counter_slot[c.handle] = k;
+      }
+  }
+  if (use.empty()) {
+    *why = "agent supports none of the requested counters";
+    return false;
+  }
+  size_t nrec = 0;
+  for (auto& c : use) {
+    rocprofiler_counter_info_v1_t info{};
+    if (rocprofiler_query_counter_info(c, ROCPROFILER_COUNTER_INFO_VERSION_1, &info) == ROCPROFILER_STATUS_SUCCESS)
+      nrec += info.dimensions_instances_count;
+  }
+  if (rocprofiler_create_counter_config(a.id, use.data(), use.size(), &a.cfg) != ROCPROFILER_STATUS_SUCCESS) {
+    *why = "create_counter_config failed (slot limits?)";
+    return false;
+  }
+  a.have_cfg = true;
+  a.recs.resize(nrec + 64);
+  return true;
+}
+
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) int gpuexp_rp_init(int ndev, const char* const* bdfs, char* err,
+                                                                     int errlen) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto fail = [&](const std::string& m) {
+    std::snprintf(err, size_t(errlen), "%s", m.c_str());
+    g_status = "unavailable: " + m;
+    return 0;
+  };
+  g_want_bdfs.assign(bdfs, bdfs + ndev);
+  int inited = 0;
+  rocprofiler_is_initialized(&inited);
+  if (inited) return fail("rocprofiler already initialised in this process (HSA loaded before the plugin)");
+  if (rocprofiler_force_configure(&configure) != ROCPROFILER_STATUS_SUCCESS)
+    return fail("rocprofiler_force_configure failed");
+  // Device counting needs the HSA runtime loaded; loading it now triggers tool_init.
+  if (hsa_init() != HSA_STATUS_SUCCESS) return fail("hsa_init failed");
+  if (!g_configured) return fail(g_err.empty() ? "tool_init did not configure any agent" : g_err);
+  int ok = 0;
+  std::string why;
+  for (auto& a : g_agents) {
+    if (a.dev < 0) continue;
+    if (!build_config(a, &why)) continue;
+    if (rocprofiler_start_context(a.ctx) != ROCPROFILER_STATUS_SUCCESS) {
+      why = "start_context failed (PMCs busy or insufficient permission?)";
+      continue;
+    }
+    a.started = true;
+    ++ok;
+  }
+  if (!ok) return fail(why.empty() ? "no agent started" : why);
+  g_status = "rocprofiler-sdk device counting on " + std::to_string(ok) + " GPU(s)";
+  return ok;
+}
+
+extern "C" __attribute__((visibility("default"))) int gpuexp_rp_sample(int dev, double dt_s, double* out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (dev < 0 || size_t(dev) >= g_agents.size()) return -1;
+  Agent& a = g_agents[size_t(dev)];
+  if (!a.started) return -1;
+  size_t n = a.recs.size();
+  if (rocprofiler_sample_device_counting_service(a.ctx, {}, ROCPROFILER_COUNTER_FLAG_NONE, a.recs.data(), &n) !=
+      ROCPROFILER_STATUS_SUCCESS)
+    return -1;
+  double v[kNumCtr] = {};
+  for (size_t i = 0; i < n; ++i) {
+    rocprofiler_counter_id_t cid{};
+    if (rocprofiler_query_record_counter_id(a.recs[i].id, &cid) != ROCPROFILER_STATUS_SUCCESS) continue;
+    auto it = a.counter_slot.find(cid.handle);
+    if (it == a.counter_slot.end()) continue;
+    int k = it->second;
+    double x = a.recs[i].counter_value;
+    v[k] = use_max(k) ? std::max(v[k], x) : v[k] + x;
+  }
+  auto now = std::chrono::steady_clock::now();
+  double d[kNumCtr];
+  bool restarted = false;
+  for (int k = 0; k < kNumCtr; ++k) {
+    d[k] = a.have_prev ? v[k] - a.prev[k] : v[k];
+    if (d[k] < 0) restarted = true;
+  }
+  double wall = a.have_prev ? std::chrono::duration<double>(now - a.prev_t).count() : dt_s;
+  std::memcpy(a.prev, v, sizeof(v));
+  a.prev_t = now;
+  bool first = !a.have_prev;
+  a.have_prev = true;
+  if (first || restarted || wall <= 0) return -1;  // need one interval of deltas
+  const double nan = std::nan("");
+  double gui = d[kGuiActive];
+  out[0] = gui > 0 && a.simd ? 100.0 * d[kMfma] / (gui * a.simd) : nan;              // MfmaUtil
+  out[1] = gui > 0 && a.cu ? 100.0 * d[kSqBusy] / (gui * a.cu) : nan;                // SQ busy per CU
+  out[2] = d[kGrbmCount] > 0 ? 100.0 * gui / d[kGrbmCount] : nan;                     // GPU busy
+  out[3] = d[kWaves] / wall;                                                          // waves/s
+  out[4] = gui > 0 && a.cu ? 100.0 * d[kLdsActive] / (gui * a.cu) : nan;             // LDS util
+  out[5] = d[kLdsActive] > 0 ? 100.0 * d[kLdsConflict] / d[kLdsActive] : 0.0;        // bank conflicts
+  out[6] = (d[kTccBubble] * 128.0 + (d[kRdReq] - d[kTccBubble]) * 64.0) / wall;     // FETCH_SIZE bytes/s
+  out[7] = ((d[kWrReq] - d[kWrReq64]) * 32.0 + d[kWrReq64] * 64.0) / wall;          // WRITE_SIZE bytes/s
+  return 0;
+}
+
+extern "C" __attribute__((visibility("default"))) void gpuexp_rp_shutdown() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (auto& a : g_agents)
+    if (a.started) {
+      rocprofiler_stop_context(a.ctx);
+      a.started = false;
+    }
+}
+
+extern "C" __attribute__((visibility("default"))) const char* gpuexp_rp_status() { return g_status.c_str(); }

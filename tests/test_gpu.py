@@ -131,6 +131,39 @@ def test_gemm_burn_throughput(native):
     assert r["tflops"] > 100  # sanity: MFMA path, not a scalar fallback
 
 
+def _feature_check(*args, timeout=300):
+    import json
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gpu_features_check.py"), *args],
+                       capture_output=True, text=True, timeout=timeout)
+    print(r.stdout[-3000:], r.stderr[-3000:])
+    line = [l for l in r.stdout.splitlines() if l.startswith("RESULT ")]
+    assert line, "feature check produced no result"
+    return json.loads(line[-1][7:])
+
+
+def test_rocprofiler_device_counters_under_gemm():
+    """MFMA/LDS/HBM counters from the rocprofiler-sdk plugin while a GEMM pod runs
+    (BASELINE config 4).  Skips — loudly — when the box denies PMC access."""
+    res = _feature_check("counters", "3")
+    if "unavailable" in res["status"] and "counters=rocprofiler" not in res["status"]:
+        pytest.skip("device counting unavailable on this box: " + res["status"])
+    assert res["amd_gpu_mfma_busy_percent"] is not None, res
+    assert res["amd_gpu_mfma_busy_percent"] > 10, res   # an MFMA GEMM is running
+    assert res["amd_gpu_gui_active_percent"] > 50, res
+    assert res["amd_gpu_hbm_read_bytes_per_second"] > 1e9, res
+    assert res["series_gpu0"] == 64, res
+
+
+def test_rccl_tracer_counts_collectives():
+    res = _feature_check("rccl")
+    assert res["rc"] == 0, res
+    assert res["files"], res
+    ops = res["ops"]
+    assert ops["allreduce"]["calls"] >= 20
+    assert ops["allreduce"]["bytes"] >= 20 * (2 << 20)
+    assert ops["allgather"]["calls"] >= 5
+
+
 def test_process_discovery_under_workload(native):
     """A child GEMM process appears in the KFD process list with its VRAM and the GPU's
     gfx activity rises while it runs."""
