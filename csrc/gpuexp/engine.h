@@ -43,7 +43,7 @@ struct EngineConfig {
   bool exclude_self = true;
   bool enable_sentinel = false;
   int sentinel_ring = 64;
-  int sentinel_spin = 2000;
+  int sentinel_spin = 500;  // ~15 us window (rocprofv3: spin 2000 ran 61 us/launch)
   bool enable_counters = false;
   std::string counters_plugin;         // path to _gpuexp_rocprof.so
   bool enable_rccl = false;

@@ -80,8 +80,32 @@ void account(int op, uint64_t bytes) {
   g_shm->ops[op].bytes.fetch_add(bytes, std::memory_order_relaxed);
 }
 
+// RCCL implements some collectives with its own public API (all-to-all = a group of
+// ncclSend/ncclRecv): only the outermost data-moving call on a thread is accounted.
+thread_local int t_depth = 0;
+
+bool moves_data(int op) {
+  switch (op) {
+    case ROCPROFILER_RCCL_API_ID_ncclAllReduce: case ROCPROFILER_RCCL_API_ID_ncclAllGather:
+    case ROCPROFILER_RCCL_API_ID_ncclReduceScatter: case ROCPROFILER_RCCL_API_ID_ncclAllToAll:
+    case ROCPROFILER_RCCL_API_ID_ncclAllToAllv: case ROCPROFILER_RCCL_API_ID_ncclBroadcast:
+    case ROCPROFILER_RCCL_API_ID_ncclReduce: case ROCPROFILER_RCCL_API_ID_ncclSend:
+    case ROCPROFILER_RCCL_API_ID_ncclRecv: case ROCPROFILER_RCCL_API_ID_ncclGather:
+    case ROCPROFILER_RCCL_API_ID_ncclScatter:
+      return true;
+    default:
+      return false;
+  }
+}
+
 void on_rccl(rocprofiler_callback_tracing_record_t rec, rocprofiler_user_data_t*, void*) {
-  if (rec.phase != ROCPROFILER_CALLBACK_PHASE_ENTER || t_in_query) return;
+  if (t_in_query || !moves_data(int(rec.operation))) return;
+  if (rec.phase == ROCPROFILER_CALLBACK_PHASE_EXIT) {
+    if (t_depth > 0) --t_depth;
+    return;
+  }
+  if (rec.phase != ROCPROFILER_CALLBACK_PHASE_ENTER) return;
+  if (t_depth++ > 0) return;  // nested inside another collective
   const auto* d = static_cast<const rocprofiler_callback_tracing_rccl_api_data_t*>(rec.payload);
   const auto& a = d->args;
   using namespace gpuexp;

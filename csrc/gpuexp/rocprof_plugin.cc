@@ -65,6 +65,9 @@ struct Agent {
   std::map<uint64_t, int> counter_slot;  // counter id handle -> Ctr
   std::vector<rocprofiler_counter_record_t> recs;
   double prev[kNumCtr] = {};
+  double last_raw[kNumCtr] = {};
+  int last_inst[kNumCtr] = {};
+  size_t last_nrec = 0;
   bool have_prev = false;
   std::chrono::steady_clock::time_point prev_t;
 };
@@ -231,6 +234,7 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_sample(int dev, 
       ROCPROFILER_STATUS_SUCCESS)
     return -1;
   double v[kNumCtr] = {};
+  int inst[kNumCtr] = {};
   for (size_t i = 0; i < n; ++i) {
     rocprofiler_counter_id_t cid{};
     if (rocprofiler_query_record_counter_id(a.recs[i].id, &cid) != ROCPROFILER_STATUS_SUCCESS) continue;
@@ -239,7 +243,11 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_sample(int dev, 
     int k = it->second;
     double x = a.recs[i].counter_value;
     v[k] = use_max(k) ? std::max(v[k], x) : v[k] + x;
+    inst[k] += 1;
   }
+  std::memcpy(a.last_raw, v, sizeof(v));
+  std::memcpy(a.last_inst, inst, sizeof(inst));
+  a.last_nrec = n;
   auto now = std::chrono::steady_clock::now();
   double d[kNumCtr];
   bool restarted = false;
@@ -276,3 +284,20 @@ extern "C" __attribute__((visibility("default"))) void gpuexp_rp_shutdown() {
 }
 
 extern "C" __attribute__((visibility("default"))) const char* gpuexp_rp_status() { return g_status.c_str(); }
+
+// Diagnostics: the raw (cumulative) reduced value and instance count of every counter in
+// the last sample, as "NAME=value/instances;..." (used by tools/gpu_features_check.py).
+extern "C" __attribute__((visibility("default"))) int gpuexp_rp_debug(int dev, char* buf, int len) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (dev < 0 || size_t(dev) >= g_agents.size()) return -1;
+  const Agent& a = g_agents[size_t(dev)];
+  std::string s = "records=" + std::to_string(a.last_nrec) + ";simd=" + std::to_string(a.simd) +
+                  ";cu=" + std::to_string(a.cu) + ";";
+  for (int k = 0; k < kNumCtr; ++k) {
+    char t[128];
+    std::snprintf(t, sizeof(t), "%s=%.0f/%d;", kNames[k], a.last_raw[k], a.last_inst[k]);
+    s += t;
+  }
+  std::snprintf(buf, size_t(len), "%s", s.c_str());
+  return 0;
+}

@@ -36,7 +36,7 @@ class Config:
     gc_after: int = 1
     # optional sources
     enable_sentinel: bool = False
-    sentinel_spin: int = 2000
+    sentinel_spin: int = 500
     enable_counters: bool = False
     counters_plugin: str = ""
     enable_rccl: bool = False

@@ -42,9 +42,15 @@ def counters(seconds: float) -> dict:
     time.sleep(seconds)
     text = e.snapshot_text()
     status = e.source_status()
+    import ctypes
+    dbg = ctypes.create_string_buffer(4096)
+    try:
+        ctypes.CDLL(n.default_rocprof_plugin()).gpuexp_rp_debug(0, dbg, 4096)
+    except OSError:
+        pass
     e.stop()
     fams = promtext.parse(text)
-    out = {"status": status}
+    out = {"status": status, "raw_counters": dbg.value.decode()}
     for name in ("amd_gpu_mfma_busy_percent", "amd_gpu_sq_busy_percent", "amd_gpu_gui_active_percent",
                  "amd_gpu_waves_per_second", "amd_gpu_lds_active_percent", "amd_gpu_lds_bank_conflict_percent",
                  "amd_gpu_hbm_read_bytes_per_second", "amd_gpu_hbm_write_bytes_per_second",
