@@ -154,6 +154,10 @@ void Engine::define_families() {
   f_self_overruns_ = add("gpuexp_tick_overruns_total", "Ticks skipped because a tick ran past its deadline", C, {});
   f_self_cpu_ = add("gpuexp_sampler_cpu_seconds_total", "CPU time used by the sampler thread", C, {});
   f_self_source_up_ = add("gpuexp_source_up", "1 if an optional source is active", G, {"source"});
+  f_self_ctr_scope_ = add("gpuexp_counters_device_scope",
+                          "1 if wave/LDS/HBM PMC counters see every process on the GPU, 0 if they are "
+                          "VMID-filtered to the exporter (not exported then)",
+                          G, {"gpu"});
 }
 
 bool Engine::start(std::string* err) {
@@ -464,14 +468,21 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
   if (counters_) have_ctr = counters_->sample(i, dt_s, &cr) && cr.ok;
   else if (cfg_.enable_counters) have_ctr = backend_->counters(d, dt_s, &cr) && cr.ok;
   if (have_ctr) {
+    // Chip-global counters are always device totals.  Wave/LDS/EA counters are exported
+    // only while they are known to see every process (scope 1, or the mock); scope 0
+    // (VMID-filtered to the exporter) would under-report by orders of magnitude.
+    int scope = counters_ ? counters_->scope(i) : 1;
+    table_.put(f_self_ctr_scope_, {std::to_string(d.index)}, scope < 0 ? kNaN : double(scope), gen);
     dput(st, i, st.ctr[0], f_mfma_, {}, cr.mfma_busy_pct, gen);
-    dput(st, i, st.ctr[1], f_sq_busy_, {}, cr.sq_busy_pct, gen);
     dput(st, i, st.ctr[2], f_gui_, {}, cr.gui_active_pct, gen);
-    dput(st, i, st.ctr[3], f_waves_, {}, cr.waves_per_s, gen);
-    dput(st, i, st.ctr[4], f_lds_, {}, cr.lds_active_pct, gen);
-    dput(st, i, st.ctr[5], f_lds_conf_, {}, cr.lds_bank_conflict_pct, gen);
-    dput(st, i, st.ctr[6], f_hbm_rd_, {}, cr.hbm_read_bps, gen);
-    dput(st, i, st.ctr[7], f_hbm_wr_, {}, cr.hbm_write_bps, gen);
+    if (scope != 0) {
+      dput(st, i, st.ctr[1], f_sq_busy_, {}, cr.sq_busy_pct, gen);
+      dput(st, i, st.ctr[3], f_waves_, {}, cr.waves_per_s, gen);
+      dput(st, i, st.ctr[4], f_lds_, {}, cr.lds_active_pct, gen);
+      dput(st, i, st.ctr[5], f_lds_conf_, {}, cr.lds_bank_conflict_pct, gen);
+      dput(st, i, st.ctr[6], f_hbm_rd_, {}, cr.hbm_read_bps, gen);
+      dput(st, i, st.ctr[7], f_hbm_wr_, {}, cr.hbm_write_bps, gen);
+    }
   }
   SentinelReading sr;
   bool have_sen = false;

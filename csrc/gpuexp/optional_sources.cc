@@ -25,6 +25,7 @@ using rp_init_fn = int (*)(int ndev, const char* const* bdfs, char* err, int err
 using rp_sample_fn = int (*)(int dev, double dt_s, double* out8);
 using rp_shutdown_fn = void (*)();
 using rp_status_fn = const char* (*)();
+using rp_scope_fn = int (*)(int dev);
 
 class PluginCounters : public CounterSource {
  public:
@@ -42,6 +43,7 @@ class PluginCounters : public CounterSource {
     sample_ = reinterpret_cast<rp_sample_fn>(::dlsym(handle_, "gpuexp_rp_sample"));
     shutdown_ = reinterpret_cast<rp_shutdown_fn>(::dlsym(handle_, "gpuexp_rp_shutdown"));
     status_fn_ = reinterpret_cast<rp_status_fn>(::dlsym(handle_, "gpuexp_rp_status"));
+    scope_fn_ = reinterpret_cast<rp_scope_fn>(::dlsym(handle_, "gpuexp_rp_scope"));
     if (!init_ || !sample_ || !shutdown_) {
       *err = "plugin " + path_ + " lacks the gpuexp_rp_* ABI";
       return false;
@@ -74,6 +76,8 @@ class PluginCounters : public CounterSource {
     return true;
   }
 
+  int scope(int dev) override { return started_ && scope_fn_ ? scope_fn_(dev) : -1; }
+
   void stop() override {
     if (started_ && shutdown_) shutdown_();
     started_ = false;
@@ -91,6 +95,7 @@ class PluginCounters : public CounterSource {
   rp_sample_fn sample_ = nullptr;
   rp_shutdown_fn shutdown_ = nullptr;
   rp_status_fn status_fn_ = nullptr;
+  rp_scope_fn scope_fn_ = nullptr;
   bool started_ = false;
 };
 

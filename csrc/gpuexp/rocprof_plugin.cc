@@ -68,6 +68,7 @@ struct Agent {
   double last_raw[kNumCtr] = {};
   int last_inst[kNumCtr] = {};
   size_t last_nrec = 0;
+  int scope = -1;  // -1 unknown, 0 wave/EA counters VMID-filtered to this process, 1 device-wide
   bool have_prev = false;
   std::chrono::steady_clock::time_point prev_t;
 };
@@ -263,8 +264,20 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_sample(int dev, 
   if (first || restarted || wall <= 0) return -1;  // need one interval of deltas
   const double nan = std::nan("");
   double gui = d[kGuiActive];
+  // Scope detection.  As a non-root client (perf_event_paranoid=3 on the test pool) the
+  // wave-level SQ counters and the TCC EA requests are VMID-filtered to THIS process,
+  // while SQ_VALU_MFMA_BUSY_CYCLES and GRBM are chip-global (measured against rocprofv3
+  // dispatch counts: profiles/r01/pmc_gemm_dispatch.txt).  A busy GPU on which the
+  // exporter sees almost no waves means the filtered set must not be exported as device
+  // totals.
+  if (d[kGrbmCount] > 0 && gui / d[kGrbmCount] > 0.5 && d[kMfma] > 0) {
+    double waves_per_s = d[kWaves] / wall;
+    a.scope = waves_per_s < 1000.0 ? 0 : 1;
+  }
   out[0] = gui > 0 && a.simd ? 100.0 * d[kMfma] / (gui * a.simd) : nan;              // MfmaUtil
-  out[1] = gui > 0 && a.cu ? 100.0 * d[kSqBusy] / (gui * a.cu) : nan;                // SQ busy per CU
+  // SQ_BUSY_CYCLES has one instance per shader engine: normalise by the instance count.
+  double se = a.last_inst[kSqBusy] > 0 ? a.last_inst[kSqBusy] : 1;
+  out[1] = gui > 0 ? std::min(100.0, 100.0 * d[kSqBusy] / (gui * se)) : nan;
   out[2] = d[kGrbmCount] > 0 ? 100.0 * gui / d[kGrbmCount] : nan;                     // GPU busy
   out[3] = d[kWaves] / wall;                                                          // waves/s
   out[4] = gui > 0 && a.cu ? 100.0 * d[kLdsActive] / (gui * a.cu) : nan;             // LDS util
@@ -284,6 +297,12 @@ extern "C" __attribute__((visibility("default"))) void gpuexp_rp_shutdown() {
 }
 
 extern "C" __attribute__((visibility("default"))) const char* gpuexp_rp_status() { return g_status.c_str(); }
+
+extern "C" __attribute__((visibility("default"))) int gpuexp_rp_scope(int dev) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (dev < 0 || size_t(dev) >= g_agents.size()) return -1;
+  return g_agents[size_t(dev)].scope;
+}
 
 // Diagnostics: the raw (cumulative) reduced value and instance count of every counter in
 // the last sample, as "NAME=value/instances;..." (used by tools/gpu_features_check.py).

@@ -32,6 +32,11 @@ class CounterSource {
   virtual ~CounterSource() = default;
   virtual bool start(const std::vector<DeviceInfo>& devs, std::string* err) = 0;
   virtual bool sample(int dev, double dt_s, CounterReading* out) = 0;
+  // -1 unknown, 0 = wave/LDS/EA counters only see this process (VMID-filtered), 1 = device-wide.
+  virtual int scope(int dev) {
+    (void)dev;
+    return -1;
+  }
   virtual void stop() = 0;
   virtual std::string status() const = 0;
 };
