@@ -1,0 +1,186 @@
+"""Control plane against fake kubelet (PodResources gRPC) and fake apiserver, plus the
+full exporter on a fake host root: device -> pod via the device plugin, PID -> pod via
+cgroups, pod UID -> namespace/name via a node-scoped pod list."""
+import os
+import time
+
+import pytest
+
+from kubernetes_gpu_exporter_amd.config import make_config
+from kubernetes_gpu_exporter_amd.k8s.controlplane import ControlPlane, Metadata
+from kubernetes_gpu_exporter_amd.k8s.fakes import FakeApiserver, FakeKubelet, FakePod
+from kubernetes_gpu_exporter_amd.k8s.filesource import FileSource, write_pod_map
+from kubernetes_gpu_exporter_amd.k8s.podresources import PodResourcesSource
+from kubernetes_gpu_exporter_amd.k8s.sources import ApiserverSource, LogdirSource, strip_container_id
+from kubernetes_gpu_exporter_amd.utils import promtext
+from kubernetes_gpu_exporter_amd.utils.fakehost import kubepods_cgroup, mi355x_node
+
+UID_A = "aaaaaaaa-0000-4000-8000-000000000001"
+UID_B = "bbbbbbbb-0000-4000-8000-000000000002"
+UID_C = "cccccccc-0000-4000-8000-000000000003"
+CID_A = "a1" * 32
+CID_B = "b2" * 32
+
+
+def pods():
+    return [
+        FakePod(UID_A, "research", "llama-train-0", "node-a", {"trainer": CID_A}, {"trainer": ["0000:72:00.0"]}),
+        FakePod(UID_B, "serving", "vllm-0", "node-a", {"server": CID_B, "sidecar": "c3" * 32},
+                {"server": ["0000:5a:00.0"]}),
+        FakePod(UID_C, "other", "elsewhere", "node-b", {"x": "d4" * 32}, {"x": ["0000:23:00.0"]}),
+    ]
+
+
+def test_strip_container_id():
+    assert strip_container_id("containerd://abc") == "abc"
+    assert strip_container_id("cri-o://abc") == "abc"
+    assert strip_container_id("abc") == "abc"  # reference sliced from offset 2 here (main.go:97)
+    assert strip_container_id("") == ""
+
+
+def test_podresources_roundtrip(tmp_path):
+    sock = str(tmp_path / "kubelet.sock")
+    k = FakeKubelet(sock, pods()).start()
+    try:
+        md = PodResourcesSource(sock).fetch()
+        assert md.owners["0000:72:00.0"] == {"namespace": "research", "pod": "llama-train-0", "container": "trainer"}
+        assert md.owners["0000:5a:00.0"]["container"] == "server"
+        assert len(md.owners) == 3  # the kubelet only reports its own node; the fake reports all
+        k.fail = True
+        with pytest.raises(Exception):
+            PodResourcesSource(sock).fetch()
+    finally:
+        k.stop()
+
+
+def test_podresources_timeout(tmp_path):
+    sock = str(tmp_path / "kubelet.sock")
+    k = FakeKubelet(sock, pods()).start()
+    k.delay = 1.0
+    try:
+        t0 = time.monotonic()
+        with pytest.raises(Exception):
+            PodResourcesSource(sock, timeout=0.2).fetch()
+        assert time.monotonic() - t0 < 0.9
+    finally:
+        k.stop()
+
+
+def test_apiserver_node_scoped(tmp_path):
+    api = FakeApiserver(pods(), token="s3cret").start()
+    tok = tmp_path / "token"
+    tok.write_text("s3cret\n")
+    try:
+        md = ApiserverSource(api.url, "node-a", str(tok)).fetch()
+        assert set(md.pods) == {UID_A, UID_B}  # node-b pod excluded (reference listed ALL pods)
+        assert md.pods[UID_B]["containers"][CID_B] == "server"
+        assert md.pods[UID_A]["namespace"] == "research"
+        assert "fieldSelector=spec.nodeName%3Dnode-a" in api.requests[-1]
+        assert "resourceVersion=0" in api.requests[-1]
+        with pytest.raises(Exception):
+            ApiserverSource(api.url, "node-a", "").fetch()  # no token -> 401
+    finally:
+        api.stop()
+
+
+def test_logdir_source(tmp_path):
+    d = tmp_path / "var/log/pods"
+    (d / f"research_llama-train-0_{UID_A}/trainer").mkdir(parents=True)
+    (d / f"kube-system_my_weird_name_{UID_B}/c").mkdir(parents=True)
+    (d / "garbage").mkdir()
+    md = LogdirSource(str(d)).fetch()
+    assert md.pods[UID_A]["name"] == "llama-train-0"
+    assert md.pods[UID_B]["name"] == "my_weird_name" and md.pods[UID_B]["namespace"] == "kube-system"
+    assert len(md.pods) == 2
+
+
+def test_file_source_reload(tmp_path):
+    p = str(tmp_path / "map.json")
+    write_pod_map(p, [{"uid": UID_A, "namespace": "n", "name": "a", "containers": {}}], {123: "/kubepods/x"})
+    s = FileSource(p)
+    assert s.fetch().pid_cgroups == {123: "/kubepods/x"}
+    time.sleep(0.01)
+    write_pod_map(p, [{"uid": UID_B, "namespace": "n", "name": "b", "containers": {}}])
+    os.utime(p, ns=(time.time_ns() + 10**6, time.time_ns() + 10**6))
+    assert list(s.fetch().pods) == [UID_B]
+
+
+class _Boom:
+    name = "boom"
+
+    def fetch(self):
+        raise RuntimeError("apiserver 503")
+
+
+class _Static:
+    name = "static"
+
+    def __init__(self, md):
+        self.md = md
+
+    def fetch(self):
+        return self.md
+
+
+def test_control_plane_isolates_failures_and_pushes_on_change(mock_engine):
+    e = mock_engine(1, http=False)
+    md = Metadata(pods={UID_A: {"uid": UID_A, "namespace": "ns", "name": "p", "containers": {}}},
+                  pid_cgroups={42: kubepods_cgroup(UID_A, CID_A)})
+    cp = ControlPlane([_Boom(), _Static(md)], interval=0.05)
+    cp.attach(e)
+    cp.refresh_once()
+    assert "boom" in cp.errors
+    e.mock_set_processes(0, [dict(pid=42, vram_bytes=7.0)])
+    e.tick(1_000_000_000)
+    assert 'pod_gpu_memory_usage{pid="42",pod="p"} 7' in e.snapshot_text()
+    # unchanged metadata is not re-pushed
+    fp = cp._last_fp
+    cp.refresh_once()
+    assert cp._last_fp == fp
+
+
+def test_full_exporter_on_fake_node(tmp_path):
+    """sysfs backend + fake kubelet + fake apiserver, through the Exporter/Config path."""
+    import shutil
+    import tempfile
+    from pathlib import Path
+
+    from kubernetes_gpu_exporter_amd.exporter import Exporter
+    root = Path(tempfile.mkdtemp(prefix="h", dir="/tmp"))  # unix socket paths max 107 chars
+    request_cleanup = lambda: shutil.rmtree(root, ignore_errors=True)  # noqa: E731
+    h = mi355x_node(root, 3)  # GPUs at 0a (idx0), 5a (idx1), 72 (idx2)
+    by_bus = {g.location_id >> 8: g for g in h.gpus}
+    h.add_process(1001, kubepods_cgroup(UID_A, CID_A), gpus={by_bus[0x72].gpu_id: (40 << 30, 200)})
+    h.add_process(1002, kubepods_cgroup(UID_B, CID_B, qos="guaranteed"), gpus={by_bus[0x5A].gpu_id: (20 << 30, 100)})
+    sock_rel = "/var/lib/kubelet/pod-resources/kubelet.sock"
+    kub = FakeKubelet(str(root) + sock_rel, pods(), node="node-a").start()
+    api = FakeApiserver(pods(), token="tok").start()
+    (tmp_path / "token").write_text("tok")
+    cfg = make_config({"backend": "sysfs", "host_root": str(root), "interval": 0, "listen": "127.0.0.1:0",
+                       "node_name": "node-a", "apiserver": api.url, "apiserver_token_file": str(tmp_path / "token"),
+                       "kubelet_socket": sock_rel, "control_interval": 0.05})
+    ex = Exporter(cfg)
+    try:
+        ex.start()
+        srcs = {s.name for s in ex._control.sources}
+        assert srcs == {"apiserver", "podresources"}, srcs
+        ex.tick(1_000_000_000)
+        ex.tick(1_100_000_000)
+        fams = promtext.parse(ex.text())
+        assert promtext.value(fams, "pod_gpu_memory_usage", pid=1001, pod="llama-train-0") == 40 << 30
+        assert promtext.value(fams, "pod_gpu_memory_usage", pid=1002, pod="vllm-0") == 20 << 30
+        up = {s[1]["bdf"]: s[1] for s in fams["amd_gpu_up"].samples}
+        assert (up["0000:72:00.0"]["namespace"], up["0000:72:00.0"]["pod"]) == ("research", "llama-train-0")
+        assert up["0000:5a:00.0"]["container"] == "server"
+        assert up["0000:23:00.0"]["pod"] == ""  # its pod runs on node-b: not ours
+        assert promtext.value(fams, "amd_pod_gpus", pod="vllm-0") == 1
+        assert promtext.value(fams, "amd_gpu_process_vram_bytes", pid=1002, container="server") == 20 << 30
+        # apiserver outage: last known metadata keeps attribution working
+        api.fail_status = 503
+        ex._control.refresh_once()
+        assert "apiserver" in ex._control.errors
+    finally:
+        ex.stop()
+        kub.stop()
+        api.stop()
+        request_cleanup()
