@@ -1,0 +1,91 @@
+"""Config precedence (CLI > env > YAML > defaults), validation, and the CLI daemon end to
+end: start, serve, SIGTERM -> clean exit (the reference's deferred nvml.Shutdown never ran,
+/root/reference/main.go:49-54)."""
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+import urllib.request
+
+import pytest
+
+from kubernetes_gpu_exporter_amd.config import Config, load_config, make_config
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_defaults_match_reference_endpoint():
+    c = Config()
+    assert c.listen == ":8000" and c.path == "/metrics"  # main.go:70-71
+    assert c.listen_host_port() == ("0.0.0.0", 8000)
+
+
+def test_precedence(tmp_path):
+    y = tmp_path / "c.yaml"
+    y.write_text("interval: 5\nlisten: ':9000'\nenable_sentinel: true\nmock_devices: 3\n")
+    env = {"GPUEXP_INTERVAL": "2", "GPUEXP_MOCK_DEVICES": "4", "NODE_NAME": "node-7"}
+    c = load_config(["--config", str(y), "--interval", "0.5"], env=env)
+    assert c.interval == 0.5            # CLI
+    assert c.mock_devices == 4          # env over YAML
+    assert c.listen == ":9000"          # YAML
+    assert c.enable_sentinel is True
+    assert c.node_name == "node-7"      # downward API
+    c = load_config(["--gzip", "false", "--devices", "0,2"], env={})
+    assert c.gzip is False and c.devices == ["0", "2"]
+    c = load_config(["--enable-counters"], env={})  # bare flag = true
+    assert c.enable_counters is True
+
+
+@pytest.mark.parametrize("bad", [
+    {"backend": "nvml"}, {"series_profile": "huge"}, {"interval": -1}, {"path": "metrics"},
+    {"listen": ":99999"}, {"mock_devices": 0}, {"log_level": "loud"}, {"nonsense": 1}, {"gzip": "maybe"},
+])
+def test_validation(bad):
+    with pytest.raises(ValueError):
+        make_config(bad)
+
+
+def test_engine_config_translation(native):
+    c = make_config({"listen": "127.0.0.1:9123", "path": "/m", "backend": "mock", "interval": 0.1,
+                     "devices": "1,3", "series_profile": "compact"})
+    ec = c.to_engine_config(native)
+    assert (ec.http.host, ec.http.port, ec.http.metrics_path) == ("127.0.0.1", 9123, "/m")
+    assert ec.backend == "mock" and ec.interval_s == 0.1 and ec.device_filter == [1, 3]
+    assert ec.series_profile == "compact"
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_cli_daemon_lifecycle(tmp_path):
+    port = _free_port()
+    trace = tmp_path / "trace.json"
+    p = subprocess.Popen([sys.executable, "-m", "kubernetes_gpu_exporter_amd", "--backend", "mock",
+                          "--mock-devices", "2", "--listen", f"127.0.0.1:{port}", "--path", "/custom",
+                          "--interval", "0.02", "--trace", str(trace)],
+                         cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    try:
+        body = None
+        for _ in range(200):
+            try:
+                body = urllib.request.urlopen(f"http://127.0.0.1:{port}/custom", timeout=1).read().decode()
+                break
+            except Exception:
+                time.sleep(0.05)
+        assert body and 'amd_gpu_up{gpu="1"' in body
+        time.sleep(0.2)
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(timeout=15) == 0
+    finally:
+        if p.poll() is None:
+            p.kill()
+    import json
+    events = [e for e in json.loads(trace.read_text()) if e]
+    assert {e["name"] for e in events} >= {"devices", "processes", "render"}
