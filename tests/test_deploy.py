@@ -1,0 +1,62 @@
+"""Deploy artefacts are consistent with the code: manifests parse, the DaemonSet's args are
+accepted by the exporter's own CLI parser, the host mounts the design needs are present,
+RBAC is read-only (the reference needed pods/exec), and every Helm value referenced by a
+template exists in values.yaml."""
+import os
+import re
+
+import yaml
+
+from kubernetes_gpu_exporter_amd.config import load_config
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+K8S = os.path.join(ROOT, "deploy", "kubernetes")
+
+
+def docs(name):
+    with open(os.path.join(K8S, name)) as fh:
+        return [d for d in yaml.safe_load_all(fh) if d]
+
+
+def test_manifests_parse():
+    for f in os.listdir(K8S):
+        assert docs(f), f
+
+
+def test_daemonset_contract():
+    (ds,) = docs("daemonset.yaml")
+    spec = ds["spec"]["template"]["spec"]
+    assert spec["hostPID"] is True  # KFD reports host PIDs
+    c = spec["containers"][0]
+    cfg = load_config(c["args"], env={"NODE_NAME": "n1"})
+    assert cfg.backend == "amdsmi" and cfg.enable_counters and cfg.enable_rccl and cfg.listen == ":8000"
+    mounts = {m["mountPath"] for m in c["volumeMounts"]}
+    assert {"/sys", "/dev/kfd", "/dev/dri", "/var/lib/kubelet/pod-resources", "/var/log/pods"} <= mounts
+    assert cfg.rccl_dir in mounts
+    assert any(e["name"] == "NODE_NAME" for e in c["env"])
+    assert c["readinessProbe"]["httpGet"]["path"] == "/readyz"
+    assert c["livenessProbe"]["httpGet"]["path"] == "/healthz"
+
+
+def test_rbac_is_read_only():
+    for d in docs("rbac.yaml"):
+        if d["kind"] == "ClusterRole":
+            for rule in d["rules"]:
+                assert set(rule["verbs"]) <= {"get", "list", "watch"}
+                assert "pods/exec" not in rule["resources"]
+
+
+def test_helm_values_referenced_exist():
+    chart = os.path.join(ROOT, "deploy", "helm", "gpuexp")
+    with open(os.path.join(chart, "values.yaml")) as fh:
+        values = yaml.safe_load(fh)
+    refs = set()
+    for f in os.listdir(os.path.join(chart, "templates")):
+        with open(os.path.join(chart, "templates", f)) as fh:
+            refs |= set(re.findall(r"\.Values\.([A-Za-z0-9_.]+)", fh.read()))
+    assert refs
+    for r in refs:
+        node = values
+        for part in r.split("."):
+            assert isinstance(node, dict) and part in node, f"values.yaml lacks {r}"
+            node = node[part]
