@@ -1,0 +1,99 @@
+// Concurrency stress for the telemetry core (run under TSAN / ASAN+UBSAN via CMake presets):
+//   - sampler thread at 100 Hz over 8 mock GPUs
+//   - HTTP server with 2 SO_REUSEPORT loops
+//   - N scraper threads on keep-alive connections (plus one gzip scraper)
+//   - a control-plane thread swapping pods / cgroup overrides / process lists / faults
+// Every response must be a complete exposition whose tick counter never goes backwards.
+// SURVEY.md §5 "Race detection / sanitizers": sampler vs HTTP vs attribution updates.
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "gpuexp/client.h"
+#include "gpuexp/engine.h"
+
+using namespace gpuexp;
+
+static double ticks_in(const std::string& body) {
+  size_t p = body.find("\ngpuexp_ticks_total ");
+  if (p == std::string::npos) return -1;
+  return std::atof(body.c_str() + p + 20);
+}
+
+int main(int argc, char** argv) {
+  double seconds = argc > 1 ? std::atof(argv[1]) : 3.0;
+  int scrapers = argc > 2 ? std::atoi(argv[2]) : 4;
+  EngineConfig cfg;
+  cfg.backend = "mock";
+  cfg.mock_devices = 8;
+  cfg.interval_s = 0.01;
+  cfg.enable_sentinel = true;
+  cfg.enable_counters = true;
+  cfg.http.host = "127.0.0.1";
+  cfg.http.port = 0;
+  cfg.http.threads = 2;
+  Engine e(cfg);
+  std::string err;
+  if (!e.start(&err)) {
+    std::fprintf(stderr, "start failed: %s\n", err.c_str());
+    return 2;
+  }
+  int port = e.http_port();
+  std::atomic<bool> stop{false};
+  std::atomic<long> scrapes{0}, bad{0};
+
+  std::vector<std::thread> th;
+  for (int s = 0; s < scrapers; ++s) {
+    th.emplace_back([&, s] {
+      ScrapeClient c("127.0.0.1", port, "/metrics", s == 0, 2000);
+      double last = -1;
+      while (!stop.load()) {
+        double ns = c.scrape();
+        if (ns < 0 || c.last_status() == 503) continue;
+        scrapes.fetch_add(1);
+        if (s == 0) continue;  // gzip body: only transport-checked
+        const std::string& b = c.last_body();
+        double t = ticks_in(b);
+        if (b.compare(0, 7, "# HELP ") != 0 || b.back() != '\n' || t < last) bad.fetch_add(1);
+        last = t;
+      }
+    });
+  }
+  th.emplace_back([&] {
+    unsigned k = 0;
+    while (!stop.load()) {
+      ++k;
+      std::vector<PodMeta> pods(2);
+      pods[0] = {"12345678-1234-1234-1234-1234567890a" + std::to_string(k % 10), "ns", "pod-" + std::to_string(k % 7),
+                 {{std::string(64, 'a'), "main"}}};
+      pods[1] = {"22345678-1234-1234-1234-1234567890ab", "ns2", "pod-b", {}};
+      e.set_pods(pods);
+      e.set_pid_cgroup(int(100 + k % 5), "/kubepods/burstable/pod12345678-1234-1234-1234-1234567890a" +
+                                              std::to_string(k % 10) + "/" + std::string(64, 'a'));
+      if (k % 50 == 0) e.clear_pid_cgroups();
+      std::vector<ProcSample> procs;
+      for (int p = 0; p < int(k % 6); ++p) {
+        ProcSample ps;
+        ps.pid = 100 + p;
+        ps.vram_bytes = 1e9 * p;
+        ps.cu_occupancy = 10;
+        procs.push_back(ps);
+      }
+      e.mock()->set_processes(int(k % 8), procs);
+      e.mock()->set_fault(int(k % 8), k % 13 == 0 ? "error" : "none");
+      e.set_device_owners({{"0000:10:00.0", DeviceOwner{"ns", "owner-" + std::to_string(k % 3), "c"}}});
+      std::this_thread::sleep_for(std::chrono::milliseconds(3));
+    }
+  });
+  std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
+  stop.store(true);
+  for (auto& t : th) t.join();
+  EngineStats st = e.stats();
+  e.stop();
+  std::printf("ticks=%llu scrapes=%ld bad=%ld series=%llu render_bytes=%llu\n", (unsigned long long)st.ticks,
+              scrapes.load(), bad.load(), (unsigned long long)st.series, (unsigned long long)st.render_bytes);
+  return (bad.load() == 0 && scrapes.load() > 100 && st.ticks > 10) ? 0 : 1;
+}
