@@ -272,6 +272,7 @@ PYBIND11_MODULE(_gpuexp, m) {
   py::class_<EngineConfig>(m, "EngineConfig")
       .def(py::init<>())
       .def_readwrite("backend", &EngineConfig::backend)
+      .def_readwrite("device_threads", &EngineConfig::device_threads)
       .def_readwrite("mock_devices", &EngineConfig::mock_devices)
       .def_readwrite("host_root", &EngineConfig::host_root)
       .def_readwrite("interval_s", &EngineConfig::interval_s)

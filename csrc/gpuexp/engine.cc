@@ -50,6 +50,58 @@ const char* kThrNames[5] = {"ppt", "socket_thermal", "vr_thermal", "hbm_thermal"
 
 }  // namespace
 
+ForkJoinPool::ForkJoinPool(int threads) {
+  for (int t = 1; t < threads; ++t) workers_.emplace_back([this] { worker(); });
+}
+
+ForkJoinPool::~ForkJoinPool() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    quit_ = true;
+  }
+  cv_.notify_all();
+  for (auto& w : workers_) w.join();
+}
+
+void ForkJoinPool::worker() {
+  uint64_t seen = 0;
+  for (;;) {
+    const std::function<void(int)>* fn;
+    int n;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return quit_ || epoch_ != seen; });
+      if (quit_) return;
+      seen = epoch_;
+      fn = fn_;
+      n = n_;
+    }
+    for (int i; (i = next_.fetch_add(1)) < n;) (*fn)(i);
+    std::lock_guard<std::mutex> lk(mu_);
+    pending_ -= 1;
+    if (pending_ == 0) done_cv_.notify_all();
+  }
+}
+
+void ForkJoinPool::run(int n, const std::function<void(int)>& fn) {
+  if (workers_.empty() || n <= 1) {
+    for (int i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    fn_ = &fn;
+    n_ = n;
+    next_.store(0);
+    pending_ = int(workers_.size());
+    ++epoch_;
+  }
+  cv_.notify_all();
+  for (int i; (i = next_.fetch_add(1)) < n;) fn(i);
+  std::unique_lock<std::mutex> lk(mu_);
+  done_cv_.wait(lk, [&] { return pending_ == 0; });
+}
+
 const char* Engine::stage_name(int i) {
   static const char* n[kStages] = {"devices", "processes", "attribution", "sentinel",
                                    "counters", "series", "render", "publish"};
@@ -186,6 +238,9 @@ bool Engine::start(std::string* err) {
     devices_ = all;
   }
   dstate_.assign(devices_.size(), DevState());
+  int nthreads = cfg_.device_threads;
+  if (nthreads <= 0) nthreads = cfg_.backend == "mock" ? 1 : std::min<int>(int(devices_.size()), 8);
+  if (nthreads > 1) pool_ = std::make_unique<ForkJoinPool>(nthreads);
   kfd_ = std::make_unique<KfdProcReader>(cfg_.host_root, cfg_.exclude_self ? self_pid_ : -1, cfg_.kfd_cu_occupancy);
   resolver_ = std::make_unique<PidResolver>(cfg_.host_root);
 
@@ -699,22 +754,29 @@ void Engine::tick_locked(uint64_t now) {
     }
   }
 
-  // 0: device telemetry
+  // 0: device telemetry (per-GPU reads fan out over the pool; each touches only its own
+  // DevState and its own backend device slot)
   uint64_t errs = 0;
-  for (size_t i = 0; i < devices_.size(); ++i) {
-    DevState& st = dstate_[i];
+  auto sample_one = [this, now](int i) {
+    DevState& st = dstate_[size_t(i)];
     if (st.cur.ok) {
       st.prev = st.cur;
       st.have_prev = true;
     }
     st.cur = DeviceSample();
     st.cur.host_ns = now;
-    backend_->sample(devices_[i], &st.cur);
+    backend_->sample(devices_[size_t(i)], &st.cur);
+  };
+  if (pool_) {
+    pool_->run(int(devices_.size()), sample_one);
+  } else {
+    for (size_t i = 0; i < devices_.size(); ++i) sample_one(int(i));
+  }
+  for (auto& st : dstate_)
     if (!st.cur.ok) {
       st.errors += 1;
       errs += 1;
     }
-  }
   ts[1] = mono_ns();
 
   // 1: processes

@@ -29,6 +29,7 @@ int main(int argc, char** argv) {
   EngineConfig cfg;
   cfg.backend = "mock";
   cfg.mock_devices = 8;
+  cfg.device_threads = 4;  // exercise the fork-join device pool under the sanitizers
   cfg.interval_s = 0.01;
   cfg.enable_sentinel = true;
   cfg.enable_counters = true;

@@ -26,6 +26,7 @@ class Config:
     # sampling
     interval: float = 1.0                  # seconds; reference: 30 s (main.go:156)
     backend: str = "auto"                  # auto | amdsmi | sysfs | mock
+    device_threads: int = 0                # per-GPU read fan-out (0 = auto, 1 = serial)
     mock_devices: int = 1
     host_root: str = ""                    # prefix for /sys and /proc (DaemonSet: /host)
     devices: list = field(default_factory=list)  # exporter GPU indices to export (empty = all)
@@ -75,6 +76,7 @@ class Config:
         ec = native.EngineConfig()
         ec.backend = self.resolved_backend()
         ec.mock_devices = int(self.mock_devices)
+        ec.device_threads = int(self.device_threads)
         ec.host_root = self.host_root
         ec.interval_s = float(self.interval)
         host, port = self.listen_host_port()

@@ -124,6 +124,22 @@ def test_end_to_end_attribution(native, tmp_path):
         e.stop()
 
 
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_parallel_device_sampling_matches_serial(native, tmp_path, threads):
+    h = mi355x_node(tmp_path, 8)
+    for i, g in enumerate(h.gpus):
+        h.set_metrics(g, power=500 + i, hotspot=40 + i)
+    e = _engine(native, tmp_path, device_threads=threads)
+    try:
+        e.tick(S)
+        fams = promtext.parse(e.snapshot_text())
+        got = sorted(s[2] for s in fams["amd_gpu_power_watts"].samples)
+        assert got == [500.0 + i for i in range(8)]
+        assert len(fams["amd_gpu_up"].samples) == 8
+    finally:
+        e.stop()
+
+
 def test_pid_reuse_is_detected(native, tmp_path):
     h = mi355x_node(tmp_path, 1)
     g0 = h.gpus[0]
