@@ -108,6 +108,8 @@ def main() -> int:
     ap.add_argument("--sentinel", type=int, default=1)
     ap.add_argument("--counters", type=int, default=0)
     ap.add_argument("--out", default="")
+    ap.add_argument("--exporter", choices=("native", "both"), default="native",
+                    help="'both' also measures the reference-architecture exporter (utils/refstyle.py)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -208,13 +210,15 @@ def main() -> int:
             cgroups[p] = kubepods_cgroup(uid, cid, qos="guaranteed")
         write_pod_map(pod_map, pods, cgroups)
         client = n.ScrapeClient("127.0.0.1", port, "/metrics", args.gzip, 5000)
+    else:
+        client = None
 
-    def step(lat: list | None):
+    def step(cl, lat: list | None):
         t_start = time.perf_counter()
         if use_gpu:
             gemm_burst(iters)
         if rank == 0:
-            ns = client.scrape()  # GPUs are busy with the burst while we scrape
+            ns = cl.scrape()  # GPUs are busy with the burst while we scrape
             if lat is not None and ns >= 0:
                 lat.append(ns / 1e3)
         if dist is not None:
@@ -224,32 +228,42 @@ def main() -> int:
         if rest > 0:
             time.sleep(rest)
 
-    for _ in range(args.warmup):
-        step(None)
-    if dist is not None:
-        dist.barrier()
-    sync()
-    lat: list = []
-    if rank == 0:
-        cpu0 = cpu_seconds_precise(exporter.pid)
-        stats0 = None
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(lat)
-    if dist is not None:
-        dist.barrier()
-    sync()
-    elapsed = time.perf_counter() - t0
-    ms_per_step = elapsed / max(1, args.steps) * 1e3
-    if dist is not None:
-        t = torch.tensor([ms_per_step], device=dev if use_gpu else "cpu", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms_per_step = float(t.item())
+    def phase(proc, cl):
+        """W untimed + K timed steps (barrier + synchronize on both sides); returns the
+        latencies, exporter CPU% over the timed window and max-over-ranks ms/step."""
+        for _ in range(args.warmup):
+            step(cl, None)
+        if dist is not None:
+            dist.barrier()
+        sync()
+        lat: list = []
+        cpu0 = cpu_seconds_precise(proc.pid) if rank == 0 else 0.0
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(cl, lat)
+        if dist is not None:
+            dist.barrier()
+        sync()
+        elapsed = time.perf_counter() - t0
+        cpu_pct = 100.0 * (cpu_seconds_precise(proc.pid) - cpu0) / elapsed if rank == 0 else 0.0
+        msps = elapsed / max(1, args.steps) * 1e3
+        if dist is not None:
+            t = torch.tensor([msps], device=dev if use_gpu else "cpu", dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            msps = float(t.item())
+        return lat, cpu_pct, msps
+
+    def stop_proc(proc):
+        proc.terminate()
+        try:
+            proc.wait(timeout=10)
+        except subprocess.TimeoutExpired:
+            proc.kill()
+
+    lat, cpu_pct, ms_per_step = phase(exporter, client if rank == 0 else None)
 
     result = None
     if rank == 0:
-        cpu1 = cpu_seconds_precise(exporter.pid)
-        cpu_pct = 100.0 * (cpu1 - cpu0) / elapsed
         body = client.last_body()
         fams = promtext.parse(body.decode() if not args.gzip else __import__("gzip").decompress(body).decode())
         per_gpu: dict = {}
@@ -297,15 +311,43 @@ def main() -> int:
             "sentinel": sentinel,
             "workload_gemm_tflops_per_gpu": round(tflops, 1) if tflops else None,
         }
+        stop_proc(exporter)
+
+    if args.exporter == "both":
+        # Same workload, same scrape pacing, against the reference-ARCHITECTURE exporter
+        # (render-on-scrape registry + vendor-library polling; utils/refstyle.py).
+        ref = rclient = None
+        if rank == 0:
+            rport = free_port()
+            cmd = [sys.executable, "-m", "kubernetes_gpu_exporter_amd.utils.refstyle", "--port", str(rport),
+                   "--interval", str(1.0 / args.sample_hz), "--devices", ",".join(str(i) for i in range(n_gpus))]
+            if backend == "mock":
+                cmd.append("--mock")
+            ref = subprocess.Popen(cmd, env=dict(os.environ, GPUEXP_POD_MAP_FILE=pod_map), cwd=ROOT,
+                                   stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            for _ in range(600):
+                try:
+                    if http_get(rport, "/metrics", 0.5)[0] == 200:
+                        break
+                except OSError:
+                    time.sleep(0.05)
+            rclient = n.ScrapeClient("127.0.0.1", rport, "/metrics", args.gzip, 5000)
+        if dist is not None:
+            dist.barrier()
+        rlat, rcpu, _ = phase(ref, rclient)
+        if rank == 0:
+            stop_proc(ref)
+            result["refstyle"] = {"p50_scrape_us": round(statistics.median(rlat), 2) if rlat else None,
+                                  "p99_scrape_us": round(pct(rlat, 0.99), 2) if rlat else None,
+                                  "exporter_cpu_percent": round(rcpu, 3), "scrape_bytes": rclient.last_bytes,
+                                  "scrape_errors": rclient.errors}
+            if rlat and lat:
+                result["speedup_p50_vs_refstyle"] = round(statistics.median(rlat) / statistics.median(lat), 2)
+    if rank == 0:
         print(json.dumps(result), flush=True)
         if args.out:
             with open(args.out, "w") as fh:
                 json.dump(result, fh, indent=1)
-        exporter.terminate()
-        try:
-            exporter.wait(timeout=10)
-        except subprocess.TimeoutExpired:
-            exporter.kill()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

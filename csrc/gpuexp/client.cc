@@ -51,8 +51,22 @@ int read_response(int fd, std::string* buf, std::string* body, bool* server_clos
   std::string headers = buf->substr(0, hdr_end);
   for (auto& c : headers) c = char(::tolower(c));
   size_t p = headers.find("content-length:");
-  if (p != std::string::npos) parse_u64(headers.c_str() + p + 15, headers.size() - p - 15, &clen);
-  *server_close = headers.find("connection: close") != std::string::npos;
+  bool http10 = headers.compare(0, 8, "http/1.0") == 0;
+  *server_close = http10 || headers.find("connection: close") != std::string::npos;
+  if (p == std::string::npos) {
+    // No length: the body runs to EOF (HTTP/1.0 servers such as prometheus_client's).
+    for (;;) {
+      ssize_t n = ::recv(fd, tmp, sizeof(tmp), 0);
+      if (n < 0) return -1;
+      if (n == 0) break;
+      buf->append(tmp, size_t(n));
+    }
+    body->assign(*buf, hdr_end + 4, std::string::npos);
+    buf->clear();
+    *server_close = true;
+    return code;
+  }
+  parse_u64(headers.c_str() + p + 15, headers.size() - p - 15, &clen);
   size_t need = hdr_end + 4 + size_t(clen);
   while (buf->size() < need) {
     ssize_t n = ::recv(fd, tmp, sizeof(tmp), 0);
