@@ -25,6 +25,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -230,6 +231,8 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_sample(int dev, 
   if (dev < 0 || size_t(dev) >= g_agents.size()) return -1;
   Agent& a = g_agents[size_t(dev)];
   if (!a.started) return -1;
+  static const bool no_sample = std::getenv("GPUEXP_RP_NOSAMPLE") != nullptr;  // diagnostics
+  if (no_sample) return -1;
   size_t n = a.recs.size();
   if (rocprofiler_sample_device_counting_service(a.ctx, {}, ROCPROFILER_COUNTER_FLAG_NONE, a.recs.data(), &n) !=
       ROCPROFILER_STATUS_SUCCESS)

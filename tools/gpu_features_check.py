@@ -39,7 +39,13 @@ def counters(seconds: float) -> dict:
     c.device_filter = [0]
     e = n.Engine(c)
     e.start()
+    from kubernetes_gpu_exporter_amd.utils.procstat import thread_cpu_seconds
+    time.sleep(0.5)
+    cpu0 = thread_cpu_seconds(os.getpid())
     time.sleep(seconds)
+    cpu1 = thread_cpu_seconds(os.getpid())
+    hot = sorted(((cpu1[k] - cpu0.get(k, 0.0)) / seconds * 100, k) for k in cpu1)[-6:]
+    print("per-thread CPU% over the window:", [(round(p, 1), k) for p, k in hot], flush=True)
     text = e.snapshot_text()
     status = e.source_status()
     import ctypes
