@@ -290,6 +290,8 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("sentinel_spin", &EngineConfig::sentinel_spin)
       .def_readwrite("enable_counters", &EngineConfig::enable_counters)
       .def_readwrite("counters_plugin", &EngineConfig::counters_plugin)
+      .def_readwrite("counters_window_ms", &EngineConfig::counters_window_ms)
+      .def_readwrite("counters_interval_ms", &EngineConfig::counters_interval_ms)
       .def_readwrite("enable_rccl", &EngineConfig::enable_rccl)
       .def_readwrite("rccl_dir", &EngineConfig::rccl_dir)
       .def_readwrite("force_amdsmi_metrics", &EngineConfig::force_amdsmi_metrics)

@@ -247,7 +247,7 @@ bool Engine::start(std::string* err) {
   // Counters first: the rocprofiler tool must register before the HSA runtime loads,
   // which the sentinel's first HIP call does.
   if (cfg_.enable_counters && cfg_.backend != "mock") {
-    counters_ = make_rocprof_counters(cfg_.counters_plugin);
+    counters_ = make_rocprof_counters(cfg_.counters_plugin, cfg_.counters_window_ms, cfg_.counters_interval_ms);
     std::string e;
     if (!counters_ || !counters_->start(devices_, &e)) {
       counters_status_ = "unavailable: " + e;

@@ -73,6 +73,8 @@ struct EngineConfig {
   int sentinel_spin = 500;  // ~15 us window (rocprofv3: spin 2000 ran 61 us/launch)
   bool enable_counters = false;
   std::string counters_plugin;         // path to _gpuexp_rocprof.so
+  int counters_window_ms = 20;         // counting window (rocprofiler context started)...
+  int counters_interval_ms = 1000;     // ...once per interval (duty cycle, see rocprof_plugin.cc)
   bool enable_rccl = false;
   std::string rccl_dir = "/dev/shm";
   bool force_amdsmi_metrics = false;

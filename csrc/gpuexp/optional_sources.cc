@@ -29,7 +29,8 @@ using rp_scope_fn = int (*)(int dev);
 
 class PluginCounters : public CounterSource {
  public:
-  explicit PluginCounters(std::string path) : path_(std::move(path)) {}
+  PluginCounters(std::string path, int window_ms, int interval_ms)
+      : path_(std::move(path)), window_ms_(window_ms), interval_ms_(interval_ms) {}
   ~PluginCounters() override { stop(); }
 
   bool start(const std::vector<DeviceInfo>& devs, std::string* err) override {
@@ -48,6 +49,9 @@ class PluginCounters : public CounterSource {
       *err = "plugin " + path_ + " lacks the gpuexp_rp_* ABI";
       return false;
     }
+    using duty_fn = void (*)(int, int);
+    if (auto duty = reinterpret_cast<duty_fn>(::dlsym(handle_, "gpuexp_rp_set_duty")))
+      duty(window_ms_, interval_ms_);
     std::vector<const char*> bdfs;
     for (auto& d : devs) bdfs.push_back(d.bdf.c_str());
     char ebuf[512] = {0};
@@ -90,6 +94,7 @@ class PluginCounters : public CounterSource {
 
  private:
   std::string path_;
+  int window_ms_, interval_ms_;
   void* handle_ = nullptr;
   rp_init_fn init_ = nullptr;
   rp_sample_fn sample_ = nullptr;
@@ -228,8 +233,9 @@ std::unique_ptr<SentinelSource> make_hip_sentinel(int ring_slots, int spin_iters
 
 std::string default_rocprof_plugin() { return self_dir() + "/_gpuexp_rocprof.so"; }
 
-std::unique_ptr<CounterSource> make_rocprof_counters(const std::string& plugin_path) {
-  return std::make_unique<PluginCounters>(plugin_path);
+std::unique_ptr<CounterSource> make_rocprof_counters(const std::string& plugin_path, int window_ms,
+                                                     int interval_ms) {
+  return std::make_unique<PluginCounters>(plugin_path, window_ms, interval_ms);
 }
 
 std::unique_ptr<RcclSource> make_rccl_source(const std::string& dir) {

@@ -22,7 +22,10 @@
 #include <rocprofiler-sdk/rocprofiler.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -70,6 +73,9 @@ struct Agent {
   int last_inst[kNumCtr] = {};
   size_t last_nrec = 0;
   int scope = -1;  // -1 unknown, 0 wave/EA counters VMID-filtered to this process, 1 device-wide
+  double latest[8] = {};
+  bool latest_valid = false;
+  uint64_t windows = 0;
   bool have_prev = false;
   std::chrono::steady_clock::time_point prev_t;
 };
@@ -192,6 +198,116 @@ bool build_config(Agent& a, std::string* why) {
 
 }  // namespace
 
+namespace {
+
+// Duty cycle.  Measured on MI355X: while a device-counting context is STARTED a
+// rocprofiler-sdk/HSA thread spins one core at 100% (even with no sample calls), so the
+// context is only started for a short window per interval: start -> read (baseline) ->
+// window -> read -> stop.  The window's deltas give the rates; the engine's tick never
+// blocks on the GPU (it takes the latest completed window).
+int g_window_ms = 20;
+int g_interval_ms = 1000;
+std::thread g_thread;
+std::atomic<bool> g_quit{false};
+std::condition_variable g_cv;
+std::mutex g_cv_mu;
+
+bool read_counts(Agent& a, double* v, int* inst) {
+  size_t n = a.recs.size();
+  if (rocprofiler_sample_device_counting_service(a.ctx, {}, ROCPROFILER_COUNTER_FLAG_NONE, a.recs.data(), &n) !=
+      ROCPROFILER_STATUS_SUCCESS)
+    return false;
+  for (int k = 0; k < kNumCtr; ++k) {
+    v[k] = 0;
+    inst[k] = 0;
+  }
+  for (size_t i = 0; i < n; ++i) {
+    rocprofiler_counter_id_t cid{};
+    if (rocprofiler_query_record_counter_id(a.recs[i].id, &cid) != ROCPROFILER_STATUS_SUCCESS) continue;
+    auto it = a.counter_slot.find(cid.handle);
+    if (it == a.counter_slot.end()) continue;
+    int k = it->second;
+    double x = a.recs[i].counter_value;
+    v[k] = use_max(k) ? std::max(v[k], x) : v[k] + x;
+    inst[k] += 1;
+  }
+  a.last_nrec = n;
+  return true;
+}
+
+void derive(Agent& a, const double* d, double wall) {
+  const double nan = std::nan("");
+  double gui = d[kGuiActive];
+  // Scope detection.  As a non-root client (perf_event_paranoid=3 on the test pool) the
+  // wave-level SQ counters and the TCC EA requests are VMID-filtered to THIS process,
+  // while SQ_VALU_MFMA_BUSY_CYCLES and GRBM are chip-global (measured against rocprofv3
+  // dispatch counts: profiles/r01/pmc_gemm_dispatch.txt).  A busy GPU on which the
+  // exporter sees almost no waves means the filtered set must not be exported as device
+  // totals.
+  if (d[kGrbmCount] > 0 && gui / d[kGrbmCount] > 0.5 && d[kMfma] > 0) a.scope = d[kWaves] / wall < 1000.0 ? 0 : 1;
+  double* out = a.latest;
+  out[0] = gui > 0 && a.simd ? 100.0 * d[kMfma] / (gui * a.simd) : nan;              // MfmaUtil
+  double se = a.last_inst[kSqBusy] > 0 ? a.last_inst[kSqBusy] : 1;                     // one per SE
+  out[1] = gui > 0 ? std::min(100.0, 100.0 * d[kSqBusy] / (gui * se)) : nan;
+  out[2] = d[kGrbmCount] > 0 ? 100.0 * gui / d[kGrbmCount] : nan;                     // GPU busy
+  out[3] = d[kWaves] / wall;                                                          // waves/s
+  out[4] = gui > 0 && a.cu ? 100.0 * d[kLdsActive] / (gui * a.cu) : nan;             // LDS util
+  out[5] = d[kLdsActive] > 0 ? 100.0 * d[kLdsConflict] / d[kLdsActive] : 0.0;        // bank conflicts
+  out[6] = (d[kTccBubble] * 128.0 + (d[kRdReq] - d[kTccBubble]) * 64.0) / wall;     // FETCH_SIZE bytes/s
+  out[7] = ((d[kWrReq] - d[kWrReq64]) * 32.0 + d[kWrReq64] * 64.0) / wall;          // WRITE_SIZE bytes/s
+  a.latest_valid = true;
+  a.windows += 1;
+}
+
+void counting_loop() {
+  while (!g_quit.load()) {
+    double base[16][kNumCtr];
+    std::chrono::steady_clock::time_point t0[16];
+    bool ok[16] = {};
+    {
+      std::lock_guard<std::mutex> lk(g_mu);
+      for (size_t i = 0; i < g_agents.size() && i < 16; ++i) {
+        Agent& a = g_agents[i];
+        if (!a.have_cfg || rocprofiler_start_context(a.ctx) != ROCPROFILER_STATUS_SUCCESS) continue;
+        a.started = true;
+        ok[i] = read_counts(a, base[i], a.last_inst);
+        t0[i] = std::chrono::steady_clock::now();
+      }
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(g_window_ms));
+    {
+      std::lock_guard<std::mutex> lk(g_mu);
+      for (size_t i = 0; i < g_agents.size() && i < 16; ++i) {
+        Agent& a = g_agents[i];
+        if (!a.started) continue;
+        double v[kNumCtr];
+        if (ok[i] && read_counts(a, v, a.last_inst)) {
+          double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0[i]).count();
+          double d[kNumCtr];
+          bool sane = wall > 0;
+          for (int k = 0; k < kNumCtr; ++k) {
+            d[k] = v[k] - base[i][k];
+            if (d[k] < 0) sane = false;
+          }
+          std::memcpy(a.last_raw, d, sizeof(d));
+          if (sane) derive(a, d, wall);
+        }
+        rocprofiler_stop_context(a.ctx);
+        a.started = false;
+      }
+    }
+    std::unique_lock<std::mutex> lk(g_cv_mu);
+    g_cv.wait_for(lk, std::chrono::milliseconds(std::max(0, g_interval_ms - g_window_ms)), [] { return g_quit.load(); });
+  }
+}
+
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) void gpuexp_rp_set_duty(int window_ms, int interval_ms) {
+  g_window_ms = std::max(1, window_ms);
+  g_interval_ms = std::max(g_window_ms, interval_ms);
+}
+
 extern "C" __attribute__((visibility("default"))) int gpuexp_rp_init(int ndev, const char* const* bdfs, char* err,
                                                                      int errlen) {
   std::lock_guard<std::mutex> lk(g_mu);
@@ -214,15 +330,20 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_init(int ndev, c
   for (auto& a : g_agents) {
     if (a.dev < 0) continue;
     if (!build_config(a, &why)) continue;
+    // Probe once that the context can start (PMC permission / exclusivity).
     if (rocprofiler_start_context(a.ctx) != ROCPROFILER_STATUS_SUCCESS) {
       why = "start_context failed (PMCs busy or insufficient permission?)";
+      a.have_cfg = false;
       continue;
     }
-    a.started = true;
+    rocprofiler_stop_context(a.ctx);
     ++ok;
   }
   if (!ok) return fail(why.empty() ? "no agent started" : why);
-  g_status = "rocprofiler-sdk device counting on " + std::to_string(ok) + " GPU(s)";
+  g_quit.store(false);
+  g_thread = std::thread(counting_loop);
+  g_status = "rocprofiler-sdk device counting on " + std::to_string(ok) + " GPU(s), " + std::to_string(g_window_ms) +
+             " ms window every " + std::to_string(g_interval_ms) + " ms";
   return ok;
 }
 
@@ -230,67 +351,16 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_sample(int dev, 
   std::lock_guard<std::mutex> lk(g_mu);
   if (dev < 0 || size_t(dev) >= g_agents.size()) return -1;
   Agent& a = g_agents[size_t(dev)];
-  if (!a.started) return -1;
-  static const bool no_sample = std::getenv("GPUEXP_RP_NOSAMPLE") != nullptr;  // diagnostics
-  if (no_sample) return -1;
-  size_t n = a.recs.size();
-  if (rocprofiler_sample_device_counting_service(a.ctx, {}, ROCPROFILER_COUNTER_FLAG_NONE, a.recs.data(), &n) !=
-      ROCPROFILER_STATUS_SUCCESS)
-    return -1;
-  double v[kNumCtr] = {};
-  int inst[kNumCtr] = {};
-  for (size_t i = 0; i < n; ++i) {
-    rocprofiler_counter_id_t cid{};
-    if (rocprofiler_query_record_counter_id(a.recs[i].id, &cid) != ROCPROFILER_STATUS_SUCCESS) continue;
-    auto it = a.counter_slot.find(cid.handle);
-    if (it == a.counter_slot.end()) continue;
-    int k = it->second;
-    double x = a.recs[i].counter_value;
-    v[k] = use_max(k) ? std::max(v[k], x) : v[k] + x;
-    inst[k] += 1;
-  }
-  std::memcpy(a.last_raw, v, sizeof(v));
-  std::memcpy(a.last_inst, inst, sizeof(inst));
-  a.last_nrec = n;
-  auto now = std::chrono::steady_clock::now();
-  double d[kNumCtr];
-  bool restarted = false;
-  for (int k = 0; k < kNumCtr; ++k) {
-    d[k] = a.have_prev ? v[k] - a.prev[k] : v[k];
-    if (d[k] < 0) restarted = true;
-  }
-  double wall = a.have_prev ? std::chrono::duration<double>(now - a.prev_t).count() : dt_s;
-  std::memcpy(a.prev, v, sizeof(v));
-  a.prev_t = now;
-  bool first = !a.have_prev;
-  a.have_prev = true;
-  if (first || restarted || wall <= 0) return -1;  // need one interval of deltas
-  const double nan = std::nan("");
-  double gui = d[kGuiActive];
-  // Scope detection.  As a non-root client (perf_event_paranoid=3 on the test pool) the
-  // wave-level SQ counters and the TCC EA requests are VMID-filtered to THIS process,
-  // while SQ_VALU_MFMA_BUSY_CYCLES and GRBM are chip-global (measured against rocprofv3
-  // dispatch counts: profiles/r01/pmc_gemm_dispatch.txt).  A busy GPU on which the
-  // exporter sees almost no waves means the filtered set must not be exported as device
-  // totals.
-  if (d[kGrbmCount] > 0 && gui / d[kGrbmCount] > 0.5 && d[kMfma] > 0) {
-    double waves_per_s = d[kWaves] / wall;
-    a.scope = waves_per_s < 1000.0 ? 0 : 1;
-  }
-  out[0] = gui > 0 && a.simd ? 100.0 * d[kMfma] / (gui * a.simd) : nan;              // MfmaUtil
-  // SQ_BUSY_CYCLES has one instance per shader engine: normalise by the instance count.
-  double se = a.last_inst[kSqBusy] > 0 ? a.last_inst[kSqBusy] : 1;
-  out[1] = gui > 0 ? std::min(100.0, 100.0 * d[kSqBusy] / (gui * se)) : nan;
-  out[2] = d[kGrbmCount] > 0 ? 100.0 * gui / d[kGrbmCount] : nan;                     // GPU busy
-  out[3] = d[kWaves] / wall;                                                          // waves/s
-  out[4] = gui > 0 && a.cu ? 100.0 * d[kLdsActive] / (gui * a.cu) : nan;             // LDS util
-  out[5] = d[kLdsActive] > 0 ? 100.0 * d[kLdsConflict] / d[kLdsActive] : 0.0;        // bank conflicts
-  out[6] = (d[kTccBubble] * 128.0 + (d[kRdReq] - d[kTccBubble]) * 64.0) / wall;     // FETCH_SIZE bytes/s
-  out[7] = ((d[kWrReq] - d[kWrReq64]) * 32.0 + d[kWrReq64] * 64.0) / wall;          // WRITE_SIZE bytes/s
+  if (!a.latest_valid) return -1;
+  std::memcpy(out, a.latest, sizeof(a.latest));
+  (void)dt_s;
   return 0;
 }
 
 extern "C" __attribute__((visibility("default"))) void gpuexp_rp_shutdown() {
+  g_quit.store(true);
+  g_cv.notify_all();
+  if (g_thread.joinable()) g_thread.join();
   std::lock_guard<std::mutex> lk(g_mu);
   for (auto& a : g_agents)
     if (a.started) {

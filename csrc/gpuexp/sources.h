@@ -40,8 +40,10 @@ class CounterSource {
   virtual void stop() = 0;
   virtual std::string status() const = 0;
 };
-// dlopen()s the rocprofiler-sdk plugin (_gpuexp_rocprof.so) next to the core.
-std::unique_ptr<CounterSource> make_rocprof_counters(const std::string& plugin_path);
+// dlopen()s the rocprofiler-sdk plugin (_gpuexp_rocprof.so) next to the core.  Counting
+// runs duty-cycled in the plugin: a `window_ms` counting window every `interval_ms`.
+std::unique_ptr<CounterSource> make_rocprof_counters(const std::string& plugin_path, int window_ms,
+                                                     int interval_ms);
 
 // One collective call record written by the RCCL tracer tool into a per-process ring.
 struct RcclTotals {

@@ -40,6 +40,8 @@ class Config:
     sentinel_spin: int = 500
     enable_counters: bool = False
     counters_plugin: str = ""
+    counters_window_ms: int = 20           # rocprofiler counting window ...
+    counters_interval_ms: int = 1000       # ... per interval (context-started spin is duty-cycled)
     enable_rccl: bool = False
     rccl_dir: str = "/var/run/gpuexp/rccl"
     # attribution / kubernetes control plane
@@ -101,6 +103,8 @@ class Config:
         else:
             from ._native import rocprof_plugin_path
             ec.counters_plugin = rocprof_plugin_path()
+        ec.counters_window_ms = int(self.counters_window_ms)
+        ec.counters_interval_ms = int(self.counters_interval_ms)
         ec.enable_rccl = bool(self.enable_rccl)
         ec.rccl_dir = self.rccl_dir
         ec.gc_after = int(self.gc_after)

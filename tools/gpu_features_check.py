@@ -35,6 +35,8 @@ def counters(seconds: float) -> dict:
     c.serve_http = False
     c.enable_counters = True
     c.counters_plugin = n.default_rocprof_plugin()
+    c.counters_window_ms = int(os.environ.get("WINDOW_MS", "20"))
+    c.counters_interval_ms = int(os.environ.get("INTERVAL_MS", "500"))
     c.enable_sentinel = True
     c.device_filter = [0]
     e = n.Engine(c)
