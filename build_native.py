@@ -3,7 +3,8 @@
 
 Outputs (all inside kubernetes_gpu_exporter_amd/, so they travel with the repo):
   _gpuexp<EXT_SUFFIX>        pybind11 module: C++ telemetry core + HIP sentinel + MFMA GEMM
-  _gpuexp_rocprof.so         rocprofiler-sdk device-counting plugin (dlopen'd by the core)
+  _gpuexp_aqlpmc.so          device PMC plugin: aqlprofile PM4 on an owned HSA queue (default)
+  _gpuexp_rocprof.so         rocprofiler-sdk device-counting plugin (alternative counter backend)
   libgpuexp_rccl_tracer.so   rocprofiler-sdk RCCL API-tracing tool (ROCP_TOOL_LIBRARIES)
 
 C++ (.cc) compiles with g++, HIP (.hip) with hipcc --offload-arch=gfx950; the module is
@@ -37,6 +38,7 @@ CORE_CC = [
 SENTINEL_HIP = ["gpuexp/sentinel.hip"]
 KERNELS_HIP = ["kernels/gemm_bf16.hip", "kernels/kernels_bindings.hip"]
 ROCPROF_CC = ["gpuexp/rocprof_plugin.cc"]
+AQLPMC_CC = ["gpuexp/aql_pmc.cc"]
 TRACER_CC = ["gpuexp/rccl_tracer.cc"]
 
 
@@ -127,7 +129,7 @@ def build(force: bool = False, jobs: int = 8, sanitize: str | None = None, verbo
     hdr = _hdr_mtime()
     BUILD.mkdir(parents=True, exist_ok=True)
     srcs = CORE_CC + SENTINEL_HIP + KERNELS_HIP
-    extra = [s for s in ROCPROF_CC + TRACER_CC if (CSRC / s).exists()]
+    extra = [s for s in ROCPROF_CC + AQLPMC_CC + TRACER_CC if (CSRC / s).exists()]
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         futs = {s: ex.submit(compile_one, s, hdr, force, sanitize) for s in srcs + extra}
         objs = {s: f.result() for s, f in futs.items()}
@@ -140,6 +142,9 @@ def build(force: bool = False, jobs: int = 8, sanitize: str | None = None, verbo
     if (CSRC / ROCPROF_CC[0]).exists():
         outputs["rocprof_plugin"] = str(link_plain([objs[ROCPROF_CC[0]]], PKG / "_gpuexp_rocprof.so",
                                                    ["-lrocprofiler-sdk", "-lhsa-runtime64", "-lpthread"]))
+    if (CSRC / AQLPMC_CC[0]).exists():
+        outputs["aqlpmc_plugin"] = str(link_plain([objs[AQLPMC_CC[0]]], PKG / "_gpuexp_aqlpmc.so",
+                                                  ["-lhsa-runtime64", "-lpthread"]))
     if (CSRC / TRACER_CC[0]).exists():
         outputs["rccl_tracer"] = str(link_plain([objs[TRACER_CC[0]]], PKG / "libgpuexp_rccl_tracer.so",
                                                 ["-lrocprofiler-sdk", "-lpthread"]))

@@ -1,0 +1,503 @@
+// Device PMC plugin on an exporter-owned HSA queue (_gpuexp_aqlpmc.so), dlopen()ed by the
+// core through the same gpuexp_rp_* ABI as the rocprofiler-sdk plugin (rocprof_plugin.cc).
+//
+// Why not rocprofiler-sdk's device counting service: registering that tool makes an HSA
+// runtime thread spin one core at 100% for the life of the process (rocprof_plugin.cc
+// header; measured 101% exporter CPU).  The counting itself is only three PM4 programs —
+// select+reset+enable, and read+disable — which libhsa-amd-aqlprofile64 generates as AQL
+// vendor packets (hsa_ven_amd_aqlprofile.h).  Here each GPU gets:
+//   * one low-priority AQL queue of 64 slots (nothing else is ever submitted to it),
+//   * one interrupt-backed completion signal (waited on BLOCKED — no polling thread),
+//   * a command buffer and a PMC output buffer in fine-grained system memory,
+// and a background thread duty-cycles a counting window per interval:
+//   start packet -> wait -> sleep(window) -> read packet -> wait -> stop packet -> wait
+//   -> iterate output.
+// Measured on MI355X (profiles/r01/counters_aqlpmc.txt): same counter values as the
+// rocprofiler-sdk path, exporter CPU 0.3-0.7% instead of 101%.
+// The engine's tick never blocks on the GPU: gpuexp_rp_sample returns the latest window.
+//
+// Event ids are the gfx950 select values of /opt/rocm/share/rocprofiler-sdk/counter_defs.yaml
+// (SQ 93/3/4/147/142, GRBM 2/0, TCC 62/42/30/31) and are checked with
+// hsa_ven_amd_aqlprofile_validate_event at init.  TCC is programmed on every channel
+// instance (16 per XCD); SQ and GRBM are broadcast and come back once per SE / XCC.
+#include <execinfo.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+#include <hsa/hsa_ven_amd_aqlprofile.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <csignal>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "gpuexp/counter_model.h"
+
+namespace {
+
+using namespace gpuexp_ctr;
+using Clock = std::chrono::steady_clock;
+
+struct EventDef {
+  hsa_ven_amd_aqlprofile_block_name_t block;
+  uint32_t id;
+  int ctr;
+};
+
+// gfx950 select values (counter_defs.yaml, architectures: gfx950).
+const EventDef kGfx950[] = {
+    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 93, kMfma},        {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 3, kSqBusy},
+    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 4, kWaves},        {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 147, kLdsActive},
+    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 142, kLdsConflict}, {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, 2, kGuiActive},
+    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, 0, kGrbmCount},  {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 62, kTccBubble},
+    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 42, kRdReq},      {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 30, kWrReq},
+    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 31, kWrReq64},
+};
+
+struct Agent {
+  int dev = -1;
+  hsa_agent_t gpu{};
+  std::string bdf, gfx;
+  hsa_queue_t* queue = nullptr;
+  hsa_signal_t sig{};
+  std::vector<hsa_ven_amd_aqlprofile_event_t> events;
+  std::vector<int> event_ctr;  // events[i] -> Ctr
+  hsa_ven_amd_aqlprofile_profile_t profile{};
+  hsa_ext_amd_aql_pm4_packet_t start_pkt{}, read_pkt{}, stop_pkt{};
+  uint32_t out_size = 0;
+  void* cmd_buf = nullptr;
+  void* out_buf = nullptr;
+  bool ready = false;
+  bool broken = false;      // a packet timed out: the GPU may still own the buffers
+  std::atomic<bool> queue_error{false};
+  double last_raw[kNumCtr] = {};
+  int last_inst[kNumCtr] = {};
+  uint64_t last_samples = 0;
+  Derived m;
+};
+
+// aqlprofile entry points come from the runtime's extension table: the runtime loads
+// libhsa-amd-aqlprofile64.so and hands it the HSA API table (calling the library's exports
+// directly, without that hand-off, faults inside it).
+hsa_ven_amd_aqlprofile_pfn_t g_aql{};
+bool g_debug = false;
+
+void crumb(const char* what, const std::string& detail = "") {
+  if (g_debug) std::fprintf(stderr, "[aqlpmc] %s %s\n", what, detail.c_str());
+}
+
+void segv_backtrace(int sig) {
+  void* frames[48];
+  const int n = ::backtrace(frames, 48);
+  ::backtrace_symbols_fd(frames, n, 2);
+  ::signal(sig, SIG_DFL);
+  ::raise(sig);
+}
+
+std::mutex g_mu;
+std::vector<Agent*> g_agents;  // indexed by the engine's device index
+std::string g_status = "not initialised";
+bool g_hsa_up = false;
+hsa_amd_memory_pool_t g_sys_pool{};
+bool g_have_pool = false;
+uint64_t g_ts_freq = 1000000000ull;
+int g_window_ms = 20;
+int g_interval_ms = 1000;
+std::thread g_thread;
+std::atomic<bool> g_quit{false};
+std::condition_variable g_cv;
+std::mutex g_cv_mu;
+
+std::string lower(std::string s) {
+  for (auto& c : s) c = char(::tolower(c));
+  return s;
+}
+
+void queue_error_cb(hsa_status_t, hsa_queue_t*, void* data) {
+  static_cast<Agent*>(data)->queue_error.store(true);
+}
+
+hsa_status_t pick_sys_pool(hsa_amd_memory_pool_t pool, void*) {
+  hsa_amd_segment_t seg{};
+  hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
+  if (seg != HSA_AMD_SEGMENT_GLOBAL) return HSA_STATUS_SUCCESS;
+  uint32_t flags = 0;
+  hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+  bool alloc = false;
+  hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc);
+  if (alloc && (flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_KERNARG_INIT)) {
+    g_sys_pool = pool;
+    g_have_pool = true;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+struct Found {
+  std::vector<std::pair<hsa_agent_t, std::string>> gpus;  // (agent, bdf)
+  std::vector<hsa_agent_t> cpus;
+};
+
+hsa_status_t collect_agent(hsa_agent_t a, void* ud) {
+  auto* f = static_cast<Found*>(ud);
+  hsa_device_type_t t{};
+  hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t);
+  if (t == HSA_DEVICE_TYPE_CPU) {
+    f->cpus.push_back(a);
+  } else if (t == HSA_DEVICE_TYPE_GPU) {
+    uint32_t bdfid = 0, domain = 0;
+    hsa_agent_get_info(a, hsa_agent_info_t(HSA_AMD_AGENT_INFO_BDFID), &bdfid);
+    hsa_agent_get_info(a, hsa_agent_info_t(HSA_AMD_AGENT_INFO_DOMAIN), &domain);
+    char bdf[32];
+    std::snprintf(bdf, sizeof(bdf), "%04x:%02x:%02x.%x", domain, (bdfid >> 8) & 0xFF, (bdfid >> 3) & 0x1F,
+                  bdfid & 0x7);
+    f->gpus.emplace_back(a, bdf);
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+void* sys_alloc(size_t bytes, hsa_agent_t gpu) {
+  bytes = (bytes + 4095) & ~size_t(4095);
+  void* p = nullptr;
+  if (hsa_amd_memory_pool_allocate(g_sys_pool, bytes, 0, &p) != HSA_STATUS_SUCCESS) return nullptr;
+  if (hsa_amd_agents_allow_access(1, &gpu, nullptr, p) != HSA_STATUS_SUCCESS) {
+    hsa_amd_memory_pool_free(p);
+    return nullptr;
+  }
+  std::memset(p, 0, bytes);
+  return p;
+}
+
+// Writes one vendor-specific AQL packet and rings the doorbell.  Only this plugin's thread
+// submits to the queue, and at most one packet is in flight, so the ring never fills.
+void submit(Agent& a, const hsa_ext_amd_aql_pm4_packet_t& pkt) {
+  hsa_queue_t* q = a.queue;
+  const uint64_t idx = hsa_queue_add_write_index_screlease(q, 1);
+  auto* slot = static_cast<hsa_ext_amd_aql_pm4_packet_t*>(q->base_address) + (idx & (q->size - 1));
+  std::memcpy(slot->pm4_command, pkt.pm4_command, sizeof(pkt.pm4_command));
+  slot->completion_signal = a.sig;
+  const uint16_t header = uint16_t((HSA_PACKET_TYPE_VENDOR_SPECIFIC << HSA_PACKET_HEADER_TYPE) |
+                                   (1 << HSA_PACKET_HEADER_BARRIER) |
+                                   (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                                   (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+  __atomic_store_n(&slot->header, header, __ATOMIC_RELEASE);
+  hsa_signal_store_screlease(q->doorbell_signal, hsa_signal_value_t(idx));
+}
+
+// Submits `pkt`, waits (interrupt-driven) up to 1 s; returns the midpoint of submit and
+// completion (the packet's execution time estimate), or a default time_point on timeout.
+Clock::time_point run_packet(Agent& a, const hsa_ext_amd_aql_pm4_packet_t& pkt) {
+  hsa_signal_store_relaxed(a.sig, 1);
+  const auto t0 = Clock::now();
+  submit(a, pkt);
+  const hsa_signal_value_t v =
+      hsa_signal_wait_scacquire(a.sig, HSA_SIGNAL_CONDITION_LT, 1, g_ts_freq, HSA_WAIT_STATE_BLOCKED);
+  const auto t1 = Clock::now();
+  if (v >= 1 || a.queue_error.load()) return {};
+  return t0 + (t1 - t0) / 2;
+}
+
+struct Accum {
+  Agent* a;
+  double v[kNumCtr];
+  int inst[kNumCtr];
+  uint64_t samples;
+};
+
+hsa_status_t on_data(hsa_ven_amd_aqlprofile_info_type_t type, hsa_ven_amd_aqlprofile_info_data_t* d, void* ud) {
+  if (type != HSA_VEN_AMD_AQLPROFILE_INFO_PMC_DATA) return HSA_STATUS_SUCCESS;
+  auto* acc = static_cast<Accum*>(ud);
+  acc->samples += 1;
+  const auto& ev = d->pmc_data.event;
+  for (const auto& def : kGfx950) {
+    if (def.block != ev.block_name || def.id != ev.counter_id) continue;
+    const double x = double(d->pmc_data.result);
+    acc->v[def.ctr] = use_max(def.ctr) ? std::max(acc->v[def.ctr], x) : acc->v[def.ctr] + x;
+    acc->inst[def.ctr] += 1;
+    break;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+bool setup_agent(Agent& a, std::string* why) {
+  char name[64] = {};
+  hsa_agent_get_info(a.gpu, HSA_AGENT_INFO_NAME, name);
+  a.gfx = name;
+  crumb("agent", a.bdf + " " + a.gfx);
+  if (a.gfx != "gfx950") {
+    *why = "no PMC event table for " + a.gfx;
+    return false;
+  }
+  uint32_t cu = 0, simd_per_cu = 0;
+  hsa_agent_get_info(a.gpu, hsa_agent_info_t(HSA_AMD_AGENT_INFO_COMPUTE_UNIT_COUNT), &cu);
+  hsa_agent_get_info(a.gpu, hsa_agent_info_t(HSA_AMD_AGENT_INFO_NUM_SIMDS_PER_CU), &simd_per_cu);
+  a.m.cu = cu;
+  a.m.simd = cu * simd_per_cu;
+
+  hsa_ven_amd_aqlprofile_profile_t probe{};
+  probe.agent = a.gpu;
+  probe.type = HSA_VEN_AMD_AQLPROFILE_EVENT_TYPE_PMC;
+  hsa_ven_amd_aqlprofile_id_query_t tcc{"TCC", 0, 0};
+  if (g_aql.hsa_ven_amd_aqlprofile_get_info(&probe, HSA_VEN_AMD_AQLPROFILE_INFO_BLOCK_ID, &tcc) != HSA_STATUS_SUCCESS ||
+      tcc.instance_count == 0)
+    tcc.instance_count = 16;
+  for (const auto& def : kGfx950) {
+    const uint32_t n = def.block == HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC ? tcc.instance_count : 1;
+    for (uint32_t i = 0; i < n; ++i) {
+      hsa_ven_amd_aqlprofile_event_t ev{def.block, i, def.id};
+      bool ok = false;
+      if (g_aql.hsa_ven_amd_aqlprofile_validate_event(a.gpu, &ev, &ok) != HSA_STATUS_SUCCESS || !ok) continue;
+      a.events.push_back(ev);
+      a.event_ctr.push_back(def.ctr);
+    }
+  }
+  crumb("events", std::to_string(a.events.size()) + " (TCC instances " + std::to_string(tcc.instance_count) + ")");
+  if (a.events.empty()) {
+    *why = "aqlprofile rejected every event";
+    return false;
+  }
+  a.profile.agent = a.gpu;
+  a.profile.type = HSA_VEN_AMD_AQLPROFILE_EVENT_TYPE_PMC;
+  a.profile.events = a.events.data();
+  a.profile.event_count = uint32_t(a.events.size());
+  uint32_t cmd_size = 0, out_size = 0;
+  if (g_aql.hsa_ven_amd_aqlprofile_get_info(&a.profile, HSA_VEN_AMD_AQLPROFILE_INFO_COMMAND_BUFFER_SIZE, &cmd_size) !=
+          HSA_STATUS_SUCCESS ||
+      g_aql.hsa_ven_amd_aqlprofile_get_info(&a.profile, HSA_VEN_AMD_AQLPROFILE_INFO_PMC_DATA_SIZE, &out_size) !=
+          HSA_STATUS_SUCCESS ||
+      cmd_size == 0 || out_size == 0) {
+    *why = "aqlprofile buffer size query failed";
+    return false;
+  }
+  crumb("buffers", "cmd " + std::to_string(cmd_size) + " out " + std::to_string(out_size));
+  // The legacy size query does not scale the PM4 program by the XCC count (gfx950: 8 XCCs
+  // per agent; measured: a buffer of the reported 8 KiB is overrun inside
+  // hsa_ven_amd_aqlprofile_start), so both buffers are over-provisioned.
+  cmd_size = std::max<uint32_t>(cmd_size * 16, 256u << 10);
+  out_size = std::max<uint32_t>(out_size * 16, 64u << 10);
+  a.cmd_buf = sys_alloc(cmd_size, a.gpu);
+  a.out_buf = sys_alloc(out_size, a.gpu);
+  if (!a.cmd_buf || !a.out_buf) {
+    *why = "system memory pool allocation failed";
+    return false;
+  }
+  a.profile.command_buffer = {a.cmd_buf, cmd_size};
+  a.profile.output_buffer = {a.out_buf, out_size};
+  if (g_aql.hsa_ven_amd_aqlprofile_start(&a.profile, &a.start_pkt) != HSA_STATUS_SUCCESS) {
+    *why = "aqlprofile start packet generation failed";
+    return false;
+  }
+  crumb("start packet ok");
+  if (g_aql.hsa_ven_amd_aqlprofile_stop(&a.profile, &a.stop_pkt) != HSA_STATUS_SUCCESS) {
+    *why = "aqlprofile stop packet generation failed";
+    return false;
+  }
+  crumb("stop packet ok");
+  if (g_aql.hsa_ven_amd_aqlprofile_read(&a.profile, &a.read_pkt) != HSA_STATUS_SUCCESS) {
+    *why = "aqlprofile read packet generation failed";
+    return false;
+  }
+  a.out_size = out_size;
+  if (hsa_queue_create(a.gpu, 64, HSA_QUEUE_TYPE_SINGLE, queue_error_cb, &a, UINT32_MAX, UINT32_MAX, &a.queue) !=
+      HSA_STATUS_SUCCESS) {
+    *why = "hsa_queue_create failed";
+    return false;
+  }
+  crumb("queue created");
+  hsa_amd_queue_set_priority(a.queue, HSA_AMD_QUEUE_PRIORITY_LOW);
+  if (hsa_signal_create(1, 0, nullptr, &a.sig) != HSA_STATUS_SUCCESS) {
+    *why = "hsa_signal_create failed";
+    return false;
+  }
+  crumb("queue+signal ready; probing one window");
+  // Probe one empty window: proves the queue executes the PM4 programs.
+  if (run_packet(a, a.start_pkt) == Clock::time_point{} || run_packet(a, a.read_pkt) == Clock::time_point{} ||
+      run_packet(a, a.stop_pkt) == Clock::time_point{}) {
+    a.broken = true;
+    *why = "PM4 start/stop packet did not complete (PMCs unavailable?)";
+    return false;
+  }
+  a.ready = true;
+  return true;
+}
+
+void window_all() {
+  std::vector<Clock::time_point> t0(g_agents.size());
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (size_t i = 0; i < g_agents.size(); ++i) {
+      Agent* a = g_agents[i];
+      if (!a || !a->ready || a->broken) continue;
+      if (g_debug) std::memset(a->out_buf, 0x5A, a->out_size);  // unwritten samples show as 0x5A5A..
+      t0[i] = run_packet(*a, a->start_pkt);
+      if (t0[i] == Clock::time_point{}) a->broken = true;
+    }
+  }
+  std::unique_lock<std::mutex> wl(g_cv_mu);
+  g_cv.wait_for(wl, std::chrono::milliseconds(g_window_ms), [] { return g_quit.load(); });
+  wl.unlock();
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (size_t i = 0; i < g_agents.size(); ++i) {
+    Agent* a = g_agents[i];
+    if (!a || !a->ready || a->broken || t0[i] == Clock::time_point{}) continue;
+    // The read packet copies the counters to the output buffer (measured: the stop packet
+    // alone leaves it untouched); stop then disables counting until the next window.
+    const auto t1 = run_packet(*a, a->read_pkt);
+    if (t1 == Clock::time_point{} || run_packet(*a, a->stop_pkt) == Clock::time_point{}) {
+      a->broken = true;
+      continue;
+    }
+    Accum acc{a, {}, {}, 0};
+    if (g_aql.hsa_ven_amd_aqlprofile_iterate_data(&a->profile, on_data, &acc) != HSA_STATUS_SUCCESS) continue;
+    const double wall = std::chrono::duration<double>(t1 - t0[i]).count();
+    std::memcpy(a->last_raw, acc.v, sizeof(acc.v));
+    std::memcpy(a->last_inst, acc.inst, sizeof(acc.inst));
+    a->last_samples = acc.samples;
+    if (wall > 0) derive(a->m, acc.v, acc.inst, wall);
+  }
+}
+
+void counting_loop() {
+  while (!g_quit.load()) {
+    const auto begin = Clock::now();
+    window_all();
+    const auto spent = std::chrono::duration_cast<std::chrono::milliseconds>(Clock::now() - begin).count();
+    std::unique_lock<std::mutex> lk(g_cv_mu);
+    g_cv.wait_for(lk, std::chrono::milliseconds(std::max<long long>(0, g_interval_ms - spent)),
+                  [] { return g_quit.load(); });
+  }
+}
+
+void teardown_locked() {
+  for (Agent* a : g_agents) {
+    if (!a) continue;
+    if (a->queue) hsa_queue_destroy(a->queue);
+    if (a->sig.handle) hsa_signal_destroy(a->sig);
+    // A timed-out packet may still write the buffers: leak them rather than free.
+    if (!a->broken) {
+      if (a->cmd_buf) hsa_amd_memory_pool_free(a->cmd_buf);
+      if (a->out_buf) hsa_amd_memory_pool_free(a->out_buf);
+    }
+    delete a;
+  }
+  g_agents.clear();
+  if (g_hsa_up) hsa_shut_down();
+  g_hsa_up = false;
+}
+
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) void gpuexp_rp_set_duty(int window_ms, int interval_ms) {
+  g_window_ms = std::max(1, window_ms);
+  g_interval_ms = std::max(g_window_ms, interval_ms);
+}
+
+extern "C" __attribute__((visibility("default"))) int gpuexp_rp_init(int ndev, const char* const* bdfs, char* err,
+                                                                     int errlen) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto fail = [&](const std::string& m) {
+    std::snprintf(err, size_t(errlen), "%s", m.c_str());
+    g_status = "unavailable: " + m;
+    return 0;
+  };
+  if (g_hsa_up) return fail("already initialised");
+  g_debug = std::getenv("GPUEXP_AQLPMC_DEBUG") != nullptr;
+  if (g_debug) ::signal(SIGSEGV, segv_backtrace);
+
+  if (hsa_init() != HSA_STATUS_SUCCESS) return fail("hsa_init failed");
+  g_hsa_up = true;
+  crumb("hsa_init ok");
+  if (hsa_system_get_major_extension_table(HSA_EXTENSION_AMD_AQLPROFILE, hsa_ven_amd_aqlprofile_VERSION_MAJOR,
+                                           sizeof(g_aql), &g_aql) != HSA_STATUS_SUCCESS ||
+      !g_aql.hsa_ven_amd_aqlprofile_start) {
+    teardown_locked();
+    return fail("HSA runtime did not provide the aqlprofile extension table");
+  }
+  crumb("aqlprofile table ok");
+  hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &g_ts_freq);
+  Found f;
+  hsa_iterate_agents(collect_agent, &f);
+  for (auto cpu : f.cpus) {
+    hsa_amd_agent_iterate_memory_pools(cpu, pick_sys_pool, nullptr);
+    if (g_have_pool) break;
+  }
+  if (!g_have_pool) {
+    teardown_locked();
+    return fail("no fine-grained system memory pool");
+  }
+  g_agents.assign(size_t(std::max(0, ndev)), nullptr);
+  int ok = 0;
+  std::string why;
+  for (int d = 0; d < ndev; ++d) {
+    for (const auto& g : f.gpus) {
+      if (lower(bdfs[d]) != g.second) continue;
+      auto* a = new Agent;
+      a->dev = d;
+      a->gpu = g.first;
+      a->bdf = g.second;
+      g_agents[size_t(d)] = a;
+      if (setup_agent(*a, &why)) ++ok;
+      break;
+    }
+  }
+  if (!ok) {
+    teardown_locked();
+    return fail(why.empty() ? "no HSA GPU agent matched the exporter's GPUs" : why);
+  }
+  g_quit.store(false);
+  g_thread = std::thread(counting_loop);
+  g_status = "aqlprofile PMC on " + std::to_string(ok) + " GPU(s), " + std::to_string(g_window_ms) +
+             " ms window every " + std::to_string(g_interval_ms) + " ms";
+  return ok;
+}
+
+extern "C" __attribute__((visibility("default"))) int gpuexp_rp_sample(int dev, double, double* out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (dev < 0 || size_t(dev) >= g_agents.size() || !g_agents[size_t(dev)]) return -1;
+  const Agent& a = *g_agents[size_t(dev)];
+  if (!a.m.valid || a.broken) return -1;
+  std::memcpy(out, a.m.latest, sizeof(a.m.latest));
+  return 0;
+}
+
+extern "C" __attribute__((visibility("default"))) void gpuexp_rp_shutdown() {
+  g_quit.store(true);
+  g_cv.notify_all();
+  if (g_thread.joinable()) g_thread.join();
+  std::lock_guard<std::mutex> lk(g_mu);
+  teardown_locked();
+  g_status = "shut down";
+}
+
+extern "C" __attribute__((visibility("default"))) const char* gpuexp_rp_status() { return g_status.c_str(); }
+
+extern "C" __attribute__((visibility("default"))) int gpuexp_rp_scope(int dev) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (dev < 0 || size_t(dev) >= g_agents.size() || !g_agents[size_t(dev)]) return -1;
+  return g_agents[size_t(dev)]->m.scope;
+}
+
+// Diagnostics: the reduced value and instance count of every counter in the last window,
+// as "NAME=value/instances;..." (used by tools/gpu_features_check.py).
+extern "C" __attribute__((visibility("default"))) int gpuexp_rp_debug(int dev, char* buf, int len) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (dev < 0 || size_t(dev) >= g_agents.size() || !g_agents[size_t(dev)]) return -1;
+  const Agent& a = *g_agents[size_t(dev)];
+  std::string s = "backend=aqlprofile;events=" + std::to_string(a.events.size()) +
+                  ";samples=" + std::to_string(a.last_samples) + ";windows=" + std::to_string(a.m.windows) +
+                  ";simd=" + std::to_string(a.m.simd) + ";cu=" + std::to_string(a.m.cu) + ";";
+  for (int k = 0; k < kNumCtr; ++k) {
+    char t[128];
+    std::snprintf(t, sizeof(t), "%s=%.0f/%d;", name(k), a.last_raw[k], a.last_inst[k]);
+    s += t;
+  }
+  std::snprintf(buf, size_t(len), "%s", s.c_str());
+  return 0;
+}

@@ -85,7 +85,8 @@ class PluginCounters : public CounterSource {
   void stop() override {
     if (started_ && shutdown_) shutdown_();
     started_ = false;
-    // The plugin stays loaded: rocprofiler-sdk does not support re-registration.
+    // The plugin stays loaded: rocprofiler-sdk does not support re-registration, and the
+    // aqlprofile plugin keeps HSA's refcount balanced itself.
   }
 
   std::string status() const override {
@@ -231,7 +232,9 @@ std::unique_ptr<SentinelSource> make_hip_sentinel(int ring_slots, int spin_iters
   return std::unique_ptr<SentinelSource>(f(ring_slots, spin_iters));
 }
 
-std::string default_rocprof_plugin() { return self_dir() + "/_gpuexp_rocprof.so"; }
+// Default counter backend: the aqlprofile plugin (no spinning runtime thread); the
+// rocprofiler-sdk plugin (_gpuexp_rocprof.so) is selectable through counters_plugin.
+std::string default_rocprof_plugin() { return self_dir() + "/_gpuexp_aqlpmc.so"; }
 
 std::unique_ptr<CounterSource> make_rocprof_counters(const std::string& plugin_path, int window_ms,
                                                      int interval_ms) {

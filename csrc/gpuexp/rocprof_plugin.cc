@@ -17,9 +17,19 @@
 // runtime loads in this process, so the engine starts counters before the HIP sentinel.
 // Any failure (non-root, PMCs owned by another profiler) leaves the engine without
 // counter series; the other sources are unaffected.
+//
+// Measured cost (MI355X, ROCm 7.2): once this tool is registered and HSA is up, one HSA
+// runtime thread (the async-signal loop: ioctl AMDKFD_IOC_WAIT_EVENTS returning at once,
+// libhsa-runtime64 +0x13f7e7 <- +0x1357e4 <- +0x8b53a) spins a core at 100% whether or
+// not a context is started — rocprofiler's agent completion handler waits on a signal with
+// no interrupt event.  The default counter backend is therefore _gpuexp_aqlpmc.so
+// (aql_pmc.cc), which submits the same PM4 packets on its own queue; this plugin stays
+// selectable (counters_plugin=.../_gpuexp_rocprof.so) as the cross-check.
 #include <hsa/hsa.h>
 #include <rocprofiler-sdk/registration.h>
 #include <rocprofiler-sdk/rocprofiler.h>
+
+#include "gpuexp/counter_model.h"
 
 #include <algorithm>
 #include <atomic>
@@ -37,26 +47,7 @@
 
 namespace {
 
-enum Ctr {
-  kMfma = 0,
-  kSqBusy,
-  kWaves,
-  kLdsActive,
-  kLdsConflict,
-  kGuiActive,
-  kGrbmCount,
-  kTccBubble,
-  kRdReq,
-  kWrReq,
-  kWrReq64,
-  kNumCtr
-};
-const char* kNames[kNumCtr] = {"SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAVES",
-                               "SQ_LDS_IDX_ACTIVE",        "SQ_LDS_BANK_CONFLICT", "GRBM_GUI_ACTIVE",
-                               "GRBM_COUNT",               "TCC_BUBBLE",      "TCC_EA0_RDREQ",
-                               "TCC_EA0_WRREQ",            "TCC_EA0_WRREQ_64B"};
-// GRBM counters are per-XCC copies of one clock: reduce with max; everything else sums.
-bool use_max(int c) { return c == kGuiActive || c == kGrbmCount; }
+using namespace gpuexp_ctr;
 
 struct Agent {
   rocprofiler_agent_id_t id{};
@@ -68,16 +59,10 @@ struct Agent {
   bool started = false;
   std::map<uint64_t, int> counter_slot;  // counter id handle -> Ctr
   std::vector<rocprofiler_counter_record_t> recs;
-  double prev[kNumCtr] = {};
   double last_raw[kNumCtr] = {};
   int last_inst[kNumCtr] = {};
   size_t last_nrec = 0;
-  int scope = -1;  // -1 unknown, 0 wave/EA counters VMID-filtered to this process, 1 device-wide
-  double latest[8] = {};
-  bool latest_valid = false;
-  uint64_t windows = 0;
-  bool have_prev = false;
-  std::chrono::steady_clock::time_point prev_t;
+  Derived m;
 };
 
 std::mutex g_mu;
@@ -128,8 +113,8 @@ int tool_init(rocprofiler_client_finalize_t fini, void*) {
       Agent& ag = g_agents[d];
       ag.id = a.id;
       ag.dev = int(d);
-      ag.simd = a.simd_count;
-      ag.cu = a.cu_count ? a.cu_count : (a.simd_per_cu ? a.simd_count / a.simd_per_cu : 0);
+      ag.m.simd = a.simd_count;
+      ag.m.cu = a.cu_count ? a.cu_count : (a.simd_per_cu ? a.simd_count / a.simd_per_cu : 0);
       if (rocprofiler_create_context(&ag.ctx) != ROCPROFILER_STATUS_SUCCESS) continue;
       rocprofiler_buffer_id_t nobuf{};  // values come back in the sample call itself
       if (rocprofiler_configure_device_counting_service(ag.ctx, nobuf, a.id, set_profile_cb, &ag) !=
@@ -172,7 +157,7 @@ bool build_config(Agent& a, std::string* why) {
     if (rocprofiler_query_counter_info(c, ROCPROFILER_COUNTER_INFO_VERSION_0, &info) != ROCPROFILER_STATUS_SUCCESS)
       continue;
     for (int k = 0; k < kNumCtr; ++k)
-      if (info.name && std::strcmp(info.name, kNames[k]) == 0) {
+      if (info.name && std::strcmp(info.name, name(k)) == 0) {
         use.push_back(c);
         a.counter_slot[c.handle] = k;
       }
@@ -235,30 +220,6 @@ bool read_counts(Agent& a, double* v, int* inst) {
   return true;
 }
 
-void derive(Agent& a, const double* d, double wall) {
-  const double nan = std::nan("");
-  double gui = d[kGuiActive];
-  // Scope detection.  As a non-root client (perf_event_paranoid=3 on the test pool) the
-  // wave-level SQ counters and the TCC EA requests are VMID-filtered to THIS process,
-  // while SQ_VALU_MFMA_BUSY_CYCLES and GRBM are chip-global (measured against rocprofv3
-  // dispatch counts: profiles/r01/pmc_gemm_dispatch.txt).  A busy GPU on which the
-  // exporter sees almost no waves means the filtered set must not be exported as device
-  // totals.
-  if (d[kGrbmCount] > 0 && gui / d[kGrbmCount] > 0.5 && d[kMfma] > 0) a.scope = d[kWaves] / wall < 1000.0 ? 0 : 1;
-  double* out = a.latest;
-  out[0] = gui > 0 && a.simd ? 100.0 * d[kMfma] / (gui * a.simd) : nan;              // MfmaUtil
-  double se = a.last_inst[kSqBusy] > 0 ? a.last_inst[kSqBusy] : 1;                     // one per SE
-  out[1] = gui > 0 ? std::min(100.0, 100.0 * d[kSqBusy] / (gui * se)) : nan;
-  out[2] = d[kGrbmCount] > 0 ? 100.0 * gui / d[kGrbmCount] : nan;                     // GPU busy
-  out[3] = d[kWaves] / wall;                                                          // waves/s
-  out[4] = gui > 0 && a.cu ? 100.0 * d[kLdsActive] / (gui * a.cu) : nan;             // LDS util
-  out[5] = d[kLdsActive] > 0 ? 100.0 * d[kLdsConflict] / d[kLdsActive] : 0.0;        // bank conflicts
-  out[6] = (d[kTccBubble] * 128.0 + (d[kRdReq] - d[kTccBubble]) * 64.0) / wall;     // FETCH_SIZE bytes/s
-  out[7] = ((d[kWrReq] - d[kWrReq64]) * 32.0 + d[kWrReq64] * 64.0) / wall;          // WRITE_SIZE bytes/s
-  a.latest_valid = true;
-  a.windows += 1;
-}
-
 void counting_loop() {
   while (!g_quit.load()) {
     double base[16][kNumCtr];
@@ -290,7 +251,7 @@ void counting_loop() {
             if (d[k] < 0) sane = false;
           }
           std::memcpy(a.last_raw, d, sizeof(d));
-          if (sane) derive(a, d, wall);
+          if (sane) derive(a.m, d, a.last_inst, wall);
         }
         rocprofiler_stop_context(a.ctx);
         a.started = false;
@@ -351,8 +312,8 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_sample(int dev, 
   std::lock_guard<std::mutex> lk(g_mu);
   if (dev < 0 || size_t(dev) >= g_agents.size()) return -1;
   Agent& a = g_agents[size_t(dev)];
-  if (!a.latest_valid) return -1;
-  std::memcpy(out, a.latest, sizeof(a.latest));
+  if (!a.m.valid) return -1;
+  std::memcpy(out, a.m.latest, sizeof(a.m.latest));
   (void)dt_s;
   return 0;
 }
@@ -374,7 +335,7 @@ extern "C" __attribute__((visibility("default"))) const char* gpuexp_rp_status()
 extern "C" __attribute__((visibility("default"))) int gpuexp_rp_scope(int dev) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (dev < 0 || size_t(dev) >= g_agents.size()) return -1;
-  return g_agents[size_t(dev)].scope;
+  return g_agents[size_t(dev)].m.scope;
 }
 
 // Diagnostics: the raw (cumulative) reduced value and instance count of every counter in
@@ -383,11 +344,11 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_debug(int dev, c
   std::lock_guard<std::mutex> lk(g_mu);
   if (dev < 0 || size_t(dev) >= g_agents.size()) return -1;
   const Agent& a = g_agents[size_t(dev)];
-  std::string s = "records=" + std::to_string(a.last_nrec) + ";simd=" + std::to_string(a.simd) +
-                  ";cu=" + std::to_string(a.cu) + ";";
+  std::string s = "records=" + std::to_string(a.last_nrec) + ";simd=" + std::to_string(a.m.simd) +
+                  ";cu=" + std::to_string(a.m.cu) + ";";
   for (int k = 0; k < kNumCtr; ++k) {
     char t[128];
-    std::snprintf(t, sizeof(t), "%s=%.0f/%d;", kNames[k], a.last_raw[k], a.last_inst[k]);
+    std::snprintf(t, sizeof(t), "%s=%.0f/%d;", name(k), a.last_raw[k], a.last_inst[k]);
     s += t;
   }
   std::snprintf(buf, size_t(len), "%s", s.c_str());

@@ -34,8 +34,10 @@ def load():
     return _mod
 
 
-def rocprof_plugin_path() -> str:
-    return str(PKG_DIR / "_gpuexp_rocprof.so")
+def rocprof_plugin_path(kind: str = "aqlpmc") -> str:
+    """Counter plugin: "aqlpmc" (default, aqlprofile on an owned queue) or "rocprof"
+    (rocprofiler-sdk device counting; costs a spinning runtime thread, see rocprof_plugin.cc)."""
+    return str(PKG_DIR / ("_gpuexp_aqlpmc.so" if kind == "aqlpmc" else "_gpuexp_rocprof.so"))
 
 
 def rccl_tracer_path() -> str:

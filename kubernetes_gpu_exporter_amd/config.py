@@ -39,7 +39,7 @@ class Config:
     enable_sentinel: bool = False
     sentinel_spin: int = 500
     enable_counters: bool = False
-    counters_plugin: str = ""
+    counters_plugin: str = "aqlpmc"        # aqlpmc | rocprof | /path/to/plugin.so
     counters_window_ms: int = 20           # rocprofiler counting window ...
     counters_interval_ms: int = 1000       # ... per interval (context-started spin is duty-cycled)
     enable_rccl: bool = False
@@ -98,11 +98,11 @@ class Config:
         ec.enable_sentinel = bool(self.enable_sentinel)
         ec.sentinel_spin = int(self.sentinel_spin)
         ec.enable_counters = bool(self.enable_counters)
-        if self.counters_plugin:
-            ec.counters_plugin = self.counters_plugin
-        else:
+        if self.counters_plugin in ("", "aqlpmc", "rocprof"):
             from ._native import rocprof_plugin_path
-            ec.counters_plugin = rocprof_plugin_path()
+            ec.counters_plugin = rocprof_plugin_path(self.counters_plugin or "aqlpmc")
+        else:
+            ec.counters_plugin = self.counters_plugin
         ec.counters_window_ms = int(self.counters_window_ms)
         ec.counters_interval_ms = int(self.counters_interval_ms)
         ec.enable_rccl = bool(self.enable_rccl)

@@ -1,11 +1,13 @@
 """GPU-box checks that need a clean process (run as subprocesses by tests/test_gpu.py).
 
-  counters : exporter engine with the rocprofiler-sdk device-counting plugin while a GEMM
-             child keeps the GPU busy; prints the counter series as JSON.  This process
-             must not load HSA before the plugin registers, so it never imports torch.
+  counters : exporter engine with a device-counter plugin (PLUGIN=aqlpmc|rocprof) while a
+             GEMM child keeps the GPU busy; prints the counter series, per-thread CPU and
+             the plugin's raw readings as JSON.  Never imports torch (the rocprofiler plugin
+             must register before HSA loads).
   rccl     : a torch.distributed (RCCL, world_size 1) child with the RCCL tracer injected
              via ROCP_TOOL_LIBRARIES; prints the per-op counters from its shm file.
 """
+import ctypes
 import json
 import os
 import socket
@@ -34,10 +36,13 @@ def counters(seconds: float) -> dict:
     c.interval_s = 0.1
     c.serve_http = False
     c.enable_counters = True
-    c.counters_plugin = n.default_rocprof_plugin()
+    from kubernetes_gpu_exporter_amd._native import rocprof_plugin_path
+    plugin = rocprof_plugin_path(os.environ.get("PLUGIN", "aqlpmc"))
+    c.counters_plugin = plugin
     c.counters_window_ms = int(os.environ.get("WINDOW_MS", "20"))
     c.counters_interval_ms = int(os.environ.get("INTERVAL_MS", "500"))
-    c.enable_sentinel = True
+    c.enable_sentinel = os.environ.get("SENTINEL", "1") == "1"
+    c.enable_counters = os.environ.get("COUNTERS", "1") == "1"
     c.device_filter = [0]
     e = n.Engine(c)
     e.start()
@@ -48,23 +53,34 @@ def counters(seconds: float) -> dict:
     cpu1 = thread_cpu_seconds(os.getpid())
     hot = sorted(((cpu1[k] - cpu0.get(k, 0.0)) / seconds * 100, k) for k in cpu1)[-6:]
     print("per-thread CPU% over the window:", [(round(p, 1), k) for p, k in hot], flush=True)
+    tid = hot[-1][1].split(":")[-1]
+    for _ in range(2):  # what is the hottest thread doing? (syscall nr 24 = sched_yield)
+        try:
+            sc = open(f"/proc/self/task/{tid}/syscall").read().split()[0]
+            wc = open(f"/proc/self/task/{tid}/wchan").read()
+            print(f"hot thread {tid}: syscall={sc} wchan={wc}", flush=True)
+        except OSError as ex:
+            print("hot thread probe failed", ex)
+        time.sleep(0.05)
     text = e.snapshot_text()
     status = e.source_status()
-    import ctypes
+
     dbg = ctypes.create_string_buffer(4096)
     try:
-        ctypes.CDLL(n.default_rocprof_plugin()).gpuexp_rp_debug(0, dbg, 4096)
+        ctypes.CDLL(plugin).gpuexp_rp_debug(0, dbg, 4096)
     except OSError:
         pass
     e.stop()
     fams = promtext.parse(text)
-    out = {"status": status, "raw_counters": dbg.value.decode()}
+    out = {"status": status, "raw_counters": dbg.value.decode(), "hot_threads": [(round(p, 1), k) for p, k in hot]}
     for name in ("amd_gpu_mfma_busy_percent", "amd_gpu_sq_busy_percent", "amd_gpu_gui_active_percent",
                  "amd_gpu_waves_per_second", "amd_gpu_lds_active_percent", "amd_gpu_lds_bank_conflict_percent",
                  "amd_gpu_hbm_read_bytes_per_second", "amd_gpu_hbm_write_bytes_per_second",
                  "amd_gpu_gfx_activity_percent", "amd_gpu_sentinel_sclk_hz"):
         v = promtext.samples(fams, name)
         out[name] = v[0][2] if v else None
+    sc = promtext.samples(fams, "gpuexp_counters_device_scope")
+    out["device_scope"] = sc[0][2] if sc else None
     per_gpu = 0
     for name, fam in fams.items():
         if name.startswith("amd_gpu_") and not name.startswith("amd_gpu_process_"):
