@@ -4,7 +4,7 @@
 
 One rank per GPU (torchrun for N>1).  Rank 0 starts the exporter as a separate process
 BEFORE touching the GPU (amdsmi backend, raw gpu_metrics fast path, HIP sentinel,
-10 Hz sampling, every GPU of the job), then every rank becomes a synthetic "GEMM pod":
+aqlprofile device counters, full series profile, 10 Hz sampling, every GPU of the job), then every rank becomes a synthetic "GEMM pod":
 each step it launches a burst of bf16 MFMA GEMMs (our HIP kernel) and, for N>1, an RCCL
 all-reduce (DP gradient traffic over xGMI).  Rank 0 scrapes /metrics once per step over a
 persistent keep-alive connection with the native client while the GPUs are busy; steps
@@ -99,14 +99,15 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--scrape-hz", type=float, default=10.0)
     ap.add_argument("--sample-hz", type=float, default=10.0)
-    ap.add_argument("--series-profile", default="standard")
+    ap.add_argument("--series-profile", default="full",
+                    help="full (default: >= 64 series/GPU incl. counters + reliability) | standard | compact")
     ap.add_argument("--backend", default="auto", help="auto | amdsmi | sysfs | mock")
     ap.add_argument("--gemm", type=int, default=8192, help="GEMM edge (M=N=K) of the synthetic pod")
     ap.add_argument("--busy", type=float, default=0.6, help="target GPU-busy fraction of each step")
     ap.add_argument("--allreduce-mb", type=float, default=64.0)
     ap.add_argument("--gzip", action="store_true", help="scrape with Accept-Encoding: gzip")
     ap.add_argument("--sentinel", type=int, default=1)
-    ap.add_argument("--counters", type=int, default=0)
+    ap.add_argument("--counters", type=int, default=1, help="device PMC counters (aqlprofile plugin)")
     ap.add_argument("--out", default="")
     ap.add_argument("--exporter", choices=("native", "both"), default="native",
                     help="'both' also measures the reference-architecture exporter (utils/refstyle.py)")
@@ -293,7 +294,7 @@ def main() -> int:
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic",
-            "config": {"model": "mi355x-per-pod-exporter (standard profile) + bf16 MFMA GEMM pods",
+            "config": {"model": f"mi355x-per-pod-exporter ({args.series_profile} profile) + bf16 MFMA GEMM pods",
                        "global_batch": n_gpus, "seq_len": 0, "parallelism": f"dp{n_gpus}",
                        "scrape_hz": args.scrape_hz, "sample_hz": args.sample_hz, "backend": backend,
                        "series_profile": args.series_profile, "gzip": args.gzip,

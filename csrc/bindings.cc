@@ -11,6 +11,7 @@
 #include "gpuexp/exposition.h"
 #include "gpuexp/gpu_metrics.h"
 #include "gpuexp/procs.h"
+#include "gpuexp/ras.h"
 #include "gpuexp/snapshot.h"
 
 namespace py = pybind11;
@@ -137,6 +138,17 @@ PYBIND11_MODULE(_gpuexp, m) {
   });
   m.def("gpu_metrics_v1_8_size", []() { return sizeof(GpuMetricsV1_8); });
   m.def("uuid_from_unique_id", &SysfsBackend::uuid_from_unique_id);
+  m.def("parse_ras_err_count", [](const std::string& body) {
+    RasTotals t;
+    bool ok = parse_ras_err_count(body, &t);
+    py::dict d;
+    d["ok"] = ok;
+    d["ce"] = t.ecc_ce;
+    d["ue"] = t.ecc_ue;
+    d["de"] = t.ecc_de;
+    return d;
+  });
+  m.def("parse_aer_total", &parse_aer_total);
   m.def("read_backend", [](const std::string& backend, const std::string& host_root, int ndev) {
     // One-shot enumerate + sample (diagnostics / tests).
     std::unique_ptr<Backend> b;
@@ -279,6 +291,7 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("serve_http", &EngineConfig::serve_http)
       .def_readwrite("http", &EngineConfig::http)
       .def_readwrite("series_profile", &EngineConfig::series_profile)
+      .def_readwrite("ras_interval_s", &EngineConfig::ras_interval_s)
       .def_readwrite("legacy_families", &EngineConfig::legacy_families)
       .def_readwrite("pod_attribution", &EngineConfig::pod_attribution)
       .def_readwrite("infer_device_owner", &EngineConfig::infer_device_owner)

@@ -72,6 +72,11 @@ void from_amdsmi_metrics(const amdsmi_gpu_metrics_t& m, DeviceSample* out) {
   out->pcie_bw_acc = m.pcie_bandwidth_acc;
   out->pcie_bw_inst = m.pcie_bandwidth_inst == ~0ull ? kNaN : double(m.pcie_bandwidth_inst);
   out->pcie_replay = m.pcie_replay_count_acc == ~0ull ? kNaN : double(m.pcie_replay_count_acc);
+  out->pcie_nak_sent = m.pcie_nak_sent_count_acc == 0xFFFFFFFFu ? kNaN : double(m.pcie_nak_sent_count_acc);
+  out->pcie_nak_rcvd = m.pcie_nak_rcvd_count_acc == 0xFFFFFFFFu ? kNaN : double(m.pcie_nak_rcvd_count_acc);
+  out->pcie_l0_recov = m.pcie_l0_to_recov_count_acc == ~0ull ? kNaN : double(m.pcie_l0_to_recov_count_acc);
+  out->xgmi_width = u16v(m.xgmi_link_width);
+  out->xgmi_speed = u16v(m.xgmi_link_speed);
   out->residency_valid = m.accumulation_counter != ~0ull;
   out->accumulation_counter = m.accumulation_counter;
   out->res_ppt = m.ppt_residency_acc;

@@ -82,6 +82,16 @@ void MockBackend::sample(const DeviceInfo& dev, DeviceSample* out) {
   out->pcie_speed_gts = 32;
   out->pcie_bw_inst = get(s, "pcie_bw_gbs", 18);
   out->pcie_replay = 0;
+  out->pcie_nak_sent = get(s, "pcie_nak_sent", 0);
+  out->pcie_nak_rcvd = get(s, "pcie_nak_rcvd", 0);
+  out->pcie_l0_recov = get(s, "pcie_l0_recov", 0);
+  out->xgmi_width = 16;
+  out->xgmi_speed = 32;
+  out->ecc_ce = get(s, "ecc_ce", 0);
+  out->ecc_ue = get(s, "ecc_ue", 0);
+  out->aer_cor = get(s, "aer_cor", 0);
+  out->aer_nonfatal = get(s, "aer_nonfatal", 0);
+  out->aer_fatal = get(s, "aer_fatal", 0);
   out->vram_max_bw_gbs = 8192;
 
   // Integrate accumulators with the scripted rates.

@@ -73,6 +73,13 @@ struct DeviceSample {
   uint64_t pcie_bw_acc = 0;         // GB/s accumulated
   double pcie_replay = kNaN;        // count
   double pcie_width = kNaN, pcie_speed_gts = kNaN;
+  // link reliability (gpu_metrics v1.8 accumulators; NaN unsupported)
+  double pcie_nak_sent = kNaN, pcie_nak_rcvd = kNaN, pcie_l0_recov = kNaN;
+  double xgmi_width = kNaN, xgmi_speed = kNaN;  // lanes, Gb/s per lane (PMFW units)
+
+  // RAS / AER error totals (sysfs ras/*_err_count and aer_dev_*; refreshed at a low rate)
+  double ecc_ce = kNaN, ecc_ue = kNaN, ecc_de = kNaN;
+  double aer_cor = kNaN, aer_nonfatal = kNaN, aer_fatal = kNaN;
 
   // throttle residency accumulators (same units as accumulation_counter)
   bool residency_valid = false;

@@ -152,6 +152,15 @@ void Engine::define_families() {
                with(D, {"reason"}));
   f_nprocs_ = add("amd_gpu_processes", "Processes with a KFD context on this GPU", G, D);
   f_cu_occ_ = add("amd_gpu_cu_occupancy", "CUs occupied by all processes on this GPU", G, D);
+  // --- full profile: link / memory reliability (error totals; not part of the 64-series load) ---
+  f_ecc_ = add("amd_gpu_ecc_errors_total", "RAS ECC error count summed over IP blocks (sysfs ras/*_err_count)", C,
+               with(D, {"type"}));
+  f_aer_ = add("amd_gpu_pcie_aer_errors_total", "PCIe AER errors reported for the GPU function", C,
+               with(D, {"severity"}));
+  f_pcie_nak_ = add("amd_gpu_pcie_nak_total", "PCIe NAKs (PMFW accumulator)", C, with(D, {"direction"}));
+  f_pcie_recov_ = add("amd_gpu_pcie_recovery_total", "PCIe L0 -> recovery transitions (PMFW accumulator)", C, D);
+  f_xgmi_width_ = add("amd_gpu_xgmi_link_width", "xGMI link width (PMFW)", G, D);
+  f_xgmi_speed_ = add("amd_gpu_xgmi_link_speed", "xGMI link speed (PMFW units)", G, D);
   f_mfma_ = add("amd_gpu_mfma_busy_percent", "MFMA (matrix core) busy: SQ_VALU_MFMA_BUSY_CYCLES per SIMD", G, D);
   f_sq_busy_ = add("amd_gpu_sq_busy_percent", "Shader sequencer busy (SQ_BUSY_CYCLES)", G, D);
   f_gui_ = add("amd_gpu_gui_active_percent", "Graphics pipe active (GRBM_GUI_ACTIVE / GRBM_COUNT)", G, D);
@@ -238,6 +247,19 @@ bool Engine::start(std::string* err) {
     devices_ = all;
   }
   dstate_.assign(devices_.size(), DevState());
+  if (cfg_.series_profile == "full" && cfg_.backend != "mock") {
+    const std::string root = cfg_.host_root.empty() ? "" : cfg_.host_root;
+    ras_.resize(devices_.size());
+    for (size_t i = 0; i < devices_.size(); ++i) {
+      const DeviceInfo& di = devices_[i];
+      if (di.render_minor >= 0)
+        ras_[i].open(root + "/sys/class/drm/renderD" + std::to_string(di.render_minor) + "/device");
+      else if (!di.bdf.empty())
+        ras_[i].open(root + "/sys/bus/pci/devices/" + di.bdf);
+    }
+    ras_cache_.assign(devices_.size(), RasTotals());
+    ras_next_ns_.assign(devices_.size(), 0);
+  }
   int nthreads = cfg_.device_threads;
   if (nthreads <= 0) nthreads = cfg_.backend == "mock" ? 1 : std::min<int>(int(devices_.size()), 8);
   if (nthreads > 1) pool_ = std::make_unique<ForkJoinPool>(nthreads);
@@ -495,6 +517,21 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
   dput(st, i, st.pcie_replay, f_pcie_replay_, {}, c.pcie_replay, gen);
   dput(st, i, st.pcie_speed, f_pcie_speed_, {}, c.pcie_speed_gts, gen);
   dput(st, i, st.pcie_width, f_pcie_width_, {}, c.pcie_width, gen);
+  if (cfg_.series_profile == "full") {
+    static const char* kEcc[3] = {"correctable", "uncorrectable", "deferred"};
+    static const char* kAer[3] = {"correctable", "nonfatal", "fatal"};
+    const double ecc[3] = {c.ecc_ce, c.ecc_ue, c.ecc_de};
+    const double aer[3] = {c.aer_cor, c.aer_nonfatal, c.aer_fatal};
+    for (int k = 0; k < 3; ++k) {
+      dput(st, i, st.ecc[k], f_ecc_, {kEcc[k]}, ecc[k], gen);
+      dput(st, i, st.aer[k], f_aer_, {kAer[k]}, aer[k], gen);
+    }
+    dput(st, i, st.nak[0], f_pcie_nak_, {"sent"}, c.pcie_nak_sent, gen);
+    dput(st, i, st.nak[1], f_pcie_nak_, {"received"}, c.pcie_nak_rcvd, gen);
+    dput(st, i, st.recov, f_pcie_recov_, {}, c.pcie_l0_recov, gen);
+    dput(st, i, st.xgmi_w, f_xgmi_width_, {}, c.xgmi_width, gen);
+    dput(st, i, st.xgmi_s, f_xgmi_speed_, {}, c.xgmi_speed, gen);
+  }
 
   if (have_prev && c.residency_valid && p.residency_valid) {
     double dacc;
@@ -766,6 +803,19 @@ void Engine::tick_locked(uint64_t now) {
     st.cur = DeviceSample();
     st.cur.host_ns = now;
     backend_->sample(devices_[size_t(i)], &st.cur);
+    if (!ras_.empty()) {
+      if (now >= ras_next_ns_[size_t(i)]) {
+        ras_[size_t(i)].read(&ras_cache_[size_t(i)]);
+        ras_next_ns_[size_t(i)] = now + uint64_t(cfg_.ras_interval_s * 1e9);
+      }
+      const RasTotals& r = ras_cache_[size_t(i)];
+      st.cur.ecc_ce = r.ecc_ce;
+      st.cur.ecc_ue = r.ecc_ue;
+      st.cur.ecc_de = r.ecc_de;
+      st.cur.aer_cor = r.aer_cor;
+      st.cur.aer_nonfatal = r.aer_nonfatal;
+      st.cur.aer_fatal = r.aer_fatal;
+    }
   };
   if (pool_) {
     pool_->run(int(devices_.size()), sample_one);

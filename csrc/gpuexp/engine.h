@@ -24,6 +24,7 @@
 #include "gpuexp/exposition.h"
 #include "gpuexp/http.h"
 #include "gpuexp/procs.h"
+#include "gpuexp/ras.h"
 #include "gpuexp/snapshot.h"
 #include "gpuexp/sources.h"
 
@@ -61,7 +62,8 @@ struct EngineConfig {
   double interval_s = 1.0;             // 0 = manual ticks only (tests)
   bool serve_http = true;
   HttpConfig http;
-  std::string series_profile = "standard";  // standard | compact | legacy
+  std::string series_profile = "standard";  // standard | full | compact | legacy
+  double ras_interval_s = 10.0;        // full profile: RAS/AER sysfs re-read period
   bool legacy_families = true;         // pod_gpu_memory_usage / docker_gpu_memory_perc_usage
   bool pod_attribution = true;
   bool infer_device_owner = true;      // single-pod GPU -> device series carry the pod
@@ -153,7 +155,7 @@ class Engine {
     SeriesRef info, up, gfx, umc, xcc[kMaxXcc], vram_used, vram_total, hbm_bw, power, power_cap,
         energy, temp[9], clk[3], xrd[kMaxXgmiLinks], xwr[kMaxXgmiLinks], xrd_rate, xwr_rate,
         links_up, pcie_bw, pcie_replay, pcie_speed, pcie_width, thr[5], nprocs, cu_occ, ctr[8],
-        sen[4];
+        sen[4], ecc[3], aer[3], nak[2], recov, xgmi_w, xgmi_s;
     uint64_t errors = 0;
     SeriesRef err_ref;
   };
@@ -182,6 +184,10 @@ class Engine {
   std::unique_ptr<CounterSource> counters_;
   std::unique_ptr<RcclSource> rccl_;
   std::unique_ptr<ForkJoinPool> pool_;
+  // full profile, real backends: RAS/AER readers + last totals (re-read every ras_interval_s)
+  std::vector<RasReader> ras_;
+  std::vector<RasTotals> ras_cache_;
+  std::vector<uint64_t> ras_next_ns_;
   std::string sentinel_status_ = "disabled", counters_status_ = "disabled";
 
   SeriesTable table_;
@@ -222,7 +228,7 @@ class Engine {
   int f_info_, f_up_, f_gfx_, f_umc_, f_xcc_, f_vram_used_, f_vram_total_, f_hbm_bw_, f_power_,
       f_power_cap_, f_energy_, f_temp_, f_clk_, f_xrd_, f_xwr_, f_xrd_rate_, f_xwr_rate_,
       f_links_up_, f_pcie_bw_, f_pcie_replay_, f_pcie_speed_, f_pcie_width_, f_thr_, f_nprocs_,
-      f_cu_occ_, f_mfma_, f_sq_busy_, f_gui_, f_waves_, f_lds_, f_lds_conf_, f_hbm_rd_,
+      f_cu_occ_, f_ecc_, f_aer_, f_pcie_nak_, f_pcie_recov_, f_xgmi_width_, f_xgmi_speed_, f_mfma_, f_sq_busy_, f_gui_, f_waves_, f_lds_, f_lds_conf_, f_hbm_rd_,
       f_hbm_wr_, f_sen_sclk_, f_sen_lat_, f_sen_xcc_, f_sen_runs_;
   int f_proc_vram_, f_proc_cu_, f_proc_sdma_;
   int f_legacy_mem_ = -1, f_legacy_perc_ = -1;

@@ -38,6 +38,11 @@ bool decode_gpu_metrics_v1_8(const void* blob, size_t len, DeviceSample* out) {
   out->pcie_bw_acc = m.pcie_bandwidth_acc;
   out->pcie_bw_inst = m.pcie_bandwidth_inst == ~0ull ? kNaN : double(m.pcie_bandwidth_inst);
   out->pcie_replay = m.pcie_replay_count_acc == ~0ull ? kNaN : double(m.pcie_replay_count_acc);
+  out->pcie_nak_sent = m.pcie_nak_sent_count_acc == 0xFFFFFFFFu ? kNaN : double(m.pcie_nak_sent_count_acc);
+  out->pcie_nak_rcvd = m.pcie_nak_rcvd_count_acc == 0xFFFFFFFFu ? kNaN : double(m.pcie_nak_rcvd_count_acc);
+  out->pcie_l0_recov = m.pcie_l0_to_recov_count_acc == ~0ull ? kNaN : double(m.pcie_l0_to_recov_count_acc);
+  out->xgmi_width = u16v(m.xgmi_link_width);
+  out->xgmi_speed = u16v(m.xgmi_link_speed);
   int nl = 0;
   for (int l = 0; l < kMaxXgmiLinks; ++l) {
     out->xgmi_read_kb[l] = m.xgmi_read_data_acc[l] == ~0ull ? 0 : m.xgmi_read_data_acc[l];

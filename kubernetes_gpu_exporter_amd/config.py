@@ -30,7 +30,8 @@ class Config:
     mock_devices: int = 1
     host_root: str = ""                    # prefix for /sys and /proc (DaemonSet: /host)
     devices: list = field(default_factory=list)  # exporter GPU indices to export (empty = all)
-    series_profile: str = "standard"       # standard | compact | legacy
+    series_profile: str = "full"           # full | standard (64/GPU BASELINE load) | compact | legacy
+    ras_interval: float = 10.0             # seconds between RAS/AER sysfs re-reads (full profile)
     legacy_families: bool = True           # pod_gpu_memory_usage / docker_gpu_memory_perc_usage
     process_source: str = "auto"           # auto | kfd | amdsmi | none
     kfd_cu_occupancy: bool = True
@@ -90,6 +91,7 @@ class Config:
         hc.enable_gzip = bool(self.gzip)
         ec.http = hc
         ec.series_profile = self.series_profile
+        ec.ras_interval_s = float(self.ras_interval)
         ec.legacy_families = bool(self.legacy_families)
         ec.pod_attribution = bool(self.pod_attribution)
         ec.infer_device_owner = bool(self.infer_device_owner)
@@ -206,8 +208,10 @@ def make_config(values: dict) -> Config:
 def validate(cfg: Config) -> None:
     if cfg.backend not in ("auto", "amdsmi", "sysfs", "mock"):
         raise ValueError(f"backend must be auto|amdsmi|sysfs|mock, got {cfg.backend}")
-    if cfg.series_profile not in ("standard", "compact", "legacy"):
-        raise ValueError(f"series_profile must be standard|compact|legacy, got {cfg.series_profile}")
+    if cfg.series_profile not in ("full", "standard", "compact", "legacy"):
+        raise ValueError(f"series_profile must be full|standard|compact|legacy, got {cfg.series_profile}")
+    if cfg.ras_interval <= 0:
+        raise ValueError("ras_interval must be > 0")
     if cfg.process_source not in ("auto", "kfd", "amdsmi", "none"):
         raise ValueError(f"process_source must be auto|kfd|amdsmi|none, got {cfg.process_source}")
     if cfg.interval < 0 or (0 < cfg.interval < 0.001):

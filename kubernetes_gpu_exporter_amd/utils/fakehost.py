@@ -105,6 +105,17 @@ class FakeHost:
         dev = f"sys/class/drm/renderD{gpu.render_minor}/device"
         self._w(f"{dev}/gpu_metrics", encode_gpu_metrics_v1_8(**kw), "wb")
 
+    def set_ras(self, gpu: FakeGpu, blocks: dict | None = None, aer: tuple = (0, 0, 0)) -> None:
+        """amdgpu ras/<block>_err_count ("ue: N\nce: N") and PCI aer_dev_* totals."""
+        dev = f"sys/class/drm/renderD{gpu.render_minor}/device"
+        for block, (ue, ce) in (blocks or {"umc": (0, 0), "gfx": (0, 0)}).items():
+            self._w(f"{dev}/ras/{block}_err_count", f"ue: {ue}\nce: {ce}\n")
+        self._w(f"{dev}/ras/features", "feature mask: 0x3fff\n")
+        names = ("correctable", "nonfatal", "fatal")
+        keys = ("TOTAL_ERR_COR", "TOTAL_ERR_NONFATAL", "TOTAL_ERR_FATAL")
+        for n, k, v in zip(names, keys, aer):
+            self._w(f"{dev}/aer_dev_{n}", f"RxErr 0\nBadTLP 0\n{k} {v}\n")
+
     def set_vram_used(self, gpu: FakeGpu, used: int) -> None:
         self._w(f"sys/class/drm/renderD{gpu.render_minor}/device/mem_info_vram_used", f"{used}\n")
 

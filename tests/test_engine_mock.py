@@ -229,3 +229,20 @@ def test_sampler_thread_runs(native):
     e.stop()
     st = e.stats()
     assert 15 <= st["ticks"] <= 40
+
+
+def test_full_profile_adds_reliability_families(mock_engine):
+    """`full` = the 64-series standard load + ECC / PCIe AER / NAK / recovery / xGMI link."""
+    e = mock_engine(2, http=False, enable_sentinel=True, enable_counters=True, series_profile="full")
+    e.mock_set_value(1, "ecc_ue", 3)
+    e.mock_set_value(1, "aer_cor", 7)
+    ticks(e, 3)
+    fams = parse(e)
+    assert dict(device_series_per_gpu(fams)) == {"0": 74, "1": 74}
+    ue = {s[1]["gpu"]: s[2] for s in fams["amd_gpu_ecc_errors_total"].samples
+          if s[1]["type"] == "uncorrectable"}
+    assert ue == {"0": 0, "1": 3}
+    assert {s[1]["severity"] for s in fams["amd_gpu_pcie_aer_errors_total"].samples} == {
+        "correctable", "nonfatal", "fatal"}
+    assert {s[1]["direction"] for s in fams["amd_gpu_pcie_nak_total"].samples} == {"sent", "received"}
+    assert fams["amd_gpu_ecc_errors_total"].type == "counter"

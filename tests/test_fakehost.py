@@ -176,3 +176,40 @@ def test_live_metric_updates(native, tmp_path):
             7 * 100 * 1024 * 1024 / 0.1)
     finally:
         e.stop()
+
+
+def test_ras_err_count_parsing(native):
+    r = native.parse_ras_err_count("ue: 2\nce: 15\n")
+    assert r["ok"] and r["ue"] == 2 and r["ce"] == 15 and r["de"] != r["de"]  # de absent -> NaN
+    r = native.parse_ras_err_count("ue: 0\nce: 1\nde: 4\n")
+    assert r["de"] == 4
+    assert not native.parse_ras_err_count("feature mask: 0x3fff\n")["ok"]
+    assert native.parse_aer_total("RxErr 0\nBadTLP 2\nTOTAL_ERR_COR 9\n") == 9
+    nan = native.parse_aer_total("garbage")
+    assert nan != nan
+
+
+def test_ras_and_aer_from_fake_sysfs(native, tmp_path):
+    """full profile on the sysfs backend: per-GPU ECC totals summed over IP blocks, AER
+    totals, both re-read only every ras_interval_s."""
+    h = mi355x_node(tmp_path, 2)
+    h.set_ras(h.gpus[0], {"umc": (1, 10), "gfx": (0, 5), "sdma": (2, 0)}, aer=(4, 1, 0))
+    e = _engine(native, tmp_path, series_profile="full", ras_interval_s=3600.0)
+    e.tick(1 * S)
+    fams = promtext.parse(e.snapshot_text())
+    ecc = {(s[1]["gpu"], s[1]["type"]): s[2] for s in fams["amd_gpu_ecc_errors_total"].samples}
+    (g,) = {k[0] for k in ecc}  # only the GPU with a ras dir exports ECC
+    assert ecc == {(g, "uncorrectable"): 3, (g, "correctable"): 15}
+    aer = {s[1]["severity"]: s[2] for s in fams["amd_gpu_pcie_aer_errors_total"].samples if s[1]["gpu"] == g}
+    assert aer == {"correctable": 4, "nonfatal": 1, "fatal": 0}
+    # a new error appears in sysfs, but the next read is an hour away -> cached totals
+    h.set_ras(h.gpus[0], {"umc": (5, 10), "gfx": (0, 5), "sdma": (2, 0)}, aer=(4, 1, 0))
+    e.tick(2 * S)
+    fams = promtext.parse(e.snapshot_text())
+    assert {s[2] for s in fams["amd_gpu_ecc_errors_total"].samples if s[1]["type"] == "uncorrectable"} == {3}
+    e.stop()
+    e2 = _engine(native, tmp_path, series_profile="full", ras_interval_s=3600.0)
+    e2.tick(1 * S)
+    fams = promtext.parse(e2.snapshot_text())
+    assert {s[2] for s in fams["amd_gpu_ecc_errors_total"].samples if s[1]["type"] == "uncorrectable"} == {7}
+    e2.stop()
