@@ -65,6 +65,11 @@ def traffic_worker(rank: int, world: int, strategy: str, steps: int, nbytes: int
     return {"calls": st.calls, "bytes": st.bytes, "seconds": st.seconds}
 
 
+def workload_worker(rank: int, world: int, name: str, steps: int, kw: dict):
+    from ..models import make, run
+    return run(make(name, **kw), steps, warmup=1)
+
+
 def main() -> int:
     import torch
     import torch.distributed as dist

@@ -60,3 +60,13 @@ def test_helm_values_referenced_exist():
         for part in r.split("."):
             assert isinstance(node, dict) and part in node, f"values.yaml lacks {r}"
             node = node[part]
+
+
+def test_synthetic_workloads_use_known_models():
+    from kubernetes_gpu_exporter_amd.models import WORKLOADS
+    for d in docs("synthetic-workloads.yaml"):
+        spec = d["spec"]["template"]["spec"] if d["kind"] == "Deployment" else d["spec"]
+        cmd = spec["containers"][0]["command"]
+        i = cmd.index("kubernetes_gpu_exporter_amd.models")
+        assert cmd[i + 1] in WORKLOADS
+        assert spec["containers"][0]["resources"]["limits"]["amd.com/gpu"] >= 1

@@ -209,3 +209,16 @@ def test_process_discovery_under_workload(native):
         e.stop()
         out, _ = child.communicate(timeout=60)
         print("child:", out.strip())
+
+
+def test_gemm_pod_model_on_gpu(native):
+    """models.GemmPod runs the HIP kernel (not a torch fallback) and matches fp32."""
+    import torch
+    from kubernetes_gpu_exporter_amd.models import GemmPod, run
+    p = GemmPod(size=512, iters=1)
+    assert p.gpu and p.c.dtype == torch.bfloat16
+    p.step()
+    ref = p.a.float() @ p.b.float().T
+    torch.testing.assert_close(p.c.float(), ref, atol=0.05, rtol=0.02)
+    big = run(GemmPod(size=4096, iters=8), steps=3, warmup=1)
+    assert big["tflops"] > 100, big
