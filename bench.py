@@ -280,6 +280,18 @@ def main() -> int:
             if v:
                 sentinel[key] = statistics.median(v)
         gfx = [s[2] for s in promtext.samples(fams, "amd_gpu_gfx_activity_percent")]
+        # diagnostics: which device families GPU 0 exports, and where the sampler's time goes
+        fam_gpu0 = {name: sum(1 for _, lab, _ in fam.samples if lab.get("gpu") == "0")
+                    for name, fam in fams.items() if name.startswith("amd_gpu_")
+                    and not name.startswith("amd_gpu_process_")}
+        stage_us = {}
+        for sname, lab, v in fams.get("gpuexp_sample_stage_duration_seconds", promtext.Family("x")).samples:
+            if sname.endswith("_sum"):
+                stage_us.setdefault(lab["stage"], [0.0, 0.0])[0] = v
+            elif sname.endswith("_count"):
+                stage_us.setdefault(lab["stage"], [0.0, 0.0])[1] = v
+        stage_us = {k: round(a / c * 1e6, 2) for k, (a, c) in stage_us.items() if c}
+        sampler_cpu = [v for _, _, v in promtext.samples(fams, "gpuexp_sampler_cpu_seconds_total")]
         tflops = 2.0 * G ** 3 * iters / (gemm_ms * iters * 1e-3) / 1e12 if gemm_ms else None
         result = {
             "metric": METRIC,
@@ -311,6 +323,9 @@ def main() -> int:
             "gpu_gfx_activity_percent": gfx,
             "sentinel": sentinel,
             "workload_gemm_tflops_per_gpu": round(tflops, 1) if tflops else None,
+            "families_gpu0": {k: v for k, v in sorted(fam_gpu0.items()) if v},
+            "sample_stage_mean_us": stage_us,
+            "sampler_thread_cpu_s": sampler_cpu[0] if sampler_cpu else None,
         }
         stop_proc(exporter)
 

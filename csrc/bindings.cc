@@ -292,6 +292,7 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("http", &EngineConfig::http)
       .def_readwrite("series_profile", &EngineConfig::series_profile)
       .def_readwrite("ras_interval_s", &EngineConfig::ras_interval_s)
+      .def_readwrite("metrics_coalesce", &EngineConfig::metrics_coalesce)
       .def_readwrite("legacy_families", &EngineConfig::legacy_families)
       .def_readwrite("pod_attribution", &EngineConfig::pod_attribution)
       .def_readwrite("infer_device_owner", &EngineConfig::infer_device_owner)

@@ -239,6 +239,7 @@ bool setup_agent(Agent& a, std::string* why) {
   hsa_agent_get_info(a.gpu, hsa_agent_info_t(HSA_AMD_AGENT_INFO_COMPUTE_UNIT_COUNT), &cu);
   hsa_agent_get_info(a.gpu, hsa_agent_info_t(HSA_AMD_AGENT_INFO_NUM_SIMDS_PER_CU), &simd_per_cu);
   a.m.cu = cu;
+  a.m.privileged = process_has_pmc_privilege();
   a.m.simd = cu * simd_per_cu;
 
   hsa_ven_amd_aqlprofile_profile_t probe{};

@@ -191,6 +191,7 @@ class AmdsmiBackend : public Backend {
           d.vram_used_file.open(dir + "/mem_info_vram_used");
           std::string e;
           if (!force_smi_ && d.gm.open(dir + "/gpu_metrics", &e)) d.fast_ok = validate(d);
+          d.gm.set_coalesce(coalesce_metrics_);
           if (!d.fast_ok)
             GPUEXP_LOG(LogLevel::kInfo, "amdsmi",
                        "gpu " + std::to_string(info.index) + ": using amdsmi_get_gpu_metrics_info per tick (" +
@@ -239,7 +240,7 @@ class AmdsmiBackend : public Backend {
   void sample(const DeviceInfo& dev, DeviceSample* out) override {
     Dev& d = devs_.at(size_t(dev.index));
     bool ok = false;
-    if (d.fast_ok) ok = d.gm.read(out);
+    if (d.fast_ok) ok = d.gm.read(out, out->host_ns);
     if (!ok) {
       amdsmi_gpu_metrics_t m{};
       amdsmi_status_t st = amdsmi_get_gpu_metrics_info(d.h, &m);

@@ -138,6 +138,7 @@ bool SysfsBackend::init(std::vector<DeviceInfo>* devices, std::string* err) {
 void SysfsBackend::open_dev_files(Dev* d) {
   std::string e;
   d->gm_ok = d->gm.open(d->dev_dir + "/gpu_metrics", &e);
+  d->gm.set_coalesce(coalesce_metrics_);
   d->vram_used.open(d->dev_dir + "/mem_info_vram_used");
   d->busy.open(d->dev_dir + "/gpu_busy_percent");
   d->mem_busy.open(d->dev_dir + "/mem_busy_percent");
@@ -174,7 +175,7 @@ void SysfsBackend::sample(const DeviceInfo& dev, DeviceSample* out) {
   Dev& d = *devs_.at(size_t(dev.index));
   bool any = false;
   if (d.gm_ok) {
-    if (d.gm.read(out)) {
+    if (d.gm.read(out, out->host_ns)) {
       any = true;
     } else {
       // The blob can vanish with the device (hot-unplug/reset): retry open once.

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 
 namespace gpuexp_ctr {
 
@@ -46,8 +47,27 @@ inline bool use_max(int c) { return c == kGuiActive || c == kGrbmCount; }
 // Number of derived outputs (the CounterSource ABI: gpuexp_rp_sample fills 8 doubles).
 constexpr int kNumOut = 8;
 
+// Wave-level SQ counters and TCC EA requests are VMID-filtered for unprivileged clients.
+// The filter is on the HARDWARE VMID, which the scheduler hands out dynamically, so an
+// unprivileged exporter sometimes sees another process's waves (a VMID collision) and
+// sometimes only its own (measured: bench at 1 Hz looked device-wide, at 10 Hz filtered).
+// No heuristic on the values can tell those apart, so scope comes from privilege:
+// CAP_SYS_ADMIN or CAP_PERFMON in the effective set (what a privileged DaemonSet has).
+inline bool process_has_pmc_privilege() {
+  FILE* f = std::fopen("/proc/self/status", "r");
+  if (!f) return false;
+  char line[256];
+  unsigned long long eff = 0;
+  while (std::fgets(line, sizeof(line), f))
+    if (std::sscanf(line, "CapEff: %llx", &eff) == 1) break;
+  std::fclose(f);
+  constexpr int kCapSysAdmin = 21, kCapPerfmon = 38;
+  return (eff >> kCapSysAdmin & 1ull) || (eff >> kCapPerfmon & 1ull);
+}
+
 struct Derived {
   uint32_t simd = 0, cu = 0;
+  bool privileged = false;  // set at init: process_has_pmc_privilege()
   int scope = -1;  // -1 unknown, 0 wave/EA counters VMID-filtered to this process, 1 device-wide
   double latest[kNumOut] = {};
   bool valid = false;
@@ -58,13 +78,13 @@ struct Derived {
 inline void derive(Derived& a, const double* d, const int* inst, double wall) {
   const double nan = std::nan("");
   const double gui = d[kGuiActive];
-  // Scope detection.  As a non-root client (perf_event_paranoid=3 on the test pool) the
-  // wave-level SQ counters and the TCC EA requests are VMID-filtered to THIS process,
-  // while SQ_VALU_MFMA_BUSY_CYCLES and GRBM are chip-global (measured against rocprofv3
-  // dispatch counts: profiles/r01/pmc_gemm_dispatch.txt).  A busy GPU on which the
-  // exporter sees almost no waves means the filtered set must not be exported as device
-  // totals.
-  if (d[kGrbmCount] > 0 && gui / d[kGrbmCount] > 0.5 && d[kMfma] > 0) a.scope = d[kWaves] / wall < 1000.0 ? 0 : 1;
+  // Scope.  SQ_VALU_MFMA_BUSY_CYCLES and GRBM are chip-global in every case (measured
+  // against rocprofv3 dispatch counts: profiles/r01/pmc_gemm_dispatch.txt); the wave/LDS/EA
+  // set is only device-wide for a privileged client (see process_has_pmc_privilege).
+  // Privileged: device-wide unless a busy MFMA window shows no waves at all (sticky 0).
+  if (!a.privileged) a.scope = 0;
+  else if (a.scope != 0) a.scope = (d[kGrbmCount] > 0 && gui / d[kGrbmCount] > 0.5 && d[kMfma] > 0 &&
+                                    d[kWaves] / wall < 1000.0) ? 0 : 1;
   double* out = a.latest;
   out[0] = gui > 0 && a.simd ? 100.0 * d[kMfma] / (gui * a.simd) : nan;             // MfmaUtil
   const double se = inst[kSqBusy] > 0 ? inst[kSqBusy] : 1;                           // one per SE

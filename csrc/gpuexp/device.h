@@ -42,6 +42,7 @@ struct DeviceSample {
   std::string error;
   uint64_t host_ns = 0;        // CLOCK_MONOTONIC at read
   uint64_t fw_ts_10ns = 0;     // PMFW timestamp (10 ns units), 0 = n/a
+  bool metrics_coalesced = false;  // decoded from the cached gpu_metrics table (no SMU fetch)
 
   double gfx_activity = kNaN;  // %
   double umc_activity = kNaN;  // %
@@ -127,6 +128,8 @@ struct SentinelReading {
 class Backend {
  public:
   virtual ~Backend() = default;
+  // gpu_metrics read coalescing (GpuMetricsReader); set before init().
+  void set_metrics_coalescing(bool on) { coalesce_metrics_ = on; }
   virtual const char* name() const = 0;
   // Enumerates devices once.  Returns false (with *err) if the backend cannot run.
   virtual bool init(std::vector<DeviceInfo>* devices, std::string* err) = 0;
@@ -157,6 +160,8 @@ class Backend {
     return name();
   }
   virtual void shutdown() {}
+ protected:
+  bool coalesce_metrics_ = true;
 };
 
 }  // namespace gpuexp

@@ -215,6 +215,10 @@ void Engine::define_families() {
   f_self_overruns_ = add("gpuexp_tick_overruns_total", "Ticks skipped because a tick ran past its deadline", C, {});
   f_self_cpu_ = add("gpuexp_sampler_cpu_seconds_total", "CPU time used by the sampler thread", C, {});
   f_self_source_up_ = add("gpuexp_source_up", "1 if an optional source is active", G, {"source"});
+  f_self_metrics_reads_ = add("gpuexp_gpu_metrics_reads_total",
+                              "gpu_metrics reads by kind: fresh (SMU table fetch) or coalesced (cached table, "
+                              "PMFW had not refreshed yet)",
+                              C, {"gpu", "kind"});
   f_self_ctr_scope_ = add("gpuexp_counters_device_scope",
                           "1 if wave/LDS/HBM PMC counters see every process on the GPU, 0 if they are "
                           "VMID-filtered to the exporter (not exported then)",
@@ -236,6 +240,7 @@ bool Engine::start(std::string* err) {
     *err = "unknown backend: " + cfg_.backend;
     return false;
   }
+  backend_->set_metrics_coalescing(cfg_.metrics_coalesce);
   std::vector<DeviceInfo> all;
   if (!backend_->init(&all, err)) return false;
   if (!cfg_.device_filter.empty()) {
@@ -247,6 +252,8 @@ bool Engine::start(std::string* err) {
     devices_ = all;
   }
   dstate_.assign(devices_.size(), DevState());
+  metrics_fresh_.assign(devices_.size(), 0);
+  metrics_coalesced_.assign(devices_.size(), 0);
   if (cfg_.series_profile == "full" && cfg_.backend != "mock") {
     const std::string root = cfg_.host_root.empty() ? "" : cfg_.host_root;
     ras_.resize(devices_.size());
@@ -430,6 +437,8 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
     std::copy(std::begin(st.xgmi_rd_rate), std::end(st.xgmi_rd_rate), std::begin(fresh.xgmi_rd_rate));
     std::copy(std::begin(st.xgmi_wr_rate), std::end(st.xgmi_wr_rate), std::begin(fresh.xgmi_wr_rate));
     fresh.rates_valid = st.rates_valid;
+    std::copy(std::begin(st.thr_last), std::end(st.thr_last), std::begin(fresh.thr_last));
+    std::copy(std::begin(st.xcc_last), std::end(st.xcc_last), std::begin(fresh.xcc_last));
     fresh.errors = st.errors;
     fresh.err_ref = st.err_ref;
     fresh.owner = keep;
@@ -533,6 +542,7 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
     dput(st, i, st.xgmi_s, f_xgmi_speed_, {}, c.xgmi_speed, gen);
   }
 
+  uint32_t nx = d.num_xcc ? std::min<uint32_t>(d.num_xcc, kMaxXcc) : kMaxXcc;
   if (have_prev && c.residency_valid && p.residency_valid) {
     double dacc;
     if (acc_delta(c.accumulation_counter, p.accumulation_counter, &dacc) && dacc > 0) {
@@ -540,19 +550,17 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
       uint64_t pr[5] = {p.res_ppt, p.res_socket_thm, p.res_vr_thm, p.res_hbm_thm, p.res_prochot};
       for (int k = 0; k < 5; ++k) {
         double dr;
-        if (acc_delta(cr[k], pr[k], &dr))
-          dput(st, i, st.thr[k], f_thr_, {kThrNames[k]}, std::min(100.0, dr * 100.0 / dacc), gen);
+        if (acc_delta(cr[k], pr[k], &dr)) st.thr_last[k] = std::min(100.0, dr * 100.0 / dacc);
       }
-      if (!compact) {
-        uint32_t nx = d.num_xcc ? std::min<uint32_t>(d.num_xcc, kMaxXcc) : kMaxXcc;
-        for (uint32_t x = 0; x < nx; ++x) {
-          double db;
-          if (acc_delta(c.gfx_busy_acc[x], p.gfx_busy_acc[x], &db))
-            dput(st, i, st.xcc[x], f_xcc_, {std::to_string(x)}, std::min(100.0, db / dacc), gen);
-        }
+      for (uint32_t x = 0; x < nx; ++x) {
+        double db;
+        if (acc_delta(c.gfx_busy_acc[x], p.gfx_busy_acc[x], &db)) st.xcc_last[x] = std::min(100.0, db / dacc);
       }
     }
   }
+  for (int k = 0; k < 5; ++k) dput(st, i, st.thr[k], f_thr_, {kThrNames[k]}, st.thr_last[k], gen);
+  if (!compact)
+    for (uint32_t x = 0; x < nx; ++x) dput(st, i, st.xcc[x], f_xcc_, {std::to_string(x)}, st.xcc_last[x], gen);
 
   // Optional sources: rocprofiler counters, sentinel (real or mock-simulated).
   CounterReading cr;
@@ -755,6 +763,12 @@ void Engine::emit_self(uint64_t gen) {
     table_.put(f_self_scrapes_, {}, double(hs.metrics_requests.load(std::memory_order_relaxed)), gen);
     table_.put(f_self_http_bytes_, {}, double(hs.bytes_sent.load(std::memory_order_relaxed)), gen);
   }
+  if (!mock_)
+    for (size_t i = 0; i < devices_.size(); ++i) {
+      const std::string g = std::to_string(devices_[i].index);
+      table_.put(f_self_metrics_reads_, {g, "fresh"}, double(metrics_fresh_[i]), gen);
+      table_.put(f_self_metrics_reads_, {g, "coalesced"}, double(metrics_coalesced_[i]), gen);
+    }
   table_.put(f_self_source_up_, {"backend:" + std::string(backend_->name())}, 1, gen);
   table_.put(f_self_source_up_, {"sentinel"}, (sentinel_ || (cfg_.enable_sentinel && mock_)) ? 1 : 0, gen);
   table_.put(f_self_source_up_, {"counters"}, (counters_ || (cfg_.enable_counters && mock_)) ? 1 : 0, gen);
@@ -803,6 +817,7 @@ void Engine::tick_locked(uint64_t now) {
     st.cur = DeviceSample();
     st.cur.host_ns = now;
     backend_->sample(devices_[size_t(i)], &st.cur);
+    (st.cur.metrics_coalesced ? metrics_coalesced_ : metrics_fresh_)[size_t(i)] += 1;
     if (!ras_.empty()) {
       if (now >= ras_next_ns_[size_t(i)]) {
         ras_[size_t(i)].read(&ras_cache_[size_t(i)]);

@@ -64,6 +64,7 @@ struct EngineConfig {
   HttpConfig http;
   std::string series_profile = "standard";  // standard | full | compact | legacy
   double ras_interval_s = 10.0;        // full profile: RAS/AER sysfs re-read period
+  bool metrics_coalesce = true;        // skip gpu_metrics SMU fetches between PMFW refreshes
   bool legacy_families = true;         // pod_gpu_memory_usage / docker_gpu_memory_perc_usage
   bool pod_attribution = true;
   bool infer_device_owner = true;      // single-pod GPU -> device series carry the pod
@@ -149,6 +150,11 @@ class Engine {
     double xgmi_rd_rate[kMaxXgmiLinks] = {};
     double xgmi_wr_rate[kMaxXgmiLinks] = {};
     bool rates_valid = false;
+    // Last residency-derived values: the PMFW accumulates them at its own rate (slower
+    // than a 100 Hz tick), so a tick without a new accumulation re-exports these instead
+    // of dropping the series.
+    double thr_last[5] = {kNaN, kNaN, kNaN, kNaN, kNaN};
+    double xcc_last[kMaxXcc] = {kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN};
     DeviceOwner owner;
     std::string owner_key;  // ns/pod/container the refs were built for
     // cached series handles (re-upserted on owner change or GC)
@@ -188,6 +194,7 @@ class Engine {
   std::vector<RasReader> ras_;
   std::vector<RasTotals> ras_cache_;
   std::vector<uint64_t> ras_next_ns_;
+  std::vector<uint64_t> metrics_fresh_, metrics_coalesced_;  // per device
   std::string sentinel_status_ = "disabled", counters_status_ = "disabled";
 
   SeriesTable table_;
@@ -236,7 +243,7 @@ class Engine {
   int f_rccl_calls_, f_rccl_bytes_;
   int f_self_build_, f_self_ticks_, f_self_stage_, f_self_scrape_, f_self_scrapes_,
       f_self_http_bytes_, f_self_render_bytes_, f_self_series_, f_self_dev_errors_,
-      f_self_overruns_, f_self_cpu_, f_self_source_up_, f_self_ctr_scope_;
+      f_self_overruns_, f_self_cpu_, f_self_source_up_, f_self_ctr_scope_, f_self_metrics_reads_;
   SeriesRef self_stage_refs_[kStages];
   uint64_t last_stage_ns_[kStages] = {};
 };

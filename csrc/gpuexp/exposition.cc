@@ -1,5 +1,7 @@
 #include "gpuexp/exposition.h"
 
+#include <cstring>
+
 #include <algorithm>
 #include <charconv>
 #include <cmath>
@@ -136,6 +138,10 @@ SeriesRef SeriesTable::upsert(int fid, const std::vector<std::string>& values) {
     }
     s.prefix.push_back('}');
   }
+  s.line = s.prefix;
+  s.line.push_back(' ');
+  s.vvalid = false;
+  s.hlines.clear();
   index_.emplace(s.key, idx);
   fam.members.push_back(idx);
   fam.dirty_order = true;
@@ -166,6 +172,7 @@ bool SeriesTable::observe(SeriesRef r, double v, uint64_t gen, const std::vector
   if (s.bounds.empty()) {
     s.bounds = bounds;
     s.buckets.assign(bounds.size(), 0);
+    s.hlines.clear();
   }
   // Buckets are stored non-cumulative; rendering accumulates.
   auto it = std::lower_bound(s.bounds.begin(), s.bounds.end(), v);
@@ -182,7 +189,10 @@ bool SeriesTable::set_histogram(SeriesRef r, const std::vector<double>& bounds,
   if (!r.valid() || r.idx >= series_.size()) return false;
   Series& s = series_[r.idx];
   if (s.ver != r.ver || s.fid < 0) return false;
-  s.bounds = bounds;
+  if (s.bounds != bounds) {
+    s.bounds = bounds;
+    s.hlines.clear();
+  }
   s.buckets.assign(bounds.size(), 0);
   for (size_t i = 0; i < bounds.size() && i < counts.size(); ++i) s.buckets[i] = counts[i];
   s.hsum = sum;
@@ -205,9 +215,12 @@ void SeriesTable::free_series(uint32_t idx) {
   s.ver += 1;
   s.labels.clear();
   s.prefix.clear();
+  s.line.clear();
   s.key.clear();
   s.bounds.clear();
   s.buckets.clear();
+  s.hlines.clear();
+  s.vvalid = false;
   free_.push_back(idx);
 }
 
@@ -229,45 +242,61 @@ void SeriesTable::sort_members(Family& f) {
   f.dirty_order = false;
 }
 
-void SeriesTable::render_histogram(std::string* out, const Series& s) const {
-  const Family& fam = families_[size_t(s.fid)];
-  // name_bucket{labels,le="x"} cumulative
-  std::string base = fam.def.name;
-  std::string labels;  // `a="x",b="y"`
-  if (s.prefix.size() > base.size() + 2) labels = s.prefix.substr(base.size() + 1, s.prefix.size() - base.size() - 2);
+void SeriesTable::append_cached_value(std::string* out, Series& s) {
+  uint64_t bits;
+  std::memcpy(&bits, &s.value, sizeof(bits));
+  if (!s.vvalid || bits != s.vbits) {
+    std::string tmp;
+    append_value(&tmp, s.value);
+    s.vlen = uint8_t(std::min(tmp.size(), sizeof(s.vtxt)));
+    std::memcpy(s.vtxt, tmp.data(), s.vlen);
+    s.vbits = bits;
+    s.vvalid = true;
+  }
+  out->append(s.vtxt, s.vlen);
+}
+
+void SeriesTable::render_histogram(std::string* out, Series& s) const {
+  // name_bucket{labels,le="x"} cumulative ... _sum, _count.  The line prefixes depend only
+  // on the labels and the (fixed) bounds: built once, then each render appends numbers.
+  if (s.hlines.size() != s.bounds.size() + 3) {
+    const Family& fam = families_[size_t(s.fid)];
+    const std::string& base = fam.def.name;
+    std::string labels;  // `a="x",b="y"`
+    if (s.prefix.size() > base.size() + 2) labels = s.prefix.substr(base.size() + 1, s.prefix.size() - base.size() - 2);
+    s.hlines.clear();
+    for (size_t i = 0; i <= s.bounds.size(); ++i) {
+      std::string l = base + "_bucket{";
+      if (!labels.empty()) l += labels + ",";
+      l += "le=\"";
+      if (i < s.bounds.size()) append_value(&l, s.bounds[i]);
+      else l += "+Inf";
+      l += "\"} ";
+      s.hlines.push_back(std::move(l));
+    }
+    for (const char* sfx : {"_sum", "_count"}) {
+      std::string l = base + sfx;
+      if (!labels.empty()) l += "{" + labels + "}";
+      l += " ";
+      s.hlines.push_back(std::move(l));
+    }
+  }
+  char buf[24];
   uint64_t cum = 0;
   for (size_t i = 0; i <= s.bounds.size(); ++i) {
-    out->append(base);
-    out->append("_bucket{");
-    if (!labels.empty()) {
-      out->append(labels);
-      out->push_back(',');
-    }
-    out->append("le=\"");
-    if (i < s.bounds.size()) {
-      cum += s.buckets[i];
-      append_value(out, s.bounds[i]);
-    } else {
-      cum = s.hcount;
-      out->append("+Inf");
-    }
-    out->append("\"} ");
-    append_value(out, double(cum));
+    cum = i < s.bounds.size() ? cum + s.buckets[i] : s.hcount;
+    out->append(s.hlines[i]);
+    auto r = std::to_chars(buf, buf + sizeof(buf), cum);
+    out->append(buf, r.ptr);
     out->push_back('\n');
   }
-  const char* sfx[2] = {"_sum", "_count"};
-  for (int k = 0; k < 2; ++k) {
-    out->append(base);
-    out->append(sfx[k]);
-    if (!labels.empty()) {
-      out->push_back('{');
-      out->append(labels);
-      out->push_back('}');
-    }
-    out->push_back(' ');
-    append_value(out, k == 0 ? s.hsum : double(s.hcount));
-    out->push_back('\n');
-  }
+  out->append(s.hlines[s.bounds.size() + 1]);
+  append_value(out, s.hsum);
+  out->push_back('\n');
+  out->append(s.hlines[s.bounds.size() + 2]);
+  auto r = std::to_chars(buf, buf + sizeof(buf), s.hcount);
+  out->append(buf, r.ptr);
+  out->push_back('\n');
 }
 
 void SeriesTable::render(std::string* out, uint64_t gen, uint64_t gc_after) {
@@ -292,15 +321,14 @@ void SeriesTable::render(std::string* out, uint64_t gen, uint64_t gc_after) {
     if (fam.dirty_order) sort_members(fam);
     out->append(fam.header);
     for (uint32_t idx : fam.members) {
-      const Series& s = series_[idx];
+      Series& s = series_[idx];
       if (s.gen != gen) continue;
       if (fam.def.type == MetricType::kHistogram) {
         render_histogram(out, s);
         continue;
       }
-      out->append(s.prefix);
-      out->push_back(' ');
-      append_value(out, s.value);
+      out->append(s.line);
+      append_cached_value(out, s);
       out->push_back('\n');
     }
   }

@@ -84,12 +84,20 @@ class SeriesTable {
     double value = 0;
     std::vector<std::string> labels;
     std::string prefix;       // `name{a="x",b="y"}` (no trailing space)
+    std::string line;         // prefix + ' ' (what render copies before the value)
     std::string key;          // interning key
+    // Formatted value cache: re-formatted only when the value's bits change (most device
+    // series — identity, capacities, link state, error totals — change rarely).
+    uint64_t vbits = 0;
+    uint8_t vlen = 0;
+    bool vvalid = false;
+    char vtxt[32];
     // histogram state
     std::vector<double> bounds;
     std::vector<uint64_t> buckets;
     double hsum = 0;
     uint64_t hcount = 0;
+    std::vector<std::string> hlines;  // `name_bucket{...,le="b"} ` per bound, +Inf, _sum, _count
   };
   struct Family {
     FamilyDef def;
@@ -99,7 +107,8 @@ class SeriesTable {
   };
   void free_series(uint32_t idx);
   void sort_members(Family& f);
-  void render_histogram(std::string* out, const Series& s) const;
+  void render_histogram(std::string* out, Series& s) const;
+  static void append_cached_value(std::string* out, Series& s);
 
   std::vector<Family> families_;
   std::vector<int> render_order_;  // family ids sorted by name

@@ -99,20 +99,46 @@ bool GpuMetricsReader::open(const std::string& path, std::string* err) {
   return true;
 }
 
-bool GpuMetricsReader::read(DeviceSample* out) {
+bool GpuMetricsReader::read(DeviceSample* out, uint64_t now_ns) {
   if (fd_ < 0) {
     out->error = "gpu_metrics not open";
     return false;
   }
+  // Guard: re-read 1.5 ms before the expected refresh so a little jitter in the PMFW
+  // period never costs a whole period of staleness.
+  constexpr uint64_t kGuardNs = 1500000;
+  if (coalesce_ && now_ns && last_n_ > 0 && period_ns_ > kGuardNs && now_ns >= t_change_ns_ &&
+      now_ns < t_change_ns_ + period_ns_ - kGuardNs) {
+    coalesced_reads_ += 1;
+    out->metrics_coalesced = true;
+    return decode_gpu_metrics_v1_8(buf_, size_t(last_n_), out);
+  }
   long n = pread_once(fd_, reinterpret_cast<char*>(buf_), sizeof(buf_));
   if (n <= 0) {
+    last_n_ = 0;
     out->error = "gpu_metrics read failed";
     return false;
   }
+  last_n_ = n;
+  fresh_reads_ += 1;
   if (!decode_gpu_metrics_v1_8(buf_, size_t(n), out)) {
+    last_n_ = 0;
     out->error = "gpu_metrics decode failed";
     return false;
   }
+  if (out->fw_ts_10ns && out->fw_ts_10ns != last_fw_ts_) {
+    if (last_fw_ts_ && out->fw_ts_10ns > last_fw_ts_) {
+      const uint64_t step = (out->fw_ts_10ns - last_fw_ts_) * 10;
+      // Only single-period steps teach the period (a longer tick spans several tables).
+      if (period_ns_ == 0 || step < period_ns_ * 3 / 2) {
+        period_ns_ = period_ns_ ? (period_ns_ * 3 + step) / 4 : step;
+        changes_ += 1;
+      }
+    }
+    last_fw_ts_ = out->fw_ts_10ns;
+    t_change_ns_ = now_ns;
+  }
+  if (changes_ < 2) t_change_ns_ = 0;  // still learning the period: keep reading
   return true;
 }
 

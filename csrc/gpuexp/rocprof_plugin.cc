@@ -52,7 +52,6 @@ using namespace gpuexp_ctr;
 struct Agent {
   rocprofiler_agent_id_t id{};
   int dev = -1;
-  uint32_t simd = 0, cu = 0;
   rocprofiler_context_id_t ctx{};
   rocprofiler_counter_config_id_t cfg{};
   bool have_cfg = false;
@@ -114,6 +113,7 @@ int tool_init(rocprofiler_client_finalize_t fini, void*) {
       ag.id = a.id;
       ag.dev = int(d);
       ag.m.simd = a.simd_count;
+      ag.m.privileged = process_has_pmc_privilege();
       ag.m.cu = a.cu_count ? a.cu_count : (a.simd_per_cu ? a.simd_count / a.simd_per_cu : 0);
       if (rocprofiler_create_context(&ag.ctx) != ROCPROFILER_STATUS_SUCCESS) continue;
       rocprofiler_buffer_id_t nobuf{};  // values come back in the sample call itself

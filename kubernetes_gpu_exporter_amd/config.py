@@ -27,6 +27,7 @@ class Config:
     interval: float = 1.0                  # seconds; reference: 30 s (main.go:156)
     backend: str = "auto"                  # auto | amdsmi | sysfs | mock
     device_threads: int = 0                # per-GPU read fan-out (0 = auto, 1 = serial)
+    metrics_coalesce: bool = True          # skip gpu_metrics SMU fetches until the PMFW refreshes
     mock_devices: int = 1
     host_root: str = ""                    # prefix for /sys and /proc (DaemonSet: /host)
     devices: list = field(default_factory=list)  # exporter GPU indices to export (empty = all)
@@ -80,6 +81,7 @@ class Config:
         ec.backend = self.resolved_backend()
         ec.mock_devices = int(self.mock_devices)
         ec.device_threads = int(self.device_threads)
+        ec.metrics_coalesce = bool(self.metrics_coalesce)
         ec.host_root = self.host_root
         ec.interval_s = float(self.interval)
         host, port = self.listen_host_port()

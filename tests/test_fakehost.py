@@ -213,3 +213,44 @@ def test_ras_and_aer_from_fake_sysfs(native, tmp_path):
     fams = promtext.parse(e2.snapshot_text())
     assert {s[2] for s in fams["amd_gpu_ecc_errors_total"].samples if s[1]["type"] == "uncorrectable"} == {7}
     e2.stop()
+
+
+def _reads(fams):
+    return {s[1]["kind"]: s[2] for s in fams["gpuexp_gpu_metrics_reads_total"].samples if s[1]["gpu"] == "0"}
+
+
+def test_gpu_metrics_reads_coalesce_to_pmfw_rate(native, tmp_path):
+    """The PMFW refreshes gpu_metrics every 20 ms; a 100 Hz sampler learns that from
+    firmware_timestamp steps and fetches a fresh table only once per refresh, while every
+    new table is still picked up within one tick."""
+    h = mi355x_node(tmp_path, 1)
+    (g,) = h.gpus
+    e = _engine(native, tmp_path)
+    ms = 1_000_000
+    base_ts = 105165583750064
+    seen = []
+    for k in range(60):  # 10 ms ticks for 600 ms; the table changes every 20 ms
+        now = 1 * S + k * 10 * ms
+        table = k // 2
+        h.set_metrics(g, fw_ts=base_ts + table * 2_000_000, power=200 + table)
+        e.tick(now)
+        fams = promtext.parse(e.snapshot_text())
+        seen.append(promtext.samples(fams, "amd_gpu_power_watts")[0][2])
+    reads = _reads(fams)
+    assert reads["coalesced"] >= 25, reads          # ~half of 60 ticks skipped the SMU fetch
+    assert reads["fresh"] + reads["coalesced"] == 60
+    # every table (power 200..229) was exported, each at most one tick late
+    assert sorted(set(seen)) == list(range(200, 230))
+    assert all(seen[k] >= 200 + k // 2 - 1 for k in range(60))
+    e.stop()
+
+
+def test_gpu_metrics_coalescing_can_be_disabled(native, tmp_path):
+    h = mi355x_node(tmp_path, 1)
+    (g,) = h.gpus
+    e = _engine(native, tmp_path, metrics_coalesce=False)
+    for k in range(20):
+        h.set_metrics(g, fw_ts=105165583750064 + (k // 2) * 2_000_000)
+        e.tick(1 * S + k * 10_000_000)
+    assert _reads(promtext.parse(e.snapshot_text())) == {"fresh": 20, "coalesced": 0}
+    e.stop()
