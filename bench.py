@@ -291,6 +291,19 @@ def main() -> int:
             elif sname.endswith("_count"):
                 stage_us.setdefault(lab["stage"], [0.0, 0.0])[1] = v
         stage_us = {k: round(a / c * 1e6, 2) for k, (a, c) in stage_us.items() if c}
+        # p50 per stage from the cumulative histogram buckets (upper bound of the median bucket)
+        buckets: dict = {}
+        for sname, lab, v in fams.get("gpuexp_sample_stage_duration_seconds", promtext.Family("x")).samples:
+            if sname.endswith("_bucket"):
+                buckets.setdefault(lab["stage"], []).append((float(lab["le"]), v))  # "+Inf" -> inf
+        stage_p50_us = {}
+        for st_name, bl in buckets.items():
+            bl.sort()
+            total = bl[-1][1]
+            le50 = next((le for le, v in bl if total and v >= total / 2), None)
+            stage_p50_us[st_name] = round(le50 * 1e6, 1) if le50 is not None else None
+        metrics_reads = {lab["kind"]: v for _, lab, v in promtext.samples(fams, "gpuexp_gpu_metrics_reads_total")
+                         if lab.get("gpu") == "0"}
         sampler_cpu = [v for _, _, v in promtext.samples(fams, "gpuexp_sampler_cpu_seconds_total")]
         tflops = 2.0 * G ** 3 * iters / (gemm_ms * iters * 1e-3) / 1e12 if gemm_ms else None
         result = {
@@ -325,6 +338,8 @@ def main() -> int:
             "workload_gemm_tflops_per_gpu": round(tflops, 1) if tflops else None,
             "families_gpu0": {k: v for k, v in sorted(fam_gpu0.items()) if v},
             "sample_stage_mean_us": stage_us,
+            "sample_stage_p50_le_us": stage_p50_us,
+            "gpu_metrics_reads_gpu0": metrics_reads,
             "sampler_thread_cpu_s": sampler_cpu[0] if sampler_cpu else None,
         }
         stop_proc(exporter)

@@ -101,6 +101,7 @@ class AmdsmiBackend : public Backend {
     GpuMetricsReader gm;
     bool fast_ok = false;
     std::string validate_msg;
+    uint64_t raw_failures = 0;  // __atomic_* access: sampler writes, describe() reads
     CachedFile vram_used_file;
     double power_cap_w = kNaN;
     std::vector<amdsmi_proc_info_t> procbuf = std::vector<amdsmi_proc_info_t>(64);
@@ -240,8 +241,14 @@ class AmdsmiBackend : public Backend {
   void sample(const DeviceInfo& dev, DeviceSample* out) override {
     Dev& d = devs_.at(size_t(dev.index));
     bool ok = false;
-    if (d.fast_ok) ok = d.gm.read(out, out->host_ns);
+    if (d.fast_ok) {
+      ok = d.gm.read(out, out->host_ns);
+      if (!ok && __atomic_fetch_add(&d.raw_failures, 1, __ATOMIC_RELAXED) == 0)
+        GPUEXP_LOG(LogLevel::kWarn, "amdsmi", "gpu " + std::to_string(dev.index) + ": raw gpu_metrics read failed (" +
+                                                  out->error + "); falling back to amdsmi_get_gpu_metrics_info");
+    }
     if (!ok) {
+      out->error.clear();
       amdsmi_gpu_metrics_t m{};
       amdsmi_status_t st = amdsmi_get_gpu_metrics_info(d.h, &m);
       if (st != AMDSMI_STATUS_SUCCESS) {
@@ -288,8 +295,15 @@ class AmdsmiBackend : public Backend {
     return true;
   }
 
+  double metrics_period_s(const DeviceInfo& dev) override {
+    return double(devs_.at(size_t(dev.index)).gm.period_ns()) * 1e-9;
+  }
+
   std::string describe(const DeviceInfo& dev) override {
     const Dev& d = devs_.at(size_t(dev.index));
+    const uint64_t fails = __atomic_load_n(&d.raw_failures, __ATOMIC_RELAXED);  // sampler thread writes
+    if (d.fast_ok && fails)
+      return "raw gpu_metrics v1.8 with " + std::to_string(fails) + " failed reads (amdsmi fallback)";
     return d.fast_ok ? "raw gpu_metrics v1.8 (validated against amdsmi)"
                      : "amdsmi_get_gpu_metrics_info (" + d.validate_msg + ")";
   }

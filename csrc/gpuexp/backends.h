@@ -97,6 +97,9 @@ class SysfsBackend : public Backend {
   std::string describe(const DeviceInfo& dev) override {
     return devs_.at(size_t(dev.index))->gm_ok ? "raw gpu_metrics v1.8 (sysfs)" : "drm sysfs + hwmon";
   }
+  double metrics_period_s(const DeviceInfo& dev) override {
+    return double(devs_.at(size_t(dev.index))->gm.period_ns()) * 1e-9;
+  }
 
   // amdsmi-compatible UUID from the KFD unique_id + PCI device id.
   static std::string uuid_from_unique_id(uint64_t unique_id, uint32_t device_id);

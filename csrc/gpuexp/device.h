@@ -155,6 +155,11 @@ class Backend {
     return false;
   }
   // Human-readable per-device source description (e.g. which metrics path is in use).
+  // Learnt PMFW gpu_metrics refresh period (GpuMetricsReader); 0 = unknown / n/a.
+  virtual double metrics_period_s(const DeviceInfo& dev) {
+    (void)dev;
+    return 0;
+  }
   virtual std::string describe(const DeviceInfo& dev) {
     (void)dev;
     return name();

@@ -219,6 +219,9 @@ void Engine::define_families() {
                               "gpu_metrics reads by kind: fresh (SMU table fetch) or coalesced (cached table, "
                               "PMFW had not refreshed yet)",
                               C, {"gpu", "kind"});
+  f_self_metrics_period_ = add("gpuexp_gpu_metrics_refresh_period_seconds",
+                               "PMFW gpu_metrics refresh period learnt from firmware timestamps (0 = learning)",
+                               G, {"gpu"});
   f_self_ctr_scope_ = add("gpuexp_counters_device_scope",
                           "1 if wave/LDS/HBM PMC counters see every process on the GPU, 0 if they are "
                           "VMID-filtered to the exporter (not exported then)",
@@ -768,6 +771,7 @@ void Engine::emit_self(uint64_t gen) {
       const std::string g = std::to_string(devices_[i].index);
       table_.put(f_self_metrics_reads_, {g, "fresh"}, double(metrics_fresh_[i]), gen);
       table_.put(f_self_metrics_reads_, {g, "coalesced"}, double(metrics_coalesced_[i]), gen);
+      table_.put(f_self_metrics_period_, {g}, backend_->metrics_period_s(devices_[i]), gen);
     }
   table_.put(f_self_source_up_, {"backend:" + std::string(backend_->name())}, 1, gen);
   table_.put(f_self_source_up_, {"sentinel"}, (sentinel_ || (cfg_.enable_sentinel && mock_)) ? 1 : 0, gen);
@@ -966,8 +970,11 @@ EngineStats Engine::stats() {
 }
 
 std::string Engine::source_status() {
-  return std::string("backend=") + (backend_ ? backend_->name() : "none") + " sentinel=" + sentinel_status_ +
-         " counters=" + counters_status_ + " rccl=" + (rccl_ ? cfg_.rccl_dir : "disabled");
+  std::string s = std::string("backend=") + (backend_ ? backend_->name() : "none") + " sentinel=" + sentinel_status_ +
+                  " counters=" + counters_status_ + " rccl=" + (rccl_ ? cfg_.rccl_dir : "disabled");
+  if (backend_)
+    for (const auto& d : devices_) s += " gpu" + std::to_string(d.index) + "=[" + backend_->describe(d) + "]";
+  return s;
 }
 
 }  // namespace gpuexp

@@ -3,7 +3,9 @@
 #include <fcntl.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstring>
+#include <utility>
 
 namespace gpuexp {
 
@@ -72,6 +74,31 @@ GpuMetricsReader::~GpuMetricsReader() {
   if (fd_ >= 0) ::close(fd_);
 }
 
+GpuMetricsReader::GpuMetricsReader(GpuMetricsReader&& o) noexcept { *this = std::move(o); }
+
+GpuMetricsReader& GpuMetricsReader::operator=(GpuMetricsReader&& o) noexcept {
+  if (this == &o) return *this;
+  if (fd_ >= 0) ::close(fd_);
+  fd_ = o.fd_;
+  o.fd_ = -1;
+  path_ = std::move(o.path_);
+  fmt_ = o.fmt_;
+  content_ = o.content_;
+  coalesce_ = o.coalesce_;
+  last_n_ = o.last_n_;
+  last_fw_ts_ = o.last_fw_ts_;
+  t_change_ns_ = o.t_change_ns_;
+  last_read_ns_ = o.last_read_ns_;
+  last_was_fresh_ = o.last_was_fresh_;
+  period_ns_ = o.period_ns_;
+  std::copy(o.steps_, o.steps_ + kSteps, steps_);
+  nsteps_ = o.nsteps_;
+  fresh_reads_ = o.fresh_reads_;
+  coalesced_reads_ = o.coalesced_reads_;
+  std::memcpy(buf_, o.buf_, sizeof(buf_));
+  return *this;
+}
+
 bool GpuMetricsReader::open(const std::string& path, std::string* err) {
   if (fd_ >= 0) ::close(fd_);
   path_ = path;
@@ -104,12 +131,14 @@ bool GpuMetricsReader::read(DeviceSample* out, uint64_t now_ns) {
     out->error = "gpu_metrics not open";
     return false;
   }
-  // Guard: re-read 1.5 ms before the expected refresh so a little jitter in the PMFW
-  // period never costs a whole period of staleness.
+  // Re-read 1.5 ms before the expected refresh so jitter in the PMFW period never costs a
+  // whole period of staleness.
   constexpr uint64_t kGuardNs = 1500000;
-  if (coalesce_ && now_ns && last_n_ > 0 && period_ns_ > kGuardNs && now_ns >= t_change_ns_ &&
-      now_ns < t_change_ns_ + period_ns_ - kGuardNs) {
+  const uint64_t window = std::min(period_ns_, kMaxCoalesceNs);
+  if (coalesce_ && now_ns && last_n_ > 0 && window > kGuardNs && t_change_ns_ && now_ns >= t_change_ns_ &&
+      now_ns < t_change_ns_ + window - kGuardNs) {
     coalesced_reads_ += 1;
+    last_was_fresh_ = false;
     out->metrics_coalesced = true;
     return decode_gpu_metrics_v1_8(buf_, size_t(last_n_), out);
   }
@@ -127,18 +156,24 @@ bool GpuMetricsReader::read(DeviceSample* out, uint64_t now_ns) {
     return false;
   }
   if (out->fw_ts_10ns && out->fw_ts_10ns != last_fw_ts_) {
-    if (last_fw_ts_ && out->fw_ts_10ns > last_fw_ts_) {
-      const uint64_t step = (out->fw_ts_10ns - last_fw_ts_) * 10;
-      // Only single-period steps teach the period (a longer tick spans several tables).
-      if (period_ns_ == 0 || step < period_ns_ * 3 / 2) {
-        period_ns_ = period_ns_ ? (period_ns_ * 3 + step) / 4 : step;
-        changes_ += 1;
+    const bool bracketed = last_was_fresh_ && last_read_ns_ && now_ns > last_read_ns_;
+    if (bracketed && last_fw_ts_ && out->fw_ts_10ns > last_fw_ts_) {
+      steps_[nsteps_ % kSteps] = (out->fw_ts_10ns - last_fw_ts_) * 10;
+      nsteps_ += 1;
+      if (nsteps_ >= 5) {
+        const int k = std::min(nsteps_, kSteps);
+        uint64_t tmp[kSteps];
+        std::copy(steps_, steps_ + k, tmp);
+        std::nth_element(tmp, tmp + k / 2, tmp + k);
+        period_ns_ = tmp[k / 2];
       }
     }
     last_fw_ts_ = out->fw_ts_10ns;
-    t_change_ns_ = now_ns;
+    // The table appeared between the previous fresh read and this one: take the midpoint.
+    t_change_ns_ = bracketed ? last_read_ns_ + (now_ns - last_read_ns_) / 2 : now_ns;
   }
-  if (changes_ < 2) t_change_ns_ = 0;  // still learning the period: keep reading
+  last_read_ns_ = now_ns;
+  last_was_fresh_ = true;
   return true;
 }
 

@@ -105,7 +105,13 @@ bool decode_gpu_metrics_v1_8(const void* blob, size_t len, DeviceSample* out);
 // lost, the kernel-side cost drops to the PMFW rate.
 class GpuMetricsReader {
  public:
+  GpuMetricsReader() = default;
   ~GpuMetricsReader();
+  // Owns its fd: move-only (a copy would close the fd under the other copy's feet).
+  GpuMetricsReader(const GpuMetricsReader&) = delete;
+  GpuMetricsReader& operator=(const GpuMetricsReader&) = delete;
+  GpuMetricsReader(GpuMetricsReader&& o) noexcept;
+  GpuMetricsReader& operator=(GpuMetricsReader&& o) noexcept;
   bool open(const std::string& path, std::string* err);
   // Reads (or re-decodes the cached table, see above) at host time `now_ns` (0 = always
   // read).  Returns false (and sets out->error) on I/O or format error.
@@ -115,6 +121,8 @@ class GpuMetricsReader {
   uint8_t content() const { return content_; }
   const std::string& path() const { return path_; }
   void set_coalesce(bool on) { coalesce_ = on; }
+  // Never reuse a table for longer than this, whatever the learnt period.
+  static constexpr uint64_t kMaxCoalesceNs = 50000000;
   uint64_t period_ns() const { return period_ns_; }
   uint64_t fresh_reads() const { return fresh_reads_; }
   uint64_t coalesced_reads() const { return coalesced_reads_; }
@@ -126,9 +134,15 @@ class GpuMetricsReader {
   bool coalesce_ = true;
   long last_n_ = 0;
   uint64_t last_fw_ts_ = 0;      // firmware_timestamp of the cached table (10 ns units)
-  uint64_t t_change_ns_ = 0;     // host time a new table was first seen
+  uint64_t t_change_ns_ = 0;     // estimated host time the cached table appeared
+  uint64_t last_read_ns_ = 0;    // host time of the last fresh read
+  bool last_was_fresh_ = false;  // no coalesced read since the previous fresh one
   uint64_t period_ns_ = 0;       // learnt PMFW refresh period (0 = unknown)
-  int changes_ = 0;
+  // Table-to-table steps seen by back-to-back fresh reads; the period is their median
+  // (a startup gap or a missed table is an outlier, not the estimate).
+  static constexpr int kSteps = 16;
+  uint64_t steps_[kSteps] = {};
+  int nsteps_ = 0;
   uint64_t fresh_reads_ = 0, coalesced_reads_ = 0;
   alignas(8) unsigned char buf_[8192];
 };

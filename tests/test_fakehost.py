@@ -254,3 +254,32 @@ def test_gpu_metrics_coalescing_can_be_disabled(native, tmp_path):
         e.tick(1 * S + k * 10_000_000)
     assert _reads(promtext.parse(e.snapshot_text())) == {"fresh": 20, "coalesced": 0}
     e.stop()
+
+
+def test_coalescing_ignores_startup_gap_and_caps_staleness(native, tmp_path):
+    """A long gap before the first regular tick (start-up) must not be learnt as the
+    refresh period: after it, still <= ~half the 100 Hz reads are coalesced and no table
+    is exported more than one tick late."""
+    h = mi355x_node(tmp_path, 1)
+    (g,) = h.gpus
+    e = _engine(native, tmp_path)
+    ms = 1_000_000
+    base = 105165583750064
+    h.set_metrics(g, fw_ts=base, power=100)
+    e.tick(1 * S)                       # first tick, then 300 ms of nothing
+    seen, expect = [], []
+    for k in range(100):                # then 100 Hz, tables every 20 ms
+        now = 1 * S + 300 * ms + k * 10 * ms
+        table = 15 + k // 2             # 300 ms = 15 tables later
+        h.set_metrics(g, fw_ts=base + table * 2_000_000, power=100 + table)
+        e.tick(now)
+        seen.append(promtext.samples(promtext.parse(e.snapshot_text()), "amd_gpu_power_watts")[0][2])
+        expect.append(100 + table)
+    fams = promtext.parse(e.snapshot_text())
+    reads = _reads(fams)
+    assert reads["coalesced"] <= 55, reads
+    assert reads["coalesced"] >= 35, reads
+    assert all(s >= x - 1 for s, x in zip(seen, expect)), list(zip(seen, expect))
+    (period,) = [s[2] for s in promtext.samples(fams, "gpuexp_gpu_metrics_refresh_period_seconds")]
+    assert abs(period - 0.020) < 1e-6
+    e.stop()

@@ -222,3 +222,25 @@ def test_gemm_pod_model_on_gpu(native):
     torch.testing.assert_close(p.c.float(), ref, atol=0.05, rtol=0.02)
     big = run(GemmPod(size=4096, iters=8), steps=3, warmup=1)
     assert big["tflops"] > 100, big
+
+
+def test_raw_metrics_path_and_pmfw_coalescing(native):
+    """The amdsmi backend reads gpu_metrics raw (no silent library fallback) and, at
+    100 Hz, learns the ~20 ms PMFW refresh and skips the SMU fetch in between."""
+    c = native.EngineConfig()
+    c.backend = "amdsmi"
+    c.interval_s = 0.01
+    c.serve_http = False
+    c.device_filter = [0]
+    e = native.Engine(c)
+    e.start()
+    time.sleep(2.0)
+    fams = promtext.parse(e.snapshot_text())
+    status = e.source_status()
+    e.stop()
+    assert "raw gpu_metrics v1.8 (validated against amdsmi)" in status, status
+    reads = {s[1]["kind"]: s[2] for s in promtext.samples(fams, "gpuexp_gpu_metrics_reads_total")}
+    frac = reads["coalesced"] / (reads["fresh"] + reads["coalesced"])
+    assert 0.3 < frac < 0.6, reads  # ~half at 100 Hz vs a 20 ms PMFW refresh; never most
+    (period,) = [s[2] for s in promtext.samples(fams, "gpuexp_gpu_metrics_refresh_period_seconds")]
+    assert 0.015 < period < 0.03, period
