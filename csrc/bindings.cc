@@ -298,6 +298,7 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("infer_device_owner", &EngineConfig::infer_device_owner)
       .def_readwrite("process_source", &EngineConfig::process_source)
       .def_readwrite("kfd_cu_occupancy", &EngineConfig::kfd_cu_occupancy)
+      .def_readwrite("kfd_detail_interval_s", &EngineConfig::kfd_detail_interval_s)
       .def_readwrite("exclude_self", &EngineConfig::exclude_self)
       .def_readwrite("enable_sentinel", &EngineConfig::enable_sentinel)
       .def_readwrite("sentinel_ring", &EngineConfig::sentinel_ring)

@@ -273,7 +273,8 @@ bool Engine::start(std::string* err) {
   int nthreads = cfg_.device_threads;
   if (nthreads <= 0) nthreads = cfg_.backend == "mock" ? 1 : std::min<int>(int(devices_.size()), 8);
   if (nthreads > 1) pool_ = std::make_unique<ForkJoinPool>(nthreads);
-  kfd_ = std::make_unique<KfdProcReader>(cfg_.host_root, cfg_.exclude_self ? self_pid_ : -1, cfg_.kfd_cu_occupancy);
+  kfd_ = std::make_unique<KfdProcReader>(cfg_.host_root, cfg_.exclude_self ? self_pid_ : -1, cfg_.kfd_cu_occupancy,
+                                         uint64_t(cfg_.kfd_detail_interval_s * 1e9));
   resolver_ = std::make_unique<PidResolver>(cfg_.host_root);
 
   // Counters first: the rocprofiler tool must register before the HSA runtime loads,
@@ -859,7 +860,7 @@ void Engine::tick_locked(uint64_t now) {
           break;
         }
     if (!from_backend) {
-      kfd_->scan(devices_, &per_dev);
+      kfd_->scan(devices_, &per_dev, now);
     } else if (cfg_.exclude_self) {
       for (auto& l : per_dev)
         l.erase(std::remove_if(l.begin(), l.end(), [this](const ProcSample& p) { return p.pid == self_pid_; }),

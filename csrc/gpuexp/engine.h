@@ -70,6 +70,7 @@ struct EngineConfig {
   bool infer_device_owner = true;      // single-pod GPU -> device series carry the pod
   std::string process_source = "auto";  // auto | kfd | amdsmi | none
   bool kfd_cu_occupancy = true;
+  double kfd_detail_interval_s = 1.0;  // cu_occupancy / sdma re-read period (0 = every tick)
   bool exclude_self = true;
   bool enable_sentinel = false;
   int sentinel_ring = 64;

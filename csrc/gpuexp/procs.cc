@@ -7,13 +7,15 @@
 
 namespace gpuexp {
 
-KfdProcReader::KfdProcReader(std::string host_root, int self_pid, bool read_cu_occupancy)
-    : root_(std::move(host_root)), self_(self_pid), read_cu_(read_cu_occupancy) {
+KfdProcReader::KfdProcReader(std::string host_root, int self_pid, bool read_cu_occupancy,
+                             uint64_t detail_interval_ns)
+    : root_(std::move(host_root)), self_(self_pid), read_cu_(read_cu_occupancy),
+      detail_every_ns_(detail_interval_ns) {
   if (!root_.empty() && root_.back() == '/') root_.pop_back();
 }
 
 void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
-                         std::vector<std::vector<ProcSample>>* per_dev) {
+                         std::vector<std::vector<ProcSample>>* per_dev, uint64_t now_ns) {
   per_dev->assign(devs.size(), {});
   ++scan_no_;
   const std::string base = root_ + "/sys/class/kfd/kfd/proc";
@@ -49,11 +51,17 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
       ps.pid = pid;
       ps.device = pd.dev;
       ps.vram_bytes = double(v);
-      long n;
-      if (pd.cu.is_open() && (n = pd.cu.read(buf, sizeof(buf) - 1)) > 0 && parse_u64(buf, size_t(n), &v))
-        ps.cu_occupancy = double(v);
-      if (pd.sdma.is_open() && (n = pd.sdma.read(buf, sizeof(buf) - 1)) > 0 && parse_u64(buf, size_t(n), &v))
-        ps.sdma_us = double(v);
+      if (!pd.detail_read || !now_ns || detail_every_ns_ == 0 || now_ns - pd.detail_ns >= detail_every_ns_) {
+        long n;
+        if (pd.cu.is_open() && (n = pd.cu.read(buf, sizeof(buf) - 1)) > 0 && parse_u64(buf, size_t(n), &v))
+          pd.cu_last = double(v);
+        if (pd.sdma.is_open() && (n = pd.sdma.read(buf, sizeof(buf) - 1)) > 0 && parse_u64(buf, size_t(n), &v))
+          pd.sdma_last = double(v);
+        pd.detail_ns = now_ns;
+        pd.detail_read = true;
+      }
+      ps.cu_occupancy = pd.cu_last;
+      ps.sdma_us = pd.sdma_last;
       ps.name = e.comm;
       (*per_dev)[size_t(pd.dev)].push_back(ps);
     }

@@ -21,15 +21,23 @@ namespace gpuexp {
 
 class KfdProcReader {
  public:
-  KfdProcReader(std::string host_root, int self_pid, bool read_cu_occupancy);
+  // detail_interval_ns: cu_occupancy / sdma are re-read at most this often (0 = every
+  // scan).  Measured on MI355X (profiles/r01/kfd_read_costs.txt): vram_<id> ~6 us,
+  // stats_<id>/cu_occupancy ~15 us (KFD asks the hardware), sdma_<id> ~7 us per process
+  // per GPU — VRAM is what the legacy families and attribution need every tick.
+  KfdProcReader(std::string host_root, int self_pid, bool read_cu_occupancy, uint64_t detail_interval_ns = 0);
   // Fills per_dev[d] with the processes that have a KFD context on device d.
-  void scan(const std::vector<DeviceInfo>& devs, std::vector<std::vector<ProcSample>>* per_dev);
+  void scan(const std::vector<DeviceInfo>& devs, std::vector<std::vector<ProcSample>>* per_dev,
+            uint64_t now_ns = 0);
   size_t tracked() const { return pids_.size(); }
 
  private:
   struct PerDev {
     int dev = -1;
     CachedFile vram, cu, sdma;
+    double cu_last = kNaN, sdma_last = kNaN;
+    uint64_t detail_ns = 0;  // last cu/sdma read
+    bool detail_read = false;
   };
   struct Entry {
     std::vector<PerDev> devs;
@@ -39,6 +47,7 @@ class KfdProcReader {
   std::string root_;
   int self_;
   bool read_cu_;
+  uint64_t detail_every_ns_;
   uint64_t scan_no_ = 0;
   std::unordered_map<int, Entry> pids_;
 };

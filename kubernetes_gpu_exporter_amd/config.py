@@ -36,6 +36,7 @@ class Config:
     legacy_families: bool = True           # pod_gpu_memory_usage / docker_gpu_memory_perc_usage
     process_source: str = "auto"           # auto | kfd | amdsmi | none
     kfd_cu_occupancy: bool = True
+    kfd_detail_interval: float = 1.0       # seconds between cu_occupancy / sdma re-reads (0 = every tick)
     gc_after: int = 1
     # optional sources
     enable_sentinel: bool = False
@@ -99,6 +100,7 @@ class Config:
         ec.infer_device_owner = bool(self.infer_device_owner)
         ec.process_source = self.process_source
         ec.kfd_cu_occupancy = bool(self.kfd_cu_occupancy)
+        ec.kfd_detail_interval_s = float(self.kfd_detail_interval)
         ec.enable_sentinel = bool(self.enable_sentinel)
         ec.sentinel_spin = int(self.sentinel_spin)
         ec.enable_counters = bool(self.enable_counters)

@@ -283,3 +283,25 @@ def test_coalescing_ignores_startup_gap_and_caps_staleness(native, tmp_path):
     (period,) = [s[2] for s in promtext.samples(fams, "gpuexp_gpu_metrics_refresh_period_seconds")]
     assert abs(period - 0.020) < 1e-6
     e.stop()
+
+
+def test_kfd_detail_files_are_rate_limited(native, tmp_path):
+    """vram_<id> is read every tick; cu_occupancy / sdma at most every
+    kfd_detail_interval_s, re-exporting the cached values in between."""
+    h = mi355x_node(tmp_path, 1)
+    (g,) = h.gpus
+    h.add_process(777, kubepods_cgroup(UID, CID), gpus={g.gpu_id: (1000, 10)})
+    e = _engine(native, tmp_path, kfd_detail_interval_s=1.0)
+
+    def proc(name):
+        return {s[1]["pid"]: s[2] for s in promtext.samples(promtext.parse(e.snapshot_text()), name)}
+
+    e.tick(1 * S)
+    assert proc("amd_gpu_process_cu_occupancy") == {"777": 10}
+    h.set_process_gpu(777, g.gpu_id, vram=2000, cu=99)
+    e.tick(1 * S + 100_000_000)           # 100 ms later: vram fresh, cu cached
+    assert proc("amd_gpu_process_vram_bytes") == {"777": 2000}
+    assert proc("amd_gpu_process_cu_occupancy") == {"777": 10}
+    e.tick(2 * S + 100_000_000)           # past the interval: cu re-read
+    assert proc("amd_gpu_process_cu_occupancy") == {"777": 99}
+    e.stop()
