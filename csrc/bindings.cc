@@ -93,6 +93,7 @@ ProcSample proc_from_dict(const py::dict& d) {
   p.vram_bytes = d.contains("vram_bytes") ? d["vram_bytes"].cast<double>() : 0.0;
   p.cu_occupancy = d.contains("cu_occupancy") ? d["cu_occupancy"].cast<double>() : kNaN;
   p.sdma_us = d.contains("sdma_us") ? d["sdma_us"].cast<double>() : kNaN;
+  p.evicted_ms = d.contains("evicted_ms") ? d["evicted_ms"].cast<double>() : kNaN;
   p.name = d.contains("name") ? d["name"].cast<std::string>() : "";
   return p;
 }

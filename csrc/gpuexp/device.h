@@ -99,6 +99,7 @@ struct ProcSample {
   double vram_bytes = 0;
   double cu_occupancy = kNaN;  // CUs (KFD stats_<id>/cu_occupancy)
   double sdma_us = kNaN;       // accumulated SDMA usage (us)
+  double evicted_ms = kNaN;    // accumulated time the process's queues were evicted (KFD stats)
   double gfx_ns = kNaN;        // engine time (amdsmi)
   std::string name;            // comm
 };

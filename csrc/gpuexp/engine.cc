@@ -180,6 +180,8 @@ void Engine::define_families() {
   f_proc_vram_ = add("amd_gpu_process_vram_bytes", "VRAM held by a process on a GPU (KFD)", G, P);
   f_proc_cu_ = add("amd_gpu_process_cu_occupancy", "CUs occupied by a process on a GPU (KFD)", G, P);
   f_proc_sdma_ = add("amd_gpu_process_sdma_seconds_total", "SDMA engine time used by a process", C, P);
+  f_proc_evicted_ = add("amd_gpu_process_evicted_seconds_total",
+                        "Time the process's GPU queues were evicted (memory pressure / preemption; KFD stats)", C, P);
   if (cfg_.legacy_families) {
     // Byte-compatible with the reference (/root/reference/main.go:22-35): names, HELP,
     // label names and order {pid, pod}.  `pid` is the host PID (the reference's intended
@@ -658,6 +660,7 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
         table_.put(f_proc_vram_, L, p.vram_bytes, gen);
         if (!std::isnan(p.cu_occupancy)) table_.put(f_proc_cu_, L, p.cu_occupancy, gen);
         if (!std::isnan(p.sdma_us)) table_.put(f_proc_sdma_, L, p.sdma_us * 1e-6, gen);
+        if (!std::isnan(p.evicted_ms)) table_.put(f_proc_evicted_, L, p.evicted_ms * 1e-3, gen);
       }
       if (!a.pod.empty()) {
         auto& la = legacy[p.pid];

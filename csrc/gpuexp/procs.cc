@@ -36,6 +36,7 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
         if (!pd.vram.open(pdir + "/vram_" + id)) continue;
         if (read_cu_) pd.cu.open(pdir + "/stats_" + id + "/cu_occupancy");
         pd.sdma.open(pdir + "/sdma_" + id);
+        pd.evicted.open(pdir + "/stats_" + id + "/evicted_ms");
         e.devs.push_back(std::move(pd));
       }
       std::string comm;
@@ -57,11 +58,15 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
           pd.cu_last = double(v);
         if (pd.sdma.is_open() && (n = pd.sdma.read(buf, sizeof(buf) - 1)) > 0 && parse_u64(buf, size_t(n), &v))
           pd.sdma_last = double(v);
+        if (pd.evicted.is_open() && (n = pd.evicted.read(buf, sizeof(buf) - 1)) > 0 &&
+            parse_u64(buf, size_t(n), &v))
+          pd.evicted_last = double(v);
         pd.detail_ns = now_ns;
         pd.detail_read = true;
       }
       ps.cu_occupancy = pd.cu_last;
       ps.sdma_us = pd.sdma_last;
+      ps.evicted_ms = pd.evicted_last;
       ps.name = e.comm;
       (*per_dev)[size_t(pd.dev)].push_back(ps);
     }

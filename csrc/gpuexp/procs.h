@@ -34,8 +34,8 @@ class KfdProcReader {
  private:
   struct PerDev {
     int dev = -1;
-    CachedFile vram, cu, sdma;
-    double cu_last = kNaN, sdma_last = kNaN;
+    CachedFile vram, cu, sdma, evicted;
+    double cu_last = kNaN, sdma_last = kNaN, evicted_last = kNaN;
     uint64_t detail_ns = 0;  // last cu/sdma read
     bool detail_read = false;
   };

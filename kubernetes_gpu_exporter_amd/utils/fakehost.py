@@ -133,11 +133,13 @@ class FakeHost:
         for gid, (vram, cu) in (gpus or {}).items():
             self.set_process_gpu(pid, gid, vram, cu)
 
-    def set_process_gpu(self, pid: int, gpu_id: int, vram: int, cu: int = 0, sdma_us: int = 0) -> None:
+    def set_process_gpu(self, pid: int, gpu_id: int, vram: int, cu: int = 0, sdma_us: int = 0,
+                        evicted_ms: int = 0) -> None:
         pd = f"sys/class/kfd/kfd/proc/{pid}"
         self._w(f"{pd}/vram_{gpu_id}", f"{vram}\n")
         self._w(f"{pd}/sdma_{gpu_id}", f"{sdma_us}\n")
         self._w(f"{pd}/stats_{gpu_id}/cu_occupancy", f"{cu}\n")
+        self._w(f"{pd}/stats_{gpu_id}/evicted_ms", f"{evicted_ms}\n")
         self._w(f"{pd}/pasid", "32769\n")
 
     def remove_process(self, pid: int) -> None:

@@ -304,4 +304,7 @@ def test_kfd_detail_files_are_rate_limited(native, tmp_path):
     assert proc("amd_gpu_process_cu_occupancy") == {"777": 10}
     e.tick(2 * S + 100_000_000)           # past the interval: cu re-read
     assert proc("amd_gpu_process_cu_occupancy") == {"777": 99}
+    h.set_process_gpu(777, g.gpu_id, vram=2000, cu=99, evicted_ms=1500)
+    e.tick(3 * S + 200_000_000)
+    assert proc("amd_gpu_process_evicted_seconds_total") == {"777": 1.5}
     e.stop()

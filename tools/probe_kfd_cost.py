@@ -57,6 +57,20 @@ def main() -> int:
                     ent[f"{f}/{sub}"] = timed(lambda q=f"{p}/{sub}": read(q), reps)
                     ent[f"{f}/{sub}:value"] = read(f"{p}/{sub}").decode(errors="replace").strip()
         out[pid] = ent
+    # DRM fdinfo of the GEMM child's render-node fds: does KFD compute show up in
+    # drm-engine-* (it does not go through the DRM scheduler)?
+    fdi = {}
+    try:
+        for fd in os.listdir(f"/proc/{child.pid}/fd"):
+            try:
+                tgt = os.readlink(f"/proc/{child.pid}/fd/{fd}")
+            except OSError:
+                continue
+            if tgt.startswith("/dev/dri/") or tgt == "/dev/kfd":
+                fdi[f"{fd}->{tgt}"] = read(f"/proc/{child.pid}/fdinfo/{fd}").decode(errors="replace")
+    except OSError as ex:
+        fdi["error"] = str(ex)
+    out["gemm_child_fdinfo"] = fdi
     child.kill()
     child.wait()
     print("RESULT " + json.dumps(out))
