@@ -6,7 +6,7 @@ timeout, on the collection path.  Here metadata is refreshed off the sampling pa
 low rate, only pushed when it changed, with per-source timeouts and error isolation:
 
   PodResourcesSource  kubelet gRPC  -> device (BDF/UUID) -> owning pod/container
-  ApiserverSource     node-scoped pod list -> pod UID -> namespace/name, container IDs
+  ApiserverSource     node-scoped list + watch -> pod UID -> namespace/name, container IDs
   LogdirSource        /var/log/pods/<ns>_<pod>_<uid>  (zero-RBAC fallback)
   FileSource          JSON map (tests, bench, non-Kubernetes schedulers)
 """
@@ -49,6 +49,9 @@ class Source:
 
     def fetch(self) -> Metadata:  # pragma: no cover - interface
         raise NotImplementedError
+
+    def close(self) -> None:
+        """Releases background resources (watch threads, channels)."""
 
 
 class ControlPlane:
@@ -93,7 +96,12 @@ class ControlPlane:
         for s in self.sources:
             try:
                 md.merge(s.fetch())
-                self.errors.pop(s.name, None)
+                # a source may keep serving its cache while its background loop fails
+                err = getattr(s, "last_error", None)
+                if err:
+                    self.errors[s.name] = err
+                else:
+                    self.errors.pop(s.name, None)
             except Exception as e:  # one failing source never blocks the others
                 self.errors[s.name] = repr(e)
                 log.warning("source %s failed: %r", s.name, e)
@@ -126,3 +134,8 @@ class ControlPlane:
         self._stop.set()
         if self._thread is not None:
             self._thread.join(timeout=5)
+        for s in self.sources:
+            try:
+                s.close()
+            except Exception as e:  # pragma: no cover - best effort at shutdown
+                log.warning("closing source %s: %r", s.name, e)

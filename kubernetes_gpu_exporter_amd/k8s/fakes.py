@@ -2,8 +2,9 @@
 
 FakeKubelet    — PodResources v1 gRPC server on a unix socket (same wire format as the
                  kubelet: `/v1.PodResourcesLister/List`).
-FakeApiserver  — HTTP server for GET /api/v1/pods with fieldSelector=spec.nodeName and
-                 bearer-token auth, returning PodList JSON shaped like the real thing.
+FakeApiserver  — HTTP server for GET /api/v1/pods (list and ?watch=1 event stream) with
+                 fieldSelector=spec.nodeName, bearer-token auth, resourceVersions,
+                 bookmarks and 410-Gone injection, shaped like the real thing.
 FakePod        — one pod: uid, namespace, name, node, containers {name: container_id},
                  GPUs {container_name: [device_ids]}.
 """
@@ -110,16 +111,58 @@ class FakeKubelet:
 
 
 class FakeApiserver:
+    """GET /api/v1/pods (list) and ?watch=1 (streaming events), node fieldSelector, bearer
+    auth.  Mutate through add_pod / update_pod / delete_pod so watchers get events with
+    increasing resourceVersions.  `fail_status` makes every request fail; `expire_before`
+    answers watches from an older resourceVersion with 410 Gone (compacted history)."""
+
     def __init__(self, pods: list[FakePod] | None = None, token: str = "test-token"):
         self.pods = list(pods or [])
         self.token = token
         self.fail_status = 0
         self.requests: list[str] = []
+        self.rv = 1
+        self.expire_before = 0
+        self._events: list[tuple[int, str, FakePod]] = []  # (rv, type, pod)
+        self._cond = threading.Condition()
+        self._stopping = False
         self._httpd = None
         self._thread = None
 
+    # --- mutations (emit watch events) ---
+    def _emit(self, typ: str, pod: FakePod) -> None:
+        with self._cond:
+            self.rv += 1
+            self._events.append((self.rv, typ, pod))
+            self._cond.notify_all()
+
+    def add_pod(self, pod: FakePod) -> None:
+        self.pods.append(pod)
+        self._emit("ADDED", pod)
+
+    def update_pod(self, pod: FakePod) -> None:
+        self.pods = [pod if p.uid == pod.uid else p for p in self.pods]
+        self._emit("MODIFIED", pod)
+
+    def delete_pod(self, uid: str) -> None:
+        gone = [p for p in self.pods if p.uid == uid]
+        self.pods = [p for p in self.pods if p.uid != uid]
+        for p in gone:
+            self._emit("DELETED", p)
+
+    def bookmark(self) -> None:
+        with self._cond:
+            self.rv += 1
+            self._events.append((self.rv, "BOOKMARK", None))
+            self._cond.notify_all()
+
     def _handler(self):
         fake = self
+
+        def obj_json(pod: FakePod, rv: int) -> dict:
+            o = pod.to_json()
+            o["metadata"]["resourceVersion"] = str(rv)
+            return o
 
         class H(BaseHTTPRequestHandler):
             def log_message(self, *a):
@@ -147,19 +190,56 @@ class FakeApiserver:
                         k, _, v = term.partition("=")
                         if k == "spec.nodeName":
                             node = v
-                items = [p.to_json() for p in fake.pods if node is None or p.node == node]
+                if q.get("watch", ["0"])[0] in ("1", "true"):
+                    return self._watch(q, node)
+                items = [obj_json(p, fake.rv) for p in fake.pods if node is None or p.node == node]
                 body = json.dumps({"kind": "PodList", "apiVersion": "v1",
-                                   "metadata": {"resourceVersion": "1"}, "items": items}).encode()
+                                   "metadata": {"resourceVersion": str(fake.rv)}, "items": items}).encode()
                 self.send_response(200)
                 self.send_header("Content-Type", "application/json")
                 self.send_header("Content-Length", str(len(body)))
                 self.end_headers()
                 self.wfile.write(body)
 
+            def _watch(self, q, node):
+                import time
+                since = int(q.get("resourceVersion", ["0"])[0] or 0)
+                deadline = time.monotonic() + float(q.get("timeoutSeconds", ["5"])[0])
+                self.send_response(200)
+                self.send_header("Content-Type", "application/json")
+                self.end_headers()  # HTTP/1.0: the stream ends when the connection closes
+                if since < fake.expire_before:
+                    ev = {"type": "ERROR", "object": {"kind": "Status", "code": 410, "reason": "Expired",
+                                                      "message": "too old resource version"}}
+                    self.wfile.write((json.dumps(ev) + "\n").encode())
+                    return
+                sent = since
+                try:
+                    while time.monotonic() < deadline and not fake._stopping and not fake.fail_status:
+                        with fake._cond:
+                            pending = [e for e in fake._events if e[0] > sent]
+                            if not pending:
+                                fake._cond.wait(0.05)
+                                continue
+                        for rv, typ, pod in pending:
+                            sent = rv
+                            if typ == "BOOKMARK":
+                                ev = {"type": typ, "object": {"kind": "Pod", "metadata": {"resourceVersion": str(rv)}}}
+                            elif node is not None and pod.node != node:
+                                continue
+                            else:
+                                ev = {"type": typ, "object": obj_json(pod, rv)}
+                            self.wfile.write((json.dumps(ev) + "\n").encode())
+                            self.wfile.flush()
+                except (BrokenPipeError, ConnectionResetError):
+                    pass
+
         return H
 
     def start(self) -> "FakeApiserver":
         self._httpd = ThreadingHTTPServer(("127.0.0.1", 0), self._handler())
+        self._httpd.daemon_threads = True
+        self._httpd.block_on_close = False
         self._thread = threading.Thread(target=self._httpd.serve_forever, daemon=True)
         self._thread.start()
         return self
@@ -170,6 +250,9 @@ class FakeApiserver:
 
     def stop(self) -> None:
         if self._httpd is not None:
+            with self._cond:
+                self._stopping = True  # open watch streams end
+                self._cond.notify_all()
             self._httpd.shutdown()
             self._httpd.server_close()
             self._httpd = None

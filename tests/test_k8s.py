@@ -71,14 +71,14 @@ def test_apiserver_node_scoped(tmp_path):
     tok = tmp_path / "token"
     tok.write_text("s3cret\n")
     try:
-        md = ApiserverSource(api.url, "node-a", str(tok)).fetch()
+        md = ApiserverSource(api.url, "node-a", str(tok), watch=False).fetch()
         assert set(md.pods) == {UID_A, UID_B}  # node-b pod excluded (reference listed ALL pods)
         assert md.pods[UID_B]["containers"][CID_B] == "server"
         assert md.pods[UID_A]["namespace"] == "research"
         assert "fieldSelector=spec.nodeName%3Dnode-a" in api.requests[-1]
         assert "resourceVersion=0" in api.requests[-1]
         with pytest.raises(Exception):
-            ApiserverSource(api.url, "node-a", "").fetch()  # no token -> 401
+            ApiserverSource(api.url, "node-a", "", watch=False).fetch()  # no token -> 401
     finally:
         api.stop()
 
@@ -177,10 +177,87 @@ def test_full_exporter_on_fake_node(tmp_path):
         assert promtext.value(fams, "amd_gpu_process_vram_bytes", pid=1002, container="server") == 20 << 30
         # apiserver outage: last known metadata keeps attribution working
         api.fail_status = 503
-        ex._control.refresh_once()
-        assert "apiserver" in ex._control.errors
+        assert _wait(lambda: ex._control.refresh_once() is not None and "apiserver" in ex._control.errors)
+        ex.tick(10_000_000_000)
+        fams = promtext.parse(ex.text())
+        assert promtext.value(fams, "pod_gpu_memory_usage", pid=1002, pod="vllm-0") == 20 << 30
     finally:
         ex.stop()
         kub.stop()
         api.stop()
         request_cleanup()
+
+
+def _wait(pred, timeout=5.0):
+    import time
+    t = time.monotonic() + timeout
+    while time.monotonic() < t:
+        if pred():
+            return True
+        time.sleep(0.02)
+    return False
+
+
+def test_apiserver_list_then_watch(tmp_path):
+    """One list, then events over a single watch: refreshes cost no requests; ADDED /
+    MODIFIED / DELETED land in the cache; other nodes' events are filtered server-side."""
+    api = FakeApiserver(pods(), token="").start()
+    src = ApiserverSource(api.url, "node-a", "", watch_timeout_s=30)
+    try:
+        assert set(src.fetch().pods) == {UID_A, UID_B}
+        assert _wait(lambda: any("watch=1" in r for r in api.requests))
+        n_req = len(api.requests)
+        new_uid = "99999999-8888-7777-6666-555555555555"
+        api.add_pod(FakePod(new_uid, "team", "late-pod", node="node-a", containers={"c": "e" * 64}))
+        api.add_pod(FakePod("11111111-0000-0000-0000-000000000000", "x", "elsewhere", node="node-b"))
+        assert _wait(lambda: new_uid in src.fetch().pods)
+        assert src.fetch().pods[new_uid]["containers"] == {"e" * 64: "c"}
+        api.update_pod(FakePod(new_uid, "team", "late-pod", node="node-a", containers={"c": "f" * 64}))
+        assert _wait(lambda: src.fetch().pods[new_uid]["containers"] == {"f" * 64: "c"})
+        api.delete_pod(UID_A)
+        assert _wait(lambda: UID_A not in src.fetch().pods)
+        assert "11111111-0000-0000-0000-000000000000" not in src.fetch().pods
+        for _ in range(20):
+            src.fetch()
+        assert len(api.requests) == n_req  # every refresh above was served from the cache
+        assert src.relists == 1
+    finally:
+        src.close()
+        api.stop()
+
+
+def test_apiserver_watch_resumes_and_relists_on_410(tmp_path):
+    api = FakeApiserver(pods(), token="").start()
+    src = ApiserverSource(api.url, "node-a", "", watch_timeout_s=1)  # server ends each watch after 1 s
+    try:
+        src.fetch()
+        assert _wait(lambda: sum("watch=1" in r for r in api.requests) >= 2, timeout=6)  # resumed
+        assert src.relists == 1
+        api.expire_before = api.rv + 100          # history compacted: next resume gets 410
+        api.bookmark()
+        assert _wait(lambda: src.relists >= 2, timeout=6)
+        api.expire_before = 0
+        late = "abababab-0000-0000-0000-000000000000"
+        api.add_pod(FakePod(late, "ns", "after-relist", node="node-a"))
+        assert _wait(lambda: late in src.fetch().pods, timeout=6)
+    finally:
+        src.close()
+        api.stop()
+
+
+def test_apiserver_outage_keeps_cache_and_recovers(tmp_path):
+    api = FakeApiserver(pods(), token="").start()
+    src = ApiserverSource(api.url, "node-a", "", watch_timeout_s=1)
+    try:
+        src.fetch()
+        api.fail_status = 503
+        import time
+        time.sleep(1.5)                           # watch ends, reconnects fail with 503
+        assert set(src.fetch().pods) == {UID_A, UID_B}  # stale cache, not an empty map
+        api.fail_status = 0
+        late = "cdcdcdcd-0000-0000-0000-000000000000"
+        api.add_pod(FakePod(late, "ns", "after-outage", node="node-a"))
+        assert _wait(lambda: late in src.fetch().pods, timeout=10)
+    finally:
+        src.close()
+        api.stop()
