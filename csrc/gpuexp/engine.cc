@@ -932,8 +932,15 @@ void Engine::tick_locked(uint64_t now) {
     ts[7] = mono_ns();
     // 7: gzip (only while clients ask for it) + publish
     snap->gz.clear();
-    if (http_ && http_->gzip_wanted_ns() && mono_ns() - http_->gzip_wanted_ns() < 60000000000ull)
-      gzip_compress(snap->body, &snap->gz, cfg_.gzip_level);
+    snap->pb.clear();
+    snap->pb_gz.clear();
+    const uint64_t tnow = mono_ns();
+    const bool want_gz = http_ && http_->gzip_wanted_ns() && tnow - http_->gzip_wanted_ns() < 60000000000ull;
+    if (want_gz) gzip_compress(snap->body, &snap->gz, cfg_.gzip_level);
+    if (http_ && http_->proto_wanted_ns() && tnow - http_->proto_wanted_ns() < 60000000000ull) {
+      table_.render_proto(&snap->pb, gen);
+      if (want_gz) gzip_compress(snap->pb, &snap->pb_gz, cfg_.gzip_level);
+    }
     store_.publish(slot);
     if (http_) http_->set_ready(true);
   } else {

@@ -348,4 +348,95 @@ size_t SeriesTable::live_series_in_family(int fid, uint64_t gen) const {
   return n;
 }
 
+namespace {
+
+// Minimal protobuf wire encoding (proto3) for metrics.proto.
+void pb_varint(std::string* out, uint64_t v) {
+  while (v >= 0x80) {
+    out->push_back(char(uint8_t(v) | 0x80));
+    v >>= 7;
+  }
+  out->push_back(char(v));
+}
+void pb_tag(std::string* out, int field, int wire) { pb_varint(out, (uint64_t(field) << 3) | uint64_t(wire)); }
+void pb_bytes(std::string* out, int field, const std::string& s) {
+  pb_tag(out, field, 2);
+  pb_varint(out, s.size());
+  out->append(s);
+}
+void pb_double(std::string* out, int field, double v) {
+  pb_tag(out, field, 1);
+  char b[8];
+  std::memcpy(b, &v, 8);
+  out->append(b, 8);
+}
+void pb_u64(std::string* out, int field, uint64_t v) {
+  pb_tag(out, field, 0);
+  pb_varint(out, v);
+}
+void pb_msg(std::string* out, int field, const std::string& body) { pb_bytes(out, field, body); }
+
+}  // namespace
+
+void SeriesTable::render_proto(std::string* out, uint64_t gen) const {
+  // metrics.proto: MetricFamily{1 name, 2 help, 3 type, 4 metric}; Metric{1 label, 2 gauge,
+  // 3 counter, 7 histogram}; LabelPair{1 name, 2 value}; Gauge/Counter{1 value};
+  // Histogram{1 sample_count, 2 sample_sum, 3 bucket}; Bucket{1 cumulative_count,
+  // 2 upper_bound}.  MetricType: COUNTER 0, GAUGE 1, HISTOGRAM 4.  Like client_golang,
+  // label pairs are sorted by name and the +Inf bucket is implicit (sample_count).
+  out->clear();
+  std::string fam_buf, metric, sub, lp;
+  std::vector<size_t> order;
+  for (int fid : render_order_) {
+    const Family& fam = families_[size_t(fid)];
+    bool any = false;
+    for (uint32_t idx : fam.members)
+      if (series_[idx].gen == gen) {
+        any = true;
+        break;
+      }
+    if (!any) continue;
+    const auto& names = fam.def.label_names;
+    order.resize(names.size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return names[a] < names[b]; });
+    fam_buf.clear();
+    pb_bytes(&fam_buf, 1, fam.def.name);
+    pb_bytes(&fam_buf, 2, fam.def.help);
+    const int type = fam.def.type == MetricType::kCounter ? 0 : fam.def.type == MetricType::kGauge ? 1 : 4;
+    pb_u64(&fam_buf, 3, uint64_t(type));
+    for (uint32_t idx : fam.members) {
+      const Series& s = series_[idx];
+      if (s.gen != gen) continue;
+      metric.clear();
+      for (size_t i : order) {
+        lp.clear();
+        pb_bytes(&lp, 1, names[i]);
+        pb_bytes(&lp, 2, i < s.labels.size() ? s.labels[i] : std::string());
+        pb_msg(&metric, 1, lp);
+      }
+      sub.clear();
+      if (fam.def.type == MetricType::kHistogram) {
+        pb_u64(&sub, 1, s.hcount);
+        pb_double(&sub, 2, s.hsum);
+        uint64_t cum = 0;
+        for (size_t b = 0; b < s.bounds.size(); ++b) {
+          cum += s.buckets[b];
+          lp.clear();
+          pb_u64(&lp, 1, cum);
+          pb_double(&lp, 2, s.bounds[b]);
+          pb_msg(&sub, 3, lp);
+        }
+        pb_msg(&metric, 7, sub);
+      } else {
+        pb_double(&sub, 1, s.value);
+        pb_msg(&metric, fam.def.type == MetricType::kCounter ? 3 : 2, sub);
+      }
+      pb_msg(&fam_buf, 4, metric);
+    }
+    pb_varint(out, fam_buf.size());
+    out->append(fam_buf);
+  }
+}
+
 }  // namespace gpuexp

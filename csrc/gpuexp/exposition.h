@@ -71,6 +71,11 @@ class SeriesTable {
   // `gc_after` generations are freed (stale-series GC; the reference never Reset() its
   // vectors, main.go:147-150, so exited PIDs stayed forever).
   void render(std::string* out, uint64_t gen, uint64_t gc_after = 1);
+  // The same live series as length-delimited io.prometheus.client.MetricFamily protobuf
+  // messages (what client_golang's promhttp serves when a scraper negotiates
+  // `application/vnd.google.protobuf; proto=io.prometheus.client.MetricFamily;
+  // encoding=delimited`).  Call after render() of the same generation (GC + ordering).
+  void render_proto(std::string* out, uint64_t gen) const;
 
   size_t live_series(uint64_t gen) const;
   size_t live_series_in_family(int fid, uint64_t gen) const;

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <cstdlib>
 #include <cstring>
 #include <unordered_map>
 
@@ -71,6 +72,35 @@ bool contains_token(const char* s, size_t n, const char* tok) {
   for (size_t i = 0; i + tl <= n; ++i)
     if (ieq_prefix(s + i, n - i, tok)) return true;
   return false;
+}
+
+// Accept-header negotiation between the text 0.0.4 exposition and client_golang's
+// delimited protobuf (expfmt.Negotiate): protobuf wins only when the client lists
+// `application/vnd.google.protobuf` with proto=io.prometheus.client.MetricFamily and
+// encoding=delimited at a q no lower than the best text/plain (or wildcard) entry.
+bool prefers_protobuf(const char* s, size_t n) {
+  double q_pb = -1, q_text = -1;
+  std::string h(s, n);
+  size_t pos = 0;
+  while (pos <= h.size()) {
+    size_t comma = h.find(',', pos);
+    if (comma == std::string::npos) comma = h.size();
+    std::string e = h.substr(pos, comma - pos);
+    pos = comma + 1;
+    for (auto& ch : e) ch = char(::tolower(static_cast<unsigned char>(ch)));
+    double q = 1.0;
+    size_t qp = e.find(";q=");
+    if (qp == std::string::npos) qp = e.find("; q=");
+    if (qp != std::string::npos) q = std::atof(e.c_str() + e.find('=', qp) + 1);
+    if (e.find("application/vnd.google.protobuf") != std::string::npos) {
+      if (e.find("proto=io.prometheus.client.metricfamily") != std::string::npos &&
+          e.find("encoding=delimited") != std::string::npos)
+        q_pb = std::max(q_pb, q);
+    } else if (e.find("text/plain") != std::string::npos || e.find("*/*") != std::string::npos) {
+      q_text = std::max(q_text, q);
+    }
+  }
+  return q_pb > 0 && q_pb >= q_text;
 }
 
 }  // namespace
@@ -277,7 +307,7 @@ void HttpServer::run(Worker* w) {
         version = line.substr(s2 + 1);
       }
       bool http10 = version == "HTTP/1.0";
-      bool want_gzip = false, conn_close = http10, conn_keep = false;
+      bool want_gzip = false, want_proto = false, conn_close = http10, conn_keep = false;
       uint64_t content_len = 0;
       size_t pos = le + 2;
       while (pos < end) {
@@ -287,6 +317,8 @@ void HttpServer::run(Worker* w) {
         size_t hn = nl - pos;
         if (ieq_prefix(h, hn, "accept-encoding:")) {
           want_gzip = contains_token(h + 16, hn - 16, "gzip");
+        } else if (ieq_prefix(h, hn, "accept:")) {
+          want_proto = prefers_protobuf(h + 7, hn - 7);
         } else if (ieq_prefix(h, hn, "connection:")) {
           if (contains_token(h + 11, hn - 11, "close")) conn_close = true;
           if (contains_token(h + 11, hn - 11, "keep-alive")) conn_keep = true;
@@ -317,10 +349,21 @@ void HttpServer::run(Worker* w) {
           respond_simple(c, 503, "Service Unavailable", "text/plain", "no sample yet\n", is_head);
         } else {
           if (want_gzip && cfg_.enable_gzip) gzip_wanted_ns_.store(t0, std::memory_order_relaxed);
-          bool gz = want_gzip && cfg_.enable_gzip && !pin->gz.empty();
-          const std::string& b = gz ? pin->gz : pin->body;
+          if (want_proto) proto_wanted_ns_.store(t0, std::memory_order_relaxed);
+          // Protobuf once the sampler has rendered it (from the tick after the first ask).
+          const bool pb = want_proto && !pin->pb.empty();
+          const std::string& plain = pb ? pin->pb : pin->body;
+          const std::string& zipped = pb ? pin->pb_gz : pin->gz;
+          bool gz = want_gzip && cfg_.enable_gzip && !zipped.empty();
+          const std::string& b = gz ? zipped : plain;
           c.head.clear();
-          c.head.append("HTTP/1.1 200 OK\r\nContent-Type: text/plain; version=0.0.4; charset=utf-8\r\n");
+          if (pb) {
+            c.head.append("HTTP/1.1 200 OK\r\nContent-Type: application/vnd.google.protobuf; "
+                          "proto=io.prometheus.client.MetricFamily; encoding=delimited\r\n");
+            stats_.proto_responses.fetch_add(1, std::memory_order_relaxed);
+          } else {
+            c.head.append("HTTP/1.1 200 OK\r\nContent-Type: text/plain; version=0.0.4; charset=utf-8\r\n");
+          }
           if (gz) {
             c.head.append("Content-Encoding: gzip\r\n");
             stats_.gzip_responses.fetch_add(1, std::memory_order_relaxed);

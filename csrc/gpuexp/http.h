@@ -36,6 +36,7 @@ struct HttpStats {
   std::atomic<uint64_t> requests{0};
   std::atomic<uint64_t> metrics_requests{0};
   std::atomic<uint64_t> gzip_responses{0};
+  std::atomic<uint64_t> proto_responses{0};
   std::atomic<uint64_t> bytes_sent{0};
   std::atomic<uint64_t> errors{0};
   std::atomic<uint64_t> accepted{0};
@@ -62,6 +63,8 @@ class HttpServer {
   // Last time (mono ns) a client asked for gzip; the sampler pre-compresses while
   // this is recent so gzip scrapes stay O(bytes) too.
   uint64_t gzip_wanted_ns() const { return gzip_wanted_ns_.load(std::memory_order_relaxed); }
+  // Last time a scraper negotiated the protobuf exposition (the sampler renders it then).
+  uint64_t proto_wanted_ns() const { return proto_wanted_ns_.load(std::memory_order_relaxed); }
   const HttpStats& stats() const { return stats_; }
 
  private:
@@ -74,6 +77,7 @@ class HttpServer {
   std::atomic<bool> running_{false};
   std::atomic<bool> ready_{false};
   std::atomic<uint64_t> gzip_wanted_ns_{0};
+  std::atomic<uint64_t> proto_wanted_ns_{0};
   HttpStats stats_;
   std::vector<std::unique_ptr<Worker>> workers_;
 };

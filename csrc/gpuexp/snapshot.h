@@ -17,6 +17,8 @@ namespace gpuexp {
 struct Snapshot {
   std::string body;     // text 0.0.4
   std::string gz;       // gzip(body), empty when not produced for this tick
+  std::string pb;       // delimited MetricFamily protobuf, only while scrapers negotiate it
+  std::string pb_gz;    // gzip(pb), only while protobuf + gzip are both asked for
   uint64_t gen = 0;     // sampler generation that produced it
   uint64_t render_ns = 0;
   uint64_t series = 0;

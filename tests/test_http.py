@@ -166,3 +166,58 @@ def test_many_connections(mock_engine):
         assert s.recv(4096).startswith(b"HTTP/1.1 200")
         s.close()
     assert e.stats()["http_requests"] >= 200
+
+
+PB_CT = "application/vnd.google.protobuf; proto=io.prometheus.client.MetricFamily; encoding=delimited"
+
+
+def test_protobuf_negotiation_matches_text(mock_engine):
+    """A Prometheus-style Accept header gets the delimited MetricFamily protobuf (from the
+    tick after the first ask), with exactly the text exposition's families and values."""
+    import math
+    from kubernetes_gpu_exporter_amd.utils import promproto
+    e = mock_engine(2, enable_counters=True, enable_sentinel=True)
+    e.tick(1_000_000_000)
+    r, body = req(e.http_port, "/metrics", headers={"Accept": promproto.ACCEPT})
+    assert r.status == 200  # first ask: text until the sampler renders protobuf
+    e.tick(2_000_000_000)
+    r, pb = req(e.http_port, "/metrics", headers={"Accept": promproto.ACCEPT})
+    assert r.getheader("Content-Type") == PB_CT
+    _, text = req(e.http_port, "/metrics")
+    fams_txt = promtext.parse(text.decode())
+    fams_pb = promproto.to_samples(promproto.parse_delimited(pb))
+    assert list(fams_pb) == sorted(fams_pb) == sorted(fams_txt)
+    for name, (typ, helptext, rows) in fams_pb.items():
+        ft = fams_txt[name]
+        assert ft.type == typ and ft.help == helptext, name
+        want = sorted((s, tuple(sorted((k, v) for k, v in lab.items() if k != "le")),
+                       float(lab["le"]) if "le" in lab else None, v) for s, lab, v in ft.samples)
+        got = sorted((s, tuple(sorted((k, v) for k, v in lab.items() if k != "le")),
+                      lab.get("le"), v) for s, lab, v in rows)
+        assert len(want) == len(got), name
+        for w, g in zip(want, got):
+            assert w[:3] == g[:3], (name, w, g)
+            assert (math.isnan(w[3]) and math.isnan(g[3])) or abs(w[3] - g[3]) <= 1e-9 * max(1.0, abs(w[3])), (w, g)
+    # gzip on top of protobuf
+    r, z = req(e.http_port, "/metrics", headers={"Accept": promproto.ACCEPT, "Accept-Encoding": "gzip"})
+    e.tick(3_000_000_000)
+    r, z = req(e.http_port, "/metrics", headers={"Accept": promproto.ACCEPT, "Accept-Encoding": "gzip"})
+    assert r.getheader("Content-Encoding") == "gzip" and r.getheader("Content-Type") == PB_CT
+    assert promproto.parse_delimited(gzip.decompress(z))
+
+
+@pytest.mark.parametrize("accept,proto", [
+    ("text/plain;version=0.0.4;q=0.9,application/vnd.google.protobuf;proto=io.prometheus.client.MetricFamily;"
+     "encoding=delimited;q=0.5", False),
+    ("application/vnd.google.protobuf;proto=io.prometheus.client.MetricFamily;encoding=text", False),
+    ("application/openmetrics-text;version=1.0.0,text/plain;version=0.0.4;q=0.5", False),
+    ("*/*", False),
+    ("application/vnd.google.protobuf;proto=io.prometheus.client.MetricFamily;encoding=delimited", True),
+])
+def test_protobuf_negotiation_respects_q(mock_engine, accept, proto):
+    e = mock_engine(1)
+    e.tick(1_000_000_000)
+    req(e.http_port, "/metrics", headers={"Accept": accept})
+    e.tick(2_000_000_000)
+    r, _ = req(e.http_port, "/metrics", headers={"Accept": accept})
+    assert (r.getheader("Content-Type") == PB_CT) is proto
