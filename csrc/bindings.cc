@@ -237,8 +237,9 @@ PYBIND11_MODULE(_gpuexp, m) {
      py::arg("timeout_ms") = 5000, py::arg("keep_last_body") = false);
 
   py::class_<ScrapeClient>(m, "ScrapeClient")
-      .def(py::init<std::string, int, std::string, bool, int>(), py::arg("host"), py::arg("port"),
-           py::arg("path") = "/metrics", py::arg("gzip") = false, py::arg("timeout_ms") = 5000)
+      .def(py::init<std::string, int, std::string, bool, int, std::string>(), py::arg("host"), py::arg("port"),
+           py::arg("path") = "/metrics", py::arg("gzip") = false, py::arg("timeout_ms") = 5000,
+           py::arg("accept") = "")
       .def("scrape", [](ScrapeClient& c) {
         py::gil_scoped_release rel;
         return c.scrape();

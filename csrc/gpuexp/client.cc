@@ -80,10 +80,12 @@ int read_response(int fd, std::string* buf, std::string* body, bool* server_clos
 
 }  // namespace
 
-ScrapeClient::ScrapeClient(std::string host, int port, std::string path, bool gzip, int timeout_ms)
+ScrapeClient::ScrapeClient(std::string host, int port, std::string path, bool gzip, int timeout_ms,
+                           const std::string& accept)
     : host_(std::move(host)), path_(std::move(path)), port_(port), timeout_ms_(timeout_ms) {
   req_ = "GET " + path_ + " HTTP/1.1\r\nHost: " + host_ + "\r\nUser-Agent: gpuexp-bench\r\n";
   if (gzip) req_ += "Accept-Encoding: gzip\r\n";
+  if (!accept.empty()) req_ += "Accept: " + accept + "\r\n";
   req_ += "\r\n";
 }
 

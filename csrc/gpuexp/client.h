@@ -21,7 +21,9 @@ struct ScrapeResult {
 // One persistent keep-alive connection; scrape() returns the latency in ns (-1 on error).
 class ScrapeClient {
  public:
-  ScrapeClient(std::string host, int port, std::string path, bool gzip, int timeout_ms);
+  // accept: optional Accept header value (e.g. the protobuf exposition's media type).
+  ScrapeClient(std::string host, int port, std::string path, bool gzip, int timeout_ms,
+               const std::string& accept = "");
   ~ScrapeClient();
   double scrape();
   int last_status() const { return status_; }

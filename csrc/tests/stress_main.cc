@@ -17,6 +17,25 @@
 
 using namespace gpuexp;
 
+// Walks a varint-length-delimited protobuf stream; true if the frames tile it exactly.
+static bool delimited_ok(const std::string& b) {
+  size_t pos = 0;
+  while (pos < b.size()) {
+    uint64_t len = 0;
+    int shift = 0;
+    while (true) {
+      if (pos >= b.size() || shift > 63) return false;
+      const uint8_t c = uint8_t(b[pos++]);
+      len |= uint64_t(c & 0x7f) << shift;
+      if (!(c & 0x80)) break;
+      shift += 7;
+    }
+    if (len == 0 || pos + len > b.size()) return false;
+    pos += size_t(len);
+  }
+  return true;
+}
+
 static double ticks_in(const std::string& body) {
   size_t p = body.find("\ngpuexp_ticks_total ");
   if (p == std::string::npos) return -1;
@@ -49,13 +68,21 @@ int main(int argc, char** argv) {
   std::vector<std::thread> th;
   for (int s = 0; s < scrapers; ++s) {
     th.emplace_back([&, s] {
-      ScrapeClient c("127.0.0.1", port, "/metrics", s == 0, 2000);
+      // scraper 0: gzip; scraper 1: protobuf exposition; the rest: plain text
+      ScrapeClient c("127.0.0.1", port, "/metrics", s == 0, 2000,
+                     s == 1 ? "application/vnd.google.protobuf;proto=io.prometheus.client.MetricFamily;"
+                              "encoding=delimited"
+                            : "");
       double last = -1;
       while (!stop.load()) {
         double ns = c.scrape();
         if (ns < 0 || c.last_status() == 503) continue;
         scrapes.fetch_add(1);
         if (s == 0) continue;  // gzip body: only transport-checked
+        if (s == 1 && !c.last_body().empty() && c.last_body()[0] != '#') {
+          if (!delimited_ok(c.last_body())) bad.fetch_add(1);  // protobuf: framing must be exact
+          continue;
+        }
         const std::string& b = c.last_body();
         double t = ticks_in(b);
         if (b.compare(0, 7, "# HELP ") != 0 || b.back() != '\n' || t < last) bad.fetch_add(1);
