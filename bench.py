@@ -106,6 +106,9 @@ def main() -> int:
     ap.add_argument("--busy", type=float, default=0.6, help="target GPU-busy fraction of each step")
     ap.add_argument("--allreduce-mb", type=float, default=64.0)
     ap.add_argument("--gzip", action="store_true", help="scrape with Accept-Encoding: gzip")
+    ap.add_argument("--proto", action="store_true",
+                    help="negotiate the protobuf exposition (Accept: delimited MetricFamily), like Prometheus "
+                         "with native histograms")
     ap.add_argument("--sentinel", type=int, default=1)
     ap.add_argument("--counters", type=int, default=1, help="device PMC counters (aqlprofile plugin)")
     ap.add_argument("--out", default="")
@@ -210,7 +213,9 @@ def main() -> int:
             pods.append({"uid": uid, "namespace": "bench", "name": f"gemm-pod-{r}", "containers": {cid: "worker"}})
             cgroups[p] = kubepods_cgroup(uid, cid, qos="guaranteed")
         write_pod_map(pod_map, pods, cgroups)
-        client = n.ScrapeClient("127.0.0.1", port, "/metrics", args.gzip, 5000)
+        from kubernetes_gpu_exporter_amd.utils import promproto
+        client = n.ScrapeClient("127.0.0.1", port, "/metrics", args.gzip, 5000,
+                                promproto.ACCEPT if args.proto else "")
     else:
         client = None
 
@@ -266,7 +271,12 @@ def main() -> int:
     result = None
     if rank == 0:
         body = client.last_body()
-        fams = promtext.parse(body.decode() if not args.gzip else __import__("gzip").decompress(body).decode())
+        if args.gzip:
+            body = __import__("gzip").decompress(body)
+        if body[:1] == b"#":
+            fams = promtext.parse(body.decode())
+        else:  # protobuf exposition
+            fams = promproto.to_promtext(promproto.parse_delimited(body))
         per_gpu: dict = {}
         for name, fam in fams.items():
             if name.startswith("amd_gpu_") and not name.startswith("amd_gpu_process_"):
@@ -322,7 +332,7 @@ def main() -> int:
             "config": {"model": f"mi355x-per-pod-exporter ({args.series_profile} profile) + bf16 MFMA GEMM pods",
                        "global_batch": n_gpus, "seq_len": 0, "parallelism": f"dp{n_gpus}",
                        "scrape_hz": args.scrape_hz, "sample_hz": args.sample_hz, "backend": backend,
-                       "series_profile": args.series_profile, "gzip": args.gzip,
+                       "series_profile": args.series_profile, "gzip": args.gzip, "protobuf": args.proto,
                        "gemm": f"{G}^3 x {iters}/step", "allreduce_mb": args.allreduce_mb if world > 1 else 0},
             "p50_scrape_us": round(statistics.median(lat), 2) if lat else None,
             "p99_scrape_us": round(pct(lat, 0.99), 2) if lat else None,

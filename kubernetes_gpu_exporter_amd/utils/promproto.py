@@ -95,3 +95,17 @@ def to_samples(families: list) -> dict:
                 rows.append((mf.name, labels, m.gauge.value))
         res[mf.name] = (typ, mf.help, rows)
     return res
+
+
+def to_promtext(families: list) -> dict:
+    """Same shape as utils.promtext.parse(): {name: Family(name, help, type, samples)}."""
+    from .promtext import Family
+    out = {}
+    for name, (typ, helptext, rows) in to_samples(families).items():
+        fam = Family(name, helptext, typ)
+        for sname, labels, v in rows:
+            lab = {k: (("+Inf" if v2 == float("inf") else repr(float(v2))) if k == "le" else v2)
+                   for k, v2 in labels.items()}
+            fam.samples.append((sname, lab, v))
+        out[name] = fam
+    return out
