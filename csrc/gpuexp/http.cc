@@ -420,6 +420,8 @@ void HttpServer::run(Worker* w) {
           }
           int one = 1;
           ::setsockopt(cfd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+          if (cfg_.socket_sndbuf > 0)
+            ::setsockopt(cfd, SOL_SOCKET, SO_SNDBUF, &cfg_.socket_sndbuf, sizeof(cfg_.socket_sndbuf));
           Conn& c = w->conns[cfd];
           c.fd = cfd;
           c.last_active_ns = mono_ns();

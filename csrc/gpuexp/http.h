@@ -26,6 +26,11 @@ struct HttpConfig {
   int max_conns = 4096;
   int idle_timeout_ms = 120000;
   bool enable_gzip = true;
+  // Send buffer of accepted sockets.  A fresh TCP socket starts at tcp_wmem[1] (16 KiB),
+  // so a 30-200 KB exposition could not be queued by one writev: the rest waited for the
+  // peer's ACK and an EPOLLOUT wake-up — measured +25 us p50 for a 26 KB body on loopback.
+  // The kernel clamps this to net.core.wmem_max.
+  int socket_sndbuf = 4 << 20;
 };
 
 // Fixed latency buckets (seconds) for gpuexp_scrape_duration_seconds.
