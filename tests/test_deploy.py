@@ -70,3 +70,19 @@ def test_synthetic_workloads_use_known_models():
         i = cmd.index("kubernetes_gpu_exporter_amd.models")
         assert cmd[i + 1] in WORKLOADS
         assert spec["containers"][0]["resources"]["limits"]["amd.com/gpu"] >= 1
+
+
+def test_rules_reference_exported_metrics():
+    """Every metric a recording/alert rule uses is one the exporter emits (docs/METRICS.md
+    is generated from the engine)."""
+    import re
+    with open(os.path.join(os.path.dirname(K8S), "..", "docs", "METRICS.md")) as fh:
+        known = set(re.findall(r"^\| `([a-z_:]+)` \|", fh.read(), re.M))
+    assert "amd_gpu_up" in known
+    used = set()
+    for d in docs("rules.yaml"):
+        for g in d["spec"]["groups"]:
+            for rule in g["rules"]:
+                for name in re.findall(r"\b((?:amd|gpuexp|pod_gpu|docker_gpu)_[a-z0-9_]+)", rule["expr"]):
+                    used.add(re.sub(r"_(bucket|sum|count)$", "", name))
+    assert used and used <= known, used - known
