@@ -129,11 +129,22 @@ def main() -> int:
     pod_map = os.path.join(tmpdir, "podmap.json")
     port = 0
     exporter = None
+    degraded = None
     if rank == 0:
         os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
         port = free_port()
-        exporter = start_exporter(args, n_gpus, backend, port, pod_map,
-                                  os.path.join(ROOT, "gpurun_out", "bench_exporter.log"))
+        log_path = os.path.join(ROOT, "gpurun_out", "bench_exporter.log")
+        try:
+            exporter = start_exporter(args, n_gpus, backend, port, pod_map, log_path)
+        except RuntimeError as ex:
+            # Never lose the measurement to an optional source: retry without the PMC
+            # counters and the sentinel, and say so in the result.
+            print(f"[bench] exporter start failed ({ex}); retrying without counters/sentinel", file=sys.stderr,
+                  flush=True)
+            args.counters, args.sentinel = 0, 0
+            degraded = str(ex)
+            port = free_port()
+            exporter = start_exporter(args, n_gpus, backend, port, pod_map, log_path)
 
     dist = None
     if world > 1:
@@ -351,6 +362,8 @@ def main() -> int:
             "sample_stage_p50_le_us": stage_p50_us,
             "gpu_metrics_reads_gpu0": metrics_reads,
             "sampler_thread_cpu_s": sampler_cpu[0] if sampler_cpu else None,
+            "optional_sources": {"counters": bool(args.counters), "sentinel": bool(args.sentinel),
+                                 "degraded_reason": degraded},
         }
         stop_proc(exporter)
 
