@@ -56,7 +56,12 @@ def start_exporter(args, n_gpus: int, backend: str, port: int, pod_map: str, log
            "--interval", str(1.0 / args.sample_hz), "--backend", backend,
            "--series-profile", args.series_profile, "--control-interval", "0.5", "--log-level", "warn"]
     if backend != "mock":
-        cmd += ["--devices", ",".join(str(i) for i in range(n_gpus))]
+        # Watch exactly the GPUs the ranks run on: HIP device i -> PCI BDF (KFD topology order,
+        # read without initialising the GPU), falling back to exporter indices.
+        from kubernetes_gpu_exporter_amd.utils.kfdself import hip_order_bdfs
+        bdfs = hip_order_bdfs()
+        devs = bdfs[:n_gpus] if len(bdfs) >= n_gpus else [str(i) for i in range(n_gpus)]
+        cmd += ["--devices", ",".join(devs)]
         if args.sentinel:
             cmd += ["--enable-sentinel", "true"]
         if args.counters:

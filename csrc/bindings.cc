@@ -316,6 +316,7 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("gzip_level", &EngineConfig::gzip_level)
       .def_readwrite("gc_after", &EngineConfig::gc_after)
       .def_readwrite("device_filter", &EngineConfig::device_filter)
+      .def_readwrite("device_filter_bdf", &EngineConfig::device_filter_bdf)
       .def_readwrite("trace_path", &EngineConfig::trace_path)
       .def_readwrite("trace_max_events", &EngineConfig::trace_max_events)
       .def_readwrite("version", &EngineConfig::version);

@@ -248,10 +248,16 @@ bool Engine::start(std::string* err) {
   backend_->set_metrics_coalescing(cfg_.metrics_coalesce);
   std::vector<DeviceInfo> all;
   if (!backend_->init(&all, err)) return false;
-  if (!cfg_.device_filter.empty()) {
-    for (auto& d : all)
-      if (std::find(cfg_.device_filter.begin(), cfg_.device_filter.end(), d.index) != cfg_.device_filter.end())
-        devices_.push_back(d);
+  if (!cfg_.device_filter.empty() || !cfg_.device_filter_bdf.empty()) {
+    auto lower = [](std::string x) {
+      for (auto& ch : x) ch = char(::tolower(static_cast<unsigned char>(ch)));
+      return x;
+    };
+    for (auto& d : all) {
+      bool want = std::find(cfg_.device_filter.begin(), cfg_.device_filter.end(), d.index) != cfg_.device_filter.end();
+      for (const auto& b : cfg_.device_filter_bdf) want = want || lower(b) == lower(d.bdf);
+      if (want) devices_.push_back(d);
+    }
     // keep backend indices: DeviceInfo::index addresses the backend's own table
   } else {
     devices_ = all;

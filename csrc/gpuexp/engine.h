@@ -85,6 +85,7 @@ struct EngineConfig {
   int gzip_level = 1;
   uint64_t gc_after = 1;               // stale series vanish this many ticks after last seen
   std::vector<int> device_filter;      // empty = all
+  std::vector<std::string> device_filter_bdf;  // also accepted: PCI BDFs ("0000:75:00.0")
   std::string trace_path;              // Chrome trace JSON of sampler stages
   size_t trace_max_events = 200000;
   std::string version = "0.1.0";

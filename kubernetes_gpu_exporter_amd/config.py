@@ -30,7 +30,7 @@ class Config:
     metrics_coalesce: bool = True          # skip gpu_metrics SMU fetches until the PMFW refreshes
     mock_devices: int = 1
     host_root: str = ""                    # prefix for /sys and /proc (DaemonSet: /host)
-    devices: list = field(default_factory=list)  # exporter GPU indices to export (empty = all)
+    devices: list = field(default_factory=list)  # GPU indices and/or PCI BDFs to export (empty = all)
     series_profile: str = "full"           # full | standard (64/GPU BASELINE load) | compact | legacy
     ras_interval: float = 10.0             # seconds between RAS/AER sysfs re-reads (full profile)
     legacy_families: bool = True           # pod_gpu_memory_usage / docker_gpu_memory_perc_usage
@@ -114,7 +114,8 @@ class Config:
         ec.enable_rccl = bool(self.enable_rccl)
         ec.rccl_dir = self.rccl_dir
         ec.gc_after = int(self.gc_after)
-        ec.device_filter = [int(d) for d in self.devices]
+        ec.device_filter = [int(d) for d in self.devices if ":" not in str(d)]
+        ec.device_filter_bdf = [str(d) for d in self.devices if ":" in str(d)]
         ec.trace_path = self.trace
         from . import __version__
         ec.version = __version__

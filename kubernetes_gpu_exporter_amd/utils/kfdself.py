@@ -71,3 +71,37 @@ def find_own_kfd_pid(device_index: int = 0, salt: int = 0, tries: int = 3) -> in
         if len(cands) == 1:
             return cands[0]
     return None
+
+
+def hip_order_bdfs(root: str = "") -> list:
+    """PCI BDFs of the GPUs in HIP device order, WITHOUT initialising the GPU (a process
+    that will spawn children must not touch HIP first).  ROCr enumerates GPU agents in
+    KFD topology node order and HIP numbers them in that order; *_VISIBLE_DEVICES lists
+    of integers are applied the way ROCr/HIP apply them."""
+    nodes = []
+    base = root + "/sys/class/kfd/kfd/topology/nodes"
+    for name in os.listdir(base) if os.path.isdir(base) else []:
+        if not name.isdigit():
+            continue
+        try:
+            kv = dict(line.split() for line in open(f"{base}/{name}/properties") if len(line.split()) == 2)
+        except OSError:
+            continue
+        if int(kv.get("simd_count", 0)) <= 0:
+            continue  # CPU node
+        minor = kv.get("drm_render_minor")
+        if not root and minor is not None and not os.access(f"/dev/dri/renderD{minor}", os.R_OK | os.W_OK):
+            continue  # ROCr skips GPUs whose render node this process cannot open
+        loc, dom = int(kv.get("location_id", 0)), int(kv.get("domain", 0))
+        nodes.append((int(name), f"{dom:04x}:{(loc >> 8) & 0xFF:02x}:{(loc >> 3) & 0x1F:02x}.{loc & 7:x}"))
+    bdfs = [b for _, b in sorted(nodes)]
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        val = os.environ.get(var, "").strip()
+        if not val:
+            continue
+        try:
+            idx = [int(x) for x in val.split(",") if x.strip() != ""]
+        except ValueError:
+            continue  # UUID lists: leave the order as is
+        bdfs = [bdfs[i] for i in idx if 0 <= i < len(bdfs)]
+    return bdfs

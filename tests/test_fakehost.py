@@ -308,3 +308,21 @@ def test_kfd_detail_files_are_rate_limited(native, tmp_path):
     e.tick(3 * S + 200_000_000)
     assert proc("amd_gpu_process_evicted_seconds_total") == {"777": 1.5}
     e.stop()
+
+
+def test_hip_order_bdfs_and_bdf_device_filter(native, tmp_path, monkeypatch):
+    """HIP device order comes from KFD topology node order (not PCI order), and the engine
+    can be told to watch GPUs by BDF."""
+    from kubernetes_gpu_exporter_amd.utils.kfdself import hip_order_bdfs
+    h = mi355x_node(tmp_path, 4)
+    for v in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    order = hip_order_bdfs(str(tmp_path))
+    assert sorted(order) == sorted(d["bdf"] for d in native.read_backend("sysfs", str(tmp_path)))
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "2,0")
+    assert hip_order_bdfs(str(tmp_path)) == [order[2], order[0]]
+    e = _engine(native, tmp_path, device_filter_bdf=[order[2].upper()])
+    e.tick(1 * S)
+    up = promtext.samples(promtext.parse(e.snapshot_text()), "amd_gpu_up")
+    assert [s[1]["bdf"] for s in up] == [order[2]]
+    e.stop()

@@ -244,3 +244,15 @@ def test_raw_metrics_path_and_pmfw_coalescing(native):
     assert 0.3 < frac < 0.6, reads  # ~half at 100 Hz vs a 20 ms PMFW refresh; never most
     (period,) = [s[2] for s in promtext.samples(fams, "gpuexp_gpu_metrics_refresh_period_seconds")]
     assert 0.015 < period < 0.03, period
+
+
+def test_hip_order_bdfs_match_torch():
+    """bench.py watches the ranks' GPUs by BDF computed without initialising HIP; it must
+    agree with HIP's own device order."""
+    import torch
+    from kubernetes_gpu_exporter_amd.utils.kfdself import hip_order_bdfs
+    bdfs = hip_order_bdfs()
+    assert len(bdfs) == torch.cuda.device_count(), bdfs
+    for i, b in enumerate(bdfs):
+        p = torch.cuda.get_device_properties(i)
+        assert b == f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0", (i, b)
