@@ -255,4 +255,5 @@ def test_hip_order_bdfs_match_torch():
     assert len(bdfs) == torch.cuda.device_count(), bdfs
     for i, b in enumerate(bdfs):
         p = torch.cuda.get_device_properties(i)
-        assert b == f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0", (i, b)
+        dom = getattr(p, "pci_domain_id", 0)
+        assert b == f"{dom:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0", (i, b)
