@@ -86,3 +86,22 @@ def test_rules_reference_exported_metrics():
                 for name in re.findall(r"\b((?:amd|gpuexp|pod_gpu|docker_gpu)_[a-z0-9_]+)", rule["expr"]):
                     used.add(re.sub(r"_(bucket|sum|count)$", "", name))
     assert used and used <= known, used - known
+
+
+def test_grafana_dashboard_uses_exported_metrics():
+    import json
+    import re
+    root = os.path.dirname(K8S)
+    with open(os.path.join(root, "..", "docs", "METRICS.md")) as fh:
+        known = set(re.findall(r"^\| `([a-z_:]+)` \|", fh.read(), re.M))
+    with open(os.path.join(root, "grafana", "gpuexp-dashboard.json")) as fh:
+        dash = json.load(fh)
+    used = set()
+    for p in dash["panels"]:
+        for t in p["targets"]:
+            for name in re.findall(r"\b((?:amd|gpuexp|pod_gpu|docker_gpu)_[a-z0-9_]+)", t["expr"]):
+                used.add(re.sub(r"_(bucket|sum|count)$", "", name))
+    for v in dash["templating"]["list"]:
+        for name in re.findall(r"\b(amd_[a-z0-9_]+)", v.get("query", "")):
+            used.add(name)
+    assert len(dash["panels"]) >= 10 and used <= known, used - known
