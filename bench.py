@@ -328,6 +328,11 @@ def main() -> int:
             total = bl[-1][1]
             le50 = next((le for le, v in bl if total and v >= total / 2), None)
             stage_p50_us[st_name] = round(le50 * 1e6, 1) if le50 is not None else None
+        # server side of a scrape (request parsed -> last byte written), all scrapes so far:
+        # the rest of the client-measured latency is loopback TCP + thread wake-ups
+        srv = {s[0].rsplit("_", 1)[-1]: s[2] for s in promtext.samples(fams, "gpuexp_scrape_duration_seconds")
+               if s[0].endswith(("_sum", "_count"))}
+        server_mean_us = round(srv["sum"] / srv["count"] * 1e6, 2) if srv.get("count") else None
         metrics_reads = {lab["kind"]: v for _, lab, v in promtext.samples(fams, "gpuexp_gpu_metrics_reads_total")
                          if lab.get("gpu") == "0"}
         sampler_cpu = [v for _, _, v in promtext.samples(fams, "gpuexp_sampler_cpu_seconds_total")]
@@ -354,6 +359,7 @@ def main() -> int:
             "p99_scrape_us": round(pct(lat, 0.99), 2) if lat else None,
             "max_scrape_us": round(max(lat), 2) if lat else None,
             "exporter_cpu_percent": round(cpu_pct, 3),
+            "server_scrape_mean_us": server_mean_us,
             "scrapes": len(lat),
             "scrape_errors": client.errors,
             "scrape_bytes": client.last_bytes,

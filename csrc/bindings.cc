@@ -377,6 +377,11 @@ PYBIND11_MODULE(_gpuexp, m) {
           d["http_bytes"] = hs->bytes_sent.load();
           d["http_errors"] = hs->errors.load();
           d["http_open_conns"] = hs->open_conns.load();
+          d["http_writev_calls"] = hs->writev_calls.load();
+          d["http_writev_ns"] = hs->writev_ns.load();
+          d["http_partial_writes"] = hs->partial_writes.load();
+          d["http_scrape_ns"] = hs->lat_sum_ns.load();
+          d["http_scrapes"] = hs->lat_count.load();
         }
         return d;
       })

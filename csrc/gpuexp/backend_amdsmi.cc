@@ -53,6 +53,7 @@ void from_amdsmi_metrics(const amdsmi_gpu_metrics_t& m, DeviceSample* out) {
   for (int i = 0; i < AMDSMI_MAX_NUM_GFX_CLKS; ++i)
     if (m.current_gfxclks[i] != 0xFFFF && m.current_gfxclks[i] != 0) {
       sum += m.current_gfxclks[i];
+      if (i < kMaxXcc) out->clk_gfx_xcc[i] = m.current_gfxclks[i];
       ++n;
     }
   out->clk_gfx = n ? sum / n : u16v(m.current_gfxclk);
@@ -168,6 +169,9 @@ class AmdsmiBackend : public Backend {
           info.name = asic.market_name;
           info.num_cu = asic.num_of_compute_units;
         }
+        uint16_t xcd = 0;  // XCDs in this partition (8 on an SPX-mode MI355X)
+        if (amdsmi_get_gpu_xcd_counter(d.h, &xcd) == AMDSMI_STATUS_SUCCESS && xcd > 0 && xcd <= kMaxXcc)
+          info.num_xcc = xcd;
         uint64_t total = 0;
         if (amdsmi_get_gpu_memory_total(d.h, AMDSMI_MEM_TYPE_VRAM, &total) == AMDSMI_STATUS_SUCCESS)
           info.vram_total = total;

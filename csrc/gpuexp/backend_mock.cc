@@ -76,6 +76,7 @@ void MockBackend::sample(const DeviceInfo& dev, DeviceSample* out) {
   out->temp_mem = get(s, "temp_mem", std::round(45 + 5 * std::sin(0.1 * t + ph)));
   out->temp_vrsoc = get(s, "temp_vrsoc", 41);
   out->clk_gfx = get(s, "clk_gfx", 2100);
+  for (uint32_t x = 0; x < dev.num_xcc && x < uint32_t(kMaxXcc); ++x) out->clk_gfx_xcc[x] = out->clk_gfx;
   out->clk_soc = get(s, "clk_soc", 1000);
   out->clk_mem = get(s, "clk_mem", 2000);
   out->pcie_width = 16;
@@ -178,6 +179,9 @@ bool MockBackend::sentinel(const DeviceInfo& dev, SentinelReading* out) {
   out->sclk_hz = get(s, "sentinel_sclk_hz", 2.1e9);
   out->dispatch_latency_s = get(s, "sentinel_latency_s", 8e-6);
   out->xcc_id = double(dev.index % 8);
+  // One wave per XCD; later workgroups of the round-robin deal start a little later.
+  for (uint32_t x = 0; x < dev.num_xcc && x < uint32_t(kMaxXcc); ++x)
+    out->xcc_latency_s[x] = out->dispatch_latency_s + 0.1e-6 * x;
   out->runs = s.started ? uint64_t(s.accum) : 0;
   return true;
 }

@@ -8,6 +8,9 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <strings.h>
+
+#include <algorithm>
 #include <cerrno>
 #include <cstring>
 
@@ -36,45 +39,74 @@ int connect_to(const std::string& host, int port, int timeout_ms) {
   return fd;
 }
 
-// Reads one HTTP response; returns status code or -1.  `buf` may hold leftover bytes.
-int read_response(int fd, std::string* buf, std::string* body, bool* server_close) {
-  char tmp[65536];
-  size_t hdr_end;
-  while ((hdr_end = buf->find("\r\n\r\n")) == std::string::npos) {
-    ssize_t n = ::recv(fd, tmp, sizeof(tmp), 0);
-    if (n <= 0) return -1;
-    buf->append(tmp, size_t(n));
+// Case-insensitive search for a header name inside [p, end); returns its value start.
+const char* find_header(const char* p, const char* end, const char* name) {
+  const size_t nl = std::strlen(name);
+  for (; p + nl <= end; ++p) {
+    if (p[0] != '\n') continue;
+    const char* h = p + 1;
+    if (size_t(end - h) < nl) break;
+    if (::strncasecmp(h, name, nl) == 0) return h + nl;
   }
-  int code = -1;
-  if (buf->size() > 12) code = std::atoi(buf->c_str() + 9);
-  uint64_t clen = 0;
-  std::string headers = buf->substr(0, hdr_end);
-  for (auto& c : headers) c = char(::tolower(c));
-  size_t p = headers.find("content-length:");
-  bool http10 = headers.compare(0, 8, "http/1.0") == 0;
-  *server_close = http10 || headers.find("connection: close") != std::string::npos;
-  if (p == std::string::npos) {
+  return nullptr;
+}
+
+// Reads one HTTP response into `rb`, straight from the socket: one copy kernel -> user,
+// no staging buffer, so the measured latency is the exporter's plus loopback TCP, not
+// the harness's memcpys (a multi-GPU exposition is ~100-200 KB).  Returns the status
+// code or -1; the body is [*body_off, *body_off + *body_len) of rb.data.
+int read_response(int fd, RecvBuf* rb, size_t* body_off, size_t* body_len, bool* server_close) {
+  auto fill = [&]() -> ssize_t {
+    if (rb->data.size() - rb->end < 16384) rb->data.resize(std::max<size_t>(rb->data.size() * 2, 1 << 16));
+    ssize_t n = ::recv(fd, rb->data.data() + rb->end, rb->data.size() - rb->end, 0);
+    if (n > 0) rb->end += size_t(n);
+    return n;
+  };
+  const char* hdr_end_p = nullptr;
+  for (size_t scanned = rb->start;;) {
+    const char* base = rb->data.data();
+    if (rb->end >= rb->start + 4) {
+      const char* from = base + std::max(rb->start, scanned >= 3 ? scanned - 3 : 0);
+      const char* hit = static_cast<const char*>(::memmem(from, size_t(base + rb->end - from), "\r\n\r\n", 4));
+      if (hit) {
+        hdr_end_p = hit;
+        break;
+      }
+      scanned = rb->end;
+    }
+    if (fill() <= 0) return -1;
+  }
+  const char* base = rb->data.data();
+  const size_t hdr_end = size_t(hdr_end_p - base);
+  const char* hs = base + rb->start;
+  int code = hdr_end - rb->start > 12 ? std::atoi(hs + 9) : -1;
+  const bool http10 = ::strncasecmp(hs, "HTTP/1.0", 8) == 0;
+  const char* conn = find_header(hs, hdr_end_p, "connection:");
+  *server_close = http10 || (conn && ::strncasecmp(conn + std::strspn(conn, " "), "close", 5) == 0);
+  const char* cl = find_header(hs, hdr_end_p, "content-length:");
+  if (!cl) {
     // No length: the body runs to EOF (HTTP/1.0 servers such as prometheus_client's).
     for (;;) {
-      ssize_t n = ::recv(fd, tmp, sizeof(tmp), 0);
+      ssize_t n = fill();
       if (n < 0) return -1;
       if (n == 0) break;
-      buf->append(tmp, size_t(n));
     }
-    body->assign(*buf, hdr_end + 4, std::string::npos);
-    buf->clear();
+    *body_off = hdr_end + 4;
+    *body_len = rb->end - *body_off;
+    rb->start = rb->end;
     *server_close = true;
     return code;
   }
-  parse_u64(headers.c_str() + p + 15, headers.size() - p - 15, &clen);
-  size_t need = hdr_end + 4 + size_t(clen);
-  while (buf->size() < need) {
-    ssize_t n = ::recv(fd, tmp, sizeof(tmp), 0);
-    if (n <= 0) return -1;
-    buf->append(tmp, size_t(n));
-  }
-  body->assign(*buf, hdr_end + 4, size_t(clen));
-  buf->erase(0, need);
+  uint64_t clen = 0;
+  const char* eol = static_cast<const char*>(std::memchr(cl, '\r', size_t(hdr_end_p + 2 - cl)));
+  parse_u64(cl, size_t((eol ? eol : hdr_end_p) - cl), &clen);
+  const size_t need = hdr_end + 4 + size_t(clen);
+  if (rb->data.size() < need) rb->data.resize(need + (1 << 16));
+  while (rb->end < need)
+    if (fill() <= 0) return -1;
+  *body_off = hdr_end + 4;
+  *body_len = size_t(clen);
+  rb->start = need;
   return code;
 }
 
@@ -96,16 +128,17 @@ ScrapeClient::~ScrapeClient() {
 double ScrapeClient::scrape() {
   if (fd_ < 0) {
     fd_ = connect_to(host_, port_, timeout_ms_);
-    buf_.clear();
+    rb_.start = rb_.end = 0;
     if (fd_ < 0) {
       ++errors_;
       return -1;
     }
   }
+  rb_.compact();
   uint64_t t0 = mono_ns();
   bool ok = ::send(fd_, req_.data(), req_.size(), MSG_NOSIGNAL) == ssize_t(req_.size());
   bool server_close = false;
-  int code = ok ? read_response(fd_, &buf_, &body_, &server_close) : -1;
+  int code = ok ? read_response(fd_, &rb_, &body_off_, &body_len_, &server_close) : -1;
   uint64_t t1 = mono_ns();
   if (code < 0) {
     ++errors_;
@@ -114,7 +147,7 @@ double ScrapeClient::scrape() {
     return -1;
   }
   status_ = code;
-  bytes_ = body_.size();
+  bytes_ = body_len_;
   if (server_close) {
     ::close(fd_);
     fd_ = -1;
@@ -130,7 +163,7 @@ ScrapeResult scrape_loop(const std::string& host, int port, const std::string& p
   if (gzip) req += "Accept-Encoding: gzip\r\n";
   req += keepalive ? "\r\n" : "Connection: close\r\n\r\n";
   int fd = -1;
-  std::string buf, body;
+  RecvBuf rb;
   timespec next;
   clock_gettime(CLOCK_MONOTONIC, &next);
   uint64_t period_ns = hz > 0 ? uint64_t(1e9 / hz) : 0;
@@ -144,16 +177,18 @@ ScrapeResult scrape_loop(const std::string& host, int port, const std::string& p
     }
     if (fd < 0) {
       fd = connect_to(host, port, timeout_ms);
-      buf.clear();
+      rb.start = rb.end = 0;
       if (fd < 0) {
         r.errors++;
         continue;
       }
     }
+    rb.compact();
+    size_t boff = 0, blen = 0;
     uint64_t t0 = mono_ns();
     bool ok = ::send(fd, req.data(), req.size(), MSG_NOSIGNAL) == ssize_t(req.size());
     bool server_close = false;
-    int code = ok ? read_response(fd, &buf, &body, &server_close) : -1;
+    int code = ok ? read_response(fd, &rb, &boff, &blen, &server_close) : -1;
     uint64_t t1 = mono_ns();
     if (code < 0) {
       r.errors++;
@@ -163,8 +198,8 @@ ScrapeResult scrape_loop(const std::string& host, int port, const std::string& p
     }
     if (code != 200) r.non200++;
     r.latency_ns.push_back(double(t1 - t0));
-    r.bytes += body.size();
-    if (keep_last_body) r.last_body = body;
+    r.bytes += blen;
+    if (keep_last_body) r.last_body.assign(rb.data.data() + boff, blen);
     if (!keepalive || server_close) {
       ::close(fd);
       fd = -1;

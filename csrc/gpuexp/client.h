@@ -18,6 +18,19 @@ struct ScrapeResult {
   double wall_s = 0;
 };
 
+// Receive buffer reused across responses: [start, end) holds unread bytes.
+struct RecvBuf {
+  std::vector<char> data = std::vector<char>(size_t(1) << 18);
+  size_t start = 0, end = 0;
+  // Moves unread bytes (a pipelined response, normally none) to the front.
+  void compact() {
+    if (start == 0) return;
+    std::copy(data.begin() + long(start), data.begin() + long(end), data.begin());
+    end -= start;
+    start = 0;
+  }
+};
+
 // One persistent keep-alive connection; scrape() returns the latency in ns (-1 on error).
 class ScrapeClient {
  public:
@@ -28,14 +41,16 @@ class ScrapeClient {
   double scrape();
   int last_status() const { return status_; }
   uint64_t last_bytes() const { return bytes_; }
-  const std::string& last_body() const { return body_; }
+  // Body of the last response (valid until the next scrape).
+  std::string last_body() const { return std::string(rb_.data.data() + body_off_, body_len_); }
   uint64_t errors() const { return errors_; }
 
  private:
   std::string host_, path_, req_;
   int port_, timeout_ms_, fd_ = -1, status_ = 0;
   uint64_t bytes_ = 0, errors_ = 0;
-  std::string buf_, body_;
+  RecvBuf rb_;
+  size_t body_off_ = 0, body_len_ = 0;
 };
 
 ScrapeResult scrape_loop(const std::string& host, int port, const std::string& path, double hz, int count,

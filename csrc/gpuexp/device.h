@@ -60,8 +60,9 @@ struct DeviceSample {
   double temp_vrgfx = kNaN, temp_vrsoc = kNaN, temp_vrmem = kNaN;
   double temp_hbm[kMaxHbm] = {kNaN, kNaN, kNaN, kNaN};
 
-  // clocks (MHz)
+  // clocks (MHz); clk_gfx is the mean over the XCDs' own gfx clocks
   double clk_gfx = kNaN, clk_soc = kNaN, clk_mem = kNaN;
+  double clk_gfx_xcc[kMaxXcc] = {kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN};
 
   // xGMI accumulators (KB) per link; link_up: 1/0, NaN unsupported
   int num_xgmi_links = 0;
@@ -117,13 +118,17 @@ struct CounterReading {
   double hbm_write_bps = kNaN;      // TCC_EA0_WRREQ * 64B / dt
 };
 
-// HIP sentinel kernel stamps for one GPU (latest completed run).
+// HIP sentinel kernel stamps for one GPU (latest completed run).  A run is one wave per
+// XCD (the dispatcher deals workgroups round-robin over the 8 XCDs), so the chip-level
+// values below aggregate per-XCD stamps.
 struct SentinelReading {
   bool ok = false;
-  double sclk_hz = kNaN;              // d(s_memtime)/d(s_memrealtime) * 100 MHz
+  double sclk_hz = kNaN;              // median over waves of d(s_memtime)/d(s_memrealtime) * 100 MHz
   double dispatch_latency_s = kNaN;   // host launch -> first wave running
-  double xcc_id = kNaN;               // XCC the wave landed on
+  double xcc_id = kNaN;               // XCC workgroup 0 landed on
   uint64_t runs = 0;                  // completed sentinel runs
+  // host launch -> wave start on each XCD (indexed by HW_REG_XCC_ID; NaN = no wave there yet)
+  double xcc_latency_s[kMaxXcc] = {kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN};
 };
 
 class Backend {

@@ -172,8 +172,13 @@ void Engine::define_families() {
   f_sen_sclk_ = add("amd_gpu_sentinel_sclk_hz", "Effective shader clock measured by the sentinel kernel", G, D);
   f_sen_lat_ = add("amd_gpu_sentinel_dispatch_latency_seconds",
                    "Host launch to first-wave start of the sentinel kernel (queue contention)", G, D);
-  f_sen_xcc_ = add("amd_gpu_sentinel_xcc_id", "XCC the last sentinel wave ran on", G, D);
+  f_sen_xcc_ = add("amd_gpu_sentinel_xcc_id", "XCC that workgroup 0 of the last sentinel run landed on", G, D);
   f_sen_runs_ = add("amd_gpu_sentinel_runs_total", "Completed sentinel kernel runs", C, D);
+  // --- full profile: per-XCD detail (8 XCDs on an SPX-mode MI355X) ---
+  f_xcc_clk_ = add("amd_gpu_xcc_clock_hz", "Per-XCD gfx clock (PMFW current_gfxclk of each XCC)", G,
+                   with(D, {"xcc"}));
+  f_sen_xlat_ = add("amd_gpu_sentinel_xcc_dispatch_latency_seconds",
+                    "Host launch to sentinel wave start on each XCD (per-XCD CU contention)", G, with(D, {"xcc"}));
 
   // --- per-process / per-pod families ---
   const std::vector<std::string> P = {"gpu", "pid", "comm", "namespace", "pod", "container"};
@@ -552,6 +557,9 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
     dput(st, i, st.recov, f_pcie_recov_, {}, c.pcie_l0_recov, gen);
     dput(st, i, st.xgmi_w, f_xgmi_width_, {}, c.xgmi_width, gen);
     dput(st, i, st.xgmi_s, f_xgmi_speed_, {}, c.xgmi_speed, gen);
+    for (int x = 0; x < kMaxXcc; ++x)
+      if (!std::isnan(c.clk_gfx_xcc[x]))
+        dput(st, i, st.xclk[x], f_xcc_clk_, {std::to_string(x)}, c.clk_gfx_xcc[x] * 1e6, gen);
   }
 
   uint32_t nx = d.num_xcc ? std::min<uint32_t>(d.num_xcc, kMaxXcc) : kMaxXcc;
@@ -605,6 +613,10 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
     dput(st, i, st.sen[1], f_sen_lat_, {}, sr.dispatch_latency_s, gen);
     dput(st, i, st.sen[2], f_sen_xcc_, {}, sr.xcc_id, gen);
     dput(st, i, st.sen[3], f_sen_runs_, {}, double(sr.runs), gen);
+    if (cfg_.series_profile == "full")
+      for (int x = 0; x < kMaxXcc; ++x)
+        if (!std::isnan(sr.xcc_latency_s[x]))
+          dput(st, i, st.sen_xlat[x], f_sen_xlat_, {std::to_string(x)}, sr.xcc_latency_s[x], gen);
   }
 }
 

@@ -58,9 +58,10 @@ bool decode_gpu_metrics_v1_8(const void* blob, size_t len, DeviceSample* out) {
   // Per-XCC gfx clocks: report the mean of the valid instances.
   double sum = 0;
   int n = 0;
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < kMaxXcc; ++i)
     if (m.current_gfxclk[i] != 0xFFFF && m.current_gfxclk[i] != 0) {
       sum += m.current_gfxclk[i];
+      out->clk_gfx_xcc[i] = m.current_gfxclk[i];
       ++n;
     }
   out->clk_gfx = n ? sum / n : kNaN;

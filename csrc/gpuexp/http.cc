@@ -239,10 +239,14 @@ void HttpServer::run(Worker* w) {
         iov[n].iov_len = c.body_len - off;
         ++n;
       }
+      const uint64_t tw = mono_ns();
       ssize_t wr = ::writev(c.fd, iov, n);
+      stats_.writev_ns.fetch_add(mono_ns() - tw, std::memory_order_relaxed);
+      stats_.writev_calls.fetch_add(1, std::memory_order_relaxed);
       if (wr < 0) {
         if (errno == EINTR) continue;
         if (errno == EAGAIN || errno == EWOULDBLOCK) {
+          stats_.partial_writes.fetch_add(1, std::memory_order_relaxed);
           epoll_event ev{};
           ev.events = EPOLLIN | EPOLLOUT;
           ev.data.fd = c.fd;

@@ -46,6 +46,11 @@ struct HttpStats {
   std::atomic<uint64_t> errors{0};
   std::atomic<uint64_t> accepted{0};
   std::atomic<uint64_t> open_conns{0};
+  // where a response's time goes: writev() syscalls, and writes the socket only took in
+  // part (the rest then waits for EPOLLOUT)
+  std::atomic<uint64_t> writev_calls{0};
+  std::atomic<uint64_t> writev_ns{0};
+  std::atomic<uint64_t> partial_writes{0};
   std::atomic<uint64_t> lat_buckets[kBuckets + 1]{};  // +Inf last, non-cumulative
   std::atomic<uint64_t> lat_sum_ns{0};
   std::atomic<uint64_t> lat_count{0};

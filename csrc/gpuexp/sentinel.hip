@@ -1,21 +1,28 @@
-// HIP sentinel: one 64-lane wave per GPU per tick, on the lowest-priority stream, that
-// stamps the shader clock (s_memtime), the 100 MHz reference clock (s_memrealtime) and
-// the XCC/CU it landed on into a pinned, host-coherent ring.  The sampler never
-// synchronizes: it drains completed slots (seq written last, system-scope release) and
-// launches the next run.  Nothing like it exists in the reference (NVML only,
-// /root/reference/main.go:16); SURVEY.md §2.2 / §7.2 step 6.
+// HIP sentinel: one 64-lane wave per XCD per GPU per tick, on the lowest-priority stream,
+// that stamps the shader clock (s_memtime), the 100 MHz reference clock (s_memrealtime)
+// and the XCC/CU it landed on into a pinned, host-coherent ring.  The sampler never
+// synchronizes: it drains completed runs (each wave writes its seq last, system-scope
+// release) and launches the next run.  Nothing like it exists in the reference (NVML
+// only, /root/reference/main.go:16); SURVEY.md §2.2 / §7.2 step 6.
+//
+// Grid = one workgroup per XCD: the dispatcher deals workgroups round-robin over the
+// XCDs (MI355X_MICROARCH.md "Workgroup dispatch, XCD placement"), so a run of 8 single-wave
+// workgroups puts one wave on each XCD.  Placement is read back, not assumed.
 //
 // Measures, per tick:
-//   sclk      = d(s_memtime) / d(s_memrealtime) * 100 MHz over a dependent ALU chain
-//               (the in-kernel clock recipe of MI355X_MICROARCH.md "DVFS give-back" (6))
-//   latency   = host launch -> first wave start, both in the HSA system time domain
-//               (GPU ticks converted with hsa_amd_profiling_convert_tick_to_system_domain)
-//   xcc_id    = HW_REG_XCC_ID of the wave (round-robin dispatch is observed, not assumed)
-// Cost: one wave on one CU for a few microseconds per tick (<0.01% of a 256-CU chip).
+//   sclk      = median over waves of d(s_memtime) / d(s_memrealtime) * 100 MHz over a
+//               dependent ALU chain (the in-kernel clock recipe of MI355X_MICROARCH.md
+//               "DVFS give-back" (6))
+//   latency   = host launch -> wave start, both in the HSA system time domain (GPU ticks
+//               converted with hsa_amd_profiling_convert_tick_to_system_domain); exported
+//               for the first wave and per XCD (a saturated XCD starts its wave late)
+//   xcc_id    = HW_REG_XCC_ID of workgroup 0
+// Cost: one wave on one CU of each XCD for ~15 us per tick (<0.01% of a 256-CU chip).
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -27,17 +34,19 @@
 
 namespace gpuexp {
 
+constexpr int kSentinelMaxWaves = kMaxXcc;
+
 struct alignas(64) SentinelSlot {
-  uint64_t seq;          // written LAST by the GPU (system-scope release)
-  uint64_t host_launch;  // HSA system timestamp taken just before the launch
+  uint64_t seq;          // written LAST by the wave (system-scope release)
   uint64_t rt0, rt1;     // s_memrealtime at start / end (100 MHz)
   uint64_t mt0, mt1;     // s_memtime at start / end (shader clock)
   uint32_t xcc_id;
   uint32_t hw_id;
-  uint32_t pad[2];
+  uint32_t pad[4];
 };
-static_assert(sizeof(SentinelSlot) == 64, "one cache line per slot");
+static_assert(sizeof(SentinelSlot) == 64, "one cache line per wave: XCDs never share a line");
 
+// ring[run_slot * kSentinelMaxWaves + blockIdx.x]
 __global__ void __launch_bounds__(64) sentinel_kernel(SentinelSlot* __restrict__ ring, uint32_t slot,
                                                       uint64_t seq, int spin) {
   if (threadIdx.x != 0) return;
@@ -55,7 +64,7 @@ __global__ void __launch_bounds__(64) sentinel_kernel(SentinelSlot* __restrict__
   uint32_t xcc, hwid;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
-  SentinelSlot* s = ring + slot;
+  SentinelSlot* s = ring + size_t(slot) * kSentinelMaxWaves + blockIdx.x;
   s->rt0 = rt0;
   s->rt1 = rt1;
   s->mt0 = mt0;
@@ -100,13 +109,16 @@ class HipSentinel : public SentinelSource {
   struct Reading {
     bool ok = false;
     double sclk_hz = 0, latency_s = 0, xcc = 0;
+    double xcc_latency_s[kMaxXcc] = {kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN};
   };
   struct Per {
     int hip = -1;
     bool ready = false;
+    int waves = 1;  // workgroups per run: one per XCD of this GPU / partition
     hipStream_t stream = nullptr;
     SentinelSlot* ring = nullptr;
     SentinelSlot* dring = nullptr;
+    std::vector<uint64_t> host_launch;  // per run slot, HSA system time just before launch
     hsa_agent_t agent{};
     bool have_agent = false;
     uint64_t launched = 0, completed = 0, stalled = 0, errors = 0;
@@ -138,7 +150,8 @@ class HipSentinel : public SentinelSource {
     hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &freq);
     sys_ns_per_tick_ = freq ? 1e9 / double(freq) : 1.0;
     per_.resize(devs.size());
-    int ok = 0;
+    int ok = 0, waves = 0;
+    const size_t ring_bytes = sizeof(SentinelSlot) * size_t(nslots_) * kSentinelMaxWaves;
     for (size_t i = 0; i < devs.size(); ++i) {
       Per& p = per_[i];
       std::string want = devs[i].bdf;
@@ -147,15 +160,15 @@ class HipSentinel : public SentinelSource {
         if (hip_bdf[size_t(h)] == want) p.hip = h;
       if (p.hip < 0) continue;
       if (hipSetDevice(p.hip) != hipSuccess) continue;
+      p.waves = devs[i].num_xcc ? std::min<int>(int(devs[i].num_xcc), kSentinelMaxWaves) : kSentinelMaxWaves;
       int least = 0, greatest = 0;
       (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
       if (hipStreamCreateWithPriority(&p.stream, hipStreamNonBlocking, least) != hipSuccess) continue;
       void* mem = nullptr;
-      if (hipHostMalloc(&mem, sizeof(SentinelSlot) * size_t(nslots_), hipHostMallocCoherent | hipHostMallocMapped) !=
-          hipSuccess)
-        continue;
+      if (hipHostMalloc(&mem, ring_bytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) continue;
       p.ring = static_cast<SentinelSlot*>(mem);
-      std::memset(mem, 0, sizeof(SentinelSlot) * size_t(nslots_));
+      std::memset(mem, 0, ring_bytes);
+      p.host_launch.assign(size_t(nslots_), 0);
       void* dptr = nullptr;
       (void)hipHostGetDevicePointer(&dptr, mem, 0);
       p.dring = static_cast<SentinelSlot*>(dptr ? dptr : mem);
@@ -169,12 +182,14 @@ class HipSentinel : public SentinelSource {
       }
       p.ready = true;
       ++ok;
+      waves += p.waves;
     }
     if (!ok) {
       *err = "no exporter GPU matched a HIP device";
       return false;
     }
-    status_ = "hip sentinel on " + std::to_string(ok) + " GPU(s), ring " + std::to_string(nslots_);
+    status_ = "hip sentinel on " + std::to_string(ok) + " GPU(s), " + std::to_string(waves) +
+              " waves/tick (one per XCD), ring " + std::to_string(nslots_);
     return true;
   }
 
@@ -191,11 +206,12 @@ class HipSentinel : public SentinelSource {
       }
       uint64_t seq = p.launched + 1;
       uint32_t slot = uint32_t(seq % uint64_t(nslots_));
-      SentinelSlot* s = p.ring + slot;
-      __atomic_store_n(&s->seq, 0ull, __ATOMIC_RELAXED);
+      SentinelSlot* s = p.ring + size_t(slot) * kSentinelMaxWaves;
+      for (int w = 0; w < p.waves; ++w) __atomic_store_n(&s[w].seq, 0ull, __ATOMIC_RELAXED);
       (void)hipSetDevice(p.hip);
-      s->host_launch = hsa_now();
-      hipLaunchKernelGGL(sentinel_kernel, dim3(1), dim3(64), 0, p.stream, p.dring, slot, seq, spin_);
+      p.host_launch[slot] = hsa_now();
+      hipLaunchKernelGGL(sentinel_kernel, dim3(unsigned(p.waves)), dim3(64), 0, p.stream, p.dring, slot, seq,
+                         spin_);
       if (hipGetLastError() != hipSuccess) {
         p.errors += 1;
         continue;
@@ -204,28 +220,46 @@ class HipSentinel : public SentinelSource {
     }
   }
 
+  // Host launch -> wave start (seconds), NaN when the clock domains disagree.
+  double wave_latency(const Per& p, const SentinelSlot& w, uint64_t host_launch) const {
+    uint64_t sys = 0;
+    if (!p.have_agent ||
+        hsa_amd_profiling_convert_tick_to_system_domain(p.agent, w.rt0, &sys) != HSA_STATUS_SUCCESS)
+      return std::nan("");
+    double lat = (double(sys) - double(host_launch)) * sys_ns_per_tick_ * 1e-9;
+    // A negative value means the GPU tick and s_memrealtime domains disagree; keep the
+    // rest of the reading and drop the latency rather than export garbage.
+    if (lat > -1e-6 && lat < 10.0) return lat < 0 ? 0 : lat;
+    return std::nan("");
+  }
+
   void drain(Per& p) {
     while (p.completed < p.launched) {
       uint64_t seq = p.completed + 1;
-      SentinelSlot* s = p.ring + (seq % uint64_t(nslots_));
-      if (__atomic_load_n(&s->seq, __ATOMIC_ACQUIRE) != seq) break;
+      uint32_t slot = uint32_t(seq % uint64_t(nslots_));
+      const SentinelSlot* s = p.ring + size_t(slot) * kSentinelMaxWaves;
+      bool done = true;
+      for (int w = 0; w < p.waves && done; ++w) done = __atomic_load_n(&s[w].seq, __ATOMIC_ACQUIRE) == seq;
+      if (!done) break;
       p.completed = seq;
-      double drt = double(s->rt1 - s->rt0);
-      double dmt = double(s->mt1 - s->mt0);
-      Reading r;
+      Reading r = p.last;  // an XCD without a wave this run keeps its previous latency
       r.ok = true;
-      r.sclk_hz = drt > 0 ? dmt / drt * 100e6 : std::nan("");
-      r.xcc = double(s->xcc_id & 0xF);
+      r.xcc = double(s[0].xcc_id & 0xF);
       r.latency_s = std::nan("");
-      if (p.have_agent) {
-        uint64_t sys = 0;
-        if (hsa_amd_profiling_convert_tick_to_system_domain(p.agent, s->rt0, &sys) == HSA_STATUS_SUCCESS) {
-          double lat = (double(sys) - double(s->host_launch)) * sys_ns_per_tick_ * 1e-9;
-          // A negative value means the GPU tick and s_memrealtime domains disagree; keep
-          // the rest of the reading and drop the latency rather than export garbage.
-          if (lat > -1e-6 && lat < 10.0) r.latency_s = lat < 0 ? 0 : lat;
-        }
+      double sclk[kSentinelMaxWaves];
+      int ns = 0;
+      for (int w = 0; w < p.waves; ++w) {
+        double drt = double(s[w].rt1 - s[w].rt0);
+        double dmt = double(s[w].mt1 - s[w].mt0);
+        if (drt > 0) sclk[ns++] = dmt / drt * 100e6;
+        double lat = wave_latency(p, s[w], p.host_launch[slot]);
+        if (std::isnan(lat)) continue;
+        if (std::isnan(r.latency_s) || lat < r.latency_s) r.latency_s = lat;
+        uint32_t x = s[w].xcc_id & 0xF;
+        if (x < uint32_t(kMaxXcc)) r.xcc_latency_s[x] = lat;
       }
+      std::nth_element(sclk, sclk + ns / 2, sclk + ns);
+      r.sclk_hz = ns ? sclk[ns / 2] : std::nan("");
       p.last = r;
     }
   }
@@ -239,6 +273,7 @@ class HipSentinel : public SentinelSource {
     out->dispatch_latency_s = p.last.latency_s;
     out->xcc_id = p.last.xcc;
     out->runs = p.completed;
+    std::copy(std::begin(p.last.xcc_latency_s), std::end(p.last.xcc_latency_s), std::begin(out->xcc_latency_s));
     return true;
   }
 

@@ -232,13 +232,18 @@ def test_sampler_thread_runs(native):
 
 
 def test_full_profile_adds_reliability_families(mock_engine):
-    """`full` = the 64-series standard load + ECC / PCIe AER / NAK / recovery / xGMI link."""
+    """`full` = the 64-series standard load + ECC / PCIe AER / NAK / recovery / xGMI link
+    + per-XCD clocks and per-XCD sentinel dispatch latency (8 XCDs)."""
     e = mock_engine(2, http=False, enable_sentinel=True, enable_counters=True, series_profile="full")
     e.mock_set_value(1, "ecc_ue", 3)
     e.mock_set_value(1, "aer_cor", 7)
     ticks(e, 3)
     fams = parse(e)
-    assert dict(device_series_per_gpu(fams)) == {"0": 74, "1": 74}
+    assert dict(device_series_per_gpu(fams)) == {"0": 90, "1": 90}
+    lat = {s[1]["xcc"]: s[2] for s in fams["amd_gpu_sentinel_xcc_dispatch_latency_seconds"].samples
+           if s[1]["gpu"] == "0"}
+    assert sorted(lat) == [str(x) for x in range(8)] and min(lat.values()) == lat["0"]
+    assert {s[2] for s in fams["amd_gpu_xcc_clock_hz"].samples} == {2.1e9}
     ue = {s[1]["gpu"]: s[2] for s in fams["amd_gpu_ecc_errors_total"].samples
           if s[1]["type"] == "uncorrectable"}
     assert ue == {"0": 0, "1": 3}

@@ -92,6 +92,27 @@ def test_exporter_tick_on_gpu(native):
         e.stop()
 
 
+def test_sentinel_one_wave_per_xcd(native):
+    """Full profile: the sentinel run puts one wave on each XCD (placement read back from
+    HW_REG_XCC_ID) and the PMFW reports each XCD's gfx clock."""
+    e = amdsmi_engine(native, enable_sentinel=True, series_profile="full")
+    try:
+        for _ in range(6):
+            e.tick()
+            time.sleep(0.05)
+        fams = promtext.parse(e.snapshot_text())
+        print(e.source_status())
+    finally:
+        e.stop()
+    lat = {lab["xcc"]: v for _, lab, v in promtext.samples(fams, "amd_gpu_sentinel_xcc_dispatch_latency_seconds")}
+    clk = {lab["xcc"]: v for _, lab, v in promtext.samples(fams, "amd_gpu_xcc_clock_hz")}
+    print("per-XCD latency:", lat, "\nper-XCD clock:", clk)
+    assert len(clk) == 8 and all(50e6 < v < 3.0e9 for v in clk.values()), clk
+    assert sorted(lat) == sorted(clk), (lat, clk)  # every XCD got a wave
+    first = promtext.value(fams, "amd_gpu_sentinel_dispatch_latency_seconds", gpu=0)
+    assert all(0 <= v < 0.5 for v in lat.values()) and 0 <= first < 0.5, (first, lat)
+
+
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 384, 512), (1024, 1024, 1024), (512, 2048, 4096)])
 def test_gemm_bf16_numerics(native, on_gpu, M, N, K):
     import torch
