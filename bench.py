@@ -5,8 +5,9 @@
 One rank per GPU (torchrun for N>1).  Rank 0 starts the exporter as a separate process
 BEFORE touching the GPU (amdsmi backend, raw gpu_metrics fast path, HIP sentinel,
 aqlprofile device counters, full series profile, 10 Hz sampling, every GPU of the job), then every rank becomes a synthetic "GEMM pod":
-each step it launches a burst of bf16 MFMA GEMMs (our HIP kernel) and, for N>1, an RCCL
-all-reduce (DP gradient traffic over xGMI).  Rank 0 scrapes /metrics once per step over a
+each step it launches a burst of bf16 MFMA GEMMs (our HIP kernel) and an RCCL all-reduce
+(DP gradient traffic over xGMI; a 1-rank all-reduce at N=1).  The RCCL tracer tool is
+injected into every rank, so collective calls/bytes are attributed per pod as well.  Rank 0 scrapes /metrics once per step over a
 persistent keep-alive connection with the native client while the GPUs are busy; steps
 are paced at the scrape rate.  Each rank's PID is mapped to a fake pod through a pod-map
 file, so the per-pod families are exercised too.
@@ -51,7 +52,7 @@ def http_get(port: int, path: str, timeout: float = 2.0) -> tuple[int, bytes]:
         c.close()
 
 
-def start_exporter(args, n_gpus: int, backend: str, port: int, pod_map: str, log_path: str):
+def start_exporter(args, n_gpus: int, backend: str, port: int, pod_map: str, log_path: str, rccl_dir: str = ""):
     cmd = [sys.executable, "-m", "kubernetes_gpu_exporter_amd", "--listen", f"127.0.0.1:{port}",
            "--interval", str(1.0 / args.sample_hz), "--backend", backend,
            "--series-profile", args.series_profile, "--control-interval", "0.5", "--log-level", "warn"]
@@ -66,9 +67,12 @@ def start_exporter(args, n_gpus: int, backend: str, port: int, pod_map: str, log
             cmd += ["--enable-sentinel", "true"]
         if args.counters:
             cmd += ["--enable-counters", "true"]
+        if rccl_dir:
+            cmd += ["--enable-rccl", "true", "--rccl-dir", rccl_dir]
     else:
         cmd += ["--mock-devices", str(n_gpus), "--enable-sentinel", "true", "--enable-counters", "true"]
     env = dict(os.environ)
+    env.pop("ROCP_TOOL_LIBRARIES", None)  # the exporter itself issues no collectives
     env["GPUEXP_POD_MAP_FILE"] = pod_map
     env["GPUEXP_POD_ATTRIBUTION"] = "true"
     logf = open(log_path, "w")
@@ -117,6 +121,9 @@ def main() -> int:
     ap.add_argument("--sentinel", type=int, default=1)
     ap.add_argument("--counters", type=int, default=1, help="device PMC counters (aqlprofile plugin)")
     ap.add_argument("--out", default="")
+    ap.add_argument("--rccl-trace", type=int, default=1,
+                    help="inject the RCCL tracer (rocprofiler-sdk tool) into every rank and export per-pod "
+                         "collective calls/bytes")
     ap.add_argument("--exporter", choices=("native", "both"), default="native",
                     help="'both' also measures the reference-architecture exporter (utils/refstyle.py)")
     args = ap.parse_args()
@@ -125,6 +132,18 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     n_gpus = max(args.gpus, world)
+
+    # RCCL visibility per pod: the tracer tool must be in the environment before the HIP
+    # runtime loads (torch's import does that), so set it before importing torch.  All
+    # ranks of one launch share the directory the exporter watches.
+    rccl_dir = ""
+    tracer = os.path.join(ROOT, "kubernetes_gpu_exporter_amd", "libgpuexp_rccl_tracer.so")
+    if args.rccl_trace and os.path.exists(tracer) and os.path.exists("/dev/kfd"):
+        run_id = os.environ.get("TORCHELASTIC_RUN_ID") or os.environ.get("MASTER_PORT") or str(os.getpid())
+        rccl_dir = os.path.join(tempfile.gettempdir(), f"gpuexp-bench-rccl-{run_id}")
+        os.makedirs(rccl_dir, exist_ok=True)
+        os.environ["ROCP_TOOL_LIBRARIES"] = tracer
+        os.environ["GPUEXP_RCCL_DIR"] = rccl_dir
 
     # --- rank 0: exporter first (before this process initialises the GPU) ---
     import torch  # noqa: E402  (import does not initialise HIP; device_count() does not either)
@@ -140,7 +159,7 @@ def main() -> int:
         port = free_port()
         log_path = os.path.join(ROOT, "gpurun_out", "bench_exporter.log")
         try:
-            exporter = start_exporter(args, n_gpus, backend, port, pod_map, log_path)
+            exporter = start_exporter(args, n_gpus, backend, port, pod_map, log_path, rccl_dir)
         except RuntimeError as ex:
             # Never lose the measurement to an optional source: retry without the PMC
             # counters and the sentinel, and say so in the result.
@@ -149,12 +168,20 @@ def main() -> int:
             args.counters, args.sentinel = 0, 0
             degraded = str(ex)
             port = free_port()
-            exporter = start_exporter(args, n_gpus, backend, port, pod_map, log_path)
+            exporter = start_exporter(args, n_gpus, backend, port, pod_map, log_path, rccl_dir)
 
     dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl" if have_gpu else "gloo")
+    elif have_gpu and backend != "mock" and args.allreduce_mb > 0:
+        # N=1 runs the same data-parallel pod (a 1-rank RCCL all-reduce per step), so the
+        # workload and the RCCL path are the same at every N.
+        import torch.distributed as dist
+        if "MASTER_ADDR" in os.environ:  # torchrun (its agent store serves the rendezvous)
+            dist.init_process_group("nccl")
+        else:
+            dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1)
     use_gpu = have_gpu and backend != "mock"
     if use_gpu:
         torch.cuda.set_device(local_rank)
@@ -210,7 +237,7 @@ def main() -> int:
             iters = int(t.item())
 
     # --- pod map: every rank's PID -> fake pod bench/gemm-pod-<rank> ---
-    pid = os.getpid()
+    own_pid = pid = os.getpid()
     if use_gpu:
         # KFD names processes by HOST pid; inside a PID namespace (no hostPID) find ours by
         # a VRAM fingerprint so the exporter can attribute this rank to its fake pod.
@@ -218,16 +245,18 @@ def main() -> int:
         pid = find_own_kfd_pid(local_rank, salt=rank) or pid
     if dist is not None:
         pids = [None] * world
-        dist.all_gather_object(pids, pid)
+        dist.all_gather_object(pids, (pid, own_pid))
     else:
-        pids = [pid]
+        pids = [(pid, own_pid)]
     if rank == 0:
         pods, cgroups = [], {}
-        for r, p in enumerate(pids):
+        for r, (p, op) in enumerate(pids):
             uid = f"00000000-0000-4000-8000-{r:012d}"
             cid = f"{r:064x}"
             pods.append({"uid": uid, "namespace": "bench", "name": f"gemm-pod-{r}", "containers": {cid: "worker"}})
-            cgroups[p] = kubepods_cgroup(uid, cid, qos="guaranteed")
+            # KFD names the rank by host PID; the RCCL tracer by its PID in the exporter's
+            # namespace — the same number unless the box runs us in a PID namespace
+            cgroups[p] = cgroups[op] = kubepods_cgroup(uid, cid, qos="guaranteed")
         write_pod_map(pod_map, pods, cgroups)
         from kubernetes_gpu_exporter_amd.utils import promproto
         client = n.ScrapeClient("127.0.0.1", port, "/metrics", args.gzip, 5000,
@@ -336,6 +365,16 @@ def main() -> int:
         metrics_reads = {lab["kind"]: v for _, lab, v in promtext.samples(fams, "gpuexp_gpu_metrics_reads_total")
                          if lab.get("gpu") == "0"}
         sampler_cpu = [v for _, _, v in promtext.samples(fams, "gpuexp_sampler_cpu_seconds_total")]
+        rccl = {}
+        for sname, lab, v in promtext.samples(fams, "amd_rccl_collective_bytes_total"):
+            rccl.setdefault(lab.get("pod") or lab.get("pid"), {}).setdefault(lab["op"], {})["bytes"] = v
+        for sname, lab, v in promtext.samples(fams, "amd_rccl_collective_calls_total"):
+            rccl.setdefault(lab.get("pod") or lab.get("pid"), {}).setdefault(lab["op"], {})["calls"] = v
+        xgmi = {}
+        for fam_name, key in (("amd_gpu_xgmi_read_bytes_per_second", "read"),
+                              ("amd_gpu_xgmi_write_bytes_per_second", "write")):
+            for _, lab, v in promtext.samples(fams, fam_name):
+                xgmi.setdefault(lab.get("gpu"), {})[key] = v
         tflops = 2.0 * G ** 3 * iters / (gemm_ms * iters * 1e-3) / 1e12 if gemm_ms else None
         result = {
             "metric": METRIC,
@@ -354,7 +393,7 @@ def main() -> int:
                        "global_batch": n_gpus, "seq_len": 0, "parallelism": f"dp{n_gpus}",
                        "scrape_hz": args.scrape_hz, "sample_hz": args.sample_hz, "backend": backend,
                        "series_profile": args.series_profile, "gzip": args.gzip, "protobuf": args.proto,
-                       "gemm": f"{G}^3 x {iters}/step", "allreduce_mb": args.allreduce_mb if world > 1 else 0},
+                       "gemm": f"{G}^3 x {iters}/step", "allreduce_mb": args.allreduce_mb if dist is not None else 0},
             "p50_scrape_us": round(statistics.median(lat), 2) if lat else None,
             "p99_scrape_us": round(pct(lat, 0.99), 2) if lat else None,
             "max_scrape_us": round(max(lat), 2) if lat else None,
@@ -368,12 +407,15 @@ def main() -> int:
             "gpu_gfx_activity_percent": gfx,
             "sentinel": sentinel,
             "workload_gemm_tflops_per_gpu": round(tflops, 1) if tflops else None,
+            "rccl_per_pod": rccl,
+            "xgmi_bytes_per_second": xgmi,
             "families_gpu0": {k: v for k, v in sorted(fam_gpu0.items()) if v},
             "sample_stage_mean_us": stage_us,
             "sample_stage_p50_le_us": stage_p50_us,
             "gpu_metrics_reads_gpu0": metrics_reads,
             "sampler_thread_cpu_s": sampler_cpu[0] if sampler_cpu else None,
             "optional_sources": {"counters": bool(args.counters), "sentinel": bool(args.sentinel),
+                                 "rccl_trace": bool(rccl_dir),
                                  "degraded_reason": degraded},
         }
         stop_proc(exporter)
