@@ -43,6 +43,10 @@ py::dict device_dict(const DeviceInfo& d) {
   o["vram_total"] = d.vram_total;
   o["num_xcc"] = d.num_xcc;
   o["num_cu"] = d.num_cu;
+  o["num_xcc"] = d.num_xcc;
+  o["partition_id"] = d.partition_id;
+  o["compute_partition"] = d.compute_partition;
+  o["memory_partition"] = d.memory_partition;
   py::list peers;
   for (int l = 0; l < kMaxXgmiLinks; ++l) peers.append(d.xgmi_peer_bdf[l]);
   o["xgmi_peers"] = peers;

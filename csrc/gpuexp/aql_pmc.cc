@@ -436,9 +436,14 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_init(int ndev, c
   g_agents.assign(size_t(std::max(0, ndev)), nullptr);
   int ok = 0;
   std::string why;
+  // Partitioned sockets (CPX/DPX/QPX) expose several agents with one BDF, in partition
+  // order, as do the exporter's devices: match the k-th device to the k-th free agent.
+  std::vector<bool> taken(f.gpus.size(), false);
   for (int d = 0; d < ndev; ++d) {
-    for (const auto& g : f.gpus) {
-      if (lower(bdfs[d]) != g.second) continue;
+    for (size_t gi = 0; gi < f.gpus.size(); ++gi) {
+      const auto& g = f.gpus[gi];
+      if (taken[gi] || lower(bdfs[d]) != g.second) continue;
+      taken[gi] = true;
       auto* a = new Agent;
       a->dev = d;
       a->gpu = g.first;

@@ -31,7 +31,7 @@ std::string smi_err(amdsmi_status_t st) {
 inline double u16v(uint16_t v) { return v == 0xFFFF ? kNaN : double(v); }
 
 // amdsmi's decoded struct -> DeviceSample (the slow-path per-tick source).
-void from_amdsmi_metrics(const amdsmi_gpu_metrics_t& m, DeviceSample* out) {
+void from_amdsmi_metrics(const amdsmi_gpu_metrics_t& m, DeviceSample* out, int xcp, int nxcc) {
   out->temp_edge = u16v(m.temperature_edge);
   out->temp_hotspot = u16v(m.temperature_hotspot);
   out->temp_mem = u16v(m.temperature_mem);
@@ -48,15 +48,22 @@ void from_amdsmi_metrics(const amdsmi_gpu_metrics_t& m, DeviceSample* out) {
   out->energy_acc = m.energy_accumulator;
   out->energy_unit_j = 15.259e-6;
   out->fw_ts_10ns = m.firmware_timestamp == ~0ull ? 0 : m.firmware_timestamp;
+  // this partition's XCDs only (same selection as decode_gpu_metrics_v1_8)
+  if (xcp < 0 || xcp >= 8) xcp = 0;
+  const int nx = nxcc > 0 && nxcc <= kMaxXcc ? nxcc : kMaxXcc;
+  const int first = xcp * nx < kMaxXcc ? xcp * nx : 0;
   double sum = 0;
   int n = 0;
-  for (int i = 0; i < AMDSMI_MAX_NUM_GFX_CLKS; ++i)
-    if (m.current_gfxclks[i] != 0xFFFF && m.current_gfxclks[i] != 0) {
-      sum += m.current_gfxclks[i];
-      if (i < kMaxXcc) out->clk_gfx_xcc[i] = m.current_gfxclks[i];
+  for (int i = 0; i < nx && first + i < AMDSMI_MAX_NUM_GFX_CLKS; ++i) {
+    const uint16_t c = m.current_gfxclks[first + i];
+    if (c != 0xFFFF && c != 0) {
+      sum += c;
+      out->clk_gfx_xcc[i] = c;
       ++n;
     }
+  }
   out->clk_gfx = n ? sum / n : u16v(m.current_gfxclk);
+  out->num_partition = m.num_partition == 0xFFFF ? 0 : m.num_partition;
   out->clk_soc = m.current_socclks[0] != 0xFFFF ? double(m.current_socclks[0]) : u16v(m.current_socclk);
   out->clk_mem = u16v(m.current_uclk);
   int nl = 0;
@@ -86,7 +93,7 @@ void from_amdsmi_metrics(const amdsmi_gpu_metrics_t& m, DeviceSample* out) {
   out->res_hbm_thm = m.hbm_thm_residency_acc;
   out->res_prochot = m.prochot_residency_acc;
   out->vram_max_bw_gbs = m.vram_max_bandwidth == ~0ull ? kNaN : double(m.vram_max_bandwidth);
-  for (int c = 0; c < kMaxXcc; ++c) out->gfx_busy_acc[c] = m.xcp_stats[0].gfx_busy_acc[c];
+  for (int c = 0; c < kMaxXcc; ++c) out->gfx_busy_acc[c] = m.xcp_stats[xcp].gfx_busy_acc[c];
 }
 
 bool same_or_both_nan(double a, double b, double tol) {
@@ -105,6 +112,7 @@ class AmdsmiBackend : public Backend {
     uint64_t raw_failures = 0;  // __atomic_* access: sampler writes, describe() reads
     CachedFile vram_used_file;
     double power_cap_w = kNaN;
+    int xcp = 0, nxcc = 0;  // compute partition of this logical GPU (see DeviceInfo)
     std::vector<amdsmi_proc_info_t> procbuf = std::vector<amdsmi_proc_info_t>(64);
   };
 
@@ -162,8 +170,17 @@ class AmdsmiBackend : public Backend {
           info.hip_id = int(en.hip_id);
         }
         amdsmi_kfd_info_t kfd{};
-        if (amdsmi_get_gpu_kfd_info(d.h, &kfd) == AMDSMI_STATUS_SUCCESS && kfd.kfd_id != ~0ull)
-          info.kfd_gpu_id = uint32_t(kfd.kfd_id);
+        if (amdsmi_get_gpu_kfd_info(d.h, &kfd) == AMDSMI_STATUS_SUCCESS) {
+          if (kfd.kfd_id != ~0ull) info.kfd_gpu_id = uint32_t(kfd.kfd_id);
+          if (kfd.current_partition_id != 0xFFFFFFFFu && kfd.current_partition_id < 8)
+            info.partition_id = int(kfd.current_partition_id);
+        }
+        char part[32] = {0};
+        if (amdsmi_get_gpu_compute_partition(d.h, part, sizeof(part) - 1) == AMDSMI_STATUS_SUCCESS)
+          info.compute_partition = trim(part);
+        std::memset(part, 0, sizeof(part));
+        if (amdsmi_get_gpu_memory_partition(d.h, part, sizeof(part) - 1) == AMDSMI_STATUS_SUCCESS)
+          info.memory_partition = trim(part);
         amdsmi_asic_info_t asic{};
         if (amdsmi_get_gpu_asic_info(d.h, &asic) == AMDSMI_STATUS_SUCCESS) {
           info.name = asic.market_name;
@@ -195,6 +212,9 @@ class AmdsmiBackend : public Backend {
           std::string dir = root_ + "/sys/class/drm/renderD" + std::to_string(info.render_minor) + "/device";
           d.vram_used_file.open(dir + "/mem_info_vram_used");
           std::string e;
+          d.gm.set_partition(info.partition_id, int(info.num_xcc));
+          d.xcp = info.partition_id;
+          d.nxcc = int(info.num_xcc);
           if (!force_smi_ && d.gm.open(dir + "/gpu_metrics", &e)) d.fast_ok = validate(d);
           d.gm.set_coalesce(coalesce_metrics_);
           if (!d.fast_ok)
@@ -225,7 +245,7 @@ class AmdsmiBackend : public Backend {
       d.validate_msg = "amdsmi metrics failed";
       return false;
     }
-    from_amdsmi_metrics(m, &b);
+    from_amdsmi_metrics(m, &b, d.xcp, d.nxcc);
     bool ok = same_or_both_nan(a.vram_max_bw_gbs, b.vram_max_bw_gbs, 0) &&
               same_or_both_nan(a.pcie_width, b.pcie_width, 0) &&
               same_or_both_nan(a.pcie_speed_gts, b.pcie_speed_gts, 0) &&
@@ -260,7 +280,7 @@ class AmdsmiBackend : public Backend {
         out->error = "amdsmi_get_gpu_metrics_info: " + smi_err(st);
         return;
       }
-      from_amdsmi_metrics(m, out);
+      from_amdsmi_metrics(m, out, d.xcp, d.nxcc);
     }
     uint64_t used = 0;
     if (d.vram_used_file.read_u64(&used)) {

@@ -113,15 +113,23 @@ bool SysfsBackend::init(std::vector<DeviceInfo>* devices, std::string* err) {
     if (read_small_file(nodes_dir + "/" + n + "/name", &name)) d.name = trim(name);
     found.push_back({(dom << 16) | (loc & 0xFFFF), d});
   }
-  // Stable exporter index order = PCI order (what HIP/amdsmi enumerate by default).
-  std::sort(found.begin(), found.end(),
-            [](const Found& a, const Found& b) { return a.bdf_sort < b.bdf_sort; });
+  // Stable exporter index order = PCI order (what HIP/amdsmi enumerate by default).  The
+  // partitions of one socket (CPX/DPX/QPX) share its BDF; KFD lists them in partition
+  // order, which the stable sort keeps, so the k-th node of a BDF is partition k.
+  std::stable_sort(found.begin(), found.end(),
+                   [](const Found& a, const Found& b) { return a.bdf_sort < b.bdf_sort; });
   for (size_t i = 0; i < found.size(); ++i) {
     DeviceInfo d = found[i].info;
     d.index = int(i);
     d.hip_id = int(i);
+    for (size_t j = i; j > 0 && found[j - 1].bdf_sort == found[i].bdf_sort; --j) d.partition_id += 1;
     auto dev = std::make_unique<Dev>();
     dev->dev_dir = root_ + "/sys/class/drm/renderD" + std::to_string(d.render_minor) + "/device";
+    std::string part;
+    if (read_small_file(dev->dev_dir + "/current_compute_partition", &part)) d.compute_partition = trim(part);
+    if (read_small_file(dev->dev_dir + "/current_memory_partition", &part)) d.memory_partition = trim(part);
+    dev->xcp = d.partition_id;
+    dev->nxcc = int(d.num_xcc);
     uint64_t total = 0;
     if (read_u64_file(dev->dev_dir + "/mem_info_vram_total", &total)) d.vram_total = total;
     open_dev_files(dev.get());
@@ -139,6 +147,7 @@ void SysfsBackend::open_dev_files(Dev* d) {
   std::string e;
   d->gm_ok = d->gm.open(d->dev_dir + "/gpu_metrics", &e);
   d->gm.set_coalesce(coalesce_metrics_);
+  d->gm.set_partition(d->xcp, d->nxcc);
   d->vram_used.open(d->dev_dir + "/mem_info_vram_used");
   d->busy.open(d->dev_dir + "/gpu_busy_percent");
   d->mem_busy.open(d->dev_dir + "/mem_busy_percent");

@@ -111,6 +111,7 @@ class SysfsBackend : public Backend {
     bool gm_ok = false;
     CachedFile vram_used, busy, mem_busy, power, temp_hot, temp_mem, temp_edge;
     double power_cap_w = kNaN;
+    int xcp = 0, nxcc = 0;  // compute partition of this logical GPU (see DeviceInfo)
   };
   void open_dev_files(Dev* d);
   void sample_fallback(Dev& d, DeviceSample* out);

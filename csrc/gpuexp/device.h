@@ -30,8 +30,14 @@ struct DeviceInfo {
   int card = -1;
   int hip_id = -1;
   uint64_t vram_total = 0;    // bytes (static)
-  uint32_t num_xcc = 0;
+  uint32_t num_xcc = 0;        // XCDs of this (logical) GPU: 8 in SPX, 1 in CPX
   uint32_t num_cu = 0;
+  // Compute / memory partitioning of the socket (amdgpu current_compute_partition /
+  // current_memory_partition): SPX|DPX|QPX|CPX and NPS1|NPS2|NPS4.  In a partitioned mode
+  // each partition is its own logical GPU (own KFD node + render node, same PCI BDF);
+  // socket-level telemetry (power, temperatures, xGMI, PCIe) is shared by all of them.
+  std::string compute_partition, memory_partition;
+  int partition_id = 0;        // XCP index of this logical GPU within its socket
   std::string xgmi_peer_bdf[kMaxXgmiLinks];  // from amdsmi_get_link_metrics (once)
 };
 
@@ -62,7 +68,8 @@ struct DeviceSample {
 
   // clocks (MHz); clk_gfx is the mean over the XCDs' own gfx clocks
   double clk_gfx = kNaN, clk_soc = kNaN, clk_mem = kNaN;
-  double clk_gfx_xcc[kMaxXcc] = {kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN};
+  double clk_gfx_xcc[kMaxXcc] = {kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN};  // this GPU's XCDs
+  int num_partition = 0;       // gpu_metrics num_partition (0 = n/a)
 
   // xGMI accumulators (KB) per link; link_up: 1/0, NaN unsupported
   int num_xgmi_links = 0;

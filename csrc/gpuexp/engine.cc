@@ -122,7 +122,8 @@ void Engine::define_families() {
   const auto& D = kDevLabels;
   // --- per-GPU device families (standard profile: 64 series per GPU) ---
   f_info_ = add("amd_gpu_info", "MI355X device identity (value is always 1)", G,
-                {"gpu", "bdf", "uuid", "name", "kfd_gpu_id", "render_node", "hip_id"});
+                {"gpu", "bdf", "uuid", "name", "kfd_gpu_id", "render_node", "hip_id", "partition",
+                 "compute_partition", "memory_partition"});
   f_up_ = add("amd_gpu_up", "1 if the last telemetry read of this GPU succeeded", G, D);
   f_gfx_ = add("amd_gpu_gfx_activity_percent", "Average graphics/compute engine activity (PMFW)", G, D);
   f_umc_ = add("amd_gpu_umc_activity_percent", "Average memory-controller (HBM3E) activity", G, D);
@@ -466,7 +467,8 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
   if (!table_.set(st.info, 1, gen)) {
     st.info = table_.upsert(f_info_, {std::to_string(d.index), d.bdf, d.uuid, d.name, std::to_string(d.kfd_gpu_id),
                                       d.render_minor >= 0 ? "renderD" + std::to_string(d.render_minor) : "",
-                                      std::to_string(d.hip_id)});
+                                      std::to_string(d.hip_id), std::to_string(d.partition_id),
+                                      d.compute_partition, d.memory_partition});
     table_.set(st.info, 1, gen);
   }
   dput(st, i, st.up, f_up_, {}, c.ok ? 1 : 0, gen);
@@ -477,7 +479,10 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
   if (!c.ok) return;  // a failed GPU exports only up=0 (+ errors); others unaffected
   bool compact = cfg_.series_profile == "compact";
 
-  dput(st, i, st.gfx, f_gfx_, {}, c.gfx_activity, gen);
+  // A compute partition (CPX/DPX/QPX) is a slice of the socket: average_gfx_activity is the
+  // socket's, so the logical GPU reports the mean busy of its own XCDs instead (below).
+  const bool partitioned = c.num_partition > 1 || (!d.compute_partition.empty() && d.compute_partition != "SPX");
+  if (!partitioned) dput(st, i, st.gfx, f_gfx_, {}, c.gfx_activity, gen);
   dput(st, i, st.umc, f_umc_, {}, c.umc_activity, gen);
   dput(st, i, st.vram_used, f_vram_used_, {}, c.vram_used, gen);
   dput(st, i, st.vram_total, f_vram_total_, {}, c.vram_total, gen);
@@ -577,6 +582,16 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
         if (acc_delta(c.gfx_busy_acc[x], p.gfx_busy_acc[x], &db)) st.xcc_last[x] = std::min(100.0, db / dacc);
       }
     }
+  }
+  if (partitioned) {
+    double sum = 0;
+    int n = 0;
+    for (uint32_t x = 0; x < nx; ++x)
+      if (!std::isnan(st.xcc_last[x])) {
+        sum += st.xcc_last[x];
+        ++n;
+      }
+    dput(st, i, st.gfx, f_gfx_, {}, n ? sum / n : kNaN, gen);
   }
   for (int k = 0; k < 5; ++k) dput(st, i, st.thr[k], f_thr_, {kThrNames[k]}, st.thr_last[k], gen);
   if (!compact)

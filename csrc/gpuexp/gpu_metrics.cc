@@ -13,7 +13,7 @@ namespace {
 inline double u16v(uint16_t v) { return v == 0xFFFF ? kNaN : double(v); }
 }  // namespace
 
-bool decode_gpu_metrics_v1_8(const void* blob, size_t len, DeviceSample* out) {
+bool decode_gpu_metrics_v1_8(const void* blob, size_t len, DeviceSample* out, int xcp, int nxcc) {
   if (len < sizeof(GpuMetricsV1_8)) return false;
   GpuMetricsV1_8 m;
   std::memcpy(&m, blob, sizeof(m));
@@ -55,19 +55,26 @@ bool decode_gpu_metrics_v1_8(const void* blob, size_t len, DeviceSample* out) {
   out->num_xgmi_links = nl;
   out->xgmi_valid = true;
   out->fw_ts_10ns = m.firmware_timestamp == ~0ull ? 0 : m.firmware_timestamp;
-  // Per-XCC gfx clocks: report the mean of the valid instances.
+  // This partition's XCDs: their gfx clocks (mean of the valid ones = clk_gfx) and busy
+  // accumulators (its own xcp_stats slot).
+  if (xcp < 0 || xcp >= 8) xcp = 0;
+  const int nx = nxcc > 0 && nxcc <= kMaxXcc ? nxcc : kMaxXcc;
+  const int first = xcp * nx < kMaxXcc ? xcp * nx : 0;
   double sum = 0;
   int n = 0;
-  for (int i = 0; i < kMaxXcc; ++i)
-    if (m.current_gfxclk[i] != 0xFFFF && m.current_gfxclk[i] != 0) {
-      sum += m.current_gfxclk[i];
-      out->clk_gfx_xcc[i] = m.current_gfxclk[i];
+  for (int i = 0; i < nx && first + i < kMaxXcc; ++i) {
+    const uint16_t c = m.current_gfxclk[first + i];
+    if (c != 0xFFFF && c != 0) {
+      sum += c;
+      out->clk_gfx_xcc[i] = c;
       ++n;
     }
+  }
   out->clk_gfx = n ? sum / n : kNaN;
   out->clk_soc = u16v(m.current_socclk[0]);
   out->clk_mem = u16v(m.current_uclk);
-  for (int c = 0; c < kMaxXcc; ++c) out->gfx_busy_acc[c] = m.xcp_stats[0].gfx_busy_acc[c];
+  out->num_partition = m.num_partition == 0xFFFF ? 0 : m.num_partition;
+  for (int c = 0; c < kMaxXcc; ++c) out->gfx_busy_acc[c] = m.xcp_stats[xcp].gfx_busy_acc[c];
   return true;
 }
 
@@ -86,6 +93,8 @@ GpuMetricsReader& GpuMetricsReader::operator=(GpuMetricsReader&& o) noexcept {
   fmt_ = o.fmt_;
   content_ = o.content_;
   coalesce_ = o.coalesce_;
+  xcp_ = o.xcp_;
+  nxcc_ = o.nxcc_;
   last_n_ = o.last_n_;
   last_fw_ts_ = o.last_fw_ts_;
   t_change_ns_ = o.t_change_ns_;
@@ -141,7 +150,7 @@ bool GpuMetricsReader::read(DeviceSample* out, uint64_t now_ns) {
     coalesced_reads_ += 1;
     last_was_fresh_ = false;
     out->metrics_coalesced = true;
-    return decode_gpu_metrics_v1_8(buf_, size_t(last_n_), out);
+    return decode_gpu_metrics_v1_8(buf_, size_t(last_n_), out, xcp_, nxcc_);
   }
   long n = pread_once(fd_, reinterpret_cast<char*>(buf_), sizeof(buf_));
   if (n <= 0) {
@@ -151,7 +160,7 @@ bool GpuMetricsReader::read(DeviceSample* out, uint64_t now_ns) {
   }
   last_n_ = n;
   fresh_reads_ += 1;
-  if (!decode_gpu_metrics_v1_8(buf_, size_t(n), out)) {
+  if (!decode_gpu_metrics_v1_8(buf_, size_t(n), out, xcp_, nxcc_)) {
     last_n_ = 0;
     out->error = "gpu_metrics decode failed";
     return false;

@@ -93,7 +93,10 @@ static_assert(offsetof(GpuMetricsV1_8, xcp_stats) == 344, "v1.8 layout");
 static_assert(sizeof(GpuMetricsV1_8) == 3872, "v1.8 size (measured blob size)");
 
 // Decodes a v1.8 blob into `out`.  Returns false if the header does not match.
-bool decode_gpu_metrics_v1_8(const void* blob, size_t len, DeviceSample* out);
+// `xcp` / `nxcc` select the compute partition a logical GPU is (SPX: xcp 0 with all 8
+// XCDs; CPX: xcp k owns XCD k): its per-XCD busy accumulators come from xcp_stats[xcp]
+// and its gfx clocks from current_gfxclk[xcp*nxcc, (xcp+1)*nxcc).  nxcc 0 = every XCD.
+bool decode_gpu_metrics_v1_8(const void* blob, size_t len, DeviceSample* out, int xcp = 0, int nxcc = 0);
 
 // Reader for one device's gpu_metrics file: keeps the fd open and pread()s from 0.
 // Reads <dev>/gpu_metrics.  Each fresh read makes the driver fetch the table from the SMU
@@ -121,6 +124,10 @@ class GpuMetricsReader {
   uint8_t content() const { return content_; }
   const std::string& path() const { return path_; }
   void set_coalesce(bool on) { coalesce_ = on; }
+  void set_partition(int xcp, int nxcc) {
+    xcp_ = xcp;
+    nxcc_ = nxcc;
+  }
   // Never reuse a table for longer than this, whatever the learnt period.
   static constexpr uint64_t kMaxCoalesceNs = 50000000;
   uint64_t period_ns() const { return period_ns_; }
@@ -132,6 +139,7 @@ class GpuMetricsReader {
   std::string path_;
   uint8_t fmt_ = 0, content_ = 0;
   bool coalesce_ = true;
+  int xcp_ = 0, nxcc_ = 0;
   long last_n_ = 0;
   uint64_t last_fw_ts_ = 0;      // firmware_timestamp of the cached table (10 ns units)
   uint64_t t_change_ns_ = 0;     // estimated host time the cached table appeared

@@ -108,7 +108,8 @@ int tool_init(rocprofiler_client_finalize_t fini, void*) {
     std::snprintf(bdf, sizeof(bdf), "%04x:%02x:%02x.%x", a.domain, (a.location_id >> 8) & 0xFF,
                   (a.location_id >> 3) & 0x1F, a.location_id & 0x7);
     for (size_t d = 0; d < g_want_bdfs.size(); ++d) {
-      if (lower(g_want_bdfs[d]) != bdf) continue;
+      // several agents share a BDF on a partitioned socket: first free device slot wins
+      if (lower(g_want_bdfs[d]) != bdf || g_agents[d].dev >= 0) continue;
       Agent& ag = g_agents[d];
       ag.id = a.id;
       ag.dev = int(d);

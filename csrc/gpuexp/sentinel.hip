@@ -152,12 +152,18 @@ class HipSentinel : public SentinelSource {
     per_.resize(devs.size());
     int ok = 0, waves = 0;
     const size_t ring_bytes = sizeof(SentinelSlot) * size_t(nslots_) * kSentinelMaxWaves;
+    // Partitioned sockets (CPX/DPX/QPX) expose several HIP devices with one BDF, in
+    // partition order, as do the exporter's devices: the k-th takes the k-th free one.
+    std::vector<bool> taken(size_t(nhip), false);
     for (size_t i = 0; i < devs.size(); ++i) {
       Per& p = per_[i];
       std::string want = devs[i].bdf;
       for (auto& c : want) c = char(::tolower(c));
-      for (int h = 0; h < nhip; ++h)
-        if (hip_bdf[size_t(h)] == want) p.hip = h;
+      for (int h = 0; h < nhip && p.hip < 0; ++h)
+        if (!taken[size_t(h)] && hip_bdf[size_t(h)] == want) {
+          p.hip = h;
+          taken[size_t(h)] = true;
+        }
       if (p.hip < 0) continue;
       if (hipSetDevice(p.hip) != hipSuccess) continue;
       p.waves = devs[i].num_xcc ? std::min<int>(int(devs[i].num_xcc), kSentinelMaxWaves) : kSentinelMaxWaves;

@@ -19,8 +19,10 @@ def encode_gpu_metrics_v1_8(*, hotspot=46, mem=34, vrsoc=41, power=244, gfx=0, u
                             ppt_res=2146364, pcie_width=16, pcie_speed=320, xgmi_width=16, xgmi_speed=38,
                             pcie_bw_acc=912039705430, pcie_bw_inst=18, xgmi_rd=None, xgmi_wr=None,
                             xgmi_status=None, fw_ts=105165583750064, gfxclk=(111,) * 8, socclk=38,
-                            uclk=2000, gfx_busy_acc=(0,) * 8) -> bytes:
-    """Packs a gpu_metrics format-1.8 blob with the field offsets the C++ decoder uses."""
+                            uclk=2000, gfx_busy_acc=(0,) * 8, num_partition=1, xcp_busy_acc=None) -> bytes:
+    """Packs a gpu_metrics format-1.8 blob with the field offsets the C++ decoder uses.
+    xcp_busy_acc: {partition: 8 per-XCD busy accumulators} for partitioned sockets
+    (xcp_stats[k], 440 bytes each); gfx_busy_acc is partition 0's."""
     xgmi_rd = list(xgmi_rd or [0] * 8)
     xgmi_wr = list(xgmi_wr or [0] * 8)
     xgmi_status = list(xgmi_status or [0xFFFF] + [1] * 7)
@@ -40,9 +42,11 @@ def encode_gpu_metrics_v1_8(*, hotspot=46, mem=34, vrsoc=41, power=244, gfx=0, u
     struct.pack_into("<8H", b, 296, *gfxclk)
     struct.pack_into("<4H", b, 312, socclk, 0xFFFF, 0xFFFF, 0xFFFF)
     struct.pack_into("<H", b, 336, uclk)
-    struct.pack_into("<H", b, 338, 1)
-    # xcp_stats[0].gfx_busy_acc at 344 + 120
+    struct.pack_into("<H", b, 338, num_partition)
+    # xcp_stats[k].gfx_busy_acc at 344 + 440 * k + 120
     struct.pack_into("<8Q", b, 344 + 120, *gfx_busy_acc)
+    for k, acc in (xcp_busy_acc or {}).items():
+        struct.pack_into("<8Q", b, 344 + 440 * k + 120, *acc)
     return bytes(b)
 
 
@@ -56,6 +60,9 @@ class FakeGpu:
     vram_total: int = 309220868096
     vram_used: int = 297766912
     metrics: dict = field(default_factory=dict)
+    num_xcc: int = 8                 # 1 per partition in CPX mode
+    compute_partition: str = "SPX"   # SPX | DPX | QPX | CPX
+    memory_partition: str = "NPS1"
 
 
 class FakeHost:
@@ -77,7 +84,7 @@ class FakeHost:
         self._w(f"{nd}/name", "ip discovery\n")
         props = {"simd_count": 1024, "simd_per_cu": 4, "array_count": 32, "location_id": gpu.location_id,
                  "domain": 0, "drm_render_minor": gpu.render_minor, "unique_id": gpu.unique_id,
-                 "device_id": gpu.device_id, "num_xcc": 8, "gfx_target_version": 90500,
+                 "device_id": gpu.device_id, "num_xcc": gpu.num_xcc, "gfx_target_version": 90500,
                  "max_engine_clk_fcompute": 2400}
         self._w(f"{nd}/properties", "".join(f"{k} {v}\n" for k, v in props.items()))
         dev = f"sys/class/drm/renderD{gpu.render_minor}/device"
@@ -85,6 +92,8 @@ class FakeHost:
         self._w(f"{dev}/mem_info_vram_used", f"{gpu.vram_used}\n")
         self._w(f"{dev}/gpu_busy_percent", "0\n")
         self._w(f"{dev}/mem_busy_percent", "0\n")
+        self._w(f"{dev}/current_compute_partition", gpu.compute_partition + "\n")
+        self._w(f"{dev}/current_memory_partition", gpu.memory_partition + "\n")
         self._w(f"{dev}/hwmon/hwmon0/power1_input", "244000000\n")
         self._w(f"{dev}/hwmon/hwmon0/power1_cap", "1400000000\n")
         self._w(f"{dev}/hwmon/hwmon0/temp2_label", "junction\n")
@@ -166,6 +175,19 @@ def kubepods_cgroup(uid: str, container_id: str, qos: str = "burstable", driver:
     if qos == "guaranteed":
         return f"/kubepods/pod{uid}/{container_id}"
     return f"/kubepods/{qos}/pod{uid}/{container_id}"
+
+
+def mi355x_cpx_socket(root, bus: int = 0x72, partitions: int = 8) -> FakeHost:
+    """One MI355X socket in CPX mode: `partitions` logical GPUs (one XCD each), each with
+    its own KFD node, gpu_id and render node but the socket's PCI BDF and gpu_metrics."""
+    h = FakeHost(root)
+    h.add_cpu_node(0)
+    for k in range(partitions):
+        h.add_gpu(1 + k, FakeGpu(gpu_id=41000 + 13 * k, location_id=bus << 8, render_minor=128 + k,
+                                 num_xcc=8 // partitions, compute_partition="CPX" if partitions == 8 else
+                                 {2: "DPX", 4: "QPX"}.get(partitions, "SPX"), memory_partition="NPS4",
+                                 vram_total=309220868096 // 4))
+    return h
 
 
 def mi355x_node(root, n_gpus: int = 8) -> FakeHost:

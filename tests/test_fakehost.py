@@ -326,3 +326,56 @@ def test_hip_order_bdfs_and_bdf_device_filter(native, tmp_path, monkeypatch):
     up = promtext.samples(promtext.parse(e.snapshot_text()), "amd_gpu_up")
     assert [s[1]["bdf"] for s in up] == [order[2]]
     e.stop()
+
+
+def test_cpx_partitions_are_logical_gpus(native, tmp_path):
+    """An MI355X socket in CPX mode: 8 logical GPUs sharing one BDF and one gpu_metrics
+    table.  Each reports its own XCD's busy (xcp_stats[k]) and clock (current_gfxclk[k])
+    as its gfx activity, not the socket's average_gfx_activity."""
+    from kubernetes_gpu_exporter_amd.utils.fakehost import mi355x_cpx_socket
+    h = mi355x_cpx_socket(tmp_path)
+    clocks = tuple(1800 + 10 * k for k in range(8))
+
+    def write(accum, busy):
+        for g in h.gpus:  # the same socket table behind every partition's render node
+            h.set_metrics(g, gfx=99, accum=accum, gfxclk=clocks, num_partition=8,
+                          xcp_busy_acc={k: (busy[k],) + (0,) * 7 for k in range(8)})
+
+    write(1000, [0] * 8)
+    devs = native.read_backend("sysfs", str(tmp_path))
+    assert [d["partition_id"] for d in devs] == list(range(8))
+    assert {d["bdf"] for d in devs} == {"0000:72:00.0"}
+    assert {(d["compute_partition"], d["memory_partition"], d["num_xcc"]) for d in devs} == {("CPX", "NPS4", 1)}
+    e = _engine(native, tmp_path, series_profile="full")
+    try:
+        e.tick(S)
+        write(2000, [10 * k * 1000 for k in range(8)])  # partition k: 10*k % busy over 1000 ticks
+        e.tick(2 * S)
+        fams = promtext.parse(e.snapshot_text())
+        info = {s[1]["gpu"]: s[1] for s in fams["amd_gpu_info"].samples}
+        assert [info[str(k)]["partition"] for k in range(8)] == [str(k) for k in range(8)]
+        assert {i["compute_partition"] for i in info.values()} == {"CPX"}
+        gfx = {s[1]["gpu"]: s[2] for s in fams["amd_gpu_gfx_activity_percent"].samples}
+        assert gfx == {str(k): 10.0 * k for k in range(8)}  # per partition, not the socket's 99 %
+        clk = {(s[1]["gpu"], s[1]["xcc"]): s[2] for s in fams["amd_gpu_xcc_clock_hz"].samples}
+        assert clk == {(str(k), "0"): clocks[k] * 1e6 for k in range(8)}
+        xcc = {(s[1]["gpu"], s[1]["xcc"]) for s in fams["amd_gpu_xcc_busy_percent"].samples}
+        assert xcc == {(str(k), "0") for k in range(8)}  # one XCD per logical GPU
+    finally:
+        e.stop()
+
+
+def test_spx_socket_keeps_socket_activity(native, tmp_path):
+    h = mi355x_node(tmp_path, 1)
+    h.set_metrics(h.gpus[0], gfx=42, accum=1000)
+    e = _engine(native, tmp_path)
+    try:
+        e.tick(S)
+        h.set_metrics(h.gpus[0], gfx=42, accum=2000, gfx_busy_acc=(50_000,) * 8)
+        e.tick(2 * S)
+        fams = promtext.parse(e.snapshot_text())
+        assert promtext.value(fams, "amd_gpu_gfx_activity_percent", gpu=0) == 42
+        (inf,) = fams["amd_gpu_info"].samples
+        assert (inf[1]["partition"], inf[1]["compute_partition"], inf[1]["memory_partition"]) == ("0", "SPX", "NPS1")
+    finally:
+        e.stop()
