@@ -42,6 +42,11 @@ def test_amdsmi_backend_and_fast_path(native):
     assert 50 < s["power_w"] < 2000
     assert s["vram_max_bw_gbs"] > 1000
     assert "validated" in d["source"], d["source"]
+    # partition identity from amdsmi (SPX/NPS1 on the gpurun boxes; CPX splits a socket)
+    print("partition:", {k: d[k] for k in ("partition_id", "compute_partition", "memory_partition", "num_xcc")})
+    assert d["compute_partition"] in ("SPX", "DPX", "QPX", "CPX"), d
+    assert d["memory_partition"].startswith("NPS"), d
+    assert d["num_xcc"] == {"SPX": 8, "DPX": 4, "QPX": 2, "CPX": 1}[d["compute_partition"]], d
 
 
 def test_raw_gpu_metrics_matches_amdsmi_python(native):
