@@ -180,8 +180,11 @@ bool MockBackend::sentinel(const DeviceInfo& dev, SentinelReading* out) {
   out->dispatch_latency_s = get(s, "sentinel_latency_s", 8e-6);
   out->xcc_id = double(dev.index % 8);
   // One wave per XCD; later workgroups of the round-robin deal start a little later.
-  for (uint32_t x = 0; x < dev.num_xcc && x < uint32_t(kMaxXcc); ++x)
+  out->mem_latency_s = get(s, "sentinel_memory_latency_s", 1.2e-6);
+  for (uint32_t x = 0; x < dev.num_xcc && x < uint32_t(kMaxXcc); ++x) {
     out->xcc_latency_s[x] = out->dispatch_latency_s + 0.1e-6 * x;
+    out->xcc_mem_latency_s[x] = out->mem_latency_s;
+  }
   out->runs = s.started ? uint64_t(s.accum) : 0;
   return true;
 }

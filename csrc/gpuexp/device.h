@@ -136,6 +136,9 @@ struct SentinelReading {
   uint64_t runs = 0;                  // completed sentinel runs
   // host launch -> wave start on each XCD (indexed by HW_REG_XCC_ID; NaN = no wave there yet)
   double xcc_latency_s[kMaxXcc] = {kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN};
+  // dependent uncached device-memory load latency (mean over waves; per XCD by XCC_ID)
+  double mem_latency_s = kNaN;
+  double xcc_mem_latency_s[kMaxXcc] = {kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN};
 };
 
 class Backend {

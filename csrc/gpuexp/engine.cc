@@ -175,11 +175,16 @@ void Engine::define_families() {
                    "Host launch to first-wave start of the sentinel kernel (queue contention)", G, D);
   f_sen_xcc_ = add("amd_gpu_sentinel_xcc_id", "XCC that workgroup 0 of the last sentinel run landed on", G, D);
   f_sen_runs_ = add("amd_gpu_sentinel_runs_total", "Completed sentinel kernel runs", C, D);
+  f_sen_mem_ = add("amd_gpu_sentinel_memory_latency_seconds",
+                   "Dependent-load latency of the sentinel's uncached device-memory chain: memory-path contention probe", G, D);
   // --- full profile: per-XCD detail (8 XCDs on an SPX-mode MI355X) ---
   f_xcc_clk_ = add("amd_gpu_xcc_clock_hz", "Per-XCD gfx clock (PMFW current_gfxclk of each XCC)", G,
                    with(D, {"xcc"}));
   f_sen_xlat_ = add("amd_gpu_sentinel_xcc_dispatch_latency_seconds",
                     "Host launch to sentinel wave start on each XCD (per-XCD CU contention)", G, with(D, {"xcc"}));
+  f_sen_xmem_ = add("amd_gpu_sentinel_xcc_memory_latency_seconds",
+                    "Sentinel memory-chain load latency seen from each XCD (memory-path contention probe)", G,
+                    with(D, {"xcc"}));
 
   // --- per-process / per-pod families ---
   const std::vector<std::string> P = {"gpu", "pid", "comm", "namespace", "pod", "container"};
@@ -628,10 +633,15 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
     dput(st, i, st.sen[1], f_sen_lat_, {}, sr.dispatch_latency_s, gen);
     dput(st, i, st.sen[2], f_sen_xcc_, {}, sr.xcc_id, gen);
     dput(st, i, st.sen[3], f_sen_runs_, {}, double(sr.runs), gen);
-    if (cfg_.series_profile == "full")
-      for (int x = 0; x < kMaxXcc; ++x)
+    if (cfg_.series_profile == "full") {
+      dput(st, i, st.sen_mem, f_sen_mem_, {}, sr.mem_latency_s, gen);
+      for (int x = 0; x < kMaxXcc; ++x) {
         if (!std::isnan(sr.xcc_latency_s[x]))
           dput(st, i, st.sen_xlat[x], f_sen_xlat_, {std::to_string(x)}, sr.xcc_latency_s[x], gen);
+        if (!std::isnan(sr.xcc_mem_latency_s[x]))
+          dput(st, i, st.sen_xmem[x], f_sen_xmem_, {std::to_string(x)}, sr.xcc_mem_latency_s[x], gen);
+      }
+    }
   }
 }
 

@@ -17,7 +17,12 @@
 //               converted with hsa_amd_profiling_convert_tick_to_system_domain); exported
 //               for the first wave and per XCD (a saturated XCD starts its wave late)
 //   xcc_id    = HW_REG_XCC_ID of workgroup 0
-// Cost: one wave on one CU of each XCD for ~15 us per tick (<0.01% of a 256-CU chip).
+//   mem lat.  = 16 dependent loads through an uncached (hipDeviceMallocUncached) 64 KiB
+//               chain, 4 KiB apart: load latency on the memory path as the running pods
+//               leave it, per XCD and averaged.  Measured on MI355X (profiles/r01/
+//               sentinel_memory_latency.txt): ~110 ns/hop idle, ~640 ns under an MFMA GEMM,
+//               ~910 ns under a 5 TB/s HBM copy -- a contention probe, not a DRAM spec.
+// Cost: one wave on one CU of each XCD for ~15 us + 16 loads per tick (<0.01% of the chip).
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
@@ -38,17 +43,25 @@ constexpr int kSentinelMaxWaves = kMaxXcc;
 
 struct alignas(64) SentinelSlot {
   uint64_t seq;          // written LAST by the wave (system-scope release)
-  uint64_t rt0, rt1;     // s_memrealtime at start / end (100 MHz)
+  uint64_t rt0, rt1;     // s_memrealtime at start / end of the clock window (100 MHz)
   uint64_t mt0, mt1;     // s_memtime at start / end (shader clock)
   uint32_t xcc_id;
   uint32_t hw_id;
-  uint32_t pad[4];
+  uint64_t chase_rt;     // s_memrealtime ticks for `hops` dependent uncached HBM loads
+  uint32_t hops;
+  uint32_t chase_end;    // last index reached (keeps the chain live; must be 0)
 };
 static_assert(sizeof(SentinelSlot) == 64, "one cache line per wave: XCDs never share a line");
 
+// Pointer chase for the memory-latency probe: `kChaseHops` 4-byte links 4 KiB apart in an
+// uncached device buffer; each hop is a dependent volatile load, so the chain time is
+// the memory path's load latency under the current traffic.  hop i -> i+1, last -> 0.
+constexpr int kChaseHops = 16;
+constexpr size_t kChaseStride = 4096 / sizeof(uint32_t);
+
 // ring[run_slot * kSentinelMaxWaves + blockIdx.x]
 __global__ void __launch_bounds__(64) sentinel_kernel(SentinelSlot* __restrict__ ring, uint32_t slot,
-                                                      uint64_t seq, int spin) {
+                                                      uint64_t seq, int spin, const uint32_t* chase, int hops) {
   if (threadIdx.x != 0) return;
   uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
   uint64_t mt0 = __builtin_amdgcn_s_memtime();
@@ -61,6 +74,11 @@ __global__ void __launch_bounds__(64) sentinel_kernel(SentinelSlot* __restrict__
   }
   uint64_t mt1 = __builtin_amdgcn_s_memtime();
   uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+  // HBM load latency under whatever the GPU is doing now: a chain of dependent loads.
+  uint32_t idx = 0;
+  uint64_t rt2 = __builtin_amdgcn_s_memrealtime();
+  for (int h = 0; h < hops; ++h) idx = reinterpret_cast<const volatile uint32_t*>(chase)[size_t(idx) * kChaseStride];
+  uint64_t rt3 = __builtin_amdgcn_s_memrealtime();
   uint32_t xcc, hwid;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
@@ -71,6 +89,9 @@ __global__ void __launch_bounds__(64) sentinel_kernel(SentinelSlot* __restrict__
   s->mt1 = mt1;
   s->xcc_id = xcc;
   s->hw_id = hwid ^ (x & 0u);  // keep x live without changing hw_id
+  s->chase_rt = rt3 - rt2;
+  s->hops = uint32_t(hops);
+  s->chase_end = idx;
   __atomic_thread_fence(__ATOMIC_RELEASE);  // orders the payload before seq (system scope below)
   __hip_atomic_store(&s->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -110,6 +131,8 @@ class HipSentinel : public SentinelSource {
     bool ok = false;
     double sclk_hz = 0, latency_s = 0, xcc = 0;
     double xcc_latency_s[kMaxXcc] = {kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN};
+    double mem_latency_s = kNaN;
+    double xcc_mem_latency_s[kMaxXcc] = {kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN};
   };
   struct Per {
     int hip = -1;
@@ -118,6 +141,8 @@ class HipSentinel : public SentinelSource {
     hipStream_t stream = nullptr;
     SentinelSlot* ring = nullptr;
     SentinelSlot* dring = nullptr;
+    uint32_t* chase = nullptr;  // uncached device buffer of the HBM latency probe
+    int hops = 0;
     std::vector<uint64_t> host_launch;  // per run slot, HSA system time just before launch
     hsa_agent_t agent{};
     bool have_agent = false;
@@ -175,6 +200,19 @@ class HipSentinel : public SentinelSource {
       p.ring = static_cast<SentinelSlot*>(mem);
       std::memset(mem, 0, ring_bytes);
       p.host_launch.assign(size_t(nslots_), 0);
+      // HBM latency probe chain (64 KiB, uncached); without it the kernel skips the probe.
+      void* chase = nullptr;
+      const size_t chase_words = size_t(kChaseHops) * kChaseStride;
+      if (hipExtMallocWithFlags(&chase, chase_words * sizeof(uint32_t), hipDeviceMallocUncached) == hipSuccess) {
+        std::vector<uint32_t> links(chase_words, 0);
+        for (int h = 0; h < kChaseHops; ++h) links[size_t(h) * kChaseStride] = uint32_t((h + 1) % kChaseHops);
+        if (hipMemcpy(chase, links.data(), chase_words * sizeof(uint32_t), hipMemcpyHostToDevice) == hipSuccess) {
+          p.chase = static_cast<uint32_t*>(chase);
+          p.hops = kChaseHops;
+        } else {
+          (void)hipFree(chase);
+        }
+      }
       void* dptr = nullptr;
       (void)hipHostGetDevicePointer(&dptr, mem, 0);
       p.dring = static_cast<SentinelSlot*>(dptr ? dptr : mem);
@@ -217,7 +255,7 @@ class HipSentinel : public SentinelSource {
       (void)hipSetDevice(p.hip);
       p.host_launch[slot] = hsa_now();
       hipLaunchKernelGGL(sentinel_kernel, dim3(unsigned(p.waves)), dim3(64), 0, p.stream, p.dring, slot, seq,
-                         spin_);
+                         spin_, p.chase, p.hops);
       if (hipGetLastError() != hipSuccess) {
         p.errors += 1;
         continue;
@@ -254,10 +292,19 @@ class HipSentinel : public SentinelSource {
       r.latency_s = std::nan("");
       double sclk[kSentinelMaxWaves];
       int ns = 0;
+      double mem_sum = 0;
+      int mem_n = 0;
       for (int w = 0; w < p.waves; ++w) {
         double drt = double(s[w].rt1 - s[w].rt0);
         double dmt = double(s[w].mt1 - s[w].mt0);
         if (drt > 0) sclk[ns++] = dmt / drt * 100e6;
+        if (s[w].hops > 0 && s[w].chase_end == 0) {  // 100 MHz ticks per hop -> seconds
+          const double hl = double(s[w].chase_rt) * 10e-9 / double(s[w].hops);
+          mem_sum += hl;
+          ++mem_n;
+          const uint32_t hx = s[w].xcc_id & 0xF;
+          if (hx < uint32_t(kMaxXcc)) r.xcc_mem_latency_s[hx] = hl;
+        }
         double lat = wave_latency(p, s[w], p.host_launch[slot]);
         if (std::isnan(lat)) continue;
         if (std::isnan(r.latency_s) || lat < r.latency_s) r.latency_s = lat;
@@ -266,6 +313,7 @@ class HipSentinel : public SentinelSource {
       }
       std::nth_element(sclk, sclk + ns / 2, sclk + ns);
       r.sclk_hz = ns ? sclk[ns / 2] : std::nan("");
+      r.mem_latency_s = mem_n ? mem_sum / mem_n : std::nan("");
       p.last = r;
     }
   }
@@ -280,6 +328,9 @@ class HipSentinel : public SentinelSource {
     out->xcc_id = p.last.xcc;
     out->runs = p.completed;
     std::copy(std::begin(p.last.xcc_latency_s), std::end(p.last.xcc_latency_s), std::begin(out->xcc_latency_s));
+    out->mem_latency_s = p.last.mem_latency_s;
+    std::copy(std::begin(p.last.xcc_mem_latency_s), std::end(p.last.xcc_mem_latency_s),
+              std::begin(out->xcc_mem_latency_s));
     return true;
   }
 
@@ -291,6 +342,7 @@ class HipSentinel : public SentinelSource {
       drain(p);
       (void)hipStreamDestroy(p.stream);
       (void)hipHostFree(p.ring);
+      if (p.chase) (void)hipFree(p.chase);
       p.ready = false;
     }
     per_.clear();

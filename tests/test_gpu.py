@@ -116,6 +116,12 @@ def test_sentinel_one_wave_per_xcd(native):
     assert sorted(lat) == sorted(clk), (lat, clk)  # every XCD got a wave
     first = promtext.value(fams, "amd_gpu_sentinel_dispatch_latency_seconds", gpu=0)
     assert all(0 <= v < 0.5 for v in lat.values()) and 0 <= first < 0.5, (first, lat)
+    # memory-latency probe: dependent uncached loads (~110 ns/hop idle on MI355X)
+    hbm = promtext.value(fams, "amd_gpu_sentinel_memory_latency_seconds", gpu=0)
+    xhbm = {lab["xcc"]: v for _, lab, v in promtext.samples(fams, "amd_gpu_sentinel_xcc_memory_latency_seconds")}
+    print("memory-chain load latency:", hbm, xhbm)
+    assert 20e-9 < hbm < 50e-6, hbm
+    assert sorted(xhbm) == sorted(clk), xhbm
 
 
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 384, 512), (1024, 1024, 1024), (512, 2048, 4096)])
