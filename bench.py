@@ -13,7 +13,11 @@ are paced at the scrape rate.  Each rank's PID is mapped to a fake pod through a
 file, so the per-pod families are exercised too.
 
 value = p50 scrape latency (us, whole job: one exporter serves all N GPUs), lower is
-better; exporter CPU% over the timed window is reported alongside.
+better; exporter CPU% over the timed window is reported alongside.  Scrapes send what
+Prometheus sends by default (`Accept-Encoding: gzip`; the exporter compresses once per
+tick on the sampler, only while someone asks); latency is request sent -> last response
+byte received.  A second timed phase repeats the K steps with identity-encoded (plain
+text) responses and reports p50_scrape_identity_us (`--no-gzip` makes that the headline).
 """
 from __future__ import annotations
 
@@ -114,7 +118,12 @@ def main() -> int:
     ap.add_argument("--gemm", type=int, default=8192, help="GEMM edge (M=N=K) of the synthetic pod")
     ap.add_argument("--busy", type=float, default=0.6, help="target GPU-busy fraction of each step")
     ap.add_argument("--allreduce-mb", type=float, default=64.0)
-    ap.add_argument("--gzip", action="store_true", help="scrape with Accept-Encoding: gzip")
+    ap.add_argument("--gzip", dest="gzip", action="store_true", default=True,
+                    help="scrape with Accept-Encoding: gzip, as Prometheus does by default (default)")
+    ap.add_argument("--no-gzip", dest="gzip", action="store_false",
+                    help="headline scrape with identity encoding (plain text on the wire)")
+    ap.add_argument("--identity-phase", type=int, default=1,
+                    help="also time K identity-encoded scrapes after the headline phase (p50_scrape_identity_us)")
     ap.add_argument("--proto", action="store_true",
                     help="negotiate the protobuf exposition (Accept: delimited MetricFamily), like Prometheus "
                          "with native histograms")
@@ -191,7 +200,7 @@ def main() -> int:
 
     from kubernetes_gpu_exporter_amd._native import load
     from kubernetes_gpu_exporter_amd.k8s.filesource import write_pod_map
-    from kubernetes_gpu_exporter_amd.utils import promtext
+    from kubernetes_gpu_exporter_amd.utils import promproto, promtext
     from kubernetes_gpu_exporter_amd.utils.fakehost import kubepods_cgroup
     from kubernetes_gpu_exporter_amd.utils.procstat import cpu_seconds_precise
     n = load()
@@ -258,7 +267,6 @@ def main() -> int:
             # namespace — the same number unless the box runs us in a PID namespace
             cgroups[p] = cgroups[op] = kubepods_cgroup(uid, cid, qos="guaranteed")
         write_pod_map(pod_map, pods, cgroups)
-        from kubernetes_gpu_exporter_amd.utils import promproto
         client = n.ScrapeClient("127.0.0.1", port, "/metrics", args.gzip, 5000,
                                 promproto.ACCEPT if args.proto else "")
     else:
@@ -279,11 +287,31 @@ def main() -> int:
         if rest > 0:
             time.sleep(rest)
 
-    def phase(proc, cl):
+    def xgmi_totals(cl) -> tuple[float, dict]:
+        """(time, {gpu: [read_bytes, write_bytes]}) summed over links, from the exporter's
+        hardware-accumulator counters in the body of the scrape `cl` just did."""
+        body = cl.last_body()
+        if args.gzip:
+            body = __import__("gzip").decompress(body)
+        fams = promtext.parse(body.decode()) if body[:1] == b"#" else \
+            promproto.to_promtext(promproto.parse_delimited(body))
+        tot: dict = {}
+        for k, fam_name in enumerate(("amd_gpu_xgmi_read_bytes_total", "amd_gpu_xgmi_write_bytes_total")):
+            for _, lab, v in promtext.samples(fams, fam_name):
+                tot.setdefault(lab.get("gpu"), [0.0, 0.0])[k] += v
+        return time.perf_counter(), tot
+
+    xgmi_window: dict = {}
+
+    def phase(proc, cl, native_exporter: bool = False):
         """W untimed + K timed steps (barrier + synchronize on both sides); returns the
         latencies, exporter CPU% over the timed window and max-over-ranks ms/step."""
         for _ in range(args.warmup):
             step(cl, None)
+        x0 = None
+        if native_exporter and rank == 0 and use_gpu:
+            cl.scrape()  # xGMI accumulators at the start of the window (untimed)
+            x0 = xgmi_totals(cl)
         if dist is not None:
             dist.barrier()
         sync()
@@ -297,6 +325,21 @@ def main() -> int:
         sync()
         elapsed = time.perf_counter() - t0
         cpu_pct = 100.0 * (cpu_seconds_precise(proc.pid) - cpu0) / elapsed if rank == 0 else 0.0
+        if x0 is not None:
+            # xGMI bytes the hardware counted over the window vs what the DP all-reduce must
+            # move: 2(N-1)/N x buffer per GPU per step for any bandwidth-optimal algorithm
+            # (ring or direct); counters lag by <= one sample period (100 ms at 10 Hz).
+            t1, tot1 = xgmi_totals(cl)
+            dt = t1 - x0[0]
+            per_gpu = {g: {"read_Bps": round((v[0] - x0[1].get(g, [0, 0])[0]) / dt),
+                           "write_Bps": round((v[1] - x0[1].get(g, [0, 0])[1]) / dt)} for g, v in tot1.items()}
+            buf = grad.numel() * grad.element_size()
+            expect = 2.0 * (world - 1) / world * buf * args.steps / elapsed if dist is not None else 0.0
+            xgmi_window.update({"window_s": round(dt, 3), "per_gpu": per_gpu,
+                                "expected_allreduce_Bps_per_gpu": round(expect)})
+            if expect > 0 and per_gpu:
+                xgmi_window["measured_over_expected_write"] = round(
+                    statistics.mean(v["write_Bps"] for v in per_gpu.values()) / expect, 3)
         msps = elapsed / max(1, args.steps) * 1e3
         if dist is not None:
             t = torch.tensor([msps], device=dev if use_gpu else "cpu", dtype=torch.float64)
@@ -311,7 +354,16 @@ def main() -> int:
         except subprocess.TimeoutExpired:
             proc.kill()
 
-    lat, cpu_pct, ms_per_step = phase(exporter, client if rank == 0 else None)
+    lat, cpu_pct, ms_per_step = phase(exporter, client if rank == 0 else None, native_exporter=True)
+    lat_id = cpu_id = None
+    if args.identity_phase and args.gzip:
+        # Same workload, same exporter, plain-text (identity) responses: the bytes on the
+        # wire grow with the GPU count here, gzip'd ones barely do.
+        id_client = n.ScrapeClient("127.0.0.1", port, "/metrics", False, 5000,
+                                   promproto.ACCEPT if args.proto else "") if rank == 0 else None
+        lat_id, cpu_id, _ = phase(exporter, id_client)
+        if rank == 0:
+            id_bytes = id_client.last_bytes
 
     result = None
     if rank == 0:
@@ -398,6 +450,11 @@ def main() -> int:
             "p99_scrape_us": round(pct(lat, 0.99), 2) if lat else None,
             "max_scrape_us": round(max(lat), 2) if lat else None,
             "exporter_cpu_percent": round(cpu_pct, 3),
+            "scrape_encoding": "gzip (Prometheus default Accept-Encoding)" if args.gzip else "identity",
+            "p50_scrape_identity_us": round(statistics.median(lat_id), 2) if lat_id else None,
+            "p99_scrape_identity_us": round(pct(lat_id, 0.99), 2) if lat_id else None,
+            "exporter_cpu_percent_identity_phase": round(cpu_id, 3) if cpu_id is not None else None,
+            "scrape_bytes_identity": id_bytes if lat_id else None,
             "server_scrape_mean_us": server_mean_us,
             "scrapes": len(lat),
             "scrape_errors": client.errors,
@@ -409,6 +466,7 @@ def main() -> int:
             "workload_gemm_tflops_per_gpu": round(tflops, 1) if tflops else None,
             "rccl_per_pod": rccl,
             "xgmi_bytes_per_second": xgmi,
+            "xgmi_timed_window": xgmi_window,
             "families_gpu0": {k: v for k, v in sorted(fam_gpu0.items()) if v},
             "sample_stage_mean_us": stage_us,
             "sample_stage_p50_le_us": stage_p50_us,
