@@ -93,15 +93,19 @@ def hip_order_bdfs(root: str = "") -> list:
         if not root and minor is not None and not os.access(f"/dev/dri/renderD{minor}", os.R_OK | os.W_OK):
             continue  # ROCr skips GPUs whose render node this process cannot open
         loc, dom = int(kv.get("location_id", 0)), int(kv.get("domain", 0))
-        nodes.append((int(name), f"{dom:04x}:{(loc >> 8) & 0xFF:02x}:{(loc >> 3) & 0x1F:02x}.{loc & 7:x}"))
-    bdfs = [b for _, b in sorted(nodes)]
+        nodes.append((int(name), f"{dom:04x}:{(loc >> 8) & 0xFF:02x}:{(loc >> 3) & 0x1F:02x}.{loc & 7:x}",
+                      f"GPU-{int(kv.get('unique_id', 0)):016x}"))
+    visible = [(b, u) for _, b, u in sorted(nodes)]
     for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
         val = os.environ.get(var, "").strip()
         if not val:
             continue
-        try:
-            idx = [int(x) for x in val.split(",") if x.strip() != ""]
-        except ValueError:
-            continue  # UUID lists: leave the order as is
-        bdfs = [bdfs[i] for i in idx if 0 <= i < len(bdfs)]
-    return bdfs
+        picked = []
+        for x in (x.strip() for x in val.split(",")):
+            if x.isdigit():
+                if int(x) < len(visible):
+                    picked.append(visible[int(x)])
+            elif x.lower().startswith("gpu-"):  # ROCr UUIDs: "GPU-" + 16 hex digits of unique_id
+                picked += [v for v in visible if v[1].lower() == x.lower()]
+        visible = picked
+    return [b for b, _ in visible]

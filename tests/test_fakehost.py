@@ -321,6 +321,12 @@ def test_hip_order_bdfs_and_bdf_device_filter(native, tmp_path, monkeypatch):
     assert sorted(order) == sorted(d["bdf"] for d in native.read_backend("sysfs", str(tmp_path)))
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "2,0")
     assert hip_order_bdfs(str(tmp_path)) == [order[2], order[0]]
+    # ROCr also takes UUIDs ("GPU-" + unique_id); visibility lists compose (HIP indexes ROCr's)
+    by_bdf = {f"0000:{g.location_id >> 8:02x}:00.0": g for g in h.gpus}
+    uuid = lambda b: f"GPU-{by_bdf[b].unique_id:016x}"  # noqa: E731
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", f"{uuid(order[3])},{uuid(order[1]).upper()},{uuid(order[0])}")
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "2,0")
+    assert hip_order_bdfs(str(tmp_path)) == [order[0], order[3]]
     e = _engine(native, tmp_path, device_filter_bdf=[order[2].upper()])
     e.tick(1 * S)
     up = promtext.samples(promtext.parse(e.snapshot_text()), "amd_gpu_up")
