@@ -251,3 +251,26 @@ def test_full_profile_adds_reliability_families(mock_engine):
         "correctable", "nonfatal", "fatal"}
     assert {s[1]["direction"] for s in fams["amd_gpu_pcie_nak_total"].samples} == {"sent", "received"}
     assert fams["amd_gpu_ecc_errors_total"].type == "counter"
+
+
+def test_chrome_trace_of_sampler_stages(mock_engine, tmp_path):
+    """--trace writes a Chrome-trace (catapult JSON array) of every sampler stage, one
+    complete ("X") event per stage per tick, bounded by trace_max_events."""
+    import json
+    path = tmp_path / "trace.json"
+    e = mock_engine(2, http=False, trace_path=str(path), trace_max_events=1000)
+    ticks(e, 5)
+    e.stop()
+    events = [ev for ev in json.loads(path.read_text()) if ev]
+    stages = collections.Counter(ev["name"] for ev in events)
+    assert {"devices", "processes", "series", "render", "publish"} <= set(stages), stages
+    assert len(set(stages.values())) == 1 and stages["render"] == 5  # every stage, every tick
+    assert all(ev["ph"] == "X" and ev["dur"] >= 0 for ev in events)
+    ts = [ev["ts"] for ev in events]
+    assert ts == sorted(ts)
+    # bounded: a long-running exporter cannot fill the disk
+    path2 = tmp_path / "small.json"
+    e2 = mock_engine(1, http=False, trace_path=str(path2), trace_max_events=7)
+    ticks(e2, 10)
+    e2.stop()
+    assert len([ev for ev in json.loads(path2.read_text()) if ev]) == 7
