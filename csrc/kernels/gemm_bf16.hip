@@ -134,15 +134,203 @@ __global__ void fill_bf16_kernel(uint16_t* __restrict__ p, size_t n, uint32_t se
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// 256x256 tile, 8 waves (2 along M x 4 along N), BK=64, loads that stay in flight across
+// barriers.  Each wave owns a 128x64 output block = 2x2 quadrants of 64x32; one K-tile is
+// four phases, one quadrant per phase (16 MFMA 16x16x32 each), ordered so that each phase
+// reads ONE new row group of the LDS tile and the group it finished with is free for the
+// K-tile two ahead:
+//   phase 1: ds_read A rows M0 (wave-row's first 64) + B rows N0 (wave-col's first 32) -> Q00
+//   phase 2: ds_read B rows N1                      -> Q01;  stage t+2: A-M0 + B-N0 groups
+//   phase 3: ds_read A rows M1 (over the M0 frags)  -> Q11;  stage t+2: B-N1 group
+//   phase 4: (registers only)                       -> Q10;  stage t+2: A-M1 group
+// A "group" is 128 tile rows x 64 K (16 KiB) = 2 global_load_lds x 16 B per thread.  Every
+// phase ends in one raw s_barrier after the wave's own ds_reads retired (lgkmcnt(0)), so a
+// group staged in phase p+1 never overwrites rows still being read (WAR).  K-tile t+1 was
+// staged during phases 2-4 of K-tile t-1; the counted wait before phase 4's barrier,
+// vmcnt(8), retires it while t+2's 8 loads stay in flight (RAW: read one barrier after the
+// wait).  No __syncthreads() in the loop (its fence would drain vmcnt to 0) and all LDS is
+// one __shared__ array (cdna_hip_programming.md §5 "Pipelining across barriers", 4(a)).
+// Epilogue: the 256x256 bf16 C tile goes through the (then idle) 128 KiB of LDS so every
+// global store is a full 16-B chunk of a 512-B row.
+// Requirements (host-checked): M%256 == N%256 == 0, K%64 == 0, K >= 128.
+// ---------------------------------------------------------------------------------------
+constexpr int kBM2 = 256, kBN2 = 256, kThreads2 = 512;
+constexpr int kTile2 = 256 * kBK;  // one operand K-tile (bf16 elements), 32 KiB
+
+// Stages one 128-row group of a 256x64 operand tile: row-block rb (8 rows) of the group
+// starts at tile row  run * run_stride + off + (rb % blocks_per_run) * 8.
+template <int kBlocksPerRun, int kRunStride>
+__device__ __forceinline__ void stage_group(const uint16_t* __restrict__ g, int ld, int row0, int k0, int off,
+                                            uint16_t* lds_tile, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int rb = wave * 2 + i;  // 0..15
+    const int trow = (rb / kBlocksPerRun) * kRunStride + off + (rb % kBlocksPerRun) * 8;
+    const int row = trow + (lane >> 3);
+    const int c = swz(row, lane & 7);
+    const uint16_t* src = g + size_t(row0 + row) * size_t(ld) + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((gptr_t)src, (lds_ptr_t)(lds_tile + trow * kBK), 16, 0, 0);
+  }
+}
+
+// A groups: M0 = rows {wr*128 + 0..63}, M1 = {wr*128 + 64..127}  (2 runs of 8 blocks)
+// B groups: N0 = rows {wc*64 + 0..31},  N1 = {wc*64 + 32..63}    (4 runs of 4 blocks)
+#define GEMM2_STAGE_A(half, t)                                                                      \
+  stage_group<8, 128>(A, K, row_a, (t) * kBK, (half) * 64, smem + ((t) & 1) * 2 * kTile2, wave, lane)
+#define GEMM2_STAGE_B(half, t)                                                                      \
+  stage_group<4, 64>(B, K, row_b, (t) * kBK, (half) * 32, smem + ((t) & 1) * 2 * kTile2 + kTile2, wave, lane)
+
+__device__ __forceinline__ void read_frags(const uint16_t* tile, int row_base, int lane, bf16x8 (&f)[4][2],
+                                           int n) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i >= n) break;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int row = row_base + i * 16 + (lane & 15);
+      const int chunk = kk * 4 + (lane >> 4);
+      f[i][kk] = *reinterpret_cast<const bf16x8*>(tile + row * kBK + swz(row, chunk) * 8);
+    }
+  }
+}
+
+__device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[4][2], const bf16x8 (&af)[4][2],
+                                              const bf16x8 (&bf)[4][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi][kk], bf[ni][kk], acc[mi][ni], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+__device__ __forceinline__ void phase_end() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");  // keep the next phase's LDS accesses below the barrier
+}
+
+__global__ void __launch_bounds__(kThreads2, 1)
+gemm_bf16_tn_256_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
+                        int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 2 * kTile2];  // 128 KiB: [buf][A|B][256][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const int nbn = N / kBN2;
+  const int nwg = (M / kBM2) * nbn;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int row_a = (wgid / nbn) * kBM2, row_b = (wgid % nbn) * kBN2;
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / kBK;  // >= 2
+  // prologue: K-tiles 0 and 1 in the loop's group order, then retire tile 0
+  GEMM2_STAGE_A(0, 0); GEMM2_STAGE_B(0, 0); GEMM2_STAGE_B(1, 0); GEMM2_STAGE_A(1, 0);
+  GEMM2_STAGE_A(0, 1); GEMM2_STAGE_B(0, 1); GEMM2_STAGE_B(1, 1); GEMM2_STAGE_A(1, 1);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  phase_end();
+
+  bf16x8 af[4][2], b0[4][2], b1[4][2];
+  const int a_row = wr * 128, b_row = wc * 64;
+  for (int t = 0; t < nk; ++t) {
+    const uint16_t* As = smem + (t & 1) * 2 * kTile2;
+    const uint16_t* Bs = As + kTile2;
+    const bool more = t + 2 < nk;
+    // phase 1
+    read_frags(As, a_row, lane, af, 4);
+    read_frags(Bs, b_row, lane, b0, 2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    mfma_quadrant(acc[0][0], af, b0);
+    phase_end();
+    // phase 2
+    read_frags(Bs, b_row + 32, lane, b1, 2);
+    if (more) { GEMM2_STAGE_A(0, t + 2); GEMM2_STAGE_B(0, t + 2); }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    mfma_quadrant(acc[0][1], af, b1);
+    phase_end();
+    // phase 3
+    read_frags(As, a_row + 64, lane, af, 4);
+    if (more) GEMM2_STAGE_B(1, t + 2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    mfma_quadrant(acc[1][1], af, b1);
+    phase_end();
+    // phase 4
+    if (more) GEMM2_STAGE_A(1, t + 2);
+    mfma_quadrant(acc[1][0], af, b0);
+    if (more)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // K-tile t+1 landed (this thread's part)
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    phase_end();
+  }
+
+  // Epilogue through LDS: every wave is past the last barrier, so no LDS reads remain.
+  // C/D map of 16x16x32: col = lane&15, row = (lane>>4)*4 + j.
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int row = wr * 128 + qm * 64 + mi * 16 + (lane >> 4) * 4 + j;
+            const int col = wc * 64 + qn * 32 + ni * 16 + (lane & 15);
+            __bf16 v = (__bf16)acc[qm][qn][mi][ni][j];
+            smem[row * kBN2 + col] = *reinterpret_cast<uint16_t*>(&v);
+          }
+  __syncthreads();
+#pragma unroll 4
+  for (int p = 0; p < (kBM2 * kBN2 / 8) / kThreads2; ++p) {  // 16 passes of 512 x 16 B
+    const int idx = p * kThreads2 + threadIdx.x;
+    const int row = idx >> 5, chunk = idx & 31;
+    const uint4 v = *reinterpret_cast<const uint4*>(smem + row * kBN2 + chunk * 8);
+    *reinterpret_cast<uint4*>(C + size_t(row_a + row) * size_t(N) + row_b + chunk * 8) = v;
+  }
+}
+#undef GEMM2_STAGE_A
+#undef GEMM2_STAGE_B
+
 bool gemm_shape_ok(int M, int N, int K) {
   return M > 0 && N > 0 && K > 0 && M % kBM == 0 && N % kBN == 0 && K % kBK == 0;
 }
 
-hipError_t launch_gemm_bf16_tn(const void* A, const void* B, void* C, int M, int N, int K, hipStream_t stream) {
+bool gemm256_shape_ok(int M, int N, int K) {
+  return M > 0 && N > 0 && K >= 2 * kBK && M % kBM2 == 0 && N % kBN2 == 0 && K % kBK == 0;
+}
+
+// variant: 0 = auto (256x256 kernel when the shape allows it), 1 = 128x128, 2 = 256x256.
+hipError_t launch_gemm_bf16_tn(const void* A, const void* B, void* C, int M, int N, int K, hipStream_t stream,
+                               int variant) {
   if (!gemm_shape_ok(M, N, K)) return hipErrorInvalidValue;
-  dim3 grid((M / kBM) * (N / kBN)), block(kThreads);
-  hipLaunchKernelGGL(gemm_bf16_tn_kernel, grid, block, 0, stream, static_cast<const uint16_t*>(A),
-                     static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M, N, K);
+  const bool big = variant == 2 || (variant == 0 && gemm256_shape_ok(M, N, K));
+  if (big) {
+    if (!gemm256_shape_ok(M, N, K)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gemm_bf16_tn_256_kernel, dim3((M / kBM2) * (N / kBN2)), dim3(kThreads2), 0, stream,
+                       static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M,
+                       N, K);
+  } else {
+    hipLaunchKernelGGL(gemm_bf16_tn_kernel, dim3((M / kBM) * (N / kBN)), dim3(kThreads), 0, stream,
+                       static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M,
+                       N, K);
+  }
   return hipGetLastError();
 }
 

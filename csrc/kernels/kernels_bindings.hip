@@ -11,7 +11,9 @@ namespace py = pybind11;
 
 namespace gpuexp {
 bool gemm_shape_ok(int M, int N, int K);
-hipError_t launch_gemm_bf16_tn(const void* A, const void* B, void* C, int M, int N, int K, hipStream_t stream);
+bool gemm256_shape_ok(int M, int N, int K);
+hipError_t launch_gemm_bf16_tn(const void* A, const void* B, void* C, int M, int N, int K, hipStream_t stream,
+                               int variant);
 hipError_t launch_fill_bf16(void* p, size_t n, uint32_t seed, hipStream_t stream);
 }  // namespace gpuexp
 
@@ -33,23 +35,31 @@ PYBIND11_MODULE(_gpuexp_kernels, m) {
     return n;
   });
   m.def("gemm_shape_ok", &gpuexp::gemm_shape_ok);
-  m.def("gemm_bf16", [](uintptr_t a, uintptr_t b, uintptr_t c, int M, int N, int K, uintptr_t stream) {
+  m.def("gemm256_shape_ok", &gpuexp::gemm256_shape_ok);
+  m.def("gemm_bf16", [](uintptr_t a, uintptr_t b, uintptr_t c, int M, int N, int K, uintptr_t stream, int variant) {
     if (!gpuexp::gemm_shape_ok(M, N, K))
       throw std::invalid_argument("gemm_bf16 needs M%128==0, N%128==0, K%64==0");
+    if (variant == 2 && !gpuexp::gemm256_shape_ok(M, N, K))
+      throw std::invalid_argument("the 256x256 kernel needs M%256==0, N%256==0, K%64==0, K>=128");
+    if (variant < 0 || variant > 2) throw std::invalid_argument("variant is 0 (auto), 1 (128x128) or 2 (256x256)");
     if (!a || !b || !c) throw std::invalid_argument("null pointer");
     check(gpuexp::launch_gemm_bf16_tn(reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b),
-                                      reinterpret_cast<void*>(c), M, N, K, reinterpret_cast<hipStream_t>(stream)),
+                                      reinterpret_cast<void*>(c), M, N, K, reinterpret_cast<hipStream_t>(stream),
+                                      variant),
           "gemm_bf16 launch");
   }, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("stream") = 0,
-     "C[M,N] = A[M,K] @ B[N,K]^T; bf16 row-major, fp32 accumulate (MFMA 16x16x32)");
+     py::arg("variant") = 0,
+     "C[M,N] = A[M,K] @ B[N,K]^T; bf16 row-major, fp32 accumulate (MFMA 16x16x32). variant: 0 auto, "
+     "1 = 128x128 tile, 2 = 256x256 tile");
   m.def("fill_bf16", [](uintptr_t p, size_t n, uint32_t seed, uintptr_t stream) {
     check(gpuexp::launch_fill_bf16(reinterpret_cast<void*>(p), n, seed, reinterpret_cast<hipStream_t>(stream)),
           "fill_bf16 launch");
   }, py::arg("ptr"), py::arg("n"), py::arg("seed") = 1, py::arg("stream") = 0);
-  m.def("gemm_burn", [](int device, int M, int N, int K, double seconds, int iters_per_sync) {
+  m.def("gemm_burn", [](int device, int M, int N, int K, double seconds, int iters_per_sync, int variant) {
     // Torch-free synthetic GEMM pod: keeps one GPU busy for `seconds` and reports the
     // achieved bf16 TFLOP/s (random operands).
-    if (!gpuexp::gemm_shape_ok(M, N, K)) throw std::invalid_argument("bad GEMM shape");
+    if (!gpuexp::gemm_shape_ok(M, N, K) || (variant == 2 && !gpuexp::gemm256_shape_ok(M, N, K)))
+      throw std::invalid_argument("bad GEMM shape");
     if (seconds <= 0 || seconds > 3600) throw std::invalid_argument("seconds out of range");
     double tflops = 0;
     long iters = 0;
@@ -69,7 +79,7 @@ PYBIND11_MODULE(_gpuexp_kernels, m) {
       auto t0 = std::chrono::steady_clock::now();
       int per = iters_per_sync > 0 ? iters_per_sync : 8;
       for (;;) {
-        for (int i = 0; i < per; ++i) (void)gpuexp::launch_gemm_bf16_tn(a, b, c, M, N, K, s);
+        for (int i = 0; i < per; ++i) check(gpuexp::launch_gemm_bf16_tn(a, b, c, M, N, K, s, variant), "gemm");
         check(hipStreamSynchronize(s), "gemm");
         iters += per;
         elapsed = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -87,5 +97,5 @@ PYBIND11_MODULE(_gpuexp_kernels, m) {
     d["seconds"] = elapsed;
     return d;
   }, py::arg("device"), py::arg("M") = 4096, py::arg("N") = 4096, py::arg("K") = 4096, py::arg("seconds") = 1.0,
-     py::arg("iters_per_sync") = 8);
+     py::arg("iters_per_sync") = 8, py::arg("variant") = 0);
 }

@@ -24,9 +24,11 @@ def kernels():
     return _mod
 
 
-def gemm_bf16(a, b, out=None, stream=None):
+def gemm_bf16(a, b, out=None, stream=None, variant: int = 0):
     """out[M,N] = a[M,K] @ b[N,K]^T for contiguous bf16 torch tensors on one GPU.
-    Shapes must satisfy M%128 == N%128 == K%64 == 0 (checked by the native op)."""
+    Shapes must satisfy M%128 == N%128 == K%64 == 0 (checked by the native op).
+    variant 0 picks the 256x256-tile kernel when M%256 == N%256 == 0 and K >= 128, else
+    the 128x128 one; 1 / 2 force the 128x128 / 256x256 kernel."""
     import torch
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
         raise TypeError("gemm_bf16 expects bf16 tensors")
@@ -43,10 +45,11 @@ def gemm_bf16(a, b, out=None, stream=None):
     elif out.shape != (M, N) or out.dtype != torch.bfloat16 or not out.is_contiguous():
         raise ValueError("bad output tensor")
     s = stream if stream is not None else torch.cuda.current_stream(a.device).cuda_stream
-    kernels().gemm_bf16(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, s)
+    kernels().gemm_bf16(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, s, variant)
     return out
 
 
-def gemm_burn(device: int = 0, size: int = 8192, seconds: float = 1.0, iters_per_sync: int = 4) -> dict:
+def gemm_burn(device: int = 0, size: int = 8192, seconds: float = 1.0, iters_per_sync: int = 4,
+              variant: int = 0) -> dict:
     """Torch-free GPU load: keeps `device` busy with size^3 GEMMs for `seconds`."""
-    return kernels().gemm_burn(device, size, size, size, seconds, iters_per_sync)
+    return kernels().gemm_burn(device, size, size, size, seconds, iters_per_sync, variant)
