@@ -1,5 +1,9 @@
 // Synthetic "HIP-GEMM pod" workload: C[M,N] (bf16) = A[M,K] . B[N,K]^T (bf16 in, fp32 acc).
+// Two kernels: the 256x256 one below the 128x128 one is the default whenever the shape
+// allows (M,N multiples of 256).  MI355X, random operands, 8192^3: 256x256 1273 TFLOP/s,
+// 128x128 934, torch.matmul (hipBLASLt) 1434; 4096^3: 1290 vs 994 (profiles/r01/gemm.txt).
 //
+// 128x128 kernel:
 // This is the load generator behind BASELINE configs 3-5 ("synthetic HIP-workload pods")
 // — the exporter itself issues no GEMMs.  Written for CDNA4 directly:
 //   * v_mfma_f32_16x16x32_bf16 (gfx950), 4 waves of 64 lanes, 128x128 block tile, BK=64;
@@ -208,17 +212,39 @@ __device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[4][2], const bf16x8 (
   __builtin_amdgcn_s_setprio(0);
 }
 
+// Ends a phase: this wave's ds_reads have landed (so the rows they read may be restaged
+// once every wave passes the barrier), then the barrier itself.
 __device__ __forceinline__ void phase_end() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");  // keep the next phase's LDS accesses below the barrier
 }
 
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Wave-row stagger: the two wave rows (waves 0-3 and 4-7; every SIMD holds one of each)
+// run one phase apart — wave row 1 passes one extra barrier before the loop and row 0 one
+// after it — so on each SIMD one wave issues its phase's ds_reads while the other keeps
+// the MFMA pipe busy.  Because a barrier interval now holds phase p of row 0 and p-1 of
+// row 1, a group read in phase p is restaged in phase p+2 at the earliest (row 1 may still
+// be reading it during row 0's p+1):
+//   phase 1: read A-M0 + B-N0 -> Q00;  stage A-M1 of K-tile t+1
+//   phase 2: read B-N1        -> Q01
+//   phase 3: read A-M1        -> Q11;  stage A-M0 + B-N0 of t+2
+//   phase 4: (registers)      -> Q10;  stage B-N1 of t+2
+// Counted waits, placed for the EARLIER row (row 1 reads one barrier after row 0 arrives,
+// so every wave waits before the barrier that precedes row 0's read): end of phase 3
+// retires t+1's A-M0/B-N0/B-N1 (then in flight: t+1's A-M1, t+2's first 4), end of phase 1
+// retires t's A-M1 (then in flight: t+1's first 6 + A-M1).
 __global__ void __launch_bounds__(kThreads2, 1)
 gemm_bf16_tn_256_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
                         int M, int N, int K) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 2 * kTile2];  // 128 KiB: [buf][A|B][256][64]
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR: branches on it are scalar
   const int wr = wave >> 2, wc = wave & 3;
 
   const int nbn = N / kBN2;
@@ -239,47 +265,46 @@ gemm_bf16_tn_256_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
         for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / kBK;  // >= 2
-  // prologue: K-tiles 0 and 1 in the loop's group order, then retire tile 0
   GEMM2_STAGE_A(0, 0); GEMM2_STAGE_B(0, 0); GEMM2_STAGE_B(1, 0); GEMM2_STAGE_A(1, 0);
-  GEMM2_STAGE_A(0, 1); GEMM2_STAGE_B(0, 1); GEMM2_STAGE_B(1, 1); GEMM2_STAGE_A(1, 1);
-  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  phase_end();
+  GEMM2_STAGE_A(0, 1); GEMM2_STAGE_B(0, 1); GEMM2_STAGE_B(1, 1);
+  wait_vm<6>();  // K-tile 0 landed; tile 1's first three groups in flight
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger: row 1 one phase behind
+  asm volatile("" ::: "memory");
 
   bf16x8 af[4][2], b0[4][2], b1[4][2];
   const int a_row = wr * 128, b_row = wc * 64;
   for (int t = 0; t < nk; ++t) {
     const uint16_t* As = smem + (t & 1) * 2 * kTile2;
     const uint16_t* Bs = As + kTile2;
-    const bool more = t + 2 < nk;
+    const bool has1 = t + 1 < nk, has2 = t + 2 < nk;
     // phase 1
     read_frags(As, a_row, lane, af, 4);
     read_frags(Bs, b_row, lane, b0, 2);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (has1) GEMM2_STAGE_A(1, t + 1);
     mfma_quadrant(acc[0][0], af, b0);
+    if (has1) wait_vm<8>(); else wait_vm<0>();  // this tile's A-M1 landed
     phase_end();
     // phase 2
     read_frags(Bs, b_row + 32, lane, b1, 2);
-    if (more) { GEMM2_STAGE_A(0, t + 2); GEMM2_STAGE_B(0, t + 2); }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     mfma_quadrant(acc[0][1], af, b1);
     phase_end();
     // phase 3
     read_frags(As, a_row + 64, lane, af, 4);
-    if (more) GEMM2_STAGE_B(1, t + 2);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (has2) { GEMM2_STAGE_A(0, t + 2); GEMM2_STAGE_B(0, t + 2); }
     mfma_quadrant(acc[1][1], af, b1);
+    if (has2) wait_vm<6>(); else if (has1) wait_vm<2>(); else wait_vm<0>();  // t+1's first 3 groups landed
     phase_end();
     // phase 4
-    if (more) GEMM2_STAGE_A(1, t + 2);
+    if (has2) GEMM2_STAGE_B(1, t + 2);
     mfma_quadrant(acc[1][0], af, b0);
-    if (more)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // K-tile t+1 landed (this thread's part)
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     phase_end();
   }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // close the stagger: row 1's last phase is done
+  asm volatile("" ::: "memory");
 
-  // Epilogue through LDS: every wave is past the last barrier, so no LDS reads remain.
+  // Epilogue through LDS: every wave's reads retired before its last barrier and the last
+  // K-tiles waited vmcnt(0), so the 128 KiB are free.
   // C/D map of 16x16x32: col = lane&15, row = (lane>>4)*4 + j.
 #pragma unroll
   for (int qm = 0; qm < 2; ++qm)
