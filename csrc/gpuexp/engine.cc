@@ -193,6 +193,9 @@ void Engine::define_families() {
   f_proc_sdma_ = add("amd_gpu_process_sdma_seconds_total", "SDMA engine time used by a process", C, P);
   f_proc_evicted_ = add("amd_gpu_process_evicted_seconds_total",
                         "Time the process's GPU queues were evicted (memory pressure / preemption; KFD stats)", C, P);
+  f_proc_gfx_ = add("amd_gpu_process_gfx_activity_percent",
+                    "GPU gfx activity attributed to a process: the GPU's activity split by the processes' "
+                    "occupied CUs (estimate on shared GPUs; exact for a sole process)", G, P);
   if (cfg_.legacy_families) {
     // Byte-compatible with the reference (/root/reference/main.go:22-35): names, HELP,
     // label names and order {pid, pod}.  `pid` is the host PID (the reference's intended
@@ -209,6 +212,9 @@ void Engine::define_families() {
   f_pod_xwr_ = add("amd_pod_xgmi_write_bytes_per_second", "xGMI transmit rate of the pod's GPUs", G, PO);
   f_pod_power_ = add("amd_pod_gpu_power_watts", "Socket power of the pod's GPUs", G, PO);
   f_pod_gfx_ = add("amd_pod_gpu_gfx_activity_percent", "Mean gfx activity of the pod's GPUs", G, PO);
+  f_pod_gfx_share_ = add("amd_pod_gfx_activity_share_percent",
+                         "GPU gfx activity of the pod's processes summed over GPUs, in percent of one GPU "
+                         "(per-process CU-occupancy split; covers shared GPUs)", G, PO);
   f_rccl_calls_ = add("amd_rccl_collective_calls_total", "RCCL collective/p2p calls by op (rocprofiler-sdk tracer)",
                       C, {"namespace", "pod", "pid", "op"});
   f_rccl_bytes_ = add("amd_rccl_collective_bytes_total", "RCCL payload bytes by op (rocprofiler-sdk tracer)", C,
@@ -681,8 +687,9 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
     double vram = 0;
     std::set<int> pids;
     int gpus = 0;
-    double xrd = 0, xwr = 0, power = 0, gfx = 0;
+    double xrd = 0, xwr = 0, power = 0, gfx = 0, gfx_share = 0;
     int gfx_n = 0;
+    bool share_known = false;
   };
   std::map<std::pair<std::string, std::string>, PodAgg> pods;
 
@@ -692,18 +699,33 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
     DevState& st = dstate_[di];
     double cu_sum = 0;
     bool cu_any = false;
-    for (auto& p : per_dev[di]) {
-      const ProcAttr& a = attr[p.pid];
+    for (auto& p : per_dev[di])
       if (!std::isnan(p.cu_occupancy)) {
         cu_sum += p.cu_occupancy;
         cu_any = true;
       }
+    // The GPU's gfx activity split over its processes.  KFD compute contexts report no
+    // per-process engine time (fdinfo drm-engine-* stays empty, profiles/r01/kfd_read_costs.txt),
+    // so the split uses each process's share of the occupied CUs; a sole process gets all
+    // of it, and with no waves resident at the CU sample the split is even.
+    const double act = st.cur.ok ? st.cur.gfx_activity : std::nan("");
+    const size_t nproc = per_dev[di].size();
+    auto gfx_share = [&](const ProcSample& p) -> double {
+      if (std::isnan(act) || nproc == 0) return std::nan("");
+      if (nproc == 1) return act;
+      if (cu_any && cu_sum > 0) return std::isnan(p.cu_occupancy) ? std::nan("") : act * p.cu_occupancy / cu_sum;
+      return act / double(nproc);
+    };
+    for (auto& p : per_dev[di]) {
+      const ProcAttr& a = attr[p.pid];
+      const double share = gfx_share(p);
       if (!legacy_only) {
         std::vector<std::string> L = {std::to_string(d.index), std::to_string(p.pid), p.name, a.ns, a.pod, a.container};
         table_.put(f_proc_vram_, L, p.vram_bytes, gen);
         if (!std::isnan(p.cu_occupancy)) table_.put(f_proc_cu_, L, p.cu_occupancy, gen);
         if (!std::isnan(p.sdma_us)) table_.put(f_proc_sdma_, L, p.sdma_us * 1e-6, gen);
         if (!std::isnan(p.evicted_ms)) table_.put(f_proc_evicted_, L, p.evicted_ms * 1e-3, gen);
+        if (!std::isnan(share)) table_.put(f_proc_gfx_, L, share, gen);
       }
       if (!a.pod.empty()) {
         auto& la = legacy[p.pid];
@@ -712,6 +734,10 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
         auto& pa = pods[{a.ns, a.pod}];
         pa.vram += p.vram_bytes;
         pa.pids.insert(p.pid);
+        if (!std::isnan(share)) {
+          pa.gfx_share += share;
+          pa.share_known = true;
+        }
       }
     }
     if (st.cur.ok && !legacy_only) {
@@ -753,6 +779,7 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
     table_.put(f_pod_vram_, L, pa.vram, gen);
     table_.put(f_pod_procs_, L, double(pa.pids.size()), gen);
     table_.put(f_pod_gpus_, L, double(pa.gpus), gen);
+    if (pa.share_known) table_.put(f_pod_gfx_share_, L, pa.gfx_share, gen);
     if (pa.gpus > 0) {
       table_.put(f_pod_xrd_, L, pa.xrd, gen);
       table_.put(f_pod_xwr_, L, pa.xwr, gen);

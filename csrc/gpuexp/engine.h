@@ -239,9 +239,9 @@ class Engine {
       f_links_up_, f_pcie_bw_, f_pcie_replay_, f_pcie_speed_, f_pcie_width_, f_thr_, f_nprocs_,
       f_cu_occ_, f_ecc_, f_aer_, f_pcie_nak_, f_pcie_recov_, f_xgmi_width_, f_xgmi_speed_, f_mfma_, f_sq_busy_, f_gui_, f_waves_, f_lds_, f_lds_conf_, f_hbm_rd_,
       f_hbm_wr_, f_sen_sclk_, f_sen_lat_, f_sen_xcc_, f_sen_runs_, f_xcc_clk_, f_sen_xlat_, f_sen_mem_, f_sen_xmem_;
-  int f_proc_vram_, f_proc_cu_, f_proc_sdma_, f_proc_evicted_;
+  int f_proc_vram_, f_proc_cu_, f_proc_sdma_, f_proc_evicted_, f_proc_gfx_;
   int f_legacy_mem_ = -1, f_legacy_perc_ = -1;
-  int f_pod_vram_, f_pod_procs_, f_pod_gpus_, f_pod_xrd_, f_pod_xwr_, f_pod_power_, f_pod_gfx_;
+  int f_pod_vram_, f_pod_procs_, f_pod_gpus_, f_pod_xrd_, f_pod_xwr_, f_pod_power_, f_pod_gfx_, f_pod_gfx_share_;
   int f_rccl_calls_, f_rccl_bytes_;
   int f_self_build_, f_self_ticks_, f_self_stage_, f_self_scrape_, f_self_scrapes_,
       f_self_http_bytes_, f_self_render_bytes_, f_self_series_, f_self_dev_errors_,

@@ -274,3 +274,31 @@ def test_chrome_trace_of_sampler_stages(mock_engine, tmp_path):
     ticks(e2, 10)
     e2.stop()
     assert len([ev for ev in json.loads(path2.read_text()) if ev]) == 7
+
+
+def test_gfx_activity_split_over_processes_and_pods(mock_engine):
+    """Shared GPU: the GPU's gfx activity is split by the processes' occupied CUs (KFD has
+    no per-process engine time for compute); a sole process gets all of it; pods sum their
+    processes' shares over GPUs, so a pod on shared GPUs still gets a utilisation series."""
+    e = mock_engine(2, http=False)
+    uid2 = "22345678-1234-1234-1234-123456789abc"
+    cg2 = CG.replace(UID.replace("-", "_"), uid2.replace("-", "_"))
+    for d in (0, 1):
+        e.mock_set_value(d, "gfx_activity", 80.0)
+    # GPU 0 shared 3:1 by two pods; GPU 1 used only by pod 2's second process
+    e.mock_set_processes(0, [dict(pid=5, vram_bytes=1.0, cu_occupancy=96), dict(pid=6, vram_bytes=2.0, cu_occupancy=32)])
+    e.mock_set_processes(1, [dict(pid=7, vram_bytes=3.0, cu_occupancy=0)])
+    e.set_pid_cgroup(5, CG)
+    e.set_pid_cgroup(6, cg2)
+    e.set_pid_cgroup(7, cg2)
+    ticks(e, 2)
+    fams = parse(e)
+    share = {s[1]["pid"]: s[2] for s in promtext.samples(fams, "amd_gpu_process_gfx_activity_percent")}
+    assert share == {"5": 60.0, "6": 20.0, "7": 80.0}
+    pod = {s[1]["pod"]: s[2] for s in promtext.samples(fams, "amd_pod_gfx_activity_share_percent")}
+    assert pod == {UID: 60.0, uid2: 100.0}  # 20% of GPU 0 + 80% of GPU 1
+    # nothing resident at the CU sample: an even split, never a division by zero
+    e.mock_set_processes(0, [dict(pid=5, cu_occupancy=0), dict(pid=6, cu_occupancy=0)])
+    ticks(e, 1, t0=10 * S)
+    share = {s[1]["pid"]: s[2] for s in promtext.samples(parse(e), "amd_gpu_process_gfx_activity_percent")}
+    assert share["5"] == share["6"] == 40.0

@@ -107,8 +107,12 @@ def cluster(tmp_path):
 
 
 def _attributed(ex) -> bool:
+    """Both control-plane inputs have arrived: pod names (apiserver, for the PID -> pod
+    join) and device grants (kubelet PodResources, for GPU -> owner)."""
     fams = _scrape(ex.port)
-    return len({lab["pod"] for _, lab, _ in promtext.samples(fams, "pod_gpu_memory_usage")}) == GPUS + 1
+    procs_ok = len({lab["pod"] for _, lab, _ in promtext.samples(fams, "pod_gpu_memory_usage")}) == GPUS + 1
+    owners_ok = all(lab["pod"] for _, lab, _ in promtext.samples(fams, "amd_gpu_up"))
+    return procs_ok and owners_ok
 
 
 def test_each_node_reports_only_its_own_pods(cluster):
