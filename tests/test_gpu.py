@@ -261,6 +261,7 @@ def test_process_discovery_under_workload(native):
     try:
         seen_pids = set()
         max_gfx = 0.0
+        max_share = 0.0
         nsp = open("/proc/self/status").read().split("NSpid:")[1].split("\n")[0].split()
         print("NSpid of test process:", nsp, "child pid", child.pid)
         deadline = time.time() + 5
@@ -270,6 +271,10 @@ def test_process_discovery_under_workload(native):
             for _, lab, v in promtext.samples(fams, "amd_gpu_process_vram_bytes"):
                 if v > 256 * (1 << 20):
                     seen_pids.add(int(lab["pid"]))
+            big = {str(p) for p in seen_pids}
+            for _, lab, v in promtext.samples(fams, "amd_gpu_process_gfx_activity_percent"):
+                if lab["pid"] in big:
+                    max_share = max(max_share, v)
             try:
                 max_gfx = max(max_gfx, promtext.value(fams, "amd_gpu_gfx_activity_percent", gpu=0))
             except KeyError:
@@ -279,6 +284,9 @@ def test_process_discovery_under_workload(native):
         print("kfd proc dir:", sorted(os.listdir("/sys/class/kfd/kfd/proc")))
         assert seen_pids, "GEMM child not found in KFD process list"
         assert max_gfx > 50
+        # the GEMM holds (nearly) every occupied CU, so it gets (nearly) all the activity
+        print("max gfx share of the GEMM process:", max_share)
+        assert max_share > 40
         if len(nsp) == 1:
             assert child.pid in seen_pids or any(p != child.pid for p in seen_pids)
     finally:
