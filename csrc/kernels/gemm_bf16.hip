@@ -1,7 +1,7 @@
 // Synthetic "HIP-GEMM pod" workload: C[M,N] (bf16) = A[M,K] . B[N,K]^T (bf16 in, fp32 acc).
 // Two kernels: the 256x256 one below the 128x128 one is the default whenever the shape
-// allows (M,N multiples of 256).  MI355X, random operands, 8192^3: 256x256 1273 TFLOP/s,
-// 128x128 934, torch.matmul (hipBLASLt) 1434; 4096^3: 1290 vs 994 (profiles/r01/gemm.txt).
+// allows (M,N multiples of 256).  MI355X, random operands, 8192^3: 256x256 1355 TFLOP/s,
+// 128x128 928, torch.matmul (hipBLASLt) 1434; 4096^3: 1301 vs 987 (profiles/r01/gemm.txt).
 //
 // 128x128 kernel:
 // This is the load generator behind BASELINE configs 3-5 ("synthetic HIP-workload pods")
@@ -239,6 +239,7 @@ __device__ __forceinline__ void wait_vm() {
 // so every wave waits before the barrier that precedes row 0's read): end of phase 3
 // retires t+1's A-M0/B-N0/B-N1 (then in flight: t+1's A-M1, t+2's first 4), end of phase 1
 // retires t's A-M1 (then in flight: t+1's first 6 + A-M1).
+template <int kGroupM>
 __global__ void __launch_bounds__(kThreads2, 1)
 gemm_bf16_tn_256_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
                         int M, int N, int K) {
@@ -247,12 +248,20 @@ gemm_bf16_tn_256_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR: branches on it are scalar
   const int wr = wave >> 2, wc = wave & 3;
 
-  const int nbn = N / kBN2;
-  const int nwg = (M / kBM2) * nbn;
+  const int nbn = N / kBN2, nbm = M / kBM2;
+  const int nwg = nbm * nbn;
   const int orig = blockIdx.x;
   const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-  const int row_a = (wgid / nbn) * kBM2, row_b = (wgid % nbn) * kBN2;
+  // Grouped tile order inside each XCD's contiguous range: kGroupM row panels x all
+  // column panels, column-major within the group, so the ~32 blocks an XCD runs at once
+  // cover a kGroupM x (32/kGroupM) patch and share its A and B panels in that XCD's L2.
+  const int in_group = kGroupM * nbn;
+  const int first_m = (wgid / in_group) * kGroupM;
+  const int gsize = nbm - first_m < kGroupM ? nbm - first_m : kGroupM;
+  const int bm = first_m + (wgid % in_group) % gsize;
+  const int bn = (wgid % in_group) / gsize;
+  const int row_a = bm * kBM2, row_b = bn * kBN2;
 
   f32x4 acc[2][2][4][2];
 #pragma unroll
@@ -341,14 +350,18 @@ bool gemm256_shape_ok(int M, int N, int K) {
   return M > 0 && N > 0 && K >= 2 * kBK && M % kBM2 == 0 && N % kBN2 == 0 && K % kBK == 0;
 }
 
-// variant: 0 = auto (256x256 kernel when the shape allows it), 1 = 128x128, 2 = 256x256.
+// variant: 0 = auto (256x256 kernel when the shape allows it), 1 = 128x128, 2 = 256x256
+// with row-major tile order per XCD, 3 / 4 = 256x256 with 4 / 8 row panels per group.
 hipError_t launch_gemm_bf16_tn(const void* A, const void* B, void* C, int M, int N, int K, hipStream_t stream,
                                int variant) {
   if (!gemm_shape_ok(M, N, K)) return hipErrorInvalidValue;
-  const bool big = variant == 2 || (variant == 0 && gemm256_shape_ok(M, N, K));
+  const bool big = variant >= 2 || (variant == 0 && gemm256_shape_ok(M, N, K));
   if (big) {
     if (!gemm256_shape_ok(M, N, K)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(gemm_bf16_tn_256_kernel, dim3((M / kBM2) * (N / kBN2)), dim3(kThreads2), 0, stream,
+    // auto = 8-row groups: 1355 vs 1265 TFLOP/s (row-major) at 8192^3, 1301 vs 1289 at 4096^3
+    auto k = variant == 2 ? gemm_bf16_tn_256_kernel<1>
+             : variant == 3 ? gemm_bf16_tn_256_kernel<4> : gemm_bf16_tn_256_kernel<8>;
+    hipLaunchKernelGGL(k, dim3((M / kBM2) * (N / kBN2)), dim3(kThreads2), 0, stream,
                        static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M,
                        N, K);
   } else {

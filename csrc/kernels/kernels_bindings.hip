@@ -39,9 +39,10 @@ PYBIND11_MODULE(_gpuexp_kernels, m) {
   m.def("gemm_bf16", [](uintptr_t a, uintptr_t b, uintptr_t c, int M, int N, int K, uintptr_t stream, int variant) {
     if (!gpuexp::gemm_shape_ok(M, N, K))
       throw std::invalid_argument("gemm_bf16 needs M%128==0, N%128==0, K%64==0");
-    if (variant == 2 && !gpuexp::gemm256_shape_ok(M, N, K))
+    if (variant >= 2 && !gpuexp::gemm256_shape_ok(M, N, K))
       throw std::invalid_argument("the 256x256 kernel needs M%256==0, N%256==0, K%64==0, K>=128");
-    if (variant < 0 || variant > 2) throw std::invalid_argument("variant is 0 (auto), 1 (128x128) or 2 (256x256)");
+    if (variant < 0 || variant > 4)
+      throw std::invalid_argument("variant is 0 (auto), 1 (128x128), 2-4 (256x256; tile group 1/4/8 rows)");
     if (!a || !b || !c) throw std::invalid_argument("null pointer");
     check(gpuexp::launch_gemm_bf16_tn(reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b),
                                       reinterpret_cast<void*>(c), M, N, K, reinterpret_cast<hipStream_t>(stream),
@@ -58,7 +59,7 @@ PYBIND11_MODULE(_gpuexp_kernels, m) {
   m.def("gemm_burn", [](int device, int M, int N, int K, double seconds, int iters_per_sync, int variant) {
     // Torch-free synthetic GEMM pod: keeps one GPU busy for `seconds` and reports the
     // achieved bf16 TFLOP/s (random operands).
-    if (!gpuexp::gemm_shape_ok(M, N, K) || (variant == 2 && !gpuexp::gemm256_shape_ok(M, N, K)))
+    if (!gpuexp::gemm_shape_ok(M, N, K) || (variant >= 2 && !gpuexp::gemm256_shape_ok(M, N, K)))
       throw std::invalid_argument("bad GEMM shape");
     if (seconds <= 0 || seconds > 3600) throw std::invalid_argument("seconds out of range");
     double tflops = 0;
