@@ -422,6 +422,8 @@ def main() -> int:
             rccl.setdefault(lab.get("pod") or lab.get("pid"), {}).setdefault(lab["op"], {})["bytes"] = v
         for sname, lab, v in promtext.samples(fams, "amd_rccl_collective_calls_total"):
             rccl.setdefault(lab.get("pod") or lab.get("pid"), {}).setdefault(lab["op"], {})["calls"] = v
+        rccl_ranks = {lab.get("pod") or lab.get("pid"): [int(lab["rank"]), int(lab["nranks"])]
+                      for _, lab, _ in promtext.samples(fams, "amd_rccl_communicator_info")}
         xgmi = {}
         for fam_name, key in (("amd_gpu_xgmi_read_bytes_per_second", "read"),
                               ("amd_gpu_xgmi_write_bytes_per_second", "write")):
@@ -465,6 +467,7 @@ def main() -> int:
             "sentinel": sentinel,
             "workload_gemm_tflops_per_gpu": round(tflops, 1) if tflops else None,
             "rccl_per_pod": rccl,
+            "rccl_rank_per_pod": rccl_ranks,
             "xgmi_bytes_per_second": xgmi,
             "xgmi_timed_window": xgmi_window,
             "families_gpu0": {k: v for k, v in sorted(fam_gpu0.items()) if v},

@@ -219,6 +219,9 @@ void Engine::define_families() {
                       C, {"namespace", "pod", "pid", "op"});
   f_rccl_bytes_ = add("amd_rccl_collective_bytes_total", "RCCL payload bytes by op (rocprofiler-sdk tracer)", C,
                       {"namespace", "pod", "pid", "op"});
+  f_rccl_comm_ = add("amd_rccl_communicator_info",
+                     "Rank and size of the largest RCCL communicator of a process (value is always 1)", G,
+                     {"namespace", "pod", "pid", "rank", "nranks"});
 
   // --- exporter self-metrics (own prefix; the reference registry had none, main.go:40) ---
   f_self_build_ = add("gpuexp_build_info", "Exporter build and backend", G, {"version", "backend"});
@@ -809,6 +812,9 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
       std::vector<std::string> L = {a.ns, a.pod, std::to_string(t.pid), t.op};
       table_.put(f_rccl_calls_, L, double(t.calls), gen);
       table_.put(f_rccl_bytes_, L, double(t.bytes), gen);
+      if (t.nranks > 0 && t.rank >= 0)
+        table_.put(f_rccl_comm_, {a.ns, a.pod, std::to_string(t.pid), std::to_string(t.rank),
+                                  std::to_string(t.nranks)}, 1, gen);
     }
   }
 }

@@ -169,6 +169,8 @@ class ShmRcclSource : public RcclSource {
         t.op = rccl_op_name(op);
         t.calls = c;
         t.bytes = m.base->ops[op].bytes.load(std::memory_order_relaxed);
+        t.rank = reinterpret_cast<volatile int32_t*>(&m.base->rank)[0];
+        t.nranks = reinterpret_cast<volatile int32_t*>(&m.base->nranks)[0];
         out->push_back(t);
       }
     }

@@ -60,17 +60,24 @@ int comm_nranks(const void* comm) {
     auto it = g_nranks.find(comm);
     if (it != g_nranks.end()) return it->second;
   }
-  using count_fn = int (*)(const void*, int*);
-  static count_fn fn = reinterpret_cast<count_fn>(::dlsym(RTLD_DEFAULT, "ncclCommCount"));
-  int n = 1;
-  if (fn && !t_in_query) {
-    t_in_query = true;  // ncclCommCount is itself traced: do not recurse
-    if (fn(comm, &n) != 0 || n < 1) n = 1;
+  using query_fn = int (*)(const void*, int*);
+  static query_fn count = reinterpret_cast<query_fn>(::dlsym(RTLD_DEFAULT, "ncclCommCount"));
+  static query_fn user_rank = reinterpret_cast<query_fn>(::dlsym(RTLD_DEFAULT, "ncclCommUserRank"));
+  int n = 1, rank = -1;
+  if (!t_in_query) {
+    t_in_query = true;  // the queries are themselves traced: do not recurse
+    if (count && (count(comm, &n) != 0 || n < 1)) n = 1;
+    if (user_rank && user_rank(comm, &rank) != 0) rank = -1;
     t_in_query = false;
   }
   std::lock_guard<std::mutex> lk(g_comm_mu);
   g_nranks[comm] = n;
-  if (g_shm) g_shm->nranks = n;
+  // The file reports the process's largest communicator (its world / data-parallel
+  // group; sub-communicators of TP/PP/EP are smaller), so the rank label is stable.
+  if (g_shm && n >= g_shm->nranks) {
+    g_shm->nranks = n;
+    g_shm->rank = rank;
+  }
   return n;
 }
 

@@ -51,6 +51,8 @@ struct RcclTotals {
   std::string op;     // allreduce, allgather, reducescatter, alltoall, send, recv, broadcast, ...
   uint64_t calls = 0;
   uint64_t bytes = 0;
+  int rank = -1;      // communicator rank of the process (-1 unknown)
+  int nranks = 0;     // communicator size (0 unknown)
 };
 class RcclSource {
  public:

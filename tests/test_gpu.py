@@ -248,6 +248,7 @@ def test_rccl_tracer_counts_collectives():
     assert ops["allreduce"]["calls"] >= 20
     assert ops["allreduce"]["bytes"] >= 20 * (2 << 20)
     assert ops["allgather"]["calls"] >= 5
+    assert res["communicator"] == [{"rank": 0, "nranks": 1}], res["communicator"]  # ncclCommUserRank/Count
 
 
 def test_process_discovery_under_workload(native):

@@ -41,6 +41,8 @@ def test_rccl_counters_attributed_to_pod(mock_engine, tmp_path):
     assert promtext.value(fams, "amd_rccl_collective_bytes_total", namespace="train", op="allreduce",
                           pid=pid) == 10 * 64 << 20
     assert promtext.value(fams, "amd_rccl_collective_calls_total", op="send") == 3
+    # rank / size of the process's communicator (the file says rank 0 of 4)
+    assert promtext.value(fams, "amd_rccl_communicator_info", pod="dp-worker-0", rank=0, nranks=4) == 1
     # the tracer keeps counting; the exporter reads the live mapping
     struct.pack_into("<QQ", m, 64, 25, 25 * 64 << 20)
     e.tick(2_000_000_000)

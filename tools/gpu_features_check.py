@@ -113,16 +113,18 @@ def rccl() -> dict:
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
     files = [f for f in os.listdir(d) if f.startswith("gpuexp-rccl-")]
     ops = {}
+    comm = []
     names = ["allreduce", "allgather", "reducescatter", "alltoall", "alltoallv", "broadcast", "reduce", "send",
              "recv", "gather", "scatter"]
     for f in files:
         b = open(os.path.join(d, f), "rb").read()
         magic, ver, ns_pid, ino, rank, nranks = struct.unpack_from("<QIiQii", b, 0)
+        comm.append({"rank": rank, "nranks": nranks})
         for i, nm in enumerate(names):
             calls, nbytes = struct.unpack_from("<QQ", b, 64 + 16 * i)
             if calls:
                 ops[nm] = {"calls": calls, "bytes": nbytes}
-    return {"rc": r.returncode, "files": files, "ops": ops, "stdout": r.stdout[-500:], "stderr": r.stderr[-1500:]}
+    return {"rc": r.returncode, "files": files, "ops": ops, "communicator": comm, "stdout": r.stdout[-500:], "stderr": r.stderr[-1500:]}
 
 
 if __name__ == "__main__":
