@@ -13,8 +13,13 @@
 //   allreduce/reduce/broadcast: count * size       allgather: sendcount * size * nranks
 //   reducescatter: recvcount * size * nranks        alltoall: count * size * nranks
 //   alltoallv: sum(sendcounts) * size               send/recv: count * size
-// nranks comes from ncclCommCount (resolved with dlsym, cached per communicator).
+// nranks (and the process's rank) come from the communicator's creation call
+// (ncclCommInitRank / ncclCommInitRankConfig EXIT: nranks, myrank, *newcomm), cached per
+// communicator; communicators made otherwise (ncclCommSplit, ncclCommInitAll) are asked
+// with ncclCommCount / ncclCommUserRank, resolved in the already-loaded librccl (torch
+// loads it RTLD_LOCAL, so a plain dlsym(RTLD_DEFAULT) does not see it).
 #include <dlfcn.h>
+#include <link.h>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -53,6 +58,35 @@ size_t dtype_size(int t) {
   }
 }
 
+// Handle of the librccl the process already loaded (never loads one itself).
+void* rccl_lib() {
+  static void* h = [] {
+    std::string name;
+    dl_iterate_phdr(
+        [](dl_phdr_info* info, size_t, void* out) -> int {
+          if (info->dlpi_name && std::strstr(info->dlpi_name, "librccl")) {
+            *static_cast<std::string*>(out) = info->dlpi_name;
+            return 1;
+          }
+          return 0;
+        },
+        &name);
+    void* lib = name.empty() ? nullptr : ::dlopen(name.c_str(), RTLD_NOW | RTLD_NOLOAD);
+    return lib ? lib : RTLD_DEFAULT;
+  }();
+  return h;
+}
+
+// Caller holds g_comm_mu.  The file reports the process's largest communicator (its world
+// / data-parallel group; TP/PP/EP sub-communicators are smaller), so the rank is stable.
+void note_comm_locked(const void* comm, int n, int rank) {
+  g_nranks[comm] = n;
+  if (g_shm && n >= g_shm->nranks) {
+    g_shm->nranks = n;
+    g_shm->rank = rank;
+  }
+}
+
 int comm_nranks(const void* comm) {
   if (!comm) return 1;
   {
@@ -61,8 +95,8 @@ int comm_nranks(const void* comm) {
     if (it != g_nranks.end()) return it->second;
   }
   using query_fn = int (*)(const void*, int*);
-  static query_fn count = reinterpret_cast<query_fn>(::dlsym(RTLD_DEFAULT, "ncclCommCount"));
-  static query_fn user_rank = reinterpret_cast<query_fn>(::dlsym(RTLD_DEFAULT, "ncclCommUserRank"));
+  static query_fn count = reinterpret_cast<query_fn>(::dlsym(rccl_lib(), "ncclCommCount"));
+  static query_fn user_rank = reinterpret_cast<query_fn>(::dlsym(rccl_lib(), "ncclCommUserRank"));
   int n = 1, rank = -1;
   if (!t_in_query) {
     t_in_query = true;  // the queries are themselves traced: do not recurse
@@ -71,13 +105,7 @@ int comm_nranks(const void* comm) {
     t_in_query = false;
   }
   std::lock_guard<std::mutex> lk(g_comm_mu);
-  g_nranks[comm] = n;
-  // The file reports the process's largest communicator (its world / data-parallel
-  // group; sub-communicators of TP/PP/EP are smaller), so the rank label is stable.
-  if (g_shm && n >= g_shm->nranks) {
-    g_shm->nranks = n;
-    g_shm->rank = rank;
-  }
+  note_comm_locked(comm, n, rank);
   return n;
 }
 
@@ -106,7 +134,23 @@ bool moves_data(int op) {
 }
 
 void on_rccl(rocprofiler_callback_tracing_record_t rec, rocprofiler_user_data_t*, void*) {
-  if (t_in_query || !moves_data(int(rec.operation))) return;
+  if (t_in_query) return;
+  if (rec.phase == ROCPROFILER_CALLBACK_PHASE_EXIT &&
+      (rec.operation == ROCPROFILER_RCCL_API_ID_ncclCommInitRank ||
+       rec.operation == ROCPROFILER_RCCL_API_ID_ncclCommInitRankConfig)) {
+    // the new communicator exists now: remember its size and this process's rank
+    const auto& a = static_cast<const rocprofiler_callback_tracing_rccl_api_data_t*>(rec.payload)->args;
+    const bool cfg = rec.operation == ROCPROFILER_RCCL_API_ID_ncclCommInitRankConfig;
+    ncclComm_t* out = cfg ? a.ncclCommInitRankConfig.comm : a.ncclCommInitRank.newcomm;
+    const int n = cfg ? a.ncclCommInitRankConfig.nranks : a.ncclCommInitRank.nranks;
+    const int rank = cfg ? a.ncclCommInitRankConfig.myrank : a.ncclCommInitRank.myrank;
+    if (out && *out && n > 0) {
+      std::lock_guard<std::mutex> lk(g_comm_mu);
+      note_comm_locked(*out, n, rank);
+    }
+    return;
+  }
+  if (!moves_data(int(rec.operation))) return;
   if (rec.phase == ROCPROFILER_CALLBACK_PHASE_EXIT) {
     if (t_depth > 0) --t_depth;
     return;
