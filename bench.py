@@ -267,10 +267,14 @@ def main() -> int:
             # namespace — the same number unless the box runs us in a PID namespace
             cgroups[p] = cgroups[op] = kubepods_cgroup(uid, cid, qos="guaranteed")
         write_pod_map(pod_map, pods, cgroups)
+        # timing=True: the server echoes when it parsed the request and started writing,
+        # so each latency splits into request wake-up / server work / response delivery
         client = n.ScrapeClient("127.0.0.1", port, "/metrics", args.gzip, 5000,
-                                promproto.ACCEPT if args.proto else "")
+                                promproto.ACCEPT if args.proto else "", True)
     else:
         client = None
+
+    splits: list = []
 
     def step(cl, lat: list | None):
         t_start = time.perf_counter()
@@ -280,6 +284,10 @@ def main() -> int:
             ns = cl.scrape()  # GPUs are busy with the burst while we scrape
             if lat is not None and ns >= 0:
                 lat.append(ns / 1e3)
+                if cl is client:
+                    t_send, t_parse, t_write, t_done = cl.last_timing()
+                    if t_parse and t_send <= t_parse <= t_write <= t_done:
+                        splits.append(((t_parse - t_send) / 1e3, (t_write - t_parse) / 1e3, (t_done - t_write) / 1e3))
         if dist is not None:
             dist.all_reduce(grad)
         sync()
@@ -458,6 +466,13 @@ def main() -> int:
             "exporter_cpu_percent_identity_phase": round(cpu_id, 3) if cpu_id is not None else None,
             "scrape_bytes_identity": id_bytes if lat_id else None,
             "server_scrape_mean_us": server_mean_us,
+            # per-scrape split (medians of each part; same-host CLOCK_MONOTONIC): request sent ->
+            # server parsed it (loopback + server thread wake-up), server parse -> write start,
+            # write start -> client has the last byte (copy + client wake-up)
+            "latency_split_p50_us": {
+                "request_to_server": round(statistics.median(x[0] for x in splits), 2),
+                "server_work": round(statistics.median(x[1] for x in splits), 2),
+                "response_to_client": round(statistics.median(x[2] for x in splits), 2)} if splits else None,
             "scrapes": len(lat),
             "scrape_errors": client.errors,
             "scrape_bytes": client.last_bytes,

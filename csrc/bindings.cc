@@ -241,9 +241,9 @@ PYBIND11_MODULE(_gpuexp, m) {
      py::arg("timeout_ms") = 5000, py::arg("keep_last_body") = false);
 
   py::class_<ScrapeClient>(m, "ScrapeClient")
-      .def(py::init<std::string, int, std::string, bool, int, std::string>(), py::arg("host"), py::arg("port"),
-           py::arg("path") = "/metrics", py::arg("gzip") = false, py::arg("timeout_ms") = 5000,
-           py::arg("accept") = "")
+      .def(py::init<std::string, int, std::string, bool, int, std::string, bool>(), py::arg("host"),
+           py::arg("port"), py::arg("path") = "/metrics", py::arg("gzip") = false, py::arg("timeout_ms") = 5000,
+           py::arg("accept") = "", py::arg("timing") = false)
       .def("scrape", [](ScrapeClient& c) {
         py::gil_scoped_release rel;
         return c.scrape();
@@ -251,7 +251,9 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_property_readonly("last_status", &ScrapeClient::last_status)
       .def_property_readonly("last_bytes", &ScrapeClient::last_bytes)
       .def_property_readonly("errors", &ScrapeClient::errors)
-      .def("last_body", [](ScrapeClient& c) { return py::bytes(c.last_body()); });
+      .def("last_body", [](ScrapeClient& c) { return py::bytes(c.last_body()); })
+      .def("last_timing", &ScrapeClient::last_timing,
+           "CLOCK_MONOTONIC ns [client send, server parsed, server writing, client done] of the last scrape");
 
   // --- SeriesTable (unit tests of the exposition layer) ---
   py::enum_<MetricType>(m, "MetricType")

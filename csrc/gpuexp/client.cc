@@ -113,10 +113,11 @@ int read_response(int fd, RecvBuf* rb, size_t* body_off, size_t* body_len, bool*
 }  // namespace
 
 ScrapeClient::ScrapeClient(std::string host, int port, std::string path, bool gzip, int timeout_ms,
-                           const std::string& accept)
+                           const std::string& accept, bool timing)
     : host_(std::move(host)), path_(std::move(path)), port_(port), timeout_ms_(timeout_ms) {
   req_ = "GET " + path_ + " HTTP/1.1\r\nHost: " + host_ + "\r\nUser-Agent: gpuexp-bench\r\n";
   if (gzip) req_ += "Accept-Encoding: gzip\r\n";
+  if (timing) req_ += "X-Gpuexp-Timing: 1\r\n";
   if (!accept.empty()) req_ += "Accept: " + accept + "\r\n";
   req_ += "\r\n";
 }
@@ -148,6 +149,22 @@ double ScrapeClient::scrape() {
   }
   status_ = code;
   bytes_ = body_len_;
+  t_send_ = t0;
+  t_done_ = t1;
+  t_srv_parse_ = t_srv_write_ = 0;
+  {
+    // the response's header block ends 4 bytes before the body
+    static const char kName[] = "\r\nX-Gpuexp-Timing: ";
+    const char* hb = rb_.data.data();
+    const char* he = hb + body_off_;
+    const char* p = std::search(hb, he, kName, kName + sizeof(kName) - 1);
+    if (p != he) {
+      p += sizeof(kName) - 1;
+      char* q = nullptr;
+      t_srv_parse_ = std::strtoull(p, &q, 10);
+      t_srv_write_ = q ? std::strtoull(q, nullptr, 10) : 0;
+    }
+  }
   if (server_close) {
     ::close(fd_);
     fd_ = -1;

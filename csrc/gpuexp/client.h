@@ -35,8 +35,9 @@ struct RecvBuf {
 class ScrapeClient {
  public:
   // accept: optional Accept header value (e.g. the protobuf exposition's media type).
+  // timing: ask the server to echo its timestamps (X-Gpuexp-Timing) for a latency split.
   ScrapeClient(std::string host, int port, std::string path, bool gzip, int timeout_ms,
-               const std::string& accept = "");
+               const std::string& accept = "", bool timing = false);
   ~ScrapeClient();
   double scrape();
   int last_status() const { return status_; }
@@ -44,8 +45,12 @@ class ScrapeClient {
   // Body of the last response (valid until the next scrape).
   std::string last_body() const { return std::string(rb_.data.data() + body_off_, body_len_); }
   uint64_t errors() const { return errors_; }
+  // Last scrape, CLOCK_MONOTONIC ns: {client send, server parsed, server writing, client done};
+  // the server fields are 0 unless timing was requested and echoed.
+  std::vector<uint64_t> last_timing() const { return {t_send_, t_srv_parse_, t_srv_write_, t_done_}; }
 
  private:
+  uint64_t t_send_ = 0, t_srv_parse_ = 0, t_srv_write_ = 0, t_done_ = 0;
   std::string host_, path_, req_;
   int port_, timeout_ms_, fd_ = -1, status_ = 0;
   uint64_t bytes_ = 0, errors_ = 0;

@@ -311,7 +311,7 @@ void HttpServer::run(Worker* w) {
         version = line.substr(s2 + 1);
       }
       bool http10 = version == "HTTP/1.0";
-      bool want_gzip = false, want_proto = false, conn_close = http10, conn_keep = false;
+      bool want_gzip = false, want_proto = false, conn_close = http10, conn_keep = false, want_timing = false;
       uint64_t content_len = 0;
       size_t pos = le + 2;
       while (pos < end) {
@@ -328,6 +328,8 @@ void HttpServer::run(Worker* w) {
           if (contains_token(h + 11, hn - 11, "keep-alive")) conn_keep = true;
         } else if (ieq_prefix(h, hn, "content-length:")) {
           parse_u64(h + 15, hn - 15, &content_len);
+        } else if (ieq_prefix(h, hn, "x-gpuexp-timing:")) {
+          want_timing = true;  // benchmark breakdown: echo the server's own timestamps
         }
         pos = nl + 2;
       }
@@ -371,6 +373,15 @@ void HttpServer::run(Worker* w) {
           if (gz) {
             c.head.append("Content-Encoding: gzip\r\n");
             stats_.gzip_responses.fetch_add(1, std::memory_order_relaxed);
+          }
+          if (want_timing) {
+            // CLOCK_MONOTONIC ns of: request parsed (after this thread woke for it), and
+            // response about to be written — a same-host client splits its latency with them
+            c.head.append("X-Gpuexp-Timing: ");
+            c.head.append(std::to_string(t0));
+            c.head.append(" ");
+            c.head.append(std::to_string(mono_ns()));
+            c.head.append("\r\n");
           }
           c.head.append("Content-Length: ");
           c.head.append(std::to_string(b.size()));

@@ -221,3 +221,26 @@ def test_protobuf_negotiation_respects_q(mock_engine, accept, proto):
     e.tick(2_000_000_000)
     r, _ = req(e.http_port, "/metrics", headers={"Accept": accept})
     assert (r.getheader("Content-Type") == PB_CT) is proto
+
+
+def test_scrape_timing_split(mock_engine, native):
+    """X-Gpuexp-Timing: the server echoes (request parsed, write started) on the client's
+    clock (same host, CLOCK_MONOTONIC), so the bench can split a scrape's latency; the
+    body is unchanged and a request without the header gets no timing header."""
+    e = mock_engine(1)
+    e.tick(1_000_000_000)
+    c = native.ScrapeClient("127.0.0.1", e.http_port, "/metrics", timing=True)
+    for _ in range(5):
+        assert c.scrape() > 0
+        t_send, t_parse, t_write, t_done = c.last_timing()
+        assert 0 < t_send <= t_parse <= t_write <= t_done
+    assert c.last_body().decode() == e.snapshot_text()
+    plain = native.ScrapeClient("127.0.0.1", e.http_port, "/metrics")
+    assert plain.scrape() > 0 and plain.last_timing()[1] == 0
+    s = socket.create_connection(("127.0.0.1", e.http_port))
+    s.sendall(b"GET /metrics HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n")
+    head = b""
+    while b"\r\n\r\n" not in head:
+        head += s.recv(65536)
+    s.close()
+    assert b"X-Gpuexp-Timing" not in head.split(b"\r\n\r\n")[0]
