@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 namespace gpuexp {
 
@@ -199,9 +200,12 @@ __device__ __forceinline__ void read_frags(const uint16_t* tile, int row_base, i
   }
 }
 
+// kPrio 0: raise the wave's priority around each 16-MFMA cluster (T5); 1: no setprio;
+// 2: static — wave row 1 (the later half) runs at priority 1 throughout, set once.
+template <int kPrio>
 __device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[4][2], const bf16x8 (&af)[4][2],
                                               const bf16x8 (&bf)[4][2]) {
-  __builtin_amdgcn_s_setprio(1);
+  if (kPrio == 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -209,7 +213,7 @@ __device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[4][2], const bf16x8 (
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni)
         acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi][kk], bf[ni][kk], acc[mi][ni], 0, 0, 0);
-  __builtin_amdgcn_s_setprio(0);
+  if (kPrio == 0) __builtin_amdgcn_s_setprio(0);
 }
 
 // Ends a phase: this wave's ds_reads have landed (so the rows they read may be restaged
@@ -239,7 +243,7 @@ __device__ __forceinline__ void wait_vm() {
 // so every wave waits before the barrier that precedes row 0's read): end of phase 3
 // retires t+1's A-M0/B-N0/B-N1 (then in flight: t+1's A-M1, t+2's first 4), end of phase 1
 // retires t's A-M1 (then in flight: t+1's first 6 + A-M1).
-template <int kGroupM>
+template <int kGroupM, int kPrio, bool kSnake = false>
 __global__ void __launch_bounds__(kThreads2, 1)
 gemm_bf16_tn_256_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
                         int M, int N, int K) {
@@ -274,15 +278,83 @@ gemm_bf16_tn_256_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
         for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / kBK;  // >= 2
+  bf16x8 af[4][2], b0[4][2], b1[4][2];
+  const int a_row = wr * 128, b_row = wc * 64;
+  if constexpr (kSnake) {
+    // Balanced reads (8/4/8/4 per phase instead of 12/4/8/0): phase 4 prefetches the B
+    // group the NEXT K-tile starts with into the B registers phase 4 does not use, and the
+    // quadrant order alternates with K-tile parity to make that possible:
+    //   even t: P1 read A-M0 -> Q00(b0) | P2 read B-N1 -> Q01 | P3 read A-M1 -> Q11 | P4 read B-N1(t+1) -> Q10(b0)
+    //   odd  t: P1 read A-M0 -> Q01(b1) | P2 read B-N0 -> Q00 | P3 read A-M1 -> Q10 | P4 read B-N0(t+1) -> Q11(b1)
+    // Staging of t+2 (buffer t&1), every group >= 2 phases after its last read under the
+    // stagger: P1 A-M1 of t+1; P3 A-M0 + the B group read at P4(t-1); P4 the B group read
+    // at P2.  Waits (before the barrier that precedes row 0's read): end of P1 retires
+    // t's A-M1; end of P2 t+1's first 4 loads (A-M0 + the prefetched B); end of P4 t+1's
+    // other B group.
+    GEMM2_STAGE_A(0, 0); GEMM2_STAGE_B(0, 0); GEMM2_STAGE_B(1, 0); GEMM2_STAGE_A(1, 0);
+    GEMM2_STAGE_A(0, 1); GEMM2_STAGE_B(1, 1); GEMM2_STAGE_B(0, 1);  // tile 1 (odd) order
+    wait_vm<6>();  // K-tile 0 landed
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger: row 1 one phase behind
+    if (kPrio == 2 && wr == 1) __builtin_amdgcn_s_setprio(1);
+    asm volatile("" ::: "memory");
+    read_frags(smem + kTile2, b_row, lane, b0, 2);  // B-N0 of tile 0 ("phase 4 of tile -1")
+    auto tile = [&](int t, auto odd_tag) {
+      constexpr bool odd = decltype(odd_tag)::value;
+      const uint16_t* As = smem + (odd ? 2 * kTile2 : 0);
+      const uint16_t* Bs = As + kTile2;
+      const uint16_t* Bn = smem + (odd ? 0 : 2 * kTile2) + kTile2;
+      const bool has1 = t + 1 < nk, has2 = t + 2 < nk;
+      // phase 1
+      read_frags(As, a_row, lane, af, 4);
+      if (has1) GEMM2_STAGE_A(1, t + 1);
+      if constexpr (odd) mfma_quadrant<kPrio>(acc[0][1], af, b1); else mfma_quadrant<kPrio>(acc[0][0], af, b0);
+      if (has1) wait_vm<8>(); else wait_vm<0>();  // this tile's A-M1 landed
+      phase_end();
+      // phase 2
+      if constexpr (odd) {
+        read_frags(Bs, b_row, lane, b0, 2);
+        mfma_quadrant<kPrio>(acc[0][0], af, b0);
+      } else {
+        read_frags(Bs, b_row + 32, lane, b1, 2);
+        mfma_quadrant<kPrio>(acc[0][1], af, b1);
+      }
+      if (has1) wait_vm<4>(); else wait_vm<0>();  // t+1's A-M0 + first B group landed
+      phase_end();
+      // phase 3
+      read_frags(As, a_row + 64, lane, af, 4);
+      if (has2) {
+        GEMM2_STAGE_A(0, t + 2);
+        if constexpr (odd) GEMM2_STAGE_B(1, t + 2); else GEMM2_STAGE_B(0, t + 2);
+      }
+      if constexpr (odd) mfma_quadrant<kPrio>(acc[1][0], af, b0); else mfma_quadrant<kPrio>(acc[1][1], af, b1);
+      phase_end();
+      // phase 4
+      if constexpr (odd) {
+        if (has1) read_frags(Bn, b_row, lane, b0, 2);
+        if (has2) GEMM2_STAGE_B(0, t + 2);
+        mfma_quadrant<kPrio>(acc[1][1], af, b1);
+      } else {
+        if (has1) read_frags(Bn, b_row + 32, lane, b1, 2);
+        if (has2) GEMM2_STAGE_B(1, t + 2);
+        mfma_quadrant<kPrio>(acc[1][0], af, b0);
+      }
+      if (has2) wait_vm<8>(); else if (has1) wait_vm<2>(); else wait_vm<0>();  // t+1's second B group
+      phase_end();
+    };
+    for (int t = 0; t < nk; t += 2) {
+      tile(t, std::false_type{});
+      if (t + 1 < nk) tile(t + 1, std::true_type{});
+    }
+  } else {
   GEMM2_STAGE_A(0, 0); GEMM2_STAGE_B(0, 0); GEMM2_STAGE_B(1, 0); GEMM2_STAGE_A(1, 0);
   GEMM2_STAGE_A(0, 1); GEMM2_STAGE_B(0, 1); GEMM2_STAGE_B(1, 1);
   wait_vm<6>();  // K-tile 0 landed; tile 1's first three groups in flight
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger: row 1 one phase behind
+  if (kPrio == 2 && wr == 1) __builtin_amdgcn_s_setprio(1);
   asm volatile("" ::: "memory");
 
-  bf16x8 af[4][2], b0[4][2], b1[4][2];
-  const int a_row = wr * 128, b_row = wc * 64;
   for (int t = 0; t < nk; ++t) {
     const uint16_t* As = smem + (t & 1) * 2 * kTile2;
     const uint16_t* Bs = As + kTile2;
@@ -291,23 +363,24 @@ gemm_bf16_tn_256_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
     read_frags(As, a_row, lane, af, 4);
     read_frags(Bs, b_row, lane, b0, 2);
     if (has1) GEMM2_STAGE_A(1, t + 1);
-    mfma_quadrant(acc[0][0], af, b0);
+    mfma_quadrant<kPrio>(acc[0][0], af, b0);
     if (has1) wait_vm<8>(); else wait_vm<0>();  // this tile's A-M1 landed
     phase_end();
     // phase 2
     read_frags(Bs, b_row + 32, lane, b1, 2);
-    mfma_quadrant(acc[0][1], af, b1);
+    mfma_quadrant<kPrio>(acc[0][1], af, b1);
     phase_end();
     // phase 3
     read_frags(As, a_row + 64, lane, af, 4);
     if (has2) { GEMM2_STAGE_A(0, t + 2); GEMM2_STAGE_B(0, t + 2); }
-    mfma_quadrant(acc[1][1], af, b1);
+    mfma_quadrant<kPrio>(acc[1][1], af, b1);
     if (has2) wait_vm<6>(); else if (has1) wait_vm<2>(); else wait_vm<0>();  // t+1's first 3 groups landed
     phase_end();
     // phase 4
     if (has2) GEMM2_STAGE_B(1, t + 2);
-    mfma_quadrant(acc[1][0], af, b0);
+    mfma_quadrant<kPrio>(acc[1][0], af, b0);
     phase_end();
+  }
   }
   if (wr == 0) __builtin_amdgcn_s_barrier();  // close the stagger: row 1's last phase is done
   asm volatile("" ::: "memory");
@@ -358,9 +431,14 @@ hipError_t launch_gemm_bf16_tn(const void* A, const void* B, void* C, int M, int
   const bool big = variant >= 2 || (variant == 0 && gemm256_shape_ok(M, N, K));
   if (big) {
     if (!gemm256_shape_ok(M, N, K)) return hipErrorInvalidValue;
-    // auto = 8-row groups: 1355 vs 1265 TFLOP/s (row-major) at 8192^3, 1301 vs 1289 at 4096^3
-    auto k = variant == 2 ? gemm_bf16_tn_256_kernel<1>
-             : variant == 3 ? gemm_bf16_tn_256_kernel<4> : gemm_bf16_tn_256_kernel<8>;
+    // auto (0) = 7: 8-row tile groups (1355 vs 1265 TFLOP/s row-major at 8192^3), per-cluster
+    // setprio (5 / 6 without it / static form: -5 %), balanced snake-B reads (+0.3-1 % over 4)
+    auto k = variant == 2   ? gemm_bf16_tn_256_kernel<1, 0>
+             : variant == 3 ? gemm_bf16_tn_256_kernel<4, 0>
+             : variant == 4 ? gemm_bf16_tn_256_kernel<8, 0>
+             : variant == 5 ? gemm_bf16_tn_256_kernel<8, 1>
+             : variant == 6 ? gemm_bf16_tn_256_kernel<8, 2>
+                            : gemm_bf16_tn_256_kernel<8, 0, true>;
     hipLaunchKernelGGL(k, dim3((M / kBM2) * (N / kBN2)), dim3(kThreads2), 0, stream,
                        static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M,
                        N, K);
