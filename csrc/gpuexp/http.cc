@@ -117,27 +117,51 @@ HttpServer::HttpServer(SnapshotStore* store, const HttpConfig& cfg) : store_(sto
 
 HttpServer::~HttpServer() { stop(); }
 
+// host "" = every interface: an IPv6 socket with IPV6_V6ONLY off accepts IPv4 too (what
+// Go's ListenAndServe(":8000") does, main.go:71), falling back to IPv4 0.0.0.0 when the
+// node has IPv6 disabled.  A literal with ':' binds that IPv6 address; otherwise IPv4.
 static int make_listener(const std::string& host, int port, bool reuseport, std::string* err) {
-  int fd = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+  const bool any = host.empty();
+  const bool v6 = any || host.find(':') != std::string::npos;
+  int fd = ::socket(v6 ? AF_INET6 : AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+  if (fd < 0 && any) return make_listener("0.0.0.0", port, reuseport, err);
   if (fd < 0) {
     *err = std::string("socket: ") + std::strerror(errno);
     return -1;
   }
-  int one = 1;
+  int one = 1, zero = 0;
   ::setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
   if (reuseport) ::setsockopt(fd, SOL_SOCKET, SO_REUSEPORT, &one, sizeof(one));
-  sockaddr_in addr{};
-  addr.sin_family = AF_INET;
-  addr.sin_port = htons(uint16_t(port));
-  std::string h = host.empty() ? "0.0.0.0" : host;
-  if (::inet_pton(AF_INET, h.c_str(), &addr.sin_addr) != 1) {
-    *err = "bad listen host: " + h;
-    ::close(fd);
-    return -1;
+  sockaddr_storage ss{};
+  socklen_t len = 0;
+  if (v6) {
+    ::setsockopt(fd, IPPROTO_IPV6, IPV6_V6ONLY, &zero, sizeof(zero));
+    auto* a6 = reinterpret_cast<sockaddr_in6*>(&ss);
+    a6->sin6_family = AF_INET6;
+    a6->sin6_port = htons(uint16_t(port));
+    a6->sin6_addr = in6addr_any;
+    if (!any && ::inet_pton(AF_INET6, host.c_str(), &a6->sin6_addr) != 1) {
+      *err = "bad listen host: " + host;
+      ::close(fd);
+      return -1;
+    }
+    len = sizeof(sockaddr_in6);
+  } else {
+    auto* a4 = reinterpret_cast<sockaddr_in*>(&ss);
+    a4->sin_family = AF_INET;
+    a4->sin_port = htons(uint16_t(port));
+    if (::inet_pton(AF_INET, host.c_str(), &a4->sin_addr) != 1) {
+      *err = "bad listen host: " + host;
+      ::close(fd);
+      return -1;
+    }
+    len = sizeof(sockaddr_in);
   }
-  if (::bind(fd, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) < 0) {
-    *err = "bind " + h + ":" + std::to_string(port) + ": " + std::strerror(errno);
+  if (::bind(fd, reinterpret_cast<sockaddr*>(&ss), len) < 0) {
+    const int e = errno;
     ::close(fd);
+    if (any && (e == EAFNOSUPPORT || e == EADDRNOTAVAIL)) return make_listener("0.0.0.0", port, reuseport, err);
+    *err = "bind " + (any ? std::string("[::]") : host) + ":" + std::to_string(port) + ": " + std::strerror(e);
     return -1;
   }
   if (::listen(fd, 1024) < 0) {
@@ -160,10 +184,11 @@ bool HttpServer::start(std::string* err) {
       return false;
     }
     if (t == 0) {
-      sockaddr_in a{};
+      sockaddr_storage a{};
       socklen_t al = sizeof(a);
       ::getsockname(w->listen_fd, reinterpret_cast<sockaddr*>(&a), &al);
-      bound_port_ = ntohs(a.sin_port);
+      bound_port_ = a.ss_family == AF_INET6 ? ntohs(reinterpret_cast<sockaddr_in6*>(&a)->sin6_port)
+                                            : ntohs(reinterpret_cast<sockaddr_in*>(&a)->sin_port);
       port = bound_port_;
     }
     w->epfd = ::epoll_create1(EPOLL_CLOEXEC);

@@ -65,8 +65,13 @@ class Config:
     trace: str = ""                        # Chrome trace JSON of sampler stages
 
     def listen_host_port(self) -> tuple[str, int]:
+        """(host, port).  An empty host (":8000", the reference's `ListenAndServe(":8000")`,
+        main.go:71) means every interface, IPv6 and IPv4 (dual-stack, as Go binds it);
+        "[::1]:8000" / "127.0.0.1:8000" bind one address."""
         host, _, port = self.listen.rpartition(":")
-        return (host or "0.0.0.0"), int(port)
+        if host.startswith("[") and host.endswith("]"):
+            host = host[1:-1]
+        return host, int(port)
 
     def resolved_backend(self) -> str:
         if self.backend != "auto":

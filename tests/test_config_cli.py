@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_defaults_match_reference_endpoint():
     c = Config()
     assert c.listen == ":8000" and c.path == "/metrics"  # main.go:70-71
-    assert c.listen_host_port() == ("0.0.0.0", 8000)
+    assert c.listen_host_port() == ("", 8000)  # all interfaces, dual-stack like Go's ":8000"
 
 
 def test_precedence(tmp_path):

@@ -244,3 +244,32 @@ def test_scrape_timing_split(mock_engine, native):
         head += s.recv(65536)
     s.close()
     assert b"X-Gpuexp-Timing" not in head.split(b"\r\n\r\n")[0]
+
+
+def test_listen_all_interfaces_is_dual_stack(native):
+    """":8000" (empty host) listens like Go's ListenAndServe(":8000") (main.go:71): IPv4
+    and IPv6 clients both reach it; an explicit IPv4 host stays IPv4-only."""
+    c = native.EngineConfig()
+    c.backend = "mock"
+    c.interval_s = 0
+    c.http.host = ""
+    c.http.port = 0
+    e = native.Engine(c)
+    e.start()
+    try:
+        e.tick(1_000_000_000)
+        port = e.http_port
+        for fam, addr in ((socket.AF_INET, "127.0.0.1"), (socket.AF_INET6, "::1")):
+            try:
+                s = socket.socket(fam, socket.SOCK_STREAM)
+                s.settimeout(5)
+                s.connect((addr, port))
+            except OSError as ex:
+                if fam == socket.AF_INET6:
+                    pytest.skip(f"no IPv6 loopback here: {ex}")
+                raise
+            s.sendall(b"GET /healthz HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n")
+            assert s.recv(4096).startswith(b"HTTP/1.1 200"), fam
+            s.close()
+    finally:
+        e.stop()
