@@ -19,7 +19,7 @@
 namespace gpuexp {
 
 struct HttpConfig {
-  std::string host = "0.0.0.0";
+  std::string host;  // "" = every interface, dual-stack (see make_listener)
   int port = 8000;                     // main.go:71 ":8000"; 0 = ephemeral
   std::string metrics_path = "/metrics";  // main.go:70
   int threads = 1;
