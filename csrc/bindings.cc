@@ -119,6 +119,7 @@ PYBIND11_MODULE(_gpuexp, m) {
     append_escaped_label_value(&s, v);
     return s;
   });
+  m.def("gzip_impl", []() { return std::string(gzip_impl()); });
   m.def("gzip", [](py::bytes b, int level) {
     std::string in = b, out;
     if (!gzip_compress(in, &out, level)) throw std::runtime_error("gzip failed");

@@ -1,12 +1,62 @@
+#include <dlfcn.h>
 #include <zlib.h>
+
+#include <cstdlib>
+#include <cstring>
 
 #include "gpuexp/snapshot.h"
 
 namespace gpuexp {
 
 namespace {
-// One deflate state per compressing thread (the sampler), reset per body instead of
-// re-initialised: saves the ~270 KB state allocation every tick.
+
+// libdeflate (loaded at run time when the node has it; its C API is declared here since
+// the image ships the runtime library without headers) compresses the exposition ~1.8x
+// faster than zlib at level 1 and a little smaller: 256 vs 459 us for an 8-GPU full
+// profile (104 KB).  GPUEXP_GZIP_IMPL=zlib forces zlib.
+struct LibDeflate {
+  void* (*alloc)(int) = nullptr;
+  size_t (*gzip)(void*, const void*, size_t, void*, size_t) = nullptr;
+  size_t (*bound)(void*, size_t) = nullptr;
+  void (*release)(void*) = nullptr;
+  bool ok = false;
+  LibDeflate() {
+    const char* impl = std::getenv("GPUEXP_GZIP_IMPL");
+    if (impl && std::strcmp(impl, "zlib") == 0) return;
+    void* h = ::dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return;
+    alloc = reinterpret_cast<void* (*)(int)>(::dlsym(h, "libdeflate_alloc_compressor"));
+    gzip = reinterpret_cast<size_t (*)(void*, const void*, size_t, void*, size_t)>(
+        ::dlsym(h, "libdeflate_gzip_compress"));
+    bound = reinterpret_cast<size_t (*)(void*, size_t)>(::dlsym(h, "libdeflate_gzip_compress_bound"));
+    release = reinterpret_cast<void (*)(void*)>(::dlsym(h, "libdeflate_free_compressor"));
+    ok = alloc && gzip && bound && release;
+  }
+};
+
+const LibDeflate& libdeflate() {
+  static const LibDeflate l;
+  return l;
+}
+
+// One compressor per compressing thread (the sampler), kept across ticks.
+struct DeflateCompressor {
+  void* c = nullptr;
+  int level = -100;
+  ~DeflateCompressor() {
+    if (c) libdeflate().release(c);
+  }
+  void* get(int lvl) {
+    if (c && lvl == level) return c;
+    if (c) libdeflate().release(c);
+    c = libdeflate().alloc(lvl < 1 ? 1 : lvl > 12 ? 12 : lvl);
+    level = lvl;
+    return c;
+  }
+};
+
+// zlib fallback: one deflate state per compressing thread, reset per body instead of
+// re-initialised (saves the ~270 KB state allocation every tick).
 struct Deflater {
   z_stream zs{};
   int level = -100;
@@ -24,9 +74,23 @@ struct Deflater {
     return ok;
   }
 };
+
 }  // namespace
 
+const char* gzip_impl() { return libdeflate().ok ? "libdeflate" : "zlib"; }
+
 bool gzip_compress(const std::string& in, std::string* out, int level) {
+  if (libdeflate().ok) {
+    thread_local DeflateCompressor dc;
+    if (void* c = dc.get(level)) {
+      out->resize(libdeflate().bound(c, in.size()));
+      const size_t n = libdeflate().gzip(c, in.data(), in.size(), &(*out)[0], out->size());
+      if (n) {
+        out->resize(n);
+        return true;
+      }
+    }
+  }
   thread_local Deflater d;
   if (!d.prepare(level)) return false;
   z_stream& zs = d.zs;

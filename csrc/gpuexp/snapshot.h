@@ -95,5 +95,7 @@ class SnapshotStore {
 
 // gzip (RFC 1952) of `in` at compression `level` into `out`.  Returns false on error.
 bool gzip_compress(const std::string& in, std::string* out, int level = 1);
+// "libdeflate" (loaded at run time when present) or "zlib".
+const char* gzip_impl();
 
 }  // namespace gpuexp

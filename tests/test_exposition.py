@@ -1,6 +1,7 @@
 """Exposition layer: value formatting, escaping, family ordering, stale-series GC,
 histograms — checked against an independent strict parser."""
 import math
+import os
 
 import pytest
 
@@ -101,3 +102,31 @@ def test_gzip_roundtrip(native):
     import gzip
     data = b"amd_gpu_up{gpu=\"0\"} 1\n" * 1000
     assert gzip.decompress(native.gzip(data)) == data
+
+
+@pytest.mark.parametrize("impl", ["default", "zlib"])
+def test_gzip_implementations(impl):
+    """libdeflate (when the node has it) and the zlib fallback both emit valid gzip for
+    bodies of every size, at every level; GPUEXP_GZIP_IMPL=zlib forces the fallback."""
+    import subprocess
+    import sys
+    code = (
+        "import gzip, os, random\n"
+        "from kubernetes_gpu_exporter_amd._native import load\n"
+        "n = load()\n"
+        "random.seed(1)\n"
+        "for size in (0, 1, 100, 65536, 300000):\n"
+        "    data = bytes(random.choice(b'amd_gpu {}=\"0123456789.\\n') for _ in range(size))\n"
+        "    for level in (1, 6, 9):\n"
+        "        assert gzip.decompress(n.gzip(data, level)) == data, (size, level)\n"
+        "print(n.gzip_impl())\n")
+    env = dict(os.environ)
+    if impl == "zlib":
+        env["GPUEXP_GZIP_IMPL"] = "zlib"
+    else:
+        env.pop("GPUEXP_GZIP_IMPL", None)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stderr
+    used = r.stdout.strip()
+    assert used == "zlib" if impl == "zlib" else used in ("libdeflate", "zlib")
