@@ -130,3 +130,34 @@ def test_gzip_implementations(impl):
     assert r.returncode == 0, r.stderr
     used = r.stdout.strip()
     assert used == "zlib" if impl == "zlib" else used in ("libdeflate", "zlib")
+
+
+def test_exposition_parses_with_prometheus_client(mock_engine):
+    """An independent parser (the official Python client's text-format parser) accepts the
+    full 8-GPU exposition, with processes, pods, histograms and escaped label values, and
+    reads back the same families, types and sample values as ours."""
+    from prometheus_client.parser import text_string_to_metric_families
+    e = mock_engine(8, http=False, series_profile="full", enable_sentinel=True, enable_counters=True)
+    uid = "12345678-1234-1234-1234-123456789abc"
+    cg = ("/kubepods.slice/kubepods-burstable.slice/kubepods-burstable-pod" + uid.replace("-", "_")
+          + ".slice/cri-containerd-" + "a" * 64 + ".scope")
+    e.mock_set_processes(0, [dict(pid=42, vram_bytes=3.0e9, cu_occupancy=64, name='we"ird\\comm')])
+    e.set_pid_cgroup(42, cg)
+    e.set_pods([dict(uid=uid, namespace="ns", name="pod-a", containers={"a" * 64: "main"})])
+    for i in range(3):
+        e.tick((i + 1) * 100_000_000)
+    text = e.snapshot_text()
+    ours = promtext.parse(text)
+    theirs = {f.name: f for f in text_string_to_metric_families(text)}
+    for name, fam in ours.items():
+        # the official parser strips _total from counter family names
+        tf = theirs.get(name) or theirs.get(name[:-6] if name.endswith("_total") else name)
+        assert tf is not None, name
+        assert tf.type == fam.type, (name, tf.type, fam.type)
+        got = {(s.name, tuple(sorted(s.labels.items()))): s.value for s in tf.samples}
+        for sname, lab, v in fam.samples:
+            key = (sname, tuple(sorted((k, str(x)) for k, x in lab.items())))
+            assert key in got, (name, key)
+            assert got[key] == v or (math.isnan(v) and math.isnan(got[key])), (key, got[key], v)
+    (comm,) = [s.labels["comm"] for s in theirs["amd_gpu_process_vram_bytes"].samples]
+    assert comm == 'we"ird\\comm'
