@@ -297,6 +297,44 @@ def test_process_discovery_under_workload(native):
         print("child:", out.strip())
 
 
+def test_two_pods_share_one_gpu(native):
+    """Two GEMM processes on one GPU (a shared GPU, no device-plugin owner): both appear
+    with their VRAM, and the GPU's gfx activity is split between them by occupied CUs —
+    the shares add up to the device activity on every tick."""
+    code = ("import sys; sys.path.insert(0, %r);"
+            "from kubernetes_gpu_exporter_amd.ops.gemm import gemm_burn;"
+            "print(gemm_burn(0, 4096, 5.0, 4), flush=True)" % ROOT)
+    kids = [subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                             text=True) for _ in range(2)]
+    e = amdsmi_engine(native, kfd_detail_interval_s=0.0)
+    try:
+        best: dict = {}
+        sums_ok = ticks = 0
+        deadline = time.time() + 4.5
+        while time.time() < deadline:
+            e.tick()
+            fams = promtext.parse(e.snapshot_text())
+            vram = {lab["pid"]: v for _, lab, v in promtext.samples(fams, "amd_gpu_process_vram_bytes")
+                    if v > 256 * (1 << 20)}
+            share = {lab["pid"]: v for _, lab, v in promtext.samples(fams, "amd_gpu_process_gfx_activity_percent")}
+            if len(vram) >= 2:
+                ticks += 1
+                act = promtext.value(fams, "amd_gpu_gfx_activity_percent", gpu=0)
+                if abs(sum(share.values()) - act) < 0.5:
+                    sums_ok += 1
+                for pid in vram:
+                    best[pid] = max(best.get(pid, 0.0), share.get(pid, 0.0))
+            time.sleep(0.2)
+        print("ticks with both:", ticks, "sum==activity:", sums_ok, "max share per pid:", best)
+        assert ticks >= 3, "the two GEMM processes were not both visible"
+        assert sums_ok == ticks
+        assert len([p for p, v in best.items() if v > 5]) >= 2, best
+    finally:
+        e.stop()
+        for k in kids:
+            print("child:", k.communicate(timeout=60)[0].strip()[-200:])
+
+
 def test_gemm_pod_model_on_gpu(native):
     """models.GemmPod runs the HIP kernel (not a torch fallback) and matches fp32."""
     import torch
