@@ -289,7 +289,8 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("max_conns", &HttpConfig::max_conns)
       .def_readwrite("idle_timeout_ms", &HttpConfig::idle_timeout_ms)
       .def_readwrite("enable_gzip", &HttpConfig::enable_gzip)
-      .def_readwrite("socket_sndbuf", &HttpConfig::socket_sndbuf);
+      .def_readwrite("socket_sndbuf", &HttpConfig::socket_sndbuf)
+      .def_readwrite("stale_after_ns", &HttpConfig::stale_after_ns);
 
   py::class_<EngineConfig>(m, "EngineConfig")
       .def(py::init<>())

@@ -226,6 +226,9 @@ void Engine::define_families() {
   // --- exporter self-metrics (own prefix; the reference registry had none, main.go:40) ---
   f_self_build_ = add("gpuexp_build_info", "Exporter build and backend", G, {"version", "backend"});
   f_self_ticks_ = add("gpuexp_ticks_total", "Sampler ticks completed", C, {});
+  f_self_last_ = add("gpuexp_last_sample_timestamp_seconds",
+                     "Unix time of the tick that produced this exposition (alert on time() - this: a stuck "
+                     "sampler keeps serving its last snapshot)", G, {});
   f_self_stage_ = add("gpuexp_sample_stage_duration_seconds", "Sampler stage duration", H, {"stage"});
   f_self_scrape_ = add("gpuexp_scrape_duration_seconds", "Server-side /metrics latency (request parsed -> last byte written)",
                        H, {});
@@ -827,6 +830,11 @@ void Engine::emit_self(uint64_t gen) {
     s = stats_;
   }
   table_.put(f_self_ticks_, {}, double(s.ticks), gen);
+  {
+    timespec rt;
+    clock_gettime(CLOCK_REALTIME, &rt);
+    table_.put(f_self_last_, {}, double(rt.tv_sec) + double(rt.tv_nsec) * 1e-9, gen);
+  }
   table_.put(f_self_overruns_, {}, double(s.overruns), gen);
   table_.put(f_self_render_bytes_, {}, double(s.render_bytes), gen);
   table_.put(f_self_series_, {}, double(s.series), gen);
@@ -1017,6 +1025,7 @@ void Engine::tick_locked(uint64_t now) {
       table_.render_proto(&snap->pb, gen);
       if (want_gz) gzip_compress(snap->pb, &snap->pb_gz, cfg_.gzip_level);
     }
+    snap->published_mono_ns = mono_ns();
     store_.publish(slot);
     if (http_) http_->set_ready(true);
   } else {

@@ -421,10 +421,18 @@ void HttpServer::run(Worker* w) {
       } else if (path == "/healthz") {
         respond_simple(c, 200, "OK", "text/plain", "ok\n", is_head);
       } else if (path == "/readyz") {
-        if (ready_.load())
-          respond_simple(c, 200, "OK", "text/plain", "ready\n", is_head);
-        else
+        uint64_t age_ns = 0;
+        if (cfg_.stale_after_ns) {
+          SnapshotStore::Pin pin = store_->acquire();
+          if (pin && pin->published_mono_ns && t0 > pin->published_mono_ns) age_ns = t0 - pin->published_mono_ns;
+        }
+        if (!ready_.load())
           respond_simple(c, 503, "Service Unavailable", "text/plain", "not ready\n", is_head);
+        else if (cfg_.stale_after_ns && age_ns > cfg_.stale_after_ns)
+          respond_simple(c, 503, "Service Unavailable", "text/plain",
+                         "stale: last sample " + std::to_string(age_ns / 1000000) + " ms ago\n", is_head);
+        else
+          respond_simple(c, 200, "OK", "text/plain", "ready\n", is_head);
       } else if (path == "/") {
         respond_simple(c, 200, "OK", "text/html",
                        "<html><head><title>MI355X GPU exporter</title></head><body>"

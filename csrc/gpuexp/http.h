@@ -31,6 +31,10 @@ struct HttpConfig {
   // peer's ACK and an EPOLLOUT wake-up — measured +25 us p50 for a 26 KB body on loopback.
   // The kernel clamps this to net.core.wmem_max.
   int socket_sndbuf = 4 << 20;
+  // /readyz answers 503 once the newest snapshot is older than this (a sampler stuck in a
+  // driver call, e.g. an SMU timeout during a GPU reset): Kubernetes then takes the pod
+  // out of the Service instead of Prometheus ingesting frozen values as current.  0 = off.
+  uint64_t stale_after_ns = 0;
 };
 
 // Fixed latency buckets (seconds) for gpuexp_scrape_duration_seconds.

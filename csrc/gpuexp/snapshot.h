@@ -22,6 +22,7 @@ struct Snapshot {
   uint64_t gen = 0;     // sampler generation that produced it
   uint64_t render_ns = 0;
   uint64_t series = 0;
+  uint64_t published_mono_ns = 0;  // CLOCK_MONOTONIC at publication (staleness checks)
 };
 
 class SnapshotStore {

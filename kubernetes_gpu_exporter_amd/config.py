@@ -23,6 +23,8 @@ class Config:
     path: str = "/metrics"                 # main.go:70
     http_threads: int = 1
     gzip: bool = True
+    stale_after: float = -1.0              # /readyz 503 when the newest sample is older (s); -1 = auto
+                                           # (max(5 s, 10 intervals)), 0 = never
     # sampling
     interval: float = 1.0                  # seconds; reference: 30 s (main.go:156)
     backend: str = "auto"                  # auto | amdsmi | sysfs | mock
@@ -97,6 +99,10 @@ class Config:
         hc.metrics_path = self.path
         hc.threads = int(self.http_threads)
         hc.enable_gzip = bool(self.gzip)
+        stale = float(self.stale_after)
+        if stale < 0:
+            stale = max(5.0, 10.0 * float(self.interval)) if float(self.interval) > 0 else 0.0
+        hc.stale_after_ns = int(stale * 1e9)
         ec.http = hc
         ec.series_profile = self.series_profile
         ec.ras_interval_s = float(self.ras_interval)

@@ -89,3 +89,14 @@ def test_cli_daemon_lifecycle(tmp_path):
     import json
     events = [e for e in json.loads(trace.read_text()) if e]
     assert {e["name"] for e in events} >= {"devices", "processes", "render"}
+
+
+def test_stale_after_defaults_follow_the_interval(native):
+    from kubernetes_gpu_exporter_amd.config import make_config
+    def ns(**kw):
+        return make_config(kw).to_engine_config(native).http.stale_after_ns
+    assert ns(interval=0.1) == 5_000_000_000      # at least 5 s
+    assert ns(interval=1.0) == 10_000_000_000     # 10 intervals
+    assert ns(interval=0) == 0                    # manual ticks: never stale
+    assert ns(interval=1.0, stale_after=2) == 2_000_000_000
+    assert ns(interval=1.0, stale_after=0) == 0

@@ -273,3 +273,38 @@ def test_listen_all_interfaces_is_dual_stack(native):
             s.close()
     finally:
         e.stop()
+
+
+def test_readyz_reports_a_stalled_sampler(native):
+    """A sampler stuck in a driver call keeps the last snapshot on /metrics (whose
+    gpuexp_last_sample_timestamp_seconds then ages) while /readyz turns 503 once the
+    snapshot is older than stale_after, and recovers with the next tick."""
+    c = native.EngineConfig()
+    c.backend = "mock"
+    c.interval_s = 0
+    c.http.host = "127.0.0.1"
+    c.http.port = 0
+    c.http.stale_after_ns = 300_000_000
+    e = native.Engine(c)
+    e.start()
+    try:
+        def get(path):
+            conn = http.client.HTTPConnection("127.0.0.1", e.http_port, timeout=5)
+            conn.request("GET", path)
+            r = conn.getresponse()
+            out = r.status, r.read().decode()
+            conn.close()
+            return out
+        assert get("/readyz")[0] == 503  # no sample yet
+        e.tick(1_000_000_000)
+        assert get("/readyz")[0] == 200
+        ts = promtext.value(promtext.parse(get("/metrics")[1]), "gpuexp_last_sample_timestamp_seconds")
+        assert abs(ts - time.time()) < 5
+        time.sleep(0.5)
+        st, body = get("/readyz")
+        assert st == 503 and body.startswith("stale: last sample"), body
+        assert get("/metrics")[0] == 200  # still served: last known values beat none
+        e.tick(2_000_000_000)
+        assert get("/readyz")[0] == 200
+    finally:
+        e.stop()
