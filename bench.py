@@ -425,6 +425,8 @@ def main() -> int:
         metrics_reads = {lab["kind"]: v for _, lab, v in promtext.samples(fams, "gpuexp_gpu_metrics_reads_total")
                          if lab.get("gpu") == "0"}
         sampler_cpu = [v for _, _, v in promtext.samples(fams, "gpuexp_sampler_cpu_seconds_total")]
+        prewake = [v for _, _, v in promtext.samples(fams, "gpuexp_http_prewake_wakeups_total")]
+        scrapes_total = [v for _, _, v in promtext.samples(fams, "gpuexp_scrapes_total")]
         rccl = {}
         for sname, lab, v in promtext.samples(fams, "amd_rccl_collective_bytes_total"):
             rccl.setdefault(lab.get("pod") or lab.get("pid"), {}).setdefault(lab["op"], {})["bytes"] = v
@@ -490,6 +492,8 @@ def main() -> int:
             "sample_stage_p50_le_us": stage_p50_us,
             "gpu_metrics_reads_gpu0": metrics_reads,
             "sampler_thread_cpu_s": sampler_cpu[0] if sampler_cpu else None,
+            "http_prewake_wakeups_per_scrape": round(prewake[0] / scrapes_total[0], 2)
+            if prewake and scrapes_total and scrapes_total[0] else None,
             "optional_sources": {"counters": bool(args.counters), "sentinel": bool(args.sentinel),
                                  "rccl_trace": bool(rccl_dir),
                                  "degraded_reason": degraded},

@@ -290,7 +290,11 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("idle_timeout_ms", &HttpConfig::idle_timeout_ms)
       .def_readwrite("enable_gzip", &HttpConfig::enable_gzip)
       .def_readwrite("socket_sndbuf", &HttpConfig::socket_sndbuf)
-      .def_readwrite("stale_after_ns", &HttpConfig::stale_after_ns);
+      .def_readwrite("stale_after_ns", &HttpConfig::stale_after_ns)
+      .def_readwrite("prewake", &HttpConfig::prewake)
+      .def_readwrite("prewake_lead_ns", &HttpConfig::prewake_lead_ns)
+      .def_readwrite("prewake_step_ns", &HttpConfig::prewake_step_ns)
+      .def_readwrite("prewake_window_ns", &HttpConfig::prewake_window_ns);
 
   py::class_<EngineConfig>(m, "EngineConfig")
       .def(py::init<>())
@@ -386,6 +390,7 @@ PYBIND11_MODULE(_gpuexp, m) {
           d["http_errors"] = hs->errors.load();
           d["http_open_conns"] = hs->open_conns.load();
           d["http_writev_calls"] = hs->writev_calls.load();
+          d["http_prewake_timer_wakeups"] = hs->prewake_timer_wakeups.load();
           d["http_writev_ns"] = hs->writev_ns.load();
           d["http_partial_writes"] = hs->partial_writes.load();
           d["http_scrape_ns"] = hs->lat_sum_ns.load();

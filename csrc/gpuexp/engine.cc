@@ -234,6 +234,8 @@ void Engine::define_families() {
                        H, {});
   f_self_scrapes_ = add("gpuexp_scrapes_total", "Scrapes of the metrics path", C, {});
   f_self_http_bytes_ = add("gpuexp_http_response_bytes_total", "HTTP response bytes written", C, {});
+  f_self_prewake_ = add("gpuexp_http_prewake_wakeups_total",
+                        "Timer wake-ups of the HTTP worker ahead of expected scrapes (scrape-phase pre-wake)", C, {});
   f_self_render_bytes_ = add("gpuexp_render_bytes", "Size of the last rendered exposition", G, {});
   f_self_series_ = add("gpuexp_series", "Series in the last rendered exposition", G, {});
   f_self_dev_errors_ = add("gpuexp_device_errors_total", "Failed telemetry reads per GPU", C, {"gpu"});
@@ -853,6 +855,8 @@ void Engine::emit_self(uint64_t gen) {
     table_.set_histogram(table_.upsert(f_self_scrape_, {}), scrape_latency_bounds(), counts, sum, cnt, gen);
     table_.put(f_self_scrapes_, {}, double(hs.metrics_requests.load(std::memory_order_relaxed)), gen);
     table_.put(f_self_http_bytes_, {}, double(hs.bytes_sent.load(std::memory_order_relaxed)), gen);
+    if (cfg_.http.prewake)
+      table_.put(f_self_prewake_, {}, double(hs.prewake_timer_wakeups.load(std::memory_order_relaxed)), gen);
   }
   if (!mock_)
     for (size_t i = 0; i < devices_.size(); ++i) {

@@ -6,6 +6,8 @@
 #include <netinet/tcp.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
+#include <sys/prctl.h>
+#include <sys/timerfd.h>
 #include <sys/socket.h>
 #include <sys/uio.h>
 #include <unistd.h>
@@ -53,6 +55,22 @@ struct Conn {
   bool is_metrics = false;
   uint64_t last_active_ns = 0;
   uint64_t req_start_ns = 0;
+  // arrival times of this connection's /metrics requests: the scrape period, learnt
+  uint64_t last_metrics_ns = 0;
+  uint64_t intervals[4] = {0, 0, 0, 0};
+  int n_intervals = 0, iv_pos = 0;
+  // Expected next /metrics arrival, or 0 when the last 4 periods are not steady.
+  uint64_t expected_next() const {
+    if (n_intervals < 4) return 0;
+    uint64_t lo = intervals[0], hi = intervals[0], sum = 0;
+    for (uint64_t v : intervals) {
+      lo = std::min(lo, v);
+      hi = std::max(hi, v);
+      sum += v;
+    }
+    if (lo < 20000000ull || hi > lo + lo / 8) return 0;  // < 20 ms or > 12% jitter
+    return last_metrics_ns + sum / 4;
+  }
 };
 
 bool ieq_prefix(const char* a, size_t alen, const char* b) {
@@ -109,6 +127,7 @@ struct HttpServer::Worker {
   int listen_fd = -1;
   int epfd = -1;
   int stopfd = -1;
+  int timerfd = -1;  // scrape pre-wake
   std::thread th;
   std::unordered_map<int, Conn> conns;
 };
@@ -199,6 +218,13 @@ bool HttpServer::start(std::string* err) {
     ::epoll_ctl(w->epfd, EPOLL_CTL_ADD, w->listen_fd, &ev);
     ev.data.fd = w->stopfd;
     ::epoll_ctl(w->epfd, EPOLL_CTL_ADD, w->stopfd, &ev);
+    if (cfg_.prewake) {
+      w->timerfd = ::timerfd_create(CLOCK_MONOTONIC, TFD_NONBLOCK | TFD_CLOEXEC);
+      if (w->timerfd >= 0) {
+        ev.data.fd = w->timerfd;
+        ::epoll_ctl(w->epfd, EPOLL_CTL_ADD, w->timerfd, &ev);
+      }
+    }
     workers_.push_back(std::move(w));
   }
   running_.store(true);
@@ -224,6 +250,7 @@ void HttpServer::stop() {
     if (w->listen_fd >= 0) ::close(w->listen_fd);
     if (w->epfd >= 0) ::close(w->epfd);
     if (w->stopfd >= 0) ::close(w->stopfd);
+    if (w->timerfd >= 0) ::close(w->timerfd);
   }
   workers_.clear();
   running_.store(false);
@@ -375,6 +402,12 @@ void HttpServer::run(Worker* w) {
         respond_simple(c, 405, "Method Not Allowed", "text/plain", "method not allowed\n", false);
       } else if (path == cfg_.metrics_path) {
         stats_.metrics_requests.fetch_add(1, std::memory_order_relaxed);
+        if (c.last_metrics_ns && t0 > c.last_metrics_ns) {
+          c.intervals[c.iv_pos] = t0 - c.last_metrics_ns;
+          c.iv_pos = (c.iv_pos + 1) & 3;
+          if (c.n_intervals < 4) ++c.n_intervals;
+        }
+        c.last_metrics_ns = t0;
         SnapshotStore::Pin pin = store_->acquire();
         if (!pin) {
           respond_simple(c, 503, "Service Unavailable", "text/plain", "no sample yet\n", is_head);
@@ -447,7 +480,29 @@ void HttpServer::run(Worker* w) {
     return true;
   };
 
+  if (w->timerfd >= 0) ::prctl(PR_SET_TIMERSLACK, 10000UL, 0, 0, 0);  // 10 us: pre-wake slices stay short
+  // Arms the pre-wake timer for the earliest expected scrape (see HttpConfig::prewake).
+  auto arm_prewake = [&]() {
+    if (w->timerfd < 0) return;
+    const uint64_t now = mono_ns();
+    uint64_t next = 0;
+    for (auto& kv : w->conns) {
+      const uint64_t e = kv.second.expected_next();
+      if (e && e + cfg_.prewake_window_ns > now && (!next || e < next)) next = e;
+    }
+    itimerspec its{};
+    if (next) {
+      // before the lead: one timer at (expected - lead); inside the window: short slices
+      const uint64_t at = now + cfg_.prewake_lead_ns < next ? next - cfg_.prewake_lead_ns
+                                                            : now + cfg_.prewake_step_ns;
+      its.it_value.tv_sec = time_t(at / 1000000000ull);
+      its.it_value.tv_nsec = long(at % 1000000000ull);
+    }
+    ::timerfd_settime(w->timerfd, TFD_TIMER_ABSTIME, &its, nullptr);  // zero disarms
+  };
+
   for (;;) {
+    arm_prewake();
     int n = ::epoll_wait(w->epfd, events, kMaxEvents, 1000);
     if (n < 0 && errno != EINTR) break;
     bool stopping = false;
@@ -455,6 +510,13 @@ void HttpServer::run(Worker* w) {
       int fd = events[i].data.fd;
       if (fd == w->stopfd) {
         stopping = true;
+        continue;
+      }
+      if (fd == w->timerfd) {
+        uint64_t expirations = 0;
+        ssize_t r = ::read(w->timerfd, &expirations, sizeof(expirations));
+        (void)r;
+        stats_.prewake_timer_wakeups.fetch_add(1, std::memory_order_relaxed);
         continue;
       }
       if (fd == w->listen_fd) {

@@ -35,6 +35,17 @@ struct HttpConfig {
   // driver call, e.g. an SMU timeout during a GPU reset): Kubernetes then takes the pod
   // out of the Service instead of Prometheus ingesting frozen values as current.  0 = off.
   uint64_t stale_after_ns = 0;
+  // Scrape-phase pre-wake.  Prometheus scrapes a target at a fixed interval, so once a
+  // connection's /metrics requests arrive at a steady period (>= 20 ms), the worker arms a
+  // timer for prewake_lead_ns before the next expected request and then sleeps in
+  // prewake_step_ns slices until it arrives (at most prewake_window_ns past the expected
+  // time).  Short sleeps keep the worker's core in a shallow idle state, so the request
+  // does not pay a deep-idle exit on the critical path: a few timer wake-ups per scrape
+  // instead of one long sleep, no spinning.
+  bool prewake = true;
+  uint64_t prewake_lead_ns = 400000;
+  uint64_t prewake_step_ns = 150000;
+  uint64_t prewake_window_ns = 3000000;
 };
 
 // Fixed latency buckets (seconds) for gpuexp_scrape_duration_seconds.
@@ -55,6 +66,7 @@ struct HttpStats {
   std::atomic<uint64_t> writev_calls{0};
   std::atomic<uint64_t> writev_ns{0};
   std::atomic<uint64_t> partial_writes{0};
+  std::atomic<uint64_t> prewake_timer_wakeups{0};  // timer expiries of the scrape pre-wake
   std::atomic<uint64_t> lat_buckets[kBuckets + 1]{};  // +Inf last, non-cumulative
   std::atomic<uint64_t> lat_sum_ns{0};
   std::atomic<uint64_t> lat_count{0};

@@ -23,6 +23,7 @@ class Config:
     path: str = "/metrics"                 # main.go:70
     http_threads: int = 1
     gzip: bool = True
+    http_prewake: bool = True              # wake shortly before a steady scraper's next request
     stale_after: float = -1.0              # /readyz 503 when the newest sample is older (s); -1 = auto
                                            # (max(5 s, 10 intervals)), 0 = never
     # sampling
@@ -99,6 +100,7 @@ class Config:
         hc.metrics_path = self.path
         hc.threads = int(self.http_threads)
         hc.enable_gzip = bool(self.gzip)
+        hc.prewake = bool(self.http_prewake)
         stale = float(self.stale_after)
         if stale < 0:
             stale = max(5.0, 10.0 * float(self.interval)) if float(self.interval) > 0 else 0.0

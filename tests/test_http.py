@@ -308,3 +308,37 @@ def test_readyz_reports_a_stalled_sampler(native):
         assert get("/readyz")[0] == 200
     finally:
         e.stop()
+
+
+def test_scrape_prewake_learns_a_steady_period(native):
+    """A scraper with a steady period (here 30 ms) is learnt after 4 intervals: the worker
+    then wakes on a timer just ahead of each expected request (short sleeps keep its core
+    out of deep idle) — a few timer wake-ups per scrape, none once scraping stops, and none
+    with prewake off."""
+    def run(prewake: bool):
+        c = native.EngineConfig()
+        c.backend = "mock"
+        c.interval_s = 0
+        c.http.host = "127.0.0.1"
+        c.http.port = 0
+        c.http.prewake = prewake
+        e = native.Engine(c)
+        e.start()
+        try:
+            e.tick(1_000_000_000)
+            cl = native.ScrapeClient("127.0.0.1", e.http_port, "/metrics")
+            t = time.monotonic()
+            for _ in range(14):
+                t += 0.030
+                time.sleep(max(0.0, t - time.monotonic()))
+                assert cl.scrape() > 0
+            woke = e.stats()["http_prewake_timer_wakeups"]
+            time.sleep(0.2)  # scraper gone: the window closes, the timer stays disarmed
+            later = e.stats()["http_prewake_timer_wakeups"]
+            return woke, later
+        finally:
+            e.stop()
+    woke, later = run(True)
+    assert 4 <= woke <= 14 * 12, woke   # armed from the 5th scrape on; bounded per scrape
+    assert later - woke <= 25           # at most one window's worth after the last scrape
+    assert run(False) == (0, 0)
