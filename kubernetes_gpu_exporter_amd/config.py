@@ -74,6 +74,13 @@ class Config:
         host, _, port = self.listen.rpartition(":")
         if host.startswith("[") and host.endswith("]"):
             host = host[1:-1]
+        if host and ":" not in host and not host.replace(".", "").isdigit():
+            import socket
+            try:  # a host name: the engine binds IP literals
+                fam, _, _, _, addr = socket.getaddrinfo(host, None, proto=socket.IPPROTO_TCP)[0]
+                host = addr[0]
+            except OSError:
+                pass  # left as is; validate() reports it
         return host, int(port)
 
     def resolved_backend(self) -> str:
@@ -243,3 +250,16 @@ def validate(cfg: Config) -> None:
         raise ValueError("mock_devices must be >= 1")
     if cfg.log_level not in ("debug", "info", "warn", "error", "off"):
         raise ValueError("log_level must be debug|info|warn|error|off")
+    if cfg.stale_after < 0 and cfg.stale_after != -1:
+        raise ValueError("stale_after must be -1 (auto), 0 (never) or > 0 seconds")
+    host, _ = cfg.listen_host_port()
+    if host and ":" not in host:
+        import ipaddress
+        try:
+            ipaddress.IPv4Address(host)
+        except ValueError:
+            try:  # a name, as Go's net.Listen accepts: resolved once, here
+                import socket
+                socket.getaddrinfo(host, None)
+            except OSError:
+                raise ValueError(f"listen host {host!r} is neither an IP address nor a resolvable name")

@@ -100,3 +100,13 @@ def test_stale_after_defaults_follow_the_interval(native):
     assert ns(interval=0) == 0                    # manual ticks: never stale
     assert ns(interval=1.0, stale_after=2) == 2_000_000_000
     assert ns(interval=1.0, stale_after=0) == 0
+
+
+def test_listen_and_stale_after_validation():
+    from kubernetes_gpu_exporter_amd.config import make_config
+    assert make_config({"listen": "[::1]:9000"}).listen_host_port() == ("::1", 9000)
+    assert make_config({"listen": "127.0.0.1:9000"}).listen_host_port() == ("127.0.0.1", 9000)
+    assert make_config({"listen": "localhost:9000"}).listen_host_port()[0] in ("127.0.0.1", "::1")
+    for bad in ({"listen": "no-such-host.invalid:9000"}, {"stale_after": -5}):
+        with pytest.raises(ValueError):
+            make_config(bad)
