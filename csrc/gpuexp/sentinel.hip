@@ -60,6 +60,14 @@ constexpr int kChaseHops = 16;
 constexpr size_t kChaseStride = 4096 / sizeof(uint32_t);
 
 // ring[run_slot * kSentinelMaxWaves + blockIdx.x]
+// Writes the pointer-chase links in place (one lane per hop): initialising the chain with a
+// kernel on the sentinel's stream instead of a copy keeps ROCr's blit/copy queues (each with
+// its own ~173 MiB context save area on MI355X) from being created at all.
+__global__ void __launch_bounds__(64) sentinel_init_chase(uint32_t* __restrict__ chase, int hops) {
+  const int h = int(threadIdx.x);
+  if (h < hops) chase[size_t(h) * kChaseStride] = uint32_t((h + 1) % hops);
+}
+
 __global__ void __launch_bounds__(64) sentinel_kernel(SentinelSlot* __restrict__ ring, uint32_t slot,
                                                       uint64_t seq, int spin, const uint32_t* chase, int hops) {
   if (threadIdx.x != 0) return;
@@ -204,9 +212,14 @@ class HipSentinel : public SentinelSource {
       void* chase = nullptr;
       const size_t chase_words = size_t(kChaseHops) * kChaseStride;
       if (hipExtMallocWithFlags(&chase, chase_words * sizeof(uint32_t), hipDeviceMallocUncached) == hipSuccess) {
-        std::vector<uint32_t> links(chase_words, 0);
-        for (int h = 0; h < kChaseHops; ++h) links[size_t(h) * kChaseStride] = uint32_t((h + 1) % kChaseHops);
-        if (hipMemcpy(chase, links.data(), chase_words * sizeof(uint32_t), hipMemcpyHostToDevice) == hipSuccess) {
+        // Initialised by a kernel on the sentinel's own stream, not by a copy: every hardware
+        // queue the runtime creates (the stream's, the null stream's, the blit queues behind
+        // hipMemcpy) costs a context save/restore area in GTT sized for the whole GPU
+        // (~173 MiB on MI355X, KFD cwsr_size x XCCs; tools/probe_queue_rss.py).
+        static_assert(kChaseHops <= 64, "one lane per hop");
+        hipLaunchKernelGGL(sentinel_init_chase, dim3(1), dim3(64), 0, p.stream, static_cast<uint32_t*>(chase),
+                           kChaseHops);
+        if (hipGetLastError() == hipSuccess && hipStreamSynchronize(p.stream) == hipSuccess) {
           p.chase = static_cast<uint32_t*>(chase);
           p.hops = kChaseHops;
         } else {
