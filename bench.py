@@ -310,6 +310,7 @@ def main() -> int:
         return time.perf_counter(), tot
 
     xgmi_window: dict = {}
+    exporter_rss_kb = [0]
 
     def phase(proc, cl, native_exporter: bool = False):
         """W untimed + K timed steps (barrier + synchronize on both sides); returns the
@@ -333,6 +334,12 @@ def main() -> int:
         sync()
         elapsed = time.perf_counter() - t0
         cpu_pct = 100.0 * (cpu_seconds_precise(proc.pid) - cpu0) / elapsed if rank == 0 else 0.0
+        if rank == 0 and native_exporter:
+            try:  # resident memory of the exporter: each GPU queue it holds pins a CWSR area
+                exporter_rss_kb[0] = int([l for l in open(f"/proc/{proc.pid}/status")
+                                          if l.startswith("VmRSS:")][0].split()[1])
+            except (OSError, IndexError, ValueError):
+                pass
         if x0 is not None:
             # xGMI bytes the hardware counted over the window vs what the DP all-reduce must
             # move: 2(N-1)/N x buffer per GPU per step for any bandwidth-optimal algorithm
@@ -462,6 +469,7 @@ def main() -> int:
             "p99_scrape_us": round(pct(lat, 0.99), 2) if lat else None,
             "max_scrape_us": round(max(lat), 2) if lat else None,
             "exporter_cpu_percent": round(cpu_pct, 3),
+            "exporter_rss_mb": round(exporter_rss_kb[0] / 1024, 1) if exporter_rss_kb[0] else None,
             "scrape_encoding": "gzip (Prometheus default Accept-Encoding)" if args.gzip else "identity",
             "p50_scrape_identity_us": round(statistics.median(lat_id), 2) if lat_id else None,
             "p99_scrape_identity_us": round(pct(lat_id, 0.99), 2) if lat_id else None,
