@@ -36,6 +36,7 @@ CORE_CC = [
     "gpuexp/optional_sources.cc", "gpuexp/client.cc", "bindings.cc",
 ]
 SENTINEL_HIP = ["gpuexp/sentinel.hip"]
+SENTINEL_HSACO = "gpuexp/sentinel_hsaco.hip"  # device-only code object for raw AQL dispatch
 KERNELS_HIP = ["kernels/gemm_bf16.hip", "kernels/kernels_bindings.hip"]
 ROCPROF_CC = ["gpuexp/rocprof_plugin.cc"]
 AQLPMC_CC = ["gpuexp/aql_pmc.cc"]
@@ -117,6 +118,18 @@ def link_hip(objs: list[Path], out: Path, libs: list[str]) -> Path:
     return out
 
 
+def build_hsaco(src: str, out: Path, hdr_mtime: float, force: bool) -> Path:
+    """A plain gfx950 code object (no host code, no offload bundle) for hsa_executable loading."""
+    s = CSRC / src
+    if not _needs(out, s, hdr_mtime, force):
+        return out
+    tmp = out.with_suffix(".tmp.hsaco")
+    _run([str(ROCM / "bin" / "hipcc"), f"--offload-arch={ARCH}", "--cuda-device-only", "--no-gpu-bundle-output",
+          "-O3", "-std=c++17", f"-I{CSRC}", "-o", str(tmp), str(s)])
+    os.replace(tmp, out)
+    return out
+
+
 def link_plain(objs: list[Path], out: Path, libs: list[str]) -> Path:
     tmp = out.with_suffix(".tmp.so")
     _run(["g++", "-shared", "-fPIC", "-o", str(tmp)] + [str(o) for o in objs] +
@@ -145,6 +158,7 @@ def build(force: bool = False, jobs: int = 8, sanitize: str | None = None, verbo
     if (CSRC / AQLPMC_CC[0]).exists():
         outputs["aqlpmc_plugin"] = str(link_plain([objs[AQLPMC_CC[0]]], PKG / "_gpuexp_aqlpmc.so",
                                                   ["-lhsa-runtime64", "-lpthread"]))
+        outputs["sentinel_hsaco"] = str(build_hsaco(SENTINEL_HSACO, PKG / "gpuexp_sentinel.hsaco", hdr, force))
     if (CSRC / TRACER_CC[0]).exists():
         outputs["rccl_tracer"] = str(link_plain([objs[TRACER_CC[0]]], PKG / "libgpuexp_rccl_tracer.so",
                                                 ["-lrocprofiler-sdk", "-lpthread"]))

@@ -316,6 +316,7 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("kfd_detail_interval_s", &EngineConfig::kfd_detail_interval_s)
       .def_readwrite("exclude_self", &EngineConfig::exclude_self)
       .def_readwrite("enable_sentinel", &EngineConfig::enable_sentinel)
+      .def_readwrite("sentinel_impl", &EngineConfig::sentinel_impl)
       .def_readwrite("sentinel_ring", &EngineConfig::sentinel_ring)
       .def_readwrite("sentinel_spin", &EngineConfig::sentinel_spin)
       .def_readwrite("enable_counters", &EngineConfig::enable_counters)

@@ -6,7 +6,7 @@
 // header; measured 101% exporter CPU).  The counting itself is only three PM4 programs —
 // select+reset+enable, and read+disable — which libhsa-amd-aqlprofile64 generates as AQL
 // vendor packets (hsa_ven_amd_aqlprofile.h).  Here each GPU gets:
-//   * one low-priority AQL queue of 64 slots (nothing else is ever submitted to it),
+//   * one low-priority AQL queue of 64 slots (shared with the sentinel, see below),
 //   * one interrupt-backed completion signal (waited on BLOCKED — no polling thread),
 //   * a command buffer and a PMC output buffer in fine-grained system memory,
 // and a background thread duty-cycles a counting window per interval:
@@ -38,7 +38,13 @@
 #include <thread>
 #include <vector>
 
+#include <dlfcn.h>
+#include <fcntl.h>
+#include <unistd.h>
+
 #include "gpuexp/counter_model.h"
+#include "gpuexp/sentinel_common.h"
+#include "gpuexp/sources.h"
 
 namespace {
 
@@ -77,6 +83,9 @@ struct Agent {
   bool ready = false;
   bool broken = false;      // a packet timed out: the GPU may still own the buffers
   std::atomic<bool> queue_error{false};
+  // The queue has two producers: the counting thread (PM4 programs) and the sampler
+  // thread (sentinel kernel dispatches, gpuexp_make_hsa_sentinel).
+  std::mutex submit_mu;
   double last_raw[kNumCtr] = {};
   int last_inst[kNumCtr] = {};
   uint64_t last_samples = 0;
@@ -175,9 +184,10 @@ void* sys_alloc(size_t bytes, hsa_agent_t gpu) {
   return p;
 }
 
-// Writes one vendor-specific AQL packet and rings the doorbell.  Only this plugin's thread
-// submits to the queue, and at most one packet is in flight, so the ring never fills.
+// Writes one vendor-specific AQL packet and rings the doorbell.  At most one PM4 packet and
+// four sentinel dispatches are ever in flight on the 64-slot queue, so it never fills.
 void submit(Agent& a, const hsa_ext_amd_aql_pm4_packet_t& pkt) {
+  std::lock_guard<std::mutex> lk(a.submit_mu);
   hsa_queue_t* q = a.queue;
   const uint64_t idx = hsa_queue_add_write_index_screlease(q, 1);
   auto* slot = static_cast<hsa_ext_amd_aql_pm4_packet_t*>(q->base_address) + (idx & (q->size - 1));
@@ -306,7 +316,7 @@ bool setup_agent(Agent& a, std::string* why) {
     return false;
   }
   a.out_size = out_size;
-  if (hsa_queue_create(a.gpu, 64, HSA_QUEUE_TYPE_SINGLE, queue_error_cb, &a, UINT32_MAX, UINT32_MAX, &a.queue) !=
+  if (hsa_queue_create(a.gpu, 64, HSA_QUEUE_TYPE_MULTI, queue_error_cb, &a, UINT32_MAX, UINT32_MAX, &a.queue) !=
       HSA_STATUS_SUCCESS) {
     *why = "hsa_queue_create failed";
     return false;
@@ -393,6 +403,246 @@ void teardown_locked() {
   g_hsa_up = false;
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Sentinel on the counters' queue.  Every GPU queue pins a context save/restore area sized
+// for the whole GPU (~173 MiB on MI355X), so instead of the HIP plugin's own stream the
+// sentinel kernel (gpuexp_sentinel.hsaco, same device code: sentinel_device.h) is
+// dispatched here as raw AQL packets on the queue the PMC programs already use.
+// ---------------------------------------------------------------------------------------
+struct KernelSym {
+  uint64_t object = 0;
+  uint32_t kernarg = 0, group = 0, priv = 0;
+};
+
+std::string plugin_dir() {
+  Dl_info info{};
+  if (::dladdr(reinterpret_cast<void*>(&plugin_dir), &info) && info.dli_fname) {
+    std::string p(info.dli_fname);
+    const size_t sl = p.rfind('/');
+    return sl == std::string::npos ? std::string(".") : p.substr(0, sl);
+  }
+  return ".";
+}
+
+bool lookup(hsa_executable_t exe, hsa_agent_t gpu, const char* name, KernelSym* k) {
+  hsa_executable_symbol_t sym{};
+  if (hsa_executable_get_symbol_by_name(exe, name, &gpu, &sym) != HSA_STATUS_SUCCESS) return false;
+  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &k->object);
+  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &k->kernarg);
+  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &k->group);
+  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &k->priv);
+  return k->object != 0;
+}
+
+hsa_status_t pick_uncached_pool(hsa_amd_memory_pool_t pool, void* data) {
+  hsa_amd_segment_t seg{};
+  hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
+  uint32_t flags = 0;
+  hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+  bool alloc = false;
+  hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc);
+  if (seg == HSA_AMD_SEGMENT_GLOBAL && alloc && (flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED)) {
+    *static_cast<hsa_amd_memory_pool_t*>(data) = pool;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+// One kernel dispatch packet (1-D grid of `groups` x 64 lanes) on the agent's queue.
+void dispatch(Agent& a, const KernelSym& k, void* kernarg, uint32_t groups, hsa_signal_t done) {
+  std::lock_guard<std::mutex> lk(a.submit_mu);
+  hsa_queue_t* q = a.queue;
+  const uint64_t idx = hsa_queue_add_write_index_screlease(q, 1);
+  auto* pkt = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address) + (idx & (q->size - 1));
+  pkt->workgroup_size_x = 64;
+  pkt->workgroup_size_y = 1;
+  pkt->workgroup_size_z = 1;
+  pkt->grid_size_x = groups * 64;
+  pkt->grid_size_y = 1;
+  pkt->grid_size_z = 1;
+  pkt->private_segment_size = k.priv;
+  pkt->group_segment_size = k.group;
+  pkt->kernel_object = k.object;
+  pkt->kernarg_address = kernarg;
+  pkt->completion_signal = done;
+  pkt->reserved0 = 0;
+  pkt->reserved2 = 0;  // the slot may have held a PM4 packet with another layout
+  const uint16_t header = uint16_t((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                                   (1 << HSA_PACKET_HEADER_BARRIER) |
+                                   (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                                   (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+  const uint16_t setup = uint16_t(1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS);
+  __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), uint32_t(header) | (uint32_t(setup) << 16), __ATOMIC_RELEASE);
+  hsa_signal_store_screlease(q->doorbell_signal, hsa_signal_value_t(idx));
+}
+
+class QueueSentinel : public gpuexp::SentinelSource {
+  struct Per {
+    Agent* a = nullptr;
+    bool ready = false;
+    hsa_executable_t exe{};
+    bool have_exe = false;
+    KernelSym run_k, init_k;
+    char* kernargs = nullptr;  // one 64-byte slot per ring slot
+    uint32_t* chase = nullptr;
+    int hops = 0;
+    gpuexp::SentinelRun run;
+  };
+
+ public:
+  QueueSentinel(int ring, int spin) : nslots_(ring < 4 ? 4 : ring), spin_(spin < 16 ? 16 : spin) {}
+  ~QueueSentinel() override { stop(); }
+
+  bool start(const std::vector<gpuexp::DeviceInfo>& devs, std::string* err) override {
+    const std::string path = plugin_dir() + "/gpuexp_sentinel.hsaco";
+    uint64_t freq = 0;
+    hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &freq);
+    sys_ns_per_tick_ = freq ? 1e9 / double(freq) : 1.0;
+    std::vector<Agent*> agents;
+    {
+      std::lock_guard<std::mutex> lk(g_mu);
+      agents = g_agents;
+    }
+    per_.resize(devs.size());
+    int ok = 0, waves = 0;
+    std::string why = "no GPU has a working PMC queue";
+    for (size_t i = 0; i < devs.size() && i < agents.size(); ++i) {
+      Agent* a = agents[i];
+      if (!a || !a->ready || a->broken) continue;
+      Per& p = per_[i];
+      p.a = a;
+      if (!setup(p, path, int(devs[i].num_xcc), &why)) {
+        release(p);
+        continue;
+      }
+      p.ready = true;
+      ++ok;
+      waves += p.run.waves;
+    }
+    if (!ok) {
+      *err = why;
+      return false;
+    }
+    status_ = "hsa sentinel on " + std::to_string(ok) + " GPU(s) (on the PMC queue: one GPU queue per GPU), " +
+              std::to_string(waves) + " waves/tick (one per XCD), ring " + std::to_string(nslots_);
+    return true;
+  }
+
+  void tick(uint64_t) override {
+    for (Per& p : per_) {
+      if (!p.ready || p.a->broken || p.a->queue_error.load()) continue;
+      gpuexp::sentinel_drain(p.run, nslots_, sys_ns_per_tick_);
+      if (p.run.launched - p.run.completed >= 4) {  // a saturated queue shows as latency
+        p.run.stalled += 1;
+        continue;
+      }
+      const uint64_t seq = p.run.launched + 1;
+      const uint32_t slot = gpuexp::sentinel_prepare(p.run, seq, nslots_);
+      gpuexp::SentinelArgs args{p.run.ring, p.chase, seq, slot, spin_, p.hops, 0};
+      char* ka = p.kernargs + size_t(slot) * 64;
+      std::memcpy(ka, &args, sizeof(args));
+      dispatch(*p.a, p.run_k, ka, uint32_t(p.run.waves), hsa_signal_t{0});
+      p.run.launched = seq;
+    }
+  }
+
+  bool read(int dev, gpuexp::SentinelReading* out) override {
+    if (dev < 0 || size_t(dev) >= per_.size() || !per_[size_t(dev)].ready) return false;
+    return gpuexp::sentinel_fill(per_[size_t(dev)].run, out);
+  }
+
+  void stop() override {
+    for (Per& p : per_) {
+      if (p.ready) {
+        // a run is microseconds long: wait (bounded) for the in-flight ones before freeing
+        for (int i = 0; i < 200 && p.run.completed < p.run.launched; ++i) {
+          gpuexp::sentinel_drain(p.run, nslots_, sys_ns_per_tick_);
+          if (p.run.completed < p.run.launched) ::usleep(500);
+        }
+        if (p.run.completed < p.run.launched) continue;  // GPU may still write: leak, do not free
+      }
+      release(p);
+    }
+    per_.clear();
+  }
+
+  std::string status() const override { return status_; }
+
+ private:
+  bool setup(Per& p, const std::string& path, int num_xcc, std::string* why) {
+    Agent& a = *p.a;
+    const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) {
+      *why = "cannot open " + path;
+      return false;
+    }
+    hsa_code_object_reader_t reader{};
+    bool ok = hsa_code_object_reader_create_from_file(fd, &reader) == HSA_STATUS_SUCCESS;
+    if (ok) {
+      ok = hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &p.exe) ==
+           HSA_STATUS_SUCCESS;
+      p.have_exe = ok;
+      ok = ok && hsa_executable_load_agent_code_object(p.exe, a.gpu, reader, nullptr, nullptr) == HSA_STATUS_SUCCESS;
+      ok = ok && hsa_executable_freeze(p.exe, nullptr) == HSA_STATUS_SUCCESS;
+      hsa_code_object_reader_destroy(reader);
+    }
+    ::close(fd);
+    if (!ok || !lookup(p.exe, a.gpu, "gpuexp_sentinel.kd", &p.run_k) ||
+        !lookup(p.exe, a.gpu, "gpuexp_sentinel_init_chase.kd", &p.init_k) ||
+        p.run_k.kernarg > 64 || p.init_k.kernarg > 64) {
+      *why = "cannot load the sentinel code object " + path;
+      return false;
+    }
+    p.run.waves = num_xcc > 0 ? std::min(num_xcc, gpuexp::kSentinelMaxWaves) : gpuexp::kSentinelMaxWaves;
+    p.run.ring = static_cast<gpuexp::SentinelSlot*>(
+        sys_alloc(sizeof(gpuexp::SentinelSlot) * size_t(nslots_) * gpuexp::kSentinelMaxWaves, a.gpu));
+    p.kernargs = static_cast<char*>(sys_alloc(size_t(nslots_ + 1) * 64, a.gpu));
+    if (!p.run.ring || !p.kernargs) {
+      *why = "sentinel ring allocation failed";
+      return false;
+    }
+    p.run.host_launch.assign(size_t(nslots_), 0);
+    p.run.agent = a.gpu;
+    p.run.have_agent = true;
+    // HBM latency chain in uncached device memory, written by a kernel (no copy queue)
+    hsa_amd_memory_pool_t pool{};
+    hsa_amd_agent_iterate_memory_pools(a.gpu, pick_uncached_pool, &pool);
+    void* chase = nullptr;
+    const size_t bytes = size_t(gpuexp::kChaseHops) * gpuexp::kChaseStride * sizeof(uint32_t);
+    if (pool.handle &&
+        hsa_amd_memory_pool_allocate(pool, bytes, HSA_AMD_MEMORY_POOL_UNCACHED_FLAG, &chase) == HSA_STATUS_SUCCESS) {
+      hsa_signal_t done{};
+      if (hsa_signal_create(1, 0, nullptr, &done) == HSA_STATUS_SUCCESS) {
+        gpuexp::SentinelInitArgs ia{static_cast<uint32_t*>(chase), gpuexp::kChaseHops, 0};
+        char* ka = p.kernargs + size_t(nslots_) * 64;  // the spare slot
+        std::memcpy(ka, &ia, sizeof(ia));
+        dispatch(a, p.init_k, ka, 1, done);
+        if (hsa_signal_wait_scacquire(done, HSA_SIGNAL_CONDITION_LT, 1, g_ts_freq, HSA_WAIT_STATE_BLOCKED) < 1) {
+          p.chase = static_cast<uint32_t*>(chase);
+          p.hops = gpuexp::kChaseHops;
+        }
+        hsa_signal_destroy(done);
+      }
+      if (!p.chase) hsa_amd_memory_pool_free(chase);
+    }
+    return true;
+  }
+
+  void release(Per& p) {
+    if (p.chase) hsa_amd_memory_pool_free(p.chase);
+    if (p.kernargs) hsa_amd_memory_pool_free(p.kernargs);
+    if (p.run.ring) hsa_amd_memory_pool_free(p.run.ring);
+    if (p.have_exe) hsa_executable_destroy(p.exe);
+    p = Per();
+  }
+
+  int nslots_;
+  int spin_;
+  double sys_ns_per_tick_ = 1.0;
+  std::vector<Per> per_;
+  std::string status_ = "not started";
+};
 }  // namespace
 
 extern "C" __attribute__((visibility("default"))) void gpuexp_rp_set_duty(int window_ms, int interval_ms) {
@@ -506,4 +756,11 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_debug(int dev, c
   }
   std::snprintf(buf, size_t(len), "%s", s.c_str());
   return 0;
+}
+
+// The sentinel on this plugin's PMC queues (see QueueSentinel); the engine asks for it after
+// gpuexp_rp_init succeeded, and falls back to the HIP plugin's own stream otherwise.
+extern "C" __attribute__((visibility("default"))) gpuexp::SentinelSource* gpuexp_make_hsa_sentinel(int ring_slots,
+                                                                                                   int spin_iters) {
+  return new QueueSentinel(ring_slots, spin_iters);
 }

@@ -326,9 +326,22 @@ bool Engine::start(std::string* err) {
     counters_status_ = "mock";
   }
   if (cfg_.enable_sentinel && cfg_.backend != "mock") {
-    sentinel_ = make_hip_sentinel(cfg_.sentinel_ring, cfg_.sentinel_spin);
-    std::string e = "libgpuexp_hip.so not loadable";
-    if (!sentinel_ || !sentinel_->start(devices_, &e)) {
+    std::string e;
+    // Prefer the counters plugin's queue (one GPU queue, and its ~173 MiB context save
+    // area, per GPU instead of two); the HIP plugin's own stream otherwise.
+    if (cfg_.sentinel_impl != "hip" && counters_) {
+      sentinel_ = make_queue_sentinel(cfg_.counters_plugin, cfg_.sentinel_ring, cfg_.sentinel_spin);
+      if (sentinel_ && !sentinel_->start(devices_, &e)) {
+        GPUEXP_LOG(LogLevel::kInfo, "sentinel", "queue sentinel unavailable (" + e + "), using HIP");
+        sentinel_.reset();
+      }
+    }
+    if (!sentinel_ && cfg_.sentinel_impl != "queue") {
+      sentinel_ = make_hip_sentinel(cfg_.sentinel_ring, cfg_.sentinel_spin);
+      e = "libgpuexp_hip.so not loadable";
+      if (sentinel_ && !sentinel_->start(devices_, &e)) sentinel_.reset();
+    }
+    if (!sentinel_) {
       sentinel_status_ = "unavailable: " + e;
       GPUEXP_LOG(LogLevel::kWarn, "sentinel", sentinel_status_);
       sentinel_.reset();

@@ -73,6 +73,7 @@ struct EngineConfig {
   double kfd_detail_interval_s = 1.0;  // cu_occupancy / sdma re-read period (0 = every tick)
   bool exclude_self = true;
   bool enable_sentinel = false;
+  std::string sentinel_impl = "auto";  // auto (PMC queue if the aqlprofile counters run, else HIP) | hip | queue
   int sentinel_ring = 64;
   int sentinel_spin = 500;  // ~15 us window (rocprofv3: spin 2000 ran 61 us/launch)
   bool enable_counters = false;

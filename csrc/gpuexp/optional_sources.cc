@@ -234,6 +234,18 @@ std::unique_ptr<SentinelSource> make_hip_sentinel(int ring_slots, int spin_iters
   return std::unique_ptr<SentinelSource>(f(ring_slots, spin_iters));
 }
 
+std::unique_ptr<SentinelSource> make_queue_sentinel(const std::string& counters_plugin, int ring_slots,
+                                                   int spin_iters) {
+  // Only from a counters plugin that is already loaded and running (RTLD_NOLOAD).
+  void* h = ::dlopen(counters_plugin.c_str(), RTLD_NOW | RTLD_LOCAL | RTLD_NOLOAD);
+  if (!h) return nullptr;
+  using factory_t = SentinelSource* (*)(int, int);
+  auto f = reinterpret_cast<factory_t>(::dlsym(h, "gpuexp_make_hsa_sentinel"));
+  ::dlclose(h);  // drops only the NOLOAD reference; the counters source keeps it loaded
+  if (!f) return nullptr;
+  return std::unique_ptr<SentinelSource>(f(ring_slots, spin_iters));
+}
+
 // Default counter backend: the aqlprofile plugin (no spinning runtime thread); the
 // rocprofiler-sdk plugin (_gpuexp_rocprof.so) is selectable through counters_plugin.
 std::string default_rocprof_plugin() { return self_dir() + "/_gpuexp_aqlpmc.so"; }

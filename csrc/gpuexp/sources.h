@@ -25,6 +25,10 @@ class SentinelSource {
 // Implemented in sentinel.hip (1 wave, lowest-priority stream, pinned host ring), built
 // as libgpuexp_hip.so and dlopen()ed from beside the core module; nullptr if unavailable.
 std::unique_ptr<SentinelSource> make_hip_sentinel(int ring_slots, int spin_iters);
+// The same sentinel kernel dispatched as raw AQL on the aqlprofile counters plugin's own
+// HSA queue (one GPU queue for both); nullptr unless that plugin is loaded and exports it.
+std::unique_ptr<SentinelSource> make_queue_sentinel(const std::string& counters_plugin, int ring_slots,
+                                                   int spin_iters);
 std::string default_rocprof_plugin();
 
 class CounterSource {

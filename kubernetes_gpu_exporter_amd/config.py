@@ -44,6 +44,7 @@ class Config:
     # optional sources
     enable_sentinel: bool = False
     sentinel_spin: int = 500
+    sentinel_impl: str = "auto"            # auto (on the PMC counters' queue when they run, else HIP) | hip | queue
     enable_counters: bool = False
     counters_plugin: str = "aqlpmc"        # aqlpmc | rocprof | /path/to/plugin.so
     counters_window_ms: int = 20           # rocprofiler counting window ...
@@ -123,6 +124,7 @@ class Config:
         ec.kfd_detail_interval_s = float(self.kfd_detail_interval)
         ec.enable_sentinel = bool(self.enable_sentinel)
         ec.sentinel_spin = int(self.sentinel_spin)
+        ec.sentinel_impl = str(self.sentinel_impl)
         ec.enable_counters = bool(self.enable_counters)
         if self.counters_plugin in ("", "aqlpmc", "rocprof"):
             from ._native import rocprof_plugin_path
@@ -250,6 +252,8 @@ def validate(cfg: Config) -> None:
         raise ValueError("mock_devices must be >= 1")
     if cfg.log_level not in ("debug", "info", "warn", "error", "off"):
         raise ValueError("log_level must be debug|info|warn|error|off")
+    if cfg.sentinel_impl not in ("auto", "hip", "queue"):
+        raise ValueError(f"sentinel_impl must be auto|hip|queue, got {cfg.sentinel_impl}")
     if cfg.stale_after < 0 and cfg.stale_after != -1:
         raise ValueError("stale_after must be -1 (auto), 0 (never) or > 0 seconds")
     host, _ = cfg.listen_host_port()

@@ -97,16 +97,24 @@ def test_exporter_tick_on_gpu(native):
         e.stop()
 
 
-def test_sentinel_one_wave_per_xcd(native):
+@pytest.mark.parametrize("impl", ["hip", "queue"])
+def test_sentinel_one_wave_per_xcd(native, impl):
     """Full profile: the sentinel run puts one wave on each XCD (placement read back from
-    HW_REG_XCC_ID) and the PMFW reports each XCD's gfx clock."""
-    e = amdsmi_engine(native, enable_sentinel=True, series_profile="full")
+    HW_REG_XCC_ID) and the PMFW reports each XCD's gfx clock — from the HIP plugin's own
+    stream and from raw AQL dispatches on the PMC counters' queue alike."""
+    kw = dict(enable_counters=True, counters_plugin=native.default_rocprof_plugin(), sentinel_impl="queue") \
+        if impl == "queue" else dict(sentinel_impl="hip")
+    e = amdsmi_engine(native, enable_sentinel=True, series_profile="full", **kw)
     try:
+        status = e.source_status()
+        if impl == "queue" and "counters=unavailable" in status:
+            pytest.skip("PMC queue unavailable on this box: " + status)
+        assert ("hsa sentinel" if impl == "queue" else "hip sentinel") in status, status
         for _ in range(6):
             e.tick()
             time.sleep(0.05)
         fams = promtext.parse(e.snapshot_text())
-        print(e.source_status())
+        print(status)
     finally:
         e.stop()
     lat = {lab["xcc"]: v for _, lab, v in promtext.samples(fams, "amd_gpu_sentinel_xcc_dispatch_latency_seconds")}
