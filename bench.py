@@ -106,6 +106,12 @@ def pct(v: list, q: float) -> float:
 
 
 def main() -> int:
+    # The result line must be the only thing on stdout. RCCL prints its version banner
+    # to fd 1 from native code at communicator init, so fd 1 is pointed at stderr for the
+    # whole run and the JSON line goes to a private duplicate of the original stdout.
+    sys.stdout.flush()
+    result_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
@@ -539,7 +545,7 @@ def main() -> int:
             if rlat and lat:
                 result["speedup_p50_vs_refstyle"] = round(statistics.median(rlat) / statistics.median(lat), 2)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=result_out, flush=True)
         if args.out:
             with open(args.out, "w") as fh:
                 json.dump(result, fh, indent=1)
