@@ -45,6 +45,8 @@ def test_bench_single_process():
     assert r.returncode == 0, r.stderr[-2000:]
     (d,) = _json_lines(r.stdout)
     _check(d, 1, 5, 1)
+    # Native libraries (RCCL's banner) and the exporter child write to stderr only.
+    assert r.stdout.strip().count("\n") == 0, r.stdout[-2000:]
 
 
 def test_bench_torchrun_two_ranks():
