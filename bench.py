@@ -74,7 +74,10 @@ def start_exporter(args, n_gpus: int, backend: str, port: int, pod_map: str, log
         if rccl_dir:
             cmd += ["--enable-rccl", "true", "--rccl-dir", rccl_dir]
     else:
-        cmd += ["--mock-devices", str(n_gpus), "--enable-sentinel", "true", "--enable-counters", "true"]
+        # Mock devices; the ranks' KFD process entries live in a fake host root that rank 0
+        # fills in once it knows every rank's PID (real KFD-reader and attribution path).
+        cmd += ["--mock-devices", str(n_gpus), "--enable-sentinel", "true", "--enable-counters", "true",
+                "--host-root", args.fake_root]
     env = dict(os.environ)
     env.pop("ROCP_TOOL_LIBRARIES", None)  # the exporter itself issues no collectives
     env["GPUEXP_POD_MAP_FILE"] = pod_map
@@ -105,13 +108,71 @@ def pct(v: list, q: float) -> float:
     return v[lo] + (v[hi] - v[lo]) * (k - lo)
 
 
+def launch_ranks(args, argv: list) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes (one per GPU, env
+    rendezvous on 127.0.0.1) and relay rank 0's result line.  This parent never imports
+    torch or touches a GPU, and never execs: every rank is a child, and the first rank
+    that fails takes the others down (their whole process groups, exporter included)."""
+    import signal
+    port = free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), GPUEXP_BENCH_LAUNCHER=str(os.getpid()))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env, cwd=ROOT,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(),
+                                      start_new_session=True))
+
+    def kill_all(sig=signal.SIGTERM):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, sig)
+                except ProcessLookupError:
+                    pass
+
+    def on_signal(signum, _frame):
+        kill_all()
+        sys.exit(128 + signum)
+
+    signal.signal(signal.SIGTERM, on_signal)
+    signal.signal(signal.SIGINT, on_signal)
+    deadline = time.time() + args.launch_timeout
+    failed = None
+    while True:
+        codes = [p.poll() for p in procs]
+        if all(c is not None for c in codes):
+            break
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad and failed is None:
+            failed = bad[0]
+            print(f"[bench] rank {failed[0]} exited with {failed[1]}; stopping the other ranks", file=sys.stderr,
+                  flush=True)
+            kill_all()
+            grace = time.time() + 20
+            while time.time() < grace and any(p.poll() is None for p in procs):
+                time.sleep(0.1)
+            kill_all(signal.SIGKILL)
+        if time.time() > deadline:
+            print(f"[bench] ranks still running after {args.launch_timeout} s; stopping them", file=sys.stderr,
+                  flush=True)
+            kill_all(signal.SIGKILL)
+            failed = failed or (-1, 124)
+        time.sleep(0.1)
+    out = procs[0].stdout.read().decode(errors="replace")
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    if failed is None and procs[0].returncode == 0 and len(lines) == 1:
+        sys.stdout.write(lines[0] + "\n")
+        sys.stdout.flush()
+        return 0
+    if out:
+        sys.stderr.write(out)
+    rc = procs[0].returncode
+    return rc if rc not in (0, None) else (failed[1] if failed and failed[1] > 0 else 1)
+
+
 def main() -> int:
-    # The result line must be the only thing on stdout. RCCL prints its version banner
-    # to fd 1 from native code at communicator init, so fd 1 is pointed at stderr for the
-    # whole run and the JSON line goes to a private duplicate of the original stdout.
-    sys.stdout.flush()
-    result_out = os.fdopen(os.dup(1), "w")
-    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
@@ -140,13 +201,32 @@ def main() -> int:
                     help="inject the RCCL tracer (rocprofiler-sdk tool) into every rank and export per-pod "
                          "collective calls/bytes")
     ap.add_argument("--exporter", choices=("native", "both"), default="native",
-                    help="'both' also measures the reference-architecture exporter (utils/refstyle.py)")
-    args = ap.parse_args()
+                    help="'both' also measures a Python prometheus_client stand-in exporter (utils/refstyle.py)")
+    ap.add_argument("--launch-timeout", type=float, default=1800.0,
+                    help="self-launch (--gpus N > 1 without torchrun): stop the ranks after this many seconds")
+    argv = sys.argv[1:]
+    args = ap.parse_args(argv)
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args, argv)
+
+    # The result line must be the only thing on stdout. RCCL prints its version banner
+    # to fd 1 from native code at communicator init, so fd 1 is pointed at stderr for the
+    # whole run and the JSON line goes to a private duplicate of the original stdout.
+    sys.stdout.flush()
+    result_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    n_gpus = max(args.gpus, world)
+    if world != args.gpus:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU is required", file=sys.stderr)
+        return 2
+    n_gpus = world
+    if os.environ.get("GPUEXP_BENCH_FAIL_RANK") == str(rank):  # test hook: a rank that dies at start
+        print(f"[bench] rank {rank}: failing on request (GPUEXP_BENCH_FAIL_RANK)", file=sys.stderr)
+        return 3
 
     # RCCL visibility per pod: the tracer tool must be in the environment before the HIP
     # runtime loads (torch's import does that), so set it before importing torch.  All
@@ -166,6 +246,8 @@ def main() -> int:
     backend = args.backend if args.backend != "auto" else ("amdsmi" if have_gpu else "mock")
     tmpdir = tempfile.mkdtemp(prefix="gpuexp-bench-")
     pod_map = os.path.join(tmpdir, "podmap.json")
+    args.fake_root = os.path.join(tmpdir, "host")
+    os.makedirs(os.path.join(args.fake_root, "sys/class/kfd/kfd/proc"), exist_ok=True)
     port = 0
     exporter = None
     degraded = None
@@ -207,7 +289,7 @@ def main() -> int:
     from kubernetes_gpu_exporter_amd._native import load
     from kubernetes_gpu_exporter_amd.k8s.filesource import write_pod_map
     from kubernetes_gpu_exporter_amd.utils import promproto, promtext
-    from kubernetes_gpu_exporter_amd.utils.fakehost import kubepods_cgroup
+    from kubernetes_gpu_exporter_amd.utils.fakehost import FakeHost, kubepods_cgroup
     from kubernetes_gpu_exporter_amd.utils.procstat import cpu_seconds_precise
     n = load()
     from kubernetes_gpu_exporter_amd.ops.gemm import kernels
@@ -272,7 +354,27 @@ def main() -> int:
             # KFD names the rank by host PID; the RCCL tracer by its PID in the exporter's
             # namespace — the same number unless the box runs us in a PID namespace
             cgroups[p] = cgroups[op] = kubepods_cgroup(uid, cid, qos="guaranteed")
+            if not use_gpu:
+                # mock GPU r (KFD gpu_id 1000 + r) holds rank r's buffers
+                FakeHost(args.fake_root).set_process_gpu(p, 1000 + r, vram=(r + 1) << 30, cu=32)
         write_pod_map(pod_map, pods, cgroups)
+        # Untimed: wait until the exporter has picked the pod map up and attributes every
+        # rank (its control plane re-reads the file every 0.5 s), so even a short warmup
+        # measures the steady state.
+        want = {p["name"] for p in pods}
+        t_attr = time.time() + 20
+        while time.time() < t_attr:
+            try:
+                st, body = http_get(port, "/metrics", 2.0)
+                got = {lab["pod"] for _, lab, _ in promtext.samples(promtext.parse(body.decode()),
+                                                                     "pod_gpu_memory_usage")}
+                if st == 200 and want <= got:
+                    break
+            except OSError:
+                pass
+            time.sleep(0.1)
+        else:
+            print(f"[bench] exporter did not attribute all {len(want)} ranks within 20 s", file=sys.stderr, flush=True)
         # timing=True: the server echoes when it parsed the request and started writing,
         # so each latency splits into request wake-up / server work / response delivery
         client = n.ScrapeClient("127.0.0.1", port, "/metrics", args.gzip, 5000,
@@ -435,6 +537,17 @@ def main() -> int:
         srv = {s[0].rsplit("_", 1)[-1]: s[2] for s in promtext.samples(fams, "gpuexp_scrape_duration_seconds")
                if s[0].endswith(("_sum", "_count"))}
         server_mean_us = round(srv["sum"] / srv["count"] * 1e6, 2) if srv.get("count") else None
+        # server-side p50/p99 over EVERY scrape of the run (warmup, both phases): upper
+        # bound of the histogram bucket holding the quantile
+        sb = sorted((float(lab["le"]), v) for _, lab, v in promtext.samples(fams, "gpuexp_scrape_duration_seconds")
+                    if "le" in lab)
+        server_q = {}
+        if sb and sb[-1][1]:
+            for qname, q in (("p50", 0.5), ("p99", 0.99)):
+                le = next(le for le, v in sb if v >= q * sb[-1][1])
+                server_q[qname] = round(le * 1e6, 1) if le != float("inf") else None
+        server_scrapes = int(sb[-1][1]) if sb else 0
+        ticks = [v for _, _, v in promtext.samples(fams, "gpuexp_ticks_total")]
         metrics_reads = {lab["kind"]: v for _, lab, v in promtext.samples(fams, "gpuexp_gpu_metrics_reads_total")
                          if lab.get("gpu") == "0"}
         sampler_cpu = [v for _, _, v in promtext.samples(fams, "gpuexp_sampler_cpu_seconds_total")]
@@ -472,13 +585,18 @@ def main() -> int:
                        "series_profile": args.series_profile, "gzip": args.gzip, "protobuf": args.proto,
                        "gemm": f"{G}^3 x {iters}/step", "allreduce_mb": args.allreduce_mb if dist is not None else 0},
             "p50_scrape_us": round(statistics.median(lat), 2) if lat else None,
-            "p99_scrape_us": round(pct(lat, 0.99), 2) if lat else None,
+            # a p99 needs >= 100 samples; below that only the max of the timed scrapes and
+            # the server-side histogram quantiles over every scrape of the run are given
+            "p99_scrape_us": round(pct(lat, 0.99), 2) if len(lat) >= 100 else None,
             "max_scrape_us": round(max(lat), 2) if lat else None,
+            "server_scrape_p50_le_us": server_q.get("p50"),
+            "server_scrape_p99_le_us": server_q.get("p99"),
+            "server_scrapes": server_scrapes,
             "exporter_cpu_percent": round(cpu_pct, 3),
             "exporter_rss_mb": round(exporter_rss_kb[0] / 1024, 1) if exporter_rss_kb[0] else None,
             "scrape_encoding": "gzip (Prometheus default Accept-Encoding)" if args.gzip else "identity",
             "p50_scrape_identity_us": round(statistics.median(lat_id), 2) if lat_id else None,
-            "p99_scrape_identity_us": round(pct(lat_id, 0.99), 2) if lat_id else None,
+            "p99_scrape_identity_us": round(pct(lat_id, 0.99), 2) if lat_id and len(lat_id) >= 100 else None,
             "exporter_cpu_percent_identity_phase": round(cpu_id, 3) if cpu_id is not None else None,
             "scrape_bytes_identity": id_bytes if lat_id else None,
             "server_scrape_mean_us": server_mean_us,
@@ -500,12 +618,19 @@ def main() -> int:
             "rccl_per_pod": rccl,
             "rccl_rank_per_pod": rccl_ranks,
             "xgmi_bytes_per_second": xgmi,
-            "xgmi_timed_window": xgmi_window,
+            # xGMI bytes the exporter's hardware counters saw vs what the DP all-reduce had to
+            # move (null at 1 rank: nothing crosses xGMI; null on the mock backend)
+            "xgmi_timed_window": dict({"measured_over_expected_write": None}, **xgmi_window),
             "families_gpu0": {k: v for k, v in sorted(fam_gpu0.items()) if v},
             "sample_stage_mean_us": stage_us,
             "sample_stage_p50_le_us": stage_p50_us,
             "gpu_metrics_reads_gpu0": metrics_reads,
             "sampler_thread_cpu_s": sampler_cpu[0] if sampler_cpu else None,
+            "sampler_cpu_us_per_tick": round(sampler_cpu[0] / ticks[0] * 1e6, 1) if sampler_cpu and ticks and ticks[0]
+            else None,
+            "sampler_cpu_us_per_tick_per_gpu": round(sampler_cpu[0] / ticks[0] * 1e6 / n_gpus, 1)
+            if sampler_cpu and ticks and ticks[0] else None,
+            "ranks": world,
             "http_prewake_wakeups_per_scrape": round(prewake[0] / scrapes_total[0], 2)
             if prewake and scrapes_total and scrapes_total[0] else None,
             "optional_sources": {"counters": bool(args.counters), "sentinel": bool(args.sentinel),

@@ -9,6 +9,7 @@ pod metadata at low rate; SIGTERM/SIGINT stop both and shut amdsmi/HIP down clea
 from __future__ import annotations
 
 import logging
+import os
 import signal
 import threading
 from typing import Optional
@@ -35,7 +36,10 @@ class Exporter:
     def start(self) -> "Exporter":
         self.engine.start()
         self._started = True
-        if self._control is None and self.cfg.pod_attribution and self.cfg.resolved_backend() != "mock":
+        # The mock backend gets a control plane only from an explicit pod map (bench, tests):
+        # it must never pick up a real node's kubelet or apiserver.
+        if self._control is None and self.cfg.pod_attribution and (
+                self.cfg.resolved_backend() != "mock" or os.environ.get("GPUEXP_POD_MAP_FILE")):
             from .k8s.controlplane import ControlPlane
             self._control = ControlPlane.from_config(self.cfg)
         if self._control is not None:

@@ -49,6 +49,43 @@ def test_bench_single_process():
     assert r.stdout.strip().count("\n") == 0, r.stdout[-2000:]
 
 
+def test_bench_self_launches_one_rank_per_gpu():
+    """`bench.py --gpus 4` with no launcher starts 4 ranks itself (gloo on CPU): 4 mock
+    GPUs, 4 GEMM pods attributed through the KFD reader + pod map, one result line."""
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--backend", "mock", "--steps", "4", "--warmup",
+                        "1"], cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    (d,) = _json_lines(r.stdout)
+    _check(d, 4, 4, 1)
+    assert d["ranks"] == 4 and d["config"]["global_batch"] == 4
+    assert d["attributed_pods"] == [f"gemm-pod-{i}" for i in range(4)]
+    assert sorted(d["series_per_gpu"]) == ["0", "1", "2", "3"]
+    assert d["p99_scrape_us"] is None  # 4 samples: no p99 claimed
+    assert d["server_scrapes"] >= 8 and d["server_scrape_p99_le_us"] > 0
+    assert d["sampler_cpu_us_per_tick_per_gpu"] > 0 and d["exporter_rss_mb"] > 0
+    assert "measured_over_expected_write" in d["xgmi_timed_window"]
+
+
+def test_bench_world_must_match_gpus():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--backend", "mock", "--steps", "1"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+    assert not _json_lines(r.stdout)
+
+
+def test_bench_failed_rank_stops_the_job():
+    env = dict(os.environ, GPUEXP_BENCH_FAIL_RANK="1", OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--backend", "mock", "--steps", "50"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode != 0
+    assert not _json_lines(r.stdout)
+    assert "rank 1 exited with 3" in r.stderr
+
+
 def test_bench_torchrun_two_ranks():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--steps", "4", "--warmup", "1"]
