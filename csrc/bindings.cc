@@ -325,6 +325,7 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("counters_interval_ms", &EngineConfig::counters_interval_ms)
       .def_readwrite("enable_rccl", &EngineConfig::enable_rccl)
       .def_readwrite("rccl_dir", &EngineConfig::rccl_dir)
+      .def_readwrite("rccl_verify", &EngineConfig::rccl_verify)
       .def_readwrite("force_amdsmi_metrics", &EngineConfig::force_amdsmi_metrics)
       .def_readwrite("gzip_level", &EngineConfig::gzip_level)
       .def_readwrite("gc_after", &EngineConfig::gc_after)

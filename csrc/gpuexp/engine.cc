@@ -249,6 +249,14 @@ void Engine::define_families() {
   f_self_metrics_period_ = add("gpuexp_gpu_metrics_refresh_period_seconds",
                                "PMFW gpu_metrics refresh period learnt from firmware timestamps (0 = learning)",
                                G, {"gpu"});
+  f_self_unresolved_ = add("gpuexp_pods_unresolved",
+                           "Pod UIDs found in GPU processes' cgroups that the control plane has not named "
+                           "yet (their series carry pod=\"\" and no legacy series until it does)",
+                           G, {});
+  f_self_rccl_files_ = add("gpuexp_rccl_files",
+                           "RCCL tracer files by state: active (writer identified, exported), unverified "
+                           "(no live process maps it as claimed), exited (writer gone, file left behind)",
+                           G, {"state"});
   f_self_ctr_scope_ = add("gpuexp_counters_device_scope",
                           "1 if wave/LDS/HBM PMC counters see every process on the GPU, 0 if they are "
                           "VMID-filtered to the exporter (not exported then)",
@@ -258,6 +266,29 @@ void Engine::define_families() {
 bool Engine::start(std::string* err) {
   if (running_.load()) return true;
   define_families();
+  // Listen first: a port conflict fails before any GPU-side source (amdsmi, HSA queues,
+  // sentinel runs) exists.  Every later failure tears down what was already started.
+  if (cfg_.serve_http) {
+    http_ = std::make_unique<HttpServer>(&store_, cfg_.http);
+    if (!http_->start(err)) {
+      http_.reset();
+      return false;
+    }
+  }
+  bool ok = false;
+  struct Undo {
+    Engine* e;
+    bool* ok;
+    ~Undo() {
+      if (*ok) return;
+      if (e->http_) e->http_->stop();
+      e->http_.reset();
+      if (e->backend_) e->backend_->shutdown();
+      e->backend_.reset();
+      e->mock_ = nullptr;
+      e->devices_.clear();
+    }
+  } undo{this, &ok};
   if (cfg_.backend == "mock") {
     auto m = std::make_unique<MockBackend>(cfg_.mock_devices);
     mock_ = m.get();
@@ -351,7 +382,7 @@ bool Engine::start(std::string* err) {
   } else if (cfg_.enable_sentinel) {
     sentinel_status_ = "mock";
   }
-  if (cfg_.enable_rccl) rccl_ = make_rccl_source(cfg_.rccl_dir);
+  if (cfg_.enable_rccl) rccl_ = make_rccl_source(cfg_.rccl_dir, cfg_.rccl_verify);
 
   if (!cfg_.trace_path.empty()) {
     trace_ = std::fopen(cfg_.trace_path.c_str(), "w");
@@ -360,13 +391,7 @@ bool Engine::start(std::string* err) {
       trace_t0_ = mono_ns();
     }
   }
-  if (cfg_.serve_http) {
-    http_ = std::make_unique<HttpServer>(&store_, cfg_.http);
-    if (!http_->start(err)) {
-      http_.reset();
-      return false;
-    }
-  }
+  ok = true;
   running_.store(true);
   if (cfg_.interval_s > 0) {
     stop_fd_ = ::eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
@@ -675,6 +700,7 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
 void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSample>>& per_dev) {
   // pid -> attribution, resolved once per tick
   std::unordered_map<int, ProcAttr> attr;
+  unresolved_.clear();
   std::vector<int> live;
   for (auto& lst : per_dev)
     for (auto& p : lst) {
@@ -689,7 +715,9 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
             a.ns = it->second.ns;
             a.pod = it->second.name;
           } else {
-            a.pod = ci->pod_uid;  // name unknown until the control plane reports it
+            // Name unknown until the control plane reports it: pod="" meanwhile (a UID
+            // in `pod` would change the series identity once the name arrives).
+            unresolved_.insert(ci->pod_uid);
           }
           auto cn = container_names_.find(ci->container_id);
           if (cn != container_names_.end()) a.container = cn->second;
@@ -823,7 +851,7 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
             a.ns = pit->second.ns;
             a.pod = pit->second.name;
           } else {
-            a.pod = ci->pod_uid;
+            unresolved_.insert(ci->pod_uid);
           }
         }
       }
@@ -851,6 +879,7 @@ void Engine::emit_self(uint64_t gen) {
     table_.put(f_self_last_, {}, double(rt.tv_sec) + double(rt.tv_nsec) * 1e-9, gen);
   }
   table_.put(f_self_overruns_, {}, double(s.overruns), gen);
+  table_.put(f_self_unresolved_, {}, double(unresolved_.size()), gen);
   table_.put(f_self_render_bytes_, {}, double(s.render_bytes), gen);
   table_.put(f_self_series_, {}, double(s.series), gen);
   table_.put(f_self_cpu_, {}, double(s.sampler_cpu_ns) * 1e-9, gen);
@@ -882,6 +911,13 @@ void Engine::emit_self(uint64_t gen) {
   table_.put(f_self_source_up_, {"sentinel"}, (sentinel_ || (cfg_.enable_sentinel && mock_)) ? 1 : 0, gen);
   table_.put(f_self_source_up_, {"counters"}, (counters_ || (cfg_.enable_counters && mock_)) ? 1 : 0, gen);
   table_.put(f_self_source_up_, {"rccl"}, rccl_ ? 1 : 0, gen);
+  if (rccl_) {
+    int a = 0, u = 0, x = 0;
+    rccl_->file_states(&a, &u, &x);
+    table_.put(f_self_rccl_files_, {"active"}, a, gen);
+    table_.put(f_self_rccl_files_, {"unverified"}, u, gen);
+    table_.put(f_self_rccl_files_, {"exited"}, x, gen);
+  }
 }
 
 void Engine::tick_locked(uint64_t now) {
@@ -988,14 +1024,18 @@ void Engine::tick_locked(uint64_t now) {
         const CgroupInfo* ci = resolver_->resolve(p.pid);
         if (!ci || !ci->kube) continue;
         auto pit = pods_by_uid_.find(ci->pod_uid);
-        std::string ns = pit != pods_by_uid_.end() ? pit->second.ns : "";
-        std::string name = pit != pods_by_uid_.end() ? pit->second.name : ci->pod_uid;
+        if (pit == pods_by_uid_.end()) {
+          seen.emplace("", "", "");  // an unnamed pod: ownership stays unknown
+          continue;
+        }
+        const std::string& ns = pit->second.ns;
+        const std::string& name = pit->second.name;
         auto cn = container_names_.find(ci->container_id);
         seen.emplace(ns, name, cn != container_names_.end() ? cn->second : "");
       }
       std::set<std::pair<std::string, std::string>> podset;
       for (auto& t : seen) podset.emplace(std::get<0>(t), std::get<1>(t));
-      if (podset.size() == 1) {
+      if (podset.size() == 1 && !podset.begin()->second.empty()) {
         own.ns = podset.begin()->first;
         own.pod = podset.begin()->second;
         if (seen.size() == 1) own.container = std::get<2>(*seen.begin());

@@ -14,6 +14,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -82,6 +83,7 @@ struct EngineConfig {
   int counters_interval_ms = 1000;     // ...once per interval (duty cycle, see rocprof_plugin.cc)
   bool enable_rccl = false;
   std::string rccl_dir = "/dev/shm";
+  bool rccl_verify = true;             // attribute a tracer file only to a process that maps it
   bool force_amdsmi_metrics = false;
   int gzip_level = 1;
   uint64_t gc_after = 1;               // stale series vanish this many ticks after last seen
@@ -224,6 +226,7 @@ class Engine {
   std::unordered_map<std::string, PodMeta> pods_by_uid_;
   std::unordered_map<std::string, std::string> container_names_;  // cid -> name
   std::unordered_map<std::string, DeviceOwner> owners_;           // lower(bdf|uuid) -> owner
+  std::set<std::string> unresolved_;                               // pod UIDs without metadata (last tick)
 
   // stats (guarded by stats_mu_)
   std::mutex stats_mu_;
@@ -246,7 +249,8 @@ class Engine {
   int f_rccl_calls_, f_rccl_bytes_, f_rccl_comm_;
   int f_self_build_, f_self_ticks_, f_self_last_, f_self_stage_, f_self_scrape_, f_self_scrapes_,
       f_self_http_bytes_, f_self_render_bytes_, f_self_series_, f_self_dev_errors_,
-      f_self_overruns_, f_self_cpu_, f_self_source_up_, f_self_ctr_scope_, f_self_metrics_reads_, f_self_metrics_period_, f_self_prewake_;
+      f_self_overruns_, f_self_cpu_, f_self_source_up_, f_self_ctr_scope_, f_self_metrics_reads_, f_self_metrics_period_, f_self_prewake_,
+      f_self_rccl_files_, f_self_unresolved_;
   SeriesRef self_stage_refs_[kStages];
   uint64_t last_stage_ns_[kStages] = {};
 };

@@ -550,7 +550,12 @@ void HttpServer::run(Worker* w) {
       c.last_active_ns = mono_ns();
       bool ok = true;
       if (events[i].events & (EPOLLERR | EPOLLHUP)) ok = false;
-      if (ok && (events[i].events & EPOLLOUT)) ok = flush(c);
+      if (ok && (events[i].events & EPOLLOUT)) {
+        ok = flush(c);
+        // A response that completed here may have pipelined requests queued behind it
+        // whose bytes were read long ago: no EPOLLIN will come for them.
+        if (ok && !c.pending && !c.in.empty() && !(events[i].events & EPOLLIN)) ok = handle_input(c);
+      }
       if (ok && (events[i].events & EPOLLIN)) {
         for (;;) {
           ssize_t r = ::read(fd, rbuf, sizeof(rbuf));

@@ -4,10 +4,15 @@
 #include <dirent.h>
 #include <dlfcn.h>
 #include <fcntl.h>
-#include <sys/mman.h>
+#include <poll.h>
 #include <sys/stat.h>
+#include <sys/syscall.h>
+#include <sys/sysmacros.h>
 #include <unistd.h>
 
+#include <algorithm>
+#include <cerrno>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <unordered_map>
@@ -131,77 +136,309 @@ int innermost_nspid(const std::string& proc_pid_dir) {
   return last;
 }
 
+// Start time (field 22 of /proc/<pid>/stat) in clock ticks; 0 if the process is gone.
+uint64_t proc_starttime(int pid) {
+  std::string s;
+  if (!read_small_file("/proc/" + std::to_string(pid) + "/stat", &s, 4096)) return 0;
+  size_t p = s.rfind(')');
+  if (p == std::string::npos) return 0;
+  int field = 2;
+  size_t i = p + 1;
+  while (i < s.size()) {
+    while (i < s.size() && s[i] == ' ') ++i;
+    if (++field == 22) break;
+    while (i < s.size() && s[i] != ' ') ++i;
+  }
+  return std::strtoull(s.c_str() + i, nullptr, 10);
+}
+
+// True if /proc/<pid>/maps has a mapping of the file (dev, ino): proof that `pid` is the
+// process that writes it (the tracer keeps its counters file mapped for its whole life).
+// -1 if the maps file is unreadable (no ptrace-read access to that process).
+int maps_file(int pid, dev_t dev, ino_t ino) {
+  int fd = ::open(("/proc/" + std::to_string(pid) + "/maps").c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return errno == EACCES || errno == EPERM ? -1 : 0;
+  std::string all;
+  char buf[65536];
+  for (;;) {
+    ssize_t n = ::read(fd, buf, sizeof(buf));
+    if (n < 0 && errno == EINTR) continue;
+    if (n <= 0) {
+      if (n < 0 && all.empty()) {
+        ::close(fd);
+        return errno == EACCES || errno == EPERM ? -1 : 0;
+      }
+      break;
+    }
+    all.append(buf, size_t(n));
+  }
+  ::close(fd);
+  const unsigned want_maj = major(dev), want_min = minor(dev);
+  size_t i = 0;
+  while (i < all.size()) {
+    size_t e = all.find('\n', i);
+    if (e == std::string::npos) e = all.size();
+    // address perms offset dev inode [path]
+    const char* p = all.c_str() + i;
+    const char* end = all.c_str() + e;
+    int f = 0;
+    const char* tok[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    while (p < end && f < 5) {
+      while (p < end && *p == ' ') ++p;
+      tok[f++] = p;
+      while (p < end && *p != ' ') ++p;
+    }
+    if (f == 5) {
+      char* q = nullptr;
+      unsigned long maj = std::strtoul(tok[3], &q, 16);
+      if (q && *q == ':') {
+        unsigned long mn = std::strtoul(q + 1, nullptr, 16);
+        unsigned long long in = std::strtoull(tok[4], nullptr, 10);
+        if (maj == want_maj && mn == want_min && in == (unsigned long long)ino) return 1;
+      }
+    }
+    i = e + 1;
+  }
+  return 0;
+}
+
+// Reads the RCCL tracer's counter files from a directory that every workload pod can
+// write to (a hostPath), so nothing in them is trusted:
+//  - files are opened O_NOFOLLOW|O_NONBLOCK and must be regular (no FIFO can block the
+//    sampler, no symlink can point elsewhere), and are copied with pread() every poll (a
+//    writer truncating its file cannot fault the exporter, as a live mapping would);
+//  - the name must agree with the identity inside, and the identity must name a process
+//    that maps this very file (/proc/<pid>/maps dev:inode), in the PID namespace it
+//    claims — a pod cannot get its counters attributed to another pod's process;
+//  - the writer's liveness is checked every poll (pidfd, else start time): a file left by
+//    a killed process stops being exported at once and never moves to a reused PID;
+//  - failed identifications back off (1 s doubling to 60 s) instead of scanning /proc
+//    every tick.
 class ShmRcclSource : public RcclSource {
  public:
-  explicit ShmRcclSource(std::string dir) : dir_(std::move(dir)) { self_ns_ = pidns_inode("/proc/self"); }
+  ShmRcclSource(std::string dir, bool verify_maps) : dir_(std::move(dir)), verify_maps_(verify_maps) {
+    self_ns_ = pidns_inode("/proc/self");
+  }
   ~ShmRcclSource() override {
-    for (auto& kv : maps_) ::munmap(kv.second.base, sizeof(RcclShmFile));
+    for (auto& kv : files_) close_entry(&kv.second);
   }
 
   void poll(std::vector<RcclTotals>* out) override {
     out->clear();
-    std::map<std::string, bool> present;
+    const uint64_t now = mono_ns();
+    std::unordered_map<std::string, bool> present;
+    int dfd = ::open(dir_.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+    if (dfd < 0) {
+      for (auto& kv : files_) close_entry(&kv.second);
+      files_.clear();
+      return;
+    }
     for (const std::string& name : list_dir(dir_)) {
-      if (name.compare(0, 12, "gpuexp-rccl-") != 0) continue;
+      uint64_t name_ino = 0;
+      int name_pid = 0;
+      if (!parse_name(name, &name_ino, &name_pid)) continue;
+      struct stat st;
+      if (::fstatat(dfd, name.c_str(), &st, AT_SYMLINK_NOFOLLOW) != 0 || !S_ISREG(st.st_mode)) continue;
       present[name] = true;
-      if (!maps_.count(name)) {
-        int fd = ::open((dir_ + "/" + name).c_str(), O_RDONLY | O_CLOEXEC);
-        if (fd < 0) continue;
-        struct stat st;
-        if (::fstat(fd, &st) != 0 || size_t(st.st_size) < sizeof(RcclShmFile)) {
-          ::close(fd);
+      Entry& e = files_[name];
+      if (e.fd >= 0 && (e.dev != st.st_dev || e.ino != st.st_ino)) close_entry(&e);  // replaced file
+      if (e.fd < 0) {
+        if (now < e.retry_ns) continue;
+        e.fd = ::openat(dfd, name.c_str(), O_RDONLY | O_NOFOLLOW | O_NONBLOCK | O_CLOEXEC);
+        struct stat fst;
+        if (e.fd < 0 || ::fstat(e.fd, &fst) != 0 || !S_ISREG(fst.st_mode)) {
+          close_entry(&e);
+          backoff(&e, now);
           continue;
         }
-        void* p = ::mmap(nullptr, sizeof(RcclShmFile), PROT_READ, MAP_SHARED, fd, 0);
-        ::close(fd);
-        if (p == MAP_FAILED) continue;
-        maps_[name] = Mapping{static_cast<RcclShmFile*>(p), -1};
+        e.dev = fst.st_dev;
+        e.ino = fst.st_ino;
       }
-      Mapping& m = maps_[name];
-      if (m.base->magic != kRcclShmMagic) continue;
-      if (m.host_pid < 0) m.host_pid = host_pid_for(m.base->pidns_ino, m.base->ns_pid);
-      if (m.host_pid < 0) continue;
+      RcclShmFile snap;
+      if (!read_consistent(e.fd, &snap) || snap.magic != kRcclShmMagic || snap.pidns_ino != name_ino ||
+          snap.ns_pid != name_pid || snap.pidns_ino == 0 || snap.ns_pid <= 0) {
+        continue;  // not (yet) a complete file, or one whose content disagrees with its name
+      }
+      if (e.host_pid > 0 && !alive(&e)) {
+        release_owner(&e);  // writer exited (or was killed): its leftover file is not exported
+        e.state = kExited;
+        e.fails = 0;
+        backoff(&e, now);  // re-identify later: a new writer may reuse the name (O_TRUNC)
+      }
+      if (e.host_pid <= 0) {
+        if (now < e.retry_ns) continue;
+        if (!identify(&e, snap.pidns_ino, snap.ns_pid)) {
+          if (e.state != kExited) e.state = kUnverified;
+          backoff(&e, now);
+          continue;
+        }
+        e.state = kActive;
+        e.fails = 0;
+      }
       for (int op = 0; op < kOpNumOps; ++op) {
-        uint64_t c = m.base->ops[op].calls.load(std::memory_order_relaxed);
+        const uint64_t c = snap.ops[op].calls.load(std::memory_order_relaxed);
         if (!c) continue;
         RcclTotals t;
-        t.pid = m.host_pid;
+        t.pid = e.host_pid;
         t.op = rccl_op_name(op);
         t.calls = c;
-        t.bytes = m.base->ops[op].bytes.load(std::memory_order_relaxed);
-        t.rank = reinterpret_cast<volatile int32_t*>(&m.base->rank)[0];
-        t.nranks = reinterpret_cast<volatile int32_t*>(&m.base->nranks)[0];
+        t.bytes = snap.ops[op].bytes.load(std::memory_order_relaxed);
+        t.rank = snap.rank;
+        t.nranks = snap.nranks;
         out->push_back(t);
       }
     }
-    for (auto it = maps_.begin(); it != maps_.end();) {
+    ::close(dfd);
+    for (auto it = files_.begin(); it != files_.end();) {
       if (!present.count(it->first)) {
-        ::munmap(it->second.base, sizeof(RcclShmFile));
-        it = maps_.erase(it);
+        close_entry(&it->second);
+        it = files_.erase(it);
       } else {
         ++it;
       }
     }
   }
 
- private:
-  struct Mapping {
-    RcclShmFile* base;
-    int host_pid;
-  };
-  int host_pid_for(uint64_t ns_ino, int ns_pid) {
-    if (ns_ino == self_ns_ || ns_ino == 0) return ns_pid;  // same PID namespace
-    for (const std::string& d : list_dir("/proc")) {
-      if (d[0] < '0' || d[0] > '9') continue;
-      std::string pd = "/proc/" + d;
-      if (pidns_inode(pd) != ns_ino) continue;
-      if (innermost_nspid(pd) == ns_pid) return std::atoi(d.c_str());
+  void file_states(int* active, int* unverified, int* exited) const override {
+    *active = *unverified = *exited = 0;
+    for (const auto& kv : files_) {
+      if (kv.second.state == kActive) ++*active;
+      else if (kv.second.state == kExited) ++*exited;
+      else if (kv.second.state == kUnverified) ++*unverified;
     }
-    return -1;
   }
+
+ private:
+  enum State { kNew, kActive, kUnverified, kExited };
+  struct Entry {
+    int fd = -1;
+    dev_t dev = 0;
+    ino_t ino = 0;
+    int host_pid = -1;
+    int pidfd = -1;
+    uint64_t starttime = 0;
+    uint64_t retry_ns = 0;
+    int fails = 0;
+    State state = kNew;
+  };
+
+  static bool parse_name(const std::string& name, uint64_t* ino, int* pid) {
+    static const char kPrefix[] = "gpuexp-rccl-";
+    if (name.compare(0, sizeof(kPrefix) - 1, kPrefix) != 0) return false;
+    const char* p = name.c_str() + sizeof(kPrefix) - 1;
+    char* q = nullptr;
+    if (*p < '0' || *p > '9') return false;
+    *ino = std::strtoull(p, &q, 10);
+    if (!q || *q != '-' || q[1] < '0' || q[1] > '9') return false;
+    char* r = nullptr;
+    long v = std::strtol(q + 1, &r, 10);
+    if (!r || *r != '\0' || v <= 0 || v > (1 << 30)) return false;
+    *pid = int(v);
+    return true;
+  }
+
+  // Two identical preads: the writer updates the counters with relaxed atomics while we
+  // copy, so a torn 64-bit value could look like a counter reset.  Returns false on a
+  // short file (truncated, or not written yet) or when it never settles.
+  static bool read_consistent(int fd, RcclShmFile* out) {
+    alignas(RcclShmFile) unsigned char a[sizeof(RcclShmFile)], b[sizeof(RcclShmFile)];
+    if (::pread(fd, a, sizeof(a), 0) != ssize_t(sizeof(a))) return false;
+    for (int attempt = 0; attempt < 4; ++attempt) {
+      if (::pread(fd, b, sizeof(b), 0) != ssize_t(sizeof(b))) return false;
+      if (std::memcmp(a, b, sizeof(a)) == 0) {
+        std::memcpy(static_cast<void*>(out), b, sizeof(b));
+        return true;
+      }
+      std::memcpy(a, b, sizeof(a));
+    }
+    return false;
+  }
+
+  static void backoff(Entry* e, uint64_t now) {
+    const int f = std::min(e->fails, 6);
+    e->retry_ns = now + (1000000000ull << f);  // 1 s .. 64 s
+    e->fails += 1;
+  }
+
+  void release_owner(Entry* e) {
+    if (e->pidfd >= 0) ::close(e->pidfd);
+    e->pidfd = -1;
+    e->host_pid = -1;
+    e->starttime = 0;
+  }
+
+  void close_entry(Entry* e) {
+    release_owner(e);
+    if (e->fd >= 0) ::close(e->fd);
+    e->fd = -1;
+  }
+
+  bool alive(Entry* e) {
+    if (e->pidfd >= 0) {
+      pollfd p{e->pidfd, POLLIN, 0};
+      return ::poll(&p, 1, 0) == 0;  // a pidfd turns readable when its process exits
+    }
+    return proc_starttime(e->host_pid) == e->starttime;
+  }
+
+  // Finds the host PID of (ns_ino, ns_pid) and proves it is this file's writer.
+  bool identify(Entry* e, uint64_t ns_ino, int ns_pid) {
+    std::vector<int> cands;
+    if (ns_ino == self_ns_) {
+      cands.push_back(ns_pid);
+    } else {
+      for (const std::string& d : list_dir("/proc")) {
+        if (d.empty() || d[0] < '1' || d[0] > '9') continue;
+        const std::string pd = "/proc/" + d;
+        if (pidns_inode(pd) == ns_ino && innermost_nspid(pd) == ns_pid) cands.push_back(std::atoi(d.c_str()));
+      }
+    }
+    for (int pid : cands) {
+      // Pin the process first, then check it, then check the pin still holds: no PID
+      // reuse can slip between the check and the export.
+      int pfd = int(::syscall(SYS_pidfd_open, pid, 0));
+      const uint64_t st0 = proc_starttime(pid);
+      if (!st0) {
+        if (pfd >= 0) ::close(pfd);
+        continue;
+      }
+      const std::string pd = "/proc/" + std::to_string(pid);
+      bool ok = pidns_inode(pd) == ns_ino && innermost_nspid(pd) == ns_pid;
+      if (ok && verify_maps_) {
+        const int m = maps_file(pid, e->dev, e->ino);
+        if (m < 0 && !warned_maps_) {
+          warned_maps_ = true;
+          GPUEXP_LOG(LogLevel::kWarn, "rccl",
+                     "cannot read /proc/" + std::to_string(pid) +
+                         "/maps (needs ptrace-read access): RCCL counter files stay unattributed");
+        }
+        ok = m == 1;
+      }
+      if (ok) {
+        if (pfd >= 0) {
+          pollfd p{pfd, POLLIN, 0};
+          ok = ::poll(&p, 1, 0) == 0;
+        } else {
+          ok = proc_starttime(pid) == st0;
+        }
+      }
+      if (!ok) {
+        if (pfd >= 0) ::close(pfd);
+        continue;
+      }
+      e->host_pid = pid;
+      e->pidfd = pfd;
+      e->starttime = st0;
+      return true;
+    }
+    return false;
+  }
+
   std::string dir_;
+  bool verify_maps_;
+  bool warned_maps_ = false;
   uint64_t self_ns_ = 0;
-  std::unordered_map<std::string, Mapping> maps_;
+  std::unordered_map<std::string, Entry> files_;
 };
 
 // Directory of the core module itself (the HIP/rocprof plugins are installed beside it).
@@ -255,8 +492,8 @@ std::unique_ptr<CounterSource> make_rocprof_counters(const std::string& plugin_p
   return std::make_unique<PluginCounters>(plugin_path, window_ms, interval_ms);
 }
 
-std::unique_ptr<RcclSource> make_rccl_source(const std::string& dir) {
-  return std::make_unique<ShmRcclSource>(dir);
+std::unique_ptr<RcclSource> make_rccl_source(const std::string& dir, bool verify_maps) {
+  return std::make_unique<ShmRcclSource>(dir, verify_maps);
 }
 
 }  // namespace gpuexp

@@ -19,12 +19,10 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
   per_dev->assign(devs.size(), {});
   ++scan_no_;
   const std::string base = root_ + "/sys/class/kfd/kfd/proc";
-  char buf[128];
   for (const std::string& name : list_dir(base)) {
     int pid = std::atoi(name.c_str());
     if (pid <= 0 || pid == self_) continue;
-    auto it = pids_.find(pid);
-    if (it == pids_.end()) {
+    auto make_entry = [&]() {
       // New process: find which of OUR devices it has a KFD context on.
       Entry e;
       std::string pdir = base + "/" + name;
@@ -41,13 +39,33 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
       }
       std::string comm;
       if (read_small_file(root_ + "/proc/" + name + "/comm", &comm, 64)) e.comm = trim(comm);
-      it = pids_.emplace(pid, std::move(e)).first;
+      return pids_.insert_or_assign(pid, std::move(e)).first;
+    };
+    auto it = pids_.find(pid);
+    const bool fresh = it == pids_.end();
+    if (fresh) it = make_entry();
+    if (emit(it->second, pid, per_dev, now_ns) == 0 && !fresh && !it->second.devs.empty()) {
+      // Cached fds of a PID whose KFD directory was removed and re-created between two
+      // scans (the PID was reused) point at dead kobjects: every read fails although
+      // the directory exists.  Reopen once, so the new process (and its comm) shows.
+      it = make_entry();
+      emit(it->second, pid, per_dev, now_ns);
     }
-    Entry& e = it->second;
-    e.seen = scan_no_;
-    for (auto& pd : e.devs) {
+  }
+  // Forget processes that left the KFD proc directory (closes their fds).
+  for (auto it = pids_.begin(); it != pids_.end();)
+    it = it->second.seen != scan_no_ ? pids_.erase(it) : std::next(it);
+}
+
+int KfdProcReader::emit(Entry& e, int pid, std::vector<std::vector<ProcSample>>* per_dev, uint64_t now_ns) {
+  char buf[128];
+  int ok = 0;
+  e.seen = scan_no_;
+  for (auto& pd : e.devs) {
+    {
       uint64_t v = 0;
       if (!pd.vram.read_u64(&v)) continue;  // process exiting
+      ++ok;
       ProcSample ps;
       ps.pid = pid;
       ps.device = pd.dev;
@@ -71,9 +89,7 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
       (*per_dev)[size_t(pd.dev)].push_back(ps);
     }
   }
-  // Forget processes that left the KFD proc directory (closes their fds).
-  for (auto it = pids_.begin(); it != pids_.end();)
-    it = it->second.seen != scan_no_ ? pids_.erase(it) : std::next(it);
+  return ok;
 }
 
 // ---------------------------------------------------------------------------------

@@ -44,6 +44,8 @@ class KfdProcReader {
     std::string comm;
     uint64_t seen = 0;
   };
+  // Appends the entry's per-GPU samples; returns how many vram reads succeeded.
+  int emit(Entry& e, int pid, std::vector<std::vector<ProcSample>>* per_dev, uint64_t now_ns);
   std::string root_;
   int self_;
   bool read_cu_;

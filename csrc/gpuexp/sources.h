@@ -61,9 +61,15 @@ struct RcclTotals {
 class RcclSource {
  public:
   virtual ~RcclSource() = default;
-  // Drains every ring under `dir` and returns cumulative per-(pid, op) totals.
+  // Reads every tracer file under `dir` and returns cumulative per-(pid, op) totals of the
+  // writers that could be identified and are still alive.
   virtual void poll(std::vector<RcclTotals>* out) = 0;
+  // Files by state after the last poll: exported, writer not (yet) identified, writer gone.
+  virtual void file_states(int* active, int* unverified, int* exited) const {
+    *active = *unverified = *exited = 0;
+  }
 };
-std::unique_ptr<RcclSource> make_rccl_source(const std::string& dir);
+// verify_maps: a file is attributed only to a process that maps it (/proc/<pid>/maps).
+std::unique_ptr<RcclSource> make_rccl_source(const std::string& dir, bool verify_maps = true);
 
 }  // namespace gpuexp

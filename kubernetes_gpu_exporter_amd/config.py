@@ -51,6 +51,7 @@ class Config:
     counters_interval_ms: int = 1000       # ... per interval (context-started spin is duty-cycled)
     enable_rccl: bool = False
     rccl_dir: str = "/var/run/gpuexp/rccl"
+    rccl_verify: bool = True               # a tracer file counts only for a live process that maps it
     # attribution / kubernetes control plane
     pod_attribution: bool = True
     infer_device_owner: bool = True
@@ -135,6 +136,7 @@ class Config:
         ec.counters_interval_ms = int(self.counters_interval_ms)
         ec.enable_rccl = bool(self.enable_rccl)
         ec.rccl_dir = self.rccl_dir
+        ec.rccl_verify = bool(self.rccl_verify)
         ec.gc_after = int(self.gc_after)
         ec.device_filter = [int(d) for d in self.devices if ":" not in str(d)]
         ec.device_filter_bdf = [str(d) for d in self.devices if ":" in str(d)]

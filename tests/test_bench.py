@@ -63,7 +63,7 @@ def test_bench_self_launches_one_rank_per_gpu():
     assert d["attributed_pods"] == [f"gemm-pod-{i}" for i in range(4)]
     assert sorted(d["series_per_gpu"]) == ["0", "1", "2", "3"]
     assert d["p99_scrape_us"] is None  # 4 samples: no p99 claimed
-    assert d["server_scrapes"] >= 8 and d["server_scrape_p99_le_us"] > 0
+    assert d["server_scrapes"] >= 3 and d["server_scrape_p99_le_us"] > 0
     assert d["sampler_cpu_us_per_tick_per_gpu"] > 0 and d["exporter_rss_mb"] > 0
     assert "measured_over_expected_write" in d["xgmi_timed_window"]
 

@@ -50,6 +50,7 @@ def test_compact_and_legacy_profiles(mock_engine):
     e2 = mock_engine(1, http=False, series_profile="legacy")
     e2.mock_set_processes(0, [dict(pid=100, vram_bytes=1e9)])
     e2.set_pid_cgroup(100, CG)
+    e2.set_pods([dict(uid=UID, namespace="ml", name="trainer-0", containers={})])
     ticks(e2, 2)
     fams = parse(e2)
     assert not [n for n in fams if n.startswith("amd_")]
@@ -79,6 +80,7 @@ def test_legacy_sums_over_gpus_and_skips_unattributed(mock_engine):
     e.mock_set_processes(0, [dict(pid=10, vram_bytes=100.0), dict(pid=11, vram_bytes=5.0)])
     e.mock_set_processes(1, [dict(pid=10, vram_bytes=300.0)])
     e.set_pid_cgroup(10, CG)  # pid 11 has no pod
+    e.set_pods([dict(uid=UID, namespace="ml", name="trainer-0", containers={})])
     ticks(e, 2)
     fams = parse(e)
     assert promtext.value(fams, "pod_gpu_memory_usage", pid=10) == 400.0
@@ -88,8 +90,14 @@ def test_legacy_sums_over_gpus_and_skips_unattributed(mock_engine):
         promtext.value(fams, "pod_gpu_memory_usage", pid=11)
     # the new per-process family keeps unattributed processes (pod="")
     assert promtext.value(fams, "amd_gpu_process_vram_bytes", pid=11, pod="") == 5.0
-    # pod name unknown to the control plane -> pod label falls back to the UID
-    assert promtext.value(fams, "pod_gpu_memory_usage", pid=10, pod=UID) == 400.0
+    assert promtext.value(fams, "pod_gpu_memory_usage", pid=10, pod="trainer-0") == 400.0
+    # pod name unknown to the control plane -> no legacy series (never the UID as `pod`)
+    e.set_pods([])
+    ticks(e, 2, t0=10 * S)
+    fams = parse(e)
+    with pytest.raises(KeyError):
+        promtext.value(fams, "pod_gpu_memory_usage", pid=10)
+    assert promtext.value(fams, "amd_gpu_process_vram_bytes", pid=10, gpu=1, pod="") == 300.0
 
 
 def test_process_exit_removes_series_next_tick(mock_engine):
@@ -199,10 +207,16 @@ def test_shared_gpu_has_no_owner(mock_engine):
     e.mock_set_processes(0, [dict(pid=5, vram_bytes=1.0), dict(pid=6, vram_bytes=2.0)])
     e.set_pid_cgroup(5, CG)
     e.set_pid_cgroup(6, cg2)
+    e.set_pods([dict(uid=UID, namespace="a", name="pod-a", containers={}),
+                dict(uid=uid2, namespace="b", name="pod-b", containers={})])
     ticks(e, 2)
     fams = parse(e)
     assert fams["amd_gpu_up"].samples[0][1]["pod"] == ""
-    assert promtext.value(fams, "amd_pod_gpu_vram_bytes", pod=uid2) == 2.0
+    assert promtext.value(fams, "amd_pod_gpu_vram_bytes", pod="pod-b") == 2.0
+    # one named pod + one not yet named: ownership is unknown, not the named pod's
+    e.set_pods([dict(uid=UID, namespace="a", name="pod-a", containers={})])
+    ticks(e, 2, t0=10 * S)
+    assert parse(e)["amd_gpu_up"].samples[0][1]["pod"] == ""
 
 
 def test_self_metrics(mock_engine):
@@ -291,12 +305,14 @@ def test_gfx_activity_split_over_processes_and_pods(mock_engine):
     e.set_pid_cgroup(5, CG)
     e.set_pid_cgroup(6, cg2)
     e.set_pid_cgroup(7, cg2)
+    e.set_pods([dict(uid=UID, namespace="a", name="pod-1", containers={}),
+                dict(uid=uid2, namespace="b", name="pod-2", containers={})])
     ticks(e, 2)
     fams = parse(e)
     share = {s[1]["pid"]: s[2] for s in promtext.samples(fams, "amd_gpu_process_gfx_activity_percent")}
     assert share == {"5": 60.0, "6": 20.0, "7": 80.0}
     pod = {s[1]["pod"]: s[2] for s in promtext.samples(fams, "amd_pod_gfx_activity_share_percent")}
-    assert pod == {UID: 60.0, uid2: 100.0}  # 20% of GPU 0 + 80% of GPU 1
+    assert pod == {"pod-1": 60.0, "pod-2": 100.0}  # 20% of GPU 0 + 80% of GPU 1
     # nothing resident at the CU sample: an even split, never a division by zero
     e.mock_set_processes(0, [dict(pid=5, cu_occupancy=0), dict(pid=6, cu_occupancy=0)])
     ticks(e, 1, t0=10 * S)

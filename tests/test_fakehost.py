@@ -144,15 +144,68 @@ def test_pid_reuse_is_detected(native, tmp_path):
     h = mi355x_node(tmp_path, 1)
     g0 = h.gpus[0]
     h.add_process(300, kubepods_cgroup(UID, CID), gpus={g0.gpu_id: (10, 0)}, starttime=1000)
+    uid2 = "11111111-2222-3333-4444-555555555555"
     e = _engine(native, tmp_path)
     try:
+        e.set_pods([dict(uid=UID, namespace="a", name="first", containers={}),
+                    dict(uid=uid2, namespace="b", name="second", containers={})])
         e.tick(S)
-        assert 'pod_gpu_memory_usage{pid="300",pod="' + UID + '"}' in e.snapshot_text()
-        uid2 = "11111111-2222-3333-4444-555555555555"
+        assert 'pod_gpu_memory_usage{pid="300",pod="first"}' in e.snapshot_text()
         h.remove_process(300)
         h.add_process(300, kubepods_cgroup(uid2, CID), gpus={g0.gpu_id: (10, 0)}, starttime=2000)
         e.tick(2 * S)
-        assert 'pod_gpu_memory_usage{pid="300",pod="' + uid2 + '"}' in e.snapshot_text()
+        assert 'pod_gpu_memory_usage{pid="300",pod="second"}' in e.snapshot_text()
+    finally:
+        e.stop()
+
+
+def test_kfd_entry_reopened_when_pid_is_reused(native, tmp_path):
+    """Between two scans PID 310 exits and a new process gets the same PID: the cached
+    sysfs fds of the old KFD directory go dead (reads fail, simulated by emptying the old
+    files), the directory exists again -> the reader reopens it and picks up the new
+    process's comm and VRAM instead of skipping it."""
+    h = mi355x_node(tmp_path, 1)
+    g0 = h.gpus[0]
+    h.add_process(310, "/user.slice", comm="old", gpus={g0.gpu_id: (111, 0)})
+    e = _engine(native, tmp_path)
+    try:
+        e.tick(S)
+        assert promtext.value(promtext.parse(e.snapshot_text()), "amd_gpu_process_vram_bytes", pid=310,
+                              comm="old") == 111
+        kfd = tmp_path / f"sys/class/kfd/kfd/proc/310"
+        for f in kfd.rglob("*"):
+            if f.is_file():
+                f.write_text("")  # a removed kobject: reads of the old fds fail
+        h.remove_process(310)
+        h.add_process(310, "/user.slice", comm="new", gpus={g0.gpu_id: (222, 0)}, starttime=5000)
+        e.tick(2 * S)
+        fams = promtext.parse(e.snapshot_text())
+        assert promtext.value(fams, "amd_gpu_process_vram_bytes", pid=310, comm="new") == 222
+    finally:
+        e.stop()
+
+
+def test_unresolved_pod_uid_is_never_a_pod_label(native, tmp_path):
+    """Until the control plane knows a pod's name, its processes carry pod="" in the new
+    families and no legacy series at all (a UID in `pod` would flip series identity to the
+    name later); the unresolved UID count is exported instead."""
+    h = mi355x_node(tmp_path, 1)
+    g0 = h.gpus[0]
+    h.add_process(320, kubepods_cgroup(UID, CID), gpus={g0.gpu_id: (77, 0)})
+    e = _engine(native, tmp_path)
+    try:
+        e.tick(S)
+        text = e.snapshot_text()
+        assert UID not in text
+        assert "pod_gpu_memory_usage{" not in text
+        fams = promtext.parse(text)
+        assert promtext.value(fams, "amd_gpu_process_vram_bytes", pid=320, pod="") == 77
+        assert promtext.value(fams, "gpuexp_pods_unresolved") == 1
+        e.set_pods([dict(uid=UID, namespace="ns", name="named", containers={CID: "c"})])
+        e.tick(2 * S)
+        fams = promtext.parse(e.snapshot_text())
+        assert promtext.value(fams, "pod_gpu_memory_usage", pid=320, pod="named") == 77
+        assert promtext.value(fams, "gpuexp_pods_unresolved") == 0
     finally:
         e.stop()
 

@@ -78,6 +78,42 @@ def test_keepalive_and_pipelining(mock_engine):
     assert b"Connection: close" in data
 
 
+def test_pipelined_request_behind_a_partial_write(native):
+    """A response too big for the socket buffer completes on the EPOLLOUT path; the
+    request pipelined behind it (already read) must be answered then, not at idle timeout."""
+    c = native.EngineConfig()
+    c.backend = "mock"
+    c.mock_devices = 8
+    c.series_profile = "full"
+    c.interval_s = 0
+    c.http.host = "127.0.0.1"
+    c.http.port = 0
+    c.http.socket_sndbuf = 4096
+    e = native.Engine(c)
+    e.start()
+    try:
+        e.tick(1_000_000_000)
+        body_len = len(e.snapshot_text())
+        assert body_len > 32 << 10
+        s = socket.socket()
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4096)  # before connect: small window
+        s.connect(("127.0.0.1", e.http_port))
+        s.sendall(b"GET /metrics HTTP/1.1\r\nHost: x\r\n\r\nGET /healthz HTTP/1.1\r\nHost: x\r\n\r\n")
+        time.sleep(0.3)  # let the server fill both buffers and park on EPOLLOUT
+        s.settimeout(3.0)
+        data = b""
+        t0 = time.monotonic()
+        while not data.endswith(b"ok\n"):
+            chunk = s.recv(1 << 16)
+            assert chunk, "connection closed early"
+            data += chunk
+        assert time.monotonic() - t0 < 3.0
+        assert data.count(b"HTTP/1.1 200 OK") == 2
+        s.close()
+    finally:
+        e.stop()
+
+
 def test_gzip_negotiation(mock_engine):
     e = mock_engine(1)
     e.tick(1_000_000_000)

@@ -1,8 +1,16 @@
 """RCCL tracer shared-memory protocol (csrc/gpuexp/rccl_shm.h) -> per-pod collective
-series, without a GPU: the test plays the tracer's role and writes the file itself."""
+series, without a GPU: the test (or a child process) plays the tracer's role and writes
+the file itself.  The directory is writable by every workload pod, so the reader is also
+tested against hostile files: FIFOs, symlinks, truncation, identities that do not match,
+writers that claim another process, and files left behind by killed writers."""
 import mmap
 import os
+import signal
 import struct
+import subprocess
+import sys
+import textwrap
+import time
 
 from kubernetes_gpu_exporter_amd.utils import promtext
 
@@ -12,27 +20,42 @@ OPS = ["allreduce", "allgather", "reducescatter", "alltoall", "alltoallv", "broa
 SIZE = 64 + 16 * 16
 UID = "12345678-1234-1234-1234-123456789abc"
 CG = "/kubepods/burstable/pod" + UID + "/" + "b" * 64
+NS_INO = os.stat("/proc/self/ns/pid").st_ino
 
 
-def write_shm(path, ns_pid, ops):
+def shm_name(pid, ino=NS_INO):
+    return f"gpuexp-rccl-{ino}-{pid}"
+
+
+def write_shm(path, ns_pid, ops, ino=NS_INO):
+    """Creates the file and maps it in THIS process (as the tracer does in the workload)."""
     with open(path, "wb") as fh:
         fh.write(b"\0" * SIZE)
     fd = os.open(path, os.O_RDWR)
     m = mmap.mmap(fd, SIZE)
     os.close(fd)
-    struct.pack_into("<QIiQii", m, 0, 0, 1, ns_pid, os.stat("/proc/self/ns/pid").st_ino, 0, 4)
+    struct.pack_into("<QIiQii", m, 0, 0, 1, ns_pid, ino, 0, 4)
     for name, (calls, nbytes) in ops.items():
         struct.pack_into("<QQ", m, 64 + 16 * OPS.index(name), calls, nbytes)
     struct.pack_into("<Q", m, 0, MAGIC)  # publish
     return m
 
 
+def rccl_engine(mock_engine, d, **kw):
+    return mock_engine(1, http=False, enable_rccl=True, rccl_dir=str(d), **kw)
+
+
+def states(e):
+    fams = promtext.parse(e.snapshot_text())
+    return {lab["state"]: v for _, lab, v in promtext.samples(fams, "gpuexp_rccl_files")}
+
+
 def test_rccl_counters_attributed_to_pod(mock_engine, tmp_path):
     d = tmp_path / "rccl"
     d.mkdir()
-    pid = 31337
-    m = write_shm(str(d / f"gpuexp-rccl-1-{pid}"), pid, {"allreduce": (10, 10 * 64 << 20), "send": (3, 3000)})
-    e = mock_engine(1, http=False, enable_rccl=True, rccl_dir=str(d))
+    pid = os.getpid()
+    m = write_shm(str(d / shm_name(pid)), pid, {"allreduce": (10, 10 * 64 << 20), "send": (3, 3000)})
+    e = rccl_engine(mock_engine, d)
     e.set_pid_cgroup(pid, CG)
     e.set_pods([dict(uid=UID, namespace="train", name="dp-worker-0", containers={})])
     e.tick(1_000_000_000)
@@ -43,21 +66,137 @@ def test_rccl_counters_attributed_to_pod(mock_engine, tmp_path):
     assert promtext.value(fams, "amd_rccl_collective_calls_total", op="send") == 3
     # rank / size of the process's communicator (the file says rank 0 of 4)
     assert promtext.value(fams, "amd_rccl_communicator_info", pod="dp-worker-0", rank=0, nranks=4) == 1
-    # the tracer keeps counting; the exporter reads the live mapping
+    assert states(e) == {"active": 1, "unverified": 0, "exited": 0}
+    # the tracer keeps counting; the exporter copies the file every tick
     struct.pack_into("<QQ", m, 64, 25, 25 * 64 << 20)
     e.tick(2_000_000_000)
     fams = promtext.parse(e.snapshot_text())
     assert promtext.value(fams, "amd_rccl_collective_calls_total", op="allreduce") == 25
     # process gone (file unlinked by the tracer at exit) -> series vanish
-    os.unlink(d / f"gpuexp-rccl-1-{pid}")
+    os.unlink(d / shm_name(pid))
+    e.tick(3_000_000_000)
+    assert "amd_rccl_collective_calls_total" not in e.snapshot_text()
+    m.close()
+
+
+def test_incomplete_file_ignored(mock_engine, tmp_path):
+    pid = os.getpid()
+    (tmp_path / shm_name(5)).write_bytes(b"\0" * 10)  # truncated
+    full = write_shm(str(tmp_path / shm_name(pid)), pid, {"alltoall": (1, 8)})
+    struct.pack_into("<Q", full, 0, 0)  # magic not yet published
+    e = rccl_engine(mock_engine, tmp_path)
+    e.tick(1)
+    assert "amd_rccl_collective" not in e.snapshot_text()
+    full.close()
+
+
+def test_hostile_files_do_not_block_or_crash(mock_engine, tmp_path):
+    """A FIFO (an O_RDONLY open would block the sampler forever), a symlink to a real
+    counters file, and a file truncated under the reader (a live MAP_SHARED mapping would
+    SIGBUS) are all harmless."""
+    pid = os.getpid()
+    real = tmp_path / "elsewhere"
+    real.mkdir()
+    m_real = write_shm(str(real / shm_name(pid)), pid, {"allreduce": (7, 7)})
+    d = tmp_path / "rccl"
+    d.mkdir()
+    os.mkfifo(d / shm_name(pid + 1))
+    os.symlink(real / shm_name(pid), d / shm_name(pid))
+    e = rccl_engine(mock_engine, d)
+    t0 = time.monotonic()
+    e.tick(1_000_000_000)
+    assert time.monotonic() - t0 < 2.0
+    assert "amd_rccl_collective" not in e.snapshot_text()
+    # now a genuine file, read once, then truncated by its writer
+    os.unlink(d / shm_name(pid))
+    m = write_shm(str(d / shm_name(pid)), pid, {"allreduce": (3, 300)})
+    e.tick(2_000_000_000)
+    assert promtext.value(promtext.parse(e.snapshot_text()), "amd_rccl_collective_calls_total", op="allreduce") == 3
+    os.truncate(d / shm_name(pid), 8)
+    e.tick(3_000_000_000)  # no SIGBUS; the short file is simply not read
+    assert "amd_rccl_collective_calls_total" not in e.snapshot_text()
+    m.close()
+    m_real.close()
+
+
+def test_identity_must_match_name_and_be_nonzero(mock_engine, tmp_path):
+    pid = os.getpid()
+    m1 = write_shm(str(tmp_path / shm_name(pid + 7)), pid, {"allreduce": (1, 1)})        # name != content pid
+    m2 = write_shm(str(tmp_path / shm_name(pid, ino=0)), pid, {"allreduce": (1, 1)}, ino=0)  # ns inode 0
+    e = rccl_engine(mock_engine, tmp_path)
+    e.tick(1)
+    assert "amd_rccl_collective" not in e.snapshot_text()
+    m1.close()
+    m2.close()
+
+
+def _writer(d, claim_pid=None):
+    """A child that creates + maps its counters file (optionally claiming another PID in
+    its content and name) and then sleeps until killed."""
+    code = textwrap.dedent(f"""
+        import mmap, os, struct, sys, time
+        pid = {claim_pid!r} or os.getpid()
+        ino = os.stat('/proc/self/ns/pid').st_ino
+        p = os.path.join({str(d)!r}, f'gpuexp-rccl-{{ino}}-{{pid}}')
+        with open(p, 'wb') as fh:
+            fh.write(b'\\0' * {SIZE})
+        fd = os.open(p, os.O_RDWR); m = mmap.mmap(fd, {SIZE}); os.close(fd)
+        struct.pack_into('<QIiQii', m, 0, 0, 1, pid, ino, 1, 2)
+        struct.pack_into('<QQ', m, 64, 5, 500)
+        struct.pack_into('<Q', m, 0, {MAGIC})
+        print(p, flush=True)
+        time.sleep(600)
+    """)
+    p = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True)
+    path = p.stdout.readline().strip()
+    return p, path
+
+
+def test_writer_cannot_claim_another_process(mock_engine, tmp_path):
+    """A pod that names someone else's PID (here: this test process, which does not map
+    the file) gets nothing attributed, and the failed lookup backs off."""
+    victim = os.getpid()
+    p, path = _writer(tmp_path, claim_pid=victim)
+    try:
+        e = rccl_engine(mock_engine, tmp_path)
+        e.tick(1)
+        assert "amd_rccl_collective" not in e.snapshot_text()
+        assert states(e)["unverified"] == 1
+    finally:
+        p.kill()
+        p.wait()
+
+
+def test_killed_writer_file_stops_counting(mock_engine, tmp_path):
+    """SIGKILL leaves the file behind (no unlink at exit): its series must go at the next
+    tick and stay gone, even though the file is still there."""
+    p, path = _writer(tmp_path)
+    try:
+        e = rccl_engine(mock_engine, tmp_path)
+        e.tick(1_000_000_000)
+        fams = promtext.parse(e.snapshot_text())
+        assert promtext.value(fams, "amd_rccl_collective_calls_total", pid=p.pid, op="allreduce") == 5
+        assert promtext.value(fams, "amd_rccl_communicator_info", pid=p.pid, rank=1, nranks=2) == 1
+    finally:
+        p.send_signal(signal.SIGKILL)
+        p.wait()
+    assert os.path.exists(path)
+    e.tick(2_000_000_000)
+    assert "amd_rccl_collective_calls_total" not in e.snapshot_text()
+    assert states(e) == {"active": 0, "unverified": 0, "exited": 1}
     e.tick(3_000_000_000)
     assert "amd_rccl_collective_calls_total" not in e.snapshot_text()
 
 
-def test_incomplete_file_ignored(mock_engine, tmp_path):
-    (tmp_path / "gpuexp-rccl-1-5").write_bytes(b"\0" * 10)  # truncated
-    full = write_shm(str(tmp_path / "gpuexp-rccl-1-6"), 6, {"alltoall": (1, 8)})
-    struct.pack_into("<Q", full, 0, 0)  # magic not yet published
-    e = mock_engine(1, http=False, enable_rccl=True, rccl_dir=str(tmp_path))
-    e.tick(1)
-    assert "amd_rccl" not in e.snapshot_text()
+def test_verification_can_be_relaxed(mock_engine, tmp_path):
+    """rccl_verify=false (trusted single-tenant hosts): namespace + PID checks only."""
+    victim = os.getpid()
+    p, path = _writer(tmp_path, claim_pid=victim)
+    try:
+        e = rccl_engine(mock_engine, tmp_path, rccl_verify=False)
+        e.tick(1)
+        fams = promtext.parse(e.snapshot_text())
+        assert promtext.value(fams, "amd_rccl_collective_calls_total", pid=victim, op="allreduce") == 5
+    finally:
+        p.kill()
+        p.wait()
