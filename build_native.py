@@ -37,7 +37,8 @@ CORE_CC = [
 ]
 SENTINEL_HIP = ["gpuexp/sentinel.hip"]
 SENTINEL_HSACO = "gpuexp/sentinel_hsaco.hip"  # device-only code object for raw AQL dispatch
-KERNELS_HIP = ["kernels/gemm_bf16.hip", "kernels/kernels_bindings.hip"]
+CALIB_HSACO = "kernels/calib_hsaco.hip"       # PMC calibration workloads, dispatched on the PMC queue
+KERNELS_HIP = ["kernels/gemm_bf16.hip", "kernels/probe_kernels.hip", "kernels/kernels_bindings.hip"]
 ROCPROF_CC = ["gpuexp/rocprof_plugin.cc"]
 AQLPMC_CC = ["gpuexp/aql_pmc.cc"]
 TRACER_CC = ["gpuexp/rccl_tracer.cc"]
@@ -159,6 +160,7 @@ def build(force: bool = False, jobs: int = 8, sanitize: str | None = None, verbo
         outputs["aqlpmc_plugin"] = str(link_plain([objs[AQLPMC_CC[0]]], PKG / "_gpuexp_aqlpmc.so",
                                                   ["-lhsa-runtime64", "-lpthread"]))
         outputs["sentinel_hsaco"] = str(build_hsaco(SENTINEL_HSACO, PKG / "gpuexp_sentinel.hsaco", hdr, force))
+        outputs["calib_hsaco"] = str(build_hsaco(CALIB_HSACO, PKG / "gpuexp_calib.hsaco", hdr, force))
     if (CSRC / TRACER_CC[0]).exists():
         outputs["rccl_tracer"] = str(link_plain([objs[TRACER_CC[0]]], PKG / "libgpuexp_rccl_tracer.so",
                                                 ["-lrocprofiler-sdk", "-lpthread"]))

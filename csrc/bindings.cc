@@ -4,6 +4,7 @@
 #include <pybind11/stl.h>
 
 #include <cmath>
+#include <cstring>
 
 #include "gpuexp/backends.h"
 #include "gpuexp/client.h"
@@ -85,9 +86,31 @@ py::dict sample_dict(const DeviceSample& s) {
   o["accumulation_counter"] = s.accumulation_counter;
   o["res_ppt"] = s.res_ppt;
   o["vram_max_bw_gbs"] = s.vram_max_bw_gbs;
-  py::list busy;
-  for (int c = 0; c < kMaxXcc; ++c) busy.append(s.gfx_busy_acc[c]);
+  py::list busy, xclk;
+  for (int c = 0; c < kMaxXcc; ++c) {
+    busy.append(s.gfx_busy_acc[c]);
+    xclk.append(s.clk_gfx_xcc[c]);
+  }
   o["gfx_busy_acc"] = busy;
+  o["clk_gfx_xcc"] = xclk;
+  o["energy_valid"] = s.energy_valid;
+  o["energy_unit_j"] = s.energy_unit_j;
+  o["residency_valid"] = s.residency_valid;
+  o["res_prochot"] = s.res_prochot;
+  o["res_socket_thm"] = s.res_socket_thm;
+  o["res_vr_thm"] = s.res_vr_thm;
+  o["res_hbm_thm"] = s.res_hbm_thm;
+  o["pcie_bw_acc"] = s.pcie_bw_acc;
+  o["pcie_replay"] = s.pcie_replay;
+  o["pcie_nak_sent"] = s.pcie_nak_sent;
+  o["pcie_nak_rcvd"] = s.pcie_nak_rcvd;
+  o["pcie_l0_recov"] = s.pcie_l0_recov;
+  o["xgmi_width"] = s.xgmi_width;
+  o["xgmi_speed"] = s.xgmi_speed;
+  o["num_partition"] = s.num_partition;
+  o["temp_edge"] = s.temp_edge;
+  o["temp_vrgfx"] = s.temp_vrgfx;
+  o["temp_vrmem"] = s.temp_vrmem;
   return o;
 }
 
@@ -141,6 +164,78 @@ PYBIND11_MODULE(_gpuexp, m) {
     if (!decode_gpu_metrics_v1_8(b.data(), b.size(), &s)) return py::none();
     s.ok = true;
     return sample_dict(s);
+  });
+  m.def("decode_gpu_metrics_raw", [](py::bytes blob) -> py::object {
+    // Every field of the v1.8 blob as stored, keyed by the amdsmi Python binding's names
+    // (amdsmi_get_gpu_metrics_info), for field-by-field parity checks on hardware.
+    std::string b = blob;
+    if (b.size() < sizeof(GpuMetricsV1_8)) return py::none();
+    GpuMetricsV1_8 g;
+    std::memcpy(&g, b.data(), sizeof(g));
+    if (g.header.format_revision != 1 || g.header.content_revision != 8) return py::none();
+    py::dict o;
+    o["temperature_hotspot"] = g.temperature_hotspot;
+    o["temperature_mem"] = g.temperature_mem;
+    o["temperature_vrsoc"] = g.temperature_vrsoc;
+    o["current_socket_power"] = g.curr_socket_power;
+    o["average_gfx_activity"] = g.average_gfx_activity;
+    o["average_umc_activity"] = g.average_umc_activity;
+    o["vram_max_bandwidth"] = g.mem_max_bandwidth;
+    o["energy_accumulator"] = g.energy_accumulator;
+    o["system_clock_counter"] = g.system_clock_counter;
+    o["accumulation_counter"] = g.accumulation_counter;
+    o["prochot_residency_acc"] = g.prochot_residency_acc;
+    o["ppt_residency_acc"] = g.ppt_residency_acc;
+    o["socket_thm_residency_acc"] = g.socket_thm_residency_acc;
+    o["vr_thm_residency_acc"] = g.vr_thm_residency_acc;
+    o["hbm_thm_residency_acc"] = g.hbm_thm_residency_acc;
+    o["gfxclk_lock_status"] = g.gfxclk_lock_status;
+    o["pcie_link_width"] = g.pcie_link_width;
+    o["pcie_link_speed"] = g.pcie_link_speed;
+    o["xgmi_link_width"] = g.xgmi_link_width;
+    o["xgmi_link_speed"] = g.xgmi_link_speed;
+    o["gfx_activity_acc"] = g.gfx_activity_acc;
+    o["mem_activity_acc"] = g.mem_activity_acc;
+    o["pcie_bandwidth_acc"] = g.pcie_bandwidth_acc;
+    o["pcie_bandwidth_inst"] = g.pcie_bandwidth_inst;
+    o["pcie_l0_to_recov_count_acc"] = g.pcie_l0_to_recov_count_acc;
+    o["pcie_replay_count_acc"] = g.pcie_replay_count_acc;
+    o["pcie_replay_rover_count_acc"] = g.pcie_replay_rover_count_acc;
+    o["pcie_nak_sent_count_acc"] = g.pcie_nak_sent_count_acc;
+    o["pcie_nak_rcvd_count_acc"] = g.pcie_nak_rcvd_count_acc;
+    o["firmware_timestamp"] = g.firmware_timestamp;
+    o["current_uclk"] = g.current_uclk;
+    o["num_partition"] = g.num_partition;
+    o["pcie_lc_perf_other_end_recovery"] = g.pcie_lc_perf_other_end_recovery;
+    auto l64 = [](const uint64_t* p, int n) {
+      py::list l;
+      for (int i = 0; i < n; ++i) l.append(p[i]);
+      return l;
+    };
+    auto l16 = [](const uint16_t* p, int n) {
+      py::list l;
+      for (int i = 0; i < n; ++i) l.append(p[i]);
+      return l;
+    };
+    o["xgmi_read_data_acc"] = l64(g.xgmi_read_data_acc, 8);
+    o["xgmi_write_data_acc"] = l64(g.xgmi_write_data_acc, 8);
+    o["xgmi_link_status"] = l16(g.xgmi_link_status, 8);
+    o["current_gfxclks"] = l16(g.current_gfxclk, 8);
+    o["current_socclks"] = l16(g.current_socclk, 4);
+    o["current_vclk0s"] = l16(g.current_vclk0, 4);
+    o["current_dclk0s"] = l16(g.current_dclk0, 4);
+    py::list busy_acc, busy_inst, low_util;
+    for (int x = 0; x < 8; ++x) {
+      busy_acc.append(l64(g.xcp_stats[x].gfx_busy_acc, 8));
+      low_util.append(l64(g.xcp_stats[x].gfx_low_utilization_acc, 8));
+      py::list inst;
+      for (int i = 0; i < 8; ++i) inst.append(g.xcp_stats[x].gfx_busy_inst[i]);
+      busy_inst.append(inst);
+    }
+    o["xcp_stats.gfx_busy_acc"] = busy_acc;
+    o["xcp_stats.gfx_busy_inst"] = busy_inst;
+    o["xcp_stats.gfx_low_utilization_acc"] = low_util;
+    return o;
   });
   m.def("gpu_metrics_v1_8_size", []() { return sizeof(GpuMetricsV1_8); });
   m.def("uuid_from_unique_id", &SysfsBackend::uuid_from_unique_id);

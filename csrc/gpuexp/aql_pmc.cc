@@ -43,6 +43,7 @@
 #include <unistd.h>
 
 #include "gpuexp/counter_model.h"
+#include "kernels/probe_args.h"
 #include "gpuexp/sentinel_common.h"
 #include "gpuexp/sources.h"
 
@@ -249,7 +250,7 @@ bool setup_agent(Agent& a, std::string* why) {
   hsa_agent_get_info(a.gpu, hsa_agent_info_t(HSA_AMD_AGENT_INFO_COMPUTE_UNIT_COUNT), &cu);
   hsa_agent_get_info(a.gpu, hsa_agent_info_t(HSA_AMD_AGENT_INFO_NUM_SIMDS_PER_CU), &simd_per_cu);
   a.m.cu = cu;
-  a.m.privileged = process_has_pmc_privilege();
+  a.m.privileged = pmc_device_scope();
   a.m.simd = cu * simd_per_cu;
 
   hsa_ven_amd_aqlprofile_profile_t probe{};
@@ -449,16 +450,16 @@ hsa_status_t pick_uncached_pool(hsa_amd_memory_pool_t pool, void* data) {
   return HSA_STATUS_SUCCESS;
 }
 
-// One kernel dispatch packet (1-D grid of `groups` x 64 lanes) on the agent's queue.
-void dispatch(Agent& a, const KernelSym& k, void* kernarg, uint32_t groups, hsa_signal_t done) {
+// One kernel dispatch packet (1-D grid of `groups` x `wg` lanes) on the agent's queue.
+void dispatch(Agent& a, const KernelSym& k, void* kernarg, uint32_t groups, hsa_signal_t done, uint16_t wg = 64) {
   std::lock_guard<std::mutex> lk(a.submit_mu);
   hsa_queue_t* q = a.queue;
   const uint64_t idx = hsa_queue_add_write_index_screlease(q, 1);
   auto* pkt = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address) + (idx & (q->size - 1));
-  pkt->workgroup_size_x = 64;
+  pkt->workgroup_size_x = wg;
   pkt->workgroup_size_y = 1;
   pkt->workgroup_size_z = 1;
-  pkt->grid_size_x = groups * 64;
+  pkt->grid_size_x = groups * wg;
   pkt->grid_size_y = 1;
   pkt->grid_size_z = 1;
   pkt->private_segment_size = k.priv;
@@ -755,6 +756,102 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_debug(int dev, c
     s += t;
   }
   std::snprintf(buf, size_t(len), "%s", s.c_str());
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// Calibration (tests/test_gpu.py::test_device_scope_pmc_calibration, tools/pmc_validate.py).
+// An unprivileged process's agent-mode SQ/TCC counters count only the dispatches of the
+// queue that programs them (profiles/r02/pmc_scope.txt), so known work is dispatched HERE,
+// on the PMC queue, while the counting windows run:
+//   kind 0: stream copy of 1 GiB (gpuexp_calib_copy): HBM read = write = 1 GiB per launch
+//   kind 1: conflict-free LDS reads; kind 2: the same reads 32-way bank-conflicted
+// 4096 blocks x 4 waves per launch, at most 4 launches queued so the windows' PM4 packets
+// never wait long behind them.  out[0] = seconds, out[1] = waves per launch,
+// out[2] = HBM bytes read per launch.  Returns 0, or -1 (see stderr).
+// ---------------------------------------------------------------------------------------
+extern "C" __attribute__((visibility("default"))) int gpuexp_rp_calibrate(int dev, int kind, int launches,
+                                                                          double* out) {
+  Agent* a = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (dev >= 0 && size_t(dev) < g_agents.size()) a = g_agents[size_t(dev)];
+  }
+  auto fail = [](const char* why) {
+    std::fprintf(stderr, "[aqlpmc] calibrate: %s\n", why);
+    return -1;
+  };
+  if (!a || !a->ready || a->broken) return fail("no working PMC queue for this device");
+  if (kind < 0 || kind > 2 || launches < 1 || launches > 1000000) return fail("bad arguments");
+  const std::string path = plugin_dir() + "/gpuexp_calib.hsaco";
+  const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return fail("cannot open gpuexp_calib.hsaco");
+  hsa_code_object_reader_t reader{};
+  hsa_executable_t exe{};
+  bool have_exe = false;
+  bool ok = hsa_code_object_reader_create_from_file(fd, &reader) == HSA_STATUS_SUCCESS;
+  if (ok) {
+    have_exe = hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr,
+                                         &exe) == HSA_STATUS_SUCCESS;
+    ok = have_exe && hsa_executable_load_agent_code_object(exe, a->gpu, reader, nullptr, nullptr) == HSA_STATUS_SUCCESS &&
+         hsa_executable_freeze(exe, nullptr) == HSA_STATUS_SUCCESS;
+    hsa_code_object_reader_destroy(reader);
+  }
+  ::close(fd);
+  KernelSym k;
+  ok = ok && lookup(exe, a->gpu, kind == 0 ? "gpuexp_calib_copy.kd" : "gpuexp_calib_lds.kd", &k) && k.kernarg <= 64;
+  if (!ok) {
+    if (have_exe) hsa_executable_destroy(exe);
+    return fail("cannot load the calibration code object");
+  }
+  constexpr uint32_t kBlocks = 4096;
+  constexpr size_t kCopyBytes = size_t(1) << 30;
+  hsa_amd_memory_pool_t pool{};
+  hsa_amd_agent_iterate_memory_pools(a->gpu, pick_uncached_pool, &pool);
+  void* buf = nullptr;
+  const size_t bytes = kind == 0 ? 2 * kCopyBytes : kBlocks * sizeof(float);
+  char* ka = static_cast<char*>(sys_alloc(64, a->gpu));
+  hsa_signal_t sig{};
+  if (!pool.handle || hsa_amd_memory_pool_allocate(pool, bytes, 0, &buf) != HSA_STATUS_SUCCESS || !ka ||
+      hsa_amd_agents_allow_access(1, &a->gpu, nullptr, buf) != HSA_STATUS_SUCCESS ||
+      hsa_signal_create(launches, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) {
+    if (buf) hsa_amd_memory_pool_free(buf);
+    if (ka) hsa_amd_memory_pool_free(ka);
+    hsa_executable_destroy(exe);
+    return fail("allocation failed");
+  }
+  if (kind == 0) {
+    gpuexp::CalibCopyArgs args{buf, static_cast<char*>(buf) + kCopyBytes, kCopyBytes / 16,
+                               uint64_t(kBlocks) * gpuexp::kProbeBlock};
+    std::memcpy(ka, &args, sizeof(args));
+  } else {
+    gpuexp::CalibLdsArgs args{static_cast<float*>(buf), 8192, kind == 2 ? 32 : 1};
+    std::memcpy(ka, &args, sizeof(args));
+  }
+  const auto t0 = Clock::now();
+  bool timed_out = false;
+  for (int i = 0; i < launches && !timed_out; ++i) {
+    // at most 4 in flight: wait until fewer than 4 of the i submitted are outstanding
+    if (i >= 4)
+      timed_out = hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, hsa_signal_value_t(launches - i + 4),
+                                            5 * g_ts_freq, HSA_WAIT_STATE_ACTIVE) >= launches - i + 4;
+    if (!timed_out) dispatch(*a, k, ka, kBlocks, sig, uint16_t(gpuexp::kProbeBlock));
+  }
+  if (!timed_out)
+    timed_out = hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, 30 * g_ts_freq,
+                                          HSA_WAIT_STATE_BLOCKED) >= 1;
+  const double secs = std::chrono::duration<double>(Clock::now() - t0).count();
+  if (timed_out) {  // the GPU may still use the buffers: leak them
+    a->broken = true;
+    return fail("calibration dispatches did not complete");
+  }
+  hsa_signal_destroy(sig);
+  hsa_amd_memory_pool_free(buf);
+  hsa_amd_memory_pool_free(ka);
+  hsa_executable_destroy(exe);
+  out[0] = secs;
+  out[1] = double(kBlocks) * (gpuexp::kProbeBlock / 64);
+  out[2] = kind == 0 ? double(kCopyBytes) : 0.0;
   return 0;
 }
 

@@ -12,6 +12,7 @@
 // monotone and within slack); a mismatch keeps amdsmi as the per-tick source.
 #include <amd_smi/amdsmi.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -109,6 +110,7 @@ class AmdsmiBackend : public Backend {
     GpuMetricsReader gm;
     bool fast_ok = false;
     std::string validate_msg;
+    int validated_fields = 0;
     uint64_t raw_failures = 0;  // __atomic_* access: sampler writes, describe() reads
     CachedFile vram_used_file;
     double power_cap_w = kNaN;
@@ -233,32 +235,85 @@ class AmdsmiBackend : public Backend {
     return true;
   }
 
-  // Reads the blob directly and through amdsmi, back to back, and compares.
+  // Reads the blob through amdsmi, directly, and through amdsmi again, and compares every
+  // field the engine exports: hardware accumulators must lie between the two amdsmi reads,
+  // static fields must agree exactly, instantaneous ones within a sensor's jitter.
   bool validate(Dev& d) {
-    DeviceSample a, b;
+    DeviceSample a, b1, b2;
+    amdsmi_gpu_metrics_t m1{}, m2{};
+    if (amdsmi_get_gpu_metrics_info(d.h, &m1) != AMDSMI_STATUS_SUCCESS) {
+      d.validate_msg = "amdsmi metrics failed";
+      return false;
+    }
     if (!d.gm.read(&a)) {
       d.validate_msg = "raw read failed";
       return false;
     }
-    amdsmi_gpu_metrics_t m{};
-    if (amdsmi_get_gpu_metrics_info(d.h, &m) != AMDSMI_STATUS_SUCCESS) {
+    if (amdsmi_get_gpu_metrics_info(d.h, &m2) != AMDSMI_STATUS_SUCCESS) {
       d.validate_msg = "amdsmi metrics failed";
       return false;
     }
-    from_amdsmi_metrics(m, &b, d.xcp, d.nxcc);
-    bool ok = same_or_both_nan(a.vram_max_bw_gbs, b.vram_max_bw_gbs, 0) &&
-              same_or_both_nan(a.pcie_width, b.pcie_width, 0) &&
-              same_or_both_nan(a.pcie_speed_gts, b.pcie_speed_gts, 0) &&
-              same_or_both_nan(a.temp_hotspot, b.temp_hotspot, 3) &&
-              same_or_both_nan(a.temp_mem, b.temp_mem, 3) &&
-              same_or_both_nan(a.clk_mem, b.clk_mem, 0) &&
-              a.num_xgmi_links == b.num_xgmi_links && a.energy_acc <= b.energy_acc &&
-              (b.energy_acc - a.energy_acc) < (1ull << 32) && a.fw_ts_10ns <= b.fw_ts_10ns &&
-              b.fw_ts_10ns - a.fw_ts_10ns < 100000000ull;  // < 1 s apart
-    for (int l = 0; ok && l < kMaxXgmiLinks; ++l)
-      ok = a.xgmi_read_kb[l] <= b.xgmi_read_kb[l] && b.xgmi_read_kb[l] - a.xgmi_read_kb[l] < (1ull << 30) &&
-           same_or_both_nan(a.xgmi_link_up[l], b.xgmi_link_up[l], 0);
-    d.validate_msg = ok ? "raw gpu_metrics v1.8 validated" : "raw decode disagrees with amdsmi";
+    from_amdsmi_metrics(m1, &b1, d.xcp, d.nxcc);
+    from_amdsmi_metrics(m2, &b2, d.xcp, d.nxcc);
+    int fields = 0;
+    std::string bad;
+    auto between = [&](const char* f, double lo, double v, double hi) {
+      ++fields;
+      const bool ok = (std::isnan(lo) && std::isnan(v) && std::isnan(hi)) || (lo <= v && v <= hi);
+      if (!ok && bad.empty()) bad = f;
+    };
+    auto near = [&](const char* f, double x, double v, double y, double tol) {
+      ++fields;
+      const bool nan = std::isnan(x) && std::isnan(v) && std::isnan(y);
+      const bool ok = nan || (v >= std::min(x, y) - tol && v <= std::max(x, y) + tol);
+      if (!ok && bad.empty()) bad = f;
+    };
+    auto acc = [&](const char* f, uint64_t lo, uint64_t v, uint64_t hi) {
+      between(f, double(lo), double(v), double(hi));
+    };
+    acc("energy_accumulator", b1.energy_acc, a.energy_acc, b2.energy_acc);
+    acc("firmware_timestamp", b1.fw_ts_10ns, a.fw_ts_10ns, b2.fw_ts_10ns);
+    acc("accumulation_counter", b1.accumulation_counter, a.accumulation_counter, b2.accumulation_counter);
+    acc("ppt_residency_acc", b1.res_ppt, a.res_ppt, b2.res_ppt);
+    acc("socket_thm_residency_acc", b1.res_socket_thm, a.res_socket_thm, b2.res_socket_thm);
+    acc("vr_thm_residency_acc", b1.res_vr_thm, a.res_vr_thm, b2.res_vr_thm);
+    acc("hbm_thm_residency_acc", b1.res_hbm_thm, a.res_hbm_thm, b2.res_hbm_thm);
+    acc("prochot_residency_acc", b1.res_prochot, a.res_prochot, b2.res_prochot);
+    acc("pcie_bandwidth_acc", b1.pcie_bw_acc, a.pcie_bw_acc, b2.pcie_bw_acc);
+    between("pcie_replay_count_acc", b1.pcie_replay, a.pcie_replay, b2.pcie_replay);
+    between("pcie_nak_sent_count_acc", b1.pcie_nak_sent, a.pcie_nak_sent, b2.pcie_nak_sent);
+    between("pcie_nak_rcvd_count_acc", b1.pcie_nak_rcvd, a.pcie_nak_rcvd, b2.pcie_nak_rcvd);
+    between("pcie_l0_to_recov_count_acc", b1.pcie_l0_recov, a.pcie_l0_recov, b2.pcie_l0_recov);
+    for (int l = 0; l < kMaxXgmiLinks; ++l) {
+      acc("xgmi_read_data_acc", b1.xgmi_read_kb[l], a.xgmi_read_kb[l], b2.xgmi_read_kb[l]);
+      acc("xgmi_write_data_acc", b1.xgmi_write_kb[l], a.xgmi_write_kb[l], b2.xgmi_write_kb[l]);
+      near("xgmi_link_status", b1.xgmi_link_up[l], a.xgmi_link_up[l], b2.xgmi_link_up[l], 0);
+    }
+    for (int x = 0; x < kMaxXcc; ++x) {
+      acc("xcp_stats.gfx_busy_acc", b1.gfx_busy_acc[x], a.gfx_busy_acc[x], b2.gfx_busy_acc[x]);
+      near("current_gfxclks", b1.clk_gfx_xcc[x], a.clk_gfx_xcc[x], b2.clk_gfx_xcc[x], 400);
+    }
+    near("vram_max_bandwidth", b1.vram_max_bw_gbs, a.vram_max_bw_gbs, b2.vram_max_bw_gbs, 0);
+    near("pcie_link_width", b1.pcie_width, a.pcie_width, b2.pcie_width, 0);
+    near("pcie_link_speed", b1.pcie_speed_gts, a.pcie_speed_gts, b2.pcie_speed_gts, 0);
+    near("xgmi_link_width", b1.xgmi_width, a.xgmi_width, b2.xgmi_width, 0);
+    near("xgmi_link_speed", b1.xgmi_speed, a.xgmi_speed, b2.xgmi_speed, 0);
+    near("current_uclk", b1.clk_mem, a.clk_mem, b2.clk_mem, 0);
+    near("current_socclk", b1.clk_soc, a.clk_soc, b2.clk_soc, 400);
+    near("temperature_hotspot", b1.temp_hotspot, a.temp_hotspot, b2.temp_hotspot, 3);
+    near("temperature_mem", b1.temp_mem, a.temp_mem, b2.temp_mem, 3);
+    near("temperature_vrsoc", b1.temp_vrsoc, a.temp_vrsoc, b2.temp_vrsoc, 3);
+    near("current_socket_power", b1.power_w, a.power_w, b2.power_w, 100);
+    near("average_gfx_activity", b1.gfx_activity, a.gfx_activity, b2.gfx_activity, 25);
+    near("average_umc_activity", b1.umc_activity, a.umc_activity, b2.umc_activity, 25);
+    near("pcie_bandwidth_inst", b1.pcie_bw_inst, a.pcie_bw_inst, b2.pcie_bw_inst, 64);
+    ++fields;
+    if ((a.num_partition != b1.num_partition || a.num_xgmi_links != b1.num_xgmi_links) && bad.empty())
+      bad = "num_partition/num_xgmi_links";
+    const bool ok = bad.empty();
+    d.validated_fields = fields;
+    d.validate_msg = ok ? "raw gpu_metrics v1.8 validated against amdsmi (" + std::to_string(fields) + " checks)"
+                        : "raw decode disagrees with amdsmi on " + bad;
     return ok;
   }
 
@@ -328,7 +383,8 @@ class AmdsmiBackend : public Backend {
     const uint64_t fails = __atomic_load_n(&d.raw_failures, __ATOMIC_RELAXED);  // sampler thread writes
     if (d.fast_ok && fails)
       return "raw gpu_metrics v1.8 with " + std::to_string(fails) + " failed reads (amdsmi fallback)";
-    return d.fast_ok ? "raw gpu_metrics v1.8 (validated against amdsmi)"
+    return d.fast_ok ? "raw gpu_metrics v1.8 (validated against amdsmi: " + std::to_string(d.validated_fields) +
+                           " field checks)"
                      : "amdsmi_get_gpu_metrics_info (" + d.validate_msg + ")";
   }
 

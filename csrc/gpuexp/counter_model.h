@@ -15,6 +15,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 
 namespace gpuexp_ctr {
 
@@ -63,6 +64,15 @@ inline bool process_has_pmc_privilege() {
   std::fclose(f);
   constexpr int kCapSysAdmin = 21, kCapPerfmon = 38;
   return (eff >> kCapSysAdmin & 1ull) || (eff >> kCapPerfmon & 1ull);
+}
+
+// Validation knob (tests/test_gpu.py::test_device_scope_pmc_*): GPUEXP_PMC_ASSUME_DEVICE_SCOPE=1
+// treats the wave/LDS/EA counters as device-wide in an unprivileged process.  Only sound
+// when every kernel on the GPU belongs to the counting process itself (the VMID filter
+// then passes all of them), which is how the calibration tests run.
+inline bool pmc_device_scope() {
+  const char* f = std::getenv("GPUEXP_PMC_ASSUME_DEVICE_SCOPE");
+  return process_has_pmc_privilege() || (f && f[0] == '1');
 }
 
 struct Derived {

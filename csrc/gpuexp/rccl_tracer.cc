@@ -13,6 +13,8 @@
 //   allreduce/reduce/broadcast: count * size       allgather: sendcount * size * nranks
 //   reducescatter: recvcount * size * nranks        alltoall: count * size * nranks
 //   alltoallv: sum(sendcounts) * size               send/recv: count * size
+//   gather: sendcount * size                        scatter: recvcount * size
+// (pinned at nranks 1/2/8 for every op by tests/test_rccl_tracer_bytes.py)
 // nranks (and the process's rank) come from the communicator's creation call
 // (ncclCommInitRank / ncclCommInitRankConfig EXIT: nranks, myrank, *newcomm), cached per
 // communicator; communicators made otherwise (ncclCommSplit, ncclCommInitAll) are asked
@@ -81,7 +83,9 @@ void* rccl_lib() {
 // / data-parallel group; TP/PP/EP sub-communicators are smaller), so the rank is stable.
 void note_comm_locked(const void* comm, int n, int rank) {
   g_nranks[comm] = n;
-  if (g_shm && n >= g_shm->nranks) {
+  // a larger communicator wins; an equal-sized one only fills in an unknown rank (never
+  // replaces a known rank with -1 from a communicator that could not be queried)
+  if (g_shm && (n > g_shm->nranks || (n == g_shm->nranks && g_shm->rank < 0 && rank >= 0))) {
     g_shm->nranks = n;
     g_shm->rank = rank;
   }

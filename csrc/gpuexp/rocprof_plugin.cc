@@ -114,7 +114,7 @@ int tool_init(rocprofiler_client_finalize_t fini, void*) {
       ag.id = a.id;
       ag.dev = int(d);
       ag.m.simd = a.simd_count;
-      ag.m.privileged = process_has_pmc_privilege();
+      ag.m.privileged = pmc_device_scope();
       ag.m.cu = a.cu_count ? a.cu_count : (a.simd_per_cu ? a.simd_count / a.simd_per_cu : 0);
       if (rocprofiler_create_context(&ag.ctx) != ROCPROFILER_STATUS_SUCCESS) continue;
       rocprofiler_buffer_id_t nobuf{};  // values come back in the sample call itself

@@ -15,6 +15,8 @@ bool gemm256_shape_ok(int M, int N, int K);
 hipError_t launch_gemm_bf16_tn(const void* A, const void* B, void* C, int M, int N, int K, hipStream_t stream,
                                int variant);
 hipError_t launch_fill_bf16(void* p, size_t n, uint32_t seed, hipStream_t stream);
+hipError_t launch_stream_copy(const void* src, void* dst, size_t bytes, int blocks, hipStream_t stream);
+hipError_t launch_lds_probe(float* out, int blocks, int iters, int stride, hipStream_t stream);
 }  // namespace gpuexp
 
 namespace {
@@ -56,6 +58,26 @@ PYBIND11_MODULE(_gpuexp_kernels, m) {
     check(gpuexp::launch_fill_bf16(reinterpret_cast<void*>(p), n, seed, reinterpret_cast<hipStream_t>(stream)),
           "fill_bf16 launch");
   }, py::arg("ptr"), py::arg("n"), py::arg("seed") = 1, py::arg("stream") = 0);
+  // PMC calibration workloads (csrc/kernels/probe_kernels.hip)
+  m.def("stream_copy", [](uintptr_t src, uintptr_t dst, size_t nbytes, int blocks, uintptr_t stream) {
+    if (!src || !dst || nbytes % 16 || blocks < 1 || blocks > (1 << 20))
+      throw std::invalid_argument("stream_copy needs non-null pointers, nbytes % 16 == 0, 1 <= blocks <= 2^20");
+    check(gpuexp::launch_stream_copy(reinterpret_cast<const void*>(src), reinterpret_cast<void*>(dst), nbytes, blocks,
+                                     reinterpret_cast<hipStream_t>(stream)),
+          "stream_copy launch");
+  }, py::call_guard<py::gil_scoped_release>(), py::arg("src"), py::arg("dst"), py::arg("nbytes"),
+     py::arg("blocks") = 4096, py::arg("stream") = 0,
+     "dst[:nbytes] = src[:nbytes] (each byte read once from and written once to HBM)");
+  m.def("lds_probe", [](uintptr_t out, int blocks, int iters, int stride, uintptr_t stream) {
+    // `out` must hold >= blocks floats (checked by the Python wrapper)
+    if (!out || blocks < 1 || blocks > (1 << 20) || iters < 1 || (stride != 1 && stride != 32))
+      throw std::invalid_argument("lds_probe needs out, 1 <= blocks <= 2^20, iters >= 1, stride 1 or 32");
+    check(gpuexp::launch_lds_probe(reinterpret_cast<float*>(out), blocks, iters, stride,
+                                   reinterpret_cast<hipStream_t>(stream)),
+          "lds_probe launch");
+  }, py::call_guard<py::gil_scoped_release>(), py::arg("out"), py::arg("blocks"), py::arg("iters"),
+     py::arg("stride"), py::arg("stream") = 0,
+     "256-thread blocks (4 waves) of ds_read_b32 from LDS: stride 1 conflict-free, stride 32 32-way conflicts");
   m.def("gemm_burn", [](int device, int M, int N, int K, double seconds, int iters_per_sync, int variant) {
     // Torch-free synthetic GEMM pod: keeps one GPU busy for `seconds` and reports the
     // achieved bf16 TFLOP/s (random operands).

@@ -1,0 +1,36 @@
+// Calibration kernels for the device PMC families, launched through HIP (bound in
+// _gpuexp_kernels as stream_copy / lds_probe): workloads whose HBM bytes, LDS bank
+// conflicts and wave counts are known in advance.  The same device code is dispatched as
+// raw AQL on the PMC queue by the aqlprofile plugin (calib_hsaco.hip), where the
+// exporter's own counters see it (tools/pmc_validate.py).
+#include "kernels/probe_device.h"
+
+namespace gpuexp {
+
+namespace {
+
+__global__ __launch_bounds__(kProbeBlock) void stream_copy_kernel(CalibCopyArgs a) {
+  stream_copy_body(static_cast<const u32x4*>(a.src), static_cast<u32x4*>(a.dst), a.n, a.stride);
+}
+
+__global__ __launch_bounds__(kProbeBlock) void lds_probe_kernel(CalibLdsArgs a) {
+  lds_probe_body(a.out, a.iters, a.stride);
+}
+
+}  // namespace
+
+hipError_t launch_stream_copy(const void* src, void* dst, size_t bytes, int blocks, hipStream_t stream) {
+  if (bytes % 16) return hipErrorInvalidValue;
+  CalibCopyArgs a{src, dst, bytes / 16,
+                  uint64_t(blocks) * kProbeBlock};
+  hipLaunchKernelGGL(stream_copy_kernel, dim3(blocks), dim3(kProbeBlock), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_lds_probe(float* out, int blocks, int iters, int stride, hipStream_t stream) {
+  CalibLdsArgs a{out, iters, stride};
+  hipLaunchKernelGGL(lds_probe_kernel, dim3(blocks), dim3(kProbeBlock), 0, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace gpuexp

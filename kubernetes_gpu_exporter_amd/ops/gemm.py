@@ -53,3 +53,26 @@ def gemm_burn(device: int = 0, size: int = 8192, seconds: float = 1.0, iters_per
               variant: int = 0) -> dict:
     """Torch-free GPU load: keeps `device` busy with size^3 GEMMs for `seconds`."""
     return kernels().gemm_burn(device, size, size, size, seconds, iters_per_sync, variant)
+
+
+def stream_copy(src, dst, stream=None, blocks: int = 4096):
+    """dst <- src (same nbytes, contiguous, one GPU) with the calibration copy kernel:
+    reads and writes each byte of HBM exactly once."""
+    import torch
+    n = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() != n or not (src.is_contiguous() and dst.is_contiguous()):
+        raise ValueError("src and dst must be contiguous and of equal size")
+    if src.device != dst.device or src.device.type != "cuda":
+        raise ValueError("tensors must be on the same GPU")
+    s = stream if stream is not None else torch.cuda.current_stream(src.device).cuda_stream
+    kernels().stream_copy(src.data_ptr(), dst.data_ptr(), n, blocks, s)
+
+
+def lds_probe(out, blocks: int, iters: int, conflicts: bool, stream=None):
+    """`blocks` x 256 threads of LDS reads; conflicts=True makes every read 32-way
+    bank-conflicted, False conflict-free.  `out`: float32 tensor with >= blocks elements."""
+    import torch
+    if out.dtype != torch.float32 or out.numel() < blocks or out.device.type != "cuda":
+        raise ValueError("out must be a float32 GPU tensor with >= blocks elements")
+    s = stream if stream is not None else torch.cuda.current_stream(out.device).cuda_stream
+    kernels().lds_probe(out.data_ptr(), blocks, iters, 32 if conflicts else 1, s)

@@ -13,6 +13,7 @@ the exporter's per-pod numbers against ground truth:
   ep       all-to-all of token blocks (MoE dispatch)              (every pair)
   cp       ring attention: KV blocks passed around a ring         (2 neighbour links)
   ulysses  2 x all-to-all per attention layer                     (every pair)
+  bcast    parameter broadcast from rank 0 + metric reduce to rank 0 (rooted trees)
 
 Bytes follow the RCCL tracer's accounting (csrc/gpuexp/rccl_tracer.cc header comment).
 """
@@ -21,7 +22,7 @@ from __future__ import annotations
 import time
 from dataclasses import dataclass, field
 
-STRATEGIES = ("dp", "tp", "pp", "sp", "ep", "cp", "ulysses")
+STRATEGIES = ("dp", "tp", "pp", "sp", "ep", "cp", "ulysses", "bcast")
 
 
 @dataclass
@@ -116,6 +117,17 @@ def run(strategy: str, steps: int = 1, nbytes: int = 1 << 20, device=None, dtype
                     st.add("recv", n * esize)
                     if check:
                         assert float(recv[0]) == rank - 1
+        elif strategy == "bcast":
+            p = full(7 if rank == 0 else 0)
+            dist.broadcast(p, src=0)
+            st.add("broadcast", n * esize)
+            m = full(rank + 1)
+            dist.reduce(m, dst=0)
+            st.add("reduce", n * esize)
+            if check:
+                assert float(p[0]) == 7
+                if rank == 0:
+                    assert float(m[0]) == world * (world + 1) / 2
         elif strategy == "cp":
             if world > 1:
                 kv = full(rank)

@@ -27,6 +27,9 @@ def test_strategy_world2(strategy):
         assert r0["calls"] == {"send": 2} and r1["calls"] == {"recv": 2}  # asymmetric by stage
     elif strategy == "cp":
         assert r0["calls"] == {"send": 2, "recv": 2} == r1["calls"]  # ring: both neighbours
+    elif strategy == "bcast":
+        assert r0["calls"] == {"broadcast": 2, "reduce": 2} == r1["calls"]
+        assert r0["bytes"] == {"broadcast": 2 * NB, "reduce": 2 * NB}
 
 
 def test_strategies_world4():

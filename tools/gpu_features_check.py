@@ -111,6 +111,13 @@ def rccl() -> dict:
         "for _ in range(5): dist.all_to_all_single(torch.empty_like(x), x)\n"
         "torch.cuda.synchronize(); dist.destroy_process_group(); print('child done', flush=True)\n")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    # per-strategy parity: tracer deltas vs the generators' TrafficStats, in a second child
+    d2 = tempfile.mkdtemp(prefix="gpuexp-rccl-parity-")
+    env2 = dict(env, GPUEXP_RCCL_DIR=d2, MASTER_PORT=str(port + 1 if port < 65535 else port - 1))
+    r2 = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "rccl_parity_child.py")], env=env2,
+                        capture_output=True, text=True, timeout=240)
+    parity_line = [l for l in r2.stdout.splitlines() if l.startswith("PARITY ")]
+    parity = json.loads(parity_line[-1][7:]) if parity_line else {"rc": r2.returncode, "stderr": r2.stderr[-1500:]}
     files = [f for f in os.listdir(d) if f.startswith("gpuexp-rccl-")]
     ops = {}
     comm = []
@@ -124,7 +131,8 @@ def rccl() -> dict:
             calls, nbytes = struct.unpack_from("<QQ", b, 64 + 16 * i)
             if calls:
                 ops[nm] = {"calls": calls, "bytes": nbytes}
-    return {"rc": r.returncode, "files": files, "ops": ops, "communicator": comm, "stdout": r.stdout[-500:], "stderr": r.stderr[-1500:]}
+    return {"rc": r.returncode, "files": files, "ops": ops, "communicator": comm, "parity": parity,
+            "stdout": r.stdout[-500:], "stderr": r.stderr[-1500:]}
 
 
 if __name__ == "__main__":
