@@ -17,7 +17,7 @@
 // The engine's tick never blocks on the GPU: gpuexp_rp_sample returns the latest window.
 //
 // Event ids are the gfx950 select values of /opt/rocm/share/rocprofiler-sdk/counter_defs.yaml
-// (SQ 93/3/4/147/142, GRBM 2/0, TCC 62/42/30/31) and are checked with
+// (SQ 93/3/4/147/142, GRBM 2/0, TCC 112/115/113/117) and are checked with
 // hsa_ven_amd_aqlprofile_validate_event at init.  TCC is programmed on every channel
 // instance (16 per XCD); SQ and GRBM are broadcast and come back once per SE / XCC.
 #include <execinfo.h>
@@ -47,6 +47,8 @@
 #include "gpuexp/sentinel_common.h"
 #include "gpuexp/sources.h"
 
+static_assert(gpuexp_ctr::kNumOut == gpuexp::kCounterOutputs, "counter plugin ABI");
+
 namespace {
 
 using namespace gpuexp_ctr;
@@ -63,9 +65,9 @@ const EventDef kGfx950[] = {
     {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 93, kMfma},        {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 3, kSqBusy},
     {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 4, kWaves},        {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 147, kLdsActive},
     {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 142, kLdsConflict}, {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, 2, kGuiActive},
-    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, 0, kGrbmCount},  {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 62, kTccBubble},
-    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 42, kRdReq},      {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 30, kWrReq},
-    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 31, kWrReq64},
+    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, 0, kGrbmCount},  {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 112, kDramRd32},
+    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 115, kDramWr32},  {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 113, kGmiRd32},
+    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 117, kGmiWr32},
 };
 
 struct Agent {

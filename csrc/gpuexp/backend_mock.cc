@@ -167,6 +167,8 @@ bool MockBackend::counters(const DeviceInfo& dev, double dt_s, CounterReading* o
   out->lds_bank_conflict_pct = get(s, "lds_bank_conflict_pct", 1.5);
   out->hbm_read_bps = get(s, "hbm_read_bps", 4e12 * busy / 100);
   out->hbm_write_bps = get(s, "hbm_write_bps", 1e12 * busy / 100);
+  out->remote_read_bps = get(s, "remote_read_bps", 0.0);
+  out->remote_write_bps = get(s, "remote_write_bps", 0.0);
   (void)dt_s;
   return true;
 }

@@ -6,9 +6,17 @@
 // slots": SQ 8, TCC 4, GRBM 2):
 //   SQ   SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT
 //   GRBM GRBM_GUI_ACTIVE GRBM_COUNT
-//   TCC  TCC_BUBBLE TCC_EA0_RDREQ TCC_EA0_WRREQ TCC_EA0_WRREQ_64B
-// Derived values follow the gfx950 formulas of /opt/rocm/share/rocprofiler-sdk/counter_defs.yaml
-// (MfmaUtil, FETCH_SIZE, WRITE_SIZE, LDS utilisation / bank-conflict ratio).
+//   TCC  TCC_EA0_RDREQ_DRAM_32B TCC_EA0_WRREQ_WRITE_DRAM_32B TCC_EA0_RDREQ_GMI_32B
+//        TCC_EA0_WRREQ_WRITE_GMI_32B
+// MFMA / LDS derivations follow the gfx950 formulas of
+// /opt/rocm/share/rocprofiler-sdk/counter_defs.yaml (MfmaUtil, LDS utilisation /
+// bank-conflict ratio).  HBM bytes do NOT use its gfx950 FETCH_SIZE: that formula weighs
+// TCC_BUBBLE as the 128-byte read count, and on MI355X TCC_BUBBLE stays 0 while every
+// TCC_EA0_RDREQ of a streaming copy is a 128-byte line (measured: FETCH_SIZE = 0.497x the
+// bytes a copy moves, profiles/r02/pmc_calibration.txt).  The DRAM-sector counters count
+// 32-byte sectors of requests that reach the memory controller (a 64-byte request counts 2),
+// so x 32 B they are HBM bytes whatever the request sizes, with traffic to memory behind GMI
+// (peer GPUs) and IO (host) in counters of their own.
 #pragma once
 
 #include <algorithm>
@@ -27,26 +35,28 @@ enum Ctr {
   kLdsConflict,
   kGuiActive,
   kGrbmCount,
-  kTccBubble,
-  kRdReq,
-  kWrReq,
-  kWrReq64,
+  kDramRd32,
+  kDramWr32,
+  kGmiRd32,
+  kGmiWr32,
   kNumCtr
 };
 
 inline const char* name(int c) {
   static const char* kNames[kNumCtr] = {"SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES",  "SQ_WAVES",
                                         "SQ_LDS_IDX_ACTIVE",        "SQ_LDS_BANK_CONFLICT",
-                                        "GRBM_GUI_ACTIVE",          "GRBM_COUNT",      "TCC_BUBBLE",
-                                        "TCC_EA0_RDREQ",            "TCC_EA0_WRREQ",   "TCC_EA0_WRREQ_64B"};
+                                        "GRBM_GUI_ACTIVE",          "GRBM_COUNT",
+                                        "TCC_EA0_RDREQ_DRAM_32B",   "TCC_EA0_WRREQ_WRITE_DRAM_32B",
+                                        "TCC_EA0_RDREQ_GMI_32B",    "TCC_EA0_WRREQ_WRITE_GMI_32B"};
   return kNames[c];
 }
 
 // GRBM counters are per-XCC copies of one clock: reduce with max; everything else sums.
 inline bool use_max(int c) { return c == kGuiActive || c == kGrbmCount; }
 
-// Number of derived outputs (the CounterSource ABI: gpuexp_rp_sample fills 8 doubles).
-constexpr int kNumOut = 8;
+// Number of derived outputs (the CounterSource ABI: gpuexp_rp_sample fills this many
+// doubles; gpuexp::kCounterOutputs in sources.h).
+constexpr int kNumOut = 10;
 
 // Wave-level SQ counters and TCC EA requests are VMID-filtered for unprivileged clients.
 // The filter is on the HARDWARE VMID, which the scheduler hands out dynamically, so an
@@ -103,8 +113,10 @@ inline void derive(Derived& a, const double* d, const int* inst, double wall) {
   out[3] = d[kWaves] / wall;                                                         // waves/s
   out[4] = gui > 0 && a.cu ? 100.0 * d[kLdsActive] / (gui * a.cu) : nan;            // LDS util
   out[5] = d[kLdsActive] > 0 ? 100.0 * d[kLdsConflict] / d[kLdsActive] : 0.0;       // bank conflicts
-  out[6] = (d[kTccBubble] * 128.0 + (d[kRdReq] - d[kTccBubble]) * 64.0) / wall;    // FETCH_SIZE B/s
-  out[7] = ((d[kWrReq] - d[kWrReq64]) * 32.0 + d[kWrReq64] * 64.0) / wall;         // WRITE_SIZE B/s
+  out[6] = d[kDramRd32] * 32.0 / wall;                                              // HBM read B/s
+  out[7] = d[kDramWr32] * 32.0 / wall;                                              // HBM write B/s
+  out[8] = d[kGmiRd32] * 32.0 / wall;                                               // remote (GMI) read B/s
+  out[9] = d[kGmiWr32] * 32.0 / wall;                                               // remote (GMI) write B/s
   a.valid = true;
   a.windows += 1;
 }

@@ -121,8 +121,10 @@ struct CounterReading {
   double waves_per_s = kNaN;        // SQ_WAVES / dt
   double lds_active_pct = kNaN;     // SQ_LDS_IDX_ACTIVE / (GUI_ACTIVE * CUs)
   double lds_bank_conflict_pct = kNaN;  // SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
-  double hbm_read_bps = kNaN;       // TCC_EA0_RDREQ * 64B * 2 (gfx950 half-count) / dt
-  double hbm_write_bps = kNaN;      // TCC_EA0_WRREQ * 64B / dt
+  double hbm_read_bps = kNaN;       // TCC_EA0_RDREQ_DRAM_32B * 32 B / dt
+  double hbm_write_bps = kNaN;      // TCC_EA0_WRREQ_WRITE_DRAM_32B * 32 B / dt
+  double remote_read_bps = kNaN;    // TCC_EA0_RDREQ_GMI_32B * 32 B / dt (memory behind GMI: peers)
+  double remote_write_bps = kNaN;   // TCC_EA0_WRREQ_WRITE_GMI_32B * 32 B / dt
 };
 
 // HIP sentinel kernel stamps for one GPU (latest completed run).  A run is one wave per

@@ -168,8 +168,16 @@ void Engine::define_families() {
   f_waves_ = add("amd_gpu_waves_per_second", "Waves dispatched per second (SQ_WAVES)", G, D);
   f_lds_ = add("amd_gpu_lds_active_percent", "LDS active cycles per CU (SQ_LDS_IDX_ACTIVE)", G, D);
   f_lds_conf_ = add("amd_gpu_lds_bank_conflict_percent", "LDS bank-conflict cycles / LDS active cycles", G, D);
-  f_hbm_rd_ = add("amd_gpu_hbm_read_bytes_per_second", "HBM read bandwidth (TCC_EA0_RDREQ)", G, D);
-  f_hbm_wr_ = add("amd_gpu_hbm_write_bytes_per_second", "HBM write bandwidth (TCC_EA0_WRREQ)", G, D);
+  f_hbm_rd_ = add("amd_gpu_hbm_read_bytes_per_second",
+                  "HBM read bandwidth: L2 read sectors from the memory controller (TCC_EA0_RDREQ_DRAM_32B x 32 B)", G, D);
+  f_hbm_wr_ = add("amd_gpu_hbm_write_bytes_per_second",
+                  "HBM write bandwidth: L2 write sectors to the memory controller (TCC_EA0_WRREQ_WRITE_DRAM_32B x 32 B)", G,
+                  D);
+  f_remote_rd_ = add("amd_gpu_remote_read_bytes_per_second",
+                     "L2 reads of memory behind GMI, e.g. a peer GPU's HBM over xGMI (TCC_EA0_RDREQ_GMI_32B x 32 B)", G, D);
+  f_remote_wr_ = add("amd_gpu_remote_write_bytes_per_second",
+                     "L2 writes to memory behind GMI, e.g. a peer GPU's HBM over xGMI (TCC_EA0_WRREQ_WRITE_GMI_32B x 32 B)",
+                     G, D);
   f_sen_sclk_ = add("amd_gpu_sentinel_sclk_hz", "Effective shader clock measured by the sentinel kernel", G, D);
   f_sen_lat_ = add("amd_gpu_sentinel_dispatch_latency_seconds",
                    "Host launch to first-wave start of the sentinel kernel (queue contention)", G, D);
@@ -674,6 +682,10 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
       dput(st, i, st.ctr[5], f_lds_conf_, {}, cr.lds_bank_conflict_pct, gen);
       dput(st, i, st.ctr[6], f_hbm_rd_, {}, cr.hbm_read_bps, gen);
       dput(st, i, st.ctr[7], f_hbm_wr_, {}, cr.hbm_write_bps, gen);
+      if (cfg_.series_profile == "full") {  // not part of the 64-series standard load
+        dput(st, i, st.ctr[8], f_remote_rd_, {}, cr.remote_read_bps, gen);
+        dput(st, i, st.ctr[9], f_remote_wr_, {}, cr.remote_write_bps, gen);
+      }
     }
   }
   SentinelReading sr;

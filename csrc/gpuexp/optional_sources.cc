@@ -27,7 +27,7 @@ namespace {
 
 // C ABI of _gpuexp_rocprof.so (csrc/gpuexp/rocprof_plugin.cc).
 using rp_init_fn = int (*)(int ndev, const char* const* bdfs, char* err, int errlen);
-using rp_sample_fn = int (*)(int dev, double dt_s, double* out8);
+using rp_sample_fn = int (*)(int dev, double dt_s, double* out);  // kCounterOutputs doubles
 using rp_shutdown_fn = void (*)();
 using rp_status_fn = const char* (*)();
 using rp_scope_fn = int (*)(int dev);
@@ -71,7 +71,7 @@ class PluginCounters : public CounterSource {
 
   bool sample(int dev, double dt_s, CounterReading* out) override {
     if (!started_) return false;
-    double v[8];
+    double v[kCounterOutputs];
     if (sample_(dev, dt_s, v) != 0) return false;
     out->ok = true;
     out->mfma_busy_pct = v[0];
@@ -82,6 +82,8 @@ class PluginCounters : public CounterSource {
     out->lds_bank_conflict_pct = v[5];
     out->hbm_read_bps = v[6];
     out->hbm_write_bps = v[7];
+    out->remote_read_bps = v[8];
+    out->remote_write_bps = v[9];
     return true;
   }
 

@@ -30,6 +30,7 @@
 #include <rocprofiler-sdk/rocprofiler.h>
 
 #include "gpuexp/counter_model.h"
+#include "gpuexp/sources.h"
 
 #include <algorithm>
 #include <atomic>
@@ -44,6 +45,8 @@
 #include <mutex>
 #include <string>
 #include <vector>
+
+static_assert(gpuexp_ctr::kNumOut == gpuexp::kCounterOutputs, "counter plugin ABI");
 
 namespace {
 

@@ -31,6 +31,9 @@ std::unique_ptr<SentinelSource> make_queue_sentinel(const std::string& counters_
                                                    int spin_iters);
 std::string default_rocprof_plugin();
 
+// Derived values a counter plugin's gpuexp_rp_sample fills, in CounterReading order.
+constexpr int kCounterOutputs = 10;
+
 class CounterSource {
  public:
   virtual ~CounterSource() = default;

@@ -253,7 +253,7 @@ def test_full_profile_adds_reliability_families(mock_engine):
     e.mock_set_value(1, "aer_cor", 7)
     ticks(e, 3)
     fams = parse(e)
-    assert dict(device_series_per_gpu(fams)) == {"0": 99, "1": 99}
+    assert dict(device_series_per_gpu(fams)) == {"0": 101, "1": 101}  # + remote (GMI) read/write
     lat = {s[1]["xcc"]: s[2] for s in fams["amd_gpu_sentinel_xcc_dispatch_latency_seconds"].samples
            if s[1]["gpu"] == "0"}
     assert sorted(lat) == [str(x) for x in range(8)] and min(lat.values()) == lat["0"]

@@ -314,7 +314,7 @@ def test_device_counters_under_gemm(plugin, monkeypatch):
     assert res["amd_gpu_gui_active_percent"] > 50, res
     if res["device_scope"] == 1:
         assert res["amd_gpu_hbm_read_bytes_per_second"] > 1e9, res
-        assert res["series_gpu0"] == 64, res
+        assert res["series_gpu0"] == 64, res  # standard profile: the remote (GMI) pair is full-profile only
     else:  # wave/LDS/EA counters VMID-filtered to the exporter: not exported as device totals
         assert res["series_gpu0"] == 58, res
     if plugin == "aqlpmc":
@@ -324,7 +324,8 @@ def test_device_counters_under_gemm(plugin, monkeypatch):
 def test_device_scope_pmc_calibration():
     """Device-scope PMC families against ground truth (tools/pmc_validate.py): HBM read and
     write of a stream copy of known bytes, waves/s of known grids, and LDS bank conflicts
-    of a conflict-free vs a 32-way-conflicted read pattern."""
+    of a conflict-free vs a 32-way-conflicted read pattern.  The workloads run on the PMC
+    queue itself (the only queue an unprivileged process's SQ/TCC counters see)."""
     import json
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_validate.py")], capture_output=True,
                        text=True, timeout=240)
@@ -339,13 +340,17 @@ def test_device_scope_pmc_calibration():
     rd = cp["amd_gpu_hbm_read_bytes_per_second"] / cp["expected_Bps"]
     wr = cp["amd_gpu_hbm_write_bytes_per_second"] / cp["expected_Bps"]
     print(f"HBM read {rd:.3f}x, write {wr:.3f}x of the copy's bytes/s")
-    assert 0.85 < rd < 1.15 and 0.85 < wr < 1.15, (rd, wr)
+    assert 0.9 < rd < 1.1 and 0.9 < wr < 1.1, (rd, wr)
+    # a local copy sends nothing to memory behind GMI (peer GPUs)
+    assert cp["amd_gpu_remote_read_bytes_per_second"] < 0.01 * cp["expected_Bps"], cp
+    assert cp["amd_gpu_remote_write_bytes_per_second"] < 0.01 * cp["expected_Bps"], cp
     for w in (cp, clean, conf):
         ratio = w["amd_gpu_waves_per_second"] / w["expected_waves_per_second"]
-        assert 0.75 < ratio < 1.25, (ratio, w)
+        assert 0.9 < ratio < 1.1, (ratio, w)
     assert clean["amd_gpu_lds_active_percent"] > 0 and conf["amd_gpu_lds_active_percent"] > 0
     assert clean["amd_gpu_lds_bank_conflict_percent"] < 10, clean
-    assert conf["amd_gpu_lds_bank_conflict_percent"] > 80, conf  # 31 of 32 cycles are conflict cycles
+    # 32-way: 31 of every 32 LDS cycles are conflict cycles (96.875 %)
+    assert abs(conf["amd_gpu_lds_bank_conflict_percent"] - 100 * 31 / 32) < 2, conf
 
 
 def test_rccl_tracer_counts_collectives():
