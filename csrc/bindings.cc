@@ -46,6 +46,10 @@ py::dict device_dict(const DeviceInfo& d) {
   o["num_cu"] = d.num_cu;
   o["num_xcc"] = d.num_xcc;
   o["partition_id"] = d.partition_id;
+  o["dev_node"] = d.dev_node;
+  py::list keys;
+  for (const auto& k : device_owner_keys(d)) keys.append(k);
+  o["owner_keys"] = keys;
   o["compute_partition"] = d.compute_partition;
   o["memory_partition"] = d.memory_partition;
   py::list peers;

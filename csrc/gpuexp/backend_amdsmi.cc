@@ -11,6 +11,7 @@
 // read back-to-back and compared field by field (static fields exactly, accumulators
 // monotone and within slack); a mismatch keeps amdsmi as the per-tick source.
 #include <amd_smi/amdsmi.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cmath>
@@ -210,8 +211,12 @@ class AmdsmiBackend : public Backend {
           }
         }
         info.index = int(devs_.size());
+        info.dev_node = render_dev_node(root_, info.render_minor, info.bdf);
         if (info.render_minor >= 0) {
           std::string dir = root_ + "/sys/class/drm/renderD" + std::to_string(info.render_minor) + "/device";
+          // partitions >= 1 sit on an XCP platform device: socket files are on the PCI function
+          if (info.dev_node != info.bdf && ::access((dir + "/gpu_metrics").c_str(), F_OK) != 0)
+            dir = root_ + "/sys/bus/pci/devices/" + info.bdf;
           d.vram_used_file.open(dir + "/mem_info_vram_used");
           std::string e;
           d.gm.set_partition(info.partition_id, int(info.num_xcc));

@@ -23,6 +23,7 @@ bool MockBackend::init(std::vector<DeviceInfo>* devices, std::string* err) {
     char buf[64];
     std::snprintf(buf, sizeof(buf), "0000:%02x:00.0", 0x10 + 0x10 * i);
     d.bdf = buf;
+    d.dev_node = d.bdf;
     std::snprintf(buf, sizeof(buf), "e2ff75a3-0000-1000-80%02x-00000000%04x", i, 0xa000 + i);
     d.uuid = buf;
     d.name = "AMD Instinct MI355X (mock)";

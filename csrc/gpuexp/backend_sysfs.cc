@@ -61,6 +61,50 @@ static std::map<std::string, uint64_t> parse_properties(const std::string& text)
   return kv;
 }
 
+namespace {
+bool file_exists(const std::string& p) { return ::access(p.c_str(), F_OK) == 0; }
+}  // namespace
+
+std::string render_dev_node(const std::string& root, int render_minor, const std::string& bdf) {
+  if (render_minor < 0) return bdf;
+  char buf[4096];
+  const std::string link = root + "/sys/class/drm/renderD" + std::to_string(render_minor) + "/device";
+  if (!::realpath(link.c_str(), buf)) return bdf;
+  std::string p(buf);
+  const size_t sl = p.rfind('/');
+  std::string base = sl == std::string::npos ? p : p.substr(sl + 1);
+  // a PCI function ("dddd:bb:dd.f") or an XCP platform device ("amdgpu_xcp.<n>")
+  const bool pci = base.size() == 12 && base[4] == ':' && base[7] == ':' && base[10] == '.';
+  const bool xcp = base.compare(0, 11, "amdgpu_xcp.") == 0 || base.compare(0, 11, "amdgpu_xcp_") == 0;
+  return pci || xcp ? base : bdf;
+}
+
+std::vector<std::string> device_owner_keys(const DeviceInfo& d) {
+  auto low = [](std::string s) {
+    for (auto& c : s) c = char(::tolower(static_cast<unsigned char>(c)));
+    return s;
+  };
+  std::vector<std::string> k;
+  const std::string node = low(d.dev_node.empty() ? d.bdf : d.dev_node);
+  const std::string bdf = low(d.bdf);
+  if (node != bdf) {
+    k.push_back(node);
+    std::string alt = node;
+    for (auto& c : alt)
+      if (c == '.') c = '_';
+    if (alt != node) k.push_back(alt);
+  }
+  if (!bdf.empty()) k.push_back(bdf + "/" + std::to_string(d.partition_id));
+  if (d.render_minor >= 0) {
+    k.push_back("renderd" + std::to_string(d.render_minor));
+    k.push_back("/dev/dri/renderd" + std::to_string(d.render_minor));
+  }
+  if (d.kfd_gpu_id) k.push_back("kfd:" + std::to_string(d.kfd_gpu_id));
+  if (!d.uuid.empty()) k.push_back(low(d.uuid));
+  if (node == bdf && !bdf.empty()) k.push_back(bdf);
+  return k;
+}
+
 std::string SysfsBackend::uuid_from_unique_id(uint64_t unique_id, uint32_t device_id) {
   // amdsmi format: <b0>ff<devid16>-0000-1000-80<b1>-<b2..b7>, where b0..b7 are the
   // big-endian bytes of the KFD unique_id (checked against amdsmi on MI355X:
@@ -128,6 +172,13 @@ bool SysfsBackend::init(std::vector<DeviceInfo>* devices, std::string* err) {
     std::string part;
     if (read_small_file(dev->dev_dir + "/current_compute_partition", &part)) d.compute_partition = trim(part);
     if (read_small_file(dev->dev_dir + "/current_memory_partition", &part)) d.memory_partition = trim(part);
+    d.dev_node = render_dev_node(root_, d.render_minor, d.bdf);
+    // Socket-level files (gpu_metrics, mem_info_*, hwmon) live on the PCI function; an
+    // XCP platform device (partitions >= 1) may not carry them.
+    if (d.dev_node != d.bdf && !file_exists(dev->dev_dir + "/gpu_metrics")) {
+      const std::string pci = root_ + "/sys/bus/pci/devices/" + d.bdf;
+      if (file_exists(pci + "/gpu_metrics")) dev->dev_dir = pci;
+    }
     dev->xcp = d.partition_id;
     dev->nxcc = int(d.num_xcc);
     uint64_t total = 0;

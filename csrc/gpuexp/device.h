@@ -38,8 +38,24 @@ struct DeviceInfo {
   // socket-level telemetry (power, temperatures, xGMI, PCIe) is shared by all of them.
   std::string compute_partition, memory_partition;
   int partition_id = 0;        // XCP index of this logical GPU within its socket
+  // The sysfs device behind the render node: the PCI BDF for a whole GPU and for partition
+  // 0 of a partitioned socket, "amdgpu_xcp.<n>" for its other partitions (platform
+  // devices).  What device plugins name a logical GPU by; unique per logical GPU where the
+  // BDF is not (see device_owner_keys).
+  std::string dev_node;
   std::string xgmi_peer_bdf[kMaxXgmiLinks];  // from amdsmi_get_link_metrics (once)
 };
+
+// Basename of realpath(<root>/sys/class/drm/renderD<minor>/device): the BDF or
+// "amdgpu_xcp.<n>"; `bdf` when the node cannot be resolved (or is not a device link).
+std::string render_dev_node(const std::string& root, int render_minor, const std::string& bdf);
+
+// Keys under which a device owner (device plugin allocation) may name this logical GPU,
+// lower-case, most specific first: the sysfs device node (and its "amdgpu_xcp_<n>"
+// spelling), "<bdf>/<partition>", the render node, "kfd:<gpu_id>", the UUID, and the bare
+// BDF only when the BDF is this GPU's own device node (a whole GPU, or partition 0) — a
+// bare BDF never names the other partitions of a socket.
+std::vector<std::string> device_owner_keys(const DeviceInfo& d);
 
 // One tick of device telemetry.  NaN = unsupported/unavailable; raw accumulators are
 // kept as integers so deltas are exact across wraps.

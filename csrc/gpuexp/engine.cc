@@ -123,7 +123,7 @@ void Engine::define_families() {
   // --- per-GPU device families (standard profile: 64 series per GPU) ---
   f_info_ = add("amd_gpu_info", "MI355X device identity (value is always 1)", G,
                 {"gpu", "bdf", "uuid", "name", "kfd_gpu_id", "render_node", "hip_id", "partition",
-                 "compute_partition", "memory_partition"});
+                 "compute_partition", "memory_partition", "device_node"});
   f_up_ = add("amd_gpu_up", "1 if the last telemetry read of this GPU succeeded", G, D);
   f_gfx_ = add("amd_gpu_gfx_activity_percent", "Average graphics/compute engine activity (PMFW)", G, D);
   f_umc_ = add("amd_gpu_umc_activity_percent", "Average memory-controller (HBM3E) activity", G, D);
@@ -327,6 +327,8 @@ bool Engine::start(std::string* err) {
     devices_ = all;
   }
   dstate_.assign(devices_.size(), DevState());
+  owner_keys_.clear();
+  for (const DeviceInfo& d : devices_) owner_keys_.push_back(device_owner_keys(d));
   metrics_fresh_.assign(devices_.size(), 0);
   metrics_coalesced_.assign(devices_.size(), 0);
   if (cfg_.series_profile == "full" && cfg_.backend != "mock") {
@@ -533,7 +535,7 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
     st.info = table_.upsert(f_info_, {std::to_string(d.index), d.bdf, d.uuid, d.name, std::to_string(d.kfd_gpu_id),
                                       d.render_minor >= 0 ? "renderD" + std::to_string(d.render_minor) : "",
                                       std::to_string(d.hip_id), std::to_string(d.partition_id),
-                                      d.compute_partition, d.memory_partition});
+                                      d.compute_partition, d.memory_partition, d.dev_node});
     table_.set(st.info, 1, gen);
   }
   dput(st, i, st.up, f_up_, {}, c.ok ? 1 : 0, gen);
@@ -1026,8 +1028,11 @@ void Engine::tick_locked(uint64_t now) {
     DevState& st = dstate_[i];
     const DeviceInfo& d = devices_[i];
     DeviceOwner own;
-    auto it = owners_.find(lower(d.bdf));
-    if (it == owners_.end()) it = owners_.find(lower(d.uuid));
+    auto it = owners_.end();
+    for (const std::string& key : owner_keys_[i]) {
+      it = owners_.find(key);
+      if (it != owners_.end()) break;
+    }
     if (it != owners_.end()) {
       own = it->second;
     } else if (cfg_.pod_attribution && cfg_.infer_device_owner) {

@@ -189,6 +189,7 @@ class Engine {
   MockBackend* mock_ = nullptr;
   std::vector<DeviceInfo> devices_;
   std::vector<DevState> dstate_;
+  std::vector<std::vector<std::string>> owner_keys_;  // per device: device_owner_keys()
   std::unique_ptr<KfdProcReader> kfd_;
   std::unique_ptr<PidResolver> resolver_;
   std::unique_ptr<SentinelSource> sentinel_;
@@ -225,7 +226,7 @@ class Engine {
   // applied (sampler thread only)
   std::unordered_map<std::string, PodMeta> pods_by_uid_;
   std::unordered_map<std::string, std::string> container_names_;  // cid -> name
-  std::unordered_map<std::string, DeviceOwner> owners_;           // lower(bdf|uuid) -> owner
+  std::unordered_map<std::string, DeviceOwner> owners_;           // lower(device id) -> owner
   std::set<std::string> unresolved_;                               // pod UIDs without metadata (last tick)
 
   // stats (guarded by stats_mu_)

@@ -58,7 +58,9 @@ class Config:
     node_name: str = ""                    # downward API NODE_NAME
     kubelet_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"
     podresources: bool = True
-    gpu_resource_names: list = field(default_factory=lambda: ["amd.com/gpu"])
+    # device-plugin resources that are GPUs: whole GPUs, and the partition-mode resources
+    # of the AMD device plugin's "mixed" strategy (amd.com/cpx_nps4, amd.com/dpx_nps2, ...)
+    gpu_resource_names: list = field(default_factory=lambda: ["amd.com/gpu", "amd.com/*px_nps*"])
     apiserver: str = ""                    # "" = in-cluster (KUBERNETES_SERVICE_HOST) if present
     apiserver_token_file: str = "/var/run/secrets/kubernetes.io/serviceaccount/token"
     apiserver_ca_file: str = "/var/run/secrets/kubernetes.io/serviceaccount/ca.crt"

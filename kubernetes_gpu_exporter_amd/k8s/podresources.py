@@ -69,13 +69,26 @@ ListPodResourcesRequest = MSG["ListPodResourcesRequest"]
 ListPodResourcesResponse = MSG["ListPodResourcesResponse"]
 
 
+def resource_matches(name: str, patterns) -> bool:
+    """Exact resource names or shell-style patterns ("amd.com/*px_nps*")."""
+    import fnmatch
+    return any(name == p or (any(ch in p for ch in "*?[") and fnmatch.fnmatchcase(name, p)) for p in patterns)
+
+
 def owners_from_response(resp, resource_names) -> dict:
-    """device_id -> {namespace, pod, container} for the GPU resources."""
+    """device_id -> {namespace, pod, container} for the GPU resources.
+
+    Device ids are passed through as the device plugin reports them (lower-cased): a PCI
+    BDF for a whole GPU, and in partition mode an id per logical GPU (the BDF for
+    partition 0, the XCP platform device "amdgpu_xcp_<n>" / "amdgpu_xcp.<n>" for the
+    others, or "<bdf>/<n>", a render node, "kfd:<gpu_id>", a UUID).  The engine matches
+    them against each logical GPU's keys (device_owner_keys in csrc/gpuexp/device.h), so
+    partitions of one socket given to different pods keep different owners."""
     owners = {}
     for pr in resp.pod_resources:
         for c in pr.containers:
             for d in c.devices:
-                if d.resource_name not in resource_names:
+                if not resource_matches(d.resource_name, resource_names):
                     continue
                 for dev_id in d.device_ids:
                     owners[dev_id.lower()] = {"namespace": pr.namespace, "pod": pr.name, "container": c.name}
@@ -87,7 +100,7 @@ class PodResourcesSource(Source):
 
     def __init__(self, socket_path: str, resource_names=("amd.com/gpu",), timeout: float = 3.0):
         self.socket_path = socket_path
-        self.resource_names = set(resource_names)
+        self.resource_names = list(resource_names)
         self.timeout = timeout
         self._channel = None
         self._list = None

@@ -63,12 +63,44 @@ class FakeGpu:
     num_xcc: int = 8                 # 1 per partition in CPX mode
     compute_partition: str = "SPX"   # SPX | DPX | QPX | CPX
     memory_partition: str = "NPS1"
+    # sysfs device behind the render node: "" = a plain directory (older fixtures); a BDF
+    # = a PCI function under sys/devices (also linked from sys/bus/pci/devices); 
+    # "amdgpu_xcp.<n>" = the platform device of a partition >= 1 of a partitioned socket
+    dev_node: str = ""
+    # partitions >= 1: keep gpu_metrics / mem_info_* / hwmon on the socket's PCI function
+    # only (the XCP platform device carries none of them)
+    files_on_pci: bool = False
 
 
 class FakeHost:
     def __init__(self, root: str | os.PathLike):
         self.root = Path(root)
         self.gpus: list[FakeGpu] = []
+
+    def _bdf(self, gpu: FakeGpu) -> str:
+        return f"0000:{(gpu.location_id >> 8) & 0xFF:02x}:{(gpu.location_id >> 3) & 0x1F:02x}.{gpu.location_id & 7:x}"
+
+    def dev_dir(self, gpu: FakeGpu) -> str:
+        """Where the device's sysfs files go (relative to the root)."""
+        if gpu.files_on_pci:
+            return f"sys/bus/pci/devices/{self._bdf(gpu)}"
+        return f"sys/class/drm/renderD{gpu.render_minor}/device"
+
+    def _link_device(self, gpu: FakeGpu) -> None:
+        if not gpu.dev_node:
+            return
+        xcp = gpu.dev_node.startswith("amdgpu_xcp")
+        real = self.root / ("sys/devices/platform" if xcp else "sys/devices/pci0000:00") / gpu.dev_node
+        real.mkdir(parents=True, exist_ok=True)
+        link = self.root / f"sys/class/drm/renderD{gpu.render_minor}/device"
+        link.parent.mkdir(parents=True, exist_ok=True)
+        if not link.is_symlink():
+            link.symlink_to(real)
+        if not xcp:
+            pci = self.root / "sys/bus/pci/devices" / gpu.dev_node
+            pci.parent.mkdir(parents=True, exist_ok=True)
+            if not pci.is_symlink():
+                pci.symlink_to(real)
 
     def _w(self, rel: str, data, mode: str = "w") -> Path:
         p = self.root / rel
@@ -87,7 +119,8 @@ class FakeHost:
                  "device_id": gpu.device_id, "num_xcc": gpu.num_xcc, "gfx_target_version": 90500,
                  "max_engine_clk_fcompute": 2400}
         self._w(f"{nd}/properties", "".join(f"{k} {v}\n" for k, v in props.items()))
-        dev = f"sys/class/drm/renderD{gpu.render_minor}/device"
+        self._link_device(gpu)
+        dev = self.dev_dir(gpu)
         self._w(f"{dev}/mem_info_vram_total", f"{gpu.vram_total}\n")
         self._w(f"{dev}/mem_info_vram_used", f"{gpu.vram_used}\n")
         self._w(f"{dev}/gpu_busy_percent", "0\n")
@@ -111,12 +144,11 @@ class FakeHost:
 
     def set_metrics(self, gpu: FakeGpu, **kw) -> None:
         gpu.metrics = kw
-        dev = f"sys/class/drm/renderD{gpu.render_minor}/device"
-        self._w(f"{dev}/gpu_metrics", encode_gpu_metrics_v1_8(**kw), "wb")
+        self._w(f"{self.dev_dir(gpu)}/gpu_metrics", encode_gpu_metrics_v1_8(**kw), "wb")
 
     def set_ras(self, gpu: FakeGpu, blocks: dict | None = None, aer: tuple = (0, 0, 0)) -> None:
         """amdgpu ras/<block>_err_count ("ue: N\nce: N") and PCI aer_dev_* totals."""
-        dev = f"sys/class/drm/renderD{gpu.render_minor}/device"
+        dev = self.dev_dir(gpu)
         for block, (ue, ce) in (blocks or {"umc": (0, 0), "gfx": (0, 0)}).items():
             self._w(f"{dev}/ras/{block}_err_count", f"ue: {ue}\nce: {ce}\n")
         self._w(f"{dev}/ras/features", "feature mask: 0x3fff\n")
@@ -126,10 +158,10 @@ class FakeHost:
             self._w(f"{dev}/aer_dev_{n}", f"RxErr 0\nBadTLP 0\n{k} {v}\n")
 
     def set_vram_used(self, gpu: FakeGpu, used: int) -> None:
-        self._w(f"sys/class/drm/renderD{gpu.render_minor}/device/mem_info_vram_used", f"{used}\n")
+        self._w(f"{self.dev_dir(gpu)}/mem_info_vram_used", f"{used}\n")
 
     def remove_gpu_metrics(self, gpu: FakeGpu) -> None:
-        (self.root / f"sys/class/drm/renderD{gpu.render_minor}/device/gpu_metrics").unlink()
+        (self.root / self.dev_dir(gpu) / "gpu_metrics").unlink()
 
     # ---- processes ----
     def add_process(self, pid: int, cgroup: str, comm: str = "python3", gpus: dict | None = None,
@@ -177,16 +209,21 @@ def kubepods_cgroup(uid: str, container_id: str, qos: str = "burstable", driver:
     return f"/kubepods/{qos}/pod{uid}/{container_id}"
 
 
-def mi355x_cpx_socket(root, bus: int = 0x72, partitions: int = 8) -> FakeHost:
+def mi355x_cpx_socket(root, bus: int = 0x72, partitions: int = 8, xcp_files: bool = True) -> FakeHost:
     """One MI355X socket in CPX mode: `partitions` logical GPUs (one XCD each), each with
-    its own KFD node, gpu_id and render node but the socket's PCI BDF and gpu_metrics."""
+    its own KFD node, gpu_id and render node but the socket's PCI BDF and gpu_metrics.
+    As amdgpu lays it out, partition 0's render node sits on the PCI function and the
+    others' on platform devices amdgpu_xcp.<k>; xcp_files=False leaves those without any
+    socket files (they are read from the PCI function then)."""
     h = FakeHost(root)
     h.add_cpu_node(0)
+    bdf = f"0000:{bus:02x}:00.0"
     for k in range(partitions):
         h.add_gpu(1 + k, FakeGpu(gpu_id=41000 + 13 * k, location_id=bus << 8, render_minor=128 + k,
                                  num_xcc=8 // partitions, compute_partition="CPX" if partitions == 8 else
                                  {2: "DPX", 4: "QPX"}.get(partitions, "SPX"), memory_partition="NPS4",
-                                 vram_total=309220868096 // 4))
+                                 vram_total=309220868096 // 4, dev_node=bdf if k == 0 else f"amdgpu_xcp.{k}",
+                                 files_on_pci=k > 0 and not xcp_files))
     return h
 
 

@@ -261,3 +261,66 @@ def test_apiserver_outage_keeps_cache_and_recovers(tmp_path):
     finally:
         src.close()
         api.stop()
+
+
+@pytest.mark.parametrize("xcp_files", [True, False])
+def test_cpx_partitions_owned_by_eight_pods(tmp_path, xcp_files):
+    """A CPX-mode MI355X socket: 8 logical GPUs with ONE PCI BDF, each allocated to its own
+    pod by the device plugin (partition-mode resource amd.com/cpx_nps4; partition 0 named
+    by the BDF, the others by their XCP platform devices).  Every logical GPU's device
+    series must carry its own pod — keyed by BDF alone they would all collapse to one."""
+    import shutil
+    import tempfile
+    from pathlib import Path
+
+    from kubernetes_gpu_exporter_amd.exporter import Exporter
+    from kubernetes_gpu_exporter_amd.utils.fakehost import mi355x_cpx_socket
+    root = Path(tempfile.mkdtemp(prefix="c", dir="/tmp"))
+    try:
+        h = mi355x_cpx_socket(root, xcp_files=xcp_files)
+        for g in h.gpus:
+            h.set_metrics(g, gfx=50, num_partition=8)
+        ids = ["0000:72:00.0"] + [f"amdgpu_xcp_{k}" for k in range(1, 8)]
+        cpods = [FakePod(f"{k:08x}-0000-4000-8000-00000000000{k}", "infer", f"shard-{k}", "node-a",
+                         {"srv": f"{k:02x}" * 32}, {"srv": [ids[k]]}) for k in range(8)]
+        sock_rel = "/var/lib/kubelet/pod-resources/kubelet.sock"
+        kub = FakeKubelet(str(root) + sock_rel, cpods, resource="amd.com/cpx_nps4", node="node-a").start()
+        cfg = make_config({"backend": "sysfs", "host_root": str(root), "interval": 0, "listen": "127.0.0.1:0",
+                           "node_name": "node-a", "kubelet_socket": sock_rel, "control_interval": 0.05,
+                           "series_profile": "full"})
+        ex = Exporter(cfg)
+        try:
+            ex.start()
+            ex.tick(1_000_000_000)
+            ex.tick(1_100_000_000)
+            fams = promtext.parse(ex.text())
+            up = {s[1]["gpu"]: s[1] for s in fams["amd_gpu_up"].samples}
+            assert {g: (l["namespace"], l["pod"], l["container"]) for g, l in up.items()} == \
+                {str(k): ("infer", f"shard-{k}", "srv") for k in range(8)}
+            info = {s[1]["gpu"]: s[1] for s in fams["amd_gpu_info"].samples}
+            assert [info[str(k)]["device_node"] for k in range(8)] == ["0000:72:00.0"] + \
+                [f"amdgpu_xcp.{k}" for k in range(1, 8)]
+            assert {s[1]["bdf"] for s in fams["amd_gpu_up"].samples} == {"0000:72:00.0"}
+            # socket telemetry read from the PCI function for every partition
+            assert {s[2] for s in fams["amd_gpu_up"].samples} == {1.0}
+            assert all(promtext.value(fams, "amd_pod_gpus", pod=f"shard-{k}") == 1 for k in range(8))
+        finally:
+            ex.stop()
+            kub.stop()
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+
+
+def test_partition_owner_keys(native, tmp_path):
+    """Which device-plugin ids name which logical GPU: the bare BDF names partition 0 only;
+    XCP names (both spellings), <bdf>/<k>, render nodes, kfd:<id> and UUIDs each name one."""
+    from kubernetes_gpu_exporter_amd.utils.fakehost import mi355x_cpx_socket
+    h = mi355x_cpx_socket(tmp_path, partitions=4)
+    devs = native.read_backend("sysfs", str(tmp_path))
+    keys = [d["owner_keys"] for d in devs]
+    assert "0000:72:00.0" in keys[0] and all("0000:72:00.0" not in k for k in keys[1:])
+    for k in range(1, 4):
+        assert {f"amdgpu_xcp.{k}", f"amdgpu_xcp_{k}", f"0000:72:00.0/{k}", f"renderd{128 + k}",
+                f"/dev/dri/renderd{128 + k}", f"kfd:{h.gpus[k].gpu_id}"} <= set(keys[k])
+    flat = [x for ks in keys for x in ks if not x.startswith("e2")]  # UUIDs: shared unique_id in the fixture
+    assert len(flat) == len(set(flat))  # no id names two logical GPUs
