@@ -47,6 +47,7 @@ py::dict device_dict(const DeviceInfo& d) {
   o["num_xcc"] = d.num_xcc;
   o["partition_id"] = d.partition_id;
   o["dev_node"] = d.dev_node;
+  o["queue_enabled"] = d.queue_enabled;
   py::list keys;
   for (const auto& k : device_owner_keys(d)) keys.append(k);
   o["owner_keys"] = keys;
@@ -425,6 +426,9 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("enable_rccl", &EngineConfig::enable_rccl)
       .def_readwrite("rccl_dir", &EngineConfig::rccl_dir)
       .def_readwrite("rccl_verify", &EngineConfig::rccl_verify)
+      .def_readwrite("metrics_min_interval_s", &EngineConfig::metrics_min_interval_s)
+      .def_readwrite("queue_devices", &EngineConfig::queue_devices)
+      .def_readwrite("queue_devices_bdf", &EngineConfig::queue_devices_bdf)
       .def_readwrite("force_amdsmi_metrics", &EngineConfig::force_amdsmi_metrics)
       .def_readwrite("gzip_level", &EngineConfig::gzip_level)
       .def_readwrite("gc_after", &EngineConfig::gc_after)

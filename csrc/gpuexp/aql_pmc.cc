@@ -692,11 +692,18 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_init(int ndev, c
   // Partitioned sockets (CPX/DPX/QPX) expose several agents with one BDF, in partition
   // order, as do the exporter's devices: match the k-th device to the k-th free agent.
   std::vector<bool> taken(f.gpus.size(), false);
+  int disabled = 0;
   for (int d = 0; d < ndev; ++d) {
+    const bool off = bdfs[d][0] == '-';  // reserve the agent, no queue (queue_devices)
+    const std::string want = lower(bdfs[d] + (off ? 1 : 0));
     for (size_t gi = 0; gi < f.gpus.size(); ++gi) {
       const auto& g = f.gpus[gi];
-      if (taken[gi] || lower(bdfs[d]) != g.second) continue;
+      if (taken[gi] || want != g.second) continue;
       taken[gi] = true;
+      if (off) {
+        ++disabled;
+        break;
+      }
       auto* a = new Agent;
       a->dev = d;
       a->gpu = g.first;
@@ -708,7 +715,9 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_init(int ndev, c
   }
   if (!ok) {
     teardown_locked();
-    return fail(why.empty() ? "no HSA GPU agent matched the exporter's GPUs" : why);
+    return fail(why.empty() ? (disabled ? "every GPU excluded by queue_devices"
+                                        : "no HSA GPU agent matched the exporter's GPUs")
+                            : why);
   }
   g_quit.store(false);
   g_thread = std::thread(counting_loop);

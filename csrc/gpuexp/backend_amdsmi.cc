@@ -224,6 +224,7 @@ class AmdsmiBackend : public Backend {
           d.nxcc = int(info.num_xcc);
           if (!force_smi_ && d.gm.open(dir + "/gpu_metrics", &e)) d.fast_ok = validate(d);
           d.gm.set_coalesce(coalesce_metrics_);
+          d.gm.set_min_fresh_interval(metrics_min_ns_);
           if (!d.fast_ok)
             GPUEXP_LOG(LogLevel::kInfo, "amdsmi",
                        "gpu " + std::to_string(info.index) + ": using amdsmi_get_gpu_metrics_info per tick (" +

@@ -198,6 +198,7 @@ void SysfsBackend::open_dev_files(Dev* d) {
   std::string e;
   d->gm_ok = d->gm.open(d->dev_dir + "/gpu_metrics", &e);
   d->gm.set_coalesce(coalesce_metrics_);
+  d->gm.set_min_fresh_interval(metrics_min_ns_);
   d->gm.set_partition(d->xcp, d->nxcc);
   d->vram_used.open(d->dev_dir + "/mem_info_vram_used");
   d->busy.open(d->dev_dir + "/gpu_busy_percent");

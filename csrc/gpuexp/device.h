@@ -44,6 +44,9 @@ struct DeviceInfo {
   // BDF is not (see device_owner_keys).
   std::string dev_node;
   std::string xgmi_peer_bdf[kMaxXgmiLinks];  // from amdsmi_get_link_metrics (once)
+  // false: no exporter-owned GPU queue on this device (no sentinel, no PMC counters); each
+  // queue pins ~346 MiB of host memory on MI355X (profiles/r02/queue_memory.txt)
+  bool queue_enabled = true;
 };
 
 // Basename of realpath(<root>/sys/class/drm/renderD<minor>/device): the BDF or
@@ -164,6 +167,7 @@ class Backend {
   virtual ~Backend() = default;
   // gpu_metrics read coalescing (GpuMetricsReader); set before init().
   void set_metrics_coalescing(bool on) { coalesce_metrics_ = on; }
+  void set_metrics_min_interval(uint64_t ns) { metrics_min_ns_ = ns; }
   virtual const char* name() const = 0;
   // Enumerates devices once.  Returns false (with *err) if the backend cannot run.
   virtual bool init(std::vector<DeviceInfo>* devices, std::string* err) = 0;
@@ -201,6 +205,7 @@ class Backend {
   virtual void shutdown() {}
  protected:
   bool coalesce_metrics_ = true;
+  uint64_t metrics_min_ns_ = 0;
 };
 
 }  // namespace gpuexp

@@ -310,6 +310,7 @@ bool Engine::start(std::string* err) {
     return false;
   }
   backend_->set_metrics_coalescing(cfg_.metrics_coalesce);
+  backend_->set_metrics_min_interval(uint64_t(std::max(0.0, cfg_.metrics_min_interval_s) * 1e9));
   std::vector<DeviceInfo> all;
   if (!backend_->init(&all, err)) return false;
   if (!cfg_.device_filter.empty() || !cfg_.device_filter_bdf.empty()) {
@@ -326,6 +327,16 @@ bool Engine::start(std::string* err) {
   } else {
     devices_ = all;
   }
+  if (!cfg_.queue_devices.empty() || !cfg_.queue_devices_bdf.empty()) {
+    for (auto& d : devices_) {
+      bool on = std::find(cfg_.queue_devices.begin(), cfg_.queue_devices.end(), d.index) != cfg_.queue_devices.end();
+      for (const auto& b : cfg_.queue_devices_bdf) on = on || lower(b) == lower(d.bdf);
+      d.queue_enabled = on;
+    }
+  }
+  const bool any_queue = std::any_of(devices_.begin(), devices_.end(), [](const DeviceInfo& d) {
+    return d.queue_enabled;
+  });
   dstate_.assign(devices_.size(), DevState());
   owner_keys_.clear();
   for (const DeviceInfo& d : devices_) owner_keys_.push_back(device_owner_keys(d));
@@ -353,7 +364,9 @@ bool Engine::start(std::string* err) {
 
   // Counters first: the rocprofiler tool must register before the HSA runtime loads,
   // which the sentinel's first HIP call does.
-  if (cfg_.enable_counters && cfg_.backend != "mock") {
+  if (cfg_.enable_counters && cfg_.backend != "mock" && !any_queue) {
+    counters_status_ = "disabled: no GPU in queue_devices";
+  } else if (cfg_.enable_counters && cfg_.backend != "mock") {
     counters_ = make_rocprof_counters(cfg_.counters_plugin, cfg_.counters_window_ms, cfg_.counters_interval_ms);
     std::string e;
     if (!counters_ || !counters_->start(devices_, &e)) {
@@ -366,7 +379,9 @@ bool Engine::start(std::string* err) {
   } else if (cfg_.enable_counters) {
     counters_status_ = "mock";
   }
-  if (cfg_.enable_sentinel && cfg_.backend != "mock") {
+  if (cfg_.enable_sentinel && cfg_.backend != "mock" && !any_queue) {
+    sentinel_status_ = "disabled: no GPU in queue_devices";
+  } else if (cfg_.enable_sentinel && cfg_.backend != "mock") {
     std::string e;
     // Prefer the counters plugin's queue (one GPU queue, and its ~173 MiB context save
     // area, per GPU instead of two); the HIP plugin's own stream otherwise.

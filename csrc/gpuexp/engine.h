@@ -66,6 +66,7 @@ struct EngineConfig {
   std::string series_profile = "standard";  // standard | full | compact | legacy
   double ras_interval_s = 10.0;        // full profile: RAS/AER sysfs re-read period
   bool metrics_coalesce = true;        // skip gpu_metrics SMU fetches between PMFW refreshes
+  double metrics_min_interval_s = 0;   // at most one SMU fetch per GPU per this many seconds (0 = no cap)
   bool legacy_families = true;         // pod_gpu_memory_usage / docker_gpu_memory_perc_usage
   bool pod_attribution = true;
   bool infer_device_owner = true;      // single-pod GPU -> device series carry the pod
@@ -89,6 +90,10 @@ struct EngineConfig {
   uint64_t gc_after = 1;               // stale series vanish this many ticks after last seen
   std::vector<int> device_filter;      // empty = all
   std::vector<std::string> device_filter_bdf;  // also accepted: PCI BDFs ("0000:75:00.0")
+  // GPUs that get the exporter's own GPU queue (sentinel + PMC counters), by index or BDF;
+  // both empty = every exported GPU.  ~346 MiB of pinned host memory per queue on MI355X.
+  std::vector<int> queue_devices;
+  std::vector<std::string> queue_devices_bdf;
   std::string trace_path;              // Chrome trace JSON of sampler stages
   size_t trace_max_events = 200000;
   std::string version = "0.1.0";

@@ -93,6 +93,7 @@ GpuMetricsReader& GpuMetricsReader::operator=(GpuMetricsReader&& o) noexcept {
   fmt_ = o.fmt_;
   content_ = o.content_;
   coalesce_ = o.coalesce_;
+  min_fresh_ns_ = o.min_fresh_ns_;
   xcp_ = o.xcp_;
   nxcc_ = o.nxcc_;
   last_n_ = o.last_n_;
@@ -147,6 +148,13 @@ bool GpuMetricsReader::read(DeviceSample* out, uint64_t now_ns) {
   const uint64_t window = std::min(period_ns_, kMaxCoalesceNs);
   if (coalesce_ && now_ns && last_n_ > 0 && window > kGuardNs && t_change_ns_ && now_ns >= t_change_ns_ &&
       now_ns < t_change_ns_ + window - kGuardNs) {
+    coalesced_reads_ += 1;
+    last_was_fresh_ = false;
+    out->metrics_coalesced = true;
+    return decode_gpu_metrics_v1_8(buf_, size_t(last_n_), out, xcp_, nxcc_);
+  }
+  if (min_fresh_ns_ && now_ns && last_n_ > 0 && last_read_ns_ && now_ns > last_read_ns_ &&
+      now_ns - last_read_ns_ < min_fresh_ns_) {
     coalesced_reads_ += 1;
     last_was_fresh_ = false;
     out->metrics_coalesced = true;

@@ -57,8 +57,12 @@ class PluginCounters : public CounterSource {
     using duty_fn = void (*)(int, int);
     if (auto duty = reinterpret_cast<duty_fn>(::dlsym(handle_, "gpuexp_rp_set_duty")))
       duty(window_ms_, interval_ms_);
+    // ABI: a BDF prefixed with '-' reserves that device's HSA agent (partition order) but
+    // gets no queue.
+    std::vector<std::string> names;
+    for (auto& d : devs) names.push_back((d.queue_enabled ? "" : "-") + d.bdf);
     std::vector<const char*> bdfs;
-    for (auto& d : devs) bdfs.push_back(d.bdf.c_str());
+    for (auto& n : names) bdfs.push_back(n.c_str());
     char ebuf[512] = {0};
     int n = init_(int(devs.size()), bdfs.data(), ebuf, sizeof(ebuf));
     if (n <= 0) {

@@ -112,21 +112,25 @@ int tool_init(rocprofiler_client_finalize_t fini, void*) {
                   (a.location_id >> 3) & 0x1F, a.location_id & 0x7);
     for (size_t d = 0; d < g_want_bdfs.size(); ++d) {
       // several agents share a BDF on a partitioned socket: first free device slot wins
-      if (lower(g_want_bdfs[d]) != bdf || g_agents[d].dev >= 0) continue;
+      const bool off = !g_want_bdfs[d].empty() && g_want_bdfs[d][0] == '-';  // queue_devices: reserve only
+      if (lower(off ? g_want_bdfs[d].substr(1) : g_want_bdfs[d]) != bdf || g_agents[d].dev >= 0) continue;
       Agent& ag = g_agents[d];
       ag.id = a.id;
       ag.dev = int(d);
+      if (off) break;
       ag.m.simd = a.simd_count;
       ag.m.privileged = pmc_device_scope();
       ag.m.cu = a.cu_count ? a.cu_count : (a.simd_per_cu ? a.simd_count / a.simd_per_cu : 0);
-      if (rocprofiler_create_context(&ag.ctx) != ROCPROFILER_STATUS_SUCCESS) continue;
+      // one agent per device slot (partitions of a socket share a BDF): stop at the first
+      if (rocprofiler_create_context(&ag.ctx) != ROCPROFILER_STATUS_SUCCESS) break;
       rocprofiler_buffer_id_t nobuf{};  // values come back in the sample call itself
       if (rocprofiler_configure_device_counting_service(ag.ctx, nobuf, a.id, set_profile_cb, &ag) !=
           ROCPROFILER_STATUS_SUCCESS) {
         g_err = "configure_device_counting_service failed for " + std::string(bdf);
-        continue;
+        break;
       }
       ++matched;
+      break;
     }
   }
   g_configured = matched > 0;

@@ -123,7 +123,7 @@ class HipSentinel : public SentinelSource {
           p.hip = h;
           taken[size_t(h)] = true;
         }
-      if (p.hip < 0) continue;
+      if (p.hip < 0 || !devs[i].queue_enabled) continue;  // disabled: its HIP device stays reserved
       if (hipSetDevice(p.hip) != hipSuccess) continue;
       p.run.waves = devs[i].num_xcc ? std::min<int>(int(devs[i].num_xcc), kSentinelMaxWaves) : kSentinelMaxWaves;
       int least = 0, greatest = 0;

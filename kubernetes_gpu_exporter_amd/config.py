@@ -31,6 +31,8 @@ class Config:
     backend: str = "auto"                  # auto | amdsmi | sysfs | mock
     device_threads: int = 0                # per-GPU read fan-out (0 = auto, 1 = serial)
     metrics_coalesce: bool = True          # skip gpu_metrics SMU fetches until the PMFW refreshes
+    metrics_min_interval: float = 0.0      # at most one gpu_metrics SMU fetch per GPU per this many s
+                                           # (0 = every PMFW refresh): bounds sampler CPU at 8 GPUs x 100 Hz
     mock_devices: int = 1
     host_root: str = ""                    # prefix for /sys and /proc (DaemonSet: /host)
     devices: list = field(default_factory=list)  # GPU indices and/or PCI BDFs to export (empty = all)
@@ -49,6 +51,9 @@ class Config:
     counters_plugin: str = "aqlpmc"        # aqlpmc | rocprof | /path/to/plugin.so
     counters_window_ms: int = 20           # rocprofiler counting window ...
     counters_interval_ms: int = 1000       # ... per interval (context-started spin is duty-cycled)
+    queue_devices: list = field(default_factory=list)  # GPUs (indices / BDFs) that get the exporter's
+                                           # own GPU queue (sentinel + PMC counters); empty = all.
+                                           # Each queue pins ~346 MiB of host memory on MI355X.
     enable_rccl: bool = False
     rccl_dir: str = "/var/run/gpuexp/rccl"
     rccl_verify: bool = True               # a tracer file counts only for a live process that maps it
@@ -102,6 +107,7 @@ class Config:
         ec.mock_devices = int(self.mock_devices)
         ec.device_threads = int(self.device_threads)
         ec.metrics_coalesce = bool(self.metrics_coalesce)
+        ec.metrics_min_interval_s = float(self.metrics_min_interval)
         ec.host_root = self.host_root
         ec.interval_s = float(self.interval)
         host, port = self.listen_host_port()
@@ -142,6 +148,8 @@ class Config:
         ec.gc_after = int(self.gc_after)
         ec.device_filter = [int(d) for d in self.devices if ":" not in str(d)]
         ec.device_filter_bdf = [str(d) for d in self.devices if ":" in str(d)]
+        ec.queue_devices = [int(d) for d in self.queue_devices if ":" not in str(d)]
+        ec.queue_devices_bdf = [str(d) for d in self.queue_devices if ":" in str(d)]
         ec.trace_path = self.trace
         from . import __version__
         ec.version = __version__
@@ -241,6 +249,8 @@ def validate(cfg: Config) -> None:
         raise ValueError(f"backend must be auto|amdsmi|sysfs|mock, got {cfg.backend}")
     if cfg.series_profile not in ("full", "standard", "compact", "legacy"):
         raise ValueError(f"series_profile must be full|standard|compact|legacy, got {cfg.series_profile}")
+    if cfg.metrics_min_interval < 0:
+        raise ValueError("metrics_min_interval must be >= 0")
     if cfg.ras_interval <= 0:
         raise ValueError("ras_interval must be > 0")
     if cfg.process_source not in ("auto", "kfd", "amdsmi", "none"):

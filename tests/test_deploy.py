@@ -105,3 +105,25 @@ def test_grafana_dashboard_uses_exported_metrics():
         for name in re.findall(r"\b(amd_[a-z0-9_]+)", v.get("query", "")):
             used.add(name)
     assert len(dash["panels"]) >= 10 and used <= known, used - known
+
+
+def test_memory_sized_for_one_queue_per_gpu():
+    """Every GPU that gets the exporter's queue pins 346 MiB on MI355X
+    (profiles/r02/queue_memory.txt): the static DaemonSet requests it for 8 GPUs, the Helm
+    chart computes it from queueDevices / gpusPerNode."""
+    (ds,) = docs("daemonset.yaml")
+    c = ds["spec"]["template"]["spec"]["containers"][0]
+
+    def mib(q):
+        return int(q[:-2]) * (1024 if q.endswith("Gi") else 1)
+    assert mib(c["resources"]["requests"]["memory"]) >= 40 + 8 * 346
+    assert mib(c["resources"]["limits"]["memory"]) >= mib(c["resources"]["requests"]["memory"])
+    chart = os.path.join(ROOT, "deploy", "helm", "gpuexp")
+    with open(os.path.join(chart, "values.yaml")) as fh:
+        values = yaml.safe_load(fh)
+    assert values["memoryPerQueueGpuMi"] >= 346 and values["gpusPerNode"] == 8
+    with open(os.path.join(chart, "templates", "daemonset.yaml")) as fh:
+        tpl = fh.read()
+    assert "mul $queueGpus .Values.memoryPerQueueGpuMi" in tpl and "--queue-devices=" in tpl
+    cfg = load_config(["--queue-devices", "0,0000:72:00.0"], env={})
+    assert cfg.queue_devices == ["0", "0000:72:00.0"]

@@ -438,3 +438,72 @@ def test_spx_socket_keeps_socket_activity(native, tmp_path):
         assert (inf[1]["partition"], inf[1]["compute_partition"], inf[1]["memory_partition"]) == ("0", "SPX", "NPS1")
     finally:
         e.stop()
+
+
+def test_gpu_metrics_min_interval_caps_fresh_reads(native, tmp_path):
+    """metrics_min_interval=0.05: at 100 Hz at most one SMU fetch per 50 ms per GPU (the
+    kernel CPU of the fetches is what grows with GPUs x Hz); tables are at most 50 ms old."""
+    h = mi355x_node(tmp_path, 1)
+    (g,) = h.gpus
+    e = _engine(native, tmp_path, metrics_min_interval_s=0.05, metrics_coalesce=False)
+    for k in range(100):  # 1 s at 100 Hz, a new table every 10 ms
+        h.set_metrics(g, fw_ts=105165583750064 + k * 1_000_000, power=300 + k)
+        e.tick(1 * S + k * 10_000_000)
+    fams = promtext.parse(e.snapshot_text())
+    reads = _reads(fams)
+    assert reads["fresh"] == 20 and reads["coalesced"] == 80, reads
+    assert promtext.samples(fams, "amd_gpu_power_watts")[0][2] >= 300 + 95  # <= 50 ms old
+    e.stop()
+
+
+def test_queue_devices_limit_gpu_queues(native, tmp_path):
+    """queue_devices picks the GPUs that get the exporter's own GPU queue (sentinel + PMC);
+    the others keep every sysfs/amdsmi family."""
+    mi355x_node(tmp_path, 4)
+    e = _engine(native, tmp_path, queue_devices=[1], queue_devices_bdf=["0000:72:00.0"])
+    try:
+        devs = {d["index"]: d for d in e.devices()}
+        on = {i for i, d in devs.items() if d["queue_enabled"]}
+        assert on == {1} | {i for i, d in devs.items() if d["bdf"] == "0000:72:00.0"}
+        assert len(on) == 2
+    finally:
+        e.stop()
+    e = _engine(native, tmp_path)
+    try:
+        assert all(d["queue_enabled"] for d in e.devices())  # default: every GPU
+    finally:
+        e.stop()
+
+
+def _sampler_cpu_per_tick(native, root, n_gpus, seconds=2.5):
+    import time
+    h = mi355x_node(root, n_gpus)
+    for i, g in enumerate(h.gpus):
+        for p in range(4):  # 4 GPU processes per GPU: KFD reads + attribution scale with them
+            h.add_process(5000 + 10 * i + p, kubepods_cgroup(UID, CID), gpus={g.gpu_id: ((p + 1) << 30, 32)})
+    c = native.EngineConfig()
+    c.backend = "sysfs"
+    c.host_root = str(root)
+    c.interval_s = 0.1
+    c.serve_http = False
+    c.series_profile = "full"
+    e = native.Engine(c)
+    e.start()
+    time.sleep(seconds)
+    st = e.stats()
+    e.stop()
+    return st["sampler_cpu_ns"] / max(1, st["ticks"]) / 1e3, st["ticks"]
+
+
+def test_sampler_cpu_scales_at_most_linearly_to_8_gpus(native, tmp_path):
+    """Real file reads on a fake 8-GPU MI355X node at 10 Hz: the sampler's CPU per tick
+    grows no faster than the GPU count (the series table, render and attribution are
+    shared work) and stays within budget: < 2 ms per tick = 2 % of a core at 10 Hz on the
+    fake filesystem.  (The real gpu_metrics SMU fetch adds 120-420 us of kernel CPU per GPU
+    per fresh read: metrics_min_interval caps that; profiles/r01/kfd_read_costs.txt.)"""
+    one, t1 = _sampler_cpu_per_tick(native, tmp_path / "n1", 1)
+    eight, t8 = _sampler_cpu_per_tick(native, tmp_path / "n8", 8)
+    print(f"sampler CPU per tick: 1 GPU {one:.0f} us ({t1} ticks), 8 GPUs {eight:.0f} us ({t8} ticks)")
+    assert t1 >= 15 and t8 >= 15
+    assert eight <= 8 * one * 1.25, (one, eight)
+    assert eight < 2000, eight
