@@ -1,16 +1,14 @@
 """`python -m kubernetes_gpu_exporter_amd [flags]` — run the exporter."""
-import logging
 import sys
 
 from .config import load_config
 from .exporter import Exporter
+from .utils import logfmt
 
 
 def main(argv=None) -> int:
     cfg = load_config(argv)
-    logging.basicConfig(level={"debug": logging.DEBUG, "info": logging.INFO, "warn": logging.WARNING,
-                               "error": logging.ERROR, "off": logging.CRITICAL}[cfg.log_level],
-                        format="ts=%(asctime)s level=%(levelname)s component=%(name)s msg=\"%(message)s\"")
+    logfmt.setup(cfg.log_level)  # same line format as the C++ core
     return Exporter(cfg).run_forever()
 
 

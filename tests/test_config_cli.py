@@ -110,3 +110,21 @@ def test_listen_and_stale_after_validation():
     for bad in ({"listen": "no-such-host.invalid:9000"}, {"stale_after": -5}):
         with pytest.raises(ValueError):
             make_config(bad)
+
+
+def test_python_logs_are_logfmt_like_the_core(capsys):
+    """Control-plane log lines use the C++ core's logfmt (csrc/gpuexp/common.cc)."""
+    import logging
+    import re
+
+    from kubernetes_gpu_exporter_amd.utils import logfmt
+    logfmt.setup("info")
+    try:
+        logging.getLogger("gpuexp.control").warning('source "x" failed:\nboom \\ done')
+        logging.getLogger("gpuexp").debug("hidden at info")
+    finally:
+        logfmt.setup("warn")
+    err = capsys.readouterr().err.strip().splitlines()
+    assert len(err) == 1, err
+    assert re.fullmatch(r'ts=\d+\.\d{3} level=warn component=control msg="source \\"x\\" failed: boom \\\\ done"',
+                        err[0]), err[0]
