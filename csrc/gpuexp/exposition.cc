@@ -105,7 +105,7 @@ SeriesRef SeriesTable::upsert(int fid, const std::vector<std::string>& values) {
     keybuf_.push_back('\0');
   }
   auto it = index_.find(keybuf_);
-  if (it != index_.end()) return SeriesRef{it->second, series_[it->second].ver};
+  if (it != index_.end()) return SeriesRef{it->second, hot_[it->second].ver};
 
   uint32_t idx;
   if (!free_.empty()) {
@@ -114,12 +114,15 @@ SeriesRef SeriesTable::upsert(int fid, const std::vector<std::string>& values) {
   } else {
     idx = uint32_t(series_.size());
     series_.emplace_back();
+    hot_.emplace_back();
   }
+  Hot& h = hot_[idx];
   Series& s = series_[idx];
-  s.fid = fid;
-  s.ver += 1;
-  s.gen = 0;
-  s.value = 0;
+  h.fid = fid;
+  h.ver += 1;
+  h.gen = 0;
+  h.value = 0;
+  h.in_cache = false;
   s.labels = values;
   s.key = keybuf_;
   s.bounds.clear();
@@ -145,30 +148,38 @@ SeriesRef SeriesTable::upsert(int fid, const std::vector<std::string>& values) {
   index_.emplace(s.key, idx);
   fam.members.push_back(idx);
   fam.dirty_order = true;
-  return SeriesRef{idx, s.ver};
+  fam.dirty = true;
+  return SeriesRef{idx, h.ver};
 }
 
 bool SeriesTable::set(SeriesRef r, double v, uint64_t gen) {
-  if (!r.valid() || r.idx >= series_.size()) return false;
-  Series& s = series_[r.idx];
-  if (s.ver != r.ver || s.fid < 0) return false;
-  s.value = v;
-  s.gen = gen;
+  if (!r.valid() || r.idx >= hot_.size()) return false;
+  Hot& h = hot_[r.idx];
+  if (h.ver != r.ver || h.fid < 0) return false;
+  uint64_t a, b;
+  std::memcpy(&a, &h.value, sizeof(a));
+  std::memcpy(&b, &v, sizeof(b));
+  if (a != b) {
+    h.value = v;
+    mark_dirty(h.fid);
+  }
+  h.gen = gen;
   return true;
 }
 
 bool SeriesTable::touch(SeriesRef r, uint64_t gen) {
-  if (!r.valid() || r.idx >= series_.size()) return false;
-  Series& s = series_[r.idx];
-  if (s.ver != r.ver || s.fid < 0) return false;
-  s.gen = gen;
+  if (!r.valid() || r.idx >= hot_.size()) return false;
+  Hot& h = hot_[r.idx];
+  if (h.ver != r.ver || h.fid < 0) return false;
+  h.gen = gen;
   return true;
 }
 
 bool SeriesTable::observe(SeriesRef r, double v, uint64_t gen, const std::vector<double>& bounds) {
-  if (!r.valid() || r.idx >= series_.size()) return false;
+  if (!r.valid() || r.idx >= hot_.size()) return false;
+  Hot& h = hot_[r.idx];
+  if (h.ver != r.ver || h.fid < 0) return false;
   Series& s = series_[r.idx];
-  if (s.ver != r.ver || s.fid < 0) return false;
   if (s.bounds.empty()) {
     s.bounds = bounds;
     s.buckets.assign(bounds.size(), 0);
@@ -179,40 +190,51 @@ bool SeriesTable::observe(SeriesRef r, double v, uint64_t gen, const std::vector
   if (it != s.bounds.end()) s.buckets[size_t(it - s.bounds.begin())] += 1;
   s.hsum += v;
   s.hcount += 1;
-  s.gen = gen;
+  h.gen = gen;
+  mark_dirty(h.fid);
   return true;
 }
 
 bool SeriesTable::set_histogram(SeriesRef r, const std::vector<double>& bounds,
                                 const std::vector<uint64_t>& counts, double sum, uint64_t count,
                                 uint64_t gen) {
-  if (!r.valid() || r.idx >= series_.size()) return false;
+  if (!r.valid() || r.idx >= hot_.size()) return false;
+  Hot& h = hot_[r.idx];
+  if (h.ver != r.ver || h.fid < 0) return false;
   Series& s = series_[r.idx];
-  if (s.ver != r.ver || s.fid < 0) return false;
+  bool changed = s.hcount != count || s.hsum != sum || s.bounds != bounds;
   if (s.bounds != bounds) {
     s.bounds = bounds;
     s.hlines.clear();
   }
-  s.buckets.assign(bounds.size(), 0);
-  for (size_t i = 0; i < bounds.size() && i < counts.size(); ++i) s.buckets[i] = counts[i];
+  s.buckets.resize(bounds.size(), 0);
+  for (size_t i = 0; i < bounds.size(); ++i) {
+    const uint64_t c = i < counts.size() ? counts[i] : 0;
+    changed = changed || s.buckets[i] != c;
+    s.buckets[i] = c;
+  }
   s.hsum = sum;
   s.hcount = count;
-  s.gen = gen;
+  h.gen = gen;
+  if (changed) mark_dirty(h.fid);
   return true;
 }
 
 double SeriesTable::value(SeriesRef r) const {
-  if (!r.valid() || r.idx >= series_.size()) return std::nan("");
-  const Series& s = series_[r.idx];
-  if (s.ver != r.ver) return std::nan("");
-  return s.value;
+  if (!r.valid() || r.idx >= hot_.size()) return std::nan("");
+  const Hot& h = hot_[r.idx];
+  if (h.ver != r.ver) return std::nan("");
+  return h.value;
 }
 
 void SeriesTable::free_series(uint32_t idx) {
+  Hot& h = hot_[idx];
   Series& s = series_[idx];
   index_.erase(s.key);
-  s.fid = -1;
-  s.ver += 1;
+  if (h.fid >= 0) mark_dirty(h.fid);
+  h.fid = -1;
+  h.ver += 1;
+  h.in_cache = false;
   s.labels.clear();
   s.prefix.clear();
   s.line.clear();
@@ -240,14 +262,17 @@ void SeriesTable::sort_members(Family& f) {
     return false;
   });
   f.dirty_order = false;
+  f.dirty = true;
 }
 
-void SeriesTable::append_cached_value(std::string* out, Series& s) {
+void SeriesTable::append_cached_value(std::string* out, uint32_t idx) {
+  Series& s = series_[idx];
+  const double v = hot_[idx].value;
   uint64_t bits;
-  std::memcpy(&bits, &s.value, sizeof(bits));
+  std::memcpy(&bits, &v, sizeof(bits));
   if (!s.vvalid || bits != s.vbits) {
     std::string tmp;
-    append_value(&tmp, s.value);
+    append_value(&tmp, v);
     s.vlen = uint8_t(std::min(tmp.size(), sizeof(s.vtxt)));
     std::memcpy(s.vtxt, tmp.data(), s.vlen);
     s.vbits = bits;
@@ -256,11 +281,12 @@ void SeriesTable::append_cached_value(std::string* out, Series& s) {
   out->append(s.vtxt, s.vlen);
 }
 
-void SeriesTable::render_histogram(std::string* out, Series& s) const {
+void SeriesTable::render_histogram(std::string* out, uint32_t idx) {
   // name_bucket{labels,le="x"} cumulative ... _sum, _count.  The line prefixes depend only
   // on the labels and the (fixed) bounds: built once, then each render appends numbers.
+  Series& s = series_[idx];
   if (s.hlines.size() != s.bounds.size() + 3) {
-    const Family& fam = families_[size_t(s.fid)];
+    const Family& fam = families_[size_t(hot_[idx].fid)];
     const std::string& base = fam.def.name;
     std::string labels;  // `a="x",b="y"`
     if (s.prefix.size() > base.size() + 2) labels = s.prefix.substr(base.size() + 1, s.prefix.size() - base.size() - 2);
@@ -301,50 +327,68 @@ void SeriesTable::render_histogram(std::string* out, Series& s) const {
 
 void SeriesTable::render(std::string* out, uint64_t gen, uint64_t gc_after) {
   out->clear();
+  last_rebuilt_ = 0;
   for (int fid : render_order_) {
     Family& fam = families_[size_t(fid)];
-    // GC pass: drop members that have been stale for longer than gc_after gens.
+    // GC + liveness pass over the dense hot array: drop members stale for longer than
+    // gc_after gens; a member whose liveness differs from the cached text dirties it.
     bool any_live = false;
     size_t w = 0;
     for (size_t i = 0; i < fam.members.size(); ++i) {
       uint32_t idx = fam.members[i];
-      Series& s = series_[idx];
-      if (s.gen + gc_after < gen) {
+      Hot& h = hot_[idx];
+      if (h.gen + gc_after < gen) {
         free_series(idx);
         continue;
       }
       fam.members[w++] = idx;
-      if (s.gen == gen) any_live = true;
+      const bool live = h.gen == gen;
+      any_live = any_live || live;
+      if (live != h.in_cache) fam.dirty = true;
     }
     fam.members.resize(w);
-    if (!any_live) continue;
-    if (fam.dirty_order) sort_members(fam);
-    out->append(fam.header);
-    for (uint32_t idx : fam.members) {
-      Series& s = series_[idx];
-      if (s.gen != gen) continue;
-      if (fam.def.type == MetricType::kHistogram) {
-        render_histogram(out, s);
-        continue;
+    if (!any_live) {
+      if (!fam.cache.empty()) {
+        fam.cache.clear();
+        for (uint32_t idx : fam.members) hot_[idx].in_cache = false;
       }
-      out->append(s.line);
-      append_cached_value(out, s);
-      out->push_back('\n');
+      fam.dirty = false;
+      continue;
     }
+    if (fam.dirty_order) sort_members(fam);
+    if (fam.dirty) {
+      ++last_rebuilt_;
+      fam.cache.clear();
+      fam.cache.append(fam.header);
+      for (uint32_t idx : fam.members) {
+        Hot& h = hot_[idx];
+        h.in_cache = h.gen == gen;
+        if (!h.in_cache) continue;
+        if (fam.def.type == MetricType::kHistogram) {
+          render_histogram(&fam.cache, idx);
+          continue;
+        }
+        fam.cache.append(series_[idx].line);
+        append_cached_value(&fam.cache, idx);
+        fam.cache.push_back('\n');
+      }
+      fam.dirty = false;
+    }
+    out->append(fam.cache);
   }
 }
 
 size_t SeriesTable::live_series(uint64_t gen) const {
   size_t n = 0;
-  for (auto& s : series_)
-    if (s.fid >= 0 && s.gen == gen) ++n;
+  for (auto& h : hot_)
+    if (h.fid >= 0 && h.gen == gen) ++n;
   return n;
 }
 
 size_t SeriesTable::live_series_in_family(int fid, uint64_t gen) const {
   size_t n = 0;
   for (uint32_t idx : families_[size_t(fid)].members)
-    if (series_[idx].gen == gen) ++n;
+    if (hot_[idx].gen == gen) ++n;
   return n;
 }
 
@@ -391,7 +435,7 @@ void SeriesTable::render_proto(std::string* out, uint64_t gen) const {
     const Family& fam = families_[size_t(fid)];
     bool any = false;
     for (uint32_t idx : fam.members)
-      if (series_[idx].gen == gen) {
+      if (hot_[idx].gen == gen) {
         any = true;
         break;
       }
@@ -407,7 +451,7 @@ void SeriesTable::render_proto(std::string* out, uint64_t gen) const {
     pb_u64(&fam_buf, 3, uint64_t(type));
     for (uint32_t idx : fam.members) {
       const Series& s = series_[idx];
-      if (s.gen != gen) continue;
+      if (hot_[idx].gen != gen) continue;
       metric.clear();
       for (size_t i : order) {
         lp.clear();
@@ -429,7 +473,7 @@ void SeriesTable::render_proto(std::string* out, uint64_t gen) const {
         }
         pb_msg(&metric, 7, sub);
       } else {
-        pb_double(&sub, 1, s.value);
+        pb_double(&sub, 1, hot_[idx].value);
         pb_msg(&metric, fam.def.type == MetricType::kCounter ? 3 : 2, sub);
       }
       pb_msg(&fam_buf, 4, metric);

@@ -78,15 +78,23 @@ class SeriesTable {
   void render_proto(std::string* out, uint64_t gen) const;
 
   size_t live_series(uint64_t gen) const;
+  // Families whose text was re-built by the last render (the rest were copied cached).
+  size_t last_rebuilt_families() const { return last_rebuilt_; }
   size_t live_series_in_family(int fid, uint64_t gen) const;
   double value(SeriesRef r) const;
 
  private:
-  struct Series {
+  // Per-series fields every tick touches, in their own dense array (hot_[idx]): setting
+  // values, the GC/liveness scan and the render-cache check never walk the large Series
+  // records, so a 10 Hz tick that starts with cold caches stays cheap.
+  struct Hot {
     int fid = -1;
     uint32_t ver = 0;
-    uint64_t gen = 0;  // last generation it was set
+    uint64_t gen = 0;       // last generation it was set
     double value = 0;
+    bool in_cache = false;  // included in its family's cached text
+  };
+  struct Series {  // cold: strings and histogram state
     std::vector<std::string> labels;
     std::string prefix;       // `name{a="x",b="y"}` (no trailing space)
     std::string line;         // prefix + ' ' (what render copies before the value)
@@ -109,18 +117,25 @@ class SeriesTable {
     std::string header;              // "# HELP ...\n# TYPE ...\n"
     std::vector<uint32_t> members;   // sorted by label values
     bool dirty_order = false;
+    // Rendered text of the family as of the last render.  Re-built only when a member's
+    // value bits, membership or liveness changed; otherwise render copies it whole.
+    std::string cache;
+    bool dirty = true;
   };
   void free_series(uint32_t idx);
   void sort_members(Family& f);
-  void render_histogram(std::string* out, Series& s) const;
-  static void append_cached_value(std::string* out, Series& s);
+  void render_histogram(std::string* out, uint32_t idx);
+  void append_cached_value(std::string* out, uint32_t idx);
+  void mark_dirty(int fid) { families_[size_t(fid)].dirty = true; }
 
   std::vector<Family> families_;
   std::vector<int> render_order_;  // family ids sorted by name
+  std::vector<Hot> hot_;
   std::vector<Series> series_;
   std::vector<uint32_t> free_;
   std::unordered_map<std::string, uint32_t> index_;
   std::string keybuf_;
+  size_t last_rebuilt_ = 0;
 };
 
 }  // namespace gpuexp
