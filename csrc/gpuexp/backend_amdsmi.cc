@@ -128,6 +128,11 @@ class AmdsmiBackend : public Backend {
   const char* name() const override { return "amdsmi"; }
 
   bool init(std::vector<DeviceInfo>* devices, std::string* err) override {
+    // amdsmi caches gpu_metrics tables for AMDSMI_GPU_METRICS_CACHE_MS: two calls around a
+    // raw read can then return one older table (seen on MI355X: equal system_clock_counter
+    // around a newer raw value).  Its reads here are validation and fallback, both of which
+    // want the current table, so no cache unless the user set one.
+    ::setenv("AMDSMI_GPU_METRICS_CACHE_MS", "0", 0);
     amdsmi_status_t st = amdsmi_init(AMDSMI_INIT_AMD_GPUS);
     if (st != AMDSMI_STATUS_SUCCESS) {
       *err = "amdsmi_init: " + smi_err(st);
@@ -222,7 +227,13 @@ class AmdsmiBackend : public Backend {
           d.gm.set_partition(info.partition_id, int(info.num_xcc));
           d.xcp = info.partition_id;
           d.nxcc = int(info.num_xcc);
-          if (!force_smi_ && d.gm.open(dir + "/gpu_metrics", &e)) d.fast_ok = validate(d);
+          if (!force_smi_ && d.gm.open(dir + "/gpu_metrics", &e)) {
+            // a bracket can still straddle a PMFW refresh oddly: a few attempts, 25 ms apart
+            for (int attempt = 0; attempt < 3 && !d.fast_ok; ++attempt) {
+              if (attempt) ::usleep(25000);
+              d.fast_ok = validate(d);
+            }
+          }
           d.gm.set_coalesce(coalesce_metrics_);
           d.gm.set_min_fresh_interval(metrics_min_ns_);
           if (!d.fast_ok)
