@@ -44,6 +44,16 @@ const std::vector<double>& stage_bounds() {
   return b;
 }
 
+// "0".."63" without a std::to_string per series per tick (label values of links / XCDs)
+const char* idx_str(int i) {
+  static const char* k[64] = {"0",  "1",  "2",  "3",  "4",  "5",  "6",  "7",  "8",  "9",  "10", "11", "12",
+                              "13", "14", "15", "16", "17", "18", "19", "20", "21", "22", "23", "24", "25",
+                              "26", "27", "28", "29", "30", "31", "32", "33", "34", "35", "36", "37", "38",
+                              "39", "40", "41", "42", "43", "44", "45", "46", "47", "48", "49", "50", "51",
+                              "52", "53", "54", "55", "56", "57", "58", "59", "60", "61", "62", "63"};
+  return i >= 0 && i < 64 ? k[i] : "?";
+}
+
 const char* kTempNames[9] = {"hotspot", "mem", "vrsoc", "edge", "vrgfx", "vrmem", "hbm0", "hbm1", "hbm2"};
 const char* kClkNames[3] = {"gfx", "soc", "mem"};
 const char* kThrNames[5] = {"ppt", "socket_thermal", "vr_thermal", "hbm_thermal", "prochot"};
@@ -510,14 +520,14 @@ void Engine::trace_event(const char* name, uint64_t start_ns, uint64_t dur_ns) {
                double(start_ns - trace_t0_) * 1e-3, double(dur_ns) * 1e-3, self_pid_);
 }
 
-void Engine::dput(DevState& st, int dev, SeriesRef& r, int fid, const std::vector<std::string>& extra,
+void Engine::dput(DevState& st, int dev, SeriesRef& r, int fid, std::initializer_list<const char*> extra,
                   double v, uint64_t gen) {
   if (std::isnan(v)) return;
-  if (table_.set(r, v, gen)) return;
+  if (table_.set(r, v, gen)) return;  // the per-tick path: no allocation, no hashing
   const DeviceInfo& d = devices_[size_t(dev)];
   std::vector<std::string> labels = {std::to_string(d.index), d.bdf, st.owner.ns, st.owner.pod,
                                      st.owner.container};
-  labels.insert(labels.end(), extra.begin(), extra.end());
+  for (const char* e : extra) labels.emplace_back(e);
   r = table_.upsert(fid, labels);
   table_.set(r, v, gen);
 }
@@ -596,8 +606,8 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
       if (std::isnan(c.xgmi_link_up[l])) continue;
       links_up += c.xgmi_link_up[l] > 0;
       if (compact) continue;
-      std::string ls = std::to_string(l);
-      const std::string& peer = d.xgmi_peer_bdf[l];
+      const char* ls = idx_str(l);
+      const char* peer = d.xgmi_peer_bdf[l].c_str();
       dput(st, i, st.xrd[l], f_xrd_, {ls, peer}, double(c.xgmi_read_kb[l]) * 1024.0, gen);
       dput(st, i, st.xwr[l], f_xwr_, {ls, peer}, double(c.xgmi_write_kb[l]) * 1024.0, gen);
     }
@@ -646,7 +656,7 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
     dput(st, i, st.xgmi_s, f_xgmi_speed_, {}, c.xgmi_speed, gen);
     for (int x = 0; x < kMaxXcc; ++x)
       if (!std::isnan(c.clk_gfx_xcc[x]))
-        dput(st, i, st.xclk[x], f_xcc_clk_, {std::to_string(x)}, c.clk_gfx_xcc[x] * 1e6, gen);
+        dput(st, i, st.xclk[x], f_xcc_clk_, {idx_str(int(x))}, c.clk_gfx_xcc[x] * 1e6, gen);
   }
 
   uint32_t nx = d.num_xcc ? std::min<uint32_t>(d.num_xcc, kMaxXcc) : kMaxXcc;
@@ -677,7 +687,7 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
   }
   for (int k = 0; k < 5; ++k) dput(st, i, st.thr[k], f_thr_, {kThrNames[k]}, st.thr_last[k], gen);
   if (!compact)
-    for (uint32_t x = 0; x < nx; ++x) dput(st, i, st.xcc[x], f_xcc_, {std::to_string(x)}, st.xcc_last[x], gen);
+    for (uint32_t x = 0; x < nx; ++x) dput(st, i, st.xcc[x], f_xcc_, {idx_str(int(x))}, st.xcc_last[x], gen);
 
   // Optional sources: rocprofiler counters, sentinel (real or mock-simulated).
   CounterReading cr;
@@ -689,7 +699,8 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
     // only while they are known to see every process (scope 1, or the mock); scope 0
     // (VMID-filtered to the exporter) would under-report by orders of magnitude.
     int scope = counters_ ? counters_->scope(i) : 1;
-    table_.put(f_self_ctr_scope_, {std::to_string(d.index)}, scope < 0 ? kNaN : double(scope), gen);
+    cput(st.self_reads[3], f_self_ctr_scope_, scope < 0 ? kNaN : double(scope), gen,
+         [&] { return std::vector<std::string>{std::to_string(d.index)}; });
     dput(st, i, st.ctr[0], f_mfma_, {}, cr.mfma_busy_pct, gen);
     dput(st, i, st.ctr[2], f_gui_, {}, cr.gui_active_pct, gen);
     if (scope != 0) {
@@ -718,9 +729,9 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
       dput(st, i, st.sen_mem, f_sen_mem_, {}, sr.mem_latency_s, gen);
       for (int x = 0; x < kMaxXcc; ++x) {
         if (!std::isnan(sr.xcc_latency_s[x]))
-          dput(st, i, st.sen_xlat[x], f_sen_xlat_, {std::to_string(x)}, sr.xcc_latency_s[x], gen);
+          dput(st, i, st.sen_xlat[x], f_sen_xlat_, {idx_str(int(x))}, sr.xcc_latency_s[x], gen);
         if (!std::isnan(sr.xcc_mem_latency_s[x]))
-          dput(st, i, st.sen_xmem[x], f_sen_xmem_, {std::to_string(x)}, sr.xcc_mem_latency_s[x], gen);
+          dput(st, i, st.sen_xmem[x], f_sen_xmem_, {idx_str(int(x))}, sr.xcc_mem_latency_s[x], gen);
       }
     }
   }
@@ -798,12 +809,25 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
       const ProcAttr& a = attr[p.pid];
       const double share = gfx_share(p);
       if (!legacy_only) {
-        std::vector<std::string> L = {std::to_string(d.index), std::to_string(p.pid), p.name, a.ns, a.pod, a.container};
-        table_.put(f_proc_vram_, L, p.vram_bytes, gen);
-        if (!std::isnan(p.cu_occupancy)) table_.put(f_proc_cu_, L, p.cu_occupancy, gen);
-        if (!std::isnan(p.sdma_us)) table_.put(f_proc_sdma_, L, p.sdma_us * 1e-6, gen);
-        if (!std::isnan(p.evicted_ms)) table_.put(f_proc_evicted_, L, p.evicted_ms * 1e-3, gen);
-        if (!std::isnan(share)) table_.put(f_proc_gfx_, L, share, gen);
+        // handles cached per (GPU, PID) for as long as the label values stay the same
+        ProcRefs& pr = proc_refs_[(uint64_t(uint32_t(di)) << 32) | uint32_t(p.pid)];
+        if (pr.comm != p.name || pr.ns != a.ns || pr.pod != a.pod || pr.container != a.container) {
+          pr = ProcRefs();
+          pr.comm = p.name;
+          pr.ns = a.ns;
+          pr.pod = a.pod;
+          pr.container = a.container;
+        }
+        pr.gen = gen;
+        auto L = [&] {
+          return std::vector<std::string>{std::to_string(d.index), std::to_string(p.pid), p.name, a.ns, a.pod,
+                                          a.container};
+        };
+        cput(pr.vram, f_proc_vram_, p.vram_bytes, gen, L);
+        if (!std::isnan(p.cu_occupancy)) cput(pr.cu, f_proc_cu_, p.cu_occupancy, gen, L);
+        if (!std::isnan(p.sdma_us)) cput(pr.sdma, f_proc_sdma_, p.sdma_us * 1e-6, gen, L);
+        if (!std::isnan(p.evicted_ms)) cput(pr.evicted, f_proc_evicted_, p.evicted_ms * 1e-3, gen, L);
+        if (!std::isnan(share)) cput(pr.gfx, f_proc_gfx_, share, gen, L);
       }
       if (!a.pod.empty()) {
         auto& la = legacy[p.pid];
@@ -845,26 +869,39 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
     // reference overwrote per device, last-device-wins, main.go:147-150).
     for (auto& kv : legacy) {
       const ProcAttr& a = attr[kv.first];
-      std::vector<std::string> L = {std::to_string(kv.first), a.pod};
-      table_.put(f_legacy_mem_, L, kv.second.used, gen);
-      table_.put(f_legacy_perc_, L, kv.second.total > 0 ? kv.second.used / kv.second.total * 100.0 : 0.0, gen);
+      ProcRefs& pr = legacy_refs_[uint64_t(uint32_t(kv.first))];
+      if (pr.pod != a.pod) {
+        pr = ProcRefs();
+        pr.pod = a.pod;
+      }
+      pr.gen = gen;
+      auto L = [&] { return std::vector<std::string>{std::to_string(kv.first), a.pod}; };
+      cput(pr.vram, f_legacy_mem_, kv.second.used, gen, L);
+      cput(pr.gfx, f_legacy_perc_, kv.second.total > 0 ? kv.second.used / kv.second.total * 100.0 : 0.0, gen, L);
     }
   }
+  // forget the handles of processes gone this tick (their series are GC'd by the table)
+  for (auto* m : {&proc_refs_, &legacy_refs_})
+    for (auto it = m->begin(); it != m->end();) it = it->second.gen != gen ? m->erase(it) : std::next(it);
   if (cfg_.series_profile == "legacy") return;
   for (auto& kv : pods) {
-    std::vector<std::string> L = {kv.first.first, kv.first.second};
+    PodRefs& r = pod_refs_[kv.first];
+    r.gen = gen;
+    auto L = [&] { return std::vector<std::string>{kv.first.first, kv.first.second}; };
     const PodAgg& pa = kv.second;
-    table_.put(f_pod_vram_, L, pa.vram, gen);
-    table_.put(f_pod_procs_, L, double(pa.pids.size()), gen);
-    table_.put(f_pod_gpus_, L, double(pa.gpus), gen);
-    if (pa.share_known) table_.put(f_pod_gfx_share_, L, pa.gfx_share, gen);
+    cput(r.ref[0], f_pod_vram_, pa.vram, gen, L);
+    cput(r.ref[1], f_pod_procs_, double(pa.pids.size()), gen, L);
+    cput(r.ref[2], f_pod_gpus_, double(pa.gpus), gen, L);
+    if (pa.share_known) cput(r.ref[3], f_pod_gfx_share_, pa.gfx_share, gen, L);
     if (pa.gpus > 0) {
-      table_.put(f_pod_xrd_, L, pa.xrd, gen);
-      table_.put(f_pod_xwr_, L, pa.xwr, gen);
-      table_.put(f_pod_power_, L, pa.power, gen);
-      if (pa.gfx_n) table_.put(f_pod_gfx_, L, pa.gfx / pa.gfx_n, gen);
+      cput(r.ref[4], f_pod_xrd_, pa.xrd, gen, L);
+      cput(r.ref[5], f_pod_xwr_, pa.xwr, gen, L);
+      cput(r.ref[6], f_pod_power_, pa.power, gen, L);
+      if (pa.gfx_n) cput(r.ref[7], f_pod_gfx_, pa.gfx / pa.gfx_n, gen, L);
     }
   }
+  for (auto it = pod_refs_.begin(); it != pod_refs_.end();)
+    it = it->second.gen != gen ? pod_refs_.erase(it) : std::next(it);
   if (rccl_) {
     std::vector<RcclTotals> tot;
     rccl_->poll(&tot);
@@ -895,23 +932,24 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
 }
 
 void Engine::emit_self(uint64_t gen) {
-  table_.put(f_self_build_, {cfg_.version, backend_->name()}, 1, gen);
+  auto none = [] { return std::vector<std::string>{}; };
+  cput(self_refs_[0], f_self_build_, 1, gen, [&] { return std::vector<std::string>{cfg_.version, backend_->name()}; });
   EngineStats s;
   {
     std::lock_guard<std::mutex> lk(stats_mu_);
     s = stats_;
   }
-  table_.put(f_self_ticks_, {}, double(s.ticks), gen);
+  cput(self_refs_[1], f_self_ticks_, double(s.ticks), gen, none);
   {
     timespec rt;
     clock_gettime(CLOCK_REALTIME, &rt);
-    table_.put(f_self_last_, {}, double(rt.tv_sec) + double(rt.tv_nsec) * 1e-9, gen);
+    cput(self_refs_[2], f_self_last_, double(rt.tv_sec) + double(rt.tv_nsec) * 1e-9, gen, none);
   }
-  table_.put(f_self_overruns_, {}, double(s.overruns), gen);
-  table_.put(f_self_unresolved_, {}, double(unresolved_.size()), gen);
-  table_.put(f_self_render_bytes_, {}, double(s.render_bytes), gen);
-  table_.put(f_self_series_, {}, double(s.series), gen);
-  table_.put(f_self_cpu_, {}, double(s.sampler_cpu_ns) * 1e-9, gen);
+  cput(self_refs_[3], f_self_overruns_, double(s.overruns), gen, none);
+  cput(self_refs_[4], f_self_unresolved_, double(unresolved_.size()), gen, none);
+  cput(self_refs_[5], f_self_render_bytes_, double(s.render_bytes), gen, none);
+  cput(self_refs_[6], f_self_series_, double(s.series), gen, none);
+  cput(self_refs_[7], f_self_cpu_, double(s.sampler_cpu_ns) * 1e-9, gen, none);
   for (int k = 0; k < kStages; ++k) {
     if (!self_stage_refs_[k].valid()) self_stage_refs_[k] = table_.upsert(f_self_stage_, {stage_name(k)});
     if (s.ticks) table_.observe(self_stage_refs_[k], double(last_stage_ns_[k]) * 1e-9, gen, stage_bounds());
@@ -923,23 +961,34 @@ void Engine::emit_self(uint64_t gen) {
     for (int b = 0; b <= HttpStats::kBuckets; ++b) counts[size_t(b)] = hs.lat_buckets[b].load(std::memory_order_relaxed);
     uint64_t cnt = hs.lat_count.load(std::memory_order_relaxed);
     double sum = double(hs.lat_sum_ns.load(std::memory_order_relaxed)) * 1e-9;
-    table_.set_histogram(table_.upsert(f_self_scrape_, {}), scrape_latency_bounds(), counts, sum, cnt, gen);
-    table_.put(f_self_scrapes_, {}, double(hs.metrics_requests.load(std::memory_order_relaxed)), gen);
-    table_.put(f_self_http_bytes_, {}, double(hs.bytes_sent.load(std::memory_order_relaxed)), gen);
+    if (!table_.set_histogram(self_refs_[8], scrape_latency_bounds(), counts, sum, cnt, gen)) {
+      self_refs_[8] = table_.upsert(f_self_scrape_, {});
+      table_.set_histogram(self_refs_[8], scrape_latency_bounds(), counts, sum, cnt, gen);
+    }
+    cput(self_refs_[9], f_self_scrapes_, double(hs.metrics_requests.load(std::memory_order_relaxed)), gen, none);
+    cput(self_refs_[10], f_self_http_bytes_, double(hs.bytes_sent.load(std::memory_order_relaxed)), gen, none);
     if (cfg_.http.prewake)
-      table_.put(f_self_prewake_, {}, double(hs.prewake_timer_wakeups.load(std::memory_order_relaxed)), gen);
+      cput(self_refs_[11], f_self_prewake_, double(hs.prewake_timer_wakeups.load(std::memory_order_relaxed)), gen,
+           none);
   }
   if (!mock_)
     for (size_t i = 0; i < devices_.size(); ++i) {
+      DevState& st = dstate_[i];
       const std::string g = std::to_string(devices_[i].index);
-      table_.put(f_self_metrics_reads_, {g, "fresh"}, double(metrics_fresh_[i]), gen);
-      table_.put(f_self_metrics_reads_, {g, "coalesced"}, double(metrics_coalesced_[i]), gen);
-      table_.put(f_self_metrics_period_, {g}, backend_->metrics_period_s(devices_[i]), gen);
+      cput(st.self_reads[0], f_self_metrics_reads_, double(metrics_fresh_[i]), gen,
+           [&] { return std::vector<std::string>{g, "fresh"}; });
+      cput(st.self_reads[1], f_self_metrics_reads_, double(metrics_coalesced_[i]), gen,
+           [&] { return std::vector<std::string>{g, "coalesced"}; });
+      cput(st.self_reads[2], f_self_metrics_period_, backend_->metrics_period_s(devices_[i]), gen,
+           [&] { return std::vector<std::string>{g}; });
     }
-  table_.put(f_self_source_up_, {"backend:" + std::string(backend_->name())}, 1, gen);
-  table_.put(f_self_source_up_, {"sentinel"}, (sentinel_ || (cfg_.enable_sentinel && mock_)) ? 1 : 0, gen);
-  table_.put(f_self_source_up_, {"counters"}, (counters_ || (cfg_.enable_counters && mock_)) ? 1 : 0, gen);
-  table_.put(f_self_source_up_, {"rccl"}, rccl_ ? 1 : 0, gen);
+  cput(self_refs_[12], f_self_source_up_, 1, gen,
+       [&] { return std::vector<std::string>{"backend:" + std::string(backend_->name())}; });
+  cput(self_refs_[13], f_self_source_up_, (sentinel_ || (cfg_.enable_sentinel && mock_)) ? 1 : 0, gen,
+       [] { return std::vector<std::string>{"sentinel"}; });
+  cput(self_refs_[14], f_self_source_up_, (counters_ || (cfg_.enable_counters && mock_)) ? 1 : 0, gen,
+       [] { return std::vector<std::string>{"counters"}; });
+  cput(self_refs_[15], f_self_source_up_, rccl_ ? 1 : 0, gen, [] { return std::vector<std::string>{"rccl"}; });
   if (rccl_) {
     int a = 0, u = 0, x = 0;
     rccl_->file_states(&a, &u, &x);

@@ -11,6 +11,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <functional>
+#include <initializer_list>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -174,6 +175,18 @@ class Engine {
         sen[4], ecc[3], aer[3], nak[2], recov, xgmi_w, xgmi_s, xclk[kMaxXcc], sen_xlat[kMaxXcc], sen_mem, sen_xmem[kMaxXcc];
     uint64_t errors = 0;
     SeriesRef err_ref;
+    SeriesRef self_reads[4];  // gpu_metrics reads fresh / coalesced, refresh period, counter scope
+  };
+  // Cached series handles of a (GPU, PID) or a pod, valid while their label values are the
+  // ones recorded here: the per-tick path then sets values without building label vectors.
+  struct ProcRefs {
+    std::string comm, ns, pod, container;
+    SeriesRef vram, cu, sdma, evicted, gfx;
+    uint64_t gen = 0;
+  };
+  struct PodRefs {
+    SeriesRef ref[8];
+    uint64_t gen = 0;
   };
   struct ProcAttr {
     std::string ns, pod, container, uid;
@@ -186,8 +199,16 @@ class Engine {
   void emit_processes(uint64_t gen, const std::vector<std::vector<ProcSample>>& per_dev);
   void emit_self(uint64_t gen);
   void trace_event(const char* name, uint64_t start_ns, uint64_t dur_ns);
-  void dput(DevState& st, int dev, SeriesRef& r, int fid, const std::vector<std::string>& extra,
+  void dput(DevState& st, int dev, SeriesRef& r, int fid, std::initializer_list<const char*> extra,
             double v, uint64_t gen);
+  // Sets `v` through the cached handle `r`; builds the label values (labels()) and
+  // re-interns only when the handle is stale.
+  template <class F>
+  void cput(SeriesRef& r, int fid, double v, uint64_t gen, F&& labels) {
+    if (table_.set(r, v, gen)) return;
+    r = table_.upsert(fid, labels());
+    table_.set(r, v, gen);
+  }
 
   EngineConfig cfg_;
   std::unique_ptr<Backend> backend_;
@@ -233,6 +254,10 @@ class Engine {
   std::unordered_map<std::string, std::string> container_names_;  // cid -> name
   std::unordered_map<std::string, DeviceOwner> owners_;           // lower(device id) -> owner
   std::set<std::string> unresolved_;                               // pod UIDs without metadata (last tick)
+  std::unordered_map<uint64_t, ProcRefs> proc_refs_;               // (device << 32 | pid) -> handles
+  std::unordered_map<uint64_t, ProcRefs> legacy_refs_;             // pid -> legacy handles (pod, vram, gfx=perc)
+  std::map<std::pair<std::string, std::string>, PodRefs> pod_refs_;  // (ns, pod) -> handles
+  SeriesRef self_refs_[16];
 
   // stats (guarded by stats_mu_)
   std::mutex stats_mu_;

@@ -72,8 +72,12 @@ class SnapshotStore {
 
   // Writer side: single thread.  Returns a free slot (not current, not pinned) or -1
   // if every other slot is pinned by slow readers (the tick is then not published).
+  // Prefers the slot published before the current one: slots ping-pong while scrapes are
+  // quick, so the render writes into buffers touched one tick ago (still in cache) rather
+  // than cycling through all kSlots cold ones.
   int begin_write() {
     int c = current_.load(std::memory_order_seq_cst);
+    if (prev_ >= 0 && prev_ != c && slots_[prev_].refs.load(std::memory_order_seq_cst) == 0) return prev_;
     for (int k = 1; k <= kSlots; ++k) {
       int i = (c + k + kSlots) % kSlots;
       if (i == c) continue;
@@ -82,7 +86,10 @@ class SnapshotStore {
     return -1;
   }
   Snapshot* slot(int i) { return &slots_[i].snap; }
-  void publish(int i) { current_.store(i, std::memory_order_seq_cst); }
+  void publish(int i) {
+    prev_ = current_.load(std::memory_order_seq_cst);
+    current_.store(i, std::memory_order_seq_cst);
+  }
   bool ready() const { return current_.load(std::memory_order_acquire) >= 0; }
 
  private:
@@ -92,6 +99,7 @@ class SnapshotStore {
   };
   Slot slots_[kSlots];
   std::atomic<int> current_{-1};
+  int prev_ = -1;  // writer thread only
 };
 
 // gzip (RFC 1952) of `in` at compression `level` into `out`.  Returns false on error.
