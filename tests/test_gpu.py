@@ -377,7 +377,9 @@ def test_rccl_tracer_counts_collectives():
     assert ops["reducescatter"]["calls"] >= 5 and ops["alltoall"]["calls"] >= 5, ops
     # every strategy's traced calls and bytes == the generator's ground truth, byte for byte
     par = res["parity"]
-    assert set(par) == {"dp", "tp", "sp", "ep", "ulysses", "bcast"}, par
+    assert set(par) == {"dp", "tp", "sp", "ep", "ulysses", "bcast", "p2p"}, par
+    # PP/CP point-to-point (grouped send+recv to self) and gather/scatter via RCCL's C API
+    assert par["p2p"]["data_ok"] is True, par["p2p"]
     for strategy, p in par.items():
         assert p["traced"] == p["expected"], (strategy, p)
 
