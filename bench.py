@@ -202,6 +202,9 @@ def main() -> int:
                          "collective calls/bytes")
     ap.add_argument("--exporter", choices=("native", "both"), default="native",
                     help="'both' also measures a Python prometheus_client stand-in exporter (utils/refstyle.py)")
+    ap.add_argument("--xgmi-patterns", type=int, default=1,
+                    help="N > 1: after the timed phases (untimed), drive a ring (CP) and an all-to-all (EP) "
+                         "pattern and report each rank's xGMI bytes per peer from the exporter's link counters")
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="self-launch (--gpus N > 1 without torchrun): stop the ranks after this many seconds")
     argv = sys.argv[1:]
@@ -340,14 +343,21 @@ def main() -> int:
         # a VRAM fingerprint so the exporter can attribute this rank to its fake pod.
         from kubernetes_gpu_exporter_amd.utils.kfdself import find_own_kfd_pid
         pid = find_own_kfd_pid(local_rank, salt=rank) or pid
+    my_bdf = ""
+    if use_gpu:
+        from kubernetes_gpu_exporter_amd.utils.kfdself import hip_order_bdfs
+        order = hip_order_bdfs()
+        my_bdf = order[local_rank].lower() if local_rank < len(order) else ""
+    elif backend == "mock":
+        my_bdf = f"0000:{0x10 + 0x10 * rank:02x}:00.0"  # mock GPU `rank` (backend_mock.cc)
     if dist is not None:
         pids = [None] * world
-        dist.all_gather_object(pids, (pid, own_pid))
+        dist.all_gather_object(pids, (pid, own_pid, my_bdf))
     else:
-        pids = [(pid, own_pid)]
+        pids = [(pid, own_pid, my_bdf)]
     if rank == 0:
         pods, cgroups = [], {}
-        for r, (p, op) in enumerate(pids):
+        for r, (p, op, _) in enumerate(pids):
             uid = f"00000000-0000-4000-8000-{r:012d}"
             cid = f"{r:064x}"
             pods.append({"uid": uid, "namespace": "bench", "name": f"gemm-pod-{r}", "containers": {cid: "worker"}})
@@ -403,19 +413,90 @@ def main() -> int:
         if rest > 0:
             time.sleep(rest)
 
-    def xgmi_totals(cl) -> tuple[float, dict]:
-        """(time, {gpu: [read_bytes, write_bytes]}) summed over links, from the exporter's
-        hardware-accumulator counters in the body of the scrape `cl` just did."""
+    def last_fams(cl):
         body = cl.last_body()
         if args.gzip:
             body = __import__("gzip").decompress(body)
-        fams = promtext.parse(body.decode()) if body[:1] == b"#" else \
+        return promtext.parse(body.decode()) if body[:1] == b"#" else \
             promproto.to_promtext(promproto.parse_delimited(body))
+
+    def xgmi_totals(cl) -> tuple[float, dict]:
+        """(time, {gpu: [read_bytes, write_bytes]}) summed over links, from the exporter's
+        hardware-accumulator counters in the body of the scrape `cl` just did."""
+        fams = last_fams(cl)
         tot: dict = {}
         for k, fam_name in enumerate(("amd_gpu_xgmi_read_bytes_total", "amd_gpu_xgmi_write_bytes_total")):
             for _, lab, v in promtext.samples(fams, fam_name):
                 tot.setdefault(lab.get("gpu"), [0.0, 0.0])[k] += v
         return time.perf_counter(), tot
+
+    def xgmi_links(cl) -> dict:
+        """{(bdf, peer_bdf): [read_bytes, write_bytes]} per xGMI link, from a fresh scrape."""
+        cl.scrape()
+        out: dict = {}
+        for k, fam_name in enumerate(("amd_gpu_xgmi_read_bytes_total", "amd_gpu_xgmi_write_bytes_total")):
+            for _, lab, v in promtext.samples(last_fams(cl), fam_name):
+                key = (lab.get("bdf", "").lower(), lab.get("peer_bdf", "").lower())
+                out.setdefault(key, [0.0, 0.0])[k] += v
+        return out
+
+    def xgmi_patterns(cl, bdfs: list) -> dict:
+        """Untimed, after the measured phases (N > 1 only): drives two traffic patterns with
+        known peers and reports, per rank, where its xGMI bytes went according to the
+        exporter's per-link accumulators (peer_bdf labels):
+          cp  ring (context parallel): rank r sends to r+1 and receives from r-1, so its
+              link bytes should sit on the links to its two ring neighbours;
+          ep  all-to-all (expert parallel): every peer gets an equal share.
+        `bdfs[r]` is rank r's GPU.  Returns {pattern: {...}}; the share values are what the
+        per-peer attribution must get right."""
+        from kubernetes_gpu_exporter_amd.parallel.collectives import run as run_pattern
+        out: dict = {}
+        nb, target_s = (256 << 20, 1.0) if use_gpu else (4 << 20, 0.2)  # mock: gloo on the CPU
+        for pattern in ("cp", "ep"):
+            run_pattern(pattern, steps=1, nbytes=nb, device=dev, check=True)  # warm the transport
+            sync()
+            t = time.perf_counter()
+            run_pattern(pattern, steps=1, nbytes=nb, device=dev, check=False)
+            sync()
+            steps = torch.tensor([max(1, int(target_s / max(1e-4, time.perf_counter() - t)))], device=dev)
+            dist.all_reduce(steps, op=dist.ReduceOp.MAX)  # every rank runs the same step count
+            dist.barrier()
+            before = None
+            if rank == 0:
+                time.sleep(0.3)  # idle: the accumulators of the last tick are final
+                before = xgmi_links(cl)
+            dist.barrier()
+            t0 = time.perf_counter()
+            st = run_pattern(pattern, steps=int(steps.item()), nbytes=nb, device=dev, check=True)
+            sync()
+            dist.barrier()
+            if rank != 0:
+                continue
+            secs = time.perf_counter() - t0
+            time.sleep(0.3)  # two sample ticks: the window's last bytes are in the accumulators
+            after = xgmi_links(cl)
+            per_rank = {}
+            for r, b in enumerate(bdfs):
+                peers, rw = {}, [0.0, 0.0]
+                for (src, peer), v in after.items():
+                    if src != b:
+                        continue
+                    v0 = before.get((src, peer), [0.0, 0.0])
+                    d = [v[0] - v0[0], v[1] - v0[1]]
+                    rw = [rw[0] + d[0], rw[1] + d[1]]
+                    pr = str(bdfs.index(peer)) if peer in bdfs else (peer or "?")
+                    peers[pr] = peers.get(pr, 0.0) + d[0] + d[1]
+                total = sum(peers.values())
+                entry = {"read_bytes": round(rw[0]), "write_bytes": round(rw[1]),
+                         "per_peer_share": {k: round(v / total, 3) for k, v in sorted(peers.items()) if total}}
+                if pattern == "cp" and total:
+                    nbr = {str((r + 1) % world), str((r - 1) % world)}
+                    entry["ring_neighbour_share"] = round(sum(v for k, v in peers.items() if k in nbr) / total, 3)
+                per_rank[str(r)] = entry
+            sent = sum(st.bytes.values()) / 2 if pattern == "cp" else st.bytes.get("alltoall", 0) * (world - 1) / world
+            out[pattern] = {"steps": int(steps.item()), "seconds": round(secs, 3),
+                            "expected_bytes_out_per_rank": round(sent), "per_rank": per_rank}
+        return out
 
     xgmi_window: dict = {}
     exporter_rss_kb = [0]
@@ -636,7 +717,13 @@ def main() -> int:
             "optional_sources": {"counters": bool(args.counters), "sentinel": bool(args.sentinel),
                                  "rccl_trace": bool(rccl_dir),
                                  "degraded_reason": degraded},
+            "xgmi_patterns": None,
         }
+    if args.xgmi_patterns and dist is not None:
+        patterns = xgmi_patterns(client, [b for _, _, b in pids])
+        if rank == 0:
+            result["xgmi_patterns"] = patterns
+    if rank == 0:
         stop_proc(exporter)
 
     if args.exporter == "both":

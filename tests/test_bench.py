@@ -66,6 +66,15 @@ def test_bench_self_launches_one_rank_per_gpu():
     assert d["server_scrapes"] >= 3 and d["server_scrape_p99_le_us"] > 0
     assert d["sampler_cpu_us_per_tick_per_gpu"] > 0 and d["exporter_rss_mb"] > 0
     assert "measured_over_expected_write" in d["xgmi_timed_window"]
+    # untimed pattern phase: ring + all-to-all ran on all ranks; per-rank link bytes are
+    # joined to peer ranks through the peer_bdf labels (mock links: synthetic bytes)
+    pat = d["xgmi_patterns"]
+    assert set(pat) == {"cp", "ep"}, pat
+    for p in pat.values():
+        assert p["steps"] >= 1 and sorted(p["per_rank"]) == ["0", "1", "2", "3"]
+        assert p["expected_bytes_out_per_rank"] > 0
+        peers = set(p["per_rank"]["0"]["per_peer_share"])
+        assert {"1", "2", "3"} <= peers, peers  # mock GPU 0's links to mock GPUs 1..3 resolve to ranks
 
 
 def test_bench_world_must_match_gpus():
