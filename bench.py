@@ -719,7 +719,7 @@ def main() -> int:
                                  "degraded_reason": degraded},
             "xgmi_patterns": None,
         }
-    if args.xgmi_patterns and dist is not None:
+    if args.xgmi_patterns and world > 1:
         patterns = xgmi_patterns(client, [b for _, _, b in pids])
         if rank == 0:
             result["xgmi_patterns"] = patterns
