@@ -832,8 +832,7 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_calibrate(int de
     return fail("allocation failed");
   }
   if (kind == 0) {
-    gpuexp::CalibCopyArgs args{buf, static_cast<char*>(buf) + kCopyBytes, kCopyBytes / 16,
-                               uint64_t(kBlocks) * gpuexp::kProbeBlock};
+    gpuexp::CalibCopyArgs args{buf, static_cast<char*>(buf) + kCopyBytes, kCopyBytes / 16, uint64_t(kBlocks)};
     std::memcpy(ka, &args, sizeof(args));
   } else {
     gpuexp::CalibLdsArgs args{static_cast<float*>(buf), 8192, kind == 2 ? 32 : 1};

@@ -7,7 +7,7 @@
 
 extern "C" __global__ void __launch_bounds__(gpuexp::kProbeBlock) gpuexp_calib_copy(gpuexp::CalibCopyArgs a) {
   gpuexp::stream_copy_body(static_cast<const gpuexp::u32x4*>(a.src), static_cast<gpuexp::u32x4*>(a.dst), a.n,
-                           a.stride);
+                           a.blocks);
 }
 
 extern "C" __global__ void __launch_bounds__(gpuexp::kProbeBlock) gpuexp_calib_lds(gpuexp::CalibLdsArgs a) {

@@ -14,7 +14,7 @@ struct CalibCopyArgs {
   const void* src;  // 16-byte vectors
   void* dst;
   uint64_t n;       // 16-byte vectors to copy
-  uint64_t stride;  // threads in the grid
+  uint64_t blocks;  // workgroups in the grid (each copies one contiguous chunk)
 };
 
 struct CalibLdsArgs {

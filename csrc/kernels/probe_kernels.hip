@@ -10,7 +10,7 @@ namespace gpuexp {
 namespace {
 
 __global__ __launch_bounds__(kProbeBlock) void stream_copy_kernel(CalibCopyArgs a) {
-  stream_copy_body(static_cast<const u32x4*>(a.src), static_cast<u32x4*>(a.dst), a.n, a.stride);
+  stream_copy_body(static_cast<const u32x4*>(a.src), static_cast<u32x4*>(a.dst), a.n, a.blocks);
 }
 
 __global__ __launch_bounds__(kProbeBlock) void lds_probe_kernel(CalibLdsArgs a) {
@@ -21,8 +21,7 @@ __global__ __launch_bounds__(kProbeBlock) void lds_probe_kernel(CalibLdsArgs a) 
 
 hipError_t launch_stream_copy(const void* src, void* dst, size_t bytes, int blocks, hipStream_t stream) {
   if (bytes % 16) return hipErrorInvalidValue;
-  CalibCopyArgs a{src, dst, bytes / 16,
-                  uint64_t(blocks) * kProbeBlock};
+  CalibCopyArgs a{src, dst, bytes / 16, uint64_t(blocks)};
   hipLaunchKernelGGL(stream_copy_kernel, dim3(blocks), dim3(kProbeBlock), 0, stream, a);
   return hipGetLastError();
 }

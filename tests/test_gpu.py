@@ -301,6 +301,37 @@ def test_gemm_burn_throughput(native):
     assert r2["tflops"] > r1["tflops"]  # the default (256x256) kernel is the faster one
 
 
+@pytest.mark.parametrize("nbytes,blocks", [(64 << 20, 4096), ((1 << 20) + 48, 7), (4096 * 16 * 256 + 16, 4096),
+                                           (16, 1)])
+def test_stream_copy_numerics(native, nbytes, blocks):
+    """The calibration copy (probe_device.h, HIP launch) is an exact byte copy for chunk
+    tails, uneven chunks and grids with more workgroups than vectors; the bytes outside
+    the destination range stay untouched."""
+    import torch
+    from kubernetes_gpu_exporter_amd.ops.gemm import stream_copy
+    g = torch.Generator(device="cuda").manual_seed(nbytes)
+    src = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda", generator=g)
+    guard = torch.full((nbytes + 4096,), 0xA5, dtype=torch.uint8, device="cuda")
+    stream_copy(src, guard[:nbytes], blocks=blocks)
+    torch.cuda.synchronize()
+    assert torch.equal(guard[:nbytes], src)
+    assert bool((guard[nbytes:] == 0xA5).all())
+
+
+@pytest.mark.parametrize("conflicts", [False, True])
+def test_lds_probe_numerics(native, conflicts):
+    """lds_probe: lane 0 of each workgroup sums table[i mod 4096] = (i mod 4096) & 7 over
+    `iters` reads (stride only moves the other lanes) — compared with the fp32 reference."""
+    import torch
+    from kubernetes_gpu_exporter_amd.ops.gemm import lds_probe
+    blocks, iters = 300, 5000
+    out = torch.zeros(blocks, dtype=torch.float32, device="cuda")
+    lds_probe(out, blocks, iters, conflicts)
+    torch.cuda.synchronize()
+    ref = float(((torch.arange(iters) % 4096) & 7).to(torch.float32).sum())
+    assert torch.equal(out.cpu(), torch.full((blocks,), ref))
+
+
 def _feature_check(*args, timeout=300):
     import json
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gpu_features_check.py"), *args],
