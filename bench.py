@@ -643,6 +643,7 @@ def main() -> int:
         sampler_cpu = [v for _, _, v in promtext.samples(fams, "gpuexp_sampler_cpu_seconds_total")]
         prewake = [v for _, _, v in promtext.samples(fams, "gpuexp_http_prewake_wakeups_total")]
         scrapes_total = [v for _, _, v in promtext.samples(fams, "gpuexp_scrapes_total")]
+        gz_where = {lab.get("where"): int(v) for _, lab, v in promtext.samples(fams, "gpuexp_gzip_compressions_total")}
         rccl = {}
         for sname, lab, v in promtext.samples(fams, "amd_rccl_collective_bytes_total"):
             rccl.setdefault(lab.get("pod") or lab.get("pid"), {}).setdefault(lab["op"], {})["bytes"] = v
@@ -721,6 +722,9 @@ def main() -> int:
             "sampler_cpu_us_per_tick_per_gpu": round(sampler_cpu[0] / ticks[0] * 1e6 / n_gpus, 1)
             if sampler_cpu and ticks and ticks[0] else None,
             "ranks": world,
+            # gzip copies made by the sampler (scrape expected before the next tick) and by the
+            # HTTP worker for off-schedule requests (each adds one compression to that scrape)
+            "gzip_compressions": gz_where or None,
             "http_prewake_wakeups_per_scrape": round(prewake[0] / scrapes_total[0], 2)
             if prewake and scrapes_total and scrapes_total[0] else None,
             "optional_sources": {"counters": bool(args.counters), "sentinel": bool(args.sentinel),

@@ -389,6 +389,7 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("max_conns", &HttpConfig::max_conns)
       .def_readwrite("idle_timeout_ms", &HttpConfig::idle_timeout_ms)
       .def_readwrite("enable_gzip", &HttpConfig::enable_gzip)
+      .def_readwrite("gzip_unsteady_hold_ns", &HttpConfig::gzip_unsteady_hold_ns)
       .def_readwrite("socket_sndbuf", &HttpConfig::socket_sndbuf)
       .def_readwrite("stale_after_ns", &HttpConfig::stale_after_ns)
       .def_readwrite("prewake", &HttpConfig::prewake)
@@ -484,6 +485,7 @@ PYBIND11_MODULE(_gpuexp, m) {
         d["series"] = s.series;
         d["device_errors"] = s.device_errors;
         d["sampler_cpu_ns"] = s.sampler_cpu_ns;
+        d["gzip_eager"] = s.gzip_eager;
         py::dict st;
         for (int k = 0; k < Engine::kStages; ++k) st[Engine::stage_name(k)] = s.stage_ns[k];
         d["stage_ns"] = st;
@@ -491,6 +493,7 @@ PYBIND11_MODULE(_gpuexp, m) {
           d["http_requests"] = hs->requests.load();
           d["http_metrics_requests"] = hs->metrics_requests.load();
           d["http_gzip_responses"] = hs->gzip_responses.load();
+          d["http_gzip_on_demand"] = hs->gzip_on_demand.load();
           d["http_bytes"] = hs->bytes_sent.load();
           d["http_errors"] = hs->errors.load();
           d["http_open_conns"] = hs->open_conns.load();

@@ -255,6 +255,10 @@ void Engine::define_families() {
   f_self_http_bytes_ = add("gpuexp_http_response_bytes_total", "HTTP response bytes written", C, {});
   f_self_prewake_ = add("gpuexp_http_prewake_wakeups_total",
                         "Timer wake-ups of the HTTP worker ahead of expected scrapes (scrape-phase pre-wake)", C, {});
+  f_self_gzip_ = add("gpuexp_gzip_compressions_total",
+                     "gzip compressions of the exposition: by the sampler (a gzip scrape was expected before "
+                     "the next tick) or per request (off schedule)",
+                     C, {"where"});
   f_self_render_bytes_ = add("gpuexp_render_bytes", "Size of the last rendered exposition", G, {});
   f_self_series_ = add("gpuexp_series", "Series in the last rendered exposition", G, {});
   f_self_dev_errors_ = add("gpuexp_device_errors_total", "Failed telemetry reads per GPU", C, {"gpu"});
@@ -288,7 +292,9 @@ bool Engine::start(std::string* err) {
   // Listen first: a port conflict fails before any GPU-side source (amdsmi, HSA queues,
   // sentinel runs) exists.  Every later failure tears down what was already started.
   if (cfg_.serve_http) {
-    http_ = std::make_unique<HttpServer>(&store_, cfg_.http);
+    HttpConfig hc = cfg_.http;
+    hc.gzip_level = cfg_.gzip_level;
+    http_ = std::make_unique<HttpServer>(&store_, hc);
     if (!http_->start(err)) {
       http_.reset();
       return false;
@@ -971,6 +977,12 @@ void Engine::emit_self(uint64_t gen) {
     if (cfg_.http.prewake)
       cput(self_refs_[11], f_self_prewake_, double(hs.prewake_timer_wakeups.load(std::memory_order_relaxed)), gen,
            none);
+    if (cfg_.http.enable_gzip) {
+      cput(self_refs_[16], f_self_gzip_, double(gzip_eager_), gen,
+           [] { return std::vector<std::string>{"sampler"}; });
+      cput(self_refs_[17], f_self_gzip_, double(hs.gzip_on_demand.load(std::memory_order_relaxed)), gen,
+           [] { return std::vector<std::string>{"request"}; });
+    }
   }
   if (!mock_)
     for (size_t i = 0; i < devices_.size(); ++i) {
@@ -1158,7 +1170,11 @@ void Engine::tick_locked(uint64_t now) {
     snap->pb.clear();
     snap->pb_gz.clear();
     const uint64_t tnow = mono_ns();
-    const bool want_gz = http_ && http_->gzip_wanted_ns() && tnow - http_->gzip_wanted_ns() < 60000000000ull;
+    // gzip copy only when a gzip scrape is expected before the tick after next (or its
+    // schedule is unknown): a 15 s Prometheus scrape costs one compression, not 150
+    const uint64_t period_ns = cfg_.interval_s > 0 ? uint64_t(cfg_.interval_s * 1e9) : 1000000000ull;
+    const bool want_gz = http_ && http_->gzip_due(tnow, 2 * period_ns + 5000000ull);
+    if (want_gz) ++gzip_eager_;
     if (want_gz) gzip_compress(snap->body, &snap->gz, cfg_.gzip_level);
     if (http_ && http_->proto_wanted_ns() && tnow - http_->proto_wanted_ns() < 60000000000ull) {
       table_.render_proto(&snap->pb, gen);
@@ -1191,6 +1207,7 @@ void Engine::tick_locked(uint64_t now) {
     stats_.device_errors += errs;
     for (int k = 0; k < kStages; ++k) stats_.stage_ns[k] = double(stage_dur[k]);
     stats_.sampler_cpu_ns += thread_cpu_ns() - cpu0;
+    stats_.gzip_eager = gzip_eager_;
   }
 }
 

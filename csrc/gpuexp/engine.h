@@ -122,6 +122,7 @@ struct EngineStats {
   uint64_t device_errors = 0;
   double stage_ns[8] = {};
   uint64_t sampler_cpu_ns = 0;
+  uint64_t gzip_eager = 0;  // snapshots published with a gzip copy
 };
 
 class Engine {
@@ -227,6 +228,7 @@ class Engine {
   std::vector<RasTotals> ras_cache_;
   std::vector<uint64_t> ras_next_ns_;
   std::vector<uint64_t> metrics_fresh_, metrics_coalesced_;  // per device
+  uint64_t gzip_eager_ = 0;  // sampler thread only; copied into stats_ per tick
   std::string sentinel_status_ = "disabled", counters_status_ = "disabled";
 
   SeriesTable table_;
@@ -257,7 +259,7 @@ class Engine {
   std::unordered_map<uint64_t, ProcRefs> proc_refs_;               // (device << 32 | pid) -> handles
   std::unordered_map<uint64_t, ProcRefs> legacy_refs_;             // pid -> legacy handles (pod, vram, gfx=perc)
   std::map<std::pair<std::string, std::string>, PodRefs> pod_refs_;  // (ns, pod) -> handles
-  SeriesRef self_refs_[16];
+  SeriesRef self_refs_[18];
 
   // stats (guarded by stats_mu_)
   std::mutex stats_mu_;
@@ -280,7 +282,7 @@ class Engine {
   int f_rccl_calls_, f_rccl_bytes_, f_rccl_comm_;
   int f_self_build_, f_self_ticks_, f_self_last_, f_self_stage_, f_self_scrape_, f_self_scrapes_,
       f_self_http_bytes_, f_self_render_bytes_, f_self_series_, f_self_dev_errors_,
-      f_self_overruns_, f_self_cpu_, f_self_source_up_, f_self_ctr_scope_, f_self_metrics_reads_, f_self_metrics_period_, f_self_prewake_,
+      f_self_overruns_, f_self_cpu_, f_self_source_up_, f_self_ctr_scope_, f_self_metrics_reads_, f_self_metrics_period_, f_self_prewake_, f_self_gzip_,
       f_self_rccl_files_, f_self_unresolved_;
   SeriesRef self_stage_refs_[kStages];
   uint64_t last_stage_ns_[kStages] = {};

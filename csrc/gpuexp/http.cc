@@ -53,6 +53,7 @@ struct Conn {
   bool pending = false;
   bool close_after = false;
   bool is_metrics = false;
+  bool gzip_client = false;  // its last /metrics request accepted gzip
   uint64_t last_active_ns = 0;
   uint64_t req_start_ns = 0;
   // arrival times of this connection's /metrics requests: the scrape period, learnt
@@ -124,6 +125,7 @@ bool prefers_protobuf(const char* s, size_t n) {
 }  // namespace
 
 struct HttpServer::Worker {
+  int index = 0;
   int listen_fd = -1;
   int epfd = -1;
   int stopfd = -1;
@@ -193,10 +195,11 @@ static int make_listener(const std::string& host, int port, bool reuseport, std:
 
 bool HttpServer::start(std::string* err) {
   if (running_.load()) return true;
-  int nthreads = std::max(1, cfg_.threads);
+  int nthreads = std::min(kMaxWorkers, std::max(1, cfg_.threads));
   int port = cfg_.port;
   for (int t = 0; t < nthreads; ++t) {
     auto w = std::make_unique<Worker>();
+    w->index = t;
     w->listen_fd = make_listener(cfg_.host, port, nthreads > 1, err);
     if (w->listen_fd < 0) {
       stop();
@@ -254,6 +257,16 @@ void HttpServer::stop() {
   }
   workers_.clear();
   running_.store(false);
+}
+
+bool HttpServer::gzip_due(uint64_t now_ns, uint64_t horizon_ns) const {
+  const uint64_t u = gzip_unsteady_ns_.load(std::memory_order_relaxed);
+  if (u && now_ns < u + cfg_.gzip_unsteady_hold_ns) return true;
+  for (const auto& g : gzip_next_ns_) {
+    const uint64_t e = g.load(std::memory_order_relaxed);
+    if (e && e <= now_ns + horizon_ns) return true;
+  }
+  return false;
 }
 
 void HttpServer::run(Worker* w) {
@@ -408,6 +421,8 @@ void HttpServer::run(Worker* w) {
           if (c.n_intervals < 4) ++c.n_intervals;
         }
         c.last_metrics_ns = t0;
+        c.gzip_client = want_gzip && cfg_.enable_gzip;
+        if (c.gzip_client && !c.expected_next()) gzip_unsteady_ns_.store(t0, std::memory_order_relaxed);
         SnapshotStore::Pin pin = store_->acquire();
         if (!pin) {
           respond_simple(c, 503, "Service Unavailable", "text/plain", "no sample yet\n", is_head);
@@ -418,8 +433,16 @@ void HttpServer::run(Worker* w) {
           const bool pb = want_proto && !pin->pb.empty();
           const std::string& plain = pb ? pin->pb : pin->body;
           const std::string& zipped = pb ? pin->pb_gz : pin->gz;
-          bool gz = want_gzip && cfg_.enable_gzip && !zipped.empty();
-          const std::string& b = gz ? zipped : plain;
+          const bool gz = want_gzip && cfg_.enable_gzip;
+          bool own = false;
+          if (gz && zipped.empty() && !is_head) {
+            // off schedule (or the first ask): compress here, for this response only
+            c.owned_body.clear();
+            own = gzip_compress(plain, &c.owned_body, cfg_.gzip_level) && !c.owned_body.empty();
+            stats_.gzip_on_demand.fetch_add(1, std::memory_order_relaxed);
+          }
+          const bool use_gz = gz && (own || !zipped.empty());
+          const std::string& b = own ? c.owned_body : (use_gz ? zipped : plain);
           c.head.clear();
           if (pb) {
             c.head.append("HTTP/1.1 200 OK\r\nContent-Type: application/vnd.google.protobuf; "
@@ -428,7 +451,7 @@ void HttpServer::run(Worker* w) {
           } else {
             c.head.append("HTTP/1.1 200 OK\r\nContent-Type: text/plain; version=0.0.4; charset=utf-8\r\n");
           }
-          if (gz) {
+          if (use_gz) {
             c.head.append("Content-Encoding: gzip\r\n");
             stats_.gzip_responses.fetch_add(1, std::memory_order_relaxed);
           }
@@ -483,13 +506,16 @@ void HttpServer::run(Worker* w) {
   if (w->timerfd >= 0) ::prctl(PR_SET_TIMERSLACK, 10000UL, 0, 0, 0);  // 10 us: pre-wake slices stay short
   // Arms the pre-wake timer for the earliest expected scrape (see HttpConfig::prewake).
   auto arm_prewake = [&]() {
-    if (w->timerfd < 0) return;
     const uint64_t now = mono_ns();
-    uint64_t next = 0;
+    uint64_t next = 0, gz_next = 0;
     for (auto& kv : w->conns) {
       const uint64_t e = kv.second.expected_next();
       if (e && e + cfg_.prewake_window_ns > now && (!next || e < next)) next = e;
+      // a steady gzip scraper gone quiet for a minute no longer holds the sampler to it
+      if (e && kv.second.gzip_client && e + 60000000000ull > now && (!gz_next || e < gz_next)) gz_next = e;
     }
+    gzip_next_ns_[w->index].store(gz_next, std::memory_order_relaxed);
+    if (w->timerfd < 0) return;
     itimerspec its{};
     if (next) {
       // before the lead: one timer at (expected - lead); inside the window: short slices

@@ -26,6 +26,10 @@ struct HttpConfig {
   int max_conns = 4096;
   int idle_timeout_ms = 120000;
   bool enable_gzip = true;
+  // how long a gzip request from a connection without a steady scrape period keeps the
+  // sampler pre-compressing every tick (see gzip_due)
+  uint64_t gzip_unsteady_hold_ns = 60000000000ull;
+  int gzip_level = 1;  // of responses the worker compresses itself (EngineConfig::gzip_level for the sampler's)
   // Send buffer of accepted sockets.  A fresh TCP socket starts at tcp_wmem[1] (16 KiB),
   // so a 30-200 KB exposition could not be queued by one writev: the rest waited for the
   // peer's ACK and an EPOLLOUT wake-up — measured +25 us p50 for a 26 KB body on loopback.
@@ -67,6 +71,9 @@ struct HttpStats {
   std::atomic<uint64_t> writev_ns{0};
   std::atomic<uint64_t> partial_writes{0};
   std::atomic<uint64_t> prewake_timer_wakeups{0};  // timer expiries of the scrape pre-wake
+  // gzip responses the worker compressed itself: the snapshot had no gzip copy because no
+  // gzip scrape was expected before the next tick (see HttpServer::gzip_due)
+  std::atomic<uint64_t> gzip_on_demand{0};
   std::atomic<uint64_t> lat_buckets[kBuckets + 1]{};  // +Inf last, non-cumulative
   std::atomic<uint64_t> lat_sum_ns{0};
   std::atomic<uint64_t> lat_count{0};
@@ -89,6 +96,12 @@ class HttpServer {
   // Last time (mono ns) a client asked for gzip; the sampler pre-compresses while
   // this is recent so gzip scrapes stay O(bytes) too.
   uint64_t gzip_wanted_ns() const { return gzip_wanted_ns_.load(std::memory_order_relaxed); }
+  // Whether a snapshot published at `now_ns` should carry a gzip copy: true while a gzip
+  // client scrapes without a steady period (within gzip_unsteady_hold_ns), or when a steady
+  // gzip client's next request is expected within `horizon_ns` (or is overdue).  Prometheus
+  // scraping every 15 s against a 10 Hz sampler thus costs one compression per scrape,
+  // not 150; a request that arrives off schedule is compressed by the worker itself.
+  bool gzip_due(uint64_t now_ns, uint64_t horizon_ns) const;
   // Last time a scraper negotiated the protobuf exposition (the sampler renders it then).
   uint64_t proto_wanted_ns() const { return proto_wanted_ns_.load(std::memory_order_relaxed); }
   const HttpStats& stats() const { return stats_; }
@@ -104,6 +117,11 @@ class HttpServer {
   std::atomic<bool> ready_{false};
   std::atomic<uint64_t> gzip_wanted_ns_{0};
   std::atomic<uint64_t> proto_wanted_ns_{0};
+  // last gzip /metrics request from a connection without a steady period
+  std::atomic<uint64_t> gzip_unsteady_ns_{0};
+  // per worker: earliest expected request of its steady gzip connections (0 = none)
+  static constexpr int kMaxWorkers = 64;
+  std::atomic<uint64_t> gzip_next_ns_[kMaxWorkers]{};
   HttpStats stats_;
   std::vector<std::unique_ptr<Worker>> workers_;
 };

@@ -118,11 +118,16 @@ def test_gzip_negotiation(mock_engine):
     e = mock_engine(1)
     e.tick(1_000_000_000)
     r, body = req(e.http_port, "/metrics", headers={"Accept-Encoding": "gzip"})
-    assert r.status == 200 and r.getheader("Content-Encoding") is None  # not yet compressed
-    e.tick(1_100_000_000)  # sampler now pre-compresses each tick
+    # the snapshot has no gzip copy yet: the worker compresses this response itself
+    assert r.status == 200 and r.getheader("Content-Encoding") == "gzip"
+    assert gzip.decompress(body).decode() == e.snapshot_text()
+    assert e.stats()["http_gzip_on_demand"] == 1
+    e.tick(1_100_000_000)  # unsteady gzip client: the sampler pre-compresses each tick
+    assert e.stats()["gzip_eager"] == 1
     r, body = req(e.http_port, "/metrics", headers={"Accept-Encoding": "gzip, deflate"})
     assert r.getheader("Content-Encoding") == "gzip"
     assert gzip.decompress(body).decode() == e.snapshot_text()
+    assert e.stats()["http_gzip_on_demand"] == 1
     r, body = req(e.http_port, "/metrics")
     assert r.getheader("Content-Encoding") is None
 
@@ -378,3 +383,50 @@ def test_scrape_prewake_learns_a_steady_period(native):
     assert 4 <= woke <= 14 * 12, woke   # armed from the 5th scrape on; bounded per scrape
     assert later - woke <= 25           # at most one window's worth after the last scrape
     assert run(False) == (0, 0)
+
+
+def test_gzip_copy_follows_the_scrape_schedule(native):
+    """A steady keep-alive gzip scraper (every 200 ms) against a 100 Hz sampler: once its
+    period is learnt, the sampler compresses only in the ticks just before each expected
+    scrape instead of every tick, and every response is still served gzip'd from the
+    snapshot (the worker compresses only off-schedule requests)."""
+    import http.client
+    c = native.EngineConfig()
+    c.backend = "mock"
+    c.mock_devices = 2
+    c.interval_s = 0.01
+    c.serve_http = True
+    c.http.host = "127.0.0.1"
+    c.http.port = 0
+    c.http.gzip_unsteady_hold_ns = 300_000_000
+    e = native.Engine(c)
+    e.start()
+    try:
+        conn = http.client.HTTPConnection("127.0.0.1", e.http_port, timeout=5)
+
+        def scrape():
+            conn.request("GET", "/metrics", headers={"Accept-Encoding": "gzip"})
+            r = conn.getresponse()
+            body = r.read()
+            assert r.status == 200 and r.getheader("Content-Encoding") == "gzip"
+            assert gzip.decompress(body).startswith(b"# HELP")
+
+        while e.stats()["ticks"] < 2:
+            time.sleep(0.01)
+        t_next = time.monotonic()
+        for i in range(22):
+            if i == 10:  # steady since the 5th scrape, unsteady hold (300 ms) over
+                s0 = e.stats()
+            scrape()
+            t_next += 0.2
+            time.sleep(max(0.0, t_next - time.monotonic()))
+        s1 = e.stats()
+        ticks = s1["ticks"] - s0["ticks"]
+        eager = s1["gzip_eager"] - s0["gzip_eager"]
+        on_demand = s1["http_gzip_on_demand"] - s0["http_gzip_on_demand"]
+        print("ticks", ticks, "eager", eager, "on_demand", on_demand)
+        # 12 scrapes over ~240 ticks: ~3 compressing ticks per scrape, not every tick
+        assert ticks > 150 and eager < 0.35 * ticks, (ticks, eager)
+        assert on_demand <= 3, on_demand
+    finally:
+        e.stop()
