@@ -5,7 +5,9 @@ kernel) for `seconds` per trial, alternating trials with no exporter and with th
 exporter sampling at 10 Hz and 100 Hz (amdsmi raw path + HIP sentinel + aqlprofile PMC
 counters, full profile) — interleaved so clock/thermal drift cancels out.  This parent
 never touches the GPU; every GPU user is a child process.
-Usage: python tools/interference.py [seconds_per_trial] [rounds]  -> prints RESULT json
+Usage: python tools/interference.py [seconds_per_trial] [rounds] [gemm|copy]  -> prints RESULT json
+  gemm  MFMA-bound pod (TFLOP/s);  copy  HBM-bound pod: the calibration stream copy of
+        1 GiB per launch (probe_device.h), read+write TB/s
 """
 import json
 import os
@@ -18,10 +20,34 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def burn(seconds: float) -> float:
-    code = (f"import sys, json; sys.path.insert(0, {ROOT!r});"
-            "from kubernetes_gpu_exporter_amd.ops.gemm import gemm_burn;"
-            f"print(json.dumps(gemm_burn(0, 8192, {seconds}, 4)), flush=True)")
+COPY_BURN = """
+import json, sys, time
+sys.path.insert(0, {root!r})
+import torch
+from kubernetes_gpu_exporter_amd.ops.gemm import stream_copy
+src = torch.empty(1 << 30, dtype=torch.uint8, device="cuda").fill_(1)
+dst = torch.empty_like(src)
+for _ in range(10):
+    stream_copy(src, dst)
+torch.cuda.synchronize()
+n, t0 = 0, time.perf_counter()
+while time.perf_counter() - t0 < {seconds}:
+    for _ in range(50):
+        stream_copy(src, dst)
+    torch.cuda.synchronize()
+    n += 50
+dt = time.perf_counter() - t0
+print(json.dumps({{"tflops": 2.0 * (1 << 30) * n / dt / 1e12}}), flush=True)  # TB/s, read+write
+"""
+
+
+def burn(seconds: float, workload: str = "gemm") -> float:
+    if workload == "copy":
+        code = COPY_BURN.format(root=ROOT, seconds=seconds)
+    else:
+        code = (f"import sys, json; sys.path.insert(0, {ROOT!r});"
+                "from kubernetes_gpu_exporter_amd.ops.gemm import gemm_burn;"
+                f"print(json.dumps(gemm_burn(0, 8192, {seconds}, 4)), flush=True)")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=seconds + 120)
     line = [l for l in r.stdout.splitlines() if l.startswith("{")]
     if r.returncode != 0 or not line:
@@ -55,14 +81,15 @@ def start_exporter(hz: float):
 def main() -> int:
     secs = float(sys.argv[1]) if len(sys.argv) > 1 else 8.0
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    workload = sys.argv[3] if len(sys.argv) > 3 else "gemm"
     res = {"none": [], "10hz": [], "100hz": []}
-    burn(2.0)  # warm clocks / code objects
+    burn(2.0, workload)  # warm clocks / code objects
     for r in range(rounds):
         for mode in ("none", "10hz", "100hz"):
             p = start_exporter(10.0 if mode == "10hz" else 100.0) if mode != "none" else None
             try:
                 time.sleep(1.0 if p else 0.0)
-                res[mode].append(burn(secs))
+                res[mode].append(burn(secs, workload))
             finally:
                 if p is not None:
                     p.terminate()
@@ -71,7 +98,8 @@ def main() -> int:
     med = {k: statistics.median(v) for k, v in res.items()}
     out = {"tflops": res, "median_tflops": {k: round(v, 1) for k, v in med.items()},
            "slowdown_pct": {k: round(100.0 * (med["none"] - med[k]) / med["none"], 3) for k in ("10hz", "100hz")},
-           "seconds_per_trial": secs, "rounds": rounds}
+           "seconds_per_trial": secs, "rounds": rounds, "workload": workload,
+           "unit": "TB/s read+write" if workload == "copy" else "TFLOP/s"}
     print("RESULT " + json.dumps(out), flush=True)
     return 0
 
