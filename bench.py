@@ -236,7 +236,7 @@ def main() -> int:
     # ranks of one launch share the directory the exporter watches.
     rccl_dir = ""
     tracer = os.path.join(ROOT, "kubernetes_gpu_exporter_amd", "libgpuexp_rccl_tracer.so")
-    if args.rccl_trace and os.path.exists(tracer) and os.path.exists("/dev/kfd"):
+    if args.rccl_trace and args.backend != "mock" and os.path.exists(tracer) and os.path.exists("/dev/kfd"):
         run_id = os.environ.get("TORCHELASTIC_RUN_ID") or os.environ.get("MASTER_PORT") or str(os.getpid())
         rccl_dir = os.path.join(tempfile.gettempdir(), f"gpuexp-bench-rccl-{run_id}")
         os.makedirs(rccl_dir, exist_ok=True)
@@ -273,7 +273,7 @@ def main() -> int:
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl" if have_gpu else "gloo")
+        dist.init_process_group("nccl" if have_gpu and backend != "mock" else "gloo")  # mock: CPU ranks
     elif have_gpu and backend != "mock" and args.allreduce_mb > 0:
         # N=1 runs the same data-parallel pod (a 1-rank RCCL all-reduce per step), so the
         # workload and the RCCL path are the same at every N.
