@@ -9,6 +9,7 @@
 #include "gpuexp/backends.h"
 #include "gpuexp/client.h"
 #include "gpuexp/engine.h"
+#include "gpuexp/kfd_events.h"
 #include "gpuexp/exposition.h"
 #include "gpuexp/gpu_metrics.h"
 #include "gpuexp/procs.h"
@@ -148,6 +149,12 @@ PYBIND11_MODULE(_gpuexp, m) {
     return s;
   });
   m.def("gzip_impl", []() { return std::string(gzip_impl()); });
+  m.def("parse_kfd_event", [](py::bytes b) -> py::object {
+    std::string s(b);
+    int ev = 0, pid = -1;
+    if (!gpuexp::parse_kfd_event(s.data(), s.size(), &ev, &pid)) return py::none();
+    return py::make_tuple(gpuexp::kfd_event_name(ev), pid);
+  }, "Parses one KFD SMI event message: (event name, pid or -1), None if malformed");
   m.def("gzip", [](py::bytes b, int level) {
     std::string in = b, out;
     if (!gzip_compress(in, &out, level)) throw std::runtime_error("gzip failed");
@@ -427,6 +434,8 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("enable_rccl", &EngineConfig::enable_rccl)
       .def_readwrite("rccl_dir", &EngineConfig::rccl_dir)
       .def_readwrite("rccl_verify", &EngineConfig::rccl_verify)
+      .def_readwrite("enable_kfd_events", &EngineConfig::enable_kfd_events)
+      .def_readwrite("kfd_path", &EngineConfig::kfd_path)
       .def_readwrite("metrics_min_interval_s", &EngineConfig::metrics_min_interval_s)
       .def_readwrite("queue_devices", &EngineConfig::queue_devices)
       .def_readwrite("queue_devices_bdf", &EngineConfig::queue_devices_bdf)
@@ -535,6 +544,8 @@ PYBIND11_MODULE(_gpuexp, m) {
         e.set_device_owners(std::move(v));
       })
       .def("set_pid_cgroup", &Engine::set_pid_cgroup)
+      .def("inject_kfd_events", [](Engine& e, int dev, py::bytes b) { e.inject_kfd_events(dev, std::string(b)); },
+           "Test hook: bytes as if read from GPU `dev`'s KFD SMI event fd (counted at the next tick)")
       .def("clear_pid_cgroups", &Engine::clear_pid_cgroups)
       .def("mock_set_value", [](Engine& e, int dev, const std::string& field, double v) {
         if (!e.mock()) throw std::runtime_error("not a mock backend");

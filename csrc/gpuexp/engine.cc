@@ -241,6 +241,13 @@ void Engine::define_families() {
   f_rccl_comm_ = add("amd_rccl_communicator_info",
                      "Rank and size of the largest RCCL communicator of a process (value is always 1)", G,
                      {"namespace", "pod", "pid", "rank", "nranks"});
+  f_kfd_ev_ = add("amd_gpu_kfd_events_total",
+                  "KFD SMI events on this GPU: vm_fault (a process's GPU page fault), thermal_throttle, "
+                  "gpu_pre_reset / gpu_post_reset, queue_eviction / queue_restore (full profile)",
+                  C, with(D, {"event"}));
+  f_pod_kfd_ev_ = add("amd_pod_gpu_kfd_events_total",
+                      "Per-process KFD SMI events (vm_fault, queue_eviction, queue_restore) of a pod's processes, "
+                      "over all GPUs", C, {"namespace", "pod", "event"});
 
   // --- exporter self-metrics (own prefix; the reference registry had none, main.go:40) ---
   f_self_build_ = add("gpuexp_build_info", "Exporter build and backend", G, {"version", "backend"});
@@ -425,6 +432,25 @@ bool Engine::start(std::string* err) {
     sentinel_status_ = "mock";
   }
   if (cfg_.enable_rccl) rccl_ = make_rccl_source(cfg_.rccl_dir, cfg_.rccl_verify);
+  if (cfg_.enable_kfd_events && cfg_.series_profile == "full") {
+    kfd_events_ = std::make_unique<KfdEventSource>();
+    if (mock_) {
+      kfd_events_->set_devices(devices_.size());  // events arrive through inject_kfd_events only
+      kfd_events_status_ = "mock (injected events)";
+    } else {
+      std::string e;
+      const int n = kfd_events_->open(devices_, cfg_.kfd_path, &e);
+      if (n == 0) {
+        kfd_events_status_ = "unavailable: " + e;
+        GPUEXP_LOG(LogLevel::kWarn, "kfd_events", kfd_events_status_);
+        kfd_events_.reset();
+      } else {
+        kfd_events_status_ = "on " + std::to_string(n) + " GPU(s), " +
+                             (kfd_events_->all_processes() ? "every process's events"
+                                                           : "device-wide events + own process (no CAP_SYS_ADMIN)");
+      }
+    }
+  }
 
   if (!cfg_.trace_path.empty()) {
     trace_ = std::fopen(cfg_.trace_path.c_str(), "w");
@@ -509,6 +535,52 @@ void Engine::set_device_owners(std::vector<std::pair<std::string, DeviceOwner>> 
   ctl_dirty_ = true;
 }
 
+void Engine::inject_kfd_events(int dev, const std::string& bytes) {
+  std::lock_guard<std::mutex> lk(ctl_mu_);
+  pending_kfd_bytes_.emplace_back(dev, bytes);
+}
+
+// Drains the KFD event fds (and injected bytes) into per-GPU counts and, for events that
+// name a process, per-pod counts (PID -> cgroup -> pod, cached by the resolver, so a
+// process killed by its own VM fault is still attributed if it was seen before).
+void Engine::count_kfd_events() {
+  std::vector<KfdEvent> evs;
+  kfd_events_->drain(&evs);
+  {
+    std::lock_guard<std::mutex> lk(ctl_mu_);
+    for (auto& b : pending_kfd_bytes_) kfd_events_->feed(b.first, b.second.data(), b.second.size(), &evs);
+    pending_kfd_bytes_.clear();
+  }
+  for (const KfdEvent& e : evs) {
+    if (e.dev < 0 || size_t(e.dev) >= dstate_.size() || e.event <= 0 || e.event >= kKfdEventIds) continue;
+    dstate_[size_t(e.dev)].kfd_events[e.event] += 1;
+    if (e.pid <= 0) continue;
+    const CgroupInfo* ci = cfg_.pod_attribution ? resolver_->resolve(e.pid) : nullptr;
+    auto pit = ci && ci->kube ? pods_by_uid_.find(ci->pod_uid) : pods_by_uid_.end();
+    if (pit == pods_by_uid_.end()) {
+      ++kfd_events_unattributed_;
+      continue;
+    }
+    pod_kfd_events_[std::make_tuple(pit->second.ns, pit->second.name, e.event)] += 1;
+  }
+}
+
+void Engine::emit_kfd_events(uint64_t gen) {
+  // a pod's counts live as long as the control plane knows the pod
+  std::set<std::pair<std::string, std::string>> live;
+  for (auto& kv : pods_by_uid_) live.emplace(kv.second.ns, kv.second.name);
+  for (auto it = pod_kfd_events_.begin(); it != pod_kfd_events_.end();) {
+    const auto& k = it->first;
+    if (!live.count({std::get<0>(k), std::get<1>(k)})) {
+      it = pod_kfd_events_.erase(it);
+      continue;
+    }
+    table_.put(f_pod_kfd_ev_, {std::get<0>(k), std::get<1>(k), kfd_event_name(std::get<2>(k))}, double(it->second),
+               gen);
+    ++it;
+  }
+}
+
 void Engine::set_pid_cgroup(int pid, const std::string& cgroup_path) {
   std::lock_guard<std::mutex> lk(ctl_mu_);
   pending_overrides_.emplace_back(pid, cgroup_path);
@@ -558,6 +630,7 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
     std::copy(std::begin(st.xcc_last), std::end(st.xcc_last), std::begin(fresh.xcc_last));
     fresh.errors = st.errors;
     fresh.err_ref = st.err_ref;
+    std::copy(std::begin(st.kfd_events), std::end(st.kfd_events), std::begin(fresh.kfd_events));
     fresh.owner = keep;
     fresh.owner_key = okey;
     st = fresh;
@@ -574,6 +647,12 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
   if (!table_.set(st.err_ref, double(st.errors), gen)) {
     st.err_ref = table_.upsert(f_self_dev_errors_, {std::to_string(d.index)});
     table_.set(st.err_ref, double(st.errors), gen);
+  }
+  if (kfd_events_) {
+    // counted whether or not this tick's telemetry read worked: a reset shows here first
+    for (size_t k = 0; k < std::size(kKfdSubscribed); ++k)
+      dput(st, i, st.kev[k], f_kfd_ev_, {kfd_event_name(kKfdSubscribed[k])},
+           double(st.kfd_events[kKfdSubscribed[k]]), gen);
   }
   if (!c.ok) return;  // a failed GPU exports only up=0 (+ errors); others unaffected
   bool compact = cfg_.series_profile == "compact";
@@ -1002,6 +1081,9 @@ void Engine::emit_self(uint64_t gen) {
   cput(self_refs_[14], f_self_source_up_, (counters_ || (cfg_.enable_counters && mock_)) ? 1 : 0, gen,
        [] { return std::vector<std::string>{"counters"}; });
   cput(self_refs_[15], f_self_source_up_, rccl_ ? 1 : 0, gen, [] { return std::vector<std::string>{"rccl"}; });
+  if (cfg_.enable_kfd_events && cfg_.series_profile == "full")
+    cput(self_refs_[18], f_self_source_up_, kfd_events_ ? 1 : 0, gen,
+         [] { return std::vector<std::string>{"kfd_events"}; });
   if (rccl_) {
     int a = 0, u = 0, x = 0;
     rccl_->file_states(&a, &u, &x);
@@ -1141,6 +1223,7 @@ void Engine::tick_locked(uint64_t now) {
 
   // 3: sentinel (drain previous run, launch next; never blocks on the GPU)
   if (sentinel_) sentinel_->tick(now);
+  if (kfd_events_) count_kfd_events();
   ts[4] = mono_ns();
   // 4: counters are sampled inside collect_device (per GPU); timed there as part of series
   ts[5] = mono_ns();
@@ -1150,6 +1233,7 @@ void Engine::tick_locked(uint64_t now) {
     if (cfg_.series_profile != "legacy") collect_device(int(i), gen, dt_s);
   }
   emit_processes(gen, per_dev);
+  if (kfd_events_) emit_kfd_events(gen);
   emit_self(gen);
   ts[6] = mono_ns();
 
@@ -1223,7 +1307,8 @@ EngineStats Engine::stats() {
 
 std::string Engine::source_status() {
   std::string s = std::string("backend=") + (backend_ ? backend_->name() : "none") + " sentinel=" + sentinel_status_ +
-                  " counters=" + counters_status_ + " rccl=" + (rccl_ ? cfg_.rccl_dir : "disabled");
+                  " counters=" + counters_status_ + " rccl=" + (rccl_ ? cfg_.rccl_dir : "disabled") +
+                  " kfd_events=" + kfd_events_status_;
   if (backend_)
     for (const auto& d : devices_) s += " gpu" + std::to_string(d.index) + "=[" + backend_->describe(d) + "]";
   return s;

@@ -12,12 +12,14 @@
 #include <cstdio>
 #include <functional>
 #include <initializer_list>
+#include <iterator>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <set>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <unordered_map>
 #include <vector>
 
@@ -25,6 +27,7 @@
 #include "gpuexp/device.h"
 #include "gpuexp/exposition.h"
 #include "gpuexp/http.h"
+#include "gpuexp/kfd_events.h"
 #include "gpuexp/procs.h"
 #include "gpuexp/ras.h"
 #include "gpuexp/snapshot.h"
@@ -86,6 +89,8 @@ struct EngineConfig {
   bool enable_rccl = false;
   std::string rccl_dir = "/dev/shm";
   bool rccl_verify = true;             // attribute a tracer file only to a process that maps it
+  bool enable_kfd_events = true;       // full profile: KFD SMI events (VM faults, resets, ...)
+  std::string kfd_path = "/dev/kfd";   // the device node itself (not under host_root)
   bool force_amdsmi_metrics = false;
   int gzip_level = 1;
   uint64_t gc_after = 1;               // stale series vanish this many ticks after last seen
@@ -151,6 +156,8 @@ class Engine {
   void set_device_owners(std::vector<std::pair<std::string, DeviceOwner>> owners);
   void set_pid_cgroup(int pid, const std::string& cgroup_path);
   void clear_pid_cgroups();
+  // Test hook: bytes as if read from device `dev`'s KFD SMI event fd (applied next tick).
+  void inject_kfd_events(int dev, const std::string& bytes);
 
   static const char* stage_name(int i);
   static constexpr int kStages = 8;
@@ -173,7 +180,9 @@ class Engine {
     SeriesRef info, up, gfx, umc, xcc[kMaxXcc], vram_used, vram_total, hbm_bw, power, power_cap,
         energy, temp[9], clk[3], xrd[kMaxXgmiLinks], xwr[kMaxXgmiLinks], xrd_rate, xwr_rate,
         links_up, pcie_bw, pcie_replay, pcie_speed, pcie_width, thr[5], nprocs, cu_occ, ctr[10],
-        sen[4], ecc[3], aer[3], nak[2], recov, xgmi_w, xgmi_s, xclk[kMaxXcc], sen_xlat[kMaxXcc], sen_mem, sen_xmem[kMaxXcc];
+        sen[4], ecc[3], aer[3], nak[2], recov, xgmi_w, xgmi_s, xclk[kMaxXcc], sen_xlat[kMaxXcc], sen_mem, sen_xmem[kMaxXcc],
+        kev[std::size(kKfdSubscribed)];
+    uint64_t kfd_events[kKfdEventIds] = {};  // KFD SMI events seen on this GPU, by id
     uint64_t errors = 0;
     SeriesRef err_ref;
     SeriesRef self_reads[4];  // gpu_metrics reads fresh / coalesced, refresh period, counter scope
@@ -199,6 +208,8 @@ class Engine {
   void collect_device(int i, uint64_t gen, double dt_s);
   void emit_processes(uint64_t gen, const std::vector<std::vector<ProcSample>>& per_dev);
   void emit_self(uint64_t gen);
+  void count_kfd_events();
+  void emit_kfd_events(uint64_t gen);
   void trace_event(const char* name, uint64_t start_ns, uint64_t dur_ns);
   void dput(DevState& st, int dev, SeriesRef& r, int fid, std::initializer_list<const char*> extra,
             double v, uint64_t gen);
@@ -222,6 +233,12 @@ class Engine {
   std::unique_ptr<SentinelSource> sentinel_;
   std::unique_ptr<CounterSource> counters_;
   std::unique_ptr<RcclSource> rccl_;
+  std::unique_ptr<KfdEventSource> kfd_events_;
+  std::string kfd_events_status_ = "disabled";
+  std::vector<std::pair<int, std::string>> pending_kfd_bytes_;  // test injection (ctl_mu_)
+  // per-process KFD events attributed to pods: (namespace, pod, event id) -> count
+  std::map<std::tuple<std::string, std::string, int>, uint64_t> pod_kfd_events_;
+  uint64_t kfd_events_unattributed_ = 0;  // per-process events whose PID resolved to no pod
   std::unique_ptr<ForkJoinPool> pool_;
   // full profile, real backends: RAS/AER readers + last totals (re-read every ras_interval_s)
   std::vector<RasReader> ras_;
@@ -259,7 +276,7 @@ class Engine {
   std::unordered_map<uint64_t, ProcRefs> proc_refs_;               // (device << 32 | pid) -> handles
   std::unordered_map<uint64_t, ProcRefs> legacy_refs_;             // pid -> legacy handles (pod, vram, gfx=perc)
   std::map<std::pair<std::string, std::string>, PodRefs> pod_refs_;  // (ns, pod) -> handles
-  SeriesRef self_refs_[18];
+  SeriesRef self_refs_[20];
 
   // stats (guarded by stats_mu_)
   std::mutex stats_mu_;
@@ -280,6 +297,7 @@ class Engine {
   int f_legacy_mem_ = -1, f_legacy_perc_ = -1;
   int f_pod_vram_, f_pod_procs_, f_pod_gpus_, f_pod_xrd_, f_pod_xwr_, f_pod_power_, f_pod_gfx_, f_pod_gfx_share_;
   int f_rccl_calls_, f_rccl_bytes_, f_rccl_comm_;
+  int f_kfd_ev_ = -1, f_pod_kfd_ev_ = -1;
   int f_self_build_, f_self_ticks_, f_self_last_, f_self_stage_, f_self_scrape_, f_self_scrapes_,
       f_self_http_bytes_, f_self_render_bytes_, f_self_series_, f_self_dev_errors_,
       f_self_overruns_, f_self_cpu_, f_self_source_up_, f_self_ctr_scope_, f_self_metrics_reads_, f_self_metrics_period_, f_self_prewake_, f_self_gzip_,

@@ -182,6 +182,43 @@ def test_exporter_tick_on_gpu(native):
         e.stop()
 
 
+def test_kfd_events_source_opens(native):
+    """The KFD SMI event fd opens on the real GPU (AMDKFD_IOC_SMI_EVENTS) and the six
+    per-GPU event counters are exported from the first tick."""
+    e = amdsmi_engine(native, series_profile="full")
+    try:
+        e.tick()
+        status = e.source_status()
+        print(status)
+        assert "kfd_events=on 1 GPU(s)" in status, status
+        fams = promtext.parse(e.snapshot_text())
+        ev = {s[1]["event"]: s[2] for s in promtext.samples(fams, "amd_gpu_kfd_events_total") if s[1]["gpu"] == "0"}
+        assert set(ev) == {"vm_fault", "thermal_throttle", "gpu_pre_reset", "gpu_post_reset", "queue_eviction",
+                           "queue_restore"}, ev
+        assert all(v >= 0 for v in ev.values())
+        up = [s[2] for s in promtext.samples(fams, "gpuexp_source_up") if s[1]["source"] == "kfd_events"]
+        assert up == [1]
+    finally:
+        e.stop()
+
+
+def test_kfd_events_real_queue_eviction():
+    """A real KFD event end to end (tools/kfd_events_check.py): invalidating a host buffer
+    registered with the GPU makes KFD evict and restore this process's queues; the engine
+    (same process, so an unprivileged event client sees them) counts both on GPU 0 and
+    attributes them to the process's pod."""
+    import json
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "kfd_events_check.py")], capture_output=True,
+                       text=True, timeout=120)
+    print(r.stdout[-3000:], r.stderr[-2000:])
+    line = [l for l in r.stdout.splitlines() if l.startswith("RESULT ")]
+    assert line, "kfd events check produced no result"
+    res = json.loads(line[-1][7:])
+    assert res["moved"]["queue_eviction"] >= 1 and res["moved"]["queue_restore"] >= 1, res
+    assert res["moved"]["vm_fault"] == 0 and res["moved"]["gpu_pre_reset"] == 0, res
+    assert res["pod"].get("probe/evicted-pod/queue_eviction", 0) >= 1, res
+
+
 @pytest.mark.parametrize("impl", ["hip", "queue"])
 def test_sentinel_one_wave_per_xcd(native, impl):
     """Full profile: the sentinel run puts one wave on each XCD (placement read back from
