@@ -54,6 +54,8 @@ class Config:
     queue_devices: list = field(default_factory=list)  # GPUs (indices / BDFs) that get the exporter's
                                            # own GPU queue (sentinel + PMC counters); empty = all.
                                            # Each queue pins ~346 MiB of host memory on MI355X.
+    enable_kfd_events: bool = True         # full profile: KFD SMI events (VM faults, resets, evictions)
+    kfd_path: str = "/dev/kfd"             # the device node (mounted directly, not under host_root)
     enable_rccl: bool = False
     rccl_dir: str = "/var/run/gpuexp/rccl"
     rccl_verify: bool = True               # a tracer file counts only for a live process that maps it
@@ -145,6 +147,8 @@ class Config:
         ec.enable_rccl = bool(self.enable_rccl)
         ec.rccl_dir = self.rccl_dir
         ec.rccl_verify = bool(self.rccl_verify)
+        ec.enable_kfd_events = bool(self.enable_kfd_events)
+        ec.kfd_path = self.kfd_path
         ec.gc_after = int(self.gc_after)
         ec.device_filter = [int(d) for d in self.devices if ":" not in str(d)]
         ec.device_filter_bdf = [str(d) for d in self.devices if ":" in str(d)]
