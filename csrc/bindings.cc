@@ -149,6 +149,11 @@ PYBIND11_MODULE(_gpuexp, m) {
     return s;
   });
   m.def("gzip_impl", []() { return std::string(gzip_impl()); });
+  m.def("parse_bad_pages", [](const std::string& body) -> py::object {
+    gpuexp::RasTotals t;
+    if (!gpuexp::parse_bad_pages(body, &t)) return py::none();
+    return py::make_tuple(int(t.pages_retired), int(t.pages_pending), int(t.pages_unreservable));
+  }, "Parses ras/gpu_vram_bad_pages: (retired, pending, unreservable) or None");
   m.def("parse_kfd_event", [](py::bytes b) -> py::object {
     std::string s(b);
     int ev = 0, pid = -1;

@@ -94,6 +94,11 @@ void MockBackend::sample(const DeviceInfo& dev, DeviceSample* out) {
   out->aer_cor = get(s, "aer_cor", 0);
   out->aer_nonfatal = get(s, "aer_nonfatal", 0);
   out->aer_fatal = get(s, "aer_fatal", 0);
+  out->pages_retired = get(s, "pages_retired", 0);
+  out->pages_pending = get(s, "pages_pending", 0);
+  out->pages_unreservable = get(s, "pages_unreservable", 0);
+  out->gtt_total = get(s, "gtt_total", 1024.0 * (1ull << 30));
+  out->gtt_used = get(s, "gtt_used", 2.0 * (1ull << 30));
   out->vram_max_bw_gbs = 8192;
 
   // Integrate accumulators with the scripted rates.

@@ -108,6 +108,10 @@ struct DeviceSample {
   // RAS / AER error totals (sysfs ras/*_err_count and aer_dev_*; refreshed at a low rate)
   double ecc_ce = kNaN, ecc_ue = kNaN, ecc_de = kNaN;
   double aer_cor = kNaN, aer_nonfatal = kNaN, aer_fatal = kNaN;
+  // HBM pages in the RAS bad-page table (refreshed with the RAS totals)
+  double pages_retired = kNaN, pages_pending = kNaN, pages_unreservable = kNaN;
+  // GTT: system memory mapped into the GPU's address space (mem_info_gtt_*, bytes)
+  double gtt_used = kNaN, gtt_total = kNaN;
 
   // throttle residency accumulators (same units as accumulation_counter)
   bool residency_valid = false;

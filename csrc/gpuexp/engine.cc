@@ -241,6 +241,13 @@ void Engine::define_families() {
   f_rccl_comm_ = add("amd_rccl_communicator_info",
                      "Rank and size of the largest RCCL communicator of a process (value is always 1)", G,
                      {"namespace", "pod", "pid", "rank", "nranks"});
+  f_pages_ = add("amd_gpu_retired_pages",
+                 "HBM pages in the RAS bad-page table by state: retired (never handed out again), pending, "
+                 "unreservable (ras/gpu_vram_bad_pages; full profile)",
+                 G, with(D, {"state"}));
+  f_gtt_used_ = add("amd_gpu_gtt_used_bytes", "System memory mapped into the GPU's address space (GTT, full profile)",
+                    G, D);
+  f_gtt_total_ = add("amd_gpu_gtt_total_bytes", "GTT size (full profile)", G, D);
   f_kfd_ev_ = add("amd_gpu_kfd_events_total",
                   "KFD SMI events on this GPU: vm_fault (a process's GPU page fault), thermal_throttle, "
                   "gpu_pre_reset / gpu_post_reset, queue_eviction / queue_restore (full profile)",
@@ -378,6 +385,21 @@ bool Engine::start(std::string* err) {
     }
     ras_cache_.assign(devices_.size(), RasTotals());
     ras_next_ns_.assign(devices_.size(), 0);
+    // GTT lives on the PCI function (a partition's amdgpu_xcp node has no mem_info_*)
+    gtt_used_f_.resize(devices_.size());
+    gtt_total_.assign(devices_.size(), kNaN);
+    for (size_t i = 0; i < devices_.size(); ++i) {
+      const DeviceInfo& di = devices_[i];
+      for (const std::string& dir : {root + "/sys/class/drm/renderD" + std::to_string(di.render_minor) + "/device",
+                                     root + "/sys/bus/pci/devices/" + di.bdf}) {
+        if (!gtt_used_f_[i].open(dir + "/mem_info_gtt_used")) continue;
+        std::string body;
+        uint64_t v = 0;
+        if (read_small_file(dir + "/mem_info_gtt_total", &body) && parse_u64(body.data(), body.size(), &v))
+          gtt_total_[i] = double(v);
+        break;
+      }
+    }
   }
   int nthreads = cfg_.device_threads;
   if (nthreads <= 0) nthreads = cfg_.backend == "mock" ? 1 : std::min<int>(int(devices_.size()), 8);
@@ -735,6 +757,11 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
       dput(st, i, st.ecc[k], f_ecc_, {kEcc[k]}, ecc[k], gen);
       dput(st, i, st.aer[k], f_aer_, {kAer[k]}, aer[k], gen);
     }
+    dput(st, i, st.pages[0], f_pages_, {"retired"}, c.pages_retired, gen);
+    dput(st, i, st.pages[1], f_pages_, {"pending"}, c.pages_pending, gen);
+    dput(st, i, st.pages[2], f_pages_, {"unreservable"}, c.pages_unreservable, gen);
+    dput(st, i, st.gtt_used, f_gtt_used_, {}, c.gtt_used, gen);
+    dput(st, i, st.gtt_total, f_gtt_total_, {}, c.gtt_total, gen);
     dput(st, i, st.nak[0], f_pcie_nak_, {"sent"}, c.pcie_nak_sent, gen);
     dput(st, i, st.nak[1], f_pcie_nak_, {"received"}, c.pcie_nak_rcvd, gen);
     dput(st, i, st.recov, f_pcie_recov_, {}, c.pcie_l0_recov, gen);
@@ -1148,6 +1175,14 @@ void Engine::tick_locked(uint64_t now) {
       st.cur.aer_cor = r.aer_cor;
       st.cur.aer_nonfatal = r.aer_nonfatal;
       st.cur.aer_fatal = r.aer_fatal;
+      st.cur.pages_retired = r.pages_retired;
+      st.cur.pages_pending = r.pages_pending;
+      st.cur.pages_unreservable = r.pages_unreservable;
+    }
+    if (!gtt_used_f_.empty()) {
+      uint64_t v = 0;
+      if (gtt_used_f_[size_t(i)].read_u64(&v)) st.cur.gtt_used = double(v);
+      st.cur.gtt_total = gtt_total_[size_t(i)];
     }
   };
   if (pool_) {

@@ -181,7 +181,7 @@ class Engine {
         energy, temp[9], clk[3], xrd[kMaxXgmiLinks], xwr[kMaxXgmiLinks], xrd_rate, xwr_rate,
         links_up, pcie_bw, pcie_replay, pcie_speed, pcie_width, thr[5], nprocs, cu_occ, ctr[10],
         sen[4], ecc[3], aer[3], nak[2], recov, xgmi_w, xgmi_s, xclk[kMaxXcc], sen_xlat[kMaxXcc], sen_mem, sen_xmem[kMaxXcc],
-        kev[std::size(kKfdSubscribed)];
+        kev[std::size(kKfdSubscribed)], pages[3], gtt_used, gtt_total;
     uint64_t kfd_events[kKfdEventIds] = {};  // KFD SMI events seen on this GPU, by id
     uint64_t errors = 0;
     SeriesRef err_ref;
@@ -244,6 +244,8 @@ class Engine {
   std::vector<RasReader> ras_;
   std::vector<RasTotals> ras_cache_;
   std::vector<uint64_t> ras_next_ns_;
+  std::vector<CachedFile> gtt_used_f_;  // full profile, real backends: mem_info_gtt_used per device
+  std::vector<double> gtt_total_;
   std::vector<uint64_t> metrics_fresh_, metrics_coalesced_;  // per device
   uint64_t gzip_eager_ = 0;  // sampler thread only; copied into stats_ per tick
   std::string sentinel_status_ = "disabled", counters_status_ = "disabled";
@@ -297,7 +299,7 @@ class Engine {
   int f_legacy_mem_ = -1, f_legacy_perc_ = -1;
   int f_pod_vram_, f_pod_procs_, f_pod_gpus_, f_pod_xrd_, f_pod_xwr_, f_pod_power_, f_pod_gfx_, f_pod_gfx_share_;
   int f_rccl_calls_, f_rccl_bytes_, f_rccl_comm_;
-  int f_kfd_ev_ = -1, f_pod_kfd_ev_ = -1;
+  int f_kfd_ev_ = -1, f_pod_kfd_ev_ = -1, f_pages_ = -1, f_gtt_used_ = -1, f_gtt_total_ = -1;
   int f_self_build_, f_self_ticks_, f_self_last_, f_self_stage_, f_self_scrape_, f_self_scrapes_,
       f_self_http_bytes_, f_self_render_bytes_, f_self_series_, f_self_dev_errors_,
       f_self_overruns_, f_self_cpu_, f_self_source_up_, f_self_ctr_scope_, f_self_metrics_reads_, f_self_metrics_period_, f_self_prewake_, f_self_gzip_,

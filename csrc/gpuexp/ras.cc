@@ -48,9 +48,40 @@ double parse_aer_total(const std::string& body) {
   return double(v);
 }
 
+bool parse_bad_pages(const std::string& body, RasTotals* t) {
+  double r = 0, p = 0, f = 0;
+  bool any = false, bad = false;
+  size_t pos = 0;
+  while (pos < body.size()) {
+    size_t eol = body.find('\n', pos);
+    if (eol == std::string::npos) eol = body.size();
+    const std::string line = trim(body.substr(pos, eol - pos));
+    pos = eol + 1;
+    if (line.empty()) continue;
+    const size_t c = line.rfind(':');
+    const std::string st = c == std::string::npos ? std::string() : trim(line.substr(c + 1));
+    if (st == "R") r += 1;
+    else if (st == "P") p += 1;
+    else if (st == "F") f += 1;
+    else {
+      bad = true;
+      continue;
+    }
+    any = true;
+  }
+  if (bad && !any) return false;
+  t->pages_retired = r;
+  t->pages_pending = p;
+  t->pages_unreservable = f;
+  return true;
+}
+
 void RasReader::open(const std::string& pci_dev_dir) {
   ras_files_.clear();
   aer_dir_.clear();
+  bad_pages_.clear();
+  if (::access((pci_dev_dir + "/ras/gpu_vram_bad_pages").c_str(), R_OK) == 0)
+    bad_pages_ = pci_dev_dir + "/ras/gpu_vram_bad_pages";
   const std::string ras = pci_dev_dir + "/ras";
   for (const auto& f : list_dir(ras)) {
     const std::string suffix = "_err_count";
@@ -66,6 +97,7 @@ bool RasReader::read(RasTotals* out) const {
   std::string body;
   for (const auto& f : ras_files_)
     if (read_small_file(f, &body)) any |= parse_ras_err_count(body, &t);
+  if (!bad_pages_.empty() && read_small_file(bad_pages_, &body, 1 << 20)) any |= parse_bad_pages(body, &t);
   if (!aer_dir_.empty()) {
     if (read_small_file(aer_dir_ + "/aer_dev_correctable", &body)) t.aer_cor = parse_aer_total(body);
     if (read_small_file(aer_dir_ + "/aer_dev_nonfatal", &body)) t.aer_nonfatal = parse_aer_total(body);

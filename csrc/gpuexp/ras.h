@@ -20,12 +20,18 @@ namespace gpuexp {
 struct RasTotals {
   double ecc_ce = kNaN, ecc_ue = kNaN, ecc_de = kNaN;
   double aer_cor = kNaN, aer_nonfatal = kNaN, aer_fatal = kNaN;
+  // HBM pages in the RAS bad-page table (ras/gpu_vram_bad_pages): retired (reserved, never
+  // handed out again), pending retirement, and ones the driver could not reserve
+  double pages_retired = kNaN, pages_pending = kNaN, pages_unreservable = kNaN;
 };
 
 // Parses one amdgpu ras/<block>_err_count body; adds into *t (NaN fields start at 0).
 bool parse_ras_err_count(const std::string& body, RasTotals* t);
 // Parses one aer_dev_* body; returns the TOTAL_ERR_* value or NaN.
 double parse_aer_total(const std::string& body);
+// Parses ras/gpu_vram_bad_pages ("0x<page> : 0x<size> : R|P|F" per page); sets the three
+// page counts of *t.  False when no line parses (and the body is not empty).
+bool parse_bad_pages(const std::string& body, RasTotals* t);
 
 class RasReader {
  public:
@@ -33,11 +39,12 @@ class RasReader {
   void open(const std::string& pci_dev_dir);
   // Re-reads every file; returns false when the device exposes neither RAS nor AER.
   bool read(RasTotals* out) const;
-  size_t files() const { return ras_files_.size() + (aer_dir_.empty() ? 0 : 3); }
+  size_t files() const { return ras_files_.size() + (aer_dir_.empty() ? 0 : 3) + (bad_pages_.empty() ? 0 : 1); }
 
  private:
   std::vector<std::string> ras_files_;
   std::string aer_dir_;
+  std::string bad_pages_;
 };
 
 }  // namespace gpuexp

@@ -157,6 +157,16 @@ class FakeHost:
         for n, k, v in zip(names, keys, aer):
             self._w(f"{dev}/aer_dev_{n}", f"RxErr 0\nBadTLP 0\n{k} {v}\n")
 
+    def set_bad_pages(self, gpu: FakeGpu, states: str) -> None:
+        """ras/gpu_vram_bad_pages, one retired-page line per character of `states`
+        (R reserved, P pending, F unreservable), in amdgpu's "0x<page> : 0x<size> : S" form."""
+        lines = "".join(f"0x{0x1000 + k:08x} : 0x00001000 : {st}\n" for k, st in enumerate(states))
+        self._w(f"{self.dev_dir(gpu)}/ras/gpu_vram_bad_pages", lines)
+
+    def set_gtt(self, gpu: FakeGpu, used: int, total: int) -> None:
+        self._w(f"{self.dev_dir(gpu)}/mem_info_gtt_used", f"{used}\n")
+        self._w(f"{self.dev_dir(gpu)}/mem_info_gtt_total", f"{total}\n")
+
     def set_vram_used(self, gpu: FakeGpu, used: int) -> None:
         self._w(f"{self.dev_dir(gpu)}/mem_info_vram_used", f"{used}\n")
 

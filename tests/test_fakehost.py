@@ -268,6 +268,32 @@ def test_ras_and_aer_from_fake_sysfs(native, tmp_path):
     e2.stop()
 
 
+def test_retired_pages_and_gtt_from_fake_sysfs(native, tmp_path):
+    """full profile: the RAS bad-page table counted by state (at the RAS rate) and GTT
+    used/total per tick."""
+    h = mi355x_node(tmp_path, 1)
+    h.set_ras(h.gpus[0])
+    h.set_bad_pages(h.gpus[0], "RRRPF")
+    h.set_gtt(h.gpus[0], 3 << 30, 1024 << 30)
+    e = _engine(native, tmp_path, series_profile="full", ras_interval_s=3600.0)
+    e.tick(1 * S)
+    fams = promtext.parse(e.snapshot_text())
+    pages = {s[1]["state"]: s[2] for s in fams["amd_gpu_retired_pages"].samples}
+    assert pages == {"retired": 3, "pending": 1, "unreservable": 1}
+    assert promtext.value(fams, "amd_gpu_gtt_used_bytes", gpu=0) == 3 << 30
+    assert promtext.value(fams, "amd_gpu_gtt_total_bytes", gpu=0) == 1024 << 30
+    h.set_gtt(h.gpus[0], 5 << 30, 1024 << 30)
+    e.tick(2 * S)
+    assert promtext.value(promtext.parse(e.snapshot_text()), "amd_gpu_gtt_used_bytes", gpu=0) == 5 << 30
+    e.stop()
+
+
+def test_bad_pages_parsing(native):
+    assert native.parse_bad_pages("0x00000100 : 0x00001000 : R\n0x00000200 : 0x00001000 : P\n") == (1, 1, 0)
+    assert native.parse_bad_pages("") == (0, 0, 0)          # an empty table: nothing retired
+    assert native.parse_bad_pages("garbage\n") is None
+
+
 def _reads(fams):
     return {s[1]["kind"]: s[2] for s in fams["gpuexp_gpu_metrics_reads_total"].samples if s[1]["gpu"] == "0"}
 

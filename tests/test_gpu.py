@@ -202,6 +202,25 @@ def test_kfd_events_source_opens(native):
         e.stop()
 
 
+def test_full_profile_gtt_and_bad_pages(native):
+    """GTT used/total from mem_info_gtt_* and, where the RAS bad-page table is readable, the
+    retired HBM pages by state (a healthy board: none unreservable)."""
+    e = amdsmi_engine(native, series_profile="full")
+    try:
+        e.tick()
+        fams = promtext.parse(e.snapshot_text())
+        total = promtext.value(fams, "amd_gpu_gtt_total_bytes", gpu=0)
+        used = promtext.value(fams, "amd_gpu_gtt_used_bytes", gpu=0)
+        print("GTT used/total:", used, total)
+        assert total > 1 << 30 and 0 <= used <= total
+        pages = {s[1]["state"]: s[2] for s in promtext.samples(fams, "amd_gpu_retired_pages") if s[1]["gpu"] == "0"}
+        print("retired pages:", pages or "table not readable here")
+        if pages:
+            assert set(pages) == {"retired", "pending", "unreservable"} and pages["unreservable"] == 0, pages
+    finally:
+        e.stop()
+
+
 def test_kfd_events_real_queue_eviction():
     """A real KFD event end to end (tools/kfd_events_check.py): invalidating a host buffer
     registered with the GPU makes KFD evict and restore this process's queues; the engine
