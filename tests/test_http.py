@@ -141,6 +141,51 @@ def test_bad_request_closes(mock_engine):
     s.close()
 
 
+def _closed(s, timeout):
+    s.settimeout(timeout)
+    try:
+        return s.recv(4096) == b""
+    except ConnectionResetError:
+        return True
+
+
+def test_oversized_header_closes(mock_engine):
+    """A request head that never ends is cut off at 16 KiB: no unbounded buffering."""
+    e = mock_engine(1)
+    e.tick(1)
+    s = socket.create_connection(("127.0.0.1", e.http_port))
+    s.sendall(b"GET /metrics HTTP/1.1\r\n" + b"X-Filler: " + b"a" * 20000)
+    assert _closed(s, 3)
+    s.close()
+    r, _ = req(e.http_port, "/healthz")  # the server itself is fine
+    assert r.status == 200
+
+
+def test_idle_and_slow_clients_are_swept(native):
+    """A connection that stops mid-request (slowloris) or idles is closed after
+    idle_timeout_ms; a live keep-alive client on the same worker is unaffected."""
+    c = native.EngineConfig()
+    c.backend = "mock"
+    c.interval_s = 0
+    c.http.host = "127.0.0.1"
+    c.http.port = 0
+    c.http.idle_timeout_ms = 1000
+    e = native.Engine(c)
+    e.start()
+    try:
+        e.tick(1)
+        slow = socket.create_connection(("127.0.0.1", e.http_port))
+        slow.sendall(b"GET /metrics HTTP/1.1\r\nHost: x\r\n")  # never finished
+        idle = socket.create_connection(("127.0.0.1", e.http_port))
+        t0 = time.monotonic()
+        assert _closed(slow, 5) and _closed(idle, 5)
+        assert 0.9 < time.monotonic() - t0 < 4.0
+        r, _ = req(e.http_port, "/healthz")
+        assert r.status == 200
+    finally:
+        e.stop()
+
+
 def test_concurrent_scrapes_see_consistent_snapshots(native):
     """Sampler at 100 Hz + 4 scraper threads: every body parses and ticks never go back."""
     c = native.EngineConfig()
