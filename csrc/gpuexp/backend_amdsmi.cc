@@ -206,7 +206,10 @@ class AmdsmiBackend : public Backend {
         // xGMI peer map: static topology, so read it once (amdsmi.h:5526).
         amdsmi_link_metrics_t lm{};
         if (amdsmi_get_link_metrics(d.h, &lm) == AMDSMI_STATUS_SUCCESS) {
-          for (uint32_t l = 0; l < lm.num_links && l < uint32_t(kMaxXgmiLinks); ++l) {
+          // Every slot, not the first num_links: on MI355X num_links counts the 7 connected
+          // links while slot 0 is the unconnected one, so the 7th peer sits in slot 7
+          // (measured, tests/test_gpu.py::test_xgmi_links_carry_amdsmi_peers).
+          for (uint32_t l = 0; l < uint32_t(kMaxXgmiLinks); ++l) {
             const auto& b = lm.links[l].bdf;
             if (b.bus_number == 0xff) continue;  // unconnected slot (measured: ff:1f.7)
             char pb[32];

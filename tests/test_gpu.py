@@ -221,6 +221,54 @@ def test_full_profile_gtt_and_bad_pages(native):
         e.stop()
 
 
+def test_xgmi_links_carry_amdsmi_peers(native):
+    """Per-link xGMI series: each link's peer_bdf and byte counters agree with amdsmi's own
+    link metrics (amdsmi_get_link_metrics) for the same link, the peers are distinct other
+    GPUs of this host, and the accumulators do not run backwards."""
+    amdsmi = pytest.importorskip("amdsmi")
+    e = amdsmi_engine(native, series_profile="full")
+    try:
+        e.tick()
+        f1 = promtext.parse(e.snapshot_text())
+        amdsmi.amdsmi_init()
+        try:
+            h = amdsmi.amdsmi_get_processor_handles()[0]
+            lm = amdsmi.amdsmi_get_link_metrics(h)
+        finally:
+            amdsmi.amdsmi_shut_down()
+        time.sleep(0.2)
+        e.tick()
+        f2 = promtext.parse(e.snapshot_text())
+    finally:
+        e.stop()
+    own = promtext.samples(f1, "amd_gpu_info")[0][1]["bdf"].lower()
+    links = {s[1]["link"]: (s[1]["peer_bdf"].lower(), s[2]) for s in promtext.samples(f1, "amd_gpu_xgmi_read_bytes_total")
+             if s[1]["gpu"] == "0"}
+    later = {s[1]["link"]: s[2] for s in promtext.samples(f2, "amd_gpu_xgmi_read_bytes_total") if s[1]["gpu"] == "0"}
+    print("links:", links)
+    print("amdsmi link metrics:", lm)
+    peers = [p for p, _ in links.values() if p]
+    assert peers, links
+    # every link that carries bytes names its peer (the 7 of an 8-GPU MI355X mesh)
+    assert all(p for p, v in links.values() if v > 0), links
+    assert len(set(peers)) == len(peers) and own not in peers, (own, peers)
+    for p in peers:
+        assert os.path.isdir(f"/sys/bus/pci/devices/{p}"), p  # a real PCI function of this host
+    for k, (_, v) in links.items():
+        assert later[k] >= v, (k, v, later[k])
+    # amdsmi's per-link KB, read between our two ticks, lies between our two readings of the
+    # link it names: the link index <-> peer association is amdsmi's own
+    t1 = {p: v / 1024 for p, v in links.values() if p}
+    t2 = {links[k][0]: later[k] / 1024 for k in links if links[k][0]}
+    checked = 0
+    for l in lm.get("links", []):
+        bdf = str(l.get("bdf", "")).lower()
+        if bdf in t1 and isinstance(l.get("read"), int):
+            assert t1[bdf] <= l["read"] <= t2[bdf], (bdf, t1[bdf], l["read"], t2[bdf])
+            checked += 1
+    print("links checked against amdsmi:", checked)
+
+
 def test_kfd_events_real_queue_eviction():
     """A real KFD event end to end (tools/kfd_events_check.py): invalidating a host buffer
     registered with the GPU makes KFD evict and restore this process's queues; the engine
