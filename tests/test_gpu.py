@@ -269,6 +269,42 @@ def test_xgmi_links_carry_amdsmi_peers(native):
     print("links checked against amdsmi:", checked)
 
 
+def test_units_are_physically_consistent(native):
+    """End-to-end units: the energy counter's rate over 2 s matches the mean of the power
+    gauge sampled at 10 Hz (J vs W), VRAM used matches amdsmi's own VRAM usage, and the
+    throttle residencies are percentages."""
+    amdsmi = pytest.importorskip("amdsmi")
+    e = amdsmi_engine(native, series_profile="full")
+    try:
+        powers, t0 = [], None
+        for k in range(21):
+            e.tick()
+            fams = promtext.parse(e.snapshot_text())
+            if k == 0:
+                t0, e0 = time.monotonic(), promtext.value(fams, "amd_gpu_energy_joules_total", gpu=0)
+            powers.append(promtext.value(fams, "amd_gpu_power_watts", gpu=0))
+            time.sleep(0.1)
+        t1, e1 = time.monotonic(), promtext.value(fams, "amd_gpu_energy_joules_total", gpu=0)
+        vram = promtext.value(fams, "amd_gpu_vram_used_bytes", gpu=0)
+        thr = [s[2] for s in promtext.samples(fams, "amd_gpu_throttle_residency_percent") if s[1]["gpu"] == "0"]
+        amdsmi.amdsmi_init()
+        try:
+            h = amdsmi.amdsmi_get_processor_handles()[0]
+            usage = amdsmi.amdsmi_get_gpu_vram_usage(h)
+        finally:
+            amdsmi.amdsmi_shut_down()
+    finally:
+        e.stop()
+    rate = (e1 - e0) / (t1 - t0)
+    mean_p = sum(powers) / len(powers)
+    print(f"energy rate {rate:.1f} W vs mean power gauge {mean_p:.1f} W; vram {vram / 2**20:.0f} MiB vs amdsmi {usage}")
+    assert 0.75 * mean_p < rate < 1.25 * mean_p, (rate, mean_p)
+    used_mb = usage.get("vram_used") if isinstance(usage, dict) else None
+    if isinstance(used_mb, (int, float)):
+        assert abs(vram / 2**20 - used_mb) < max(256, 0.02 * used_mb), (vram, used_mb)
+    assert all(0 <= v <= 100 for v in thr), thr
+
+
 def test_kfd_events_real_queue_eviction():
     """A real KFD event end to end (tools/kfd_events_check.py): invalidating a host buffer
     registered with the GPU makes KFD evict and restore this process's queues; the engine
