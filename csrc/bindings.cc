@@ -149,6 +149,11 @@ PYBIND11_MODULE(_gpuexp, m) {
     return s;
   });
   m.def("gzip_impl", []() { return std::string(gzip_impl()); });
+  m.def("xgmi_peers_from_sysfs", [](const std::string& root, const std::string& bdf) {
+    std::string peers[gpuexp::kMaxXgmiLinks];
+    gpuexp::xgmi_peers_from_sysfs(root, bdf, peers);
+    return std::vector<std::string>(std::begin(peers), std::end(peers));
+  }, "xGMI link index -> peer BDF from amdgpu's xgmi_port_num files ('' = no link)");
   m.def("parse_bad_pages", [](const std::string& body) -> py::object {
     gpuexp::RasTotals t;
     if (!gpuexp::parse_bad_pages(body, &t)) return py::none();

@@ -218,6 +218,9 @@ class AmdsmiBackend : public Backend {
             info.xgmi_peer_bdf[l] = pb;
           }
         }
+        bool any_peer = false;
+        for (const auto& pb : info.xgmi_peer_bdf) any_peer = any_peer || !pb.empty();
+        if (!any_peer) xgmi_peers_from_sysfs(root_, info.bdf, info.xgmi_peer_bdf);  // amdgpu's own port map
         info.index = int(devs_.size());
         info.dev_node = render_dev_node(root_, info.render_minor, info.bdf);
         if (info.render_minor >= 0) {

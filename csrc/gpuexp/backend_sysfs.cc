@@ -8,6 +8,7 @@
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
 #include <sstream>
 
 #include "gpuexp/backends.h"
@@ -77,6 +78,44 @@ std::string render_dev_node(const std::string& root, int render_minor, const std
   const bool pci = base.size() == 12 && base[4] == ':' && base[7] == ':' && base[10] == '.';
   const bool xcp = base.compare(0, 11, "amdgpu_xcp.") == 0 || base.compare(0, 11, "amdgpu_xcp_") == 0;
   return pci || xcp ? base : bdf;
+}
+
+namespace {
+// One xgmi_port_num line: "<node>:<port> ->  <peer node>:<peer port>" (hex, node ids from 1,
+// shared by every GPU of the hive; amdgpu_xgmi.c).
+bool parse_port_line(const std::string& line, unsigned* node, unsigned* port, unsigned* peer) {
+  unsigned pp = 0;
+  return std::sscanf(line.c_str(), " %x:%x -> %x:%x", node, port, peer, &pp) == 4;
+}
+}  // namespace
+
+int xgmi_peers_from_sysfs(const std::string& root, const std::string& bdf, std::string peers[kMaxXgmiLinks]) {
+  // node id -> BDF, from the first line of every GPU's own listing
+  std::map<unsigned, std::string> node_bdf;
+  const std::string pci = root + "/sys/bus/pci/devices";
+  std::string body;
+  for (const std::string& dev : list_dir(pci)) {
+    if (!read_small_file(pci + "/" + dev + "/xgmi_port_num", &body)) continue;
+    unsigned node = 0, port = 0, peer = 0;
+    if (parse_port_line(body.substr(0, body.find('\n')), &node, &port, &peer)) node_bdf[node] = dev;
+  }
+  if (!read_small_file(pci + "/" + bdf + "/xgmi_port_num", &body)) return 0;
+  int n = 0;
+  size_t pos = 0;
+  while (pos < body.size()) {
+    size_t eol = body.find('\n', pos);
+    if (eol == std::string::npos) eol = body.size();
+    unsigned node = 0, port = 0, peer = 0;
+    if (parse_port_line(body.substr(pos, eol - pos), &node, &port, &peer) && port < unsigned(kMaxXgmiLinks)) {
+      auto it = node_bdf.find(peer);
+      if (it != node_bdf.end()) {
+        peers[port] = it->second;
+        ++n;
+      }
+    }
+    pos = eol + 1;
+  }
+  return n;
 }
 
 std::vector<std::string> device_owner_keys(const DeviceInfo& d) {
@@ -183,6 +222,7 @@ bool SysfsBackend::init(std::vector<DeviceInfo>* devices, std::string* err) {
     dev->nxcc = int(d.num_xcc);
     uint64_t total = 0;
     if (read_u64_file(dev->dev_dir + "/mem_info_vram_total", &total)) d.vram_total = total;
+    xgmi_peers_from_sysfs(root_, d.bdf, d.xgmi_peer_bdf);
     open_dev_files(dev.get());
     devices->push_back(d);
     devs_.push_back(std::move(dev));

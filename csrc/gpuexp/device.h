@@ -60,6 +60,13 @@ std::string render_dev_node(const std::string& root, int render_minor, const std
 // bare BDF never names the other partitions of a socket.
 std::vector<std::string> device_owner_keys(const DeviceInfo& d);
 
+// xGMI link index -> peer GPU PCI BDF for the GPU at `bdf`, from amdgpu's per-device
+// xgmi_port_num listings under <root>/sys/bus/pci/devices ("<node>:<port> ->  <peer
+// node>:<peer port>" per link; node ids shared across the hive).  gpu_metrics's
+// xgmi_*_data_acc[l] is source port l (checked against amdsmi_get_link_metrics on MI355X).
+// Fills peers[port]; returns how many links resolved.
+int xgmi_peers_from_sysfs(const std::string& root, const std::string& bdf, std::string peers[kMaxXgmiLinks]);
+
 // One tick of device telemetry.  NaN = unsupported/unavailable; raw accumulators are
 // kept as integers so deltas are exact across wraps.
 struct DeviceSample {

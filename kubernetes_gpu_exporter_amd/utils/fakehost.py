@@ -157,6 +157,23 @@ class FakeHost:
         for n, k, v in zip(names, keys, aer):
             self._w(f"{dev}/aer_dev_{n}", f"RxErr 0\nBadTLP 0\n{k} {v}\n")
 
+    def set_xgmi_ports(self) -> dict:
+        """amdgpu's xgmi_port_num for every socket (one per distinct BDF) of the hive, in the
+        kernel's "<node>:<port> ->  <peer node>:<peer port>" form: node ids 1..n in GPU order,
+        socket i's port p (1..n-1) wired to socket (i + p) % n.  Returns {bdf: {port: peer bdf}}."""
+        bdfs = list(dict.fromkeys(self._bdf(g) for g in self.gpus))
+        n = len(bdfs)
+        wiring = {}
+        for i, b in enumerate(bdfs):
+            lines, ports = [], {}
+            for p in range(1, n):
+                j = (i + p) % n
+                lines.append(f"{i + 1:02x}:{p:02x} ->  {j + 1:02x}:{n - p:02x}\n")
+                ports[p] = bdfs[j]
+            self._w(f"sys/bus/pci/devices/{b}/xgmi_port_num", "".join(lines))
+            wiring[b] = ports
+        return wiring
+
     def set_bad_pages(self, gpu: FakeGpu, states: str) -> None:
         """ras/gpu_vram_bad_pages, one retired-page line per character of `states`
         (R reserved, P pending, F unreservable), in amdgpu's "0x<page> : 0x<size> : S" form."""

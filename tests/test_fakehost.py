@@ -288,6 +288,26 @@ def test_retired_pages_and_gtt_from_fake_sysfs(native, tmp_path):
     e.stop()
 
 
+def test_xgmi_peers_from_port_listings(native, tmp_path):
+    """The sysfs backend names each xGMI link's peer from amdgpu's xgmi_port_num files:
+    link index = source port, peer node id -> that GPU's BDF."""
+    h = mi355x_node(tmp_path, 8)
+    wiring = h.set_xgmi_ports()
+    b0 = h._bdf(h.gpus[0])
+    peers = native.xgmi_peers_from_sysfs(str(tmp_path), b0)
+    assert peers[0] == "" and {p: peers[p] for p in range(1, 8)} == wiring[b0]
+    assert len(set(peers[1:])) == 7 and b0 not in peers
+    e = _engine(native, tmp_path, series_profile="standard")
+    e.tick(1 * S)
+    fams = promtext.parse(e.snapshot_text())
+    got = {}
+    for _, lab, _ in promtext.samples(fams, "amd_gpu_xgmi_read_bytes_total"):
+        if lab["bdf"] == b0:
+            got[int(lab["link"])] = lab["peer_bdf"]
+    assert got and all(got[p] == wiring[b0][p] for p in got), (got, wiring[b0])
+    e.stop()
+
+
 def test_bad_pages_parsing(native):
     assert native.parse_bad_pages("0x00000100 : 0x00001000 : R\n0x00000200 : 0x00001000 : P\n") == (1, 1, 0)
     assert native.parse_bad_pages("") == (0, 0, 0)          # an empty table: nothing retired

@@ -267,6 +267,14 @@ def test_xgmi_links_carry_amdsmi_peers(native):
             assert t1[bdf] <= l["read"] <= t2[bdf], (bdf, t1[bdf], l["read"], t2[bdf])
             checked += 1
     print("links checked against amdsmi:", checked)
+    # amdgpu's own port map (what the sysfs-only backend uses): slot l of amdsmi's link list
+    # is source port l of xgmi_port_num
+    sys_peers = native.xgmi_peers_from_sysfs("", own)
+    print("sysfs port map:", sys_peers)
+    smi = [str(l.get("bdf", "")).lower() for l in lm.get("links", [])]
+    for l, b in enumerate(smi[:8]):
+        if b and not b.startswith("ffff"):
+            assert sys_peers[l] == b, (l, b, sys_peers)
 
 
 def test_units_are_physically_consistent(native):
