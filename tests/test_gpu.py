@@ -313,6 +313,36 @@ def test_units_are_physically_consistent(native):
     assert all(0 <= v <= 100 for v in thr), thr
 
 
+def test_xcc_busy_agrees_with_gfx_activity_under_gemm(native):
+    """Per-XCD busy (the exporter's own gfx_busy_acc deltas) against the PMFW's
+    average_gfx_activity while a GEMM pod saturates the GPU: both near 100 %, and their
+    means within 15 points of each other; the gauges stay in 0-100."""
+    child = subprocess.Popen([sys.executable, "-c",
+                              "import sys; sys.path.insert(0, %r);"
+                              "from kubernetes_gpu_exporter_amd.ops.gemm import gemm_burn;"
+                              "print(gemm_burn(0, 8192, 5.0, 4), flush=True)" % ROOT],
+                             stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    e = amdsmi_engine(native, series_profile="full")
+    try:
+        time.sleep(2.0)  # the burn is up (torch import + warm-up)
+        gfx, xcc = [], []
+        for _ in range(15):
+            e.tick()
+            fams = promtext.parse(e.snapshot_text())
+            gfx.append(promtext.value(fams, "amd_gpu_gfx_activity_percent", gpu=0))
+            xcc.extend(s[2] for s in promtext.samples(fams, "amd_gpu_xcc_busy_percent") if s[1]["gpu"] == "0")
+            time.sleep(0.1)
+    finally:
+        e.stop()
+        out, _ = child.communicate(timeout=60)
+    print("gemm:", out.strip()[-300:])
+    mg, mx = sum(gfx) / len(gfx), sum(xcc) / max(1, len(xcc))
+    print(f"gfx_activity mean {mg:.1f} %, per-XCD busy mean {mx:.1f} % over {len(xcc)} samples")
+    assert xcc and all(0 <= v <= 100.5 for v in xcc), xcc
+    assert mg > 60 and mx > 60, (mg, mx)
+    assert abs(mg - mx) < 15, (mg, mx)
+
+
 def test_kfd_events_real_queue_eviction():
     """A real KFD event end to end (tools/kfd_events_check.py): invalidating a host buffer
     registered with the GPU makes KFD evict and restore this process's queues; the engine
