@@ -701,7 +701,7 @@ def main() -> int:
             "scrapes": len(lat),
             "scrape_errors": client.errors,
             "scrape_bytes": client.last_bytes,
-            "series_per_gpu": {k: v for k, v in sorted(per_gpu.items()) if k is not None},
+            "series_per_gpu": dict(sorted((k, v) for k, v in per_gpu.items() if k is not None)),
             "attributed_pods": sorted(attributed),
             "gpu_gfx_activity_percent": gfx,
             "sentinel": sentinel,

@@ -445,6 +445,7 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("rccl_dir", &EngineConfig::rccl_dir)
       .def_readwrite("rccl_verify", &EngineConfig::rccl_verify)
       .def_readwrite("enable_kfd_events", &EngineConfig::enable_kfd_events)
+      .def_readwrite("firmware_info", &EngineConfig::firmware_info)
       .def_readwrite("kfd_path", &EngineConfig::kfd_path)
       .def_readwrite("metrics_min_interval_s", &EngineConfig::metrics_min_interval_s)
       .def_readwrite("queue_devices", &EngineConfig::queue_devices)

@@ -223,6 +223,7 @@ class AmdsmiBackend : public Backend {
         if (!any_peer) xgmi_peers_from_sysfs(root_, info.bdf, info.xgmi_peer_bdf);  // amdgpu's own port map
         info.index = int(devs_.size());
         info.dev_node = render_dev_node(root_, info.render_minor, info.bdf);
+        read_board_info(root_, &info);
         if (info.render_minor >= 0) {
           std::string dir = root_ + "/sys/class/drm/renderD" + std::to_string(info.render_minor) + "/device";
           // partitions >= 1 sit on an XCP platform device: socket files are on the PCI function

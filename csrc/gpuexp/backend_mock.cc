@@ -27,6 +27,12 @@ bool MockBackend::init(std::vector<DeviceInfo>* devices, std::string* err) {
     std::snprintf(buf, sizeof(buf), "e2ff75a3-0000-1000-80%02x-00000000%04x", i, 0xa000 + i);
     d.uuid = buf;
     d.name = "AMD Instinct MI355X (mock)";
+    d.vbios_version = "113-M3550100-100";
+    d.product_name = "AMD Instinct MI355X";
+    d.product_number = "102-M3550-00";
+    std::snprintf(buf, sizeof(buf), "MOCK%08d", i);
+    d.serial_number = buf;
+    d.firmware = {{"mec", "0x0000009f"}, {"rlc", "0x00000036"}, {"smc", "0x00554500"}, {"sos", "0x00360054"}};
     d.kfd_gpu_id = kfd_base_ + uint32_t(i);
     d.render_minor = 128 + i;
     d.card = i;

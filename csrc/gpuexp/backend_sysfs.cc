@@ -118,6 +118,30 @@ int xgmi_peers_from_sysfs(const std::string& root, const std::string& bdf, std::
   return n;
 }
 
+void read_board_info(const std::string& root, DeviceInfo* d) {
+  const std::string dir = root + "/sys/bus/pci/devices/" + d->bdf;
+  auto rd = [&](const char* f) {
+    std::string v;
+    return read_small_file(dir + "/" + f, &v, 256) ? trim(v) : std::string();
+  };
+  d->vbios_version = rd("vbios_version");
+  d->product_name = rd("product_name");
+  d->product_number = rd("product_number");
+  d->serial_number = rd("serial_number");
+  d->firmware.clear();
+  const std::string suffix = "_fw_version";
+  std::vector<std::string> files = list_dir(dir + "/fw_version");
+  std::sort(files.begin(), files.end());
+  for (const std::string& f : files) {
+    if (f.size() <= suffix.size() || f.compare(f.size() - suffix.size(), suffix.size(), suffix) != 0) continue;
+    std::string v;
+    if (!read_small_file(dir + "/fw_version/" + f, &v, 64)) continue;
+    v = trim(v);
+    if (v.empty() || v == "0x00000000") continue;  // block not loaded on this ASIC
+    d->firmware.emplace_back(f.substr(0, f.size() - suffix.size()), v);
+  }
+}
+
 std::vector<std::string> device_owner_keys(const DeviceInfo& d) {
   auto low = [](std::string s) {
     for (auto& c : s) c = char(::tolower(static_cast<unsigned char>(c)));
@@ -212,6 +236,7 @@ bool SysfsBackend::init(std::vector<DeviceInfo>* devices, std::string* err) {
     if (read_small_file(dev->dev_dir + "/current_compute_partition", &part)) d.compute_partition = trim(part);
     if (read_small_file(dev->dev_dir + "/current_memory_partition", &part)) d.memory_partition = trim(part);
     d.dev_node = render_dev_node(root_, d.render_minor, d.bdf);
+    read_board_info(root_, &d);
     // Socket-level files (gpu_metrics, mem_info_*, hwmon) live on the PCI function; an
     // XCP platform device (partitions >= 1) may not carry them.
     if (d.dev_node != d.bdf && !file_exists(dev->dev_dir + "/gpu_metrics")) {

@@ -10,6 +10,7 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "gpuexp/common.h"
@@ -44,6 +45,9 @@ struct DeviceInfo {
   // BDF is not (see device_owner_keys).
   std::string dev_node;
   std::string xgmi_peer_bdf[kMaxXgmiLinks];  // from amdsmi_get_link_metrics (once)
+  // Board identity and firmware (amdgpu sysfs on the PCI function, read once; "" = n/a)
+  std::string vbios_version, product_name, product_number, serial_number;
+  std::vector<std::pair<std::string, std::string>> firmware;  // (component, version), fw_version/*_fw_version
   // false: no exporter-owned GPU queue on this device (no sentinel, no PMC counters); each
   // queue pins ~346 MiB of host memory on MI355X (profiles/r02/queue_memory.txt)
   bool queue_enabled = true;
@@ -66,6 +70,11 @@ std::vector<std::string> device_owner_keys(const DeviceInfo& d);
 // xgmi_*_data_acc[l] is source port l (checked against amdsmi_get_link_metrics on MI355X).
 // Fills peers[port]; returns how many links resolved.
 int xgmi_peers_from_sysfs(const std::string& root, const std::string& bdf, std::string peers[kMaxXgmiLinks]);
+
+// Fills d->vbios_version / product_* / serial_number / firmware from <root>/sys/bus/pci/
+// devices/<bdf> (vbios_version, product_name, product_number, serial_number and
+// fw_version/<component>_fw_version).  Missing or unreadable files stay empty.
+void read_board_info(const std::string& root, DeviceInfo* d);
 
 // One tick of device telemetry.  NaN = unsupported/unavailable; raw accumulators are
 // kept as integers so deltas are exact across wraps.

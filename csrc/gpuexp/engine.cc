@@ -3,6 +3,7 @@
 #include <sys/eventfd.h>
 #include <sys/poll.h>
 #include <sys/timerfd.h>
+#include <sys/utsname.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -241,6 +242,13 @@ void Engine::define_families() {
   f_rccl_comm_ = add("amd_rccl_communicator_info",
                      "Rank and size of the largest RCCL communicator of a process (value is always 1)", G,
                      {"namespace", "pod", "pid", "rank", "nranks"});
+  f_board_ = add("amd_gpu_board_info", "Board identity: product, serial number, VBIOS (value is always 1; full profile)",
+                 G, {"gpu", "bdf", "product_name", "product_number", "serial_number", "vbios_version"});
+  f_fw_ = add("amd_gpu_firmware_info",
+              "Loaded firmware versions by component, from amdgpu fw_version/ (value is always 1; full profile)", G,
+              {"gpu", "bdf", "component", "version"});
+  f_driver_ = add("amd_driver_info", "amdgpu driver and kernel release of the node (value is always 1; full profile)", G,
+                  {"version", "kernel"});
   f_pages_ = add("amd_gpu_retired_pages",
                  "HBM pages in the RAS bad-page table by state: retired (never handed out again), pending, "
                  "unreservable (ras/gpu_vram_bad_pages; full profile)",
@@ -454,6 +462,14 @@ bool Engine::start(std::string* err) {
     sentinel_status_ = "mock";
   }
   if (cfg_.enable_rccl) rccl_ = make_rccl_source(cfg_.rccl_dir, cfg_.rccl_verify);
+  {
+    std::string v;
+    driver_version_ = read_small_file((cfg_.host_root.empty() ? "" : cfg_.host_root) + "/sys/module/amdgpu/version", &v, 128)
+                          ? trim(v)
+                          : (mock_ ? "mock" : "in-kernel");  // DKMS builds carry a version file
+    struct utsname u{};
+    kernel_release_ = ::uname(&u) == 0 ? u.release : "";
+  }
   if (cfg_.enable_kfd_events && cfg_.series_profile == "full") {
     kfd_events_ = std::make_unique<KfdEventSource>();
     if (mock_) {
@@ -666,6 +682,19 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
     table_.set(st.info, 1, gen);
   }
   dput(st, i, st.up, f_up_, {}, c.ok ? 1 : 0, gen);
+  if (cfg_.series_profile == "full") {
+    cput(st.board, f_board_, 1, gen, [&] {
+      return std::vector<std::string>{std::to_string(d.index), d.bdf, d.product_name, d.product_number,
+                                      d.serial_number, d.vbios_version};
+    });
+    if (cfg_.firmware_info) {
+      st.fw.resize(d.firmware.size());
+      for (size_t k = 0; k < d.firmware.size(); ++k)
+        cput(st.fw[k], f_fw_, 1, gen, [&] {
+          return std::vector<std::string>{std::to_string(d.index), d.bdf, d.firmware[k].first, d.firmware[k].second};
+        });
+    }
+  }
   if (!table_.set(st.err_ref, double(st.errors), gen)) {
     st.err_ref = table_.upsert(f_self_dev_errors_, {std::to_string(d.index)});
     table_.set(st.err_ref, double(st.errors), gen);
@@ -1111,6 +1140,8 @@ void Engine::emit_self(uint64_t gen) {
   if (cfg_.enable_kfd_events && cfg_.series_profile == "full")
     cput(self_refs_[18], f_self_source_up_, kfd_events_ ? 1 : 0, gen,
          [] { return std::vector<std::string>{"kfd_events"}; });
+  if (cfg_.series_profile == "full")
+    cput(self_refs_[20], f_driver_, 1, gen, [&] { return std::vector<std::string>{driver_version_, kernel_release_}; });
   if (rccl_) {
     int a = 0, u = 0, x = 0;
     rccl_->file_states(&a, &u, &x);

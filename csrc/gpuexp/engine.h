@@ -90,6 +90,7 @@ struct EngineConfig {
   std::string rccl_dir = "/dev/shm";
   bool rccl_verify = true;             // attribute a tracer file only to a process that maps it
   bool enable_kfd_events = true;       // full profile: KFD SMI events (VM faults, resets, ...)
+  bool firmware_info = true;           // full profile: amd_gpu_firmware_info (one series per loaded firmware)
   std::string kfd_path = "/dev/kfd";   // the device node itself (not under host_root)
   bool force_amdsmi_metrics = false;
   int gzip_level = 1;
@@ -181,7 +182,8 @@ class Engine {
         energy, temp[9], clk[3], xrd[kMaxXgmiLinks], xwr[kMaxXgmiLinks], xrd_rate, xwr_rate,
         links_up, pcie_bw, pcie_replay, pcie_speed, pcie_width, thr[5], nprocs, cu_occ, ctr[10],
         sen[4], ecc[3], aer[3], nak[2], recov, xgmi_w, xgmi_s, xclk[kMaxXcc], sen_xlat[kMaxXcc], sen_mem, sen_xmem[kMaxXcc],
-        kev[std::size(kKfdSubscribed)], pages[3], gtt_used, gtt_total;
+        kev[std::size(kKfdSubscribed)], pages[3], gtt_used, gtt_total, board;
+    std::vector<SeriesRef> fw;  // amd_gpu_firmware_info, one per component
     uint64_t kfd_events[kKfdEventIds] = {};  // KFD SMI events seen on this GPU, by id
     uint64_t errors = 0;
     SeriesRef err_ref;
@@ -278,7 +280,7 @@ class Engine {
   std::unordered_map<uint64_t, ProcRefs> proc_refs_;               // (device << 32 | pid) -> handles
   std::unordered_map<uint64_t, ProcRefs> legacy_refs_;             // pid -> legacy handles (pod, vram, gfx=perc)
   std::map<std::pair<std::string, std::string>, PodRefs> pod_refs_;  // (ns, pod) -> handles
-  SeriesRef self_refs_[20];
+  SeriesRef self_refs_[21];
 
   // stats (guarded by stats_mu_)
   std::mutex stats_mu_;
@@ -300,6 +302,8 @@ class Engine {
   int f_pod_vram_, f_pod_procs_, f_pod_gpus_, f_pod_xrd_, f_pod_xwr_, f_pod_power_, f_pod_gfx_, f_pod_gfx_share_;
   int f_rccl_calls_, f_rccl_bytes_, f_rccl_comm_;
   int f_kfd_ev_ = -1, f_pod_kfd_ev_ = -1, f_pages_ = -1, f_gtt_used_ = -1, f_gtt_total_ = -1;
+  int f_board_ = -1, f_fw_ = -1, f_driver_ = -1;
+  std::string driver_version_, kernel_release_;
   int f_self_build_, f_self_ticks_, f_self_last_, f_self_stage_, f_self_scrape_, f_self_scrapes_,
       f_self_http_bytes_, f_self_render_bytes_, f_self_series_, f_self_dev_errors_,
       f_self_overruns_, f_self_cpu_, f_self_source_up_, f_self_ctr_scope_, f_self_metrics_reads_, f_self_metrics_period_, f_self_prewake_, f_self_gzip_,

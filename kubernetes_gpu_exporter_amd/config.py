@@ -55,6 +55,7 @@ class Config:
                                            # own GPU queue (sentinel + PMC counters); empty = all.
                                            # Each queue pins ~346 MiB of host memory on MI355X.
     enable_kfd_events: bool = True         # full profile: KFD SMI events (VM faults, resets, evictions)
+    firmware_info: bool = True             # full profile: amd_gpu_firmware_info per loaded firmware
     kfd_path: str = "/dev/kfd"             # the device node (mounted directly, not under host_root)
     enable_rccl: bool = False
     rccl_dir: str = "/var/run/gpuexp/rccl"
@@ -148,6 +149,7 @@ class Config:
         ec.rccl_dir = self.rccl_dir
         ec.rccl_verify = bool(self.rccl_verify)
         ec.enable_kfd_events = bool(self.enable_kfd_events)
+        ec.firmware_info = bool(self.firmware_info)
         ec.kfd_path = self.kfd_path
         ec.gc_after = int(self.gc_after)
         ec.device_filter = [int(d) for d in self.devices if ":" not in str(d)]

@@ -174,6 +174,17 @@ class FakeHost:
             wiring[b] = ports
         return wiring
 
+    def set_board(self, gpu: FakeGpu, serial: str = "PV0A1B2C3D", firmware: dict | None = None) -> None:
+        """Board identity (vbios_version, product_name/_number, serial_number) and
+        fw_version/<component>_fw_version on the PCI function."""
+        b = f"sys/bus/pci/devices/{self._bdf(gpu)}"
+        self._w(f"{b}/vbios_version", "113-M3550100-100\n")
+        self._w(f"{b}/product_name", "AMD Instinct MI355X\n")
+        self._w(f"{b}/product_number", "102-M3550-00\n")
+        self._w(f"{b}/serial_number", f"{serial}\n")
+        for comp, ver in (firmware or {"mec": "0x0000009f", "smc": "0x00554500", "vcn": "0x00000000"}).items():
+            self._w(f"{b}/fw_version/{comp}_fw_version", f"{ver}\n")
+
     def set_bad_pages(self, gpu: FakeGpu, states: str) -> None:
         """ras/gpu_vram_bad_pages, one retired-page line per character of `states`
         (R reserved, P pending, F unreservable), in amdgpu's "0x<page> : 0x<size> : S" form."""

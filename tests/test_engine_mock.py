@@ -248,13 +248,14 @@ def test_sampler_thread_runs(native):
 def test_full_profile_adds_reliability_families(mock_engine):
     """`full` = the 64-series standard load + ECC / PCIe AER / NAK / recovery / xGMI link
     + per-XCD clocks, per-XCD sentinel dispatch latency and HBM latency (chip + 8 XCDs)
-    + the 6 KFD SMI event counters + retired HBM pages by state + GTT used/total."""
+    + the 6 KFD SMI event counters + retired HBM pages by state + GTT used/total + board
+    identity and firmware versions."""
     e = mock_engine(2, http=False, enable_sentinel=True, enable_counters=True, series_profile="full")
     e.mock_set_value(1, "ecc_ue", 3)
     e.mock_set_value(1, "aer_cor", 7)
     ticks(e, 3)
     fams = parse(e)
-    assert dict(device_series_per_gpu(fams)) == {"0": 112, "1": 112}  # + retired pages (3), GTT (2)
+    assert dict(device_series_per_gpu(fams)) == {"0": 117, "1": 117}  # + board (1), firmware (4 in mock)
     lat = {s[1]["xcc"]: s[2] for s in fams["amd_gpu_sentinel_xcc_dispatch_latency_seconds"].samples
            if s[1]["gpu"] == "0"}
     assert sorted(lat) == [str(x) for x in range(8)] and min(lat.values()) == lat["0"]

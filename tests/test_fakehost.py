@@ -308,6 +308,27 @@ def test_xgmi_peers_from_port_listings(native, tmp_path):
     e.stop()
 
 
+def test_board_and_firmware_info(native, tmp_path):
+    """full profile: board identity and the loaded firmware versions from amdgpu sysfs
+    (a block reporting 0x00000000 is not loaded and is skipped), once per GPU."""
+    h = mi355x_node(tmp_path, 2)
+    h.set_board(h.gpus[0], serial="PV0A1B2C3D")
+    e = _engine(native, tmp_path, series_profile="full")
+    e.tick(1 * S)
+    fams = promtext.parse(e.snapshot_text())
+    b0 = h._bdf(h.gpus[0])
+    board = [lab for _, lab, _ in promtext.samples(fams, "amd_gpu_board_info") if lab["bdf"] == b0]
+    assert board and board[0]["serial_number"] == "PV0A1B2C3D" and board[0]["vbios_version"] == "113-M3550100-100"
+    fw = {lab["component"]: lab["version"] for _, lab, _ in promtext.samples(fams, "amd_gpu_firmware_info")
+          if lab["bdf"] == b0}
+    assert fw == {"mec": "0x0000009f", "smc": "0x00554500"}
+    e.stop()
+    e2 = _engine(native, tmp_path, series_profile="full", firmware_info=False)
+    e2.tick(1 * S)
+    assert not promtext.samples(promtext.parse(e2.snapshot_text()), "amd_gpu_firmware_info")
+    e2.stop()
+
+
 def test_bad_pages_parsing(native):
     assert native.parse_bad_pages("0x00000100 : 0x00001000 : R\n0x00000200 : 0x00001000 : P\n") == (1, 1, 0)
     assert native.parse_bad_pages("") == (0, 0, 0)          # an empty table: nothing retired

@@ -203,8 +203,9 @@ def test_kfd_events_source_opens(native):
 
 
 def test_full_profile_gtt_and_bad_pages(native):
-    """GTT used/total from mem_info_gtt_* and, where the RAS bad-page table is readable, the
-    retired HBM pages by state (a healthy board: none unreservable)."""
+    """GTT used/total from mem_info_gtt_*, board identity and loaded firmware versions, and,
+    where the RAS bad-page table is readable, the retired HBM pages by state (a healthy
+    board: none unreservable)."""
     e = amdsmi_engine(native, series_profile="full")
     try:
         e.tick()
@@ -213,6 +214,14 @@ def test_full_profile_gtt_and_bad_pages(native):
         used = promtext.value(fams, "amd_gpu_gtt_used_bytes", gpu=0)
         print("GTT used/total:", used, total)
         assert total > 1 << 30 and 0 <= used <= total
+        board = [lab for _, lab, _ in promtext.samples(fams, "amd_gpu_board_info") if lab["gpu"] == "0"]
+        fw = {lab["component"]: lab["version"] for _, lab, _ in promtext.samples(fams, "amd_gpu_firmware_info")
+              if lab["gpu"] == "0"}
+        drv = [lab for _, lab, _ in promtext.samples(fams, "amd_driver_info")]
+        print("board:", board, "\nfirmware:", fw, "\ndriver:", drv)
+        assert board and board[0]["vbios_version"], board
+        assert len(fw) >= 3 and all(v.startswith("0x") for v in fw.values()), fw
+        assert drv and drv[0]["kernel"], drv
         pages = {s[1]["state"]: s[2] for s in promtext.samples(fams, "amd_gpu_retired_pages") if s[1]["gpu"] == "0"}
         print("retired pages:", pages or "table not readable here")
         if pages:
