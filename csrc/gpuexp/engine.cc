@@ -231,6 +231,9 @@ void Engine::define_families() {
   f_pod_xrd_ = add("amd_pod_xgmi_read_bytes_per_second", "xGMI receive rate of the pod's GPUs", G, PO);
   f_pod_xwr_ = add("amd_pod_xgmi_write_bytes_per_second", "xGMI transmit rate of the pod's GPUs", G, PO);
   f_pod_power_ = add("amd_pod_gpu_power_watts", "Socket power of the pod's GPUs", G, PO);
+  f_pod_energy_ = add("amd_pod_gpu_energy_joules_total",
+                      "GPU energy used by the pod: its GPUs' hardware energy counters, and on a shared GPU the "
+                      "pod's CU-occupancy share of it (chargeback)", C, PO);
   f_pod_gfx_ = add("amd_pod_gpu_gfx_activity_percent", "Mean gfx activity of the pod's GPUs", G, PO);
   f_pod_gfx_share_ = add("amd_pod_gfx_activity_share_percent",
                          "GPU gfx activity of the pod's processes summed over GPUs, in percent of one GPU "
@@ -919,6 +922,7 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
     std::set<int> pids;
     int gpus = 0;
     double xrd = 0, xwr = 0, power = 0, gfx = 0, gfx_share = 0;
+    double energy_j = 0;  // this tick
     int gfx_n = 0;
     bool share_known = false;
   };
@@ -941,12 +945,21 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
     // of it, and with no waves resident at the CU sample the split is even.
     const double act = st.cur.ok ? st.cur.gfx_activity : std::nan("");
     const size_t nproc = per_dev[di].size();
-    auto gfx_share = [&](const ProcSample& p) -> double {
-      if (std::isnan(act) || nproc == 0) return std::nan("");
-      if (nproc == 1) return act;
-      if (cu_any && cu_sum > 0) return std::isnan(p.cu_occupancy) ? std::nan("") : act * p.cu_occupancy / cu_sum;
-      return act / double(nproc);
+    // a process's fraction of the GPU: its share of the occupied CUs (see above)
+    auto frac = [&](const ProcSample& p) -> double {
+      if (nproc == 0) return std::nan("");
+      if (nproc == 1) return 1.0;
+      if (cu_any && cu_sum > 0) return std::isnan(p.cu_occupancy) ? std::nan("") : p.cu_occupancy / cu_sum;
+      return 1.0 / double(nproc);
     };
+    auto gfx_share = [&](const ProcSample& p) -> double { return std::isnan(act) ? act : act * frac(p); };
+    // energy this GPU used since the last tick, from its hardware accumulator (exact)
+    double energy_j = std::nan("");
+    if (st.cur.ok && st.have_prev && st.cur.energy_valid && st.prev.energy_valid) {
+      double dacc;
+      if (acc_delta(st.cur.energy_acc, st.prev.energy_acc, &dacc)) energy_j = dacc * st.cur.energy_unit_j;
+    }
+    const bool shared = st.owner.pod.empty();
     for (auto& p : per_dev[di]) {
       const ProcAttr& a = attr[p.pid];
       const double share = gfx_share(p);
@@ -978,6 +991,8 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
         auto& pa = pods[{a.ns, a.pod}];
         pa.vram += p.vram_bytes;
         pa.pids.insert(p.pid);
+        const double f = frac(p);
+        if (shared && !std::isnan(energy_j) && !std::isnan(f)) pa.energy_j += energy_j * f;
         if (!std::isnan(share)) {
           pa.gfx_share += share;
           pa.share_known = true;
@@ -999,6 +1014,7 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
             pa.xwr += st.xgmi_wr_rate[l];
           }
         if (!std::isnan(st.cur.power_w)) pa.power += st.cur.power_w;
+        if (!std::isnan(energy_j)) pa.energy_j += energy_j;  // an owned GPU's energy is all the pod's
         if (!std::isnan(st.cur.gfx_activity)) {
           pa.gfx += st.cur.gfx_activity;
           pa.gfx_n += 1;
@@ -1044,6 +1060,22 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
   }
   for (auto it = pod_refs_.begin(); it != pod_refs_.end();)
     it = it->second.gen != gen ? pod_refs_.erase(it) : std::next(it);
+  // Energy per pod: a counter that lives as long as the control plane knows the pod, so a
+  // pod between GPU processes keeps its total.
+  for (auto& kv : pods)
+    if (kv.second.energy_j > 0) pod_energy_j_[kv.first] += kv.second.energy_j;
+  {
+    std::set<std::pair<std::string, std::string>> known;
+    for (auto& kv : pods_by_uid_) known.emplace(kv.second.ns, kv.second.name);
+    for (auto it = pod_energy_j_.begin(); it != pod_energy_j_.end();) {
+      if (!known.count(it->first)) {
+        it = pod_energy_j_.erase(it);
+        continue;
+      }
+      table_.put(f_pod_energy_, {it->first.first, it->first.second}, it->second, gen);
+      ++it;
+    }
+  }
   if (rccl_) {
     std::vector<RcclTotals> tot;
     rccl_->poll(&tot);

@@ -280,6 +280,7 @@ class Engine {
   std::unordered_map<uint64_t, ProcRefs> proc_refs_;               // (device << 32 | pid) -> handles
   std::unordered_map<uint64_t, ProcRefs> legacy_refs_;             // pid -> legacy handles (pod, vram, gfx=perc)
   std::map<std::pair<std::string, std::string>, PodRefs> pod_refs_;  // (ns, pod) -> handles
+  std::map<std::pair<std::string, std::string>, double> pod_energy_j_;  // (ns, pod) -> joules so far
   SeriesRef self_refs_[21];
 
   // stats (guarded by stats_mu_)
@@ -299,7 +300,8 @@ class Engine {
       f_hbm_wr_, f_sen_sclk_, f_sen_lat_, f_sen_xcc_, f_sen_runs_, f_xcc_clk_, f_sen_xlat_, f_sen_mem_, f_sen_xmem_;
   int f_proc_vram_, f_proc_cu_, f_proc_sdma_, f_proc_evicted_, f_proc_gfx_;
   int f_legacy_mem_ = -1, f_legacy_perc_ = -1;
-  int f_pod_vram_, f_pod_procs_, f_pod_gpus_, f_pod_xrd_, f_pod_xwr_, f_pod_power_, f_pod_gfx_, f_pod_gfx_share_;
+  int f_pod_vram_, f_pod_procs_, f_pod_gpus_, f_pod_xrd_, f_pod_xwr_, f_pod_power_, f_pod_gfx_, f_pod_gfx_share_,
+      f_pod_energy_ = -1;
   int f_rccl_calls_, f_rccl_bytes_, f_rccl_comm_;
   int f_kfd_ev_ = -1, f_pod_kfd_ev_ = -1, f_pages_ = -1, f_gtt_used_ = -1, f_gtt_total_ = -1;
   int f_board_ = -1, f_fw_ = -1, f_driver_ = -1;

@@ -5,6 +5,7 @@ import collections
 import pytest
 
 from kubernetes_gpu_exporter_amd.utils import promtext
+from kubernetes_gpu_exporter_amd.utils.fakehost import kubepods_cgroup
 
 S = 1_000_000_000
 UID = "12345678-1234-1234-1234-123456789abc"
@@ -320,3 +321,38 @@ def test_gfx_activity_split_over_processes_and_pods(mock_engine):
     ticks(e, 1, t0=10 * S)
     share = {s[1]["pid"]: s[2] for s in promtext.samples(parse(e), "amd_gpu_process_gfx_activity_percent")}
     assert share["5"] == share["6"] == 40.0
+
+
+def test_pod_energy_from_hardware_counters(native, mock_engine):
+    """amd_pod_gpu_energy_joules_total: an owned GPU's energy counter goes to its pod; a
+    shared GPU's is split by the processes' CU-occupancy shares; totals persist while the
+    control plane knows the pod."""
+    uids = {p: f"00000000-0000-4000-8000-00000000000{i}" for i, p in enumerate("abc", 1)}
+    cids = {p: p * 64 for p in "abc"}
+    e = mock_engine(2, series_profile="standard")
+    e.set_pods([{"uid": uids[p], "namespace": "ns", "name": f"pod-{p}", "containers": {cids[p]: "w"}} for p in "abc"])
+    for pid, p in ((100, "a"), (200, "b"), (300, "c")):
+        e.set_pid_cgroup(pid, kubepods_cgroup(uids[p], cids[p]))
+    e.set_device_owners({"0000:10:00.0": {"namespace": "ns", "pod": "pod-a", "container": "w"}})
+    e.mock_set_value(0, "power_w", 500)
+    e.mock_set_value(1, "power_w", 800)
+    e.mock_set_processes(0, [{"pid": 100, "vram_bytes": 1 << 30, "cu_occupancy": 200, "name": "a"}])
+    e.mock_set_processes(1, [{"pid": 200, "vram_bytes": 1 << 30, "cu_occupancy": 48, "name": "b"},
+                             {"pid": 300, "vram_bytes": 1 << 30, "cu_occupancy": 16, "name": "c"}])
+    for t in range(1, 5):  # 3 one-second intervals
+        e.tick(t * 1_000_000_000)
+    fams = promtext.parse(e.snapshot_text())
+    en = {s[1]["pod"]: s[2] for s in promtext.samples(fams, "amd_pod_gpu_energy_joules_total")}
+    assert en["pod-a"] == pytest.approx(3 * 500, rel=0.01)
+    assert en["pod-b"] == pytest.approx(3 * 800 * 0.75, rel=0.01)
+    assert en["pod-c"] == pytest.approx(3 * 800 * 0.25, rel=0.01)
+    # pod-c's process exits: its total stays; the pod leaves the control plane: it goes
+    e.mock_set_processes(1, [{"pid": 200, "vram_bytes": 1 << 30, "cu_occupancy": 48, "name": "b"}])
+    e.tick(5 * 1_000_000_000)
+    fams = promtext.parse(e.snapshot_text())
+    en2 = {s[1]["pod"]: s[2] for s in promtext.samples(fams, "amd_pod_gpu_energy_joules_total")}
+    assert en2["pod-c"] == pytest.approx(en["pod-c"]) and en2["pod-b"] == pytest.approx(en["pod-b"] + 800, rel=0.01)
+    e.set_pods([{"uid": uids[p], "namespace": "ns", "name": f"pod-{p}", "containers": {cids[p]: "w"}} for p in "ab"])
+    e.tick(6 * 1_000_000_000)
+    fams = promtext.parse(e.snapshot_text())
+    assert "pod-c" not in {s[1]["pod"] for s in promtext.samples(fams, "amd_pod_gpu_energy_joules_total")}

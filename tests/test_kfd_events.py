@@ -79,3 +79,4 @@ def test_kfd_events_full_profile_only(native, mock_engine):
     off = mock_engine(1, series_profile="full", enable_kfd_events=False)
     off.tick(1_000_000_000)
     assert not promtext.samples(promtext.parse(off.snapshot_text()), "amd_gpu_kfd_events_total")
+
