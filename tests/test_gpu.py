@@ -352,6 +352,51 @@ def test_xcc_busy_agrees_with_gfx_activity_under_gemm(native):
     assert abs(mg - mx) < 15, (mg, mx)
 
 
+def test_pod_energy_tracks_gpu_energy(native):
+    """A GEMM pod alone on the GPU (owner inferred from its process): its
+    amd_pod_gpu_energy_joules_total grows by the GPU's own energy-counter delta."""
+    from kubernetes_gpu_exporter_amd.utils.fakehost import kubepods_cgroup
+    child = subprocess.Popen([sys.executable, "-c",
+                              "import sys; sys.path.insert(0, %r);"
+                              "from kubernetes_gpu_exporter_amd.ops.gemm import gemm_burn;"
+                              "print(gemm_burn(0, 8192, 6.0, 4), flush=True)" % ROOT],
+                             stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    e = amdsmi_engine(native)
+    try:
+        pid, deadline = None, time.time() + 20
+        while pid is None and time.time() < deadline:
+            e.tick()
+            fams = promtext.parse(e.snapshot_text())
+            big = [int(lab["pid"]) for _, lab, v in promtext.samples(fams, "amd_gpu_process_vram_bytes")
+                   if v > 256 * (1 << 20)]
+            pid = big[0] if big else None
+            time.sleep(0.2)
+        assert pid, "GEMM child not found"
+        uid, cid = "0e0e0e0e-0000-4000-8000-000000000001", "ef" * 32
+        e.set_pods([{"uid": uid, "namespace": "ml", "name": "gemm", "containers": {cid: "main"}}])
+        e.set_pid_cgroup(pid, kubepods_cgroup(uid, cid))
+        for _ in range(3):
+            e.tick()
+            time.sleep(0.1)
+
+        def both():
+            e.tick()
+            f = promtext.parse(e.snapshot_text())
+            pod = [s[2] for s in promtext.samples(f, "amd_pod_gpu_energy_joules_total") if s[1]["pod"] == "gemm"]
+            return (pod[0] if pod else 0.0), promtext.value(f, "amd_gpu_energy_joules_total", gpu=0)
+        p0, g0 = both()
+        for _ in range(20):
+            time.sleep(0.1)
+            e.tick()
+        p1, g1 = both()
+    finally:
+        e.stop()
+        child.communicate(timeout=60)
+    print(f"pod energy +{p1 - p0:.1f} J, GPU energy +{g1 - g0:.1f} J")
+    assert g1 - g0 > 100  # a busy MI355X over ~2 s
+    assert abs((p1 - p0) - (g1 - g0)) <= 0.02 * (g1 - g0), (p1 - p0, g1 - g0)
+
+
 def test_kfd_events_real_queue_eviction():
     """A real KFD event end to end (tools/kfd_events_check.py): invalidating a host buffer
     registered with the GPU makes KFD evict and restore this process's queues; the engine
