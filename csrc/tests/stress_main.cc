@@ -52,6 +52,7 @@ int main(int argc, char** argv) {
   cfg.interval_s = 0.01;
   cfg.enable_sentinel = true;
   cfg.enable_counters = true;
+  cfg.series_profile = "full";  // every family, KFD events and per-pod energy included
   cfg.http.host = "127.0.0.1";
   cfg.http.port = 0;
   cfg.http.threads = 2;
@@ -113,6 +114,10 @@ int main(int argc, char** argv) {
       e.mock()->set_processes(int(k % 8), procs);
       e.mock()->set_fault(int(k % 8), k % 13 == 0 ? "error" : "none");
       e.set_device_owners({{"0000:10:00.0", DeviceOwner{"ns", "owner-" + std::to_string(k % 3), "c"}}});
+      // KFD events for the sampler to count and attribute (split lines exercise the
+      // per-device tail buffer)
+      e.inject_kfd_events(int(k % 8), "9 " + std::to_string(k) + " -" + std::to_string(100 + k % 5) + " 0 2\n1 6");
+      e.inject_kfd_events(int(k % 8), "5:python3\n2 0:1\n");
       std::this_thread::sleep_for(std::chrono::milliseconds(3));
     }
   });
