@@ -616,6 +616,11 @@ def test_device_scope_pmc_calibration():
     wr = cp["amd_gpu_hbm_write_bytes_per_second"] / cp["expected_Bps"]
     print(f"HBM read {rd:.3f}x, write {wr:.3f}x of the copy's bytes/s")
     assert 0.9 < rd < 1.1 and 0.9 < wr < 1.1, (rd, wr)
+    # the PMFW's UMC-activity estimate (amd_gpu_hbm_bandwidth_bytes_per_second, device-wide,
+    # no PMC needed) against the copy's read + write bytes
+    est = cp["amd_gpu_hbm_bandwidth_bytes_per_second"] / (2 * cp["expected_Bps"])
+    print(f"UMC-activity HBM estimate {est:.3f}x of the copy's read+write bytes/s")
+    assert 0.85 < est < 1.15, est
     # a local copy sends nothing to memory behind GMI (peer GPUs)
     assert cp["amd_gpu_remote_read_bytes_per_second"] < 0.01 * cp["expected_Bps"], cp
     assert cp["amd_gpu_remote_write_bytes_per_second"] < 0.01 * cp["expected_Bps"], cp

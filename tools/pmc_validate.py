@@ -28,7 +28,8 @@ sys.path.insert(0, ROOT)
 FAMILIES = ("amd_gpu_hbm_read_bytes_per_second", "amd_gpu_hbm_write_bytes_per_second", "amd_gpu_waves_per_second",
             "amd_gpu_lds_active_percent", "amd_gpu_lds_bank_conflict_percent", "amd_gpu_gui_active_percent",
             "amd_gpu_sq_busy_percent", "amd_gpu_mfma_busy_percent", "amd_gpu_remote_read_bytes_per_second",
-            "amd_gpu_remote_write_bytes_per_second")
+            "amd_gpu_remote_write_bytes_per_second", "amd_gpu_hbm_bandwidth_bytes_per_second",
+            "amd_gpu_umc_activity_percent")
 WORKLOADS = (("copy", 0), ("lds_clean", 1), ("lds_32way", 2))
 
 
