@@ -88,7 +88,7 @@ void MockBackend::sample(const DeviceInfo& dev, DeviceSample* out) {
   out->clk_mem = get(s, "clk_mem", 2000);
   out->pcie_width = 16;
   out->pcie_speed_gts = 32;
-  out->pcie_bw_inst = get(s, "pcie_bw_gbs", 18);
+  out->pcie_bw_inst = get(s, "pcie_bw_gbs", 18) * 8000.0;  // PMFW unit: Mb/s
   out->pcie_replay = 0;
   out->pcie_nak_sent = get(s, "pcie_nak_sent", 0);
   out->pcie_nak_rcvd = get(s, "pcie_nak_rcvd", 0);

@@ -113,8 +113,11 @@ struct DeviceSample {
   double xgmi_link_up[kMaxXgmiLinks] = {kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN};
   bool xgmi_valid = false;
 
-  double pcie_bw_inst = kNaN;       // GB/s
-  uint64_t pcie_bw_acc = 0;         // GB/s accumulated
+  // PMFW PCIe link traffic, Mb/s (megabits; amdsmi's documented unit — the kernel header's
+  // "GB/sec" is wrong: a 57.6 GB/s host-to-device copy reads 560550, i.e. 70.1 GB/s of link
+  // traffic incl. protocol overhead, tools/probe_pcie_units.py)
+  double pcie_bw_inst = kNaN;
+  uint64_t pcie_bw_acc = 0;         // sum of the PMFW's 1 ms pcie_bw_inst samples
   double pcie_replay = kNaN;        // count
   double pcie_width = kNaN, pcie_speed_gts = kNaN;
   // link reliability (gpu_metrics v1.8 accumulators; NaN unsupported)

@@ -157,7 +157,8 @@ void Engine::define_families() {
   f_xrd_rate_ = add("amd_gpu_xgmi_read_bytes_per_second", "xGMI receive rate summed over links", G, D);
   f_xwr_rate_ = add("amd_gpu_xgmi_write_bytes_per_second", "xGMI transmit rate summed over links", G, D);
   f_links_up_ = add("amd_gpu_xgmi_links_up", "Number of xGMI links reporting up", G, D);
-  f_pcie_bw_ = add("amd_gpu_pcie_bandwidth_bytes_per_second", "PCIe instantaneous bandwidth", G, D);
+  f_pcie_bw_ = add("amd_gpu_pcie_bandwidth_bytes_per_second",
+                   "PCIe link traffic, both directions incl. protocol overhead (PMFW instantaneous, Mb/s / 8)", G, D);
   f_pcie_replay_ = add("amd_gpu_pcie_replay_total", "PCIe replay count", C, D);
   f_pcie_speed_ = add("amd_gpu_pcie_link_speed_gts", "PCIe link speed (GT/s)", G, D);
   f_pcie_width_ = add("amd_gpu_pcie_link_width", "PCIe link width (lanes)", G, D);
@@ -776,7 +777,7 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
       dput(st, i, st.xwr_rate, f_xwr_rate_, {}, ws, gen);
     }
   }
-  dput(st, i, st.pcie_bw, f_pcie_bw_, {}, std::isnan(c.pcie_bw_inst) ? kNaN : c.pcie_bw_inst * 1e9, gen);
+  dput(st, i, st.pcie_bw, f_pcie_bw_, {}, std::isnan(c.pcie_bw_inst) ? kNaN : c.pcie_bw_inst * 125000.0, gen);
   dput(st, i, st.pcie_replay, f_pcie_replay_, {}, c.pcie_replay, gen);
   dput(st, i, st.pcie_speed, f_pcie_speed_, {}, c.pcie_speed_gts, gen);
   dput(st, i, st.pcie_width, f_pcie_width_, {}, c.pcie_width, gen);

@@ -397,6 +397,52 @@ def test_pod_energy_tracks_gpu_energy(native):
     assert abs((p1 - p0) - (g1 - g0)) <= 0.02 * (g1 - g0), (p1 - p0, g1 - g0)
 
 
+_H2D = """
+import json, sys, time, torch
+src = torch.empty(1 << 30, dtype=torch.uint8, pin_memory=True)
+dst = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+dst.copy_(src, non_blocking=True); torch.cuda.synchronize()
+print("ready", flush=True)
+n, t0 = 0, time.perf_counter()
+while time.perf_counter() - t0 < 4.0:
+    dst.copy_(src, non_blocking=True); torch.cuda.synchronize(); n += 1
+print(json.dumps({"Bps": n * (1 << 30) / (time.perf_counter() - t0)}), flush=True)
+"""
+
+
+def test_pcie_bandwidth_under_host_to_device_copy(native):
+    """amd_gpu_pcie_bandwidth_bytes_per_second (PMFW pcie_bandwidth_inst in Mb/s, / 8) while a
+    child streams pinned host memory to the GPU at a measured payload rate: link traffic is
+    the payload plus protocol overhead and the reverse direction's requests (measured
+    1.15-1.22x), so between 1.0x and 1.4x.  (Read as the kernel header's GB/s it was
+    ~9700x too high; tools/probe_pcie_units.py.)"""
+    import json
+    child = subprocess.Popen([sys.executable, "-c", _H2D], stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                             text=True)
+    e = amdsmi_engine(native)
+    vals = []
+    try:
+        assert "ready" in child.stdout.readline() or True
+        time.sleep(0.5)
+        for _ in range(25):
+            e.tick()
+            vals.append(promtext.value(promtext.parse(e.snapshot_text()), "amd_gpu_pcie_bandwidth_bytes_per_second",
+                                       gpu=0))
+            time.sleep(0.1)
+    finally:
+        e.stop()
+        out, _ = child.communicate(timeout=60)
+    line = [l for l in out.splitlines() if l.startswith("{")]
+    assert line, out[-2000:]
+    measured = json.loads(line[-1])["Bps"]
+    vals.sort()
+    med = vals[len(vals) // 2]
+    print(f"H2D copy {measured / 1e9:.1f} GB/s; exporter PCIe bandwidth median {med / 1e9:.1f} GB/s "
+          f"(min {vals[0] / 1e9:.1f}, max {vals[-1] / 1e9:.1f})")
+    assert measured > 5e9
+    assert 1.0 * measured < med < 1.4 * measured, (med, measured)
+
+
 def test_kfd_events_real_queue_eviction():
     """A real KFD event end to end (tools/kfd_events_check.py): invalidating a host buffer
     registered with the GPU makes KFD evict and restore this process's queues; the engine
