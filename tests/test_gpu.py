@@ -303,11 +303,19 @@ def test_units_are_physically_consistent(native):
             time.sleep(0.1)
         t1, e1 = time.monotonic(), promtext.value(fams, "amd_gpu_energy_joules_total", gpu=0)
         vram = promtext.value(fams, "amd_gpu_vram_used_bytes", gpu=0)
+        cap = promtext.value(fams, "amd_gpu_power_cap_watts", gpu=0)
+        clk = {s[1]["clock"]: s[2] for s in promtext.samples(fams, "amd_gpu_clock_hz") if s[1]["gpu"] == "0"}
         thr = [s[2] for s in promtext.samples(fams, "amd_gpu_throttle_residency_percent") if s[1]["gpu"] == "0"]
         amdsmi.amdsmi_init()
         try:
             h = amdsmi.amdsmi_get_processor_handles()[0]
             usage = amdsmi.amdsmi_get_gpu_vram_usage(h)
+            smi_clk = {}
+            for name in ("GFX", "MEM", "SOC"):
+                try:
+                    smi_clk[name.lower()] = amdsmi.amdsmi_get_clock_info(h, getattr(amdsmi.AmdSmiClkType, name))
+                except Exception as ex:  # noqa: BLE001
+                    smi_clk[name.lower()] = str(ex)
         finally:
             amdsmi.amdsmi_shut_down()
     finally:
@@ -320,6 +328,13 @@ def test_units_are_physically_consistent(native):
     if isinstance(used_mb, (int, float)):
         assert abs(vram / 2**20 - used_mb) < max(256, 0.02 * used_mb), (vram, used_mb)
     assert all(0 <= v <= 100 for v in thr), thr
+    print("power cap", cap, "W; clocks", clk, "\namdsmi clock info:", smi_clk)
+    for name, info in smi_clk.items():
+        if isinstance(info, dict) and isinstance(info.get("clk"), (int, float)) and name in clk:
+            mhz = clk[name] / 1e6
+            assert abs(mhz - info["clk"]) <= max(150, 0.25 * info["clk"]), (name, mhz, info)
+    assert 300 < cap < 2500 and max(powers) <= 1.1 * cap, (cap, max(powers))
+    assert 0 < clk.get("gfx", 0) <= 3.0e9 and 0.5e9 < clk.get("mem", 0) < 3.0e9, clk
 
 
 def test_xcc_busy_agrees_with_gfx_activity_under_gemm(native):
