@@ -165,7 +165,9 @@ void Engine::define_families() {
   f_thr_ = add("amd_gpu_throttle_residency_percent", "Share of the last tick spent throttled, by reason", G,
                with(D, {"reason"}));
   f_nprocs_ = add("amd_gpu_processes", "Processes with a KFD context on this GPU", G, D);
-  f_cu_occ_ = add("amd_gpu_cu_occupancy", "CUs occupied by all processes on this GPU", G, D);
+  f_cu_occ_ = add("amd_gpu_cu_occupancy",
+                  "Resident waves of all processes on this GPU in CU-equivalents (KFD: waves / max waves per CU; "
+                  "a GEMM holding 8 waves on each of 256 CUs reads 64)", G, D);
   // --- full profile: link / memory reliability (error totals; not part of the 64-series load) ---
   f_ecc_ = add("amd_gpu_ecc_errors_total", "RAS ECC error count summed over IP blocks (sysfs ras/*_err_count)", C,
                with(D, {"type"}));
@@ -210,7 +212,8 @@ void Engine::define_families() {
   // --- per-process / per-pod families ---
   const std::vector<std::string> P = {"gpu", "pid", "comm", "namespace", "pod", "container"};
   f_proc_vram_ = add("amd_gpu_process_vram_bytes", "VRAM held by a process on a GPU (KFD)", G, P);
-  f_proc_cu_ = add("amd_gpu_process_cu_occupancy", "CUs occupied by a process on a GPU (KFD)", G, P);
+  f_proc_cu_ = add("amd_gpu_process_cu_occupancy",
+                   "Resident waves of a process on a GPU in CU-equivalents (KFD stats_<id>/cu_occupancy)", G, P);
   f_proc_sdma_ = add("amd_gpu_process_sdma_seconds_total", "SDMA engine time used by a process", C, P);
   f_proc_evicted_ = add("amd_gpu_process_evicted_seconds_total",
                         "Time the process's GPU queues were evicted (memory pressure / preemption; KFD stats)", C, P);

@@ -349,19 +349,24 @@ def test_xcc_busy_agrees_with_gfx_activity_under_gemm(native):
     e = amdsmi_engine(native, series_profile="full")
     try:
         time.sleep(2.0)  # the burn is up (torch import + warm-up)
-        gfx, xcc = [], []
+        gfx, xcc, cu = [], [], []
         for _ in range(15):
             e.tick()
             fams = promtext.parse(e.snapshot_text())
             gfx.append(promtext.value(fams, "amd_gpu_gfx_activity_percent", gpu=0))
             xcc.extend(s[2] for s in promtext.samples(fams, "amd_gpu_xcc_busy_percent") if s[1]["gpu"] == "0")
+            cu.append(promtext.value(fams, "amd_gpu_cu_occupancy", gpu=0))
             time.sleep(0.1)
     finally:
         e.stop()
         out, _ = child.communicate(timeout=60)
     print("gemm:", out.strip()[-300:])
     mg, mx = sum(gfx) / len(gfx), sum(xcc) / max(1, len(xcc))
-    print(f"gfx_activity mean {mg:.1f} %, per-XCD busy mean {mx:.1f} % over {len(xcc)} samples")
+    print(f"gfx_activity mean {mg:.1f} %, per-XCD busy mean {mx:.1f} % over {len(xcc)} samples; "
+          f"occupied CUs {sorted(cu)}")
+    # KFD cu_occupancy = resident waves / max waves per CU ("CU-equivalents"): the 256x256
+    # GEMM keeps 8 waves per CU resident, which reads 64 of 256 (measured)
+    assert 0 < sorted(cu)[len(cu) // 2] <= 256, cu
     assert xcc and all(0 <= v <= 100.5 for v in xcc), xcc
     assert mg > 60 and mx > 60, (mg, mx)
     assert abs(mg - mx) < 15, (mg, mx)
