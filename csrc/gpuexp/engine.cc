@@ -167,7 +167,7 @@ void Engine::define_families() {
   f_nprocs_ = add("amd_gpu_processes", "Processes with a KFD context on this GPU", G, D);
   f_cu_occ_ = add("amd_gpu_cu_occupancy",
                   "Resident waves of all processes on this GPU in CU-equivalents (KFD: waves / max waves per CU; "
-                  "a GEMM holding 8 waves on each of 256 CUs reads 64)", G, D);
+                  "the bench's saturating 256x256 GEMM reads 64 on MI355X)", G, D);
   // --- full profile: link / memory reliability (error totals; not part of the 64-series load) ---
   f_ecc_ = add("amd_gpu_ecc_errors_total", "RAS ECC error count summed over IP blocks (sysfs ras/*_err_count)", C,
                with(D, {"type"}));
