@@ -692,6 +692,8 @@ def test_device_scope_pmc_calibration():
     if "counters=unavailable" in res["status"]:
         pytest.skip("device counting unavailable on this box: " + res["status"])
     cp, clean, conf = res["copy"], res["lds_clean"], res["lds_32way"]
+    for w in (cp, clean, conf):  # each read window lies inside its workload's busy period
+        assert w.get("busy_at_tick", True), w
     assert cp["device_scope"] == 1, cp
     rd = cp["amd_gpu_hbm_read_bytes_per_second"] / cp["expected_Bps"]
     wr = cp["amd_gpu_hbm_write_bytes_per_second"] / cp["expected_Bps"]

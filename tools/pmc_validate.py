@@ -62,7 +62,9 @@ def main() -> int:
                 out[name] = {"error": "calibration dispatch failed"}
                 continue
             per_launch = probe[0] / 20
-            launches = max(20, int(1.8 / per_launch))
+            # ~3 s of work: the last tick (at 1.5 s) must read a window inside the busy period
+            # even when the 20-launch probe overestimated the per-launch time
+            launches = max(20, int(3.0 / per_launch))
             res = (ctypes.c_double * 3)()
             rc = [None]
             th = threading.Thread(target=lambda: rc.__setitem__(0, lib.gpuexp_rp_calibrate(0, kind, launches, res)))
@@ -75,7 +77,8 @@ def main() -> int:
             busy_s = time.monotonic() - t0
             fams = promtext.parse(e.snapshot_text())
             th.join()
-            got = {"launches": launches, "rc": rc[0], "seconds": res[0], "ticked_at_s": round(busy_s, 3)}
+            got = {"launches": launches, "rc": rc[0], "seconds": res[0], "ticked_at_s": round(busy_s, 3),
+                   "busy_at_tick": bool(res[0] > busy_s)}
             for fam in FAMILIES:
                 v = promtext.samples(fams, fam)
                 got[fam] = v[0][2] if v else None
