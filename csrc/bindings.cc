@@ -446,6 +446,8 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("rccl_verify", &EngineConfig::rccl_verify)
       .def_readwrite("enable_kfd_events", &EngineConfig::enable_kfd_events)
       .def_readwrite("firmware_info", &EngineConfig::firmware_info)
+      .def_readwrite("state_file", &EngineConfig::state_file)
+      .def_readwrite("state_interval_s", &EngineConfig::state_interval_s)
       .def_readwrite("kfd_path", &EngineConfig::kfd_path)
       .def_readwrite("metrics_min_interval_s", &EngineConfig::metrics_min_interval_s)
       .def_readwrite("queue_devices", &EngineConfig::queue_devices)

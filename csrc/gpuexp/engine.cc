@@ -477,6 +477,7 @@ bool Engine::start(std::string* err) {
     struct utsname u{};
     kernel_release_ = ::uname(&u) == 0 ? u.release : "";
   }
+  if (!cfg_.state_file.empty()) load_state();
   if (cfg_.enable_kfd_events && cfg_.series_profile == "full") {
     kfd_events_ = std::make_unique<KfdEventSource>();
     if (mock_) {
@@ -523,6 +524,10 @@ void Engine::stop() {
   if (sampler_.joinable()) sampler_.join();
   if (stop_fd_ >= 0) ::close(stop_fd_);
   stop_fd_ = -1;
+  if (!cfg_.state_file.empty()) {
+    std::lock_guard<std::mutex> lk(tick_mu_);
+    save_state();
+  }
   if (http_) http_->stop();
   if (sentinel_) sentinel_->stop();
   if (counters_) counters_->stop();
@@ -572,6 +577,7 @@ void Engine::set_pods(std::vector<PodMeta> pods) {
   std::lock_guard<std::mutex> lk(ctl_mu_);
   pending_pods_ = std::move(pods);
   ctl_dirty_ = true;
+  pods_pushed_ = true;
 }
 
 void Engine::set_device_owners(std::vector<std::pair<std::string, DeviceOwner>> owners) {
@@ -616,7 +622,8 @@ void Engine::emit_kfd_events(uint64_t gen) {
   for (auto& kv : pods_by_uid_) live.emplace(kv.second.ns, kv.second.name);
   for (auto it = pod_kfd_events_.begin(); it != pod_kfd_events_.end();) {
     const auto& k = it->first;
-    if (!live.count({std::get<0>(k), std::get<1>(k)})) {
+    // restored from the state file while the pod list is not here yet: keep (and export)
+    if (pods_known_ && !live.count({std::get<0>(k), std::get<1>(k)})) {
       it = pod_kfd_events_.erase(it);
       continue;
     }
@@ -624,6 +631,86 @@ void Engine::emit_kfd_events(uint64_t gen) {
                gen);
     ++it;
   }
+}
+
+std::string Engine::device_key(size_t i) const {
+  return lower(devices_[i].bdf) + "/" + std::to_string(devices_[i].partition_id);
+}
+
+// State file: one record per line, tab-separated (Kubernetes names carry no tabs):
+//   gpuexp-state 1
+//   pod_energy <ns> <pod> <joules>
+//   pod_event  <ns> <pod> <event id> <count>
+//   dev_event  <bdf>/<partition> <event id> <count>
+void Engine::load_state() {
+  std::string body;
+  if (!read_small_file(cfg_.state_file, &body, 16u << 20)) {
+    state_status_ = "no state yet (" + cfg_.state_file + ")";
+    return;
+  }
+  if (body.compare(0, 14, "gpuexp-state 1") != 0) {
+    state_status_ = "ignored: unknown format in " + cfg_.state_file;
+    GPUEXP_LOG(LogLevel::kWarn, "state", state_status_);
+    return;
+  }
+  std::unordered_map<std::string, size_t> dev_by_key;
+  for (size_t i = 0; i < devices_.size(); ++i) dev_by_key[device_key(i)] = i;
+  size_t n = 0, pos = body.find('\n');
+  while (pos != std::string::npos && pos + 1 < body.size()) {
+    size_t eol = body.find('\n', pos + 1);
+    const std::string line = body.substr(pos + 1, (eol == std::string::npos ? body.size() : eol) - pos - 1);
+    pos = eol;
+    std::vector<std::string> f;
+    for (size_t a = 0, b; a <= line.size(); a = b + 1) {
+      b = line.find('\t', a);
+      if (b == std::string::npos) b = line.size();
+      f.push_back(line.substr(a, b - a));
+    }
+    if (f[0] == "pod_energy" && f.size() == 4) {
+      pod_energy_j_[{f[1], f[2]}] = std::strtod(f[3].c_str(), nullptr);
+      ++n;
+    } else if (f[0] == "pod_event" && f.size() == 5) {
+      const int ev = std::atoi(f[3].c_str());
+      if (ev > 0 && ev < kKfdEventIds) pod_kfd_events_[std::make_tuple(f[1], f[2], ev)] = std::strtoull(f[4].c_str(), nullptr, 10);
+      ++n;
+    } else if (f[0] == "dev_event" && f.size() == 4) {
+      auto it = dev_by_key.find(f[1]);
+      const int ev = std::atoi(f[2].c_str());
+      if (it != dev_by_key.end() && ev > 0 && ev < kKfdEventIds)
+        dstate_[it->second].kfd_events[ev] = std::strtoull(f[3].c_str(), nullptr, 10);
+      ++n;
+    }
+  }
+  state_status_ = "restored " + std::to_string(n) + " records from " + cfg_.state_file;
+  GPUEXP_LOG(LogLevel::kInfo, "state", state_status_);
+}
+
+bool Engine::save_state() {
+  state_saved_ns_ = mono_ns();
+  std::string out = "gpuexp-state 1\n";
+  char num[64];
+  for (auto& kv : pod_energy_j_) {
+    std::snprintf(num, sizeof(num), "%.17g", kv.second);
+    out += "pod_energy\t" + kv.first.first + "\t" + kv.first.second + "\t" + num + "\n";
+  }
+  for (auto& kv : pod_kfd_events_)
+    out += "pod_event\t" + std::get<0>(kv.first) + "\t" + std::get<1>(kv.first) + "\t" +
+           std::to_string(std::get<2>(kv.first)) + "\t" + std::to_string(kv.second) + "\n";
+  for (size_t i = 0; i < dstate_.size() && i < devices_.size(); ++i)
+    for (int ev = 1; ev < kKfdEventIds; ++ev)
+      if (dstate_[i].kfd_events[ev])
+        out += "dev_event\t" + device_key(i) + "\t" + std::to_string(ev) + "\t" +
+               std::to_string(dstate_[i].kfd_events[ev]) + "\n";
+  const std::string tmp = cfg_.state_file + ".tmp";
+  FILE* f = std::fopen(tmp.c_str(), "w");
+  bool ok = f && std::fwrite(out.data(), 1, out.size(), f) == out.size();
+  if (f) ok = (std::fclose(f) == 0) && ok;
+  ok = ok && std::rename(tmp.c_str(), cfg_.state_file.c_str()) == 0;
+  if (!ok) {
+    state_status_ = "save failed: " + cfg_.state_file;
+    GPUEXP_LOG(LogLevel::kWarn, "state", state_status_);
+  }
+  return ok;
 }
 
 void Engine::set_pid_cgroup(int pid, const std::string& cgroup_path) {
@@ -1072,7 +1159,7 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
     std::set<std::pair<std::string, std::string>> known;
     for (auto& kv : pods_by_uid_) known.emplace(kv.second.ns, kv.second.name);
     for (auto it = pod_energy_j_.begin(); it != pod_energy_j_.end();) {
-      if (!known.count(it->first)) {
+      if (pods_known_ && !known.count(it->first)) {
         it = pod_energy_j_.erase(it);
         continue;
       }
@@ -1214,6 +1301,7 @@ void Engine::tick_locked(uint64_t now) {
       owners_.clear();
       for (auto& o : pending_owners_) owners_[lower(o.first)] = o.second;
       ctl_dirty_ = false;
+      pods_known_ = pods_known_ || pods_pushed_;
     }
   }
 
@@ -1368,6 +1456,7 @@ void Engine::tick_locked(uint64_t now) {
     }
     snap->published_mono_ns = mono_ns();
     store_.publish(slot);
+    if (!cfg_.state_file.empty() && tnow - state_saved_ns_ >= uint64_t(cfg_.state_interval_s * 1e9)) save_state();
     if (http_) http_->set_ready(true);
   } else {
     ts[7] = mono_ns();
@@ -1410,7 +1499,7 @@ EngineStats Engine::stats() {
 std::string Engine::source_status() {
   std::string s = std::string("backend=") + (backend_ ? backend_->name() : "none") + " sentinel=" + sentinel_status_ +
                   " counters=" + counters_status_ + " rccl=" + (rccl_ ? cfg_.rccl_dir : "disabled") +
-                  " kfd_events=" + kfd_events_status_;
+                  " kfd_events=" + kfd_events_status_ + " state=" + state_status_;
   if (backend_)
     for (const auto& d : devices_) s += " gpu" + std::to_string(d.index) + "=[" + backend_->describe(d) + "]";
   return s;

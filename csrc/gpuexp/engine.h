@@ -91,6 +91,11 @@ struct EngineConfig {
   bool rccl_verify = true;             // attribute a tracer file only to a process that maps it
   bool enable_kfd_events = true;       // full profile: KFD SMI events (VM faults, resets, ...)
   bool firmware_info = true;           // full profile: amd_gpu_firmware_info (one series per loaded firmware)
+  // Checkpoint of the exporter's own accumulations (per-pod energy, KFD event counts) so
+  // they continue across exporter restarts; "" = off.  Written every state_interval_s and
+  // at stop (write + rename), read at start.
+  std::string state_file;
+  double state_interval_s = 10.0;
   std::string kfd_path = "/dev/kfd";   // the device node itself (not under host_root)
   bool force_amdsmi_metrics = false;
   int gzip_level = 1;
@@ -212,6 +217,9 @@ class Engine {
   void emit_self(uint64_t gen);
   void count_kfd_events();
   void emit_kfd_events(uint64_t gen);
+  std::string device_key(size_t i) const;  // "<bdf>/<partition>": stable across restarts
+  void load_state();
+  bool save_state();
   void trace_event(const char* name, uint64_t start_ns, uint64_t dur_ns);
   void dput(DevState& st, int dev, SeriesRef& r, int fid, std::initializer_list<const char*> extra,
             double v, uint64_t gen);
@@ -241,6 +249,10 @@ class Engine {
   // per-process KFD events attributed to pods: (namespace, pod, event id) -> count
   std::map<std::tuple<std::string, std::string, int>, uint64_t> pod_kfd_events_;
   uint64_t kfd_events_unattributed_ = 0;  // per-process events whose PID resolved to no pod
+  bool pods_pushed_ = false;   // ctl_mu_: the control plane has delivered a pod list
+  bool pods_known_ = false;    // sampler: ...applied; per-pod totals are GC'd only from then on
+  uint64_t state_saved_ns_ = 0;
+  std::string state_status_ = "disabled";
   std::unique_ptr<ForkJoinPool> pool_;
   // full profile, real backends: RAS/AER readers + last totals (re-read every ras_interval_s)
   std::vector<RasReader> ras_;

@@ -56,6 +56,8 @@ class Config:
                                            # Each queue pins ~346 MiB of host memory on MI355X.
     enable_kfd_events: bool = True         # full profile: KFD SMI events (VM faults, resets, evictions)
     firmware_info: bool = True             # full profile: amd_gpu_firmware_info per loaded firmware
+    state_file: str = ""                   # checkpoint of per-pod energy / KFD event totals ("" = off)
+    state_interval: float = 10.0           # seconds between checkpoint writes (and one at shutdown)
     kfd_path: str = "/dev/kfd"             # the device node (mounted directly, not under host_root)
     enable_rccl: bool = False
     rccl_dir: str = "/var/run/gpuexp/rccl"
@@ -150,6 +152,8 @@ class Config:
         ec.rccl_verify = bool(self.rccl_verify)
         ec.enable_kfd_events = bool(self.enable_kfd_events)
         ec.firmware_info = bool(self.firmware_info)
+        ec.state_file = self.state_file
+        ec.state_interval_s = float(self.state_interval)
         ec.kfd_path = self.kfd_path
         ec.gc_after = int(self.gc_after)
         ec.device_filter = [int(d) for d in self.devices if ":" not in str(d)]
@@ -257,6 +261,8 @@ def validate(cfg: Config) -> None:
         raise ValueError(f"series_profile must be full|standard|compact|legacy, got {cfg.series_profile}")
     if cfg.metrics_min_interval < 0:
         raise ValueError("metrics_min_interval must be >= 0")
+    if cfg.state_interval <= 0:
+        raise ValueError("state_interval must be > 0")
     if cfg.ras_interval <= 0:
         raise ValueError("ras_interval must be > 0")
     if cfg.process_source not in ("auto", "kfd", "amdsmi", "none"):

@@ -356,3 +356,60 @@ def test_pod_energy_from_hardware_counters(native, mock_engine):
     e.tick(6 * 1_000_000_000)
     fams = promtext.parse(e.snapshot_text())
     assert "pod-c" not in {s[1]["pod"] for s in promtext.samples(fams, "amd_pod_gpu_energy_joules_total")}
+
+
+def test_state_file_carries_pod_totals_across_restarts(native, mock_engine, tmp_path):
+    """Checkpoint/resume of the exporter's own accumulations: per-pod energy and KFD event
+    counts, and per-GPU event counts, continue from the state file after a restart (kept
+    until the control plane has delivered its pod list, then GC'd as usual)."""
+    state = str(tmp_path / "state")
+    uid, cid = "00000000-0000-4000-8000-0000000000aa", "ab" * 32
+    pods = [{"uid": uid, "namespace": "ns", "name": "trainer", "containers": {cid: "w"}}]
+
+    def engine():
+        e = mock_engine(1, series_profile="full", state_file=state)
+        e.mock_set_value(0, "power_w", 400)
+        e.mock_set_processes(0, [{"pid": 100, "vram_bytes": 1 << 30, "cu_occupancy": 10, "name": "t"}])
+        e.set_pid_cgroup(100, kubepods_cgroup(uid, cid))
+        return e
+
+    def totals(e):
+        f = promtext.parse(e.snapshot_text())
+        en = {s[1]["pod"]: s[2] for s in promtext.samples(f, "amd_pod_gpu_energy_joules_total")}
+        pev = {(s[1]["pod"], s[1]["event"]): s[2] for s in promtext.samples(f, "amd_pod_gpu_kfd_events_total")}
+        dev = {s[1]["event"]: s[2] for s in promtext.samples(f, "amd_gpu_kfd_events_total")}
+        return en, pev, dev
+
+    a = engine()
+    a.set_pods(pods)
+    a.inject_kfd_events(0, b"1 64:t\n2 0:1\n")
+    for t in range(1, 5):
+        a.tick(t * 1_000_000_000)
+    en1, pev1, dev1 = totals(a)
+    assert en1["trainer"] == pytest.approx(3 * 400, rel=0.01) and pev1[("trainer", "vm_fault")] == 1
+    a.stop()  # final save
+    assert open(state).read().startswith("gpuexp-state 1\n")
+
+    b = engine()
+    assert "restored" in b.source_status()
+    b.tick(10_000_000_000)  # no pod list yet: restored totals are kept, not GC'd
+    en2, pev2, dev2 = totals(b)
+    assert en2 == en1 and pev2 == pev1 and dev2["vm_fault"] == 1 and dev2["thermal_throttle"] == 1
+    b.set_pods(pods)
+    for t in range(11, 14):
+        b.tick(t * 1_000_000_000)
+    en3, _, _ = totals(b)
+    assert en3["trainer"] == pytest.approx(en1["trainer"] + 3 * 400, rel=0.01)  # continues, no reset
+    b.set_pods([])
+    b.tick(14_000_000_000)
+    assert not totals(b)[0]  # the pod is gone: its total goes with it
+    b.stop()
+
+
+def test_state_file_with_unknown_format_is_ignored(native, mock_engine, tmp_path):
+    state = tmp_path / "state"
+    state.write_text("something else\npod_energy\tns\tp\t1e9\n")
+    e = mock_engine(1, series_profile="full", state_file=str(state))
+    assert "ignored" in e.source_status()
+    e.tick(1_000_000_000)
+    assert not promtext.samples(promtext.parse(e.snapshot_text()), "amd_pod_gpu_energy_joules_total")
