@@ -12,6 +12,8 @@
 #include <thread>
 #include <vector>
 
+#include <unistd.h>
+
 #include "gpuexp/client.h"
 #include "gpuexp/engine.h"
 
@@ -53,6 +55,8 @@ int main(int argc, char** argv) {
   cfg.enable_sentinel = true;
   cfg.enable_counters = true;
   cfg.series_profile = "full";  // every family, KFD events and per-pod energy included
+  cfg.state_file = "/tmp/gpuexp-stress-state-" + std::to_string(::getpid());  // checkpoint every 50 ms
+  cfg.state_interval_s = 0.05;
   cfg.http.host = "127.0.0.1";
   cfg.http.port = 0;
   cfg.http.threads = 2;
@@ -126,6 +130,7 @@ int main(int argc, char** argv) {
   for (auto& t : th) t.join();
   EngineStats st = e.stats();
   e.stop();
+  std::remove(cfg.state_file.c_str());
   std::printf("ticks=%llu scrapes=%ld bad=%ld series=%llu render_bytes=%llu\n", (unsigned long long)st.ticks,
               scrapes.load(), bad.load(), (unsigned long long)st.series, (unsigned long long)st.render_bytes);
   return (bad.load() == 0 && scrapes.load() > 100 && st.ticks > 10) ? 0 : 1;
