@@ -649,6 +649,7 @@ def main() -> int:
             rccl.setdefault(lab.get("pod") or lab.get("pid"), {}).setdefault(lab["op"], {})["bytes"] = v
         for sname, lab, v in promtext.samples(fams, "amd_rccl_collective_calls_total"):
             rccl.setdefault(lab.get("pod") or lab.get("pid"), {}).setdefault(lab["op"], {})["calls"] = v
+        rccl_files = {lab.get("state"): int(v) for _, lab, v in promtext.samples(fams, "gpuexp_rccl_files")}
         rccl_ranks = {lab.get("pod") or lab.get("pid"): [int(lab["rank"]), int(lab["nranks"])]
                       for _, lab, _ in promtext.samples(fams, "amd_rccl_communicator_info")}
         xgmi = {}
@@ -708,6 +709,7 @@ def main() -> int:
             "workload_gemm_tflops_per_gpu": round(tflops, 1) if tflops else None,
             "rccl_per_pod": rccl,
             "rccl_rank_per_pod": rccl_ranks,
+            "rccl_files": rccl_files or None,  # tracer files by state (active = writer proven)
             "xgmi_bytes_per_second": xgmi,
             # xGMI bytes the exporter's hardware counters saw vs what the DP all-reduce had to
             # move (null at 1 rank: nothing crosses xGMI; null on the mock backend)

@@ -5,6 +5,7 @@
 #include <dlfcn.h>
 #include <fcntl.h>
 #include <poll.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <sys/syscall.h>
 #include <sys/sysmacros.h>
@@ -12,6 +13,7 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -158,28 +160,39 @@ uint64_t proc_starttime(int pid) {
   return std::strtoull(s.c_str() + i, nullptr, 10);
 }
 
-// True if /proc/<pid>/maps has a mapping of the file (dev, ino): proof that `pid` is the
-// process that writes it (the tracer keeps its counters file mapped for its whole life).
-// -1 if the maps file is unreadable (no ptrace-read access to that process).
-int maps_file(int pid, dev_t dev, ino_t ino) {
-  int fd = ::open(("/proc/" + std::to_string(pid) + "/maps").c_str(), O_RDONLY | O_CLOEXEC);
-  if (fd < 0) return errno == EACCES || errno == EPERM ? -1 : 0;
-  std::string all;
+// The identity /proc/<pid>/maps gives a mapped file: device major:minor and inode.
+struct MapsId {
+  unsigned long maj = 0, mn = 0;
+  unsigned long long ino = 0;
+  bool operator==(const MapsId& o) const { return maj == o.maj && mn == o.mn && ino == o.ino; }
+};
+
+// Reads a maps file whole; 0 ok, -1 unreadable for lack of access, -2 other failure.
+int read_maps(const std::string& path, std::string* all) {
+  int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return errno == EACCES || errno == EPERM ? -1 : -2;
   char buf[65536];
   for (;;) {
     ssize_t n = ::read(fd, buf, sizeof(buf));
     if (n < 0 && errno == EINTR) continue;
     if (n <= 0) {
-      if (n < 0 && all.empty()) {
+      if (n < 0 && all->empty()) {
+        const int err = errno;
         ::close(fd);
-        return errno == EACCES || errno == EPERM ? -1 : 0;
+        return err == EACCES || err == EPERM ? -1 : -2;
       }
       break;
     }
-    all.append(buf, size_t(n));
+    all->append(buf, size_t(n));
   }
   ::close(fd);
-  const unsigned want_maj = major(dev), want_min = minor(dev);
+  return 0;
+}
+
+// Calls fn(start address, identity) for each file-backed line of a maps text until fn
+// returns true; returns whether it did.
+template <class F>
+bool scan_maps(const std::string& all, F fn) {
   size_t i = 0;
   while (i < all.size()) {
     size_t e = all.find('\n', i);
@@ -196,16 +209,52 @@ int maps_file(int pid, dev_t dev, ino_t ino) {
     }
     if (f == 5) {
       char* q = nullptr;
-      unsigned long maj = std::strtoul(tok[3], &q, 16);
+      MapsId id;
+      id.maj = std::strtoul(tok[3], &q, 16);
       if (q && *q == ':') {
-        unsigned long mn = std::strtoul(q + 1, nullptr, 16);
-        unsigned long long in = std::strtoull(tok[4], nullptr, 10);
-        if (maj == want_maj && mn == want_min && in == (unsigned long long)ino) return 1;
+        id.mn = std::strtoul(q + 1, nullptr, 16);
+        id.ino = std::strtoull(tok[4], nullptr, 10);
+        if (id.ino && fn(std::strtoull(tok[0], nullptr, 16), id)) return true;
       }
     }
     i = e + 1;
   }
-  return 0;
+  return false;
+}
+
+// The identity /proc/<pid>/maps shows for a mapping of `fd`'s file.  It is not always
+// fstat()'s: on overlayfs (a container's /tmp) maps names the backing upper file's device,
+// fstat() the overlay's (MI355X gpurun box: 00:d1 vs 00:d2, same inode).  So the exporter
+// maps one page of the file itself — read-only and never touched, so a writer truncating
+// it cannot fault us — and reads its own mapping's line.  Falls back to fstat().
+MapsId maps_identity(int fd, const struct stat& st) {
+  MapsId id;
+  id.maj = major(st.st_dev);
+  id.mn = minor(st.st_dev);
+  id.ino = (unsigned long long)st.st_ino;
+  void* p = ::mmap(nullptr, 4096, PROT_READ, MAP_SHARED, fd, 0);
+  if (p == MAP_FAILED) return id;
+  std::string all;
+  if (read_maps("/proc/self/maps", &all) == 0) {
+    const unsigned long long want = (unsigned long long)(uintptr_t)p;
+    scan_maps(all, [&](unsigned long long start, const MapsId& m) {
+      if (start != want) return false;
+      id = m;
+      return true;
+    });
+  }
+  ::munmap(p, 4096);
+  return id;
+}
+
+// True if /proc/<pid>/maps has a mapping of the file with exactly this identity: proof
+// that `pid` is the process that writes it (the tracer keeps its counters file mapped for
+// its whole life).  -1 if the maps file is unreadable (no ptrace-read access to that process).
+int maps_file(int pid, const MapsId& want) {
+  std::string all;
+  const int rc = read_maps("/proc/" + std::to_string(pid) + "/maps", &all);
+  if (rc != 0) return rc == -1 ? -1 : 0;
+  return scan_maps(all, [&](unsigned long long, const MapsId& m) { return m == want; }) ? 1 : 0;
 }
 
 // Reads the RCCL tracer's counter files from a directory that every workload pod can
@@ -259,6 +308,7 @@ class ShmRcclSource : public RcclSource {
         }
         e.dev = fst.st_dev;
         e.ino = fst.st_ino;
+        e.maps_id = maps_identity(e.fd, fst);
       }
       RcclShmFile snap;
       if (!read_consistent(e.fd, &snap) || snap.magic != kRcclShmMagic || snap.pidns_ino != name_ino ||
@@ -320,6 +370,7 @@ class ShmRcclSource : public RcclSource {
     int fd = -1;
     dev_t dev = 0;
     ino_t ino = 0;
+    MapsId maps_id;  // how /proc/<pid>/maps names this file (see maps_identity)
     int host_pid = -1;
     int pidfd = -1;
     uint64_t starttime = 0;
@@ -411,7 +462,7 @@ class ShmRcclSource : public RcclSource {
       const std::string pd = "/proc/" + std::to_string(pid);
       bool ok = pidns_inode(pd) == ns_ino && innermost_nspid(pd) == ns_pid;
       if (ok && verify_maps_) {
-        const int m = maps_file(pid, e->dev, e->ino);
+        const int m = maps_file(pid, e->maps_id);
         if (m < 0 && !warned_maps_) {
           warned_maps_ = true;
           GPUEXP_LOG(LogLevel::kWarn, "rccl",

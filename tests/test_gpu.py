@@ -869,3 +869,48 @@ def test_hip_order_bdfs_match_torch():
         p = torch.cuda.get_device_properties(i)
         dom = getattr(p, "pci_domain_id", 0)
         assert b == f"{dom:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0", (i, b)
+
+
+def test_rccl_tracer_through_exporter(native, tmp_path):
+    """End to end on silicon: a tracer-injected RCCL process writes its counters file and
+    the exporter's RCCL source proves the writer (PID namespace, /proc/<pid>/maps of the
+    file, pidfd) and exports its calls and bytes under that PID while it runs."""
+    from kubernetes_gpu_exporter_amd._native import rccl_tracer_path
+    d = str(tmp_path)
+    port = 29500 + os.getpid() % 1000
+    env = dict(os.environ, ROCP_TOOL_LIBRARIES=rccl_tracer_path(), GPUEXP_RCCL_DIR=d,
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    code = ("import time, torch, torch.distributed as dist\n"
+            "dist.init_process_group('nccl', rank=0, world_size=1)\n"
+            "torch.cuda.set_device(0)\n"
+            "x = torch.ones(1 << 20, device='cuda', dtype=torch.bfloat16)\n"
+            "t = time.time()\n"
+            "while time.time() - t < 6:\n"
+            "    dist.all_reduce(x); torch.cuda.synchronize(); time.sleep(0.01)\n"
+            "dist.destroy_process_group()\n")
+    child = subprocess.Popen([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE,
+                             stderr=subprocess.STDOUT, text=True)
+    e = amdsmi_engine(native, enable_rccl=True, rccl_dir=d, series_profile="full")
+    try:
+        calls, files, listing = 0.0, {}, []
+        deadline = time.time() + 60
+        while time.time() < deadline and child.poll() is None:
+            e.tick()
+            fams = promtext.parse(e.snapshot_text())
+            files = {lab["state"]: v for _, lab, v in promtext.samples(fams, "gpuexp_rccl_files")}
+            for _, lab, v in promtext.samples(fams, "amd_rccl_collective_calls_total"):
+                if lab["op"] == "allreduce":
+                    calls = max(calls, v)
+                    pid = int(lab["pid"])
+            listing = os.listdir(d)
+            if calls >= 10:
+                break
+            time.sleep(0.2)
+        print("tracer files:", listing, "states:", files, "allreduce calls:", calls)
+        assert calls >= 10, (listing, files, e.source_status())
+        assert files.get("active") == 1, files
+        assert pid == child.pid or len(open("/proc/self/status").read().split("NSpid:")[1].split("\n")[0].split()) > 1
+    finally:
+        e.stop()
+        out, _ = child.communicate(timeout=60)
+        print("child:", out.strip()[-500:])
