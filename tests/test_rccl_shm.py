@@ -200,3 +200,49 @@ def test_verification_can_be_relaxed(mock_engine, tmp_path):
     finally:
         p.kill()
         p.wait()
+
+
+def _overlay(tmp_path):
+    """An overlayfs mount under tmp_path (a container's /tmp is one), or None where this
+    process may not mount."""
+    parts = {k: tmp_path / k for k in ("lower", "upper", "work", "merged")}
+    for p in parts.values():
+        p.mkdir()
+    opts = f"lowerdir={parts['lower']},upperdir={parts['upper']},workdir={parts['work']}"
+    r = subprocess.run(["mount", "-t", "overlay", "overlay", "-o", opts, str(parts["merged"])],
+                       capture_output=True, text=True)
+    return parts["merged"] if r.returncode == 0 else None
+
+
+def test_writer_proof_on_overlayfs(mock_engine, tmp_path):
+    """On some kernels' overlayfs /proc/<pid>/maps names the backing upper file's device
+    while fstat() on the overlay path gives the overlay's (the MI355X gpurun boxes' /tmp:
+    profiles/r02/maps_overlay.txt; this container's kernel shows the overlay's in both, so
+    here it is a regression guard): the writer proof must hold for the real writer and still
+    refuse a process that does not map the file.  On silicon the mismatch case is covered by
+    test_gpu.py::test_rccl_tracer_through_exporter."""
+    import pytest
+    merged = _overlay(tmp_path)
+    if merged is None:
+        pytest.skip("cannot mount overlayfs here")
+    try:
+        d = merged / "rccl"
+        d.mkdir()
+        p, path = _writer(d)
+        q, qpath = _writer(d, claim_pid=os.getpid())  # claims this test process
+        try:
+            st = os.stat(path)
+            maps_dev = [l.split()[3] for l in open(f"/proc/{p.pid}/maps") if path.rsplit("/", 1)[1] in l]
+            print("fstat dev", f"{os.major(st.st_dev):02x}:{os.minor(st.st_dev):02x}", "maps dev", maps_dev)
+            e = rccl_engine(mock_engine, d)
+            e.tick(1_000_000_000)
+            fams = promtext.parse(e.snapshot_text())
+            assert promtext.value(fams, "amd_rccl_collective_calls_total", pid=p.pid, op="allreduce") == 5
+            assert states(e) == {"active": 1, "unverified": 1, "exited": 0}
+            e.stop()
+        finally:
+            for w in (p, q):
+                w.kill()
+                w.wait()
+    finally:
+        subprocess.run(["umount", "-l", str(merged)], capture_output=True)
