@@ -417,6 +417,66 @@ def test_pod_energy_tracks_gpu_energy(native):
     assert abs((p1 - p0) - (g1 - g0)) <= 0.02 * (g1 - g0), (p1 - p0, g1 - g0)
 
 
+def test_pod_energy_survives_exporter_restart(native, tmp_path):
+    """Checkpoint/resume on silicon: a GEMM pod's energy total is written to the state file
+    when the exporter stops, comes back in the next exporter before the pod list does, and
+    keeps growing from there (no counter reset for Prometheus to see)."""
+    from kubernetes_gpu_exporter_amd.utils.fakehost import kubepods_cgroup
+    state = str(tmp_path / "state")
+    child = subprocess.Popen([sys.executable, "-c",
+                              "import sys; sys.path.insert(0, %r);"
+                              "from kubernetes_gpu_exporter_amd.ops.gemm import gemm_burn;"
+                              "print(gemm_burn(0, 8192, 8.0, 4), flush=True)" % ROOT],
+                             stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    uid, cid = "0e0e0e0e-0000-4000-8000-000000000002", "cd" * 32
+    pods = [{"uid": uid, "namespace": "ml", "name": "gemm", "containers": {cid: "main"}}]
+
+    def pod_energy(e):
+        f = promtext.parse(e.snapshot_text())
+        v = [s[2] for s in promtext.samples(f, "amd_pod_gpu_energy_joules_total") if s[1]["pod"] == "gemm"]
+        return v[0] if v else None
+
+    a = b = None
+    try:
+        a = amdsmi_engine(native, state_file=state)
+        pid, deadline = None, time.time() + 20
+        while pid is None and time.time() < deadline:
+            a.tick()
+            fams = promtext.parse(a.snapshot_text())
+            big = [int(lab["pid"]) for _, lab, v in promtext.samples(fams, "amd_gpu_process_vram_bytes")
+                   if v > 256 * (1 << 20)]
+            pid = big[0] if big else None
+            time.sleep(0.2)
+        assert pid, "GEMM child not found"
+        a.set_pods(pods)
+        a.set_pid_cgroup(pid, kubepods_cgroup(uid, cid))
+        for _ in range(15):
+            a.tick()
+            time.sleep(0.1)
+        e1 = pod_energy(a)
+        a.stop()  # final checkpoint
+        a = None
+        assert e1 and e1 > 50, e1
+        b = amdsmi_engine(native, state_file=state)
+        assert "restored" in b.source_status(), b.source_status()
+        b.tick()
+        e2 = pod_energy(b)  # before any pod list: the restored total, unchanged
+        b.set_pods(pods)
+        b.set_pid_cgroup(pid, kubepods_cgroup(uid, cid))
+        for _ in range(15):
+            b.tick()
+            time.sleep(0.1)
+        e3 = pod_energy(b)
+    finally:
+        for e in (a, b):
+            if e is not None:
+                e.stop()
+        child.communicate(timeout=60)
+    print(f"pod energy: {e1:.1f} J at stop, {e2:.1f} J restored, {e3:.1f} J after 1.5 s more")
+    assert e2 == pytest.approx(e1, rel=1e-9)
+    assert e3 > e2 + 50  # a busy MI355X draws hundreds of watts
+
+
 _H2D = """
 import json, sys, time, torch
 src = torch.empty(1 << 30, dtype=torch.uint8, pin_memory=True)
