@@ -237,7 +237,10 @@ def main() -> int:
     rccl_dir = ""
     tracer = os.path.join(ROOT, "kubernetes_gpu_exporter_amd", "libgpuexp_rccl_tracer.so")
     if args.rccl_trace and args.backend != "mock" and os.path.exists(tracer) and os.path.exists("/dev/kfd"):
-        run_id = os.environ.get("TORCHELASTIC_RUN_ID") or os.environ.get("MASTER_PORT") or str(os.getpid())
+        # one directory per launch, shared by its ranks (torchrun's static rendezvous names
+        # every run "none", so the port tells back-to-back launches apart)
+        run_id = "-".join(v for v in (os.environ.get("TORCHELASTIC_RUN_ID"), os.environ.get("MASTER_PORT")) if v) \
+            or str(os.getpid())
         rccl_dir = os.path.join(tempfile.gettempdir(), f"gpuexp-bench-rccl-{run_id}")
         os.makedirs(rccl_dir, exist_ok=True)
         os.environ["ROCP_TOOL_LIBRARIES"] = tracer
