@@ -276,7 +276,10 @@ def main() -> int:
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl" if have_gpu and backend != "mock" else "gloo")  # mock: CPU ranks
+        import datetime
+        # a rank that hangs in a collective ends the job in minutes, not after the 10 min default
+        dist.init_process_group("nccl" if have_gpu and backend != "mock" else "gloo",  # mock: CPU ranks
+                                timeout=datetime.timedelta(seconds=300))
     elif have_gpu and backend != "mock" and args.allreduce_mb > 0:
         # N=1 runs the same data-parallel pod (a 1-rank RCCL all-reduce per step), so the
         # workload and the RCCL path are the same at every N.
