@@ -138,6 +138,10 @@ PYBIND11_MODULE(_gpuexp, m) {
 
   m.def("mono_ns", &mono_ns);
   m.def("set_log_level", [](int lvl) { set_log_level(static_cast<LogLevel>(lvl)); });
+  m.def("set_log_json", [](bool json) { set_log_json(json); });
+  m.def("log", [](int lvl, const std::string& component, const std::string& msg) {
+    log_msg(static_cast<LogLevel>(lvl), component.c_str(), msg);
+  });
   m.def("format_value", [](double v) {
     std::string s;
     append_value(&s, v);

@@ -12,23 +12,42 @@
 namespace gpuexp {
 
 static std::atomic<int> g_log_level{static_cast<int>(LogLevel::kWarn)};
+static std::atomic<bool> g_log_json{false};
 static std::mutex g_log_mu;
 
 void set_log_level(LogLevel lvl) { g_log_level.store(static_cast<int>(lvl)); }
 LogLevel log_level() { return static_cast<LogLevel>(g_log_level.load(std::memory_order_relaxed)); }
+void set_log_json(bool json) { g_log_json.store(json); }
 
+// One record per line on stderr, logfmt (default) or JSON (log_format), with the same keys
+// as the Python control plane's records (utils/logfmt.py), so both halves of the exporter
+// interleave into one parseable stream.
 void log_msg(LogLevel lvl, const char* component, const std::string& msg) {
   static const char* names[] = {"debug", "info", "warn", "error", "off"};
   timespec ts;
   clock_gettime(CLOCK_REALTIME, &ts);
+  const bool json = g_log_json.load(std::memory_order_relaxed);
   std::lock_guard<std::mutex> lk(g_log_mu);
-  std::fprintf(stderr, "ts=%ld.%03ld level=%s component=%s msg=\"", long(ts.tv_sec),
-               long(ts.tv_nsec / 1000000), names[static_cast<int>(lvl)], component);
+  if (json)
+    std::fprintf(stderr, "{\"ts\":%ld.%03ld,\"level\":\"%s\",\"component\":\"%s\",\"msg\":\"", long(ts.tv_sec),
+                 long(ts.tv_nsec / 1000000), names[static_cast<int>(lvl)], component);
+  else
+    std::fprintf(stderr, "ts=%ld.%03ld level=%s component=%s msg=\"", long(ts.tv_sec),
+                 long(ts.tv_nsec / 1000000), names[static_cast<int>(lvl)], component);
   for (char c : msg) {
-    if (c == '"' || c == '\\') std::fputc('\\', stderr);
-    std::fputc(c == '\n' ? ' ' : c, stderr);
+    const unsigned char u = static_cast<unsigned char>(c);
+    if (c == '"' || c == '\\') {
+      std::fputc('\\', stderr);
+      std::fputc(c, stderr);
+    } else if (c == '\n') {
+      std::fputc(' ', stderr);
+    } else if (json && u < 0x20) {
+      std::fprintf(stderr, "\\u%04x", u);  // JSON forbids raw control characters
+    } else {
+      std::fputc(c, stderr);
+    }
   }
-  std::fputs("\"\n", stderr);
+  std::fputs(json ? "\"}\n" : "\"\n", stderr);
 }
 
 bool read_small_file(const std::string& path, std::string* out, size_t max_bytes) {

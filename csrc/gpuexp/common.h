@@ -35,6 +35,7 @@ inline uint64_t thread_cpu_ns() {
 enum class LogLevel : int { kDebug = 0, kInfo = 1, kWarn = 2, kError = 3, kOff = 4 };
 void set_log_level(LogLevel lvl);
 LogLevel log_level();
+void set_log_json(bool json);  // records as JSON objects instead of logfmt
 void log_msg(LogLevel lvl, const char* component, const std::string& msg);
 
 #define GPUEXP_LOG(lvl, comp, msg)                                    \

@@ -8,7 +8,7 @@ from .utils import logfmt
 
 def main(argv=None) -> int:
     cfg = load_config(argv)
-    logfmt.setup(cfg.log_level)  # same line format as the C++ core
+    logfmt.setup(cfg.log_level, cfg.log_format)  # same record format as the C++ core
     return Exporter(cfg).run_forever()
 
 

@@ -79,6 +79,7 @@ class Config:
     control_timeout: float = 3.0           # per-call timeout for gRPC / apiserver
     # diagnostics
     log_level: str = "warn"
+    log_format: str = "logfmt"             # logfmt | json (both the C++ core and the control plane)
     trace: str = ""                        # Chrome trace JSON of sampler stages
 
     def listen_host_port(self) -> tuple[str, int]:
@@ -278,6 +279,8 @@ def validate(cfg: Config) -> None:
         raise ValueError("mock_devices must be >= 1")
     if cfg.log_level not in ("debug", "info", "warn", "error", "off"):
         raise ValueError("log_level must be debug|info|warn|error|off")
+    if cfg.log_format not in ("logfmt", "json"):
+        raise ValueError("log_format must be logfmt|json")
     if cfg.sentinel_impl not in ("auto", "hip", "queue"):
         raise ValueError(f"sentinel_impl must be auto|hip|queue, got {cfg.sentinel_impl}")
     if cfg.stale_after < 0 and cfg.stale_after != -1:

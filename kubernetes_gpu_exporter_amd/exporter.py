@@ -27,6 +27,7 @@ class Exporter:
         self.cfg = cfg
         self.native = load()
         self.native.set_log_level(_LEVELS[cfg.log_level])
+        self.native.set_log_json(cfg.log_format == "json")
         self.engine = self.native.Engine(cfg.to_engine_config(self.native))
         self._control = control_plane
         self._stop = threading.Event()

@@ -128,3 +128,31 @@ def test_python_logs_are_logfmt_like_the_core(capsys):
     assert len(err) == 1, err
     assert re.fullmatch(r'ts=\d+\.\d{3} level=warn component=control msg="source \\"x\\" failed: boom \\\\ done"',
                         err[0]), err[0]
+
+
+def test_json_log_format_from_both_halves(capfd, native):
+    """log_format=json: the C++ core and the Python control plane both write one JSON object
+    per line with the same keys (escaped quotes, backslashes and control characters)."""
+    import json
+    import logging
+
+    from kubernetes_gpu_exporter_amd.utils import logfmt
+    assert make_config({"log_format": "json"}).log_format == "json"
+    with pytest.raises(ValueError):
+        make_config({"log_format": "xml"})
+    logfmt.setup("info", "json")
+    native.set_log_json(True)
+    try:
+        native.log(2, "sampler", 'gpu "0" \\ read\x01failed\nretrying')
+        logging.getLogger("gpuexp.control").warning('source "x"\nfailed')
+    finally:
+        native.set_log_json(False)
+        logfmt.setup("warn")
+    lines = [l for l in capfd.readouterr().err.splitlines() if l.strip()]
+    recs = [json.loads(l) for l in lines]
+    assert [sorted(r) for r in recs] == [["component", "level", "msg", "ts"]] * 2, lines
+    core, py = recs
+    assert core["component"] == "sampler" and core["level"] == "warn"
+    assert core["msg"] == 'gpu "0" \\ read\x01failed retrying'
+    assert py["component"] == "control" and py["msg"] == 'source "x" failed'
+    assert abs(core["ts"] - py["ts"]) < 60
