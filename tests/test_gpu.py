@@ -913,7 +913,9 @@ def test_raw_metrics_path_and_pmfw_coalescing(native):
     # tick and the next fresh read waits one more tick); never all of them
     assert 0.3 < frac < 0.75, reads
     (period,) = [s[2] for s in promtext.samples(fams, "gpuexp_gpu_metrics_refresh_period_seconds")]
-    assert 0.015 < period < 0.03, period
+    # ~20 ms on most boxes; one idle box's firmware stepped every 30.0 ms (learnt 0.0300036 s):
+    # the learnt value follows the firmware, so accept anything up to the reuse cap (50 ms)
+    assert 0.015 < period < 0.05, period
     # fresh reads track the refresh rate, not the tick rate: at most one per refresh period
     assert reads["fresh"] * period < 2.0 * 1.5, (reads, period)
 
