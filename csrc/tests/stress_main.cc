@@ -3,6 +3,8 @@
 //   - HTTP server with 2 SO_REUSEPORT loops
 //   - N scraper threads on keep-alive connections (plus one gzip scraper)
 //   - a control-plane thread swapping pods / cgroup overrides / process lists / faults
+//   - an RCCL-tracer stand-in that rewrites, truncates and replaces its counters file
+//     (the exporter's writer proof maps the file itself, see optional_sources.cc)
 // Every response must be a complete exposition whose tick counter never goes backwards.
 // SURVEY.md §5 "Race detection / sanitizers": sampler vs HTTP vs attribution updates.
 #include <atomic>
@@ -12,10 +14,14 @@
 #include <thread>
 #include <vector>
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include "gpuexp/client.h"
 #include "gpuexp/engine.h"
+#include "gpuexp/rccl_shm.h"
 
 using namespace gpuexp;
 
@@ -57,6 +63,10 @@ int main(int argc, char** argv) {
   cfg.series_profile = "full";  // every family, KFD events and per-pod energy included
   cfg.state_file = "/tmp/gpuexp-stress-state-" + std::to_string(::getpid());  // checkpoint every 50 ms
   cfg.state_interval_s = 0.05;
+  char rccl_tmpl[] = "/tmp/gpuexp-stress-rccl-XXXXXX";
+  const std::string rccl_dir = ::mkdtemp(rccl_tmpl) ? rccl_tmpl : "";
+  cfg.enable_rccl = !rccl_dir.empty();
+  cfg.rccl_dir = rccl_dir;
   cfg.http.host = "127.0.0.1";
   cfg.http.port = 0;
   cfg.http.threads = 2;
@@ -68,7 +78,7 @@ int main(int argc, char** argv) {
   }
   int port = e.http_port();
   std::atomic<bool> stop{false};
-  std::atomic<long> scrapes{0}, bad{0};
+  std::atomic<long> scrapes{0}, bad{0}, rccl_seen{0};
 
   std::vector<std::thread> th;
   for (int s = 0; s < scrapers; ++s) {
@@ -90,6 +100,7 @@ int main(int argc, char** argv) {
         }
         const std::string& b = c.last_body();
         double t = ticks_in(b);
+        if (b.find("\namd_rccl_collective_calls_total{") != std::string::npos) rccl_seen.fetch_add(1);
         if (b.compare(0, 7, "# HELP ") != 0 || b.back() != '\n' || t < last) bad.fetch_add(1);
         last = t;
       }
@@ -125,13 +136,58 @@ int main(int argc, char** argv) {
       std::this_thread::sleep_for(std::chrono::milliseconds(3));
     }
   });
+  struct stat ns_st {};
+  const bool have_ns = ::stat("/proc/self/ns/pid", &ns_st) == 0;
+  const std::string rccl_path = rccl_dir + "/gpuexp-rccl-" + std::to_string(uint64_t(ns_st.st_ino)) + "-" +
+                                std::to_string(::getpid());
+  if (cfg.enable_rccl && have_ns) {
+    th.emplace_back([&] {
+      // The tracer's life cycle, compressed: create + map + publish, count, then either
+      // truncate the file under the reader or unlink it and start over with a new inode.
+      for (unsigned k = 0; !stop.load(); ++k) {
+        int fd = ::open(rccl_path.c_str(), O_RDWR | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+        if (fd < 0) return;
+        if (::ftruncate(fd, sizeof(RcclShmFile)) != 0) {
+          ::close(fd);
+          return;
+        }
+        void* p = ::mmap(nullptr, sizeof(RcclShmFile), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        ::close(fd);
+        if (p == MAP_FAILED) return;
+        auto* f = static_cast<RcclShmFile*>(p);
+        f->version = 1;
+        f->ns_pid = int32_t(::getpid());
+        f->pidns_ino = uint64_t(ns_st.st_ino);
+        f->rank = 0;
+        f->nranks = 2;
+        __atomic_store_n(&f->magic, kRcclShmMagic, __ATOMIC_RELEASE);
+        for (int i = 0; i < 100 && !stop.load(); ++i) {
+          f->ops[0].calls.fetch_add(1, std::memory_order_relaxed);
+          f->ops[0].bytes.fetch_add(1u << 20, std::memory_order_relaxed);
+          std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        }
+        ::munmap(p, sizeof(RcclShmFile));
+        if (k % 2 == 0) {
+          if (::truncate(rccl_path.c_str(), 8) != 0) return;  // short file: must be skipped, not fault
+        } else {
+          ::unlink(rccl_path.c_str());  // replaced by a new inode next round
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(15));
+      }
+    });
+  }
   std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
   stop.store(true);
   for (auto& t : th) t.join();
   EngineStats st = e.stats();
   e.stop();
   std::remove(cfg.state_file.c_str());
-  std::printf("ticks=%llu scrapes=%ld bad=%ld series=%llu render_bytes=%llu\n", (unsigned long long)st.ticks,
-              scrapes.load(), bad.load(), (unsigned long long)st.series, (unsigned long long)st.render_bytes);
+  if (!rccl_dir.empty()) {
+    ::unlink(rccl_path.c_str());
+    ::rmdir(rccl_dir.c_str());
+  }
+  std::printf("ticks=%llu scrapes=%ld bad=%ld series=%llu render_bytes=%llu rccl_scrapes=%ld\n",
+              (unsigned long long)st.ticks, scrapes.load(), bad.load(), (unsigned long long)st.series,
+              (unsigned long long)st.render_bytes, rccl_seen.load());
   return (bad.load() == 0 && scrapes.load() > 100 && st.ticks > 10) ? 0 : 1;
 }
