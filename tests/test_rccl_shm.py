@@ -209,8 +209,11 @@ def _overlay(tmp_path):
     for p in parts.values():
         p.mkdir()
     opts = f"lowerdir={parts['lower']},upperdir={parts['upper']},workdir={parts['work']}"
-    r = subprocess.run(["mount", "-t", "overlay", "overlay", "-o", opts, str(parts["merged"])],
-                       capture_output=True, text=True)
+    try:
+        r = subprocess.run(["mount", "-t", "overlay", "overlay", "-o", opts, str(parts["merged"])],
+                           capture_output=True, text=True, timeout=30)
+    except (OSError, subprocess.TimeoutExpired):  # no mount(8), or it hung
+        return None
     return parts["merged"] if r.returncode == 0 else None
 
 
