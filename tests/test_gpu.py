@@ -939,7 +939,10 @@ def test_rccl_tracer_through_exporter(native, tmp_path):
     file, pidfd) and exports its calls and bytes under that PID while it runs."""
     from kubernetes_gpu_exporter_amd._native import rccl_tracer_path
     d = str(tmp_path)
-    port = 29500 + os.getpid() % 1000
+    import socket
+    with socket.socket() as s:  # a free port for the child's TCP store
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
     env = dict(os.environ, ROCP_TOOL_LIBRARIES=rccl_tracer_path(), GPUEXP_RCCL_DIR=d,
                MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
     code = ("import time, torch, torch.distributed as dist\n"
