@@ -66,6 +66,7 @@ def test_bench_self_launches_one_rank_per_gpu():
     assert d["server_scrapes"] >= 3 and d["server_scrape_p99_le_us"] > 0
     assert d["sampler_cpu_us_per_tick_per_gpu"] > 0 and d["exporter_rss_mb"] > 0
     assert "measured_over_expected_write" in d["xgmi_timed_window"]
+    assert "rccl_files" in d  # tracer file states (None on the mock backend: no tracer)
     # untimed pattern phase: ring + all-to-all ran on all ranks; per-rank link bytes are
     # joined to peer ranks through the peer_bdf labels (mock links: synthetic bytes)
     pat = d["xgmi_patterns"]
