@@ -2,9 +2,11 @@
 """Headline benchmark (BASELINE.json): p50 scrape latency + exporter CPU% at N MI355X,
 10 Hz, 64 series/GPU, under synthetic HIP-workload pods.
 
-One rank per GPU (torchrun for N>1).  Rank 0 starts the exporter as a separate process
-BEFORE touching the GPU (amdsmi backend, raw gpu_metrics fast path, HIP sentinel,
-aqlprofile device counters, full series profile, 10 Hz sampling, every GPU of the job), then every rank becomes a synthetic "GEMM pod":
+One rank per GPU: under torchrun, or started by this script itself for `--gpus N` > 1
+(the parent never touches the GPU).  Rank 0 starts the exporter as a separate process
+BEFORE touching the GPU (amdsmi backend, raw gpu_metrics fast path, sentinel kernel on the
+aqlprofile PMC queue, full series profile, 10 Hz sampling, every GPU of the job), then
+every rank becomes a synthetic "GEMM pod":
 each step it launches a burst of bf16 MFMA GEMMs (our HIP kernel) and an RCCL all-reduce
 (DP gradient traffic over xGMI; a 1-rank all-reduce at N=1).  The RCCL tracer tool is
 injected into every rank, so collective calls/bytes are attributed per pod as well.  Rank 0 scrapes /metrics once per step over a
