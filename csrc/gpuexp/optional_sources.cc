@@ -316,16 +316,20 @@ class ShmRcclSource : public RcclSource {
         continue;  // not (yet) a complete file, or one whose content disagrees with its name
       }
       if (e.host_pid > 0 && !alive(&e)) {
-        release_owner(&e);  // writer exited (or was killed): its leftover file is not exported
+        close_entry(&e);  // writer exited (or was killed): its leftover file is not exported
         e.state = kExited;
         e.fails = 0;
         backoff(&e, now);  // re-identify later: a new writer may reuse the name (O_TRUNC)
+        continue;
       }
       if (e.host_pid <= 0) {
         if (now < e.retry_ns) continue;
         if (!identify(&e, snap.pidns_ino, snap.ns_pid)) {
           if (e.state != kExited) e.state = kUnverified;
           backoff(&e, now);
+          // no fd is held for a file nobody is proven to write: files left by killed pods
+          // (or planted by a hostile one) cost a directory entry check per poll, not an fd
+          close_entry(&e);
           continue;
         }
         e.state = kActive;

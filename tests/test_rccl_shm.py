@@ -162,6 +162,9 @@ def test_writer_cannot_claim_another_process(mock_engine, tmp_path):
         e.tick(1)
         assert "amd_rccl_collective" not in e.snapshot_text()
         assert states(e)["unverified"] == 1
+        held = [f for f in os.listdir("/proc/self/fd")
+                if os.path.realpath(f"/proc/self/fd/{f}") == os.path.realpath(path)]
+        assert not held, held  # an unproven file holds no fd either
     finally:
         p.kill()
         p.wait()
@@ -186,6 +189,9 @@ def test_killed_writer_file_stops_counting(mock_engine, tmp_path):
     assert states(e) == {"active": 0, "unverified": 0, "exited": 1}
     e.tick(3_000_000_000)
     assert "amd_rccl_collective_calls_total" not in e.snapshot_text()
+    # a leftover file holds no fd in the exporter (killed pods must not grow its fd count)
+    held = [f for f in os.listdir("/proc/self/fd") if os.path.realpath(f"/proc/self/fd/{f}") == os.path.realpath(path)]
+    assert not held, held
 
 
 def test_verification_can_be_relaxed(mock_engine, tmp_path):
