@@ -443,11 +443,14 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("sentinel_spin", &EngineConfig::sentinel_spin)
       .def_readwrite("enable_counters", &EngineConfig::enable_counters)
       .def_readwrite("counters_plugin", &EngineConfig::counters_plugin)
+      .def_readwrite("counters_mode", &EngineConfig::counters_mode)
+      .def_readwrite("counters_sync_us", &EngineConfig::counters_sync_us)
       .def_readwrite("counters_window_ms", &EngineConfig::counters_window_ms)
       .def_readwrite("counters_interval_ms", &EngineConfig::counters_interval_ms)
       .def_readwrite("enable_rccl", &EngineConfig::enable_rccl)
       .def_readwrite("rccl_dir", &EngineConfig::rccl_dir)
       .def_readwrite("rccl_verify", &EngineConfig::rccl_verify)
+      .def_readwrite("rccl_scan_interval_s", &EngineConfig::rccl_scan_interval_s)
       .def_readwrite("enable_kfd_events", &EngineConfig::enable_kfd_events)
       .def_readwrite("firmware_info", &EngineConfig::firmware_info)
       .def_readwrite("state_file", &EngineConfig::state_file)

@@ -9,12 +9,19 @@
 //   * one low-priority AQL queue of 64 slots (shared with the sentinel, see below),
 //   * one interrupt-backed completion signal (waited on BLOCKED — no polling thread),
 //   * a command buffer and a PMC output buffer in fine-grained system memory,
-// and a background thread duty-cycles a counting window per interval:
-//   start packet -> wait -> sleep(window) -> read packet -> wait -> stop packet -> wait
-//   -> iterate output.
+// and a background thread runs the counting in one of two modes:
+//   continuous (default): one start packet at init, then one read packet per engine tick
+//     (gpuexp_rp_kick at the tick's start; gpuexp_rp_sync before the tick exports), so
+//     every tick exports the deltas over exactly its own interval and no wall time goes
+//     uncounted.  What a read does to running counters (keep counting / reset / stop) is
+//     probed on the GPU at init (read_semantics) rather than assumed.
+//   duty: start packet -> wait -> sleep(window) -> read packet -> wait -> stop packet ->
+//     wait -> iterate output, one window per interval (the round-1/2 behaviour).
 // Measured on MI355X (profiles/r01/counters_aqlpmc.txt): same counter values as the
-// rocprofiler-sdk path, exporter CPU 0.3-0.7% instead of 101%.
-// The engine's tick never blocks on the GPU: gpuexp_rp_sample returns the latest window.
+// rocprofiler-sdk path, exporter CPU 0.3-0.7% instead of 101%; continuous vs duty costs:
+// profiles/r03/pmc_continuous_cost.txt.
+// The engine's tick never blocks on the GPU beyond a bounded sync: gpuexp_rp_sample returns
+// the latest completed window.
 //
 // Event ids are the gfx950 select values of /opt/rocm/share/rocprofiler-sdk/counter_defs.yaml
 // (SQ 93/3/4/147/142, GRBM 2/0, TCC 112/115/113/117) and are checked with
@@ -40,6 +47,8 @@
 
 #include <dlfcn.h>
 #include <fcntl.h>
+#include <sys/prctl.h>
+#include <time.h>
 #include <unistd.h>
 
 #include "gpuexp/counter_model.h"
@@ -67,7 +76,7 @@ const EventDef kGfx950[] = {
     {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 142, kLdsConflict}, {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, 2, kGuiActive},
     {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, 0, kGrbmCount},  {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 112, kDramRd32},
     {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 115, kDramWr32},  {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 113, kGmiRd32},
-    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 117, kGmiWr32},
+    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 117, kGmiWr32},  {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 2, kSqCycles},
 };
 
 struct Agent {
@@ -84,14 +93,32 @@ struct Agent {
   void* cmd_buf = nullptr;
   void* out_buf = nullptr;
   bool ready = false;
-  bool broken = false;      // a packet timed out: the GPU may still own the buffers
+  std::atomic<bool> broken{false};  // a packet timed out: the GPU may still own the buffers
   std::atomic<bool> queue_error{false};
   // The queue has two producers: the counting thread (PM4 programs) and the sampler
   // thread (sentinel kernel dispatches, gpuexp_make_hsa_sentinel).
   std::mutex submit_mu;
+  // Continuous mode: the counters as of the last read (cumulative semantics) and when
+  // that read executed (the start of the next window).
+  double cum[kNumCtr] = {};
+  bool have_cum = false;
+  Clock::time_point t_last{};
+  Clock::time_point t_submit{};
+  // Continuous mode: a read packet that has not completed yet (the queue is stalled, e.g.
+  // behind a sentinel dispatch the workload's waves leave no room for).  It is waited for
+  // again next round instead of giving the GPU up; t_checked = when it was last seen pending.
+  bool read_inflight = false;
+  Clock::time_point t_checked{};
+  std::atomic<uint64_t> stalls{0};  // rounds in which this GPU's read had not completed
+  std::atomic<uint64_t> resets{0};  // windows dropped because a counter went backwards (wrap / reset)
+  // Written by the counting thread, read by gpuexp_rp_sample / _debug (m_mu).
+  std::mutex m_mu;
   double last_raw[kNumCtr] = {};
   int last_inst[kNumCtr] = {};
   uint64_t last_samples = 0;
+  double last_window_s = 0;
+  double pub_cum[kNumCtr] = {};  // continuous, cumulative reads: raw totals since counting started
+  Clock::time_point t_window_end{};  // continuous: end of the last published window
   Derived m;
 };
 
@@ -126,6 +153,27 @@ std::thread g_thread;
 std::atomic<bool> g_quit{false};
 std::condition_variable g_cv;
 std::mutex g_cv_mu;
+// Continuous mode (gpuexp_rp_set_continuous): counting is started once and never stopped;
+// the engine kicks one read round per tick (g_kick_seq), and gpuexp_rp_sync waits for it
+// (g_done_seq, g_done_cv).  All three under g_cv_mu.
+bool g_continuous = false;
+uint64_t g_kick_seq = 0, g_done_seq = 0;
+std::condition_variable g_done_cv;
+std::atomic<uint64_t> g_thread_cpu_ns{0};  // the counting thread's own CPU, published per round
+
+uint64_t own_cpu_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
+}
+// What a read packet does to the counters, probed on the GPU at init (read_semantics):
+// kCumulative: they keep counting (deltas of successive reads); kResets: each read returns
+// the counts since the previous read; kStops: counting stops at a read (re-armed after).
+enum ReadMode { kReadUnknown, kCumulative, kResets, kStops };
+ReadMode g_read_mode = kReadUnknown;
+const char* read_mode_name(ReadMode m) {
+  return m == kCumulative ? "cumulative" : m == kResets ? "resets at read" : m == kStops ? "stops at read" : "?";
+}
 
 std::string lower(std::string s) {
   for (auto& c : s) c = char(::tolower(c));
@@ -188,8 +236,12 @@ void* sys_alloc(size_t bytes, hsa_agent_t gpu) {
 }
 
 // Writes one vendor-specific AQL packet and rings the doorbell.  At most one PM4 packet and
-// four sentinel dispatches are ever in flight on the 64-slot queue, so it never fills.
-void submit(Agent& a, const hsa_ext_amd_aql_pm4_packet_t& pkt) {
+// one sentinel dispatch are ever in flight on the 64-slot queue, so it never fills.
+// barrier=false lets the packet processor run it without waiting for earlier packets to
+// COMPLETE: the continuous read packets use that, so a sentinel dispatch that cannot get a
+// SIMD (measured: next to waves issuing MFMAs back-to-back for seconds, even at wave
+// priority 3) does not hold the counter reads behind it.
+void submit(Agent& a, const hsa_ext_amd_aql_pm4_packet_t& pkt, bool barrier = true) {
   std::lock_guard<std::mutex> lk(a.submit_mu);
   hsa_queue_t* q = a.queue;
   const uint64_t idx = hsa_queue_add_write_index_screlease(q, 1);
@@ -197,7 +249,7 @@ void submit(Agent& a, const hsa_ext_amd_aql_pm4_packet_t& pkt) {
   std::memcpy(slot->pm4_command, pkt.pm4_command, sizeof(pkt.pm4_command));
   slot->completion_signal = a.sig;
   const uint16_t header = uint16_t((HSA_PACKET_TYPE_VENDOR_SPECIFIC << HSA_PACKET_HEADER_TYPE) |
-                                   (1 << HSA_PACKET_HEADER_BARRIER) |
+                                   ((barrier ? 1 : 0) << HSA_PACKET_HEADER_BARRIER) |
                                    (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                                    (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
   __atomic_store_n(&slot->header, header, __ATOMIC_RELEASE);
@@ -206,15 +258,24 @@ void submit(Agent& a, const hsa_ext_amd_aql_pm4_packet_t& pkt) {
 
 // Submits `pkt`, waits (interrupt-driven) up to 1 s; returns the midpoint of submit and
 // completion (the packet's execution time estimate), or a default time_point on timeout.
-Clock::time_point run_packet(Agent& a, const hsa_ext_amd_aql_pm4_packet_t& pkt) {
+// Split form, so one round can have a packet in flight on every GPU at once.
+void post_packet(Agent& a, const hsa_ext_amd_aql_pm4_packet_t& pkt, bool barrier = true) {
   hsa_signal_store_relaxed(a.sig, 1);
-  const auto t0 = Clock::now();
-  submit(a, pkt);
+  a.t_submit = Clock::now();
+  submit(a, pkt, barrier);
+}
+
+Clock::time_point wait_packet(Agent& a) {
   const hsa_signal_value_t v =
       hsa_signal_wait_scacquire(a.sig, HSA_SIGNAL_CONDITION_LT, 1, g_ts_freq, HSA_WAIT_STATE_BLOCKED);
   const auto t1 = Clock::now();
   if (v >= 1 || a.queue_error.load()) return {};
-  return t0 + (t1 - t0) / 2;
+  return a.t_submit + (t1 - a.t_submit) / 2;
+}
+
+Clock::time_point run_packet(Agent& a, const hsa_ext_amd_aql_pm4_packet_t& pkt) {
+  post_packet(a, pkt);
+  return wait_packet(a);
 }
 
 struct Accum {
@@ -325,7 +386,14 @@ bool setup_agent(Agent& a, std::string* why) {
     return false;
   }
   crumb("queue created");
-  hsa_amd_queue_set_priority(a.queue, HSA_AMD_QUEUE_PRIORITY_LOW);
+  {
+    // experiment knob (profiles/r03/mfma_calibration.txt): low | normal | high
+    const char* pr = std::getenv("GPUEXP_PMC_QUEUE_PRIORITY");
+    const std::string p = pr ? pr : "low";
+    hsa_amd_queue_set_priority(a.queue, p == "high"     ? HSA_AMD_QUEUE_PRIORITY_HIGH
+                                        : p == "normal" ? HSA_AMD_QUEUE_PRIORITY_NORMAL
+                                                        : HSA_AMD_QUEUE_PRIORITY_LOW);
+  }
   if (hsa_signal_create(1, 0, nullptr, &a.sig) != HSA_STATUS_SUCCESS) {
     *why = "hsa_signal_create failed";
     return false;
@@ -342,25 +410,44 @@ bool setup_agent(Agent& a, std::string* why) {
   return true;
 }
 
+// The counting thread is the only user of an agent's signal and PM4 packets once the
+// thread runs; g_agents itself changes only before it starts and after it is joined, so
+// rounds take no global lock (gpuexp_rp_sample never waits behind a GPU round trip).
+bool usable(const Agent* a) { return a && a->ready && !a->broken.load(); }
+
+// Reads the output buffer the last read packet filled: reduced value + instances per counter.
+bool collect(Agent& a, Accum* acc) {
+  *acc = Accum{&a, {}, {}, 0};
+  return g_aql.hsa_ven_amd_aqlprofile_iterate_data(&a.profile, on_data, acc) == HSA_STATUS_SUCCESS;
+}
+
+void publish(Agent& a, const double* d, const Accum& acc, double wall, Clock::time_point end = {},
+             const double* cum = nullptr) {
+  std::lock_guard<std::mutex> lk(a.m_mu);
+  a.t_window_end = end;
+  if (cum) std::memcpy(a.pub_cum, cum, sizeof(a.pub_cum));
+  std::memcpy(a.last_raw, d, sizeof(a.last_raw));
+  std::memcpy(a.last_inst, acc.inst, sizeof(acc.inst));
+  a.last_samples = acc.samples;
+  a.last_window_s = wall;
+  if (wall > 0) derive(a.m, d, acc.inst, wall);
+}
+
 void window_all() {
   std::vector<Clock::time_point> t0(g_agents.size());
-  {
-    std::lock_guard<std::mutex> lk(g_mu);
-    for (size_t i = 0; i < g_agents.size(); ++i) {
-      Agent* a = g_agents[i];
-      if (!a || !a->ready || a->broken) continue;
-      if (g_debug) std::memset(a->out_buf, 0x5A, a->out_size);  // unwritten samples show as 0x5A5A..
-      t0[i] = run_packet(*a, a->start_pkt);
-      if (t0[i] == Clock::time_point{}) a->broken = true;
-    }
+  for (size_t i = 0; i < g_agents.size(); ++i) {
+    Agent* a = g_agents[i];
+    if (!usable(a)) continue;
+    if (g_debug) std::memset(a->out_buf, 0x5A, a->out_size);  // unwritten samples show as 0x5A5A..
+    t0[i] = run_packet(*a, a->start_pkt);
+    if (t0[i] == Clock::time_point{}) a->broken = true;
   }
   std::unique_lock<std::mutex> wl(g_cv_mu);
   g_cv.wait_for(wl, std::chrono::milliseconds(g_window_ms), [] { return g_quit.load(); });
   wl.unlock();
-  std::lock_guard<std::mutex> lk(g_mu);
   for (size_t i = 0; i < g_agents.size(); ++i) {
     Agent* a = g_agents[i];
-    if (!a || !a->ready || a->broken || t0[i] == Clock::time_point{}) continue;
+    if (!usable(a) || t0[i] == Clock::time_point{}) continue;
     // The read packet copies the counters to the output buffer (measured: the stop packet
     // alone leaves it untouched); stop then disables counting until the next window.
     const auto t1 = run_packet(*a, a->read_pkt);
@@ -368,20 +455,150 @@ void window_all() {
       a->broken = true;
       continue;
     }
-    Accum acc{a, {}, {}, 0};
-    if (g_aql.hsa_ven_amd_aqlprofile_iterate_data(&a->profile, on_data, &acc) != HSA_STATUS_SUCCESS) continue;
-    const double wall = std::chrono::duration<double>(t1 - t0[i]).count();
-    std::memcpy(a->last_raw, acc.v, sizeof(acc.v));
-    std::memcpy(a->last_inst, acc.inst, sizeof(acc.inst));
-    a->last_samples = acc.samples;
-    if (wall > 0) derive(a->m, acc.v, acc.inst, wall);
+    Accum acc;
+    if (!collect(*a, &acc)) continue;
+    publish(*a, acc.v, acc, std::chrono::duration<double>(t1 - t0[i]).count());
   }
 }
 
+// Continuous mode, one round: a read packet in flight on every GPU at once, then per GPU
+// the window since its previous read.  Counting itself never pauses (kStops: re-armed
+// right after the read, a gap of one PM4 packet).
+void read_round() {
+  const auto begin = Clock::now();
+  // a stalled GPU costs the round at most this long (the other GPUs' reads are in flight)
+  const auto deadline = begin + std::chrono::milliseconds(std::min(1000, g_interval_ms));
+  for (Agent* a : g_agents)
+    if (usable(a) && !a->read_inflight) {
+      post_packet(*a, a->read_pkt, /*barrier=*/false);
+      a->read_inflight = true;
+      a->t_checked = a->t_submit;
+    }
+  for (Agent* a : g_agents) {
+    if (!usable(a) || !a->read_inflight) continue;
+    const double left = std::chrono::duration<double>(deadline - Clock::now()).count();
+    const uint64_t ticks = left > 0 ? uint64_t(left * double(g_ts_freq)) : 0;
+    const hsa_signal_value_t v = hsa_signal_wait_scacquire(a->sig, HSA_SIGNAL_CONDITION_LT, 1, ticks,
+                                                           HSA_WAIT_STATE_BLOCKED);
+    const auto now = Clock::now();
+    if (a->queue_error.load()) {
+      a->broken = true;
+      continue;
+    }
+    if (v >= 1) {  // still queued: try again next round, the counters keep running
+      a->t_checked = now;
+      ++a->stalls;
+      continue;
+    }
+    a->read_inflight = false;
+    // the read executed between the last time it was seen pending and now
+    const auto t = a->t_checked + (now - a->t_checked) / 2;
+    Accum acc;
+    if (!collect(*a, &acc)) continue;
+    const double wall = std::chrono::duration<double>(t - a->t_last).count();
+    if (g_read_mode == kCumulative) {
+      double d[kNumCtr];
+      bool backwards = false;
+      for (int k = 0; k < kNumCtr; ++k) {
+        d[k] = acc.v[k] - a->cum[k];
+        backwards = backwards || d[k] < 0;
+      }
+      const bool first = !a->have_cum;
+      std::memcpy(a->cum, acc.v, sizeof(a->cum));
+      a->have_cum = true;
+      a->t_last = t;
+      if (backwards) ++a->resets;  // wrapped or reset under us: this window is unknown
+      if (!first && !backwards) publish(*a, d, acc, wall, t, acc.v);
+    } else {
+      publish(*a, acc.v, acc, wall, t);
+      a->t_last = t;
+      if (g_read_mode == kStops) {
+        const auto ts = run_packet(*a, a->start_pkt);
+        if (ts == Clock::time_point{}) a->broken = true;
+        else a->t_last = ts;
+      }
+    }
+  }
+}
+
+// Starts counting on `a` for good: start packet, then (cumulative) the baseline read.
+bool arm_continuous(Agent& a) {
+  const auto ts = run_packet(a, a.start_pkt);
+  if (ts == Clock::time_point{}) return false;
+  a.t_last = ts;
+  a.have_cum = false;
+  if (g_read_mode == kCumulative) {
+    const auto tr = run_packet(a, a.read_pkt);
+    Accum acc;
+    if (tr == Clock::time_point{} || !collect(a, &acc)) return false;
+    std::memcpy(a.cum, acc.v, sizeof(a.cum));
+    a.have_cum = true;
+    a.t_last = tr;
+  }
+  return true;
+}
+
+// What does a read packet do to running counters?  GRBM_COUNT is the free-running GRBM
+// clock, so over start, 5 ms, read, 5 ms, read it reads c1 then either ~2 c1 (still
+// counting), ~c1 (reset by the read) or exactly c1 (stopped by the read).
+ReadMode read_semantics(Agent& a, std::string* why) {
+  const auto ts = run_packet(a, a.start_pkt);
+  double c[2] = {0, 0};
+  Clock::time_point t[2];
+  for (int i = 0; i < 2; ++i) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    t[i] = run_packet(a, a.read_pkt);
+    Accum acc;
+    if (ts == Clock::time_point{} || t[i] == Clock::time_point{} || !collect(a, &acc)) {
+      *why = "PM4 read packet did not complete";
+      return kReadUnknown;
+    }
+    c[i] = acc.v[kGrbmCount];
+  }
+  run_packet(a, a.stop_pkt);
+  if (c[0] <= 0) {
+    *why = "GRBM_COUNT did not advance after the start packet";
+    return kReadUnknown;
+  }
+  crumb("read semantics", "GRBM_COUNT " + std::to_string(c[0]) + " -> " + std::to_string(c[1]));
+  if (c[1] == c[0]) return kStops;
+  // expected ratio if cumulative: (t1 - ts) / (t0 - ts), ~2
+  const double expect = std::chrono::duration<double>(t[1] - ts).count() /
+                        std::max(1e-9, std::chrono::duration<double>(t[0] - ts).count());
+  return c[1] / c[0] > 0.5 * (1.0 + expect) ? kCumulative : kResets;
+}
+
 void counting_loop() {
+  ::prctl(PR_SET_NAME, "gpuexp-pmc", 0, 0, 0);
+  if (g_continuous) {
+    uint64_t served = 0;
+    while (!g_quit.load()) {
+      uint64_t target;
+      {
+        std::unique_lock<std::mutex> lk(g_cv_mu);
+        // a tick's kick, or on our own every interval when nothing kicks (manual engines)
+        g_cv.wait_for(lk, std::chrono::milliseconds(g_interval_ms),
+                      [&] { return g_quit.load() || g_kick_seq != served; });
+        if (g_quit.load()) break;
+        target = g_kick_seq;
+      }
+      read_round();
+      g_thread_cpu_ns.store(own_cpu_ns());
+      served = target;
+      {
+        std::lock_guard<std::mutex> lk(g_cv_mu);
+        g_done_seq = target;
+      }
+      g_done_cv.notify_all();
+    }
+    for (Agent* a : g_agents)
+      if (usable(a) && !a->read_inflight) run_packet(*a, a->stop_pkt);
+    return;
+  }
   while (!g_quit.load()) {
     const auto begin = Clock::now();
     window_all();
+    g_thread_cpu_ns.store(own_cpu_ns());
     const auto spent = std::chrono::duration_cast<std::chrono::milliseconds>(Clock::now() - begin).count();
     std::unique_lock<std::mutex> lk(g_cv_mu);
     g_cv.wait_for(lk, std::chrono::milliseconds(std::max<long long>(0, g_interval_ms - spent)),
@@ -394,8 +611,8 @@ void teardown_locked() {
     if (!a) continue;
     if (a->queue) hsa_queue_destroy(a->queue);
     if (a->sig.handle) hsa_signal_destroy(a->sig);
-    // A timed-out packet may still write the buffers: leak them rather than free.
-    if (!a->broken) {
+    // A timed-out (or still queued) packet may still write the buffers: leak them.
+    if (!a->broken && !a->read_inflight) {
       if (a->cmd_buf) hsa_amd_memory_pool_free(a->cmd_buf);
       if (a->out_buf) hsa_amd_memory_pool_free(a->out_buf);
     }
@@ -536,7 +753,9 @@ class QueueSentinel : public gpuexp::SentinelSource {
     for (Per& p : per_) {
       if (!p.ready || p.a->broken || p.a->queue_error.load()) continue;
       gpuexp::sentinel_drain(p.run, nslots_, sys_ns_per_tick_);
-      if (p.run.launched - p.run.completed >= 4) {  // a saturated queue shows as latency
+      // one run at a time: a run the workload leaves no SIMD for waits (and shows its wait as
+      // dispatch latency once it runs) without a second one queued behind it
+      if (p.run.launched - p.run.completed >= 1) {
         p.run.stalled += 1;
         continue;
       }
@@ -649,8 +868,37 @@ class QueueSentinel : public gpuexp::SentinelSource {
 }  // namespace
 
 extern "C" __attribute__((visibility("default"))) void gpuexp_rp_set_duty(int window_ms, int interval_ms) {
+  g_continuous = false;
   g_window_ms = std::max(1, window_ms);
   g_interval_ms = std::max(g_window_ms, interval_ms);
+}
+
+// Continuous counting: started once, read once per gpuexp_rp_kick (one engine tick), or
+// every `fallback_ms` when nothing kicks.
+extern "C" __attribute__((visibility("default"))) void gpuexp_rp_set_continuous(int fallback_ms) {
+  g_continuous = true;
+  g_interval_ms = std::max(10, fallback_ms);
+}
+
+extern "C" __attribute__((visibility("default"))) void gpuexp_rp_kick() {
+  {
+    std::lock_guard<std::mutex> lk(g_cv_mu);
+    ++g_kick_seq;
+  }
+  g_cv.notify_all();
+}
+
+// CPU time the counting thread has used so far (charged to the engine's sampler account).
+extern "C" __attribute__((visibility("default"))) uint64_t gpuexp_rp_cpu_ns() { return g_thread_cpu_ns.load(); }
+
+// Waits up to `timeout_us` for the round of the last kick; 0 = done, 1 = timed out.
+extern "C" __attribute__((visibility("default"))) int gpuexp_rp_sync(int timeout_us) {
+  std::unique_lock<std::mutex> lk(g_cv_mu);
+  const uint64_t want = g_kick_seq;
+  return g_done_cv.wait_for(lk, std::chrono::microseconds(std::max(0, timeout_us)),
+                            [&] { return g_done_seq >= want || g_quit.load(); })
+             ? 0
+             : 1;
 }
 
 extern "C" __attribute__((visibility("default"))) int gpuexp_rp_init(int ndev, const char* const* bdfs, char* err,
@@ -719,18 +967,52 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_init(int ndev, c
                                         : "no HSA GPU agent matched the exporter's GPUs")
                             : why);
   }
+  if (g_continuous) {
+    // probe the read packet's effect once (first working GPU), then arm every GPU
+    g_read_mode = kReadUnknown;
+    for (Agent* a : g_agents) {
+      if (!usable(a)) continue;
+      g_read_mode = read_semantics(*a, &why);
+      break;
+    }
+    if (g_read_mode == kReadUnknown) {
+      teardown_locked();
+      return fail("continuous counting: " + why);
+    }
+    ok = 0;
+    for (Agent* a : g_agents) {
+      if (!usable(a)) continue;
+      if (arm_continuous(*a)) ++ok;
+      else a->broken = true;
+    }
+    if (!ok) {
+      teardown_locked();
+      return fail("continuous counting: start/read packets did not complete");
+    }
+  }
   g_quit.store(false);
+  {
+    std::lock_guard<std::mutex> lk(g_cv_mu);
+    g_kick_seq = g_done_seq = 0;
+  }
   g_thread = std::thread(counting_loop);
-  g_status = "aqlprofile PMC on " + std::to_string(ok) + " GPU(s), " + std::to_string(g_window_ms) +
-             " ms window every " + std::to_string(g_interval_ms) + " ms";
+  g_status = "aqlprofile PMC on " + std::to_string(ok) + " GPU(s), " +
+             (g_continuous ? std::string("continuous (one read per tick; read packets: ") +
+                                 read_mode_name(g_read_mode) + ")"
+                           : std::to_string(g_window_ms) + " ms window every " + std::to_string(g_interval_ms) +
+                                 " ms");
   return ok;
 }
 
 extern "C" __attribute__((visibility("default"))) int gpuexp_rp_sample(int dev, double, double* out) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (dev < 0 || size_t(dev) >= g_agents.size() || !g_agents[size_t(dev)]) return -1;
-  const Agent& a = *g_agents[size_t(dev)];
+  Agent& a = *g_agents[size_t(dev)];
+  std::lock_guard<std::mutex> mk(a.m_mu);
   if (!a.m.valid || a.broken) return -1;
+  // continuous: a GPU whose reads have been stuck for 2 fallback intervals (4 ticks) has no
+  // current window; exporting the last one as current would be wrong
+  if (g_continuous && Clock::now() - a.t_window_end > std::chrono::milliseconds(2 * g_interval_ms)) return -1;
   std::memcpy(out, a.m.latest, sizeof(a.m.latest));
   return 0;
 }
@@ -738,6 +1020,7 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_sample(int dev, 
 extern "C" __attribute__((visibility("default"))) void gpuexp_rp_shutdown() {
   g_quit.store(true);
   g_cv.notify_all();
+  g_done_cv.notify_all();
   if (g_thread.joinable()) g_thread.join();
   std::lock_guard<std::mutex> lk(g_mu);
   teardown_locked();
@@ -749,6 +1032,7 @@ extern "C" __attribute__((visibility("default"))) const char* gpuexp_rp_status()
 extern "C" __attribute__((visibility("default"))) int gpuexp_rp_scope(int dev) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (dev < 0 || size_t(dev) >= g_agents.size() || !g_agents[size_t(dev)]) return -1;
+  std::lock_guard<std::mutex> mk(g_agents[size_t(dev)]->m_mu);
   return g_agents[size_t(dev)]->m.scope;
 }
 
@@ -757,10 +1041,21 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_scope(int dev) {
 extern "C" __attribute__((visibility("default"))) int gpuexp_rp_debug(int dev, char* buf, int len) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (dev < 0 || size_t(dev) >= g_agents.size() || !g_agents[size_t(dev)]) return -1;
-  const Agent& a = *g_agents[size_t(dev)];
+  Agent& a = *g_agents[size_t(dev)];
+  std::lock_guard<std::mutex> mk(a.m_mu);
+  char win[64];
+  std::snprintf(win, sizeof(win), "%.6f", a.last_window_s);
   std::string s = "backend=aqlprofile;events=" + std::to_string(a.events.size()) +
                   ";samples=" + std::to_string(a.last_samples) + ";windows=" + std::to_string(a.m.windows) +
-                  ";simd=" + std::to_string(a.m.simd) + ";cu=" + std::to_string(a.m.cu) + ";";
+                  ";simd=" + std::to_string(a.m.simd) + ";cu=" + std::to_string(a.m.cu) +
+                  ";mode=" + (g_continuous ? read_mode_name(g_read_mode) : "duty") + ";window_s=" + win +
+                  ";resets=" + std::to_string(a.resets.load()) + ";stalls=" + std::to_string(a.stalls.load()) + ";";
+  if (g_continuous && g_read_mode == kCumulative) {
+    char c[160];
+    std::snprintf(c, sizeof(c), "cum_MFMA=%.0f;cum_GRBM_COUNT=%.0f;cum_GUI=%.0f;", a.pub_cum[kMfma],
+                  a.pub_cum[kGrbmCount], a.pub_cum[kGuiActive]);
+    s += c;
+  }
   for (int k = 0; k < kNumCtr; ++k) {
     char t[128];
     std::snprintf(t, sizeof(t), "%s=%.0f/%d;", name(k), a.last_raw[k], a.last_inst[k]);

@@ -1,6 +1,7 @@
 // Mock GPU backend (BASELINE config 1: "mock-GPU backend on CPU, 1 fake device").
 // Values are smooth deterministic functions of the injected sample time, so tests can
 // assert exact rates; every field can be pinned and faults injected from Python.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 
@@ -174,6 +175,9 @@ bool MockBackend::counters(const DeviceInfo& dev, double dt_s, CounterReading* o
   out->gui_active_pct = get(s, "gui_active_pct", busy);
   out->sq_busy_pct = get(s, "sq_busy_pct", busy * 0.95);
   out->mfma_busy_pct = get(s, "mfma_busy_pct", busy * 0.6);
+  // while-active utilisation = busy share of the GUI-active share
+  const double gui = out->gui_active_pct;
+  out->mfma_util_pct = get(s, "mfma_util_pct", gui > 0 ? std::min(100.0, out->mfma_busy_pct * 100.0 / gui) : 0.0);
   out->waves_per_s = get(s, "waves_per_s", 1e6 * busy);
   out->lds_active_pct = get(s, "lds_active_pct", busy * 0.3);
   out->lds_bank_conflict_pct = get(s, "lds_bank_conflict_pct", 1.5);

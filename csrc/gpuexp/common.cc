@@ -2,6 +2,7 @@
 
 #include <dirent.h>
 #include <fcntl.h>
+#include <sys/prctl.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -10,6 +11,8 @@
 #include <mutex>
 
 namespace gpuexp {
+
+void set_thread_name(const char* name) { ::prctl(PR_SET_NAME, name, 0, 0, 0); }
 
 static std::atomic<int> g_log_level{static_cast<int>(LogLevel::kWarn)};
 static std::atomic<bool> g_log_json{false};

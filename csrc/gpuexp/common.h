@@ -30,6 +30,12 @@ inline uint64_t thread_cpu_ns() {
   return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
 }
 
+// Names the calling thread (/proc/<pid>/task/<tid>/comm, 15 chars): the exporter's threads
+// are gpuexp-sampler, gpuexp-dev (per-GPU read pool), gpuexp-http, gpuexp-pmc, so their CPU
+// can be told apart from outside (tests/test_fakehost.py checks the sampler's own account
+// against them).
+void set_thread_name(const char* name);
+
 // Leveled logging to stderr in logfmt.  The reference printed every pod every cycle to
 // stdout (main.go:81,89,108); here nothing is logged per tick at info level.
 enum class LogLevel : int { kDebug = 0, kInfo = 1, kWarn = 2, kError = 3, kOff = 4 };

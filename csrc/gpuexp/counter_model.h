@@ -39,6 +39,7 @@ enum Ctr {
   kDramWr32,
   kGmiRd32,
   kGmiWr32,
+  kSqCycles,
   kNumCtr
 };
 
@@ -47,7 +48,8 @@ inline const char* name(int c) {
                                         "SQ_LDS_IDX_ACTIVE",        "SQ_LDS_BANK_CONFLICT",
                                         "GRBM_GUI_ACTIVE",          "GRBM_COUNT",
                                         "TCC_EA0_RDREQ_DRAM_32B",   "TCC_EA0_WRREQ_WRITE_DRAM_32B",
-                                        "TCC_EA0_RDREQ_GMI_32B",    "TCC_EA0_WRREQ_WRITE_GMI_32B"};
+                                        "TCC_EA0_RDREQ_GMI_32B",    "TCC_EA0_WRREQ_WRITE_GMI_32B",
+                                        "SQ_CYCLES"};
   return kNames[c];
 }
 
@@ -56,7 +58,7 @@ inline bool use_max(int c) { return c == kGuiActive || c == kGrbmCount; }
 
 // Number of derived outputs (the CounterSource ABI: gpuexp_rp_sample fills this many
 // doubles; gpuexp::kCounterOutputs in sources.h).
-constexpr int kNumOut = 10;
+constexpr int kNumOut = 11;
 
 // Wave-level SQ counters and TCC EA requests are VMID-filtered for unprivileged clients.
 // The filter is on the HARDWARE VMID, which the scheduler hands out dynamically, so an
@@ -106,7 +108,13 @@ inline void derive(Derived& a, const double* d, const int* inst, double wall) {
   else if (a.scope != 0) a.scope = (d[kGrbmCount] > 0 && gui / d[kGrbmCount] > 0.5 && d[kMfma] > 0 &&
                                     d[kWaves] / wall < 1000.0) ? 0 : 1;
   double* out = a.latest;
-  out[0] = gui > 0 && a.simd ? 100.0 * d[kMfma] / (gui * a.simd) : nan;             // MfmaUtil
+  // MFMA busy over ELAPSED cycles (GRBM_COUNT, the free-running GRBM clock): the share of
+  // the window's wall time the matrix cores of all SIMDs were issuing, so an idle GPU
+  // reads 0 whatever it ran before (the DCGM tensor-active semantics).  out[10] is
+  // counter_defs.yaml's MfmaUtil, over GUI-ACTIVE cycles only: a GEMM that runs for 1 % of
+  // the window reads ~90 there and ~1 here.
+  out[0] = d[kGrbmCount] > 0 && a.simd ? std::min(100.0, 100.0 * d[kMfma] / (d[kGrbmCount] * a.simd)) : nan;
+  out[10] = gui > 0 && a.simd ? std::min(100.0, 100.0 * d[kMfma] / (gui * a.simd)) : nan;  // MfmaUtil
   const double se = inst[kSqBusy] > 0 ? inst[kSqBusy] : 1;                           // one per SE
   out[1] = gui > 0 ? std::min(100.0, 100.0 * d[kSqBusy] / (gui * se)) : nan;
   out[2] = d[kGrbmCount] > 0 ? 100.0 * gui / d[kGrbmCount] : nan;                    // GPU busy

@@ -157,7 +157,8 @@ struct ProcSample {
 // rocprofiler-sdk device-counting derived values for one GPU over one tick.
 struct CounterReading {
   bool ok = false;
-  double mfma_busy_pct = kNaN;      // SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE * SIMDs)
+  double mfma_busy_pct = kNaN;      // SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_COUNT * SIMDs): share of wall time
+  double mfma_util_pct = kNaN;      // SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE * SIMDs): MfmaUtil
   double sq_busy_pct = kNaN;        // SQ_BUSY_CYCLES / GRBM_GUI_ACTIVE
   double gui_active_pct = kNaN;     // GRBM_GUI_ACTIVE / GRBM_COUNT
   double waves_per_s = kNaN;        // SQ_WAVES / dt

@@ -56,6 +56,10 @@ const char* idx_str(int i) {
   return i >= 0 && i < 64 ? k[i] : "?";
 }
 
+// True on an engine's own sampler thread (set in run_sampler): that thread charges its
+// whole clock to the sampler account, a manual tick_now() caller only the tick itself.
+thread_local bool tl_sampler_thread = false;
+
 const char* kTempNames[9] = {"hotspot", "mem", "vrsoc", "edge", "vrgfx", "vrmem", "hbm0", "hbm1", "hbm2"};
 const char* kClkNames[3] = {"gfx", "soc", "mem"};
 const char* kThrNames[5] = {"ppt", "socket_thermal", "vr_thermal", "hbm_thermal", "prochot"};
@@ -63,7 +67,16 @@ const char* kThrNames[5] = {"ppt", "socket_thermal", "vr_thermal", "hbm_thermal"
 }  // namespace
 
 ForkJoinPool::ForkJoinPool(int threads) {
-  for (int t = 1; t < threads; ++t) workers_.emplace_back([this] { worker(); });
+  const size_t n = threads > 1 ? size_t(threads - 1) : 0;
+  wcpu_.reset(new std::atomic<uint64_t>[n > 0 ? n : 1]);
+  for (size_t t = 0; t < n; ++t) wcpu_[t].store(0);
+  for (size_t t = 0; t < n; ++t) workers_.emplace_back([this, t] { worker(t); });
+}
+
+uint64_t ForkJoinPool::cpu_ns_total() const {
+  uint64_t s = 0;
+  for (size_t t = 0; t < workers_.size(); ++t) s += wcpu_[t].load();
+  return s;
 }
 
 ForkJoinPool::~ForkJoinPool() {
@@ -75,7 +88,8 @@ ForkJoinPool::~ForkJoinPool() {
   for (auto& w : workers_) w.join();
 }
 
-void ForkJoinPool::worker() {
+void ForkJoinPool::worker(size_t idx) {
+  set_thread_name("gpuexp-dev");
   uint64_t seen = 0;
   for (;;) {
     const std::function<void(int)>* fn;
@@ -89,6 +103,7 @@ void ForkJoinPool::worker() {
       n = n_;
     }
     for (int i; (i = next_.fetch_add(1)) < n;) (*fn)(i);
+    wcpu_[idx].store(thread_cpu_ns());  // before pending_ drops: run() sees it
     std::lock_guard<std::mutex> lk(mu_);
     pending_ -= 1;
     if (pending_ == 0) done_cv_.notify_all();
@@ -177,7 +192,12 @@ void Engine::define_families() {
   f_pcie_recov_ = add("amd_gpu_pcie_recovery_total", "PCIe L0 -> recovery transitions (PMFW accumulator)", C, D);
   f_xgmi_width_ = add("amd_gpu_xgmi_link_width", "xGMI link width (PMFW)", G, D);
   f_xgmi_speed_ = add("amd_gpu_xgmi_link_speed", "xGMI link speed (PMFW units)", G, D);
-  f_mfma_ = add("amd_gpu_mfma_busy_percent", "MFMA (matrix core) busy: SQ_VALU_MFMA_BUSY_CYCLES per SIMD", G, D);
+  f_mfma_ = add("amd_gpu_mfma_busy_percent",
+                "MFMA (matrix core) busy: share of the last tick's wall time the matrix cores of all SIMDs were "
+                "issuing (SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_COUNT x SIMDs))", G, D);
+  f_mfma_util_ = add("amd_gpu_mfma_util_percent",
+                     "MFMA utilisation while the GPU was active (rocprof MfmaUtil: SQ_VALU_MFMA_BUSY_CYCLES / "
+                     "(GRBM_GUI_ACTIVE x SIMDs))", G, D);
   f_sq_busy_ = add("amd_gpu_sq_busy_percent", "Shader sequencer busy (SQ_BUSY_CYCLES)", G, D);
   f_gui_ = add("amd_gpu_gui_active_percent", "Graphics pipe active (GRBM_GUI_ACTIVE / GRBM_COUNT)", G, D);
   f_waves_ = add("amd_gpu_waves_per_second", "Waves dispatched per second (SQ_WAVES)", G, D);
@@ -292,7 +312,9 @@ void Engine::define_families() {
   f_self_series_ = add("gpuexp_series", "Series in the last rendered exposition", G, {});
   f_self_dev_errors_ = add("gpuexp_device_errors_total", "Failed telemetry reads per GPU", C, {"gpu"});
   f_self_overruns_ = add("gpuexp_tick_overruns_total", "Ticks skipped because a tick ran past its deadline", C, {});
-  f_self_cpu_ = add("gpuexp_sampler_cpu_seconds_total", "CPU time used by the sampler thread", C, {});
+  f_self_cpu_ = add("gpuexp_sampler_cpu_seconds_total",
+                    "CPU time of the sampling work: the sampler thread, its per-GPU read threads and the PMC "
+                    "counter thread (not the HTTP server)", C, {});
   f_self_source_up_ = add("gpuexp_source_up", "1 if an optional source is active", G, {"source"});
   f_self_metrics_reads_ = add("gpuexp_gpu_metrics_reads_total",
                               "gpu_metrics reads by kind: fresh (SMU table fetch) or coalesced (cached table, "
@@ -306,9 +328,17 @@ void Engine::define_families() {
                            "yet (their series carry pod=\"\" and no legacy series until it does)",
                            G, {});
   f_self_rccl_files_ = add("gpuexp_rccl_files",
-                           "RCCL tracer files by state: active (writer identified, exported), unverified "
-                           "(no live process maps it as claimed), exited (writer gone, file left behind)",
+                           "RCCL tracer directory entries by state: active (writer identified, exported), "
+                           "unverified (no live process maps it as claimed), exited (writer gone, file left "
+                           "behind), ignored (not a tracer file, not a regular file, or over the 1024-file cap)",
                            G, {"state"});
+  f_self_rccl_scans_ = add("gpuexp_rccl_dir_scans_total",
+                           "Listings of the RCCL tracer directory (only when it changed, at most once per "
+                           "rccl_scan_interval_s)", C, {});
+  f_self_ctr_late_ = add("gpuexp_counters_late_ticks_total",
+                         "Ticks that exported the previous counter window because this tick's PMC read had not "
+                         "completed within counters_sync_us (continuous counters)",
+                         C, {});
   f_self_ctr_scope_ = add("gpuexp_counters_device_scope",
                           "1 if wave/LDS/HBM PMC counters see every process on the GPU, 0 if they are "
                           "VMID-filtered to the exporter (not exported then)",
@@ -428,7 +458,12 @@ bool Engine::start(std::string* err) {
   if (cfg_.enable_counters && cfg_.backend != "mock" && !any_queue) {
     counters_status_ = "disabled: no GPU in queue_devices";
   } else if (cfg_.enable_counters && cfg_.backend != "mock") {
-    counters_ = make_rocprof_counters(cfg_.counters_plugin, cfg_.counters_window_ms, cfg_.counters_interval_ms);
+    const bool continuous = cfg_.counters_mode == "continuous";
+    // continuous: every tick kicks a read; the plugin's own timer (2 ticks) only covers
+    // engines without a sampler thread
+    const int interval_ms = continuous && cfg_.interval_s > 0 ? std::max(10, int(cfg_.interval_s * 2000))
+                                                              : cfg_.counters_interval_ms;
+    counters_ = make_rocprof_counters(cfg_.counters_plugin, cfg_.counters_window_ms, interval_ms, continuous);
     std::string e;
     if (!counters_ || !counters_->start(devices_, &e)) {
       counters_status_ = "unavailable: " + e;
@@ -468,7 +503,7 @@ bool Engine::start(std::string* err) {
   } else if (cfg_.enable_sentinel) {
     sentinel_status_ = "mock";
   }
-  if (cfg_.enable_rccl) rccl_ = make_rccl_source(cfg_.rccl_dir, cfg_.rccl_verify);
+  if (cfg_.enable_rccl) rccl_ = make_rccl_source(cfg_.rccl_dir, cfg_.rccl_verify, cfg_.rccl_scan_interval_s);
   {
     std::string v;
     driver_version_ = read_small_file((cfg_.host_root.empty() ? "" : cfg_.host_root) + "/sys/module/amdgpu/version", &v, 128)
@@ -540,6 +575,8 @@ void Engine::stop() {
 }
 
 void Engine::run_sampler() {
+  set_thread_name("gpuexp-sampler");
+  tl_sampler_thread = true;
   int tfd = ::timerfd_create(CLOCK_MONOTONIC, TFD_CLOEXEC);
   uint64_t period = uint64_t(cfg_.interval_s * 1e9);
   if (period < 1000000) period = 1000000;  // 1 kHz cap
@@ -938,6 +975,7 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
     cput(st.self_reads[3], f_self_ctr_scope_, scope < 0 ? kNaN : double(scope), gen,
          [&] { return std::vector<std::string>{std::to_string(d.index)}; });
     dput(st, i, st.ctr[0], f_mfma_, {}, cr.mfma_busy_pct, gen);
+    if (cfg_.series_profile == "full") dput(st, i, st.mfma_util, f_mfma_util_, {}, cr.mfma_util_pct, gen);
     dput(st, i, st.ctr[2], f_gui_, {}, cr.gui_active_pct, gen);
     if (scope != 0) {
       dput(st, i, st.ctr[1], f_sq_busy_, {}, cr.sq_busy_pct, gen);
@@ -1260,6 +1298,8 @@ void Engine::emit_self(uint64_t gen) {
   cput(self_refs_[14], f_self_source_up_, (counters_ || (cfg_.enable_counters && mock_)) ? 1 : 0, gen,
        [] { return std::vector<std::string>{"counters"}; });
   cput(self_refs_[15], f_self_source_up_, rccl_ ? 1 : 0, gen, [] { return std::vector<std::string>{"rccl"}; });
+  if (counters_ && cfg_.counters_mode == "continuous")
+    cput(self_refs_[19], f_self_ctr_late_, double(counters_late_), gen, none);
   if (cfg_.enable_kfd_events && cfg_.series_profile == "full")
     cput(self_refs_[18], f_self_source_up_, kfd_events_ ? 1 : 0, gen,
          [] { return std::vector<std::string>{"kfd_events"}; });
@@ -1271,6 +1311,8 @@ void Engine::emit_self(uint64_t gen) {
     table_.put(f_self_rccl_files_, {"active"}, a, gen);
     table_.put(f_self_rccl_files_, {"unverified"}, u, gen);
     table_.put(f_self_rccl_files_, {"exited"}, x, gen);
+    table_.put(f_self_rccl_files_, {"ignored"}, rccl_->ignored(), gen);
+    table_.put(f_self_rccl_scans_, {}, double(rccl_->scans()), gen);
   }
 }
 
@@ -1281,6 +1323,9 @@ void Engine::tick_locked(uint64_t now) {
   last_tick_now_ = now;
   uint64_t ts[kStages + 1];
   ts[0] = mono_ns();
+  // continuous counters: this tick's read goes out now and is collected before the series
+  // stage, so the exported window is exactly the last tick interval
+  if (counters_) counters_->kick();
 
   // Control-plane updates (pushed from Python at low rate).
   {
@@ -1415,7 +1460,8 @@ void Engine::tick_locked(uint64_t now) {
   if (sentinel_) sentinel_->tick(now);
   if (kfd_events_) count_kfd_events();
   ts[4] = mono_ns();
-  // 4: counters are sampled inside collect_device (per GPU); timed there as part of series
+  // 4: counters: wait (bounded) for this tick's read round; sampled in collect_device
+  if (counters_ && !counters_->sync(cfg_.counters_sync_us)) counters_late_ += 1;
   ts[5] = mono_ns();
 
   // 5: series
@@ -1481,7 +1527,27 @@ void Engine::tick_locked(uint64_t now) {
     }
     stats_.device_errors += errs;
     for (int k = 0; k < kStages; ++k) stats_.stage_ns[k] = double(stage_dur[k]);
-    stats_.sampler_cpu_ns += thread_cpu_ns() - cpu0;
+    // every thread that worked for this tick: the sampler, the per-GPU read pool, and the
+    // counter plugin's thread (its PM4 read rounds since the last tick)
+    // The sampler thread charges its whole clock since the last tick (timerfd wake-ups
+    // included); a manual tick_now() from another thread charges the tick itself.
+    const uint64_t own = thread_cpu_ns();
+    uint64_t cpu = own - cpu0;
+    if (tl_sampler_thread) {
+      if (sampler_cpu_seen_ && own >= sampler_cpu_seen_) cpu = own - sampler_cpu_seen_;
+      sampler_cpu_seen_ = own;
+    }
+    if (pool_) {
+      const uint64_t p = pool_->cpu_ns_total();
+      if (p >= pool_cpu_seen_) cpu += p - pool_cpu_seen_;
+      pool_cpu_seen_ = p;
+    }
+    if (counters_) {
+      const uint64_t c = counters_->cpu_ns();
+      if (c >= counters_cpu_seen_) cpu += c - counters_cpu_seen_;
+      counters_cpu_seen_ = c;
+    }
+    stats_.sampler_cpu_ns += cpu;
     stats_.gzip_eager = gzip_eager_;
   }
 }

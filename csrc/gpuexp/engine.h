@@ -45,15 +45,19 @@ class ForkJoinPool {
   // Runs fn(i) for i in [0, n) on the pool + the caller; returns when all are done.
   void run(int n, const std::function<void(int)>& fn);
   int threads() const { return int(workers_.size()) + 1; }
+  // Cumulative thread CPU of the workers (each publishes its own clock after every run(),
+  // before run() returns; so it includes their wake-up and lock costs, not only the items).
+  uint64_t cpu_ns_total() const;
 
  private:
-  void worker();
+  void worker(size_t idx);
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   std::vector<std::thread> workers_;
   const std::function<void(int)>* fn_ = nullptr;
   int n_ = 0;
   std::atomic<int> next_{0};
+  std::unique_ptr<std::atomic<uint64_t>[]> wcpu_;
   int pending_ = 0;
   uint64_t epoch_ = 0;
   bool quit_ = false;
@@ -83,12 +87,17 @@ struct EngineConfig {
   int sentinel_ring = 64;
   int sentinel_spin = 500;  // ~15 us window (rocprofv3: spin 2000 ran 61 us/launch)
   bool enable_counters = false;
-  std::string counters_plugin;         // path to _gpuexp_rocprof.so
-  int counters_window_ms = 20;         // counting window (rocprofiler context started)...
-  int counters_interval_ms = 1000;     // ...once per interval (duty cycle, see rocprof_plugin.cc)
+  std::string counters_plugin;         // path to _gpuexp_aqlpmc.so / _gpuexp_rocprof.so
+  // continuous: counting never pauses and is read once per tick (aqlprofile plugin);
+  // duty: a counters_window_ms window every counters_interval_ms (either plugin)
+  std::string counters_mode = "continuous";
+  int counters_window_ms = 20;         // duty: counting window...
+  int counters_interval_ms = 1000;     // ...once per interval (see rocprof_plugin.cc)
+  int counters_sync_us = 2000;         // continuous: longest a tick waits for its own counter read
   bool enable_rccl = false;
   std::string rccl_dir = "/dev/shm";
   bool rccl_verify = true;             // attribute a tracer file only to a process that maps it
+  double rccl_scan_interval_s = 1.0;   // list the tracer directory at most this often (when it changed)
   bool enable_kfd_events = true;       // full profile: KFD SMI events (VM faults, resets, ...)
   bool firmware_info = true;           // full profile: amd_gpu_firmware_info (one series per loaded firmware)
   // Checkpoint of the exporter's own accumulations (per-pod energy, KFD event counts) so
@@ -187,7 +196,7 @@ class Engine {
         energy, temp[9], clk[3], xrd[kMaxXgmiLinks], xwr[kMaxXgmiLinks], xrd_rate, xwr_rate,
         links_up, pcie_bw, pcie_replay, pcie_speed, pcie_width, thr[5], nprocs, cu_occ, ctr[10],
         sen[4], ecc[3], aer[3], nak[2], recov, xgmi_w, xgmi_s, xclk[kMaxXcc], sen_xlat[kMaxXcc], sen_mem, sen_xmem[kMaxXcc],
-        kev[std::size(kKfdSubscribed)], pages[3], gtt_used, gtt_total, board;
+        kev[std::size(kKfdSubscribed)], pages[3], gtt_used, gtt_total, board, mfma_util;
     std::vector<SeriesRef> fw;  // amd_gpu_firmware_info, one per component
     uint64_t kfd_events[kKfdEventIds] = {};  // KFD SMI events seen on this GPU, by id
     uint64_t errors = 0;
@@ -262,6 +271,9 @@ class Engine {
   std::vector<double> gtt_total_;
   std::vector<uint64_t> metrics_fresh_, metrics_coalesced_;  // per device
   uint64_t gzip_eager_ = 0;  // sampler thread only; copied into stats_ per tick
+  uint64_t counters_late_ = 0;
+  // thread clocks already charged to gpuexp_sampler_cpu_seconds_total (sampler thread only)
+  uint64_t counters_cpu_seen_ = 0, pool_cpu_seen_ = 0, sampler_cpu_seen_ = 0;  // ticks whose counter read missed counters_sync_us (sampler thread)
   std::string sentinel_status_ = "disabled", counters_status_ = "disabled";
 
   SeriesTable table_;
@@ -309,7 +321,7 @@ class Engine {
       f_power_cap_, f_energy_, f_temp_, f_clk_, f_xrd_, f_xwr_, f_xrd_rate_, f_xwr_rate_,
       f_links_up_, f_pcie_bw_, f_pcie_replay_, f_pcie_speed_, f_pcie_width_, f_thr_, f_nprocs_,
       f_cu_occ_, f_ecc_, f_aer_, f_pcie_nak_, f_pcie_recov_, f_xgmi_width_, f_xgmi_speed_, f_mfma_, f_sq_busy_, f_gui_, f_waves_, f_lds_, f_lds_conf_, f_hbm_rd_, f_remote_rd_, f_remote_wr_,
-      f_hbm_wr_, f_sen_sclk_, f_sen_lat_, f_sen_xcc_, f_sen_runs_, f_xcc_clk_, f_sen_xlat_, f_sen_mem_, f_sen_xmem_;
+      f_hbm_wr_, f_sen_sclk_, f_sen_lat_, f_sen_xcc_, f_sen_runs_, f_xcc_clk_, f_sen_xlat_, f_sen_mem_, f_sen_xmem_, f_mfma_util_ = -1;
   int f_proc_vram_, f_proc_cu_, f_proc_sdma_, f_proc_evicted_, f_proc_gfx_;
   int f_legacy_mem_ = -1, f_legacy_perc_ = -1;
   int f_pod_vram_, f_pod_procs_, f_pod_gpus_, f_pod_xrd_, f_pod_xwr_, f_pod_power_, f_pod_gfx_, f_pod_gfx_share_,
@@ -321,7 +333,7 @@ class Engine {
   int f_self_build_, f_self_ticks_, f_self_last_, f_self_stage_, f_self_scrape_, f_self_scrapes_,
       f_self_http_bytes_, f_self_render_bytes_, f_self_series_, f_self_dev_errors_,
       f_self_overruns_, f_self_cpu_, f_self_source_up_, f_self_ctr_scope_, f_self_metrics_reads_, f_self_metrics_period_, f_self_prewake_, f_self_gzip_,
-      f_self_rccl_files_, f_self_unresolved_;
+      f_self_rccl_files_, f_self_unresolved_, f_self_ctr_late_ = -1, f_self_rccl_scans_ = -1;
   SeriesRef self_stage_refs_[kStages];
   uint64_t last_stage_ns_[kStages] = {};
 };

@@ -270,6 +270,7 @@ bool HttpServer::gzip_due(uint64_t now_ns, uint64_t horizon_ns) const {
 }
 
 void HttpServer::run(Worker* w) {
+  set_thread_name("gpuexp-http");
   constexpr int kMaxEvents = 256;
   epoll_event events[kMaxEvents];
   char rbuf[16384];

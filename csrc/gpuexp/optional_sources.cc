@@ -34,10 +34,14 @@ using rp_shutdown_fn = void (*)();
 using rp_status_fn = const char* (*)();
 using rp_scope_fn = int (*)(int dev);
 
+using rp_kick_fn = void (*)();
+using rp_cpu_fn = uint64_t (*)();
+using rp_sync_fn = int (*)(int timeout_us);
+
 class PluginCounters : public CounterSource {
  public:
-  PluginCounters(std::string path, int window_ms, int interval_ms)
-      : path_(std::move(path)), window_ms_(window_ms), interval_ms_(interval_ms) {}
+  PluginCounters(std::string path, int window_ms, int interval_ms, bool continuous)
+      : path_(std::move(path)), window_ms_(window_ms), interval_ms_(interval_ms), continuous_(continuous) {}
   ~PluginCounters() override { stop(); }
 
   bool start(const std::vector<DeviceInfo>& devs, std::string* err) override {
@@ -57,8 +61,18 @@ class PluginCounters : public CounterSource {
       return false;
     }
     using duty_fn = void (*)(int, int);
-    if (auto duty = reinterpret_cast<duty_fn>(::dlsym(handle_, "gpuexp_rp_set_duty")))
+    using cont_fn = void (*)(int);
+    auto cont = reinterpret_cast<cont_fn>(::dlsym(handle_, "gpuexp_rp_set_continuous"));
+    if (continuous_ && cont) {
+      // counting never stops; one read per engine tick (kick/sync), or every interval_ms
+      // when no tick kicks (manual-tick engines)
+      cont(interval_ms_);
+      kick_ = reinterpret_cast<rp_kick_fn>(::dlsym(handle_, "gpuexp_rp_kick"));
+      sync_ = reinterpret_cast<rp_sync_fn>(::dlsym(handle_, "gpuexp_rp_sync"));
+    } else if (auto duty = reinterpret_cast<duty_fn>(::dlsym(handle_, "gpuexp_rp_set_duty"))) {
       duty(window_ms_, interval_ms_);
+    }
+    cpu_ = reinterpret_cast<rp_cpu_fn>(::dlsym(handle_, "gpuexp_rp_cpu_ns"));
     // ABI: a BDF prefixed with '-' reserves that device's HSA agent (partition order) but
     // gets no queue.
     std::vector<std::string> names;
@@ -81,6 +95,7 @@ class PluginCounters : public CounterSource {
     if (sample_(dev, dt_s, v) != 0) return false;
     out->ok = true;
     out->mfma_busy_pct = v[0];
+    out->mfma_util_pct = v[10];
     out->sq_busy_pct = v[1];
     out->gui_active_pct = v[2];
     out->waves_per_s = v[3];
@@ -94,6 +109,14 @@ class PluginCounters : public CounterSource {
   }
 
   int scope(int dev) override { return started_ && scope_fn_ ? scope_fn_(dev) : -1; }
+
+  void kick() override {
+    if (started_ && kick_) kick_();
+  }
+
+  uint64_t cpu_ns() override { return started_ && cpu_ ? cpu_() : 0; }
+
+  bool sync(int timeout_us) override { return !(started_ && sync_) || sync_(timeout_us) == 0; }
 
   void stop() override {
     if (started_ && shutdown_) shutdown_();
@@ -109,6 +132,10 @@ class PluginCounters : public CounterSource {
  private:
   std::string path_;
   int window_ms_, interval_ms_;
+  bool continuous_;
+  rp_kick_fn kick_ = nullptr;
+  rp_sync_fn sync_ = nullptr;
+  rp_cpu_fn cpu_ = nullptr;
   void* handle_ = nullptr;
   rp_init_fn init_ = nullptr;
   rp_sample_fn sample_ = nullptr;
@@ -266,74 +293,73 @@ int maps_file(int pid, const MapsId& want) {
 //    that maps this very file (/proc/<pid>/maps dev:inode), in the PID namespace it
 //    claims — a pod cannot get its counters attributed to another pod's process;
 //  - the writer's liveness is checked every poll (pidfd, else start time): a file left by
-//    a killed process stops being exported at once and never moves to a reused PID;
-//  - failed identifications back off (1 s doubling to 60 s) instead of scanning /proc
-//    every tick.
+//    a killed process stops being exported at once and never moves to a reused PID.
+// Cost is bounded whatever the directory holds (a pod can fill it):
+//  - the directory is listed only when its mtime changed, and then at most once per
+//    `scan_interval` (1 s default); a tick otherwise touches only the files already proven
+//    active (one fstatat, two preads and a pidfd poll each);
+//  - at most kMaxTracked names are tracked; everything else (names that are not tracer
+//    files, non-regular entries, names over the cap) is only counted, as "ignored";
+//  - a file whose writer is unproven is retried with a doubling backoff (1 s .. 64 s); one
+//    whose writer exited is re-examined only when its inode, size or mtime changes (a new
+//    writer re-creating it), never on a timer;
+//  - /proc is walked at most once per listing, into one (pidns, nspid) -> pid map that
+//    every identification of that listing shares.
 class ShmRcclSource : public RcclSource {
  public:
-  ShmRcclSource(std::string dir, bool verify_maps) : dir_(std::move(dir)), verify_maps_(verify_maps) {
+  static constexpr size_t kMaxTracked = 1024;
+
+  ShmRcclSource(std::string dir, bool verify_maps, uint64_t scan_interval_ns)
+      : dir_(std::move(dir)), verify_maps_(verify_maps), scan_interval_ns_(scan_interval_ns) {
     self_ns_ = pidns_inode("/proc/self");
   }
   ~ShmRcclSource() override {
     for (auto& kv : files_) close_entry(&kv.second);
+    if (dfd_ >= 0) ::close(dfd_);
   }
 
   void poll(std::vector<RcclTotals>* out) override {
     out->clear();
     const uint64_t now = mono_ns();
-    std::unordered_map<std::string, bool> present;
-    int dfd = ::open(dir_.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
-    if (dfd < 0) {
-      for (auto& kv : files_) close_entry(&kv.second);
-      files_.clear();
+    if (dfd_ < 0) {
+      dfd_ = ::open(dir_.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+      if (dfd_ < 0) {
+        for (auto& kv : files_) close_entry(&kv.second);
+        files_.clear();
+        return;
+      }
+      scanned_ = false;
+    }
+    struct stat dst;
+    if (::fstat(dfd_, &dst) != 0 || dst.st_nlink == 0) {  // directory removed: reopen next poll
+      ::close(dfd_);
+      dfd_ = -1;
       return;
     }
-    for (const std::string& name : list_dir(dir_)) {
-      uint64_t name_ino = 0;
-      int name_pid = 0;
-      if (!parse_name(name, &name_ino, &name_pid)) continue;
+    const bool changed = !scanned_ || dst.st_mtim.tv_sec != dir_mtime_.tv_sec ||
+                         dst.st_mtim.tv_nsec != dir_mtime_.tv_nsec;
+    // a listing when the directory changed (rate-limited) or a retry is due
+    if ((changed || (next_retry_ns_ && now >= next_retry_ns_)) && (!scanned_ || now - last_scan_ns_ >= scan_interval_ns_)) {
+      dir_mtime_ = dst.st_mtim;
+      scan(now);
+    }
+    for (auto& kv : files_) {
+      Entry& e = kv.second;
+      if (e.state != kActive || e.fd < 0) continue;
       struct stat st;
-      if (::fstatat(dfd, name.c_str(), &st, AT_SYMLINK_NOFOLLOW) != 0 || !S_ISREG(st.st_mode)) continue;
-      present[name] = true;
-      Entry& e = files_[name];
-      if (e.fd >= 0 && (e.dev != st.st_dev || e.ino != st.st_ino)) close_entry(&e);  // replaced file
-      if (e.fd < 0) {
-        if (now < e.retry_ns) continue;
-        e.fd = ::openat(dfd, name.c_str(), O_RDONLY | O_NOFOLLOW | O_NONBLOCK | O_CLOEXEC);
-        struct stat fst;
-        if (e.fd < 0 || ::fstat(e.fd, &fst) != 0 || !S_ISREG(fst.st_mode)) {
-          close_entry(&e);
-          backoff(&e, now);
-          continue;
-        }
-        e.dev = fst.st_dev;
-        e.ino = fst.st_ino;
-        e.maps_id = maps_identity(e.fd, fst);
-      }
-      RcclShmFile snap;
-      if (!read_consistent(e.fd, &snap) || snap.magic != kRcclShmMagic || snap.pidns_ino != name_ino ||
-          snap.ns_pid != name_pid || snap.pidns_ino == 0 || snap.ns_pid <= 0) {
-        continue;  // not (yet) a complete file, or one whose content disagrees with its name
-      }
-      if (e.host_pid > 0 && !alive(&e)) {
-        close_entry(&e);  // writer exited (or was killed): its leftover file is not exported
-        e.state = kExited;
-        e.fails = 0;
-        backoff(&e, now);  // re-identify later: a new writer may reuse the name (O_TRUNC)
+      if (::fstatat(dfd_, kv.first.c_str(), &st, AT_SYMLINK_NOFOLLOW) != 0 || st.st_dev != e.dev ||
+          st.st_ino != e.ino) {
+        close_entry(&e);  // unlinked or replaced: the next listing sees what is there now
+        e.state = kNew;
         continue;
       }
-      if (e.host_pid <= 0) {
-        if (now < e.retry_ns) continue;
-        if (!identify(&e, snap.pidns_ino, snap.ns_pid)) {
-          if (e.state != kExited) e.state = kUnverified;
-          backoff(&e, now);
-          // no fd is held for a file nobody is proven to write: files left by killed pods
-          // (or planted by a hostile one) cost a directory entry check per poll, not an fd
-          close_entry(&e);
-          continue;
-        }
-        e.state = kActive;
-        e.fails = 0;
+      RcclShmFile snap;
+      if (!read_consistent(e.fd, &snap) || snap.magic != kRcclShmMagic || snap.pidns_ino != e.name_ino ||
+          snap.ns_pid != e.name_pid)
+        continue;  // truncated or rewritten under us: nothing to export this tick
+      if (!alive(&e)) {
+        mark_exited(&e, st);
+        continue;
       }
       for (int op = 0; op < kOpNumOps; ++op) {
         const uint64_t c = snap.ops[op].calls.load(std::memory_order_relaxed);
@@ -348,15 +374,6 @@ class ShmRcclSource : public RcclSource {
         out->push_back(t);
       }
     }
-    ::close(dfd);
-    for (auto it = files_.begin(); it != files_.end();) {
-      if (!present.count(it->first)) {
-        close_entry(&it->second);
-        it = files_.erase(it);
-      } else {
-        ++it;
-      }
-    }
   }
 
   void file_states(int* active, int* unverified, int* exited) const override {
@@ -368,12 +385,17 @@ class ShmRcclSource : public RcclSource {
     }
   }
 
+  int ignored() const override { return ignored_; }
+  uint64_t scans() const override { return scans_; }
+
  private:
   enum State { kNew, kActive, kUnverified, kExited };
   struct Entry {
     int fd = -1;
     dev_t dev = 0;
     ino_t ino = 0;
+    uint64_t name_ino = 0;  // identity the name claims
+    int name_pid = 0;
     MapsId maps_id;  // how /proc/<pid>/maps names this file (see maps_identity)
     int host_pid = -1;
     int pidfd = -1;
@@ -381,7 +403,12 @@ class ShmRcclSource : public RcclSource {
     uint64_t retry_ns = 0;
     int fails = 0;
     State state = kNew;
+    // kExited: the file as it was when its writer was found gone
+    ino_t gone_ino = 0;
+    off_t gone_size = 0;
+    struct timespec gone_mtime {};
   };
+  using ProcMap = std::map<std::pair<uint64_t, int>, std::vector<int>>;  // (pidns, nspid) -> host pids
 
   static bool parse_name(const std::string& name, uint64_t* ino, int* pid) {
     static const char kPrefix[] = "gpuexp-rccl-";
@@ -396,6 +423,134 @@ class ShmRcclSource : public RcclSource {
     if (!r || *r != '\0' || v <= 0 || v > (1 << 30)) return false;
     *pid = int(v);
     return true;
+  }
+
+  // One listing: new names are examined (capped), gone names forgotten, exited files
+  // re-examined only if they changed, unverified ones when their backoff expires.
+  void scan(uint64_t now) {
+    last_scan_ns_ = now;
+    scanned_ = true;
+    ++scans_;
+    int ignored = 0;
+    next_retry_ns_ = 0;
+    std::unordered_map<std::string, bool> present;
+    std::unique_ptr<ProcMap> procs;  // built on first need, shared by this listing
+    const int lfd = ::dup(dfd_);
+    DIR* d = lfd >= 0 ? ::fdopendir(lfd) : nullptr;
+    if (!d) {
+      if (lfd >= 0) ::close(lfd);
+      return;
+    }
+    ::rewinddir(d);
+    while (dirent* de = ::readdir(d)) {
+      if (de->d_name[0] == '.') continue;
+      const std::string name(de->d_name);
+      uint64_t name_ino = 0;
+      int name_pid = 0;
+      if (!parse_name(name, &name_ino, &name_pid)) {
+        ++ignored;  // not a tracer file: no syscall spent on it
+        continue;
+      }
+      auto it = files_.find(name);
+      if (it == files_.end() && files_.size() >= kMaxTracked) {
+        ++ignored;
+        continue;
+      }
+      if (it != files_.end() && it->second.state == kActive && it->second.fd >= 0) {
+        present[name] = true;  // checked every tick
+        continue;
+      }
+      struct stat st;
+      if (::fstatat(dfd_, name.c_str(), &st, AT_SYMLINK_NOFOLLOW) != 0 || !S_ISREG(st.st_mode)) {
+        ++ignored;  // FIFO, symlink, directory, ...: never opened
+        if (it != files_.end()) {
+          close_entry(&it->second);
+          files_.erase(it);
+        }
+        continue;
+      }
+      present[name] = true;
+      Entry& e = it != files_.end() ? it->second : files_[name];
+      e.name_ino = name_ino;
+      e.name_pid = name_pid;
+      if (e.state == kExited) {
+        if (st.st_ino == e.gone_ino && st.st_size == e.gone_size && st.st_mtim.tv_sec == e.gone_mtime.tv_sec &&
+            st.st_mtim.tv_nsec == e.gone_mtime.tv_nsec)
+          continue;  // same leftover file: nothing new to prove
+        // it changed (a new writer re-creating the name?): examine once, and not again
+        // until it changes again
+        e.gone_ino = st.st_ino;
+        e.gone_size = st.st_size;
+        e.gone_mtime = st.st_mtim;
+      }
+      if (e.state == kUnverified && now < e.retry_ns) {
+        note_retry(e.retry_ns);
+        continue;
+      }
+      examine(name, &e, now, &procs);
+    }
+    ::closedir(d);
+    ignored_ = ignored;
+    for (auto it = files_.begin(); it != files_.end();) {
+      if (!present.count(it->first)) {
+        close_entry(&it->second);
+        it = files_.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
+
+  // Opens a tracer file, checks its content against its name and proves its writer.
+  void examine(const std::string& name, Entry* e, uint64_t now, std::unique_ptr<ProcMap>* procs) {
+    close_entry(e);
+    e->fd = ::openat(dfd_, name.c_str(), O_RDONLY | O_NOFOLLOW | O_NONBLOCK | O_CLOEXEC);
+    struct stat fst;
+    if (e->fd < 0 || ::fstat(e->fd, &fst) != 0 || !S_ISREG(fst.st_mode)) {
+      close_entry(e);
+      unverified(e, now);
+      return;
+    }
+    e->dev = fst.st_dev;
+    e->ino = fst.st_ino;
+    RcclShmFile snap;
+    if (!read_consistent(e->fd, &snap) || snap.magic != kRcclShmMagic || snap.pidns_ino != e->name_ino ||
+        snap.ns_pid != e->name_pid || snap.pidns_ino == 0 || snap.ns_pid <= 0) {
+      // not (yet) a complete file, or one whose content disagrees with its name
+      close_entry(e);
+      unverified(e, now);
+      return;
+    }
+    e->maps_id = maps_identity(e->fd, fst);
+    if (!identify(e, snap.pidns_ino, snap.ns_pid, procs)) {
+      close_entry(e);  // no fd for a file nobody is proven to write
+      unverified(e, now);
+      return;
+    }
+    e->state = kActive;
+    e->fails = 0;
+  }
+
+  void unverified(Entry* e, uint64_t now) {
+    if (e->state == kExited) return;  // re-examined when the file changes, not on a timer
+    e->state = kUnverified;
+    const int f = std::min(e->fails, 6);
+    e->retry_ns = now + (1000000000ull << f);  // 1 s .. 64 s
+    e->fails += 1;
+    note_retry(e->retry_ns);
+  }
+
+  void note_retry(uint64_t t) {
+    if (!next_retry_ns_ || t < next_retry_ns_) next_retry_ns_ = t;
+  }
+
+  void mark_exited(Entry* e, const struct stat& st) {
+    close_entry(e);  // writer exited (or was killed): its leftover file is not exported
+    e->state = kExited;
+    e->fails = 0;
+    e->gone_ino = st.st_ino;
+    e->gone_size = st.st_size;
+    e->gone_mtime = st.st_mtim;
   }
 
   // Two identical preads: the writer updates the counters with relaxed atomics while we
@@ -413,12 +568,6 @@ class ShmRcclSource : public RcclSource {
       std::memcpy(a, b, sizeof(a));
     }
     return false;
-  }
-
-  static void backoff(Entry* e, uint64_t now) {
-    const int f = std::min(e->fails, 6);
-    e->retry_ns = now + (1000000000ull << f);  // 1 s .. 64 s
-    e->fails += 1;
   }
 
   void release_owner(Entry* e) {
@@ -442,17 +591,27 @@ class ShmRcclSource : public RcclSource {
     return proc_starttime(e->host_pid) == e->starttime;
   }
 
+  static std::unique_ptr<ProcMap> build_proc_map() {
+    auto m = std::make_unique<ProcMap>();
+    for (const std::string& d : list_dir("/proc")) {
+      if (d.empty() || d[0] < '1' || d[0] > '9') continue;
+      const std::string pd = "/proc/" + d;
+      const uint64_t ns = pidns_inode(pd);
+      const int nspid = ns ? innermost_nspid(pd) : -1;
+      if (nspid > 0) (*m)[{ns, nspid}].push_back(std::atoi(d.c_str()));
+    }
+    return m;
+  }
+
   // Finds the host PID of (ns_ino, ns_pid) and proves it is this file's writer.
-  bool identify(Entry* e, uint64_t ns_ino, int ns_pid) {
+  bool identify(Entry* e, uint64_t ns_ino, int ns_pid, std::unique_ptr<ProcMap>* procs) {
     std::vector<int> cands;
     if (ns_ino == self_ns_) {
       cands.push_back(ns_pid);
     } else {
-      for (const std::string& d : list_dir("/proc")) {
-        if (d.empty() || d[0] < '1' || d[0] > '9') continue;
-        const std::string pd = "/proc/" + d;
-        if (pidns_inode(pd) == ns_ino && innermost_nspid(pd) == ns_pid) cands.push_back(std::atoi(d.c_str()));
-      }
+      if (!*procs) *procs = build_proc_map();
+      auto it = (*procs)->find({ns_ino, ns_pid});
+      if (it != (*procs)->end()) cands = it->second;
     }
     for (int pid : cands) {
       // Pin the process first, then check it, then check the pin still holds: no PID
@@ -497,8 +656,14 @@ class ShmRcclSource : public RcclSource {
 
   std::string dir_;
   bool verify_maps_;
+  uint64_t scan_interval_ns_;
   bool warned_maps_ = false;
   uint64_t self_ns_ = 0;
+  int dfd_ = -1;
+  bool scanned_ = false;
+  struct timespec dir_mtime_ {};
+  uint64_t last_scan_ns_ = 0, next_retry_ns_ = 0, scans_ = 0;
+  int ignored_ = 0;
   std::unordered_map<std::string, Entry> files_;
 };
 
@@ -549,12 +714,12 @@ std::unique_ptr<SentinelSource> make_queue_sentinel(const std::string& counters_
 std::string default_rocprof_plugin() { return self_dir() + "/_gpuexp_aqlpmc.so"; }
 
 std::unique_ptr<CounterSource> make_rocprof_counters(const std::string& plugin_path, int window_ms,
-                                                     int interval_ms) {
-  return std::make_unique<PluginCounters>(plugin_path, window_ms, interval_ms);
+                                                     int interval_ms, bool continuous) {
+  return std::make_unique<PluginCounters>(plugin_path, window_ms, interval_ms, continuous);
 }
 
-std::unique_ptr<RcclSource> make_rccl_source(const std::string& dir, bool verify_maps) {
-  return std::make_unique<ShmRcclSource>(dir, verify_maps);
+std::unique_ptr<RcclSource> make_rccl_source(const std::string& dir, bool verify_maps, double scan_interval_s) {
+  return std::make_unique<ShmRcclSource>(dir, verify_maps, uint64_t(std::max(0.0, scan_interval_s) * 1e9));
 }
 
 }  // namespace gpuexp

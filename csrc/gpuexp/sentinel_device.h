@@ -19,6 +19,12 @@ __device__ __forceinline__ void sentinel_init_chase_body(uint32_t* __restrict__ 
 // ring[run_slot * kSentinelMaxWaves + blockIdx.x]
 __device__ __forceinline__ void sentinel_body(SentinelSlot* __restrict__ ring, uint32_t slot, uint64_t seq, int spin,
                                               const uint32_t* chase, int hops) {
+  // Highest wave priority for the few microseconds this runs: next to workload waves that
+  // issue MFMAs back-to-back for seconds (a persistent GEMM / attention kernel), a
+  // priority-0 sentinel wave lost every VALU issue slot and never finished, and the PMC read
+  // packets queued behind its dispatch stalled with it (measured on MI355X with the MFMA
+  // duty kernel at 100 %: tools/mfma_calibration.py, profiles/r03/mfma_calibration.txt).
+  __builtin_amdgcn_s_setprio(3);
   if (threadIdx.x != 0) return;
   uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
   uint64_t mt0 = __builtin_amdgcn_s_memtime();

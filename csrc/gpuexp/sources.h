@@ -32,12 +32,24 @@ std::unique_ptr<SentinelSource> make_queue_sentinel(const std::string& counters_
 std::string default_rocprof_plugin();
 
 // Derived values a counter plugin's gpuexp_rp_sample fills, in CounterReading order.
-constexpr int kCounterOutputs = 10;
+constexpr int kCounterOutputs = 11;
 
 class CounterSource {
  public:
   virtual ~CounterSource() = default;
   virtual bool start(const std::vector<DeviceInfo>& devs, std::string* err) = 0;
+  // Continuous mode: kick() at the start of a tick asks the plugin for one counter read per
+  // GPU (non-blocking); sync() waits, at most `timeout_us`, for that round, so the values
+  // sample() returns in the same tick cover exactly the last tick interval.  Duty-cycled
+  // plugins ignore both.  sync() returns false when the round did not finish in time (the
+  // previous window is exported again).
+  virtual void kick() {}
+  // Cumulative CPU time of the plugin's own thread(s), ns (0 if unknown).
+  virtual uint64_t cpu_ns() { return 0; }
+  virtual bool sync(int timeout_us) {
+    (void)timeout_us;
+    return true;
+  }
   virtual bool sample(int dev, double dt_s, CounterReading* out) = 0;
   // -1 unknown, 0 = wave/LDS/EA counters only see this process (VMID-filtered), 1 = device-wide.
   virtual int scope(int dev) {
@@ -47,10 +59,11 @@ class CounterSource {
   virtual void stop() = 0;
   virtual std::string status() const = 0;
 };
-// dlopen()s the rocprofiler-sdk plugin (_gpuexp_rocprof.so) next to the core.  Counting
-// runs duty-cycled in the plugin: a `window_ms` counting window every `interval_ms`.
+// dlopen()s a counter plugin (_gpuexp_aqlpmc.so or _gpuexp_rocprof.so) next to the core.
+// continuous (aqlprofile plugin only): counting runs without a break and is read once per
+// engine tick; otherwise duty-cycled: a `window_ms` counting window every `interval_ms`.
 std::unique_ptr<CounterSource> make_rocprof_counters(const std::string& plugin_path, int window_ms,
-                                                     int interval_ms);
+                                                     int interval_ms, bool continuous = false);
 
 // One collective call record written by the RCCL tracer tool into a per-process ring.
 struct RcclTotals {
@@ -71,8 +84,14 @@ class RcclSource {
   virtual void file_states(int* active, int* unverified, int* exited) const {
     *active = *unverified = *exited = 0;
   }
+  // Directory entries the last listing skipped: not tracer files, not regular files, or
+  // over the tracked-file cap.
+  virtual int ignored() const { return 0; }
+  virtual uint64_t scans() const { return 0; }  // directory listings so far
 };
 // verify_maps: a file is attributed only to a process that maps it (/proc/<pid>/maps).
-std::unique_ptr<RcclSource> make_rccl_source(const std::string& dir, bool verify_maps = true);
+// scan_interval_s: the directory is listed at most this often (and only when it changed).
+std::unique_ptr<RcclSource> make_rccl_source(const std::string& dir, bool verify_maps = true,
+                                             double scan_interval_s = 1.0);
 
 }  // namespace gpuexp

@@ -23,4 +23,17 @@ struct CalibLdsArgs {
   int stride;  // 1 (conflict-free) or 32 (32-way bank conflicts)
 };
 
+// MFMA duty-cycle workload (mfma_duty_body): every wave alternates `on_ticks` of
+// back-to-back v_mfma_f32_32x32x16_bf16 with `period_ticks - on_ticks` of s_sleep, for
+// `total_ticks`, on the 100 MHz s_memrealtime clock.  Launched with 2 waves per SIMD the
+// matrix cores are busy for on/period of the wall time while the kernel stays resident.
+struct CalibMfmaArgs {
+  float* out;             // >= blocks floats (sink, keeps the MFMAs live)
+  uint64_t* mfma_count;   // >= blocks * 4 counters: MFMAs issued per wave
+  uint64_t period_ticks;  // s_memrealtime ticks (10 ns) per on/off period
+  uint64_t on_ticks;      // MFMA phase of each period (<= period_ticks)
+  uint64_t total_ticks;   // run length
+};
+constexpr int kMfmaPerCheck = 32;  // MFMAs between two clock reads (32 x 32 cycles)
+
 }  // namespace gpuexp

@@ -49,8 +49,9 @@ class Config:
     sentinel_impl: str = "auto"            # auto (on the PMC counters' queue when they run, else HIP) | hip | queue
     enable_counters: bool = False
     counters_plugin: str = "aqlpmc"        # aqlpmc | rocprof | /path/to/plugin.so
-    counters_window_ms: int = 20           # rocprofiler counting window ...
-    counters_interval_ms: int = 1000       # ... per interval (context-started spin is duty-cycled)
+    counters_mode: str = "continuous"      # continuous (never paused, read every tick; aqlpmc) | duty
+    counters_window_ms: int = 20           # duty: counting window ...
+    counters_interval_ms: int = 1000       # ... per interval (the rocprof plugin's spin is duty-cycled)
     queue_devices: list = field(default_factory=list)  # GPUs (indices / BDFs) that get the exporter's
                                            # own GPU queue (sentinel + PMC counters); empty = all.
                                            # Each queue pins ~346 MiB of host memory on MI355X.
@@ -146,6 +147,7 @@ class Config:
             ec.counters_plugin = rocprof_plugin_path(self.counters_plugin or "aqlpmc")
         else:
             ec.counters_plugin = self.counters_plugin
+        ec.counters_mode = str(self.counters_mode)
         ec.counters_window_ms = int(self.counters_window_ms)
         ec.counters_interval_ms = int(self.counters_interval_ms)
         ec.enable_rccl = bool(self.enable_rccl)
@@ -283,6 +285,8 @@ def validate(cfg: Config) -> None:
         raise ValueError("log_format must be logfmt|json")
     if cfg.sentinel_impl not in ("auto", "hip", "queue"):
         raise ValueError(f"sentinel_impl must be auto|hip|queue, got {cfg.sentinel_impl}")
+    if cfg.counters_mode not in ("continuous", "duty"):
+        raise ValueError(f"counters_mode must be continuous|duty, got {cfg.counters_mode}")
     if cfg.stale_after < 0 and cfg.stale_after != -1:
         raise ValueError("stale_after must be -1 (auto), 0 (never) or > 0 seconds")
     host, _ = cfg.listen_host_port()

@@ -256,7 +256,7 @@ def test_full_profile_adds_reliability_families(mock_engine):
     e.mock_set_value(1, "aer_cor", 7)
     ticks(e, 3)
     fams = parse(e)
-    assert dict(device_series_per_gpu(fams)) == {"0": 117, "1": 117}  # + board (1), firmware (4 in mock)
+    assert dict(device_series_per_gpu(fams)) == {"0": 118, "1": 118}  # + board (1), firmware (4 in mock), MFMA util (1)
     lat = {s[1]["xcc"]: s[2] for s in fams["amd_gpu_sentinel_xcc_dispatch_latency_seconds"].samples
            if s[1]["gpu"] == "0"}
     assert sorted(lat) == [str(x) for x in range(8)] and min(lat.values()) == lat["0"]

@@ -42,12 +42,18 @@ def write_shm(path, ns_pid, ops, ino=NS_INO):
 
 
 def rccl_engine(mock_engine, d, **kw):
+    # these tests change the directory between manual ticks a few ms apart: list it every
+    # time it changed (the default lists it at most once a second: test_junk_directory_*)
+    kw.setdefault("rccl_scan_interval_s", 0.0)
     return mock_engine(1, http=False, enable_rccl=True, rccl_dir=str(d), **kw)
 
 
-def states(e):
+def states(e, ignored=False):
     fams = promtext.parse(e.snapshot_text())
-    return {lab["state"]: v for _, lab, v in promtext.samples(fams, "gpuexp_rccl_files")}
+    st = {lab["state"]: v for _, lab, v in promtext.samples(fams, "gpuexp_rccl_files")}
+    if not ignored:
+        st.pop("ignored", None)
+    return st
 
 
 def test_rccl_counters_attributed_to_pod(mock_engine, tmp_path):
@@ -130,9 +136,10 @@ def test_identity_must_match_name_and_be_nonzero(mock_engine, tmp_path):
     m2.close()
 
 
-def _writer(d, claim_pid=None):
+def _writer(d, claim_pid=None, count_every_s=0.0):
     """A child that creates + maps its counters file (optionally claiming another PID in
-    its content and name) and then sleeps until killed."""
+    its content and name) and then sleeps until killed (count_every_s > 0: it adds one
+    allreduce call of 100 bytes at that period instead)."""
     code = textwrap.dedent(f"""
         import mmap, os, struct, sys, time
         pid = {claim_pid!r} or os.getpid()
@@ -145,7 +152,15 @@ def _writer(d, claim_pid=None):
         struct.pack_into('<QQ', m, 64, 5, 500)
         struct.pack_into('<Q', m, 0, {MAGIC})
         print(p, flush=True)
-        time.sleep(600)
+        n, period = 5, {count_every_s!r}
+        t_end = time.time() + 600
+        while time.time() < t_end:
+            if period <= 0:
+                time.sleep(600)
+                continue
+            time.sleep(period)
+            n += 1
+            struct.pack_into('<QQ', m, 64, n, 100 * n)
     """)
     p = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True)
     path = p.stdout.readline().strip()
@@ -255,3 +270,66 @@ def test_writer_proof_on_overlayfs(mock_engine, tmp_path):
                 w.wait()
     finally:
         subprocess.run(["umount", "-l", str(merged)], capture_output=True)
+
+
+def test_junk_directory_costs_bounded(mock_engine, tmp_path):
+    """The tracer directory is a hostPath every workload pod can write.  10,000 junk
+    entries (plain files with other names, FIFOs and symlinks with tracer names, files
+    with tracer names nobody maps) next to 8 live tracer files: at 100 Hz the sampler's
+    CPU per tick stays under 1 ms and its p99 tick (wall, so including this box's
+    scheduling noise under a parallel test run) under 5 ms, the directory is listed about
+    once a second (not per tick), the junk is counted as ignored / unverified, and the 8
+    live files' counters keep advancing."""
+    import json
+    d = tmp_path / "rccl"
+    d.mkdir()
+    victim = os.getpid() + 100000
+    for i in range(7000):
+        (d / f"junk-{i}").write_bytes(b"x")
+    for i in range(1000):
+        os.mkfifo(d / shm_name(victim + i))
+    for i in range(1000):
+        os.symlink("/etc/hostname", d / shm_name(victim + 1000 + i))
+    for i in range(1000):  # well-formed names, content claiming processes that do not exist
+        (d / shm_name(victim + 2000 + i)).write_bytes(b"\0" * SIZE)
+    writers = [_writer(d, count_every_s=0.02) for _ in range(8)]
+    trace = tmp_path / "trace.json"
+    try:
+        e = mock_engine(1, http=False, enable_rccl=True, rccl_dir=str(d), interval_s=0.01,
+                        trace_path=str(trace))
+        for p, _ in writers:
+            e.set_pid_cgroup(p.pid, CG)
+        e.set_pods([dict(uid=UID, namespace="train", name="dp-worker-0", containers={})])
+        time.sleep(1.5)
+
+        def calls():
+            fams = promtext.parse(e.snapshot_text())
+            return {lab["pid"]: v for _, lab, v in promtext.samples(fams, "amd_rccl_collective_calls_total")
+                    if lab["op"] == "allreduce"}
+        first = calls()
+        time.sleep(1.5)
+        second = calls()
+        st = states(e, ignored=True)
+        scans = promtext.value(promtext.parse(e.snapshot_text()), "gpuexp_rccl_dir_scans_total")
+        es = e.stats()
+        cpu_per_tick_us = es["sampler_cpu_ns"] / max(1, es["ticks"]) / 1e3
+        e.stop()
+    finally:
+        for p, _ in writers:
+            p.kill()
+            p.wait()
+    assert sorted(first) == sorted(str(p.pid) for p, _ in writers), first
+    assert all(second[k] > first[k] for k in first), (first, second)
+    assert st["active"] == 8, st
+    assert scans <= 6, scans  # ~1 listing per second over the 3 s (the writers never touch the dir)
+    assert st["ignored"] >= 9000, st   # 7000 other names + 2000 FIFOs / symlinks
+    assert st["unverified"] >= 1000 - 8 or st["unverified"] + st["ignored"] >= 9990, st
+    # per-tick sampler time from the Chrome trace (8 stage events per tick)
+    ev = [x for x in json.loads(trace.read_text()) if x.get("ph") == "X"]
+    per_tick = [sum(x["dur"] for x in ev[i:i + 8]) for i in range(0, len(ev) - 7, 8)]
+    per_tick = sorted(per_tick[len(per_tick) // 4:])  # after start-up
+    p99 = per_tick[int(0.99 * (len(per_tick) - 1))]
+    print(f"{len(per_tick)} ticks: p50 {per_tick[len(per_tick) // 2]:.0f} us, p99 {p99:.0f} us, "
+          f"sampler CPU {cpu_per_tick_us:.0f} us/tick, {scans:.0f} listings, states {st}")
+    assert cpu_per_tick_us < 1000, cpu_per_tick_us
+    assert p99 < 5000, p99
