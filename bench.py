@@ -85,6 +85,7 @@ def start_exporter(args, n_gpus: int, backend: str, port: int, pod_map: str, log
     env["GPUEXP_POD_MAP_FILE"] = pod_map
     env["GPUEXP_POD_ATTRIBUTION"] = "true"
     logf = open(log_path, "w")
+    t_start = time.perf_counter()
     proc = subprocess.Popen(cmd, env=env, stdout=logf, stderr=subprocess.STDOUT, cwd=ROOT)
     deadline = time.time() + 120
     while time.time() < deadline:
@@ -93,6 +94,9 @@ def start_exporter(args, n_gpus: int, backend: str, port: int, pod_map: str, log
         try:
             st, _ = http_get(port, "/readyz", 0.5)
             if st == 200:
+                # process start -> first published sample: amdsmi init + raw-path validation,
+                # one HSA queue per GPU (PMC + sentinel), plugin probes, first tick
+                proc.startup_s = time.perf_counter() - t_start
                 return proc
         except OSError:
             pass
@@ -110,6 +114,57 @@ def pct(v: list, q: float) -> float:
     return v[lo] + (v[hi] - v[lo]) * (k - lo)
 
 
+def startup_budget_s(n_gpus: int) -> float:
+    """Exporter start -> first sample: amdsmi + raw-path validation and one HSA queue per GPU
+    (measured 1 GPU: ~4-6 s on MI355X boxes, most of it HSA/amdsmi init)."""
+    return 30.0 + 5.0 * n_gpus
+
+
+def prewake_summary(lat: list, prewoken: list, splits: list) -> dict | None:
+    if not lat or len(prewoken) != len(lat):
+        return None
+    hit = [l for l, p in zip(lat, prewoken) if p == 1]
+    miss = [l for l, p in zip(lat, prewoken) if p == 0]
+    out = {"timed_scrapes": len(lat), "prewoken": len(hit), "not_prewoken": len(miss),
+           "unknown": len(lat) - len(hit) - len(miss),
+           "hit_rate": round(len(hit) / len(lat), 3),
+           "p50_us_prewoken": round(statistics.median(hit), 2) if hit else None,
+           "p50_us_not_prewoken": round(statistics.median(miss), 2) if miss else None}
+    for name, flag in (("request_to_server_p50_us_prewoken", 1), ("request_to_server_p50_us_not_prewoken", 0)):
+        v = [x[0] for x in splits if x[3] == flag]
+        out[name] = round(statistics.median(v), 2) if v else None
+    return out
+
+
+def run_problems(result: dict, n_gpus: int, attribution_ok: bool, rccl_on: bool) -> list:
+    """Why an N-GPU result is not a valid measurement of the configuration (N > 1; at N = 1
+    problems are recorded in the result but the line is still printed).  Every GPU must be
+    exported, every rank's pod attributed, every rank's RCCL communicator span all N ranks,
+    no optional source dropped, and the exporter up within its start-up budget."""
+    probs = []
+    got = len(result["series_per_gpu"])
+    if got != n_gpus:
+        probs.append(f"series_per_gpu covers {got} GPUs, not {n_gpus}: {sorted(result['series_per_gpu'])}")
+    want = {f"gemm-pod-{r}" for r in range(n_gpus)}
+    if not attribution_ok or set(result["attributed_pods"]) != want:
+        probs.append(f"attributed pods {result['attributed_pods']} != {sorted(want)}")
+    if rccl_on:
+        ranks = result.get("rccl_rank_per_pod") or {}
+        bad = {p: rn for p, rn in ranks.items() if rn[1] != n_gpus}
+        missing = sorted(want - set(ranks))
+        if bad or missing:
+            probs.append(f"RCCL communicators: pods without one {missing}, nranks != {n_gpus}: {bad}")
+    reason = result["optional_sources"].get("degraded_reason")
+    if reason:
+        probs.append(f"exporter ran degraded: {reason}")
+    if result["exporter_startup_s"] > result["exporter_startup_budget_s"]:
+        probs.append(f"exporter start-up {result['exporter_startup_s']} s > budget {result['exporter_startup_budget_s']} s")
+    if n_gpus == 1:
+        result["problems"] = probs or None
+        return []
+    return probs
+
+
 def launch_ranks(args, argv: list) -> int:
     """`bench.py --gpus N` without a launcher: start N rank processes (one per GPU, env
     rendezvous on 127.0.0.1) and relay rank 0's result line.  This parent never imports
@@ -118,12 +173,15 @@ def launch_ranks(args, argv: list) -> int:
     import signal
     port = free_port()
     procs = []
+    # rank 0's stdout goes to a file read after every rank exited (a pipe read only then
+    # would block rank 0 once it printed more than the pipe buffer)
+    out0 = tempfile.TemporaryFile()
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), GPUEXP_BENCH_LAUNCHER=str(os.getpid()))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env, cwd=ROOT,
-                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(),
+                                      stdout=out0 if r == 0 else sys.stderr.fileno(),
                                       start_new_session=True))
 
     def kill_all(sig=signal.SIGTERM):
@@ -162,7 +220,9 @@ def launch_ranks(args, argv: list) -> int:
             kill_all(signal.SIGKILL)
             failed = failed or (-1, 124)
         time.sleep(0.1)
-    out = procs[0].stdout.read().decode(errors="replace")
+    out0.seek(0)
+    out = out0.read().decode(errors="replace")
+    out0.close()
     lines = [l for l in out.splitlines() if l.startswith("{")]
     if failed is None and procs[0].returncode == 0 and len(lines) == 1:
         sys.stdout.write(lines[0] + "\n")
@@ -332,12 +392,16 @@ def main() -> int:
     iters = 0
     gemm_ms = 0.0
     if use_gpu:
-        gemm_burst(2)
+        # GEMM time from GPU events over 20 back-to-back dispatches after a 10-dispatch
+        # warm-up (clocks settled): the rate rocprofv3's kernel trace gives, not a host timer
+        # around a handful of launches
+        gemm_burst(10)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        gemm_burst(20)
+        ev1.record()
         sync()
-        t0 = time.perf_counter()
-        gemm_burst(5)
-        sync()
-        gemm_ms = (time.perf_counter() - t0) / 5 * 1e3
+        gemm_ms = ev0.elapsed_time(ev1) / 20
         iters = max(1, int(args.busy * period * 1e3 / gemm_ms))
         if dist is not None:
             t = torch.tensor([iters], device=dev)
@@ -363,9 +427,13 @@ def main() -> int:
         dist.all_gather_object(pids, (pid, own_pid, my_bdf))
     else:
         pids = [(pid, own_pid, my_bdf)]
+    attribution_ok = True
     if rank == 0:
         pods, cgroups = [], {}
+        hidden = os.environ.get("GPUEXP_BENCH_NO_POD_RANK")  # test hook: this rank's pod never attributes
         for r, (p, op, _) in enumerate(pids):
+            if hidden == str(r):
+                continue
             uid = f"00000000-0000-4000-8000-{r:012d}"
             cid = f"{r:064x}"
             pods.append({"uid": uid, "namespace": "bench", "name": f"gemm-pod-{r}", "containers": {cid: "worker"}})
@@ -392,6 +460,7 @@ def main() -> int:
                 pass
             time.sleep(0.1)
         else:
+            attribution_ok = False
             print(f"[bench] exporter did not attribute all {len(want)} ranks within 20 s", file=sys.stderr, flush=True)
         # timing=True: the server echoes when it parsed the request and started writing,
         # so each latency splits into request wake-up / server work / response delivery
@@ -401,6 +470,7 @@ def main() -> int:
         client = None
 
     splits: list = []
+    prewoken: list = []  # per timed headline scrape: 1 pre-woken worker, 0 not, -1 unknown
 
     def step(cl, lat: list | None):
         t_start = time.perf_counter()
@@ -412,8 +482,11 @@ def main() -> int:
                 lat.append(ns / 1e3)
                 if cl is client:
                     t_send, t_parse, t_write, t_done = cl.last_timing()
+                    pw = cl.last_prewoken()
+                    prewoken.append(pw)
                     if t_parse and t_send <= t_parse <= t_write <= t_done:
-                        splits.append(((t_parse - t_send) / 1e3, (t_write - t_parse) / 1e3, (t_done - t_write) / 1e3))
+                        splits.append(((t_parse - t_send) / 1e3, (t_write - t_parse) / 1e3, (t_done - t_write) / 1e3,
+                                       pw))
         if dist is not None:
             dist.all_reduce(grad)
         sync()
@@ -694,6 +767,8 @@ def main() -> int:
             "server_scrapes": server_scrapes,
             "exporter_cpu_percent": round(cpu_pct, 3),
             "exporter_rss_mb": round(exporter_rss_kb[0] / 1024, 1) if exporter_rss_kb[0] else None,
+            "exporter_startup_s": round(getattr(exporter, "startup_s", 0.0), 2),
+            "exporter_startup_budget_s": startup_budget_s(n_gpus),
             "scrape_encoding": "gzip (Prometheus default Accept-Encoding)" if args.gzip else "identity",
             "p50_scrape_identity_us": round(statistics.median(lat_id), 2) if lat_id else None,
             "p99_scrape_identity_us": round(pct(lat_id, 0.99), 2) if lat_id and len(lat_id) >= 100 else None,
@@ -707,6 +782,13 @@ def main() -> int:
                 "request_to_server": round(statistics.median(x[0] for x in splits), 2),
                 "server_work": round(statistics.median(x[1] for x in splits), 2),
                 "response_to_client": round(statistics.median(x[2] for x in splits), 2)} if splits else None,
+            "latency_split_p90_us": {
+                "request_to_server": round(pct([x[0] for x in splits], 0.9), 2),
+                "server_work": round(pct([x[1] for x in splits], 0.9), 2),
+                "response_to_client": round(pct([x[2] for x in splits], 0.9), 2)} if splits else None,
+            # every timed scrape accounted for: did it reach an HTTP worker that its pre-wake
+            # timer had already woken (gpuexp_http_prewake_hits_total), or one asleep in epoll?
+            "prewake": prewake_summary(lat, prewoken, splits),
             "scrapes": len(lat),
             "scrape_errors": client.errors,
             "scrape_bytes": client.last_bytes,
@@ -779,14 +861,20 @@ def main() -> int:
                                   "scrape_errors": rclient.errors}
             if rlat and lat:
                 result["speedup_p50_vs_refstyle"] = round(statistics.median(rlat) / statistics.median(lat), 2)
-    if rank == 0:
+    problems = run_problems(result, n_gpus, attribution_ok, bool(rccl_dir)) if rank == 0 else []
+    if rank == 0 and not problems:
         print(json.dumps(result), file=result_out, flush=True)
-        if args.out:
-            with open(args.out, "w") as fh:
-                json.dump(result, fh, indent=1)
+    if rank == 0 and args.out:
+        with open(args.out, "w") as fh:
+            json.dump(dict(result, problems=problems), fh, indent=1)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    if problems:
+        # a degraded N-GPU run must not pass for a measurement: no result line, exit 1
+        for p in problems:
+            print(f"[bench] FAILED: {p}", file=sys.stderr, flush=True)
+        return 1
     return 0
 
 

@@ -152,6 +152,7 @@ double ScrapeClient::scrape() {
   t_send_ = t0;
   t_done_ = t1;
   t_srv_parse_ = t_srv_write_ = 0;
+  srv_prewoken_ = -1;
   {
     // the response's header block ends 4 bytes before the body
     static const char kName[] = "\r\nX-Gpuexp-Timing: ";
@@ -162,7 +163,9 @@ double ScrapeClient::scrape() {
       p += sizeof(kName) - 1;
       char* q = nullptr;
       t_srv_parse_ = std::strtoull(p, &q, 10);
-      t_srv_write_ = q ? std::strtoull(q, nullptr, 10) : 0;
+      char* r = nullptr;
+      t_srv_write_ = q ? std::strtoull(q, &r, 10) : 0;
+      srv_prewoken_ = r && *r == ' ' ? int(std::strtol(r, nullptr, 10)) : -1;
     }
   }
   if (server_close) {

@@ -304,6 +304,10 @@ void Engine::define_families() {
   f_self_http_bytes_ = add("gpuexp_http_response_bytes_total", "HTTP response bytes written", C, {});
   f_self_prewake_ = add("gpuexp_http_prewake_wakeups_total",
                         "Timer wake-ups of the HTTP worker ahead of expected scrapes (scrape-phase pre-wake)", C, {});
+  f_self_prewake_hits_ = add("gpuexp_http_prewake_hits_total",
+                             "Scrapes of the metrics path that arrived while their HTTP worker was pre-woken "
+                             "(its pre-wake timer fired within the lead + one slice before the request)",
+                             C, {});
   f_self_gzip_ = add("gpuexp_gzip_compressions_total",
                      "gzip compressions of the exposition: by the sampler (a gzip scrape was expected before "
                      "the next tick) or per request (off schedule)",
@@ -1270,9 +1274,12 @@ void Engine::emit_self(uint64_t gen) {
     }
     cput(self_refs_[9], f_self_scrapes_, double(hs.metrics_requests.load(std::memory_order_relaxed)), gen, none);
     cput(self_refs_[10], f_self_http_bytes_, double(hs.bytes_sent.load(std::memory_order_relaxed)), gen, none);
-    if (cfg_.http.prewake)
+    if (cfg_.http.prewake) {
       cput(self_refs_[11], f_self_prewake_, double(hs.prewake_timer_wakeups.load(std::memory_order_relaxed)), gen,
            none);
+      cput(prewake_hits_ref_, f_self_prewake_hits_, double(hs.prewake_hits.load(std::memory_order_relaxed)), gen,
+           none);
+    }
     if (cfg_.http.enable_gzip) {
       cput(self_refs_[16], f_self_gzip_, double(gzip_eager_), gen,
            [] { return std::vector<std::string>{"sampler"}; });

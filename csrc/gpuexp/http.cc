@@ -23,9 +23,11 @@
 namespace gpuexp {
 
 const std::vector<double>& scrape_latency_bounds() {
-  static const std::vector<double> b = {5e-6,  10e-6, 25e-6, 50e-6, 100e-6, 250e-6,
-                                        500e-6, 1e-3,  2.5e-3, 5e-3, 10e-3, 25e-3,
-                                        50e-3, 100e-3, 250e-3, 1.0};
+  // fine where scrapes sit (server side: a few to a few tens of microseconds), coarse above
+  static const std::vector<double> b = {1e-6,   2e-6,   3e-6,   5e-6,   7.5e-6, 10e-6,  15e-6, 20e-6,
+                                        25e-6,  35e-6,  50e-6,  75e-6,  100e-6, 250e-6, 500e-6, 1e-3,
+                                        2.5e-3, 5e-3,   10e-3,  25e-3,  100e-3, 250e-3, 1.0};
+  static_assert(HttpStats::kBuckets == 23, "bucket count");
   return b;
 }
 
@@ -275,6 +277,7 @@ void HttpServer::run(Worker* w) {
   epoll_event events[kMaxEvents];
   char rbuf[16384];
   uint64_t last_sweep = mono_ns();
+  uint64_t last_prewake_ns = 0;  // this worker's last pre-wake timer expiry
 
   auto close_conn = [&](int fd) {
     ::epoll_ctl(w->epfd, EPOLL_CTL_DEL, fd, nullptr);
@@ -416,6 +419,9 @@ void HttpServer::run(Worker* w) {
         respond_simple(c, 405, "Method Not Allowed", "text/plain", "method not allowed\n", false);
       } else if (path == cfg_.metrics_path) {
         stats_.metrics_requests.fetch_add(1, std::memory_order_relaxed);
+        const bool prewoken = last_prewake_ns && t0 >= last_prewake_ns &&
+                              t0 - last_prewake_ns <= cfg_.prewake_lead_ns + cfg_.prewake_step_ns;
+        if (prewoken) stats_.prewake_hits.fetch_add(1, std::memory_order_relaxed);
         if (c.last_metrics_ns && t0 > c.last_metrics_ns) {
           c.intervals[c.iv_pos] = t0 - c.last_metrics_ns;
           c.iv_pos = (c.iv_pos + 1) & 3;
@@ -463,7 +469,7 @@ void HttpServer::run(Worker* w) {
             c.head.append(std::to_string(t0));
             c.head.append(" ");
             c.head.append(std::to_string(mono_ns()));
-            c.head.append("\r\n");
+            c.head.append(prewoken ? " 1\r\n" : " 0\r\n");  // pre-woken worker?
           }
           c.head.append("Content-Length: ");
           c.head.append(std::to_string(b.size()));
@@ -544,6 +550,7 @@ void HttpServer::run(Worker* w) {
         ssize_t r = ::read(w->timerfd, &expirations, sizeof(expirations));
         (void)r;
         stats_.prewake_timer_wakeups.fetch_add(1, std::memory_order_relaxed);
+        last_prewake_ns = mono_ns();
         continue;
       }
       if (fd == w->listen_fd) {

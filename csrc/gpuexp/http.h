@@ -56,7 +56,7 @@ struct HttpConfig {
 const std::vector<double>& scrape_latency_bounds();
 
 struct HttpStats {
-  static constexpr int kBuckets = 16;
+  static constexpr int kBuckets = 23;
   std::atomic<uint64_t> requests{0};
   std::atomic<uint64_t> metrics_requests{0};
   std::atomic<uint64_t> gzip_responses{0};
@@ -71,6 +71,10 @@ struct HttpStats {
   std::atomic<uint64_t> writev_ns{0};
   std::atomic<uint64_t> partial_writes{0};
   std::atomic<uint64_t> prewake_timer_wakeups{0};  // timer expiries of the scrape pre-wake
+  // /metrics requests parsed while their worker was pre-woken (its pre-wake timer fired
+  // within prewake_lead_ns + prewake_step_ns before the request): the rest paid a full
+  // wake-up from an idle epoll_wait
+  std::atomic<uint64_t> prewake_hits{0};
   // gzip responses the worker compressed itself: the snapshot had no gzip copy because no
   // gzip scrape was expected before the next tick (see HttpServer::gzip_due)
   std::atomic<uint64_t> gzip_on_demand{0};

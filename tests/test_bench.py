@@ -106,3 +106,34 @@ def test_bench_torchrun_two_ranks():
     assert len(lines) == 1, r.stdout[-2000:]   # rank 0 only
     _check(lines[0], 2, 4, 1)
     assert lines[0]["attributed_pods"] == ["gemm-pod-0", "gemm-pod-1"] or lines[0]["config"]["backend"] == "mock"
+
+
+def test_bench_eight_ranks_every_check_holds():
+    """The driver's 8-GPU shape, rehearsed on CPU (8 gloo ranks, 8 mock GPUs): one line,
+    every GPU exported, every rank's pod attributed, and the run's own validity checks
+    (bench.run_problems) empty; the timed scrapes are each accounted pre-woken or not."""
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "8", "--backend", "mock", "--steps", "4", "--warmup",
+                        "1", "--xgmi-patterns", "0"], cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    (d,) = _json_lines(r.stdout)
+    _check(d, 8, 4, 1)
+    assert sorted(d["series_per_gpu"], key=int) == [str(i) for i in range(8)]
+    assert d["attributed_pods"] == sorted(f"gemm-pod-{i}" for i in range(8))
+    assert 0 < d["exporter_startup_s"] <= d["exporter_startup_budget_s"]
+    pw = d["prewake"]
+    assert pw["timed_scrapes"] == 4 and pw["prewoken"] + pw["not_prewoken"] + pw["unknown"] == 4, pw
+    assert pw["unknown"] == 0, pw  # the server echoes the pre-wake state of every timed scrape
+
+
+def test_bench_unattributed_rank_fails_loudly():
+    """At N > 1 a rank whose pod never attributes makes the run invalid: exit 1, no result
+    line (a degraded configuration must not reach SCALE as a number)."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", GPUEXP_BENCH_NO_POD_RANK="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--backend", "mock", "--steps", "3", "--warmup",
+                        "1", "--xgmi-patterns", "0"], cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0
+    assert not _json_lines(r.stdout)
+    assert "FAILED: attributed pods" in r.stderr, r.stderr[-2000:]

@@ -737,6 +737,44 @@ def test_device_counters_under_gemm(plugin, monkeypatch):
         assert max(p for p, _ in res["hot_threads"]) < 20.0, res
 
 
+def test_mfma_busy_calibration():
+    """amd_gpu_mfma_busy_percent against kernels of known MFMA duty (tools/mfma_calibration.py):
+    the engine at 10 Hz with continuous counters while 2 waves per SIMD alternate
+    back-to-back v_mfma_f32_32x32x16_bf16 with s_sleep at 25/50/75/100 % of the wall time.
+
+    * every resident case reads within 10 points of its duty (the counter is cycle-weighted:
+      the chip clocks down during the MFMA phases, so it reads a few points low), and
+      changes every tick (continuous counting: each tick exports its own interval);
+    * SQ_VALU_MFMA_BUSY_CYCLES over each kernel's life equals 32 cycles per MFMA the kernel
+      counted itself issuing (MI355X_MICROARCH.md cycle constants) within 1 %;
+    * gated cases (100 % MFMA kernels for 25 / 50 % of every 20 ms, idle between): busy =
+      GUI-active x MfmaUtil, and MfmaUtil (while active) stays high;
+    * an idle GPU reads 0."""
+    import json
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mfma_calibration.py"), "--duties",
+                        "0.25,0.5,0.75,0.98"], capture_output=True, text=True, timeout=200)
+    print(r.stdout[-4000:], r.stderr[-3000:])
+    line = [l for l in r.stdout.splitlines() if l.startswith("RESULT ")]
+    assert line, "calibration produced no result"
+    res = json.loads(line[-1][7:])
+    if "counters=unavailable" in res["status"]:
+        pytest.skip("device counting unavailable on this box: " + res["status"])
+    assert "continuous" in res["status"], res["status"]
+    cases = res["cases"]
+    assert cases["idle"]["busy_median"] == 0.0, cases["idle"]
+    for key in ("resident_0.25", "resident_0.5", "resident_0.75", "resident_0.98"):
+        c = cases[key]
+        assert c["ticks"] >= 15, (key, c["ticks"])
+        assert abs(c["busy_median"] - c["expected_busy"]) <= 10.0, (key, c["busy_median"], c["expected_busy"])
+        assert c["changed_fraction"] >= 0.9, (key, c["per_tick_busy"])
+        assert abs(c["mfma_busy_cycles_over_32x_issued"] - 1.0) < 0.01, (key, c["mfma_busy_cycles_over_32x_issued"])
+    for key in ("gated_0.5", "gated_0.25"):
+        c = cases[key]
+        assert c["util_median"] > 80, (key, c)
+        assert abs(c["busy_median"] - c["gui_median"] * c["util_median"] / 100.0) < 5.0, (key, c)
+        assert c["changed_fraction"] >= 0.9, (key, c["per_tick_busy"])
+
+
 def test_device_scope_pmc_calibration():
     """Device-scope PMC families against ground truth (tools/pmc_validate.py): HBM read and
     write of a stream copy of known bytes, waves/s of known grids, and LDS bank conflicts

@@ -276,8 +276,9 @@ def test_junk_directory_costs_bounded(mock_engine, tmp_path):
     """The tracer directory is a hostPath every workload pod can write.  10,000 junk
     entries (plain files with other names, FIFOs and symlinks with tracer names, files
     with tracer names nobody maps) next to 8 live tracer files: at 100 Hz the sampler's
-    CPU per tick stays under 1 ms and its p99 tick (wall, so including this box's
-    scheduling noise under a parallel test run) under 5 ms, the directory is listed about
+    CPU per tick stays under 1 ms (a listing per tick of 10,000 entries would cost several),
+    its p50 tick under 2 ms and p99 under 20 ms (wall clock, so including this box's
+    scheduling noise under a parallel test run), the directory is listed about
     once a second (not per tick), the junk is counted as ignored / unverified, and the 8
     live files' counters keep advancing."""
     import json
@@ -332,4 +333,5 @@ def test_junk_directory_costs_bounded(mock_engine, tmp_path):
     print(f"{len(per_tick)} ticks: p50 {per_tick[len(per_tick) // 2]:.0f} us, p99 {p99:.0f} us, "
           f"sampler CPU {cpu_per_tick_us:.0f} us/tick, {scans:.0f} listings, states {st}")
     assert cpu_per_tick_us < 1000, cpu_per_tick_us
-    assert p99 < 5000, p99
+    assert per_tick[len(per_tick) // 2] < 2000, per_tick[len(per_tick) // 2]
+    assert p99 < 20000, p99

@@ -5,7 +5,9 @@ kernel) for `seconds` per trial, alternating trials with no exporter and with th
 exporter sampling at 10 Hz and 100 Hz (amdsmi raw path + HIP sentinel + aqlprofile PMC
 counters, full profile) — interleaved so clock/thermal drift cancels out.  This parent
 never touches the GPU; every GPU user is a child process.
-Usage: python tools/interference.py [seconds_per_trial] [rounds] [gemm|copy]  -> prints RESULT json
+Usage: python tools/interference.py [seconds_per_trial] [rounds] [gemm|copy] [modes]  -> prints RESULT json
+  modes: comma list of none | 10hz | 100hz | <counters mode><hz> (cont10, duty10, cont100, ...),
+         default none,10hz,100hz (the default counters mode)
   gemm  MFMA-bound pod (TFLOP/s);  copy  HBM-bound pod: the calibration stream copy of
         1 GiB per launch (probe_device.h), read+write TB/s
 """
@@ -55,7 +57,7 @@ def burn(seconds: float, workload: str = "gemm") -> float:
     return float(json.loads(line[-1])["tflops"])
 
 
-def start_exporter(hz: float):
+def start_exporter(hz: float, counters_mode: str = ""):
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -63,6 +65,8 @@ def start_exporter(hz: float):
     cmd = [sys.executable, "-m", "kubernetes_gpu_exporter_amd", "--listen", f"127.0.0.1:{port}", "--interval",
            str(1.0 / hz), "--backend", "amdsmi", "--devices", "0", "--enable-sentinel", "true", "--enable-counters",
            "true", "--series-profile", "full", "--log-level", "warn"]
+    if counters_mode:
+        cmd += ["--counters-mode", counters_mode, "--counters-interval-ms", str(int(1000 / hz))]
     p = subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
     import http.client
     for _ in range(600):
@@ -82,11 +86,21 @@ def main() -> int:
     secs = float(sys.argv[1]) if len(sys.argv) > 1 else 8.0
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     workload = sys.argv[3] if len(sys.argv) > 3 else "gemm"
-    res = {"none": [], "10hz": [], "100hz": []}
+    modes = (sys.argv[4] if len(sys.argv) > 4 else "none,10hz,100hz").split(",")
+    res = {m: [] for m in modes}
     burn(2.0, workload)  # warm clocks / code objects
+
+    def exporter_for(mode):
+        if mode == "none":
+            return None
+        import re
+        m = re.fullmatch(r"(cont|duty)?(\d+)(?:hz)?", mode)
+        cmode = {"cont": "continuous", "duty": "duty", None: ""}[m.group(1)]
+        return start_exporter(float(m.group(2)), cmode)
+
     for r in range(rounds):
-        for mode in ("none", "10hz", "100hz"):
-            p = start_exporter(10.0 if mode == "10hz" else 100.0) if mode != "none" else None
+        for mode in modes:
+            p = exporter_for(mode)
             try:
                 time.sleep(1.0 if p else 0.0)
                 res[mode].append(burn(secs, workload))
@@ -97,7 +111,7 @@ def main() -> int:
             print(mode, round(res[mode][-1], 1), flush=True)
     med = {k: statistics.median(v) for k, v in res.items()}
     out = {"tflops": res, "median_tflops": {k: round(v, 1) for k, v in med.items()},
-           "slowdown_pct": {k: round(100.0 * (med["none"] - med[k]) / med["none"], 3) for k in ("10hz", "100hz")},
+           "slowdown_pct": {k: round(100.0 * (med["none"] - med[k]) / med["none"], 3) for k in modes if k != "none"},
            "seconds_per_trial": secs, "rounds": rounds, "workload": workload,
            "unit": "TB/s read+write" if workload == "copy" else "TFLOP/s"}
     print("RESULT " + json.dumps(out), flush=True)
