@@ -538,34 +538,39 @@ bool arm_continuous(Agent& a) {
   return true;
 }
 
-// What does a read packet do to running counters?  GRBM_COUNT is the free-running GRBM
-// clock, so over start, 5 ms, read, 5 ms, read it reads c1 then either ~2 c1 (still
-// counting), ~c1 (reset by the read) or exactly c1 (stopped by the read).
+// What does a read packet do to running counters?  start, 20 ms, read (B), then at once a
+// second read (C), on GRBM_COUNT (the GRBM clock count, which always advances while
+// counting):
+//   C == B exactly      -> the read stopped counting;
+//   C >  B              -> cumulative (C = B + the few microseconds between the reads);
+//   C <  B / 2          -> each read resets (C counts only those few microseconds).
+// Only the ORDER of B and C decides, never a ratio to elapsed time: GRBM_COUNT runs at the
+// current GFX clock, which DPM moves by 5x between idle and busy (a ratio test misread a
+// GPU clocking down after a workload as "resets").  Anything else: unknown.
 ReadMode read_semantics(Agent& a, std::string* why) {
   const auto ts = run_packet(a, a.start_pkt);
   double c[2] = {0, 0};
-  Clock::time_point t[2];
   for (int i = 0; i < 2; ++i) {
-    std::this_thread::sleep_for(std::chrono::milliseconds(5));
-    t[i] = run_packet(a, a.read_pkt);
+    if (i == 0) std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    const auto t = run_packet(a, a.read_pkt);
     Accum acc;
-    if (ts == Clock::time_point{} || t[i] == Clock::time_point{} || !collect(a, &acc)) {
+    if (ts == Clock::time_point{} || t == Clock::time_point{} || !collect(a, &acc)) {
       *why = "PM4 read packet did not complete";
       return kReadUnknown;
     }
     c[i] = acc.v[kGrbmCount];
   }
   run_packet(a, a.stop_pkt);
+  crumb("read semantics", "GRBM_COUNT B=" + std::to_string(c[0]) + " C=" + std::to_string(c[1]));
   if (c[0] <= 0) {
     *why = "GRBM_COUNT did not advance after the start packet";
     return kReadUnknown;
   }
-  crumb("read semantics", "GRBM_COUNT " + std::to_string(c[0]) + " -> " + std::to_string(c[1]));
   if (c[1] == c[0]) return kStops;
-  // expected ratio if cumulative: (t1 - ts) / (t0 - ts), ~2
-  const double expect = std::chrono::duration<double>(t[1] - ts).count() /
-                        std::max(1e-9, std::chrono::duration<double>(t[0] - ts).count());
-  return c[1] / c[0] > 0.5 * (1.0 + expect) ? kCumulative : kResets;
+  if (c[1] > c[0]) return kCumulative;
+  if (c[1] < 0.5 * c[0]) return kResets;
+  *why = "read packet semantics unclear (GRBM_COUNT " + std::to_string(c[0]) + " then " + std::to_string(c[1]) + ")";
+  return kReadUnknown;
 }
 
 void counting_loop() {
@@ -893,6 +898,7 @@ extern "C" __attribute__((visibility("default"))) uint64_t gpuexp_rp_cpu_ns() { 
 
 // Waits up to `timeout_us` for the round of the last kick; 0 = done, 1 = timed out.
 extern "C" __attribute__((visibility("default"))) int gpuexp_rp_sync(int timeout_us) {
+  if (!g_continuous) return 0;  // duty windows (incl. the fallback): nothing per tick to wait for
   std::unique_lock<std::mutex> lk(g_cv_mu);
   const uint64_t want = g_kick_seq;
   return g_done_cv.wait_for(lk, std::chrono::microseconds(std::max(0, timeout_us)),
@@ -976,12 +982,15 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_init(int ndev, c
       break;
     }
     if (g_read_mode == kReadUnknown) {
-      teardown_locked();
-      return fail("continuous counting: " + why);
+      // counting still works window by window: fall back to the duty cycle (status says so)
+      std::fprintf(stderr, "[aqlpmc] continuous counting unavailable (%s): duty-cycled windows instead\n",
+                   why.c_str());
+      g_continuous = false;
+      g_window_ms = std::max(1, std::min(20, g_interval_ms / 2));
     }
-    ok = 0;
+    if (g_continuous) ok = 0;
     for (Agent* a : g_agents) {
-      if (!usable(a)) continue;
+      if (!g_continuous || !usable(a)) continue;
       if (arm_continuous(*a)) ++ok;
       else a->broken = true;
     }
