@@ -538,7 +538,7 @@ PYBIND11_MODULE(_gpuexp, m) {
         return d;
       })
       .def("source_status", &Engine::source_status)
-      .def("set_pods", [](Engine& e, py::list pods) {
+      .def("set_pods", [](Engine& e, py::list pods, bool complete) {
         std::vector<PodMeta> v;
         for (auto item : pods) {
           py::dict d = item.cast<py::dict>();
@@ -551,8 +551,10 @@ PYBIND11_MODULE(_gpuexp, m) {
               p.containers.emplace_back(kv.first.cast<std::string>(), kv.second.cast<std::string>());
           v.push_back(std::move(p));
         }
-        e.set_pods(std::move(v));
-      })
+        e.set_pods(std::move(v), complete);
+      }, py::arg("pods"), py::arg("complete") = true,
+         "complete=False: a source failed this refresh; the list is applied for names but never used to "
+         "drop per-pod totals")
       .def("set_device_owners", [](Engine& e, py::dict owners) {
         std::vector<std::pair<std::string, DeviceOwner>> v;
         for (auto kv : owners) {

@@ -1,5 +1,6 @@
 #include "gpuexp/engine.h"
 
+#include <fcntl.h>
 #include <sys/eventfd.h>
 #include <sys/poll.h>
 #include <sys/timerfd.h>
@@ -254,6 +255,12 @@ void Engine::define_families() {
   f_pod_gpus_ = add("amd_pod_gpus", "GPUs attributed to a pod", G, PO);
   f_pod_xrd_ = add("amd_pod_xgmi_read_bytes_per_second", "xGMI receive rate of the pod's GPUs", G, PO);
   f_pod_xwr_ = add("amd_pod_xgmi_write_bytes_per_second", "xGMI transmit rate of the pod's GPUs", G, PO);
+  f_pod_xrd_total_ = add("amd_pod_xgmi_read_bytes_total",
+                         "xGMI bytes received by the pod's GPUs (per-tick link accumulator deltas; on a shared GPU "
+                         "the pod's CU-occupancy share)", C, PO);
+  f_pod_xwr_total_ = add("amd_pod_xgmi_write_bytes_total",
+                         "xGMI bytes sent by the pod's GPUs (per-tick link accumulator deltas; on a shared GPU the "
+                         "pod's CU-occupancy share)", C, PO);
   f_pod_power_ = add("amd_pod_gpu_power_watts", "Socket power of the pod's GPUs", G, PO);
   f_pod_energy_ = add("amd_pod_gpu_energy_joules_total",
                       "GPU energy used by the pod: its GPUs' hardware energy counters, and on a shared GPU the "
@@ -614,11 +621,11 @@ void Engine::tick_now(uint64_t now_ns) {
   tick_locked(now_ns);
 }
 
-void Engine::set_pods(std::vector<PodMeta> pods) {
+void Engine::set_pods(std::vector<PodMeta> pods, bool complete) {
   std::lock_guard<std::mutex> lk(ctl_mu_);
   pending_pods_ = std::move(pods);
   ctl_dirty_ = true;
-  pods_pushed_ = true;
+  pending_complete_ = complete;
 }
 
 void Engine::set_device_owners(std::vector<std::pair<std::string, DeviceOwner>> owners) {
@@ -664,7 +671,7 @@ void Engine::emit_kfd_events(uint64_t gen) {
   for (auto it = pod_kfd_events_.begin(); it != pod_kfd_events_.end();) {
     const auto& k = it->first;
     // restored from the state file while the pod list is not here yet: keep (and export)
-    if (pods_known_ && !live.count({std::get<0>(k), std::get<1>(k)})) {
+    if (pods_complete_ && !live.count({std::get<0>(k), std::get<1>(k)})) {
       it = pod_kfd_events_.erase(it);
       continue;
     }
@@ -682,16 +689,17 @@ std::string Engine::device_key(size_t i) const {
 //   gpuexp-state 1
 //   pod_energy <ns> <pod> <joules>
 //   pod_event  <ns> <pod> <event id> <count>
+//   pod_xgmi   <ns> <pod> <read bytes> <write bytes>
 //   dev_event  <bdf>/<partition> <event id> <count>
 void Engine::load_state() {
   std::string body;
   if (!read_small_file(cfg_.state_file, &body, 16u << 20)) {
-    state_status_ = "no state yet (" + cfg_.state_file + ")";
+    set_state_status("no state yet (" + cfg_.state_file + ")");
     return;
   }
   if (body.compare(0, 14, "gpuexp-state 1") != 0) {
-    state_status_ = "ignored: unknown format in " + cfg_.state_file;
-    GPUEXP_LOG(LogLevel::kWarn, "state", state_status_);
+    set_state_status("ignored: unknown format in " + cfg_.state_file);
+    GPUEXP_LOG(LogLevel::kWarn, "state", "ignored: unknown format in " + cfg_.state_file);
     return;
   }
   std::unordered_map<std::string, size_t> dev_by_key;
@@ -710,6 +718,9 @@ void Engine::load_state() {
     if (f[0] == "pod_energy" && f.size() == 4) {
       pod_energy_j_[{f[1], f[2]}] = std::strtod(f[3].c_str(), nullptr);
       ++n;
+    } else if (f[0] == "pod_xgmi" && f.size() == 5) {
+      pod_xgmi_[{f[1], f[2]}] = {std::strtod(f[3].c_str(), nullptr), std::strtod(f[4].c_str(), nullptr)};
+      ++n;
     } else if (f[0] == "pod_event" && f.size() == 5) {
       const int ev = std::atoi(f[3].c_str());
       if (ev > 0 && ev < kKfdEventIds) pod_kfd_events_[std::make_tuple(f[1], f[2], ev)] = std::strtoull(f[4].c_str(), nullptr, 10);
@@ -722,8 +733,8 @@ void Engine::load_state() {
       ++n;
     }
   }
-  state_status_ = "restored " + std::to_string(n) + " records from " + cfg_.state_file;
-  GPUEXP_LOG(LogLevel::kInfo, "state", state_status_);
+  set_state_status("restored " + std::to_string(n) + " records from " + cfg_.state_file);
+  GPUEXP_LOG(LogLevel::kInfo, "state", "restored " + std::to_string(n) + " records from " + cfg_.state_file);
 }
 
 bool Engine::save_state() {
@@ -734,6 +745,12 @@ bool Engine::save_state() {
     std::snprintf(num, sizeof(num), "%.17g", kv.second);
     out += "pod_energy\t" + kv.first.first + "\t" + kv.first.second + "\t" + num + "\n";
   }
+  for (auto& kv : pod_xgmi_) {
+    char rd[64], wr[64];
+    std::snprintf(rd, sizeof(rd), "%.17g", kv.second.first);
+    std::snprintf(wr, sizeof(wr), "%.17g", kv.second.second);
+    out += "pod_xgmi\t" + kv.first.first + "\t" + kv.first.second + "\t" + rd + "\t" + wr + "\n";
+  }
   for (auto& kv : pod_kfd_events_)
     out += "pod_event\t" + std::get<0>(kv.first) + "\t" + std::get<1>(kv.first) + "\t" +
            std::to_string(std::get<2>(kv.first)) + "\t" + std::to_string(kv.second) + "\n";
@@ -742,14 +759,26 @@ bool Engine::save_state() {
       if (dstate_[i].kfd_events[ev])
         out += "dev_event\t" + device_key(i) + "\t" + std::to_string(ev) + "\t" +
                std::to_string(dstate_[i].kfd_events[ev]) + "\n";
+  // write + fsync + rename + fsync(dir): after a node crash the file is the old state or
+  // the new one, never a renamed-but-empty one (the point of a hostPath checkpoint)
   const std::string tmp = cfg_.state_file + ".tmp";
   FILE* f = std::fopen(tmp.c_str(), "w");
   bool ok = f && std::fwrite(out.data(), 1, out.size(), f) == out.size();
+  if (f) ok = std::fflush(f) == 0 && ::fsync(::fileno(f)) == 0 && ok;
   if (f) ok = (std::fclose(f) == 0) && ok;
   ok = ok && std::rename(tmp.c_str(), cfg_.state_file.c_str()) == 0;
+  if (ok) {
+    const size_t sl = cfg_.state_file.rfind('/');
+    const std::string dir = sl == std::string::npos ? "." : (sl == 0 ? "/" : cfg_.state_file.substr(0, sl));
+    const int dfd = ::open(dir.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+    if (dfd >= 0) {
+      ::fsync(dfd);
+      ::close(dfd);
+    }
+  }
   if (!ok) {
-    state_status_ = "save failed: " + cfg_.state_file;
-    GPUEXP_LOG(LogLevel::kWarn, "state", state_status_);
+    set_state_status("save failed: " + cfg_.state_file);
+    GPUEXP_LOG(LogLevel::kWarn, "state", "save failed: " + cfg_.state_file);
   }
   return ok;
 }
@@ -1056,6 +1085,7 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
     int gpus = 0;
     double xrd = 0, xwr = 0, power = 0, gfx = 0, gfx_share = 0;
     double energy_j = 0;  // this tick
+    double xrd_b = 0, xwr_b = 0;  // xGMI bytes this tick (owned GPUs whole, shared GPUs by share)
     int gfx_n = 0;
     bool share_known = false;
   };
@@ -1092,6 +1122,23 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
       double dacc;
       if (acc_delta(st.cur.energy_acc, st.prev.energy_acc, &dacc)) energy_j = dacc * st.cur.energy_unit_j;
     }
+    // xGMI bytes this GPU moved since the last tick, summed over links (hardware accumulators)
+    double xgmi_rd_b = std::nan(""), xgmi_wr_b = std::nan("");
+    if (st.cur.ok && st.have_prev && st.cur.xgmi_valid && st.prev.xgmi_valid) {
+      double r = 0, w = 0;
+      bool ok = true;
+      for (int l = 0; l < kMaxXgmiLinks && ok; ++l) {
+        double dr, dw;
+        ok = acc_delta(st.cur.xgmi_read_kb[l], st.prev.xgmi_read_kb[l], &dr) &&
+             acc_delta(st.cur.xgmi_write_kb[l], st.prev.xgmi_write_kb[l], &dw);
+        r += ok ? dr : 0;
+        w += ok ? dw : 0;
+      }
+      if (ok) {  // a reset link skips the tick (as the rates do)
+        xgmi_rd_b = r * 1024.0;
+        xgmi_wr_b = w * 1024.0;
+      }
+    }
     const bool shared = st.owner.pod.empty();
     for (auto& p : per_dev[di]) {
       const ProcAttr& a = attr[p.pid];
@@ -1126,6 +1173,10 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
         pa.pids.insert(p.pid);
         const double f = frac(p);
         if (shared && !std::isnan(energy_j) && !std::isnan(f)) pa.energy_j += energy_j * f;
+        if (shared && !std::isnan(xgmi_rd_b) && !std::isnan(f)) {
+          pa.xrd_b += xgmi_rd_b * f;
+          pa.xwr_b += xgmi_wr_b * f;
+        }
         if (!std::isnan(share)) {
           pa.gfx_share += share;
           pa.share_known = true;
@@ -1148,6 +1199,10 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
           }
         if (!std::isnan(st.cur.power_w)) pa.power += st.cur.power_w;
         if (!std::isnan(energy_j)) pa.energy_j += energy_j;  // an owned GPU's energy is all the pod's
+        if (!std::isnan(xgmi_rd_b)) {  // ...and so is its xGMI traffic
+          pa.xrd_b += xgmi_rd_b;
+          pa.xwr_b += xgmi_wr_b;
+        }
         if (!std::isnan(st.cur.gfx_activity)) {
           pa.gfx += st.cur.gfx_activity;
           pa.gfx_n += 1;
@@ -1193,19 +1248,35 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
   }
   for (auto it = pod_refs_.begin(); it != pod_refs_.end();)
     it = it->second.gen != gen ? pod_refs_.erase(it) : std::next(it);
-  // Energy per pod: a counter that lives as long as the control plane knows the pod, so a
-  // pod between GPU processes keeps its total.
-  for (auto& kv : pods)
+  // Energy and xGMI bytes per pod: counters that live as long as the control plane knows
+  // the pod, so a pod between GPU processes keeps its totals (and an exporter restart too,
+  // through the state file).
+  for (auto& kv : pods) {
     if (kv.second.energy_j > 0) pod_energy_j_[kv.first] += kv.second.energy_j;
+    if (kv.second.xrd_b > 0 || kv.second.xwr_b > 0) {
+      auto& x = pod_xgmi_[kv.first];
+      x.first += kv.second.xrd_b;
+      x.second += kv.second.xwr_b;
+    }
+  }
   {
     std::set<std::pair<std::string, std::string>> known;
     for (auto& kv : pods_by_uid_) known.emplace(kv.second.ns, kv.second.name);
     for (auto it = pod_energy_j_.begin(); it != pod_energy_j_.end();) {
-      if (pods_known_ && !known.count(it->first)) {
+      if (pods_complete_ && !known.count(it->first)) {
         it = pod_energy_j_.erase(it);
         continue;
       }
       table_.put(f_pod_energy_, {it->first.first, it->first.second}, it->second, gen);
+      ++it;
+    }
+    for (auto it = pod_xgmi_.begin(); it != pod_xgmi_.end();) {
+      if (pods_complete_ && !known.count(it->first)) {
+        it = pod_xgmi_.erase(it);
+        continue;
+      }
+      table_.put(f_pod_xrd_total_, {it->first.first, it->first.second}, it->second.first, gen);
+      table_.put(f_pod_xwr_total_, {it->first.first, it->first.second}, it->second.second, gen);
       ++it;
     }
   }
@@ -1353,7 +1424,10 @@ void Engine::tick_locked(uint64_t now) {
       owners_.clear();
       for (auto& o : pending_owners_) owners_[lower(o.first)] = o.second;
       ctl_dirty_ = false;
-      pods_known_ = pods_known_ || pods_pushed_;
+      // per-pod totals (energy, xGMI bytes, KFD events; possibly restored from the state
+      // file) are garbage-collected against a pod list only if that list is complete: a
+      // refresh in which a source failed must not wipe them
+      pods_complete_ = pending_complete_;
     }
   }
 
@@ -1572,7 +1646,7 @@ EngineStats Engine::stats() {
 std::string Engine::source_status() {
   std::string s = std::string("backend=") + (backend_ ? backend_->name() : "none") + " sentinel=" + sentinel_status_ +
                   " counters=" + counters_status_ + " rccl=" + (rccl_ ? cfg_.rccl_dir : "disabled") +
-                  " kfd_events=" + kfd_events_status_ + " state=" + state_status_;
+                  " kfd_events=" + kfd_events_status_ + " state=" + state_status();
   if (backend_)
     for (const auto& d : devices_) s += " gpu" + std::to_string(d.index) + "=[" + backend_->describe(d) + "]";
   return s;

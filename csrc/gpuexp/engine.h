@@ -167,7 +167,8 @@ class Engine {
   std::string source_status();
 
   // Control-plane inputs (any thread; applied at the next tick).
-  void set_pods(std::vector<PodMeta> pods);
+  // complete: every metadata source answered (a partial list never GCs per-pod totals).
+  void set_pods(std::vector<PodMeta> pods, bool complete = true);
   void set_device_owners(std::vector<std::pair<std::string, DeviceOwner>> owners);
   void set_pid_cgroup(int pid, const std::string& cgroup_path);
   void clear_pid_cgroups();
@@ -258,10 +259,21 @@ class Engine {
   // per-process KFD events attributed to pods: (namespace, pod, event id) -> count
   std::map<std::tuple<std::string, std::string, int>, uint64_t> pod_kfd_events_;
   uint64_t kfd_events_unattributed_ = 0;  // per-process events whose PID resolved to no pod
-  bool pods_pushed_ = false;   // ctl_mu_: the control plane has delivered a pod list
-  bool pods_known_ = false;    // sampler: ...applied; per-pod totals are GC'd only from then on
+  bool pending_complete_ = false;  // ctl_mu_: the pending pod list came from a complete refresh
+  bool pods_complete_ = false;     // sampler: the applied pod list is complete (per-pod GC allowed)
   uint64_t state_saved_ns_ = 0;
+  // read by source_status() from any thread while save_state() may rewrite it on the
+  // sampler thread: only through these, under status_mu_
   std::string state_status_ = "disabled";
+  mutable std::mutex status_mu_;
+  void set_state_status(std::string s) {
+    std::lock_guard<std::mutex> lk(status_mu_);
+    state_status_ = std::move(s);
+  }
+  std::string state_status() const {
+    std::lock_guard<std::mutex> lk(status_mu_);
+    return state_status_;
+  }
   std::unique_ptr<ForkJoinPool> pool_;
   // full profile, real backends: RAS/AER readers + last totals (re-read every ras_interval_s)
   std::vector<RasReader> ras_;
@@ -305,6 +317,8 @@ class Engine {
   std::unordered_map<uint64_t, ProcRefs> legacy_refs_;             // pid -> legacy handles (pod, vram, gfx=perc)
   std::map<std::pair<std::string, std::string>, PodRefs> pod_refs_;  // (ns, pod) -> handles
   std::map<std::pair<std::string, std::string>, double> pod_energy_j_;  // (ns, pod) -> joules so far
+  // (ns, pod) -> xGMI bytes (read, write) so far
+  std::map<std::pair<std::string, std::string>, std::pair<double, double>> pod_xgmi_;
   SeriesRef self_refs_[21];
 
   // stats (guarded by stats_mu_)
@@ -325,7 +339,7 @@ class Engine {
   int f_proc_vram_, f_proc_cu_, f_proc_sdma_, f_proc_evicted_, f_proc_gfx_;
   int f_legacy_mem_ = -1, f_legacy_perc_ = -1;
   int f_pod_vram_, f_pod_procs_, f_pod_gpus_, f_pod_xrd_, f_pod_xwr_, f_pod_power_, f_pod_gfx_, f_pod_gfx_share_,
-      f_pod_energy_ = -1;
+      f_pod_energy_ = -1, f_pod_xrd_total_ = -1, f_pod_xwr_total_ = -1;
   int f_rccl_calls_, f_rccl_bytes_, f_rccl_comm_;
   int f_kfd_ev_ = -1, f_pod_kfd_ev_ = -1, f_pages_ = -1, f_gtt_used_ = -1, f_gtt_total_ = -1;
   int f_board_ = -1, f_fw_ = -1, f_driver_ = -1;

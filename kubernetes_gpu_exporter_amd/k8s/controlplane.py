@@ -50,6 +50,13 @@ class Source:
     def fetch(self) -> Metadata:  # pragma: no cover - interface
         raise NotImplementedError
 
+    @property
+    def has_synced(self) -> bool:
+        """False while the source has never produced a complete answer (e.g. the apiserver
+        list has not succeeded yet): its (empty) pods are then not a statement that pods
+        are gone."""
+        return True
+
     def close(self) -> None:
         """Releases background resources (watch threads, channels)."""
 
@@ -66,6 +73,7 @@ class ControlPlane:
         self._pushed_pids: set = set()
         self.errors: dict = {}
         self.refreshes = 0
+        self.last_complete = False
 
     @classmethod
     def from_config(cls, cfg) -> "ControlPlane":
@@ -93,9 +101,11 @@ class ControlPlane:
 
     def refresh_once(self) -> Metadata:
         md = Metadata()
+        complete = True  # every source answered: only then may the engine drop per-pod totals
         for s in self.sources:
             try:
                 md.merge(s.fetch())
+                complete = complete and bool(getattr(s, "has_synced", True))
                 # a source may keep serving its cache while its background loop fails
                 err = getattr(s, "last_error", None)
                 if err:
@@ -103,11 +113,13 @@ class ControlPlane:
                 else:
                     self.errors.pop(s.name, None)
             except Exception as e:  # one failing source never blocks the others
+                complete = False
                 self.errors[s.name] = repr(e)
                 log.warning("source %s failed: %r", s.name, e)
-        fp = md.fingerprint()
+        self.last_complete = complete
+        fp = md.fingerprint() + ("" if complete else "#partial")
         if self.engine is not None and fp != self._last_fp:
-            self.engine.set_pods(list(md.pods.values()))
+            self.engine.set_pods(list(md.pods.values()), complete)
             self.engine.set_device_owners(md.owners)
             pids = {int(p) for p in md.pid_cgroups}
             if self._pushed_pids - pids:

@@ -201,6 +201,10 @@ class ApiserverSource(Source):
                 self._synced = False
 
     # --- Source ---
+    @property
+    def has_synced(self) -> bool:
+        return self.relists > 0  # the node's pod list has been read in full at least once
+
     def fetch(self) -> Metadata:
         if not self.watch:
             self._list()

@@ -413,3 +413,72 @@ def test_state_file_with_unknown_format_is_ignored(native, mock_engine, tmp_path
     assert "ignored" in e.source_status()
     e.tick(1_000_000_000)
     assert not promtext.samples(promtext.parse(e.snapshot_text()), "amd_pod_gpu_energy_joules_total")
+
+
+def test_pod_xgmi_byte_counters(native, mock_engine, tmp_path):
+    """amd_pod_xgmi_{read,write}_bytes_total: per-tick xGMI link-accumulator deltas of the
+    pod's GPUs (an owned GPU's whole, a shared GPU's by CU-occupancy share), kept while the
+    control plane knows the pod, moved with an ownership change, not dropped by an
+    incomplete refresh, and carried across an exporter restart by the state file."""
+    state = str(tmp_path / "state")
+    uids = {p: f"00000000-0000-4000-8000-00000000001{i}" for i, p in enumerate("abc", 1)}
+    cids = {p: p * 64 for p in "abc"}
+    K = 7 * 1024  # 7 links per mock GPU, kB -> B
+    pods = [{"uid": uids[p], "namespace": "ns", "name": f"pod-{p}", "containers": {cids[p]: "w"}} for p in "abc"]
+
+    def engine():
+        e = mock_engine(2, series_profile="standard", state_file=state)
+        for pid, p in ((100, "a"), (200, "b"), (300, "c")):
+            e.set_pid_cgroup(pid, kubepods_cgroup(uids[p], cids[p]))
+        e.mock_set_value(0, "xgmi_read_rate_kbps", 1000)
+        e.mock_set_value(0, "xgmi_write_rate_kbps", 2000)
+        e.mock_set_value(1, "xgmi_read_rate_kbps", 4000)
+        e.mock_set_value(1, "xgmi_write_rate_kbps", 0)
+        e.mock_set_processes(0, [{"pid": 100, "vram_bytes": 1 << 30, "cu_occupancy": 200, "name": "a"}])
+        e.mock_set_processes(1, [{"pid": 200, "vram_bytes": 1 << 30, "cu_occupancy": 48, "name": "b"},
+                                 {"pid": 300, "vram_bytes": 1 << 30, "cu_occupancy": 16, "name": "c"}])
+        return e
+
+    def totals(e):
+        f = promtext.parse(e.snapshot_text())
+        rd = {s[1]["pod"]: s[2] for s in promtext.samples(f, "amd_pod_xgmi_read_bytes_total")}
+        wr = {s[1]["pod"]: s[2] for s in promtext.samples(f, "amd_pod_xgmi_write_bytes_total")}
+        return rd, wr
+
+    e = engine()
+    e.set_pods(pods)
+    e.set_device_owners({"0000:10:00.0": {"namespace": "ns", "pod": "pod-a", "container": "w"}})
+    for t in range(1, 5):  # 3 one-second intervals
+        e.tick(t * S)
+    rd, wr = totals(e)
+    assert rd["pod-a"] == pytest.approx(3 * 1000 * K, rel=1e-3) and wr["pod-a"] == pytest.approx(3 * 2000 * K, rel=1e-3)
+    assert rd["pod-b"] == pytest.approx(3 * 4000 * K * 0.75, rel=1e-3)
+    assert rd["pod-c"] == pytest.approx(3 * 4000 * K * 0.25, rel=1e-3) and wr["pod-c"] == 0
+    # GPU 0 changes hands: its bytes from now on are pod-b's; pod-a keeps what it had
+    e.set_device_owners({"0000:10:00.0": {"namespace": "ns", "pod": "pod-b", "container": "w"}})
+    e.tick(5 * S)
+    rd2, wr2 = totals(e)
+    assert rd2["pod-a"] == pytest.approx(rd["pod-a"])
+    assert rd2["pod-b"] == pytest.approx(rd["pod-b"] + 1000 * K + 4000 * K * 0.75, rel=1e-3)
+    # a refresh in which a source failed (pod-c missing from it) drops nothing...
+    e.set_pods(pods[:2], False)
+    e.tick(6 * S)
+    assert "pod-c" in totals(e)[0]
+    # ...a complete one without pod-c does
+    e.set_pods(pods[:2])
+    e.tick(7 * S)
+    rd3, _ = totals(e)
+    assert "pod-c" not in rd3
+    e.stop()  # final save
+    assert "pod_xgmi\tns\tpod-a\t" in open(state).read()
+
+    b = engine()
+    b.tick(10 * S)  # no pod list yet: restored totals exported as they were
+    assert totals(b)[0]["pod-a"] == pytest.approx(rd3["pod-a"])
+    b.set_pods(pods[1:2], False)  # an incomplete first refresh without pod-a (apiserver down)...
+    b.tick(11 * S)
+    assert totals(b)[0]["pod-a"] == pytest.approx(rd3["pod-a"])  # ...keeps pod-a's restored total
+    b.set_pods(pods[1:2])  # a complete one without it drops it
+    b.tick(12 * S)
+    assert "pod-a" not in totals(b)[0]
+    b.stop()

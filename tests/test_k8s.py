@@ -139,6 +139,35 @@ def test_control_plane_isolates_failures_and_pushes_on_change(mock_engine):
     assert cp._last_fp == fp
 
 
+def test_failed_refresh_never_drops_restored_pod_totals(mock_engine, tmp_path):
+    """the first refresh runs while the apiserver is down.  Its (partial) pod
+    list must not garbage-collect the per-pod totals restored from --state-file; the first
+    complete refresh does, for pods that are really gone."""
+    state = tmp_path / "state"
+    state.write_text("gpuexp-state 1\npod_energy\tns\tgone\t123\npod_energy\tns\tp\t7\n"
+                     "pod_xgmi\tns\tgone\t1000\t2000\n")
+    e = mock_engine(1, http=False, series_profile="full", state_file=str(state))
+    md = Metadata(pods={UID_A: {"uid": UID_A, "namespace": "ns", "name": "p", "containers": {}}})
+    cp = ControlPlane([_Static(md), _Boom()], interval=0.05)
+    cp.attach(e)
+    cp.refresh_once()
+    assert cp.last_complete is False
+
+    def energy():
+        f = promtext.parse(e.snapshot_text())
+        return {s[1]["pod"]: s[2] for s in promtext.samples(f, "amd_pod_gpu_energy_joules_total")}
+    e.tick(1_000_000_000)
+    e.tick(2_000_000_000)
+    assert energy() == {"gone": 123, "p": 7}
+    assert promtext.value(promtext.parse(e.snapshot_text()), "amd_pod_xgmi_write_bytes_total", pod="gone") == 2000
+    cp.sources = [_Static(md)]  # the apiserver is back: a complete refresh
+    cp.refresh_once()
+    assert cp.last_complete is True
+    e.tick(3_000_000_000)
+    assert energy() == {"p": 7}
+    assert "amd_pod_xgmi_write_bytes_total" not in e.snapshot_text()
+
+
 def test_full_exporter_on_fake_node(tmp_path):
     """sysfs backend + fake kubelet + fake apiserver, through the Exporter/Config path."""
     import shutil
