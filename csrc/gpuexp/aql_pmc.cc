@@ -160,6 +160,8 @@ bool g_continuous = false;
 uint64_t g_kick_seq = 0, g_done_seq = 0;
 std::condition_variable g_done_cv;
 std::atomic<uint64_t> g_thread_cpu_ns{0};  // the counting thread's own CPU, published per round
+// where a continuous read round's CPU goes (counting thread clock): post / wait / collect
+std::atomic<uint64_t> g_round_cpu[3] = {}, g_rounds{0};
 
 uint64_t own_cpu_ns() {
   timespec ts;
@@ -466,6 +468,7 @@ void window_all() {
 // right after the read, a gap of one PM4 packet).
 void read_round() {
   const auto begin = Clock::now();
+  uint64_t c0 = own_cpu_ns(), cw = 0, cc = 0;
   // a stalled GPU costs the round at most this long (the other GPUs' reads are in flight)
   const auto deadline = begin + std::chrono::milliseconds(std::min(1000, g_interval_ms));
   for (Agent* a : g_agents)
@@ -474,13 +477,17 @@ void read_round() {
       a->read_inflight = true;
       a->t_checked = a->t_submit;
     }
+  const uint64_t c1 = own_cpu_ns();
   for (Agent* a : g_agents) {
     if (!usable(a) || !a->read_inflight) continue;
+    const uint64_t w0 = own_cpu_ns();
     const double left = std::chrono::duration<double>(deadline - Clock::now()).count();
     const uint64_t ticks = left > 0 ? uint64_t(left * double(g_ts_freq)) : 0;
     const hsa_signal_value_t v = hsa_signal_wait_scacquire(a->sig, HSA_SIGNAL_CONDITION_LT, 1, ticks,
                                                            HSA_WAIT_STATE_BLOCKED);
     const auto now = Clock::now();
+    const uint64_t w1 = own_cpu_ns();
+    cw += w1 - w0;
     if (a->queue_error.load()) {
       a->broken = true;
       continue;
@@ -494,7 +501,10 @@ void read_round() {
     // the read executed between the last time it was seen pending and now
     const auto t = a->t_checked + (now - a->t_checked) / 2;
     Accum acc;
-    if (!collect(*a, &acc)) continue;
+    const uint64_t k0 = own_cpu_ns();
+    const bool got = collect(*a, &acc);
+    cc += own_cpu_ns() - k0;
+    if (!got) continue;
     const double wall = std::chrono::duration<double>(t - a->t_last).count();
     if (g_read_mode == kCumulative) {
       double d[kNumCtr];
@@ -519,6 +529,10 @@ void read_round() {
       }
     }
   }
+  g_round_cpu[0] += c1 - c0;
+  g_round_cpu[1] += cw;
+  g_round_cpu[2] += cc;
+  ++g_rounds;
 }
 
 // Starts counting on `a` for good: start packet, then (cumulative) the baseline read.
@@ -1059,6 +1073,12 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_debug(int dev, c
                   ";simd=" + std::to_string(a.m.simd) + ";cu=" + std::to_string(a.m.cu) +
                   ";mode=" + (g_continuous ? read_mode_name(g_read_mode) : "duty") + ";window_s=" + win +
                   ";resets=" + std::to_string(a.resets.load()) + ";stalls=" + std::to_string(a.stalls.load()) + ";";
+  if (const uint64_t r = g_rounds.load()) {
+    char c[160];
+    std::snprintf(c, sizeof(c), "rounds=%llu;round_cpu_us_post=%.2f;round_cpu_us_wait=%.2f;round_cpu_us_collect=%.2f;",
+                  (unsigned long long)r, g_round_cpu[0] / 1e3 / r, g_round_cpu[1] / 1e3 / r, g_round_cpu[2] / 1e3 / r);
+    s += c;
+  }
   if (g_continuous && g_read_mode == kCumulative) {
     char c[160];
     std::snprintf(c, sizeof(c), "cum_MFMA=%.0f;cum_GRBM_COUNT=%.0f;cum_GUI=%.0f;", a.pub_cum[kMfma],

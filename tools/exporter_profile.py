@@ -4,6 +4,7 @@ gpu_metrics path, aqlprofile PMC counters in continuous mode, sentinel dispatche
 on the counters' queue, full profile) at `hz` for `seconds`, then stops it and exits
 normally, so a profiler wrapping this process can flush:
   rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o exporter -- python3 tools/exporter_profile.py 10 5
+(a third argument `nocounters` runs the same without the PMC plugin: the HIP sentinel then)
 Torch-free: the sentinel's and the PMC programs' queue is the only GPU queue the exporter
 creates.  Prints the engine's source status and how many sentinel runs completed, so the
 profile's dispatch count can be checked against it.
@@ -28,7 +29,7 @@ def main() -> int:
     c.serve_http = False
     c.series_profile = "full"
     c.enable_sentinel = True
-    c.enable_counters = True
+    c.enable_counters = "nocounters" not in sys.argv[3:]
     c.counters_plugin = rocprof_plugin_path("aqlpmc")
     c.device_filter = [0]
     e = n.Engine(c)
@@ -37,8 +38,16 @@ def main() -> int:
     time.sleep(secs)
     fams = promtext.parse(e.snapshot_text())
     st = e.stats()
+    import ctypes
+    dbg = ctypes.create_string_buffer(4096)
+    if c.enable_counters:
+        ctypes.CDLL(rocprof_plugin_path("aqlpmc")).gpuexp_rp_debug(0, dbg, 4096)
+    print("plugin:", ";".join(x for x in dbg.value.decode().split(";") if x.startswith(("round", "rounds", "mode",
+                                                                                         "stalls", "window"))))
+    cpu = [v for _, _, v in promtext.samples(fams, "gpuexp_sampler_cpu_seconds_total")]
+    print(f"sampler CPU per tick {cpu[0] / st['ticks'] * 1e6:.0f} us" if cpu and st["ticks"] else "", flush=True)
     e.stop()
-    runs = promtext.value(fams, "amd_gpu_sentinel_runs_total", gpu=0)
+    runs = sum(v for _, _, v in promtext.samples(fams, "amd_gpu_sentinel_runs_total"))
     late = [v for _, _, v in promtext.samples(fams, "gpuexp_counters_late_ticks_total")]
     print(f"ticks {st['ticks']}, sentinel runs completed {runs:.0f}, counter reads late {late}, "
           f"counters stage mean {st['stage_ns']['counters'] / 1e3:.1f} us (last tick)", flush=True)
