@@ -267,11 +267,26 @@ void post_packet(Agent& a, const hsa_ext_amd_aql_pm4_packet_t& pkt, bool barrier
   submit(a, pkt, barrier);
 }
 
+// Waits for a completion signal by sleeping and looking, never by spinning: ROCr's own
+// wait (hsa_signal_wait_*, even HSA_WAIT_STATE_BLOCKED) busy-polls ~200 us before it
+// sleeps, and a PM4 read program takes about that long, so every read cost ~211 us of
+// CPU per GPU (measured: tools/exporter_profile.py round_cpu_us_wait).  Sleeping 60 us,
+// then 100 us slices, costs a few us per read and adds < 100 us of latency, which the
+// tick absorbs (the read is kicked at the tick's start and needed only at its series stage).
+bool wait_signal(hsa_signal_t sig, Clock::time_point deadline) {
+  for (int i = 0;; ++i) {
+    if (hsa_signal_load_scacquire(sig) < 1) return true;
+    const auto now = Clock::now();
+    if (now >= deadline) return false;
+    const auto step = std::chrono::microseconds(i == 0 ? 60 : 100);
+    std::this_thread::sleep_for(std::min<Clock::duration>(step, deadline - now));
+  }
+}
+
 Clock::time_point wait_packet(Agent& a) {
-  const hsa_signal_value_t v =
-      hsa_signal_wait_scacquire(a.sig, HSA_SIGNAL_CONDITION_LT, 1, g_ts_freq, HSA_WAIT_STATE_BLOCKED);
+  const bool done = wait_signal(a.sig, Clock::now() + std::chrono::seconds(1));
   const auto t1 = Clock::now();
-  if (v >= 1 || a.queue_error.load()) return {};
+  if (!done || a.queue_error.load()) return {};
   return a.t_submit + (t1 - a.t_submit) / 2;
 }
 
@@ -481,10 +496,7 @@ void read_round() {
   for (Agent* a : g_agents) {
     if (!usable(a) || !a->read_inflight) continue;
     const uint64_t w0 = own_cpu_ns();
-    const double left = std::chrono::duration<double>(deadline - Clock::now()).count();
-    const uint64_t ticks = left > 0 ? uint64_t(left * double(g_ts_freq)) : 0;
-    const hsa_signal_value_t v = hsa_signal_wait_scacquire(a->sig, HSA_SIGNAL_CONDITION_LT, 1, ticks,
-                                                           HSA_WAIT_STATE_BLOCKED);
+    const bool done = wait_signal(a->sig, deadline);
     const auto now = Clock::now();
     const uint64_t w1 = own_cpu_ns();
     cw += w1 - w0;
@@ -492,7 +504,7 @@ void read_round() {
       a->broken = true;
       continue;
     }
-    if (v >= 1) {  // still queued: try again next round, the counters keep running
+    if (!done) {  // still queued: try again next round, the counters keep running
       a->t_checked = now;
       ++a->stalls;
       continue;
@@ -589,6 +601,7 @@ ReadMode read_semantics(Agent& a, std::string* why) {
 
 void counting_loop() {
   ::prctl(PR_SET_NAME, "gpuexp-pmc", 0, 0, 0);
+  ::prctl(PR_SET_TIMERSLACK, 10000UL, 0, 0, 0);  // 10 us: the wait_signal slices stay short
   if (g_continuous) {
     uint64_t served = 0;
     while (!g_quit.load()) {
