@@ -447,21 +447,25 @@ def main() -> int:
         # Untimed: wait until the exporter has picked the pod map up and attributes every
         # rank (its control plane re-reads the file every 0.5 s), so even a short warmup
         # measures the steady state.
+        # With the RCCL tracer on, also until every rank's communicator is attributed to its
+        # pod (each rank has run collectives by now: the GEMM-count all-reduce above).
         want = {p["name"] for p in pods}
         t_attr = time.time() + 20
         while time.time() < t_attr:
             try:
                 st, body = http_get(port, "/metrics", 2.0)
-                got = {lab["pod"] for _, lab, _ in promtext.samples(promtext.parse(body.decode()),
-                                                                     "pod_gpu_memory_usage")}
-                if st == 200 and want <= got:
+                fams0 = promtext.parse(body.decode())
+                got = {lab["pod"] for _, lab, _ in promtext.samples(fams0, "pod_gpu_memory_usage")}
+                comm = {lab["pod"] for _, lab, _ in promtext.samples(fams0, "amd_rccl_communicator_info")}
+                if st == 200 and want <= got and (not rccl_dir or want <= comm):
                     break
             except OSError:
                 pass
             time.sleep(0.1)
         else:
             attribution_ok = False
-            print(f"[bench] exporter did not attribute all {len(want)} ranks within 20 s", file=sys.stderr, flush=True)
+            print(f"[bench] exporter did not attribute all {len(want)} ranks (GPU processes"
+                  f"{' and RCCL communicators' if rccl_dir else ''}) within 20 s", file=sys.stderr, flush=True)
         # timing=True: the server echoes when it parsed the request and started writing,
         # so each latency splits into request wake-up / server work / response delivery
         client = n.ScrapeClient("127.0.0.1", port, "/metrics", args.gzip, 5000,
