@@ -114,7 +114,8 @@ int main(int argc, char** argv) {
       pods[0] = {"12345678-1234-1234-1234-1234567890a" + std::to_string(k % 10), "ns", "pod-" + std::to_string(k % 7),
                  {{std::string(64, 'a'), "main"}}};
       pods[1] = {"22345678-1234-1234-1234-1234567890ab", "ns2", "pod-b", {}};
-      e.set_pods(pods);
+      e.set_pods(pods, k % 3 != 0);  // every third refresh "incomplete" (a source failed)
+      if (k % 4 == 0) (void)e.source_status();  // races save_state()'s status updates
       e.set_pid_cgroup(int(100 + k % 5), "/kubepods/burstable/pod12345678-1234-1234-1234-1234567890a" +
                                               std::to_string(k % 10) + "/" + std::string(64, 'a'));
       if (k % 50 == 0) e.clear_pid_cgroups();
