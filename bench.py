@@ -136,6 +136,15 @@ def prewake_summary(lat: list, prewoken: list, splits: list) -> dict | None:
     return out
 
 
+def request_split(splits: list, q: float) -> dict | None:
+    d = [x[4] for x in splits if x[4] is not None]
+    w = [x[5] for x in splits if x[5] is not None]
+    if not d:
+        return None
+    return {"send_to_socket_queue": round(pct(d, q), 2), "socket_queue_to_parsed": round(pct(w, q), 2),
+            "timestamped": len(d)}
+
+
 def run_problems(result: dict, n_gpus: int, attribution_ok: bool, rccl_on: bool) -> list:
     """Why an N-GPU result is not a valid measurement of the configuration (N > 1; at N = 1
     problems are recorded in the result but the line is still printed).  Every GPU must be
@@ -487,10 +496,13 @@ def main() -> int:
                 if cl is client:
                     t_send, t_parse, t_write, t_done = cl.last_timing()
                     pw = cl.last_prewoken()
+                    rx = cl.last_server_rx()  # kernel receive time of the request on the server socket
                     prewoken.append(pw)
                     if t_parse and t_send <= t_parse <= t_write <= t_done:
+                        rx_ok = bool(rx) and t_send <= rx <= t_parse
                         splits.append(((t_parse - t_send) / 1e3, (t_write - t_parse) / 1e3, (t_done - t_write) / 1e3,
-                                       pw))
+                                       pw, (rx - t_send) / 1e3 if rx_ok else None,
+                                       (t_parse - rx) / 1e3 if rx_ok else None))
         if dist is not None:
             dist.all_reduce(grad)
         sync()
@@ -790,6 +802,11 @@ def main() -> int:
                 "request_to_server": round(pct([x[0] for x in splits], 0.9), 2),
                 "server_work": round(pct([x[1] for x in splits], 0.9), 2),
                 "response_to_client": round(pct([x[2] for x in splits], 0.9), 2)} if splits else None,
+            # request_to_server split by the kernel's receive timestamp on the server socket:
+            # client send() -> request queued on the server socket (loopback delivery), and
+            # queued -> parsed (the server thread's wake-up + read)
+            "request_split_p50_us": request_split(splits, 0.5),
+            "request_split_p90_us": request_split(splits, 0.9),
             # every timed scrape accounted for: did it reach an HTTP worker that its pre-wake
             # timer had already woken (gpuexp_http_prewake_hits_total), or one asleep in epoll?
             "prewake": prewake_summary(lat, prewoken, splits),

@@ -374,6 +374,8 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_property_readonly("last_bytes", &ScrapeClient::last_bytes)
       .def_property_readonly("errors", &ScrapeClient::errors)
       .def("last_body", [](ScrapeClient& c) { return py::bytes(c.last_body()); })
+      .def("last_server_rx", &ScrapeClient::last_server_rx,
+           "CLOCK_MONOTONIC ns when the server's kernel queued the last request (0 = unknown)")
       .def("last_prewoken", &ScrapeClient::last_prewoken,
            "1 if the server's worker was pre-woken for the last request, 0 if not, -1 unknown")
       .def("last_timing", &ScrapeClient::last_timing,

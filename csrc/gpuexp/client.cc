@@ -153,6 +153,7 @@ double ScrapeClient::scrape() {
   t_done_ = t1;
   t_srv_parse_ = t_srv_write_ = 0;
   srv_prewoken_ = -1;
+  t_srv_rx_ = 0;
   {
     // the response's header block ends 4 bytes before the body
     static const char kName[] = "\r\nX-Gpuexp-Timing: ";
@@ -165,7 +166,9 @@ double ScrapeClient::scrape() {
       t_srv_parse_ = std::strtoull(p, &q, 10);
       char* r = nullptr;
       t_srv_write_ = q ? std::strtoull(q, &r, 10) : 0;
-      srv_prewoken_ = r && *r == ' ' ? int(std::strtol(r, nullptr, 10)) : -1;
+      char* s2 = nullptr;
+      srv_prewoken_ = r && *r == ' ' ? int(std::strtol(r, &s2, 10)) : -1;
+      t_srv_rx_ = s2 && *s2 == ' ' ? std::strtoull(s2, nullptr, 10) : 0;
     }
   }
   if (server_close) {

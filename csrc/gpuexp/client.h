@@ -50,10 +50,13 @@ class ScrapeClient {
   std::vector<uint64_t> last_timing() const { return {t_send_, t_srv_parse_, t_srv_write_, t_done_}; }
   // 1 if the server's worker was pre-woken for the last request, 0 if not, -1 unknown.
   int last_prewoken() const { return srv_prewoken_; }
+  // CLOCK_MONOTONIC ns at which the server's kernel queued the request (0 = not known).
+  uint64_t last_server_rx() const { return t_srv_rx_; }
 
  private:
   uint64_t t_send_ = 0, t_srv_parse_ = 0, t_srv_write_ = 0, t_done_ = 0;
   int srv_prewoken_ = -1;
+  uint64_t t_srv_rx_ = 0;
   std::string host_, path_, req_;
   int port_, timeout_ms_, fd_ = -1, status_ = 0;
   uint64_t bytes_ = 0, errors_ = 0;

@@ -58,6 +58,12 @@ struct Conn {
   bool gzip_client = false;  // its last /metrics request accepted gzip
   uint64_t last_active_ns = 0;
   uint64_t req_start_ns = 0;
+  // Benchmark diagnostics: once a request asked for X-Gpuexp-Timing, the socket carries
+  // kernel receive timestamps (SO_TIMESTAMPNS) and rx_mono_ns is when the kernel queued
+  // the last bytes read (CLOCK_MONOTONIC), splitting "request sent -> parsed" into loopback
+  // delivery and this server's wake-up + read.
+  bool rx_ts = false;
+  uint64_t rx_mono_ns = 0;
   // arrival times of this connection's /metrics requests: the scrape period, learnt
   uint64_t last_metrics_ns = 0;
   uint64_t intervals[4] = {0, 0, 0, 0};
@@ -464,12 +470,19 @@ void HttpServer::run(Worker* w) {
           }
           if (want_timing) {
             // CLOCK_MONOTONIC ns of: request parsed (after this thread woke for it), and
-            // response about to be written — a same-host client splits its latency with them
+            // response about to be written — a same-host client splits its latency with them —
+            // then the pre-woken flag and the kernel's receive time of the request (0 = none)
             c.head.append("X-Gpuexp-Timing: ");
             c.head.append(std::to_string(t0));
             c.head.append(" ");
             c.head.append(std::to_string(mono_ns()));
-            c.head.append(prewoken ? " 1\r\n" : " 0\r\n");  // pre-woken worker?
+            c.head.append(prewoken ? " 1 " : " 0 ");
+            c.head.append(std::to_string(c.rx_ts ? c.rx_mono_ns : 0));
+            c.head.append("\r\n");
+            if (!c.rx_ts) {
+              int one = 1;
+              c.rx_ts = ::setsockopt(c.fd, SOL_SOCKET, SO_TIMESTAMPNS, &one, sizeof(one)) == 0;
+            }
           }
           c.head.append("Content-Length: ");
           c.head.append(std::to_string(b.size()));
@@ -592,7 +605,29 @@ void HttpServer::run(Worker* w) {
       }
       if (ok && (events[i].events & EPOLLIN)) {
         for (;;) {
-          ssize_t r = ::read(fd, rbuf, sizeof(rbuf));
+          ssize_t r;
+          if (c.rx_ts) {  // recvmsg for the receive timestamp (benchmark connections only)
+            iovec iov{rbuf, sizeof(rbuf)};
+            alignas(cmsghdr) char cbuf[CMSG_SPACE(sizeof(timespec))];
+            msghdr mh{};
+            mh.msg_iov = &iov;
+            mh.msg_iovlen = 1;
+            mh.msg_control = cbuf;
+            mh.msg_controllen = sizeof(cbuf);
+            r = ::recvmsg(fd, &mh, 0);
+            for (cmsghdr* cm = r > 0 ? CMSG_FIRSTHDR(&mh) : nullptr; cm; cm = CMSG_NXTHDR(&mh, cm)) {
+              if (cm->cmsg_level != SOL_SOCKET || cm->cmsg_type != SCM_TIMESTAMPNS) continue;
+              timespec ts;
+              std::memcpy(&ts, CMSG_DATA(cm), sizeof(ts));
+              timespec rt;
+              clock_gettime(CLOCK_REALTIME, &rt);
+              const int64_t now_real = int64_t(rt.tv_sec) * 1000000000ll + rt.tv_nsec;
+              const int64_t rx_real = int64_t(ts.tv_sec) * 1000000000ll + ts.tv_nsec;
+              c.rx_mono_ns = uint64_t(int64_t(mono_ns()) - (now_real - rx_real));  // same instant, other clock
+            }
+          } else {
+            r = ::read(fd, rbuf, sizeof(rbuf));
+          }
           if (r > 0) {
             c.in.append(rbuf, size_t(r));
             if (size_t(r) < sizeof(rbuf)) break;
