@@ -261,6 +261,8 @@ void Engine::define_families() {
   f_pod_xwr_total_ = add("amd_pod_xgmi_write_bytes_total",
                          "xGMI bytes sent by the pod's GPUs (per-tick link accumulator deltas; on a shared GPU the "
                          "pod's CU-occupancy share)", C, PO);
+  f_pod_mfma_ = add("amd_pod_gpu_mfma_busy_percent",
+                    "Mean MFMA busy of the pod's GPUs (amd_gpu_mfma_busy_percent of each GPU it owns)", G, PO);
   f_pod_power_ = add("amd_pod_gpu_power_watts", "Socket power of the pod's GPUs", G, PO);
   f_pod_energy_ = add("amd_pod_gpu_energy_joules_total",
                       "GPU energy used by the pod: its GPUs' hardware energy counters, and on a shared GPU the "
@@ -996,6 +998,7 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
     for (uint32_t x = 0; x < nx; ++x) dput(st, i, st.xcc[x], f_xcc_, {idx_str(int(x))}, st.xcc_last[x], gen);
 
   // Optional sources: rocprofiler counters, sentinel (real or mock-simulated).
+  st.mfma_last = kNaN;
   CounterReading cr;
   bool have_ctr = false;
   if (counters_) have_ctr = counters_->sample(i, dt_s, &cr) && cr.ok;
@@ -1008,6 +1011,7 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
     cput(st.self_reads[3], f_self_ctr_scope_, scope < 0 ? kNaN : double(scope), gen,
          [&] { return std::vector<std::string>{std::to_string(d.index)}; });
     dput(st, i, st.ctr[0], f_mfma_, {}, cr.mfma_busy_pct, gen);
+    st.mfma_last = cr.mfma_busy_pct;
     if (cfg_.series_profile == "full") dput(st, i, st.mfma_util, f_mfma_util_, {}, cr.mfma_util_pct, gen);
     dput(st, i, st.ctr[2], f_gui_, {}, cr.gui_active_pct, gen);
     if (scope != 0) {
@@ -1086,7 +1090,8 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
     double xrd = 0, xwr = 0, power = 0, gfx = 0, gfx_share = 0;
     double energy_j = 0;  // this tick
     double xrd_b = 0, xwr_b = 0;  // xGMI bytes this tick (owned GPUs whole, shared GPUs by share)
-    int gfx_n = 0;
+    double mfma = 0;
+    int gfx_n = 0, mfma_n = 0;
     bool share_known = false;
   };
   std::map<std::pair<std::string, std::string>, PodAgg> pods;
@@ -1207,6 +1212,10 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
           pa.gfx += st.cur.gfx_activity;
           pa.gfx_n += 1;
         }
+        if (!std::isnan(st.mfma_last)) {
+          pa.mfma += st.mfma_last;
+          pa.mfma_n += 1;
+        }
       }
     }
   }
@@ -1244,6 +1253,7 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
       cput(r.ref[5], f_pod_xwr_, pa.xwr, gen, L);
       cput(r.ref[6], f_pod_power_, pa.power, gen, L);
       if (pa.gfx_n) cput(r.ref[7], f_pod_gfx_, pa.gfx / pa.gfx_n, gen, L);
+      if (pa.mfma_n) cput(r.ref[8], f_pod_mfma_, pa.mfma / pa.mfma_n, gen, L);
     }
   }
   for (auto it = pod_refs_.begin(); it != pod_refs_.end();)

@@ -190,6 +190,7 @@ class Engine {
     // of dropping the series.
     double thr_last[5] = {kNaN, kNaN, kNaN, kNaN, kNaN};
     double xcc_last[kMaxXcc] = {kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN};
+    double mfma_last = kNaN;  // this tick's amd_gpu_mfma_busy_percent (NaN: no counter window)
     DeviceOwner owner;
     std::string owner_key;  // ns/pod/container the refs were built for
     // cached series handles (re-upserted on owner change or GC)
@@ -212,7 +213,7 @@ class Engine {
     uint64_t gen = 0;
   };
   struct PodRefs {
-    SeriesRef ref[8];
+    SeriesRef ref[9];
     uint64_t gen = 0;
   };
   struct ProcAttr {
@@ -338,6 +339,7 @@ class Engine {
       f_hbm_wr_, f_sen_sclk_, f_sen_lat_, f_sen_xcc_, f_sen_runs_, f_xcc_clk_, f_sen_xlat_, f_sen_mem_, f_sen_xmem_, f_mfma_util_ = -1;
   int f_proc_vram_, f_proc_cu_, f_proc_sdma_, f_proc_evicted_, f_proc_gfx_;
   int f_legacy_mem_ = -1, f_legacy_perc_ = -1;
+  int f_pod_mfma_ = -1;
   int f_pod_vram_, f_pod_procs_, f_pod_gpus_, f_pod_xrd_, f_pod_xwr_, f_pod_power_, f_pod_gfx_, f_pod_gfx_share_,
       f_pod_energy_ = -1, f_pod_xrd_total_ = -1, f_pod_xwr_total_ = -1;
   int f_rccl_calls_, f_rccl_bytes_, f_rccl_comm_;

@@ -482,3 +482,21 @@ def test_pod_xgmi_byte_counters(native, mock_engine, tmp_path):
     b.tick(12 * S)
     assert "pod-a" not in totals(b)[0]
     b.stop()
+
+
+def test_pod_mfma_busy_is_the_mean_of_its_gpus(native, mock_engine):
+    """amd_pod_gpu_mfma_busy_percent: the mean MFMA busy of the GPUs a pod owns (device
+    plugin map), from the same per-tick counter window as amd_gpu_mfma_busy_percent."""
+    uid, cid = "00000000-0000-4000-8000-0000000000c1", "c1" * 32
+    e = mock_engine(3, enable_counters=True)
+    e.set_pods([{"uid": uid, "namespace": "ml", "name": "trainer", "containers": {cid: "w"}}])
+    e.set_device_owners({"0000:10:00.0": {"namespace": "ml", "pod": "trainer", "container": "w"},
+                         "0000:20:00.0": {"namespace": "ml", "pod": "trainer", "container": "w"}})
+    e.mock_set_value(0, "mfma_busy_pct", 80.0)
+    e.mock_set_value(1, "mfma_busy_pct", 40.0)
+    e.mock_set_value(2, "mfma_busy_pct", 5.0)  # not the pod's
+    e.tick(S)
+    e.tick(2 * S)
+    fams = promtext.parse(e.snapshot_text())
+    assert promtext.value(fams, "amd_gpu_mfma_busy_percent", gpu=0) == 80.0
+    assert promtext.value(fams, "amd_pod_gpu_mfma_busy_percent", pod="trainer") == 60.0
