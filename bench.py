@@ -784,6 +784,9 @@ def main() -> int:
             "exporter_cpu_percent": round(cpu_pct, 3),
             "exporter_rss_mb": round(exporter_rss_kb[0] / 1024, 1) if exporter_rss_kb[0] else None,
             "exporter_startup_s": round(getattr(exporter, "startup_s", 0.0), 2),
+            # the engine's own share of it (start() -> first sample; gpuexp_startup_seconds)
+            "engine_startup_s": next((round(v, 3) for _, _, v in promtext.samples(fams, "gpuexp_startup_seconds")),
+                                     None),
             "exporter_startup_budget_s": startup_budget_s(n_gpus),
             "scrape_encoding": "gzip (Prometheus default Accept-Encoding)" if args.gzip else "identity",
             "p50_scrape_identity_us": round(statistics.median(lat_id), 2) if lat_id else None,

@@ -303,6 +303,10 @@ void Engine::define_families() {
   // --- exporter self-metrics (own prefix; the reference registry had none, main.go:40) ---
   f_self_build_ = add("gpuexp_build_info", "Exporter build and backend", G, {"version", "backend"});
   f_self_ticks_ = add("gpuexp_ticks_total", "Sampler ticks completed", C, {});
+  f_self_startup_ = add("gpuexp_startup_seconds",
+                        "Engine start to its first sample: backend init (amdsmi + raw-path validation), one "
+                        "HSA queue per GPU with PMC programs and sentinel, plugin probes",
+                        G, {});
   f_self_last_ = add("gpuexp_last_sample_timestamp_seconds",
                      "Unix time of the tick that produced this exposition (alert on time() - this: a stuck "
                      "sampler keeps serving its last snapshot)", G, {});
@@ -360,6 +364,7 @@ void Engine::define_families() {
 
 bool Engine::start(std::string* err) {
   if (running_.load()) return true;
+  start_mono_ns_ = mono_ns();
   define_families();
   // Listen first: a port conflict fails before any GPU-side source (amdsmi, HSA queues,
   // sentinel runs) exists.  Every later failure tears down what was already started.
@@ -1328,6 +1333,7 @@ void Engine::emit_self(uint64_t gen) {
     s = stats_;
   }
   cput(self_refs_[1], f_self_ticks_, double(s.ticks), gen, none);
+  if (startup_ns_) cput(startup_ref_, f_self_startup_, double(startup_ns_) * 1e-9, gen, none);
   {
     timespec rt;
     clock_gettime(CLOCK_REALTIME, &rt);
@@ -1411,6 +1417,7 @@ void Engine::tick_locked(uint64_t now) {
   last_tick_now_ = now;
   uint64_t ts[kStages + 1];
   ts[0] = mono_ns();
+  if (!startup_ns_ && start_mono_ns_ && ts[0] > start_mono_ns_) startup_ns_ = ts[0] - start_mono_ns_;
   // continuous counters: this tick's read goes out now and is collected before the series
   // stage, so the exported window is exactly the last tick interval
   if (counters_) counters_->kick();

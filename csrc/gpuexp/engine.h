@@ -285,6 +285,7 @@ class Engine {
   std::vector<uint64_t> metrics_fresh_, metrics_coalesced_;  // per device
   uint64_t gzip_eager_ = 0;  // sampler thread only; copied into stats_ per tick
   uint64_t counters_late_ = 0;
+  uint64_t start_mono_ns_ = 0, startup_ns_ = 0;  // start() entry; start() -> first tick
   // thread clocks already charged to gpuexp_sampler_cpu_seconds_total (sampler thread only)
   uint64_t counters_cpu_seen_ = 0, pool_cpu_seen_ = 0, sampler_cpu_seen_ = 0;  // ticks whose counter read missed counters_sync_us (sampler thread)
   std::string sentinel_status_ = "disabled", counters_status_ = "disabled";
@@ -349,8 +350,8 @@ class Engine {
   int f_self_build_, f_self_ticks_, f_self_last_, f_self_stage_, f_self_scrape_, f_self_scrapes_,
       f_self_http_bytes_, f_self_render_bytes_, f_self_series_, f_self_dev_errors_,
       f_self_overruns_, f_self_cpu_, f_self_source_up_, f_self_ctr_scope_, f_self_metrics_reads_, f_self_metrics_period_, f_self_prewake_, f_self_gzip_,
-      f_self_rccl_files_, f_self_unresolved_, f_self_ctr_late_ = -1, f_self_rccl_scans_ = -1, f_self_prewake_hits_ = -1;
-  SeriesRef prewake_hits_ref_;
+      f_self_rccl_files_, f_self_unresolved_, f_self_ctr_late_ = -1, f_self_rccl_scans_ = -1, f_self_prewake_hits_ = -1, f_self_startup_ = -1;
+  SeriesRef prewake_hits_ref_, startup_ref_;
   SeriesRef self_stage_refs_[kStages];
   uint64_t last_stage_ns_[kStages] = {};
 };
