@@ -33,6 +33,7 @@
 #include <hsa/hsa_ven_amd_aqlprofile.h>
 
 #include <algorithm>
+#include <cctype>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -120,6 +121,9 @@ struct Agent {
   double pub_cum[kNumCtr] = {};  // continuous, cumulative reads: raw totals since counting started
   Clock::time_point t_window_end{};  // continuous: end of the last published window
   Derived m;
+  std::string coord_names;  // aqlprofile's coordinates of the first MFMA sample (debug line; m_mu)
+  double cum_xm[kMaxXcc] = {}, cum_xg[kMaxXcc] = {};  // continuous, cumulative: per-XCC totals
+  std::string last_xsamples;  // debug (GPUEXP_AQLPMC_DEBUG): the last read's MFMA / GRBM samples
 };
 
 // aqlprofile entry points come from the runtime's extension table: the runtime loads
@@ -300,7 +304,43 @@ struct Accum {
   double v[kNumCtr];
   int inst[kNumCtr];
   uint64_t samples;
+  double xm[kMaxXcc];  // SQ_VALU_MFMA_BUSY_CYCLES per XCC
+  double xg[kMaxXcc];  // GRBM_COUNT per XCC
+  int nxcc;            // XCCs seen in both counters (0: coordinates unavailable)
+  int xm_n, xg_n;      // highest XCC + 1 seen per counter
+  bool x_unmapped;     // a sample of either counter fell outside the XCC layout
+  int x_seen[2];       // sample_id 0 seen so far, per counter (sample_xcc)
+  int xm_cnt[kMaxXcc];  // MFMA samples per XCC (one per SE: equal on every XCC)
+  // debug: the MFMA / GRBM_COUNT samples in callback order (sample_id, XCC, value)
+  struct S {
+    uint32_t id;
+    int xcc;
+    double v;
+  } xs[2][64];
+  int xs_n[2];
 };
+
+struct CoordProbe {
+  std::string names;
+};
+
+hsa_status_t on_coord(int, int, int, int coordinate, const char* name, void* ud) {
+  auto* p = static_cast<CoordProbe*>(ud);
+  p->names += (p->names.empty() ? "" : ",") + std::string(name ? name : "?") + "=" + std::to_string(coordinate);
+  return HSA_STATUS_SUCCESS;
+}
+
+// XCC of a sample of SQ_VALU_MFMA_BUSY_CYCLES (k = 0) or GRBM_COUNT (k = 1), from its place in
+// the output: aqlprofile returns a counter's samples XCC by XCC, numbering them from 0 again
+// in every XCC (SQ: sample_id = SE 0..3; GRBM: 0 once per XCC), so the XCC is the number of
+// sample_id 0 seen before.  Its event coordinates do not say it (gfx950: "XCD=0,INSTANCE=0,
+// SE=s" for all eight XCDs).  The order is ground-truthed against HW_REG_XCC_ID by an MFMA
+// kernel confined to one XCC (profiles/r03/xcc_mfma_calibration.txt).
+int sample_xcc(Accum* acc, int k, uint32_t sample_id) {
+  if (sample_id == 0) acc->x_seen[k] += 1;
+  const int xcc = acc->x_seen[k] - 1;
+  return xcc >= 0 && xcc < kMaxXcc ? xcc : -1;
+}
 
 hsa_status_t on_data(hsa_ven_amd_aqlprofile_info_type_t type, hsa_ven_amd_aqlprofile_info_data_t* d, void* ud) {
   if (type != HSA_VEN_AMD_AQLPROFILE_INFO_PMC_DATA) return HSA_STATUS_SUCCESS;
@@ -312,6 +352,28 @@ hsa_status_t on_data(hsa_ven_amd_aqlprofile_info_type_t type, hsa_ven_amd_aqlpro
     const double x = double(d->pmc_data.result);
     acc->v[def.ctr] = use_max(def.ctr) ? std::max(acc->v[def.ctr], x) : acc->v[def.ctr] + x;
     acc->inst[def.ctr] += 1;
+    if (def.ctr == kMfma || def.ctr == kGrbmCount) {
+      const int k = def.ctr == kMfma ? 0 : 1;
+      const int xcc = sample_xcc(acc, k, d->sample_id);
+      if (k == 0 && d->sample_id == 0 && acc->x_seen[0] == 1 && acc->a->coord_names.empty()) {
+        CoordProbe p;  // once, for the debug line
+        if (g_aql.hsa_ven_amd_aqlprofile_iterate_event_coord)
+          g_aql.hsa_ven_amd_aqlprofile_iterate_event_coord(acc->a->gpu, ev, 0, on_coord, &p);
+        std::lock_guard<std::mutex> lk(acc->a->m_mu);
+        acc->a->coord_names = p.names.empty() ? "none" : p.names;
+      }
+      if (acc->xs_n[k] < 64) acc->xs[k][acc->xs_n[k]++] = {d->sample_id, xcc, x};
+      if (xcc < 0) {
+        acc->x_unmapped = true;
+      } else if (k == 0) {
+        acc->xm[xcc] += x;
+        acc->xm_cnt[xcc] += 1;
+        acc->xm_n = std::max(acc->xm_n, xcc + 1);
+      } else {
+        acc->xg[xcc] = std::max(acc->xg[xcc], x);
+        acc->xg_n = std::max(acc->xg_n, xcc + 1);
+      }
+    }
     break;
   }
   return HSA_STATUS_SUCCESS;
@@ -434,20 +496,42 @@ bool usable(const Agent* a) { return a && a->ready && !a->broken.load(); }
 
 // Reads the output buffer the last read packet filled: reduced value + instances per counter.
 bool collect(Agent& a, Accum* acc) {
-  *acc = Accum{&a, {}, {}, 0};
-  return g_aql.hsa_ven_amd_aqlprofile_iterate_data(&a.profile, on_data, acc) == HSA_STATUS_SUCCESS;
+  *acc = Accum{};
+  acc->a = &a;
+  const bool ok = g_aql.hsa_ven_amd_aqlprofile_iterate_data(&a.profile, on_data, acc) == HSA_STATUS_SUCCESS;
+  // per-XCC only when every sample of both counters has an XCC, both agree on the XCC count
+  // and every XCC has as many SQ samples (SEs) as the first
+  bool even = acc->xm_n > 0;
+  for (int x = 1; x < acc->xm_n; ++x) even = even && acc->xm_cnt[x] == acc->xm_cnt[0];
+  acc->nxcc = !acc->x_unmapped && even && acc->xm_n == acc->xg_n ? acc->xm_n : 0;
+  return ok;
 }
 
+// d / xm / xg: this window's deltas (chip counters, per-XCC MFMA cycles, per-XCC GRBM_COUNT).
 void publish(Agent& a, const double* d, const Accum& acc, double wall, Clock::time_point end = {},
-             const double* cum = nullptr) {
+             const double* cum = nullptr, const double* xm = nullptr, const double* xg = nullptr) {
+  std::string xsamples;
+  if (g_debug)
+    for (int k = 0; k < 2; ++k) {
+      xsamples += k ? ";grbm_samples=" : "mfma_samples=";
+      for (int j = 0; j < acc.xs_n[k]; ++j) {
+        char t[64];
+        std::snprintf(t, sizeof(t), "%s%u@%d:%.0f", j ? "," : "", acc.xs[k][j].id, acc.xs[k][j].xcc, acc.xs[k][j].v);
+        xsamples += t;
+      }
+    }
   std::lock_guard<std::mutex> lk(a.m_mu);
+  if (g_debug) a.last_xsamples = std::move(xsamples);
   a.t_window_end = end;
   if (cum) std::memcpy(a.pub_cum, cum, sizeof(a.pub_cum));
   std::memcpy(a.last_raw, d, sizeof(a.last_raw));
   std::memcpy(a.last_inst, acc.inst, sizeof(acc.inst));
   a.last_samples = acc.samples;
   a.last_window_s = wall;
-  if (wall > 0) derive(a.m, d, acc.inst, wall);
+  if (wall > 0) {
+    derive(a.m, d, acc.inst, wall);
+    derive_xcc(a.m, xm ? xm : acc.xm, xg ? xg : acc.xg, acc.nxcc);
+  }
 }
 
 void window_all() {
@@ -519,18 +603,24 @@ void read_round() {
     if (!got) continue;
     const double wall = std::chrono::duration<double>(t - a->t_last).count();
     if (g_read_mode == kCumulative) {
-      double d[kNumCtr];
+      double d[kNumCtr], xm[kMaxXcc], xg[kMaxXcc];
       bool backwards = false;
       for (int k = 0; k < kNumCtr; ++k) {
         d[k] = acc.v[k] - a->cum[k];
         backwards = backwards || d[k] < 0;
       }
+      for (int x = 0; x < acc.nxcc; ++x) {
+        xm[x] = std::max(0.0, acc.xm[x] - a->cum_xm[x]);
+        xg[x] = std::max(0.0, acc.xg[x] - a->cum_xg[x]);
+      }
       const bool first = !a->have_cum;
       std::memcpy(a->cum, acc.v, sizeof(a->cum));
+      std::memcpy(a->cum_xm, acc.xm, sizeof(a->cum_xm));
+      std::memcpy(a->cum_xg, acc.xg, sizeof(a->cum_xg));
       a->have_cum = true;
       a->t_last = t;
       if (backwards) ++a->resets;  // wrapped or reset under us: this window is unknown
-      if (!first && !backwards) publish(*a, d, acc, wall, t, acc.v);
+      if (!first && !backwards) publish(*a, d, acc, wall, t, acc.v, xm, xg);
     } else {
       publish(*a, acc.v, acc, wall, t);
       a->t_last = t;
@@ -558,6 +648,8 @@ bool arm_continuous(Agent& a) {
     Accum acc;
     if (tr == Clock::time_point{} || !collect(a, &acc)) return false;
     std::memcpy(a.cum, acc.v, sizeof(a.cum));
+    std::memcpy(a.cum_xm, acc.xm, sizeof(a.cum_xm));
+    std::memcpy(a.cum_xg, acc.xg, sizeof(a.cum_xg));
     a.have_cum = true;
     a.t_last = tr;
   }
@@ -1053,6 +1145,20 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_sample(int dev, 
   return 0;
 }
 
+// Per-XCC MFMA busy of the window gpuexp_rp_sample returns: fills out[0..n) and returns n
+// (the GPU's XCC count), or 0 when the samples' XCC coordinates are unknown / no window.
+extern "C" __attribute__((visibility("default"))) int gpuexp_rp_sample_xcc(int dev, double* out, int max) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (dev < 0 || size_t(dev) >= g_agents.size() || !g_agents[size_t(dev)] || max <= 0) return 0;
+  Agent& a = *g_agents[size_t(dev)];
+  std::lock_guard<std::mutex> mk(a.m_mu);
+  if (!a.m.valid || a.broken) return 0;
+  if (g_continuous && Clock::now() - a.t_window_end > std::chrono::milliseconds(2 * g_interval_ms)) return 0;
+  const int n = std::min(max, a.m.nxcc);
+  for (int x = 0; x < n; ++x) out[x] = a.m.xcc_busy[x];
+  return n;
+}
+
 extern "C" __attribute__((visibility("default"))) void gpuexp_rp_shutdown() {
   g_quit.store(true);
   g_cv.notify_all();
@@ -1103,6 +1209,14 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_debug(int dev, c
     std::snprintf(t, sizeof(t), "%s=%.0f/%d;", name(k), a.last_raw[k], a.last_inst[k]);
     s += t;
   }
+  s += "coords=" + a.coord_names + ";nxcc=" + std::to_string(a.m.nxcc) + ";xcc_busy=";
+  for (int x = 0; x < a.m.nxcc; ++x) {
+    char t[32];
+    std::snprintf(t, sizeof(t), "%s%.2f", x ? "," : "", a.m.xcc_busy[x]);
+    s += t;
+  }
+  s += ";";
+  if (!a.last_xsamples.empty()) s += a.last_xsamples + ";";
   std::snprintf(buf, size_t(len), "%s", s.c_str());
   return 0;
 }

@@ -60,6 +60,9 @@ inline bool use_max(int c) { return c == kGuiActive || c == kGrbmCount; }
 // doubles; gpuexp::kCounterOutputs in sources.h).
 constexpr int kNumOut = 11;
 
+// Per-XCC MFMA busy (gpuexp_rp_sample_xcc): at most this many XCCs per GPU.
+constexpr int kMaxXcc = 16;
+
 // Wave-level SQ counters and TCC EA requests are VMID-filtered for unprivileged clients.
 // The filter is on the HARDWARE VMID, which the scheduler hands out dynamically, so an
 // unprivileged exporter sometimes sees another process's waves (a VMID collision) and
@@ -92,6 +95,10 @@ struct Derived {
   bool privileged = false;  // set at init: process_has_pmc_privilege()
   int scope = -1;  // -1 unknown, 0 wave/EA counters VMID-filtered to this process, 1 device-wide
   double latest[kNumOut] = {};
+  // Per-XCC MFMA busy of the latest window (NaN: that XCC's GRBM clock did not advance);
+  // nxcc = 0 until the samples' XCC coordinates are known.
+  double xcc_busy[kMaxXcc] = {};
+  int nxcc = 0;
   bool valid = false;
   uint64_t windows = 0;
 };
@@ -127,6 +134,27 @@ inline void derive(Derived& a, const double* d, const int* inst, double wall) {
   out[9] = d[kGmiWr32] * 32.0 / wall;                                               // remote (GMI) write B/s
   a.valid = true;
   a.windows += 1;
+}
+
+// Per-XCC MFMA busy: the chip formula with one XCC's share of the SIMDs.  mfma[x] sums that
+// XCC's SQ instances (one per SE), grbm[x] is that XCC's own GRBM_COUNT.  Each XCD runs its
+// own clock (DPM lowers a busy XCD's clock while idle ones stay high), so busy cycles are
+// only comparable with the same XCD's elapsed cycles: the chip value becomes the mean of the
+// per-XCC shares whenever they are known (the max-GRBM_COUNT formula of derive() read 10.3
+// instead of 11.0 with one XCD 88 % busy: profiles/r03/xcc_mfma_calibration.txt).
+inline void derive_xcc(Derived& a, const double* mfma, const double* grbm, int nxcc) {
+  const double simd = nxcc > 0 ? double(a.simd) / nxcc : 0;
+  double sum = 0;
+  int n = 0;
+  for (int x = 0; x < nxcc && x < kMaxXcc; ++x) {
+    a.xcc_busy[x] = grbm[x] > 0 && simd > 0 ? std::min(100.0, 100.0 * mfma[x] / (grbm[x] * simd)) : std::nan("");
+    if (!std::isnan(a.xcc_busy[x])) {
+      sum += a.xcc_busy[x];
+      ++n;
+    }
+  }
+  a.nxcc = std::min(nxcc, kMaxXcc);
+  if (n == a.nxcc && n > 0) a.latest[0] = sum / n;
 }
 
 }  // namespace gpuexp_ctr

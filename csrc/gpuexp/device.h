@@ -168,6 +168,10 @@ struct CounterReading {
   double hbm_write_bps = kNaN;      // TCC_EA0_WRREQ_WRITE_DRAM_32B * 32 B / dt
   double remote_read_bps = kNaN;    // TCC_EA0_RDREQ_GMI_32B * 32 B / dt (memory behind GMI: peers)
   double remote_write_bps = kNaN;   // TCC_EA0_WRREQ_WRITE_GMI_32B * 32 B / dt
+  // mfma_busy_pct of each XCC (its SQ instances over its own GRBM_COUNT x its SIMDs);
+  // nxcc = 0 when the counter source cannot attribute samples to XCCs
+  int nxcc = 0;
+  double xcc_mfma_busy_pct[kMaxXcc] = {kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN};
 };
 
 // HIP sentinel kernel stamps for one GPU (latest completed run).  A run is one wave per

@@ -195,7 +195,7 @@ void Engine::define_families() {
   f_xgmi_speed_ = add("amd_gpu_xgmi_link_speed", "xGMI link speed (PMFW units)", G, D);
   f_mfma_ = add("amd_gpu_mfma_busy_percent",
                 "MFMA (matrix core) busy: share of the last tick's wall time the matrix cores of all SIMDs were "
-                "issuing (SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_COUNT x SIMDs))", G, D);
+                "issuing (SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_COUNT x SIMDs), per XCD over its own clock, averaged)", G, D);
   f_mfma_util_ = add("amd_gpu_mfma_util_percent",
                      "MFMA utilisation while the GPU was active (rocprof MfmaUtil: SQ_VALU_MFMA_BUSY_CYCLES / "
                      "(GRBM_GUI_ACTIVE x SIMDs))", G, D);
@@ -226,6 +226,9 @@ void Engine::define_families() {
                    with(D, {"xcc"}));
   f_sen_xlat_ = add("amd_gpu_sentinel_xcc_dispatch_latency_seconds",
                     "Host launch to sentinel wave start on each XCD (per-XCD CU contention)", G, with(D, {"xcc"}));
+  f_xcc_mfma_ = add("amd_gpu_xcc_mfma_busy_percent",
+                    "MFMA busy of each XCD: its SQ_VALU_MFMA_BUSY_CYCLES / (its GRBM_COUNT x its SIMDs); "
+                    "amd_gpu_mfma_busy_percent is their mean", G, with(D, {"xcc"}));
   f_sen_xmem_ = add("amd_gpu_sentinel_xcc_memory_latency_seconds",
                     "Sentinel memory-chain load latency seen from each XCD (memory-path contention probe)", G,
                     with(D, {"xcc"}));
@@ -1017,7 +1020,11 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
          [&] { return std::vector<std::string>{std::to_string(d.index)}; });
     dput(st, i, st.ctr[0], f_mfma_, {}, cr.mfma_busy_pct, gen);
     st.mfma_last = cr.mfma_busy_pct;
-    if (cfg_.series_profile == "full") dput(st, i, st.mfma_util, f_mfma_util_, {}, cr.mfma_util_pct, gen);
+    if (cfg_.series_profile == "full") {
+      dput(st, i, st.mfma_util, f_mfma_util_, {}, cr.mfma_util_pct, gen);
+      for (int x = 0; x < cr.nxcc && x < kMaxXcc; ++x)
+        dput(st, i, st.xmfma[x], f_xcc_mfma_, {idx_str(x)}, cr.xcc_mfma_busy_pct[x], gen);
+    }
     dput(st, i, st.ctr[2], f_gui_, {}, cr.gui_active_pct, gen);
     if (scope != 0) {
       dput(st, i, st.ctr[1], f_sq_busy_, {}, cr.sq_busy_pct, gen);

@@ -36,6 +36,7 @@ using rp_scope_fn = int (*)(int dev);
 
 using rp_kick_fn = void (*)();
 using rp_cpu_fn = uint64_t (*)();
+using rp_sample_xcc_fn = int (*)(int, double*, int);
 using rp_sync_fn = int (*)(int timeout_us);
 
 class PluginCounters : public CounterSource {
@@ -73,6 +74,7 @@ class PluginCounters : public CounterSource {
       duty(window_ms_, interval_ms_);
     }
     cpu_ = reinterpret_cast<rp_cpu_fn>(::dlsym(handle_, "gpuexp_rp_cpu_ns"));
+    sample_xcc_ = reinterpret_cast<rp_sample_xcc_fn>(::dlsym(handle_, "gpuexp_rp_sample_xcc"));  // optional
     // ABI: a BDF prefixed with '-' reserves that device's HSA agent (partition order) but
     // gets no queue.
     std::vector<std::string> names;
@@ -105,6 +107,7 @@ class PluginCounters : public CounterSource {
     out->hbm_write_bps = v[7];
     out->remote_read_bps = v[8];
     out->remote_write_bps = v[9];
+    out->nxcc = sample_xcc_ ? std::max(0, sample_xcc_(dev, out->xcc_mfma_busy_pct, kMaxXcc)) : 0;
     return true;
   }
 
@@ -136,6 +139,7 @@ class PluginCounters : public CounterSource {
   rp_kick_fn kick_ = nullptr;
   rp_sync_fn sync_ = nullptr;
   rp_cpu_fn cpu_ = nullptr;
+  rp_sample_xcc_fn sample_xcc_ = nullptr;
   void* handle_ = nullptr;
   rp_init_fn init_ = nullptr;
   rp_sample_fn sample_ = nullptr;

@@ -18,7 +18,7 @@ hipError_t launch_fill_bf16(void* p, size_t n, uint32_t seed, hipStream_t stream
 hipError_t launch_stream_copy(const void* src, void* dst, size_t bytes, int blocks, hipStream_t stream);
 hipError_t launch_lds_probe(float* out, int blocks, int iters, int stride, hipStream_t stream);
 hipError_t launch_mfma_duty(float* out, uint64_t* counts, int blocks, double duty, double period_s, double seconds,
-                            hipStream_t stream);
+                            uint32_t xcc_mask, hipStream_t stream);
 }  // namespace gpuexp
 
 namespace {
@@ -81,16 +81,16 @@ PYBIND11_MODULE(_gpuexp_kernels, m) {
      py::arg("stride"), py::arg("stream") = 0,
      "256-thread blocks (4 waves) of ds_read_b32 from LDS: stride 1 conflict-free, stride 32 32-way conflicts");
   m.def("mfma_duty", [](uintptr_t out, uintptr_t counts, int blocks, double duty, double period_s, double seconds,
-                        uintptr_t stream) {
+                        uintptr_t stream, uint32_t xcc_mask) {
     // `out` >= blocks floats, `counts` >= blocks * 4 uint64 (checked by the Python wrapper)
     check(gpuexp::launch_mfma_duty(reinterpret_cast<float*>(out), reinterpret_cast<uint64_t*>(counts), blocks, duty,
-                                   period_s, seconds, reinterpret_cast<hipStream_t>(stream)),
+                                   period_s, seconds, xcc_mask, reinterpret_cast<hipStream_t>(stream)),
           "mfma_duty launch");
   }, py::call_guard<py::gil_scoped_release>(), py::arg("out"), py::arg("counts"), py::arg("blocks"), py::arg("duty"),
-     py::arg("period_s") = 0.002, py::arg("seconds") = 1.0, py::arg("stream") = 0,
+     py::arg("period_s") = 0.002, py::arg("seconds") = 1.0, py::arg("stream") = 0, py::arg("xcc_mask") = 0,
      "256-thread blocks alternating back-to-back v_mfma_f32_32x32x16_bf16 (duty x period) with s_sleep, for "
      "`seconds` (s_memrealtime-timed); 2 blocks per CU = 2 waves per SIMD keep the matrix cores busy `duty` of "
-     "the wall time");
+     "the wall time.  xcc_mask != 0: only blocks on those XCCs (HW_REG_XCC_ID) run, the rest exit at once");
   m.def("gemm_burn", [](int device, int M, int N, int K, double seconds, int iters_per_sync, int variant) {
     // Torch-free synthetic GEMM pod: keeps one GPU busy for `seconds` and reports the
     // achieved bf16 TFLOP/s (random operands).

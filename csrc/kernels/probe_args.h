@@ -33,6 +33,7 @@ struct CalibMfmaArgs {
   uint64_t period_ticks;  // s_memrealtime ticks (10 ns) per on/off period
   uint64_t on_ticks;      // MFMA phase of each period (<= period_ticks)
   uint64_t total_ticks;   // run length
+  uint32_t xcc_mask;      // XCCs (HW_REG_XCC_ID bits) whose blocks run; 0 = every XCC
 };
 constexpr int kMfmaPerCheck = 32;  // MFMAs between two clock reads (32 x 32 cycles)
 

@@ -67,6 +67,17 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 // back-to-back, so the extra chains only make that independent of the compiler's schedule.
 __device__ inline void mfma_duty_body(const CalibMfmaArgs& a) {
   const int lane = threadIdx.x & 63;
+  if (a.xcc_mask) {  // XCC-targeted run: blocks that landed elsewhere leave at once
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    if (!(a.xcc_mask >> (xcc & 31) & 1u)) {
+      if (lane == 0) {
+        a.out[blockIdx.x] = 0.f;
+        a.mfma_count[blockIdx.x * (kProbeBlock / 64) + (threadIdx.x >> 6)] = 0;
+      }
+      return;
+    }
+  }
   bf16x8 x, y;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {

@@ -23,12 +23,13 @@ __global__ __launch_bounds__(kProbeBlock) void mfma_duty_kernel(CalibMfmaArgs a)
 
 // Host checks (the kernel's loop relies on them): period > 0, on <= period, a bounded run.
 hipError_t launch_mfma_duty(float* out, uint64_t* counts, int blocks, double duty, double period_s, double seconds,
-                            hipStream_t stream) {
+                            uint32_t xcc_mask, hipStream_t stream) {
   if (!out || !counts || blocks < 1 || blocks > (1 << 16) || !(duty >= 0 && duty <= 1) || !(period_s >= 1e-5) ||
       period_s > 1.0 || !(seconds > 0) || seconds > 60)
     return hipErrorInvalidValue;
   const uint64_t period = uint64_t(period_s * 1e8 + 0.5);  // 100 MHz s_memrealtime ticks
-  CalibMfmaArgs a{out, counts, period, uint64_t(double(period) * duty + 0.5), uint64_t(seconds * 1e8)};
+  CalibMfmaArgs a{out, counts, period, uint64_t(double(period) * duty + 0.5), uint64_t(seconds * 1e8),
+                  xcc_mask};
   if (a.on_ticks > a.period_ticks) a.on_ticks = a.period_ticks;
   hipLaunchKernelGGL(mfma_duty_kernel, dim3(blocks), dim3(kProbeBlock), 0, stream, a);
   return hipGetLastError();

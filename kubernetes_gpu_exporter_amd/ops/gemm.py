@@ -79,19 +79,24 @@ def lds_probe(out, blocks: int, iters: int, conflicts: bool, stream=None):
 
 
 def mfma_duty(device: int, duty: float, seconds: float, period_s: float = 0.002, stream=None,
-              blocks: int | None = None):
+              blocks: int | None = None, xcc_mask: int = 0):
     """Launches the MFMA duty-cycle calibration kernel on `device` (non-blocking): 2 blocks
     of 4 waves per CU (2 waves per SIMD) alternate back-to-back v_mfma_f32_32x32x16_bf16 for
-    duty x period_s with s_sleep for the rest, for `seconds`.  Returns (out, counts) tensors;
-    counts[w] = MFMAs wave w issued (valid after the kernel finished)."""
+    duty x period_s with s_sleep for the rest, for `seconds`.  xcc_mask != 0 runs only the
+    blocks that land on those XCCs (bit x = HW_REG_XCC_ID x); the others exit at once.
+    Returns (out, counts) tensors; counts[w] = MFMAs wave w issued (valid after the kernel
+    finished; 0 for the waves of skipped blocks)."""
     import torch
     if not (0.0 <= duty <= 1.0) or not (0 < seconds <= 60) or not (1e-5 <= period_s <= 1.0):
         raise ValueError("duty in [0,1], 0 < seconds <= 60, 1e-5 <= period_s <= 1")
+    if not (0 <= xcc_mask < 1 << 32):
+        raise ValueError("xcc_mask is a 32-bit XCC bit set")
     dev = torch.device(f"cuda:{device}")
     if blocks is None:
         blocks = 2 * torch.cuda.get_device_properties(dev).multi_processor_count
     out = torch.zeros(blocks, dtype=torch.float32, device=dev)
     counts = torch.zeros(blocks * 4, dtype=torch.int64, device=dev)
     s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
-    kernels().mfma_duty(out.data_ptr(), counts.data_ptr(), blocks, float(duty), float(period_s), float(seconds), s)
+    kernels().mfma_duty(out.data_ptr(), counts.data_ptr(), blocks, float(duty), float(period_s), float(seconds), s,
+                        int(xcc_mask))
     return out, counts

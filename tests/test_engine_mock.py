@@ -250,13 +250,14 @@ def test_full_profile_adds_reliability_families(mock_engine):
     """`full` = the 64-series standard load + ECC / PCIe AER / NAK / recovery / xGMI link
     + per-XCD clocks, per-XCD sentinel dispatch latency and HBM latency (chip + 8 XCDs)
     + the 6 KFD SMI event counters + retired HBM pages by state + GTT used/total + board
-    identity and firmware versions."""
+    identity and firmware versions + MFMA util + per-XCD MFMA busy."""
     e = mock_engine(2, http=False, enable_sentinel=True, enable_counters=True, series_profile="full")
     e.mock_set_value(1, "ecc_ue", 3)
     e.mock_set_value(1, "aer_cor", 7)
     ticks(e, 3)
     fams = parse(e)
-    assert dict(device_series_per_gpu(fams)) == {"0": 118, "1": 118}  # + board (1), firmware (4 in mock), MFMA util (1)
+    # + board (1), firmware (4 in mock), MFMA util (1), per-XCD MFMA busy (8)
+    assert dict(device_series_per_gpu(fams)) == {"0": 126, "1": 126}
     lat = {s[1]["xcc"]: s[2] for s in fams["amd_gpu_sentinel_xcc_dispatch_latency_seconds"].samples
            if s[1]["gpu"] == "0"}
     assert sorted(lat) == [str(x) for x in range(8)] and min(lat.values()) == lat["0"]
@@ -482,6 +483,22 @@ def test_pod_xgmi_byte_counters(native, mock_engine, tmp_path):
     b.tick(12 * S)
     assert "pod-a" not in totals(b)[0]
     b.stop()
+
+
+def test_xcc_mfma_busy_series(mock_engine):
+    """amd_gpu_xcc_mfma_busy_percent: one series per XCD of the GPU, full profile only,
+    from the same counter window as the chip value."""
+    e = mock_engine(1, http=False, enable_counters=True, series_profile="full")
+    e.mock_set_value(0, "mfma_busy_pct", 30.0)
+    e.mock_set_value(0, "xcc_mfma_busy_pct", 30.0)
+    ticks(e, 2)
+    fams = parse(e)
+    xs = {s[1]["xcc"]: s[2] for s in fams["amd_gpu_xcc_mfma_busy_percent"].samples if s[1]["gpu"] == "0"}
+    assert sorted(xs) == [str(x) for x in range(8)] and set(xs.values()) == {30.0}
+    assert promtext.value(fams, "amd_gpu_mfma_busy_percent", gpu=0) == 30.0
+    std = mock_engine(1, http=False, enable_counters=True)
+    ticks(std, 2)
+    assert "amd_gpu_xcc_mfma_busy_percent" not in parse(std)
 
 
 def test_pod_mfma_busy_is_the_mean_of_its_gpus(native, mock_engine):

@@ -775,6 +775,32 @@ def test_mfma_busy_calibration():
         assert c["changed_fraction"] >= 0.9, (key, c["per_tick_busy"])
 
 
+def test_xcc_mfma_busy_calibration():
+    """amd_gpu_xcc_mfma_busy_percent against an MFMA kernel confined to one XCD: the duty
+    kernel at 90 % whose blocks leave at once unless HW_REG_XCC_ID is the target.  That XCD
+    reads within 10 points of 90, every other XCD reads ~0, and the chip value is the mean
+    of the eight (each XCD's busy cycles over its own elapsed cycles)."""
+    import json
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mfma_calibration.py"), "--duties", "",
+                        "--xcc-cases", "2,5", "--xcc-duty", "0.9", "--no-gated"],
+                       capture_output=True, text=True, timeout=120)
+    print(r.stdout[-4000:], r.stderr[-3000:])
+    line = [l for l in r.stdout.splitlines() if l.startswith("RESULT ")]
+    assert line, "calibration produced no result"
+    res = json.loads(line[-1][7:])
+    if "counters=unavailable" in res["status"]:
+        pytest.skip("device counting unavailable on this box: " + res["status"])
+    assert res["cases"]["idle"]["xcc_median"] == {str(x): 0.0 for x in range(8)}, res["cases"]["idle"]
+    for x in (2, 5):
+        c = res["cases"][f"xcc_{x}"]
+        xs = c["xcc_median"]
+        assert sorted(xs) == [str(i) for i in range(8)], xs
+        assert abs(xs[str(x)] - 90.0) <= 10.0, (x, xs)
+        assert all(v < 1.0 for k, v in xs.items() if k != str(x)), (x, xs)
+        assert abs(c["busy_median"] - sum(xs.values()) / 8) < 0.5, (x, c["busy_median"], xs)
+        assert c["waves_that_ran"] == c["waves"] // 8, c
+
+
 def test_device_scope_pmc_calibration():
     """Device-scope PMC families against ground truth (tools/pmc_validate.py): HBM read and
     write of a stream copy of known bytes, waves/s of known grids, and LDS bank conflicts

@@ -15,8 +15,12 @@ Cases:
   gated d    : the host runs 100 % MFMA kernels for d of every 20 ms and leaves the GPU idle
                in between: busy ~100 d, GUI active ~100 d, util ~100.
   idle       : no kernel at all: busy ~0.
+  xcc x      : (--xcc-cases) the resident kernel at --xcc-duty on XCC x only (its other
+               blocks exit at once): amd_gpu_xcc_mfma_busy_percent{xcc=x} ~100 d, the other
+               XCCs ~0, the chip value ~100 d / 8 = the mean of the XCCs.
 Every tick of a case is recorded, so "changes every tick" is checked too.
-Usage: python tools/mfma_calibration.py [--mode continuous|duty] [--hz 10]  -> RESULT json
+Usage: python tools/mfma_calibration.py [--mode continuous|duty] [--hz 10] [--xcc-cases 0,5]
+  -> RESULT json
 """
 import argparse
 import json
@@ -36,6 +40,9 @@ def main() -> int:
     ap.add_argument("--seconds", type=float, default=2.6, help="kernel run per resident case")
     ap.add_argument("--duties", default="0,0.25,0.5,0.75,1")
     ap.add_argument("--no-sentinel", action="store_true")
+    ap.add_argument("--xcc-cases", default="", help="comma-separated XCCs to run the XCC-targeted case on")
+    ap.add_argument("--xcc-duty", type=float, default=0.9)
+    ap.add_argument("--no-gated", action="store_true")
     args = ap.parse_args()
 
     import torch  # one HIP runtime per process: torch's, loaded before the exporter's plugins
@@ -71,8 +78,8 @@ def main() -> int:
 
     def raw():
         """The plugin's last window: raw per-counter deltas (reduced) + window length."""
-        buf = ctypes.create_string_buffer(4096)
-        plugin.gpuexp_rp_debug(0, buf, 4096)
+        buf = ctypes.create_string_buffer(8192)
+        plugin.gpuexp_rp_debug(0, buf, 8192)
         return buf.value.decode()
 
     def val(fams, name, **kw):
@@ -96,9 +103,12 @@ def main() -> int:
                 last = tk
                 continue
             last = tk
-            rows.append({k: val(fams, f, gpu=0) for k, f in (
+            row = {k: val(fams, f, gpu=0) for k, f in (
                 ("busy", "amd_gpu_mfma_busy_percent"), ("util", "amd_gpu_mfma_util_percent"),
-                ("gui", "amd_gpu_gui_active_percent"), ("clk", "amd_gpu_sentinel_sclk_hz"))})
+                ("gui", "amd_gpu_gui_active_percent"), ("clk", "amd_gpu_sentinel_sclk_hz"))}
+            row["xcc"] = {int(lab["xcc"]): v for _, lab, v in promtext.samples(fams, "amd_gpu_xcc_mfma_busy_percent")
+                          if lab.get("gpu") == "0"}
+            rows.append(row)
         return rows
 
     def summary(rows, expect_busy, expect_util=None, extra=None):
@@ -117,9 +127,10 @@ def main() -> int:
 
     res = {"status": status, "mode": args.mode, "hz": args.hz, "simds": simds, "cases": {}}
     time.sleep(1.0)
-    res["cases"]["idle"] = summary(ticks_during(1.5), 0.0, None, {"raw_window": raw()})
+    idle_rows = ticks_during(1.5)
+    res["cases"]["idle"] = summary(idle_rows, 0.0, None, {"raw_window": raw()})
     print("idle", res["cases"]["idle"]["busy_median"], flush=True)
-    for d in [float(x) for x in args.duties.split(",")]:
+    for d in [float(x) for x in args.duties.split(",") if x.strip()]:
         def cum_mfma():
             kv = dict(x.split("=", 1) for x in raw().split(";") if "=" in x)
             return float(kv["cum_MFMA"]) if "cum_MFMA" in kv else None
@@ -148,8 +159,29 @@ def main() -> int:
                                      "raw_window": raw_window})
         print(key, res["cases"][key]["busy_median"], res["cases"][key]["util_median"], "from count", from_count,
               "busy cycles / (32 x MFMAs issued)", cycles_ratio, flush=True)
+    def xcc_medians(rows):
+        xs = sorted({x for r in rows for x in r["xcc"]})
+        return {str(x): statistics.median([r["xcc"][x] for r in rows if x in r["xcc"]]) for x in xs}
+
+    res["cases"]["idle"]["xcc_median"] = xcc_medians(idle_rows)
+    for x in [int(v) for v in args.xcc_cases.split(",") if v.strip()]:
+        time.sleep(0.25)
+        t_launch = time.perf_counter()
+        out, counts = mfma_duty(0, args.xcc_duty, args.seconds, period_s=0.002, xcc_mask=1 << x)
+        rows = ticks_during(args.seconds - 0.35, skip=0.45)
+        raw_window = raw()
+        torch.cuda.synchronize()
+        run_s = time.perf_counter() - t_launch
+        c = counts.cpu()
+        key = f"xcc_{x}"
+        res["cases"][key] = summary(rows, 100.0 * args.xcc_duty / 8, None, {
+            "xcc": x, "xcc_duty": args.xcc_duty, "xcc_median": xcc_medians(rows), "run_s": run_s,
+            "waves_that_ran": int((c > 0).sum().item()), "waves": int(c.numel()), "mfma_issued": int(c.sum().item()),
+            "raw_window": raw_window})
+        print(key, "chip", res["cases"][key]["busy_median"], "per-XCC", res["cases"][key]["xcc_median"],
+              "waves ran", res["cases"][key]["waves_that_ran"], "/", res["cases"][key]["waves"], flush=True)
     # gated: kernel at 100 % for on_ms of every 20 ms, idle in between
-    for on_ms in (10.0, 5.0):
+    for on_ms in (() if args.no_gated else (10.0, 5.0)):
         period = 0.020
 
         def step(on=on_ms / 1000.0):
