@@ -207,6 +207,7 @@ bool MockBackend::sentinel(const DeviceInfo& dev, SentinelReading* out) {
     out->xcc_mem_latency_s[x] = out->mem_latency_s;
   }
   out->runs = s.started ? uint64_t(s.accum) : 0;
+  out->pending_s = get(s, "sentinel_pending_s", 0.0);
   return true;
 }
 

@@ -188,6 +188,9 @@ struct SentinelReading {
   // dependent uncached device-memory load latency (mean over waves; per XCD by XCC_ID)
   double mem_latency_s = kNaN;
   double xcc_mem_latency_s[kMaxXcc] = {kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN};
+  // how long the oldest launched run has been waiting to finish (0: none outstanding): grows
+  // while the GPU gives a one-wave kernel no slot (compute starvation) or stops (hang)
+  double pending_s = kNaN;
 };
 
 class Backend {

@@ -219,6 +219,9 @@ void Engine::define_families() {
                    "Host launch to first-wave start of the sentinel kernel (queue contention)", G, D);
   f_sen_xcc_ = add("amd_gpu_sentinel_xcc_id", "XCC that workgroup 0 of the last sentinel run landed on", G, D);
   f_sen_runs_ = add("amd_gpu_sentinel_runs_total", "Completed sentinel kernel runs", C, D);
+  f_sen_pend_ = add("amd_gpu_sentinel_pending_seconds",
+                    "How long the sentinel's outstanding run has waited to finish (0: none outstanding). Grows "
+                    "while the workload leaves a one-wave kernel no CU slot, or without bound on a hung GPU", G, D);
   f_sen_mem_ = add("amd_gpu_sentinel_memory_latency_seconds",
                    "Dependent-load latency of the sentinel's uncached device-memory chain: memory-path contention probe", G, D);
   // --- full profile: per-XCD detail (8 XCDs on an SPX-mode MI355X) ---
@@ -1049,6 +1052,7 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
     dput(st, i, st.sen[2], f_sen_xcc_, {}, sr.xcc_id, gen);
     dput(st, i, st.sen[3], f_sen_runs_, {}, double(sr.runs), gen);
     if (cfg_.series_profile == "full") {
+      dput(st, i, st.sen_pend, f_sen_pend_, {}, sr.pending_s, gen);
       dput(st, i, st.sen_mem, f_sen_mem_, {}, sr.mem_latency_s, gen);
       for (int x = 0; x < kMaxXcc; ++x) {
         if (!std::isnan(sr.xcc_latency_s[x]))

@@ -198,7 +198,7 @@ class Engine {
         energy, temp[9], clk[3], xrd[kMaxXgmiLinks], xwr[kMaxXgmiLinks], xrd_rate, xwr_rate,
         links_up, pcie_bw, pcie_replay, pcie_speed, pcie_width, thr[5], nprocs, cu_occ, ctr[10],
         sen[4], ecc[3], aer[3], nak[2], recov, xgmi_w, xgmi_s, xclk[kMaxXcc], sen_xlat[kMaxXcc], sen_mem, sen_xmem[kMaxXcc],
-        kev[std::size(kKfdSubscribed)], pages[3], gtt_used, gtt_total, board, mfma_util, xmfma[kMaxXcc];
+        kev[std::size(kKfdSubscribed)], pages[3], gtt_used, gtt_total, board, mfma_util, xmfma[kMaxXcc], sen_pend;
     std::vector<SeriesRef> fw;  // amd_gpu_firmware_info, one per component
     uint64_t kfd_events[kKfdEventIds] = {};  // KFD SMI events seen on this GPU, by id
     uint64_t errors = 0;
@@ -337,7 +337,7 @@ class Engine {
       f_power_cap_, f_energy_, f_temp_, f_clk_, f_xrd_, f_xwr_, f_xrd_rate_, f_xwr_rate_,
       f_links_up_, f_pcie_bw_, f_pcie_replay_, f_pcie_speed_, f_pcie_width_, f_thr_, f_nprocs_,
       f_cu_occ_, f_ecc_, f_aer_, f_pcie_nak_, f_pcie_recov_, f_xgmi_width_, f_xgmi_speed_, f_mfma_, f_sq_busy_, f_gui_, f_waves_, f_lds_, f_lds_conf_, f_hbm_rd_, f_remote_rd_, f_remote_wr_,
-      f_hbm_wr_, f_sen_sclk_, f_sen_lat_, f_sen_xcc_, f_sen_runs_, f_xcc_clk_, f_sen_xlat_, f_sen_mem_, f_sen_xmem_, f_mfma_util_, f_xcc_mfma_ = -1;
+      f_hbm_wr_, f_sen_sclk_, f_sen_lat_, f_sen_xcc_, f_sen_runs_, f_xcc_clk_, f_sen_xlat_, f_sen_mem_, f_sen_xmem_, f_mfma_util_, f_xcc_mfma_, f_sen_pend_ = -1;
   int f_proc_vram_, f_proc_cu_, f_proc_sdma_, f_proc_evicted_, f_proc_gfx_;
   int f_legacy_mem_ = -1, f_legacy_perc_ = -1;
   int f_pod_mfma_ = -1;

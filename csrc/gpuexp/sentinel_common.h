@@ -68,6 +68,9 @@ struct SentinelRun {
   hsa_agent_t agent{};
   bool have_agent = false;
   uint64_t launched = 0, completed = 0, stalled = 0, errors = 0;
+  // at the last drain (the start of a tick, before its launch): age of the oldest run still
+  // outstanding, 0 when every earlier launch had finished
+  double pending_s = 0;
   SentinelReading last;
 };
 
@@ -124,13 +127,22 @@ inline void sentinel_drain(SentinelRun& p, int nslots, double sys_ns_per_tick) {
     r.mem_latency_s = mem_n ? mem_sum / mem_n : std::nan("");
     p.last = r;
   }
+  p.pending_s = 0;
+  if (p.completed < p.launched) {
+    const uint64_t launch = p.host_launch[size_t((p.completed + 1) % uint64_t(nslots))];
+    const uint64_t now = sentinel_hsa_now();
+    p.pending_s = now > launch ? double(now - launch) * sys_ns_per_tick * 1e-9 : 1e-9;
+  }
 }
 
-// The latest reading of a run, or false before the first completed run.
+// The latest reading plus pending_s (as of the last drain); false until a run completed or
+// one is found outstanding.  Before the first completion only pending_s is set.
 inline bool sentinel_fill(const SentinelRun& p, SentinelReading* out) {
-  if (!p.last.ok) return false;
+  if (!p.last.ok && !(p.pending_s > 0)) return false;
   *out = p.last;
+  out->ok = true;
   out->runs = p.completed;
+  out->pending_s = p.pending_s;
   return true;
 }
 

@@ -256,8 +256,8 @@ def test_full_profile_adds_reliability_families(mock_engine):
     e.mock_set_value(1, "aer_cor", 7)
     ticks(e, 3)
     fams = parse(e)
-    # + board (1), firmware (4 in mock), MFMA util (1), per-XCD MFMA busy (8)
-    assert dict(device_series_per_gpu(fams)) == {"0": 126, "1": 126}
+    # + board (1), firmware (4 in mock), MFMA util (1), per-XCD MFMA busy (8), sentinel pending (1)
+    assert dict(device_series_per_gpu(fams)) == {"0": 127, "1": 127}
     lat = {s[1]["xcc"]: s[2] for s in fams["amd_gpu_sentinel_xcc_dispatch_latency_seconds"].samples
            if s[1]["gpu"] == "0"}
     assert sorted(lat) == [str(x) for x in range(8)] and min(lat.values()) == lat["0"]
@@ -499,6 +499,17 @@ def test_xcc_mfma_busy_series(mock_engine):
     std = mock_engine(1, http=False, enable_counters=True)
     ticks(std, 2)
     assert "amd_gpu_xcc_mfma_busy_percent" not in parse(std)
+
+
+def test_sentinel_pending_seconds(mock_engine):
+    """amd_gpu_sentinel_pending_seconds (full profile): 0 while runs complete, the scripted
+    wait while one is outstanding."""
+    e = mock_engine(1, http=False, enable_sentinel=True, series_profile="full")
+    ticks(e, 2)
+    assert promtext.value(parse(e), "amd_gpu_sentinel_pending_seconds", gpu=0) == 0.0
+    e.mock_set_value(0, "sentinel_pending_s", 75.0)
+    ticks(e, 1, t0=10 * S)
+    assert promtext.value(parse(e), "amd_gpu_sentinel_pending_seconds", gpu=0) == 75.0
 
 
 def test_pod_mfma_busy_is_the_mean_of_its_gpus(native, mock_engine):

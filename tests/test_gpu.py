@@ -779,10 +779,12 @@ def test_xcc_mfma_busy_calibration():
     """amd_gpu_xcc_mfma_busy_percent against an MFMA kernel confined to one XCD: the duty
     kernel at 90 % whose blocks leave at once unless HW_REG_XCC_ID is the target.  That XCD
     reads within 10 points of 90, every other XCD reads ~0, and the chip value is the mean
-    of the eight (each XCD's busy cycles over its own elapsed cycles)."""
+    of the eight (each XCD's busy cycles over its own elapsed cycles).  Then 2 s of MFMAs on
+    every SIMD: amd_gpu_sentinel_pending_seconds grows while the sentinel's run waits behind
+    them and is 0 before and after."""
     import json
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mfma_calibration.py"), "--duties", "",
-                        "--xcc-cases", "2,5", "--xcc-duty", "0.9", "--no-gated"],
+                        "--xcc-cases", "2,5", "--xcc-duty", "0.9", "--no-gated", "--starve", "2.0"],
                        capture_output=True, text=True, timeout=120)
     print(r.stdout[-4000:], r.stderr[-3000:])
     line = [l for l in r.stdout.splitlines() if l.startswith("RESULT ")]
@@ -799,6 +801,11 @@ def test_xcc_mfma_busy_calibration():
         assert all(v < 1.0 for k, v in xs.items() if k != str(x)), (x, xs)
         assert abs(c["busy_median"] - sum(xs.values()) / 8) < 0.5, (x, c["busy_median"], xs)
         assert c["waves_that_ran"] == c["waves"] // 8, c
+    st = res["cases"]["starve"]
+    # 2 s of MFMAs on every SIMD: the sentinel's run waits behind them, then completes
+    assert st["pending_before"] == 0.0, st
+    assert st["pending_max"] >= 0.8, st
+    assert st["pending_after"] == 0.0, st
 
 
 def test_device_scope_pmc_calibration():

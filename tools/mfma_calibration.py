@@ -43,6 +43,9 @@ def main() -> int:
     ap.add_argument("--xcc-cases", default="", help="comma-separated XCCs to run the XCC-targeted case on")
     ap.add_argument("--xcc-duty", type=float, default=0.9)
     ap.add_argument("--no-gated", action="store_true")
+    ap.add_argument("--sentinel-impl", default="auto", help="auto (on the PMC queue) | hip (its own HIP stream)")
+    ap.add_argument("--starve", type=float, default=0.0,
+                    help="seconds of a 100 %% MFMA kernel that leaves the sentinel no slot (pending gauge case)")
     args = ap.parse_args()
 
     import torch  # one HIP runtime per process: torch's, loaded before the exporter's plugins
@@ -59,6 +62,7 @@ def main() -> int:
     c.series_profile = "full"
     c.enable_counters = True
     c.enable_sentinel = not args.no_sentinel
+    c.sentinel_impl = args.sentinel_impl
     c.counters_plugin = rocprof_plugin_path("aqlpmc")
     c.counters_mode = args.mode
     c.counters_window_ms = 20
@@ -198,6 +202,34 @@ def main() -> int:
                                     {"raw_window": raw()})
         print(key, res["cases"][key]["busy_median"], res["cases"][key]["util_median"], res["cases"][key]["gui_median"],
               flush=True)
+    if args.starve > 0:
+        # 8 blocks of 4 waves per CU = every wave slot of every SIMD, each wave issuing MFMAs
+        # back to back for `starve` s (the grid's later blocks wait for the first ones): the
+        # one-wave sentinel run cannot start, so amd_gpu_sentinel_pending_seconds must grow,
+        # and drop to 0 once the kernel is gone
+        def pend():
+            return val(promtext.parse(e.snapshot_text()), "amd_gpu_sentinel_pending_seconds", gpu=0)
+        time.sleep(0.3)
+        before = pend()
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
+        ev = torch.cuda.Event()
+        t0 = time.perf_counter()
+        mfma_duty(0, 1.0, args.starve, period_s=0.002, blocks=8 * cus)
+        ev.record()
+        seen = []
+        while not ev.query() and time.perf_counter() - t0 < 4 * args.starve + 5:
+            time.sleep(0.1)
+            seen.append(pend())
+        torch.cuda.synchronize()
+        run_s = time.perf_counter() - t0
+        time.sleep(0.5)
+        kv = dict(x.split("=", 1) for x in raw().split(";") if "=" in x)
+        res["cases"]["starve"] = {"seconds": args.starve, "kernel_s": run_s, "pending_before": before,
+                                  "pmc_read_stalls": int(kv.get("stalls", -1)),
+                                  "pending_during": [round(v, 3) if v is not None else None for v in seen],
+                                  "pending_max": max([v for v in seen if v is not None] or [0]),
+                                  "pending_after": pend()}
+        print("starve", res["cases"]["starve"], flush=True)
     res["raw_counters"] = raw()
     res["stage_counters_ms_last"] = e.stats()["stage_ns"]["counters"] / 1e6
     e.stop()
