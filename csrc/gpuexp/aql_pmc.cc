@@ -90,7 +90,7 @@ struct Agent {
   std::vector<int> event_ctr;  // events[i] -> Ctr
   hsa_ven_amd_aqlprofile_profile_t profile{};
   hsa_ext_amd_aql_pm4_packet_t start_pkt{}, read_pkt{}, stop_pkt{};
-  uint32_t out_size = 0;
+  uint32_t out_size = 0, cmd_size = 0;
   void* cmd_buf = nullptr;
   void* out_buf = nullptr;
   bool ready = false;
@@ -124,6 +124,17 @@ struct Agent {
   std::string coord_names;  // aqlprofile's coordinates of the first MFMA sample (debug line; m_mu)
   double cum_xm[kMaxXcc] = {}, cum_xg[kMaxXcc] = {};  // continuous, cumulative: per-XCC totals
   std::string last_xsamples;  // debug (GPUEXP_AQLPMC_DEBUG): the last read's MFMA / GRBM samples
+  // Read rescue (continuous, cumulative; see rescue_reads): a second queue that only ever
+  // carries read packets, with its own profile, command and output buffers.
+  int stuck_rounds = 0;  // consecutive rounds this GPU's read had not completed
+  std::atomic<bool> rescued{false};  // reads go to rq from now on (read by _debug)
+  bool orphan = false;   // the read abandoned on `queue` (its completion, on sig, is ignored)
+  hsa_queue_t* rq = nullptr;
+  hsa_signal_t rsig{};
+  hsa_ven_amd_aqlprofile_profile_t rprofile{};
+  hsa_ext_amd_aql_pm4_packet_t rstart_pkt{}, rread_pkt{};
+  void* rcmd_buf = nullptr;
+  void* rout_buf = nullptr;
 };
 
 // aqlprofile entry points come from the runtime's extension table: the runtime loads
@@ -247,19 +258,22 @@ void* sys_alloc(size_t bytes, hsa_agent_t gpu) {
 // COMPLETE: the continuous read packets use that, so a sentinel dispatch that cannot get a
 // SIMD (measured: next to waves issuing MFMAs back-to-back for seconds, even at wave
 // priority 3) does not hold the counter reads behind it.
-void submit(Agent& a, const hsa_ext_amd_aql_pm4_packet_t& pkt, bool barrier = true) {
+void submit_on(Agent& a, hsa_queue_t* q, hsa_signal_t sig, const hsa_ext_amd_aql_pm4_packet_t& pkt, bool barrier) {
   std::lock_guard<std::mutex> lk(a.submit_mu);
-  hsa_queue_t* q = a.queue;
   const uint64_t idx = hsa_queue_add_write_index_screlease(q, 1);
   auto* slot = static_cast<hsa_ext_amd_aql_pm4_packet_t*>(q->base_address) + (idx & (q->size - 1));
   std::memcpy(slot->pm4_command, pkt.pm4_command, sizeof(pkt.pm4_command));
-  slot->completion_signal = a.sig;
+  slot->completion_signal = sig;
   const uint16_t header = uint16_t((HSA_PACKET_TYPE_VENDOR_SPECIFIC << HSA_PACKET_HEADER_TYPE) |
                                    ((barrier ? 1 : 0) << HSA_PACKET_HEADER_BARRIER) |
                                    (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                                    (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
   __atomic_store_n(&slot->header, header, __ATOMIC_RELEASE);
   hsa_signal_store_screlease(q->doorbell_signal, hsa_signal_value_t(idx));
+}
+
+void submit(Agent& a, const hsa_ext_amd_aql_pm4_packet_t& pkt, bool barrier = true) {
+  submit_on(a, a.queue, a.sig, pkt, barrier);
 }
 
 // Submits `pkt`, waits (interrupt-driven) up to 1 s; returns the midpoint of submit and
@@ -459,6 +473,7 @@ bool setup_agent(Agent& a, std::string* why) {
     return false;
   }
   a.out_size = out_size;
+  a.cmd_size = cmd_size;
   if (hsa_queue_create(a.gpu, 64, HSA_QUEUE_TYPE_MULTI, queue_error_cb, &a, UINT32_MAX, UINT32_MAX, &a.queue) !=
       HSA_STATUS_SUCCESS) {
     *why = "hsa_queue_create failed";
@@ -498,7 +513,9 @@ bool usable(const Agent* a) { return a && a->ready && !a->broken.load(); }
 bool collect(Agent& a, Accum* acc) {
   *acc = Accum{};
   acc->a = &a;
-  const bool ok = g_aql.hsa_ven_amd_aqlprofile_iterate_data(&a.profile, on_data, acc) == HSA_STATUS_SUCCESS;
+  // after a rescue the reads land in the rescue profile's output buffer
+  auto* prof = a.rescued.load() ? &a.rprofile : &a.profile;
+  const bool ok = g_aql.hsa_ven_amd_aqlprofile_iterate_data(prof, on_data, acc) == HSA_STATUS_SUCCESS;
   // per-XCC only when every sample of both counters has an XCC, both agree on the XCC count
   // and every XCC has as many SQ samples (SEs) as the first
   bool even = acc->xm_n > 0;
@@ -562,6 +579,55 @@ void window_all() {
   }
 }
 
+// Read rescue.  The sentinel shares the counters' queue (one ~173 MiB context-save area per
+// GPU instead of two), and the packet processor does not look past a kernel dispatch whose
+// waves cannot be placed: a workload holding every wave slot for seconds (measured: 8
+// blocks x 4 waves per CU issuing MFMAs, tools/mfma_calibration.py --starve) holds every
+// read behind the sentinel run, and the counters go stale exactly when the GPU is busiest.
+// After kRescueRounds stuck rounds, reads move for good to a second queue of their own: the
+// counters are chip state, so a read packet from any queue copies the same running totals
+// (cumulative mode only: there a read changes nothing, and the abandoned read on the first
+// queue, which still runs once the sentinel does, is harmless).  The second queue and its
+// context-save area exist only on GPUs that needed them.  GPUEXP_PMC_READ_RESCUE=0 disables.
+constexpr int kRescueRounds = 3;
+
+bool rescue_enabled() {
+  const char* e = std::getenv("GPUEXP_PMC_READ_RESCUE");
+  return !(e && e[0] == '0');
+}
+
+bool rescue_reads(Agent& a) {
+  a.rprofile = a.profile;
+  a.rcmd_buf = sys_alloc(a.cmd_size, a.gpu);
+  a.rout_buf = sys_alloc(a.out_size, a.gpu);
+  bool ok = a.rcmd_buf && a.rout_buf;
+  if (ok) {
+    a.rprofile.command_buffer = {a.rcmd_buf, a.cmd_size};
+    a.rprofile.output_buffer = {a.rout_buf, a.out_size};
+    // the start program is generated (the read program is built after it) but never run:
+    // it would re-program and reset the running counters
+    ok = g_aql.hsa_ven_amd_aqlprofile_start(&a.rprofile, &a.rstart_pkt) == HSA_STATUS_SUCCESS &&
+         g_aql.hsa_ven_amd_aqlprofile_read(&a.rprofile, &a.rread_pkt) == HSA_STATUS_SUCCESS;
+  }
+  ok = ok && hsa_queue_create(a.gpu, 64, HSA_QUEUE_TYPE_MULTI, queue_error_cb, &a, UINT32_MAX, UINT32_MAX, &a.rq) ==
+                 HSA_STATUS_SUCCESS;
+  if (ok) hsa_amd_queue_set_priority(a.rq, HSA_AMD_QUEUE_PRIORITY_LOW);
+  ok = ok && hsa_signal_create(1, 0, nullptr, &a.rsig) == HSA_STATUS_SUCCESS;
+  if (!ok) {
+    if (a.rq) hsa_queue_destroy(a.rq);
+    if (a.rcmd_buf) hsa_amd_memory_pool_free(a.rcmd_buf);
+    if (a.rout_buf) hsa_amd_memory_pool_free(a.rout_buf);
+    a.rq = nullptr;
+    a.rcmd_buf = a.rout_buf = nullptr;
+    return false;
+  }
+  a.rescued = true;
+  a.orphan = true;
+  std::fprintf(stderr, "[aqlpmc] gpu %s: counter reads stuck behind a sentinel run the workload leaves no wave "
+               "slot for; reads moved to a queue of their own\n", a.bdf.c_str());
+  return true;
+}
+
 // Continuous mode, one round: a read packet in flight on every GPU at once, then per GPU
 // the window since its previous read.  Counting itself never pauses (kStops: re-armed
 // right after the read, a gap of one PM4 packet).
@@ -572,7 +638,13 @@ void read_round() {
   const auto deadline = begin + std::chrono::milliseconds(std::min(1000, g_interval_ms));
   for (Agent* a : g_agents)
     if (usable(a) && !a->read_inflight) {
-      post_packet(*a, a->read_pkt, /*barrier=*/false);
+      if (a->rescued) {
+        hsa_signal_store_relaxed(a->rsig, 1);
+        a->t_submit = Clock::now();
+        submit_on(*a, a->rq, a->rsig, a->rread_pkt, /*barrier=*/false);
+      } else {
+        post_packet(*a, a->read_pkt, /*barrier=*/false);
+      }
       a->read_inflight = true;
       a->t_checked = a->t_submit;
     }
@@ -580,7 +652,7 @@ void read_round() {
   for (Agent* a : g_agents) {
     if (!usable(a) || !a->read_inflight) continue;
     const uint64_t w0 = own_cpu_ns();
-    const bool done = wait_signal(a->sig, deadline);
+    const bool done = wait_signal(a->rescued ? a->rsig : a->sig, deadline);
     const auto now = Clock::now();
     const uint64_t w1 = own_cpu_ns();
     cw += w1 - w0;
@@ -591,9 +663,14 @@ void read_round() {
     if (!done) {  // still queued: try again next round, the counters keep running
       a->t_checked = now;
       ++a->stalls;
+      // the first queue is stuck: the next round reads on a queue of its own
+      if (!a->rescued && g_read_mode == kCumulative && ++a->stuck_rounds >= kRescueRounds && rescue_enabled() &&
+          rescue_reads(*a))
+        a->read_inflight = false;
       continue;
     }
     a->read_inflight = false;
+    a->stuck_rounds = 0;
     // the read executed between the last time it was seen pending and now
     const auto t = a->t_checked + (now - a->t_checked) / 2;
     Accum acc;
@@ -715,8 +792,16 @@ void counting_loop() {
       }
       g_done_cv.notify_all();
     }
-    for (Agent* a : g_agents)
-      if (usable(a) && !a->read_inflight) run_packet(*a, a->stop_pkt);
+    for (Agent* a : g_agents) {
+      if (!usable(a) || a->read_inflight) continue;
+      if (a->rescued) {  // the first queue may still be stuck: stop from the rescue queue
+        hsa_signal_store_relaxed(a->rsig, 1);
+        submit_on(*a, a->rq, a->rsig, a->stop_pkt, true);
+        wait_signal(a->rsig, Clock::now() + std::chrono::seconds(1));
+      } else {
+        run_packet(*a, a->stop_pkt);
+      }
+    }
     return;
   }
   while (!g_quit.load()) {
@@ -733,12 +818,18 @@ void counting_loop() {
 void teardown_locked() {
   for (Agent* a : g_agents) {
     if (!a) continue;
+    // an abandoned read (rescue) that never ran may still write the first buffers
+    const bool orphan_pending = a->orphan && a->sig.handle && hsa_signal_load_scacquire(a->sig) >= 1;
     if (a->queue) hsa_queue_destroy(a->queue);
+    if (a->rq) hsa_queue_destroy(a->rq);
     if (a->sig.handle) hsa_signal_destroy(a->sig);
+    if (a->rsig.handle) hsa_signal_destroy(a->rsig);
     // A timed-out (or still queued) packet may still write the buffers: leak them.
     if (!a->broken && !a->read_inflight) {
-      if (a->cmd_buf) hsa_amd_memory_pool_free(a->cmd_buf);
-      if (a->out_buf) hsa_amd_memory_pool_free(a->out_buf);
+      if (!orphan_pending && a->cmd_buf) hsa_amd_memory_pool_free(a->cmd_buf);
+      if (!orphan_pending && a->out_buf) hsa_amd_memory_pool_free(a->out_buf);
+      if (a->rcmd_buf) hsa_amd_memory_pool_free(a->rcmd_buf);
+      if (a->rout_buf) hsa_amd_memory_pool_free(a->rout_buf);
     }
     delete a;
   }
@@ -1191,7 +1282,8 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_debug(int dev, c
                   ";samples=" + std::to_string(a.last_samples) + ";windows=" + std::to_string(a.m.windows) +
                   ";simd=" + std::to_string(a.m.simd) + ";cu=" + std::to_string(a.m.cu) +
                   ";mode=" + (g_continuous ? read_mode_name(g_read_mode) : "duty") + ";window_s=" + win +
-                  ";resets=" + std::to_string(a.resets.load()) + ";stalls=" + std::to_string(a.stalls.load()) + ";";
+                  ";resets=" + std::to_string(a.resets.load()) + ";stalls=" + std::to_string(a.stalls.load()) +
+                  ";rescued=" + (a.rescued.load() ? "1" : "0") + ";";
   if (const uint64_t r = g_rounds.load()) {
     char c[160];
     std::snprintf(c, sizeof(c), "rounds=%llu;round_cpu_us_post=%.2f;round_cpu_us_wait=%.2f;round_cpu_us_collect=%.2f;",

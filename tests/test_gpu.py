@@ -344,11 +344,18 @@ def test_xcc_busy_agrees_with_gfx_activity_under_gemm(native):
     child = subprocess.Popen([sys.executable, "-c",
                               "import sys; sys.path.insert(0, %r);"
                               "from kubernetes_gpu_exporter_amd.ops.gemm import gemm_burn;"
-                              "print(gemm_burn(0, 8192, 5.0, 4), flush=True)" % ROOT],
+                              "print(gemm_burn(0, 8192, 8.0, 4), flush=True)" % ROOT],
                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     e = amdsmi_engine(native, series_profile="full")
     try:
-        time.sleep(2.0)  # the burn is up (torch import + warm-up)
+        # the burn is up once its waves show in KFD (a fresh box's first imports take seconds)
+        t0 = time.time()
+        while time.time() - t0 < 60 and child.poll() is None:
+            e.tick()
+            if promtext.value(promtext.parse(e.snapshot_text()), "amd_gpu_cu_occupancy", gpu=0) > 0:
+                break
+            time.sleep(0.2)
+        time.sleep(0.5)
         gfx, xcc, cu = [], [], []
         for _ in range(15):
             e.tick()
@@ -365,8 +372,10 @@ def test_xcc_busy_agrees_with_gfx_activity_under_gemm(native):
     print(f"gfx_activity mean {mg:.1f} %, per-XCD busy mean {mx:.1f} % over {len(xcc)} samples; "
           f"occupied CUs {sorted(cu)}")
     # KFD cu_occupancy = resident waves / max waves per CU ("CU-equivalents"): the 256x256
-    # GEMM, 100 % busy on every XCD, reads 64 of 256 (measured)
-    assert 0 < sorted(cu)[len(cu) // 2] <= 256, cu
+    # GEMM, 100 % busy on every XCD, reads 64 of 256 (measured).  KFD's per-process read
+    # comes back 0 on some ticks of a continuously busy GPU (measured: 10 of 15 on one box,
+    # 0 of 15 on others), so only its range and that it saw the waves at all are asserted.
+    assert 0 < max(cu) <= 256 and min(cu) >= 0, cu
     assert xcc and all(0 <= v <= 100.5 for v in xcc), xcc
     assert mg > 60 and mx > 60, (mg, mx)
     assert abs(mg - mx) < 15, (mg, mx)
@@ -781,7 +790,8 @@ def test_xcc_mfma_busy_calibration():
     reads within 10 points of 90, every other XCD reads ~0, and the chip value is the mean
     of the eight (each XCD's busy cycles over its own elapsed cycles).  Then 2 s of MFMAs on
     every SIMD: amd_gpu_sentinel_pending_seconds grows while the sentinel's run waits behind
-    them and is 0 before and after."""
+    them and is 0 before and after, and the counter reads stuck behind that run move to a
+    queue of their own, so MFMA busy stays exported (~100 %) through the starvation."""
     import json
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mfma_calibration.py"), "--duties", "",
                         "--xcc-cases", "2,5", "--xcc-duty", "0.9", "--no-gated", "--starve", "2.0"],
@@ -806,6 +816,12 @@ def test_xcc_mfma_busy_calibration():
     assert st["pending_before"] == 0.0, st
     assert st["pending_max"] >= 0.8, st
     assert st["pending_after"] == 0.0, st
+    # the counter reads held behind that run moved to a queue of their own (read rescue):
+    # MFMA busy kept being exported through the starvation, near 100 %
+    assert st["rescued"] == "1", st
+    during = st["busy_during"][8:]  # from 0.8 s on (3 stuck rounds + the move)
+    assert sum(v is not None for v in during) >= 0.8 * len(during), st
+    assert min(v for v in during if v is not None) > 80.0, st
 
 
 def test_device_scope_pmc_calibration():

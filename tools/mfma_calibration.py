@@ -207,8 +207,14 @@ def main() -> int:
         # back to back for `starve` s (the grid's later blocks wait for the first ones): the
         # one-wave sentinel run cannot start, so amd_gpu_sentinel_pending_seconds must grow,
         # and drop to 0 once the kernel is gone
-        def pend():
-            return val(promtext.parse(e.snapshot_text()), "amd_gpu_sentinel_pending_seconds", gpu=0)
+        def pend(with_busy=False):
+            fams = promtext.parse(e.snapshot_text())
+            p = val(fams, "amd_gpu_sentinel_pending_seconds", gpu=0)
+            if with_busy:
+                ticks.append(val(fams, "gpuexp_ticks_total"))
+                return p, val(fams, "amd_gpu_mfma_busy_percent", gpu=0)
+            return p
+        ticks = []
         time.sleep(0.3)
         before = pend()
         cus = torch.cuda.get_device_properties(0).multi_processor_count
@@ -216,16 +222,20 @@ def main() -> int:
         t0 = time.perf_counter()
         mfma_duty(0, 1.0, args.starve, period_s=0.002, blocks=8 * cus)
         ev.record()
-        seen = []
+        seen, busy = [], []
         while not ev.query() and time.perf_counter() - t0 < 4 * args.starve + 5:
             time.sleep(0.1)
-            seen.append(pend())
+            p, b = pend(True)
+            seen.append(p)
+            busy.append(b)
         torch.cuda.synchronize()
         run_s = time.perf_counter() - t0
         time.sleep(0.5)
         kv = dict(x.split("=", 1) for x in raw().split(";") if "=" in x)
         res["cases"]["starve"] = {"seconds": args.starve, "kernel_s": run_s, "pending_before": before,
-                                  "pmc_read_stalls": int(kv.get("stalls", -1)),
+                                  "pmc_read_stalls": int(kv.get("stalls", -1)), "rescued": kv.get("rescued"),
+                                  "busy_during": [round(v, 2) if v is not None else None for v in busy],
+                                  "ticks_during": ticks,
                                   "pending_during": [round(v, 3) if v is not None else None for v in seen],
                                   "pending_max": max([v for v in seen if v is not None] or [0]),
                                   "pending_after": pend()}
