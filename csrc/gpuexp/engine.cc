@@ -269,6 +269,9 @@ void Engine::define_families() {
                          "pod's CU-occupancy share)", C, PO);
   f_pod_mfma_ = add("amd_pod_gpu_mfma_busy_percent",
                     "Mean MFMA busy of the pod's GPUs (amd_gpu_mfma_busy_percent of each GPU it owns)", G, PO);
+  f_pod_hbm_ = add("amd_pod_gpu_hbm_bandwidth_bytes_per_second",
+                   "HBM bandwidth of the pod's GPUs (sum of amd_gpu_hbm_bandwidth_bytes_per_second over the GPUs it owns)",
+                   G, PO);
   f_pod_power_ = add("amd_pod_gpu_power_watts", "Socket power of the pod's GPUs", G, PO);
   f_pod_energy_ = add("amd_pod_gpu_energy_joules_total",
                       "GPU energy used by the pod: its GPUs' hardware energy counters, and on a shared GPU the "
@@ -1106,8 +1109,8 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
     double xrd = 0, xwr = 0, power = 0, gfx = 0, gfx_share = 0;
     double energy_j = 0;  // this tick
     double xrd_b = 0, xwr_b = 0;  // xGMI bytes this tick (owned GPUs whole, shared GPUs by share)
-    double mfma = 0;
-    int gfx_n = 0, mfma_n = 0;
+    double mfma = 0, hbm = 0;
+    int gfx_n = 0, mfma_n = 0, hbm_n = 0;
     bool share_known = false;
   };
   std::map<std::pair<std::string, std::string>, PodAgg> pods;
@@ -1232,6 +1235,10 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
           pa.mfma += st.mfma_last;
           pa.mfma_n += 1;
         }
+        if (!std::isnan(st.cur.umc_activity) && st.cur.vram_max_bw_gbs > 0) {
+          pa.hbm += st.cur.umc_activity / 100.0 * st.cur.vram_max_bw_gbs * 1e9;  // as amd_gpu_hbm_bandwidth
+          pa.hbm_n += 1;
+        }
       }
     }
   }
@@ -1270,6 +1277,7 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
       cput(r.ref[6], f_pod_power_, pa.power, gen, L);
       if (pa.gfx_n) cput(r.ref[7], f_pod_gfx_, pa.gfx / pa.gfx_n, gen, L);
       if (pa.mfma_n) cput(r.ref[8], f_pod_mfma_, pa.mfma / pa.mfma_n, gen, L);
+      if (pa.hbm_n) cput(r.ref[9], f_pod_hbm_, pa.hbm, gen, L);
     }
   }
   for (auto it = pod_refs_.begin(); it != pod_refs_.end();)

@@ -213,7 +213,7 @@ class Engine {
     uint64_t gen = 0;
   };
   struct PodRefs {
-    SeriesRef ref[9];
+    SeriesRef ref[10];
     uint64_t gen = 0;
   };
   struct ProcAttr {
@@ -340,7 +340,7 @@ class Engine {
       f_hbm_wr_, f_sen_sclk_, f_sen_lat_, f_sen_xcc_, f_sen_runs_, f_xcc_clk_, f_sen_xlat_, f_sen_mem_, f_sen_xmem_, f_mfma_util_, f_xcc_mfma_, f_sen_pend_ = -1;
   int f_proc_vram_, f_proc_cu_, f_proc_sdma_, f_proc_evicted_, f_proc_gfx_;
   int f_legacy_mem_ = -1, f_legacy_perc_ = -1;
-  int f_pod_mfma_ = -1;
+  int f_pod_mfma_ = -1, f_pod_hbm_ = -1;
   int f_pod_vram_, f_pod_procs_, f_pod_gpus_, f_pod_xrd_, f_pod_xwr_, f_pod_power_, f_pod_gfx_, f_pod_gfx_share_,
       f_pod_energy_ = -1, f_pod_xrd_total_ = -1, f_pod_xwr_total_ = -1;
   int f_rccl_calls_, f_rccl_bytes_, f_rccl_comm_;

@@ -512,6 +512,23 @@ def test_sentinel_pending_seconds(mock_engine):
     assert promtext.value(parse(e), "amd_gpu_sentinel_pending_seconds", gpu=0) == 75.0
 
 
+def test_pod_hbm_bandwidth_is_the_sum_of_its_gpus(native, mock_engine):
+    """amd_pod_gpu_hbm_bandwidth_bytes_per_second: the HBM bandwidth of the GPUs a pod owns,
+    summed (the same PMFW-derived value as amd_gpu_hbm_bandwidth_bytes_per_second)."""
+    uid, cid = "00000000-0000-4000-8000-0000000000c2", "c2" * 32
+    e = mock_engine(3)
+    e.set_pods([{"uid": uid, "namespace": "ml", "name": "reader", "containers": {cid: "w"}}])
+    e.set_device_owners({"0000:10:00.0": {"namespace": "ml", "pod": "reader", "container": "w"},
+                         "0000:20:00.0": {"namespace": "ml", "pod": "reader", "container": "w"}})
+    e.tick(S)
+    e.tick(2 * S)
+    fams = promtext.parse(e.snapshot_text())
+    g = [promtext.value(fams, "amd_gpu_hbm_bandwidth_bytes_per_second", gpu=i) for i in range(3)]
+    assert g[0] > 0 and g[1] > 0
+    pod = promtext.value(fams, "amd_pod_gpu_hbm_bandwidth_bytes_per_second", pod="reader")
+    assert abs(pod - (g[0] + g[1])) <= 1e-6 * pod
+
+
 def test_pod_mfma_busy_is_the_mean_of_its_gpus(native, mock_engine):
     """amd_pod_gpu_mfma_busy_percent: the mean MFMA busy of the GPUs a pod owns (device
     plugin map), from the same per-tick counter window as amd_gpu_mfma_busy_percent."""
