@@ -273,6 +273,11 @@ void Engine::define_families() {
                    "HBM bandwidth of the pod's GPUs (sum of amd_gpu_hbm_bandwidth_bytes_per_second over the GPUs it owns)",
                    G, PO);
   f_pod_power_ = add("amd_pod_gpu_power_watts", "Socket power of the pod's GPUs", G, PO);
+  f_pod_alloc_s_ = add("amd_pod_gpu_allocated_seconds_total",
+                       "GPU-seconds the pod has held GPUs (device-plugin allocation; one GPU for one second = 1)", C, PO);
+  f_pod_busy_s_ = add("amd_pod_gpu_busy_seconds_total",
+                      "GPU-seconds the pod's GPUs were busy (per-XCD gfx_busy accumulators; a shared GPU's busy time "
+                      "split by the pod's CU-occupancy share)", C, PO);
   f_pod_energy_ = add("amd_pod_gpu_energy_joules_total",
                       "GPU energy used by the pod: its GPUs' hardware energy counters, and on a shared GPU the "
                       "pod's CU-occupancy share of it (chargeback)", C, PO);
@@ -737,6 +742,9 @@ void Engine::load_state() {
     } else if (f[0] == "pod_xgmi" && f.size() == 5) {
       pod_xgmi_[{f[1], f[2]}] = {std::strtod(f[3].c_str(), nullptr), std::strtod(f[4].c_str(), nullptr)};
       ++n;
+    } else if (f[0] == "pod_gpu_seconds" && f.size() == 5) {
+      pod_gpu_s_[{f[1], f[2]}] = {std::strtod(f[3].c_str(), nullptr), std::strtod(f[4].c_str(), nullptr)};
+      ++n;
     } else if (f[0] == "pod_event" && f.size() == 5) {
       const int ev = std::atoi(f[3].c_str());
       if (ev > 0 && ev < kKfdEventIds) pod_kfd_events_[std::make_tuple(f[1], f[2], ev)] = std::strtoull(f[4].c_str(), nullptr, 10);
@@ -766,6 +774,12 @@ bool Engine::save_state() {
     std::snprintf(rd, sizeof(rd), "%.17g", kv.second.first);
     std::snprintf(wr, sizeof(wr), "%.17g", kv.second.second);
     out += "pod_xgmi\t" + kv.first.first + "\t" + kv.first.second + "\t" + rd + "\t" + wr + "\n";
+  }
+  for (auto& kv : pod_gpu_s_) {
+    char al[64], bu[64];
+    std::snprintf(al, sizeof(al), "%.17g", kv.second.first);
+    std::snprintf(bu, sizeof(bu), "%.17g", kv.second.second);
+    out += "pod_gpu_seconds\t" + kv.first.first + "\t" + kv.first.second + "\t" + al + "\t" + bu + "\n";
   }
   for (auto& kv : pod_kfd_events_)
     out += "pod_event\t" + std::get<0>(kv.first) + "\t" + std::get<1>(kv.first) + "\t" +
@@ -1111,6 +1125,7 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
     double xrd_b = 0, xwr_b = 0;  // xGMI bytes this tick (owned GPUs whole, shared GPUs by share)
     double mfma = 0, hbm = 0;
     int gfx_n = 0, mfma_n = 0, hbm_n = 0;
+    double alloc_s = 0, busy_s = 0;  // GPU-seconds this tick
     bool share_known = false;
   };
   std::map<std::pair<std::string, std::string>, PodAgg> pods;
@@ -1145,6 +1160,21 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
     if (st.cur.ok && st.have_prev && st.cur.energy_valid && st.prev.energy_valid) {
       double dacc;
       if (acc_delta(st.cur.energy_acc, st.prev.energy_acc, &dacc)) energy_j = dacc * st.cur.energy_unit_j;
+    }
+    // this tick's length and the GPU's busy fraction over it (mean of the per-XCD busy from
+    // the gfx_busy accumulators; the PMFW's gfx activity where those are missing)
+    double tick_s = std::nan(""), busy_frac = std::nan("");
+    if (st.cur.ok && st.have_prev && st.cur.host_ns > st.prev.host_ns) {
+      tick_s = double(st.cur.host_ns - st.prev.host_ns) * 1e-9;
+      if (tick_s > 60.0) tick_s = std::nan("");  // a stalled sampler: do not credit the gap
+      double sum = 0;
+      int n = 0;
+      for (int x = 0; x < kMaxXcc; ++x)
+        if (!std::isnan(st.xcc_last[x])) {
+          sum += st.xcc_last[x];
+          ++n;
+        }
+      busy_frac = n ? sum / n / 100.0 : st.cur.gfx_activity / 100.0;
     }
     // xGMI bytes this GPU moved since the last tick, summed over links (hardware accumulators)
     double xgmi_rd_b = std::nan(""), xgmi_wr_b = std::nan("");
@@ -1201,6 +1231,7 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
           pa.xrd_b += xgmi_rd_b * f;
           pa.xwr_b += xgmi_wr_b * f;
         }
+        if (shared && !std::isnan(tick_s) && !std::isnan(busy_frac) && !std::isnan(f)) pa.busy_s += busy_frac * tick_s * f;
         if (!std::isnan(share)) {
           pa.gfx_share += share;
           pa.share_known = true;
@@ -1226,6 +1257,10 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
         if (!std::isnan(xgmi_rd_b)) {  // ...and so is its xGMI traffic
           pa.xrd_b += xgmi_rd_b;
           pa.xwr_b += xgmi_wr_b;
+        }
+        if (!std::isnan(tick_s)) {  // ...and its time, busy or not
+          pa.alloc_s += tick_s;
+          if (!std::isnan(busy_frac)) pa.busy_s += busy_frac * tick_s;
         }
         if (!std::isnan(st.cur.gfx_activity)) {
           pa.gfx += st.cur.gfx_activity;
@@ -1292,6 +1327,11 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
       x.first += kv.second.xrd_b;
       x.second += kv.second.xwr_b;
     }
+    if (kv.second.alloc_s > 0 || kv.second.busy_s > 0) {
+      auto& g = pod_gpu_s_[kv.first];
+      g.first += kv.second.alloc_s;
+      g.second += kv.second.busy_s;
+    }
   }
   {
     std::set<std::pair<std::string, std::string>> known;
@@ -1311,6 +1351,15 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
       }
       table_.put(f_pod_xrd_total_, {it->first.first, it->first.second}, it->second.first, gen);
       table_.put(f_pod_xwr_total_, {it->first.first, it->first.second}, it->second.second, gen);
+      ++it;
+    }
+    for (auto it = pod_gpu_s_.begin(); it != pod_gpu_s_.end();) {
+      if (pods_complete_ && !known.count(it->first)) {
+        it = pod_gpu_s_.erase(it);
+        continue;
+      }
+      table_.put(f_pod_alloc_s_, {it->first.first, it->first.second}, it->second.first, gen);
+      table_.put(f_pod_busy_s_, {it->first.first, it->first.second}, it->second.second, gen);
       ++it;
     }
   }

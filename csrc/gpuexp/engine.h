@@ -321,6 +321,8 @@ class Engine {
   std::map<std::pair<std::string, std::string>, double> pod_energy_j_;  // (ns, pod) -> joules so far
   // (ns, pod) -> xGMI bytes (read, write) so far
   std::map<std::pair<std::string, std::string>, std::pair<double, double>> pod_xgmi_;
+  // (ns, pod) -> (GPU-seconds allocated, GPU-seconds busy) so far (state file: pod_gpu_seconds)
+  std::map<std::pair<std::string, std::string>, std::pair<double, double>> pod_gpu_s_;
   SeriesRef self_refs_[21];
 
   // stats (guarded by stats_mu_)
@@ -342,7 +344,7 @@ class Engine {
   int f_legacy_mem_ = -1, f_legacy_perc_ = -1;
   int f_pod_mfma_ = -1, f_pod_hbm_ = -1;
   int f_pod_vram_, f_pod_procs_, f_pod_gpus_, f_pod_xrd_, f_pod_xwr_, f_pod_power_, f_pod_gfx_, f_pod_gfx_share_,
-      f_pod_energy_ = -1, f_pod_xrd_total_ = -1, f_pod_xwr_total_ = -1;
+      f_pod_energy_ = -1, f_pod_xrd_total_ = -1, f_pod_xwr_total_ = -1, f_pod_alloc_s_ = -1, f_pod_busy_s_ = -1;
   int f_rccl_calls_, f_rccl_bytes_, f_rccl_comm_;
   int f_kfd_ev_ = -1, f_pod_kfd_ev_ = -1, f_pages_ = -1, f_gtt_used_ = -1, f_gtt_total_ = -1;
   int f_board_ = -1, f_fw_ = -1, f_driver_ = -1;

@@ -379,27 +379,31 @@ def test_state_file_carries_pod_totals_across_restarts(native, mock_engine, tmp_
         en = {s[1]["pod"]: s[2] for s in promtext.samples(f, "amd_pod_gpu_energy_joules_total")}
         pev = {(s[1]["pod"], s[1]["event"]): s[2] for s in promtext.samples(f, "amd_pod_gpu_kfd_events_total")}
         dev = {s[1]["event"]: s[2] for s in promtext.samples(f, "amd_gpu_kfd_events_total")}
-        return en, pev, dev
+        busy = {s[1]["pod"]: s[2] for s in promtext.samples(f, "amd_pod_gpu_busy_seconds_total")}
+        return en, pev, dev, busy
 
     a = engine()
     a.set_pods(pods)
     a.inject_kfd_events(0, b"1 64:t\n2 0:1\n")
     for t in range(1, 5):
         a.tick(t * 1_000_000_000)
-    en1, pev1, dev1 = totals(a)
+    en1, pev1, dev1, busy1 = totals(a)
     assert en1["trainer"] == pytest.approx(3 * 400, rel=0.01) and pev1[("trainer", "vm_fault")] == 1
+    assert 0 < busy1["trainer"] <= 3.0  # the sole process of a shared GPU: all its busy time
     a.stop()  # final save
     assert open(state).read().startswith("gpuexp-state 1\n")
 
     b = engine()
     assert "restored" in b.source_status()
     b.tick(10_000_000_000)  # no pod list yet: restored totals are kept, not GC'd
-    en2, pev2, dev2 = totals(b)
+    en2, pev2, dev2, busy2 = totals(b)
     assert en2 == en1 and pev2 == pev1 and dev2["vm_fault"] == 1 and dev2["thermal_throttle"] == 1
+    assert busy2 == busy1
     b.set_pods(pods)
     for t in range(11, 14):
         b.tick(t * 1_000_000_000)
-    en3, _, _ = totals(b)
+    en3, _, _, busy3 = totals(b)
+    assert busy3["trainer"] > busy1["trainer"]
     assert en3["trainer"] == pytest.approx(en1["trainer"] + 3 * 400, rel=0.01)  # continues, no reset
     b.set_pods([])
     b.tick(14_000_000_000)
@@ -510,6 +514,29 @@ def test_sentinel_pending_seconds(mock_engine):
     e.mock_set_value(0, "sentinel_pending_s", 75.0)
     ticks(e, 1, t0=10 * S)
     assert promtext.value(parse(e), "amd_gpu_sentinel_pending_seconds", gpu=0) == 75.0
+
+
+def test_pod_gpu_seconds(native, mock_engine):
+    """amd_pod_gpu_allocated_seconds_total / amd_pod_gpu_busy_seconds_total: GPU-seconds a pod
+    held its GPUs, and how many of them they were busy (the mean per-XCD busy of each tick,
+    times the tick)."""
+    uid, cid = "00000000-0000-4000-8000-0000000000c3", "c3" * 32
+    e = mock_engine(2)
+    e.set_pods([{"uid": uid, "namespace": "ml", "name": "holder", "containers": {cid: "w"}}])
+    e.set_device_owners({"0000:10:00.0": {"namespace": "ml", "pod": "holder", "container": "w"},
+                         "0000:20:00.0": {"namespace": "ml", "pod": "holder", "container": "w"}})
+    busy = 0.0
+    for t in range(1, 6):  # 4 one-second ticks after the first
+        e.tick(t * 1_000_000_000)
+        fams = promtext.parse(e.snapshot_text())
+        if t > 1:
+            for g in ("0", "1"):
+                xs = [s[2] for s in promtext.samples(fams, "amd_gpu_xcc_busy_percent") if s[1]["gpu"] == g]
+                busy += sum(xs) / len(xs) / 100.0
+    alloc = promtext.value(fams, "amd_pod_gpu_allocated_seconds_total", pod="holder")
+    got = promtext.value(fams, "amd_pod_gpu_busy_seconds_total", pod="holder")
+    assert alloc == pytest.approx(8.0)  # 2 GPUs x 4 s
+    assert 0 < got <= alloc and got == pytest.approx(busy, rel=1e-6)
 
 
 def test_pod_hbm_bandwidth_is_the_sum_of_its_gpus(native, mock_engine):
