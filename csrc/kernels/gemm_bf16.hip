@@ -1,7 +1,8 @@
 // Synthetic "HIP-GEMM pod" workload: C[M,N] (bf16) = A[M,K] . B[N,K]^T (bf16 in, fp32 acc).
 // Two kernels: the 256x256 one below the 128x128 one is the default whenever the shape
-// allows (M,N multiples of 256).  MI355X, random operands, 8192^3: 256x256 1355 TFLOP/s,
-// 128x128 928, torch.matmul (hipBLASLt) 1434; 4096^3: 1301 vs 987 (profiles/r01/gemm.txt).
+// allows (M,N multiples of 256); its default form is the ping-pong variant 8: MI355X,
+// random operands, 8192^3 1459 TFLOP/s vs 1666 for torch.matmul (hipBLASLt) and 1361 for
+// the previous one-barrier-per-phase form (profiles/r03/gemm_variants.log).
 //
 // 128x128 kernel:
 // This is the load generator behind BASELINE configs 3-5 ("synthetic HIP-workload pods")
@@ -412,6 +413,195 @@ gemm_bf16_tn_256_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
     *reinterpret_cast<uint4*>(C + size_t(row_a + row) * size_t(N) + row_b + chunk * 8) = v;
   }
 }
+// ---------------------------------------------------------------------------------------
+// Ping-pong form of the 256x256 kernel (variant 8, the default): same tile, waves, LDS
+// image, snake-B read order and epilogue, but every phase is
+//   ds_reads of this phase's group -> stage ONE group (2 glds) -> counted vmcnt ->
+//   s_barrier -> lgkmcnt(0) -> setprio(1), 16 MFMA, setprio(0) -> s_barrier
+// and wave row 1 runs one barrier behind row 0, so on every SIMD one wave's MFMA cluster
+// runs while the other wave's reads and DMA issue run (cdna_hip_programming.md, "The 256²
+// 8-phase template").  With two barriers per phase a group is restaged >= 2 phases after
+// its last read and read >= 1 phase after the wait that retires it.  Numbering phases
+// g = 4t + p - 1, the group reads of K-tile t are
+//   Bf(t) at 4t-1 (read ahead into the idle B registers), A-M0 at 4t, Bs(t) at 4t+1,
+//   A-M1 at 4t+2        (Bf = B-N0 for even t, B-N1 for odd t; Bs the other half)
+// and one group is staged per phase:
+//   P1 A-M1(t+1),  P2 Bf(t+2),  P3 A-M0(t+2),  P4 Bs(t+2)
+// (its DMA issued before the phase's ds_reads) so every group is issued 2 phases after its last read in the same buffer, and 6 phases
+// before its first read: each phase waits for the group issued 5 phases earlier (vmcnt =
+// 2 x the groups issued since, 10 in steady state; pp_wait below), 1 phase before the read.
+// ---------------------------------------------------------------------------------------
+// s_waitcnt through the builtin, not inline asm, so the compiler's own wait tracking sees
+// it (gfx9 encoding: vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8]); otherwise it
+// re-waits lgkmcnt(0) for reads these waits already retired.
+constexpr int waitcnt_vm(int n) { return (n & 0xF) | (0x7 << 4) | (0xF << 8) | (((n >> 4) & 3) << 14); }
+constexpr int kWaitLgkm0 = 0xF | (0x7 << 4) | (0x3 << 14);
+
+template <int N>
+__device__ __forceinline__ void pp_vm() {
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(N));
+}
+
+__device__ __forceinline__ void pp_wait(int p, bool has1, bool has2) {
+  // groups issued in the 4 phases before this one and in this one (see the table above)
+  if (has2) { pp_vm<10>(); return; }
+  if (!has1) {
+    if (p == 1) pp_vm<2>(); else pp_vm<0>();
+    return;
+  }
+  switch (p) {
+    case 1: pp_vm<10>(); break;
+    case 2: pp_vm<8>(); break;
+    case 3: pp_vm<6>(); break;
+    default: pp_vm<4>(); break;
+  }
+}
+
+// barrier A of a phase: every wave's counted wait is behind it; this wave's reads retire
+__device__ __forceinline__ void pp_barrier_a() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// barrier B: the MFMA cluster is issued; the next phase's LDS traffic stays below it
+__device__ __forceinline__ void pp_barrier_b() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ void pp_mfma(f32x4 (&acc)[4][2], const bf16x8 (&af)[4][2], const bf16x8 (&bf)[4][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi][kk], bf[ni][kk], acc[mi][ni], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <int kGroupM>
+__global__ void __launch_bounds__(kThreads2, 1)
+gemm_bf16_tn_256pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
+                          int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 2 * kTile2];  // 128 KiB: [buf][A|B][256][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const int nbn = N / kBN2, nbm = M / kBM2;
+  const int nwg = nbm * nbn;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int in_group = kGroupM * nbn;
+  const int first_m = (wgid / in_group) * kGroupM;
+  const int gsize = nbm - first_m < kGroupM ? nbm - first_m : kGroupM;
+  const int bm = first_m + (wgid % in_group) % gsize;
+  const int bn = (wgid % in_group) / gsize;
+  const int row_a = bm * kBM2, row_b = bn * kBN2;
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / kBK;  // >= 2
+  bf16x8 af[4][2], b0[4][2], b1[4][2];
+  const int a_row = wr * 128, b_row = wc * 64;
+  // prologue: K-tile 0 whole, then K-tile 1's Bf, A-M0, Bs (the groups steady state stages
+  // at phases -3..-1); wait for tile 0, then row 1 falls one barrier behind
+  GEMM2_STAGE_B(0, 0); GEMM2_STAGE_A(0, 0); GEMM2_STAGE_B(1, 0); GEMM2_STAGE_A(1, 0);
+  GEMM2_STAGE_B(1, 1); GEMM2_STAGE_A(0, 1); GEMM2_STAGE_B(0, 1);
+  wait_vm<6>();
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  read_frags(smem + kTile2, b_row, lane, b0, 2);  // Bf(0) = B-N0 of tile 0, "phase -1"
+
+  // Each phase issues its DMA before its ds_reads (reads after the DMA need no wait; the
+  // other order makes the compiler drain the reads before the DMA).
+  auto tile = [&](int t, auto odd_tag) {
+    constexpr bool odd = decltype(odd_tag)::value;
+    const bool has1 = t + 1 < nk, has2 = t + 2 < nk;
+    const uint16_t* As = smem + (odd ? 2 * kTile2 : 0);
+    const uint16_t* Bs = As + kTile2;
+    const uint16_t* Bn = smem + (odd ? 0 : 2 * kTile2) + kTile2;  // K-tile t+1's B
+    // P1: stage A-M1(t+1); read A-M0; quadrant (M0, Bf)
+    if (has1) GEMM2_STAGE_A(1, t + 1);
+    read_frags(As, a_row, lane, af, 4);
+    pp_wait(1, has1, has2);
+    pp_barrier_a();
+    if constexpr (odd) pp_mfma(acc[0][1], af, b1); else pp_mfma(acc[0][0], af, b0);
+    pp_barrier_b();
+    // P2: stage Bf(t+2) (same half as Bf(t)); read Bs(t); quadrant (M0, Bs)
+    if (has2) { if constexpr (odd) GEMM2_STAGE_B(1, t + 2); else GEMM2_STAGE_B(0, t + 2); }
+    if constexpr (odd) read_frags(Bs, b_row, lane, b0, 2); else read_frags(Bs, b_row + 32, lane, b1, 2);
+    pp_wait(2, has1, has2);
+    pp_barrier_a();
+    if constexpr (odd) pp_mfma(acc[0][0], af, b0); else pp_mfma(acc[0][1], af, b1);
+    pp_barrier_b();
+    // P3: stage A-M0(t+2); read A-M1; quadrant (M1, Bs)
+    if (has2) GEMM2_STAGE_A(0, t + 2);
+    read_frags(As, a_row + 64, lane, af, 4);
+    pp_wait(3, has1, has2);
+    pp_barrier_a();
+    if constexpr (odd) pp_mfma(acc[1][0], af, b0); else pp_mfma(acc[1][1], af, b1);
+    pp_barrier_b();
+    // P4: stage Bs(t+2); read Bf(t+1) into the B registers this phase does not use; (M1, Bf)
+    if (has2) { if constexpr (odd) GEMM2_STAGE_B(0, t + 2); else GEMM2_STAGE_B(1, t + 2); }
+    if (has1) {
+      if constexpr (odd) read_frags(Bn, b_row, lane, b0, 2); else read_frags(Bn, b_row + 32, lane, b1, 2);
+    }
+    pp_wait(4, has1, has2);
+    pp_barrier_a();
+    if constexpr (odd) pp_mfma(acc[1][1], af, b1); else pp_mfma(acc[1][0], af, b0);
+    pp_barrier_b();
+  };
+  for (int t = 0; t < nk; t += 2) {
+    tile(t, std::false_type{});
+    if (t + 1 < nk) tile(t + 1, std::true_type{});
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // close the stagger: row 1's last MFMA cluster is issued
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // no DMA in flight, every wave's reads retired: the 128 KiB are free
+
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int row = wr * 128 + qm * 64 + mi * 16 + (lane >> 4) * 4 + j;
+            const int col = wc * 64 + qn * 32 + ni * 16 + (lane & 15);
+            __bf16 v = (__bf16)acc[qm][qn][mi][ni][j];
+            smem[row * kBN2 + col] = *reinterpret_cast<uint16_t*>(&v);
+          }
+  __syncthreads();
+#pragma unroll 4
+  for (int p = 0; p < (kBM2 * kBN2 / 8) / kThreads2; ++p) {
+    const int idx = p * kThreads2 + threadIdx.x;
+    const int row = idx >> 5, chunk = idx & 31;
+    const uint4 v = *reinterpret_cast<const uint4*>(smem + row * kBN2 + chunk * 8);
+    *reinterpret_cast<uint4*>(C + size_t(row_a + row) * size_t(N) + row_b + chunk * 8) = v;
+  }
+}
 #undef GEMM2_STAGE_A
 #undef GEMM2_STAGE_B
 
@@ -424,15 +614,25 @@ bool gemm256_shape_ok(int M, int N, int K) {
 }
 
 // variant: 0 = auto (256x256 kernel when the shape allows it), 1 = 128x128, 2 = 256x256
-// with row-major tile order per XCD, 3 / 4 = 256x256 with 4 / 8 row panels per group.
+// with row-major tile order per XCD, 3 / 4 = 256x256 with 4 / 8 row panels per group,
+// 5-7 priority / read-schedule forms, 8 = ping-pong phases (two barriers per phase).
 hipError_t launch_gemm_bf16_tn(const void* A, const void* B, void* C, int M, int N, int K, hipStream_t stream,
                                int variant) {
   if (!gemm_shape_ok(M, N, K)) return hipErrorInvalidValue;
   const bool big = variant >= 2 || (variant == 0 && gemm256_shape_ok(M, N, K));
   if (big) {
     if (!gemm256_shape_ok(M, N, K)) return hipErrorInvalidValue;
-    // auto (0) = 7: 8-row tile groups (1355 vs 1265 TFLOP/s row-major at 8192^3), per-cluster
-    // setprio (5 / 6 without it / static form: -5 %), balanced snake-B reads (+0.3-1 % over 4)
+    if (variant == 8) {
+      hipLaunchKernelGGL(gemm_bf16_tn_256pp_kernel<8>, dim3((M / kBM2) * (N / kBN2)), dim3(kThreads2), 0, stream,
+                         static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C),
+                         M, N, K);
+      return hipGetLastError();
+    }
+    // auto (0) = 8: ping-pong phases, 1405 vs 1275 TFLOP/s for 7 at 8192^3, 1329 vs 1156 at
+    // 4096^3 (profiles/r03/gemm_variants.log).  7: 8-row tile groups (1355 vs 1265 TFLOP/s
+    // row-major), per-cluster setprio (5 / 6 without it / static form: -5 %), balanced
+    // snake-B reads (+0.3-1 % over 4)
+    if (variant == 0) variant = 8;
     auto k = variant == 2   ? gemm_bf16_tn_256_kernel<1, 0>
              : variant == 3 ? gemm_bf16_tn_256_kernel<4, 0>
              : variant == 4 ? gemm_bf16_tn_256_kernel<8, 0>

@@ -656,7 +656,7 @@ def test_gemm_256_matches_128_bitwise_every_run(native, on_gpu, M, N, K):
     ref = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     s = torch.cuda.current_stream().cuda_stream
     kernels().gemm_bf16(a.data_ptr(), b.data_ptr(), ref.data_ptr(), M, N, K, s, 1)
-    for variant in (2, 3, 4, 5, 6, 7):  # tile orders, priority forms, snake-B read schedule
+    for variant in (2, 3, 4, 5, 6, 7, 8):  # tile orders, priority forms, snake-B reads, ping-pong
         for _ in range(4):
             c = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
             kernels().gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, s, variant)
