@@ -605,6 +605,209 @@ gemm_bf16_tn_256pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __rest
 #undef GEMM2_STAGE_A
 #undef GEMM2_STAGE_B
 
+// ---------------------------------------------------------------------------------------
+// 4-wave form of the 256x256 tile (variant 9): one wave per SIMD, each wave owns a 128x128
+// output block (8x8 MFMA tiles, 256 fp32 accumulators per lane, in AGPRs), so a K-tile
+// costs every wave (128 + 128) rows of LDS reads instead of 8 waves x (128 + 64): a third
+// fewer ds_reads per tile.  With no SIMD partner to ping-pong with, a wave hides its own
+// reads: a K-tile is two K=32 slices, and while one slice's 64 MFMAs run (row mi of the
+// 8x8 block = 8 MFMAs), the other slice's fragments are read into place: A row mi's new
+// fragment into the register row mi just finished with, the B fragments into a second B
+// set (A 32 + 2 x B 32 = 96 fragment VGPRs):
+//   slice 0 (A0, B0) || read A1 in place, B1      (tile t, k 32-63)
+//   lgkmcnt(0); vmcnt(0) [tile t+1 landed]; s_barrier [every wave is done with tile t]
+//   stage tile t+2 (16 glds) into tile t's buffer
+//   slice 1 (A1, B1) || read A0 in place, B0      (tile t+1, k 0-31)
+// One barrier per K-tile; tile t+2's DMA has one K-tile of MFMA work to land.
+// Same LDS image and swizzle as the kernels above; same K order, so bit-identical output.
+// Measured (profiles/r03/gemm_variants.log): 1246-1274 TFLOP/s at 8192^3 against 1436-1441
+// for the ping-pong variant 8 on the same boxes, with a third fewer LDS instructions, no
+// bank conflicts and 7x fewer LDS-wait cycles (profiles/r03/gemm_pmc_4wave.txt); spreading
+// the reads between MFMAs and spacing accumulator chains 8 MFMAs apart moved it < 2 %.
+// Kept as an A/B arm, not the default.  (The 16x16x32 form of this layout, 64 f32x4
+// accumulators, makes hipcc shuttle accumulators between AGPRs and VGPRs every K-tile.)
+// ---------------------------------------------------------------------------------------
+constexpr int kThreads4 = 256;
+
+// Stages one 256x64 operand K-tile: wave-instruction i covers rows [(i*4 + wave)*8, +8);
+// the per-lane source differs between instructions only by i*32 rows (swz does not depend
+// on i), so one address register pair serves all 8.
+__device__ __forceinline__ void stage_tile_w4(const uint16_t* __restrict__ lane_src, size_t row32, uint16_t* lds_tile,
+                                              int wave) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int rblk = i * 4 + wave;
+    __builtin_amdgcn_global_load_lds((gptr_t)(lane_src + size_t(i) * row32), (lds_ptr_t)(lds_tile + rblk * 8 * kBK),
+                                     16, 0, 0);
+  }
+}
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+template <int kGroupM>
+__global__ void __launch_bounds__(kThreads4, 1)
+gemm_bf16_tn_256w4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
+                          int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 2 * kTile2];  // 128 KiB: [buf][A|B][256][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int nbn = N / kBN2, nbm = M / kBM2;
+  const int nwg = nbm * nbn;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int in_group = kGroupM * nbn;
+  const int first_m = (wgid / in_group) * kGroupM;
+  const int gsize = nbm - first_m < kGroupM ? nbm - first_m : kGroupM;
+  const int bm = first_m + (wgid % in_group) % gsize;
+  const int bn = (wgid % in_group) / gsize;
+  const int row_a = bm * kBM2, row_b = bn * kBN2;
+
+  // 128x128 per wave as 4x4 tiles of v_mfma_f32_32x32x16_bf16: 16 accumulators of 16 fp32
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int nk = K / kBK;  // >= 2
+  const int srow = wave * 8 + (lane >> 3);
+  const int schunk = swz(srow, lane & 7);
+  const uint16_t* a_src = A + size_t(row_a + srow) * size_t(K) + schunk * 8;
+  const uint16_t* b_src = B + size_t(row_b + srow) * size_t(K) + schunk * 8;
+  const size_t row32 = size_t(32) * size_t(K);
+  // 32x32x16 operand fragment: lane l holds row l%32, K elements (l/32)*8..+8 of a 16-deep
+  // step; fragment (tile i, step k16) of slice kk reads chunk kk*4 + k16*2 + l/32 of row
+  // base + i*32 + l%32, and the swizzle ((row>>1)&7) depends only on l%32: one offset per
+  // (operand, kk, k16), tiles as i*32 rows of immediate offset
+  const int l31 = lane & 31;
+  const int rsw = (l31 >> 1) & 7;
+  int a_off[2][2], b_off[2][2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int k16 = 0; k16 < 2; ++k16) {
+      const int c = ((kk * 4 + k16 * 2 + (lane >> 5)) ^ rsw) * 8;
+      a_off[kk][k16] = (wm * 128 + l31) * kBK + c;
+      b_off[kk][k16] = kTile2 + (wn * 128 + l31) * kBK + c;
+    }
+
+  bf16x8 a[4][2], b0[4][2], b1[4][2];
+  stage_tile_w4(a_src, row32, smem, wave);
+  stage_tile_w4(b_src, row32, smem + kTile2, wave);
+  stage_tile_w4(a_src + kBK, row32, smem + 2 * kTile2, wave);
+  stage_tile_w4(b_src + kBK, row32, smem + 3 * kTile2, wave);
+  pp_vm<16>();  // K-tile 0 landed (tile 1's 16 loads may be in flight)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int k16 = 0; k16 < 2; ++k16) {
+      a[i][k16] = *reinterpret_cast<const bf16x8*>(smem + a_off[0][k16] + i * 32 * kBK);
+      b0[i][k16] = *reinterpret_cast<const bf16x8*>(smem + b_off[0][k16] + i * 32 * kBK);
+    }
+
+  // two rows of a slice (16 MFMAs): both rows' first 16-deep step, then both rows' second,
+  // so the two MFMAs that chain through one accumulator are 8 MFMAs apart
+  auto rows = [&](int m0, const bf16x8 (&bb)[4][2]) {
+#pragma unroll
+    for (int k16 = 0; k16 < 2; ++k16)
+#pragma unroll
+      for (int m = m0; m < m0 + 2; ++m)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          acc[m][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m][k16], bb[ni][k16], acc[m][ni], 0, 0, 0);
+  };
+  // one fragment (both 16-deep steps of a slice) of B tile n / A tile m: 2 ds_read_b128
+  auto rb = [&](const uint16_t* buf, int kk, int n, bf16x8 (&bb)[4][2]) {
+#pragma unroll
+    for (int k16 = 0; k16 < 2; ++k16)
+      bb[n][k16] = *reinterpret_cast<const bf16x8*>(buf + b_off[kk][k16] + n * 32 * kBK);
+  };
+  auto ra = [&](const uint16_t* buf, int kk, int m) {
+#pragma unroll
+    for (int k16 = 0; k16 < 2; ++k16)
+      a[m][k16] = *reinterpret_cast<const bf16x8*>(buf + a_off[kk][k16] + m * 32 * kBK);
+  };
+  // Per slice, the next slice's B fragments are read first (every row of the next slice
+  // needs all of them) and its A fragments after, each into rows already finished (A rows
+  // 2-3 only once their MFMAs are issued), spread between the MFMAs (bunched, the 4 waves'
+  // reads fill the LDS queue together and stall MFMA issue).  The barrier sits after rows
+  // 0-1 of slice 1: by then every read of tile t has long been issued.
+#define W4_SPREAD(per, n)                                 \
+  for (int i_ = 0; i_ < (n); ++i_) {                      \
+    __builtin_amdgcn_sched_group_barrier(0x008, per, 0);  \
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);    \
+  }
+  for (int t = 0; t < nk; ++t) {
+    const uint16_t* cur = smem + (t & 1) * 2 * kTile2;
+    const uint16_t* nxt = smem + ((t + 1) & 1) * 2 * kTile2;
+    // slice 0: (a = k 0-31, b0); read k 32-63 of tile t: b1, then a
+    rows(0, b0);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) rb(cur, 1, n, b1);
+    W4_SPREAD(2, 8)
+    rows(2, b0); ra(cur, 1, 0); ra(cur, 1, 1); ra(cur, 1, 2); ra(cur, 1, 3);
+    W4_SPREAD(4, 4)
+    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+    // slice 1: (a = k 32-63, b1)
+    rows(0, b1);
+    __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // this wave is done reading tile t
+    pp_vm<0>();                              // tile t+1 landed (the only DMA in flight)
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 2 < nk) {
+      uint16_t* dst = smem + (t & 1) * 2 * kTile2;
+      stage_tile_w4(a_src + (t + 2) * kBK, row32, dst, wave);
+      stage_tile_w4(b_src + (t + 2) * kBK, row32, dst + kTile2, wave);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // read k 0-31 of tile t+1 (after the last tile: the other buffer's stale rows, in
+    // bounds and unused)
+    rows(2, b1);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) rb(nxt, 0, n, b0);
+    ra(nxt, 0, 0); ra(nxt, 0, 1);
+    W4_SPREAD(1, 12)
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    ra(nxt, 0, 2); ra(nxt, 0, 3);
+    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+  }
+#undef W4_SPREAD
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave's reads retired, no DMA in flight: the 128 KiB are free
+
+  // C/D map of 32x32x16: col = lane%32, row = (e/4)*8 + (lane/32)*4 + e%4
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = wm * 128 + mi * 32 + (e >> 2) * 8 + (lane >> 5) * 4 + (e & 3);
+        const int col = wn * 128 + ni * 32 + l31;
+        __bf16 v = (__bf16)acc[mi][ni][e];
+        smem[row * kBN2 + col] = *reinterpret_cast<uint16_t*>(&v);
+      }
+  __syncthreads();
+#pragma unroll 4
+  for (int p = 0; p < (kBM2 * kBN2 / 8) / kThreads4; ++p) {  // 32 passes of 256 x 16 B
+    const int idx = p * kThreads4 + threadIdx.x;
+    const int row = idx >> 5, chunk = idx & 31;
+    const uint4 v = *reinterpret_cast<const uint4*>(smem + row * kBN2 + chunk * 8);
+    *reinterpret_cast<uint4*>(C + size_t(row_a + row) * size_t(N) + row_b + chunk * 8) = v;
+  }
+}
+
 bool gemm_shape_ok(int M, int N, int K) {
   return M > 0 && N > 0 && K > 0 && M % kBM == 0 && N % kBN == 0 && K % kBK == 0;
 }
@@ -615,13 +818,20 @@ bool gemm256_shape_ok(int M, int N, int K) {
 
 // variant: 0 = auto (256x256 kernel when the shape allows it), 1 = 128x128, 2 = 256x256
 // with row-major tile order per XCD, 3 / 4 = 256x256 with 4 / 8 row panels per group,
-// 5-7 priority / read-schedule forms, 8 = ping-pong phases (two barriers per phase).
+// 5-7 priority / read-schedule forms, 8 = ping-pong phases (two barriers per phase),
+// 9 = 4 waves of 128x128.
 hipError_t launch_gemm_bf16_tn(const void* A, const void* B, void* C, int M, int N, int K, hipStream_t stream,
                                int variant) {
   if (!gemm_shape_ok(M, N, K)) return hipErrorInvalidValue;
   const bool big = variant >= 2 || (variant == 0 && gemm256_shape_ok(M, N, K));
   if (big) {
     if (!gemm256_shape_ok(M, N, K)) return hipErrorInvalidValue;
+    if (variant == 9) {
+      hipLaunchKernelGGL(gemm_bf16_tn_256w4_kernel<8>, dim3((M / kBM2) * (N / kBN2)), dim3(kThreads4), 0, stream,
+                         static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C),
+                         M, N, K);
+      return hipGetLastError();
+    }
     if (variant == 8) {
       hipLaunchKernelGGL(gemm_bf16_tn_256pp_kernel<8>, dim3((M / kBM2) * (N / kBN2)), dim3(kThreads2), 0, stream,
                          static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C),

@@ -45,8 +45,8 @@ PYBIND11_MODULE(_gpuexp_kernels, m) {
       throw std::invalid_argument("gemm_bf16 needs M%128==0, N%128==0, K%64==0");
     if (variant >= 2 && !gpuexp::gemm256_shape_ok(M, N, K))
       throw std::invalid_argument("the 256x256 kernel needs M%256==0, N%256==0, K%64==0, K>=128");
-    if (variant < 0 || variant > 8)
-      throw std::invalid_argument("variant is 0 (auto), 1 (128x128), 2-8 (256x256 tile orders / priority / read schedules / ping-pong)");
+    if (variant < 0 || variant > 9)
+      throw std::invalid_argument("variant is 0 (auto), 1 (128x128), 2-9 (256x256 tile orders / priority / read schedules / ping-pong / 4 waves)");
     if (!a || !b || !c) throw std::invalid_argument("null pointer");
     check(gpuexp::launch_gemm_bf16_tn(reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b),
                                       reinterpret_cast<void*>(c), M, N, K, reinterpret_cast<hipStream_t>(stream),

@@ -664,6 +664,43 @@ def test_gemm_256_matches_128_bitwise_every_run(native, on_gpu, M, N, K):
             assert torch.equal(c, ref), (variant, (c.float() - ref.float()).abs().max().item())
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (768, 512, 320), (2048, 2048, 2048), (4096, 4096, 1024)])
+def test_gemm_4wave_kernel_every_run(native, on_gpu, M, N, K):
+    """Variant 9 (4 waves of 128x128, v_mfma_f32_32x32x16_bf16): its MFMA shape sums K in
+    16-deep steps, so it is checked against the fp32 reference of the same op rather than
+    bit-for-bit against the 16x16x32 kernels; repeated runs must agree bit-for-bit (a tile
+    read before its DMA landed, or restaged while read, shows up as a mismatch)."""
+    import torch
+    torch.manual_seed(2)
+    a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    b = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+    s = torch.cuda.current_stream().cuda_stream
+    ref = a.float() @ b.float().T
+    first = None
+    for _ in range(4):
+        c = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+        kernels().gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, s, 9)
+        torch.cuda.synchronize()
+        err = (c.float() - ref).abs()
+        assert (err <= 1e-2 * ref.abs() + 1e-2 * K ** 0.5).all(), err.max().item()
+        if first is None:
+            first = c
+        else:
+            assert torch.equal(c, first)
+
+
+def test_gemm_4wave_identity_asymmetric(native, on_gpu):
+    """A = I with an asymmetric B through the 32x32x16 C layout and the LDS epilogue."""
+    import torch
+    M = N = K = 512
+    a = torch.eye(M, K, device="cuda", dtype=torch.bfloat16)
+    b = (torch.arange(N * K, device="cuda", dtype=torch.float32).reshape(N, K) % 97).to(torch.bfloat16)
+    c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    kernels().gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, 0, 9)
+    torch.cuda.synchronize()
+    assert torch.equal(c, b.T.contiguous())
+
+
 def test_gemm_rejects_bad_shapes(native):
     with pytest.raises(ValueError):
         kernels().gemm_bf16(1, 1, 1, 100, 128, 64, 0)

@@ -41,12 +41,22 @@ def main() -> int:
                 c.fill_(float("nan"))
                 k.gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), n, n, n, s, v)
                 torch.cuda.synchronize()
-                if not torch.equal(c, ref):
+                same = torch.equal(c, ref)
+                if rep == 0:
+                    first = c.clone()
+                elif not torch.equal(c, first):
+                    print(f"RUN-TO-RUN MISMATCH n={n} variant={v} rep={rep}", flush=True)
+                    return 1
+                if not same and v != 9:  # 9 sums K in 16-deep MFMA steps: not bitwise
                     print(f"MISMATCH n={n} variant={v} rep={rep}: max diff "
                           f"{(c.float() - ref.float()).abs().max().item()}", flush=True)
                     return 1
             err = ((c[:512].float() - ref32).abs() / (ref32.abs() + 1.0)).max().item()
-            print(f"n={n} variant={v}: bitwise == 128x128 kernel, max rel err vs fp32 {err:.2e}", flush=True)
+            if err > 2e-2:
+                print(f"n={n} variant={v}: max rel err vs fp32 {err:.2e} TOO LARGE", flush=True)
+                return 1
+            print(f"n={n} variant={v}: {'bitwise == 128x128 kernel, ' if same else ''}"
+                  f"max rel err vs fp32 {err:.2e}", flush=True)
 
         def run(fn):
             for _ in range(10):
