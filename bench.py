@@ -772,7 +772,9 @@ def main() -> int:
                        "global_batch": n_gpus, "seq_len": 0, "parallelism": f"dp{n_gpus}",
                        "scrape_hz": args.scrape_hz, "sample_hz": args.sample_hz, "backend": backend,
                        "series_profile": args.series_profile, "gzip": args.gzip, "protobuf": args.proto,
-                       "gemm": f"{G}^3 x {iters}/step", "allreduce_mb": args.allreduce_mb if dist is not None else 0},
+                       "gemm": f"{G}^3 x {iters}/step",
+                       "gemm_kernel_variant": kern.gemm_variant(G, G, G, 0) if kern is not None else None,
+                       "allreduce_mb": args.allreduce_mb if dist is not None else 0},
             "p50_scrape_us": round(statistics.median(lat), 2) if lat else None,
             # a p99 needs >= 100 samples; below that only the max of the timed scrapes and
             # the server-side histogram quantiles over every scrape of the run are given

@@ -820,12 +820,24 @@ bool gemm256_shape_ok(int M, int N, int K) {
 // with row-major tile order per XCD, 3 / 4 = 256x256 with 4 / 8 row panels per group,
 // 5-7 priority / read-schedule forms, 8 = ping-pong phases (two barriers per phase),
 // 9 = 4 waves of 128x128.
+// The kernel a launch with `variant` runs (0 = auto), or -1 if the shape does not fit it.
+// auto = 8 (256x256 ping-pong) when M%256 == N%256 == 0 and K >= 128, else 1 (128x128):
+// 8 runs at 1436-1459 vs 1361 TFLOP/s for 7 at 8192^3 (1319-1365 vs 1190 at 4096^3;
+// profiles/r03/gemm_variants.log).  7: 8-row tile groups (1355 vs 1265 TFLOP/s row-major),
+// per-cluster setprio (5 / 6 without it / static form: -5 %), balanced snake-B reads
+// (+0.3-1 % over 4).  9: 4 waves of 128x128 (1246-1274).
+int resolve_gemm_variant(int M, int N, int K, int variant) {
+  if (!gemm_shape_ok(M, N, K) || variant < 0 || variant > 9) return -1;
+  if (variant == 0) return gemm256_shape_ok(M, N, K) ? 8 : 1;
+  if (variant >= 2 && !gemm256_shape_ok(M, N, K)) return -1;
+  return variant;
+}
+
 hipError_t launch_gemm_bf16_tn(const void* A, const void* B, void* C, int M, int N, int K, hipStream_t stream,
                                int variant) {
-  if (!gemm_shape_ok(M, N, K)) return hipErrorInvalidValue;
-  const bool big = variant >= 2 || (variant == 0 && gemm256_shape_ok(M, N, K));
-  if (big) {
-    if (!gemm256_shape_ok(M, N, K)) return hipErrorInvalidValue;
+  variant = resolve_gemm_variant(M, N, K, variant);
+  if (variant < 0) return hipErrorInvalidValue;
+  if (variant >= 2) {
     if (variant == 9) {
       hipLaunchKernelGGL(gemm_bf16_tn_256w4_kernel<8>, dim3((M / kBM2) * (N / kBN2)), dim3(kThreads4), 0, stream,
                          static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C),
@@ -838,11 +850,6 @@ hipError_t launch_gemm_bf16_tn(const void* A, const void* B, void* C, int M, int
                          M, N, K);
       return hipGetLastError();
     }
-    // auto (0) = 8: ping-pong phases, 1405 vs 1275 TFLOP/s for 7 at 8192^3, 1329 vs 1156 at
-    // 4096^3 (profiles/r03/gemm_variants.log).  7: 8-row tile groups (1355 vs 1265 TFLOP/s
-    // row-major), per-cluster setprio (5 / 6 without it / static form: -5 %), balanced
-    // snake-B reads (+0.3-1 % over 4)
-    if (variant == 0) variant = 8;
     auto k = variant == 2   ? gemm_bf16_tn_256_kernel<1, 0>
              : variant == 3 ? gemm_bf16_tn_256_kernel<4, 0>
              : variant == 4 ? gemm_bf16_tn_256_kernel<8, 0>

@@ -12,6 +12,7 @@ namespace py = pybind11;
 namespace gpuexp {
 bool gemm_shape_ok(int M, int N, int K);
 bool gemm256_shape_ok(int M, int N, int K);
+int resolve_gemm_variant(int M, int N, int K, int variant);
 hipError_t launch_gemm_bf16_tn(const void* A, const void* B, void* C, int M, int N, int K, hipStream_t stream,
                                int variant);
 hipError_t launch_fill_bf16(void* p, size_t n, uint32_t seed, hipStream_t stream);
@@ -40,6 +41,10 @@ PYBIND11_MODULE(_gpuexp_kernels, m) {
   });
   m.def("gemm_shape_ok", &gpuexp::gemm_shape_ok);
   m.def("gemm256_shape_ok", &gpuexp::gemm256_shape_ok);
+  m.def("gemm_variant", &gpuexp::resolve_gemm_variant, py::arg("M"), py::arg("N"), py::arg("K"),
+        py::arg("variant") = 0,
+        "The GEMM kernel variant a gemm_bf16 call with these arguments runs (0 = auto resolved), -1 if the shape "
+        "does not fit it.  Host-only: no GPU needed.");
   m.def("gemm_bf16", [](uintptr_t a, uintptr_t b, uintptr_t c, int M, int N, int K, uintptr_t stream, int variant) {
     if (!gpuexp::gemm_shape_ok(M, N, K))
       throw std::invalid_argument("gemm_bf16 needs M%128==0, N%128==0, K%64==0");
