@@ -1,7 +1,7 @@
 // Synthetic "HIP-GEMM pod" workload: C[M,N] (bf16) = A[M,K] . B[N,K]^T (bf16 in, fp32 acc).
 // Two kernels: the 256x256 one below the 128x128 one is the default whenever the shape
 // allows (M,N multiples of 256); its default form is the ping-pong variant 8: MI355X,
-// random operands, 8192^3 1459 TFLOP/s vs 1666 for torch.matmul (hipBLASLt) and 1361 for
+// random operands, 8192^3 1453-1459 TFLOP/s (89 % of torch.matmul / hipBLASLt) vs 1358-1361 for
 // the previous one-barrier-per-phase form (profiles/r03/gemm_variants.log).
 //
 // 128x128 kernel:
@@ -844,8 +844,8 @@ hipError_t launch_gemm_bf16_tn(const void* A, const void* B, void* C, int M, int
                          M, N, K);
       return hipGetLastError();
     }
-    if (variant == 8) {
-      hipLaunchKernelGGL(gemm_bf16_tn_256pp_kernel<8>, dim3((M / kBM2) * (N / kBN2)), dim3(kThreads2), 0, stream,
+    if (variant == 8) {  // 4-row tile groups: 1456 vs 1444 (8 rows), 1398 (16) at 8192^3, 1355 vs 1318 at 4096^3
+      hipLaunchKernelGGL(gemm_bf16_tn_256pp_kernel<4>, dim3((M / kBM2) * (N / kBN2)), dim3(kThreads2), 0, stream,
                          static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C),
                          M, N, K);
       return hipGetLastError();
