@@ -620,10 +620,11 @@ gemm_bf16_tn_256pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __rest
 //   slice 1 (A1, B1) || read A0 in place, B0      (tile t+1, k 0-31)
 // One barrier per K-tile; tile t+2's DMA has one K-tile of MFMA work to land.
 // Same LDS image and swizzle as the kernels above; same K order, so bit-identical output.
-// Measured (profiles/r03/gemm_variants.log): 1246-1274 TFLOP/s at 8192^3 against 1436-1441
+// Measured (profiles/r03/gemm_variants.log): 1246-1286 TFLOP/s at 8192^3 against 1434-1441
 // for the ping-pong variant 8 on the same boxes, with a third fewer LDS instructions, no
 // bank conflicts and 7x fewer LDS-wait cycles (profiles/r03/gemm_pmc_4wave.txt); spreading
-// the reads between MFMAs and spacing accumulator chains 8 MFMAs apart moved it < 2 %.
+// the reads and the DMA between MFMAs and spacing accumulator chains 8 MFMAs apart moved
+// it < 4 %.
 // Kept as an A/B arm, not the default.  (The 16x16x32 form of this layout, 64 f32x4
 // accumulators, makes hipcc shuttle accumulators between AGPRs and VGPRs every K-tile.)
 // ---------------------------------------------------------------------------------------
@@ -765,20 +766,30 @@ gemm_bf16_tn_256w4_kernel(const uint16_t* __restrict__ A, const uint16_t* __rest
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    if (t + 2 < nk) {
+    // Tile t+2's 16 DMA instructions go out one per MFMA of the last two rows (a burst of
+    // them stalls the wave at issue).  Past the end the last tile is restaged into a buffer
+    // nothing reads any more (in bounds, no branch in the loop).
+    {
       uint16_t* dst = smem + (t & 1) * 2 * kTile2;
-      stage_tile_w4(a_src + (t + 2) * kBK, row32, dst, wave);
-      stage_tile_w4(b_src + (t + 2) * kBK, row32, dst + kTile2, wave);
+      const int ts = t + 2 < nk ? t + 2 : nk - 1;
+      stage_tile_w4(a_src + ts * kBK, row32, dst, wave);
+      stage_tile_w4(b_src + ts * kBK, row32, dst + kTile2, wave);
     }
-    __builtin_amdgcn_sched_barrier(0);
     // read k 0-31 of tile t+1 (after the last tile: the other buffer's stale rows, in
     // bounds and unused)
     rows(2, b1);
 #pragma unroll
     for (int n = 0; n < 4; ++n) rb(nxt, 0, n, b0);
     ra(nxt, 0, 0); ra(nxt, 0, 1);
-    W4_SPREAD(1, 12)
-    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    for (int i_ = 0; i_ < 12; ++i_) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    for (int i_ = 0; i_ < 4; ++i_) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+    }
     ra(nxt, 0, 2); ra(nxt, 0, 3);
     __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
   }
