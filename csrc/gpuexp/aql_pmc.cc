@@ -78,6 +78,7 @@ const EventDef kGfx950[] = {
     {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_GRBM, 0, kGrbmCount},  {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 112, kDramRd32},
     {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 115, kDramWr32},  {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 113, kGmiRd32},
     {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 117, kGmiWr32},  {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 2, kSqCycles},
+    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 52, kMopsBf16},    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 56, kMopsF8},
 };
 
 struct Agent {
@@ -1336,7 +1337,7 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_calibrate(int de
     return -1;
   };
   if (!a || !a->ready || a->broken) return fail("no working PMC queue for this device");
-  if (kind < 0 || kind > 2 || launches < 1 || launches > 1000000) return fail("bad arguments");
+  if (kind < 0 || kind > 4 || launches < 1 || launches > 1000000) return fail("bad arguments");
   const std::string path = plugin_dir() + "/gpuexp_calib.hsaco";
   const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
   if (fd < 0) return fail("cannot open gpuexp_calib.hsaco");
@@ -1353,7 +1354,9 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_calibrate(int de
   }
   ::close(fd);
   KernelSym k;
-  ok = ok && lookup(exe, a->gpu, kind == 0 ? "gpuexp_calib_copy.kd" : "gpuexp_calib_lds.kd", &k) && k.kernarg <= 64;
+  // kinds: 0 stream copy, 1 / 2 LDS reads (conflict-free / 32-way), 3 / 4 fixed MFMA work (bf16 / fp8)
+  const char* sym = kind == 0 ? "gpuexp_calib_copy.kd" : kind <= 2 ? "gpuexp_calib_lds.kd" : "gpuexp_calib_mfma.kd";
+  ok = ok && lookup(exe, a->gpu, sym, &k) && k.kernarg <= 64;
   if (!ok) {
     if (have_exe) hsa_executable_destroy(exe);
     return fail("cannot load the calibration code object");
@@ -1363,7 +1366,8 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_calibrate(int de
   hsa_amd_memory_pool_t pool{};
   hsa_amd_agent_iterate_memory_pools(a->gpu, pick_uncached_pool, &pool);
   void* buf = nullptr;
-  const size_t bytes = kind == 0 ? 2 * kCopyBytes : kBlocks * sizeof(float);
+  constexpr uint32_t kMfmaIters = 4096;  // ~3 ms per launch on MI355X at the bf16 rate
+  const size_t bytes = kind == 0 ? 2 * kCopyBytes : kBlocks * (gpuexp::kProbeBlock / 64) * sizeof(float);
   char* ka = static_cast<char*>(sys_alloc(64, a->gpu));
   hsa_signal_t sig{};
   if (!pool.handle || hsa_amd_memory_pool_allocate(pool, bytes, 0, &buf) != HSA_STATUS_SUCCESS || !ka ||
@@ -1377,8 +1381,11 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_calibrate(int de
   if (kind == 0) {
     gpuexp::CalibCopyArgs args{buf, static_cast<char*>(buf) + kCopyBytes, kCopyBytes / 16, uint64_t(kBlocks)};
     std::memcpy(ka, &args, sizeof(args));
-  } else {
+  } else if (kind <= 2) {
     gpuexp::CalibLdsArgs args{static_cast<float*>(buf), 8192, kind == 2 ? 32 : 1};
+    std::memcpy(ka, &args, sizeof(args));
+  } else {
+    gpuexp::CalibMfmaCountArgs args{static_cast<float*>(buf), kMfmaIters, uint32_t(kind - 3)};
     std::memcpy(ka, &args, sizeof(args));
   }
   const auto t0 = Clock::now();
@@ -1404,7 +1411,11 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_calibrate(int de
   hsa_executable_destroy(exe);
   out[0] = secs;
   out[1] = double(kBlocks) * (gpuexp::kProbeBlock / 64);
-  out[2] = kind == 0 ? double(kCopyBytes) : 0.0;
+  // per launch: bytes copied (kind 0) or MFMA FLOPs issued (kinds 3, 4)
+  out[2] = kind == 0 ? double(kCopyBytes)
+           : kind >= 3 ? double(kBlocks) * (gpuexp::kProbeBlock / 64) * kMfmaIters * gpuexp::kMfmaCountChains *
+                             gpuexp::kMfma32x32x16Flops
+                       : 0.0;
   return 0;
 }
 

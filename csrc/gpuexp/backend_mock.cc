@@ -185,6 +185,9 @@ bool MockBackend::counters(const DeviceInfo& dev, double dt_s, CounterReading* o
   out->hbm_write_bps = get(s, "hbm_write_bps", 1e12 * busy / 100);
   out->remote_read_bps = get(s, "remote_read_bps", 0.0);
   out->remote_write_bps = get(s, "remote_write_bps", 0.0);
+  // a bf16 pod at the MFMA busy share of a 2.5 PFLOP/s dense peak unless scripted
+  out->mfma_bf16_flops = get(s, "mfma_bf16_flops", 2.5e15 * out->mfma_busy_pct / 100);
+  out->mfma_fp8_flops = get(s, "mfma_fp8_flops", 0.0);
   // every XCD equally busy unless scripted ("xcc_mfma_busy_pct" sets them all)
   out->nxcc = int(std::min<uint32_t>(dev.num_xcc, uint32_t(kMaxXcc)));
   for (int x = 0; x < out->nxcc; ++x) out->xcc_mfma_busy_pct[x] = get(s, "xcc_mfma_busy_pct", out->mfma_busy_pct);

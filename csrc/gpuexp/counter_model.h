@@ -5,6 +5,7 @@
 // One pass within the gfx950 per-block slot limits (MI355X_MICROARCH.md "rocprofv3 PMC
 // slots": SQ 8, TCC 4, GRBM 2):
 //   SQ   SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT
+//        SQ_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F8
 //   GRBM GRBM_GUI_ACTIVE GRBM_COUNT
 //   TCC  TCC_EA0_RDREQ_DRAM_32B TCC_EA0_WRREQ_WRITE_DRAM_32B TCC_EA0_RDREQ_GMI_32B
 //        TCC_EA0_WRREQ_WRITE_GMI_32B
@@ -40,6 +41,8 @@ enum Ctr {
   kGmiRd32,
   kGmiWr32,
   kSqCycles,
+  kMopsBf16,  // MFMA work in units of 512 FLOPs (counter_defs.yaml: MFMA FLOPs = MOPS x 512)
+  kMopsF8,
   kNumCtr
 };
 
@@ -49,7 +52,8 @@ inline const char* name(int c) {
                                         "GRBM_GUI_ACTIVE",          "GRBM_COUNT",
                                         "TCC_EA0_RDREQ_DRAM_32B",   "TCC_EA0_WRREQ_WRITE_DRAM_32B",
                                         "TCC_EA0_RDREQ_GMI_32B",    "TCC_EA0_WRREQ_WRITE_GMI_32B",
-                                        "SQ_CYCLES"};
+                                        "SQ_CYCLES",                "SQ_INSTS_VALU_MFMA_MOPS_BF16",
+                                        "SQ_INSTS_VALU_MFMA_MOPS_F8"};
   return kNames[c];
 }
 
@@ -58,7 +62,7 @@ inline bool use_max(int c) { return c == kGuiActive || c == kGrbmCount; }
 
 // Number of derived outputs (the CounterSource ABI: gpuexp_rp_sample fills this many
 // doubles; gpuexp::kCounterOutputs in sources.h).
-constexpr int kNumOut = 11;
+constexpr int kNumOut = 13;
 
 // Per-XCC MFMA busy (gpuexp_rp_sample_xcc): at most this many XCCs per GPU.
 constexpr int kMaxXcc = 16;
@@ -132,6 +136,8 @@ inline void derive(Derived& a, const double* d, const int* inst, double wall) {
   out[7] = d[kDramWr32] * 32.0 / wall;                                              // HBM write B/s
   out[8] = d[kGmiRd32] * 32.0 / wall;                                               // remote (GMI) read B/s
   out[9] = d[kGmiWr32] * 32.0 / wall;                                               // remote (GMI) write B/s
+  out[11] = d[kMopsBf16] * 512.0 / wall;                                            // bf16 MFMA FLOP/s
+  out[12] = d[kMopsF8] * 512.0 / wall;                                              // fp8 MFMA FLOP/s
   a.valid = true;
   a.windows += 1;
 }

@@ -168,6 +168,8 @@ struct CounterReading {
   double hbm_write_bps = kNaN;      // TCC_EA0_WRREQ_WRITE_DRAM_32B * 32 B / dt
   double remote_read_bps = kNaN;    // TCC_EA0_RDREQ_GMI_32B * 32 B / dt (memory behind GMI: peers)
   double remote_write_bps = kNaN;   // TCC_EA0_WRREQ_WRITE_GMI_32B * 32 B / dt
+  double mfma_bf16_flops = kNaN;    // SQ_INSTS_VALU_MFMA_MOPS_BF16 * 512 / dt
+  double mfma_fp8_flops = kNaN;     // SQ_INSTS_VALU_MFMA_MOPS_F8 * 512 / dt
   // mfma_busy_pct of each XCC (its SQ instances over its own GRBM_COUNT x its SIMDs);
   // nxcc = 0 when the counter source cannot attribute samples to XCCs
   int nxcc = 0;

@@ -199,6 +199,9 @@ void Engine::define_families() {
   f_mfma_util_ = add("amd_gpu_mfma_util_percent",
                      "MFMA utilisation while the GPU was active (rocprof MfmaUtil: SQ_VALU_MFMA_BUSY_CYCLES / "
                      "(GRBM_GUI_ACTIVE x SIMDs))", G, D);
+  f_mfma_flops_ = add("amd_gpu_mfma_flops_per_second",
+                      "Matrix-core work done, by operand type: FLOP/s over the last tick "
+                      "(SQ_INSTS_VALU_MFMA_MOPS_<type> x 512)", G, with(D, {"dtype"}));
   f_sq_busy_ = add("amd_gpu_sq_busy_percent", "Shader sequencer busy (SQ_BUSY_CYCLES)", G, D);
   f_gui_ = add("amd_gpu_gui_active_percent", "Graphics pipe active (GRBM_GUI_ACTIVE / GRBM_COUNT)", G, D);
   f_waves_ = add("amd_gpu_waves_per_second", "Waves dispatched per second (SQ_WAVES)", G, D);
@@ -269,6 +272,9 @@ void Engine::define_families() {
                          "pod's CU-occupancy share)", C, PO);
   f_pod_mfma_ = add("amd_pod_gpu_mfma_busy_percent",
                     "Mean MFMA busy of the pod's GPUs (amd_gpu_mfma_busy_percent of each GPU it owns)", G, PO);
+  f_pod_flops_ = add("amd_pod_gpu_mfma_flops_per_second",
+                     "MFMA FLOP/s of the pod's GPUs by operand type (sum of amd_gpu_mfma_flops_per_second over "
+                     "the GPUs it owns)", G, with(PO, {"dtype"}));
   f_pod_hbm_ = add("amd_pod_gpu_hbm_bandwidth_bytes_per_second",
                    "HBM bandwidth of the pod's GPUs (sum of amd_gpu_hbm_bandwidth_bytes_per_second over the GPUs it owns)",
                    G, PO);
@@ -1027,6 +1033,7 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
 
   // Optional sources: rocprofiler counters, sentinel (real or mock-simulated).
   st.mfma_last = kNaN;
+  st.flops_last[0] = st.flops_last[1] = kNaN;
   CounterReading cr;
   bool have_ctr = false;
   if (counters_) have_ctr = counters_->sample(i, dt_s, &cr) && cr.ok;
@@ -1056,6 +1063,11 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
       if (cfg_.series_profile == "full") {  // not part of the 64-series standard load
         dput(st, i, st.ctr[8], f_remote_rd_, {}, cr.remote_read_bps, gen);
         dput(st, i, st.ctr[9], f_remote_wr_, {}, cr.remote_write_bps, gen);
+        // SQ instruction counters: VMID-filtered like the wave counts, so device scope only
+        dput(st, i, st.mflops[0], f_mfma_flops_, {"bf16"}, cr.mfma_bf16_flops, gen);
+        dput(st, i, st.mflops[1], f_mfma_flops_, {"fp8"}, cr.mfma_fp8_flops, gen);
+        st.flops_last[0] = cr.mfma_bf16_flops;
+        st.flops_last[1] = cr.mfma_fp8_flops;
       }
     }
   }
@@ -1123,8 +1135,8 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
     double xrd = 0, xwr = 0, power = 0, gfx = 0, gfx_share = 0;
     double energy_j = 0;  // this tick
     double xrd_b = 0, xwr_b = 0;  // xGMI bytes this tick (owned GPUs whole, shared GPUs by share)
-    double mfma = 0, hbm = 0;
-    int gfx_n = 0, mfma_n = 0, hbm_n = 0;
+    double mfma = 0, hbm = 0, flops[2] = {0, 0};
+    int gfx_n = 0, mfma_n = 0, hbm_n = 0, flops_n = 0;
     double alloc_s = 0, busy_s = 0;  // GPU-seconds this tick
     bool share_known = false;
   };
@@ -1270,6 +1282,11 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
           pa.mfma += st.mfma_last;
           pa.mfma_n += 1;
         }
+        if (!std::isnan(st.flops_last[0]) && !std::isnan(st.flops_last[1])) {  // an owned GPU's work is the pod's
+          pa.flops[0] += st.flops_last[0];
+          pa.flops[1] += st.flops_last[1];
+          pa.flops_n += 1;
+        }
         if (!std::isnan(st.cur.umc_activity) && st.cur.vram_max_bw_gbs > 0) {
           pa.hbm += st.cur.umc_activity / 100.0 * st.cur.vram_max_bw_gbs * 1e9;  // as amd_gpu_hbm_bandwidth
           pa.hbm_n += 1;
@@ -1313,6 +1330,12 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
       if (pa.gfx_n) cput(r.ref[7], f_pod_gfx_, pa.gfx / pa.gfx_n, gen, L);
       if (pa.mfma_n) cput(r.ref[8], f_pod_mfma_, pa.mfma / pa.mfma_n, gen, L);
       if (pa.hbm_n) cput(r.ref[9], f_pod_hbm_, pa.hbm, gen, L);
+      if (pa.flops_n) {
+        static const char* kTypes[2] = {"bf16", "fp8"};
+        for (int k = 0; k < 2; ++k)
+          cput(r.ref[10 + k], f_pod_flops_, pa.flops[k], gen,
+               [&] { return std::vector<std::string>{kv.first.first, kv.first.second, kTypes[k]}; });
+      }
     }
   }
   for (auto it = pod_refs_.begin(); it != pod_refs_.end();)

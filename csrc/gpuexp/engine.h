@@ -191,6 +191,7 @@ class Engine {
     double thr_last[5] = {kNaN, kNaN, kNaN, kNaN, kNaN};
     double xcc_last[kMaxXcc] = {kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN};
     double mfma_last = kNaN;  // this tick's amd_gpu_mfma_busy_percent (NaN: no counter window)
+    double flops_last[2] = {kNaN, kNaN};  // this tick's bf16 / fp8 MFMA FLOP/s (NaN: not device-wide)
     DeviceOwner owner;
     std::string owner_key;  // ns/pod/container the refs were built for
     // cached series handles (re-upserted on owner change or GC)
@@ -198,7 +199,7 @@ class Engine {
         energy, temp[9], clk[3], xrd[kMaxXgmiLinks], xwr[kMaxXgmiLinks], xrd_rate, xwr_rate,
         links_up, pcie_bw, pcie_replay, pcie_speed, pcie_width, thr[5], nprocs, cu_occ, ctr[10],
         sen[4], ecc[3], aer[3], nak[2], recov, xgmi_w, xgmi_s, xclk[kMaxXcc], sen_xlat[kMaxXcc], sen_mem, sen_xmem[kMaxXcc],
-        kev[std::size(kKfdSubscribed)], pages[3], gtt_used, gtt_total, board, mfma_util, xmfma[kMaxXcc], sen_pend;
+        kev[std::size(kKfdSubscribed)], pages[3], gtt_used, gtt_total, board, mfma_util, xmfma[kMaxXcc], sen_pend, mflops[2];
     std::vector<SeriesRef> fw;  // amd_gpu_firmware_info, one per component
     uint64_t kfd_events[kKfdEventIds] = {};  // KFD SMI events seen on this GPU, by id
     uint64_t errors = 0;
@@ -213,7 +214,7 @@ class Engine {
     uint64_t gen = 0;
   };
   struct PodRefs {
-    SeriesRef ref[10];
+    SeriesRef ref[12];
     uint64_t gen = 0;
   };
   struct ProcAttr {
@@ -339,10 +340,10 @@ class Engine {
       f_power_cap_, f_energy_, f_temp_, f_clk_, f_xrd_, f_xwr_, f_xrd_rate_, f_xwr_rate_,
       f_links_up_, f_pcie_bw_, f_pcie_replay_, f_pcie_speed_, f_pcie_width_, f_thr_, f_nprocs_,
       f_cu_occ_, f_ecc_, f_aer_, f_pcie_nak_, f_pcie_recov_, f_xgmi_width_, f_xgmi_speed_, f_mfma_, f_sq_busy_, f_gui_, f_waves_, f_lds_, f_lds_conf_, f_hbm_rd_, f_remote_rd_, f_remote_wr_,
-      f_hbm_wr_, f_sen_sclk_, f_sen_lat_, f_sen_xcc_, f_sen_runs_, f_xcc_clk_, f_sen_xlat_, f_sen_mem_, f_sen_xmem_, f_mfma_util_, f_xcc_mfma_, f_sen_pend_ = -1;
+      f_hbm_wr_, f_sen_sclk_, f_sen_lat_, f_sen_xcc_, f_sen_runs_, f_xcc_clk_, f_sen_xlat_, f_sen_mem_, f_sen_xmem_, f_mfma_util_, f_xcc_mfma_, f_sen_pend_, f_mfma_flops_ = -1;
   int f_proc_vram_, f_proc_cu_, f_proc_sdma_, f_proc_evicted_, f_proc_gfx_;
   int f_legacy_mem_ = -1, f_legacy_perc_ = -1;
-  int f_pod_mfma_ = -1, f_pod_hbm_ = -1;
+  int f_pod_mfma_ = -1, f_pod_hbm_ = -1, f_pod_flops_ = -1;
   int f_pod_vram_, f_pod_procs_, f_pod_gpus_, f_pod_xrd_, f_pod_xwr_, f_pod_power_, f_pod_gfx_, f_pod_gfx_share_,
       f_pod_energy_ = -1, f_pod_xrd_total_ = -1, f_pod_xwr_total_ = -1, f_pod_alloc_s_ = -1, f_pod_busy_s_ = -1;
   int f_rccl_calls_, f_rccl_bytes_, f_rccl_comm_;

@@ -107,6 +107,8 @@ class PluginCounters : public CounterSource {
     out->hbm_write_bps = v[7];
     out->remote_read_bps = v[8];
     out->remote_write_bps = v[9];
+    out->mfma_bf16_flops = v[11];
+    out->mfma_fp8_flops = v[12];
     out->nxcc = sample_xcc_ ? std::max(0, sample_xcc_(dev, out->xcc_mfma_busy_pct, kMaxXcc)) : 0;
     return true;
   }

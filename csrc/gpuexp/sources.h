@@ -32,7 +32,7 @@ std::unique_ptr<SentinelSource> make_queue_sentinel(const std::string& counters_
 std::string default_rocprof_plugin();
 
 // Derived values a counter plugin's gpuexp_rp_sample fills, in CounterReading order.
-constexpr int kCounterOutputs = 11;
+constexpr int kCounterOutputs = 13;
 
 class CounterSource {
  public:

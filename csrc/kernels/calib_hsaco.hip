@@ -13,3 +13,7 @@ extern "C" __global__ void __launch_bounds__(gpuexp::kProbeBlock) gpuexp_calib_c
 extern "C" __global__ void __launch_bounds__(gpuexp::kProbeBlock) gpuexp_calib_lds(gpuexp::CalibLdsArgs a) {
   gpuexp::lds_probe_body(a.out, a.iters, a.stride);
 }
+
+extern "C" __global__ void __launch_bounds__(gpuexp::kProbeBlock) gpuexp_calib_mfma(gpuexp::CalibMfmaCountArgs a) {
+  gpuexp::mfma_count_body(a);
+}

@@ -37,4 +37,14 @@ struct CalibMfmaArgs {
 };
 constexpr int kMfmaPerCheck = 32;  // MFMAs between two clock reads (32 x 32 cycles)
 
+// Fixed MFMA work for the FLOP-counter calibration (mfma_count_body): every wave issues
+// exactly 4 x iters v_mfma_f32_32x32x16 of one operand type, 32768 FLOPs each.
+struct CalibMfmaCountArgs {
+  float* out;      // >= blocks floats (sink, keeps the MFMAs live)
+  uint32_t iters;
+  uint32_t type;   // 0 bf16 (v_mfma_f32_32x32x16_bf16), 1 fp8 (v_mfma_f32_32x32x16_fp8_fp8)
+};
+constexpr int kMfmaCountChains = 4;
+constexpr double kMfma32x32x16Flops = 2.0 * 32 * 32 * 16;
+
 }  // namespace gpuexp

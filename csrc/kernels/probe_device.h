@@ -125,4 +125,40 @@ __device__ inline void mfma_duty_body(const CalibMfmaArgs& a) {
   }
 }
 
+// Fixed MFMA work (CalibMfmaCountArgs): 4 independent accumulator chains, iters rounds,
+// operands built from the lane id; the sum of the accumulators is the sink.
+__device__ inline void mfma_count_body(const CalibMfmaCountArgs& a) {
+  const int lane = threadIdx.x & 63;
+  f32x16 acc[kMfmaCountChains];
+#pragma unroll
+  for (int c = 0; c < kMfmaCountChains; ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
+  if (a.type == 0) {
+    bf16x8 x, y;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      x[j] = __bf16(float((lane * 7 + j * 3) % 13) * 0.0625f - 0.375f);
+      y[j] = __bf16(float((lane * 5 + j * 11) % 17) * 0.03125f - 0.25f);
+    }
+    for (uint32_t i = 0; i < a.iters; ++i)
+#pragma unroll
+      for (int c = 0; c < kMfmaCountChains; ++c) acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, acc[c], 0, 0, 0);
+  } else {
+    // 8 OCP e4m3 bytes per lane: small values (exponent field 5-6) of either sign
+    const long x = long(0x3038303830383038ull ^ (uint64_t(lane & 7) << 8));
+    const long y = long(0x2c3428342c342834ull ^ (uint64_t(lane & 3) << 16));
+    for (uint32_t i = 0; i < a.iters; ++i)
+#pragma unroll
+      for (int c = 0; c < kMfmaCountChains; ++c)
+        acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(x, y, acc[c], 0, 0, 0);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < kMfmaCountChains; ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s += acc[c][r];
+  if (lane == 0) a.out[blockIdx.x * (kProbeBlock / 64) + (threadIdx.x >> 6)] = s;
+}
+
 }  // namespace gpuexp

@@ -250,14 +250,18 @@ def test_full_profile_adds_reliability_families(mock_engine):
     """`full` = the 64-series standard load + ECC / PCIe AER / NAK / recovery / xGMI link
     + per-XCD clocks, per-XCD sentinel dispatch latency and HBM latency (chip + 8 XCDs)
     + the 6 KFD SMI event counters + retired HBM pages by state + GTT used/total + board
-    identity and firmware versions + MFMA util + per-XCD MFMA busy."""
+    identity and firmware versions + MFMA util + per-XCD MFMA busy + MFMA FLOP/s by type."""
     e = mock_engine(2, http=False, enable_sentinel=True, enable_counters=True, series_profile="full")
     e.mock_set_value(1, "ecc_ue", 3)
     e.mock_set_value(1, "aer_cor", 7)
     ticks(e, 3)
     fams = parse(e)
-    # + board (1), firmware (4 in mock), MFMA util (1), per-XCD MFMA busy (8), sentinel pending (1)
-    assert dict(device_series_per_gpu(fams)) == {"0": 127, "1": 127}
+    # + board (1), firmware (4 in mock), MFMA util (1), per-XCD MFMA busy (8), sentinel pending (1),
+    # MFMA FLOP/s for bf16 and fp8 (2)
+    assert dict(device_series_per_gpu(fams)) == {"0": 129, "1": 129}
+    flops = {s[1]["dtype"]: s[2] for s in fams["amd_gpu_mfma_flops_per_second"].samples if s[1]["gpu"] == "0"}
+    busy = fams["amd_gpu_mfma_busy_percent"].samples[0][2]
+    assert flops == {"bf16": pytest.approx(2.5e15 * busy / 100), "fp8": 0.0}, flops
     lat = {s[1]["xcc"]: s[2] for s in fams["amd_gpu_sentinel_xcc_dispatch_latency_seconds"].samples
            if s[1]["gpu"] == "0"}
     assert sorted(lat) == [str(x) for x in range(8)] and min(lat.values()) == lat["0"]
@@ -572,3 +576,29 @@ def test_pod_mfma_busy_is_the_mean_of_its_gpus(native, mock_engine):
     fams = promtext.parse(e.snapshot_text())
     assert promtext.value(fams, "amd_gpu_mfma_busy_percent", gpu=0) == 80.0
     assert promtext.value(fams, "amd_pod_gpu_mfma_busy_percent", pod="trainer") == 60.0
+
+
+def test_mfma_flops_by_type_per_gpu_and_pod(native, mock_engine):
+    """amd_gpu_mfma_flops_per_second{dtype} (SQ_INSTS_VALU_MFMA_MOPS_<type> x 512, full
+    profile, device-scope counters only) and amd_pod_gpu_mfma_flops_per_second: the sum over
+    the GPUs a pod owns, per operand type."""
+    uid, cid = "00000000-0000-4000-8000-0000000000c2", "c2" * 32
+    e = mock_engine(3, enable_counters=True, series_profile="full")
+    e.set_pods([{"uid": uid, "namespace": "ml", "name": "trainer", "containers": {cid: "w"}}])
+    e.set_device_owners({"0000:10:00.0": {"namespace": "ml", "pod": "trainer", "container": "w"},
+                         "0000:20:00.0": {"namespace": "ml", "pod": "trainer", "container": "w"}})
+    e.mock_set_value(0, "mfma_bf16_flops", 1.2e15)
+    e.mock_set_value(1, "mfma_bf16_flops", 0.8e15)
+    e.mock_set_value(1, "mfma_fp8_flops", 2.0e15)
+    e.mock_set_value(2, "mfma_bf16_flops", 9e14)  # not the pod's
+    e.tick(S)
+    e.tick(2 * S)
+    fams = promtext.parse(e.snapshot_text())
+    assert promtext.value(fams, "amd_gpu_mfma_flops_per_second", gpu=1, dtype="fp8") == 2.0e15
+    assert promtext.value(fams, "amd_pod_gpu_mfma_flops_per_second", pod="trainer", dtype="bf16") == 2.0e15
+    assert promtext.value(fams, "amd_pod_gpu_mfma_flops_per_second", pod="trainer", dtype="fp8") == 2.0e15
+    # standard profile: the 64-series load without the per-type FLOP families
+    e2 = mock_engine(1, enable_counters=True, series_profile="standard")
+    e2.tick(S)
+    e2.tick(2 * S)
+    assert "amd_gpu_mfma_flops_per_second" not in promtext.parse(e2.snapshot_text())

@@ -863,8 +863,9 @@ def test_xcc_mfma_busy_calibration():
 
 def test_device_scope_pmc_calibration():
     """Device-scope PMC families against ground truth (tools/pmc_validate.py): HBM read and
-    write of a stream copy of known bytes, waves/s of known grids, and LDS bank conflicts
-    of a conflict-free vs a 32-way-conflicted read pattern.  The workloads run on the PMC
+    write of a stream copy of known bytes, waves/s of known grids, LDS bank conflicts of a
+    conflict-free vs a 32-way-conflicted read pattern, and MFMA FLOP/s by operand type of a
+    known number of bf16 / fp8 MFMAs.  The workloads run on the PMC
     queue itself (the only queue an unprivileged process's SQ/TCC counters see)."""
     import json
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_validate.py")], capture_output=True,
@@ -898,6 +899,15 @@ def test_device_scope_pmc_calibration():
     assert clean["amd_gpu_lds_bank_conflict_percent"] < 10, clean
     # 32-way: 31 of every 32 LDS cycles are conflict cycles (96.875 %)
     assert abs(conf["amd_gpu_lds_bank_conflict_percent"] - 100 * 31 / 32) < 2, conf
+    # MFMA FLOP/s by operand type against a fixed count of 32x32x16 MFMAs per wave
+    # (measured 1.0004x bf16, 0.9997x fp8: profiles/r03/mfma_flops_calibration.txt)
+    for name, dtype, other in (("mfma_bf16", "bf16", "fp8"), ("mfma_fp8", "fp8", "bf16")):
+        w = res[name]
+        assert w.get("busy_at_tick", True) and "expected_flops_per_second" in w, w
+        ratio = w["flops_" + dtype] / w["expected_flops_per_second"]
+        print(f"{dtype} MFMA FLOP/s {ratio:.4f}x of the issued work")
+        assert 0.97 < ratio < 1.03, (name, ratio, w)
+        assert w["flops_" + other] < 0.01 * w["expected_flops_per_second"], (name, w)
 
 
 def test_rccl_tracer_counts_collectives():

@@ -11,6 +11,8 @@ GPUEXP_PMC_ASSUME_DEVICE_SCOPE=1 the device-scope families are exported and comp
             waves/s = 16384 / t_launch
   lds_clean ds_read_b32, 32 distinct banks per lane group: bank-conflict % ~ 0
   lds_32way the same reads, all 32 lanes of a group on one bank: 31 of 32 cycles extra
+  mfma_bf16 / mfma_fp8  a fixed number of v_mfma_f32_32x32x16_{bf16,fp8_fp8} per wave:
+            FLOP/s of that type = FLOPs per launch / t_launch, the other type ~ 0
 
 Prints one line `RESULT {json}` (run by tests/test_gpu.py::test_device_scope_pmc_calibration).
 Never imports torch: the plugin's HSA runtime is the only GPU runtime in the process.
@@ -30,7 +32,7 @@ FAMILIES = ("amd_gpu_hbm_read_bytes_per_second", "amd_gpu_hbm_write_bytes_per_se
             "amd_gpu_sq_busy_percent", "amd_gpu_mfma_busy_percent", "amd_gpu_remote_read_bytes_per_second",
             "amd_gpu_remote_write_bytes_per_second", "amd_gpu_hbm_bandwidth_bytes_per_second",
             "amd_gpu_umc_activity_percent")
-WORKLOADS = (("copy", 0), ("lds_clean", 1), ("lds_32way", 2))
+WORKLOADS = (("copy", 0), ("lds_clean", 1), ("lds_32way", 2), ("mfma_bf16", 3), ("mfma_fp8", 4))
 
 
 def main() -> int:
@@ -89,6 +91,10 @@ def main() -> int:
             got["expected_waves_per_second"] = res[1] / t
             if kind == 0:
                 got["expected_Bps"] = res[2] / t
+            if kind >= 3:
+                got["expected_flops_per_second"] = res[2] / t
+                for _, lab, v in promtext.samples(fams, "amd_gpu_mfma_flops_per_second"):
+                    got["flops_" + lab["dtype"]] = v
             dbg = ctypes.create_string_buffer(4096)
             lib.gpuexp_rp_debug(0, dbg, 4096)
             got["raw"] = dbg.value.decode()
