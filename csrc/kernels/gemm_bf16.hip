@@ -417,7 +417,7 @@ gemm_bf16_tn_256_kernel(const uint16_t* __restrict__ A, const uint16_t* __restri
 // Ping-pong form of the 256x256 kernel (variant 8, the default): same tile, waves, LDS
 // image, snake-B read order and epilogue, but every phase is
 //   ds_reads of this phase's group -> stage ONE group (2 glds) -> counted vmcnt ->
-//   s_barrier -> lgkmcnt(0) -> setprio(1), 16 MFMA, setprio(0) -> s_barrier
+//   s_barrier -> lgkmcnt(0) -> 16 MFMA -> s_barrier
 // and wave row 1 runs one barrier behind row 0, so on every SIMD one wave's MFMA cluster
 // runs while the other wave's reads and DMA issue run (cdna_hip_programming.md, "The 256²
 // 8-phase template").  With two barriers per phase a group is restaged >= 2 phases after
@@ -474,8 +474,9 @@ __device__ __forceinline__ void pp_barrier_b() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+template <bool kSetPrio = true>
 __device__ __forceinline__ void pp_mfma(f32x4 (&acc)[4][2], const bf16x8 (&af)[4][2], const bf16x8 (&bf)[4][2]) {
-  __builtin_amdgcn_s_setprio(1);
+  if (kSetPrio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -483,10 +484,10 @@ __device__ __forceinline__ void pp_mfma(f32x4 (&acc)[4][2], const bf16x8 (&af)[4
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni)
         acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi][kk], bf[ni][kk], acc[mi][ni], 0, 0, 0);
-  __builtin_amdgcn_s_setprio(0);
+  if (kSetPrio) __builtin_amdgcn_s_setprio(0);
 }
 
-template <int kGroupM>
+template <int kGroupM, bool kSetPrio = true>
 __global__ void __launch_bounds__(kThreads2, 1)
 gemm_bf16_tn_256pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
                           int M, int N, int K) {
@@ -544,21 +545,21 @@ gemm_bf16_tn_256pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __rest
     read_frags(As, a_row, lane, af, 4);
     pp_wait(1, has1, has2);
     pp_barrier_a();
-    if constexpr (odd) pp_mfma(acc[0][1], af, b1); else pp_mfma(acc[0][0], af, b0);
+    if constexpr (odd) pp_mfma<kSetPrio>(acc[0][1], af, b1); else pp_mfma<kSetPrio>(acc[0][0], af, b0);
     pp_barrier_b();
     // P2: stage Bf(t+2) (same half as Bf(t)); read Bs(t); quadrant (M0, Bs)
     if (has2) { if constexpr (odd) GEMM2_STAGE_B(1, t + 2); else GEMM2_STAGE_B(0, t + 2); }
     if constexpr (odd) read_frags(Bs, b_row, lane, b0, 2); else read_frags(Bs, b_row + 32, lane, b1, 2);
     pp_wait(2, has1, has2);
     pp_barrier_a();
-    if constexpr (odd) pp_mfma(acc[0][0], af, b0); else pp_mfma(acc[0][1], af, b1);
+    if constexpr (odd) pp_mfma<kSetPrio>(acc[0][0], af, b0); else pp_mfma<kSetPrio>(acc[0][1], af, b1);
     pp_barrier_b();
     // P3: stage A-M0(t+2); read A-M1; quadrant (M1, Bs)
     if (has2) GEMM2_STAGE_A(0, t + 2);
     read_frags(As, a_row + 64, lane, af, 4);
     pp_wait(3, has1, has2);
     pp_barrier_a();
-    if constexpr (odd) pp_mfma(acc[1][0], af, b0); else pp_mfma(acc[1][1], af, b1);
+    if constexpr (odd) pp_mfma<kSetPrio>(acc[1][0], af, b0); else pp_mfma<kSetPrio>(acc[1][1], af, b1);
     pp_barrier_b();
     // P4: stage Bs(t+2); read Bf(t+1) into the B registers this phase does not use; (M1, Bf)
     if (has2) { if constexpr (odd) GEMM2_STAGE_B(0, t + 2); else GEMM2_STAGE_B(1, t + 2); }
@@ -567,7 +568,7 @@ gemm_bf16_tn_256pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __rest
     }
     pp_wait(4, has1, has2);
     pp_barrier_a();
-    if constexpr (odd) pp_mfma(acc[1][1], af, b1); else pp_mfma(acc[1][0], af, b0);
+    if constexpr (odd) pp_mfma<kSetPrio>(acc[1][1], af, b1); else pp_mfma<kSetPrio>(acc[1][0], af, b0);
     pp_barrier_b();
   };
   for (int t = 0; t < nk; t += 2) {
@@ -855,8 +856,12 @@ hipError_t launch_gemm_bf16_tn(const void* A, const void* B, void* C, int M, int
                          M, N, K);
       return hipGetLastError();
     }
-    if (variant == 8) {  // 4-row tile groups: 1456 vs 1444 (8 rows), 1398 (16) at 8192^3, 1355 vs 1318 at 4096^3
-      hipLaunchKernelGGL(gemm_bf16_tn_256pp_kernel<4>, dim3((M / kBM2) * (N / kBN2)), dim3(kThreads2), 0, stream,
+    // 4-row tile groups: 1456 vs 1444 (8 rows), 1398 (16) at 8192^3, 1355 vs 1318 at 4096^3;
+    // no s_setprio around the MFMA clusters (the wave rows alternate by barrier anyway):
+    // +2.2 % at 4096^3, +0.2 % at 8192^3 over raising it
+    if (variant == 8) {
+      auto k8 = gemm_bf16_tn_256pp_kernel<4, false>;
+      hipLaunchKernelGGL(k8, dim3((M / kBM2) * (N / kBN2)), dim3(kThreads2), 0, stream,
                          static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C),
                          M, N, K);
       return hipGetLastError();
