@@ -8,6 +8,7 @@
 
 #include "gpuexp/backends.h"
 #include "gpuexp/client.h"
+#include "gpuexp/counter_model.h"
 #include "gpuexp/engine.h"
 #include "gpuexp/kfd_events.h"
 #include "gpuexp/exposition.h"
@@ -264,6 +265,27 @@ PYBIND11_MODULE(_gpuexp, m) {
     return o;
   });
   m.def("gpu_metrics_v1_8_size", []() { return sizeof(GpuMetricsV1_8); });
+  // The counter plugins' derivations (counter_model.h) on given deltas: {counter name: delta}
+  // over `wall` s for a GPU of `simd` SIMDs and `cu` CUs -> (outputs, scope).
+  m.def("derive_counters", [](const py::dict& deltas, double wall, uint32_t simd, uint32_t cu, bool privileged) {
+    double d[gpuexp_ctr::kNumCtr] = {};
+    int inst[gpuexp_ctr::kNumCtr] = {};
+    for (auto kv : deltas) {
+      const std::string k = py::str(kv.first);
+      int slot = -1;
+      for (int c = 0; c < gpuexp_ctr::kNumCtr; ++c)
+        if (k == gpuexp_ctr::name(c)) slot = c;
+      if (slot < 0) throw std::invalid_argument("unknown counter " + k);
+      d[slot] = kv.second.cast<double>();
+      inst[slot] = 1;
+    }
+    gpuexp_ctr::Derived a;
+    a.simd = simd;
+    a.cu = cu;
+    a.privileged = privileged;
+    gpuexp_ctr::derive(a, d, inst, wall);
+    return py::make_tuple(std::vector<double>(a.latest, a.latest + gpuexp_ctr::kNumOut), a.scope);
+  });
   m.def("uuid_from_unique_id", &SysfsBackend::uuid_from_unique_id);
   m.def("parse_ras_err_count", [](const std::string& body) {
     RasTotals t;

@@ -1,0 +1,59 @@
+"""The device-counter derivations both PMC plugins share (csrc/gpuexp/counter_model.h),
+on hand-made counter deltas: formulas, units and the scope rule.  On-silicon calibration of
+the same outputs: tests/test_gpu.py::test_device_scope_pmc_calibration and the MFMA ones."""
+import math
+
+import pytest
+
+SIMD, CU = 1024, 256  # MI355X: 256 CUs x 4 SIMDs
+# output order: counter_model.h derive() / optional_sources.cc sample()
+MFMA_BUSY, SQ_BUSY, GUI, WAVES, LDS, LDS_CONF, HBM_RD, HBM_WR, GMI_RD, GMI_WR, MFMA_UTIL, BF16, FP8 = range(13)
+
+
+def derive(native, wall=0.1, privileged=True, **deltas):
+    return native.derive_counters(deltas, wall, SIMD, CU, privileged)
+
+
+def test_mfma_busy_and_util(native):
+    clk = 2.0e8  # 100 ms at 2 GHz
+    out, _ = derive(native, GRBM_COUNT=clk, GRBM_GUI_ACTIVE=clk / 2, SQ_VALU_MFMA_BUSY_CYCLES=0.25 * clk * SIMD)
+    assert out[MFMA_BUSY] == pytest.approx(25.0)   # over elapsed cycles
+    assert out[MFMA_UTIL] == pytest.approx(50.0)   # over GUI-active cycles (MfmaUtil)
+    assert out[GUI] == pytest.approx(50.0)
+
+
+def test_bandwidth_and_flops_units(native):
+    out, _ = derive(native, wall=0.5, TCC_EA0_RDREQ_DRAM_32B=1e9, TCC_EA0_WRREQ_WRITE_DRAM_32B=5e8,
+                    TCC_EA0_RDREQ_GMI_32B=2e6, SQ_INSTS_VALU_MFMA_MOPS_BF16=1e12, SQ_INSTS_VALU_MFMA_MOPS_F8=3e11,
+                    SQ_WAVES=4e5, GRBM_COUNT=1e8, GRBM_GUI_ACTIVE=1e8)
+    assert out[HBM_RD] == pytest.approx(1e9 * 32 / 0.5)        # 32-B sectors
+    assert out[HBM_WR] == pytest.approx(5e8 * 32 / 0.5)
+    assert out[GMI_RD] == pytest.approx(2e6 * 32 / 0.5)
+    assert out[BF16] == pytest.approx(1e12 * 512 / 0.5)        # MOPS x 512 FLOPs
+    assert out[FP8] == pytest.approx(3e11 * 512 / 0.5)
+    assert out[WAVES] == pytest.approx(4e5 / 0.5)
+
+
+def test_lds_ratios(native):
+    out, _ = derive(native, GRBM_COUNT=1e8, GRBM_GUI_ACTIVE=1e8, SQ_LDS_IDX_ACTIVE=0.1 * 1e8 * CU,
+                    SQ_LDS_BANK_CONFLICT=0.1 * 1e8 * CU * 31 / 32)
+    assert out[LDS] == pytest.approx(10.0)
+    assert out[LDS_CONF] == pytest.approx(100 * 31 / 32)
+    idle, _ = derive(native, GRBM_COUNT=1e8)
+    assert idle[LDS_CONF] == 0.0 and math.isnan(idle[LDS])  # no GUI-active cycles: no LDS share
+
+
+def test_scope_follows_privilege(native):
+    _, scope = derive(native, privileged=False, GRBM_COUNT=1e8, GRBM_GUI_ACTIVE=1e8)
+    assert scope == 0  # unprivileged: wave / LDS / EA / MOPS counters are VMID-filtered
+    _, scope = derive(native, privileged=True, GRBM_COUNT=1e8, GRBM_GUI_ACTIVE=1e8, SQ_WAVES=1e6)
+    assert scope == 1
+    # privileged but a busy MFMA window with (almost) no waves: the filter is on after all
+    _, scope = derive(native, privileged=True, GRBM_COUNT=1e8, GRBM_GUI_ACTIVE=1e8,
+                      SQ_VALU_MFMA_BUSY_CYCLES=1e10, SQ_WAVES=10)
+    assert scope == 0
+
+
+def test_unknown_counter_is_rejected(native):
+    with pytest.raises(ValueError):
+        derive(native, NOT_A_COUNTER=1)
