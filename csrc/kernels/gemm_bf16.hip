@@ -1,8 +1,8 @@
 // Synthetic "HIP-GEMM pod" workload: C[M,N] (bf16) = A[M,K] . B[N,K]^T (bf16 in, fp32 acc).
 // Two kernels: the 256x256 one below the 128x128 one is the default whenever the shape
 // allows (M,N multiples of 256); its default form is the ping-pong variant 8: MI355X,
-// random operands, 8192^3 1453-1459 TFLOP/s (89 % of torch.matmul / hipBLASLt) vs 1358-1361 for
-// the previous one-barrier-per-phase form (profiles/r03/gemm_variants.log).
+// random operands, 8192^3 1497 TFLOP/s (91 % of torch.matmul / hipBLASLt; 93 % at 4096^3) vs
+// 1357 for the previous one-barrier-per-phase form (profiles/r03/gemm_variants.log).
 //
 // 128x128 kernel:
 // This is the load generator behind BASELINE configs 3-5 ("synthetic HIP-workload pods")
