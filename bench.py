@@ -85,8 +85,13 @@ def start_exporter(args, n_gpus: int, backend: str, port: int, pod_map: str, log
     env["GPUEXP_POD_MAP_FILE"] = pod_map
     env["GPUEXP_POD_ATTRIBUTION"] = "true"
     logf = open(log_path, "w")
+    if os.environ.get("GPUEXP_BENCH_FAIL_EXPORTER_WITH_COUNTERS") == "1" and args.counters:
+        raise RuntimeError("exporter start failed on request (GPUEXP_BENCH_FAIL_EXPORTER_WITH_COUNTERS)")  # test hook
     t_start = time.perf_counter()
-    proc = subprocess.Popen(cmd, env=env, stdout=logf, stderr=subprocess.STDOUT, cwd=ROOT)
+    # A/B hook: start the exporter of another checkout (tools/devices_ab.sh runs an older
+    # round's exporter under this bench's workload); never set in a measurement of this tree
+    exp_root = os.environ.get("GPUEXP_BENCH_EXPORTER_ROOT") or ROOT
+    proc = subprocess.Popen(cmd, env=env, stdout=logf, stderr=subprocess.STDOUT, cwd=exp_root)
     deadline = time.time() + 120
     while time.time() < deadline:
         if proc.poll() is not None:
@@ -146,10 +151,10 @@ def request_split(splits: list, q: float) -> dict | None:
 
 
 def run_problems(result: dict, n_gpus: int, attribution_ok: bool, rccl_on: bool) -> list:
-    """Why an N-GPU result is not a valid measurement of the configuration (N > 1; at N = 1
-    problems are recorded in the result but the line is still printed).  Every GPU must be
-    exported, every rank's pod attributed, every rank's RCCL communicator span all N ranks,
-    no optional source dropped, and the exporter up within its start-up budget."""
+    """Why a result is not a valid measurement of the configuration, at any N (1 included:
+    a run without the PMC counters or the sentinel must not pass for the headline).  Every
+    GPU must be exported, every rank's pod attributed, every rank's RCCL communicator span
+    all N ranks, no optional source dropped, and the exporter up within its start-up budget."""
     probs = []
     got = len(result["series_per_gpu"])
     if got != n_gpus:
@@ -168,9 +173,7 @@ def run_problems(result: dict, n_gpus: int, attribution_ok: bool, rccl_on: bool)
         probs.append(f"exporter ran degraded: {reason}")
     if result["exporter_startup_s"] > result["exporter_startup_budget_s"]:
         probs.append(f"exporter start-up {result['exporter_startup_s']} s > budget {result['exporter_startup_budget_s']} s")
-    if n_gpus == 1:
-        result["problems"] = probs or None
-        return []
+    result["problems"] = probs or None
     return probs
 
 
@@ -335,10 +338,11 @@ def main() -> int:
         try:
             exporter = start_exporter(args, n_gpus, backend, port, pod_map, log_path, rccl_dir)
         except RuntimeError as ex:
-            # Never lose the measurement to an optional source: retry without the PMC
-            # counters and the sentinel, and say so in the result.
-            print(f"[bench] exporter start failed ({ex}); retrying without counters/sentinel", file=sys.stderr,
-                  flush=True)
+            # Retry without the PMC counters and the sentinel so the run still reports where
+            # its time went (--out, stderr), but such a run is degraded: run_problems refuses
+            # it, so it exits 1 with no result line, at every N.
+            print(f"[bench] exporter start failed ({ex}); retrying without counters/sentinel (the run will be "
+                  "reported as degraded, with no result line)", file=sys.stderr, flush=True)
             args.counters, args.sentinel = 0, 0
             degraded = str(ex)
             port = free_port()
@@ -738,6 +742,10 @@ def main() -> int:
         metrics_reads = {lab["kind"]: v for _, lab, v in promtext.samples(fams, "gpuexp_gpu_metrics_reads_total")
                          if lab.get("gpu") == "0"}
         sampler_cpu = [v for _, _, v in promtext.samples(fams, "gpuexp_sampler_cpu_seconds_total")]
+        # the devices stage split (whole run): mean per tick of each part, summed over GPUs
+        dev_parts = {lab["part"]: v for _, lab, v in promtext.samples(fams, "gpuexp_device_read_seconds_total")}
+        fetch_cpu = {lab["gpu"]: v for _, lab, v in promtext.samples(fams, "gpuexp_gpu_metrics_fetch_cpu_seconds_total")}
+        fetch_cap = {lab["gpu"]: v for _, lab, v in promtext.samples(fams, "gpuexp_gpu_metrics_min_interval_seconds")}
         prewake = [v for _, _, v in promtext.samples(fams, "gpuexp_http_prewake_wakeups_total")]
         scrapes_total = [v for _, _, v in promtext.samples(fams, "gpuexp_scrapes_total")]
         gz_where = {lab.get("where"): int(v) for _, lab, v in promtext.samples(fams, "gpuexp_gzip_compressions_total")}
@@ -834,6 +842,12 @@ def main() -> int:
             "sample_stage_mean_us": stage_us,
             "sample_stage_p50_le_us": stage_p50_us,
             "gpu_metrics_reads_gpu0": metrics_reads,
+            "device_read_mean_us_per_tick": {k: round(v / ticks[0] * 1e6, 2) for k, v in sorted(dev_parts.items())}
+            if dev_parts and ticks and ticks[0] else None,
+            "gpu_metrics_fetch_cpu_us_per_fresh_read_gpu0": round(fetch_cpu["0"] / metrics_reads["fresh"] * 1e6, 1)
+            if fetch_cpu.get("0") and metrics_reads.get("fresh") else None,
+            "gpu_metrics_min_interval_s": fetch_cap or None,
+            "counters_kick": os.environ.get("GPUEXP_COUNTERS_KICK", "default"),
             "sampler_thread_cpu_s": sampler_cpu[0] if sampler_cpu else None,
             "sampler_cpu_us_per_tick": round(sampler_cpu[0] / ticks[0] * 1e6, 1) if sampler_cpu and ticks and ticks[0]
             else None,

@@ -471,6 +471,7 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("counters_plugin", &EngineConfig::counters_plugin)
       .def_readwrite("counters_mode", &EngineConfig::counters_mode)
       .def_readwrite("counters_sync_us", &EngineConfig::counters_sync_us)
+      .def_readwrite("counters_kick", &EngineConfig::counters_kick)
       .def_readwrite("counters_window_ms", &EngineConfig::counters_window_ms)
       .def_readwrite("counters_interval_ms", &EngineConfig::counters_interval_ms)
       .def_readwrite("enable_rccl", &EngineConfig::enable_rccl)
@@ -483,6 +484,9 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("state_interval_s", &EngineConfig::state_interval_s)
       .def_readwrite("kfd_path", &EngineConfig::kfd_path)
       .def_readwrite("metrics_min_interval_s", &EngineConfig::metrics_min_interval_s)
+      .def_readwrite("metrics_cpu_budget", &EngineConfig::metrics_cpu_budget)
+      .def_readwrite("metrics_max_interval_s", &EngineConfig::metrics_max_interval_s)
+      .def_readwrite("fake_metrics_cost_us", &EngineConfig::fake_metrics_cost_us)
       .def_readwrite("queue_devices", &EngineConfig::queue_devices)
       .def_readwrite("queue_devices_bdf", &EngineConfig::queue_devices_bdf)
       .def_readwrite("force_amdsmi_metrics", &EngineConfig::force_amdsmi_metrics)
@@ -544,6 +548,9 @@ PYBIND11_MODULE(_gpuexp, m) {
         py::dict st;
         for (int k = 0; k < Engine::kStages; ++k) st[Engine::stage_name(k)] = s.stage_ns[k];
         d["stage_ns"] = st;
+        py::dict sc;
+        for (int k = 0; k < Engine::kStages; ++k) sc[Engine::stage_name(k)] = s.stage_cpu_ns[k];
+        d["stage_cpu_ns"] = sc;
         if (const HttpStats* hs = e.http_stats()) {
           d["http_requests"] = hs->requests.load();
           d["http_metrics_requests"] = hs->metrics_requests.load();

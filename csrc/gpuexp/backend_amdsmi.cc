@@ -243,6 +243,7 @@ class AmdsmiBackend : public Backend {
           }
           d.gm.set_coalesce(coalesce_metrics_);
           d.gm.set_min_fresh_interval(metrics_min_ns_);
+          d.gm.set_fake_cost(fake_metrics_cost_ns_);
           if (!d.fast_ok)
             GPUEXP_LOG(LogLevel::kInfo, "amdsmi",
                        "gpu " + std::to_string(info.index) + ": using amdsmi_get_gpu_metrics_info per tick (" +
@@ -353,7 +354,10 @@ class AmdsmiBackend : public Backend {
     if (!ok) {
       out->error.clear();
       amdsmi_gpu_metrics_t m{};
+      const uint64_t w0 = mono_ns(), c0 = thread_cpu_ns();
       amdsmi_status_t st = amdsmi_get_gpu_metrics_info(d.h, &m);
+      out->metrics_cpu_ns = thread_cpu_ns() - c0;
+      out->metrics_wall_ns = mono_ns() - w0;
       if (st != AMDSMI_STATUS_SUCCESS) {
         out->ok = false;
         out->error = "amdsmi_get_gpu_metrics_info: " + smi_err(st);
@@ -362,11 +366,13 @@ class AmdsmiBackend : public Backend {
       from_amdsmi_metrics(m, out, d.xcp, d.nxcc);
     }
     uint64_t used = 0;
+    const uint64_t v0 = mono_ns();
     if (d.vram_used_file.read_u64(&used)) {
       out->vram_used = double(used);
     } else if (amdsmi_get_gpu_memory_usage(d.h, AMDSMI_MEM_TYPE_VRAM, &used) == AMDSMI_STATUS_SUCCESS) {
       out->vram_used = double(used);
     }
+    out->vram_wall_ns = mono_ns() - v0;
     out->vram_total = double(dev.vram_total);
     out->power_cap_w = d.power_cap_w;
     out->ok = true;
@@ -400,6 +406,10 @@ class AmdsmiBackend : public Backend {
 
   double metrics_period_s(const DeviceInfo& dev) override {
     return double(devs_.at(size_t(dev.index)).gm.period_ns()) * 1e-9;
+  }
+
+  void update_metrics_min_interval(const DeviceInfo& dev, uint64_t ns) override {
+    devs_.at(size_t(dev.index)).gm.set_min_fresh_interval(ns);
   }
 
   std::string describe(const DeviceInfo& dev) override {

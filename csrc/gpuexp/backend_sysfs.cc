@@ -264,6 +264,7 @@ void SysfsBackend::open_dev_files(Dev* d) {
   d->gm_ok = d->gm.open(d->dev_dir + "/gpu_metrics", &e);
   d->gm.set_coalesce(coalesce_metrics_);
   d->gm.set_min_fresh_interval(metrics_min_ns_);
+  d->gm.set_fake_cost(fake_metrics_cost_ns_);
   d->gm.set_partition(d->xcp, d->nxcc);
   d->vram_used.open(d->dev_dir + "/mem_info_vram_used");
   d->busy.open(d->dev_dir + "/gpu_busy_percent");
@@ -312,6 +313,7 @@ void SysfsBackend::sample(const DeviceInfo& dev, DeviceSample* out) {
   }
   if (!any) sample_fallback(d, out);
   uint64_t used = 0;
+  const uint64_t v0 = mono_ns();
   if (d.vram_used.read_u64(&used)) {
     out->vram_used = double(used);
     any = true;
@@ -319,6 +321,7 @@ void SysfsBackend::sample(const DeviceInfo& dev, DeviceSample* out) {
     out->vram_used = double(used);
     any = true;
   }
+  out->vram_wall_ns = mono_ns() - v0;
   out->vram_total = double(dev.vram_total);
   out->power_cap_w = d.power_cap_w;
   out->ok = any || !std::isnan(out->gfx_activity) || !std::isnan(out->power_w);

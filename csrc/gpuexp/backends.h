@@ -100,6 +100,9 @@ class SysfsBackend : public Backend {
   double metrics_period_s(const DeviceInfo& dev) override {
     return double(devs_.at(size_t(dev.index))->gm.period_ns()) * 1e-9;
   }
+  void update_metrics_min_interval(const DeviceInfo& dev, uint64_t ns) override {
+    devs_.at(size_t(dev.index))->gm.set_min_fresh_interval(ns);
+  }
 
   // amdsmi-compatible UUID from the KFD unique_id + PCI device id.
   static std::string uuid_from_unique_id(uint64_t unique_id, uint32_t device_id);

@@ -84,6 +84,10 @@ struct DeviceSample {
   uint64_t host_ns = 0;        // CLOCK_MONOTONIC at read
   uint64_t fw_ts_10ns = 0;     // PMFW timestamp (10 ns units), 0 = n/a
   bool metrics_coalesced = false;  // decoded from the cached gpu_metrics table (no SMU fetch)
+  // What this sample's reads cost (filled by the backend; the engine's devices-stage split,
+  // gpuexp_device_read_duration_seconds): gpu_metrics wall + thread CPU (a fresh read is an
+  // SMU round trip the kernel busy-waits on; ~0 when coalesced), the VRAM-used file, wall.
+  uint64_t metrics_wall_ns = 0, metrics_cpu_ns = 0, vram_wall_ns = 0;
 
   double gfx_activity = kNaN;  // %
   double umc_activity = kNaN;  // %
@@ -201,6 +205,15 @@ class Backend {
   // gpu_metrics read coalescing (GpuMetricsReader); set before init().
   void set_metrics_coalescing(bool on) { coalesce_metrics_ = on; }
   void set_metrics_min_interval(uint64_t ns) { metrics_min_ns_ = ns; }
+  // Tests only: burn this much thread CPU per fresh gpu_metrics read, so a fake host root
+  // carries the SMU fetch's measured cost (a real fetch is kernel busy-wait); set before init().
+  void set_fake_metrics_cost(uint64_t ns) { fake_metrics_cost_ns_ = ns; }
+  // Per-GPU cap on fresh gpu_metrics reads, changed while running (the engine's "auto"
+  // policy, EngineConfig::metrics_min_interval_s < 0).  Sampler thread only.
+  virtual void update_metrics_min_interval(const DeviceInfo& dev, uint64_t ns) {
+    (void)dev;
+    (void)ns;
+  }
   virtual const char* name() const = 0;
   // Enumerates devices once.  Returns false (with *err) if the backend cannot run.
   virtual bool init(std::vector<DeviceInfo>* devices, std::string* err) = 0;
@@ -239,6 +252,7 @@ class Backend {
  protected:
   bool coalesce_metrics_ = true;
   uint64_t metrics_min_ns_ = 0;
+  uint64_t fake_metrics_cost_ns_ = 0;
 };
 
 }  // namespace gpuexp

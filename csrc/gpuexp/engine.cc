@@ -136,6 +136,11 @@ const char* Engine::stage_name(int i) {
   return n[i];
 }
 
+const char* Engine::dev_part_name(int i) {
+  static const char* n[kDevParts] = {"counters_kick", "control", "gpu_metrics", "vram", "ras", "gtt"};
+  return n[i];
+}
+
 Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) { self_pid_ = int(::getpid()); }
 
 Engine::~Engine() { stop(); }
@@ -331,6 +336,18 @@ void Engine::define_families() {
                      "Unix time of the tick that produced this exposition (alert on time() - this: a stuck "
                      "sampler keeps serving its last snapshot)", G, {});
   f_self_stage_ = add("gpuexp_sample_stage_duration_seconds", "Sampler stage duration", H, {"stage"});
+  // counters, not histograms: 6 parts x 11 bucket lines would be re-rendered and re-gzipped
+  // every tick for a split whose means (rate / rate(gpuexp_ticks_total)) are what matters
+  f_self_dev_part_ = add("gpuexp_device_read_seconds_total",
+                         "The devices stage split: time in each part (counters_kick: PMC read submitted; "
+                         "control: control-plane apply; gpu_metrics: SMU fetch or cached decode; vram; ras; "
+                         "gtt), summed over GPUs", C, {"part"});
+  f_self_fetch_cpu_ = add("gpuexp_gpu_metrics_fetch_cpu_seconds_total",
+                          "Thread CPU of fresh gpu_metrics reads (each one an SMU round trip the kernel "
+                          "busy-waits on)", C, {"gpu"});
+  f_self_fetch_cap_ = add("gpuexp_gpu_metrics_min_interval_seconds",
+                          "Current cap on fresh gpu_metrics reads per GPU (metrics_min_interval; auto: the "
+                          "measured fetch CPU x GPUs / metrics_cpu_budget)", G, {"gpu"});
   f_self_scrape_ = add("gpuexp_scrape_duration_seconds", "Server-side /metrics latency (request parsed -> last byte written)",
                        H, {});
   f_self_scrapes_ = add("gpuexp_scrapes_total", "Scrapes of the metrics path", C, {});
@@ -425,6 +442,7 @@ bool Engine::start(std::string* err) {
   }
   backend_->set_metrics_coalescing(cfg_.metrics_coalesce);
   backend_->set_metrics_min_interval(uint64_t(std::max(0.0, cfg_.metrics_min_interval_s) * 1e9));
+  backend_->set_fake_metrics_cost(cfg_.fake_metrics_cost_us * 1000ull);
   std::vector<DeviceInfo> all;
   if (!backend_->init(&all, err)) return false;
   if (!cfg_.device_filter.empty() || !cfg_.device_filter_bdf.empty()) {
@@ -484,8 +502,12 @@ bool Engine::start(std::string* err) {
       }
     }
   }
+  // auto = serial: a fresh gpu_metrics read is kernel busy-wait (its CPU is the same on any
+  // thread) and waking a pool costs more CPU than the parallel reads save wall time
+  // (8 fake GPUs at 100 Hz: 9.8 % vs 6.3 % of a core, profiles/r04/devices_split.txt); a
+  // pool only shortens the tick's wall time (8 x 0.45 ms at most), so it stays opt-in.
   int nthreads = cfg_.device_threads;
-  if (nthreads <= 0) nthreads = cfg_.backend == "mock" ? 1 : std::min<int>(int(devices_.size()), 8);
+  if (nthreads <= 0) nthreads = 1;
   if (nthreads > 1) pool_ = std::make_unique<ForkJoinPool>(nthreads);
   kfd_ = std::make_unique<KfdProcReader>(cfg_.host_root, cfg_.exclude_self ? self_pid_ : -1, cfg_.kfd_cu_occupancy,
                                          uint64_t(cfg_.kfd_detail_interval_s * 1e9));
@@ -868,6 +890,9 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
     std::copy(std::begin(st.xcc_last), std::end(st.xcc_last), std::begin(fresh.xcc_last));
     fresh.errors = st.errors;
     fresh.err_ref = st.err_ref;
+    fresh.fetch_cost_ns = st.fetch_cost_ns;  // the fetch policy's state is the GPU's, not the owner's
+    fresh.fetch_cpu_s = st.fetch_cpu_s;
+    fresh.fetch_cap_ns = st.fetch_cap_ns;
     std::copy(std::begin(st.kfd_events), std::end(st.kfd_events), std::begin(fresh.kfd_events));
     fresh.owner = keep;
     fresh.owner_key = okey;
@@ -1435,6 +1460,9 @@ void Engine::emit_self(uint64_t gen) {
   cput(self_refs_[5], f_self_render_bytes_, double(s.render_bytes), gen, none);
   cput(self_refs_[6], f_self_series_, double(s.series), gen, none);
   cput(self_refs_[7], f_self_cpu_, double(s.sampler_cpu_ns) * 1e-9, gen, none);
+  for (int k = 0; k < kDevParts; ++k)
+    cput(dev_part_refs_[k], f_self_dev_part_, dev_part_total_s_[k], gen,
+         [&] { return std::vector<std::string>{dev_part_name(k)}; });
   for (int k = 0; k < kStages; ++k) {
     if (!self_stage_refs_[k].valid()) self_stage_refs_[k] = table_.upsert(f_self_stage_, {stage_name(k)});
     if (s.ticks) table_.observe(self_stage_refs_[k], double(last_stage_ns_[k]) * 1e-9, gen, stage_bounds());
@@ -1475,6 +1503,10 @@ void Engine::emit_self(uint64_t gen) {
            [&] { return std::vector<std::string>{g, "coalesced"}; });
       cput(st.self_reads[2], f_self_metrics_period_, backend_->metrics_period_s(devices_[i]), gen,
            [&] { return std::vector<std::string>{g}; });
+      cput(st.fetch_cpu, f_self_fetch_cpu_, st.fetch_cpu_s, gen, [&] { return std::vector<std::string>{g}; });
+      const double cap = cfg_.metrics_min_interval_s < 0 ? double(st.fetch_cap_ns) * 1e-9
+                                                          : std::max(0.0, cfg_.metrics_min_interval_s);
+      cput(st.fetch_cap, f_self_fetch_cap_, cap, gen, [&] { return std::vector<std::string>{g}; });
     }
   cput(self_refs_[12], f_self_source_up_, 1, gen,
        [&] { return std::vector<std::string>{"backend:" + std::string(backend_->name())}; });
@@ -1501,17 +1533,49 @@ void Engine::emit_self(uint64_t gen) {
   }
 }
 
+// metrics_min_interval "auto": all GPUs' SMU fetches together may use metrics_cpu_budget of
+// one core.  With c_i the measured thread CPU of GPU i's fresh read, every GPU gets the cap
+// T = sum(c_i) / budget (one fetch per GPU per T): 1 GPU at 0.25 ms and 1.5 % -> 17 ms, under
+// a 10 Hz tick, so every tick is fresh; 8 GPUs -> 133 ms, a fresh table every other tick.
+// A cap at or below the tick period is no cap (0); above it, the cap is rounded UP to whole
+// ticks (k = ceil(T / period): a fetch every k-th tick keeps the budget) and half a period
+// comes off, so tick jitter never skips one more fetch than that.
+void Engine::update_fetch_policy() {
+  double sum_ns = 0;
+  for (const auto& st : dstate_) sum_ns += st.fetch_cost_ns;
+  if (sum_ns <= 0 || cfg_.metrics_cpu_budget <= 0) return;  // nothing measured yet: no cap
+  const double period = cfg_.interval_s > 0 ? cfg_.interval_s * 1e9 : 0;
+  double cap = std::min(sum_ns / cfg_.metrics_cpu_budget, cfg_.metrics_max_interval_s * 1e9);
+  if (period > 0) cap = cap <= period ? 0 : (std::ceil(cap / period) - 0.5) * period;
+  for (size_t i = 0; i < dstate_.size(); ++i) {
+    DevState& st = dstate_[i];
+    const double prev = double(st.fetch_cap_ns);
+    // re-set only on a 5 % change (the EWMA moves a little every fresh read)
+    if (std::fabs(cap - prev) <= 0.05 * std::max(cap, prev) && !(cap == 0 && prev != 0)) continue;
+    st.fetch_cap_ns = uint64_t(cap);
+    backend_->update_metrics_min_interval(devices_[i], st.fetch_cap_ns);
+  }
+}
+
 void Engine::tick_locked(uint64_t now) {
   uint64_t cpu0 = thread_cpu_ns();
   uint64_t gen = ++gen_;
   double dt_s = last_tick_now_ && now > last_tick_now_ ? double(now - last_tick_now_) * 1e-9 : 0.0;
   last_tick_now_ = now;
-  uint64_t ts[kStages + 1];
+  uint64_t ts[kStages + 1], cs[kStages + 1];  // stage boundaries: wall, sampler-thread CPU
   ts[0] = mono_ns();
+  cs[0] = cpu0;
   if (!startup_ns_ && start_mono_ns_ && ts[0] > start_mono_ns_) startup_ns_ = ts[0] - start_mono_ns_;
-  // continuous counters: this tick's read goes out now and is collected before the series
-  // stage, so the exported window is exactly the last tick interval
-  if (counters_) counters_->kick();
+  // continuous counters: this tick's read goes out now (or right after the device reads)
+  // and is collected before the series stage, so the exported window is one tick interval
+  resolver_->begin_tick(now);
+  uint64_t part[kDevParts] = {};
+  const bool kick_late = cfg_.counters_kick == "after_devices";
+  if (counters_ && !kick_late) {
+    counters_->kick();
+    part[0] = mono_ns() - ts[0];
+  }
+  const uint64_t c0 = mono_ns();
 
   // Control-plane updates (pushed from Python at low rate).
   {
@@ -1538,6 +1602,7 @@ void Engine::tick_locked(uint64_t now) {
       pods_complete_ = pending_complete_;
     }
   }
+  part[1] = mono_ns() - c0;
 
   // 0: device telemetry (per-GPU reads fan out over the pool; each touches only its own
   // DevState and its own backend device slot)
@@ -1552,7 +1617,9 @@ void Engine::tick_locked(uint64_t now) {
     st.cur.host_ns = now;
     backend_->sample(devices_[size_t(i)], &st.cur);
     (st.cur.metrics_coalesced ? metrics_coalesced_ : metrics_fresh_)[size_t(i)] += 1;
+    st.ras_ns = st.gtt_ns = 0;
     if (!ras_.empty()) {
+      const uint64_t r0 = mono_ns();
       if (now >= ras_next_ns_[size_t(i)]) {
         ras_[size_t(i)].read(&ras_cache_[size_t(i)]);
         ras_next_ns_[size_t(i)] = now + uint64_t(cfg_.ras_interval_s * 1e9);
@@ -1567,11 +1634,14 @@ void Engine::tick_locked(uint64_t now) {
       st.cur.pages_retired = r.pages_retired;
       st.cur.pages_pending = r.pages_pending;
       st.cur.pages_unreservable = r.pages_unreservable;
+      st.ras_ns = mono_ns() - r0;
     }
     if (!gtt_used_f_.empty()) {
+      const uint64_t g0 = mono_ns();
       uint64_t v = 0;
       if (gtt_used_f_[size_t(i)].read_u64(&v)) st.cur.gtt_used = double(v);
       st.cur.gtt_total = gtt_total_[size_t(i)];
+      st.gtt_ns = mono_ns() - g0;
     }
   };
   if (pool_) {
@@ -1579,12 +1649,31 @@ void Engine::tick_locked(uint64_t now) {
   } else {
     for (size_t i = 0; i < devices_.size(); ++i) sample_one(int(i));
   }
-  for (auto& st : dstate_)
+  for (auto& st : dstate_) {
     if (!st.cur.ok) {
       st.errors += 1;
       errs += 1;
     }
+    part[2] += st.cur.metrics_wall_ns;
+    part[3] += st.cur.vram_wall_ns;
+    part[4] += st.ras_ns;
+    part[5] += st.gtt_ns;
+    if (!st.cur.metrics_coalesced && st.cur.metrics_cpu_ns) {
+      st.fetch_cpu_s += double(st.cur.metrics_cpu_ns) * 1e-9;
+      // EWMA over fresh reads (a few outliers, e.g. a preempted read, barely move it)
+      const double c = double(st.cur.metrics_cpu_ns);
+      st.fetch_cost_ns = st.fetch_cost_ns > 0 ? 0.9 * st.fetch_cost_ns + 0.1 * c : c;
+    }
+  }
+  if (cfg_.metrics_min_interval_s < 0) update_fetch_policy();
+  if (counters_ && kick_late) {
+    const uint64_t k0 = mono_ns();
+    counters_->kick();
+    part[0] = mono_ns() - k0;
+  }
   ts[1] = mono_ns();
+  cs[1] = thread_cpu_ns();
+  for (int k = 0; k < kDevParts; ++k) dev_part_total_s_[k] += double(part[k]) * 1e-9;
 
   // 1: processes
   std::vector<std::vector<ProcSample>> per_dev(devices_.size());
@@ -1605,6 +1694,7 @@ void Engine::tick_locked(uint64_t now) {
     }
   }
   ts[2] = mono_ns();
+  cs[2] = thread_cpu_ns();
 
   // 2: device ownership (device plugin map first, then single-pod inference).
   for (size_t i = 0; i < devices_.size(); ++i) {
@@ -1644,14 +1734,17 @@ void Engine::tick_locked(uint64_t now) {
     st.owner = own;
   }
   ts[3] = mono_ns();
+  cs[3] = thread_cpu_ns();
 
   // 3: sentinel (drain previous run, launch next; never blocks on the GPU)
   if (sentinel_) sentinel_->tick(now);
   if (kfd_events_) count_kfd_events();
   ts[4] = mono_ns();
+  cs[4] = thread_cpu_ns();
   // 4: counters: wait (bounded) for this tick's read round; sampled in collect_device
   if (counters_ && !counters_->sync(cfg_.counters_sync_us)) counters_late_ += 1;
   ts[5] = mono_ns();
+  cs[5] = thread_cpu_ns();
 
   // 5: series
   for (size_t i = 0; i < devices_.size(); ++i) {
@@ -1661,6 +1754,7 @@ void Engine::tick_locked(uint64_t now) {
   if (kfd_events_) emit_kfd_events(gen);
   emit_self(gen);
   ts[6] = mono_ns();
+  cs[6] = thread_cpu_ns();
 
   // 6: render into a free snapshot slot
   int slot = store_.begin_write();
@@ -1674,6 +1768,7 @@ void Engine::tick_locked(uint64_t now) {
     nseries = table_.live_series(gen);
     snap->series = nseries;
     ts[7] = mono_ns();
+    cs[7] = thread_cpu_ns();
     // 7: gzip (only while clients ask for it) + publish
     snap->gz.clear();
     snap->pb.clear();
@@ -1695,14 +1790,21 @@ void Engine::tick_locked(uint64_t now) {
     if (http_) http_->set_ready(true);
   } else {
     ts[7] = mono_ns();
+    cs[7] = thread_cpu_ns();
   }
   uint64_t tend = mono_ns();
+  cs[kStages] = thread_cpu_ns();
   uint64_t stage_dur[kStages] = {ts[1] - ts[0], ts[2] - ts[1], ts[3] - ts[2], ts[4] - ts[3],
                                  ts[5] - ts[4], ts[6] - ts[5], ts[7] - ts[6], tend - ts[7]};
   for (int k = 0; k < kStages; ++k) {
     last_stage_ns_[k] = stage_dur[k];
     uint64_t start = k == 0 ? ts[0] : (k < kStages - 1 ? ts[k] : ts[7]);
     trace_event(stage_name(k), start, stage_dur[k]);
+    if (k == 0 && trace_) {  // the devices stage's parts, inside its span
+      trace_event("devices/control", c0, part[1]);
+      for (size_t i = 0; i < dstate_.size(); ++i)  // per GPU (they overlap on the read pool)
+        if (dstate_[i].cur.metrics_wall_ns) trace_event("devices/gpu_metrics", c0 + part[1], dstate_[i].cur.metrics_wall_ns);
+    }
   }
   {
     std::lock_guard<std::mutex> lk(stats_mu_);
@@ -1715,7 +1817,10 @@ void Engine::tick_locked(uint64_t now) {
       stats_.series = nseries;
     }
     stats_.device_errors += errs;
-    for (int k = 0; k < kStages; ++k) stats_.stage_ns[k] = double(stage_dur[k]);
+    for (int k = 0; k < kStages; ++k) {
+      stats_.stage_ns[k] = double(stage_dur[k]);
+      stats_.stage_cpu_ns[k] += cs[k + 1] - cs[k];  // the sampler thread's own CPU per stage
+    }
     // every thread that worked for this tick: the sampler, the per-GPU read pool, and the
     // counter plugin's thread (its PM4 read rounds since the last tick)
     // The sampler thread charges its whole clock since the last tick (timerfd wake-ups

@@ -65,7 +65,7 @@ class ForkJoinPool {
 
 struct EngineConfig {
   std::string backend = "mock";        // mock | sysfs | amdsmi
-  int device_threads = 0;              // 0 = auto (one per GPU up to 8 for real backends), 1 = serial
+  int device_threads = 0;              // 0 = auto (serial), N > 1 = a pool of N reader threads
   int mock_devices = 1;
   std::string host_root;               // "" == "/"
   double interval_s = 1.0;             // 0 = manual ticks only (tests)
@@ -74,7 +74,14 @@ struct EngineConfig {
   std::string series_profile = "standard";  // standard | full | compact | legacy
   double ras_interval_s = 10.0;        // full profile: RAS/AER sysfs re-read period
   bool metrics_coalesce = true;        // skip gpu_metrics SMU fetches between PMFW refreshes
-  double metrics_min_interval_s = 0;   // at most one SMU fetch per GPU per this many seconds (0 = no cap)
+  // At most one SMU fetch per GPU per this many seconds (0 = no cap).  < 0 = auto: the cap
+  // follows the measured CPU of a fresh fetch so that all GPUs' fetches together stay within
+  // metrics_cpu_budget of one core (between fetches the cached table is re-decoded; the
+  // per-tick activity signals come from the PMC counters, read every tick).
+  double metrics_min_interval_s = -1;
+  double metrics_cpu_budget = 0.015;   // auto: fraction of one core for SMU fetches (all GPUs)
+  double metrics_max_interval_s = 1.0;  // auto: never staler than this
+  uint64_t fake_metrics_cost_us = 0;   // tests only: thread CPU burnt per fresh gpu_metrics read
   bool legacy_families = true;         // pod_gpu_memory_usage / docker_gpu_memory_perc_usage
   bool pod_attribution = true;
   bool infer_device_owner = true;      // single-pod GPU -> device series carry the pod
@@ -94,6 +101,10 @@ struct EngineConfig {
   int counters_window_ms = 20;         // duty: counting window...
   int counters_interval_ms = 1000;     // ...once per interval (see rocprof_plugin.cc)
   int counters_sync_us = 2000;         // continuous: longest a tick waits for its own counter read
+  // continuous: when a tick's PMC read goes out.  "start": before the device reads;
+  // "after_devices": once the gpu_metrics SMU fetches are done (a PM4 read in flight while
+  // the SMU serves the metrics table slows the fetch, profiles/r04/devices_split.txt).
+  std::string counters_kick = "start";
   bool enable_rccl = false;
   std::string rccl_dir = "/dev/shm";
   bool rccl_verify = true;             // attribute a tracer file only to a process that maps it
@@ -141,6 +152,7 @@ struct EngineStats {
   uint64_t series = 0;
   uint64_t device_errors = 0;
   double stage_ns[8] = {};
+  uint64_t stage_cpu_ns[8] = {};  // cumulative sampler-thread CPU per stage (pool / PMC threads not split)
   uint64_t sampler_cpu_ns = 0;
   uint64_t gzip_eager = 0;  // snapshots published with a gzip copy
 };
@@ -177,6 +189,11 @@ class Engine {
 
   static const char* stage_name(int i);
   static constexpr int kStages = 8;
+  // The devices stage split (gpuexp_device_read_seconds_total{part}): PMC read kick,
+  // control-plane apply, gpu_metrics (SMU fetch or cached decode), VRAM-used file, RAS/AER
+  // files, GTT file.  Per-GPU parts are summed over GPUs (wall time on whichever thread).
+  static const char* dev_part_name(int i);
+  static constexpr int kDevParts = 6;
 
  private:
   struct DevState {
@@ -205,6 +222,11 @@ class Engine {
     uint64_t errors = 0;
     SeriesRef err_ref;
     SeriesRef self_reads[4];  // gpu_metrics reads fresh / coalesced, refresh period, counter scope
+    SeriesRef fetch_cpu, fetch_cap;  // SMU-fetch CPU so far; current fetch cap (auto policy)
+    uint64_t ras_ns = 0, gtt_ns = 0;  // this tick's RAS / GTT read time (sample_one)
+    double fetch_cost_ns = 0;        // EWMA thread CPU of a fresh gpu_metrics read (0 = none yet)
+    double fetch_cpu_s = 0;          // thread CPU of every fresh gpu_metrics read so far
+    uint64_t fetch_cap_ns = 0;       // cap currently set on the backend's reader
   };
   // Cached series handles of a (GPU, PID) or a pod, valid while their label values are the
   // ones recorded here: the per-tick path then sets values without building label vectors.
@@ -227,6 +249,7 @@ class Engine {
   void collect_device(int i, uint64_t gen, double dt_s);
   void emit_processes(uint64_t gen, const std::vector<std::vector<ProcSample>>& per_dev);
   void emit_self(uint64_t gen);
+  void update_fetch_policy();
   void count_kfd_events();
   void emit_kfd_events(uint64_t gen);
   std::string device_key(size_t i) const;  // "<bdf>/<partition>": stable across restarts
@@ -357,6 +380,9 @@ class Engine {
   SeriesRef prewake_hits_ref_, startup_ref_;
   SeriesRef self_stage_refs_[kStages];
   uint64_t last_stage_ns_[kStages] = {};
+  SeriesRef dev_part_refs_[kDevParts];
+  double dev_part_total_s_[kDevParts] = {};  // sampler thread
+  int f_self_dev_part_ = -1, f_self_fetch_cpu_ = -1, f_self_fetch_cap_ = -1;
 };
 
 }  // namespace gpuexp

@@ -94,6 +94,7 @@ GpuMetricsReader& GpuMetricsReader::operator=(GpuMetricsReader&& o) noexcept {
   content_ = o.content_;
   coalesce_ = o.coalesce_;
   min_fresh_ns_ = o.min_fresh_ns_;
+  fake_cost_ns_ = o.fake_cost_ns_;
   xcp_ = o.xcp_;
   nxcc_ = o.nxcc_;
   last_n_ = o.last_n_;
@@ -160,7 +161,13 @@ bool GpuMetricsReader::read(DeviceSample* out, uint64_t now_ns) {
     out->metrics_coalesced = true;
     return decode_gpu_metrics_v1_8(buf_, size_t(last_n_), out, xcp_, nxcc_);
   }
+  const uint64_t w0 = mono_ns(), c0 = thread_cpu_ns();
   long n = pread_once(fd_, reinterpret_cast<char*>(buf_), sizeof(buf_));
+  if (fake_cost_ns_)
+    while (thread_cpu_ns() - c0 < fake_cost_ns_) {
+    }
+  out->metrics_cpu_ns = thread_cpu_ns() - c0;
+  out->metrics_wall_ns = mono_ns() - w0;
   if (n <= 0) {
     last_n_ = 0;
     out->error = "gpu_metrics read failed";

@@ -288,19 +288,40 @@ const CgroupInfo* PidResolver::resolve(int pid) {
     }
     return &e.info;
   }
-  uint64_t st = 0;
-  bool have_st = read_starttime(pid, &st);
   auto it = cache_.find(pid);
-  if (it != cache_.end() && it->second.ok && (!have_st || it->second.starttime == st))
-    return &it->second.info;
+  if (it != cache_.end() && it->second.ok) {
+    Entry& e = it->second;
+    if (e.epoch == epoch_) return &e.info;  // already checked this tick
+    char b[32];
+    const bool alive = !e.comm || e.comm->read(b, sizeof(b)) > 0;
+    if (alive && now_ns_ >= e.st_checked_ns && now_ns_ - e.st_checked_ns < kStarttimeEveryNs) {
+      e.epoch = epoch_;
+      return &e.info;
+    }
+    uint64_t st = 0;
+    const bool have_st = read_starttime(pid, &st);
+    if (alive && (!have_st || e.starttime == st)) {
+      e.epoch = epoch_;
+      e.st_checked_ns = now_ns_;
+      return &e.info;
+    }
+  }
+  uint64_t st = 0;
+  const bool have_st = read_starttime(pid, &st);
   std::string content;
-  if (!read_small_file(root_ + "/proc/" + std::to_string(pid) + "/cgroup", &content)) {
+  const std::string dir = root_ + "/proc/" + std::to_string(pid);
+  if (!read_small_file(dir + "/cgroup", &content)) {
     cache_.erase(pid);
     return nullptr;
   }
   Entry& e = cache_[pid];
-  e.starttime = st;
+  e = Entry();
+  e.starttime = have_st ? st : 0;
   e.ok = true;
+  e.epoch = epoch_;
+  e.st_checked_ns = now_ns_;
+  e.comm = std::make_shared<CachedFile>();
+  if (!e.comm->open(dir + "/comm")) e.comm.reset();
   parse_proc_cgroup(content, &e.info);
   return &e.info;
 }

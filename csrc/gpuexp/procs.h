@@ -71,9 +71,20 @@ bool parse_kube_cgroup_path(const std::string& path, CgroupInfo* out);
 bool parse_proc_cgroup(const std::string& content, CgroupInfo* out);
 
 // Caches pid -> CgroupInfo keyed on (pid, starttime) so PID reuse is detected.
+// The reuse check costs one cheap read per PID per tick: a cached fd of /proc/<pid>/comm
+// (reads of a /proc/<pid> file fail with ESRCH once that process is gone, so a new process
+// under the same PID cannot pass it), and the starttime in /proc/<pid>/stat at most once a
+// second (generating stat sums over every thread of the process: 4 us for one thread,
+// tens of us for a framework process with hundreds).  Called at most once per PID per tick
+// whatever the number of callers.
 class PidResolver {
  public:
   explicit PidResolver(std::string host_root);
+  // Starts a tick at (engine) time now_ns: every PID is re-checked once in it.
+  void begin_tick(uint64_t now_ns) {
+    ++epoch_;
+    now_ns_ = now_ns;
+  }
   // Returns nullptr if the PID cannot be read (other PID namespace, exited).
   const CgroupInfo* resolve(int pid);
   // Test/bench hook: pretend /proc/<pid>/cgroup contains `cgroup_path`.
@@ -86,8 +97,13 @@ class PidResolver {
     uint64_t starttime = 0;
     bool ok = false;
     CgroupInfo info;
+    std::shared_ptr<CachedFile> comm;  // /proc/<pid>/comm, kept open (liveness)
+    uint64_t epoch = 0;                // tick it was last checked in
+    uint64_t st_checked_ns = 0;        // engine time of the last starttime check
   };
   bool read_starttime(int pid, uint64_t* st);
+  static constexpr uint64_t kStarttimeEveryNs = 1000000000ull;
+  uint64_t epoch_ = 1, now_ns_ = 0;
   std::string root_;
   std::unordered_map<int, Entry> cache_;
   std::unordered_map<int, std::string> overrides_;

@@ -255,8 +255,25 @@ void tool_fini(void*) {
 
 }  // namespace
 
+// The rocprofiler-sdk this tool was compiled against (10000 * major + 100 * minor + patch).
+// The RCCL domain id and the RCCL API argument layout it uses are that version's, so it
+// loads only under a runtime of the same major version at or above it; an older (or the
+// next major) runtime gets no configuration and the workload runs untraced instead of
+// tracing whatever domain that id means there.  GPUEXP_RCCL_TRACER_ANY_SDK=1 overrides.
+constexpr uint32_t kBuiltSdk = ROCPROFILER_VERSION_MAJOR * 10000 + ROCPROFILER_VERSION_MINOR * 100 + ROCPROFILER_VERSION_PATCH;
+
+extern "C" __attribute__((visibility("default"))) uint32_t gpuexp_rccl_tracer_built_sdk_version() { return kBuiltSdk; }
+
 extern "C" __attribute__((visibility("default"))) rocprofiler_tool_configure_result_t* rocprofiler_configure(
-    uint32_t, const char*, uint32_t, rocprofiler_client_id_t* id) {
+    uint32_t version, const char*, uint32_t, rocprofiler_client_id_t* id) {
+  const char* any = std::getenv("GPUEXP_RCCL_TRACER_ANY_SDK");
+  const bool ok = version / 10000 == kBuiltSdk / 10000 && version >= kBuiltSdk / 100 * 100;
+  if (!ok && !(any && any[0] == '1')) {
+    std::fprintf(stderr, "[gpuexp-rccl-tracer] rocprofiler-sdk %u.%u.%u is not the 1.%u+ this tracer was built for; "
+                 "not loading (RCCL collectives of this process are not traced)\n",
+                 version / 10000, version / 100 % 100, version % 100, kBuiltSdk / 100 % 100);
+    return nullptr;
+  }
   id->name = "gpuexp-rccl-tracer";
   static rocprofiler_tool_configure_result_t cfg{sizeof(rocprofiler_tool_configure_result_t), &tool_init,
                                                  &tool_fini, nullptr};

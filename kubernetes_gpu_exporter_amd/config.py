@@ -29,10 +29,12 @@ class Config:
     # sampling
     interval: float = 1.0                  # seconds; reference: 30 s (main.go:156)
     backend: str = "auto"                  # auto | amdsmi | sysfs | mock
-    device_threads: int = 0                # per-GPU read fan-out (0 = auto, 1 = serial)
+    device_threads: int = 0                # per-GPU read fan-out (0 = auto = serial, N > 1 = pool)
     metrics_coalesce: bool = True          # skip gpu_metrics SMU fetches until the PMFW refreshes
-    metrics_min_interval: float = 0.0      # at most one gpu_metrics SMU fetch per GPU per this many s
-                                           # (0 = every PMFW refresh): bounds sampler CPU at 8 GPUs x 100 Hz
+    metrics_min_interval: str = "auto"     # at most one gpu_metrics SMU fetch per GPU per this many s
+                                           # (0 = every PMFW refresh; auto = as often as metrics_cpu_budget
+                                           # allows at the measured fetch cost): bounds sampler CPU at 8 GPUs
+    metrics_cpu_budget: float = 1.5        # auto: % of one core all GPUs' SMU fetches may use together
     mock_devices: int = 1
     host_root: str = ""                    # prefix for /sys and /proc (DaemonSet: /host)
     devices: list = field(default_factory=list)  # GPU indices and/or PCI BDFs to export (empty = all)
@@ -52,6 +54,7 @@ class Config:
     counters_mode: str = "continuous"      # continuous (never paused, read every tick; aqlpmc) | duty
     counters_window_ms: int = 20           # duty: counting window ...
     counters_interval_ms: int = 1000       # ... per interval (the rocprof plugin's spin is duty-cycled)
+    counters_kick: str = "start"           # continuous: a tick's PMC read goes out at its start | after_devices
     queue_devices: list = field(default_factory=list)  # GPUs (indices / BDFs) that get the exporter's
                                            # own GPU queue (sentinel + PMC counters); empty = all.
                                            # Each queue pins ~346 MiB of host memory on MI355X.
@@ -99,6 +102,11 @@ class Config:
                 pass  # left as is; validate() reports it
         return host, int(port)
 
+    def metrics_min_interval_s(self) -> float:
+        """Seconds, or -1 for auto (the engine's budget-driven cap)."""
+        v = str(self.metrics_min_interval).strip().lower()
+        return -1.0 if v == "auto" else float(v)
+
     def resolved_backend(self) -> str:
         if self.backend != "auto":
             return self.backend
@@ -114,7 +122,8 @@ class Config:
         ec.mock_devices = int(self.mock_devices)
         ec.device_threads = int(self.device_threads)
         ec.metrics_coalesce = bool(self.metrics_coalesce)
-        ec.metrics_min_interval_s = float(self.metrics_min_interval)
+        ec.metrics_min_interval_s = self.metrics_min_interval_s()
+        ec.metrics_cpu_budget = float(self.metrics_cpu_budget) / 100.0
         ec.host_root = self.host_root
         ec.interval_s = float(self.interval)
         host, port = self.listen_host_port()
@@ -150,6 +159,7 @@ class Config:
         ec.counters_mode = str(self.counters_mode)
         ec.counters_window_ms = int(self.counters_window_ms)
         ec.counters_interval_ms = int(self.counters_interval_ms)
+        ec.counters_kick = str(self.counters_kick)
         ec.enable_rccl = bool(self.enable_rccl)
         ec.rccl_dir = self.rccl_dir
         ec.rccl_verify = bool(self.rccl_verify)
@@ -262,8 +272,15 @@ def validate(cfg: Config) -> None:
         raise ValueError(f"backend must be auto|amdsmi|sysfs|mock, got {cfg.backend}")
     if cfg.series_profile not in ("full", "standard", "compact", "legacy"):
         raise ValueError(f"series_profile must be full|standard|compact|legacy, got {cfg.series_profile}")
-    if cfg.metrics_min_interval < 0:
-        raise ValueError("metrics_min_interval must be >= 0")
+    try:
+        if cfg.metrics_min_interval_s() < 0 and str(cfg.metrics_min_interval).strip().lower() != "auto":
+            raise ValueError
+    except ValueError:
+        raise ValueError(f"metrics_min_interval must be 'auto' or seconds >= 0, got {cfg.metrics_min_interval!r}")
+    if not (0 <= cfg.metrics_cpu_budget <= 100):
+        raise ValueError("metrics_cpu_budget must be a percentage of one core, 0-100 (0 = no cap under auto)")
+    if cfg.counters_kick not in ("start", "after_devices"):
+        raise ValueError(f"counters_kick must be start|after_devices, got {cfg.counters_kick}")
     if cfg.state_interval <= 0:
         raise ValueError("state_interval must be > 0")
     if cfg.ras_interval <= 0:

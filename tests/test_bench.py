@@ -137,3 +137,26 @@ def test_bench_unattributed_rank_fails_loudly():
     assert r.returncode != 0
     assert not _json_lines(r.stdout)
     assert "FAILED: attributed pods" in r.stderr, r.stderr[-2000:]
+
+
+def test_bench_degraded_single_gpu_run_fails_loudly():
+    """At N = 1 too: an exporter that only starts without the PMC counters and the sentinel is
+    a degraded configuration -> exit 1, no result line, the reason on stderr (round 3 printed
+    the headline anyway)."""
+    env = dict(os.environ, GPUEXP_BENCH_FAIL_EXPORTER_WITH_COUNTERS="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--backend", "mock"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 1, r.stderr[-2000:]
+    assert not _json_lines(r.stdout)
+    assert "FAILED: exporter ran degraded" in r.stderr, r.stderr[-2000:]
+
+
+def test_bench_unattributed_single_gpu_fails_loudly():
+    env = dict(os.environ, GPUEXP_BENCH_NO_POD_RANK="0")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--backend", "mock"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 1
+    assert not _json_lines(r.stdout)
+    assert "FAILED: attributed pods" in r.stderr, r.stderr[-2000:]

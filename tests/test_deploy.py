@@ -127,3 +127,77 @@ def test_memory_sized_for_one_queue_per_gpu():
     assert "mul $queueGpus .Values.memoryPerQueueGpuMi" in tpl and "--queue-devices=" in tpl
     cfg = load_config(["--queue-devices", "0,0000:72:00.0"], env={})
     assert cfg.queue_devices == ["0", "0000:72:00.0"]
+
+
+def _hostpaths(spec):
+    return {v["name"]: v["hostPath"] for v in spec.get("volumes", []) if "hostPath" in v}
+
+
+def test_workload_hostpaths_are_created_by_the_daemonset():
+    """Every hostPath a workload example mounts exists once the exporter DaemonSet ran on the
+    node: it is a DaemonSet hostPath volume of type DirectoryOrCreate.  (Round 3 shipped a
+    workload mounting /opt/gpuexp/lib with type Directory that nothing created.)"""
+    (ds,) = docs("daemonset.yaml")
+    ds_spec = ds["spec"]["template"]["spec"]
+    created = {hp["path"] for hp in _hostpaths(ds_spec).values() if hp.get("type") == "DirectoryOrCreate"}
+    checked = 0
+    for f in ("example-workload.yaml", "synthetic-workloads.yaml"):
+        for d in docs(f):
+            spec = d["spec"]["template"]["spec"] if d["kind"] == "Deployment" else d["spec"]
+            for name, hp in _hostpaths(spec).items():
+                assert hp["path"] in created, (f, name, hp)
+                checked += 1
+    assert checked >= 3
+
+
+def test_rccl_tracer_is_installed_where_workloads_load_it():
+    """The init container installs libgpuexp_rccl_tracer.so into the host directory the
+    example workload mounts, and the workload's ROCP_TOOL_LIBRARIES names that file."""
+    from kubernetes_gpu_exporter_amd.utils.install_tracer import TRACER
+    (ds,) = docs("daemonset.yaml")
+    ds_spec = ds["spec"]["template"]["spec"]
+    (init,) = [c for c in ds_spec["initContainers"] if c["name"] == "install-rccl-tracer"]
+    assert init["command"][:3] == ["python3", "-m", "kubernetes_gpu_exporter_amd.utils.install_tracer"]
+    dest = init["command"][3]
+    (m,) = [m for m in init["volumeMounts"] if m["mountPath"] == dest]
+    host_dir = _hostpaths(ds_spec)[m["name"]]["path"]
+    (pod,) = docs("example-workload.yaml")
+    c = pod["spec"]["containers"][0]
+    env = {e["name"]: e["value"] for e in c["env"]}
+    tool = env["ROCP_TOOL_LIBRARIES"]
+    mount_dir, fname = os.path.split(tool)
+    assert fname == TRACER
+    (wm,) = [m for m in c["volumeMounts"] if m["mountPath"] == mount_dir]
+    assert wm.get("readOnly") is True
+    assert _hostpaths(pod["spec"])[wm["name"]]["path"] == host_dir
+    # the Helm chart does the same when rccl.installTracer is on
+    chart = os.path.join(ROOT, "deploy", "helm", "gpuexp")
+    with open(os.path.join(chart, "templates", "daemonset.yaml")) as fh:
+        tpl = fh.read()
+    assert "install-rccl-tracer" in tpl and "kubernetes_gpu_exporter_amd.utils.install_tracer" in tpl
+    with open(os.path.join(chart, "values.yaml")) as fh:
+        values = yaml.safe_load(fh)
+    assert values["rccl"]["installTracer"] is True and values["rccl"]["tracerHostDir"] == host_dir
+
+
+def test_memory_limits_cover_the_read_rescue_worst_case():
+    """Worst case: every queue GPU's PMC reads rescued at once (a node-wide job holding every
+    wave slot): 40 MiB + 8 x (346 MiB queues + 173 MiB rescue queue).  The static limit covers
+    it, and so does the Helm limit for 1..8 queue GPUs."""
+    (ds,) = docs("daemonset.yaml")
+    c = ds["spec"]["template"]["spec"]["containers"][0]
+
+    def mib(q):
+        return int(q[:-2]) * (1024 if q.endswith("Gi") else 1)
+    worst = lambda n: 40 + n * (346 + 173)  # noqa: E731
+    assert mib(c["resources"]["limits"]["memory"]) >= worst(8)
+    chart = os.path.join(ROOT, "deploy", "helm", "gpuexp")
+    with open(os.path.join(chart, "values.yaml")) as fh:
+        v = yaml.safe_load(fh)
+    with open(os.path.join(chart, "templates", "daemonset.yaml")) as fh:
+        tpl = fh.read()
+    assert "mul $queueGpus .Values.memoryPerRescueQueueMi" in tpl
+    assert "add $mem $rescue .Values.resources.memoryLimitHeadroomMi" in tpl
+    for n in range(1, 9):
+        limit = 100 + n * v["memoryPerQueueGpuMi"] + n * v["memoryPerRescueQueueMi"] + v["resources"]["memoryLimitHeadroomMi"]
+        assert limit >= worst(n), (n, limit, worst(n))

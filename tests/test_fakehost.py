@@ -524,6 +524,56 @@ def test_gpu_metrics_min_interval_caps_fresh_reads(native, tmp_path):
     e.stop()
 
 
+def test_devices_stage_split_exported(native, tmp_path):
+    """The devices stage split into its parts (gpuexp_device_read_seconds_total{part}):
+    counters of seconds, the per-GPU parts summed over GPUs.  On the fake host the
+    gpu_metrics and VRAM reads are real file reads (the fetch with an injected 200 us of
+    CPU, the SMU round trip), so those parts advance, and the fetch CPU is accounted per GPU."""
+    mi355x_node(tmp_path, 2)
+    e = _engine(native, tmp_path, series_profile="full", fake_metrics_cost_us=200, metrics_min_interval_s=0.0)
+    try:
+        for k in range(5):
+            e.tick((k + 1) * S)
+        fams = promtext.parse(e.snapshot_text())
+    finally:
+        e.stop()
+    parts = {lab["part"]: v for _, lab, v in promtext.samples(fams, "gpuexp_device_read_seconds_total")}
+    assert set(parts) == {"counters_kick", "control", "gpu_metrics", "vram", "ras", "gtt"}, parts
+    assert parts["gpu_metrics"] >= 5 * 2 * 200e-6, parts
+    assert parts["vram"] > 0 and parts["control"] > 0, parts
+    cpu = {lab["gpu"]: v for _, lab, v in promtext.samples(fams, "gpuexp_gpu_metrics_fetch_cpu_seconds_total")}
+    assert set(cpu) == {"0", "1"} and all(5 * 190e-6 <= v < 5 * 2e-3 for v in cpu.values()), cpu
+    caps = {lab["gpu"]: v for _, lab, v in promtext.samples(fams, "gpuexp_gpu_metrics_min_interval_seconds")}
+    assert caps == {"0": 0.0, "1": 0.0}  # a fixed metrics_min_interval of 0: no cap
+
+
+@pytest.mark.parametrize("n_gpus,want_cap", [(8, 8 * 250e-6 / 0.015), (1, 250e-6 / 0.015)])
+def test_gpu_metrics_auto_interval_holds_cpu_budget(native, tmp_path, n_gpus, want_cap):
+    """metrics_min_interval auto: the fetch cap follows the measured CPU of a fresh read so that
+    all GPUs' SMU fetches together stay within metrics_cpu_budget of one core.  Here each fresh
+    read costs 250 us of CPU (injected) and the budget is 1.5 %: 8 GPUs -> one fetch per GPU per
+    133 ms, 1 GPU -> per 17 ms (under a 100 Hz tick stream: every other tick)."""
+    mi355x_node(tmp_path, n_gpus)
+    e = _engine(native, tmp_path, metrics_min_interval_s=-1.0, metrics_cpu_budget=0.015,
+                fake_metrics_cost_us=250, metrics_coalesce=False)
+    try:
+        for k in range(200):  # 2 s at 100 Hz (manual ticks)
+            e.tick(S + k * 10_000_000)
+        fams = promtext.parse(e.snapshot_text())
+    finally:
+        e.stop()
+    caps = [v for _, _, v in promtext.samples(fams, "gpuexp_gpu_metrics_min_interval_seconds")]
+    assert len(caps) == n_gpus and all(0.95 * want_cap <= c <= 1.3 * want_cap for c in caps), (caps, want_cap)
+    fresh = [v for _, lab, v in promtext.samples(fams, "gpuexp_gpu_metrics_reads_total") if lab["kind"] == "fresh"]
+    cpu = sum(v for _, _, v in promtext.samples(fams, "gpuexp_gpu_metrics_fetch_cpu_seconds_total"))
+    per_gpu_hz = [f / 2.0 for f in fresh]
+    print(f"{n_gpus} GPUs: cap {caps[0] * 1e3:.1f} ms, fresh reads/s per GPU {per_gpu_hz}, fetch CPU "
+          f"{100 * cpu / 2.0:.2f} % of a core")
+    # the first tick of each GPU is fresh (nothing measured yet), then one per cap
+    assert all(f <= 2.0 / want_cap * 1.1 + 2 for f in fresh), fresh
+    assert 100 * cpu / 2.0 <= 1.5 * 1.25, cpu
+
+
 def test_queue_devices_limit_gpu_queues(native, tmp_path):
     """queue_devices picks the GPUs that get the exporter's own GPU queue (sentinel + PMC);
     the others keep every sysfs/amdsmi family."""
@@ -551,14 +601,21 @@ def _loaded_node(root, n_gpus):
     return h
 
 
-def _fakehost_engine(native, root, interval_s):
+# Thread CPU of one fresh gpu_metrics read on MI355X: the kernel busy-waits on the SMU round
+# trip (profiles/r03/read_costs.txt: 206 us idle; profiles/r04/devices_split.txt under the
+# bench's GEMM pod).  Injected per fresh read on the fake host so CPU budgets include it.
+SMU_FETCH_CPU_US = 206
+
+
+def _fakehost_engine(native, root, interval_s, fetch_cost_us=0, device_threads=0):
     c = native.EngineConfig()
+    c.fake_metrics_cost_us = fetch_cost_us
     c.backend = "sysfs"
     c.host_root = str(root)
     c.interval_s = interval_s
     c.serve_http = False
     c.series_profile = "full"
-    c.device_threads = 8  # the per-GPU read pool at every GPU count (1 GPU: reads inline)
+    c.device_threads = device_threads  # 0 = auto (serial); > 1 = the per-GPU read pool
     e = native.Engine(c)
     e.start()
     return e
@@ -595,7 +652,7 @@ def test_sampler_cpu_account_matches_thread_clocks(native, tmp_path):
     against the kernel's own per-thread clocks within 10 %."""
     import time
     _loaded_node(tmp_path, 8)
-    e = _fakehost_engine(native, tmp_path, 0.01)
+    e = _fakehost_engine(native, tmp_path, 0.01, device_threads=8)
     try:
         time.sleep(4.0)
         threads = _threads_cpu_ns(("gpuexp-sampler", "gpuexp-dev"))
@@ -610,16 +667,17 @@ def test_sampler_cpu_account_matches_thread_clocks(native, tmp_path):
     assert 0.9 < account / threads < 1.1, (account, threads)
 
 
-@pytest.mark.parametrize("hz,budget_pct", [(10, 3.0), (100, 30.0)])
+@pytest.mark.parametrize("hz,budget_pct", [(10, 2.5), (100, 10.0)])
 def test_whole_process_cpu_8_gpus(native, tmp_path, hz, budget_pct):
     """Whole-process CPU (getrusage: every thread, user + system) of an 8-GPU fake-host
-    engine, full profile, 4 processes per GPU, at 10 and 100 Hz.  The fake filesystem has no
-    SMU fetch (a real gpu_metrics read adds 120-420 us of kernel time per GPU per fresh read,
-    profiles/r01/kfd_read_costs.txt), so this bounds the exporter's own work."""
+    engine, full profile, 4 processes per GPU, at 10 and 100 Hz, with the measured CPU of a
+    real SMU fetch burnt per fresh gpu_metrics read (SMU_FETCH_CPU_US) and the shipped fetch
+    policy (metrics_min_interval auto, 1.5 % of a core for fetches): the 8-GPU projection of
+    VERDICT r03 task 2 (<= 2.5 % at 10 Hz, <= 10 % at 100 Hz)."""
     import resource
     import time
     _loaded_node(tmp_path, 8)
-    e = _fakehost_engine(native, tmp_path, 1.0 / hz)
+    e = _fakehost_engine(native, tmp_path, 1.0 / hz, fetch_cost_us=SMU_FETCH_CPU_US)
     try:
         time.sleep(1.0)
         r0, t0 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter()
