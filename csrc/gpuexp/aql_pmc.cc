@@ -24,7 +24,7 @@
 // the latest completed window.
 //
 // Event ids are the gfx950 select values of /opt/rocm/share/rocprofiler-sdk/counter_defs.yaml
-// (SQ 93/3/4/147/142, GRBM 2/0, TCC 112/115/113/117) and are checked with
+// (SQ 93/3/4/147/142, GRBM 2/0, TCC 112/115/113/117, SPI 91/120/103/109) and are checked with
 // hsa_ven_amd_aqlprofile_validate_event at init.  TCC is programmed on every channel
 // instance (16 per XCD); SQ and GRBM are broadcast and come back once per SE / XCC.
 #include <execinfo.h>
@@ -79,6 +79,8 @@ const EventDef kGfx950[] = {
     {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 115, kDramWr32},  {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 113, kGmiRd32},
     {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC, 117, kGmiWr32},  {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 2, kSqCycles},
     {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 52, kMopsBf16},    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 56, kMopsF8},
+    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SPI, 91, kSpiResStall}, {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SPI, 120, kSpiLdsFull},
+    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SPI, 103, kSpiWaveFull}, {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SPI, 109, kSpiVgprFull},
 };
 
 struct Agent {
@@ -126,10 +128,17 @@ struct Agent {
   double cum_xm[kMaxXcc] = {}, cum_xg[kMaxXcc] = {};  // continuous, cumulative: per-XCC totals
   std::string last_xsamples;  // debug (GPUEXP_AQLPMC_DEBUG): the last read's MFMA / GRBM samples
   // Read rescue (continuous, cumulative; see rescue_reads): a second queue that only ever
-  // carries read packets, with its own profile, command and output buffers.
+  // carries read packets, with its own profile, command and output buffers.  Temporary:
+  // once the read abandoned on the first queue has run (the queue drains again), reads go
+  // back there, and after kProbationRounds completed reads the rescue queue is destroyed.
   int stuck_rounds = 0;  // consecutive rounds this GPU's read had not completed
-  std::atomic<bool> rescued{false};  // reads go to rq from now on (read by _debug)
-  bool orphan = false;   // the read abandoned on `queue` (its completion, on sig, is ignored)
+  std::atomic<bool> rescued{false};  // reads go to rq now (read by _debug)
+  std::atomic<uint64_t> rescues{0}, releases{0}, rearms{0};  // events so far (read by _debug / _health)
+  bool orphan = false;   // the read abandoned on `queue` has not completed yet (its sig is pending)
+  bool read_on_rq = false;  // the read in flight / last collected went to rq (its output buffer)
+  int probation = 0;     // back on the first queue with rq still alive: completed reads to go
+  bool was_pending = false;  // this round's read was already in flight before the round
+  int zero_grbm = 0;         // consecutive windows in which GRBM_COUNT did not advance
   hsa_queue_t* rq = nullptr;
   hsa_signal_t rsig{};
   hsa_ven_amd_aqlprofile_profile_t rprofile{};
@@ -417,7 +426,11 @@ bool setup_agent(Agent& a, std::string* why) {
   if (g_aql.hsa_ven_amd_aqlprofile_get_info(&probe, HSA_VEN_AMD_AQLPROFILE_INFO_BLOCK_ID, &tcc) != HSA_STATUS_SUCCESS ||
       tcc.instance_count == 0)
     tcc.instance_count = 16;
+  // GPUEXP_PMC_NO_SPI=1: without the SPI occupancy-limiter events (and the fallback below)
+  const char* no_spi = std::getenv("GPUEXP_PMC_NO_SPI");
+  const bool want_spi = !(no_spi && no_spi[0] == '1');
   for (const auto& def : kGfx950) {
+    if (def.block == HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SPI && !want_spi) continue;
     const uint32_t n = def.block == HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC ? tcc.instance_count : 1;
     for (uint32_t i = 0; i < n; ++i) {
       hsa_ven_amd_aqlprofile_event_t ev{def.block, i, def.id};
@@ -460,8 +473,27 @@ bool setup_agent(Agent& a, std::string* why) {
   a.profile.command_buffer = {a.cmd_buf, cmd_size};
   a.profile.output_buffer = {a.out_buf, out_size};
   if (g_aql.hsa_ven_amd_aqlprofile_start(&a.profile, &a.start_pkt) != HSA_STATUS_SUCCESS) {
-    *why = "aqlprofile start packet generation failed";
-    return false;
+    // the SPI block's counters are the newest addition: without them rather than nothing
+    auto spi = [](const hsa_ven_amd_aqlprofile_event_t& e) { return e.block_name == HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SPI; };
+    if (std::any_of(a.events.begin(), a.events.end(), spi)) {
+      std::vector<hsa_ven_amd_aqlprofile_event_t> ev;
+      std::vector<int> ctr;
+      for (size_t i = 0; i < a.events.size(); ++i)
+        if (!spi(a.events[i])) {
+          ev.push_back(a.events[i]);
+          ctr.push_back(a.event_ctr[i]);
+        }
+      a.events.swap(ev);
+      a.event_ctr.swap(ctr);
+      a.profile.events = a.events.data();
+      a.profile.event_count = uint32_t(a.events.size());
+      std::fprintf(stderr, "[aqlpmc] gpu %s: aqlprofile refused the SPI events; counting without them\n",
+                   a.bdf.c_str());
+    }
+    if (g_aql.hsa_ven_amd_aqlprofile_start(&a.profile, &a.start_pkt) != HSA_STATUS_SUCCESS) {
+      *why = "aqlprofile start packet generation failed";
+      return false;
+    }
   }
   crumb("start packet ok");
   if (g_aql.hsa_ven_amd_aqlprofile_stop(&a.profile, &a.stop_pkt) != HSA_STATUS_SUCCESS) {
@@ -514,8 +546,8 @@ bool usable(const Agent* a) { return a && a->ready && !a->broken.load(); }
 bool collect(Agent& a, Accum* acc) {
   *acc = Accum{};
   acc->a = &a;
-  // after a rescue the reads land in the rescue profile's output buffer
-  auto* prof = a.rescued.load() ? &a.rprofile : &a.profile;
+  // a read on the rescue queue lands in the rescue profile's output buffer
+  auto* prof = a.read_on_rq ? &a.rprofile : &a.profile;
   const bool ok = g_aql.hsa_ven_amd_aqlprofile_iterate_data(prof, on_data, acc) == HSA_STATUS_SUCCESS;
   // per-XCC only when every sample of both counters has an XCC, both agree on the XCC count
   // and every XCC has as many SQ samples (SEs) as the first
@@ -589,8 +621,14 @@ void window_all() {
 // counters are chip state, so a read packet from any queue copies the same running totals
 // (cumulative mode only: there a read changes nothing, and the abandoned read on the first
 // queue, which still runs once the sentinel does, is harmless).  The second queue and its
-// context-save area exist only on GPUs that needed them.  GPUEXP_PMC_READ_RESCUE=0 disables.
+// ~173 MiB context-save area exist only while a GPU needs them: when the abandoned read
+// completes (the first queue drains again; measured 0.8 s after a 6 s starvation,
+// profiles/r03/sentinel_starvation.txt) reads return to the first queue, and after
+// kProbationRounds completed reads there the rescue queue is destroyed (end_rescue); a read
+// stuck again during probation moves back to the still-existing rescue queue at once.
+// GPUEXP_PMC_READ_RESCUE=0 disables.
 constexpr int kRescueRounds = 3;
+constexpr int kProbationRounds = 5;
 
 bool rescue_enabled() {
   const char* e = std::getenv("GPUEXP_PMC_READ_RESCUE");
@@ -624,52 +662,97 @@ bool rescue_reads(Agent& a) {
   }
   a.rescued = true;
   a.orphan = true;
+  a.rescues += 1;
   std::fprintf(stderr, "[aqlpmc] gpu %s: counter reads stuck behind a sentinel run the workload leaves no wave "
                "slot for; reads moved to a queue of their own\n", a.bdf.c_str());
   return true;
 }
 
-// Continuous mode, one round: a read packet in flight on every GPU at once, then per GPU
-// the window since its previous read.  Counting itself never pauses (kStops: re-armed
-// right after the read, a gap of one PM4 packet).
+// Releases the rescue queue (its context-save area) once reads run on the first queue again.
+void end_rescue(Agent& a) {
+  if (a.rq) hsa_queue_destroy(a.rq);
+  if (a.rsig.handle) hsa_signal_destroy(a.rsig);
+  if (a.rcmd_buf) hsa_amd_memory_pool_free(a.rcmd_buf);
+  if (a.rout_buf) hsa_amd_memory_pool_free(a.rout_buf);
+  a.rq = nullptr;
+  a.rsig = hsa_signal_t{};
+  a.rcmd_buf = a.rout_buf = nullptr;
+  a.probation = 0;
+  a.releases += 1;
+  std::fprintf(stderr, "[aqlpmc] gpu %s: counter reads complete on the first queue again; rescue queue released\n",
+               a.bdf.c_str());
+}
+
+// Counting restarted from scratch: start packet, then (cumulative) a new baseline read.
+bool arm_continuous(Agent& a);
+
+// A window whose counters went backwards (another profiler reset or re-programmed them) or
+// whose GRBM_COUNT did not advance over real time (counting stopped under us): start the
+// counters again with our own selects.  On the first queue only (a rescued GPU's first
+// queue is stuck; its windows are dropped until the rescue ends).
+void rearm(Agent& a) {
+  if (a.rescued || a.orphan) return;
+  a.rearms += 1;
+  std::fprintf(stderr, "[aqlpmc] gpu %s: counters reset or stopped by someone else; re-armed\n", a.bdf.c_str());
+  if (!arm_continuous(a)) a.broken = true;
+}
+
+// Continuous mode, one round: a read packet in flight on every GPU at once, then each GPU
+// collected as soon as its read completes (one polling loop over all of them, sleeping
+// between looks), so one stuck GPU never delays the others' windows.  A GPU whose read was
+// already pending before this round gets one look, not the round's deadline.  Counting
+// itself never pauses (kStops: re-armed right after the read, a gap of one PM4 packet).
 void read_round() {
   const auto begin = Clock::now();
   uint64_t c0 = own_cpu_ns(), cw = 0, cc = 0;
   // a stalled GPU costs the round at most this long (the other GPUs' reads are in flight)
   const auto deadline = begin + std::chrono::milliseconds(std::min(1000, g_interval_ms));
-  for (Agent* a : g_agents)
-    if (usable(a) && !a->read_inflight) {
+  std::vector<Agent*> waiting;
+  for (Agent* a : g_agents) {
+    if (!usable(a)) continue;
+    if (a->rescued && a->orphan && hsa_signal_load_scacquire(a->sig) < 1) {
+      // the read abandoned on the first queue ran: that queue moves again; reads go back
+      // there (the rescue queue stays until kProbationRounds reads there complete)
+      // (a rescue read still in flight is collected first: read_on_rq keeps its buffer)
+      a->orphan = false;
+      a->rescued = false;
+      a->probation = kProbationRounds;
+    }
+    a->was_pending = a->read_inflight;
+    if (!a->read_inflight) {
       if (a->rescued) {
         hsa_signal_store_relaxed(a->rsig, 1);
         a->t_submit = Clock::now();
         submit_on(*a, a->rq, a->rsig, a->rread_pkt, /*barrier=*/false);
+        a->read_on_rq = true;
       } else {
         post_packet(*a, a->read_pkt, /*barrier=*/false);
+        a->read_on_rq = false;
       }
       a->read_inflight = true;
       a->t_checked = a->t_submit;
     }
+    waiting.push_back(a);
+  }
   const uint64_t c1 = own_cpu_ns();
-  for (Agent* a : g_agents) {
-    if (!usable(a) || !a->read_inflight) continue;
-    const uint64_t w0 = own_cpu_ns();
-    const bool done = wait_signal(a->rescued ? a->rsig : a->sig, deadline);
-    const auto now = Clock::now();
-    const uint64_t w1 = own_cpu_ns();
-    cw += w1 - w0;
-    if (a->queue_error.load()) {
-      a->broken = true;
-      continue;
+
+  auto stuck = [&](Agent* a, Clock::time_point now) {  // still queued: look again next round
+    a->t_checked = now;
+    ++a->stalls;
+    // stuck again while on probation (the rescue queue still exists): back to it at once
+    if (a->read_on_rq || g_read_mode != kCumulative || ++a->stuck_rounds < (a->rq ? 1 : kRescueRounds)) return;
+    if (a->rq) {
+      a->rescued = true;
+      a->orphan = true;
+      a->probation = 0;
+      a->read_inflight = false;
+      a->stuck_rounds = 0;
+    } else if (rescue_enabled() && rescue_reads(*a)) {
+      a->read_inflight = false;
+      a->stuck_rounds = 0;
     }
-    if (!done) {  // still queued: try again next round, the counters keep running
-      a->t_checked = now;
-      ++a->stalls;
-      // the first queue is stuck: the next round reads on a queue of its own
-      if (!a->rescued && g_read_mode == kCumulative && ++a->stuck_rounds >= kRescueRounds && rescue_enabled() &&
-          rescue_reads(*a))
-        a->read_inflight = false;
-      continue;
-    }
+  };
+  auto done = [&](Agent* a, Clock::time_point now) {
     a->read_inflight = false;
     a->stuck_rounds = 0;
     // the read executed between the last time it was seen pending and now
@@ -678,7 +761,8 @@ void read_round() {
     const uint64_t k0 = own_cpu_ns();
     const bool got = collect(*a, &acc);
     cc += own_cpu_ns() - k0;
-    if (!got) continue;
+    if (!a->read_on_rq && a->probation > 0 && --a->probation == 0 && a->rq) end_rescue(*a);
+    if (!got) return;
     const double wall = std::chrono::duration<double>(t - a->t_last).count();
     if (g_read_mode == kCumulative) {
       double d[kNumCtr], xm[kMaxXcc], xg[kMaxXcc];
@@ -697,8 +781,17 @@ void read_round() {
       std::memcpy(a->cum_xg, acc.xg, sizeof(a->cum_xg));
       a->have_cum = true;
       a->t_last = t;
+      // GRBM_COUNT always advances while counting runs: 5 ms of wall time without a cycle
+      // means counting was stopped under us
+      a->zero_grbm = !first && !backwards && d[kGrbmCount] <= 0 && wall > 0.005 ? a->zero_grbm + 1 : 0;
+      const bool stopped = a->zero_grbm >= 2;  // two windows in a row: not a fluke
       if (backwards) ++a->resets;  // wrapped or reset under us: this window is unknown
-      if (!first && !backwards) publish(*a, d, acc, wall, t, acc.v, xm, xg);
+      if (backwards || stopped) {
+        a->zero_grbm = 0;
+        rearm(*a);
+        return;
+      }
+      if (!first) publish(*a, d, acc, wall, t, acc.v, xm, xg);
     } else {
       publish(*a, acc.v, acc, wall, t);
       a->t_last = t;
@@ -708,6 +801,36 @@ void read_round() {
         else a->t_last = ts;
       }
     }
+  };
+
+  for (int i = 0; !waiting.empty(); ++i) {
+    const uint64_t w0 = own_cpu_ns();
+    auto now = Clock::now();
+    for (auto it = waiting.begin(); it != waiting.end();) {
+      Agent* a = *it;
+      if (a->queue_error.load()) {
+        a->broken = true;
+        it = waiting.erase(it);
+        continue;
+      }
+      if (hsa_signal_load_scacquire(a->read_on_rq ? a->rsig : a->sig) < 1) {
+        cw += own_cpu_ns() - w0;
+        done(a, now);
+        it = waiting.erase(it);
+        continue;
+      }
+      if (a->was_pending || now >= deadline) {  // one look for an old read; none past the deadline
+        stuck(a, now);
+        it = waiting.erase(it);
+        continue;
+      }
+      ++it;
+    }
+    if (waiting.empty()) break;
+    now = Clock::now();
+    std::this_thread::sleep_for(std::min<Clock::duration>(std::chrono::microseconds(i == 0 ? 60 : 100),
+                                                          deadline > now ? deadline - now : Clock::duration(0)));
+    cw += own_cpu_ns() - w0;
   }
   g_round_cpu[0] += c1 - c0;
   g_round_cpu[1] += cw;
@@ -1263,6 +1386,21 @@ extern "C" __attribute__((visibility("default"))) void gpuexp_rp_shutdown() {
 
 extern "C" __attribute__((visibility("default"))) const char* gpuexp_rp_status() { return g_status.c_str(); }
 
+// Read health of one GPU (gpuexp::CounterHealth order): stalls, resets, rearms, rescues,
+// rescue releases, rescue active.  0, or -1 for an unknown device.
+extern "C" __attribute__((visibility("default"))) int gpuexp_rp_health(int dev, uint64_t* out, int n) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (dev < 0 || size_t(dev) >= g_agents.size() || !g_agents[size_t(dev)] || n < 6) return -1;
+  const Agent& a = *g_agents[size_t(dev)];
+  out[0] = a.stalls.load();
+  out[1] = a.resets.load();
+  out[2] = a.rearms.load();
+  out[3] = a.rescues.load();
+  out[4] = a.releases.load();
+  out[5] = a.rescued.load() ? 1 : 0;
+  return 0;
+}
+
 extern "C" __attribute__((visibility("default"))) int gpuexp_rp_scope(int dev) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (dev < 0 || size_t(dev) >= g_agents.size() || !g_agents[size_t(dev)]) return -1;
@@ -1284,7 +1422,10 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_debug(int dev, c
                   ";simd=" + std::to_string(a.m.simd) + ";cu=" + std::to_string(a.m.cu) +
                   ";mode=" + (g_continuous ? read_mode_name(g_read_mode) : "duty") + ";window_s=" + win +
                   ";resets=" + std::to_string(a.resets.load()) + ";stalls=" + std::to_string(a.stalls.load()) +
-                  ";rescued=" + (a.rescued.load() ? "1" : "0") + ";";
+                  ";rescued=" + (a.rescues.load() ? "1" : "0") +
+                  ";rescue_active=" + (a.rescued.load() ? "1" : "0") + ";rescues=" + std::to_string(a.rescues.load()) +
+                  ";rescue_releases=" + std::to_string(a.releases.load()) + ";rearms=" + std::to_string(a.rearms.load()) +
+                  ";";
   if (const uint64_t r = g_rounds.load()) {
     char c[160];
     std::snprintf(c, sizeof(c), "rounds=%llu;round_cpu_us_post=%.2f;round_cpu_us_wait=%.2f;round_cpu_us_collect=%.2f;",

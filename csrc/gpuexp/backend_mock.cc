@@ -188,6 +188,11 @@ bool MockBackend::counters(const DeviceInfo& dev, double dt_s, CounterReading* o
   // a bf16 pod at the MFMA busy share of a 2.5 PFLOP/s dense peak unless scripted
   out->mfma_bf16_flops = get(s, "mfma_bf16_flops", 2.5e15 * out->mfma_busy_pct / 100);
   out->mfma_fp8_flops = get(s, "mfma_fp8_flops", 0.0);
+  // occupancy limiters: waves wait for a CU a quarter of the busy time, mostly for LDS
+  out->dispatch_stall_pct = get(s, "dispatch_stall_pct", busy * 0.25);
+  out->lds_limited_pct = get(s, "lds_limited_pct", 80.0);
+  out->wave_limited_pct = get(s, "wave_limited_pct", 10.0);
+  out->vgpr_limited_pct = get(s, "vgpr_limited_pct", 0.0);
   // every XCD equally busy unless scripted ("xcc_mfma_busy_pct" sets them all)
   out->nxcc = int(std::min<uint32_t>(dev.num_xcc, uint32_t(kMaxXcc)));
   for (int x = 0; x < out->nxcc; ++x) out->xcc_mfma_busy_pct[x] = get(s, "xcc_mfma_busy_pct", out->mfma_busy_pct);

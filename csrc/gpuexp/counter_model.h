@@ -9,6 +9,9 @@
 //   GRBM GRBM_GUI_ACTIVE GRBM_COUNT
 //   TCC  TCC_EA0_RDREQ_DRAM_32B TCC_EA0_WRREQ_WRITE_DRAM_32B TCC_EA0_RDREQ_GMI_32B
 //        TCC_EA0_WRREQ_WRITE_GMI_32B
+//   SPI  SPI_RA_RES_STALL_CSN SPI_RA_LDS_CU_FULL_CSN SPI_RA_WAVE_SIMD_FULL_CSN
+//        SPI_RA_VGPR_SIMD_FULL_CSN (the dispatcher's resource allocator: what keeps a compute
+//        wave that is ready to launch from getting a CU -- LDS, wave slots, VGPRs)
 // MFMA / LDS derivations follow the gfx950 formulas of
 // /opt/rocm/share/rocprofiler-sdk/counter_defs.yaml (MfmaUtil, LDS utilisation /
 // bank-conflict ratio).  HBM bytes do NOT use its gfx950 FETCH_SIZE: that formula weighs
@@ -43,6 +46,10 @@ enum Ctr {
   kSqCycles,
   kMopsBf16,  // MFMA work in units of 512 FLOPs (counter_defs.yaml: MFMA FLOPs = MOPS x 512)
   kMopsF8,
+  kSpiResStall,  // arbiter cycles with a compute wave request that fits nowhere
+  kSpiLdsFull,   // per such cycle: CUs whose free LDS cannot take the wave
+  kSpiWaveFull,  // per such cycle: SIMDs with no free wave slot
+  kSpiVgprFull,  // per such cycle: SIMDs with too few free VGPRs
   kNumCtr
 };
 
@@ -53,7 +60,9 @@ inline const char* name(int c) {
                                         "TCC_EA0_RDREQ_DRAM_32B",   "TCC_EA0_WRREQ_WRITE_DRAM_32B",
                                         "TCC_EA0_RDREQ_GMI_32B",    "TCC_EA0_WRREQ_WRITE_GMI_32B",
                                         "SQ_CYCLES",                "SQ_INSTS_VALU_MFMA_MOPS_BF16",
-                                        "SQ_INSTS_VALU_MFMA_MOPS_F8"};
+                                        "SQ_INSTS_VALU_MFMA_MOPS_F8", "SPI_RA_RES_STALL_CSN",
+                                        "SPI_RA_LDS_CU_FULL_CSN",   "SPI_RA_WAVE_SIMD_FULL_CSN",
+                                        "SPI_RA_VGPR_SIMD_FULL_CSN"};
   return kNames[c];
 }
 
@@ -62,7 +71,7 @@ inline bool use_max(int c) { return c == kGuiActive || c == kGrbmCount; }
 
 // Number of derived outputs (the CounterSource ABI: gpuexp_rp_sample fills this many
 // doubles; gpuexp::kCounterOutputs in sources.h).
-constexpr int kNumOut = 13;
+constexpr int kNumOut = 17;
 
 // Per-XCC MFMA busy (gpuexp_rp_sample_xcc): at most this many XCCs per GPU.
 constexpr int kMaxXcc = 16;
@@ -138,6 +147,22 @@ inline void derive(Derived& a, const double* d, const int* inst, double wall) {
   out[9] = d[kGmiWr32] * 32.0 / wall;                                               // remote (GMI) write B/s
   out[11] = d[kMopsBf16] * 512.0 / wall;                                            // bf16 MFMA FLOP/s
   out[12] = d[kMopsF8] * 512.0 / wall;                                              // fp8 MFMA FLOP/s
+  // Occupancy limiters, from the SPI resource allocator (one instance per SE).  out[13]: the
+  // share of the window's cycles in which an SE had a compute wave ready that fit on none of
+  // its CUs.  out[14..16]: over those stalled cycles, the share of the SE's CUs whose LDS was
+  // too full for it / of its SIMDs without a free wave slot / without enough VGPRs, i.e.
+  // what capped residency.  0 when no wave waited (nothing was limited).
+  const double spi = inst[kSpiResStall] > 0 ? inst[kSpiResStall] : 0;
+  const double stall = d[kSpiResStall];
+  out[13] = spi > 0 && d[kGrbmCount] > 0 ? std::min(100.0, 100.0 * stall / (spi * d[kGrbmCount])) : nan;
+  const double cu_se = spi > 0 ? double(a.cu) / spi : 0, simd_se = spi > 0 ? double(a.simd) / spi : 0;
+  auto share = [&](double full, double per_se) {
+    if (spi <= 0 || per_se <= 0) return nan;
+    return stall > 0 ? std::min(100.0, 100.0 * full / (stall * per_se)) : 0.0;
+  };
+  out[14] = share(d[kSpiLdsFull], cu_se);
+  out[15] = share(d[kSpiWaveFull], simd_se);
+  out[16] = share(d[kSpiVgprFull], simd_se);
   a.valid = true;
   a.windows += 1;
 }

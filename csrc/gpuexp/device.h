@@ -85,7 +85,7 @@ struct DeviceSample {
   uint64_t fw_ts_10ns = 0;     // PMFW timestamp (10 ns units), 0 = n/a
   bool metrics_coalesced = false;  // decoded from the cached gpu_metrics table (no SMU fetch)
   // What this sample's reads cost (filled by the backend; the engine's devices-stage split,
-  // gpuexp_device_read_duration_seconds): gpu_metrics wall + thread CPU (a fresh read is an
+  // gpuexp_device_read_seconds_total): gpu_metrics wall + thread CPU (a fresh read is an
   // SMU round trip the kernel busy-waits on; ~0 when coalesced), the VRAM-used file, wall.
   uint64_t metrics_wall_ns = 0, metrics_cpu_ns = 0, vram_wall_ns = 0;
 
@@ -174,6 +174,10 @@ struct CounterReading {
   double remote_write_bps = kNaN;   // TCC_EA0_WRREQ_WRITE_GMI_32B * 32 B / dt
   double mfma_bf16_flops = kNaN;    // SQ_INSTS_VALU_MFMA_MOPS_BF16 * 512 / dt
   double mfma_fp8_flops = kNaN;     // SQ_INSTS_VALU_MFMA_MOPS_F8 * 512 / dt
+  // occupancy limiters (SPI resource allocator, counter_model.h): share of cycles a ready
+  // compute wave fit nowhere; over those cycles, share of CUs LDS-full / SIMDs wave-slot-full /
+  // SIMDs VGPR-full
+  double dispatch_stall_pct = kNaN, lds_limited_pct = kNaN, wave_limited_pct = kNaN, vgpr_limited_pct = kNaN;
   // mfma_busy_pct of each XCC (its SQ instances over its own GRBM_COUNT x its SIMDs);
   // nxcc = 0 when the counter source cannot attribute samples to XCCs
   int nxcc = 0;

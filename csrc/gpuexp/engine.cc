@@ -207,6 +207,15 @@ void Engine::define_families() {
   f_mfma_flops_ = add("amd_gpu_mfma_flops_per_second",
                       "Matrix-core work done, by operand type: FLOP/s over the last tick "
                       "(SQ_INSTS_VALU_MFMA_MOPS_<type> x 512)", G, with(D, {"dtype"}));
+  f_disp_stall_ = add("amd_gpu_dispatch_stall_percent",
+                      "Share of the time a compute wave ready to launch fitted on no CU of its shader engine "
+                      "(SPI resource allocator; device-wide only, full profile)",
+                      G, D);
+  f_occ_lim_ = add("amd_gpu_occupancy_limiter_percent",
+                   "While compute waves waited for a CU: the share of CUs whose free LDS could not take the "
+                   "wave (resource=lds: LDS occupancy), of SIMDs without a free wave slot (wave_slots) or "
+                   "without enough free VGPRs (vgpr); 0 when no wave waited (device-wide only, full profile)",
+                   G, with(D, {"resource"}));
   f_sq_busy_ = add("amd_gpu_sq_busy_percent", "Shader sequencer busy (SQ_BUSY_CYCLES)", G, D);
   f_gui_ = add("amd_gpu_gui_active_percent", "Graphics pipe active (GRBM_GUI_ACTIVE / GRBM_COUNT)", G, D);
   f_waves_ = add("amd_gpu_waves_per_second", "Waves dispatched per second (SQ_WAVES)", G, D);
@@ -393,6 +402,15 @@ void Engine::define_families() {
                          "Ticks that exported the previous counter window because this tick's PMC read had not "
                          "completed within counters_sync_us (continuous counters)",
                          C, {});
+  f_self_ctr_events_ = add("gpuexp_counters_events_total",
+                           "PMC read health per GPU: read_stall (a read still queued at the round's end), "
+                           "reset (a window dropped: counters went backwards), rearm (counting restarted after "
+                           "another profiler reset or stopped it), rescue / rescue_release (reads moved to a "
+                           "queue of their own behind a starved sentinel run, and back)",
+                           C, {"gpu", "event"});
+  f_self_ctr_rescue_ = add("gpuexp_counters_rescue_active",
+                           "1 while a GPU's PMC reads run on a rescue queue (+173 MiB pinned while it lasts)", G,
+                           {"gpu"});
   f_self_ctr_scope_ = add("gpuexp_counters_device_scope",
                           "1 if wave/LDS/HBM PMC counters see every process on the GPU, 0 if they are "
                           "VMID-filtered to the exporter (not exported then)",
@@ -1093,8 +1111,24 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
         dput(st, i, st.mflops[1], f_mfma_flops_, {"fp8"}, cr.mfma_fp8_flops, gen);
         st.flops_last[0] = cr.mfma_bf16_flops;
         st.flops_last[1] = cr.mfma_fp8_flops;
+        // what capped residency (SPI resource allocator; VMID-filtered like the SQ waves
+        // unless profiles/r04/spi_scope.txt shows otherwise)
+        static const char* kRes[3] = {"lds", "wave_slots", "vgpr"};
+        const double lim[3] = {cr.lds_limited_pct, cr.wave_limited_pct, cr.vgpr_limited_pct};
+        dput(st, i, st.disp_stall, f_disp_stall_, {}, cr.dispatch_stall_pct, gen);
+        for (int k = 0; k < 3; ++k) dput(st, i, st.occ_lim[k], f_occ_lim_, {kRes[k]}, lim[k], gen);
       }
     }
+  }
+  CounterHealth ch;
+  if (counters_ && cfg_.series_profile == "full" && counters_->health(i, &ch)) {
+    static const char* kEv[5] = {"read_stall", "reset", "rearm", "rescue", "rescue_release"};
+    const uint64_t v[5] = {ch.stalls, ch.resets, ch.rearms, ch.rescues, ch.releases};
+    for (int k = 0; k < 5; ++k)
+      cput(st.ctr_health[k], f_self_ctr_events_, double(v[k]), gen,
+           [&] { return std::vector<std::string>{std::to_string(d.index), kEv[k]}; });
+    cput(st.ctr_health[5], f_self_ctr_rescue_, ch.rescue_active ? 1 : 0, gen,
+         [&] { return std::vector<std::string>{std::to_string(d.index)}; });
   }
   SentinelReading sr;
   bool have_sen = false;

@@ -216,7 +216,8 @@ class Engine {
         energy, temp[9], clk[3], xrd[kMaxXgmiLinks], xwr[kMaxXgmiLinks], xrd_rate, xwr_rate,
         links_up, pcie_bw, pcie_replay, pcie_speed, pcie_width, thr[5], nprocs, cu_occ, ctr[10],
         sen[4], ecc[3], aer[3], nak[2], recov, xgmi_w, xgmi_s, xclk[kMaxXcc], sen_xlat[kMaxXcc], sen_mem, sen_xmem[kMaxXcc],
-        kev[std::size(kKfdSubscribed)], pages[3], gtt_used, gtt_total, board, mfma_util, xmfma[kMaxXcc], sen_pend, mflops[2];
+        kev[std::size(kKfdSubscribed)], pages[3], gtt_used, gtt_total, board, mfma_util, xmfma[kMaxXcc], sen_pend, mflops[2],
+        disp_stall, occ_lim[3], ctr_health[6];
     std::vector<SeriesRef> fw;  // amd_gpu_firmware_info, one per component
     uint64_t kfd_events[kKfdEventIds] = {};  // KFD SMI events seen on this GPU, by id
     uint64_t errors = 0;
@@ -367,6 +368,7 @@ class Engine {
   int f_proc_vram_, f_proc_cu_, f_proc_sdma_, f_proc_evicted_, f_proc_gfx_;
   int f_legacy_mem_ = -1, f_legacy_perc_ = -1;
   int f_pod_mfma_ = -1, f_pod_hbm_ = -1, f_pod_flops_ = -1;
+  int f_disp_stall_ = -1, f_occ_lim_ = -1, f_self_ctr_events_ = -1, f_self_ctr_rescue_ = -1;
   int f_pod_vram_, f_pod_procs_, f_pod_gpus_, f_pod_xrd_, f_pod_xwr_, f_pod_power_, f_pod_gfx_, f_pod_gfx_share_,
       f_pod_energy_ = -1, f_pod_xrd_total_ = -1, f_pod_xwr_total_ = -1, f_pod_alloc_s_ = -1, f_pod_busy_s_ = -1;
   int f_rccl_calls_, f_rccl_bytes_, f_rccl_comm_;

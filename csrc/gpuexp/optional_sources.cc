@@ -38,6 +38,7 @@ using rp_kick_fn = void (*)();
 using rp_cpu_fn = uint64_t (*)();
 using rp_sample_xcc_fn = int (*)(int, double*, int);
 using rp_sync_fn = int (*)(int timeout_us);
+using rp_health_fn = int (*)(int dev, uint64_t* out, int n);
 
 class PluginCounters : public CounterSource {
  public:
@@ -75,6 +76,7 @@ class PluginCounters : public CounterSource {
     }
     cpu_ = reinterpret_cast<rp_cpu_fn>(::dlsym(handle_, "gpuexp_rp_cpu_ns"));
     sample_xcc_ = reinterpret_cast<rp_sample_xcc_fn>(::dlsym(handle_, "gpuexp_rp_sample_xcc"));  // optional
+    health_ = reinterpret_cast<rp_health_fn>(::dlsym(handle_, "gpuexp_rp_health"));  // optional
     // ABI: a BDF prefixed with '-' reserves that device's HSA agent (partition order) but
     // gets no queue.
     std::vector<std::string> names;
@@ -109,11 +111,27 @@ class PluginCounters : public CounterSource {
     out->remote_write_bps = v[9];
     out->mfma_bf16_flops = v[11];
     out->mfma_fp8_flops = v[12];
+    out->dispatch_stall_pct = v[13];
+    out->lds_limited_pct = v[14];
+    out->wave_limited_pct = v[15];
+    out->vgpr_limited_pct = v[16];
     out->nxcc = sample_xcc_ ? std::max(0, sample_xcc_(dev, out->xcc_mfma_busy_pct, kMaxXcc)) : 0;
     return true;
   }
 
   int scope(int dev) override { return started_ && scope_fn_ ? scope_fn_(dev) : -1; }
+
+  bool health(int dev, CounterHealth* out) override {
+    uint64_t v[6] = {};
+    if (!started_ || !health_ || health_(dev, v, 6) != 0) return false;
+    out->stalls = v[0];
+    out->resets = v[1];
+    out->rearms = v[2];
+    out->rescues = v[3];
+    out->releases = v[4];
+    out->rescue_active = v[5] != 0;
+    return true;
+  }
 
   void kick() override {
     if (started_ && kick_) kick_();
@@ -142,6 +160,7 @@ class PluginCounters : public CounterSource {
   rp_sync_fn sync_ = nullptr;
   rp_cpu_fn cpu_ = nullptr;
   rp_sample_xcc_fn sample_xcc_ = nullptr;
+  rp_health_fn health_ = nullptr;
   void* handle_ = nullptr;
   rp_init_fn init_ = nullptr;
   rp_sample_fn sample_ = nullptr;

@@ -32,7 +32,16 @@ std::unique_ptr<SentinelSource> make_queue_sentinel(const std::string& counters_
 std::string default_rocprof_plugin();
 
 // Derived values a counter plugin's gpuexp_rp_sample fills, in CounterReading order.
-constexpr int kCounterOutputs = 13;
+constexpr int kCounterOutputs = 17;
+
+// Health of a GPU's counter reads (continuous mode), cumulative: reads found still queued,
+// windows dropped because the counters went backwards, re-arms after another profiler reset
+// or stopped them, moves to a rescue queue and its releases; rescue_active = reads are on the
+// rescue queue now.
+struct CounterHealth {
+  uint64_t stalls = 0, resets = 0, rearms = 0, rescues = 0, releases = 0;
+  bool rescue_active = false;
+};
 
 class CounterSource {
  public:
@@ -55,6 +64,11 @@ class CounterSource {
   virtual int scope(int dev) {
     (void)dev;
     return -1;
+  }
+  virtual bool health(int dev, CounterHealth* out) {
+    (void)dev;
+    (void)out;
+    return false;
   }
   virtual void stop() = 0;
   virtual std::string status() const = 0;

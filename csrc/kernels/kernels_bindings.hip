@@ -18,6 +18,7 @@ hipError_t launch_gemm_bf16_tn(const void* A, const void* B, void* C, int M, int
 hipError_t launch_fill_bf16(void* p, size_t n, uint32_t seed, hipStream_t stream);
 hipError_t launch_stream_copy(const void* src, void* dst, size_t bytes, int blocks, hipStream_t stream);
 hipError_t launch_lds_probe(float* out, int blocks, int iters, int stride, hipStream_t stream);
+hipError_t launch_occupancy_hog(int kind, float* out, int blocks, double seconds, hipStream_t stream);
 hipError_t launch_mfma_duty(float* out, uint64_t* counts, int blocks, double duty, double period_s, double seconds,
                             uint32_t xcc_mask, hipStream_t stream);
 }  // namespace gpuexp
@@ -96,6 +97,15 @@ PYBIND11_MODULE(_gpuexp_kernels, m) {
      "256-thread blocks alternating back-to-back v_mfma_f32_32x32x16_bf16 (duty x period) with s_sleep, for "
      "`seconds` (s_memrealtime-timed); 2 blocks per CU = 2 waves per SIMD keep the matrix cores busy `duty` of "
      "the wall time.  xcc_mask != 0: only blocks on those XCCs (HW_REG_XCC_ID) run, the rest exit at once");
+  m.def("occupancy_hog", [](int kind, uintptr_t out, int blocks, double seconds, uintptr_t stream) {
+    // `out` >= blocks floats (checked by the Python wrapper)
+    check(gpuexp::launch_occupancy_hog(kind, reinterpret_cast<float*>(out), blocks, seconds,
+                                       reinterpret_cast<hipStream_t>(stream)),
+          "occupancy_hog launch");
+  }, py::call_guard<py::gil_scoped_release>(), py::arg("kind"), py::arg("out"), py::arg("blocks"),
+     py::arg("seconds"), py::arg("stream") = 0,
+     "Blocks that hold a resource for `seconds` each: kind 0 = 1 wave + 64 KiB LDS per block (LDS-limited), "
+     "kind 1 = 8 waves per block, no LDS (wave-slot-limited)");
   m.def("gemm_burn", [](int device, int M, int N, int K, double seconds, int iters_per_sync, int variant) {
     // Torch-free synthetic GEMM pod: keeps one GPU busy for `seconds` and reports the
     // achieved bf16 TFLOP/s (random operands).

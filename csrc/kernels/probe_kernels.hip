@@ -19,7 +19,45 @@ __global__ __launch_bounds__(kProbeBlock) void lds_probe_kernel(CalibLdsArgs a) 
 
 __global__ __launch_bounds__(kProbeBlock) void mfma_duty_kernel(CalibMfmaArgs a) { mfma_duty_body(a); }
 
+// Occupancy-limiter calibration (tools/probe_spi_scope.py, amd_gpu_occupancy_limiter_percent):
+// blocks that only hold resources for `ticks` of the 100 MHz s_memrealtime clock, launched in
+// more generations than fit, so ready waves queue in the dispatcher for a known reason.
+//   lds:   1 wave per block + 64 KiB of LDS: LDS (160 KiB per CU) admits 2 blocks = 2 waves per
+//          CU while 30 wave slots stay free -> the limiter is LDS
+//   waves: 8 waves per block, no LDS, few VGPRs: 4 blocks fill a CU's 32 wave slots -> the
+//          limiter is wave slots
+constexpr int kHogLdsBytes = 64 * 1024;
+
+__device__ inline void hold_for(uint64_t ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+__global__ __launch_bounds__(64) void occupancy_hog_lds_kernel(float* out, uint64_t ticks) {
+  __shared__ float lds[kHogLdsBytes / sizeof(float)];
+  const int t = int(threadIdx.x);
+  for (int i = t; i < kHogLdsBytes / int(sizeof(float)); i += 64) lds[i] = float(i + blockIdx.x);
+  __syncthreads();
+  hold_for(ticks);
+  // the allocation must be live: one value read back per block
+  if (t == 0) out[blockIdx.x] = lds[(blockIdx.x * 97) % (kHogLdsBytes / sizeof(float))];
+}
+
+__global__ __launch_bounds__(512) void occupancy_hog_waves_kernel(float* out, uint64_t ticks) {
+  hold_for(ticks);
+  if (threadIdx.x == 0) out[blockIdx.x] = float(blockIdx.x);
+}
+
 }  // namespace
+
+hipError_t launch_occupancy_hog(int kind, float* out, int blocks, double seconds, hipStream_t stream) {
+  if (!out || blocks < 1 || blocks > (1 << 20) || !(seconds > 0) || seconds > 10 || (kind != 0 && kind != 1))
+    return hipErrorInvalidValue;
+  const uint64_t ticks = uint64_t(seconds * 1e8);
+  if (kind == 0) hipLaunchKernelGGL(occupancy_hog_lds_kernel, dim3(blocks), dim3(64), 0, stream, out, ticks);
+  else hipLaunchKernelGGL(occupancy_hog_waves_kernel, dim3(blocks), dim3(512), 0, stream, out, ticks);
+  return hipGetLastError();
+}
 
 // Host checks (the kernel's loop relies on them): period > 0, on <= period, a bounded run.
 hipError_t launch_mfma_duty(float* out, uint64_t* counts, int blocks, double duty, double period_s, double seconds,

@@ -100,3 +100,20 @@ def mfma_duty(device: int, duty: float, seconds: float, period_s: float = 0.002,
     kernels().mfma_duty(out.data_ptr(), counts.data_ptr(), blocks, float(duty), float(period_s), float(seconds), s,
                         int(xcc_mask))
     return out, counts
+
+
+def occupancy_hog(device: int, kind: str, seconds: float, generations: int = 4, stream=None):
+    """Launches blocks that each hold a resource for `seconds` (non-blocking), `generations`
+    times as many as fit at once, so ready waves queue in the dispatcher for a known reason:
+    kind "lds" = 1 wave + 64 KiB LDS per block (2 per CU fit: LDS-limited), "waves" = 8 waves
+    per block, no LDS (4 per CU fit: wave-slot-limited).  Returns the sink tensor."""
+    import torch
+    if kind not in ("lds", "waves") or not (0 < seconds <= 10) or not (1 <= generations <= 64):
+        raise ValueError("kind lds|waves, 0 < seconds <= 10, 1 <= generations <= 64")
+    dev = torch.device(f"cuda:{device}")
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    blocks = cus * (2 if kind == "lds" else 4) * generations
+    out = torch.zeros(blocks, dtype=torch.float32, device=dev)
+    s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    kernels().occupancy_hog(0 if kind == "lds" else 1, out.data_ptr(), blocks, float(seconds), s)
+    return out

@@ -856,6 +856,12 @@ def test_xcc_mfma_busy_calibration():
     # the counter reads held behind that run moved to a queue of their own (read rescue):
     # MFMA busy kept being exported through the starvation, near 100 %
     assert st["rescued"] == "1", st
+    # ... temporarily: once the first queue drains, reads return there and the rescue queue
+    # (its 173 MiB context save area) is released; the process's RSS returns to within
+    # 10 MiB of where it was before the starvation
+    assert st["rescue_active_after"] == "0" and st["rescues"] == st["rescue_releases"], st
+    rss = st["rss_mib"]
+    assert abs(rss["after"] - rss["before"]) <= 10.0, rss
     during = st["busy_during"][8:]  # from 0.8 s on (3 stuck rounds + the move)
     assert sum(v is not None for v in during) >= 0.8 * len(during), st
     # near 100 % while the grid runs; the grid's blocks run in generations (every wave slot

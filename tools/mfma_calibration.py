@@ -215,6 +215,11 @@ def main() -> int:
                 return p, val(fams, "amd_gpu_mfma_busy_percent", gpu=0)
             return p
         ticks = []
+
+        def rss_mib():  # this process holds the engine, so its queues' pinned areas
+            with open("/proc/self/status") as fh:
+                return int([l for l in fh if l.startswith("VmRSS:")][0].split()[1]) / 1024.0
+        rss = {"before": rss_mib()}
         time.sleep(0.3)
         before = pend()
         cus = torch.cuda.get_device_properties(0).multi_processor_count
@@ -223,17 +228,35 @@ def main() -> int:
         mfma_duty(0, 1.0, args.starve, period_s=0.002, blocks=8 * cus)
         ev.record()
         seen, busy = [], []
+        rss_during = []
         while not ev.query() and time.perf_counter() - t0 < 4 * args.starve + 5:
             time.sleep(0.1)
             p, b = pend(True)
             seen.append(p)
             busy.append(b)
+            rss_during.append(rss_mib())
         torch.cuda.synchronize()
         run_s = time.perf_counter() - t0
         time.sleep(0.5)
+        # the rescue queue is released once reads complete on the first queue again
+        # (kProbationRounds ticks after the abandoned read ran): wait for that, bounded
+        t_rel = time.perf_counter()
+        while time.perf_counter() - t_rel < 5.0:
+            kv = dict(x.split("=", 1) for x in raw().split(";") if "=" in x)
+            if kv.get("rescue_active") == "0" and kv.get("rescues") == kv.get("rescue_releases"):
+                break
+            time.sleep(0.1)
+        released_after_s = round(time.perf_counter() - t_rel + 0.5, 2)
+        time.sleep(0.3)
+        rss["during_max"] = max(rss_during) if rss_during else None
+        rss["after"] = rss_mib()
         kv = dict(x.split("=", 1) for x in raw().split(";") if "=" in x)
         res["cases"]["starve"] = {"seconds": args.starve, "kernel_s": run_s, "pending_before": before,
                                   "pmc_read_stalls": int(kv.get("stalls", -1)), "rescued": kv.get("rescued"),
+                                  "rescue_active_after": kv.get("rescue_active"), "rescues": kv.get("rescues"),
+                                  "rescue_releases": kv.get("rescue_releases"),
+                                  "released_after_kernel_s": released_after_s,
+                                  "rss_mib": {k: round(v, 1) if v is not None else None for k, v in rss.items()},
                                   "busy_during": [round(v, 2) if v is not None else None for v in busy],
                                   "ticks_during": ticks,
                                   "pending_during": [round(v, 3) if v is not None else None for v in seen],
