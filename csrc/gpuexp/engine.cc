@@ -337,6 +337,11 @@ void Engine::define_families() {
   // --- exporter self-metrics (own prefix; the reference registry had none, main.go:40) ---
   f_self_build_ = add("gpuexp_build_info", "Exporter build and backend", G, {"version", "backend"});
   f_self_ticks_ = add("gpuexp_ticks_total", "Sampler ticks completed", C, {});
+  f_self_pods_complete_ = add("gpuexp_pod_list_complete",
+                              "1 if the applied pod list came from a refresh in which every metadata source "
+                              "answered (per-pod totals of pods missing from it are dropped at once); 0: a source "
+                              "failed, and totals of missing pods are kept for pod_totals_ttl (1 h)",
+                              G, {});
   f_self_startup_ = add("gpuexp_startup_seconds",
                         "Engine start to its first sample: backend init (amdsmi + raw-path validation), one "
                         "HSA queue per GPU with PMC programs and sentinel, plugin probes",
@@ -737,8 +742,12 @@ void Engine::emit_kfd_events(uint64_t gen) {
   for (auto& kv : pods_by_uid_) live.emplace(kv.second.ns, kv.second.name);
   for (auto it = pod_kfd_events_.begin(); it != pod_kfd_events_.end();) {
     const auto& k = it->first;
-    // restored from the state file while the pod list is not here yet: keep (and export)
-    if (pods_complete_ && !live.count({std::get<0>(k), std::get<1>(k)})) {
+    // restored from the state file while the pod list is not here yet: keep (and export);
+    // gone from a complete list, or from every partial one for the TTL: drop
+    const std::pair<std::string, std::string> pk{std::get<0>(k), std::get<1>(k)};
+    auto lk = pod_last_known_ns_.find(pk);
+    const bool expired = lk != pod_last_known_ns_.end() && mono_ns() - lk->second > uint64_t(cfg_.pod_totals_ttl_s * 1e9);
+    if (!live.count(pk) && (pods_complete_ || expired)) {
       it = pod_kfd_events_.erase(it);
       continue;
     }
@@ -1302,7 +1311,12 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
           pa.xrd_b += xgmi_rd_b * f;
           pa.xwr_b += xgmi_wr_b * f;
         }
-        if (shared && !std::isnan(tick_s) && !std::isnan(busy_frac) && !std::isnan(f)) pa.busy_s += busy_frac * tick_s * f;
+        // a shared GPU's time is split like its busy time, so busy <= allocated for every pod
+        // (the rules' busy / allocated ratio stays a ratio)
+        if (shared && !std::isnan(tick_s) && !std::isnan(f)) {
+          pa.alloc_s += tick_s * f;
+          if (!std::isnan(busy_frac)) pa.busy_s += busy_frac * tick_s * f;
+        }
         if (!std::isnan(share)) {
           pa.gfx_share += share;
           pa.share_known = true;
@@ -1418,8 +1432,22 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
   {
     std::set<std::pair<std::string, std::string>> known;
     for (auto& kv : pods_by_uid_) known.emplace(kv.second.ns, kv.second.name);
+    // A pod's totals go when a complete pod list no longer has it -- or, while refreshes stay
+    // partial (a metadata source keeps failing), once no applied list has had it for
+    // pod_totals_ttl_s (so the maps and the state file cannot grow with every pod ever run).
+    const uint64_t now_ns = mono_ns();
+    auto gone = [&](const std::pair<std::string, std::string>& k) {
+      if (known.count(k)) return false;
+      if (pods_complete_) return true;
+      auto it = pod_last_known_ns_.find(k);
+      if (it == pod_last_known_ns_.end()) {  // restored from the state file, never listed yet
+        pod_last_known_ns_[k] = now_ns;
+        return false;
+      }
+      return now_ns - it->second > uint64_t(cfg_.pod_totals_ttl_s * 1e9);
+    };
     for (auto it = pod_energy_j_.begin(); it != pod_energy_j_.end();) {
-      if (pods_complete_ && !known.count(it->first)) {
+      if (gone(it->first)) {
         it = pod_energy_j_.erase(it);
         continue;
       }
@@ -1427,7 +1455,7 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
       ++it;
     }
     for (auto it = pod_xgmi_.begin(); it != pod_xgmi_.end();) {
-      if (pods_complete_ && !known.count(it->first)) {
+      if (gone(it->first)) {
         it = pod_xgmi_.erase(it);
         continue;
       }
@@ -1436,7 +1464,7 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
       ++it;
     }
     for (auto it = pod_gpu_s_.begin(); it != pod_gpu_s_.end();) {
-      if (pods_complete_ && !known.count(it->first)) {
+      if (gone(it->first)) {
         it = pod_gpu_s_.erase(it);
         continue;
       }
@@ -1444,6 +1472,11 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
       table_.put(f_pod_busy_s_, {it->first.first, it->first.second}, it->second.second, gen);
       ++it;
     }
+    for (auto it = pod_last_known_ns_.begin(); it != pod_last_known_ns_.end();)
+      it = !known.count(it->first) && !pod_energy_j_.count(it->first) && !pod_xgmi_.count(it->first) &&
+                   !pod_gpu_s_.count(it->first)
+               ? pod_last_known_ns_.erase(it)
+               : std::next(it);
   }
   if (rccl_) {
     std::vector<RcclTotals> tot;
@@ -1491,6 +1524,7 @@ void Engine::emit_self(uint64_t gen) {
   }
   cput(self_refs_[3], f_self_overruns_, double(s.overruns), gen, none);
   cput(self_refs_[4], f_self_unresolved_, double(unresolved_.size()), gen, none);
+  cput(pods_complete_ref_, f_self_pods_complete_, pods_complete_ ? 1 : 0, gen, none);
   cput(self_refs_[5], f_self_render_bytes_, double(s.render_bytes), gen, none);
   cput(self_refs_[6], f_self_series_, double(s.series), gen, none);
   cput(self_refs_[7], f_self_cpu_, double(s.sampler_cpu_ns) * 1e-9, gen, none);
@@ -1634,6 +1668,8 @@ void Engine::tick_locked(uint64_t now) {
       // file) are garbage-collected against a pod list only if that list is complete: a
       // refresh in which a source failed must not wipe them
       pods_complete_ = pending_complete_;
+      const uint64_t applied = mono_ns();
+      for (auto& kv : pods_by_uid_) pod_last_known_ns_[{kv.second.ns, kv.second.name}] = applied;
     }
   }
   part[1] = mono_ns() - c0;

@@ -116,6 +116,9 @@ struct EngineConfig {
   // at stop (write + rename), read at start.
   std::string state_file;
   double state_interval_s = 10.0;
+  // Per-pod totals of a pod that no applied pod list has had for this long are dropped even
+  // while the lists are partial (a metadata source keeps failing); complete lists drop at once.
+  double pod_totals_ttl_s = 3600.0;
   std::string kfd_path = "/dev/kfd";   // the device node itself (not under host_root)
   bool force_amdsmi_metrics = false;
   int gzip_level = 1;
@@ -348,6 +351,10 @@ class Engine {
   std::map<std::pair<std::string, std::string>, std::pair<double, double>> pod_xgmi_;
   // (ns, pod) -> (GPU-seconds allocated, GPU-seconds busy) so far (state file: pod_gpu_seconds)
   std::map<std::pair<std::string, std::string>, std::pair<double, double>> pod_gpu_s_;
+  // (ns, pod) -> last time an applied pod list had it (GC of per-pod totals under partial lists)
+  std::map<std::pair<std::string, std::string>, uint64_t> pod_last_known_ns_;
+  SeriesRef pods_complete_ref_;
+  int f_self_pods_complete_ = -1;
   SeriesRef self_refs_[21];
 
   // stats (guarded by stats_mu_)

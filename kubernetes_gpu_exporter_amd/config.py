@@ -62,6 +62,8 @@ class Config:
     firmware_info: bool = True             # full profile: amd_gpu_firmware_info per loaded firmware
     state_file: str = ""                   # checkpoint of per-pod energy / KFD event totals ("" = off)
     state_interval: float = 10.0           # seconds between checkpoint writes (and one at shutdown)
+    pod_totals_ttl: float = 3600.0         # per-pod totals of a pod absent from every (partial) pod list
+                                           # this long are dropped (complete lists drop them at once)
     kfd_path: str = "/dev/kfd"             # the device node (mounted directly, not under host_root)
     enable_rccl: bool = False
     rccl_dir: str = "/var/run/gpuexp/rccl"
@@ -167,6 +169,7 @@ class Config:
         ec.firmware_info = bool(self.firmware_info)
         ec.state_file = self.state_file
         ec.state_interval_s = float(self.state_interval)
+        ec.pod_totals_ttl_s = float(self.pod_totals_ttl)
         ec.kfd_path = self.kfd_path
         ec.gc_after = int(self.gc_after)
         ec.device_filter = [int(d) for d in self.devices if ":" not in str(d)]
@@ -283,6 +286,8 @@ def validate(cfg: Config) -> None:
         raise ValueError(f"counters_kick must be start|after_devices, got {cfg.counters_kick}")
     if cfg.state_interval <= 0:
         raise ValueError("state_interval must be > 0")
+    if cfg.pod_totals_ttl <= 0:
+        raise ValueError("pod_totals_ttl must be > 0")
     if cfg.ras_interval <= 0:
         raise ValueError("ras_interval must be > 0")
     if cfg.process_source not in ("auto", "kfd", "amdsmi", "none"):

@@ -605,3 +605,54 @@ def test_mfma_flops_by_type_per_gpu_and_pod(native, mock_engine):
     e2.tick(S)
     e2.tick(2 * S)
     assert "amd_gpu_mfma_flops_per_second" not in promtext.parse(e2.snapshot_text())
+
+
+def test_pod_gpu_seconds_on_a_shared_gpu(native, mock_engine):
+    """A GPU no device plugin owns, used by two pods' processes 3:1 by CU occupancy: each pod is
+    credited that share of the GPU's time as allocated AND of its busy time, so busy <= allocated
+    for both (round 3 credited busy only: busy / allocated was +Inf for such pods)."""
+    uids = {p: f"00000000-0000-4000-8000-0000000000d{i}" for i, p in enumerate("ab", 1)}
+    cids = {p: p * 64 for p in "ab"}
+    e = mock_engine(1)
+    e.set_pods([{"uid": uids[p], "namespace": "ns", "name": f"pod-{p}", "containers": {cids[p]: "w"}} for p in "ab"])
+    e.set_pid_cgroup(100, kubepods_cgroup(uids["a"], cids["a"]))
+    e.set_pid_cgroup(200, kubepods_cgroup(uids["b"], cids["b"]))
+    e.mock_set_processes(0, [{"pid": 100, "vram_bytes": 1 << 30, "cu_occupancy": 48, "name": "a"},
+                             {"pid": 200, "vram_bytes": 1 << 30, "cu_occupancy": 16, "name": "b"}])
+    for t in range(1, 6):  # 4 one-second ticks after the first
+        e.tick(t * S)
+    fams = promtext.parse(e.snapshot_text())
+    alloc = {s[1]["pod"]: s[2] for s in promtext.samples(fams, "amd_pod_gpu_allocated_seconds_total")}
+    busy = {s[1]["pod"]: s[2] for s in promtext.samples(fams, "amd_pod_gpu_busy_seconds_total")}
+    assert alloc["pod-a"] == pytest.approx(4 * 0.75) and alloc["pod-b"] == pytest.approx(4 * 0.25)
+    for p in ("pod-a", "pod-b"):
+        assert 0 < busy[p] <= alloc[p], (p, busy, alloc)
+
+
+def test_pod_totals_expire_under_partial_pod_lists(native, mock_engine):
+    """Per-pod totals of a pod that left are dropped at once by a complete pod list; while every
+    refresh is partial (a metadata source keeps failing) they are kept, but only for
+    pod_totals_ttl, and gpuexp_pod_list_complete says which case applies."""
+    import time
+    uid, cid = "00000000-0000-4000-8000-0000000000e1", "e1" * 32
+    e = mock_engine(1, pod_totals_ttl_s=0.5)
+    e.set_pods([{"uid": uid, "namespace": "ns", "name": "gone", "containers": {cid: "w"}}], True)
+    e.set_pid_cgroup(100, kubepods_cgroup(uid, cid))
+    e.mock_set_processes(0, [{"pid": 100, "vram_bytes": 1 << 30, "cu_occupancy": 48, "name": "a"}])
+    e.tick(S)
+    e.tick(2 * S)
+    fams = promtext.parse(e.snapshot_text())
+    assert promtext.value(fams, "gpuexp_pod_list_complete") == 1
+    assert promtext.value(fams, "amd_pod_gpu_energy_joules_total", pod="gone") > 0
+    e.mock_set_processes(0, [])
+    e.set_pods([], False)  # partial refresh without the pod: totals kept...
+    e.tick(3 * S)
+    fams = promtext.parse(e.snapshot_text())
+    assert promtext.value(fams, "gpuexp_pod_list_complete") == 0
+    assert promtext.value(fams, "amd_pod_gpu_energy_joules_total", pod="gone") > 0
+    time.sleep(0.6)  # ...until no applied list has had the pod for the TTL
+    e.set_pods([], False)
+    e.tick(4 * S)
+    fams = promtext.parse(e.snapshot_text())
+    assert not promtext.samples(fams, "amd_pod_gpu_energy_joules_total")
+    assert not promtext.samples(fams, "amd_pod_gpu_allocated_seconds_total")
