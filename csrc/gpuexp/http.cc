@@ -68,17 +68,21 @@ struct Conn {
   uint64_t last_metrics_ns = 0;
   uint64_t intervals[4] = {0, 0, 0, 0};
   int n_intervals = 0, iv_pos = 0;
-  // Expected next /metrics arrival, or 0 when the last 4 periods are not steady.
+  // Expected next /metrics arrival, or 0 when the last (up to 4) periods are not steady.
+  // Two steady periods arm it (a scraper's third request is already pre-woken: with 4, a
+  // 5-scrape warm-up left the first timed scrapes cold); one odd
+  // period among the last four disarms it.
   uint64_t expected_next() const {
-    if (n_intervals < 4) return 0;
+    if (n_intervals < 2) return 0;
     uint64_t lo = intervals[0], hi = intervals[0], sum = 0;
-    for (uint64_t v : intervals) {
+    for (int k = 0; k < n_intervals; ++k) {
+      const uint64_t v = intervals[k];
       lo = std::min(lo, v);
       hi = std::max(hi, v);
       sum += v;
     }
     if (lo < 20000000ull || hi > lo + lo / 8) return 0;  // < 20 ms or > 12% jitter
-    return last_metrics_ns + sum / 4;
+    return last_metrics_ns + sum / uint64_t(n_intervals);
   }
 };
 

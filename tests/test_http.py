@@ -397,7 +397,7 @@ def test_readyz_reports_a_stalled_sampler(native):
 
 
 def test_scrape_prewake_learns_a_steady_period(native):
-    """A scraper with a steady period (here 30 ms) is learnt after 4 intervals: the worker
+    """A scraper with a steady period (here 30 ms) is learnt after 2 intervals: the worker
     then wakes on a timer just ahead of each expected request (short sleeps keep its core
     out of deep idle) — a few timer wake-ups per scrape, none once scraping stops, and none
     with prewake off."""
@@ -425,7 +425,7 @@ def test_scrape_prewake_learns_a_steady_period(native):
         finally:
             e.stop()
     woke, later = run(True)
-    assert 4 <= woke <= 14 * 12, woke   # armed from the 5th scrape on; bounded per scrape
+    assert 4 <= woke <= 14 * 12, woke   # armed from the 3rd scrape on; bounded per scrape
     assert later - woke <= 25           # at most one window's worth after the last scrape
     assert run(False) == (0, 0)
 
