@@ -766,11 +766,7 @@ void read_round() {
     const double wall = std::chrono::duration<double>(t - a->t_last).count();
     if (g_read_mode == kCumulative) {
       double d[kNumCtr], xm[kMaxXcc], xg[kMaxXcc];
-      bool backwards = false;
-      for (int k = 0; k < kNumCtr; ++k) {
-        d[k] = acc.v[k] - a->cum[k];
-        backwards = backwards || d[k] < 0;
-      }
+      for (int k = 0; k < kNumCtr; ++k) d[k] = acc.v[k] - a->cum[k];
       for (int x = 0; x < acc.nxcc; ++x) {
         xm[x] = std::max(0.0, acc.xm[x] - a->cum_xm[x]);
         xg[x] = std::max(0.0, acc.xg[x] - a->cum_xg[x]);
@@ -781,17 +777,13 @@ void read_round() {
       std::memcpy(a->cum_xg, acc.xg, sizeof(a->cum_xg));
       a->have_cum = true;
       a->t_last = t;
-      // GRBM_COUNT always advances while counting runs: 5 ms of wall time without a cycle
-      // means counting was stopped under us
-      a->zero_grbm = !first && !backwards && d[kGrbmCount] <= 0 && wall > 0.005 ? a->zero_grbm + 1 : 0;
-      const bool stopped = a->zero_grbm >= 2;  // two windows in a row: not a fluke
-      if (backwards) ++a->resets;  // wrapped or reset under us: this window is unknown
-      if (backwards || stopped) {
-        a->zero_grbm = 0;
+      const WindowAction act = window_action(d, first, wall, &a->zero_grbm);
+      if (act == kRearm) {
+        ++a->resets;  // reset / re-programmed / stopped under us: this window is unknown
         rearm(*a);
         return;
       }
-      if (!first) publish(*a, d, acc, wall, t, acc.v, xm, xg);
+      if (act == kPublish) publish(*a, d, acc, wall, t, acc.v, xm, xg);
     } else {
       publish(*a, acc.v, acc, wall, t);
       a->t_last = t;

@@ -167,6 +167,25 @@ inline void derive(Derived& a, const double* d, const int* inst, double wall) {
   a.windows += 1;
 }
 
+// Continuous cumulative counting: what to do with a window of deltas `d` (this read minus
+// the previous one) that spans `wall` seconds.  Counters that went backwards were reset or
+// re-programmed by someone else (another profiler's start packet); a GRBM_COUNT that did not
+// advance over real time means counting was stopped under us (GRBM_COUNT always advances
+// while counting runs) -- two such windows in a row, so one fluke never costs a re-arm.  Both
+// re-arm counting with our own selects (aql_pmc.cc rearm).  The first window after (re)arming
+// has no previous read to subtract: skipped.
+enum WindowAction { kPublish = 0, kSkip = 1, kRearm = 2 };
+inline WindowAction window_action(const double* d, bool first, double wall, int* zero_grbm) {
+  bool backwards = false;
+  for (int k = 0; k < kNumCtr; ++k) backwards = backwards || d[k] < 0;
+  *zero_grbm = !first && !backwards && d[kGrbmCount] <= 0 && wall > 0.005 ? *zero_grbm + 1 : 0;
+  if (!first && (backwards || *zero_grbm >= 2)) {
+    *zero_grbm = 0;
+    return kRearm;
+  }
+  return first ? kSkip : kPublish;
+}
+
 // Per-XCC MFMA busy: the chip formula with one XCC's share of the SIMDs.  mfma[x] sums that
 // XCC's SQ instances (one per SE), grbm[x] is that XCC's own GRBM_COUNT.  Each XCD runs its
 // own clock (DPM lowers a busy XCD's clock while idle ones stay high), so busy cycles are

@@ -7,7 +7,8 @@ import pytest
 
 SIMD, CU = 1024, 256  # MI355X: 256 CUs x 4 SIMDs
 # output order: counter_model.h derive() / optional_sources.cc sample()
-MFMA_BUSY, SQ_BUSY, GUI, WAVES, LDS, LDS_CONF, HBM_RD, HBM_WR, GMI_RD, GMI_WR, MFMA_UTIL, BF16, FP8 = range(13)
+(MFMA_BUSY, SQ_BUSY, GUI, WAVES, LDS, LDS_CONF, HBM_RD, HBM_WR, GMI_RD, GMI_WR, MFMA_UTIL, BF16, FP8,
+ STALL, LIM_LDS, LIM_WAVES, LIM_VGPR) = range(17)
 
 
 def derive(native, wall=0.1, privileged=True, **deltas):
@@ -57,3 +58,50 @@ def test_scope_follows_privilege(native):
 def test_unknown_counter_is_rejected(native):
     with pytest.raises(ValueError):
         derive(native, NOT_A_COUNTER=1)
+
+
+def test_occupancy_limiters(native):
+    """SPI resource-allocator counters: the stall share is over elapsed cycles (per SE); each
+    limiter is the share of the SE's CUs (LDS) or SIMDs (wave slots, VGPRs) that were full
+    over the stalled cycles.  (derive_counters passes each counter as one instance, i.e. one
+    SE holding all CUs.)"""
+    clk = 2.0e8
+    out, _ = derive(native, GRBM_COUNT=clk, GRBM_GUI_ACTIVE=clk, SPI_RA_RES_STALL_CSN=0.4 * clk,
+                    SPI_RA_LDS_CU_FULL_CSN=0.4 * clk * CU * 0.9, SPI_RA_WAVE_SIMD_FULL_CSN=0.4 * clk * SIMD * 0.05,
+                    SPI_RA_VGPR_SIMD_FULL_CSN=0)
+    assert out[STALL] == pytest.approx(40.0)
+    assert out[LIM_LDS] == pytest.approx(90.0)
+    assert out[LIM_WAVES] == pytest.approx(5.0)
+    assert out[LIM_VGPR] == 0.0
+    idle, _ = derive(native, GRBM_COUNT=clk, GRBM_GUI_ACTIVE=clk, SPI_RA_RES_STALL_CSN=0, SPI_RA_LDS_CU_FULL_CSN=0,
+                     SPI_RA_WAVE_SIMD_FULL_CSN=0, SPI_RA_VGPR_SIMD_FULL_CSN=0)
+    assert idle[STALL] == 0.0 and idle[LIM_LDS] == 0.0 and idle[LIM_WAVES] == 0.0  # nothing waited
+    none, _ = derive(native, GRBM_COUNT=clk, GRBM_GUI_ACTIVE=clk)  # no SPI counters programmed
+    assert math.isnan(none[STALL]) and math.isnan(none[LIM_LDS])
+
+
+def _deltas(native, grbm=2e8, **kw):
+    names = native.counter_names()
+    d = [0.0] * len(names)
+    d[names.index("GRBM_COUNT")] = grbm
+    for k, v in kw.items():
+        d[names.index(k)] = v
+    return d
+
+
+def test_window_action_rearms_after_a_foreign_reset_or_stop(native):
+    """Continuous counting's per-window decision (aql_pmc.cc read_round): a counter that went
+    backwards (another profiler's start packet reset / re-programmed them) re-arms at once;
+    GRBM_COUNT standing still over real time (someone stopped counting) re-arms on the second
+    such window; the first window after arming is skipped (no previous read)."""
+    act = native.counter_window_action
+    assert act(_deltas(native), True, 0.1) == ("skip", 0)
+    assert act(_deltas(native), False, 0.1) == ("publish", 0)
+    back = _deltas(native, SQ_WAVES=-5.0)
+    assert act(back, False, 0.1) == ("rearm", 0)
+    stopped = _deltas(native, grbm=0.0)
+    a1, z1 = act(stopped, False, 0.1)
+    assert (a1, z1) == ("publish", 1)  # one fluke: still exported (all-zero window)
+    assert act(stopped, False, 0.1, z1) == ("rearm", 0)  # the second in a row: re-arm
+    assert act(_deltas(native), False, 0.1, 1) == ("publish", 0)  # a moving window clears the streak
+    assert act(stopped, False, 0.001, 1) == ("publish", 0)  # too short to tell: no streak
