@@ -219,7 +219,10 @@ void Engine::define_families() {
   f_sq_busy_ = add("amd_gpu_sq_busy_percent", "Shader sequencer busy (SQ_BUSY_CYCLES)", G, D);
   f_gui_ = add("amd_gpu_gui_active_percent", "Graphics pipe active (GRBM_GUI_ACTIVE / GRBM_COUNT)", G, D);
   f_waves_ = add("amd_gpu_waves_per_second", "Waves dispatched per second (SQ_WAVES)", G, D);
-  f_lds_ = add("amd_gpu_lds_active_percent", "LDS active cycles per CU (SQ_LDS_IDX_ACTIVE)", G, D);
+  f_lds_ = add("amd_gpu_lds_active_percent",
+               "LDS ACTIVITY: cycles per CU in which the LDS served an instruction (SQ_LDS_IDX_ACTIVE); how much "
+               "LDS space waves hold (LDS OCCUPANCY) is amd_gpu_occupancy_limiter_percent{resource=\"lds\"}",
+               G, D);
   f_lds_conf_ = add("amd_gpu_lds_bank_conflict_percent", "LDS bank-conflict cycles / LDS active cycles", G, D);
   f_hbm_rd_ = add("amd_gpu_hbm_read_bytes_per_second",
                   "HBM read bandwidth: L2 read sectors from the memory controller (TCC_EA0_RDREQ_DRAM_32B x 32 B)", G, D);
