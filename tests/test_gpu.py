@@ -182,6 +182,32 @@ def test_exporter_tick_on_gpu(native):
         e.stop()
 
 
+def test_devices_stage_split_on_mi355x(native):
+    """The devices stage split on real hardware: a fresh gpu_metrics read is an SMU round trip
+    the kernel busy-waits on, so its thread CPU is tens to hundreds of microseconds (idle:
+    ~206 us, profiles/r03/read_costs.txt), it is the bulk of the stage, and the auto fetch
+    policy at 1 GPU caps nothing at 10 Hz (one GPU's fetches fit the 1.5 % budget)."""
+    e = amdsmi_engine(native, series_profile="full", interval_s=0.1)
+    try:
+        time.sleep(2.0)
+        fams = promtext.parse(e.snapshot_text())
+        st = e.stats()
+    finally:
+        e.stop()
+    parts = {lab["part"]: v for _, lab, v in promtext.samples(fams, "gpuexp_device_read_seconds_total")}
+    assert set(parts) == {"counters_kick", "control", "gpu_metrics", "vram", "ras", "gtt"}, parts
+    fresh = promtext.value(fams, "gpuexp_gpu_metrics_reads_total", gpu=0, kind="fresh")
+    cpu = promtext.value(fams, "gpuexp_gpu_metrics_fetch_cpu_seconds_total", gpu=0)
+    per_read_us = cpu / fresh * 1e6
+    print(f"ticks {st['ticks']}, parts per tick (us): "
+          f"{ {k: round(v / st['ticks'] * 1e6, 1) for k, v in parts.items()} }, fresh reads {fresh}, "
+          f"fetch CPU {per_read_us:.1f} us per fresh read, stage CPU (us/tick): "
+          f"{ {k: round(v / st['ticks'] / 1e3, 1) for k, v in st['stage_cpu_ns'].items()} }")
+    assert fresh >= 10 and 20 <= per_read_us <= 2000, (fresh, per_read_us)
+    assert parts["gpu_metrics"] >= 0.5 * sum(parts.values()), parts
+    assert promtext.value(fams, "gpuexp_gpu_metrics_min_interval_seconds", gpu=0) == 0.0
+
+
 def test_kfd_events_source_opens(native):
     """The KFD SMI event fd opens on the real GPU (AMDKFD_IOC_SMI_EVENTS) and the six
     per-GPU event counters are exported from the first tick."""
