@@ -499,6 +499,7 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("metrics_min_interval_s", &EngineConfig::metrics_min_interval_s)
       .def_readwrite("metrics_cpu_budget", &EngineConfig::metrics_cpu_budget)
       .def_readwrite("pod_totals_ttl_s", &EngineConfig::pod_totals_ttl_s)
+      .def_readwrite("kfd_rescan_interval_s", &EngineConfig::kfd_rescan_interval_s)
       .def_readwrite("metrics_max_interval_s", &EngineConfig::metrics_max_interval_s)
       .def_readwrite("fake_metrics_cost_us", &EngineConfig::fake_metrics_cost_us)
       .def_readwrite("queue_devices", &EngineConfig::queue_devices)

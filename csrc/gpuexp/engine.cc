@@ -536,7 +536,8 @@ bool Engine::start(std::string* err) {
   if (nthreads <= 0) nthreads = 1;
   if (nthreads > 1) pool_ = std::make_unique<ForkJoinPool>(nthreads);
   kfd_ = std::make_unique<KfdProcReader>(cfg_.host_root, cfg_.exclude_self ? self_pid_ : -1, cfg_.kfd_cu_occupancy,
-                                         uint64_t(cfg_.kfd_detail_interval_s * 1e9));
+                                         uint64_t(cfg_.kfd_detail_interval_s * 1e9),
+                                         uint64_t(cfg_.kfd_rescan_interval_s * 1e9));
   resolver_ = std::make_unique<PidResolver>(cfg_.host_root);
 
   // Counters first: the rocprofiler tool must register before the HSA runtime loads,

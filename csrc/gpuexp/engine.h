@@ -88,6 +88,9 @@ struct EngineConfig {
   std::string process_source = "auto";  // auto | kfd | amdsmi | none
   bool kfd_cu_occupancy = true;
   double kfd_detail_interval_s = 1.0;  // cu_occupancy / sdma re-read period (0 = every tick)
+  // KFD proc directory listed at least this often (and on its mtime moving, or a tracked
+  // process vanishing); tracked processes' VRAM is read every tick either way (0 = list every tick)
+  double kfd_rescan_interval_s = 0.5;
   bool exclude_self = true;
   bool enable_sentinel = false;
   std::string sentinel_impl = "auto";  // auto (PMC queue if the aqlprofile counters run, else HIP) | hip | queue

@@ -5,12 +5,14 @@
 #include <cstring>
 #include <unordered_set>
 
+#include <sys/stat.h>
+
 namespace gpuexp {
 
 KfdProcReader::KfdProcReader(std::string host_root, int self_pid, bool read_cu_occupancy,
-                             uint64_t detail_interval_ns)
+                             uint64_t detail_interval_ns, uint64_t rescan_interval_ns)
     : root_(std::move(host_root)), self_(self_pid), read_cu_(read_cu_occupancy),
-      detail_every_ns_(detail_interval_ns) {
+      detail_every_ns_(detail_interval_ns), rescan_ns_(rescan_interval_ns) {
   if (!root_.empty() && root_.back() == '/') root_.pop_back();
 }
 
@@ -19,6 +21,30 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
   per_dev->assign(devs.size(), {});
   ++scan_no_;
   const std::string base = root_ + "/sys/class/kfd/kfd/proc";
+  // The directory listing is the scan's most expensive step (a cold getdents: ~20 us on
+  // MI355X sysfs, profiles/r03/read_costs.txt, more on a busy host) and new GPU processes are
+  // rare: list when the directory's mtime moved (kernfs stamps it on add/remove where it
+  // keeps attributes), at least every rescan_ns, and whenever a tracked process vanished;
+  // in between, read the tracked processes' files only (an exited process's reads fail).
+  struct stat sb {};
+  const bool have_mtime = ::stat(base.c_str(), &sb) == 0;
+  const bool moved = have_mtime && (sb.st_mtim.tv_sec != mtime_.tv_sec || sb.st_mtim.tv_nsec != mtime_.tv_nsec);
+  if (have_mtime) mtime_ = sb.st_mtim;
+  const bool list = !now_ns || !rescan_ns_ || moved || relist_ || now_ns - last_list_ns_ >= rescan_ns_ ||
+                    now_ns < last_list_ns_;
+  if (!list) {
+    for (auto it = pids_.begin(); it != pids_.end();) {
+      if (emit(it->second, it->first, per_dev, now_ns) == 0 && !it->second.devs.empty()) {
+        relist_ = true;  // gone (or its PID reused): the next tick lists the directory again
+        it = pids_.erase(it);
+        continue;
+      }
+      ++it;
+    }
+    return;
+  }
+  relist_ = false;
+  last_list_ns_ = now_ns;
   for (const std::string& name : list_dir(base)) {
     int pid = std::atoi(name.c_str());
     if (pid <= 0 || pid == self_) continue;

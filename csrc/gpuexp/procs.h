@@ -9,6 +9,7 @@
 #pragma once
 
 #include <cstdint>
+#include <ctime>
 #include <memory>
 #include <string>
 #include <unordered_map>
@@ -25,7 +26,8 @@ class KfdProcReader {
   // scan).  Measured on MI355X (profiles/r01/kfd_read_costs.txt): vram_<id> ~6 us,
   // stats_<id>/cu_occupancy ~15 us (KFD asks the hardware), sdma_<id> ~7 us per process
   // per GPU — VRAM is what the legacy families and attribution need every tick.
-  KfdProcReader(std::string host_root, int self_pid, bool read_cu_occupancy, uint64_t detail_interval_ns = 0);
+  KfdProcReader(std::string host_root, int self_pid, bool read_cu_occupancy, uint64_t detail_interval_ns = 0,
+                uint64_t rescan_interval_ns = 0);
   // Fills per_dev[d] with the processes that have a KFD context on device d.
   void scan(const std::vector<DeviceInfo>& devs, std::vector<std::vector<ProcSample>>* per_dev,
             uint64_t now_ns = 0);
@@ -50,6 +52,10 @@ class KfdProcReader {
   int self_;
   bool read_cu_;
   uint64_t detail_every_ns_;
+  uint64_t rescan_ns_ = 0;       // list the KFD proc directory at least this often (0: every scan)
+  uint64_t last_list_ns_ = 0;
+  bool relist_ = false;          // a tracked process vanished: list at the next scan
+  timespec mtime_{};             // the directory's mtime at the last look
   uint64_t scan_no_ = 0;
   std::unordered_map<int, Entry> pids_;
 };

@@ -44,6 +44,7 @@ class Config:
     process_source: str = "auto"           # auto | kfd | amdsmi | none
     kfd_cu_occupancy: bool = True
     kfd_detail_interval: float = 1.0       # seconds between cu_occupancy / sdma re-reads (0 = every tick)
+    kfd_rescan_interval: float = 0.5       # KFD proc directory listed at least this often (also on change)
     gc_after: int = 1
     # optional sources
     enable_sentinel: bool = False
@@ -149,6 +150,7 @@ class Config:
         ec.process_source = self.process_source
         ec.kfd_cu_occupancy = bool(self.kfd_cu_occupancy)
         ec.kfd_detail_interval_s = float(self.kfd_detail_interval)
+        ec.kfd_rescan_interval_s = float(self.kfd_rescan_interval)
         ec.enable_sentinel = bool(self.enable_sentinel)
         ec.sentinel_spin = int(self.sentinel_spin)
         ec.sentinel_impl = str(self.sentinel_impl)

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Exporter CPU projection for 1/2/4/8 MI355X from a fake-host node (profiles/r04/
+cpu_projection.txt; VERDICT r03 task 2).
+
+The engine runs in this process on the sysfs backend over a fake /sys + /proc tree
+(utils/fakehost.py: MI355X topology, 4 GPU processes per GPU attributed to a pod), full
+series profile, and burns the measured thread CPU of a real SMU fetch on every fresh
+gpu_metrics read (--fetch-us, from tools/probe_fetch_cost.py on MI355X).  Whole-process CPU
+(getrusage: every thread) over a steady window, with the shipped fetch policy
+(metrics_min_interval auto, --budget % of one core for all GPUs' fetches) and, for
+comparison, with every tick fetching (metrics_min_interval 0).  A projection of the
+per-GPU costs, not a measurement of an 8-GPU node (the driver's SCALE run is that).
+Usage: python tools/project_cpu.py [--fetch-us 206,450] [--hz 10,100] [--seconds 4]
+"""
+import argparse
+import os
+import resource
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def measure(native, n_gpus: int, hz: float, fetch_us: int, policy: str, budget: float, seconds: float) -> dict:
+    import test_fakehost as tf
+    root = tempfile.mkdtemp(prefix="gpuexp-proj-")
+    tf._loaded_node(root, n_gpus)
+    c = native.EngineConfig()
+    c.backend = "sysfs"
+    c.host_root = root
+    c.interval_s = 1.0 / hz
+    c.serve_http = False
+    c.series_profile = "full"
+    c.fake_metrics_cost_us = fetch_us
+    c.metrics_min_interval_s = -1.0 if policy == "auto" else 0.0
+    c.metrics_cpu_budget = budget / 100.0
+    e = native.Engine(c)
+    e.start()
+    try:
+        time.sleep(1.0)
+        r0, t0, s0 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter(), e.stats()
+        time.sleep(seconds)
+        r1, t1, s1 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter(), e.stats()
+    finally:
+        e.stop()
+    cpu = (r1.ru_utime - r0.ru_utime) + (r1.ru_stime - r0.ru_stime)
+    ticks = max(1, s1["ticks"] - s0["ticks"])
+    return {"gpus": n_gpus, "hz": hz, "fetch_us": fetch_us, "policy": policy,
+            "process_cpu_pct": round(100.0 * cpu / (t1 - t0), 2),
+            "sampler_us_per_tick": round((s1["sampler_cpu_ns"] - s0["sampler_cpu_ns"]) / ticks / 1e3, 1)}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--fetch-us", default="206,450")
+    ap.add_argument("--hz", default="10,100")
+    ap.add_argument("--gpus", default="1,2,4,8")
+    ap.add_argument("--budget", type=float, default=1.5)
+    ap.add_argument("--seconds", type=float, default=4.0)
+    args = ap.parse_args()
+    from kubernetes_gpu_exporter_amd._native import load
+    native = load()
+    print(f"# fake-host projection, full profile, 4 processes/GPU, budget {args.budget} % (auto policy)")
+    print(f"{'gpus':>4} {'hz':>5} {'fetch_us':>8} {'policy':>6} {'cpu_%':>7} {'sampler_us/tick':>15}")
+    for fetch in (int(x) for x in args.fetch_us.split(",")):
+        for hz in (float(x) for x in args.hz.split(",")):
+            for n in (int(x) for x in args.gpus.split(",")):
+                for policy in ("auto", "every"):
+                    r = measure(native, n, hz, fetch, policy, args.budget, args.seconds)
+                    print(f"{r['gpus']:>4} {r['hz']:>5g} {r['fetch_us']:>8} {r['policy']:>6} "
+                          f"{r['process_cpu_pct']:>7.2f} {r['sampler_us_per_tick']:>15.1f}", flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
