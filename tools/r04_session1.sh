@@ -12,4 +12,4 @@ timeout -k 10 240 python -u -m pytest tests/test_gpu.py -x -v --timeout 200 --ti
   -k "xcc_mfma_busy_calibration" > gpurun_out/r04/starve.log 2>&1
 grep -E "starve|PASS|FAIL" gpurun_out/r04/starve.log | tail -3 || true
 echo "[s1] devices A/B $(date +%T)"
-tools/devices_ab.sh "${1:-2}" off duty cont late r02
+tools/devices_ab.sh "${1:-2}" off duty cont late
