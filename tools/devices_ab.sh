@@ -26,8 +26,15 @@ for rep in $(seq 1 "$reps"); do
       *) echo "unknown arm $arm"; exit 2 ;;
     esac
     echo "[ab] rep $rep arm $arm $(date +%T)"
+    rc=0
     env "${envs[@]}" timeout -k 10 180 python -u bench.py --steps 40 --warmup 5 --identity-phase 0 \
-      "${extra[@]}" --out "gpurun_out/ab/$arm.$rep.json" > "gpurun_out/ab/$arm.$rep.out" 2> "gpurun_out/ab/$arm.$rep.err"
+      "${extra[@]}" --out "gpurun_out/ab/$arm.$rep.json" > "gpurun_out/ab/$arm.$rep.out" 2> "gpurun_out/ab/$arm.$rep.err" || rc=$?
+    # rc 1 = the run flagged a problem (its --out JSON says which): keep going; anything else
+    # (timeout, abort, crash) ends the A/B
+    if [ $rc -ne 0 ]; then
+      echo "[ab] $arm.$rep rc=$rc: $(grep -h FAILED gpurun_out/ab/$arm.$rep.err | head -3)"
+      [ $rc -eq 1 ] || exit $rc
+    fi
     python3 - "$arm" "$rep" <<'PY'
 import json, sys
 r = json.load(open(f"gpurun_out/ab/{sys.argv[1]}.{sys.argv[2]}.json"))
