@@ -84,7 +84,9 @@ def start_exporter(args, n_gpus: int, backend: str, port: int, pod_map: str, log
     env.pop("ROCP_TOOL_LIBRARIES", None)  # the exporter itself issues no collectives
     env["GPUEXP_POD_MAP_FILE"] = pod_map
     env["GPUEXP_POD_ATTRIBUTION"] = "true"
-    logf = open(log_path, "w")
+    logf = open(log_path, "a")  # append: a failed first start's output survives the retry
+    logf.write(f"--- exporter start {time.strftime('%H:%M:%S')}: {' '.join(cmd)}\n")
+    logf.flush()
     if os.environ.get("GPUEXP_BENCH_FAIL_EXPORTER_WITH_COUNTERS") == "1" and args.counters:
         raise RuntimeError("exporter start failed on request (GPUEXP_BENCH_FAIL_EXPORTER_WITH_COUNTERS)")  # test hook
     t_start = time.perf_counter()

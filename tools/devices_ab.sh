@@ -2,7 +2,7 @@
 # Devices-stage A/B under the bench's GEMM pod (VERDICT r03 "do this" #1): which part of the
 # exporter's devices stage grew from round 2 (177 us) to round 3 (500 us), and what fixes it.
 # Arms, interleaved, REPS rounds (each arm = one short bench.py run on the same box):
-#   off        no PMC counters (sentinel on its own HIP stream)
+#   off        no PMC counters, no sentinel (no exporter GPU queue)
 #   duty       PMC counters, 20 ms windows
 #   cont       continuous PMC, read kicked at the tick's start (round-3 default)
 #   late       continuous PMC, read kicked after the gpu_metrics SMU fetch
@@ -16,7 +16,7 @@ for rep in $(seq 1 "$reps"); do
   for arm in $arms; do
     extra=(); envs=()
     case $arm in
-      off) extra=(--counters 0) ;;
+      off) extra=(--counters 0 --sentinel 0) ;;  # no exporter GPU queue at all (flagged degraded: rc 1)
       duty) envs=(GPUEXP_COUNTERS_MODE=duty) ;;
       cont) envs=(GPUEXP_COUNTERS_KICK=start) ;;
       late) envs=(GPUEXP_COUNTERS_KICK=after_devices) ;;
