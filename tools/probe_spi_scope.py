@@ -36,11 +36,17 @@ sys.path.insert(0, {root!r})
 import torch
 from kubernetes_gpu_exporter_amd.ops.gemm import occupancy_hog
 torch.zeros(1, device="cuda:0")
+kind, seconds, stream_no = sys.argv[1], float(sys.argv[2]), int(sys.argv[3])
+# HIP gives each new stream its own hardware queue, round robin over GPU_MAX_HW_QUEUES (4):
+# stream k > 0 is the k-th created stream, 0 the null stream
+streams = [torch.cuda.Stream() for _ in range(stream_no)]
+s = streams[-1] if streams else torch.cuda.current_stream()
+torch.cuda.synchronize()
 print("ready", flush=True)
-kind, seconds = sys.argv[1], float(sys.argv[2])
 sys.stdin.readline()  # go
 t = time.perf_counter()
-out = occupancy_hog(0, kind, seconds / 4, generations=4)
+with torch.cuda.stream(s):
+    out = occupancy_hog(0, kind, seconds / 4, generations=4, stream=s.cuda_stream)
 torch.cuda.synchronize()
 print("done", round(time.perf_counter() - t, 3), flush=True)
 """
@@ -50,6 +56,9 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=2.0)
     ap.add_argument("--hz", type=float, default=10.0)
+    ap.add_argument("--streams", default="0", help="comma-separated stream numbers to run every case on "
+                    "(0 = the null stream, k = the k-th new stream: a different hardware queue each)")
+    ap.add_argument("--kinds", default="lds,waves")
     args = ap.parse_args()
 
     import torch
@@ -115,27 +124,33 @@ def main() -> int:
     time.sleep(0.5)
     res["cases"]["idle"] = summary(record(1.5))
     print("idle", res["cases"]["idle"], flush=True)
-    for kind in ("lds", "waves"):
-        p = subprocess.Popen([sys.executable, "-c", CHILD.format(root=ROOT), kind, str(args.seconds)],
-                             stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
-        assert p.stdout.readline().strip() == "ready"
-        p.stdin.write("go\n")
-        p.stdin.flush()
-        rows = record(args.seconds * 0.9)
-        done = p.stdout.readline().strip()
-        p.wait(timeout=60)
-        key = f"{kind}_other"
-        res["cases"][key] = dict(summary(rows), child=done)
-        print(key, res["cases"][key], flush=True)
-        time.sleep(0.5)
-        t = time.perf_counter()
-        occupancy_hog(0, kind, args.seconds / 4, generations=4)
-        rows = record(args.seconds * 0.9)
-        torch.cuda.synchronize()
-        key = f"{kind}_self"
-        res["cases"][key] = dict(summary(rows), run_s=round(time.perf_counter() - t, 3))
-        print(key, res["cases"][key], flush=True)
-        time.sleep(0.5)
+    own_streams: list = []
+    for sn in (int(x) for x in args.streams.split(",")):
+        while len(own_streams) < sn:
+            own_streams.append(torch.cuda.Stream())
+        sfx = "" if sn == 0 else f"_s{sn}"
+        for kind in args.kinds.split(","):
+            p = subprocess.Popen([sys.executable, "-c", CHILD.format(root=ROOT), kind, str(args.seconds), str(sn)],
+                                 stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+            assert p.stdout.readline().strip() == "ready"
+            p.stdin.write("go\n")
+            p.stdin.flush()
+            rows = record(args.seconds * 0.9)
+            done = p.stdout.readline().strip()
+            p.wait(timeout=60)
+            key = f"{kind}_other{sfx}"
+            res["cases"][key] = dict(summary(rows), child=done)
+            print(key, res["cases"][key], flush=True)
+            time.sleep(0.5)
+            t = time.perf_counter()
+            st = own_streams[sn - 1] if sn else torch.cuda.current_stream()
+            occupancy_hog(0, kind, args.seconds / 4, generations=4, stream=st.cuda_stream)
+            rows = record(args.seconds * 0.9)
+            torch.cuda.synchronize()
+            key = f"{kind}_self{sfx}"
+            res["cases"][key] = dict(summary(rows), run_s=round(time.perf_counter() - t, 3))
+            print(key, res["cases"][key], flush=True)
+            time.sleep(0.5)
     e.stop()
     print("RESULT " + json.dumps(res), flush=True)
     return 0
