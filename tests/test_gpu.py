@@ -888,6 +888,10 @@ def test_xcc_mfma_busy_calibration():
     assert st["rescue_active_after"] == "0" and st["rescues"] == st["rescue_releases"], st
     rss = st["rss_mib"]
     assert abs(rss["after"] - rss["before"]) <= 10.0, rss
+    # ... and the self-metrics say so
+    ev = st["counters_events"]
+    assert ev.get("rescue", 0) >= 1 and ev.get("rescue_release", 0) == ev.get("rescue"), ev
+    assert st["rescue_active_metric"] == 0.0, st
     during = st["busy_during"][8:]  # from 0.8 s on (3 stuck rounds + the move)
     assert sum(v is not None for v in during) >= 0.8 * len(during), st
     # near 100 % while the grid runs; the grid's blocks run in generations (every wave slot

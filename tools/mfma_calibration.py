@@ -251,12 +251,17 @@ def main() -> int:
         rss["during_max"] = max(rss_during) if rss_during else None
         rss["after"] = rss_mib()
         kv = dict(x.split("=", 1) for x in raw().split(";") if "=" in x)
+        fams_after = promtext.parse(e.snapshot_text())
+        events = {lab["event"]: v for _, lab, v in promtext.samples(fams_after, "gpuexp_counters_events_total")
+                  if lab.get("gpu") == "0"}
+        active = [v for _, lab, v in promtext.samples(fams_after, "gpuexp_counters_rescue_active") if lab.get("gpu") == "0"]
         res["cases"]["starve"] = {"seconds": args.starve, "kernel_s": run_s, "pending_before": before,
                                   "pmc_read_stalls": int(kv.get("stalls", -1)), "rescued": kv.get("rescued"),
                                   "rescue_active_after": kv.get("rescue_active"), "rescues": kv.get("rescues"),
                                   "rescue_releases": kv.get("rescue_releases"),
                                   "released_after_kernel_s": released_after_s,
                                   "rss_mib": {k: round(v, 1) if v is not None else None for k, v in rss.items()},
+                                  "counters_events": events, "rescue_active_metric": active[0] if active else None,
                                   "busy_during": [round(v, 2) if v is not None else None for v in busy],
                                   "ticks_during": ticks,
                                   "pending_during": [round(v, 3) if v is not None else None for v in seen],
