@@ -620,8 +620,13 @@ def main() -> int:
             step(cl, None)
         x0 = None
         if native_exporter and rank == 0 and use_gpu:
-            cl.scrape()  # xGMI accumulators at the start of the window (untimed)
-            x0 = xgmi_totals(cl)
+            # xGMI accumulators at the start of the window (untimed), on a connection of its
+            # own: an extra request on the timed connection would break the steady scrape
+            # period the server learns per connection (pre-wake), as Prometheus never does
+            side = n.ScrapeClient("127.0.0.1", port, "/metrics", args.gzip, 5000,
+                                  promproto.ACCEPT if args.proto else "")
+            side.scrape()
+            x0 = xgmi_totals(side)
         if dist is not None:
             dist.barrier()
         sync()

@@ -209,12 +209,12 @@ void Engine::define_families() {
                       "(SQ_INSTS_VALU_MFMA_MOPS_<type> x 512)", G, with(D, {"dtype"}));
   f_disp_stall_ = add("amd_gpu_dispatch_stall_percent",
                       "Share of the time a compute wave ready to launch fitted on no CU of its shader engine "
-                      "(SPI resource allocator; device-wide only, full profile)",
+                      "(SPI resource allocator; every process's waves, full profile)",
                       G, D);
   f_occ_lim_ = add("amd_gpu_occupancy_limiter_percent",
                    "While compute waves waited for a CU: the share of CUs whose free LDS could not take the "
                    "wave (resource=lds: LDS occupancy), of SIMDs without a free wave slot (wave_slots) or "
-                   "without enough free VGPRs (vgpr); 0 when no wave waited (device-wide only, full profile)",
+                   "without enough free VGPRs (vgpr); 0 when no wave waited (every process's waves, full profile)",
                    G, with(D, {"resource"}));
   f_sq_busy_ = add("amd_gpu_sq_busy_percent", "Shader sequencer busy (SQ_BUSY_CYCLES)", G, D);
   f_gui_ = add("amd_gpu_gui_active_percent", "Graphics pipe active (GRBM_GUI_ACTIVE / GRBM_COUNT)", G, D);
@@ -1124,13 +1124,16 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
         dput(st, i, st.mflops[1], f_mfma_flops_, {"fp8"}, cr.mfma_fp8_flops, gen);
         st.flops_last[0] = cr.mfma_bf16_flops;
         st.flops_last[1] = cr.mfma_fp8_flops;
-        // what capped residency (SPI resource allocator; VMID-filtered like the SQ waves
-        // unless profiles/r04/spi_scope.txt shows otherwise)
-        static const char* kRes[3] = {"lds", "wave_slots", "vgpr"};
-        const double lim[3] = {cr.lds_limited_pct, cr.wave_limited_pct, cr.vgpr_limited_pct};
-        dput(st, i, st.disp_stall, f_disp_stall_, {}, cr.dispatch_stall_pct, gen);
-        for (int k = 0; k < 3; ++k) dput(st, i, st.occ_lim[k], f_occ_lim_, {kRes[k]}, lim[k], gen);
       }
+    }
+    if (cfg_.series_profile == "full") {
+      // What capped residency, from the SPI resource allocator.  Not VMID-filtered like the
+      // SQ wave counters: an unprivileged exporter sees other processes' waves on every
+      // hardware queue (profiles/r04/spi_scope.txt), so exported at any scope.
+      static const char* kRes[3] = {"lds", "wave_slots", "vgpr"};
+      const double lim[3] = {cr.lds_limited_pct, cr.wave_limited_pct, cr.vgpr_limited_pct};
+      dput(st, i, st.disp_stall, f_disp_stall_, {}, cr.dispatch_stall_pct, gen);
+      for (int k = 0; k < 3; ++k) dput(st, i, st.occ_lim[k], f_occ_lim_, {kRes[k]}, lim[k], gen);
     }
   }
   CounterHealth ch;

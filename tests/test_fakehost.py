@@ -602,9 +602,11 @@ def _loaded_node(root, n_gpus):
 
 
 # Thread CPU of one fresh gpu_metrics read on MI355X: the kernel busy-waits on the SMU round
-# trip (profiles/r03/read_costs.txt: 206 us idle; profiles/r04/devices_split.txt under the
-# bench's GEMM pod).  Injected per fresh read on the fake host so CPU budgets include it.
-SMU_FETCH_CPU_US = 206
+# trip.  profiles/r04/fetch_cost.log (tools/probe_fetch_cost.py, one reader at 10 Hz): p50
+# 130 us idle, 382 us under a bf16 GEMM pod (the SMU answers slower under load; the bench's
+# driver-form runs saw 364-393 us).  The loaded figure is injected per fresh read on the fake
+# host so the CPU budgets below include it.
+SMU_FETCH_CPU_US = 382
 
 
 def _fakehost_engine(native, root, interval_s, fetch_cost_us=0, device_threads=0):

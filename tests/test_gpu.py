@@ -900,6 +900,31 @@ def test_xcc_mfma_busy_calibration():
     assert statistics.median(v for v in during if v is not None) > 80.0, st
 
 
+def test_occupancy_limiters_see_other_processes():
+    """LDS occupancy as a device-wide signal (SPI resource-allocator counters,
+    amd_gpu_occupancy_limiter_percent / amd_gpu_dispatch_stall_percent), against kernels of
+    known limiter run by ANOTHER process, four generations of blocks queued: 1 wave + 64 KiB
+    of LDS per block -> LDS limits (lds ~100, wave_slots ~0); 8 waves per block, no LDS ->
+    wave slots limit (wave_slots ~100, lds ~0); the dispatcher stalled all the time (~100).
+    Idle: nothing waits (0).  Read from the engine's own exposition on an unprivileged box."""
+    import json
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "probe_spi_scope.py"), "--seconds", "2.0",
+                        "--no-self", "--exported"], capture_output=True, text=True, timeout=150)
+    print(r.stdout[-3000:], r.stderr[-2000:])
+    line = [l for l in r.stdout.splitlines() if l.startswith("RESULT ")]
+    assert line, "probe produced no result"
+    res = json.loads(line[-1][7:])
+    if "counters=unavailable" in res["status"]:
+        pytest.skip("device counting unavailable on this box: " + res["status"])
+    cases = res["cases"]
+    idle = cases["idle"]["exported_median"]
+    assert idle["stall"] == 0.0 and idle["lds"] == 0.0, idle
+    lds = cases["lds_other"]["exported_median"]
+    assert lds["stall"] > 90 and lds["lds"] > 90 and lds["wave_slots"] < 5, lds
+    waves = cases["waves_other"]["exported_median"]
+    assert waves["stall"] > 90 and waves["wave_slots"] > 90 and waves["lds"] < 5, waves
+
+
 def test_device_scope_pmc_calibration():
     """Device-scope PMC families against ground truth (tools/pmc_validate.py): HBM read and
     write of a stream copy of known bytes, waves/s of known grids, LDS bank conflicts of a

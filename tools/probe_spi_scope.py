@@ -59,6 +59,9 @@ def main() -> int:
     ap.add_argument("--streams", default="0", help="comma-separated stream numbers to run every case on "
                     "(0 = the null stream, k = the k-th new stream: a different hardware queue each)")
     ap.add_argument("--kinds", default="lds,waves")
+    ap.add_argument("--no-self", action="store_true", help="only the other-process cases")
+    ap.add_argument("--exported", action="store_true",
+                    help="also record the engine's exported amd_gpu_occupancy_limiter_percent per case")
     args = ap.parse_args()
 
     import torch
@@ -95,9 +98,17 @@ def main() -> int:
         raw = {k: kv.get(k) for k in ("SPI_RA_RES_STALL_CSN", "SPI_RA_LDS_CU_FULL_CSN", "SPI_RA_WAVE_SIMD_FULL_CSN",
                                       "SPI_RA_VGPR_SIMD_FULL_CSN", "GRBM_COUNT", "GRBM_GUI_ACTIVE", "SQ_WAVES")}
         ok = plugin.gpuexp_rp_sample(0, 0.0, out) == 0
-        return {"stall": out[13] if ok else None, "lds": out[14] if ok else None, "waves": out[15] if ok else None,
-                "vgpr": out[16] if ok else None, "gui": out[2] if ok else None, "raw": raw,
-                "window_s": float(kv.get("window_s", "nan"))}
+        w = {"stall": out[13] if ok else None, "lds": out[14] if ok else None, "waves": out[15] if ok else None,
+             "vgpr": out[16] if ok else None, "gui": out[2] if ok else None, "raw": raw,
+             "window_s": float(kv.get("window_s", "nan"))}
+        if args.exported:
+            from kubernetes_gpu_exporter_amd.utils import promtext
+            fams = promtext.parse(e.snapshot_text())
+            w["exported"] = {lab["resource"]: v for _, lab, v in
+                             promtext.samples(fams, "amd_gpu_occupancy_limiter_percent") if lab.get("gpu") == "0"}
+            st = [v for _, lab, v in promtext.samples(fams, "amd_gpu_dispatch_stall_percent") if lab.get("gpu") == "0"]
+            w["exported"]["stall"] = st[0] if st else None
+        return w
 
     def record(seconds, skip=0.3):
         rows = []
@@ -116,9 +127,15 @@ def main() -> int:
         def med(k):
             v = [r[k] for r in rows if r[k] is not None]
             return round(statistics.median(v), 2) if v else None
-        return {"windows": len(rows), "stall_median": med("stall"), "lds_median": med("lds"),
-                "waves_median": med("waves"), "vgpr_median": med("vgpr"), "gui_median": med("gui"),
-                "raw_example": rows[len(rows) // 2]["raw"] if rows else None}
+        out = {"windows": len(rows), "stall_median": med("stall"), "lds_median": med("lds"),
+               "waves_median": med("waves"), "vgpr_median": med("vgpr"), "gui_median": med("gui"),
+               "raw_example": rows[len(rows) // 2]["raw"] if rows else None}
+        if args.exported and rows:
+            ex = [r["exported"] for r in rows]
+            out["exported_median"] = {k: (round(statistics.median([x[k] for x in ex if x.get(k) is not None]), 2)
+                                          if any(x.get(k) is not None for x in ex) else None)
+                                      for k in ("stall", "lds", "wave_slots", "vgpr")}
+        return out
 
     res = {"status": status, "cases": {}}
     time.sleep(0.5)
@@ -142,6 +159,8 @@ def main() -> int:
             res["cases"][key] = dict(summary(rows), child=done)
             print(key, res["cases"][key], flush=True)
             time.sleep(0.5)
+            if args.no_self:
+                continue
             t = time.perf_counter()
             st = own_streams[sn - 1] if sn else torch.cuda.current_stream()
             occupancy_hog(0, kind, args.seconds / 4, generations=4, stream=st.cuda_stream)
