@@ -50,6 +50,8 @@ enum Ctr {
   kSpiLdsFull,   // per such cycle: CUs whose free LDS cannot take the wave
   kSpiWaveFull,  // per such cycle: SIMDs with no free wave slot
   kSpiVgprFull,  // per such cycle: SIMDs with too few free VGPRs
+  kSpiWave,      // SPI_CSN_WAVE: compute waves launched (experiment: GPUEXP_PMC_SPI_WAVES=1)
+  kSpiTg,        // SPI_CSN_NUM_THREADGROUPS: compute workgroups launched (same)
   kNumCtr
 };
 
@@ -62,7 +64,8 @@ inline const char* name(int c) {
                                         "SQ_CYCLES",                "SQ_INSTS_VALU_MFMA_MOPS_BF16",
                                         "SQ_INSTS_VALU_MFMA_MOPS_F8", "SPI_RA_RES_STALL_CSN",
                                         "SPI_RA_LDS_CU_FULL_CSN",   "SPI_RA_WAVE_SIMD_FULL_CSN",
-                                        "SPI_RA_VGPR_SIMD_FULL_CSN"};
+                                        "SPI_RA_VGPR_SIMD_FULL_CSN", "SPI_CSN_WAVE",
+                                        "SPI_CSN_NUM_THREADGROUPS"};
   return kNames[c];
 }
 

@@ -96,7 +96,8 @@ def main() -> int:
         plugin.gpuexp_rp_debug(0, buf, 8192)
         kv = dict(x.split("=", 1) for x in buf.value.decode().split(";") if "=" in x)
         raw = {k: kv.get(k) for k in ("SPI_RA_RES_STALL_CSN", "SPI_RA_LDS_CU_FULL_CSN", "SPI_RA_WAVE_SIMD_FULL_CSN",
-                                      "SPI_RA_VGPR_SIMD_FULL_CSN", "GRBM_COUNT", "GRBM_GUI_ACTIVE", "SQ_WAVES")}
+                                      "SPI_RA_VGPR_SIMD_FULL_CSN", "GRBM_COUNT", "GRBM_GUI_ACTIVE", "SQ_WAVES",
+                                      "SPI_CSN_WAVE", "SPI_CSN_NUM_THREADGROUPS")}
         ok = plugin.gpuexp_rp_sample(0, 0.0, out) == 0
         w = {"stall": out[13] if ok else None, "lds": out[14] if ok else None, "waves": out[15] if ok else None,
              "vgpr": out[16] if ok else None, "gui": out[2] if ok else None, "raw": raw,
