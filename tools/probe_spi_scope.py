@@ -128,7 +128,12 @@ def main() -> int:
         def med(k):
             v = [r[k] for r in rows if r[k] is not None]
             return round(statistics.median(v), 2) if v else None
-        out = {"windows": len(rows), "stall_median": med("stall"), "lds_median": med("lds"),
+        def tot(k):  # sum over the recorded windows of a raw counter ("value/instances")
+            v = [float(r["raw"][k].split("/")[0]) for r in rows if r["raw"].get(k)]
+            return round(sum(v)) if v else None
+        out = {"windows": len(rows), "sum_spi_waves": tot("SPI_CSN_WAVE"),
+               "sum_spi_workgroups": tot("SPI_CSN_NUM_THREADGROUPS"), "sum_sq_waves": tot("SQ_WAVES"),
+               "stall_median": med("stall"), "lds_median": med("lds"),
                "waves_median": med("waves"), "vgpr_median": med("vgpr"), "gui_median": med("gui"),
                "raw_example": rows[len(rows) // 2]["raw"] if rows else None}
         if args.exported and rows:
