@@ -81,6 +81,14 @@ struct Conn {
     if (lo < 20000000ull || hi > lo + lo / 8) return 0;  // < 20 ms or > 12% jitter
     return last_metrics_ns + (a + b) / 2;
   }
+  // How early the next request may come: twice the spread of the two newest periods (a
+  // scraper whose requests wander by 1 ms needs the worker awake 1-2 ms ahead; a steady
+  // one keeps the minimum lead).
+  uint64_t jitter_lead(uint64_t min_lead, uint64_t max_lead) const {
+    if (n_intervals < 2) return min_lead;
+    const uint64_t a = intervals[(iv_pos + 3) & 3], b = intervals[(iv_pos + 2) & 3];
+    return std::clamp<uint64_t>(2 * (a > b ? a - b : b - a), min_lead, max_lead);
+  }
 };
 
 bool ieq_prefix(const char* a, size_t alen, const char* b) {
@@ -427,7 +435,7 @@ void HttpServer::run(Worker* w) {
       } else if (path == cfg_.metrics_path) {
         stats_.metrics_requests.fetch_add(1, std::memory_order_relaxed);
         const bool prewoken = last_prewake_ns && t0 >= last_prewake_ns &&
-                              t0 - last_prewake_ns <= cfg_.prewake_lead_ns + cfg_.prewake_step_ns;
+                              t0 - last_prewake_ns <= cfg_.prewake_max_lead_ns + cfg_.prewake_step_ns;
         if (prewoken) stats_.prewake_hits.fetch_add(1, std::memory_order_relaxed);
         if (c.last_metrics_ns && t0 > c.last_metrics_ns) {
           c.intervals[c.iv_pos] = t0 - c.last_metrics_ns;
@@ -528,10 +536,13 @@ void HttpServer::run(Worker* w) {
   // Arms the pre-wake timer for the earliest expected scrape (see HttpConfig::prewake).
   auto arm_prewake = [&]() {
     const uint64_t now = mono_ns();
-    uint64_t next = 0, gz_next = 0;
+    uint64_t next = 0, gz_next = 0, lead = cfg_.prewake_lead_ns;
     for (auto& kv : w->conns) {
       const uint64_t e = kv.second.expected_next();
-      if (e && e + cfg_.prewake_window_ns > now && (!next || e < next)) next = e;
+      if (e && e + cfg_.prewake_window_ns > now && (!next || e < next)) {
+        next = e;
+        lead = kv.second.jitter_lead(cfg_.prewake_lead_ns, cfg_.prewake_max_lead_ns);
+      }
       // a steady gzip scraper gone quiet for a minute no longer holds the sampler to it
       if (e && kv.second.gzip_client && e + 60000000000ull > now && (!gz_next || e < gz_next)) gz_next = e;
     }
@@ -540,8 +551,7 @@ void HttpServer::run(Worker* w) {
     itimerspec its{};
     if (next) {
       // before the lead: one timer at (expected - lead); inside the window: short slices
-      const uint64_t at = now + cfg_.prewake_lead_ns < next ? next - cfg_.prewake_lead_ns
-                                                            : now + cfg_.prewake_step_ns;
+      const uint64_t at = now + lead < next ? next - lead : now + cfg_.prewake_step_ns;
       its.it_value.tv_sec = time_t(at / 1000000000ull);
       its.it_value.tv_nsec = long(at % 1000000000ull);
     }

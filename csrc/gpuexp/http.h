@@ -47,7 +47,8 @@ struct HttpConfig {
   // does not pay a deep-idle exit on the critical path: a few timer wake-ups per scrape
   // instead of one long sleep, no spinning.
   bool prewake = true;
-  uint64_t prewake_lead_ns = 400000;
+  uint64_t prewake_lead_ns = 400000;       // ... at least; twice the connection's period jitter,
+  uint64_t prewake_max_lead_ns = 1500000;  // ... at most
   uint64_t prewake_step_ns = 150000;
   uint64_t prewake_window_ns = 3000000;
 };
@@ -72,7 +73,7 @@ struct HttpStats {
   std::atomic<uint64_t> partial_writes{0};
   std::atomic<uint64_t> prewake_timer_wakeups{0};  // timer expiries of the scrape pre-wake
   // /metrics requests parsed while their worker was pre-woken (its pre-wake timer fired
-  // within prewake_lead_ns + prewake_step_ns before the request): the rest paid a full
+  // within prewake_max_lead_ns + prewake_step_ns before the request): the rest paid a full
   // wake-up from an idle epoll_wait
   std::atomic<uint64_t> prewake_hits{0};
   // gzip responses the worker compressed itself: the snapshot had no gzip copy because no
