@@ -691,6 +691,9 @@ def main() -> int:
         body = client.last_body()
         if args.gzip:
             body = __import__("gzip").decompress(body)
+        if os.environ.get("GPUEXP_BENCH_DUMP_EXPOSITION"):  # evidence: the last timed scrape's body
+            with open(os.environ["GPUEXP_BENCH_DUMP_EXPOSITION"], "wb") as f:
+                f.write(body)
         if body[:1] == b"#":
             fams = promtext.parse(body.decode())
         else:  # protobuf exposition
