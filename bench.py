@@ -376,7 +376,7 @@ def main() -> int:
     from kubernetes_gpu_exporter_amd.k8s.filesource import write_pod_map
     from kubernetes_gpu_exporter_amd.utils import promproto, promtext
     from kubernetes_gpu_exporter_amd.utils.fakehost import FakeHost, kubepods_cgroup
-    from kubernetes_gpu_exporter_amd.utils.procstat import cpu_seconds_precise
+    from kubernetes_gpu_exporter_amd.utils.procstat import cpu_seconds_precise, thread_cpu_ns_by_name
     n = load()
     from kubernetes_gpu_exporter_amd.ops.gemm import kernels
     kern = kernels() if use_gpu else None
@@ -612,6 +612,7 @@ def main() -> int:
 
     xgmi_window: dict = {}
     exporter_rss_kb = [0]
+    cpu_by_thread: dict = {}
 
     def phase(proc, cl, native_exporter: bool = False):
         """W untimed + K timed steps (barrier + synchronize on both sides); returns the
@@ -632,6 +633,7 @@ def main() -> int:
         sync()
         lat: list = []
         cpu0 = cpu_seconds_precise(proc.pid) if rank == 0 else 0.0
+        by0 = thread_cpu_ns_by_name(proc.pid) if rank == 0 else {}
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step(cl, lat)
@@ -641,6 +643,11 @@ def main() -> int:
         elapsed = time.perf_counter() - t0
         cpu_pct = 100.0 * (cpu_seconds_precise(proc.pid) - cpu0) / elapsed if rank == 0 else 0.0
         if rank == 0 and native_exporter:
+            # where the exporter's CPU went, per thread name (us per step over the window)
+            by1 = thread_cpu_ns_by_name(proc.pid)
+            cpu_by_thread.clear()
+            cpu_by_thread.update({k: round((v - by0.get(k, 0)) / 1e3 / max(1, args.steps), 1)
+                                  for k, v in sorted(by1.items()) if v - by0.get(k, 0) > 0})
             try:  # resident memory of the exporter: each GPU queue it holds pins a CWSR area
                 exporter_rss_kb[0] = int([l for l in open(f"/proc/{proc.pid}/status")
                                           if l.startswith("VmRSS:")][0].split()[1])
@@ -802,6 +809,7 @@ def main() -> int:
             "server_scrape_p99_le_us": server_q.get("p99"),
             "server_scrapes": server_scrapes,
             "exporter_cpu_percent": round(cpu_pct, 3),
+            "exporter_cpu_us_per_step_by_thread": cpu_by_thread,
             "exporter_rss_mb": round(exporter_rss_kb[0] / 1024, 1) if exporter_rss_kb[0] else None,
             "exporter_startup_s": round(getattr(exporter, "startup_s", 0.0), 2),
             # the engine's own share of it (start() -> first sample; gpuexp_startup_seconds)

@@ -31,6 +31,26 @@ def cpu_seconds_precise(pid: int) -> float:
     return total * 1e-9 if total else cpu_seconds(pid)
 
 
+def thread_cpu_ns_by_name(pid: int) -> dict:
+    """Run time (ns, schedstat) of `pid`'s threads summed per thread name: where an
+    exporter's CPU goes (gpuexp-sampler, gpuexp-http, the PMC thread, Python ...)."""
+    out: dict = {}
+    try:
+        tids = os.listdir(f"/proc/{pid}/task")
+    except OSError:
+        return out
+    for tid in tids:
+        try:
+            with open(f"/proc/{pid}/task/{tid}/comm") as fh:
+                name = fh.read().strip()
+            with open(f"/proc/{pid}/task/{tid}/schedstat") as fh:
+                ns = int(fh.read().split()[0])
+        except (OSError, ValueError, IndexError):
+            continue
+        out[name] = out.get(name, 0) + ns
+    return out
+
+
 def thread_cpu_seconds(pid: int) -> dict:
     """Per-thread CPU seconds, keyed by thread name (sampler / http / python ...)."""
     out = {}
