@@ -188,6 +188,16 @@ std::condition_variable g_done_cv;
 std::atomic<uint64_t> g_thread_cpu_ns{0};  // the counting thread's own CPU, published per round
 // where a continuous read round's CPU goes (counting thread clock): post / wait / collect
 std::atomic<uint64_t> g_round_cpu[3] = {}, g_rounds{0};
+// Inline rounds (continuous mode; GPUEXP_PMC_INLINE=1 turns it on): the
+// engine's sampler posts the round's read packets itself at gpuexp_rp_kick and collects them
+// at gpuexp_rp_sync, after its device reads (~100-400 us later: the reads are done by then),
+// so a tick costs the counting thread no wake-ups at all; the thread only runs rounds when
+// nothing has kicked for a second (an engine that is not ticking).  Without it the thread
+// wakes per kick plus once per 60/100 us wait slice and the sampler waits on its condvar.
+bool g_inline = false;
+std::mutex g_round_mu;  // one round at a time, whichever thread runs it
+bool g_live = false;    // under g_round_mu: agents armed, the counting thread running
+std::atomic<uint64_t> g_last_kick_ns{0};
 
 uint64_t own_cpu_ns() {
   timespec ts;
@@ -708,12 +718,18 @@ void rearm(Agent& a) {
 // between looks), so one stuck GPU never delays the others' windows.  A GPU whose read was
 // already pending before this round gets one look, not the round's deadline.  Counting
 // itself never pauses (kStops: re-armed right after the read, a gap of one PM4 packet).
-void read_round() {
-  const auto begin = Clock::now();
-  uint64_t c0 = own_cpu_ns(), cw = 0, cc = 0;
-  // a stalled GPU costs the round at most this long (the other GPUs' reads are in flight)
-  const auto deadline = begin + std::chrono::milliseconds(std::min(1000, g_interval_ms));
+// Split in two (post_round / finish_round) so the engine's sampler can run it inline.
+struct Round {
   std::vector<Agent*> waiting;
+  uint64_t cpu_post = 0, cpu_wait = 0, cpu_collect = 0;
+  bool open = false;
+};
+Round g_round;  // under g_round_mu
+
+void post_round(Round& r) {
+  const uint64_t c0 = own_cpu_ns();
+  r.waiting.clear();
+  r.cpu_wait = r.cpu_collect = 0;
   for (Agent* a : g_agents) {
     if (!usable(a)) continue;
     if (a->rescued && a->orphan && hsa_signal_load_scacquire(a->sig) < 1) {
@@ -738,10 +754,16 @@ void read_round() {
       a->read_inflight = true;
       a->t_checked = a->t_submit;
     }
-    waiting.push_back(a);
+    r.waiting.push_back(a);
   }
-  const uint64_t c1 = own_cpu_ns();
+  r.open = true;
+  r.cpu_post = own_cpu_ns() - c0;
+}
 
+// Collects the round's reads until each completed or `deadline`.  final: a read still
+// pending at the deadline is stuck (counted, rescued after kRescueRounds); otherwise it stays
+// in flight and the next round gives it its one look.  Returns true when none is left.
+bool finish_round(Round& r, Clock::time_point deadline, bool final) {
   auto stuck = [&](Agent* a, Clock::time_point now) {  // still queued: look again next round
     a->t_checked = now;
     ++a->stalls;
@@ -766,7 +788,7 @@ void read_round() {
     Accum acc;
     const uint64_t k0 = own_cpu_ns();
     const bool got = collect(*a, &acc);
-    cc += own_cpu_ns() - k0;
+    r.cpu_collect += own_cpu_ns() - k0;
     if (!a->read_on_rq && a->probation > 0 && --a->probation == 0 && a->rq) end_rescue(*a);
     if (!got) return;
     const double wall = std::chrono::duration<double>(t - a->t_last).count();
@@ -801,6 +823,7 @@ void read_round() {
     }
   };
 
+  auto& waiting = r.waiting;
   for (int i = 0; !waiting.empty(); ++i) {
     const uint64_t w0 = own_cpu_ns();
     auto now = Clock::now();
@@ -812,28 +835,50 @@ void read_round() {
         continue;
       }
       if (hsa_signal_load_scacquire(a->read_on_rq ? a->rsig : a->sig) < 1) {
-        cw += own_cpu_ns() - w0;
+        r.cpu_wait += own_cpu_ns() - w0;
         done(a, now);
         it = waiting.erase(it);
         continue;
       }
-      if (a->was_pending || now >= deadline) {  // one look for an old read; none past the deadline
+      if (a->was_pending) {  // one look for an old read
+        stuck(a, now);
+        it = waiting.erase(it);
+        continue;
+      }
+      if (now >= deadline) {
+        if (!final) {  // stays in flight: the next round looks once more
+          a->t_checked = now;
+          ++it;
+          continue;
+        }
         stuck(a, now);
         it = waiting.erase(it);
         continue;
       }
       ++it;
     }
-    if (waiting.empty()) break;
+    if (waiting.empty() || now >= deadline) break;
     now = Clock::now();
     std::this_thread::sleep_for(std::min<Clock::duration>(std::chrono::microseconds(i == 0 ? 60 : 100),
                                                           deadline > now ? deadline - now : Clock::duration(0)));
-    cw += own_cpu_ns() - w0;
+    r.cpu_wait += own_cpu_ns() - w0;
   }
-  g_round_cpu[0] += c1 - c0;
-  g_round_cpu[1] += cw;
-  g_round_cpu[2] += cc;
+  const bool all = waiting.empty();
+  waiting.clear();
+  r.open = false;
+  g_round_cpu[0] += r.cpu_post;
+  g_round_cpu[1] += r.cpu_wait;
+  g_round_cpu[2] += r.cpu_collect;
   ++g_rounds;
+  return all;
+}
+
+void read_round() {
+  const auto begin = Clock::now();
+  // a stalled GPU costs the round at most this long (the other GPUs' reads are in flight)
+  const auto deadline = begin + std::chrono::milliseconds(std::min(1000, g_interval_ms));
+  post_round(g_round);
+  finish_round(g_round, deadline, /*final=*/true);
 }
 
 // Starts counting on `a` for good: start packet, then (cumulative) the baseline read.
@@ -893,7 +938,27 @@ ReadMode read_semantics(Agent& a, std::string* why) {
 void counting_loop() {
   ::prctl(PR_SET_NAME, "gpuexp-pmc", 0, 0, 0);
   ::prctl(PR_SET_TIMERSLACK, 10000UL, 0, 0, 0);  // 10 us: the wait_signal slices stay short
-  if (g_continuous) {
+  if (g_continuous && g_inline) {
+    // the engine runs the rounds (gpuexp_rp_kick / gpuexp_rp_sync); this thread only keeps
+    // counting read when nothing has kicked for a second
+    bool idle = false;
+    while (!g_quit.load()) {
+      {
+        std::unique_lock<std::mutex> lk(g_cv_mu);
+        g_cv.wait_for(lk, std::chrono::milliseconds(idle ? g_interval_ms : std::max(g_interval_ms, 1000)),
+                      [] { return g_quit.load(); });
+      }
+      if (g_quit.load()) break;
+      const uint64_t last = g_last_kick_ns.load();
+      const uint64_t now = uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                        Clock::now().time_since_epoch()).count());
+      idle = !last || now - last > 1000000000ull;
+      if (!idle) continue;
+      std::lock_guard<std::mutex> rl(g_round_mu);
+      read_round();
+      g_thread_cpu_ns.store(own_cpu_ns());
+    }
+  } else if (g_continuous) {
     uint64_t served = 0;
     while (!g_quit.load()) {
       uint64_t target;
@@ -905,7 +970,10 @@ void counting_loop() {
         if (g_quit.load()) break;
         target = g_kick_seq;
       }
-      read_round();
+      {
+        std::lock_guard<std::mutex> rl(g_round_mu);
+        read_round();
+      }
       g_thread_cpu_ns.store(own_cpu_ns());
       served = target;
       {
@@ -914,6 +982,9 @@ void counting_loop() {
       }
       g_done_cv.notify_all();
     }
+  }
+  if (g_continuous) {
+    std::lock_guard<std::mutex> rl(g_round_mu);
     for (Agent* a : g_agents) {
       if (!usable(a) || a->read_inflight) continue;
       if (a->rescued) {  // the first queue may still be stuck: stop from the rescue queue
@@ -1218,6 +1289,13 @@ extern "C" __attribute__((visibility("default"))) void gpuexp_rp_set_continuous(
 }
 
 extern "C" __attribute__((visibility("default"))) void gpuexp_rp_kick() {
+  if (g_continuous && g_inline) {  // post the round's reads from the caller (no wake-up)
+    g_last_kick_ns.store(uint64_t(
+        std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count()));
+    std::lock_guard<std::mutex> rl(g_round_mu);
+    if (g_live) post_round(g_round);
+    return;
+  }
   {
     std::lock_guard<std::mutex> lk(g_cv_mu);
     ++g_kick_seq;
@@ -1231,6 +1309,14 @@ extern "C" __attribute__((visibility("default"))) uint64_t gpuexp_rp_cpu_ns() { 
 // Waits up to `timeout_us` for the round of the last kick; 0 = done, 1 = timed out.
 extern "C" __attribute__((visibility("default"))) int gpuexp_rp_sync(int timeout_us) {
   if (!g_continuous) return 0;  // duty windows (incl. the fallback): nothing per tick to wait for
+  if (g_inline) {  // collect the reads posted at the kick (normally complete by now)
+    std::lock_guard<std::mutex> rl(g_round_mu);
+    if (!g_live || !g_round.open) return 0;
+    return finish_round(g_round, Clock::now() + std::chrono::microseconds(std::max(0, timeout_us)),
+                        /*final=*/false)
+               ? 0
+               : 1;
+  }
   std::unique_lock<std::mutex> lk(g_cv_mu);
   const uint64_t want = g_kick_seq;
   return g_done_cv.wait_for(lk, std::chrono::microseconds(std::max(0, timeout_us)),
@@ -1336,10 +1422,16 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_init(int ndev, c
     std::lock_guard<std::mutex> lk(g_cv_mu);
     g_kick_seq = g_done_seq = 0;
   }
+  if (const char* e = std::getenv("GPUEXP_PMC_INLINE")) g_inline = e[0] != '0';
   g_thread = std::thread(counting_loop);
+  {
+    std::lock_guard<std::mutex> rl(g_round_mu);
+    g_round = Round{};
+    g_live = true;
+  }
   g_status = "aqlprofile PMC on " + std::to_string(ok) + " GPU(s), " +
              (g_continuous ? std::string("continuous (one read per tick; read packets: ") +
-                                 read_mode_name(g_read_mode) + ")"
+                                 read_mode_name(g_read_mode) + (g_inline ? "; rounds run by the sampler" : "") + ")"
                            : std::to_string(g_window_ms) + " ms window every " + std::to_string(g_interval_ms) +
                                  " ms");
   return ok;
@@ -1373,6 +1465,10 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_sample_xcc(int d
 }
 
 extern "C" __attribute__((visibility("default"))) void gpuexp_rp_shutdown() {
+  {
+    std::lock_guard<std::mutex> rl(g_round_mu);  // no inline round from here on
+    g_live = false;
+  }
   g_quit.store(true);
   g_cv.notify_all();
   g_done_cv.notify_all();
