@@ -875,6 +875,11 @@ def main() -> int:
             # gzip copies made by the sampler (scrape expected before the next tick) and by the
             # HTTP worker for off-schedule requests (each adds one compression to that scrape)
             "gzip_compressions": gz_where or None,
+            # KFD process scans over the run: directory listings vs tracked-only reads, and how
+            # many processes the node's KFD proc directory holds (other GPUs' included)
+            "kfd_proc_scans": {lab.get("kind"): v for _, lab, v in promtext.samples(fams, "gpuexp_kfd_proc_scans_total")}
+            or None,
+            "kfd_procs_tracked": next((v for _, _, v in promtext.samples(fams, "gpuexp_kfd_procs_tracked")), None),
             "http_prewake_wakeups_per_scrape": round(prewake[0] / scrapes_total[0], 2)
             if prewake and scrapes_total and scrapes_total[0] else None,
             "optional_sources": {"counters": bool(args.counters), "sentinel": bool(args.sentinel),

@@ -3,6 +3,7 @@
 #include <fcntl.h>
 #include <sys/eventfd.h>
 #include <sys/poll.h>
+#include <sys/prctl.h>
 #include <sys/timerfd.h>
 #include <sys/utsname.h>
 #include <unistd.h>
@@ -345,6 +346,13 @@ void Engine::define_families() {
                               "answered (per-pod totals of pods missing from it are dropped at once); 0: a source "
                               "failed, and totals of missing pods are kept for pod_totals_ttl (1 h)",
                               G, {});
+  f_self_kfd_scans_ = add("gpuexp_kfd_proc_scans_total",
+                          "KFD process scans by kind: list (the /sys/class/kfd/kfd/proc directory was listed: "
+                          "its mtime moved, a tracked process left, or kfd_rescan_interval passed) or tracked "
+                          "(only the known processes' files were read)",
+                          C, {"kind"});
+  f_self_kfd_tracked_ = add("gpuexp_kfd_procs_tracked",
+                            "Processes in the KFD proc directory the exporter tracks (any GPU of the node)", G, {});
   f_self_startup_ = add("gpuexp_startup_seconds",
                         "Engine start to its first sample: backend init (amdsmi + raw-path validation), one "
                         "HSA queue per GPU with PMC programs and sentinel, plugin probes",
@@ -425,8 +433,23 @@ void Engine::define_families() {
                           G, {"gpu"});
 }
 
+namespace {
+// Runtime libraries started here (amdsmi, ROCr/HSA, HIP) create threads of their own, which
+// inherit the creating thread's name: named "gpuexp-rt" they show apart from the host
+// process's threads in per-thread CPU accounting (bench.py exporter_cpu_us_per_step_by_thread).
+struct RuntimeThreadsName {
+  char saved[17] = {};
+  RuntimeThreadsName() {
+    ::prctl(PR_GET_NAME, saved, 0, 0, 0);
+    set_thread_name("gpuexp-rt");
+  }
+  ~RuntimeThreadsName() { set_thread_name(saved); }
+};
+}  // namespace
+
 bool Engine::start(std::string* err) {
   if (running_.load()) return true;
+  RuntimeThreadsName rt_name;
   start_mono_ns_ = mono_ns();
   define_families();
   // Listen first: a port conflict fails before any GPU-side source (amdsmi, HSA queues,
@@ -1532,6 +1555,13 @@ void Engine::emit_self(uint64_t gen) {
   cput(self_refs_[3], f_self_overruns_, double(s.overruns), gen, none);
   cput(self_refs_[4], f_self_unresolved_, double(unresolved_.size()), gen, none);
   cput(pods_complete_ref_, f_self_pods_complete_, pods_complete_ ? 1 : 0, gen, none);
+  if (kfd_) {
+    cput(kfd_scan_refs_[0], f_self_kfd_scans_, double(kfd_->lists()), gen,
+         [] { return std::vector<std::string>{"list"}; });
+    cput(kfd_scan_refs_[1], f_self_kfd_scans_, double(kfd_->scans() - kfd_->lists()), gen,
+         [] { return std::vector<std::string>{"tracked"}; });
+    cput(kfd_scan_refs_[2], f_self_kfd_tracked_, double(kfd_->tracked()), gen, none);
+  }
   cput(self_refs_[5], f_self_render_bytes_, double(s.render_bytes), gen, none);
   cput(self_refs_[6], f_self_series_, double(s.series), gen, none);
   cput(self_refs_[7], f_self_cpu_, double(s.sampler_cpu_ns) * 1e-9, gen, none);

@@ -357,7 +357,8 @@ class Engine {
   // (ns, pod) -> last time an applied pod list had it (GC of per-pod totals under partial lists)
   std::map<std::pair<std::string, std::string>, uint64_t> pod_last_known_ns_;
   SeriesRef pods_complete_ref_;
-  int f_self_pods_complete_ = -1;
+  SeriesRef kfd_scan_refs_[3];
+  int f_self_pods_complete_ = -1, f_self_kfd_scans_ = -1, f_self_kfd_tracked_ = -1;
   SeriesRef self_refs_[21];
 
   // stats (guarded by stats_mu_)

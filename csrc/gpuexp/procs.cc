@@ -45,6 +45,7 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
   }
   relist_ = false;
   last_list_ns_ = now_ns;
+  ++lists_;
   for (const std::string& name : list_dir(base)) {
     int pid = std::atoi(name.c_str());
     if (pid <= 0 || pid == self_) continue;

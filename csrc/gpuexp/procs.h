@@ -32,6 +32,8 @@ class KfdProcReader {
   void scan(const std::vector<DeviceInfo>& devs, std::vector<std::vector<ProcSample>>* per_dev,
             uint64_t now_ns = 0);
   size_t tracked() const { return pids_.size(); }
+  uint64_t lists() const { return lists_; }    // scans that listed the directory
+  uint64_t scans() const { return scan_no_; }  // all scans
 
  private:
   struct PerDev {
@@ -56,7 +58,7 @@ class KfdProcReader {
   uint64_t last_list_ns_ = 0;
   bool relist_ = false;          // a tracked process vanished: list at the next scan
   timespec mtime_{};             // the directory's mtime at the last look
-  uint64_t scan_no_ = 0;
+  uint64_t scan_no_ = 0, lists_ = 0;
   std::unordered_map<int, Entry> pids_;
 };
 

@@ -85,7 +85,8 @@ class Exporter:
         signal.signal(signal.SIGINT, _handler)
         self.start()
         log.info("serving %s on %s (%s)", self.cfg.path, self.cfg.listen, self.engine.source_status())
-        while not self._stop.wait(1.0):
-            pass
+        # no timeout: lock waits are interrupted by signals, the handler sets the event, and
+        # the main thread wakes only then (a 1 s poll cost a wake-up per second for nothing)
+        self._stop.wait()
         self.stop()
         return 0

@@ -139,6 +139,39 @@ def test_control_plane_isolates_failures_and_pushes_on_change(mock_engine):
     assert cp._last_fp == fp
 
 
+def test_control_plane_skips_unchanged_cached_sources(tmp_path):
+    """A FileSource hands back its cached Metadata until the file changes: the refresh then
+    skips the merge and fingerprint (and pushes nothing); a new file is pushed again."""
+    p = str(tmp_path / "map.json")
+    write_pod_map(p, [{"uid": UID_A, "namespace": "n", "name": "a", "containers": {}}])
+
+    class _Eng:
+        def __init__(self):
+            self.pushes = 0
+
+        def set_pods(self, pods, complete):
+            self.pushes += 1
+
+        def set_device_owners(self, owners):
+            pass
+
+        def set_pid_cgroup(self, pid, path):
+            pass
+
+        def clear_pid_cgroups(self):
+            pass
+
+    eng = _Eng()
+    cp = ControlPlane([FileSource(p)], interval=0.05)
+    cp.attach(eng)
+    first = cp.refresh_once()
+    assert eng.pushes == 1 and list(first.pods) == [UID_A]
+    assert cp.refresh_once() is first and cp.refreshes == 2 and eng.pushes == 1
+    write_pod_map(p, [{"uid": UID_B, "namespace": "n", "name": "b", "containers": {}}])
+    os.utime(p, ns=(time.time_ns() + 10**6, time.time_ns() + 10**6))
+    assert list(cp.refresh_once().pods) == [UID_B] and eng.pushes == 2
+
+
 def test_failed_refresh_never_drops_restored_pod_totals(mock_engine, tmp_path):
     """the first refresh runs while the apiserver is down.  Its (partial) pod
     list must not garbage-collect the per-pod totals restored from --state-file; the first

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 GPU session 6: PMC read rounds run by the sampler (inline, no counting-thread
-# wake-ups) vs by the counting thread.  Counter GPU tests (incl. the starvation / rescue
+# wake-ups) vs by the counting thread; then the unit of KFD's per-process sdma_<id> file.  Counter GPU tests (incl. the starvation / rescue
 # case) with inline rounds first, then the driver's bench command interleaved per arm.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/r04s6
@@ -11,4 +11,5 @@ bash tools/gpu_session.sh \
   "150::GPUEXP_PMC_INLINE=1 python -u bench.py --gpus 1 --steps 20 --warmup 5 --out gpurun_out/r04s6/inline.2.json" \
   "150::GPUEXP_PMC_INLINE=0 python -u bench.py --gpus 1 --steps 20 --warmup 5 --out gpurun_out/r04s6/thread.2.json" \
   "150::GPUEXP_PMC_INLINE=1 python -u bench.py --gpus 1 --steps 100 --warmup 10 --out gpurun_out/r04s6/inline.100.json" \
-  "150::GPUEXP_PMC_INLINE=0 python -u bench.py --gpus 1 --steps 100 --warmup 10 --out gpurun_out/r04s6/thread.100.json"
+  "150::GPUEXP_PMC_INLINE=0 python -u bench.py --gpus 1 --steps 100 --warmup 10 --out gpurun_out/r04s6/thread.100.json" \
+  "90::python -u tools/probe_sdma_units.py --seconds 1.5 > gpurun_out/r04s6/sdma_units.log 2>&1; grep -v RESULT gpurun_out/r04s6/sdma_units.log | cut -c1-300"
