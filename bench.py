@@ -880,6 +880,8 @@ def main() -> int:
             "kfd_proc_scans": {lab.get("kind"): v for _, lab, v in promtext.samples(fams, "gpuexp_kfd_proc_scans_total")}
             or None,
             "kfd_procs_tracked": next((v for _, _, v in promtext.samples(fams, "gpuexp_kfd_procs_tracked")), None),
+            "http_rx_cpu_moves": next((v for _, _, v in promtext.samples(fams, "gpuexp_http_rx_cpu_moves_total")),
+                                      None),
             "http_prewake_wakeups_per_scrape": round(prewake[0] / scrapes_total[0], 2)
             if prewake and scrapes_total and scrapes_total[0] else None,
             "optional_sources": {"counters": bool(args.counters), "sentinel": bool(args.sentinel),

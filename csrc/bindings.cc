@@ -453,6 +453,7 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("socket_sndbuf", &HttpConfig::socket_sndbuf)
       .def_readwrite("stale_after_ns", &HttpConfig::stale_after_ns)
       .def_readwrite("prewake", &HttpConfig::prewake)
+      .def_readwrite("follow_rx_cpu", &HttpConfig::follow_rx_cpu)
       .def_readwrite("prewake_lead_ns", &HttpConfig::prewake_lead_ns)
       .def_readwrite("prewake_step_ns", &HttpConfig::prewake_step_ns)
       .def_readwrite("prewake_window_ns", &HttpConfig::prewake_window_ns);
@@ -571,6 +572,7 @@ PYBIND11_MODULE(_gpuexp, m) {
           d["http_metrics_requests"] = hs->metrics_requests.load();
           d["http_gzip_responses"] = hs->gzip_responses.load();
           d["http_gzip_on_demand"] = hs->gzip_on_demand.load();
+          d["http_rx_cpu_moves"] = hs->rx_cpu_moves.load();
           d["http_bytes"] = hs->bytes_sent.load();
           d["http_errors"] = hs->errors.load();
           d["http_open_conns"] = hs->open_conns.load();

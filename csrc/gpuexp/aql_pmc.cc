@@ -725,10 +725,17 @@ struct Round {
   bool open = false;
 };
 Round g_round;  // under g_round_mu
+// Reads of an inline round that outlived the engine's sync wait: the counting thread keeps
+// looking at them (60/100 us slices, as the thread-run round does) until they complete or
+// the next kick takes them over, so a slow read's window still gets its completion time
+// to within a slice.  Under g_round_mu.
+std::vector<Agent*> g_leftover;
+std::atomic<bool> g_leftover_flag{false};  // set by sync, taken by the thread
 
 void post_round(Round& r) {
   const uint64_t c0 = own_cpu_ns();
   r.waiting.clear();
+  g_leftover.clear();
   r.cpu_wait = r.cpu_collect = 0;
   for (Agent* a : g_agents) {
     if (!usable(a)) continue;
@@ -760,69 +767,75 @@ void post_round(Round& r) {
   r.cpu_post = own_cpu_ns() - c0;
 }
 
-// Collects the round's reads until each completed or `deadline`.  final: a read still
-// pending at the deadline is stuck (counted, rescued after kRescueRounds); otherwise it stays
-// in flight and the next round gives it its one look.  Returns true when none is left.
-bool finish_round(Round& r, Clock::time_point deadline, bool final) {
-  auto stuck = [&](Agent* a, Clock::time_point now) {  // still queued: look again next round
-    a->t_checked = now;
-    ++a->stalls;
-    // stuck again while on probation (the rescue queue still exists): back to it at once
-    if (a->read_on_rq || g_read_mode != kCumulative || ++a->stuck_rounds < (a->rq ? 1 : kRescueRounds)) return;
-    if (a->rq) {
-      a->rescued = true;
-      a->orphan = true;
-      a->probation = 0;
-      a->read_inflight = false;
-      a->stuck_rounds = 0;
-    } else if (rescue_enabled() && rescue_reads(*a)) {
-      a->read_inflight = false;
-      a->stuck_rounds = 0;
-    }
-  };
-  auto done = [&](Agent* a, Clock::time_point now) {
+// A read still queued at its round's end (final): look again next round; after
+// kRescueRounds such rounds the reads move to a rescue queue.
+void round_stuck(Agent* a, Clock::time_point now) {
+  a->t_checked = now;
+  ++a->stalls;
+  // stuck again while on probation (the rescue queue still exists): back to it at once
+  if (a->read_on_rq || g_read_mode != kCumulative || ++a->stuck_rounds < (a->rq ? 1 : kRescueRounds)) return;
+  if (a->rq) {
+    a->rescued = true;
+    a->orphan = true;
+    a->probation = 0;
     a->read_inflight = false;
     a->stuck_rounds = 0;
-    // the read executed between the last time it was seen pending and now
-    const auto t = a->t_checked + (now - a->t_checked) / 2;
-    Accum acc;
-    const uint64_t k0 = own_cpu_ns();
-    const bool got = collect(*a, &acc);
-    r.cpu_collect += own_cpu_ns() - k0;
-    if (!a->read_on_rq && a->probation > 0 && --a->probation == 0 && a->rq) end_rescue(*a);
-    if (!got) return;
-    const double wall = std::chrono::duration<double>(t - a->t_last).count();
-    if (g_read_mode == kCumulative) {
-      double d[kNumCtr], xm[kMaxXcc], xg[kMaxXcc];
-      for (int k = 0; k < kNumCtr; ++k) d[k] = acc.v[k] - a->cum[k];
-      for (int x = 0; x < acc.nxcc; ++x) {
-        xm[x] = std::max(0.0, acc.xm[x] - a->cum_xm[x]);
-        xg[x] = std::max(0.0, acc.xg[x] - a->cum_xg[x]);
-      }
-      const bool first = !a->have_cum;
-      std::memcpy(a->cum, acc.v, sizeof(a->cum));
-      std::memcpy(a->cum_xm, acc.xm, sizeof(a->cum_xm));
-      std::memcpy(a->cum_xg, acc.xg, sizeof(a->cum_xg));
-      a->have_cum = true;
-      a->t_last = t;
-      const WindowAction act = window_action(d, first, wall, &a->zero_grbm);
-      if (act == kRearm) {
-        ++a->resets;  // reset / re-programmed / stopped under us: this window is unknown
-        rearm(*a);
-        return;
-      }
-      if (act == kPublish) publish(*a, d, acc, wall, t, acc.v, xm, xg);
-    } else {
-      publish(*a, acc.v, acc, wall, t);
-      a->t_last = t;
-      if (g_read_mode == kStops) {
-        const auto ts = run_packet(*a, a->start_pkt);
-        if (ts == Clock::time_point{}) a->broken = true;
-        else a->t_last = ts;
-      }
-    }
-  };
+  } else if (rescue_enabled() && rescue_reads(*a)) {
+    a->read_inflight = false;
+    a->stuck_rounds = 0;
+  }
+}
 
+// A read that completed (seen at `now`): collect, derive and publish its window.
+void round_done(Round& r, Agent* a, Clock::time_point now) {
+  a->read_inflight = false;
+  a->stuck_rounds = 0;
+  // the read executed between the last time it was seen pending and now
+  const auto t = a->t_checked + (now - a->t_checked) / 2;
+  Accum acc;
+  const uint64_t k0 = own_cpu_ns();
+  const bool got = collect(*a, &acc);
+  r.cpu_collect += own_cpu_ns() - k0;
+  if (!a->read_on_rq && a->probation > 0 && --a->probation == 0 && a->rq) end_rescue(*a);
+  if (!got) return;
+  const double wall = std::chrono::duration<double>(t - a->t_last).count();
+  if (g_read_mode == kCumulative) {
+    double d[kNumCtr], xm[kMaxXcc], xg[kMaxXcc];
+    for (int k = 0; k < kNumCtr; ++k) d[k] = acc.v[k] - a->cum[k];
+    for (int x = 0; x < acc.nxcc; ++x) {
+      xm[x] = std::max(0.0, acc.xm[x] - a->cum_xm[x]);
+      xg[x] = std::max(0.0, acc.xg[x] - a->cum_xg[x]);
+    }
+    const bool first = !a->have_cum;
+    std::memcpy(a->cum, acc.v, sizeof(a->cum));
+    std::memcpy(a->cum_xm, acc.xm, sizeof(a->cum_xm));
+    std::memcpy(a->cum_xg, acc.xg, sizeof(a->cum_xg));
+    a->have_cum = true;
+    a->t_last = t;
+    const WindowAction act = window_action(d, first, wall, &a->zero_grbm);
+    if (act == kRearm) {
+      ++a->resets;  // reset / re-programmed / stopped under us: this window is unknown
+      rearm(*a);
+      return;
+    }
+    if (act == kPublish) publish(*a, d, acc, wall, t, acc.v, xm, xg);
+  } else {
+    publish(*a, acc.v, acc, wall, t);
+    a->t_last = t;
+    if (g_read_mode == kStops) {
+      const auto ts = run_packet(*a, a->start_pkt);
+      if (ts == Clock::time_point{}) a->broken = true;
+      else a->t_last = ts;
+    }
+  }
+}
+
+
+// Collects the round's reads until each completed or `deadline`.  final: a read still
+// pending at the deadline is stuck (counted, rescued after kRescueRounds); otherwise it stays
+// in flight (handed to the counting thread, g_leftover) and the next round gives it its one
+// look.  Returns true when none is left.
+bool finish_round(Round& r, Clock::time_point deadline, bool final) {
   auto& waiting = r.waiting;
   for (int i = 0; !waiting.empty(); ++i) {
     const uint64_t w0 = own_cpu_ns();
@@ -836,22 +849,22 @@ bool finish_round(Round& r, Clock::time_point deadline, bool final) {
       }
       if (hsa_signal_load_scacquire(a->read_on_rq ? a->rsig : a->sig) < 1) {
         r.cpu_wait += own_cpu_ns() - w0;
-        done(a, now);
+        round_done(r, a, now);
         it = waiting.erase(it);
         continue;
       }
       if (a->was_pending) {  // one look for an old read
-        stuck(a, now);
+        round_stuck(a, now);
         it = waiting.erase(it);
         continue;
       }
       if (now >= deadline) {
-        if (!final) {  // stays in flight: the next round looks once more
+        if (!final) {  // stays in flight
           a->t_checked = now;
           ++it;
           continue;
         }
-        stuck(a, now);
+        round_stuck(a, now);
         it = waiting.erase(it);
         continue;
       }
@@ -864,6 +877,7 @@ bool finish_round(Round& r, Clock::time_point deadline, bool final) {
     r.cpu_wait += own_cpu_ns() - w0;
   }
   const bool all = waiting.empty();
+  if (!all && !final) g_leftover = waiting;
   waiting.clear();
   r.open = false;
   g_round_cpu[0] += r.cpu_post;
@@ -871,6 +885,35 @@ bool finish_round(Round& r, Clock::time_point deadline, bool final) {
   g_round_cpu[2] += r.cpu_collect;
   ++g_rounds;
   return all;
+}
+
+// Counting thread: follows g_leftover until each read completed, the next kick took it
+// over (post_round clears the list), or a fallback interval passed (then the next round's
+// one look decides).
+void follow_leftover() {
+  Round r;
+  const auto give_up = Clock::now() + std::chrono::milliseconds(g_interval_ms);
+  for (int i = 0;; ++i) {
+    {
+      std::lock_guard<std::mutex> rl(g_round_mu);
+      if (!g_live || g_leftover.empty()) return;
+      const auto now = Clock::now();
+      for (auto it = g_leftover.begin(); it != g_leftover.end();) {
+        Agent* a = *it;
+        if (!a->read_inflight || a->queue_error.load()) {
+          it = g_leftover.erase(it);
+        } else if (hsa_signal_load_scacquire(a->read_on_rq ? a->rsig : a->sig) < 1) {
+          round_done(r, a, now);
+          it = g_leftover.erase(it);
+        } else {
+          a->t_checked = now;
+          ++it;
+        }
+      }
+      if (g_leftover.empty() || now >= give_up) return;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(i == 0 ? 60 : 100));
+  }
 }
 
 void read_round() {
@@ -946,9 +989,14 @@ void counting_loop() {
       {
         std::unique_lock<std::mutex> lk(g_cv_mu);
         g_cv.wait_for(lk, std::chrono::milliseconds(idle ? g_interval_ms : std::max(g_interval_ms, 1000)),
-                      [] { return g_quit.load(); });
+                      [] { return g_quit.load() || g_leftover_flag.load(); });
       }
       if (g_quit.load()) break;
+      if (g_leftover_flag.exchange(false)) {  // reads that outlived the sampler's sync wait
+        follow_leftover();
+        g_thread_cpu_ns.store(own_cpu_ns());
+        continue;
+      }
       const uint64_t last = g_last_kick_ns.load();
       const uint64_t now = uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
                                         Clock::now().time_since_epoch()).count());
@@ -1310,12 +1358,19 @@ extern "C" __attribute__((visibility("default"))) uint64_t gpuexp_rp_cpu_ns() { 
 extern "C" __attribute__((visibility("default"))) int gpuexp_rp_sync(int timeout_us) {
   if (!g_continuous) return 0;  // duty windows (incl. the fallback): nothing per tick to wait for
   if (g_inline) {  // collect the reads posted at the kick (normally complete by now)
-    std::lock_guard<std::mutex> rl(g_round_mu);
-    if (!g_live || !g_round.open) return 0;
-    return finish_round(g_round, Clock::now() + std::chrono::microseconds(std::max(0, timeout_us)),
-                        /*final=*/false)
-               ? 0
-               : 1;
+    {
+      std::lock_guard<std::mutex> rl(g_round_mu);
+      if (!g_live || !g_round.open) return 0;
+      if (finish_round(g_round, Clock::now() + std::chrono::microseconds(std::max(0, timeout_us)),
+                       /*final=*/false))
+        return 0;
+    }
+    g_leftover_flag.store(true);
+    {
+      std::lock_guard<std::mutex> lk(g_cv_mu);  // (no lost wake-up against the thread's wait)
+    }
+    g_cv.notify_all();
+    return 1;
   }
   std::unique_lock<std::mutex> lk(g_cv_mu);
   const uint64_t want = g_kick_seq;

@@ -383,6 +383,10 @@ void Engine::define_families() {
                              "Scrapes of the metrics path that arrived while their HTTP worker was pre-woken "
                              "(its pre-wake timer fired within the lead + one slice before the request)",
                              C, {});
+  f_self_rx_moves_ = add("gpuexp_http_rx_cpu_moves_total",
+                         "Times an HTTP worker moved to the CPU a steady scraper's requests arrive on "
+                         "(http follow_rx_cpu; 0 when off)",
+                         C, {});
   f_self_gzip_ = add("gpuexp_gzip_compressions_total",
                      "gzip compressions of the exposition: by the sampler (a gzip scrape was expected before "
                      "the next tick) or per request (off schedule)",
@@ -457,6 +461,7 @@ bool Engine::start(std::string* err) {
   if (cfg_.serve_http) {
     HttpConfig hc = cfg_.http;
     hc.gzip_level = cfg_.gzip_level;
+    if (const char* e = std::getenv("GPUEXP_HTTP_FOLLOW_RX_CPU")) hc.follow_rx_cpu = e[0] != '0';
     http_ = std::make_unique<HttpServer>(&store_, hc);
     if (!http_->start(err)) {
       http_.reset();
@@ -1591,6 +1596,7 @@ void Engine::emit_self(uint64_t gen) {
       cput(prewake_hits_ref_, f_self_prewake_hits_, double(hs.prewake_hits.load(std::memory_order_relaxed)), gen,
            none);
     }
+    cput(rx_moves_ref_, f_self_rx_moves_, double(hs.rx_cpu_moves.load(std::memory_order_relaxed)), gen, none);
     if (cfg_.http.enable_gzip) {
       cput(self_refs_[16], f_self_gzip_, double(gzip_eager_), gen,
            [] { return std::vector<std::string>{"sampler"}; });

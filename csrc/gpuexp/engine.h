@@ -358,6 +358,8 @@ class Engine {
   std::map<std::pair<std::string, std::string>, uint64_t> pod_last_known_ns_;
   SeriesRef pods_complete_ref_;
   SeriesRef kfd_scan_refs_[3];
+  SeriesRef rx_moves_ref_;
+  int f_self_rx_moves_ = -1;
   int f_self_pods_complete_ = -1, f_self_kfd_scans_ = -1, f_self_kfd_tracked_ = -1;
   SeriesRef self_refs_[21];
 

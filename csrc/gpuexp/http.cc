@@ -6,6 +6,7 @@
 #include <netinet/tcp.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
+#include <sched.h>
 #include <sys/prctl.h>
 #include <sys/timerfd.h>
 #include <sys/socket.h>
@@ -149,6 +150,9 @@ struct HttpServer::Worker {
   int timerfd = -1;  // scrape pre-wake
   std::thread th;
   std::unordered_map<int, Conn> conns;
+  int pinned_cpu = -1;  // follow_rx_cpu: the CPU this worker is pinned to (-1: its own mask)
+  cpu_set_t own_mask;   // the thread's affinity at start
+  bool have_mask = false;
 };
 
 HttpServer::HttpServer(SnapshotStore* store, const HttpConfig& cfg) : store_(store), cfg_(cfg) {}
@@ -288,6 +292,33 @@ bool HttpServer::gzip_due(uint64_t now_ns, uint64_t horizon_ns) const {
 
 void HttpServer::run(Worker* w) {
   set_thread_name("gpuexp-http");
+  if (cfg_.follow_rx_cpu) {
+    CPU_ZERO(&w->own_mask);
+    w->have_mask = ::sched_getaffinity(0, sizeof(w->own_mask), &w->own_mask) == 0;
+  }
+  // follow_rx_cpu: after a steady connection's /metrics response, move to the CPU its
+  // requests arrive on; with no (or several) steady connections, back to the own mask
+  auto follow_rx = [&](const Conn* steady) {
+    if (!w->have_mask) return;
+    int cpu = -1;
+    if (steady) {
+      socklen_t len = sizeof(cpu);
+      if (::getsockopt(steady->fd, SOL_SOCKET, SO_INCOMING_CPU, &cpu, &len) != 0 || cpu < 0 ||
+          cpu >= CPU_SETSIZE || !CPU_ISSET(cpu, &w->own_mask))
+        cpu = -1;
+    }
+    if (cpu == w->pinned_cpu) return;
+    if (cpu >= 0) {
+      cpu_set_t one;
+      CPU_ZERO(&one);
+      CPU_SET(cpu, &one);
+      if (::sched_setaffinity(0, sizeof(one), &one) != 0) return;
+      stats_.rx_cpu_moves.fetch_add(1, std::memory_order_relaxed);
+    } else if (::sched_setaffinity(0, sizeof(w->own_mask), &w->own_mask) != 0) {
+      return;
+    }
+    w->pinned_cpu = cpu;
+  };
   constexpr int kMaxEvents = 256;
   epoll_event events[kMaxEvents];
   char rbuf[16384];
@@ -527,7 +558,18 @@ void HttpServer::run(Worker* w) {
       } else {
         respond_simple(c, 404, "Not Found", "text/plain", "not found\n", is_head);
       }
+      const bool was_metrics = c.is_metrics;
       if (!flush(c)) return false;
+      if (cfg_.follow_rx_cpu && was_metrics && !c.pending) {
+        const Conn* steady = nullptr;
+        int n_steady = 0;
+        for (auto& kv : w->conns)
+          if (kv.second.expected_next()) {
+            steady = &kv.second;
+            ++n_steady;
+          }
+        follow_rx(n_steady == 1 ? steady : nullptr);
+      }
     }
     return true;
   };

@@ -51,6 +51,11 @@ struct HttpConfig {
   uint64_t prewake_max_lead_ns = 1500000;  // ... at most
   uint64_t prewake_step_ns = 150000;
   uint64_t prewake_window_ns = 3000000;
+  // Serve a steady scraper from the CPU its requests arrive on (SO_INCOMING_CPU: where the
+  // kernel ran the receive path, the NIC queue's CPU, or the client's own for loopback): the
+  // worker is pinned there while exactly one steady /metrics connection is open, so the
+  // request's receive wakes it without a cross-CPU wake-up.  Env GPUEXP_HTTP_FOLLOW_RX_CPU.
+  bool follow_rx_cpu = false;
 };
 
 // Fixed latency buckets (seconds) for gpuexp_scrape_duration_seconds.
@@ -79,6 +84,7 @@ struct HttpStats {
   // gzip responses the worker compressed itself: the snapshot had no gzip copy because no
   // gzip scrape was expected before the next tick (see HttpServer::gzip_due)
   std::atomic<uint64_t> gzip_on_demand{0};
+  std::atomic<uint64_t> rx_cpu_moves{0};  // follow_rx_cpu: worker re-pinned to a new CPU
   std::atomic<uint64_t> lat_buckets[kBuckets + 1]{};  // +Inf last, non-cumulative
   std::atomic<uint64_t> lat_sum_ns{0};
   std::atomic<uint64_t> lat_count{0};

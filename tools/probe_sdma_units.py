@@ -18,7 +18,10 @@ import time
 
 CHILD = r"""
 import sys, time, torch
+sys.path.insert(0, {root!r})
+from kubernetes_gpu_exporter_amd.utils.kfdself import find_own_kfd_pid
 torch.zeros(1, device="cuda:0"); torch.cuda.synchronize()
+hostpid = find_own_kfd_pid(0)  # KFD names processes by host PID (the box may be a container)
 dev = torch.empty(256 << 20, dtype=torch.uint8, device="cuda:0")
 dev2 = torch.empty_like(dev)
 page = torch.empty(256 << 20, dtype=torch.uint8)
@@ -31,7 +34,7 @@ phases = {
     "d2h_pinned": lambda: pin.copy_(dev, non_blocking=True),
     "d2d": lambda: dev2.copy_(dev),
 }
-print("ready", flush=True)
+print("ready", hostpid, flush=True)
 for line in sys.stdin:
     name, secs = line.split()
     t0 = time.perf_counter(); n = 0
@@ -48,9 +51,14 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=1.5)
     args = ap.parse_args()
-    p = subprocess.Popen([sys.executable, "-c", CHILD], stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
-    assert p.stdout.readline().strip() == "ready"
-    files = sorted(glob.glob(f"/sys/class/kfd/kfd/proc/{p.pid}/sdma_*"))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.Popen([sys.executable, "-c", CHILD.replace("{root!r}", repr(root))], stdin=subprocess.PIPE,
+                         stdout=subprocess.PIPE, text=True)
+    ready = p.stdout.readline().split()
+    assert ready and ready[0] == "ready", ready
+    hostpid = int(ready[1]) if len(ready) > 1 and ready[1] != "None" else p.pid
+    print("child pid", p.pid, "KFD pid", hostpid, flush=True)
+    files = sorted(glob.glob(f"/sys/class/kfd/kfd/proc/{hostpid}/sdma_*"))
     print("files:", files, flush=True)
 
     def raw():
