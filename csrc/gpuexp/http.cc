@@ -319,17 +319,29 @@ void HttpServer::run(Worker* w) {
     }
     w->pinned_cpu = cpu;
   };
+  auto follow_steady = [&]() {
+    const Conn* steady = nullptr;
+    int n_steady = 0;
+    for (auto& kv : w->conns)
+      if (kv.second.expected_next()) {
+        steady = &kv.second;
+        ++n_steady;
+      }
+    follow_rx(n_steady == 1 ? steady : nullptr);
+  };
   constexpr int kMaxEvents = 256;
   epoll_event events[kMaxEvents];
   char rbuf[16384];
   uint64_t last_sweep = mono_ns();
   uint64_t last_prewake_ns = 0;  // this worker's last pre-wake timer expiry
 
+  bool refollow = false;  // follow_rx_cpu: a connection closed, re-check the pinning
   auto close_conn = [&](int fd) {
     ::epoll_ctl(w->epfd, EPOLL_CTL_DEL, fd, nullptr);
     ::close(fd);
     w->conns.erase(fd);
     stats_.open_conns.fetch_sub(1, std::memory_order_relaxed);
+    refollow = cfg_.follow_rx_cpu;
   };
 
   // Writes as much of the pending response as the socket takes.  Returns false if the
@@ -560,16 +572,7 @@ void HttpServer::run(Worker* w) {
       }
       const bool was_metrics = c.is_metrics;
       if (!flush(c)) return false;
-      if (cfg_.follow_rx_cpu && was_metrics && !c.pending) {
-        const Conn* steady = nullptr;
-        int n_steady = 0;
-        for (auto& kv : w->conns)
-          if (kv.second.expected_next()) {
-            steady = &kv.second;
-            ++n_steady;
-          }
-        follow_rx(n_steady == 1 ? steady : nullptr);
-      }
+      if (cfg_.follow_rx_cpu && was_metrics && !c.pending) follow_steady();
     }
     return true;
   };
@@ -601,6 +604,10 @@ void HttpServer::run(Worker* w) {
   };
 
   for (;;) {
+    if (refollow) {  // the steady scraper may be gone: unpin (or follow the one left)
+      refollow = false;
+      follow_steady();
+    }
     arm_prewake();
     int n = ::epoll_wait(w->epfd, events, kMaxEvents, 1000);
     if (n < 0 && errno != EINTR) break;

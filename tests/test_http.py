@@ -430,6 +430,71 @@ def test_scrape_prewake_learns_a_steady_period(native):
     assert run(False) == (0, 0)
 
 
+def _thread_cpus(name: str) -> set:
+    """CPUs the first thread of this process named `name` may run on."""
+    import os
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            if open(f"/proc/self/task/{tid}/comm").read().strip() == name:
+                return os.sched_getaffinity(int(tid))
+        except OSError:
+            continue
+    return set()
+
+
+def test_http_worker_follows_a_steady_scrapers_rx_cpu(native):
+    """follow_rx_cpu: once one steady scraper is learnt, the worker is pinned to the CPU its
+    requests arrive on (SO_INCOMING_CPU: the client's own CPU on loopback) and, with no steady
+    connection left, returns to its own CPU mask.  Off: never pinned."""
+    import os
+    import socket
+    own = os.sched_getaffinity(0)
+    if len(own) < 2:
+        pytest.skip("needs 2+ CPUs")
+
+    def run(follow: bool):
+        c = native.EngineConfig()
+        c.backend = "mock"
+        c.interval_s = 0
+        c.http.host = "127.0.0.1"
+        c.http.port = 0
+        c.http.follow_rx_cpu = follow
+        e = native.Engine(c)
+        e.start()
+        try:
+            e.tick(1_000_000_000)
+            cpu = min(own)
+            os.sched_setaffinity(0, {cpu})  # the scraping thread sends from one known CPU
+            try:
+                cl = native.ScrapeClient("127.0.0.1", e.http_port, "/metrics")
+                t = time.monotonic()
+                for _ in range(8):
+                    t += 0.030
+                    time.sleep(max(0.0, t - time.monotonic()))
+                    assert cl.scrape() > 0
+                pinned = _thread_cpus("gpuexp-http")
+                moves = e.stats()["http_rx_cpu_moves"]
+                del cl  # closes the connection: no steady scraper left
+                s = socket.create_connection(("127.0.0.1", e.http_port))
+                s.sendall(b"GET /metrics HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n")
+                while s.recv(65536):
+                    pass
+                s.close()
+                time.sleep(0.05)
+                after = _thread_cpus("gpuexp-http")
+            finally:
+                os.sched_setaffinity(0, own)
+            return pinned, moves, after, cpu
+        finally:
+            e.stop()
+
+    pinned, moves, after, cpu = run(True)
+    assert pinned == {cpu} and moves >= 1, (pinned, moves)
+    assert after == own, after
+    pinned, moves, after, _ = run(False)
+    assert pinned == own and moves == 0 and after == own
+
+
 def test_gzip_copy_follows_the_scrape_schedule(native):
     """A steady keep-alive gzip scraper (every 200 ms) against a 100 Hz sampler: once its
     period is learnt, the sampler compresses only in the ticks just before each expected
