@@ -475,6 +475,7 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("infer_device_owner", &EngineConfig::infer_device_owner)
       .def_readwrite("process_source", &EngineConfig::process_source)
       .def_readwrite("kfd_cu_occupancy", &EngineConfig::kfd_cu_occupancy)
+      .def_readwrite("kfd_sdma", &EngineConfig::kfd_sdma)
       .def_readwrite("kfd_detail_interval_s", &EngineConfig::kfd_detail_interval_s)
       .def_readwrite("exclude_self", &EngineConfig::exclude_self)
       .def_readwrite("enable_sentinel", &EngineConfig::enable_sentinel)
@@ -486,6 +487,7 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("counters_mode", &EngineConfig::counters_mode)
       .def_readwrite("counters_sync_us", &EngineConfig::counters_sync_us)
       .def_readwrite("counters_kick", &EngineConfig::counters_kick)
+      .def_readwrite("counters_inline", &EngineConfig::counters_inline)
       .def_readwrite("counters_window_ms", &EngineConfig::counters_window_ms)
       .def_readwrite("counters_interval_ms", &EngineConfig::counters_interval_ms)
       .def_readwrite("enable_rccl", &EngineConfig::enable_rccl)

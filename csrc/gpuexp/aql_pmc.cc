@@ -188,7 +188,8 @@ std::condition_variable g_done_cv;
 std::atomic<uint64_t> g_thread_cpu_ns{0};  // the counting thread's own CPU, published per round
 // where a continuous read round's CPU goes (counting thread clock): post / wait / collect
 std::atomic<uint64_t> g_round_cpu[3] = {}, g_rounds{0};
-// Inline rounds (continuous mode; GPUEXP_PMC_INLINE=1 turns it on): the
+// Inline rounds (continuous mode; gpuexp_rp_set_inline, which the engine calls when its
+// sampler ticks periodically; GPUEXP_PMC_INLINE=0/1 overrides): the
 // engine's sampler posts the round's read packets itself at gpuexp_rp_kick and collects them
 // at gpuexp_rp_sync, after its device reads (~100-400 us later: the reads are done by then),
 // so a tick costs the counting thread no wake-ups at all; the thread only runs rounds when
@@ -1328,6 +1329,11 @@ extern "C" __attribute__((visibility("default"))) void gpuexp_rp_set_duty(int wi
   g_window_ms = std::max(1, window_ms);
   g_interval_ms = std::max(g_window_ms, interval_ms);
 }
+
+// Inline rounds (before gpuexp_rp_init): the caller of gpuexp_rp_kick / gpuexp_rp_sync runs
+// each round itself.  Only for an engine that kicks every tick: with sparse manual ticks the
+// counting thread's own rounds keep the windows short (thread mode).
+extern "C" __attribute__((visibility("default"))) void gpuexp_rp_set_inline(int on) { g_inline = on != 0; }
 
 // Continuous counting: started once, read once per gpuexp_rp_kick (one engine tick), or
 // every `fallback_ms` when nothing kicks.

@@ -87,6 +87,9 @@ struct EngineConfig {
   bool infer_device_owner = true;      // single-pod GPU -> device series carry the pod
   std::string process_source = "auto";  // auto | kfd | amdsmi | none
   bool kfd_cu_occupancy = true;
+  // KFD's per-process sdma_<gpu_id>: off by default, it is not SDMA time on MI355X
+  // (profiles/r04/sdma_units.txt: one jump of 1.24e12 at the first copy, then flat)
+  bool kfd_sdma = false;
   double kfd_detail_interval_s = 1.0;  // cu_occupancy / sdma re-read period (0 = every tick)
   // KFD proc directory listed at least this often (and on its mtime moving, or a tracked
   // process vanishing); tracked processes' VRAM is read every tick either way (0 = list every tick)
@@ -108,6 +111,7 @@ struct EngineConfig {
   // "after_devices": once the gpu_metrics SMU fetches are done (a PM4 read in flight while
   // the SMU serves the metrics table slows the fetch, profiles/r04/devices_split.txt).
   std::string counters_kick = "start";
+  bool counters_inline = true;  // continuous + periodic ticks: the sampler runs the read rounds
   bool enable_rccl = false;
   std::string rccl_dir = "/dev/shm";
   bool rccl_verify = true;             // attribute a tracer file only to a process that maps it

@@ -42,8 +42,12 @@ using rp_health_fn = int (*)(int dev, uint64_t* out, int n);
 
 class PluginCounters : public CounterSource {
  public:
-  PluginCounters(std::string path, int window_ms, int interval_ms, bool continuous)
-      : path_(std::move(path)), window_ms_(window_ms), interval_ms_(interval_ms), continuous_(continuous) {}
+  PluginCounters(std::string path, int window_ms, int interval_ms, bool continuous, bool inline_rounds)
+      : path_(std::move(path)),
+        window_ms_(window_ms),
+        interval_ms_(interval_ms),
+        continuous_(continuous),
+        inline_(inline_rounds) {}
   ~PluginCounters() override { stop(); }
 
   bool start(const std::vector<DeviceInfo>& devs, std::string* err) override {
@@ -69,6 +73,8 @@ class PluginCounters : public CounterSource {
       // counting never stops; one read per engine tick (kick/sync), or every interval_ms
       // when no tick kicks (manual-tick engines)
       cont(interval_ms_);
+      using inline_fn = void (*)(int);
+      if (auto inl = reinterpret_cast<inline_fn>(::dlsym(handle_, "gpuexp_rp_set_inline"))) inl(inline_ ? 1 : 0);
       kick_ = reinterpret_cast<rp_kick_fn>(::dlsym(handle_, "gpuexp_rp_kick"));
       sync_ = reinterpret_cast<rp_sync_fn>(::dlsym(handle_, "gpuexp_rp_sync"));
     } else if (auto duty = reinterpret_cast<duty_fn>(::dlsym(handle_, "gpuexp_rp_set_duty"))) {
@@ -156,6 +162,7 @@ class PluginCounters : public CounterSource {
   std::string path_;
   int window_ms_, interval_ms_;
   bool continuous_;
+  bool inline_;  // continuous: the engine's sampler runs each read round (gpuexp_rp_set_inline)
   rp_kick_fn kick_ = nullptr;
   rp_sync_fn sync_ = nullptr;
   rp_cpu_fn cpu_ = nullptr;
@@ -739,8 +746,8 @@ std::unique_ptr<SentinelSource> make_queue_sentinel(const std::string& counters_
 std::string default_rocprof_plugin() { return self_dir() + "/_gpuexp_aqlpmc.so"; }
 
 std::unique_ptr<CounterSource> make_rocprof_counters(const std::string& plugin_path, int window_ms,
-                                                     int interval_ms, bool continuous) {
-  return std::make_unique<PluginCounters>(plugin_path, window_ms, interval_ms, continuous);
+                                                     int interval_ms, bool continuous, bool inline_rounds) {
+  return std::make_unique<PluginCounters>(plugin_path, window_ms, interval_ms, continuous, inline_rounds);
 }
 
 std::unique_ptr<RcclSource> make_rccl_source(const std::string& dir, bool verify_maps, double scan_interval_s) {

@@ -10,8 +10,8 @@
 namespace gpuexp {
 
 KfdProcReader::KfdProcReader(std::string host_root, int self_pid, bool read_cu_occupancy,
-                             uint64_t detail_interval_ns, uint64_t rescan_interval_ns)
-    : root_(std::move(host_root)), self_(self_pid), read_cu_(read_cu_occupancy),
+                             uint64_t detail_interval_ns, uint64_t rescan_interval_ns, bool read_sdma)
+    : root_(std::move(host_root)), self_(self_pid), read_cu_(read_cu_occupancy), read_sdma_(read_sdma),
       detail_every_ns_(detail_interval_ns), rescan_ns_(rescan_interval_ns) {
   if (!root_.empty() && root_.back() == '/') root_.pop_back();
 }
@@ -60,7 +60,7 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
         std::string id = std::to_string(d.kfd_gpu_id);
         if (!pd.vram.open(pdir + "/vram_" + id)) continue;
         if (read_cu_) pd.cu.open(pdir + "/stats_" + id + "/cu_occupancy");
-        pd.sdma.open(pdir + "/sdma_" + id);
+        if (read_sdma_) pd.sdma.open(pdir + "/sdma_" + id);
         pd.evicted.open(pdir + "/stats_" + id + "/evicted_ms");
         e.devs.push_back(std::move(pd));
       }

@@ -26,8 +26,9 @@ class KfdProcReader {
   // scan).  Measured on MI355X (profiles/r01/kfd_read_costs.txt): vram_<id> ~6 us,
   // stats_<id>/cu_occupancy ~15 us (KFD asks the hardware), sdma_<id> ~7 us per process
   // per GPU — VRAM is what the legacy families and attribution need every tick.
+  // read_sdma: also read sdma_<id> (the engine's kfd_sdma; off by default, see EngineConfig).
   KfdProcReader(std::string host_root, int self_pid, bool read_cu_occupancy, uint64_t detail_interval_ns = 0,
-                uint64_t rescan_interval_ns = 0);
+                uint64_t rescan_interval_ns = 0, bool read_sdma = true);
   // Fills per_dev[d] with the processes that have a KFD context on device d.
   void scan(const std::vector<DeviceInfo>& devs, std::vector<std::vector<ProcSample>>* per_dev,
             uint64_t now_ns = 0);
@@ -53,6 +54,7 @@ class KfdProcReader {
   std::string root_;
   int self_;
   bool read_cu_;
+  bool read_sdma_;
   uint64_t detail_every_ns_;
   uint64_t rescan_ns_ = 0;       // list the KFD proc directory at least this often (0: every scan)
   uint64_t last_list_ns_ = 0;

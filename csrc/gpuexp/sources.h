@@ -76,8 +76,11 @@ class CounterSource {
 // dlopen()s a counter plugin (_gpuexp_aqlpmc.so or _gpuexp_rocprof.so) next to the core.
 // continuous (aqlprofile plugin only): counting runs without a break and is read once per
 // engine tick; otherwise duty-cycled: a `window_ms` counting window every `interval_ms`.
+// inline_rounds (continuous): the engine's sampler posts and collects each read round itself
+// (no counting-thread wake-up per tick); for an engine that ticks periodically.
 std::unique_ptr<CounterSource> make_rocprof_counters(const std::string& plugin_path, int window_ms,
-                                                     int interval_ms, bool continuous = false);
+                                                     int interval_ms, bool continuous = false,
+                                                     bool inline_rounds = false);
 
 // One collective call record written by the RCCL tracer tool into a per-process ring.
 struct RcclTotals {

@@ -43,6 +43,7 @@ class Config:
     legacy_families: bool = True           # pod_gpu_memory_usage / docker_gpu_memory_perc_usage
     process_source: str = "auto"           # auto | kfd | amdsmi | none
     kfd_cu_occupancy: bool = True
+    kfd_sdma_activity: bool = False        # KFD sdma_<id> per process: not SDMA time on MI355X (profiles/r04)
     kfd_detail_interval: float = 1.0       # seconds between cu_occupancy / sdma re-reads (0 = every tick)
     kfd_rescan_interval: float = 0.5       # KFD proc directory listed at least this often (also on change)
     gc_after: int = 1
@@ -56,6 +57,8 @@ class Config:
     counters_window_ms: int = 20           # duty: counting window ...
     counters_interval_ms: int = 1000       # ... per interval (the rocprof plugin's spin is duty-cycled)
     counters_kick: str = "start"           # continuous: a tick's PMC read goes out at its start | after_devices
+    counters_inline: bool = True           # continuous: the sampler posts/collects each tick's PMC read itself
+    http_follow_rx_cpu: bool = False       # pin the HTTP worker to the CPU a steady scraper's requests arrive on
     queue_devices: list = field(default_factory=list)  # GPUs (indices / BDFs) that get the exporter's
                                            # own GPU queue (sentinel + PMC counters); empty = all.
                                            # Each queue pins ~346 MiB of host memory on MI355X.
@@ -137,6 +140,7 @@ class Config:
         hc.threads = int(self.http_threads)
         hc.enable_gzip = bool(self.gzip)
         hc.prewake = bool(self.http_prewake)
+        hc.follow_rx_cpu = bool(self.http_follow_rx_cpu)
         stale = float(self.stale_after)
         if stale < 0:
             stale = max(5.0, 10.0 * float(self.interval)) if float(self.interval) > 0 else 0.0
@@ -149,6 +153,7 @@ class Config:
         ec.infer_device_owner = bool(self.infer_device_owner)
         ec.process_source = self.process_source
         ec.kfd_cu_occupancy = bool(self.kfd_cu_occupancy)
+        ec.kfd_sdma = bool(self.kfd_sdma_activity)
         ec.kfd_detail_interval_s = float(self.kfd_detail_interval)
         ec.kfd_rescan_interval_s = float(self.kfd_rescan_interval)
         ec.enable_sentinel = bool(self.enable_sentinel)
@@ -164,6 +169,7 @@ class Config:
         ec.counters_window_ms = int(self.counters_window_ms)
         ec.counters_interval_ms = int(self.counters_interval_ms)
         ec.counters_kick = str(self.counters_kick)
+        ec.counters_inline = bool(self.counters_inline)
         ec.enable_rccl = bool(self.enable_rccl)
         ec.rccl_dir = self.rccl_dir
         ec.rccl_verify = bool(self.rccl_verify)

@@ -431,6 +431,23 @@ def test_kfd_detail_files_are_rate_limited(native, tmp_path):
     e.stop()
 
 
+def test_kfd_sdma_family_is_opt_in(native, tmp_path):
+    """KFD's per-process sdma_<id> is not SDMA time on MI355X (profiles/r04/sdma_units.txt:
+    one jump of 1.24e12 at a process's first copy, then flat under 55 GB/s of copies), so
+    amd_gpu_process_sdma_seconds_total is exported only with kfd_sdma_activity."""
+    h = mi355x_node(tmp_path, 1)
+    (g,) = h.gpus
+    h.add_process(777, kubepods_cgroup(UID, CID), gpus={g.gpu_id: (1000, 10)})
+    h.set_process_gpu(777, g.gpu_id, vram=1000, cu=10, sdma_us=2_500_000)
+    for opt_in, want in ((False, {}), (True, {"777": 2.5})):
+        e = _engine(native, tmp_path, kfd_sdma=opt_in)
+        e.tick(1 * S)
+        got = {s[1]["pid"]: s[2] for s in promtext.samples(promtext.parse(e.snapshot_text()),
+                                                            "amd_gpu_process_sdma_seconds_total")}
+        e.stop()
+        assert got == want, (opt_in, got)
+
+
 def test_hip_order_bdfs_and_bdf_device_filter(native, tmp_path, monkeypatch):
     """HIP device order comes from KFD topology node order (not PCI order), and the engine
     can be told to watch GPUs by BDF."""
