@@ -26,6 +26,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import signal
 import socket
 import statistics
 import subprocess
@@ -61,7 +62,10 @@ def http_get(port: int, path: str, timeout: float = 2.0) -> tuple[int, bytes]:
 def start_exporter(args, n_gpus: int, backend: str, port: int, pod_map: str, log_path: str, rccl_dir: str = ""):
     cmd = [sys.executable, "-m", "kubernetes_gpu_exporter_amd", "--listen", f"127.0.0.1:{port}",
            "--interval", str(1.0 / args.sample_hz), "--backend", backend,
-           "--series-profile", args.series_profile, "--control-interval", "0.5", "--log-level", "warn"]
+           "--series-profile", args.series_profile, "--log-level", "warn"]
+    if os.environ.get("GPUEXP_BENCH_EXPORTER_ROOT"):
+        # an older checkout (A/B hook) may not re-read pod metadata on SIGHUP: poll fast instead
+        cmd += ["--control-interval", "0.5"]
     if backend != "mock":
         # Watch exactly the GPUs the ranks run on: HIP device i -> PCI BDF (KFD topology order,
         # read without initialising the GPU), falling back to exporter indices.
@@ -459,8 +463,12 @@ def main() -> int:
                 # mock GPU r (KFD gpu_id 1000 + r) holds rank r's buffers
                 FakeHost(args.fake_root).set_process_gpu(p, 1000 + r, vram=(r + 1) << 30, cu=32)
         write_pod_map(pod_map, pods, cgroups)
+        if exporter is not None and not os.environ.get("GPUEXP_BENCH_EXPORTER_ROOT"):
+            # the exporter's control plane refreshes every 5 s (its default); SIGHUP makes it
+            # read the new pod map now
+            exporter.send_signal(signal.SIGHUP)
         # Untimed: wait until the exporter has picked the pod map up and attributes every
-        # rank (its control plane re-reads the file every 0.5 s), so even a short warmup
+        # rank (SIGHUP above: its control plane re-reads the file at once), so even a short warmup
         # measures the steady state.
         # With the RCCL tracer on, also until every rank's communicator is attributed to its
         # pod (each rank has run collectives by now: the GEMM-count all-reduce above).

@@ -81,8 +81,13 @@ class Exporter:
             log.info("signal %s: shutting down", signum)
             self._stop.set()
 
+        def _refresh(signum, frame):
+            if self._control is not None and hasattr(self._control, "refresh_soon"):
+                self._control.refresh_soon()
+
         signal.signal(signal.SIGTERM, _handler)
         signal.signal(signal.SIGINT, _handler)
+        signal.signal(signal.SIGHUP, _refresh)  # re-read pod metadata now
         self.start()
         log.info("serving %s on %s (%s)", self.cfg.path, self.cfg.listen, self.engine.source_status())
         # no timeout: lock waits are interrupted by signals, the handler sets the event, and

@@ -72,6 +72,7 @@ class ControlPlane:
         self.engine = None
         self._thread: Optional[threading.Thread] = None
         self._stop = threading.Event()
+        self._kick = threading.Event()  # refresh_soon(): refresh now instead of at the interval
         self._last_fp = None
         self._pushed_pids: set = set()
         self.errors: dict = {}
@@ -159,15 +160,22 @@ class ControlPlane:
         while not self._stop.is_set():
             t0 = time.monotonic()
             self.refresh_once()
-            self._stop.wait(max(0.05, self.interval - (time.monotonic() - t0)))
+            self._kick.wait(max(0.05, self.interval - (time.monotonic() - t0)))
+            self._kick.clear()
 
     def start(self) -> None:
         self.refresh_once()
         self._thread = threading.Thread(target=self._run, name="gpuexp-control", daemon=True)
         self._thread.start()
 
+    def refresh_soon(self) -> None:
+        """Refreshes at once instead of at the next interval (SIGHUP to the exporter: e.g. a
+        pod map file rewritten by a scheduler, or an operator who wants new pods now)."""
+        self._kick.set()
+
     def stop(self) -> None:
         self._stop.set()
+        self._kick.set()
         if self._thread is not None:
             self._thread.join(timeout=5)
         for s in self.sources:

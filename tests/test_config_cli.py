@@ -91,6 +91,59 @@ def test_cli_daemon_lifecycle(tmp_path):
     assert {e["name"] for e in events} >= {"devices", "processes", "render"}
 
 
+def test_cli_sighup_refreshes_instead_of_exiting(tmp_path):
+    """SIGHUP asks the control plane to re-read pod metadata now (the bench sends it after
+    writing its pod map); the daemon keeps serving and still exits cleanly on SIGTERM."""
+    port = _free_port()
+    pod_map = tmp_path / "pods.json"
+    pod_map.write_text('{"pods": [], "pid_cgroups": {}, "device_owners": {}}')
+    env = dict(os.environ, GPUEXP_POD_MAP_FILE=str(pod_map))
+    p = subprocess.Popen([sys.executable, "-m", "kubernetes_gpu_exporter_amd", "--backend", "mock",
+                          "--listen", f"127.0.0.1:{port}", "--interval", "0.05", "--control-interval", "60"],
+                         cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    try:
+        for _ in range(200):
+            try:
+                urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=1).read()
+                break
+            except Exception:
+                time.sleep(0.05)
+        p.send_signal(signal.SIGHUP)
+        time.sleep(0.3)
+        assert p.poll() is None
+        assert urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=1).status == 200
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(timeout=15) == 0
+    finally:
+        if p.poll() is None:
+            p.kill()
+
+
+def test_control_plane_refresh_soon():
+    from kubernetes_gpu_exporter_amd.k8s.controlplane import ControlPlane, Metadata
+
+    class _Src:
+        name = "src"
+
+        def fetch(self):
+            return Metadata()
+
+    cp = ControlPlane([_Src()], interval=60.0)
+    cp.start()
+    try:
+        n0 = cp.refreshes
+        time.sleep(0.1)
+        assert cp.refreshes == n0  # the interval has not passed
+        cp.refresh_soon()
+        for _ in range(100):
+            if cp.refreshes > n0:
+                break
+            time.sleep(0.01)
+        assert cp.refreshes == n0 + 1
+    finally:
+        cp.stop()
+
+
 def test_stale_after_defaults_follow_the_interval(native):
     from kubernetes_gpu_exporter_amd.config import make_config
     def ns(**kw):
