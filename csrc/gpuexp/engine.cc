@@ -466,6 +466,9 @@ bool Engine::start(std::string* err) {
     HttpConfig hc = cfg_.http;
     hc.gzip_level = cfg_.gzip_level;
     if (const char* e = std::getenv("GPUEXP_HTTP_FOLLOW_RX_CPU")) hc.follow_rx_cpu = e[0] != '0';
+    // experiment knobs (A/B on a box): pre-wake slice and minimum lead, microseconds
+    if (const char* e = std::getenv("GPUEXP_HTTP_PREWAKE_STEP_US")) hc.prewake_step_ns = uint64_t(std::atoll(e)) * 1000;
+    if (const char* e = std::getenv("GPUEXP_HTTP_PREWAKE_LEAD_US")) hc.prewake_lead_ns = uint64_t(std::atoll(e)) * 1000;
     http_ = std::make_unique<HttpServer>(&store_, hc);
     if (!http_->start(err)) {
       http_.reset();
