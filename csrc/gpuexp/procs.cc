@@ -316,6 +316,10 @@ const CgroupInfo* PidResolver::resolve(int pid) {
     return &e.info;
   }
   auto it = cache_.find(pid);
+  if (it != cache_.end() && !it->second.ok) {  // failed before: not again this tick or for a while
+    const Entry& e = it->second;
+    if (e.epoch == epoch_ || (now_ns_ >= e.failed_ns && now_ns_ - e.failed_ns < kRetryFailedNs)) return nullptr;
+  }
   if (it != cache_.end() && it->second.ok) {
     Entry& e = it->second;
     if (e.epoch == epoch_) return &e.info;  // already checked this tick
@@ -338,7 +342,10 @@ const CgroupInfo* PidResolver::resolve(int pid) {
   std::string content;
   const std::string dir = root_ + "/proc/" + std::to_string(pid);
   if (!read_small_file(dir + "/cgroup", &content)) {
-    cache_.erase(pid);
+    Entry& f = cache_[pid];
+    f = Entry();  // ok = false
+    f.epoch = epoch_;
+    f.failed_ns = now_ns_;
     return nullptr;
   }
   Entry& e = cache_[pid];

@@ -95,7 +95,8 @@ class PidResolver {
     ++epoch_;
     now_ns_ = now_ns;
   }
-  // Returns nullptr if the PID cannot be read (other PID namespace, exited).
+  // Returns nullptr if the PID cannot be read (other PID namespace, exited).  A failure is
+  // remembered: the PID is not looked up again within the tick nor for kRetryFailedNs.
   const CgroupInfo* resolve(int pid);
   // Test/bench hook: pretend /proc/<pid>/cgroup contains `cgroup_path`.
   void set_override(int pid, const std::string& cgroup_path);
@@ -110,9 +111,13 @@ class PidResolver {
     std::shared_ptr<CachedFile> comm;  // /proc/<pid>/comm, kept open (liveness)
     uint64_t epoch = 0;                // tick it was last checked in
     uint64_t st_checked_ns = 0;        // engine time of the last starttime check
+    uint64_t failed_ns = 0;            // !ok: engine time of the failed lookup
   };
   bool read_starttime(int pid, uint64_t* st);
   static constexpr uint64_t kStarttimeEveryNs = 1000000000ull;
+  // An unreadable PID (a host PID from inside a PID namespace, hidepid, a process gone) was
+  // looked up again on every call: 2 failed opens per call, 2 calls per process per tick.
+  static constexpr uint64_t kRetryFailedNs = 1000000000ull;
   uint64_t epoch_ = 1, now_ns_ = 0;
   std::string root_;
   std::unordered_map<int, Entry> cache_;

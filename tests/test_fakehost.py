@@ -431,6 +431,33 @@ def test_kfd_detail_files_are_rate_limited(native, tmp_path):
     e.stop()
 
 
+def test_unreadable_pid_is_not_looked_up_every_tick(native, tmp_path):
+    """A GPU process whose /proc/<pid> the exporter cannot read (a host PID seen from inside
+    a PID namespace, hidepid, a process on its way out) is looked up again at most once a
+    second, not on every call of every tick; once readable it is attributed."""
+    import shutil
+    h = mi355x_node(tmp_path, 1)
+    (g,) = h.gpus
+    h.add_process(4242, kubepods_cgroup(UID, CID), gpus={g.gpu_id: (1000, 10)})
+    shutil.rmtree(tmp_path / "proc" / "4242")  # KFD lists it; /proc does not show it
+    e = _engine(native, tmp_path)
+    e.set_pods([dict(uid=UID, namespace="research", name="llama-train-0", containers={CID: "trainer"})])
+
+    def attributed():
+        f = promtext.parse(e.snapshot_text())
+        return [lab["pod"] for _, lab, _ in promtext.samples(f, "amd_gpu_process_vram_bytes")
+                if lab["pid"] == "4242"]
+
+    e.tick(1 * S)
+    assert attributed() == [""]               # exported, unattributed
+    h.add_process(4242, kubepods_cgroup(UID, CID), gpus={g.gpu_id: (1000, 10)})
+    e.tick(1 * S + 300_000_000)               # within the retry interval: not looked up again
+    assert attributed() == [""]
+    e.tick(2 * S + 100_000_000)               # past it: found
+    assert attributed() == ["llama-train-0"]
+    e.stop()
+
+
 def test_kfd_sdma_family_is_opt_in(native, tmp_path):
     """KFD's per-process sdma_<id> is not SDMA time on MI355X (profiles/r04/sdma_units.txt:
     one jump of 1.24e12 at a process's first copy, then flat under 55 GB/s of copies), so
