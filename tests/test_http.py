@@ -431,6 +431,40 @@ def test_scrape_prewake_learns_a_steady_period(native):
     assert run(False) == (0, 0)
 
 
+def test_prewake_survives_one_late_scrape(native):
+    """One late scrape (a pause between a benchmark's warm-up and its timed window, a GC
+    stall in the scraper) costs only its own pre-wake: the learnt period is the newest
+    interval another recent one agrees with, so the next request is pre-woken again."""
+    c = native.EngineConfig()
+    c.backend = "mock"
+    c.interval_s = 0
+    c.http.host = "127.0.0.1"
+    c.http.port = 0
+    e = native.Engine(c)
+    e.start()
+    try:
+        e.tick(1_000_000_000)
+        cl = native.ScrapeClient("127.0.0.1", e.http_port, "/metrics")
+        t = time.monotonic()
+
+        def scrape_at(dt):
+            nonlocal t
+            t += dt
+            time.sleep(max(0.0, t - time.monotonic()))
+            assert cl.scrape() > 0
+
+        for _ in range(6):
+            scrape_at(0.050)
+        scrape_at(0.110)  # late
+        h0 = e.stats()["http_prewake_hits"]
+        for _ in range(4):
+            scrape_at(0.050)
+        hits = e.stats()["http_prewake_hits"] - h0
+    finally:
+        e.stop()
+    assert hits >= 3, hits  # the 4 on-period scrapes after the late one (one may jitter out)
+
+
 def _thread_cpus(name: str) -> set:
     """CPUs the first thread of this process named `name` may run on."""
     import os
