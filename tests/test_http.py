@@ -453,12 +453,12 @@ def test_prewake_survives_one_late_scrape(native):
             time.sleep(max(0.0, t - time.monotonic()))
             assert cl.scrape() > 0
 
-        for _ in range(6):
-            scrape_at(0.050)
-        scrape_at(0.110)  # late
+        for _ in range(5):
+            scrape_at(0.100)
+        scrape_at(0.190)  # late
         h0 = e.stats()["http_prewake_hits"]
         for _ in range(4):
-            scrape_at(0.050)
+            scrape_at(0.100)
         hits = e.stats()["http_prewake_hits"] - h0
     finally:
         e.stop()
