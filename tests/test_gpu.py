@@ -797,6 +797,7 @@ def test_device_counters_under_gemm(plugin, monkeypatch):
     res = _feature_check("counters", "3")
     if "counters=unavailable" in res["status"]:
         pytest.skip("device counting unavailable on this box: " + res["status"])
+    assert res["gemm_running_at_snapshot"], res
     assert res["amd_gpu_mfma_busy_percent"] is not None, res
     assert res["amd_gpu_mfma_busy_percent"] > 10, res   # an MFMA GEMM is running
     assert res["amd_gpu_gui_active_percent"] > 50, res

@@ -25,7 +25,8 @@ def counters(seconds: float) -> dict:
     child = subprocess.Popen([sys.executable, "-c",
                               f"import sys; sys.path.insert(0, {ROOT!r});"
                               "from kubernetes_gpu_exporter_amd.ops.gemm import gemm_burn;"
-                              f"print(gemm_burn(0, 8192, {seconds + 3}, 4), flush=True)"],
+                              # long enough to outlast a slow plugin start; stopped after the snapshot
+                              f"print(gemm_burn(0, 8192, {seconds + 20}, 4), flush=True)"],
                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     time.sleep(2.0)  # let the child start its GEMM loop
     from kubernetes_gpu_exporter_amd._native import load
@@ -64,6 +65,7 @@ def counters(seconds: float) -> dict:
         time.sleep(0.05)
     text = e.snapshot_text()
     status = e.source_status()
+    gemm_running = child.poll() is None  # the snapshot's window lies inside the GEMM's run
 
     dbg = ctypes.create_string_buffer(4096)
     try:
@@ -72,7 +74,8 @@ def counters(seconds: float) -> dict:
         pass
     e.stop()
     fams = promtext.parse(text)
-    out = {"status": status, "raw_counters": dbg.value.decode(), "hot_threads": [(round(p, 1), k) for p, k in hot]}
+    out = {"status": status, "raw_counters": dbg.value.decode(), "hot_threads": [(round(p, 1), k) for p, k in hot],
+           "gemm_running_at_snapshot": gemm_running}
     for name in ("amd_gpu_mfma_busy_percent", "amd_gpu_sq_busy_percent", "amd_gpu_gui_active_percent",
                  "amd_gpu_waves_per_second", "amd_gpu_lds_active_percent", "amd_gpu_lds_bank_conflict_percent",
                  "amd_gpu_hbm_read_bytes_per_second", "amd_gpu_hbm_write_bytes_per_second",
@@ -86,6 +89,7 @@ def counters(seconds: float) -> dict:
         if name.startswith("amd_gpu_") and not name.startswith("amd_gpu_process_"):
             per_gpu += sum(1 for s in fam.samples if s[1].get("gpu") == "0")
     out["series_gpu0"] = per_gpu
+    child.terminate()
     child.wait(timeout=60)
     return out
 
