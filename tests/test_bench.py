@@ -45,6 +45,10 @@ def test_bench_single_process():
     assert r.returncode == 0, r.stderr[-2000:]
     (d,) = _json_lines(r.stdout)
     _check(d, 1, 5, 1)
+    # where the exporter's CPU went, per thread name, and its KFD scans (diagnostics)
+    assert d["exporter_cpu_us_per_step_by_thread"].get("gpuexp-sampler", 0) > 0, d["exporter_cpu_us_per_step_by_thread"]
+    assert set(d["kfd_proc_scans"]) == {"list", "tracked"} and d["kfd_procs_tracked"] >= 1, d
+    assert d["http_rx_cpu_moves"] == 0  # follow_rx_cpu is off by default
     # Native libraries (RCCL's banner) and the exporter child write to stderr only.
     assert r.stdout.strip().count("\n") == 0, r.stdout[-2000:]
 
