@@ -24,7 +24,7 @@
 // the latest completed window.
 //
 // Event ids are the gfx950 select values of /opt/rocm/share/rocprofiler-sdk/counter_defs.yaml
-// (SQ 93/3/4/147/142, GRBM 2/0, TCC 112/115/113/117, SPI 91/120/103/109) and are checked with
+// (SQ 93/3/4/147/142, GRBM 2/0, TCC 112/115/113/117, SPI 91/120/103/109/115) and are checked with
 // hsa_ven_amd_aqlprofile_validate_event at init.  TCC is programmed on every channel
 // instance (16 per XCD); SQ and GRBM are broadcast and come back once per SE / XCC.
 #include <execinfo.h>
@@ -81,7 +81,7 @@ const EventDef kGfx950[] = {
     {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 52, kMopsBf16},    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SQ, 56, kMopsF8},
     {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SPI, 91, kSpiResStall}, {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SPI, 120, kSpiLdsFull},
     {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SPI, 103, kSpiWaveFull}, {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SPI, 109, kSpiVgprFull},
-    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SPI, 52, kSpiWave},     {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SPI, 49, kSpiTg},
+    {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SPI, 115, kSpiSgprFull},
 };
 
 struct Agent {
@@ -441,13 +441,8 @@ bool setup_agent(Agent& a, std::string* why) {
   // GPUEXP_PMC_NO_SPI=1: without the SPI occupancy-limiter events (and the fallback below)
   const char* no_spi = std::getenv("GPUEXP_PMC_NO_SPI");
   const bool want_spi = !(no_spi && no_spi[0] == '1');
-  // experiment (GPUEXP_PMC_SPI_WAVES=1): SPI_CSN_WAVE / _NUM_THREADGROUPS as device-wide wave
-  // and workgroup counts, if they see other processes like the allocator counters do
-  const char* spi_waves = std::getenv("GPUEXP_PMC_SPI_WAVES");
-  const bool want_spi_waves = spi_waves && spi_waves[0] == '1';
   for (const auto& def : kGfx950) {
     if (def.block == HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SPI && !want_spi) continue;
-    if ((def.ctr == kSpiWave || def.ctr == kSpiTg) && !want_spi_waves) continue;
     const uint32_t n = def.block == HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_TCC ? tcc.instance_count : 1;
     for (uint32_t i = 0; i < n; ++i) {
       hsa_ven_amd_aqlprofile_event_t ev{def.block, i, def.id};

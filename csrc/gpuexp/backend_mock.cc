@@ -193,6 +193,7 @@ bool MockBackend::counters(const DeviceInfo& dev, double dt_s, CounterReading* o
   out->lds_limited_pct = get(s, "lds_limited_pct", 80.0);
   out->wave_limited_pct = get(s, "wave_limited_pct", 10.0);
   out->vgpr_limited_pct = get(s, "vgpr_limited_pct", 0.0);
+  out->sgpr_limited_pct = get(s, "sgpr_limited_pct", 0.0);
   // every XCD equally busy unless scripted ("xcc_mfma_busy_pct" sets them all)
   out->nxcc = int(std::min<uint32_t>(dev.num_xcc, uint32_t(kMaxXcc)));
   for (int x = 0; x < out->nxcc; ++x) out->xcc_mfma_busy_pct[x] = get(s, "xcc_mfma_busy_pct", out->mfma_busy_pct);

@@ -50,8 +50,7 @@ enum Ctr {
   kSpiLdsFull,   // per such cycle: CUs whose free LDS cannot take the wave
   kSpiWaveFull,  // per such cycle: SIMDs with no free wave slot
   kSpiVgprFull,  // per such cycle: SIMDs with too few free VGPRs
-  kSpiWave,      // SPI_CSN_WAVE: compute waves launched (experiment: GPUEXP_PMC_SPI_WAVES=1)
-  kSpiTg,        // SPI_CSN_NUM_THREADGROUPS: compute workgroups launched (same)
+  kSpiSgprFull,  // per such cycle: SIMDs with too few free SGPRs
   kNumCtr
 };
 
@@ -64,8 +63,7 @@ inline const char* name(int c) {
                                         "SQ_CYCLES",                "SQ_INSTS_VALU_MFMA_MOPS_BF16",
                                         "SQ_INSTS_VALU_MFMA_MOPS_F8", "SPI_RA_RES_STALL_CSN",
                                         "SPI_RA_LDS_CU_FULL_CSN",   "SPI_RA_WAVE_SIMD_FULL_CSN",
-                                        "SPI_RA_VGPR_SIMD_FULL_CSN", "SPI_CSN_WAVE",
-                                        "SPI_CSN_NUM_THREADGROUPS"};
+                                        "SPI_RA_VGPR_SIMD_FULL_CSN", "SPI_RA_SGPR_SIMD_FULL_CSN"};
   return kNames[c];
 }
 
@@ -74,7 +72,7 @@ inline bool use_max(int c) { return c == kGuiActive || c == kGrbmCount; }
 
 // Number of derived outputs (the CounterSource ABI: gpuexp_rp_sample fills this many
 // doubles; gpuexp::kCounterOutputs in sources.h).
-constexpr int kNumOut = 17;
+constexpr int kNumOut = 18;
 
 // Per-XCC MFMA busy (gpuexp_rp_sample_xcc): at most this many XCCs per GPU.
 constexpr int kMaxXcc = 16;
@@ -154,9 +152,9 @@ inline void derive(Derived& a, const double* d, const int* inst, double wall) {
   // share of the allocator's arbitration cycles in which an SE had a compute wave ready that
   // fit on none of its CUs; the allocator arbitrates every kSpiArbClocks clocks (measured on
   // MI355X: a permanently stalled queue reads 24.9-25.0 % of GRBM_COUNT, profiles/r04/
-  // spi_scope.txt).  out[14..16]: over those stalled cycles, the share of the SE's CUs whose
-  // LDS was too full for it / of its SIMDs without a free wave slot / without enough VGPRs,
-  // i.e. what capped residency.  0 when no wave waited (nothing was limited).
+  // spi_scope.txt).  out[14..17]: over those stalled cycles, the share of the SE's CUs whose
+  // LDS was too full for it / of its SIMDs without a free wave slot / without enough VGPRs /
+  // without enough SGPRs, i.e. what capped residency.  0 when no wave waited.
   constexpr double kSpiArbClocks = 4.0;
   const double spi = inst[kSpiResStall] > 0 ? inst[kSpiResStall] : 0;
   const double stall = d[kSpiResStall];
@@ -171,6 +169,7 @@ inline void derive(Derived& a, const double* d, const int* inst, double wall) {
   out[14] = share(d[kSpiLdsFull], cu_se);
   out[15] = share(d[kSpiWaveFull], simd_se);
   out[16] = share(d[kSpiVgprFull], simd_se);
+  out[17] = share(d[kSpiSgprFull], simd_se);
   a.valid = true;
   a.windows += 1;
 }

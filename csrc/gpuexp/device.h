@@ -177,7 +177,8 @@ struct CounterReading {
   // occupancy limiters (SPI resource allocator, counter_model.h): share of cycles a ready
   // compute wave fit nowhere; over those cycles, share of CUs LDS-full / SIMDs wave-slot-full /
   // SIMDs VGPR-full
-  double dispatch_stall_pct = kNaN, lds_limited_pct = kNaN, wave_limited_pct = kNaN, vgpr_limited_pct = kNaN;
+  double dispatch_stall_pct = kNaN, lds_limited_pct = kNaN, wave_limited_pct = kNaN, vgpr_limited_pct = kNaN,
+         sgpr_limited_pct = kNaN;
   // mfma_busy_pct of each XCC (its SQ instances over its own GRBM_COUNT x its SIMDs);
   // nxcc = 0 when the counter source cannot attribute samples to XCCs
   int nxcc = 0;

@@ -214,8 +214,9 @@ void Engine::define_families() {
                       G, D);
   f_occ_lim_ = add("amd_gpu_occupancy_limiter_percent",
                    "While compute waves waited for a CU: the share of CUs whose free LDS could not take the "
-                   "wave (resource=lds: LDS occupancy), of SIMDs without a free wave slot (wave_slots) or "
-                   "without enough free VGPRs (vgpr); 0 when no wave waited (every process's waves, full profile)",
+                   "wave (resource=lds: LDS occupancy), of SIMDs without a free wave slot (wave_slots), "
+                   "without enough free VGPRs (vgpr) or SGPRs (sgpr); 0 when no wave waited (every process's "
+                   "waves, full profile)",
                    G, with(D, {"resource"}));
   f_sq_busy_ = add("amd_gpu_sq_busy_percent", "Shader sequencer busy (SQ_BUSY_CYCLES)", G, D);
   f_gui_ = add("amd_gpu_gui_active_percent", "Graphics pipe active (GRBM_GUI_ACTIVE / GRBM_COUNT)", G, D);
@@ -1169,10 +1170,10 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
       // What capped residency, from the SPI resource allocator.  Not VMID-filtered like the
       // SQ wave counters: an unprivileged exporter sees other processes' waves on every
       // hardware queue (profiles/r04/spi_scope.txt), so exported at any scope.
-      static const char* kRes[3] = {"lds", "wave_slots", "vgpr"};
-      const double lim[3] = {cr.lds_limited_pct, cr.wave_limited_pct, cr.vgpr_limited_pct};
+      static const char* kRes[4] = {"lds", "wave_slots", "vgpr", "sgpr"};
+      const double lim[4] = {cr.lds_limited_pct, cr.wave_limited_pct, cr.vgpr_limited_pct, cr.sgpr_limited_pct};
       dput(st, i, st.disp_stall, f_disp_stall_, {}, cr.dispatch_stall_pct, gen);
-      for (int k = 0; k < 3; ++k) dput(st, i, st.occ_lim[k], f_occ_lim_, {kRes[k]}, lim[k], gen);
+      for (int k = 0; k < 4; ++k) dput(st, i, st.occ_lim[k], f_occ_lim_, {kRes[k]}, lim[k], gen);
     }
   }
   CounterHealth ch;

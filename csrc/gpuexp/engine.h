@@ -227,7 +227,7 @@ class Engine {
         links_up, pcie_bw, pcie_replay, pcie_speed, pcie_width, thr[5], nprocs, cu_occ, ctr[10],
         sen[4], ecc[3], aer[3], nak[2], recov, xgmi_w, xgmi_s, xclk[kMaxXcc], sen_xlat[kMaxXcc], sen_mem, sen_xmem[kMaxXcc],
         kev[std::size(kKfdSubscribed)], pages[3], gtt_used, gtt_total, board, mfma_util, xmfma[kMaxXcc], sen_pend, mflops[2],
-        disp_stall, occ_lim[3], ctr_health[6];
+        disp_stall, occ_lim[4], ctr_health[6];
     std::vector<SeriesRef> fw;  // amd_gpu_firmware_info, one per component
     uint64_t kfd_events[kKfdEventIds] = {};  // KFD SMI events seen on this GPU, by id
     uint64_t errors = 0;

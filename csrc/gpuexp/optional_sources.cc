@@ -121,6 +121,7 @@ class PluginCounters : public CounterSource {
     out->lds_limited_pct = v[14];
     out->wave_limited_pct = v[15];
     out->vgpr_limited_pct = v[16];
+    out->sgpr_limited_pct = v[17];
     out->nxcc = sample_xcc_ ? std::max(0, sample_xcc_(dev, out->xcc_mfma_busy_pct, kMaxXcc)) : 0;
     return true;
   }

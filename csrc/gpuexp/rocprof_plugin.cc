@@ -165,7 +165,7 @@ bool build_config(Agent& a, std::string* why) {
     if (rocprofiler_query_counter_info(c, ROCPROFILER_COUNTER_INFO_VERSION_0, &info) != ROCPROFILER_STATUS_SUCCESS)
       continue;
     for (int k = 0; k < kNumCtr; ++k)
-      if (k != kSpiWave && k != kSpiTg && info.name && std::strcmp(info.name, name(k)) == 0) {  // SPI_CSN_*: aqlpmc experiment only
+      if (info.name && std::strcmp(info.name, name(k)) == 0) {
         use.push_back(c);
         a.counter_slot[c.handle] = k;
       }

@@ -32,7 +32,7 @@ std::unique_ptr<SentinelSource> make_queue_sentinel(const std::string& counters_
 std::string default_rocprof_plugin();
 
 // Derived values a counter plugin's gpuexp_rp_sample fills, in CounterReading order.
-constexpr int kCounterOutputs = 17;
+constexpr int kCounterOutputs = 18;
 
 // Health of a GPU's counter reads (continuous mode), cumulative: reads found still queued,
 // windows dropped because the counters went backwards, re-arms after another profiler reset

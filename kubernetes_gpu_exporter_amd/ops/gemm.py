@@ -102,18 +102,24 @@ def mfma_duty(device: int, duty: float, seconds: float, period_s: float = 0.002,
     return out, counts
 
 
+_HOG_KINDS = {"lds": (0, 2), "waves": (1, 4), "vgpr": (2, 4), "sgpr": (3, 28)}  # kernel, blocks per CU that fit
+
+
 def occupancy_hog(device: int, kind: str, seconds: float, generations: int = 4, stream=None):
     """Launches blocks that each hold a resource for `seconds` (non-blocking), `generations`
     times as many as fit at once, so ready waves queue in the dispatcher for a known reason:
     kind "lds" = 1 wave + 64 KiB LDS per block (2 per CU fit: LDS-limited), "waves" = 8 waves
-    per block, no LDS (4 per CU fit: wave-slot-limited).  Returns the sink tensor."""
+    per block, no LDS (4 per CU fit: wave-slot-limited), "vgpr" = 1 wave of 400 registers per
+    lane (1 per SIMD fits: VGPR-limited), "sgpr" = 1 wave of 108 SGPRs (7 per SIMD fit, of 8
+    slots: SGPR-limited).  Returns the sink tensor."""
     import torch
-    if kind not in ("lds", "waves") or not (0 < seconds <= 10) or not (1 <= generations <= 64):
-        raise ValueError("kind lds|waves, 0 < seconds <= 10, 1 <= generations <= 64")
+    if kind not in _HOG_KINDS or not (0 < seconds <= 10) or not (1 <= generations <= 64):
+        raise ValueError("kind lds|waves|vgpr|sgpr, 0 < seconds <= 10, 1 <= generations <= 64")
+    code, per_cu = _HOG_KINDS[kind]
     dev = torch.device(f"cuda:{device}")
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    blocks = cus * (2 if kind == "lds" else 4) * generations
+    blocks = cus * per_cu * generations
     out = torch.zeros(blocks, dtype=torch.float32, device=dev)
     s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
-    kernels().occupancy_hog(0 if kind == "lds" else 1, out.data_ptr(), blocks, float(seconds), s)
+    kernels().occupancy_hog(code, out.data_ptr(), blocks, float(seconds), s)
     return out

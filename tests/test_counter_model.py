@@ -8,7 +8,7 @@ import pytest
 SIMD, CU = 1024, 256  # MI355X: 256 CUs x 4 SIMDs
 # output order: counter_model.h derive() / optional_sources.cc sample()
 (MFMA_BUSY, SQ_BUSY, GUI, WAVES, LDS, LDS_CONF, HBM_RD, HBM_WR, GMI_RD, GMI_WR, MFMA_UTIL, BF16, FP8,
- STALL, LIM_LDS, LIM_WAVES, LIM_VGPR) = range(17)
+ STALL, LIM_LDS, LIM_WAVES, LIM_VGPR, LIM_SGPR) = range(18)
 
 
 def derive(native, wall=0.1, privileged=True, **deltas):
@@ -62,18 +62,19 @@ def test_unknown_counter_is_rejected(native):
 
 def test_occupancy_limiters(native):
     """SPI resource-allocator counters: the stall share is over elapsed cycles (per SE); each
-    limiter is the share of the SE's CUs (LDS) or SIMDs (wave slots, VGPRs) that were full
+    limiter is the share of the SE's CUs (LDS) or SIMDs (wave slots, VGPRs, SGPRs) that were full
     over the stalled cycles.  (derive_counters passes each counter as one instance, i.e. one
     SE holding all CUs.)"""
     clk = 2.0e8
     # the allocator arbitrates every 4th clock: 0.1 x clk stalled arbitration cycles = 40 %
     out, _ = derive(native, GRBM_COUNT=clk, GRBM_GUI_ACTIVE=clk, SPI_RA_RES_STALL_CSN=0.1 * clk,
                     SPI_RA_LDS_CU_FULL_CSN=0.1 * clk * CU * 0.9, SPI_RA_WAVE_SIMD_FULL_CSN=0.1 * clk * SIMD * 0.05,
-                    SPI_RA_VGPR_SIMD_FULL_CSN=0)
+                    SPI_RA_VGPR_SIMD_FULL_CSN=0, SPI_RA_SGPR_SIMD_FULL_CSN=0.1 * clk * SIMD * 0.25)
     assert out[STALL] == pytest.approx(40.0)
     assert out[LIM_LDS] == pytest.approx(90.0)
     assert out[LIM_WAVES] == pytest.approx(5.0)
     assert out[LIM_VGPR] == 0.0
+    assert out[LIM_SGPR] == pytest.approx(25.0)
     idle, _ = derive(native, GRBM_COUNT=clk, GRBM_GUI_ACTIVE=clk, SPI_RA_RES_STALL_CSN=0, SPI_RA_LDS_CU_FULL_CSN=0,
                      SPI_RA_WAVE_SIMD_FULL_CSN=0, SPI_RA_VGPR_SIMD_FULL_CSN=0)
     assert idle[STALL] == 0.0 and idle[LIM_LDS] == 0.0 and idle[LIM_WAVES] == 0.0  # nothing waited

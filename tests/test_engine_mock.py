@@ -257,10 +257,10 @@ def test_full_profile_adds_reliability_families(mock_engine):
     ticks(e, 3)
     fams = parse(e)
     # + board (1), firmware (4 in mock), MFMA util (1), per-XCD MFMA busy (8), sentinel pending (1),
-    # MFMA FLOP/s for bf16 and fp8 (2), dispatch stall (1), occupancy limiters lds/wave_slots/vgpr (3)
-    assert dict(device_series_per_gpu(fams)) == {"0": 133, "1": 133}
+    # MFMA FLOP/s for bf16 and fp8 (2), dispatch stall (1), occupancy limiters lds/wave_slots/vgpr/sgpr (4)
+    assert dict(device_series_per_gpu(fams)) == {"0": 134, "1": 134}
     lim = {s[1]["resource"]: s[2] for s in fams["amd_gpu_occupancy_limiter_percent"].samples if s[1]["gpu"] == "0"}
-    assert lim == {"lds": 80.0, "wave_slots": 10.0, "vgpr": 0.0}, lim
+    assert lim == {"lds": 80.0, "wave_slots": 10.0, "vgpr": 0.0, "sgpr": 0.0}, lim
     assert promtext.value(fams, "amd_gpu_dispatch_stall_percent", gpu=0) > 0
     flops = {s[1]["dtype"]: s[2] for s in fams["amd_gpu_mfma_flops_per_second"].samples if s[1]["gpu"] == "0"}
     busy = fams["amd_gpu_mfma_busy_percent"].samples[0][2]

@@ -6,7 +6,7 @@ The exporter engine runs in THIS process (aqlprofile counters, continuous, 10 Hz
 on the PMC queue).  The load runs in a CHILD process, so a counter that only counts this
 process's VMID (the SQ wave counters do for an unprivileged client, profiles/r02/
 pmc_scope.txt) sees nothing of it; the same kernels from this process are the control.
-Per tick the derived values come straight from the plugin (gpuexp_rp_sample outputs 13-16:
+Per tick the derived values come straight from the plugin (gpuexp_rp_sample outputs 13-17:
 dispatch stall %, LDS / wave-slot / VGPR limiter %) and the raw window deltas from its
 debug line, whatever the engine's export gating.
 
@@ -14,6 +14,8 @@ Cases (each `--seconds` long, 4 generations of blocks queued):
   idle           no kernel
   lds_other      occupancy_hog kind lds   (1 wave + 64 KiB LDS per block) in the child
   waves_other    occupancy_hog kind waves (8 waves, no LDS per block)      in the child
+  vgpr_other     occupancy_hog kind vgpr (1 wave of 400 registers per lane) in the child (--kinds)
+  sgpr_other     occupancy_hog kind sgpr (1 wave of 108 SGPRs)             in the child (--kinds)
   lds_self       the lds kernel from this process (control: VMID-matched)
   waves_self     the waves kernel from this process
 Usage: python tools/probe_spi_scope.py [--seconds 2.0] -> RESULT json
@@ -89,18 +91,18 @@ def main() -> int:
         return 0
     plugin = ctypes.CDLL(rocprof_plugin_path("aqlpmc"))
     plugin.gpuexp_rp_sample.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]
-    out = (ctypes.c_double * 17)()
+    out = (ctypes.c_double * 32)()  # >= the plugin ABI's output count (counter_model.h kNumOut)
     buf = ctypes.create_string_buffer(8192)
 
     def window():
         plugin.gpuexp_rp_debug(0, buf, 8192)
         kv = dict(x.split("=", 1) for x in buf.value.decode().split(";") if "=" in x)
         raw = {k: kv.get(k) for k in ("SPI_RA_RES_STALL_CSN", "SPI_RA_LDS_CU_FULL_CSN", "SPI_RA_WAVE_SIMD_FULL_CSN",
-                                      "SPI_RA_VGPR_SIMD_FULL_CSN", "GRBM_COUNT", "GRBM_GUI_ACTIVE", "SQ_WAVES",
-                                      "SPI_CSN_WAVE", "SPI_CSN_NUM_THREADGROUPS")}
+                                      "SPI_RA_VGPR_SIMD_FULL_CSN", "SPI_RA_SGPR_SIMD_FULL_CSN", "GRBM_COUNT",
+                                      "GRBM_GUI_ACTIVE", "SQ_WAVES")}
         ok = plugin.gpuexp_rp_sample(0, 0.0, out) == 0
         w = {"stall": out[13] if ok else None, "lds": out[14] if ok else None, "waves": out[15] if ok else None,
-             "vgpr": out[16] if ok else None, "gui": out[2] if ok else None, "raw": raw,
+             "vgpr": out[16] if ok else None, "sgpr": out[17] if ok else None, "gui": out[2] if ok else None, "raw": raw,
              "window_s": float(kv.get("window_s", "nan"))}
         if args.exported:
             from kubernetes_gpu_exporter_amd.utils import promtext
@@ -131,16 +133,16 @@ def main() -> int:
         def tot(k):  # sum over the recorded windows of a raw counter ("value/instances")
             v = [float(r["raw"][k].split("/")[0]) for r in rows if r["raw"].get(k)]
             return round(sum(v)) if v else None
-        out = {"windows": len(rows), "sum_spi_waves": tot("SPI_CSN_WAVE"),
-               "sum_spi_workgroups": tot("SPI_CSN_NUM_THREADGROUPS"), "sum_sq_waves": tot("SQ_WAVES"),
+        out = {"windows": len(rows), "sum_sq_waves": tot("SQ_WAVES"),
                "stall_median": med("stall"), "lds_median": med("lds"),
-               "waves_median": med("waves"), "vgpr_median": med("vgpr"), "gui_median": med("gui"),
+               "waves_median": med("waves"), "vgpr_median": med("vgpr"), "sgpr_median": med("sgpr"),
+               "gui_median": med("gui"),
                "raw_example": rows[len(rows) // 2]["raw"] if rows else None}
         if args.exported and rows:
             ex = [r["exported"] for r in rows]
             out["exported_median"] = {k: (round(statistics.median([x[k] for x in ex if x.get(k) is not None]), 2)
                                           if any(x.get(k) is not None for x in ex) else None)
-                                      for k in ("stall", "lds", "wave_slots", "vgpr")}
+                                      for k in ("stall", "lds", "wave_slots", "vgpr", "sgpr")}
         return out
 
     res = {"status": status, "cases": {}}
