@@ -902,15 +902,17 @@ def test_xcc_mfma_busy_calibration():
 
 
 def test_occupancy_limiters_see_other_processes():
-    """LDS occupancy as a device-wide signal (SPI resource-allocator counters,
+    """Occupancy limiters as device-wide signals (SPI resource-allocator counters,
     amd_gpu_occupancy_limiter_percent / amd_gpu_dispatch_stall_percent), against kernels of
     known limiter run by ANOTHER process, four generations of blocks queued: 1 wave + 64 KiB
-    of LDS per block -> LDS limits (lds ~100, wave_slots ~0); 8 waves per block, no LDS ->
-    wave slots limit (wave_slots ~100, lds ~0); the dispatcher stalled all the time (~100).
-    Idle: nothing waits (0).  Read from the engine's own exposition on an unprivileged box."""
+    of LDS per block -> LDS limits; 8 waves per block, no LDS -> wave slots; 1 wave of 400
+    registers per lane -> VGPRs; 1 wave of 108 SGPRs -> SGPRs (7 of a SIMD's 8 slots fill
+    first).  The dispatcher is stalled most of the time; idle: nothing waits (0).  Read from
+    the engine's own exposition on an unprivileged box (profiles/r04/spi_scope.txt)."""
     import json
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "probe_spi_scope.py"), "--seconds", "2.0",
-                        "--no-self", "--exported"], capture_output=True, text=True, timeout=150)
+                        "--no-self", "--exported", "--kinds", "lds,waves,vgpr,sgpr"],
+                       capture_output=True, text=True, timeout=200)
     print(r.stdout[-3000:], r.stderr[-2000:])
     line = [l for l in r.stdout.splitlines() if l.startswith("RESULT ")]
     assert line, "probe produced no result"
@@ -920,10 +922,13 @@ def test_occupancy_limiters_see_other_processes():
     cases = res["cases"]
     idle = cases["idle"]["exported_median"]
     assert idle["stall"] == 0.0 and idle["lds"] == 0.0, idle
-    lds = cases["lds_other"]["exported_median"]
-    assert lds["stall"] > 90 and lds["lds"] > 90 and lds["wave_slots"] < 5, lds
-    waves = cases["waves_other"]["exported_median"]
-    assert waves["stall"] > 90 and waves["wave_slots"] > 90 and waves["lds"] < 5, waves
+    others = {"lds", "wave_slots", "vgpr", "sgpr"}
+    for case, limiter, stall in (("lds_other", "lds", 90), ("waves_other", "wave_slots", 90),
+                                 ("vgpr_other", "vgpr", 90), ("sgpr_other", "sgpr", 50)):
+        m = cases[case]["exported_median"]
+        assert m["stall"] > stall and m[limiter] > 90, (case, m)
+        # the LDS kernel's waves also leave 2 of 4 SIMDs without VGPRs for the next (vgpr ~50)
+        assert all(m[o] < 5 for o in others - {limiter} - ({"vgpr"} if case == "lds_other" else set())), (case, m)
 
 
 def test_device_scope_pmc_calibration():
