@@ -984,7 +984,7 @@ void counting_loop() {
     while (!g_quit.load()) {
       {
         std::unique_lock<std::mutex> lk(g_cv_mu);
-        g_cv.wait_for(lk, std::chrono::milliseconds(idle ? g_interval_ms : std::max(g_interval_ms, 1000)),
+        g_cv.wait_for(lk, std::chrono::milliseconds(idle ? g_interval_ms : std::max(2 * g_interval_ms, 1000)),
                       [] { return g_quit.load() || g_leftover_flag.load(); });
       }
       if (g_quit.load()) break;
@@ -996,7 +996,8 @@ void counting_loop() {
       const uint64_t last = g_last_kick_ns.load();
       const uint64_t now = uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
                                         Clock::now().time_since_epoch()).count());
-      idle = !last || now - last > 1000000000ull;
+      // no kick for a second, or for two fallback intervals of a slow (e.g. 1 Hz) engine
+      idle = !last || now - last > std::max<uint64_t>(1000000000ull, 2000000ull * uint64_t(g_interval_ms));
       if (!idle) continue;
       std::lock_guard<std::mutex> rl(g_round_mu);
       read_round();
