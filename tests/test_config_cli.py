@@ -144,6 +144,15 @@ def test_control_plane_refresh_soon():
         cp.stop()
 
 
+def test_round4_keys_reach_the_engine(native):
+    from kubernetes_gpu_exporter_amd.config import make_config
+    ec = make_config({}).to_engine_config(native)
+    assert ec.counters_inline is True and ec.http.follow_rx_cpu is False and ec.kfd_sdma is False
+    ec = make_config({"counters_inline": False, "http_follow_rx_cpu": True,
+                      "kfd_sdma_activity": True}).to_engine_config(native)
+    assert ec.counters_inline is False and ec.http.follow_rx_cpu is True and ec.kfd_sdma is True
+
+
 def test_stale_after_defaults_follow_the_interval(native):
     from kubernetes_gpu_exporter_amd.config import make_config
     def ns(**kw):
