@@ -397,6 +397,10 @@ PYBIND11_MODULE(_gpuexp, m) {
      py::arg("count") = 100, py::arg("gzip") = false, py::arg("keepalive") = true,
      py::arg("timeout_ms") = 5000, py::arg("keep_last_body") = false);
 
+  m.def("scrape_period_ns", [](std::vector<uint64_t> newest_first) {
+    return learnt_scrape_period_ns(newest_first.data(), int(std::min<size_t>(newest_first.size(), 4)));
+  }, py::arg("intervals_newest_first"), "The scrape period the HTTP pre-wake learns from request intervals (ns)");
+
   py::class_<ScrapeClient>(m, "ScrapeClient")
       .def(py::init<std::string, int, std::string, bool, int, std::string, bool>(), py::arg("host"),
            py::arg("port"), py::arg("path") = "/metrics", py::arg("gzip") = false, py::arg("timeout_ms") = 5000,

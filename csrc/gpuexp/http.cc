@@ -23,6 +23,26 @@
 
 namespace gpuexp {
 
+uint64_t learnt_scrape_period_ns(const uint64_t* newest_first, int n) {
+  for (int k = 0; k < n; ++k) {
+    const uint64_t a = newest_first[k];
+    if (a < 20000000ull) continue;  // < 20 ms: not a scrape period the pre-wake follows
+    uint64_t sum = a;
+    int agree = 0;
+    for (int j = 0; j < n; ++j) {
+      if (j == k) continue;
+      const uint64_t b = newest_first[j];
+      const uint64_t lo = std::min(a, b), hi = std::max(a, b);
+      if (hi <= lo + lo / 8) {  // within 12 %
+        sum += b;
+        ++agree;
+      }
+    }
+    if (agree) return sum / uint64_t(agree + 1);
+  }
+  return 0;
+}
+
 const std::vector<double>& scrape_latency_bounds() {
   // fine where scrapes sit (server side: a few to a few tens of microseconds), coarse above
   static const std::vector<double> b = {1e-6,   2e-6,   3e-6,   5e-6,   7.5e-6, 10e-6,  15e-6, 20e-6,
@@ -78,24 +98,10 @@ struct Conn {
   // pre-woken in every round-4 driver-form run).  A real period change is learnt after two
   // intervals at the new period.
   uint64_t period_ns() const {
+    uint64_t newest_first[4];
     const int n = std::min(n_intervals, 4);
-    for (int k = 0; k < n; ++k) {  // newest first
-      const uint64_t a = intervals[(iv_pos + 3 - k) & 3];
-      if (a < 20000000ull) continue;
-      uint64_t sum = a;
-      int agree = 0;
-      for (int j = 0; j < n; ++j) {
-        if (j == k) continue;
-        const uint64_t b = intervals[(iv_pos + 3 - j) & 3];
-        const uint64_t lo = std::min(a, b), hi = std::max(a, b);
-        if (hi <= lo + lo / 8) {
-          sum += b;
-          ++agree;
-        }
-      }
-      if (agree) return sum / uint64_t(agree + 1);
-    }
-    return 0;
+    for (int k = 0; k < n; ++k) newest_first[k] = intervals[(iv_pos + 3 - k) & 3];
+    return learnt_scrape_period_ns(newest_first, n);
   }
   uint64_t expected_next() const {
     if (n_intervals < 2) return 0;

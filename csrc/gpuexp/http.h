@@ -58,6 +58,11 @@ struct HttpConfig {
   bool follow_rx_cpu = false;
 };
 
+// The scrape period a connection's pre-wake follows, from its newest (up to 4) request
+// intervals, newest first: the newest interval that another one agrees with within 12 % (and
+// >= 20 ms), averaged with its partners; 0 = no steady period.
+uint64_t learnt_scrape_period_ns(const uint64_t* newest_first, int n);
+
 // Fixed latency buckets (seconds) for gpuexp_scrape_duration_seconds.
 const std::vector<double>& scrape_latency_bounds();
 

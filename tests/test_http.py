@@ -431,10 +431,26 @@ def test_scrape_prewake_learns_a_steady_period(native):
     assert run(False) == (0, 0)
 
 
+def test_scrape_period_survives_one_late_scrape(native):
+    """The learnt scrape period (the pre-wake's schedule): the newest request interval that
+    another recent one agrees with within 12 %, so one late scrape (a pause between a
+    benchmark's warm-up and its timed window, a GC stall in the scraper) costs only its own
+    pre-wake; with "the two newest must agree" it cost the next two as well."""
+    ms = 1_000_000
+    p = native.scrape_period_ns
+    assert p([100 * ms, 100 * ms]) == 100 * ms                            # two steady periods arm it
+    assert p([100 * ms]) == 0 and p([]) == 0
+    assert p([190 * ms, 100 * ms, 100 * ms, 100 * ms]) == 100 * ms        # a late one does not disarm it
+    assert p([100 * ms, 190 * ms, 100 * ms, 100 * ms]) == 100 * ms        # nor right after it
+    assert p([50 * ms, 50 * ms, 100 * ms, 100 * ms]) == 50 * ms           # a new period wins after two
+    assert p([104 * ms, 96 * ms]) == 100 * ms                             # jitter within 12 % averages
+    assert p([130 * ms, 100 * ms]) == 0                                   # beyond it: no period
+    assert p([10 * ms, 10 * ms, 10 * ms]) == 0                            # < 20 ms: not pre-woken
+
+
 def test_prewake_survives_one_late_scrape(native):
-    """One late scrape (a pause between a benchmark's warm-up and its timed window, a GC
-    stall in the scraper) costs only its own pre-wake: the learnt period is the newest
-    interval another recent one agrees with, so the next request is pre-woken again."""
+    """End to end: after one late scrape the worker is pre-woken again (timing-based, so
+    only the weak form is asserted under a loaded CPU; the rule itself is pinned above)."""
     c = native.EngineConfig()
     c.backend = "mock"
     c.interval_s = 0
@@ -462,7 +478,7 @@ def test_prewake_survives_one_late_scrape(native):
         hits = e.stats()["http_prewake_hits"] - h0
     finally:
         e.stop()
-    assert hits >= 3, hits  # the 4 on-period scrapes after the late one (one may jitter out)
+    assert hits >= 2, hits
 
 
 def _thread_cpus(name: str) -> set:
