@@ -46,23 +46,27 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
   relist_ = false;
   last_list_ns_ = now_ns;
   ++lists_;
+  // Opens device `di`'s files of a process directory; false if it has no context there (yet).
+  auto open_dev = [&](const std::string& pdir, size_t di, PerDev* pd) {
+    const DeviceInfo& d = devs[di];
+    pd->dev = int(di);  // position in `devs` (the engine's device order)
+    const std::string id = std::to_string(d.kfd_gpu_id);
+    if (!pd->vram.open(pdir + "/vram_" + id)) return false;
+    if (read_cu_) pd->cu.open(pdir + "/stats_" + id + "/cu_occupancy");
+    if (read_sdma_) pd->sdma.open(pdir + "/sdma_" + id);
+    pd->evicted.open(pdir + "/stats_" + id + "/evicted_ms");
+    return true;
+  };
   for (const std::string& name : list_dir(base)) {
     int pid = std::atoi(name.c_str());
     if (pid <= 0 || pid == self_) continue;
+    const std::string pdir = base + "/" + name;
     auto make_entry = [&]() {
       // New process: find which of OUR devices it has a KFD context on.
       Entry e;
-      std::string pdir = base + "/" + name;
       for (size_t di = 0; di < devs.size(); ++di) {
-        const DeviceInfo& d = devs[di];
         PerDev pd;
-        pd.dev = int(di);  // position in `devs` (the engine's device order)
-        std::string id = std::to_string(d.kfd_gpu_id);
-        if (!pd.vram.open(pdir + "/vram_" + id)) continue;
-        if (read_cu_) pd.cu.open(pdir + "/stats_" + id + "/cu_occupancy");
-        if (read_sdma_) pd.sdma.open(pdir + "/sdma_" + id);
-        pd.evicted.open(pdir + "/stats_" + id + "/evicted_ms");
-        e.devs.push_back(std::move(pd));
+        if (open_dev(pdir, di, &pd)) e.devs.push_back(std::move(pd));
       }
       std::string comm;
       if (read_small_file(root_ + "/proc/" + name + "/comm", &comm, 64)) e.comm = trim(comm);
@@ -70,7 +74,19 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
     };
     auto it = pids_.find(pid);
     const bool fresh = it == pids_.end();
-    if (fresh) it = make_entry();
+    if (fresh) {
+      it = make_entry();
+    } else if (it->second.devs.size() < devs.size()) {
+      // KFD adds a process's vram_<gpu_id> when it first uses that GPU, which can be after its
+      // directory appeared (or after the listing that found it, mid-creation): look for the
+      // GPUs it had no files for at every listing, or it would never show on them.
+      for (size_t di = 0; di < devs.size(); ++di) {
+        bool have = false;
+        for (const PerDev& pd : it->second.devs) have = have || pd.dev == int(di);
+        PerDev pd;
+        if (!have && open_dev(pdir, di, &pd)) it->second.devs.push_back(std::move(pd));
+      }
+    }
     if (emit(it->second, pid, per_dev, now_ns) == 0 && !fresh && !it->second.devs.empty()) {
       // Cached fds of a PID whose KFD directory was removed and re-created between two
       // scans (the PID was reused) point at dead kobjects: every read fails although

@@ -431,6 +431,31 @@ def test_kfd_detail_files_are_rate_limited(native, tmp_path):
     e.stop()
 
 
+def test_process_found_on_a_gpu_it_starts_using_later(native, tmp_path):
+    """KFD adds a process's vram_<gpu_id> when the process first uses that GPU, which can be
+    after its directory appeared (or mid-creation, while a listing runs): a tracked process
+    is looked for on its missing GPUs at every listing, so it shows there too."""
+    h = mi355x_node(tmp_path, 2)
+    g0, g1 = h.gpus
+    h.add_process(4242, kubepods_cgroup(UID, CID), gpus={g0.gpu_id: (1000, 10)})
+    e = _engine(native, tmp_path, kfd_rescan_interval_s=0.5)
+
+    def gpus_of_4242():
+        f = promtext.parse(e.snapshot_text())
+        return sorted(lab["gpu"] for _, lab, _ in promtext.samples(f, "amd_gpu_process_vram_bytes")
+                      if lab["pid"] == "4242")
+
+    e.tick(1 * S)
+    first = gpus_of_4242()
+    assert len(first) == 1, first
+    h.set_process_gpu(4242, g1.gpu_id, vram=2000, cu=5)  # starts using the other GPU
+    e.tick(1 * S + 100_000_000)                           # tracked-only scan: not yet
+    assert gpus_of_4242() == first
+    e.tick(2 * S)                                         # the next listing finds it
+    assert gpus_of_4242() == ["0", "1"]
+    e.stop()
+
+
 def test_unreadable_pid_is_not_looked_up_every_tick(native, tmp_path):
     """A GPU process whose /proc/<pid> the exporter cannot read (a host PID seen from inside
     a PID namespace, hidepid, a process on its way out) is looked up again at most once a
