@@ -16,26 +16,44 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def vram_used() -> int:
-    for f in sorted(glob.glob("/sys/class/drm/card*/device/mem_info_vram_used")):
+def our_gpu() -> tuple:
+    """(KFD gpu_id, PCI BDF) of the GPU this process sees first (the box shows the host's
+    whole KFD topology; other GPUs belong to other tenants)."""
+    from kubernetes_gpu_exporter_amd.utils.kfdself import hip_order_bdfs
+    bdf = hip_order_bdfs()[0].lower()
+    dom, bus, rest = bdf.split(":")
+    dev, fn = rest.split(".")
+    want = (int(bus, 16) << 8) | (int(dev, 16) << 3) | int(fn)
+    for node in glob.glob("/sys/class/kfd/kfd/topology/nodes/*"):
         try:
-            return int(open(f).read())
+            gid = int(open(node + "/gpu_id").read().strip() or 0)
+            kv = dict(line.split() for line in open(node + "/properties") if len(line.split()) == 2)
+            if gid and int(kv.get("location_id", -1)) == want and int(kv.get("domain", 0)) == int(dom, 16):
+                return gid, bdf
         except (OSError, ValueError):
             continue
-    return -1
+    return 0, bdf
+
+
+GPU_ID, BDF = our_gpu()
+
+
+def vram_used() -> int:
+    """Used VRAM of OUR GPU (device-wide: every process on it)."""
+    try:
+        return int(open(f"/sys/bus/pci/devices/{BDF}/mem_info_vram_used").read())
+    except (OSError, ValueError):
+        return -1
 
 
 def kfd_vram() -> dict:
-    """pid -> summed vram_<id> of every process in the KFD proc directory (host PIDs)."""
+    """pid -> vram_<our gpu_id> of every process in the KFD proc directory (host PIDs)."""
     out = {}
-    for d in glob.glob("/sys/class/kfd/kfd/proc/*"):
-        tot = 0
-        for f in glob.glob(d + "/vram_*"):
-            try:
-                tot += int(open(f).read())
-            except (OSError, ValueError):
-                pass
-        out[os.path.basename(d)] = tot
+    for f in glob.glob(f"/sys/class/kfd/kfd/proc/*/vram_{GPU_ID}"):
+        try:
+            out[f.split("/")[-2]] = int(open(f).read())
+        except (OSError, ValueError):
+            pass
     return out
 
 
@@ -80,7 +98,7 @@ def run(n, counters: bool, sentinel: bool, kfd_events: bool) -> dict:
             "device_delta_mib": round((during - before) / 2**20, 1),
             "new_kfd_processes_mib": {p: round(v / 2**20, 1) for p, v in new.items()},
             "grown_kfd_processes_mib": {p: round(v / 2**20, 1) for p, v in grown.items()},
-            "status": status[:120]}
+            "gpu_id": GPU_ID, "bdf": BDF, "status": status[:120]}
 
 
 def main() -> int:
