@@ -90,6 +90,7 @@ def run(n, counters: bool, sentinel: bool, kfd_events: bool) -> dict:
     during = vram_used()
     k1 = kfd_vram()
     status = e.source_status()
+    rss = [int(l.split()[1]) for l in open("/proc/self/status") if l.startswith("VmRSS:")][0]
     e.stop()
     new = {p: v for p, v in k1.items() if p not in k0}
     grown = {p: v - k0[p] for p, v in k1.items() if p in k0 and v != k0[p]}
@@ -98,6 +99,8 @@ def run(n, counters: bool, sentinel: bool, kfd_events: bool) -> dict:
             "device_delta_mib": round((during - before) / 2**20, 1),
             "new_kfd_processes_mib": {p: round(v / 2**20, 1) for p, v in new.items()},
             "grown_kfd_processes_mib": {p: round(v / 2**20, 1) for p, v in grown.items()},
+            "rss_mib": round(rss / 1024, 1),
+            "env": {k: v for k, v in os.environ.items() if k.startswith("HSA_") and k != "HSA_ENABLE_IPC_MODE_LEGACY"},
             "gpu_id": GPU_ID, "bdf": BDF, "status": status[:120]}
 
 
@@ -108,7 +111,10 @@ def main() -> int:
         return 0
     import subprocess
     rows = []
-    for counters, sentinel, kfd_events in (("0", "0", "0"), ("0", "0", "1"), ("1", "0", "1"), ("1", "1", "1")):
+    configs = (("0", "0", "0"), ("0", "0", "1"), ("1", "0", "1"), ("1", "1", "1"))
+    if "--queue-only" in sys.argv:  # the HSA-queue configuration only (runtime setting A/B)
+        configs = (("1", "1", "1"),)
+    for counters, sentinel, kfd_events in configs:
         r = subprocess.run([sys.executable, os.path.abspath(__file__), "--one", counters, sentinel, kfd_events],
                            capture_output=True, text=True, timeout=120)
         line = [l for l in r.stdout.splitlines() if l.startswith("{")]
