@@ -460,6 +460,8 @@ bool Engine::start(std::string* err) {
   if (running_.load()) return true;
   RuntimeThreadsName rt_name;
   start_mono_ns_ = mono_ns();
+  counters_kick_mode_ = cfg_.counters_kick != "auto" ? cfg_.counters_kick
+                        : (cfg_.interval_s > 0 && cfg_.interval_s < 0.05 ? "end" : "start");
   define_families();
   // Listen first: a port conflict fails before any GPU-side source (amdsmi, HSA queues,
   // sentinel runs) exists.  Every later failure tears down what was already started.
@@ -1693,8 +1695,14 @@ void Engine::tick_locked(uint64_t now) {
   // and is collected before the series stage, so the exported window is one tick interval
   resolver_->begin_tick(now);
   uint64_t part[kDevParts] = {};
-  const bool kick_late = cfg_.counters_kick == "after_devices";
-  if (counters_ && !kick_late) {
+  // "end" (auto below 50 ms ticks): the read for this tick went out at the end of the previous
+  // one, so it has completed by the counters stage -- at 100 Hz most ticks have no SMU fetch
+  // to hide a ~200 us PM4 read behind, and waiting for it cost 2-3 sleep/wake-ups per tick;
+  // the exported window then ends one tick earlier (10 ms at 100 Hz)
+  const std::string& kick_mode = counters_kick_mode_;
+  const bool kick_late = kick_mode == "after_devices";
+  const bool kick_end = kick_mode == "end";
+  if (counters_ && !kick_late && !kick_end) {
     counters_->kick();
     part[0] = mono_ns() - ts[0];
   }
@@ -1917,6 +1925,7 @@ void Engine::tick_locked(uint64_t now) {
     ts[7] = mono_ns();
     cs[7] = thread_cpu_ns();
   }
+  if (counters_ && kick_end) counters_->kick();  // next tick's read, completing while we sleep
   uint64_t tend = mono_ns();
   cs[kStages] = thread_cpu_ns();
   uint64_t stage_dur[kStages] = {ts[1] - ts[0], ts[2] - ts[1], ts[3] - ts[2], ts[4] - ts[3],

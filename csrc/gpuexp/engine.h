@@ -110,7 +110,9 @@ struct EngineConfig {
   // continuous: when a tick's PMC read goes out.  "start": before the device reads;
   // "after_devices": once the gpu_metrics SMU fetches are done (a PM4 read in flight while
   // the SMU serves the metrics table slows the fetch, profiles/r04/devices_split.txt).
-  std::string counters_kick = "start";
+  // continuous: when a tick's PMC read goes out -- "start" of the tick, "after_devices", "end"
+  // of the previous tick, or "auto" (end below 50 ms ticks, else start)
+  std::string counters_kick = "auto";
   bool counters_inline = true;  // continuous + periodic ticks: the sampler runs the read rounds
   bool enable_rccl = false;
   std::string rccl_dir = "/dev/shm";
@@ -323,6 +325,7 @@ class Engine {
   uint64_t start_mono_ns_ = 0, startup_ns_ = 0;  // start() entry; start() -> first tick
   // thread clocks already charged to gpuexp_sampler_cpu_seconds_total (sampler thread only)
   uint64_t counters_cpu_seen_ = 0, pool_cpu_seen_ = 0, sampler_cpu_seen_ = 0;  // ticks whose counter read missed counters_sync_us (sampler thread)
+  std::string counters_kick_mode_ = "start";  // cfg_.counters_kick with "auto" resolved
   std::string sentinel_status_ = "disabled", counters_status_ = "disabled";
 
   SeriesTable table_;

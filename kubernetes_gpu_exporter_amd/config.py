@@ -56,7 +56,8 @@ class Config:
     counters_mode: str = "continuous"      # continuous (never paused, read every tick; aqlpmc) | duty
     counters_window_ms: int = 20           # duty: counting window ...
     counters_interval_ms: int = 1000       # ... per interval (the rocprof plugin's spin is duty-cycled)
-    counters_kick: str = "start"           # continuous: a tick's PMC read goes out at its start | after_devices
+    counters_kick: str = "auto"            # continuous: a tick's PMC read goes out at its start | after_devices |
+                                           # end of the previous tick | auto (end below 50 ms ticks, else start)
     counters_inline: bool = True           # continuous: the sampler posts/collects each tick's PMC read itself
     http_follow_rx_cpu: bool = False       # pin the HTTP worker to the CPU a steady scraper's requests arrive on
     queue_devices: list = field(default_factory=list)  # GPUs (indices / BDFs) that get the exporter's
@@ -290,8 +291,8 @@ def validate(cfg: Config) -> None:
         raise ValueError(f"metrics_min_interval must be 'auto' or seconds >= 0, got {cfg.metrics_min_interval!r}")
     if not (0 <= cfg.metrics_cpu_budget <= 100):
         raise ValueError("metrics_cpu_budget must be a percentage of one core, 0-100 (0 = no cap under auto)")
-    if cfg.counters_kick not in ("start", "after_devices"):
-        raise ValueError(f"counters_kick must be start|after_devices, got {cfg.counters_kick}")
+    if cfg.counters_kick not in ("auto", "start", "after_devices", "end"):
+        raise ValueError(f"counters_kick must be auto|start|after_devices|end, got {cfg.counters_kick}")
     if cfg.state_interval <= 0:
         raise ValueError("state_interval must be > 0")
     if cfg.pod_totals_ttl <= 0:
