@@ -76,7 +76,14 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
     const bool fresh = it == pids_.end();
     if (fresh) {
       it = make_entry();
-    } else if (it->second.devs.size() < devs.size()) {
+    } else if (it->second.comm.empty() && it->second.comm_tries < kCommTries) {
+      // comm unreadable when the process was found (mid-exec, or /proc lagging KFD): retry
+      // at the next few listings instead of keeping comm="" for the process's lifetime
+      ++it->second.comm_tries;
+      std::string comm;
+      if (read_small_file(root_ + "/proc/" + name + "/comm", &comm, 64)) it->second.comm = trim(comm);
+    }
+    if (!fresh && it->second.devs.size() < devs.size()) {
       // KFD adds a process's vram_<gpu_id> when it first uses that GPU, which can be after its
       // directory appeared (or after the listing that found it, mid-creation): look for the
       // GPUs it had no files for at every listing, or it would never show on them.

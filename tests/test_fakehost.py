@@ -431,6 +431,27 @@ def test_kfd_detail_files_are_rate_limited(native, tmp_path):
     e.stop()
 
 
+def test_comm_read_again_when_empty_at_discovery(native, tmp_path):
+    """A process found while its /proc/<pid>/comm was not readable yet gets its comm label at
+    a later listing instead of keeping comm=\"\" for its lifetime."""
+    h = mi355x_node(tmp_path, 1)
+    (g,) = h.gpus
+    h.add_process(777, kubepods_cgroup(UID, CID), comm="trainer", gpus={g.gpu_id: (1000, 10)})
+    (tmp_path / "proc" / "777" / "comm").unlink()
+    e = _engine(native, tmp_path, kfd_rescan_interval_s=0.5)
+
+    def comms():
+        f = promtext.parse(e.snapshot_text())
+        return {lab["comm"] for _, lab, _ in promtext.samples(f, "amd_gpu_process_vram_bytes") if lab["pid"] == "777"}
+
+    e.tick(1 * S)
+    assert comms() == {""}
+    (tmp_path / "proc" / "777" / "comm").write_text("trainer\n")
+    e.tick(2 * S)  # the next listing reads it
+    assert comms() == {"trainer"}
+    e.stop()
+
+
 def test_process_found_on_a_gpu_it_starts_using_later(native, tmp_path):
     """KFD adds a process's vram_<gpu_id> when the process first uses that GPU, which can be
     after its directory appeared (or mid-creation, while a listing runs): a tracked process
