@@ -70,6 +70,7 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
       }
       std::string comm;
       if (read_small_file(root_ + "/proc/" + name + "/comm", &comm, 64)) e.comm = trim(comm);
+      e.probe_ns = now_ns;
       return pids_.insert_or_assign(pid, std::move(e)).first;
     };
     auto it = pids_.find(pid);
@@ -83,10 +84,13 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
       std::string comm;
       if (read_small_file(root_ + "/proc/" + name + "/comm", &comm, 64)) it->second.comm = trim(comm);
     }
-    if (!fresh && it->second.devs.size() < devs.size()) {
+    if (!fresh && it->second.devs.size() < devs.size() &&
+        (!now_ns || now_ns < it->second.probe_ns || now_ns - it->second.probe_ns >= kReprobeNs)) {
       // KFD adds a process's vram_<gpu_id> when it first uses that GPU, which can be after its
       // directory appeared (or after the listing that found it, mid-creation): look for the
-      // GPUs it had no files for at every listing, or it would never show on them.
+      // GPUs it had no files for at a listing every kReprobeNs, or it would never show on them
+      // (a process on 1 of 8 GPUs costs 7 failed opens per look).
+      it->second.probe_ns = now_ns;
       for (size_t di = 0; di < devs.size(); ++di) {
         bool have = false;
         for (const PerDev& pd : it->second.devs) have = have || pd.dev == int(di);

@@ -48,9 +48,11 @@ class KfdProcReader {
     std::vector<PerDev> devs;
     std::string comm;
     int comm_tries = 0;  // re-reads of an empty comm at later listings
+    uint64_t probe_ns = 0;  // last look for GPUs it had no files for
     uint64_t seen = 0;
   };
   static constexpr int kCommTries = 3;
+  static constexpr uint64_t kReprobeNs = 1000000000ull;
   // Appends the entry's per-GPU samples; returns how many vram reads succeeded.
   int emit(Entry& e, int pid, std::vector<std::vector<ProcSample>>* per_dev, uint64_t now_ns);
   std::string root_;
