@@ -182,6 +182,35 @@ def test_exporter_tick_on_gpu(native):
         e.stop()
 
 
+def test_counters_at_100hz_read_kicked_at_the_previous_tick_end(native):
+    """A 100 Hz engine (counters_kick auto -> "end"): each tick's PMC read goes out at the end
+    of the previous tick, so it has completed by the counters stage -- the stage stays short,
+    no tick misses its window, and the counter families are exported
+    (profiles/r04/kick_end_100hz.txt)."""
+    from kubernetes_gpu_exporter_amd._native import rocprof_plugin_path
+    e = amdsmi_engine(native, interval_s=0.01, enable_counters=True, enable_sentinel=True,
+                      counters_plugin=rocprof_plugin_path("aqlpmc"), series_profile="full")
+    try:
+        if "counters=unavailable" in e.source_status():
+            pytest.skip("device counting unavailable on this box: " + e.source_status())
+        time.sleep(0.5)
+        s0 = e.stats()
+        time.sleep(2.0)
+        s1 = e.stats()
+        fams = promtext.parse(e.snapshot_text())
+    finally:
+        e.stop()
+    ticks = s1["ticks"] - s0["ticks"]
+    counters_us = (s1["stage_cpu_ns"]["counters"] - s0["stage_cpu_ns"]["counters"]) / max(1, ticks) / 1e3
+    late = promtext.value(fams, "gpuexp_counters_late_ticks_total")
+    print(f"{ticks} ticks, counters stage {counters_us:.1f} us CPU per tick, late {late}")
+    assert ticks > 150
+    assert promtext.value(fams, "amd_gpu_gui_active_percent", gpu=0) >= 0
+    assert promtext.value(fams, "amd_gpu_mfma_busy_percent", gpu=0) >= 0
+    assert late <= 0.05 * s1["ticks"], late
+    assert counters_us < 100, counters_us
+
+
 def test_devices_stage_split_on_mi355x(native):
     """The devices stage split on real hardware: a fresh gpu_metrics read is an SMU round trip
     the kernel busy-waits on, so its thread CPU is tens to hundreds of microseconds (idle:
