@@ -33,7 +33,8 @@ CORE_CC = [
     "gpuexp/common.cc", "gpuexp/exposition.cc", "gpuexp/gzip.cc", "gpuexp/http.cc",
     "gpuexp/gpu_metrics.cc", "gpuexp/backend_mock.cc", "gpuexp/backend_sysfs.cc",
     "gpuexp/backend_amdsmi.cc", "gpuexp/procs.cc", "gpuexp/ras.cc", "gpuexp/kfd_events.cc", "gpuexp/engine.cc",
-    "gpuexp/optional_sources.cc", "gpuexp/client.cc", "bindings.cc",
+    "gpuexp/optional_sources.cc", "gpuexp/client.cc", "gpuexp/pmc_rounds.cc", "gpuexp/pmc_harness.cc",
+    "bindings.cc",
 ]
 SENTINEL_HIP = ["gpuexp/sentinel.hip"]
 SENTINEL_HSACO = "gpuexp/sentinel_hsaco.hip"  # device-only code object for raw AQL dispatch
@@ -157,7 +158,8 @@ def build(force: bool = False, jobs: int = 8, sanitize: str | None = None, verbo
         outputs["rocprof_plugin"] = str(link_plain([objs[ROCPROF_CC[0]]], PKG / "_gpuexp_rocprof.so",
                                                    ["-lrocprofiler-sdk", "-lhsa-runtime64", "-lpthread"]))
     if (CSRC / AQLPMC_CC[0]).exists():
-        outputs["aqlpmc_plugin"] = str(link_plain([objs[AQLPMC_CC[0]]], PKG / "_gpuexp_aqlpmc.so",
+        outputs["aqlpmc_plugin"] = str(link_plain([objs[AQLPMC_CC[0]], objs["gpuexp/pmc_rounds.cc"]],
+                                                  PKG / "_gpuexp_aqlpmc.so",
                                                   ["-lhsa-runtime64", "-lpthread"]))
         outputs["sentinel_hsaco"] = str(build_hsaco(SENTINEL_HSACO, PKG / "gpuexp_sentinel.hsaco", hdr, force))
         outputs["calib_hsaco"] = str(build_hsaco(CALIB_HSACO, PKG / "gpuexp_calib.hsaco", hdr, force))

@@ -13,6 +13,7 @@
 #include "gpuexp/kfd_events.h"
 #include "gpuexp/exposition.h"
 #include "gpuexp/gpu_metrics.h"
+#include "gpuexp/pmc_fake.h"
 #include "gpuexp/procs.h"
 #include "gpuexp/ras.h"
 #include "gpuexp/snapshot.h"
@@ -294,6 +295,117 @@ PYBIND11_MODULE(_gpuexp, m) {
     static const char* kNames[3] = {"publish", "skip", "rearm"};
     return py::make_tuple(kNames[act], zero_grbm);
   }, py::arg("deltas"), py::arg("first"), py::arg("wall"), py::arg("zero_grbm") = 0);
+  // Re-arm back-off decision (counter_model.h rearm_on_reset / rearm_due / rearm_done) over a
+  // script of (t_ms, event) with event "backwards" | "stopped" | "armed" | "check"; returns the
+  // state after each: (waiting, due_ms, backoff_ms, conflicts, due_now).
+  m.def("rearm_policy", [](const std::vector<std::pair<double, std::string>>& events, const std::string& mode,
+                           double base_ms, double max_ms, double calm_ms) {
+    gpuexp_ctr::RearmConfig c;
+    c.mode = mode == "off" ? gpuexp_ctr::kRearmOff : mode == "now" ? gpuexp_ctr::kRearmNow : gpuexp_ctr::kRearmBackoff;
+    c.base_ns = int64_t(base_ms * 1e6);
+    c.max_ns = int64_t(max_ms * 1e6);
+    c.calm_ns = int64_t(calm_ms * 1e6);
+    gpuexp_ctr::RearmState s;
+    py::list out;
+    for (auto& ev : events) {
+      const int64_t t = int64_t(ev.first * 1e6) + 1;
+      if (ev.second == "backwards" || ev.second == "stopped") gpuexp_ctr::rearm_on_reset(s, c, t, ev.second == "backwards");
+      else if (ev.second == "armed") gpuexp_ctr::rearm_done(s, t);
+      else if (ev.second != "check") throw std::invalid_argument("unknown event " + ev.second);
+      out.append(py::make_tuple(s.waiting, (s.due_ns - 1) / 1e6, s.backoff_ns / 1e6, s.conflicts,
+                                gpuexp_ctr::rearm_due(s, c, t)));
+    }
+    return out;
+  }, py::arg("events"), py::arg("mode") = "backoff", py::arg("base_ms") = 2000.0, py::arg("max_ms") = 64000.0,
+     py::arg("calm_ms") = 300000.0);
+  // The PMC read machine (pmc_rounds.h) on scripted fake GPUs (pmc_fake.h): see
+  // tests/test_pmc_rounds.py.  Runs for ticks x tick_us with the GIL released.
+  m.def("pmc_harness", [](const py::dict& d) {
+    using namespace gpuexp_pmc;
+    HarnessConfig c;
+    auto geti = [&](const char* k, int def) { return d.contains(k) ? d[k].cast<int>() : def; };
+    auto getb = [&](const char* k, bool def) { return d.contains(k) ? d[k].cast<bool>() : def; };
+    c.gpus = geti("gpus", 8);
+    c.ticks = geti("ticks", 60);
+    c.tick_us = geti("tick_us", 10000);
+    c.work_us = geti("work_us", 300);
+    c.sync_us = geti("sync_us", 2000);
+    c.inline_rounds = getb("inline", true);
+    c.kick_at_end = getb("kick_at_end", false);
+    c.reader = getb("reader", true);
+    MachineConfig& mc = c.machine;
+    const std::string mode = d.contains("mode") ? d["mode"].cast<std::string>() : "cumulative";
+    mc.mode = mode == "resets" ? kResets : mode == "stops" ? kStops : kCumulative;
+    mc.interval_ms = geti("interval_ms", 1000);
+    mc.rescue = getb("rescue", true);
+    mc.rescue_rounds = geti("rescue_rounds", 3);
+    mc.probation_rounds = geti("probation_rounds", 5);
+    mc.first_slice_us = geti("first_slice_us", 60);
+    mc.slice_us = geti("slice_us", 100);
+    mc.log = getb("log", false);
+    const std::string rearm = d.contains("rearm") ? d["rearm"].cast<std::string>() : "backoff";
+    mc.rearm.mode = rearm == "off" ? gpuexp_ctr::kRearmOff : rearm == "now" ? gpuexp_ctr::kRearmNow
+                                                                            : gpuexp_ctr::kRearmBackoff;
+    mc.rearm.base_ns = int64_t(geti("rearm_base_ms", 2000)) * 1000000ll;
+    mc.rearm.max_ns = int64_t(geti("rearm_max_ms", 64000)) * 1000000ll;
+    if (d.contains("scripts"))
+      for (auto item : d["scripts"].cast<py::list>()) {
+        py::dict sd = item.cast<py::dict>();
+        FakeScript s;
+        if (sd.contains("latency_us")) s.latency_us = sd["latency_us"].cast<int64_t>();
+        if (sd.contains("stalls")) s.stalls = sd["stalls"].cast<std::vector<std::pair<int64_t, int64_t>>>();
+        if (sd.contains("resets")) s.resets = sd["resets"].cast<std::vector<int64_t>>();
+        if (sd.contains("stops")) s.stops = sd["stops"].cast<std::vector<std::pair<int64_t, int64_t>>>();
+        if (sd.contains("queue_error_at")) s.queue_error_at = sd["queue_error_at"].cast<int64_t>();
+        if (sd.contains("rescue_fails")) s.rescue_fails = sd["rescue_fails"].cast<bool>();
+        if (sd.contains("rate")) s.rate = sd["rate"].cast<double>();
+        if (sd.contains("read_mode")) s.read_mode = sd["read_mode"].cast<int>();
+        c.scripts.push_back(s);
+      }
+    const double tol = d.contains("rate_tolerance") ? d["rate_tolerance"].cast<double>() : 0.1;
+    HarnessOutcome o;
+    {
+      py::gil_scoped_release nogil;
+      o = run_pmc_harness(c, tol);
+    }
+    py::dict r;
+    r["ticks"] = o.ticks;
+    r["late_syncs"] = o.late_syncs;
+    r["max_sync_us"] = o.max_sync_us;
+    r["max_kick_us"] = o.max_kick_us;
+    r["reader_calls"] = o.reader_calls;
+    r["armed_all"] = o.armed_all;
+    py::list gl;
+    for (auto& g : o.gpus) {
+      py::dict x;
+      x["stalls"] = g.health.stalls;
+      x["resets"] = g.health.resets;
+      x["rearms"] = g.health.rearms;
+      x["rescues"] = g.health.rescues;
+      x["releases"] = g.health.releases;
+      x["rescue_active"] = g.health.rescue_active;
+      x["waiting_rearm"] = g.health.waiting_rearm;
+      x["conflicts"] = g.health.conflicts;
+      x["broken"] = g.health.broken;
+      x["windows"] = g.windows;
+      x["fresh_ticks"] = g.fresh_ticks;
+      x["bad_windows"] = g.bad_windows;
+      x["worst_rate_err"] = g.worst_rate_err;
+      x["packets"] = g.packets;
+      x["reads_completed"] = g.reads_completed;
+      x["uncollected"] = g.uncollected;
+      x["double_collected"] = g.double_collected;
+      x["arms"] = g.arms;
+      x["max_lateness_us"] = g.max_lateness_us;
+      x["rescue_opened"] = g.rescue_opened;
+      x["rescue_closed"] = g.rescue_closed;
+      x["misuse"] = g.misuse;
+      x["rescue_open_at_end"] = g.rescue_open_at_end;
+      gl.append(x);
+    }
+    r["gpus"] = gl;
+    return r;
+  });
   m.def("counter_names", []() {
     std::vector<std::string> v;
     for (int k = 0; k < gpuexp_ctr::kNumCtr; ++k) v.push_back(gpuexp_ctr::name(k));

@@ -53,6 +53,7 @@
 #include <unistd.h>
 
 #include "gpuexp/counter_model.h"
+#include "gpuexp/pmc_rounds.h"
 #include "kernels/probe_args.h"
 #include "gpuexp/sentinel_common.h"
 #include "gpuexp/sources.h"
@@ -84,7 +85,10 @@ const EventDef kGfx950[] = {
     {HSA_VEN_AMD_AQLPROFILE_BLOCK_NAME_SPI, 115, kSpiSgprFull},
 };
 
-struct Agent {
+// One GPU: its HSA queue(s), signals and aqlprofile programs.  The read machine
+// (pmc_rounds.cc) drives it through the ReadPort interface; init, the duty-cycled windows and
+// the sentinel / calibration dispatches use it directly.
+struct Agent : public gpuexp_pmc::ReadPort {
   int dev = -1;
   hsa_agent_t gpu{};
   std::string bdf, gfx;
@@ -98,54 +102,36 @@ struct Agent {
   void* cmd_buf = nullptr;
   void* out_buf = nullptr;
   bool ready = false;
-  std::atomic<bool> broken{false};  // a packet timed out: the GPU may still own the buffers
   std::atomic<bool> queue_error{false};
-  // The queue has two producers: the counting thread (PM4 programs) and the sampler
+  // The queue has two producers: the read machine / init (PM4 programs) and the sampler
   // thread (sentinel kernel dispatches, gpuexp_make_hsa_sentinel).
   std::mutex submit_mu;
-  // Continuous mode: the counters as of the last read (cumulative semantics) and when
-  // that read executed (the start of the next window).
-  double cum[kNumCtr] = {};
-  bool have_cum = false;
-  Clock::time_point t_last{};
-  Clock::time_point t_submit{};
-  // Continuous mode: a read packet that has not completed yet (the queue is stalled, e.g.
-  // behind a sentinel dispatch the workload's waves leave no room for).  It is waited for
-  // again next round instead of giving the GPU up; t_checked = when it was last seen pending.
-  bool read_inflight = false;
-  Clock::time_point t_checked{};
-  std::atomic<uint64_t> stalls{0};  // rounds in which this GPU's read had not completed
-  std::atomic<uint64_t> resets{0};  // windows dropped because a counter went backwards (wrap / reset)
-  // Written by the counting thread, read by gpuexp_rp_sample / _debug (m_mu).
-  std::mutex m_mu;
-  double last_raw[kNumCtr] = {};
-  int last_inst[kNumCtr] = {};
-  uint64_t last_samples = 0;
-  double last_window_s = 0;
-  double pub_cum[kNumCtr] = {};  // continuous, cumulative reads: raw totals since counting started
-  Clock::time_point t_window_end{};  // continuous: end of the last published window
-  Derived m;
-  std::string coord_names;  // aqlprofile's coordinates of the first MFMA sample (debug line; m_mu)
-  double cum_xm[kMaxXcc] = {}, cum_xg[kMaxXcc] = {};  // continuous, cumulative: per-XCC totals
-  std::string last_xsamples;  // debug (GPUEXP_AQLPMC_DEBUG): the last read's MFMA / GRBM samples
-  // Read rescue (continuous, cumulative; see rescue_reads): a second queue that only ever
-  // carries read packets, with its own profile, command and output buffers.  Temporary:
-  // once the read abandoned on the first queue has run (the queue drains again), reads go
-  // back there, and after kProbationRounds completed reads the rescue queue is destroyed.
-  int stuck_rounds = 0;  // consecutive rounds this GPU's read had not completed
-  std::atomic<bool> rescued{false};  // reads go to rq now (read by _debug)
-  std::atomic<uint64_t> rescues{0}, releases{0}, rearms{0};  // events so far (read by _debug / _health)
-  bool orphan = false;   // the read abandoned on `queue` has not completed yet (its sig is pending)
-  bool read_on_rq = false;  // the read in flight / last collected went to rq (its output buffer)
-  int probation = 0;     // back on the first queue with rq still alive: completed reads to go
-  bool was_pending = false;  // this round's read was already in flight before the round
-  int zero_grbm = 0;         // consecutive windows in which GRBM_COUNT did not advance
+  Clock::time_point t_submit{};  // run_packet (init, duty windows)
+  Derived model;                 // SIMD / CU counts, privilege (the machine's derivations)
+  // Read rescue (pmc_rounds.cc): a second queue that only ever carries read packets, with its
+  // own profile, command and output buffers; exists between open_rescue and close_rescue.
   hsa_queue_t* rq = nullptr;
   hsa_signal_t rsig{};
   hsa_ven_amd_aqlprofile_profile_t rprofile{};
   hsa_ext_amd_aql_pm4_packet_t rstart_pkt{}, rread_pkt{};
   void* rcmd_buf = nullptr;
   void* rout_buf = nullptr;
+  // debug (GPUEXP_AQLPMC_DEBUG): aqlprofile's coordinates of the first MFMA sample and the last
+  // read's MFMA / GRBM samples
+  std::mutex dbg_mu;
+  std::string coord_names, last_xsamples;
+
+  // ReadPort (pmc_rounds.h); defined below
+  void post_read(int q) override;
+  void post_arm(bool baseline_read) override;
+  void post_start() override;
+  void post_stop(int q) override;
+  bool done(int q) override;
+  bool failed() override { return queue_error.load(); }
+  bool collect(int q, gpuexp_pmc::Sample* out) override;
+  bool open_rescue() override;
+  void close_rescue() override;
+  std::string label() const override { return bdf; }
 };
 
 // aqlprofile entry points come from the runtime's extension table: the runtime loads
@@ -175,44 +161,38 @@ bool g_have_pool = false;
 uint64_t g_ts_freq = 1000000000ull;
 int g_window_ms = 20;
 int g_interval_ms = 1000;
+// Duty-cycled windows (gpuexp_rp_set_duty, or continuous counting unavailable): this
+// thread's start -> sleep(window) -> read -> stop loop.
 std::thread g_thread;
 std::atomic<bool> g_quit{false};
 std::condition_variable g_cv;
 std::mutex g_cv_mu;
+std::atomic<uint64_t> g_thread_cpu_ns{0};  // the duty thread's own CPU, published per window
 // Continuous mode (gpuexp_rp_set_continuous): counting is started once and never stopped;
-// the engine kicks one read round per tick (g_kick_seq), and gpuexp_rp_sync waits for it
-// (g_done_seq, g_done_cv).  All three under g_cv_mu.
+// the engine kicks one read round per tick, run by the read machine (pmc_rounds.h).
 bool g_continuous = false;
-uint64_t g_kick_seq = 0, g_done_seq = 0;
-std::condition_variable g_done_cv;
-std::atomic<uint64_t> g_thread_cpu_ns{0};  // the counting thread's own CPU, published per round
-// where a continuous read round's CPU goes (counting thread clock): post / wait / collect
-std::atomic<uint64_t> g_round_cpu[3] = {}, g_rounds{0};
 // Inline rounds (continuous mode; gpuexp_rp_set_inline, which the engine calls when its
-// sampler ticks periodically; GPUEXP_PMC_INLINE=0/1 overrides): the
-// engine's sampler posts the round's read packets itself at gpuexp_rp_kick and collects them
-// at gpuexp_rp_sync, after its device reads (~100-400 us later: the reads are done by then),
-// so a tick costs the counting thread no wake-ups at all; the thread only runs rounds when
-// nothing has kicked for a second (an engine that is not ticking).  Without it the thread
-// wakes per kick plus once per 60/100 us wait slice and the sampler waits on its condvar.
+// sampler ticks periodically; GPUEXP_PMC_INLINE=0/1 overrides): the engine's sampler posts
+// the round's read packets itself at gpuexp_rp_kick and collects them at gpuexp_rp_sync, after
+// its device reads (~100-400 us later: the reads are done by then), so a tick costs the
+// counting thread no wake-ups at all.
 bool g_inline = false;
-std::mutex g_round_mu;  // one round at a time, whichever thread runs it
-bool g_live = false;    // under g_round_mu: agents armed, the counting thread running
-std::atomic<uint64_t> g_last_kick_ns{0};
+// The read machine: created at init (every mode: it also publishes duty windows), destroyed at
+// shutdown after the engine's sampler has stopped kicking.
+std::atomic<gpuexp_pmc::RoundMachine*> g_machine{nullptr};
 
 uint64_t own_cpu_ns() {
   timespec ts;
   clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
   return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
 }
-// What a read packet does to the counters, probed on the GPU at init (read_semantics):
-// kCumulative: they keep counting (deltas of successive reads); kResets: each read returns
-// the counts since the previous read; kStops: counting stops at a read (re-armed after).
-enum ReadMode { kReadUnknown, kCumulative, kResets, kStops };
+using gpuexp_pmc::ReadMode;
+using gpuexp_pmc::kReadUnknown;
+using gpuexp_pmc::kCumulative;
+using gpuexp_pmc::kResets;
+using gpuexp_pmc::kStops;
+using gpuexp_pmc::read_mode_name;
 ReadMode g_read_mode = kReadUnknown;
-const char* read_mode_name(ReadMode m) {
-  return m == kCumulative ? "cumulative" : m == kResets ? "resets at read" : m == kStops ? "stops at read" : "?";
-}
 
 std::string lower(std::string s) {
   for (auto& c : s) c = char(::tolower(c));
@@ -391,12 +371,14 @@ hsa_status_t on_data(hsa_ven_amd_aqlprofile_info_type_t type, hsa_ven_amd_aqlpro
     if (def.ctr == kMfma || def.ctr == kGrbmCount) {
       const int k = def.ctr == kMfma ? 0 : 1;
       const int xcc = sample_xcc(acc, k, d->sample_id);
-      if (k == 0 && d->sample_id == 0 && acc->x_seen[0] == 1 && acc->a->coord_names.empty()) {
-        CoordProbe p;  // once, for the debug line
-        if (g_aql.hsa_ven_amd_aqlprofile_iterate_event_coord)
-          g_aql.hsa_ven_amd_aqlprofile_iterate_event_coord(acc->a->gpu, ev, 0, on_coord, &p);
-        std::lock_guard<std::mutex> lk(acc->a->m_mu);
-        acc->a->coord_names = p.names.empty() ? "none" : p.names;
+      if (g_debug && k == 0 && d->sample_id == 0 && acc->x_seen[0] == 1) {
+        std::lock_guard<std::mutex> lk(acc->a->dbg_mu);
+        if (acc->a->coord_names.empty()) {  // once, for the debug line
+          CoordProbe p;
+          if (g_aql.hsa_ven_amd_aqlprofile_iterate_event_coord)
+            g_aql.hsa_ven_amd_aqlprofile_iterate_event_coord(acc->a->gpu, ev, 0, on_coord, &p);
+          acc->a->coord_names = p.names.empty() ? "none" : p.names;
+        }
       }
       if (acc->xs_n[k] < 64) acc->xs[k][acc->xs_n[k]++] = {d->sample_id, xcc, x};
       if (xcc < 0) {
@@ -427,9 +409,9 @@ bool setup_agent(Agent& a, std::string* why) {
   uint32_t cu = 0, simd_per_cu = 0;
   hsa_agent_get_info(a.gpu, hsa_agent_info_t(HSA_AMD_AGENT_INFO_COMPUTE_UNIT_COUNT), &cu);
   hsa_agent_get_info(a.gpu, hsa_agent_info_t(HSA_AMD_AGENT_INFO_NUM_SIMDS_PER_CU), &simd_per_cu);
-  a.m.cu = cu;
-  a.m.privileged = pmc_device_scope();
-  a.m.simd = cu * simd_per_cu;
+  a.model.cu = cu;
+  a.model.privileged = pmc_device_scope();
+  a.model.simd = cu * simd_per_cu;
 
   hsa_ven_amd_aqlprofile_profile_t probe{};
   probe.agent = a.gpu;
@@ -549,54 +531,135 @@ bool setup_agent(Agent& a, std::string* why) {
   return true;
 }
 
-// The counting thread is the only user of an agent's signal and PM4 packets once the
-// thread runs; g_agents itself changes only before it starts and after it is joined, so
-// rounds take no global lock (gpuexp_rp_sample never waits behind a GPU round trip).
 bool usable(const Agent* a) { return a && a->ready && !a->broken.load(); }
 
-// Reads the output buffer the last read packet filled: reduced value + instances per counter.
-bool collect(Agent& a, Accum* acc) {
+// Reads the output buffer the last read packet on queue q filled: reduced value + instances per
+// counter.  The first queue's reads land in the agent's profile buffer, the rescue queue's in
+// the rescue profile's.
+bool collect(Agent& a, int q, Accum* acc) {
   *acc = Accum{};
   acc->a = &a;
-  // a read on the rescue queue lands in the rescue profile's output buffer
-  auto* prof = a.read_on_rq ? &a.rprofile : &a.profile;
+  auto* prof = q == 1 ? &a.rprofile : &a.profile;
   const bool ok = g_aql.hsa_ven_amd_aqlprofile_iterate_data(prof, on_data, acc) == HSA_STATUS_SUCCESS;
   // per-XCC only when every sample of both counters has an XCC, both agree on the XCC count
   // and every XCC has as many SQ samples (SEs) as the first
   bool even = acc->xm_n > 0;
   for (int x = 1; x < acc->xm_n; ++x) even = even && acc->xm_cnt[x] == acc->xm_cnt[0];
   acc->nxcc = !acc->x_unmapped && even && acc->xm_n == acc->xg_n ? acc->xm_n : 0;
+  if (g_debug) {
+    std::string xs;
+    for (int k = 0; k < 2; ++k) {
+      xs += k ? ";grbm_samples=" : "mfma_samples=";
+      for (int j = 0; j < acc->xs_n[k]; ++j) {
+        char t[64];
+        std::snprintf(t, sizeof(t), "%s%u@%d:%.0f", j ? "," : "", acc->xs[k][j].id, acc->xs[k][j].xcc,
+                      acc->xs[k][j].v);
+        xs += t;
+      }
+    }
+    std::lock_guard<std::mutex> lk(a.dbg_mu);
+    a.last_xsamples = std::move(xs);
+  }
   return ok;
 }
 
-// d / xm / xg: this window's deltas (chip counters, per-XCC MFMA cycles, per-XCC GRBM_COUNT).
-void publish(Agent& a, const double* d, const Accum& acc, double wall, Clock::time_point end = {},
-             const double* cum = nullptr, const double* xm = nullptr, const double* xg = nullptr) {
-  std::string xsamples;
-  if (g_debug)
-    for (int k = 0; k < 2; ++k) {
-      xsamples += k ? ";grbm_samples=" : "mfma_samples=";
-      for (int j = 0; j < acc.xs_n[k]; ++j) {
-        char t[64];
-        std::snprintf(t, sizeof(t), "%s%u@%d:%.0f", j ? "," : "", acc.xs[k][j].id, acc.xs[k][j].xcc, acc.xs[k][j].v);
-        xsamples += t;
-      }
-    }
-  std::lock_guard<std::mutex> lk(a.m_mu);
-  if (g_debug) a.last_xsamples = std::move(xsamples);
-  a.t_window_end = end;
-  if (cum) std::memcpy(a.pub_cum, cum, sizeof(a.pub_cum));
-  std::memcpy(a.last_raw, d, sizeof(a.last_raw));
-  std::memcpy(a.last_inst, acc.inst, sizeof(acc.inst));
-  a.last_samples = acc.samples;
-  a.last_window_s = wall;
-  if (wall > 0) {
-    derive(a.m, d, acc.inst, wall);
-    derive_xcc(a.m, xm ? xm : acc.xm, xg ? xg : acc.xg, acc.nxcc);
+gpuexp_pmc::Sample to_sample(const Accum& acc) {
+  gpuexp_pmc::Sample s;
+  std::memcpy(s.v, acc.v, sizeof(s.v));
+  std::memcpy(s.inst, acc.inst, sizeof(s.inst));
+  s.samples = acc.samples;
+  std::memcpy(s.xm, acc.xm, sizeof(s.xm));
+  std::memcpy(s.xg, acc.xg, sizeof(s.xg));
+  s.nxcc = acc.nxcc;
+  return s;
+}
+
+// ---- ReadPort on HSA: every call comes from the read machine under its round lock ----
+void Agent::post_read(int q) {
+  if (q == 1) {
+    hsa_signal_store_relaxed(rsig, 1);
+    submit_on(*this, rq, rsig, rread_pkt, /*barrier=*/false);
+  } else {
+    hsa_signal_store_relaxed(sig, 1);
+    submit_on(*this, queue, sig, read_pkt, /*barrier=*/false);
   }
 }
 
-void window_all() {
+// Start program, then (cumulative) the baseline read behind a barrier; one completion signal,
+// on the last packet.  No wait: the machine looks at the signal in its rounds.
+void Agent::post_arm(bool baseline_read) {
+  hsa_signal_store_relaxed(sig, 1);
+  if (baseline_read) {
+    submit_on(*this, queue, hsa_signal_t{0}, start_pkt, /*barrier=*/true);
+    submit_on(*this, queue, sig, read_pkt, /*barrier=*/true);
+  } else {
+    submit_on(*this, queue, sig, start_pkt, /*barrier=*/true);
+  }
+}
+
+void Agent::post_start() { submit_on(*this, queue, hsa_signal_t{0}, start_pkt, /*barrier=*/true); }
+
+void Agent::post_stop(int q) {
+  hsa_signal_t s = q == 1 ? rsig : sig;
+  hsa_signal_store_relaxed(s, 1);
+  submit_on(*this, q == 1 ? rq : queue, s, stop_pkt, /*barrier=*/true);
+}
+
+bool Agent::done(int q) { return hsa_signal_load_scacquire(q == 1 ? rsig : sig) < 1; }
+
+bool Agent::collect(int q, gpuexp_pmc::Sample* out) {
+  Accum acc;
+  if (!::collect(*this, q, &acc)) return false;
+  *out = to_sample(acc);
+  return true;
+}
+
+// Read rescue.  The sentinel shares the counters' queue (one ~173 MiB context-save area per
+// GPU instead of two), and the packet processor does not look past a kernel dispatch whose
+// waves cannot be placed: a workload holding every wave slot for seconds (measured: 8
+// blocks x 4 waves per CU issuing MFMAs, tools/mfma_calibration.py --starve) holds every
+// read behind the sentinel run, and the counters go stale exactly when the GPU is busiest.
+// After rescue_rounds stuck rounds the read machine moves reads to a second queue of their own:
+// the counters are chip state, so a read packet from any queue copies the same running totals
+// (cumulative mode only: there a read changes nothing, and the abandoned read on the first
+// queue, which still runs once the sentinel does, is harmless).  The second queue and its
+// ~173 MiB context-save area exist only while a GPU needs them (measured: the first queue
+// drains 0.8 s after a 6 s starvation, profiles/r03/sentinel_starvation.txt).
+// GPUEXP_PMC_READ_RESCUE=0 disables.
+bool Agent::open_rescue() {
+  rprofile = profile;
+  rcmd_buf = sys_alloc(cmd_size, gpu);
+  rout_buf = sys_alloc(out_size, gpu);
+  bool ok = rcmd_buf && rout_buf;
+  if (ok) {
+    rprofile.command_buffer = {rcmd_buf, cmd_size};
+    rprofile.output_buffer = {rout_buf, out_size};
+    // the start program is generated (the read program is built after it) but never run:
+    // it would re-program and reset the running counters
+    ok = g_aql.hsa_ven_amd_aqlprofile_start(&rprofile, &rstart_pkt) == HSA_STATUS_SUCCESS &&
+         g_aql.hsa_ven_amd_aqlprofile_read(&rprofile, &rread_pkt) == HSA_STATUS_SUCCESS;
+  }
+  ok = ok && hsa_queue_create(gpu, 64, HSA_QUEUE_TYPE_MULTI, queue_error_cb, this, UINT32_MAX, UINT32_MAX, &rq) ==
+                 HSA_STATUS_SUCCESS;
+  if (ok) hsa_amd_queue_set_priority(rq, HSA_AMD_QUEUE_PRIORITY_LOW);
+  ok = ok && hsa_signal_create(1, 0, nullptr, &rsig) == HSA_STATUS_SUCCESS;
+  if (!ok) close_rescue();
+  return ok;
+}
+
+// Releases the rescue queue (its context-save area), its signal and buffers.
+void Agent::close_rescue() {
+  if (rq) hsa_queue_destroy(rq);
+  if (rsig.handle) hsa_signal_destroy(rsig);
+  if (rcmd_buf) hsa_amd_memory_pool_free(rcmd_buf);
+  if (rout_buf) hsa_amd_memory_pool_free(rout_buf);
+  rq = nullptr;
+  rsig = hsa_signal_t{};
+  rcmd_buf = rout_buf = nullptr;
+}
+
+// Duty-cycled windows: start, sleep(window), read, stop on every GPU, one window per interval.
+void window_all(gpuexp_pmc::RoundMachine& m) {
   std::vector<Clock::time_point> t0(g_agents.size());
   for (size_t i = 0; i < g_agents.size(); ++i) {
     Agent* a = g_agents[i];
@@ -619,324 +682,9 @@ void window_all() {
       continue;
     }
     Accum acc;
-    if (!collect(*a, &acc)) continue;
-    publish(*a, acc.v, acc, std::chrono::duration<double>(t1 - t0[i]).count());
+    if (!collect(*a, 0, &acc)) continue;
+    m.publish_window(int(i), acc.v, to_sample(acc), std::chrono::duration<double>(t1 - t0[i]).count());
   }
-}
-
-// Read rescue.  The sentinel shares the counters' queue (one ~173 MiB context-save area per
-// GPU instead of two), and the packet processor does not look past a kernel dispatch whose
-// waves cannot be placed: a workload holding every wave slot for seconds (measured: 8
-// blocks x 4 waves per CU issuing MFMAs, tools/mfma_calibration.py --starve) holds every
-// read behind the sentinel run, and the counters go stale exactly when the GPU is busiest.
-// After kRescueRounds stuck rounds, reads move for good to a second queue of their own: the
-// counters are chip state, so a read packet from any queue copies the same running totals
-// (cumulative mode only: there a read changes nothing, and the abandoned read on the first
-// queue, which still runs once the sentinel does, is harmless).  The second queue and its
-// ~173 MiB context-save area exist only while a GPU needs them: when the abandoned read
-// completes (the first queue drains again; measured 0.8 s after a 6 s starvation,
-// profiles/r03/sentinel_starvation.txt) reads return to the first queue, and after
-// kProbationRounds completed reads there the rescue queue is destroyed (end_rescue); a read
-// stuck again during probation moves back to the still-existing rescue queue at once.
-// GPUEXP_PMC_READ_RESCUE=0 disables.
-constexpr int kRescueRounds = 3;
-constexpr int kProbationRounds = 5;
-
-bool rescue_enabled() {
-  const char* e = std::getenv("GPUEXP_PMC_READ_RESCUE");
-  return !(e && e[0] == '0');
-}
-
-bool rescue_reads(Agent& a) {
-  a.rprofile = a.profile;
-  a.rcmd_buf = sys_alloc(a.cmd_size, a.gpu);
-  a.rout_buf = sys_alloc(a.out_size, a.gpu);
-  bool ok = a.rcmd_buf && a.rout_buf;
-  if (ok) {
-    a.rprofile.command_buffer = {a.rcmd_buf, a.cmd_size};
-    a.rprofile.output_buffer = {a.rout_buf, a.out_size};
-    // the start program is generated (the read program is built after it) but never run:
-    // it would re-program and reset the running counters
-    ok = g_aql.hsa_ven_amd_aqlprofile_start(&a.rprofile, &a.rstart_pkt) == HSA_STATUS_SUCCESS &&
-         g_aql.hsa_ven_amd_aqlprofile_read(&a.rprofile, &a.rread_pkt) == HSA_STATUS_SUCCESS;
-  }
-  ok = ok && hsa_queue_create(a.gpu, 64, HSA_QUEUE_TYPE_MULTI, queue_error_cb, &a, UINT32_MAX, UINT32_MAX, &a.rq) ==
-                 HSA_STATUS_SUCCESS;
-  if (ok) hsa_amd_queue_set_priority(a.rq, HSA_AMD_QUEUE_PRIORITY_LOW);
-  ok = ok && hsa_signal_create(1, 0, nullptr, &a.rsig) == HSA_STATUS_SUCCESS;
-  if (!ok) {
-    if (a.rq) hsa_queue_destroy(a.rq);
-    if (a.rcmd_buf) hsa_amd_memory_pool_free(a.rcmd_buf);
-    if (a.rout_buf) hsa_amd_memory_pool_free(a.rout_buf);
-    a.rq = nullptr;
-    a.rcmd_buf = a.rout_buf = nullptr;
-    return false;
-  }
-  a.rescued = true;
-  a.orphan = true;
-  a.rescues += 1;
-  std::fprintf(stderr, "[aqlpmc] gpu %s: counter reads stuck behind a sentinel run the workload leaves no wave "
-               "slot for; reads moved to a queue of their own\n", a.bdf.c_str());
-  return true;
-}
-
-// Releases the rescue queue (its context-save area) once reads run on the first queue again.
-void end_rescue(Agent& a) {
-  if (a.rq) hsa_queue_destroy(a.rq);
-  if (a.rsig.handle) hsa_signal_destroy(a.rsig);
-  if (a.rcmd_buf) hsa_amd_memory_pool_free(a.rcmd_buf);
-  if (a.rout_buf) hsa_amd_memory_pool_free(a.rout_buf);
-  a.rq = nullptr;
-  a.rsig = hsa_signal_t{};
-  a.rcmd_buf = a.rout_buf = nullptr;
-  a.probation = 0;
-  a.releases += 1;
-  std::fprintf(stderr, "[aqlpmc] gpu %s: counter reads complete on the first queue again; rescue queue released\n",
-               a.bdf.c_str());
-}
-
-// Counting restarted from scratch: start packet, then (cumulative) a new baseline read.
-bool arm_continuous(Agent& a);
-
-// A window whose counters went backwards (another profiler reset or re-programmed them) or
-// whose GRBM_COUNT did not advance over real time (counting stopped under us): start the
-// counters again with our own selects.  On the first queue only (a rescued GPU's first
-// queue is stuck; its windows are dropped until the rescue ends).
-void rearm(Agent& a) {
-  if (a.rescued || a.orphan) return;
-  a.rearms += 1;
-  std::fprintf(stderr, "[aqlpmc] gpu %s: counters reset or stopped by someone else; re-armed\n", a.bdf.c_str());
-  if (!arm_continuous(a)) a.broken = true;
-}
-
-// Continuous mode, one round: a read packet in flight on every GPU at once, then each GPU
-// collected as soon as its read completes (one polling loop over all of them, sleeping
-// between looks), so one stuck GPU never delays the others' windows.  A GPU whose read was
-// already pending before this round gets one look, not the round's deadline.  Counting
-// itself never pauses (kStops: re-armed right after the read, a gap of one PM4 packet).
-// Split in two (post_round / finish_round) so the engine's sampler can run it inline.
-struct Round {
-  std::vector<Agent*> waiting;
-  uint64_t cpu_post = 0, cpu_wait = 0, cpu_collect = 0;
-  bool open = false;
-};
-Round g_round;  // under g_round_mu
-// Reads of an inline round that outlived the engine's sync wait: the counting thread keeps
-// looking at them (60/100 us slices, as the thread-run round does) until they complete or
-// the next kick takes them over, so a slow read's window still gets its completion time
-// to within a slice.  Under g_round_mu.
-std::vector<Agent*> g_leftover;
-std::atomic<bool> g_leftover_flag{false};  // set by sync, taken by the thread
-
-void post_round(Round& r) {
-  const uint64_t c0 = own_cpu_ns();
-  r.waiting.clear();
-  g_leftover.clear();
-  r.cpu_wait = r.cpu_collect = 0;
-  for (Agent* a : g_agents) {
-    if (!usable(a)) continue;
-    if (a->rescued && a->orphan && hsa_signal_load_scacquire(a->sig) < 1) {
-      // the read abandoned on the first queue ran: that queue moves again; reads go back
-      // there (the rescue queue stays until kProbationRounds reads there complete)
-      // (a rescue read still in flight is collected first: read_on_rq keeps its buffer)
-      a->orphan = false;
-      a->rescued = false;
-      a->probation = kProbationRounds;
-    }
-    a->was_pending = a->read_inflight;
-    if (!a->read_inflight) {
-      if (a->rescued) {
-        hsa_signal_store_relaxed(a->rsig, 1);
-        a->t_submit = Clock::now();
-        submit_on(*a, a->rq, a->rsig, a->rread_pkt, /*barrier=*/false);
-        a->read_on_rq = true;
-      } else {
-        post_packet(*a, a->read_pkt, /*barrier=*/false);
-        a->read_on_rq = false;
-      }
-      a->read_inflight = true;
-      a->t_checked = a->t_submit;
-    }
-    r.waiting.push_back(a);
-  }
-  r.open = true;
-  r.cpu_post = own_cpu_ns() - c0;
-}
-
-// A read still queued at its round's end (final): look again next round; after
-// kRescueRounds such rounds the reads move to a rescue queue.
-void round_stuck(Agent* a, Clock::time_point now) {
-  a->t_checked = now;
-  ++a->stalls;
-  // stuck again while on probation (the rescue queue still exists): back to it at once
-  if (a->read_on_rq || g_read_mode != kCumulative || ++a->stuck_rounds < (a->rq ? 1 : kRescueRounds)) return;
-  if (a->rq) {
-    a->rescued = true;
-    a->orphan = true;
-    a->probation = 0;
-    a->read_inflight = false;
-    a->stuck_rounds = 0;
-  } else if (rescue_enabled() && rescue_reads(*a)) {
-    a->read_inflight = false;
-    a->stuck_rounds = 0;
-  }
-}
-
-// A read that completed (seen at `now`): collect, derive and publish its window.
-void round_done(Round& r, Agent* a, Clock::time_point now) {
-  a->read_inflight = false;
-  a->stuck_rounds = 0;
-  // the read executed between the last time it was seen pending and now
-  const auto t = a->t_checked + (now - a->t_checked) / 2;
-  Accum acc;
-  const uint64_t k0 = own_cpu_ns();
-  const bool got = collect(*a, &acc);
-  r.cpu_collect += own_cpu_ns() - k0;
-  if (!a->read_on_rq && a->probation > 0 && --a->probation == 0 && a->rq) end_rescue(*a);
-  if (!got) return;
-  const double wall = std::chrono::duration<double>(t - a->t_last).count();
-  if (g_read_mode == kCumulative) {
-    double d[kNumCtr], xm[kMaxXcc], xg[kMaxXcc];
-    for (int k = 0; k < kNumCtr; ++k) d[k] = acc.v[k] - a->cum[k];
-    for (int x = 0; x < acc.nxcc; ++x) {
-      xm[x] = std::max(0.0, acc.xm[x] - a->cum_xm[x]);
-      xg[x] = std::max(0.0, acc.xg[x] - a->cum_xg[x]);
-    }
-    const bool first = !a->have_cum;
-    std::memcpy(a->cum, acc.v, sizeof(a->cum));
-    std::memcpy(a->cum_xm, acc.xm, sizeof(a->cum_xm));
-    std::memcpy(a->cum_xg, acc.xg, sizeof(a->cum_xg));
-    a->have_cum = true;
-    a->t_last = t;
-    const WindowAction act = window_action(d, first, wall, &a->zero_grbm);
-    if (act == kRearm) {
-      ++a->resets;  // reset / re-programmed / stopped under us: this window is unknown
-      rearm(*a);
-      return;
-    }
-    if (act == kPublish) publish(*a, d, acc, wall, t, acc.v, xm, xg);
-  } else {
-    publish(*a, acc.v, acc, wall, t);
-    a->t_last = t;
-    if (g_read_mode == kStops) {
-      const auto ts = run_packet(*a, a->start_pkt);
-      if (ts == Clock::time_point{}) a->broken = true;
-      else a->t_last = ts;
-    }
-  }
-}
-
-
-// Collects the round's reads until each completed or `deadline`.  final: a read still
-// pending at the deadline is stuck (counted, rescued after kRescueRounds); otherwise it stays
-// in flight (handed to the counting thread, g_leftover) and the next round gives it its one
-// look.  Returns true when none is left.
-bool finish_round(Round& r, Clock::time_point deadline, bool final) {
-  auto& waiting = r.waiting;
-  for (int i = 0; !waiting.empty(); ++i) {
-    const uint64_t w0 = own_cpu_ns();
-    auto now = Clock::now();
-    for (auto it = waiting.begin(); it != waiting.end();) {
-      Agent* a = *it;
-      if (a->queue_error.load()) {
-        a->broken = true;
-        it = waiting.erase(it);
-        continue;
-      }
-      if (hsa_signal_load_scacquire(a->read_on_rq ? a->rsig : a->sig) < 1) {
-        r.cpu_wait += own_cpu_ns() - w0;
-        round_done(r, a, now);
-        it = waiting.erase(it);
-        continue;
-      }
-      if (a->was_pending) {  // one look for an old read
-        round_stuck(a, now);
-        it = waiting.erase(it);
-        continue;
-      }
-      if (now >= deadline) {
-        if (!final) {  // stays in flight
-          a->t_checked = now;
-          ++it;
-          continue;
-        }
-        round_stuck(a, now);
-        it = waiting.erase(it);
-        continue;
-      }
-      ++it;
-    }
-    if (waiting.empty() || now >= deadline) break;
-    now = Clock::now();
-    std::this_thread::sleep_for(std::min<Clock::duration>(std::chrono::microseconds(i == 0 ? 60 : 100),
-                                                          deadline > now ? deadline - now : Clock::duration(0)));
-    r.cpu_wait += own_cpu_ns() - w0;
-  }
-  const bool all = waiting.empty();
-  if (!all && !final) g_leftover = waiting;
-  waiting.clear();
-  r.open = false;
-  g_round_cpu[0] += r.cpu_post;
-  g_round_cpu[1] += r.cpu_wait;
-  g_round_cpu[2] += r.cpu_collect;
-  ++g_rounds;
-  return all;
-}
-
-// Counting thread: follows g_leftover until each read completed, the next kick took it
-// over (post_round clears the list), or a fallback interval passed (then the next round's
-// one look decides).
-void follow_leftover() {
-  Round r;
-  const auto give_up = Clock::now() + std::chrono::milliseconds(g_interval_ms);
-  for (int i = 0;; ++i) {
-    {
-      std::lock_guard<std::mutex> rl(g_round_mu);
-      if (!g_live || g_leftover.empty()) return;
-      const auto now = Clock::now();
-      for (auto it = g_leftover.begin(); it != g_leftover.end();) {
-        Agent* a = *it;
-        if (!a->read_inflight || a->queue_error.load()) {
-          it = g_leftover.erase(it);
-        } else if (hsa_signal_load_scacquire(a->read_on_rq ? a->rsig : a->sig) < 1) {
-          round_done(r, a, now);
-          it = g_leftover.erase(it);
-        } else {
-          a->t_checked = now;
-          ++it;
-        }
-      }
-      if (g_leftover.empty() || now >= give_up) return;
-    }
-    std::this_thread::sleep_for(std::chrono::microseconds(i == 0 ? 60 : 100));
-  }
-}
-
-void read_round() {
-  const auto begin = Clock::now();
-  // a stalled GPU costs the round at most this long (the other GPUs' reads are in flight)
-  const auto deadline = begin + std::chrono::milliseconds(std::min(1000, g_interval_ms));
-  post_round(g_round);
-  finish_round(g_round, deadline, /*final=*/true);
-}
-
-// Starts counting on `a` for good: start packet, then (cumulative) the baseline read.
-bool arm_continuous(Agent& a) {
-  const auto ts = run_packet(a, a.start_pkt);
-  if (ts == Clock::time_point{}) return false;
-  a.t_last = ts;
-  a.have_cum = false;
-  if (g_read_mode == kCumulative) {
-    const auto tr = run_packet(a, a.read_pkt);
-    Accum acc;
-    if (tr == Clock::time_point{} || !collect(a, &acc)) return false;
-    std::memcpy(a.cum, acc.v, sizeof(a.cum));
-    std::memcpy(a.cum_xm, acc.xm, sizeof(a.cum_xm));
-    std::memcpy(a.cum_xg, acc.xg, sizeof(a.cum_xg));
-    a.have_cum = true;
-    a.t_last = tr;
-  }
-  return true;
 }
 
 // What does a read packet do to running counters?  start, 20 ms, read (B), then at once a
@@ -955,7 +703,7 @@ ReadMode read_semantics(Agent& a, std::string* why) {
     if (i == 0) std::this_thread::sleep_for(std::chrono::milliseconds(20));
     const auto t = run_packet(a, a.read_pkt);
     Accum acc;
-    if (ts == Clock::time_point{} || t == Clock::time_point{} || !collect(a, &acc)) {
+    if (ts == Clock::time_point{} || t == Clock::time_point{} || !collect(a, 0, &acc)) {
       *why = "PM4 read packet did not complete";
       return kReadUnknown;
     }
@@ -967,84 +715,18 @@ ReadMode read_semantics(Agent& a, std::string* why) {
     *why = "GRBM_COUNT did not advance after the start packet";
     return kReadUnknown;
   }
-  if (c[1] == c[0]) return kStops;
+  if (c[1] == c[0]) return gpuexp_pmc::kStops;
   if (c[1] > c[0]) return kCumulative;
   if (c[1] < 0.5 * c[0]) return kResets;
   *why = "read packet semantics unclear (GRBM_COUNT " + std::to_string(c[0]) + " then " + std::to_string(c[1]) + ")";
   return kReadUnknown;
 }
 
-void counting_loop() {
+void duty_loop(gpuexp_pmc::RoundMachine* m) {
   ::prctl(PR_SET_NAME, "gpuexp-pmc", 0, 0, 0);
-  ::prctl(PR_SET_TIMERSLACK, 10000UL, 0, 0, 0);  // 10 us: the wait_signal slices stay short
-  if (g_continuous && g_inline) {
-    // the engine runs the rounds (gpuexp_rp_kick / gpuexp_rp_sync); this thread only keeps
-    // counting read when nothing has kicked for a second
-    bool idle = false;
-    while (!g_quit.load()) {
-      {
-        std::unique_lock<std::mutex> lk(g_cv_mu);
-        g_cv.wait_for(lk, std::chrono::milliseconds(idle ? g_interval_ms : std::max(2 * g_interval_ms, 1000)),
-                      [] { return g_quit.load() || g_leftover_flag.load(); });
-      }
-      if (g_quit.load()) break;
-      if (g_leftover_flag.exchange(false)) {  // reads that outlived the sampler's sync wait
-        follow_leftover();
-        g_thread_cpu_ns.store(own_cpu_ns());
-        continue;
-      }
-      const uint64_t last = g_last_kick_ns.load();
-      const uint64_t now = uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
-                                        Clock::now().time_since_epoch()).count());
-      // no kick for a second, or for two fallback intervals of a slow (e.g. 1 Hz) engine
-      idle = !last || now - last > std::max<uint64_t>(1000000000ull, 2000000ull * uint64_t(g_interval_ms));
-      if (!idle) continue;
-      std::lock_guard<std::mutex> rl(g_round_mu);
-      read_round();
-      g_thread_cpu_ns.store(own_cpu_ns());
-    }
-  } else if (g_continuous) {
-    uint64_t served = 0;
-    while (!g_quit.load()) {
-      uint64_t target;
-      {
-        std::unique_lock<std::mutex> lk(g_cv_mu);
-        // a tick's kick, or on our own every interval when nothing kicks (manual engines)
-        g_cv.wait_for(lk, std::chrono::milliseconds(g_interval_ms),
-                      [&] { return g_quit.load() || g_kick_seq != served; });
-        if (g_quit.load()) break;
-        target = g_kick_seq;
-      }
-      {
-        std::lock_guard<std::mutex> rl(g_round_mu);
-        read_round();
-      }
-      g_thread_cpu_ns.store(own_cpu_ns());
-      served = target;
-      {
-        std::lock_guard<std::mutex> lk(g_cv_mu);
-        g_done_seq = target;
-      }
-      g_done_cv.notify_all();
-    }
-  }
-  if (g_continuous) {
-    std::lock_guard<std::mutex> rl(g_round_mu);
-    for (Agent* a : g_agents) {
-      if (!usable(a) || a->read_inflight) continue;
-      if (a->rescued) {  // the first queue may still be stuck: stop from the rescue queue
-        hsa_signal_store_relaxed(a->rsig, 1);
-        submit_on(*a, a->rq, a->rsig, a->stop_pkt, true);
-        wait_signal(a->rsig, Clock::now() + std::chrono::seconds(1));
-      } else {
-        run_packet(*a, a->stop_pkt);
-      }
-    }
-    return;
-  }
   while (!g_quit.load()) {
     const auto begin = Clock::now();
-    window_all();
+    window_all(*m);
     g_thread_cpu_ns.store(own_cpu_ns());
     const auto spent = std::chrono::duration_cast<std::chrono::milliseconds>(Clock::now() - begin).count();
     std::unique_lock<std::mutex> lk(g_cv_mu);
@@ -1056,18 +738,17 @@ void counting_loop() {
 void teardown_locked() {
   for (Agent* a : g_agents) {
     if (!a) continue;
-    // an abandoned read (rescue) that never ran may still write the first buffers
-    const bool orphan_pending = a->orphan && a->sig.handle && hsa_signal_load_scacquire(a->sig) >= 1;
     if (a->queue) hsa_queue_destroy(a->queue);
-    if (a->rq) hsa_queue_destroy(a->rq);
     if (a->sig.handle) hsa_signal_destroy(a->sig);
-    if (a->rsig.handle) hsa_signal_destroy(a->rsig);
-    // A timed-out (or still queued) packet may still write the buffers: leak them.
-    if (!a->broken && !a->read_inflight) {
-      if (!orphan_pending && a->cmd_buf) hsa_amd_memory_pool_free(a->cmd_buf);
-      if (!orphan_pending && a->out_buf) hsa_amd_memory_pool_free(a->out_buf);
-      if (a->rcmd_buf) hsa_amd_memory_pool_free(a->rcmd_buf);
-      if (a->rout_buf) hsa_amd_memory_pool_free(a->rout_buf);
+    // A timed-out (or still queued, or abandoned and never run) packet may still write the
+    // buffers: the read machine marks such a GPU broken at its stop, and they are leaked.
+    if (!a->broken) {
+      a->close_rescue();
+      if (a->cmd_buf) hsa_amd_memory_pool_free(a->cmd_buf);
+      if (a->out_buf) hsa_amd_memory_pool_free(a->out_buf);
+    } else {
+      if (a->rq) hsa_queue_destroy(a->rq);
+      if (a->rsig.handle) hsa_signal_destroy(a->rsig);
     }
     delete a;
   }
@@ -1076,6 +757,26 @@ void teardown_locked() {
   g_hsa_up = false;
 }
 
+// Read-machine settings from the environment (docs/CONFIG.md "PMC read machine").
+gpuexp_pmc::MachineConfig machine_config(ReadMode mode) {
+  gpuexp_pmc::MachineConfig c;
+  c.mode = mode;
+  c.interval_ms = g_interval_ms;
+  c.inline_rounds = g_inline;
+  const char* e = std::getenv("GPUEXP_PMC_READ_RESCUE");
+  c.rescue = !(e && e[0] == '0');
+  if (const char* r = std::getenv("GPUEXP_PMC_REARM")) {
+    const std::string v = r;
+    c.rearm.mode = v == "off" || v == "0" ? gpuexp_ctr::kRearmOff
+                   : v == "now"           ? gpuexp_ctr::kRearmNow
+                                          : gpuexp_ctr::kRearmBackoff;
+  }
+  if (const char* b = std::getenv("GPUEXP_PMC_REARM_BACKOFF_MS")) {
+    const long ms = std::strtol(b, nullptr, 10);
+    if (ms > 0) c.rearm.base_ns = int64_t(ms) * 1000000ll;
+  }
+  return c;
+}
 
 // ---------------------------------------------------------------------------------------
 // Sentinel on the counters' queue.  Every GPU queue pins a context save/restore area sized
@@ -1339,47 +1040,20 @@ extern "C" __attribute__((visibility("default"))) void gpuexp_rp_set_continuous(
 }
 
 extern "C" __attribute__((visibility("default"))) void gpuexp_rp_kick() {
-  if (g_continuous && g_inline) {  // post the round's reads from the caller (no wake-up)
-    g_last_kick_ns.store(uint64_t(
-        std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count()));
-    std::lock_guard<std::mutex> rl(g_round_mu);
-    if (g_live) post_round(g_round);
-    return;
-  }
-  {
-    std::lock_guard<std::mutex> lk(g_cv_mu);
-    ++g_kick_seq;
-  }
-  g_cv.notify_all();
+  if (auto* m = g_machine.load()) m->kick();
 }
 
-// CPU time the counting thread has used so far (charged to the engine's sampler account).
-extern "C" __attribute__((visibility("default"))) uint64_t gpuexp_rp_cpu_ns() { return g_thread_cpu_ns.load(); }
+// CPU time the counting thread (continuous) or duty thread has used so far (charged to the
+// engine's sampler account).
+extern "C" __attribute__((visibility("default"))) uint64_t gpuexp_rp_cpu_ns() {
+  auto* m = g_machine.load();
+  return g_continuous && m ? m->thread_cpu_ns() : g_thread_cpu_ns.load();
+}
 
 // Waits up to `timeout_us` for the round of the last kick; 0 = done, 1 = timed out.
 extern "C" __attribute__((visibility("default"))) int gpuexp_rp_sync(int timeout_us) {
-  if (!g_continuous) return 0;  // duty windows (incl. the fallback): nothing per tick to wait for
-  if (g_inline) {  // collect the reads posted at the kick (normally complete by now)
-    {
-      std::lock_guard<std::mutex> rl(g_round_mu);
-      if (!g_live || !g_round.open) return 0;
-      if (finish_round(g_round, Clock::now() + std::chrono::microseconds(std::max(0, timeout_us)),
-                       /*final=*/false))
-        return 0;
-    }
-    g_leftover_flag.store(true);
-    {
-      std::lock_guard<std::mutex> lk(g_cv_mu);  // (no lost wake-up against the thread's wait)
-    }
-    g_cv.notify_all();
-    return 1;
-  }
-  std::unique_lock<std::mutex> lk(g_cv_mu);
-  const uint64_t want = g_kick_seq;
-  return g_done_cv.wait_for(lk, std::chrono::microseconds(std::max(0, timeout_us)),
-                            [&] { return g_done_seq >= want || g_quit.load(); })
-             ? 0
-             : 1;
+  auto* m = g_machine.load();
+  return m ? m->sync(timeout_us) : 0;
 }
 
 extern "C" __attribute__((visibility("default"))) int gpuexp_rp_init(int ndev, const char* const* bdfs, char* err,
@@ -1463,29 +1137,24 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_init(int ndev, c
       g_continuous = false;
       g_window_ms = std::max(1, std::min(20, g_interval_ms / 2));
     }
-    if (g_continuous) ok = 0;
-    for (Agent* a : g_agents) {
-      if (!g_continuous || !usable(a)) continue;
-      if (arm_continuous(*a)) ++ok;
-      else a->broken = true;
-    }
+  }
+  if (const char* e = std::getenv("GPUEXP_PMC_INLINE")) g_inline = e[0] != '0';
+  auto* m = new gpuexp_pmc::RoundMachine(machine_config(g_continuous ? g_read_mode : kReadUnknown));
+  for (Agent* a : g_agents) m->add(usable(a) ? a : nullptr, a ? a->model : Derived{});
+  if (g_continuous) {
+    ok = 0;
+    for (int d = 0; d < ndev; ++d)
+      if (usable(g_agents[size_t(d)]) && m->arm_sync(d)) ++ok;
     if (!ok) {
+      delete m;
       teardown_locked();
       return fail("continuous counting: start/read packets did not complete");
     }
   }
   g_quit.store(false);
-  {
-    std::lock_guard<std::mutex> lk(g_cv_mu);
-    g_kick_seq = g_done_seq = 0;
-  }
-  if (const char* e = std::getenv("GPUEXP_PMC_INLINE")) g_inline = e[0] != '0';
-  g_thread = std::thread(counting_loop);
-  {
-    std::lock_guard<std::mutex> rl(g_round_mu);
-    g_round = Round{};
-    g_live = true;
-  }
+  g_machine.store(m);
+  if (g_continuous) m->start();
+  else g_thread = std::thread(duty_loop, m);
   g_status = "aqlprofile PMC on " + std::to_string(ok) + " GPU(s), " +
              (g_continuous ? std::string("continuous (one read per tick; read packets: ") +
                                  read_mode_name(g_read_mode) + (g_inline ? "; rounds run by the sampler" : "") + ")"
@@ -1495,42 +1164,25 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_init(int ndev, c
 }
 
 extern "C" __attribute__((visibility("default"))) int gpuexp_rp_sample(int dev, double, double* out) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (dev < 0 || size_t(dev) >= g_agents.size() || !g_agents[size_t(dev)]) return -1;
-  Agent& a = *g_agents[size_t(dev)];
-  std::lock_guard<std::mutex> mk(a.m_mu);
-  if (!a.m.valid || a.broken) return -1;
-  // continuous: a GPU whose reads have been stuck for 2 fallback intervals (4 ticks) has no
-  // current window; exporting the last one as current would be wrong
-  if (g_continuous && Clock::now() - a.t_window_end > std::chrono::milliseconds(2 * g_interval_ms)) return -1;
-  std::memcpy(out, a.m.latest, sizeof(a.m.latest));
-  return 0;
+  auto* m = g_machine.load();
+  return m ? m->sample(dev, out) : -1;
 }
 
 // Per-XCC MFMA busy of the window gpuexp_rp_sample returns: fills out[0..n) and returns n
 // (the GPU's XCC count), or 0 when the samples' XCC coordinates are unknown / no window.
 extern "C" __attribute__((visibility("default"))) int gpuexp_rp_sample_xcc(int dev, double* out, int max) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (dev < 0 || size_t(dev) >= g_agents.size() || !g_agents[size_t(dev)] || max <= 0) return 0;
-  Agent& a = *g_agents[size_t(dev)];
-  std::lock_guard<std::mutex> mk(a.m_mu);
-  if (!a.m.valid || a.broken) return 0;
-  if (g_continuous && Clock::now() - a.t_window_end > std::chrono::milliseconds(2 * g_interval_ms)) return 0;
-  const int n = std::min(max, a.m.nxcc);
-  for (int x = 0; x < n; ++x) out[x] = a.m.xcc_busy[x];
-  return n;
+  auto* m = g_machine.load();
+  return m ? m->sample_xcc(dev, out, max) : 0;
 }
 
 extern "C" __attribute__((visibility("default"))) void gpuexp_rp_shutdown() {
-  {
-    std::lock_guard<std::mutex> rl(g_round_mu);  // no inline round from here on
-    g_live = false;
-  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto* m = g_machine.exchange(nullptr);
+  if (m) m->stop();  // joins the counting thread, stops counting (bounded)
   g_quit.store(true);
   g_cv.notify_all();
-  g_done_cv.notify_all();
   if (g_thread.joinable()) g_thread.join();
-  std::lock_guard<std::mutex> lk(g_mu);
+  delete m;
   teardown_locked();
   g_status = "shut down";
 }
@@ -1540,68 +1192,36 @@ extern "C" __attribute__((visibility("default"))) const char* gpuexp_rp_status()
 // Read health of one GPU (gpuexp::CounterHealth order): stalls, resets, rearms, rescues,
 // rescue releases, rescue active.  0, or -1 for an unknown device.
 extern "C" __attribute__((visibility("default"))) int gpuexp_rp_health(int dev, uint64_t* out, int n) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (dev < 0 || size_t(dev) >= g_agents.size() || !g_agents[size_t(dev)] || n < 6) return -1;
-  const Agent& a = *g_agents[size_t(dev)];
-  out[0] = a.stalls.load();
-  out[1] = a.resets.load();
-  out[2] = a.rearms.load();
-  out[3] = a.rescues.load();
-  out[4] = a.releases.load();
-  out[5] = a.rescued.load() ? 1 : 0;
+  auto* m = g_machine.load();
+  gpuexp_pmc::Health h;
+  if (!m || n < 6 || !m->health(dev, &h)) return -1;
+  out[0] = h.stalls;
+  out[1] = h.resets;
+  out[2] = h.rearms;
+  out[3] = h.rescues;
+  out[4] = h.releases;
+  out[5] = h.rescue_active ? 1 : 0;
   return 0;
 }
 
 extern "C" __attribute__((visibility("default"))) int gpuexp_rp_scope(int dev) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (dev < 0 || size_t(dev) >= g_agents.size() || !g_agents[size_t(dev)]) return -1;
-  std::lock_guard<std::mutex> mk(g_agents[size_t(dev)]->m_mu);
-  return g_agents[size_t(dev)]->m.scope;
+  auto* m = g_machine.load();
+  return m ? m->scope(dev) : -1;
 }
 
 // Diagnostics: the reduced value and instance count of every counter in the last window,
 // as "NAME=value/instances;..." (used by tools/gpu_features_check.py).
 extern "C" __attribute__((visibility("default"))) int gpuexp_rp_debug(int dev, char* buf, int len) {
   std::lock_guard<std::mutex> lk(g_mu);
-  if (dev < 0 || size_t(dev) >= g_agents.size() || !g_agents[size_t(dev)]) return -1;
+  auto* m = g_machine.load();
+  if (!m || dev < 0 || size_t(dev) >= g_agents.size() || !g_agents[size_t(dev)]) return -1;
   Agent& a = *g_agents[size_t(dev)];
-  std::lock_guard<std::mutex> mk(a.m_mu);
-  char win[64];
-  std::snprintf(win, sizeof(win), "%.6f", a.last_window_s);
-  std::string s = "backend=aqlprofile;events=" + std::to_string(a.events.size()) +
-                  ";samples=" + std::to_string(a.last_samples) + ";windows=" + std::to_string(a.m.windows) +
-                  ";simd=" + std::to_string(a.m.simd) + ";cu=" + std::to_string(a.m.cu) +
-                  ";mode=" + (g_continuous ? read_mode_name(g_read_mode) : "duty") + ";window_s=" + win +
-                  ";resets=" + std::to_string(a.resets.load()) + ";stalls=" + std::to_string(a.stalls.load()) +
-                  ";rescued=" + (a.rescues.load() ? "1" : "0") +
-                  ";rescue_active=" + (a.rescued.load() ? "1" : "0") + ";rescues=" + std::to_string(a.rescues.load()) +
-                  ";rescue_releases=" + std::to_string(a.releases.load()) + ";rearms=" + std::to_string(a.rearms.load()) +
-                  ";";
-  if (const uint64_t r = g_rounds.load()) {
-    char c[160];
-    std::snprintf(c, sizeof(c), "rounds=%llu;round_cpu_us_post=%.2f;round_cpu_us_wait=%.2f;round_cpu_us_collect=%.2f;",
-                  (unsigned long long)r, g_round_cpu[0] / 1e3 / r, g_round_cpu[1] / 1e3 / r, g_round_cpu[2] / 1e3 / r);
-    s += c;
+  std::string s = "backend=aqlprofile;events=" + std::to_string(a.events.size()) + ";" + m->debug(dev);
+  {
+    std::lock_guard<std::mutex> dk(a.dbg_mu);
+    s += "coords=" + a.coord_names + ";";
+    if (!a.last_xsamples.empty()) s += a.last_xsamples + ";";
   }
-  if (g_continuous && g_read_mode == kCumulative) {
-    char c[160];
-    std::snprintf(c, sizeof(c), "cum_MFMA=%.0f;cum_GRBM_COUNT=%.0f;cum_GUI=%.0f;", a.pub_cum[kMfma],
-                  a.pub_cum[kGrbmCount], a.pub_cum[kGuiActive]);
-    s += c;
-  }
-  for (int k = 0; k < kNumCtr; ++k) {
-    char t[128];
-    std::snprintf(t, sizeof(t), "%s=%.0f/%d;", name(k), a.last_raw[k], a.last_inst[k]);
-    s += t;
-  }
-  s += "coords=" + a.coord_names + ";nxcc=" + std::to_string(a.m.nxcc) + ";xcc_busy=";
-  for (int x = 0; x < a.m.nxcc; ++x) {
-    char t[32];
-    std::snprintf(t, sizeof(t), "%s%.2f", x ? "," : "", a.m.xcc_busy[x]);
-    s += t;
-  }
-  s += ";";
-  if (!a.last_xsamples.empty()) s += a.last_xsamples + ";";
   std::snprintf(buf, size_t(len), "%s", s.c_str());
   return 0;
 }

@@ -193,6 +193,58 @@ inline WindowAction window_action(const double* d, bool first, double wall, int*
   return first ? kSkip : kPublish;
 }
 
+// Re-arming after a foreign reset (pmc_rounds.cc).  The PMC selects are chip state: another
+// profiler on the GPU (rocprofv3, omniperf) that programs them also resets ours, and
+// re-programming them at once would silently corrupt ITS session.  So the exporter does not
+// fight: after a reset its windows are withheld (the counter families go absent, the health
+// counter `reset` rises) and it re-arms only once the counters have been left alone for a
+// back-off that doubles with every further reset it sees (another profiler resets them per
+// dispatch or per session), up to max_ns.  Counters that merely stopped (GRBM_COUNT standing
+// still: the other profiler finished) do not extend the back-off.  A reset soon after our own
+// re-arm doubles it too; a re-arm calm_ns after the last one starts from base_ns again.
+// GPUEXP_PMC_REARM: backoff (default) | off (never re-arm: withheld until restart) | now
+// (re-arm at the first reset, the round-4 behaviour).
+enum RearmMode { kRearmOff = 0, kRearmBackoff = 1, kRearmNow = 2 };
+struct RearmConfig {
+  RearmMode mode = kRearmBackoff;
+  int64_t base_ns = 2000000000ll;     // first back-off (GPUEXP_PMC_REARM_BACKOFF_MS)
+  int64_t max_ns = 64000000000ll;
+  int64_t calm_ns = 300000000000ll;
+};
+struct RearmState {
+  bool waiting = false;     // counters not ours since a reset: windows withheld, re-arm pending
+  int64_t due_ns = 0;       // when to re-arm (while waiting)
+  int64_t backoff_ns = 0;   // current back-off (0: not set yet = base)
+  int64_t last_arm_ns = 0;  // when counting was last (re)armed by us (0: never)
+  uint64_t conflicts = 0;   // resets that extended the back-off
+};
+
+// A window said the counters were reset (backwards) or stopped (!backwards) under us.
+inline void rearm_on_reset(RearmState& s, const RearmConfig& c, int64_t now, bool backwards) {
+  if (s.backoff_ns <= 0 || (!s.waiting && s.last_arm_ns && now - s.last_arm_ns > c.calm_ns)) s.backoff_ns = c.base_ns;
+  if (!s.waiting) {
+    s.waiting = true;
+    if (backwards && s.last_arm_ns && now - s.last_arm_ns < 2 * s.backoff_ns) {  // right after our re-arm
+      s.backoff_ns = std::min(2 * s.backoff_ns, c.max_ns);
+      ++s.conflicts;
+    }
+    s.due_ns = c.mode == kRearmNow ? now : now + s.backoff_ns;
+    return;
+  }
+  if (backwards) {  // reset again while we wait: someone is using the counters; wait longer
+    ++s.conflicts;
+    s.backoff_ns = std::min(2 * s.backoff_ns, c.max_ns);
+    s.due_ns = c.mode == kRearmNow ? now : now + s.backoff_ns;
+  }
+}
+inline bool rearm_due(const RearmState& s, const RearmConfig& c, int64_t now) {
+  return s.waiting && c.mode != kRearmOff && now >= s.due_ns;
+}
+inline void rearm_done(RearmState& s, int64_t now) {
+  s.waiting = false;
+  s.last_arm_ns = now;
+}
+
 // Per-XCC MFMA busy: the chip formula with one XCC's share of the SIMDs.  mfma[x] sums that
 // XCC's SQ instances (one per SE), grbm[x] is that XCC's own GRBM_COUNT.  Each XCD runs its
 // own clock (DPM lowers a busy XCD's clock while idle ones stay high), so busy cycles are

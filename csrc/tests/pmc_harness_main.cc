@@ -1,0 +1,100 @@
+// The PMC read machine (csrc/gpuexp/pmc_rounds.h) on 8 scripted fake GPUs, run under TSan and
+// ASan+UBSan by the CMake presets (tests/test_sanitizers.py).  One machine runs inline rounds
+// (the sampler thread kicks and syncs, the counting thread follows leftovers) and a second one
+// runs thread-mode rounds, both at once, each with a concurrent reader.  Per GPU the script is:
+//   0 healthy            1 slow (reads outlive every sync: the leftover hand-off)
+//   2 one foreign reset  3 queue 0 stuck for 30 ticks (rescue -> probation -> release)
+//   4 another profiler resetting 4 times (back-off doubles; one re-arm)
+//   5 someone else stops counting   6 queue error   7 reads complete during the sync wait
+// Exit status 0 when every invariant holds; each violation is printed.
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <thread>
+
+#include "gpuexp/pmc_fake.h"
+
+using namespace gpuexp_pmc;
+
+static HarnessConfig combined(bool inline_rounds, int scale) {
+  HarnessConfig c;
+  c.gpus = 8;
+  c.tick_us = 20000 * scale;
+  c.ticks = 90;
+  c.work_us = 300;
+  c.sync_us = 1000;
+  c.inline_rounds = inline_rounds;
+  c.machine.rearm.base_ns = 100000000ll * scale;
+  c.machine.log = false;
+  const int64_t ms = 1000 * scale;
+  c.scripts.resize(8);
+  c.scripts[1].latency_us = 3000;
+  c.scripts[2].resets = {300 * ms};
+  c.scripts[3].stalls = {{200 * ms, 800 * ms}};
+  c.scripts[4].resets = {300 * ms, 350 * ms, 400 * ms, 450 * ms};
+  c.scripts[5].stops = {{300 * ms, -1}};
+  c.scripts[6].queue_error_at = 500 * ms;
+  c.scripts[7].latency_us = 400;
+  return c;
+}
+
+static int check(const char* name, const HarnessOutcome& o) {
+  int bad = 0;
+  auto fail = [&](int gpu, const std::string& what) {
+    std::fprintf(stderr, "[%s] gpu %d: %s\n", name, gpu, what.c_str());
+    ++bad;
+  };
+  if (!o.armed_all) fail(-1, "init arm failed");
+  for (int i = 0; i < int(o.gpus.size()); ++i) {
+    const GpuOutcome& g = o.gpus[size_t(i)];
+    if (g.double_collected) fail(i, "a read collected twice");
+    if (g.misuse) fail(i, "rescue queue misuse (double open/close or a post on a closed queue)");
+    if (g.rescue_opened != g.rescue_closed || g.rescue_open_at_end) fail(i, "rescue queue left behind");
+    const int allowed_uncollected = (i == 3 || i == 6) ? 1 : 0;  // the abandoned read / the failed queue's
+    if (g.uncollected > allowed_uncollected) fail(i, "completed reads never collected: " + std::to_string(g.uncollected));
+    if (i != 6 && g.bad_windows) fail(i, "windows with wrong rates: " + std::to_string(g.bad_windows));
+  }
+  auto& g2 = o.gpus[2];
+  if (g2.health.resets != 1 || g2.health.rearms != 1 || g2.arms != 1) fail(2, "foreign reset: want 1 reset, 1 re-arm");
+  auto& g3 = o.gpus[3];
+  if (g3.health.rescues != 1 || g3.health.releases != 1 || g3.health.stalls < 3) fail(3, "stuck queue: want 1 rescue, 1 release");
+  auto& g4 = o.gpus[4];
+  if (g4.health.rearms != 1 || g4.arms != 1 || g4.health.conflicts != 3) fail(4, "profiler: want 1 re-arm after 3 back-off doublings");
+  auto& g5 = o.gpus[5];
+  if (g5.health.resets != 1 || g5.health.rearms != 1) fail(5, "stopped counters: want 1 re-arm");
+  if (!o.gpus[6].health.broken) fail(6, "queue error not seen");
+  // healthy GPUs: a window per tick (a few ticks may see two and the next none: scheduling)
+  for (int i : {0, 1, 7}) {
+    const GpuOutcome& g = o.gpus[size_t(i)];
+    if (g.windows + 3 < uint64_t(o.ticks) || g.fresh_ticks < o.ticks * 9 / 10)
+      fail(i, "healthy GPU missed windows: " + std::to_string(g.windows) + " windows, " +
+                  std::to_string(g.fresh_ticks) + " fresh ticks");
+  }
+  return bad;
+}
+
+int main(int argc, char** argv) {
+  const int scale = argc > 1 ? std::max(1, std::atoi(argv[1])) : 1;  // slower ticks under sanitizers
+  HarnessOutcome a, b;
+  std::thread ti([&] { a = run_pmc_harness(combined(true, scale), 0.3); });
+  std::thread tt([&] { b = run_pmc_harness(combined(false, scale), 0.3); });
+  ti.join();
+  tt.join();
+  const int bad = check("inline", a) + check("thread", b);
+  for (auto* o : {&a, &b})
+    std::printf("%s: ticks %d late_syncs %d max_sync_us %lld reader_calls %llu\n", o == &a ? "inline" : "thread",
+                o->ticks, o->late_syncs, (long long)o->max_sync_us, (unsigned long long)o->reader_calls);
+  for (auto* o : {&a, &b})
+    for (size_t i = 0; i < o->gpus.size(); ++i) {
+      const GpuOutcome& g = o->gpus[i];
+      std::printf("  %s gpu %zu: windows %llu fresh %d worst_rate_err %.3f lateness %lld us stalls %llu resets %llu "
+                  "rearms %llu rescues %llu releases %llu conflicts %llu broken %d uncollected %d\n",
+                  o == &a ? "inline" : "thread", i, (unsigned long long)g.windows, g.fresh_ticks, g.worst_rate_err,
+                  (long long)g.max_lateness_us, (unsigned long long)g.health.stalls,
+                  (unsigned long long)g.health.resets, (unsigned long long)g.health.rearms,
+                  (unsigned long long)g.health.rescues, (unsigned long long)g.health.releases,
+                  (unsigned long long)g.health.conflicts, int(g.health.broken), g.uncollected);
+    }
+  std::printf("%s\n", bad ? "FAIL" : "OK");
+  return bad ? 1 : 0;
+}

@@ -1,6 +1,10 @@
 """Host-side sanitizer runs of the core: CMake presets tsan / asan build the
-static core + the concurrency stress driver (sampler 100 Hz x 8 mock GPUs, 2 HTTP loops,
-4 keep-alive scrapers incl. gzip, control-plane churn) and run it for 3 s."""
+static core + two drivers and run them:
+  * gpuexp_stress: sampler 100 Hz x 8 mock GPUs, 2 HTTP loops, 4 keep-alive scrapers incl.
+    gzip, control-plane churn, for 3 s;
+  * gpuexp_pmc_harness: the aqlprofile plugin's read machine (pmc_rounds.cc) on 8 scripted fake
+    GPUs (slow, stuck -> rescue -> release, foreign resets, another profiler, stopped counters,
+    queue error), an inline-round machine and a thread-mode one at once, each with a reader."""
 import os
 import shutil
 import subprocess
@@ -28,3 +32,11 @@ def test_stress_under_sanitizer(preset, env):
     assert r.returncode == 0, out[-5000:]
     assert "WARNING: ThreadSanitizer" not in out and "ERROR: AddressSanitizer" not in out
     assert "runtime error" not in out  # UBSan
+    # the PMC read machine's invariants, at 3x slower ticks (sanitizer overhead)
+    r = subprocess.run([os.path.join(ROOT, f"build/cmake-{preset}/gpuexp_pmc_harness"), "3"],
+                       env=dict(os.environ, **env), capture_output=True, text=True, timeout=120)
+    out = r.stdout + r.stderr
+    print(out[-3000:])
+    assert r.returncode == 0 and out.rstrip().endswith("OK"), out[-5000:]
+    assert "WARNING: ThreadSanitizer" not in out and "ERROR: AddressSanitizer" not in out
+    assert "runtime error" not in out
