@@ -9,6 +9,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstring>
 #include <set>
@@ -792,6 +793,8 @@ void Engine::emit_kfd_events(uint64_t gen) {
     // gone from a complete list, or from every partial one for the TTL: drop
     const std::pair<std::string, std::string> pk{std::get<0>(k), std::get<1>(k)};
     auto lk = pod_last_known_ns_.find(pk);
+    if (lk == pod_last_known_ns_.end() && !live.count(pk))  // never listed yet: the TTL starts now
+      lk = pod_last_known_ns_.emplace(pk, mono_ns()).first;
     const bool expired = lk != pod_last_known_ns_.end() && mono_ns() - lk->second > uint64_t(cfg_.pod_totals_ttl_s * 1e9);
     if (!live.count(pk) && (pods_complete_ || expired)) {
       it = pod_kfd_events_.erase(it);
@@ -1521,9 +1524,15 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
       table_.put(f_pod_busy_s_, {it->first.first, it->first.second}, it->second.second, gen);
       ++it;
     }
+    // a pod's stamp lives while any of its totals does (KFD event counts included: they expire
+    // in emit_kfd_events against the same stamp)
+    auto has_kfd = [&](const std::pair<std::string, std::string>& k) {
+      auto kt = pod_kfd_events_.lower_bound(std::make_tuple(k.first, k.second, INT_MIN));
+      return kt != pod_kfd_events_.end() && std::get<0>(kt->first) == k.first && std::get<1>(kt->first) == k.second;
+    };
     for (auto it = pod_last_known_ns_.begin(); it != pod_last_known_ns_.end();)
       it = !known.count(it->first) && !pod_energy_j_.count(it->first) && !pod_xgmi_.count(it->first) &&
-                   !pod_gpu_s_.count(it->first)
+                   !pod_gpu_s_.count(it->first) && !has_kfd(it->first)
                ? pod_last_known_ns_.erase(it)
                : std::next(it);
   }

@@ -358,7 +358,12 @@ const CgroupInfo* PidResolver::resolve(int pid) {
     }
     uint64_t st = 0;
     const bool have_st = read_starttime(pid, &st);
-    if (alive && (!have_st || e.starttime == st)) {
+    if (!have_st || e.starttime == st) {
+      // Same process (its start time matches), or /proc/<pid> is gone: the process exited (its
+      // comm read fails with ESRCH).  A PID whose /proc entry does not exist cannot have been
+      // reused, so the cached attribution still names it -- count_kfd_events attributes the VM
+      // fault of a process that fault killed (engine.cc) -- until gc() drops it with the PID.
+      // Never replaced by a failed lookup.
       e.epoch = epoch_;
       e.st_checked_ns = now_ns_;
       return &e.info;

@@ -159,34 +159,43 @@ bool build_config(Agent& a, std::string* why) {
         return ROCPROFILER_STATUS_SUCCESS;
       },
       &all);
-  std::vector<rocprofiler_counter_id_t> use;
-  for (auto& c : all) {
-    rocprofiler_counter_info_v0_t info{};
-    if (rocprofiler_query_counter_info(c, ROCPROFILER_COUNTER_INFO_VERSION_0, &info) != ROCPROFILER_STATUS_SUCCESS)
-      continue;
-    for (int k = 0; k < kNumCtr; ++k)
-      if (info.name && std::strcmp(info.name, name(k)) == 0) {
-        use.push_back(c);
-        a.counter_slot[c.handle] = k;
-      }
+  // The SPI occupancy-limiter counters are the newest addition: when the config cannot hold
+  // them (or GPUEXP_PMC_NO_SPI=1), count without them rather than lose every counter -- the
+  // same fallback as aql_pmc.cc's setup_agent.
+  const char* no_spi = std::getenv("GPUEXP_PMC_NO_SPI");
+  for (int attempt = (no_spi && no_spi[0] == '1') ? 1 : 0; attempt < 2; ++attempt) {
+    std::vector<rocprofiler_counter_id_t> use;
+    a.counter_slot.clear();
+    for (auto& c : all) {
+      rocprofiler_counter_info_v0_t info{};
+      if (rocprofiler_query_counter_info(c, ROCPROFILER_COUNTER_INFO_VERSION_0, &info) != ROCPROFILER_STATUS_SUCCESS)
+        continue;
+      for (int k = 0; k < kNumCtr; ++k)
+        if (info.name && std::strcmp(info.name, name(k)) == 0 && !(attempt == 1 && std::strncmp(info.name, "SPI_", 4) == 0)) {
+          use.push_back(c);
+          a.counter_slot[c.handle] = k;
+        }
+    }
+    if (use.empty()) {
+      *why = "agent supports none of the requested counters";
+      return false;
+    }
+    size_t nrec = 0;
+    for (auto& c : use) {
+      rocprofiler_counter_info_v1_t info{};
+      if (rocprofiler_query_counter_info(c, ROCPROFILER_COUNTER_INFO_VERSION_1, &info) == ROCPROFILER_STATUS_SUCCESS)
+        nrec += info.dimensions_instances_count;
+    }
+    if (rocprofiler_create_counter_config(a.id, use.data(), use.size(), &a.cfg) == ROCPROFILER_STATUS_SUCCESS) {
+      if (attempt == 1 && !(no_spi && no_spi[0] == '1'))
+        std::fprintf(stderr, "[rocprof] the counter config cannot hold the SPI events; counting without them\n");
+      a.have_cfg = true;
+      a.recs.resize(nrec + 64);
+      return true;
+    }
   }
-  if (use.empty()) {
-    *why = "agent supports none of the requested counters";
-    return false;
-  }
-  size_t nrec = 0;
-  for (auto& c : use) {
-    rocprofiler_counter_info_v1_t info{};
-    if (rocprofiler_query_counter_info(c, ROCPROFILER_COUNTER_INFO_VERSION_1, &info) == ROCPROFILER_STATUS_SUCCESS)
-      nrec += info.dimensions_instances_count;
-  }
-  if (rocprofiler_create_counter_config(a.id, use.data(), use.size(), &a.cfg) != ROCPROFILER_STATUS_SUCCESS) {
-    *why = "create_counter_config failed (slot limits?)";
-    return false;
-  }
-  a.have_cfg = true;
-  a.recs.resize(nrec + 64);
-  return true;
+  *why = "create_counter_config failed (slot limits?)";
+  return false;
 }
 
 }  // namespace

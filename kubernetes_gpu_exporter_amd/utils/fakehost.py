@@ -203,10 +203,15 @@ class FakeHost:
 
     # ---- processes ----
     def add_process(self, pid: int, cgroup: str, comm: str = "python3", gpus: dict | None = None,
-                    starttime: int = 1000) -> None:
-        """gpus: {gpu_id: (vram_bytes, cu_occupancy)}"""
+                    starttime: int = 1000, comm_readable: bool = True) -> None:
+        """gpus: {gpu_id: (vram_bytes, cu_occupancy)}.  comm_readable=False makes reads of the
+        process's comm fail the way they do once it has exited (ESRCH on an open fd): the fake's
+        comm is a directory, which opens but fails every read (an unlinked file stays readable)."""
         self._w(f"proc/{pid}/cgroup", f"0::{cgroup}\n")
-        self._w(f"proc/{pid}/comm", comm + "\n")
+        if comm_readable:
+            self._w(f"proc/{pid}/comm", comm + "\n")
+        else:
+            (self.root / f"proc/{pid}/comm").mkdir(parents=True, exist_ok=True)
         fields = ["S"] + ["0"] * 18 + [str(starttime)] + ["0"] * 10
         self._w(f"proc/{pid}/stat", f"{pid} ({comm}) " + " ".join(fields) + "\n")
         for gid, (vram, cu) in (gpus or {}).items():

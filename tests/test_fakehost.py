@@ -797,3 +797,26 @@ def test_sampler_cpu_scales_at_most_linearly_to_8_gpus(native, tmp_path):
     assert t1 >= 15 and t8 >= 15
     assert eight <= 8 * one * 1.25, (one, eight)
     assert eight < 2000, eight
+
+
+def test_vm_fault_of_an_exited_process_keeps_its_pod(native, mock_engine, tmp_path):
+    """A process killed by its own VM fault is gone (no /proc/<pid>, comm reads fail) by the time
+    the fault event is counted; the resolver's cached attribution must still name its pod (a PID
+    whose /proc entry does not exist cannot have been reused), not be replaced by a failed lookup.
+    (Mock devices, since KFD events need /dev/kfd; the PID -> cgroup walk reads the fake /proc.)"""
+    h = FakeHost(tmp_path)
+    h.add_process(4242, kubepods_cgroup(UID, CID), comm_readable=False)
+    e = mock_engine(1, series_profile="full", host_root=str(tmp_path))
+    e.set_pods([dict(uid=UID, namespace="ml", name="trainer-0", containers={CID: "main"})])
+    e.mock_set_processes(0, [{"pid": 4242, "vram_bytes": 1 << 30, "cu_occupancy": 8, "name": "python3"}])
+    e.tick(S)
+    e.tick(S + S // 10)  # alive: comm unreadable, but the start time matches -> cached
+    assert promtext.value(promtext.parse(e.snapshot_text()), "pod_gpu_memory_usage", pid=4242) == 1 << 30
+    e.mock_set_processes(0, [])
+    h.remove_process(4242)
+    e.inject_kfd_events(0, b"1 1092:python3\n")  # 0x1092 = 4242
+    e.tick(S + 2 * S // 10)
+    fams = promtext.parse(e.snapshot_text())
+    pod = {(s[1]["pod"], s[1]["event"]): s[2] for s in promtext.samples(fams, "amd_pod_gpu_kfd_events_total")}
+    assert pod == {("trainer-0", "vm_fault"): 1}
+    assert 'pid="4242"' not in e.snapshot_text()  # its process series are gone all the same

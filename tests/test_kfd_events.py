@@ -80,3 +80,30 @@ def test_kfd_events_full_profile_only(native, mock_engine):
     off.tick(1_000_000_000)
     assert not promtext.samples(promtext.parse(off.snapshot_text()), "amd_gpu_kfd_events_total")
 
+
+
+def test_pod_kfd_event_totals_expire_under_partial_pod_lists(native, mock_engine):
+    """Per-pod KFD event counts follow the same TTL as the other per-pod totals while every pod
+    refresh is partial: kept for pod_totals_ttl_s after the last list that had the pod, then
+    dropped (not kept for ever once the pod's energy totals expired first)."""
+    import time
+    e = mock_engine(1, series_profile="full", pod_totals_ttl_s=0.5)
+    e.set_pods([{"uid": UID, "namespace": "ml", "name": "gone", "containers": {CID: "main"}}], True)
+    e.set_pid_cgroup(4242, kubepods_cgroup(UID, CID))
+    e.mock_set_processes(0, [{"pid": 4242, "vram_bytes": 1 << 30, "cu_occupancy": 8, "name": "a"}])
+    e.tick(1_000_000_000)
+    e.inject_kfd_events(0, b"1 1092:python3\n")
+    e.tick(1_100_000_000)
+    pod = lambda f: {(s[1]["pod"], s[1]["event"]): s[2] for s in promtext.samples(f, "amd_pod_gpu_kfd_events_total")}
+    assert pod(promtext.parse(e.snapshot_text())) == {("gone", "vm_fault"): 1}
+    e.mock_set_processes(0, [])
+    e.set_pods([], False)  # partial refreshes without the pod: kept ...
+    e.tick(1_200_000_000)
+    assert pod(promtext.parse(e.snapshot_text())) == {("gone", "vm_fault"): 1}
+    time.sleep(0.6)  # ... until no applied list has had the pod for the TTL
+    for t in (1_300_000_000, 1_400_000_000, 1_500_000_000):
+        e.set_pods([], False)
+        e.tick(t)
+    fams = promtext.parse(e.snapshot_text())
+    assert not promtext.samples(fams, "amd_pod_gpu_energy_joules_total")
+    assert pod(fams) == {}

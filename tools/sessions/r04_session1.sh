@@ -2,7 +2,7 @@
 # Round-4 GPU session 1: SPI occupancy-limiter scope probe, read-rescue release + RSS, and the
 # devices-stage A/B under the bench's GEMM pod.  Each step under its own limit; a
 # timeout/abort/segfault stops the session (tools/gpu_session.sh); test failures do not.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/r04
 bash tools/gpu_session.sh \
   "150::python -u tools/probe_spi_scope.py --seconds 2.0 > gpurun_out/r04/spi_scope.log 2>&1; grep -E '^(status|idle|lds_|waves_)' gpurun_out/r04/spi_scope.log" \

@@ -2,7 +2,7 @@
 # Round-4 GPU session 11 (final-tree checks: outlier-robust pre-wake period, PID negative cache, SIGHUP pod-map pickup): GPU tier +
 # smoke, the driver's bench command x3, one 100-step run, and a rocprofv3 kernel trace of the
 # exporter's default path.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/r04s11
 bash tools/gpu_session.sh \
   "500::python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/r04s11/pytest_gpu.log 2>&1; tail -4 gpurun_out/r04s11/pytest_gpu.log" \

@@ -2,7 +2,7 @@
 # Round-4 GPU session 13: the occupancy limiters against VGPR- and SGPR-limited kernels too,
 # then BASELINE configs 1 (mock backend), 2 (1 Hz) and 5 (100 Hz scrape + sample) on the final
 # tree, plus two more driver-form runs.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/r04s13
 bash tools/gpu_session.sh \
   "200::python -u tools/probe_spi_scope.py --seconds 2.0 --no-self --exported --kinds lds,waves,vgpr,sgpr > gpurun_out/r04s13/spi_limiters.log 2>&1; grep -E '^(idle|lds_|waves_|vgpr_|sgpr_)' gpurun_out/r04s13/spi_limiters.log | cut -c1-330" \

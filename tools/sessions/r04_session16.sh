@@ -2,7 +2,7 @@
 # Round-4 GPU session 16 (final-tree checks after the PMC idle-fallback change): GPU tier +
 # smoke, the driver's bench command x3, one 100-step run, and a rocprofv3 kernel trace of the
 # exporter's default path.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/r04s16
 bash tools/gpu_session.sh \
   "600::python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread > gpurun_out/r04s16/pytest_gpu.log 2>&1; tail -4 gpurun_out/r04s16/pytest_gpu.log" \

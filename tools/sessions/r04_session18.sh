@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU session 18: after the KFD reader's re-probe of missing GPUs -- the process and
 # attribution GPU tests, smoke, and the driver's bench command twice.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/r04s18
 bash tools/gpu_session.sh \
   "300::python -u -m pytest tests/test_gpu.py -v --timeout 240 --timeout-method thread -k 'process or pods or exporter_tick or rccl_tracer_through or pod_energy' > gpurun_out/r04s18/pytest_procs.log 2>&1; tail -4 gpurun_out/r04s18/pytest_procs.log" \

@@ -3,7 +3,7 @@
 # the driver-form bench x3, the GPU test tier and smoke, and a rocprofv3 kernel summary of
 # the default exporter path.  Each step under its own limit; a timeout/abort/segfault stops
 # the session (tools/gpu_session.sh).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/r04
 export TMPDIR=/tmp
 bash tools/gpu_session.sh \

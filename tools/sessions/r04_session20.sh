@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU session 20: which runtime allocation is the exporter's 487 MiB of VRAM?  The
 # queue-holding configuration under ROCr settings that move or shrink queue memory.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/r04s20
 P="python -u tools/probe_exporter_vram.py --queue-only"
 bash tools/gpu_session.sh \

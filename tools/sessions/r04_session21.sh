@@ -2,7 +2,7 @@
 # Round-4 GPU session 21: BASELINE config 5 (100 Hz) with the PMC read kicked at the end of the
 # previous tick (counters_kick auto) vs at the tick's start, interleaved; then the driver form
 # (10 Hz: auto = start, unchanged) and the counter GPU tests.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/r04s21
 B="python -u bench.py --sample-hz 100 --scrape-hz 100 --steps 1000 --warmup 100 --identity-phase 0"
 bash tools/gpu_session.sh \

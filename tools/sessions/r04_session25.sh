@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU session 25: the driver's bench command 10 times back to back on one box (the
 # distribution a single end-of-round run draws from).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/r04s25
 steps=()
 for i in $(seq 1 10); do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU session 26: the driver's bench command 10 times on another box, then BASELINE
 # config 5 (100 Hz) twice.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/r04s26
 steps=()
 for i in $(seq 1 10); do

@@ -2,7 +2,7 @@
 # Round-4 GPU session 27: the counter GPU tests with the PMC read forced to the previous tick's
 # end at every rate (GPUEXP_COUNTERS_KICK=end), and with the counting thread running the rounds
 # (GPUEXP_PMC_INLINE=0): the non-default settings stay correct.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/r04s27
 K="counters or calibration or limiters or exporter_tick or devices_stage"
 bash tools/gpu_session.sh \

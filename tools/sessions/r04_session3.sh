@@ -2,7 +2,7 @@
 # Round-4 GPU session 3 (final-tree checks): GPU tier + smoke, the driver's bench command x3
 # (pre-wake from the two newest periods), BASELINE config 2 (1 Hz), config 5 (100 Hz), and
 # config 1 (mock backend) on this box's CPU.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/r04s3
 bash tools/gpu_session.sh \
   "500::python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/r04s3/pytest_gpu.log 2>&1; tail -4 gpurun_out/r04s3/pytest_gpu.log" \

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU session 5: where the exporter's CPU goes per thread on a real box, what one
 # sleep/wake-up costs there, and the exposition body the driver's scrape receives.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/r04s5
 bash tools/gpu_session.sh \
   "60::python -u tools/probe_wakeup_cost.py --seconds 3 > gpurun_out/r04s5/wakeup_cost.log 2>&1; cat gpurun_out/r04s5/wakeup_cost.log" \

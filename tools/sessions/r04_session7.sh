@@ -5,7 +5,7 @@
 #   B  inline PMC rounds
 #   C  inline PMC rounds + HTTP worker following the scraper's receive CPU
 # (3) the unit of KFD's per-process sdma_<id> file (child found by its KFD host PID).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/r04s7
 A="GPUEXP_PMC_INLINE=0 GPUEXP_HTTP_FOLLOW_RX_CPU=0"
 B="GPUEXP_PMC_INLINE=1 GPUEXP_HTTP_FOLLOW_RX_CPU=0"

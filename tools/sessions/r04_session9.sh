@@ -3,7 +3,7 @@
 # under), then the pre-wake A/B at 100 scrapes per run: slices of 150 us (default) / 300 us /
 # pre-wake off, interleaved x2.  First a driver-form run of the tree (bench now signals the
 # exporter after writing its pod map instead of a 0.5 s control-plane poll).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/r04s9
 B="python -u bench.py --gpus 1 --steps 100 --warmup 10 --identity-phase 0"
 bash tools/gpu_session.sh \
