@@ -30,7 +30,7 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("GPUEXP_OFFLOAD_ARCH", "gfx950")
 
 CORE_CC = [
-    "gpuexp/common.cc", "gpuexp/exposition.cc", "gpuexp/gzip.cc", "gpuexp/http.cc",
+    "gpuexp/common.cc", "gpuexp/exposition.cc", "gpuexp/deflate_tmpl.cc", "gpuexp/gzip.cc", "gpuexp/http.cc",
     "gpuexp/gpu_metrics.cc", "gpuexp/backend_mock.cc", "gpuexp/backend_sysfs.cc",
     "gpuexp/backend_amdsmi.cc", "gpuexp/procs.cc", "gpuexp/ras.cc", "gpuexp/kfd_events.cc", "gpuexp/engine.cc",
     "gpuexp/optional_sources.cc", "gpuexp/client.cc", "gpuexp/pmc_rounds.cc", "gpuexp/pmc_harness.cc",

@@ -553,6 +553,18 @@ PYBIND11_MODULE(_gpuexp, m) {
         t.render(&out, gen, gc_after);
         return out;
       }, py::arg("gen"), py::arg("gc_after") = 1)
+      .def("render_compiled", [](SeriesTable& t, uint64_t gen, uint64_t gc_after, bool gzip) {
+        std::string out, gz;
+        t.render_compiled(&out, gzip ? &gz : nullptr, gen, gc_after);
+        return py::make_tuple(out, py::bytes(gz));
+      }, py::arg("gen"), py::arg("gc_after") = 1, py::arg("gzip") = true,
+         "(text, gzip bytes) of the fixed-layout renderer")
+      .def("last_relayouts", &SeriesTable::last_relayouts)
+      .def("code_builds", &SeriesTable::code_builds)
+      .def("set_histogram", [](SeriesTable& t, int fid, std::vector<std::string> labels, std::vector<double> bounds,
+                               std::vector<uint64_t> counts, double sum, uint64_t count, uint64_t gen) {
+        t.set_histogram(t.upsert(fid, labels), bounds, counts, sum, count, gen);
+      })
       .def("live_series", &SeriesTable::live_series);
 
   // --- Engine ---
@@ -625,6 +637,7 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("queue_devices_bdf", &EngineConfig::queue_devices_bdf)
       .def_readwrite("force_amdsmi_metrics", &EngineConfig::force_amdsmi_metrics)
       .def_readwrite("gzip_level", &EngineConfig::gzip_level)
+      .def_readwrite("exposition", &EngineConfig::exposition)
       .def_readwrite("gc_after", &EngineConfig::gc_after)
       .def_readwrite("device_filter", &EngineConfig::device_filter)
       .def_readwrite("device_filter_bdf", &EngineConfig::device_filter_bdf)
@@ -679,6 +692,8 @@ PYBIND11_MODULE(_gpuexp, m) {
         d["device_errors"] = s.device_errors;
         d["sampler_cpu_ns"] = s.sampler_cpu_ns;
         d["gzip_eager"] = s.gzip_eager;
+        d["relayouts"] = s.relayouts;
+        d["code_builds"] = s.code_builds;
         py::dict st;
         for (int k = 0; k < Engine::kStages; ++k) st[Engine::stage_name(k)] = s.stage_ns[k];
         d["stage_ns"] = st;

@@ -461,6 +461,7 @@ bool Engine::start(std::string* err) {
   if (running_.load()) return true;
   RuntimeThreadsName rt_name;
   start_mono_ns_ = mono_ns();
+  compiled_ = cfg_.exposition != "classic";
   counters_kick_mode_ = cfg_.counters_kick != "auto" ? cfg_.counters_kick
                         : (cfg_.interval_s > 0 && cfg_.interval_s < 0.05 ? "end" : "start");
   define_families();
@@ -1903,7 +1904,14 @@ void Engine::tick_locked(uint64_t now) {
   uint64_t rbytes = 0, nseries = 0;
   if (slot >= 0) {
     Snapshot* snap = store_.slot(slot);
-    table_.render(&snap->body, gen, cfg_.gc_after);
+    // gzip copy only when a gzip scrape is expected before the tick after next (or its
+    // schedule is unknown): a 15 s Prometheus scrape costs one compression, not 150
+    const uint64_t period_ns = cfg_.interval_s > 0 ? uint64_t(cfg_.interval_s * 1e9) : 1000000000ull;
+    const bool want_gz = http_ && http_->gzip_due(mono_ns(), 2 * period_ns + 5000000ull);
+    if (want_gz) ++gzip_eager_;
+    snap->gz.clear();
+    if (compiled_) table_.render_compiled(&snap->body, want_gz ? &snap->gz : nullptr, gen, cfg_.gc_after);
+    else table_.render(&snap->body, gen, cfg_.gc_after);
     snap->gen = gen;
     snap->render_ns = now;
     rbytes = snap->body.size();
@@ -1911,17 +1919,11 @@ void Engine::tick_locked(uint64_t now) {
     snap->series = nseries;
     ts[7] = mono_ns();
     cs[7] = thread_cpu_ns();
-    // 7: gzip (only while clients ask for it) + publish
-    snap->gz.clear();
+    // 7: gzip (classic; compiled emitted it with the body) + publish
     snap->pb.clear();
     snap->pb_gz.clear();
     const uint64_t tnow = mono_ns();
-    // gzip copy only when a gzip scrape is expected before the tick after next (or its
-    // schedule is unknown): a 15 s Prometheus scrape costs one compression, not 150
-    const uint64_t period_ns = cfg_.interval_s > 0 ? uint64_t(cfg_.interval_s * 1e9) : 1000000000ull;
-    const bool want_gz = http_ && http_->gzip_due(tnow, 2 * period_ns + 5000000ull);
-    if (want_gz) ++gzip_eager_;
-    if (want_gz) gzip_compress(snap->body, &snap->gz, cfg_.gzip_level);
+    if (want_gz && !compiled_) gzip_compress(snap->body, &snap->gz, cfg_.gzip_level);
     if (http_ && http_->proto_wanted_ns() && tnow - http_->proto_wanted_ns() < 60000000000ull) {
       table_.render_proto(&snap->pb, gen);
       if (want_gz) gzip_compress(snap->pb, &snap->pb_gz, cfg_.gzip_level);
@@ -1986,6 +1988,8 @@ void Engine::tick_locked(uint64_t now) {
     }
     stats_.sampler_cpu_ns += cpu;
     stats_.gzip_eager = gzip_eager_;
+    stats_.relayouts += table_.last_relayouts();
+    stats_.code_builds = table_.code_builds();
   }
 }
 

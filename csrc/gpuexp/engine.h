@@ -131,6 +131,9 @@ struct EngineConfig {
   std::string kfd_path = "/dev/kfd";   // the device node itself (not under host_root)
   bool force_amdsmi_metrics = false;
   int gzip_level = 1;
+  // "compiled": fixed-layout body patched in place, gzip from pre-encoded static bits
+  // (SeriesTable::render_compiled); "classic": re-render changed families, compress the body.
+  std::string exposition = "compiled";
   uint64_t gc_after = 1;               // stale series vanish this many ticks after last seen
   std::vector<int> device_filter;      // empty = all
   std::vector<std::string> device_filter_bdf;  // also accepted: PCI BDFs ("0000:75:00.0")
@@ -167,6 +170,8 @@ struct EngineStats {
   uint64_t stage_cpu_ns[8] = {};  // cumulative sampler-thread CPU per stage (pool / PMC threads not split)
   uint64_t sampler_cpu_ns = 0;
   uint64_t gzip_eager = 0;  // snapshots published with a gzip copy
+  uint64_t relayouts = 0;   // compiled exposition: families laid out again (0 per tick in steady state)
+  uint64_t code_builds = 0; // compiled exposition: Huffman code builds
 };
 
 class Engine {
@@ -283,6 +288,7 @@ class Engine {
   EngineConfig cfg_;
   std::unique_ptr<Backend> backend_;
   MockBackend* mock_ = nullptr;
+  bool compiled_ = true;  // cfg_.exposition == "compiled" (set at start)
   std::vector<DeviceInfo> devices_;
   std::vector<DevState> dstate_;
   std::vector<std::vector<std::string>> owner_keys_;  // per device: device_owner_keys()

@@ -123,6 +123,8 @@ SeriesRef SeriesTable::upsert(int fid, const std::vector<std::string>& values) {
   h.gen = 0;
   h.value = 0;
   h.in_cache = false;
+  h.stamp += 1;
+  s.widths.clear();
   s.labels = values;
   s.key = keybuf_;
   s.bounds.clear();
@@ -161,6 +163,7 @@ bool SeriesTable::set(SeriesRef r, double v, uint64_t gen) {
   std::memcpy(&b, &v, sizeof(b));
   if (a != b) {
     h.value = v;
+    h.stamp += 1;
     mark_dirty(h.fid);
   }
   h.gen = gen;
@@ -191,6 +194,7 @@ bool SeriesTable::observe(SeriesRef r, double v, uint64_t gen, const std::vector
   s.hsum += v;
   s.hcount += 1;
   h.gen = gen;
+  h.stamp += 1;
   mark_dirty(h.fid);
   return true;
 }
@@ -216,7 +220,10 @@ bool SeriesTable::set_histogram(SeriesRef r, const std::vector<double>& bounds,
   s.hsum = sum;
   s.hcount = count;
   h.gen = gen;
-  if (changed) mark_dirty(h.fid);
+  if (changed) {
+    h.stamp += 1;
+    mark_dirty(h.fid);
+  }
   return true;
 }
 
@@ -235,6 +242,8 @@ void SeriesTable::free_series(uint32_t idx) {
   h.fid = -1;
   h.ver += 1;
   h.in_cache = false;
+  h.stamp += 1;
+  s.widths.clear();
   s.labels.clear();
   s.prefix.clear();
   s.line.clear();
@@ -265,7 +274,7 @@ void SeriesTable::sort_members(Family& f) {
   f.dirty = true;
 }
 
-void SeriesTable::append_cached_value(std::string* out, uint32_t idx) {
+void SeriesTable::format_cached(uint32_t idx) {
   Series& s = series_[idx];
   const double v = hot_[idx].value;
   uint64_t bits;
@@ -278,12 +287,14 @@ void SeriesTable::append_cached_value(std::string* out, uint32_t idx) {
     s.vbits = bits;
     s.vvalid = true;
   }
-  out->append(s.vtxt, s.vlen);
 }
 
-void SeriesTable::render_histogram(std::string* out, uint32_t idx) {
-  // name_bucket{labels,le="x"} cumulative ... _sum, _count.  The line prefixes depend only
-  // on the labels and the (fixed) bounds: built once, then each render appends numbers.
+void SeriesTable::append_cached_value(std::string* out, uint32_t idx) {
+  format_cached(idx);
+  out->append(series_[idx].vtxt, series_[idx].vlen);
+}
+
+void SeriesTable::build_hlines(uint32_t idx) {
   Series& s = series_[idx];
   if (s.hlines.size() != s.bounds.size() + 3) {
     const Family& fam = families_[size_t(hot_[idx].fid)];
@@ -307,6 +318,13 @@ void SeriesTable::render_histogram(std::string* out, uint32_t idx) {
       s.hlines.push_back(std::move(l));
     }
   }
+}
+
+void SeriesTable::render_histogram(std::string* out, uint32_t idx) {
+  // name_bucket{labels,le="x"} cumulative ... _sum, _count.  The line prefixes depend only
+  // on the labels and the (fixed) bounds: built once, then each render appends numbers.
+  build_hlines(idx);
+  Series& s = series_[idx];
   char buf[24];
   uint64_t cum = 0;
   for (size_t i = 0; i <= s.bounds.size(); ++i) {
@@ -376,6 +394,191 @@ void SeriesTable::render(std::string* out, uint64_t gen, uint64_t gc_after) {
     }
     out->append(fam.cache);
   }
+}
+
+void SeriesTable::field_texts(uint32_t idx) {
+  const Hot& h = hot_[idx];
+  Series& s = series_[idx];
+  if (families_[size_t(h.fid)].def.type != MetricType::kHistogram) {
+    format_cached(idx);
+    scratch_.resize(32);
+    scratch_len_.assign(1, s.vlen);
+    std::memcpy(scratch_.data(), s.vtxt, s.vlen);
+    return;
+  }
+  const size_t nf = s.bounds.size() + 3;
+  scratch_.resize(32 * nf);
+  scratch_len_.resize(nf);
+  uint64_t cum = 0;
+  auto put_u64 = [&](size_t f, uint64_t v) {
+    auto r = std::to_chars(&scratch_[32 * f], &scratch_[32 * f] + 32, v);
+    scratch_len_[f] = uint8_t(r.ptr - &scratch_[32 * f]);
+  };
+  for (size_t i = 0; i <= s.bounds.size(); ++i) {
+    cum = i < s.bounds.size() ? cum + s.buckets[i] : s.hcount;
+    put_u64(i, cum);
+  }
+  std::string tmp;
+  append_value(&tmp, s.hsum);
+  const size_t fs = s.bounds.size() + 1;
+  scratch_len_[fs] = uint8_t(std::min<size_t>(tmp.size(), 32));
+  std::memcpy(&scratch_[32 * fs], tmp.data(), scratch_len_[fs]);
+  put_u64(fs + 1, s.hcount);
+}
+
+void SeriesTable::layout_family(int fid, uint64_t gen, std::string* body) {
+  Family& fam = families_[size_t(fid)];
+  Layout& L = layouts_[size_t(fid)];
+  L.members.clear();
+  L.vers.clear();
+  L.first_field.clear();
+  L.stamps.clear();
+  L.seg.fields.clear();
+  const size_t base = body->size();
+  body->append(fam.header);
+  const bool hist = fam.def.type == MetricType::kHistogram;
+  for (uint32_t idx : fam.members) {
+    Hot& h = hot_[idx];
+    if (h.gen != gen) continue;
+    Series& s = series_[idx];
+    field_texts(idx);
+    const size_t nf = scratch_len_.size();
+    if (s.widths.size() != nf) s.widths.assign(nf, 0);
+    if (hist) build_hlines(idx);
+    L.members.push_back(idx);
+    L.vers.push_back(h.ver);
+    L.first_field.push_back(uint32_t(L.seg.fields.size()));
+    L.stamps.push_back(h.stamp);
+    for (size_t f = 0; f < nf; ++f) {
+      body->append(hist ? s.hlines[f] : s.line);
+      const uint8_t len = scratch_len_[f];
+      s.widths[f] = std::max(s.widths[f], len);
+      L.seg.fields.push_back({uint32_t(body->size() - base), s.widths[f]});
+      body->append(&scratch_[32 * f], len);
+      body->append(size_t(s.widths[f] - len), ' ');
+      body->push_back('\n');
+    }
+  }
+  L.seg.base = base;
+  L.seg.len = body->size() - base;
+  L.seg.parsed = false;
+  L.seg.code_epoch = 0;
+  L.seg.layout_ver += 1;
+  L.valid = true;
+  L.relayout = false;
+}
+
+void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t gen, uint64_t gc_after) {
+  last_rebuilt_ = 0;
+  last_relayouts_ = 0;
+  bool rebuild = false;  // some family is laid out again, appears or disappears
+  if (layouts_.size() != families_.size()) {
+    layouts_.resize(families_.size());  // csegs_ points into layouts_: rebuilt below
+    for (auto& L : layouts_) L.valid = false;
+    rebuild = true;
+  }
+  for (int fid : render_order_) {
+    Family& fam = families_[size_t(fid)];
+    Layout& L = layouts_[size_t(fid)];
+    fam.dirty = true;  // render()'s per-family text cache is not kept alongside
+    bool any_live = false;
+    size_t w = 0;
+    for (size_t i = 0; i < fam.members.size(); ++i) {
+      const uint32_t idx = fam.members[i];
+      if (hot_[idx].gen + gc_after < gen) {
+        free_series(idx);
+        continue;
+      }
+      fam.members[w++] = idx;
+      any_live = any_live || hot_[idx].gen == gen;
+    }
+    fam.members.resize(w);
+    if (!any_live) {
+      if (L.valid) rebuild = true;
+      L.valid = false;
+      continue;
+    }
+    if (fam.dirty_order) sort_members(fam);
+    if (!L.valid) {
+      L.relayout = true;
+      rebuild = true;
+      continue;
+    }
+    // the same live members in the same order as laid out?
+    size_t k = 0;
+    bool same = true;
+    for (uint32_t idx : fam.members) {
+      if (hot_[idx].gen != gen) continue;
+      if (k >= L.members.size() || L.members[k] != idx || L.vers[k] != hot_[idx].ver) {
+        same = false;
+        break;
+      }
+      ++k;
+    }
+    if (!same || k != L.members.size()) {
+      L.relayout = true;
+      rebuild = true;
+      continue;
+    }
+    // patch the fields of changed members in place; a value that outgrew its field lays the
+    // family out again
+    for (size_t m = 0; m < L.members.size(); ++m) {
+      const uint32_t idx = L.members[m];
+      if (hot_[idx].stamp == L.stamps[m]) continue;
+      field_texts(idx);
+      const size_t nf = scratch_len_.size();
+      const TmplField* fl = &L.seg.fields[L.first_field[m]];
+      bool fits = L.first_field[m] + nf <= L.seg.fields.size();
+      for (size_t f = 0; fits && f < nf; ++f) fits = scratch_len_[f] <= fl[f].width;
+      if (!fits) {
+        L.relayout = true;
+        rebuild = true;
+        break;
+      }
+      for (size_t f = 0; f < nf; ++f) {
+        char* dst = &cbody_[L.seg.base + fl[f].off];
+        std::memcpy(dst, &scratch_[32 * f], scratch_len_[f]);
+        std::memset(dst + scratch_len_[f], ' ', fl[f].width - scratch_len_[f]);
+      }
+      L.stamps[m] = hot_[idx].stamp;
+    }
+  }
+  if (rebuild) {
+    cbody_next_.clear();
+    csegs_.clear();
+    for (int fid : render_order_) {
+      Layout& L = layouts_[size_t(fid)];
+      if (!L.valid && !L.relayout) continue;
+      if (L.relayout) {
+        layout_family(fid, gen, &cbody_next_);
+        ++last_relayouts_;
+        ++last_rebuilt_;
+        relaid_bytes_ += L.seg.len;
+      } else {
+        const size_t nb = cbody_next_.size();
+        cbody_next_.append(cbody_, L.seg.base, L.seg.len);
+        L.seg.base = nb;
+      }
+      csegs_.push_back(&L.seg);
+    }
+    cbody_.swap(cbody_next_);
+  }
+  out->assign(cbody_);
+  if (!gz) return;
+  // (re-)parse laid-out segments and those whose matches reached into a segment laid out since
+  for (size_t i = 0; i < csegs_.size(); ++i)
+    if (!TemplateDeflate::parse_valid(csegs_, i)) {
+      if (csegs_[i]->parsed) relaid_bytes_ += csegs_[i]->len;  // a dependant: its bits change too
+      TemplateDeflate::parse(cbody_.data(), csegs_, i);
+    }
+  // The code is complete (any segment encodes under it); it is rebuilt for compression once an
+  // eighth of the body was laid out since the last build.
+  if (!deflate_.have_code() || relaid_bytes_ * 8 > cbody_.size()) {
+    deflate_.build_code(cbody_.data(), csegs_);
+    relaid_bytes_ = 0;
+    ++code_builds_;
+  }
+  deflate_.encode_gzip(cbody_.data(), cbody_.size(), crc32_fast(0, cbody_.data(), cbody_.size()), csegs_, gz);
 }
 
 size_t SeriesTable::live_series(uint64_t gen) const {

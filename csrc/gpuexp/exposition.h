@@ -12,6 +12,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include "gpuexp/deflate_tmpl.h"
+
 namespace gpuexp {
 
 enum class MetricType : uint8_t { kGauge = 0, kCounter = 1, kHistogram = 2 };
@@ -77,6 +79,18 @@ class SeriesTable {
   // encoding=delimited`).  Call after render() of the same generation (GC + ordering).
   void render_proto(std::string* out, uint64_t gen) const;
 
+  // Fixed-layout rendering: the samples render() gives, with every value in a blank-padded
+  // field whose width only grows (per series), so the body keeps its layout from tick to tick.
+  // Between layout changes (a series appears or goes, a value outgrows its field) a tick only
+  // patches the fields whose values changed, and -- with `gz` -- emits the gzip member from the
+  // pre-encoded static bits plus the field bytes (TemplateDeflate).  Do not mix with render()
+  // on one table.
+  void render_compiled(std::string* out, std::string* gz, uint64_t gen, uint64_t gc_after = 1);
+  // Families laid out again by the last render_compiled (0 in steady state).
+  size_t last_relayouts() const { return last_relayouts_; }
+  uint64_t code_builds() const { return code_builds_; }
+  const TemplateDeflate& deflater() const { return deflate_; }
+
   size_t live_series(uint64_t gen) const;
   // Families whose text was re-built by the last render (the rest were copied cached).
   size_t last_rebuilt_families() const { return last_rebuilt_; }
@@ -93,6 +107,7 @@ class SeriesTable {
     uint64_t gen = 0;       // last generation it was set
     double value = 0;
     bool in_cache = false;  // included in its family's cached text
+    uint32_t stamp = 0;     // bumped on every value/histogram change (render_compiled)
   };
   struct Series {  // cold: strings and histogram state
     std::vector<std::string> labels;
@@ -111,6 +126,7 @@ class SeriesTable {
     double hsum = 0;
     uint64_t hcount = 0;
     std::vector<std::string> hlines;  // `name_bucket{...,le="b"} ` per bound, +Inf, _sum, _count
+    std::vector<uint8_t> widths;      // render_compiled field widths (value, or each histogram line)
   };
   struct Family {
     FamilyDef def;
@@ -122,9 +138,26 @@ class SeriesTable {
     std::string cache;
     bool dirty = true;
   };
+  // render_compiled state of one family: its live members as laid out, its segment of the
+  // body, and per member the fields it owns and the stamp they were written with.
+  struct Layout {
+    bool valid = false;
+    bool relayout = false;
+    std::vector<uint32_t> members;
+    std::vector<uint32_t> vers;
+    std::vector<uint32_t> first_field;  // per member; fields of one member are contiguous
+    std::vector<uint32_t> stamps;       // per member
+    TmplSegment seg;
+  };
+  // Field texts of series `idx` (1 for a gauge/counter, bounds + 3 for a histogram) into
+  // scratch_ / scratch_len_.
+  void field_texts(uint32_t idx);
+  void layout_family(int fid, uint64_t gen, std::string* body);
   void free_series(uint32_t idx);
   void sort_members(Family& f);
   void render_histogram(std::string* out, uint32_t idx);
+  void build_hlines(uint32_t idx);
+  void format_cached(uint32_t idx);  // (re)fills the series' vtxt cache
   void append_cached_value(std::string* out, uint32_t idx);
   void mark_dirty(int fid) { families_[size_t(fid)].dirty = true; }
 
@@ -136,6 +169,16 @@ class SeriesTable {
   std::unordered_map<std::string, uint32_t> index_;
   std::string keybuf_;
   size_t last_rebuilt_ = 0;
+  // render_compiled
+  std::vector<Layout> layouts_;  // by family id
+  std::string cbody_, cbody_next_;
+  std::vector<TmplSegment*> csegs_;
+  TemplateDeflate deflate_;
+  size_t last_relayouts_ = 0;
+  uint64_t code_builds_ = 0;
+  size_t relaid_bytes_ = 0;  // bytes laid out again since the code was last built
+  std::vector<char> scratch_;  // field_texts output, 32 bytes per field
+  std::vector<uint8_t> scratch_len_;
 };
 
 }  // namespace gpuexp

@@ -47,6 +47,8 @@ class Config:
     kfd_detail_interval: float = 1.0       # seconds between cu_occupancy / sdma re-reads (0 = every tick)
     kfd_rescan_interval: float = 0.5       # KFD proc directory listed at least this often (also on change)
     gc_after: int = 1
+    exposition: str = "compiled"           # compiled (fixed-layout body, values patched in place, gzip from
+                                           # pre-encoded static bits) | classic (re-render + compress)
     # optional sources
     enable_sentinel: bool = False
     sentinel_spin: int = 500
@@ -181,6 +183,7 @@ class Config:
         ec.pod_totals_ttl_s = float(self.pod_totals_ttl)
         ec.kfd_path = self.kfd_path
         ec.gc_after = int(self.gc_after)
+        ec.exposition = str(self.exposition)
         ec.device_filter = [int(d) for d in self.devices if ":" not in str(d)]
         ec.device_filter_bdf = [str(d) for d in self.devices if ":" in str(d)]
         ec.queue_devices = [int(d) for d in self.queue_devices if ":" not in str(d)]
@@ -291,6 +294,8 @@ def validate(cfg: Config) -> None:
         raise ValueError(f"metrics_min_interval must be 'auto' or seconds >= 0, got {cfg.metrics_min_interval!r}")
     if not (0 <= cfg.metrics_cpu_budget <= 100):
         raise ValueError("metrics_cpu_budget must be a percentage of one core, 0-100 (0 = no cap under auto)")
+    if cfg.exposition not in ("compiled", "classic"):
+        raise ValueError(f"exposition must be compiled|classic, got {cfg.exposition}")
     if cfg.counters_kick not in ("auto", "start", "after_devices", "end"):
         raise ValueError(f"counters_kick must be auto|start|after_devices|end, got {cfg.counters_kick}")
     if cfg.state_interval <= 0:

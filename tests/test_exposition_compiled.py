@@ -1,0 +1,166 @@
+"""The fixed-layout exposition (SeriesTable::render_compiled, csrc/gpuexp/deflate_tmpl.cc):
+every tick it must parse to exactly the samples the classic renderer gives, and its gzip
+member must inflate (Python's zlib, an independent inflater) to exactly its text -- through
+value churn, series appearing and going, values outgrowing their fields, histograms and
+escaped labels.  Reference counterpart: promhttp's render + gzip on every scrape
+(/root/reference/main.go:68-70)."""
+import gzip
+import math
+import random
+import zlib
+
+import pytest
+
+from kubernetes_gpu_exporter_amd.utils import promtext
+
+
+def _same(a, b):
+    """promtext.parse results equal, NaN == NaN."""
+    assert a.keys() == b.keys()
+    for name in a:
+        fa, fb = a[name], b[name]
+        assert fa.type == fb.type and fa.help == fb.help, name
+        sa = sorted(fa.samples, key=lambda s: (s[0], sorted(s[1].items())))
+        sb = sorted(fb.samples, key=lambda s: (s[0], sorted(s[1].items())))
+        assert len(sa) == len(sb), name
+        for (na, la, va), (nb, lb, vb) in zip(sa, sb):
+            assert na == nb and la == lb, (na, la, nb, lb)
+            assert va == vb or (math.isnan(va) and math.isnan(vb)), (na, la, va, vb)
+
+
+def _tables(native, nfam=24):
+    out = []
+    for _ in range(2):
+        t = native.SeriesTable()
+        ids = []
+        for i in range(nfam):
+            ty = (native.MetricType.gauge, native.MetricType.counter)[i % 2]
+            ids.append(t.add_family(f"m{i:02d}_metric_{'x' * (i % 5)}", f"help of family {i}: \\ and \n", ty, ["gpu", "k"]))
+        h = t.add_family("lat_seconds", "a histogram", native.MetricType.histogram, ["gpu"])
+        out.append((t, ids, h))
+    return out
+
+
+def _value(rng, gen):
+    return rng.choice([rng.random() * 1000, float(rng.randint(0, 10 ** rng.randint(1, 15))), 0.0, -3.25,
+                       float("nan"), float("inf"), float("-inf"), gen * 1.5, 1e-300, 2.0 ** 60])
+
+
+@pytest.mark.parametrize("churn", [0.0, 0.05])
+def test_compiled_matches_classic_every_tick(native, churn):
+    (a, ia, ha), (b, ib, hb) = _tables(native)
+    rng = random.Random(7)
+    for gen in range(1, 120):
+        for i in range(len(ia)):
+            for g in range(8):
+                for k in ("a", 'q"\\z\n') if i % 3 == 0 else ("a",):
+                    if gen > 1 and rng.random() < churn:
+                        continue  # not set this tick: gone (gc_after 1) -> the family is laid out again
+                    v = _value(rng, gen) if rng.random() < 0.5 else float(g)
+                    a.put(ia[i], [str(g), k], v, gen)
+                    b.put(ib[i], [str(g), k], v, gen)
+        for g in range(3):
+            v = rng.random() * 10
+            a.observe(ha, [str(g)], v, gen, [0.1, 1.0, 5.0])
+            b.observe(hb, [str(g)], v, gen, [0.1, 1.0, 5.0])
+        ref = a.render(gen, 1)
+        txt, gz = b.render_compiled(gen, 1, True)
+        _same(promtext.parse(ref), promtext.parse(txt))
+        assert gzip.decompress(gz) == txt.encode(), gen
+        assert zlib.decompress(gz, 31) == txt.encode()  # zlib's own inflater, gzip wrapper
+
+
+def test_steady_state_does_not_relayout(native):
+    (t, ids, h), _ = _tables(native, 8)
+    for gen in range(1, 60):
+        for i, f in enumerate(ids):
+            for g in range(4):
+                # same text length every tick (3-digit integers): fields never grow
+                t.put(f, [str(g), "a"], float(100 + (gen * 7 + i + g) % 900), gen)
+        txt, gz = t.render_compiled(gen, 1, True)
+        if gen > 1:
+            assert t.last_relayouts() == 0, gen
+        assert gzip.decompress(gz) == txt.encode()
+    assert t.code_builds() == 1
+
+
+def test_outgrown_field_relayouts_only_its_family(native):
+    (t, ids, h), _ = _tables(native, 6)
+    for gen in range(1, 4):
+        for f in ids:
+            t.put(f, ["0", "a"], 5.0, gen)
+        t.render_compiled(gen, 1, True)
+    for f in ids:
+        t.put(f, ["0", "a"], 5.0, 4)
+    t.put(ids[3], ["0", "a"], 123456789.125, 4)  # outgrows its 1-byte field
+    txt, gz = t.render_compiled(4, 1, True)
+    assert t.last_relayouts() == 1
+    assert gzip.decompress(gz) == txt.encode()
+    # back to a short value: the field keeps its width (blank-padded), no new layout
+    for f in ids:
+        t.put(f, ["0", "a"], 5.0, 5)
+    txt, gz = t.render_compiled(5, 1, True)
+    assert t.last_relayouts() == 0
+    line = [ln for ln in txt.splitlines() if ln.startswith("m03_")][0]
+    assert line.endswith("5" + " " * (len("123456789.125") - 1))
+    assert promtext.parse(txt)["m03_metric_xxx"].samples[0][2] == 5.0
+    assert gzip.decompress(gz) == txt.encode()
+
+
+def test_compiled_gzip_is_close_to_zlib(native):
+    """Static bytes are LZ77-parsed once per layout (matches reach back into the preceding
+    families), values are literals: the member stays within ~25 % of zlib level 1 on a body
+    shaped like the exporter's (many families with the same label sets)."""
+    t = native.SeriesTable()
+    ids = [t.add_family(f"amd_gpu_{n}", f"The {n.replace('_', ' ')} of the GPU, from the PMFW metrics table",
+                        native.MetricType.gauge, ["gpu", "xcc"])
+           for n in ("xcc_busy_percent", "xcc_clock_hz", "xcc_mfma_busy_percent", "xcc_temperature_celsius",
+                     "xcc_power_watts", "xcc_util_percent", "xcc_waves", "xcc_lds_bytes")]
+    for gen in range(1, 4):
+        for f in ids:
+            for g in range(8):
+                for x in range(8):
+                    t.put(f, [str(g), str(x)], float((g * 8 + x) * 37 % 101), gen)
+        txt, gz = t.render_compiled(gen, 1, True)
+    z1 = len(zlib.compress(txt.encode(), 1))
+    assert len(gz) <= 1.25 * z1, (len(gz), z1)
+
+
+def test_engine_compiled_and_classic_expose_the_same_samples(mock_engine):
+    """The two engine exposition modes on the 8-GPU mock node, tick for tick."""
+    a = mock_engine(8, http=False, series_profile="full", exposition="classic")
+    b = mock_engine(8, http=False, series_profile="full", exposition="compiled")
+    for i in range(1, 6):
+        a.tick(i * 100_000_000)
+        b.tick(i * 100_000_000)
+        pa, pb = promtext.parse(a.snapshot_text()), promtext.parse(b.snapshot_text())
+        # self-metrics (tick CPU, stage times) legitimately differ between two engines
+        for p in (pa, pb):
+            for name in [n for n in p if n.startswith("gpuexp_")]:
+                del p[name]
+        _same(pa, pb)
+
+
+def test_engine_gzip_scrape_inflates_to_the_identity_body(mock_engine):
+    """A gzip scrape is served from the member the sampler emitted with the body (compiled
+    mode) and inflates to the identity body of the same snapshot."""
+    import http.client
+    e = mock_engine(2, series_profile="full")
+
+    def get(enc):
+        c = http.client.HTTPConnection("127.0.0.1", e.http_port, timeout=5)
+        c.request("GET", "/metrics", headers={"Accept-Encoding": enc})
+        r = c.getresponse()
+        body = r.read()
+        c.close()
+        return r.getheader("Content-Encoding"), body
+
+    e.tick(100_000_000)
+    get("gzip")  # a gzip client: the sampler emits a gzip member with every snapshot from now on
+    for i in range(2, 6):
+        e.tick(i * 100_000_000)
+        enc, gz = get("gzip")
+        assert enc == "gzip"
+        _, ident = get("identity")
+        assert gzip.decompress(gz) == ident == e.snapshot_text().encode()
+    assert e.stats()["gzip_eager"] >= 4

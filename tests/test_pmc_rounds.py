@@ -154,7 +154,10 @@ def test_another_profiler_is_not_fought(native):
 def test_rearm_modes_on_the_machine(native, mode, rearms, waiting):
     scripts = [{} for _ in range(8)]
     scripts[2]["resets"] = [300 * MS]
-    r = run(native, rearm=mode, scripts=scripts)
+    # "now" re-arms inside the round that saw the reset: the next window's start is the arm's
+    # completion, estimated to half a polling interval -- on a loaded CPU (xdist) a 20 ms window
+    # can be off by more than the default 40 %
+    r = run(native, rearm=mode, scripts=scripts, rate_tolerance=0.6)
     g2 = r["gpus"][2]
     assert g2["rearms"] == rearms and g2["waiting_rearm"] is waiting and g2["bad_windows"] == 0
     if mode == "now":

@@ -24,7 +24,24 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
-def measure(native, n_gpus: int, hz: float, fetch_us: int, policy: str, budget: float, seconds: float) -> dict:
+SCRAPER = r"""
+import sys, time
+sys.path.insert(0, sys.argv[1])
+from kubernetes_gpu_exporter_amd._native import load
+n = load()
+c = n.ScrapeClient("127.0.0.1", int(sys.argv[2]), "/metrics", sys.argv[4] == "gzip", 5000, "", True)
+period = 1.0 / float(sys.argv[3])
+t = time.perf_counter()
+while True:
+    c.scrape()
+    t += period
+    time.sleep(max(0.0, t - time.perf_counter()))
+"""
+
+
+def measure(native, n_gpus: int, hz: float, fetch_us: int, policy: str, budget: float, seconds: float,
+            scrape: str = "none", exposition: str = "compiled") -> dict:
+    import subprocess
     import test_fakehost as tf
     root = tempfile.mkdtemp(prefix="gpuexp-proj-")
     tf._loaded_node(root, n_gpus)
@@ -32,25 +49,42 @@ def measure(native, n_gpus: int, hz: float, fetch_us: int, policy: str, budget: 
     c.backend = "sysfs"
     c.host_root = root
     c.interval_s = 1.0 / hz
-    c.serve_http = False
+    c.serve_http = scrape != "none"
+    if c.serve_http:
+        h = c.http
+        h.port = 0
+        h.host = "127.0.0.1"
+        c.http = h
     c.series_profile = "full"
+    c.exposition = exposition
     c.fake_metrics_cost_us = fetch_us
     c.metrics_min_interval_s = -1.0 if policy == "auto" else 0.0
     c.metrics_cpu_budget = budget / 100.0
     e = native.Engine(c)
     e.start()
+    scraper = None
+    if scrape != "none":  # another process, so its CPU is not the exporter's
+        scraper = subprocess.Popen([sys.executable, "-c", SCRAPER, ROOT, str(e.http_port), str(hz), scrape])
     try:
         time.sleep(1.0)
         r0, t0, s0 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter(), e.stats()
         time.sleep(seconds)
         r1, t1, s1 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter(), e.stats()
     finally:
+        if scraper:
+            scraper.kill()
+            scraper.wait()
         e.stop()
     cpu = (r1.ru_utime - r0.ru_utime) + (r1.ru_stime - r0.ru_stime)
     ticks = max(1, s1["ticks"] - s0["ticks"])
-    return {"gpus": n_gpus, "hz": hz, "fetch_us": fetch_us, "policy": policy,
+    stages = {k: round((s1["stage_cpu_ns"][k] - s0["stage_cpu_ns"][k]) / ticks / 1e3, 1) for k in s1["stage_cpu_ns"]}
+    return {"gpus": n_gpus, "hz": hz, "fetch_us": fetch_us, "policy": policy, "scrape": scrape,
+            "exposition": exposition, "body_bytes": s1.get("render_bytes"),
             "process_cpu_pct": round(100.0 * cpu / (t1 - t0), 2),
-            "sampler_us_per_tick": round((s1["sampler_cpu_ns"] - s0["sampler_cpu_ns"]) / ticks / 1e3, 1)}
+            "sampler_us_per_tick": round((s1["sampler_cpu_ns"] - s0["sampler_cpu_ns"]) / ticks / 1e3, 1),
+            "stage_us_per_tick": stages,
+            "relayouts_per_tick": round((s1.get("relayouts", 0) - s0.get("relayouts", 0)) / ticks, 3),
+            "code_builds": s1.get("code_builds", 0) - s0.get("code_builds", 0)}
 
 
 def main() -> int:
@@ -60,18 +94,28 @@ def main() -> int:
     ap.add_argument("--gpus", default="1,2,4,8")
     ap.add_argument("--budget", type=float, default=1.5)
     ap.add_argument("--seconds", type=float, default=4.0)
+    ap.add_argument("--policies", default="auto,every")
+    ap.add_argument("--scrape", default="none", help="none | gzip | identity: a scraper process at the tick rate")
+    ap.add_argument("--exposition", default="compiled", help="compiled | classic (comma list to compare)")
+    ap.add_argument("--stages", action="store_true", help="also print the sampler thread's CPU per stage")
     args = ap.parse_args()
     from kubernetes_gpu_exporter_amd._native import load
     native = load()
     print(f"# fake-host projection, full profile, 4 processes/GPU, budget {args.budget} % (auto policy)")
-    print(f"{'gpus':>4} {'hz':>5} {'fetch_us':>8} {'policy':>6} {'cpu_%':>7} {'sampler_us/tick':>15}")
+    print(f"{'gpus':>4} {'hz':>5} {'fetch_us':>8} {'policy':>6} {'cpu_%':>7} {'sampler_us/tick':>15}  exposition")
     for fetch in (int(x) for x in args.fetch_us.split(",")):
         for hz in (float(x) for x in args.hz.split(",")):
             for n in (int(x) for x in args.gpus.split(",")):
-                for policy in ("auto", "every"):
-                    r = measure(native, n, hz, fetch, policy, args.budget, args.seconds)
+                for policy in args.policies.split(","):
+                  for expo in args.exposition.split(","):
+                    r = measure(native, n, hz, fetch, policy, args.budget, args.seconds, args.scrape, expo)
                     print(f"{r['gpus']:>4} {r['hz']:>5g} {r['fetch_us']:>8} {r['policy']:>6} "
-                          f"{r['process_cpu_pct']:>7.2f} {r['sampler_us_per_tick']:>15.1f}", flush=True)
+                          f"{r['process_cpu_pct']:>7.2f} {r['sampler_us_per_tick']:>15.1f}  "
+                          f"{expo} scrape={args.scrape}", flush=True)
+                    if args.stages:
+                        print("      stage us/tick: " + " ".join(f"{k}={v}" for k, v in r["stage_us_per_tick"].items())
+                              + f"  relayouts/tick={r['relayouts_per_tick']} code_builds={r['code_builds']}"
+                              + f" body={r['body_bytes']}", flush=True)
     return 0
 
 
