@@ -20,10 +20,12 @@ constexpr uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6,
 // order in which the code-length code lengths are sent (§3.2.7)
 constexpr uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-constexpr int kMinMatch = 3;
+constexpr int kMinMatch = 4;  // hashed on 4 bytes: far fewer chain collisions in label-heavy text
 constexpr int kMaxMatch = 258;
 constexpr uint32_t kWindow = 32768;
-constexpr int kChainDepth = 48;
+constexpr int kChainDepth = 8;
+constexpr int kNiceMatch = 48;  // stop searching at a match this long
+constexpr int kLazyBelow = 24;  // look one byte ahead only after a shorter match
 constexpr int kHashBits = 13;
 
 int len_sym(int len) {  // 257..285
@@ -202,29 +204,26 @@ bool TemplateDeflate::parse_valid(const std::vector<TmplSegment*>& segs, size_t 
   return true;
 }
 
-void TemplateDeflate::parse(const char* body, const std::vector<TmplSegment*>& segs, size_t i, size_t lookback) {
-  TmplSegment* seg = segs[i];
-  seg->toks.clear();
-  seg->words.clear();
-  seg->piece_bits.clear();
-  seg->deps.clear();
-  seg->code_epoch = 0;
-  // window [w0, end): lookback bytes of the preceding segments, then the segment
+void TemplateDeflate::parse(const char* body, const std::vector<TmplSegment*>& segs, size_t i0, size_t i1,
+                            size_t lookback) {
+  if (i1 <= i0) return;
+  // window [w0, end): lookback bytes before segs[i0], then the run's segments; one hash state
+  // for the whole run, so consecutive segments are hashed once (a segment's lookback is the
+  // tail of the one before it)
   lookback = std::min<size_t>(lookback, kWindow - kMaxMatch);
-  const size_t w0 = seg->base > lookback ? seg->base - lookback : 0;
-  const size_t end = seg->base + seg->len;
+  const size_t w0 = segs[i0]->base > lookback ? segs[i0]->base - lookback : 0;
+  const size_t end = segs[i1 - 1]->base + segs[i1 - 1]->len;
   const unsigned char* s = reinterpret_cast<const unsigned char*>(body + w0);
   const uint32_t n = uint32_t(end - w0);
-  const uint32_t start = uint32_t(seg->base - w0);
-  // static_end[p]: where the static run containing p ends (the next field's start, or the end of
-  // the run inside the window); p itself if p is inside a field
+  // static_end[p]: where the static run containing p ends (the next field's start, or n); p
+  // itself if p is inside a field
   thread_local std::vector<uint32_t> static_end;
   static_end.assign(n, n);
   {
-    size_t first = i;
+    size_t first = i0;
     while (first > 0 && segs[first - 1]->base + segs[first - 1]->len > w0) --first;
     uint32_t p = 0;
-    for (size_t j = first; j <= i; ++j) {
+    for (size_t j = first; j < i1; ++j) {
       const TmplSegment* sj = segs[j];
       for (const TmplField& f : sj->fields) {
         const size_t fo = sj->base + f.off, fe = fo + f.width;
@@ -238,86 +237,109 @@ void TemplateDeflate::parse(const char* body, const std::vector<TmplSegment*>& s
   }
   thread_local std::vector<int32_t> head, prev;
   head.assign(size_t(1) << kHashBits, -1);
-  prev.assign(n, -1);
+  prev.resize(n);
   auto hash = [&](uint32_t p) {
-    uint32_t v = 0;
-    std::memcpy(&v, s + p, 3);
+    uint32_t v;
+    std::memcpy(&v, s + p, 4);
     return (v * 2654435761u) >> (32 - kHashBits);
   };
   auto insert = [&](uint32_t p) {
-    if (p + kMinMatch > static_end[p]) return;  // fewer than 3 static bytes: never a source
+    if (p + kMinMatch > static_end[p]) return;  // fewer than 4 static bytes: never a source
     const uint32_t h = hash(p);
     prev[p] = head[h];
     head[h] = int32_t(p);
   };
-  for (uint32_t p = 0; p < start; ++p) insert(p);
-  uint32_t min_src = start;
-  auto best_at = [&](uint32_t p, uint32_t* dist) -> int {
-    const uint32_t lim = std::min<uint32_t>(kMaxMatch, static_end[p] - p);
-    if (lim < uint32_t(kMinMatch)) return 0;
-    int best = 0;
-    int depth = kChainDepth;
-    for (int32_t q = head[hash(p)]; q >= 0 && depth-- > 0; q = prev[size_t(q)]) {
-      const uint32_t d = p - uint32_t(q);
-      if (d > kWindow) break;
-      const uint32_t ql = std::min(lim, static_end[size_t(q)] - uint32_t(q));
-      uint32_t l = 0;
-      while (l < ql && s[size_t(q) + l] == s[p + l]) ++l;
-      // prefer the nearer of equal matches (positions come nearest first): fewer dependencies
-      if (int(l) > best) {
-        best = int(l);
-        *dist = d;
-        if (l == lim) break;
+  // common prefix length of s+a and s+b, at most lim (8 bytes at a time)
+  auto common = [&](uint32_t a, uint32_t b, uint32_t lim) {
+    uint32_t l = 0;
+    while (l + 8 <= lim) {
+      uint64_t x, y;
+      std::memcpy(&x, s + a + l, 8);
+      std::memcpy(&y, s + b + l, 8);
+      if (x != y) return l + uint32_t(__builtin_ctzll(x ^ y) >> 3);
+      l += 8;
+    }
+    while (l < lim && s[a + l] == s[b + l]) ++l;
+    return l;
+  };
+  const uint32_t start0 = uint32_t(segs[i0]->base - w0);
+  for (uint32_t p = 0; p < start0; ++p) insert(p);
+  for (size_t i = i0; i < i1; ++i) {
+    TmplSegment* seg = segs[i];
+    seg->toks.clear();
+    seg->words.clear();
+    seg->piece_bits.clear();
+    seg->deps.clear();
+    seg->code_epoch = 0;
+    const uint32_t start = uint32_t(seg->base - w0);
+    const uint32_t seg_end = start + uint32_t(seg->len);
+    uint32_t min_src = start;
+    auto best_at = [&](uint32_t p, uint32_t* dist) -> int {
+      const uint32_t lim = std::min<uint32_t>({uint32_t(kMaxMatch), static_end[p] - p, seg_end - p});
+      if (lim < uint32_t(kMinMatch)) return 0;
+      int best = 0;
+      int depth = kChainDepth;
+      for (int32_t q = head[hash(p)]; q >= 0 && depth-- > 0; q = prev[size_t(q)]) {
+        const uint32_t d = p - uint32_t(q);
+        if (d > kWindow) break;
+        const uint32_t ql = std::min(lim, static_end[size_t(q)] - uint32_t(q));
+        if (int(ql) <= best || s[size_t(q) + size_t(best)] != s[p + size_t(best)]) continue;
+        const uint32_t l = common(uint32_t(q), p, ql);
+        if (int(l) > best) {  // nearest first: a tie keeps the nearer source (fewer dependencies)
+          best = int(l);
+          *dist = d;
+          if (l == lim || best >= kNiceMatch) break;
+        }
       }
-    }
-    return best >= kMinMatch ? best : 0;
-  };
-  uint32_t lit_start = 0, lit_n = 0;
-  auto flush_lits = [&]() {
-    if (lit_n) seg->toks.push_back({0, lit_n, lit_start - start});
-    lit_n = 0;
-  };
-  size_t fi = 0;
-  uint32_t p = start;
-  while (p < n) {
-    if (fi < seg->fields.size() && p == start + seg->fields[fi].off) {
-      flush_lits();
-      seg->toks.push_back({2, 0, uint32_t(fi)});
-      p += seg->fields[fi].width;
-      ++fi;
-      continue;
-    }
-    uint32_t d = 0;
-    int l = best_at(p, &d);
-    if (l) {
-      // one-step lazy: a longer match at p+1 wins over this one
-      uint32_t d2 = 0;
+      return best >= kMinMatch ? best : 0;
+    };
+    uint32_t lit_start = 0, lit_n = 0;
+    auto flush_lits = [&]() {
+      if (lit_n) seg->toks.push_back({0, lit_n, lit_start - start});
+      lit_n = 0;
+    };
+    size_t fi = 0;
+    uint32_t p = start;
+    while (p < seg_end) {
+      if (fi < seg->fields.size() && p == start + seg->fields[fi].off) {
+        flush_lits();
+        seg->toks.push_back({2, 0, uint32_t(fi)});
+        p += seg->fields[fi].width;
+        ++fi;
+        continue;
+      }
+      uint32_t d = 0;
+      const int l = best_at(p, &d);
+      if (l) {
+        // one-step lazy: a longer match at p+1 wins over this one
+        uint32_t d2 = 0;
+        insert(p);
+        const int l2 = (l < kLazyBelow && p + 1 < seg_end && static_end[p + 1] > p + 1) ? best_at(p + 1, &d2) : 0;
+        if (l2 > l + 1) {
+          if (!lit_n) lit_start = p;
+          ++lit_n;
+          ++p;
+          continue;  // p (now p+1) re-searched next iteration
+        }
+        flush_lits();
+        seg->toks.push_back({1, uint32_t(l), d});
+        min_src = std::min(min_src, p - d);
+        for (uint32_t k = 1; k < uint32_t(l); ++k) insert(p + k);
+        p += uint32_t(l);
+        continue;
+      }
       insert(p);
-      const int l2 = (p + 1 < n && static_end[p + 1] > p + 1) ? best_at(p + 1, &d2) : 0;
-      if (l2 > l + 1) {
-        if (!lit_n) lit_start = p;
-        ++lit_n;
-        ++p;
-        continue;  // p (now p+1) re-searched next iteration
-      }
-      flush_lits();
-      seg->toks.push_back({1, uint32_t(l), d});
-      min_src = std::min(min_src, p - d);
-      for (uint32_t k = 1; k < uint32_t(l); ++k) insert(p + k);
-      p += uint32_t(l);
-      continue;
+      if (!lit_n) lit_start = p;
+      ++lit_n;
+      ++p;
     }
-    insert(p);
-    if (!lit_n) lit_start = p;
-    ++lit_n;
-    ++p;
+    flush_lits();
+    // the preceding segments the matches read from, nearest first
+    const size_t src = w0 + min_src;
+    for (size_t j = i; j > 0 && src < segs[j - 1]->base + segs[j - 1]->len; --j)
+      seg->deps.emplace_back(segs[j - 1], segs[j - 1]->layout_ver);
+    seg->parsed = true;
   }
-  flush_lits();
-  // the preceding segments the matches read from, nearest first
-  const size_t src = w0 + min_src;
-  for (size_t j = i; j > 0 && src < segs[j - 1]->base + segs[j - 1]->len; --j)
-    seg->deps.emplace_back(segs[j - 1], segs[j - 1]->layout_ver);
-  seg->parsed = true;
 }
 
 void TemplateDeflate::build_code(const char* body, const std::vector<TmplSegment*>& segs) {

@@ -58,10 +58,11 @@ struct TmplSegment {
 
 class TemplateDeflate {
  public:
-  // LZ77 parse of segs[i]'s static bytes (hash chains with one-step lazy matching).  The window
-  // is the segment plus up to `lookback` bytes of the segments before it (their static bytes
-  // only); segs tile `body`.
-  static void parse(const char* body, const std::vector<TmplSegment*>& segs, size_t i, size_t lookback = 8192);
+  // LZ77 parse of the static bytes of segs[i0, i1) (hash chains with one-step lazy matching).
+  // A segment's matches reach up to `lookback` bytes back into the segments before it (their
+  // static bytes only); segs tile `body`.  A run of consecutive segments shares one hash state.
+  static void parse(const char* body, const std::vector<TmplSegment*>& segs, size_t i0, size_t i1,
+                    size_t lookback = 8192);
   // Whether segs[i]'s parse still holds (its cross-segment references point at the same bytes).
   static bool parse_valid(const std::vector<TmplSegment*>& segs, size_t i);
 

@@ -452,6 +452,13 @@ void SeriesTable::layout_family(int fid, uint64_t gen, std::string* body) {
     for (size_t f = 0; f < nf; ++f) {
       body->append(hist ? s.hlines[f] : s.line);
       const uint8_t len = scratch_len_[f];
+      if (s.widths[f] && len > s.widths[f]) {
+        // outgrown: a field that changes length once will again -- leave room (an integer two more
+        // digits, a fraction the typical longest shortest-round-trip form) so it settles
+        const char* t = &scratch_[32 * f];
+        const bool frac = std::memchr(t, '.', len) || std::memchr(t, 'e', len);
+        s.widths[f] = uint8_t(std::min<int>(32, frac ? std::max<int>(len, 20) : len + 2));
+      }
       s.widths[f] = std::max(s.widths[f], len);
       L.seg.fields.push_back({uint32_t(body->size() - base), s.widths[f]});
       body->append(&scratch_[32 * f], len);
@@ -565,15 +572,23 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
   }
   out->assign(cbody_);
   if (!gz) return;
-  // (re-)parse laid-out segments and those whose matches reached into a segment laid out since
-  for (size_t i = 0; i < csegs_.size(); ++i)
-    if (!TemplateDeflate::parse_valid(csegs_, i)) {
-      if (csegs_[i]->parsed) relaid_bytes_ += csegs_[i]->len;  // a dependant: its bits change too
-      TemplateDeflate::parse(cbody_.data(), csegs_, i);
+  // (re-)parse laid-out segments and those whose matches reached into a segment laid out
+  // since; consecutive ones as one run
+  for (size_t i = 0; i < csegs_.size();) {
+    if (TemplateDeflate::parse_valid(csegs_, i)) {
+      ++i;
+      continue;
     }
-  // The code is complete (any segment encodes under it); it is rebuilt for compression once an
-  // eighth of the body was laid out since the last build.
-  if (!deflate_.have_code() || relaid_bytes_ * 8 > cbody_.size()) {
+    size_t j = i;
+    for (; j < csegs_.size() && !TemplateDeflate::parse_valid(csegs_, j); ++j)
+      if (csegs_[j]->parsed) relaid_bytes_ += csegs_[j]->len;  // a dependant: its bits change too
+    TemplateDeflate::parse(cbody_.data(), csegs_, i, j);
+    i = j;
+  }
+  // The code is complete (any segment encodes under it); it is rebuilt for compression once as
+  // many bytes as the body holds were laid out or re-parsed since the last build (a build
+  // re-encodes every segment: ~0.7 ms for an 8-GPU body).
+  if (!deflate_.have_code() || relaid_bytes_ > cbody_.size()) {
     deflate_.build_code(cbody_.data(), csegs_);
     relaid_bytes_ = 0;
     ++code_builds_;

@@ -96,13 +96,25 @@ def test_outgrown_field_relayouts_only_its_family(native):
     txt, gz = t.render_compiled(4, 1, True)
     assert t.last_relayouts() == 1
     assert gzip.decompress(gz) == txt.encode()
-    # back to a short value: the field keeps its width (blank-padded), no new layout
+    # back to a short value: the field keeps its width (blank-padded; an outgrown fraction
+    # field gets the room of a typical longest round-trip form, 20), no new layout
     for f in ids:
         t.put(f, ["0", "a"], 5.0, 5)
     txt, gz = t.render_compiled(5, 1, True)
     assert t.last_relayouts() == 0
     line = [ln for ln in txt.splitlines() if ln.startswith("m03_")][0]
-    assert line.endswith("5" + " " * (len("123456789.125") - 1))
+    assert line.endswith("5" + " " * 19)
+    # an outgrown integer field keeps two more digits of room
+    for f in ids:
+        t.put(f, ["0", "a"], 5.0, 6)
+    t.put(ids[1], ["0", "a"], 1234.0, 6)
+    t.render_compiled(6, 1, True)
+    assert t.last_relayouts() == 1
+    for f in ids:
+        t.put(f, ["0", "a"], 5.0, 7)
+    t.put(ids[1], ["0", "a"], 123456.0, 7)
+    txt, gz = t.render_compiled(7, 1, True)
+    assert t.last_relayouts() == 0 and gzip.decompress(gz) == txt.encode()
     assert promtext.parse(txt)["m03_metric_xxx"].samples[0][2] == 5.0
     assert gzip.decompress(gz) == txt.encode()
 
