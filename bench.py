@@ -126,9 +126,10 @@ def pct(v: list, q: float) -> float:
 
 
 def startup_budget_s(n_gpus: int) -> float:
-    """Exporter start -> first sample: amdsmi + raw-path validation and one HSA queue per GPU
-    (measured 1 GPU: ~4-6 s on MI355X boxes, most of it HSA/amdsmi init)."""
-    return 30.0 + 5.0 * n_gpus
+    """Exporter start -> first sample: amdsmi + raw-path validation and one HSA queue per GPU.
+    Measured on MI355X at 1 GPU: 0.25 s (engine 0.12 s; BENCH_r04.json), so a 20x regression
+    fails the run."""
+    return 5.0 + 1.5 * n_gpus
 
 
 def prewake_summary(lat: list, prewoken: list, splits: list) -> dict | None:
@@ -619,6 +620,12 @@ def main() -> int:
         return out
 
     xgmi_window: dict = {}
+    fresh0: dict = {}  # per-GPU fresh gpu_metrics reads at the start of the timed window
+    window_s = [0.0]
+
+    def fresh_reads(fams) -> dict:
+        return {lab["gpu"]: v for _, lab, v in promtext.samples(fams, "gpuexp_gpu_metrics_reads_total")
+                if lab.get("kind") == "fresh"}
     exporter_rss_kb = [0]
     cpu_by_thread: dict = {}
 
@@ -636,6 +643,8 @@ def main() -> int:
                                   promproto.ACCEPT if args.proto else "")
             side.scrape()
             x0 = xgmi_totals(side)
+            fresh0.clear()
+            fresh0.update(fresh_reads(last_fams(side)))
         if dist is not None:
             dist.barrier()
         sync()
@@ -649,6 +658,8 @@ def main() -> int:
             dist.barrier()
         sync()
         elapsed = time.perf_counter() - t0
+        if native_exporter:
+            window_s[0] = elapsed
         cpu_pct = 100.0 * (cpu_seconds_precise(proc.pid) - cpu0) / elapsed if rank == 0 else 0.0
         if rank == 0 and native_exporter:
             # where the exporter's CPU went, per thread name (us per step over the window)
@@ -788,6 +799,12 @@ def main() -> int:
             for _, lab, v in promtext.samples(fams, fam_name):
                 xgmi.setdefault(lab.get("gpu"), {})[key] = v
         tflops = 2.0 * G ** 3 * iters / (gemm_ms * iters * 1e-3) / 1e12 if gemm_ms else None
+        # how often each GPU's gpu_metrics table was fetched fresh over the timed window (the
+        # auto fetch policy caps it at 1 / gpuexp_gpu_metrics_min_interval_seconds: at 8 GPUs a
+        # "10 Hz" exporter refreshes power / clocks / activity at ~3-5 Hz)
+        fresh1 = fresh_reads(fams)
+        fresh_hz = ({g: round((fresh1[g] - fresh0[g]) / window_s[0], 2) for g in sorted(fresh1, key=int)
+                     if g in fresh0} if fresh0 and window_s[0] > 0 else None)
         result = {
             "metric": METRIC,
             "value": round(statistics.median(lat), 2) if lat else None,
@@ -807,7 +824,8 @@ def main() -> int:
                        "series_profile": args.series_profile, "gzip": args.gzip, "protobuf": args.proto,
                        "gemm": f"{G}^3 x {iters}/step",
                        "gemm_kernel_variant": kern.gemm_variant(G, G, G, 0) if kern is not None else None,
-                       "allreduce_mb": args.allreduce_mb if dist is not None else 0},
+                       "allreduce_mb": args.allreduce_mb if dist is not None else 0,
+                       "gpu_metrics_fresh_hz": fresh_hz},
             "p50_scrape_us": round(statistics.median(lat), 2) if lat else None,
             # a p99 needs >= 100 samples; below that only the max of the timed scrapes and
             # the server-side histogram quantiles over every scrape of the run are given
@@ -873,6 +891,7 @@ def main() -> int:
             "gpu_metrics_fetch_cpu_us_per_fresh_read_gpu0": round(fetch_cpu["0"] / metrics_reads["fresh"] * 1e6, 1)
             if fetch_cpu.get("0") and metrics_reads.get("fresh") else None,
             "gpu_metrics_min_interval_s": fetch_cap or None,
+            "gpu_metrics_fresh_hz": fresh_hz,
             "counters_kick": os.environ.get("GPUEXP_COUNTERS_KICK", "default"),
             "sampler_thread_cpu_s": sampler_cpu[0] if sampler_cpu else None,
             "sampler_cpu_us_per_tick": round(sampler_cpu[0] / ticks[0] * 1e6, 1) if sampler_cpu and ticks and ticks[0]

@@ -379,6 +379,11 @@ void Engine::define_families() {
   f_self_fetch_cap_ = add("gpuexp_gpu_metrics_min_interval_seconds",
                           "Current cap on fresh gpu_metrics reads per GPU (metrics_min_interval; auto: the "
                           "measured fetch CPU x GPUs / metrics_cpu_budget)", G, {"gpu"});
+  f_self_metrics_age_ = add("gpuexp_gpu_metrics_age_seconds",
+                            "Age of the GPU's gpu_metrics table at this tick: seconds since it was last fetched "
+                            "fresh from the SMU (0 on a fresh tick).  The families it feeds (power, temperatures, "
+                            "clocks, activity, throttle residency, xGMI/PCIe bytes) are this old; under the auto "
+                            "fetch policy it cycles up to about the min interval", G, {"gpu"});
   f_self_scrape_ = add("gpuexp_scrape_duration_seconds", "Server-side /metrics latency (request parsed -> last byte written)",
                        H, {});
   f_self_scrapes_ = add("gpuexp_scrapes_total", "Scrapes of the metrics path", C, {});
@@ -970,6 +975,7 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
     fresh.fetch_cost_ns = st.fetch_cost_ns;  // the fetch policy's state is the GPU's, not the owner's
     fresh.fetch_cpu_s = st.fetch_cpu_s;
     fresh.fetch_cap_ns = st.fetch_cap_ns;
+    fresh.metrics_fresh_ns = st.metrics_fresh_ns;
     std::copy(std::begin(st.kfd_events), std::end(st.kfd_events), std::begin(fresh.kfd_events));
     fresh.owner = keep;
     fresh.owner_key = okey;
@@ -1642,6 +1648,9 @@ void Engine::emit_self(uint64_t gen) {
       const double cap = cfg_.metrics_min_interval_s < 0 ? double(st.fetch_cap_ns) * 1e-9
                                                           : std::max(0.0, cfg_.metrics_min_interval_s);
       cput(st.fetch_cap, f_self_fetch_cap_, cap, gen, [&] { return std::vector<std::string>{g}; });
+      const double age = st.metrics_fresh_ns && last_tick_now_ >= st.metrics_fresh_ns
+                             ? double(last_tick_now_ - st.metrics_fresh_ns) * 1e-9 : kNaN;
+      cput(st.metrics_age, f_self_metrics_age_, age, gen, [&] { return std::vector<std::string>{g}; });
     }
   cput(self_refs_[12], f_self_source_up_, 1, gen,
        [&] { return std::vector<std::string>{"backend:" + std::string(backend_->name())}; });
@@ -1760,6 +1769,7 @@ void Engine::tick_locked(uint64_t now) {
     st.cur.host_ns = now;
     backend_->sample(devices_[size_t(i)], &st.cur);
     (st.cur.metrics_coalesced ? metrics_coalesced_ : metrics_fresh_)[size_t(i)] += 1;
+    if (st.cur.ok && !st.cur.metrics_coalesced) st.metrics_fresh_ns = now;
     st.ras_ns = st.gtt_ns = 0;
     if (!ras_.empty()) {
       const uint64_t r0 = mono_ns();

@@ -245,6 +245,8 @@ class Engine {
     double fetch_cost_ns = 0;        // EWMA thread CPU of a fresh gpu_metrics read (0 = none yet)
     double fetch_cpu_s = 0;          // thread CPU of every fresh gpu_metrics read so far
     uint64_t fetch_cap_ns = 0;       // cap currently set on the backend's reader
+    uint64_t metrics_fresh_ns = 0;   // tick time of the last fresh gpu_metrics read (0 = none yet)
+    SeriesRef metrics_age;
   };
   // Cached series handles of a (GPU, PID) or a pod, valid while their label values are the
   // ones recorded here: the per-tick path then sets values without building label vectors.
@@ -410,7 +412,7 @@ class Engine {
   uint64_t last_stage_ns_[kStages] = {};
   SeriesRef dev_part_refs_[kDevParts];
   double dev_part_total_s_[kDevParts] = {};  // sampler thread
-  int f_self_dev_part_ = -1, f_self_fetch_cpu_ = -1, f_self_fetch_cap_ = -1;
+  int f_self_dev_part_ = -1, f_self_fetch_cpu_ = -1, f_self_fetch_cap_ = -1, f_self_metrics_age_ = -1;
 };
 
 }  // namespace gpuexp

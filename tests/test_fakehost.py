@@ -664,6 +664,44 @@ def test_gpu_metrics_auto_interval_holds_cpu_budget(native, tmp_path, n_gpus, wa
     assert 100 * cpu / 2.0 <= 1.5 * 1.25, cpu
 
 
+def test_gpu_metrics_freshness_is_one_fetch_per_cap(native, tmp_path):
+    """VERDICT r04 task 3: at 8 GPUs the auto fetch policy caps fresh gpu_metrics reads, so a
+    "100 Hz" exporter refreshes the gpu_metrics families at 1 / cap.  The age gauge and the
+    fresh-read counters say so per GPU: over 4 s of 10 ms ticks every GPU's fresh reads are one
+    per ceil(cap / tick) ticks, and its table is never older than the cap."""
+    import math
+    mi355x_node(tmp_path, 8)
+    e = _engine(native, tmp_path, metrics_min_interval_s=-1.0, metrics_cpu_budget=0.015,
+                fake_metrics_cost_us=SMU_FETCH_CPU_US, metrics_coalesce=False, series_profile="full")
+    tick = 0.01
+    try:
+        for k in range(100):  # 1 s to learn the fetch cost and settle the cap
+            e.tick(S + k * 10_000_000)
+        f0 = promtext.parse(e.snapshot_text())
+        ages = {str(g): [] for g in range(8)}
+        for k in range(100, 500):  # 4 s
+            e.tick(S + k * 10_000_000)
+            f1 = promtext.parse(e.snapshot_text())
+            for _, lab, v in promtext.samples(f1, "gpuexp_gpu_metrics_age_seconds"):
+                ages[lab["gpu"]].append(v)
+    finally:
+        e.stop()
+
+    def fresh(f):
+        return {lab["gpu"]: v for _, lab, v in promtext.samples(f, "gpuexp_gpu_metrics_reads_total")
+                if lab["kind"] == "fresh"}
+
+    caps = {lab["gpu"]: v for _, lab, v in promtext.samples(f1, "gpuexp_gpu_metrics_min_interval_seconds")}
+    n0, n1 = fresh(f0), fresh(f1)
+    for g in map(str, range(8)):
+        cap = caps[g]
+        assert 0.1 < cap < 0.4, caps  # 8 x ~382 us / 1.5 % ~= 0.2 s
+        every = math.ceil(round(cap / tick, 6))  # a fetch every `every` ticks
+        hz = (n1[g] - n0[g]) / 4.0
+        assert abs(hz - 1.0 / (every * tick)) <= 1.0 / 4.0 + 1e-9, (g, hz, cap, every)
+        assert max(ages[g]) <= cap + tick + 1e-9 and min(ages[g]) == 0.0, (g, max(ages[g]), cap)
+
+
 def test_queue_devices_limit_gpu_queues(native, tmp_path):
     """queue_devices picks the GPUs that get the exporter's own GPU queue (sentinel + PMC);
     the others keep every sysfs/amdsmi family."""
