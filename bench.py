@@ -621,6 +621,7 @@ def main() -> int:
 
     xgmi_window: dict = {}
     fresh0: dict = {}  # per-GPU fresh gpu_metrics reads at the start of the timed window
+    counters0: dict = {}  # exporter self counters at the start of the timed window
     window_s = [0.0]
 
     def fresh_reads(fams) -> dict:
@@ -643,8 +644,14 @@ def main() -> int:
                                   promproto.ACCEPT if args.proto else "")
             side.scrape()
             x0 = xgmi_totals(side)
+            f0 = last_fams(side)
             fresh0.clear()
-            fresh0.update(fresh_reads(last_fams(side)))
+            fresh0.update(fresh_reads(f0))
+            for name in ("gpuexp_http_prewake_hits_total", "gpuexp_http_prewake_hits_narrow_total",
+                         "gpuexp_scrapes_total"):
+                v = [x for _, _, x in promtext.samples(f0, name)]
+                if v:
+                    counters0[name] = v[0]
         if dist is not None:
             dist.barrier()
         sync()
@@ -867,6 +874,16 @@ def main() -> int:
             # every timed scrape accounted for: did it reach an HTTP worker that its pre-wake
             # timer had already woken (gpuexp_http_prewake_hits_total), or one asleep in epoll?
             "prewake": prewake_summary(lat, prewoken, splits),
+            # scrapes of the timed window (+ the window-start side scrape) pre-woken under the current
+            # hit window (lead + jitter allowance + one slice) and under round 3's (lead + one slice)
+            "prewake_hits_window": {
+                k: round(next((x for _, _, x in promtext.samples(fams, name)), 0.0) - counters0[name])
+                for k, name in (("hits", "gpuexp_http_prewake_hits_total"),
+                                ("hits_round3_window", "gpuexp_http_prewake_hits_narrow_total"),
+                                ("scrapes", "gpuexp_scrapes_total")) if name in counters0} or None,
+            # exporter settings the run overrode through the environment (A/B arms)
+            "exporter_env": {k: v for k, v in sorted(os.environ.items()) if k.startswith("GPUEXP_")
+                             and k not in ("GPUEXP_BENCH_DUMP_EXPOSITION",)} or None,
             "scrapes": len(lat),
             "scrape_errors": client.errors,
             "scrape_bytes": client.last_bytes,

@@ -712,6 +712,7 @@ PYBIND11_MODULE(_gpuexp, m) {
           d["http_writev_calls"] = hs->writev_calls.load();
           d["http_prewake_timer_wakeups"] = hs->prewake_timer_wakeups.load();
           d["http_prewake_hits"] = hs->prewake_hits.load();
+          d["http_prewake_hits_narrow"] = hs->prewake_hits_narrow.load();
           d["http_writev_ns"] = hs->writev_ns.load();
           d["http_partial_writes"] = hs->partial_writes.load();
           d["http_scrape_ns"] = hs->lat_sum_ns.load();

@@ -394,6 +394,9 @@ void Engine::define_families() {
                              "Scrapes of the metrics path that arrived while their HTTP worker was pre-woken "
                              "(its pre-wake timer fired within the lead + one slice before the request)",
                              C, {});
+  f_self_prewake_hits_narrow_ = add("gpuexp_http_prewake_hits_narrow_total",
+                                    "Pre-woken scrapes under round 3's narrower window (timer fired within the "
+                                    "minimum lead + one slice before the request)", C, {});
   f_self_rx_moves_ = add("gpuexp_http_rx_cpu_moves_total",
                          "Times an HTTP worker moved to the CPU a steady scraper's requests arrive on "
                          "(http follow_rx_cpu; 0 when off)",
@@ -1625,6 +1628,8 @@ void Engine::emit_self(uint64_t gen) {
            none);
       cput(prewake_hits_ref_, f_self_prewake_hits_, double(hs.prewake_hits.load(std::memory_order_relaxed)), gen,
            none);
+      cput(prewake_hits_narrow_ref_, f_self_prewake_hits_narrow_,
+           double(hs.prewake_hits_narrow.load(std::memory_order_relaxed)), gen, none);
     }
     cput(rx_moves_ref_, f_self_rx_moves_, double(hs.rx_cpu_moves.load(std::memory_order_relaxed)), gen, none);
     if (cfg_.http.enable_gzip) {

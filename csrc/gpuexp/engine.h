@@ -407,7 +407,8 @@ class Engine {
       f_self_http_bytes_, f_self_render_bytes_, f_self_series_, f_self_dev_errors_,
       f_self_overruns_, f_self_cpu_, f_self_source_up_, f_self_ctr_scope_, f_self_metrics_reads_, f_self_metrics_period_, f_self_prewake_, f_self_gzip_,
       f_self_rccl_files_, f_self_unresolved_, f_self_ctr_late_ = -1, f_self_rccl_scans_ = -1, f_self_prewake_hits_ = -1, f_self_startup_ = -1;
-  SeriesRef prewake_hits_ref_, startup_ref_;
+  SeriesRef prewake_hits_ref_, prewake_hits_narrow_ref_, startup_ref_;
+  int f_self_prewake_hits_narrow_ = -1;
   SeriesRef self_stage_refs_[kStages];
   uint64_t last_stage_ns_[kStages] = {};
   SeriesRef dev_part_refs_[kDevParts];

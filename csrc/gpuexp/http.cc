@@ -513,6 +513,8 @@ void HttpServer::run(Worker* w) {
         const bool prewoken = last_prewake_ns && t0 >= last_prewake_ns &&
                               t0 - last_prewake_ns <= cfg_.prewake_max_lead_ns + cfg_.prewake_step_ns;
         if (prewoken) stats_.prewake_hits.fetch_add(1, std::memory_order_relaxed);
+        if (prewoken && t0 - last_prewake_ns <= cfg_.prewake_lead_ns + cfg_.prewake_step_ns)
+          stats_.prewake_hits_narrow.fetch_add(1, std::memory_order_relaxed);
         if (c.last_metrics_ns && t0 > c.last_metrics_ns) {
           c.intervals[c.iv_pos] = t0 - c.last_metrics_ns;
           c.iv_pos = (c.iv_pos + 1) & 3;

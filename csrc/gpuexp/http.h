@@ -86,6 +86,9 @@ struct HttpStats {
   // within prewake_max_lead_ns + prewake_step_ns before the request): the rest paid a full
   // wake-up from an idle epoll_wait
   std::atomic<uint64_t> prewake_hits{0};
+  // the same with round 3's narrower window (timer within prewake_lead_ns + one slice), so hit
+  // rates stay comparable across the window change
+  std::atomic<uint64_t> prewake_hits_narrow{0};
   // gzip responses the worker compressed itself: the snapshot had no gzip copy because no
   // gzip scrape was expected before the next tick (see HttpServer::gzip_due)
   std::atomic<uint64_t> gzip_on_demand{0};
