@@ -156,6 +156,9 @@ struct ProcSample {
   double evicted_ms = kNaN;    // accumulated time the process's queues were evicted (KFD stats)
   double gfx_ns = kNaN;        // engine time (amdsmi)
   std::string name;            // comm
+  // The KFD reader's identity of this process: one id per KFD proc entry, never reused, so two
+  // samples with the same id are the same process (0: the sample did not come from KFD)
+  uint64_t kfd_id = 0;
 };
 
 // rocprofiler-sdk device-counting derived values for one GPU over one tick.

@@ -1233,7 +1233,7 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
       if (attr.count(p.pid)) continue;
       ProcAttr a;
       if (cfg_.pod_attribution) {
-        const CgroupInfo* ci = resolver_->resolve(p.pid);
+        const CgroupInfo* ci = resolver_->resolve(p.pid, p.kfd_id);
         if (ci && ci->kube) {
           a.uid = ci->pod_uid;
           auto it = pods_by_uid_.find(ci->pod_uid);
@@ -1869,7 +1869,7 @@ void Engine::tick_locked(uint64_t now) {
     } else if (cfg_.pod_attribution && cfg_.infer_device_owner) {
       std::set<std::tuple<std::string, std::string, std::string>> seen;
       for (auto& p : per_dev[i]) {
-        const CgroupInfo* ci = resolver_->resolve(p.pid);
+        const CgroupInfo* ci = resolver_->resolve(p.pid, p.kfd_id);
         if (!ci || !ci->kube) continue;
         auto pit = pods_by_uid_.find(ci->pod_uid);
         if (pit == pods_by_uid_.end()) {

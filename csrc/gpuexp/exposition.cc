@@ -488,66 +488,62 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
     Family& fam = families_[size_t(fid)];
     Layout& L = layouts_[size_t(fid)];
     fam.dirty = true;  // render()'s per-family text cache is not kept alongside
+    if (fam.dirty_order) {  // a new member: laid out again (sorting first, so GC below keeps order)
+      sort_members(fam);
+      L.relayout = true;
+    }
+    // one pass: GC, liveness, the same live members in the same order as laid out, and the
+    // fields of changed members patched in place (a value that outgrew its field, or a
+    // membership change, lays the family out again)
     bool any_live = false;
-    size_t w = 0;
-    for (size_t i = 0; i < fam.members.size(); ++i) {
+    bool patch = L.valid && !L.relayout;
+    size_t w = 0, k = 0;
+    const size_t nm = fam.members.size();
+    for (size_t i = 0; i < nm; ++i) {
+      if (i + 4 < nm) __builtin_prefetch(&hot_[fam.members[i + 4]]);
       const uint32_t idx = fam.members[i];
-      if (hot_[idx].gen + gc_after < gen) {
-        free_series(idx);
+      const Hot& h = hot_[idx];
+      if (h.gen + gc_after < gen) {
+        free_series(idx);  // (stale: not in the live sequence compared below)
         continue;
       }
       fam.members[w++] = idx;
-      any_live = any_live || hot_[idx].gen == gen;
+      if (h.gen != gen) continue;
+      any_live = true;
+      if (!patch) continue;
+      if (k >= L.members.size() || L.members[k] != idx || L.vers[k] != h.ver) {
+        patch = false;
+        continue;
+      }
+      if (h.stamp != L.stamps[k]) {
+        field_texts(idx);
+        const size_t nf = scratch_len_.size();
+        const TmplField* fl = &L.seg.fields[L.first_field[k]];
+        bool fits = L.first_field[k] + nf <= L.seg.fields.size();
+        for (size_t f = 0; fits && f < nf; ++f) fits = scratch_len_[f] <= fl[f].width;
+        if (!fits) {
+          patch = false;
+          continue;
+        }
+        for (size_t f = 0; f < nf; ++f) {
+          char* dst = &cbody_[L.seg.base + fl[f].off];
+          std::memcpy(dst, &scratch_[32 * f], scratch_len_[f]);
+          std::memset(dst + scratch_len_[f], ' ', fl[f].width - scratch_len_[f]);
+        }
+        L.stamps[k] = h.stamp;
+      }
+      ++k;
     }
     fam.members.resize(w);
     if (!any_live) {
       if (L.valid) rebuild = true;
       L.valid = false;
+      L.relayout = false;
       continue;
     }
-    if (fam.dirty_order) sort_members(fam);
-    if (!L.valid) {
+    if (!patch || k != L.members.size()) {
       L.relayout = true;
       rebuild = true;
-      continue;
-    }
-    // the same live members in the same order as laid out?
-    size_t k = 0;
-    bool same = true;
-    for (uint32_t idx : fam.members) {
-      if (hot_[idx].gen != gen) continue;
-      if (k >= L.members.size() || L.members[k] != idx || L.vers[k] != hot_[idx].ver) {
-        same = false;
-        break;
-      }
-      ++k;
-    }
-    if (!same || k != L.members.size()) {
-      L.relayout = true;
-      rebuild = true;
-      continue;
-    }
-    // patch the fields of changed members in place; a value that outgrew its field lays the
-    // family out again
-    for (size_t m = 0; m < L.members.size(); ++m) {
-      const uint32_t idx = L.members[m];
-      if (hot_[idx].stamp == L.stamps[m]) continue;
-      field_texts(idx);
-      const size_t nf = scratch_len_.size();
-      const TmplField* fl = &L.seg.fields[L.first_field[m]];
-      bool fits = L.first_field[m] + nf <= L.seg.fields.size();
-      for (size_t f = 0; fits && f < nf; ++f) fits = scratch_len_[f] <= fl[f].width;
-      if (!fits) {
-        L.relayout = true;
-        rebuild = true;
-        break;
-      }
-      for (size_t f = 0; f < nf; ++f) {
-        char* dst = &cbody_[L.seg.base + fl[f].off];
-        std::memcpy(dst, &scratch_[32 * f], scratch_len_[f]);
-        std::memset(dst + scratch_len_[f], ' ', fl[f].width - scratch_len_[f]);
-      }
-      L.stamps[m] = hot_[idx].stamp;
     }
   }
   if (rebuild) {

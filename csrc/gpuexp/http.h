@@ -45,8 +45,10 @@ struct HttpConfig {
   // prewake_step_ns slices until it arrives (at most prewake_window_ns past the expected
   // time).  Short sleeps keep the worker's core in a shallow idle state, so the request
   // does not pay a deep-idle exit on the critical path: a few timer wake-ups per scrape
-  // instead of one long sleep, no spinning.
-  bool prewake = true;
+  // instead of one long sleep, no spinning.  Off by default from round 5: five interleaved
+  // on/off pairs at the driver's command did not beat the pair-wise drift in p50 while costing
+  // the HTTP thread ~2x the CPU per scrape (profiles/r05/prewake_ab.txt).
+  bool prewake = false;
   uint64_t prewake_lead_ns = 400000;       // ... at least; twice the connection's period jitter,
   uint64_t prewake_max_lead_ns = 1500000;  // ... at most
   uint64_t prewake_step_ns = 150000;

@@ -5,7 +5,9 @@
 #include <cstring>
 #include <unordered_set>
 
+#include <fcntl.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 namespace gpuexp {
 
@@ -14,6 +16,10 @@ KfdProcReader::KfdProcReader(std::string host_root, int self_pid, bool read_cu_o
     : root_(std::move(host_root)), self_(self_pid), read_cu_(read_cu_occupancy), read_sdma_(read_sdma),
       detail_every_ns_(detail_interval_ns), rescan_ns_(rescan_interval_ns) {
   if (!root_.empty() && root_.back() == '/') root_.pop_back();
+}
+
+KfdProcReader::~KfdProcReader() {
+  if (dir_fd_ >= 0) ::close(dir_fd_);
 }
 
 void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
@@ -27,7 +33,13 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
   // keeps attributes), at least every rescan_ns, and whenever a tracked process vanished;
   // in between, read the tracked processes' files only (an exited process's reads fail).
   struct stat sb {};
-  const bool have_mtime = ::stat(base.c_str(), &sb) == 0;
+  if (dir_fd_ < 0) dir_fd_ = ::open(base.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+  bool have_mtime = dir_fd_ >= 0 && ::fstat(dir_fd_, &sb) == 0;
+  if (have_mtime && sb.st_nlink == 0) {  // the directory itself was removed (KFD reloaded): reopen
+    ::close(dir_fd_);
+    dir_fd_ = ::open(base.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+    have_mtime = dir_fd_ >= 0 && ::fstat(dir_fd_, &sb) == 0;
+  }
   const bool moved = have_mtime && (sb.st_mtim.tv_sec != mtime_.tv_sec || sb.st_mtim.tv_nsec != mtime_.tv_nsec);
   if (have_mtime) mtime_ = sb.st_mtim;
   const bool list = !now_ns || !rescan_ns_ || moved || relist_ || now_ns - last_list_ns_ >= rescan_ns_ ||
@@ -71,6 +83,7 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
       std::string comm;
       if (read_small_file(root_ + "/proc/" + name + "/comm", &comm, 64)) e.comm = trim(comm);
       e.probe_ns = now_ns;
+      e.id = ++next_id_;
       return pids_.insert_or_assign(pid, std::move(e)).first;
     };
     auto it = pids_.find(pid);
@@ -140,6 +153,7 @@ int KfdProcReader::emit(Entry& e, int pid, std::vector<std::vector<ProcSample>>*
       ps.sdma_us = pd.sdma_last;
       ps.evicted_ms = pd.evicted_last;
       ps.name = e.comm;
+      ps.kfd_id = e.id;
       (*per_dev)[size_t(pd.dev)].push_back(ps);
     }
   }
@@ -331,7 +345,7 @@ bool PidResolver::read_starttime(int pid, uint64_t* st) {
   return parse_u64(s.c_str() + i, s.size() - i, st);
 }
 
-const CgroupInfo* PidResolver::resolve(int pid) {
+const CgroupInfo* PidResolver::resolve(int pid, uint64_t kfd_id) {
   auto ov = overrides_.find(pid);
   if (ov != overrides_.end()) {
     Entry& e = cache_[pid];
@@ -350,10 +364,15 @@ const CgroupInfo* PidResolver::resolve(int pid) {
   if (it != cache_.end() && it->second.ok) {
     Entry& e = it->second;
     if (e.epoch == epoch_) return &e.info;  // already checked this tick
+    if (kfd_id && e.kfd_id == kfd_id) {     // KFD read this same process this tick
+      e.epoch = epoch_;
+      return &e.info;
+    }
     char b[32];
     const bool alive = !e.comm || e.comm->read(b, sizeof(b)) > 0;
     if (alive && now_ns_ >= e.st_checked_ns && now_ns_ - e.st_checked_ns < kStarttimeEveryNs) {
       e.epoch = epoch_;
+      if (kfd_id) e.kfd_id = kfd_id;
       return &e.info;
     }
     uint64_t st = 0;
@@ -366,6 +385,7 @@ const CgroupInfo* PidResolver::resolve(int pid) {
       // Never replaced by a failed lookup.
       e.epoch = epoch_;
       e.st_checked_ns = now_ns_;
+      if (kfd_id && have_st) e.kfd_id = kfd_id;  // (a gone process is not vouched for by KFD)
       return &e.info;
     }
   }
@@ -388,6 +408,7 @@ const CgroupInfo* PidResolver::resolve(int pid) {
   e.st_checked_ns = now_ns_;
   e.comm = std::make_shared<CachedFile>();
   if (!e.comm->open(dir + "/comm")) e.comm.reset();
+  e.kfd_id = kfd_id;
   parse_proc_cgroup(content, &e.info);
   return &e.info;
 }

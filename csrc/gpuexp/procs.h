@@ -29,6 +29,9 @@ class KfdProcReader {
   // read_sdma: also read sdma_<id> (the engine's kfd_sdma; off by default, see EngineConfig).
   KfdProcReader(std::string host_root, int self_pid, bool read_cu_occupancy, uint64_t detail_interval_ns = 0,
                 uint64_t rescan_interval_ns = 0, bool read_sdma = true);
+  ~KfdProcReader();
+  KfdProcReader(const KfdProcReader&) = delete;
+  KfdProcReader& operator=(const KfdProcReader&) = delete;
   // Fills per_dev[d] with the processes that have a KFD context on device d.
   void scan(const std::vector<DeviceInfo>& devs, std::vector<std::vector<ProcSample>>* per_dev,
             uint64_t now_ns = 0);
@@ -50,6 +53,7 @@ class KfdProcReader {
     int comm_tries = 0;  // re-reads of an empty comm at later listings
     uint64_t probe_ns = 0;  // last look for GPUs it had no files for
     uint64_t seen = 0;
+    uint64_t id = 0;        // ProcSample::kfd_id
   };
   static constexpr int kCommTries = 3;
   static constexpr uint64_t kReprobeNs = 1000000000ull;
@@ -64,7 +68,8 @@ class KfdProcReader {
   uint64_t last_list_ns_ = 0;
   bool relist_ = false;          // a tracked process vanished: list at the next scan
   timespec mtime_{};             // the directory's mtime at the last look
-  uint64_t scan_no_ = 0, lists_ = 0;
+  int dir_fd_ = -1;              // the KFD proc directory, kept open: fstat per scan, no path walk
+  uint64_t scan_no_ = 0, lists_ = 0, next_id_ = 0;
   std::unordered_map<int, Entry> pids_;
 };
 
@@ -101,7 +106,10 @@ class PidResolver {
   }
   // Returns nullptr if the PID cannot be read (other PID namespace, exited).  A failure is
   // remembered: the PID is not looked up again within the tick nor for kRetryFailedNs.
-  const CgroupInfo* resolve(int pid);
+  // `kfd_id` (ProcSample::kfd_id, 0 = none): the KFD reader read this very process this tick.
+  // A cached entry checked under the same id needs no liveness read: the id outlives neither
+  // the process nor a reuse of its PID (KfdProcReader re-creates the entry for either).
+  const CgroupInfo* resolve(int pid, uint64_t kfd_id = 0);
   // Test/bench hook: pretend /proc/<pid>/cgroup contains `cgroup_path`.
   void set_override(int pid, const std::string& cgroup_path);
   void clear_overrides();
@@ -116,6 +124,7 @@ class PidResolver {
     uint64_t epoch = 0;                // tick it was last checked in
     uint64_t st_checked_ns = 0;        // engine time of the last starttime check
     uint64_t failed_ns = 0;            // !ok: engine time of the failed lookup
+    uint64_t kfd_id = 0;               // KFD identity it was last checked under (0 = none)
   };
   bool read_starttime(int pid, uint64_t* st);
   static constexpr uint64_t kStarttimeEveryNs = 1000000000ull;

@@ -23,7 +23,8 @@ class Config:
     path: str = "/metrics"                 # main.go:70
     http_threads: int = 1
     gzip: bool = True
-    http_prewake: bool = True              # wake shortly before a steady scraper's next request
+    http_prewake: bool = False             # wake shortly before a steady scraper's next request (off: no
+                                           # p50 gain beyond run-to-run drift, profiles/r05/prewake_ab.txt)
     stale_after: float = -1.0              # /readyz 503 when the newest sample is older (s); -1 = auto
                                            # (max(5 s, 10 intervals)), 0 = never
     # sampling

@@ -228,6 +228,16 @@ class FakeHost:
 
     def remove_process(self, pid: int) -> None:
         import shutil
+        # As on the real filesystems, files a reader still holds open stop reading once the
+        # process is gone (sysfs: the KFD kobject is removed, -ENODEV; procfs: -ESRCH), where
+        # an unlinked tmpfs file would keep its old contents: empty them first.
+        for d in (self.root / f"sys/class/kfd/kfd/proc/{pid}", self.root / f"proc/{pid}"):
+            for f in d.rglob("*") if d.exists() else ():
+                if f.is_file():
+                    try:
+                        f.write_bytes(b"")
+                    except OSError:
+                        pass
         shutil.rmtree(self.root / f"sys/class/kfd/kfd/proc/{pid}", ignore_errors=True)
         shutil.rmtree(self.root / f"proc/{pid}", ignore_errors=True)
 

@@ -457,6 +457,7 @@ def test_prewake_survives_one_late_scrape(native):
     c.interval_s = 0
     c.http.host = "127.0.0.1"
     c.http.port = 0
+    c.http.prewake = True  # (off by default)
     e = native.Engine(c)
     e.start()
     try:

@@ -31,6 +31,52 @@ def build_lib() -> str:
     return out
 
 
+def leaf_lines(path: str, func: str, top: int = 25):
+    """Source lines of the leaf PCs whose innermost frame is `func` (addr2line -i)."""
+    samples, maps = [], []
+    with open(path) as f:
+        in_maps = False
+        for line in f:
+            if line.startswith("MAPS"):
+                in_maps = True
+                continue
+            if not in_maps:
+                samples.append([int(x, 16) for x in line.split()])
+            else:
+                p = line.split()
+                if len(p) >= 6 and "x" in p[1]:
+                    a, b = (int(x, 16) for x in p[0].split("-"))
+                    maps.append((a, b, int(p[2], 16), p[5]))
+    maps.sort()
+    starts = [m[0] for m in maps]
+    cnt = collections.Counter()
+    for s in samples:
+        if len(s) < 3:
+            continue
+        pc = s[2]
+        i = bisect.bisect_right(starts, pc) - 1
+        if i >= 0 and pc < maps[i][1]:
+            cnt[(maps[i][3], pc - maps[i][0] + maps[i][2])] += 1
+    by_file = collections.defaultdict(list)
+    for (fn, off), k in cnt.items():
+        by_file[fn].append((off, k))
+    lines = collections.Counter()
+    for fn, lst in by_file.items():
+        if not fn.startswith("/") or not os.path.exists(fn):
+            continue
+        r = subprocess.run(["addr2line", "-f", "-C", "-e", fn] + [hex(o) for o, _ in lst],
+                           capture_output=True, text=True).stdout.splitlines()
+        for j, (o, k) in enumerate(lst):
+            if 2 * j + 1 >= len(r):
+                break
+            name, loc = r[2 * j], r[2 * j + 1]
+            if func in name:
+                lines[loc.split("/")[-1]] += k
+    tot = sum(lines.values()) or 1
+    for loc, k in lines.most_common(top):
+        print(f"{100 * k / tot:6.1f}  {loc}")
+
+
 def symbolize(path: str):
     samples, maps = [], []
     with open(path) as f:
@@ -92,6 +138,7 @@ def main() -> int:
                     help="sleep between ticks (a sampler wakes with cold caches; 0 = back-to-back)")
     ap.add_argument("--gzip", action="store_true", help="serve HTTP with a 100 Hz gzip scraper (another process)")
     ap.add_argument("--exposition", default="compiled")
+    ap.add_argument("--lines", default="", help="also print the source lines of leaf samples in this function")
     args = ap.parse_args()
     lib = ctypes.CDLL(build_lib())
     import test_fakehost as tf
@@ -155,6 +202,9 @@ def main() -> int:
     print(f"\n{'incl%':>6}  function")
     for f, k in incl_c.most_common(args.top):
         print(f"{100 * k / tot:6.1f}  {f[:150]}")
+    if args.lines:
+        print(f"\nleaf source lines in {args.lines}:")
+        leaf_lines(trace, args.lines)
     return 0
 
 
