@@ -560,6 +560,8 @@ PYBIND11_MODULE(_gpuexp, m) {
       }, py::arg("gen"), py::arg("gc_after") = 1, py::arg("gzip") = true,
          "(text, gzip bytes) of the fixed-layout renderer")
       .def("last_relayouts", &SeriesTable::last_relayouts)
+      .def("last_skipped", &SeriesTable::last_skipped)
+      .def("library_gzips", &SeriesTable::library_gzips)
       .def("code_builds", &SeriesTable::code_builds)
       .def("set_histogram", [](SeriesTable& t, int fid, std::vector<std::string> labels, std::vector<double> bounds,
                                std::vector<uint64_t> counts, double sum, uint64_t count, uint64_t gen) {

@@ -271,6 +271,7 @@ void TemplateDeflate::parse(const char* body, const std::vector<TmplSegment*>& s
     seg->piece_bits.clear();
     seg->deps.clear();
     seg->code_epoch = 0;
+    seg->splice_valid = false;
     const uint32_t start = uint32_t(seg->base - w0);
     const uint32_t seg_end = start + uint32_t(seg->len);
     uint32_t min_src = start;
@@ -501,6 +502,48 @@ void TemplateDeflate::encode_static(const char* body, TmplSegment* seg) const {
   seg->field_bytes = 0;
   for (const TmplField& f : seg->fields) seg->field_bytes += f.width;
   seg->code_epoch = code_epoch_;
+  seg->splice_valid = false;
+}
+
+void TemplateDeflate::splice(const char* body, TmplSegment* seg) const {
+  // bound: the static bits, 15 bits per field byte, and room for the writer's 8-byte stores
+  seg->spliced.assign((seg->static_bits + 15 * seg->field_bytes) / 64 + 3, 0);
+  unsigned char* start = reinterpret_cast<unsigned char*>(seg->spliced.data());
+  BitWriter bw(start);
+  const uint64_t* w = seg->words.data();
+  const unsigned char* s = reinterpret_cast<const unsigned char*>(body) + seg->base;
+  const size_t npieces = seg->piece_bits.size();
+  for (size_t i = 0; i < npieces; ++i) {
+    const size_t nb = seg->piece_bits[i];
+    bw.put_words(w, nb);
+    w += (nb + 63) >> 6;
+    if (i == seg->fields.size()) break;
+    const TmplField& f = seg->fields[i];
+    const unsigned char* fp = s + f.off;
+    uint32_t k = 0;
+    for (; k < f.width && fp[k] != ' '; ++k) {
+      const Code& c = lit_[fp[k]];
+      bw.put(c.code, c.len);
+    }
+    uint32_t pad = f.width - k;
+    while (pad > 64) {  // only for absurd widths
+      bw.put(pad_bits_[64] & 0xffffffffu, std::min<unsigned>(32, pad_len_[64]));
+      if (pad_len_[64] > 32) bw.put(pad_bits_[64] >> 32, pad_len_[64] - 32u);
+      pad -= 64;
+    }
+    if (pad) {
+      const unsigned pl = pad_len_[pad];
+      if (pl > 32) {
+        bw.put(pad_bits_[pad] & 0xffffffffu, 32);
+        bw.put(pad_bits_[pad] >> 32, pl - 32);
+      } else {
+        bw.put(pad_bits_[pad], pl);
+      }
+    }
+  }
+  seg->spliced_bits = size_t(bw.p - start) * 8 + bw.n;
+  if (bw.n) std::memcpy(bw.p, &bw.acc, 8);  // the pending bits (the rest of the buffer is zero)
+  seg->splice_valid = true;
 }
 
 void TemplateDeflate::encode_gzip(const char* body, size_t body_len, uint32_t crc,
@@ -533,40 +576,10 @@ void TemplateDeflate::encode_gzip(const char* body, size_t body_len, uint32_t cr
   };
   for (TmplSegment* seg : segs) {
     literals(pos, seg->base);  // bytes between segments (none when segments tile the body)
-    const uint64_t* w = seg->words.data();
-    const unsigned char* s = b + seg->base;
-    const size_t npieces = seg->piece_bits.size();
-    for (size_t i = 0; i < npieces; ++i) {
-      const size_t nb = seg->piece_bits[i];
-      bw.put_words(w, nb);
-      w += (nb + 63) >> 6;
-      if (i == seg->fields.size()) break;
-      const TmplField& f = seg->fields[i];
-      const unsigned char* fp = s + f.off;
-      uint32_t k = 0;
-      for (; k < f.width && fp[k] != ' '; ++k) {
-        const Code& c = lit_[fp[k]];
-        bw.put(c.code, c.len);
-        field_bits += c.len;
-      }
-      uint32_t pad = f.width - k;
-      while (pad > 64) {  // only for absurd widths
-        bw.put(pad_bits_[64] & 0xffffffffu, std::min<unsigned>(32, pad_len_[64]));
-        if (pad_len_[64] > 32) bw.put(pad_bits_[64] >> 32, pad_len_[64] - 32u);
-        pad -= 64;
-      }
-      if (pad) {
-        const unsigned pl = pad_len_[pad];
-        if (pl > 32) {
-          bw.put(pad_bits_[pad] & 0xffffffffu, 32);
-          bw.put(pad_bits_[pad] >> 32, pl - 32);
-        } else {
-          bw.put(pad_bits_[pad], pl);
-        }
-        field_bits += pl;
-      }
-    }
+    if (!seg->splice_valid) splice(body, seg);
+    bw.put_words(seg->spliced.data(), seg->spliced_bits);
     static_bits += seg->static_bits;
+    field_bits += seg->spliced_bits - seg->static_bits;
     pos = seg->base + seg->len;
   }
   literals(pos, body_len);

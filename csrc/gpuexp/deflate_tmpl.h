@@ -50,6 +50,12 @@ struct TmplSegment {
   uint64_t code_epoch = 0;           // epoch of the code `words` were encoded with
   size_t static_bits = 0;            // sum of piece_bits
   size_t field_bytes = 0;            // sum of field widths
+  // The segment's whole bit string (static pieces + the fields' bytes as they stand), kept
+  // between encodes: the owner clears splice_valid when it patches a field; parse and a new
+  // code clear it too.  An unchanged segment is then one spliced copy per encode.
+  std::vector<uint64_t> spliced;
+  size_t spliced_bits = 0;
+  bool splice_valid = false;
   bool parsed = false;
   // Matches may reach back into preceding segments' static bytes: the parse is valid while the
   // same segments, at the same layout versions, precede this one (nearest first).
@@ -85,6 +91,7 @@ class TemplateDeflate {
 
  private:
   void encode_static(const char* body, TmplSegment* seg) const;
+  void splice(const char* body, TmplSegment* seg) const;
   struct Code {
     uint16_t code = 0;  // bit-reversed (deflate writes Huffman codes MSB-first into an LSB-first stream)
     uint8_t len = 0;

@@ -1,5 +1,7 @@
 #include "gpuexp/exposition.h"
 
+#include "gpuexp/snapshot.h"  // gzip_compress
+
 #include <cstring>
 
 #include <algorithm>
@@ -9,25 +11,25 @@
 
 namespace gpuexp {
 
-void append_value(std::string* out, double v) {
+size_t format_value(char* buf, double v) {
   if (std::isnan(v)) {
-    out->append("NaN");
-    return;
+    std::memcpy(buf, "NaN", 3);
+    return 3;
   }
   if (std::isinf(v)) {
-    out->append(v > 0 ? "+Inf" : "-Inf");
-    return;
+    std::memcpy(buf, v > 0 ? "+Inf" : "-Inf", 4);
+    return 4;
   }
-  char buf[40];
   // Integral values (bytes, counts, PIDs) print without exponent, like Go's
   // strconv 'g' for <1e21 only when they are short; Prometheus parses either form.
-  if (v == std::floor(v) && std::fabs(v) < 9007199254740992.0) {
-    auto r = std::to_chars(buf, buf + sizeof(buf), static_cast<long long>(v));
-    out->append(buf, r.ptr);
-    return;
-  }
-  auto r = std::to_chars(buf, buf + sizeof(buf), v);
-  out->append(buf, r.ptr);
+  if (v == std::floor(v) && std::fabs(v) < 9007199254740992.0)
+    return size_t(std::to_chars(buf, buf + 40, static_cast<long long>(v)).ptr - buf);
+  return size_t(std::to_chars(buf, buf + 40, v).ptr - buf);
+}
+
+void append_value(std::string* out, double v) {
+  char buf[40];
+  out->append(buf, format_value(buf, v));
 }
 
 void append_escaped_label_value(std::string* out, const std::string& v) {
@@ -80,6 +82,7 @@ int SeriesTable::add_family(const FamilyDef& def) {
   static const char* tn[] = {"gauge", "counter", "histogram"};
   f.header += "\n# TYPE " + def.name + " " + tn[int(def.type)] + "\n";
   families_.push_back(std::move(f));
+  fam_hot_.emplace_back();
   int fid = int(families_.size() - 1);
   render_order_.push_back(fid);
   std::sort(render_order_.begin(), render_order_.end(), [this](int a, int b) {
@@ -123,6 +126,7 @@ SeriesRef SeriesTable::upsert(int fid, const std::vector<std::string>& values) {
   h.gen = 0;
   h.value = 0;
   h.in_cache = false;
+  h.laid = false;
   h.stamp += 1;
   s.widths.clear();
   s.labels = values;
@@ -149,8 +153,10 @@ SeriesRef SeriesTable::upsert(int fid, const std::vector<std::string>& values) {
   s.hlines.clear();
   index_.emplace(s.key, idx);
   fam.members.push_back(idx);
-  fam.dirty_order = true;
-  fam.dirty = true;
+  FamHot& fh = fam_hot_[size_t(fid)];
+  fh.nmembers += 1;
+  fh.dirty_order = true;
+  fh.dirty = true;
   return SeriesRef{idx, h.ver};
 }
 
@@ -161,12 +167,8 @@ bool SeriesTable::set(SeriesRef r, double v, uint64_t gen) {
   uint64_t a, b;
   std::memcpy(&a, &h.value, sizeof(a));
   std::memcpy(&b, &v, sizeof(b));
-  if (a != b) {
-    h.value = v;
-    h.stamp += 1;
-    mark_dirty(h.fid);
-  }
-  h.gen = gen;
+  if (a != b) h.value = v;
+  note_set(h, gen, a != b);
   return true;
 }
 
@@ -174,7 +176,7 @@ bool SeriesTable::touch(SeriesRef r, uint64_t gen) {
   if (!r.valid() || r.idx >= hot_.size()) return false;
   Hot& h = hot_[r.idx];
   if (h.ver != r.ver || h.fid < 0) return false;
-  h.gen = gen;
+  note_set(h, gen, false);
   return true;
 }
 
@@ -193,9 +195,7 @@ bool SeriesTable::observe(SeriesRef r, double v, uint64_t gen, const std::vector
   if (it != s.bounds.end()) s.buckets[size_t(it - s.bounds.begin())] += 1;
   s.hsum += v;
   s.hcount += 1;
-  h.gen = gen;
-  h.stamp += 1;
-  mark_dirty(h.fid);
+  note_set(h, gen, true);
   return true;
 }
 
@@ -219,11 +219,7 @@ bool SeriesTable::set_histogram(SeriesRef r, const std::vector<double>& bounds,
   }
   s.hsum = sum;
   s.hcount = count;
-  h.gen = gen;
-  if (changed) {
-    h.stamp += 1;
-    mark_dirty(h.fid);
-  }
+  note_set(h, gen, changed);
   return true;
 }
 
@@ -238,10 +234,16 @@ void SeriesTable::free_series(uint32_t idx) {
   Hot& h = hot_[idx];
   Series& s = series_[idx];
   index_.erase(s.key);
-  if (h.fid >= 0) mark_dirty(h.fid);
+  if (h.fid >= 0) {
+    FamHot& f = fam_hot_[size_t(h.fid)];
+    f.dirty = true;
+    f.nmembers -= 1;
+    if (h.laid) f.laid_valid = false;  // (cannot happen while laid: only stale members are freed)
+  }
   h.fid = -1;
   h.ver += 1;
   h.in_cache = false;
+  h.laid = false;
   h.stamp += 1;
   s.widths.clear();
   s.labels.clear();
@@ -255,7 +257,8 @@ void SeriesTable::free_series(uint32_t idx) {
   free_.push_back(idx);
 }
 
-void SeriesTable::sort_members(Family& f) {
+void SeriesTable::sort_members(int fid) {
+  Family& f = families_[size_t(fid)];
   std::sort(f.members.begin(), f.members.end(), [this](uint32_t a, uint32_t b) {
     const auto& la = series_[a].labels;
     const auto& lb = series_[b].labels;
@@ -270,8 +273,18 @@ void SeriesTable::sort_members(Family& f) {
     }
     return false;
   });
-  f.dirty_order = false;
-  f.dirty = true;
+  fam_hot_[size_t(fid)].dirty_order = false;
+  fam_hot_[size_t(fid)].dirty = true;
+}
+
+void SeriesTable::unlay(int fid) {
+  Layout& L = layouts_[size_t(fid)];
+  for (const LaidMember& m : L.members) {
+    Hot& h = hot_[m.idx];
+    if (h.ver == m.ver && h.fid == fid) h.laid = false;
+  }
+  fam_hot_[size_t(fid)].laid_valid = false;
+  fam_hot_[size_t(fid)].nlaid = 0;
 }
 
 void SeriesTable::format_cached(uint32_t idx) {
@@ -280,10 +293,10 @@ void SeriesTable::format_cached(uint32_t idx) {
   uint64_t bits;
   std::memcpy(&bits, &v, sizeof(bits));
   if (!s.vvalid || bits != s.vbits) {
-    std::string tmp;
-    append_value(&tmp, v);
-    s.vlen = uint8_t(std::min(tmp.size(), sizeof(s.vtxt)));
-    std::memcpy(s.vtxt, tmp.data(), s.vlen);
+    char buf[40];
+    const size_t n = format_value(buf, v);
+    s.vlen = uint8_t(std::min(n, sizeof(s.vtxt)));
+    std::memcpy(s.vtxt, buf, s.vlen);
     s.vbits = bits;
     s.vvalid = true;
   }
@@ -362,7 +375,7 @@ void SeriesTable::render(std::string* out, uint64_t gen, uint64_t gc_after) {
       fam.members[w++] = idx;
       const bool live = h.gen == gen;
       any_live = any_live || live;
-      if (live != h.in_cache) fam.dirty = true;
+      if (live != h.in_cache) fam_hot_[size_t(fid)].dirty = true;
     }
     fam.members.resize(w);
     if (!any_live) {
@@ -370,11 +383,11 @@ void SeriesTable::render(std::string* out, uint64_t gen, uint64_t gc_after) {
         fam.cache.clear();
         for (uint32_t idx : fam.members) hot_[idx].in_cache = false;
       }
-      fam.dirty = false;
+      fam_hot_[size_t(fid)].dirty = false;
       continue;
     }
-    if (fam.dirty_order) sort_members(fam);
-    if (fam.dirty) {
+    if (fam_hot_[size_t(fid)].dirty_order) sort_members(fid);
+    if (fam_hot_[size_t(fid)].dirty) {
       ++last_rebuilt_;
       fam.cache.clear();
       fam.cache.append(fam.header);
@@ -390,7 +403,7 @@ void SeriesTable::render(std::string* out, uint64_t gen, uint64_t gc_after) {
         append_cached_value(&fam.cache, idx);
         fam.cache.push_back('\n');
       }
-      fam.dirty = false;
+      fam_hot_[size_t(fid)].dirty = false;
     }
     out->append(fam.cache);
   }
@@ -418,21 +431,19 @@ void SeriesTable::field_texts(uint32_t idx) {
     cum = i < s.bounds.size() ? cum + s.buckets[i] : s.hcount;
     put_u64(i, cum);
   }
-  std::string tmp;
-  append_value(&tmp, s.hsum);
+  char tmp[40];
+  const size_t tn = format_value(tmp, s.hsum);
   const size_t fs = s.bounds.size() + 1;
-  scratch_len_[fs] = uint8_t(std::min<size_t>(tmp.size(), 32));
-  std::memcpy(&scratch_[32 * fs], tmp.data(), scratch_len_[fs]);
+  scratch_len_[fs] = uint8_t(std::min<size_t>(tn, 32));
+  std::memcpy(&scratch_[32 * fs], tmp, scratch_len_[fs]);
   put_u64(fs + 1, s.hcount);
 }
 
 void SeriesTable::layout_family(int fid, uint64_t gen, std::string* body) {
   Family& fam = families_[size_t(fid)];
   Layout& L = layouts_[size_t(fid)];
+  unlay(fid);
   L.members.clear();
-  L.vers.clear();
-  L.first_field.clear();
-  L.stamps.clear();
   L.seg.fields.clear();
   const size_t base = body->size();
   body->append(fam.header);
@@ -445,16 +456,16 @@ void SeriesTable::layout_family(int fid, uint64_t gen, std::string* body) {
     const size_t nf = scratch_len_.size();
     if (s.widths.size() != nf) s.widths.assign(nf, 0);
     if (hist) build_hlines(idx);
-    L.members.push_back(idx);
-    L.vers.push_back(h.ver);
-    L.first_field.push_back(uint32_t(L.seg.fields.size()));
-    L.stamps.push_back(h.stamp);
+    L.members.push_back({idx, h.ver, h.stamp, uint32_t(L.seg.fields.size())});
+    h.laid = true;
     for (size_t f = 0; f < nf; ++f) {
       body->append(hist ? s.hlines[f] : s.line);
       const uint8_t len = scratch_len_[f];
-      if (s.widths[f] && len > s.widths[f]) {
-        // outgrown: a field that changes length once will again -- leave room (an integer two more
-        // digits, a fraction the typical longest shortest-round-trip form) so it settles
+      // Room to grow, so the body settles within a few ticks: a field that outgrew its width (and
+      // a counter's or histogram's from the start: they only grow) gets two more digits if it is
+      // an integer, the typical longest shortest-round-trip form (20) if it is a fraction.
+      const bool grows = s.widths[f] ? len > s.widths[f] : fam.def.type != MetricType::kGauge;
+      if (grows) {
         const char* t = &scratch_[32 * f];
         const bool frac = std::memchr(t, '.', len) || std::memchr(t, 'e', len);
         s.widths[f] = uint8_t(std::min<int>(32, frac ? std::max<int>(len, 20) : len + 2));
@@ -470,26 +481,47 @@ void SeriesTable::layout_family(int fid, uint64_t gen, std::string* body) {
   L.seg.len = body->size() - base;
   L.seg.parsed = false;
   L.seg.code_epoch = 0;
+  L.seg.splice_valid = false;
   L.seg.layout_ver += 1;
   L.valid = true;
   L.relayout = false;
+  FamHot& fh = fam_hot_[size_t(fid)];
+  fh.laid_valid = true;
+  fh.nlaid = uint32_t(L.members.size());
+  // this generation's counts as the layout sees them (every member laid out is live now)
+  fh.live_laid = fh.gen == gen ? uint32_t(L.members.size()) : 0;
 }
 
 void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t gen, uint64_t gc_after) {
   last_rebuilt_ = 0;
   last_relayouts_ = 0;
+  last_skipped_ = 0;
   bool rebuild = false;  // some family is laid out again, appears or disappears
   if (layouts_.size() != families_.size()) {
     layouts_.resize(families_.size());  // csegs_ points into layouts_: rebuilt below
-    for (auto& L : layouts_) L.valid = false;
+    for (size_t f = 0; f < layouts_.size(); ++f) {
+      layouts_[f].valid = false;
+      fam_hot_[f].laid_valid = false;
+    }
     rebuild = true;
   }
+  // Families can be passed over by their FamHot counts alone only if every generation since the
+  // last pass was rendered (a skipped publish would leave its changes unpatched).
+  const bool consecutive = compiled_gen_ && gen == compiled_gen_ + 1;
+  compiled_gen_ = gen;
   for (int fid : render_order_) {
+    FamHot& fh = fam_hot_[size_t(fid)];
+    // unchanged since the last pass: every laid-out member set again, none changed, no other
+    // member live or waiting for GC
+    if (consecutive && fh.laid_valid && !fh.dirty_order && fh.gen == gen && fh.changed == 0 &&
+        fh.live == fh.nlaid && fh.live_laid == fh.nlaid && fh.nmembers == fh.nlaid) {
+      ++last_skipped_;
+      continue;
+    }
     Family& fam = families_[size_t(fid)];
     Layout& L = layouts_[size_t(fid)];
-    fam.dirty = true;  // render()'s per-family text cache is not kept alongside
-    if (fam.dirty_order) {  // a new member: laid out again (sorting first, so GC below keeps order)
-      sort_members(fam);
+    if (fh.dirty_order) {  // a new member: laid out again (sorting first, so GC below keeps order)
+      sort_members(fid);
       L.relayout = true;
     }
     // one pass: GC, liveness, the same live members in the same order as laid out, and the
@@ -511,15 +543,16 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
       if (h.gen != gen) continue;
       any_live = true;
       if (!patch) continue;
-      if (k >= L.members.size() || L.members[k] != idx || L.vers[k] != h.ver) {
+      if (k >= L.members.size() || L.members[k].idx != idx || L.members[k].ver != h.ver) {
         patch = false;
         continue;
       }
-      if (h.stamp != L.stamps[k]) {
+      LaidMember& lm = L.members[k];
+      if (h.stamp != lm.stamp) {
         field_texts(idx);
         const size_t nf = scratch_len_.size();
-        const TmplField* fl = &L.seg.fields[L.first_field[k]];
-        bool fits = L.first_field[k] + nf <= L.seg.fields.size();
+        const TmplField* fl = &L.seg.fields[lm.first_field];
+        bool fits = lm.first_field + nf <= L.seg.fields.size();
         for (size_t f = 0; fits && f < nf; ++f) fits = scratch_len_[f] <= fl[f].width;
         if (!fits) {
           patch = false;
@@ -530,13 +563,17 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
           std::memcpy(dst, &scratch_[32 * f], scratch_len_[f]);
           std::memset(dst + scratch_len_[f], ' ', fl[f].width - scratch_len_[f]);
         }
-        L.stamps[k] = h.stamp;
+        lm.stamp = h.stamp;
+        L.seg.splice_valid = false;
       }
       ++k;
     }
     fam.members.resize(w);
     if (!any_live) {
-      if (L.valid) rebuild = true;
+      if (L.valid) {
+        rebuild = true;
+        unlay(fid);
+      }
       L.valid = false;
       L.relayout = false;
       continue;
@@ -547,6 +584,8 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
     }
   }
   if (rebuild) {
+    parse_check_ = true;  // (checked at the next gzip encode, which may be ticks later)
+    rebuild_gen_ = gen;
     cbody_next_.clear();
     csegs_.clear();
     for (int fid : render_order_) {
@@ -568,9 +607,18 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
   }
   out->assign(cbody_);
   if (!gz) return;
+  // While the layout still moves (warm-up: values reaching their widths; a process appearing)
+  // the whole body goes through the library compressor: a parse costs more than one
+  // compression, and would be thrown away by the next layout change.  After kStableRenders
+  // renders without a layout change the changed segments are parsed once.
+  if (parse_check_ && gen - rebuild_gen_ < kStableRenders) {
+    if (!gzip_compress(cbody_, gz, 1)) gz->clear();
+    ++library_gzips_;
+    return;
+  }
   // (re-)parse laid-out segments and those whose matches reached into a segment laid out
-  // since; consecutive ones as one run
-  for (size_t i = 0; i < csegs_.size();) {
+  // since; consecutive ones as one run (only after a rebuild: otherwise every parse stands)
+  for (size_t i = 0; parse_check_ && i < csegs_.size();) {
     if (TemplateDeflate::parse_valid(csegs_, i)) {
       ++i;
       continue;
@@ -581,6 +629,7 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
     TemplateDeflate::parse(cbody_.data(), csegs_, i, j);
     i = j;
   }
+  parse_check_ = false;
   // The code is complete (any segment encodes under it); it is rebuilt for compression once as
   // many bytes as the body holds were laid out or re-parsed since the last build (a build
   // re-encodes every segment: ~0.7 ms for an 8-GPU body).

@@ -36,6 +36,8 @@ struct SeriesRef {
 // Appends `v` in the shortest round-trip form ("NaN", "+Inf", "-Inf" for specials;
 // integers without exponent up to 2^53).
 void append_value(std::string* out, double v);
+// The same into buf (>= 40 bytes); returns the length.
+size_t format_value(char* buf, double v);
 void append_escaped_label_value(std::string* out, const std::string& v);
 void append_escaped_help(std::string* out, const std::string& v);
 bool valid_metric_name(const std::string& s);
@@ -88,6 +90,8 @@ class SeriesTable {
   void render_compiled(std::string* out, std::string* gz, uint64_t gen, uint64_t gc_after = 1);
   // Families laid out again by the last render_compiled (0 in steady state).
   size_t last_relayouts() const { return last_relayouts_; }
+  size_t last_skipped() const { return last_skipped_; }
+  uint64_t library_gzips() const { return library_gzips_; }
   uint64_t code_builds() const { return code_builds_; }
   const TemplateDeflate& deflater() const { return deflate_; }
 
@@ -108,6 +112,21 @@ class SeriesTable {
     double value = 0;
     bool in_cache = false;  // included in its family's cached text
     uint32_t stamp = 0;     // bumped on every value/histogram change (render_compiled)
+    bool laid = false;      // a member of its family's compiled layout
+  };
+  // Per-family state every set() touches, dense by family id (a few KB: stays in cache through
+  // the series stage), so render_compiled can pass over a family with no change without walking
+  // its members.
+  struct FamHot {
+    uint64_t gen = 0;        // generation of the three counts below
+    uint32_t live = 0;       // members set this generation
+    uint32_t live_laid = 0;  // ... of which in the compiled layout
+    uint32_t changed = 0;    // value / histogram changes this generation
+    uint32_t nmembers = 0;
+    uint32_t nlaid = 0;      // members in the compiled layout (laid_valid)
+    bool laid_valid = false;
+    bool dirty = true;       // render(): the cached text is stale
+    bool dirty_order = false;
   };
   struct Series {  // cold: strings and histogram state
     std::vector<std::string> labels;
@@ -131,22 +150,22 @@ class SeriesTable {
   struct Family {
     FamilyDef def;
     std::string header;              // "# HELP ...\n# TYPE ...\n"
-    std::vector<uint32_t> members;   // sorted by label values
-    bool dirty_order = false;
+    std::vector<uint32_t> members;   // sorted by label values (FamHot::dirty_order: not yet)
     // Rendered text of the family as of the last render.  Re-built only when a member's
-    // value bits, membership or liveness changed; otherwise render copies it whole.
+    // value bits, membership or liveness changed (FamHot::dirty); otherwise render copies it.
     std::string cache;
-    bool dirty = true;
   };
   // render_compiled state of one family: its live members as laid out, its segment of the
   // body, and per member the fields it owns and the stamp they were written with.
+  struct LaidMember {
+    uint32_t idx, ver;
+    uint32_t stamp;        // the value stamp its fields were written with
+    uint32_t first_field;  // fields of one member are contiguous
+  };
   struct Layout {
     bool valid = false;
     bool relayout = false;
-    std::vector<uint32_t> members;
-    std::vector<uint32_t> vers;
-    std::vector<uint32_t> first_field;  // per member; fields of one member are contiguous
-    std::vector<uint32_t> stamps;       // per member
+    std::vector<LaidMember> members;  // one array: the per-tick pass streams through it
     TmplSegment seg;
   };
   // Field texts of series `idx` (1 for a gauge/counter, bounds + 3 for a histogram) into
@@ -154,14 +173,34 @@ class SeriesTable {
   void field_texts(uint32_t idx);
   void layout_family(int fid, uint64_t gen, std::string* body);
   void free_series(uint32_t idx);
-  void sort_members(Family& f);
+  void sort_members(int fid);
+  // bookkeeping of a set/observe/touch of series `h` at `gen` (changed: its value changed)
+  void note_set(Hot& h, uint64_t gen, bool changed) {
+    FamHot& f = fam_hot_[size_t(h.fid)];
+    if (f.gen != gen) {
+      f.gen = gen;
+      f.live = f.live_laid = f.changed = 0;
+    }
+    if (h.gen != gen) {
+      ++f.live;
+      if (h.laid) ++f.live_laid;
+      h.gen = gen;
+    }
+    if (changed) {
+      ++f.changed;
+      f.dirty = true;
+      h.stamp += 1;
+    }
+  }
+  void unlay(int fid);  // the family's compiled layout is gone: its members are no longer laid
   void render_histogram(std::string* out, uint32_t idx);
   void build_hlines(uint32_t idx);
   void format_cached(uint32_t idx);  // (re)fills the series' vtxt cache
   void append_cached_value(std::string* out, uint32_t idx);
-  void mark_dirty(int fid) { families_[size_t(fid)].dirty = true; }
+  void mark_dirty(int fid) { fam_hot_[size_t(fid)].dirty = true; }
 
   std::vector<Family> families_;
+  std::vector<FamHot> fam_hot_;  // by family id
   std::vector<int> render_order_;  // family ids sorted by name
   std::vector<Hot> hot_;
   std::vector<Series> series_;
@@ -175,6 +214,12 @@ class SeriesTable {
   std::vector<TmplSegment*> csegs_;
   TemplateDeflate deflate_;
   size_t last_relayouts_ = 0;
+  uint64_t compiled_gen_ = 0;  // generation of the last render_compiled
+  bool parse_check_ = true;    // segments were laid out since their parses were last checked
+  uint64_t rebuild_gen_ = 0;   // generation of the last layout change
+  uint64_t library_gzips_ = 0; // gzip members made by the library compressor (layout not settled)
+  static constexpr uint64_t kStableRenders = 4;
+  size_t last_skipped_ = 0;    // families passed over unchanged by the last render_compiled
   uint64_t code_builds_ = 0;
   size_t relaid_bytes_ = 0;  // bytes laid out again since the code was last built
   std::vector<char> scratch_;  // field_texts output, 32 bytes per field

@@ -68,6 +68,8 @@ def test_compiled_matches_classic_every_tick(native, churn):
         _same(promtext.parse(ref), promtext.parse(txt))
         assert gzip.decompress(gz) == txt.encode(), gen
         assert zlib.decompress(gz, 31) == txt.encode()  # zlib's own inflater, gzip wrapper
+    if churn == 0.0:  # values settle in their widths: most members come from the compiled encoder
+        assert b.library_gzips() < 119 // 2 and b.code_builds() >= 1, (b.library_gzips(), b.code_builds())
 
 
 def test_steady_state_does_not_relayout(native):
@@ -82,6 +84,62 @@ def test_steady_state_does_not_relayout(native):
             assert t.last_relayouts() == 0, gen
         assert gzip.decompress(gz) == txt.encode()
     assert t.code_builds() == 1
+
+
+def test_unchanged_families_are_passed_over(native):
+    """A family whose laid-out members were all set again with the same values is passed over
+    without walking its members; one changed value is still patched, a skipped generation
+    (a publish without a render) forces a full pass, and a member gone stale is noticed."""
+    (t, ids, h), _ = _tables(native, 6)
+    for gen in range(1, 5):
+        for f in ids:
+            for g in range(3):
+                t.put(f, [str(g), "a"], float(g), gen)
+        t.render_compiled(gen, 1, True)
+    assert t.last_skipped() == len(ids)
+    for f in ids:
+        for g in range(3):
+            t.put(f, [str(g), "a"], 7.0 if (f == ids[2] and g == 1) else float(g), 5)
+    txt, gz = t.render_compiled(5, 1, True)
+    assert t.last_skipped() == len(ids) - 1
+    assert promtext.value(promtext.parse(txt), "m02_metric_xx", gpu="1", k="a") == 7.0
+    assert gzip.decompress(gz) == txt.encode()
+    # generation 6 set but never rendered: 7 must look at every family again
+    for gen, v in ((6, 8.0), (7, 8.0)):
+        for f in ids:
+            for g in range(3):
+                t.put(f, [str(g), "a"], v if (f == ids[4] and g == 0) else float(g), gen)
+    txt, gz = t.render_compiled(7, 1, True)
+    assert t.last_skipped() == 0
+    assert promtext.value(promtext.parse(txt), "m04_metric_xxxx", gpu="0", k="a") == 8.0
+    # a member not set: its family is walked and laid out again without it
+    for f in ids:
+        for g in range(3):
+            if not (f == ids[0] and g == 2):
+                t.put(f, [str(g), "a"], float(g), 8)
+    txt, gz = t.render_compiled(8, 1, True)
+    assert t.last_relayouts() == 1
+    assert [lab["gpu"] for _, lab, _ in promtext.parse(txt)["m00_metric_"].samples] == ["0", "1"]
+    assert gzip.decompress(gz) == txt.encode()
+
+
+def test_library_compressor_while_the_layout_settles(native):
+    """A layout change sends the next renders' gzip through the library compressor; the
+    compiled encoder takes over once the layout held for 4 renders (one parse, not one per
+    change)."""
+    (t, ids, h), _ = _tables(native, 4)
+    gen = 0
+    used = []
+    for v in (5.0, 5.0, 5.0, 5.0, 5.0, 5.0, 123456.0, 5.0, 5.0, 5.0, 5.0, 5.0, 5.0):
+        gen += 1
+        for f in ids:
+            t.put(f, ["0", "a"], v if f == ids[1] else 1.0, gen)
+        before = t.library_gzips()
+        txt, gz = t.render_compiled(gen, 1, True)
+        used.append(t.library_gzips() - before)
+        assert gzip.decompress(gz) == txt.encode()
+    # first layout at 1, settled from 5; the field outgrown at 7 -> library 7..10, compiled from 11
+    assert used == [1, 1, 1, 1, 0, 0, 1, 1, 1, 1, 0, 0, 0], used
 
 
 def test_outgrown_field_relayouts_only_its_family(native):
