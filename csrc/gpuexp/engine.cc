@@ -1224,16 +1224,28 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
 }
 
 void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSample>>& per_dev) {
-  // pid -> attribution, resolved once per tick
-  std::unordered_map<int, ProcAttr> attr;
+  // pid -> attribution, resolved once per tick (and kept while KFD vouches for the process)
   unresolved_.clear();
   std::vector<int> live;
   for (auto& lst : per_dev)
     for (auto& p : lst) {
-      if (attr.count(p.pid)) continue;
-      ProcAttr a;
+      ProcAttr& a = attr_cache_[p.pid];
+      if (a.seen == gen) continue;
+      a.seen = gen;
+      live.push_back(p.pid);
+      if (p.kfd_id && a.kfd_id == p.kfd_id && a.ctl_epoch == ctl_epoch_) {
+        if (!a.uid.empty() && a.pod.empty()) unresolved_.insert(a.uid);
+        continue;
+      }
+      a.ns.clear();
+      a.pod.clear();
+      a.container.clear();
+      a.uid.clear();
+      a.kfd_id = p.kfd_id;
+      a.ctl_epoch = ctl_epoch_;
       if (cfg_.pod_attribution) {
         const CgroupInfo* ci = resolver_->resolve(p.pid, p.kfd_id);
+        if (!ci) a.kfd_id = 0;  // not looked up (unreadable /proc/<pid>): ask the resolver again
         if (ci && ci->kube) {
           a.uid = ci->pod_uid;
           auto it = pods_by_uid_.find(ci->pod_uid);
@@ -1249,9 +1261,9 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
           if (cn != container_names_.end()) a.container = cn->second;
         }
       }
-      attr.emplace(p.pid, a);
-      live.push_back(p.pid);
     }
+  for (auto it = attr_cache_.begin(); it != attr_cache_.end();)
+    it = it->second.seen != gen ? attr_cache_.erase(it) : std::next(it);
   resolver_->gc(live);
 
   struct PidAgg {
@@ -1337,7 +1349,7 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
     }
     const bool shared = st.owner.pod.empty();
     for (auto& p : per_dev[di]) {
-      const ProcAttr& a = attr[p.pid];
+      const ProcAttr& a = attr_cache_[p.pid];
       const double share = gfx_share(p);
       if (!legacy_only) {
         // handles cached per (GPU, PID) for as long as the label values stay the same
@@ -1433,7 +1445,7 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
     // Legacy families: one series per attributed host PID, summed over GPUs (the
     // reference overwrote per device, last-device-wins, main.go:147-150).
     for (auto& kv : legacy) {
-      const ProcAttr& a = attr[kv.first];
+      const ProcAttr& a = attr_cache_[kv.first];
       ProcRefs& pr = legacy_refs_[uint64_t(uint32_t(kv.first))];
       if (pr.pod != a.pod) {
         pr = ProcRefs();
@@ -1551,8 +1563,8 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
     rccl_->poll(&tot);
     for (auto& t : tot) {
       ProcAttr a;
-      auto it = attr.find(t.pid);
-      if (it != attr.end()) a = it->second;
+      auto it = attr_cache_.find(t.pid);
+      if (it != attr_cache_.end()) a = it->second;
       else if (cfg_.pod_attribution) {
         const CgroupInfo* ci = resolver_->resolve(t.pid);
         if (ci && ci->kube) {
@@ -1738,10 +1750,13 @@ void Engine::tick_locked(uint64_t now) {
     if (clear_overrides_) {
       resolver_->clear_overrides();
       clear_overrides_ = false;
+      ++ctl_epoch_;
     }
+    if (!pending_overrides_.empty()) ++ctl_epoch_;
     for (auto& o : pending_overrides_) resolver_->set_override(o.first, o.second);
     pending_overrides_.clear();
     if (ctl_dirty_) {
+      ++ctl_epoch_;
       pods_by_uid_.clear();
       container_names_.clear();
       for (auto& p : pending_pods_) {
@@ -1857,7 +1872,6 @@ void Engine::tick_locked(uint64_t now) {
   // 2: device ownership (device plugin map first, then single-pod inference).
   for (size_t i = 0; i < devices_.size(); ++i) {
     DevState& st = dstate_[i];
-    const DeviceInfo& d = devices_[i];
     DeviceOwner own;
     auto it = owners_.end();
     for (const std::string& key : owner_keys_[i]) {

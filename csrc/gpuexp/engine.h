@@ -261,7 +261,12 @@ class Engine {
   };
   struct ProcAttr {
     std::string ns, pod, container, uid;
+    // cached across ticks while KFD reads the same process (ProcSample::kfd_id) and no pod
+    // list / cgroup override was applied since (ctl_epoch_)
+    uint64_t kfd_id = 0, ctl_epoch = 0, seen = 0;
   };
+  std::unordered_map<int, ProcAttr> attr_cache_;  // sampler thread
+  uint64_t ctl_epoch_ = 1;
 
   void define_families();
   void run_sampler();
