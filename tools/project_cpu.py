@@ -56,7 +56,8 @@ def measure(native, n_gpus: int, hz: float, fetch_us: int, policy: str, budget: 
         h.host = "127.0.0.1"
         c.http = h
     c.series_profile = "full"
-    c.exposition = exposition
+    if hasattr(c, "exposition"):  # (an older tree, --root, has only the classic one)
+        c.exposition = exposition
     c.fake_metrics_cost_us = fetch_us
     c.metrics_min_interval_s = -1.0 if policy == "auto" else 0.0
     c.metrics_cpu_budget = budget / 100.0
@@ -64,7 +65,7 @@ def measure(native, n_gpus: int, hz: float, fetch_us: int, policy: str, budget: 
     e.start()
     scraper = None
     if scrape != "none":  # another process, so its CPU is not the exporter's
-        scraper = subprocess.Popen([sys.executable, "-c", SCRAPER, ROOT, str(e.http_port), str(hz), scrape])
+        scraper = subprocess.Popen([sys.executable, "-c", SCRAPER, PKG_ROOT, str(e.http_port), str(hz), scrape])
     try:
         time.sleep(1.0)
         r0, t0, s0 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter(), e.stats()
@@ -87,8 +88,13 @@ def measure(native, n_gpus: int, hz: float, fetch_us: int, policy: str, budget: 
             "code_builds": s1.get("code_builds", 0) - s0.get("code_builds", 0)}
 
 
+PKG_ROOT = ROOT
+
+
 def main() -> int:
+    global PKG_ROOT
     ap = argparse.ArgumentParser()
+    ap.add_argument("--root", default=ROOT, help="tree whose built package to measure (e.g. an older round's)")
     ap.add_argument("--fetch-us", default="206,450")
     ap.add_argument("--hz", default="10,100")
     ap.add_argument("--gpus", default="1,2,4,8")
@@ -99,6 +105,8 @@ def main() -> int:
     ap.add_argument("--exposition", default="compiled", help="compiled | classic (comma list to compare)")
     ap.add_argument("--stages", action="store_true", help="also print the sampler thread's CPU per stage")
     args = ap.parse_args()
+    PKG_ROOT = os.path.abspath(args.root)
+    sys.path.insert(0, PKG_ROOT)
     from kubernetes_gpu_exporter_amd._native import load
     native = load()
     print(f"# fake-host projection, full profile, 4 processes/GPU, budget {args.budget} % (auto policy)")
