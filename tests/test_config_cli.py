@@ -41,6 +41,7 @@ def test_precedence(tmp_path):
 @pytest.mark.parametrize("bad", [
     {"backend": "nvml"}, {"series_profile": "huge"}, {"interval": -1}, {"path": "metrics"},
     {"listen": ":99999"}, {"mock_devices": 0}, {"log_level": "loud"}, {"nonsense": 1}, {"gzip": "maybe"},
+    {"exposition": "fast"},
 ])
 def test_validation(bad):
     with pytest.raises(ValueError):
@@ -151,6 +152,14 @@ def test_round4_keys_reach_the_engine(native):
     ec = make_config({"counters_inline": False, "http_follow_rx_cpu": True,
                       "kfd_sdma_activity": True}).to_engine_config(native)
     assert ec.counters_inline is False and ec.http.follow_rx_cpu is True and ec.kfd_sdma is True
+
+
+def test_round5_keys_reach_the_engine(native):
+    ec = make_config({}).to_engine_config(native)
+    assert ec.exposition == "compiled" and ec.http.prewake is False  # profiles/r05/prewake_ab.txt
+    c = load_config(["--http-prewake"], env={"GPUEXP_EXPOSITION": "classic"})
+    ec = c.to_engine_config(native)
+    assert ec.exposition == "classic" and ec.http.prewake is True
 
 
 def test_stale_after_defaults_follow_the_interval(native):
