@@ -16,6 +16,7 @@
 
 #include <fcntl.h>
 #include <sys/mman.h>
+#include <zlib.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -42,6 +43,27 @@ static bool delimited_ok(const std::string& b) {
     pos += size_t(len);
   }
   return true;
+}
+
+// Inflates a gzip member (zlib's inflater, independent of the exporter's encoder); false if it
+// is not one complete, valid member.
+static bool gunzip(const std::string& in, std::string* out) {
+  z_stream zs{};
+  if (inflateInit2(&zs, 16 + 15) != Z_OK) return false;
+  out->clear();
+  zs.next_in = reinterpret_cast<Bytef*>(const_cast<char*>(in.data()));
+  zs.avail_in = uInt(in.size());
+  char buf[65536];
+  int rc;
+  do {
+    zs.next_out = reinterpret_cast<Bytef*>(buf);
+    zs.avail_out = sizeof(buf);
+    rc = inflate(&zs, Z_NO_FLUSH);
+    out->append(buf, sizeof(buf) - zs.avail_out);
+  } while (rc == Z_OK);
+  const bool ok = rc == Z_STREAM_END && zs.avail_in == 0;
+  inflateEnd(&zs);
+  return ok;
 }
 
 static double ticks_in(const std::string& body) {
@@ -93,12 +115,16 @@ int main(int argc, char** argv) {
         double ns = c.scrape();
         if (ns < 0 || c.last_status() == 503) continue;
         scrapes.fetch_add(1);
-        if (s == 0) continue;  // gzip body: only transport-checked
         if (s == 1 && !c.last_body().empty() && c.last_body()[0] != '#') {
           if (!delimited_ok(c.last_body())) bad.fetch_add(1);  // protobuf: framing must be exact
           continue;
         }
-        const std::string& b = c.last_body();
+        std::string inflated;
+        if (s == 0 && !gunzip(c.last_body(), &inflated)) {  // gzip: a valid member of a valid body
+          bad.fetch_add(1);
+          continue;
+        }
+        const std::string& b = s == 0 ? inflated : c.last_body();
         double t = ticks_in(b);
         if (b.find("\namd_rccl_collective_calls_total{") != std::string::npos) rccl_seen.fetch_add(1);
         if (b.compare(0, 7, "# HELP ") != 0 || b.back() != '\n' || t < last) bad.fetch_add(1);
