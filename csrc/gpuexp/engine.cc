@@ -406,6 +406,10 @@ void Engine::define_families() {
                      "the next tick) or per request (off schedule)",
                      C, {"where"});
   f_self_render_bytes_ = add("gpuexp_render_bytes", "Size of the last rendered exposition", G, {});
+  f_self_expo_ = add("gpuexp_exposition_events_total",
+                     "Compiled exposition: families laid out again (a series appeared or went, a value outgrew "
+                     "its field), gzip members made by the library compressor while the layout settled, and "
+                     "Huffman code builds (0 per tick in steady state)", C, {"event"});
   f_self_series_ = add("gpuexp_series", "Series in the last rendered exposition", G, {});
   f_self_dev_errors_ = add("gpuexp_device_errors_total", "Failed telemetry reads per GPU", C, {"gpu"});
   f_self_overruns_ = add("gpuexp_tick_overruns_total", "Ticks skipped because a tick ran past its deadline", C, {});
@@ -1683,6 +1687,13 @@ void Engine::emit_self(uint64_t gen) {
          [] { return std::vector<std::string>{"kfd_events"}; });
   if (cfg_.series_profile == "full")
     cput(self_refs_[20], f_driver_, 1, gen, [&] { return std::vector<std::string>{driver_version_, kernel_release_}; });
+  if (compiled_) {
+    cput(expo_refs_[0], f_self_expo_, double(expo_relayouts_), gen, [] { return std::vector<std::string>{"relayout"}; });
+    cput(expo_refs_[1], f_self_expo_, double(table_.library_gzips()), gen,
+         [] { return std::vector<std::string>{"library_gzip"}; });
+    cput(expo_refs_[2], f_self_expo_, double(table_.code_builds()), gen,
+         [] { return std::vector<std::string>{"code_build"}; });
+  }
   if (rccl_) {
     int a = 0, u = 0, x = 0;
     rccl_->file_states(&a, &u, &x);
@@ -2018,6 +2029,7 @@ void Engine::tick_locked(uint64_t now) {
     stats_.sampler_cpu_ns += cpu;
     stats_.gzip_eager = gzip_eager_;
     stats_.relayouts += table_.last_relayouts();
+    expo_relayouts_ += table_.last_relayouts();
     stats_.code_builds = table_.code_builds();
   }
 }

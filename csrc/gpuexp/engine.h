@@ -382,6 +382,9 @@ class Engine {
   int f_self_rx_moves_ = -1;
   int f_self_pods_complete_ = -1, f_self_kfd_scans_ = -1, f_self_kfd_tracked_ = -1;
   SeriesRef self_refs_[21];
+  SeriesRef expo_refs_[3];
+  int f_self_expo_ = -1;
+  uint64_t expo_relayouts_ = 0;  // sampler thread
 
   // stats (guarded by stats_mu_)
   std::mutex stats_mu_;
