@@ -5,6 +5,7 @@
 
 #include <cmath>
 #include <cstring>
+#include <map>
 
 #include "gpuexp/backends.h"
 #include "gpuexp/client.h"
@@ -559,6 +560,16 @@ PYBIND11_MODULE(_gpuexp, m) {
         return py::make_tuple(out, py::bytes(gz));
       }, py::arg("gen"), py::arg("gc_after") = 1, py::arg("gzip") = true,
          "(text, gzip bytes) of the fixed-layout renderer")
+      .def("render_compiled_slot", [](SeriesTable& t, uint64_t gen, int slot, uint64_t gc_after) {
+        // the engine's snapshot slots: buffers kept between calls, each with the generation it holds
+        static thread_local std::map<std::pair<const SeriesTable*, int>, std::pair<std::string, uint64_t>> slots;
+        auto& sl = slots[{&t, slot}];
+        std::string gz;
+        t.render_compiled(&sl.first, &gz, gen, gc_after, sl.second);
+        sl.second = gen;
+        return py::make_tuple(sl.first, py::bytes(gz), t.last_copied());
+      }, py::arg("gen"), py::arg("slot"), py::arg("gc_after") = 1,
+         "render_compiled into a kept buffer (slot): (text, gzip, bytes copied into the buffer)")
       .def("last_relayouts", &SeriesTable::last_relayouts)
       .def("last_skipped", &SeriesTable::last_skipped)
       .def("library_gzips", &SeriesTable::library_gzips)

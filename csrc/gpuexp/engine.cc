@@ -1950,7 +1950,8 @@ void Engine::tick_locked(uint64_t now) {
     const bool want_gz = http_ && http_->gzip_due(mono_ns(), 2 * period_ns + 5000000ull);
     if (want_gz) ++gzip_eager_;
     snap->gz.clear();
-    if (compiled_) table_.render_compiled(&snap->body, want_gz ? &snap->gz : nullptr, gen, cfg_.gc_after);
+    // (the slot's previous generation: only the fields changed since are copied into it)
+    if (compiled_) table_.render_compiled(&snap->body, want_gz ? &snap->gz : nullptr, gen, cfg_.gc_after, snap->gen);
     else table_.render(&snap->body, gen, cfg_.gc_after);
     snap->gen = gen;
     snap->render_ns = now;

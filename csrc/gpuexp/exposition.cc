@@ -456,7 +456,7 @@ void SeriesTable::layout_family(int fid, uint64_t gen, std::string* body) {
     const size_t nf = scratch_len_.size();
     if (s.widths.size() != nf) s.widths.assign(nf, 0);
     if (hist) build_hlines(idx);
-    L.members.push_back({idx, h.ver, h.stamp, uint32_t(L.seg.fields.size())});
+    L.members.push_back({idx, h.ver, h.stamp, uint32_t(L.seg.fields.size()), gen});
     h.laid = true;
     for (size_t f = 0; f < nf; ++f) {
       body->append(hist ? s.hlines[f] : s.line);
@@ -486,13 +486,15 @@ void SeriesTable::layout_family(int fid, uint64_t gen, std::string* body) {
   L.valid = true;
   L.relayout = false;
   FamHot& fh = fam_hot_[size_t(fid)];
+  fh.change_gen = gen;
   fh.laid_valid = true;
   fh.nlaid = uint32_t(L.members.size());
   // this generation's counts as the layout sees them (every member laid out is live now)
   fh.live_laid = fh.gen == gen ? uint32_t(L.members.size()) : 0;
 }
 
-void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t gen, uint64_t gc_after) {
+void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t gen, uint64_t gc_after,
+                                  uint64_t out_gen) {
   last_rebuilt_ = 0;
   last_relayouts_ = 0;
   last_skipped_ = 0;
@@ -564,6 +566,8 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
           std::memset(dst + scratch_len_[f], ' ', fl[f].width - scratch_len_[f]);
         }
         lm.stamp = h.stamp;
+        lm.change_gen = gen;
+        fh.change_gen = gen;
         L.seg.splice_valid = false;
       }
       ++k;
@@ -605,7 +609,30 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
     }
     cbody_.swap(cbody_next_);
   }
-  out->assign(cbody_);
+  // Into `out`: the changed fields only, if `out` holds this layout's body as of out_gen.
+  if (out_gen && out_gen < gen && out_gen >= rebuild_gen_ && out->size() == cbody_.size()) {
+    size_t copied = 0;
+    char* o = &(*out)[0];
+    for (int fid : render_order_) {
+      if (fam_hot_[size_t(fid)].change_gen <= out_gen) continue;
+      const Layout& L = layouts_[size_t(fid)];
+      if (!L.valid) continue;
+      const size_t nm = L.members.size();
+      for (size_t m = 0; m < nm; ++m) {
+        if (L.members[m].change_gen <= out_gen) continue;
+        const size_t f1 = m + 1 < nm ? L.members[m + 1].first_field : L.seg.fields.size();
+        for (size_t f = L.members[m].first_field; f < f1; ++f) {
+          const TmplField& tf = L.seg.fields[f];
+          std::memcpy(o + L.seg.base + tf.off, cbody_.data() + L.seg.base + tf.off, tf.width);
+          copied += tf.width;
+        }
+      }
+    }
+    last_copied_ = copied;
+  } else {
+    out->assign(cbody_);
+    last_copied_ = cbody_.size();
+  }
   if (!gz) return;
   // While the layout still moves (warm-up: values reaching their widths; a process appearing)
   // the whole body goes through the library compressor: a parse costs more than one

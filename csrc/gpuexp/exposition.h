@@ -87,11 +87,17 @@ class SeriesTable {
   // patches the fields whose values changed, and -- with `gz` -- emits the gzip member from the
   // pre-encoded static bits plus the field bytes (TemplateDeflate).  Do not mix with render()
   // on one table.
-  void render_compiled(std::string* out, std::string* gz, uint64_t gen, uint64_t gc_after = 1);
+  // `out_gen`: the generation `out` holds a render_compiled body of (0 = none, e.g. a fresh
+  // snapshot slot): if the layout has not changed since, only the fields changed after it are
+  // copied into `out` instead of the whole body.
+  void render_compiled(std::string* out, std::string* gz, uint64_t gen, uint64_t gc_after = 1,
+                       uint64_t out_gen = 0);
   // Families laid out again by the last render_compiled (0 in steady state).
   size_t last_relayouts() const { return last_relayouts_; }
   size_t last_skipped() const { return last_skipped_; }
   uint64_t library_gzips() const { return library_gzips_; }
+  // Bytes copied into `out` by the last render_compiled (the whole body, or the changed fields).
+  size_t last_copied() const { return last_copied_; }
   uint64_t code_builds() const { return code_builds_; }
   const TemplateDeflate& deflater() const { return deflate_; }
 
@@ -127,6 +133,7 @@ class SeriesTable {
     bool laid_valid = false;
     bool dirty = true;       // render(): the cached text is stale
     bool dirty_order = false;
+    uint64_t change_gen = 0;  // generation a field of the family was last written in (render_compiled)
   };
   struct Series {  // cold: strings and histogram state
     std::vector<std::string> labels;
@@ -161,6 +168,7 @@ class SeriesTable {
     uint32_t idx, ver;
     uint32_t stamp;        // the value stamp its fields were written with
     uint32_t first_field;  // fields of one member are contiguous
+    uint64_t change_gen;   // generation its fields were last written in
   };
   struct Layout {
     bool valid = false;
@@ -217,6 +225,7 @@ class SeriesTable {
   uint64_t compiled_gen_ = 0;  // generation of the last render_compiled
   bool parse_check_ = true;    // segments were laid out since their parses were last checked
   uint64_t rebuild_gen_ = 0;   // generation of the last layout change
+  size_t last_copied_ = 0;
   uint64_t library_gzips_ = 0; // gzip members made by the library compressor (layout not settled)
   static constexpr uint64_t kStableRenders = 4;
   size_t last_skipped_ = 0;    // families passed over unchanged by the last render_compiled

@@ -142,6 +142,32 @@ def test_library_compressor_while_the_layout_settles(native):
     assert used == [1, 1, 1, 1, 0, 0, 1, 1, 1, 1, 0, 0, 0], used
 
 
+@pytest.mark.parametrize("churn", [0.0, 0.03])
+def test_snapshot_slots_get_only_the_changed_fields(native, churn):
+    """Two snapshot slots used in turn (the engine's ping-pong): a slot that holds the current
+    layout as of two generations ago gets only the fields changed since copied in, and its
+    text is every tick exactly the classic renderer's samples and the gzip member's content."""
+    (a, ia, ha), (b, ib, hb) = _tables(native, 10)
+    rng = random.Random(3)
+    copied = []
+    for gen in range(1, 80):
+        for i in range(len(ia)):
+            for g in range(4):
+                if gen > 1 and rng.random() < churn:
+                    continue
+                v = float(rng.randint(100, 999)) if rng.random() < 0.2 else float(g + i)
+                a.put(ia[i], [str(g), "a"], v, gen)
+                b.put(ib[i], [str(g), "a"], v, gen)
+        ref = a.render(gen, 1)
+        txt, gz, n = b.render_compiled_slot(gen, gen % 2)
+        _same(promtext.parse(ref), promtext.parse(txt))
+        assert gzip.decompress(gz) == txt.encode(), gen
+        copied.append((n, len(txt)))
+    if churn == 0.0:  # steady layout: a fraction of the body per tick
+        tail = copied[20:]
+        assert all(n < size / 4 for n, size in tail), tail[:5]
+
+
 def test_outgrown_field_relayouts_only_its_family(native):
     (t, ids, h), _ = _tables(native, 6)
     for gen in range(1, 4):
