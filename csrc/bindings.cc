@@ -707,6 +707,8 @@ PYBIND11_MODULE(_gpuexp, m) {
         d["gzip_eager"] = s.gzip_eager;
         d["relayouts"] = s.relayouts;
         d["code_builds"] = s.code_builds;
+        d["families_skipped"] = s.families_skipped;
+        d["families_rendered"] = s.families_rendered;
         py::dict st;
         for (int k = 0; k < Engine::kStages; ++k) st[Engine::stage_name(k)] = s.stage_ns[k];
         d["stage_ns"] = st;

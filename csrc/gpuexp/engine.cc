@@ -1622,20 +1622,35 @@ void Engine::emit_self(uint64_t gen) {
   for (int k = 0; k < kDevParts; ++k)
     cput(dev_part_refs_[k], f_self_dev_part_, dev_part_total_s_[k], gen,
          [&] { return std::vector<std::string>{dev_part_name(k)}; });
+  // histograms: accumulated every tick, published at most once a second (see engine.h)
+  const uint64_t hnow = last_tick_now_;
+  const bool publish_hist = !self_hist_pub_ns_ || hnow < self_hist_pub_ns_ || hnow - self_hist_pub_ns_ >= 1000000000ull;
+  if (publish_hist) self_hist_pub_ns_ = hnow;
+  const std::vector<double>& sb = stage_bounds();
   for (int k = 0; k < kStages; ++k) {
     if (!self_stage_refs_[k].valid()) self_stage_refs_[k] = table_.upsert(f_self_stage_, {stage_name(k)});
-    if (s.ticks) table_.observe(self_stage_refs_[k], double(last_stage_ns_[k]) * 1e-9, gen, stage_bounds());
-    else table_.touch(self_stage_refs_[k], gen);
+    std::vector<uint64_t>& h = stage_hist_[k];
+    if (h.size() != sb.size() + 1) h.assign(sb.size() + 1, 0);
+    if (s.ticks) {
+      const double v = double(last_stage_ns_[k]) * 1e-9;
+      h[size_t(std::lower_bound(sb.begin(), sb.end(), v) - sb.begin())] += 1;
+      stage_hist_sum_[k] += v;
+      stage_hist_n_[k] += 1;
+    }
+    if (!publish_hist || !table_.set_histogram(self_stage_refs_[k], sb, h, stage_hist_sum_[k], stage_hist_n_[k], gen))
+      table_.touch(self_stage_refs_[k], gen);
   }
   if (http_) {
     const HttpStats& hs = http_->stats();
-    std::vector<uint64_t> counts(HttpStats::kBuckets + 1);
-    for (int b = 0; b <= HttpStats::kBuckets; ++b) counts[size_t(b)] = hs.lat_buckets[b].load(std::memory_order_relaxed);
-    uint64_t cnt = hs.lat_count.load(std::memory_order_relaxed);
-    double sum = double(hs.lat_sum_ns.load(std::memory_order_relaxed)) * 1e-9;
-    if (!table_.set_histogram(self_refs_[8], scrape_latency_bounds(), counts, sum, cnt, gen)) {
-      self_refs_[8] = table_.upsert(f_self_scrape_, {});
-      table_.set_histogram(self_refs_[8], scrape_latency_bounds(), counts, sum, cnt, gen);
+    if (publish_hist || !table_.touch(self_refs_[8], gen)) {
+      std::vector<uint64_t> counts(HttpStats::kBuckets + 1);
+      for (int b = 0; b <= HttpStats::kBuckets; ++b) counts[size_t(b)] = hs.lat_buckets[b].load(std::memory_order_relaxed);
+      uint64_t cnt = hs.lat_count.load(std::memory_order_relaxed);
+      double sum = double(hs.lat_sum_ns.load(std::memory_order_relaxed)) * 1e-9;
+      if (!table_.set_histogram(self_refs_[8], scrape_latency_bounds(), counts, sum, cnt, gen)) {
+        self_refs_[8] = table_.upsert(f_self_scrape_, {});
+        table_.set_histogram(self_refs_[8], scrape_latency_bounds(), counts, sum, cnt, gen);
+      }
     }
     cput(self_refs_[9], f_self_scrapes_, double(hs.metrics_requests.load(std::memory_order_relaxed)), gen, none);
     cput(self_refs_[10], f_self_http_bytes_, double(hs.bytes_sent.load(std::memory_order_relaxed)), gen, none);
@@ -2030,6 +2045,8 @@ void Engine::tick_locked(uint64_t now) {
     stats_.sampler_cpu_ns += cpu;
     stats_.gzip_eager = gzip_eager_;
     stats_.relayouts += table_.last_relayouts();
+    stats_.families_skipped += table_.last_skipped();
+    stats_.families_rendered += table_.last_walked();
     expo_relayouts_ += table_.last_relayouts();
     stats_.code_builds = table_.code_builds();
   }

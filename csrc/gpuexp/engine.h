@@ -172,6 +172,8 @@ struct EngineStats {
   uint64_t gzip_eager = 0;  // snapshots published with a gzip copy
   uint64_t relayouts = 0;   // compiled exposition: families laid out again (0 per tick in steady state)
   uint64_t code_builds = 0; // compiled exposition: Huffman code builds
+  uint64_t families_skipped = 0;  // compiled exposition: families passed over unchanged (cumulative)
+  uint64_t families_rendered = 0; // ... and families walked (cumulative)
 };
 
 class Engine {
@@ -383,6 +385,13 @@ class Engine {
   int f_self_pods_complete_ = -1, f_self_kfd_scans_ = -1, f_self_kfd_tracked_ = -1;
   SeriesRef self_refs_[21];
   SeriesRef expo_refs_[3];
+  // The self-observability histograms (per-stage tick time, scrape latency) accumulate every
+  // tick here and are published into the table at most once a second: re-rendering and
+  // re-splicing ~120 bucket lines per tick was most of a 100 Hz tick's exposition work.
+  std::vector<uint64_t> stage_hist_[8];
+  double stage_hist_sum_[8] = {};
+  uint64_t stage_hist_n_[8] = {};
+  uint64_t self_hist_pub_ns_ = 0;
   int f_self_expo_ = -1;
   uint64_t expo_relayouts_ = 0;  // sampler thread
 

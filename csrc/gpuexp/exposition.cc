@@ -498,6 +498,7 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
   last_rebuilt_ = 0;
   last_relayouts_ = 0;
   last_skipped_ = 0;
+  last_walked_ = 0;
   bool rebuild = false;  // some family is laid out again, appears or disappears
   if (layouts_.size() != families_.size()) {
     layouts_.resize(families_.size());  // csegs_ points into layouts_: rebuilt below
@@ -513,6 +514,7 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
   compiled_gen_ = gen;
   for (int fid : render_order_) {
     FamHot& fh = fam_hot_[size_t(fid)];
+    if (fh.nmembers == 0 && !fh.laid_valid) continue;  // no series (an optional source off): nothing to do
     // unchanged since the last pass: every laid-out member set again, none changed, no other
     // member live or waiting for GC
     if (consecutive && fh.laid_valid && !fh.dirty_order && fh.gen == gen && fh.changed == 0 &&
@@ -522,6 +524,7 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
     }
     Family& fam = families_[size_t(fid)];
     Layout& L = layouts_[size_t(fid)];
+    ++last_walked_;
     if (fh.dirty_order) {  // a new member: laid out again (sorting first, so GC below keeps order)
       sort_members(fid);
       L.relayout = true;

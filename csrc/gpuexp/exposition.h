@@ -95,6 +95,7 @@ class SeriesTable {
   // Families laid out again by the last render_compiled (0 in steady state).
   size_t last_relayouts() const { return last_relayouts_; }
   size_t last_skipped() const { return last_skipped_; }
+  size_t last_walked() const { return last_walked_; }
   uint64_t library_gzips() const { return library_gzips_; }
   // Bytes copied into `out` by the last render_compiled (the whole body, or the changed fields).
   size_t last_copied() const { return last_copied_; }
@@ -229,6 +230,7 @@ class SeriesTable {
   uint64_t library_gzips_ = 0; // gzip members made by the library compressor (layout not settled)
   static constexpr uint64_t kStableRenders = 4;
   size_t last_skipped_ = 0;    // families passed over unchanged by the last render_compiled
+  size_t last_walked_ = 0;     // families whose members the last render_compiled walked
   uint64_t code_builds_ = 0;
   size_t relaid_bytes_ = 0;  // bytes laid out again since the code was last built
   std::vector<char> scratch_;  // field_texts output, 32 bytes per field
