@@ -38,6 +38,10 @@ bool wait_until(std::condition_variable& cv, std::unique_lock<std::mutex>& lk, C
 }
 }  // namespace
 
+constexpr double kMaxTimeUncFrac = 0.05;  // a window is published when its ends are this well-timed
+constexpr double kAnchorUncS = 250e-6;     // a read timed this well can start a window
+constexpr std::chrono::microseconds kPromptRead{300};  // a read not held up completes within this
+
 struct RoundMachine::Slot {
   ReadPort* port = nullptr;
   bool ready = false;  // armed at init (arm_sync)
@@ -47,9 +51,13 @@ struct RoundMachine::Slot {
   bool arming = false;    // ... and it is a (re-)arm: start program + baseline read
   bool was_pending = false;  // the pending packet predates this round: one look
   Clock::time_point t_checked{};  // last time the pending packet was seen not complete
+  bool seen_pending = false;      // ... by a look after it was posted (its execution time is then
+                                  // known only to within [t_checked, the look that saw it done])
+  Clock::time_point t_post{};     // when the pending packet was posted
   double cum[kNumCtr] = {}, cum_xm[kMaxXcc] = {}, cum_xg[kMaxXcc] = {};
   bool have_cum = false;
   Clock::time_point t_last{};  // when the last read executed (the start of the next window)
+  double t_last_unc = 0;       // half-width of t_last's uncertainty (s); 0 for a prompt read
   int zero_grbm = 0;
   int stuck_rounds = 0;
   bool rq_open = false;   // the rescue queue exists
@@ -59,6 +67,7 @@ struct RoundMachine::Slot {
   RearmState rs;
   // ---- health: atomics (readers on any thread) ----
   std::atomic<uint64_t> stalls{0}, resets{0}, rearms{0}, rescues{0}, releases{0}, conflicts{0};
+  std::atomic<uint64_t> merged{0};  // reads whose time was too uncertain: merged into the next window
   std::atomic<bool> rescue_active{false}, waiting_rearm{false};
   // ---- published window: m_mu ----
   mutable std::mutex m_mu;
@@ -111,6 +120,7 @@ bool RoundMachine::arm_sync(int dev) {
   }
   const auto now = Clock::now();
   s.t_last = pending + (now - pending) / 2;
+  s.t_last_unc = std::chrono::duration<double>(now - pending).count() / 2;
   s.have_cum = false;
   if (cfg_.mode == kCumulative) {
     Sample smp;
@@ -208,13 +218,16 @@ void RoundMachine::post_round_locked(Clock::time_point now) {
         s.port->post_arm(cfg_.mode == kCumulative);
         s.q = 0;
         s.arming = true;
+        s.seen_pending = false;
       } else {
         s.q = s.rescued ? 1 : 0;
         s.port->post_read(s.q);
         s.arming = false;
+        s.seen_pending = false;
       }
       s.inflight = true;
       s.t_checked = now;
+      s.t_post = now;
     }
     round_.waiting.push_back(int(i));
   }
@@ -223,6 +236,7 @@ void RoundMachine::post_round_locked(Clock::time_point now) {
 
 void RoundMachine::round_stuck(Slot& s, int dev, Clock::time_point now) {
   s.t_checked = now;
+  s.seen_pending = true;
   ++s.stalls;
   // rescue reads and (re-)arms are never rescued; nor are reads outside cumulative mode (a
   // second queue's read would reset / stop the counters the abandoned one still reads)
@@ -250,8 +264,17 @@ void RoundMachine::round_done(Slot& s, int dev, Clock::time_point now) {
   s.stuck_rounds = 0;
   const bool arming = s.arming;
   s.arming = false;
-  // the packet executed between the last time it was seen pending and now
-  const auto t = s.t_checked + (now - s.t_checked) / 2;
+  // The packet executed between the last time it was seen pending and now.  A read never seen
+  // pending ran promptly after it was posted (t_checked): reads complete in 50-600 us unless a
+  // sentinel run holds the queue, and then a look finds them pending.  Its time is taken from the
+  // post, not from how late the look came (a look delayed by scheduling would otherwise move the
+  // window's end by half the delay).
+  // (A look within kPromptRead of the post that finds it pending says nothing more: it is still
+  // a prompt read.  Held reads are those still pending later than that.)
+  const auto since = now - s.t_checked;
+  const bool held = s.seen_pending && s.t_checked - s.t_post > kPromptRead;
+  const auto t = held ? s.t_checked + since / 2 : s.t_checked + std::min<Clock::duration>(since, kPromptRead) / 2;
+  const double unc = held ? std::chrono::duration<double>(since).count() / 2 : 0.0;
   Sample smp;
   const uint64_t k0 = own_cpu_ns();
   const bool got = s.port->collect(s.q, &smp);
@@ -267,6 +290,7 @@ void RoundMachine::round_done(Slot& s, int dev, Clock::time_point now) {
   if (arming) {
     if (!got) return;  // the re-arm stays due: posted again next round
     s.t_last = t;
+    s.t_last_unc = unc;
     s.zero_grbm = 0;
     s.have_cum = false;
     if (cfg_.mode == kCumulative) {
@@ -297,11 +321,33 @@ void RoundMachine::round_done(Slot& s, int dev, Clock::time_point now) {
       xg[x] = std::max(0.0, smp.xg[x] - s.cum_xg[x]);
     }
     const bool first = !s.have_cum;
+    // A read that stalled behind a sentinel run is seen complete only at the next round's look:
+    // its execution time is uncertain by up to half a tick, and a window ending (or starting) there
+    // would carry that error into every rate (a 23 % FLOP/s error on silicon).  Its counts are
+    // not lost -- the baseline stays at the last well-timed read, so the next window spans both
+    // intervals with well-known ends.  (The error shrinks with the window: a long merged window
+    // is accepted once both uncertainties are under 5 % of it.)  A badly-timed read that ends an
+    // accepted long window leaves the next window's start uncertain; the next well-timed read
+    // then drops that short window and starts a fresh one (below), so one window is lost, not ten.
+    if (!first && !backwards && unc + s.t_last_unc > kMaxTimeUncFrac * wall) {
+      ++s.merged;
+      if (unc <= kAnchorUncS) {
+        // this read's own time is good (the bad one was the window's start): the window's counts
+        // are dropped unpublished and the next window starts here, well-timed
+        std::memcpy(s.cum, smp.v, sizeof(s.cum));
+        std::memcpy(s.cum_xm, smp.xm, sizeof(s.cum_xm));
+        std::memcpy(s.cum_xg, smp.xg, sizeof(s.cum_xg));
+        s.t_last = t;
+        s.t_last_unc = unc;
+      }
+      return;
+    }
     std::memcpy(s.cum, smp.v, sizeof(s.cum));
     std::memcpy(s.cum_xm, smp.xm, sizeof(s.cum_xm));
     std::memcpy(s.cum_xg, smp.xg, sizeof(s.cum_xg));
     s.have_cum = true;
     s.t_last = t;
+    s.t_last_unc = unc;
     const WindowAction act = window_action(d, first, wall, &s.zero_grbm);
     if (act == kRearm) {
       // reset / re-programmed / stopped under us: this window is unknown
@@ -319,9 +365,18 @@ void RoundMachine::round_done(Slot& s, int dev, Clock::time_point now) {
     }
     if (act == kPublish && !s.rs.waiting) publish(s, d, smp, wall, t, smp.v, xm, xg);
   } else {
-    publish(s, smp.v, smp, wall, t, nullptr, nullptr, nullptr);
+    // each read restarts the counts: a badly-timed window cannot be merged, only withheld
+    if (unc + s.t_last_unc <= kMaxTimeUncFrac * wall) publish(s, smp.v, smp, wall, t, nullptr, nullptr, nullptr);
+    else ++s.merged;
     s.t_last = t;
-    if (cfg_.mode == kStops) s.port->post_start();  // counting stopped at the read: again (one PM4 gap)
+    s.t_last_unc = unc;
+    if (cfg_.mode == kStops) {
+      // counting stopped at the read: again (one PM4 gap).  The next window counts from the start
+      // packet, posted now -- not from the read, which may have been collected late.
+      s.port->post_start();
+      s.t_last = Clock::now();
+      s.t_last_unc = 0;
+    }
   }
 }
 
@@ -344,6 +399,7 @@ void RoundMachine::look_locked(Clock::time_point now, bool at_deadline, bool fin
       it = w.erase(it);
     } else {
       s.t_checked = now;
+      s.seen_pending = true;
       ++it;
     }
   }
@@ -576,7 +632,7 @@ std::string RoundMachine::debug(int dev) {
   std::lock_guard<std::mutex> lk(s.m_mu);
   char win[64];
   std::snprintf(win, sizeof(win), "%.6f", s.last_window_s);
-  std::string out = "samples=" + std::to_string(s.last_samples) + ";windows=" + std::to_string(s.m.windows) +
+  std::string out = "samples=" + std::to_string(s.last_samples) + ";windows=" + std::to_string(s.m.windows) + ";merged=" + std::to_string(s.merged.load()) +
                     ";simd=" + std::to_string(s.m.simd) + ";cu=" + std::to_string(s.m.cu) +
                     ";mode=" + (cfg_.mode != kReadUnknown ? read_mode_name(cfg_.mode) : "duty") + ";window_s=" + win +
                     ";resets=" + std::to_string(s.resets.load()) + ";stalls=" + std::to_string(s.stalls.load()) +

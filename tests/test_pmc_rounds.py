@@ -29,11 +29,20 @@ def run(native, **kw):
     return native.pmc_harness(cfg)
 
 
+def _hiccup_bound(r, stalled):
+    """Worst rate error allowed for the stalled GPU: 10 %, or the healthy GPUs' worst plus 5
+    points when the harness thread itself was descheduled (that hits every GPU at once)."""
+    others = [g["worst_rate_err"] for i, g in enumerate(r["gpus"]) if i != stalled and not g["broken"]]
+    return max(0.1, max(others) + 0.05)
+
+
 def healthy(g, ticks):
     assert g["double_collected"] == 0 and g["uncollected"] == 0
     assert g["bad_windows"] == 0, g
     assert g["stalls"] == 0 and g["rescues"] == 0 and g["resets"] == 0 and not g["broken"]
-    assert g["windows"] >= ticks - 3 and g["fresh_ticks"] >= 0.9 * ticks, g
+    # (a window whose ends are timed worse than 5 % of it -- a look delayed by scheduling on this
+    # shared CPU -- is merged into the next one rather than published: a few may be missing)
+    assert g["windows"] >= ticks - 5 and g["fresh_ticks"] >= 0.85 * ticks, g
 
 
 # ---------------------------------------------------------------------------------------------
@@ -104,7 +113,7 @@ def test_stuck_gpu_never_holds_the_other_seven(native, inline):
     assert g3["rescue_opened"] == g3["rescue_closed"] == 1 and not g3["rescue_open_at_end"] and g3["misuse"] == 0
     assert not g3["rescue_active"]
     assert g3["double_collected"] == 0 and g3["uncollected"] == 1   # the read abandoned on queue 0
-    assert g3["bad_windows"] == 0
+    assert g3["bad_windows"] == 0 and g3["worst_rate_err"] < _hiccup_bound(r, 3), g3
     # the rescue queue kept GPU 3's windows coming during most of the 600 ms stall
     assert g3["windows"] >= r["ticks"] - 8, g3
 
@@ -119,7 +128,9 @@ def test_leftover_reads_are_collected_exactly_once(native):
     g1 = r["gpus"][1]
     assert g1["double_collected"] == 0 and g1["uncollected"] == 0
     assert g1["reads_completed"] >= r["ticks"]
-    assert g1["windows"] >= r["ticks"] - 3 and g1["bad_windows"] == 0
+    # (a read collected after the sync is timed only to within the counting thread's look: the
+    # few whose look came late are merged into the next window rather than published mistimed)
+    assert g1["windows"] >= r["ticks"] - 8 and g1["bad_windows"] == 0
     assert g1["stalls"] == 0  # seen complete before the next round's one look
     for i in (0, 2, 3, 4, 5, 6, 7):
         healthy(r["gpus"][i], r["ticks"])
@@ -192,6 +203,11 @@ def test_rescue_unavailable_only_stalls(native):
     assert g3["rescues"] == 0 and g3["rescue_opened"] == 0 and g3["misuse"] == 0 and g3["stalls"] >= 10
     assert g3["double_collected"] == 0 and g3["uncollected"] == 0 and g3["bad_windows"] == 0
     assert not g3["broken"] and g3["windows"] >= r["ticks"] - 25  # back after the stall
+    # the read that sat out the stall is seen complete only at the next round's look: its time is
+    # uncertain by half a tick, so no window may end or start there (round 4 published a 29 % rate
+    # error here; on silicon 23 % in the fp8 FLOP/s calibration, profiles/r05/session4).  The
+    # stalled GPU's worst window is no worse than what a scheduling hiccup does to every GPU.
+    assert g3["worst_rate_err"] < _hiccup_bound(r, 3), g3
 
 
 @pytest.mark.parametrize("read_mode,mode", [(1, "resets"), (2, "stops")])
@@ -230,8 +246,8 @@ def test_eight_agents_inline_and_thread_machines_at_once(native):
             assert x["uncollected"] <= (1 if i in (3, 6) else 0), (inline, i, x)
             if i != 6:
                 assert x["bad_windows"] == 0, (inline, i, x)
-        for i in (0, 1, 7):
-            assert g[i]["windows"] >= r["ticks"] - 3, (inline, i, g[i])
+        for i in (0, 1, 7):  # (GPU 1's 3 ms reads outlast the sync: a few merged windows)
+            assert g[i]["windows"] >= r["ticks"] - (8 if i == 1 else 5), (inline, i, g[i])
         assert (g[2]["resets"], g[2]["rearms"], g[2]["arms"]) == (1, 1, 1)
         assert (g[3]["rescues"], g[3]["releases"]) == (1, 1) and g[3]["stalls"] >= 3
         assert (g[4]["rearms"], g[4]["conflicts"]) == (1, 3)
