@@ -2,6 +2,8 @@
 
 #include "gpuexp/snapshot.h"  // gzip_compress
 
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include <algorithm>
@@ -83,6 +85,7 @@ int SeriesTable::add_family(const FamilyDef& def) {
   f.header += "\n# TYPE " + def.name + " " + tn[int(def.type)] + "\n";
   families_.push_back(std::move(f));
   fam_hot_.emplace_back();
+  debug_relayout_ = std::getenv("GPUEXP_DEBUG_RELAYOUT") != nullptr;
   int fid = int(families_.size() - 1);
   render_order_.push_back(fid);
   std::sort(render_order_.begin(), render_order_.end(), [this](int a, int b) {
@@ -442,6 +445,8 @@ void SeriesTable::field_texts(uint32_t idx) {
 void SeriesTable::layout_family(int fid, uint64_t gen, std::string* body) {
   Family& fam = families_[size_t(fid)];
   Layout& L = layouts_[size_t(fid)];
+  if (debug_relayout_) std::fprintf(stderr, "[exposition] gen %llu: %s laid out again (%s)\n", (unsigned long long)gen,
+                                    fam.def.name.c_str(), L.why);
   unlay(fid);
   L.members.clear();
   L.seg.fields.clear();
@@ -528,6 +533,7 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
     if (fh.dirty_order) {  // a new member: laid out again (sorting first, so GC below keeps order)
       sort_members(fid);
       L.relayout = true;
+      L.why = "new_series";
     }
     // one pass: GC, liveness, the same live members in the same order as laid out, and the
     // fields of changed members patched in place (a value that outgrew its field, or a
@@ -550,6 +556,7 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
       if (!patch) continue;
       if (k >= L.members.size() || L.members[k].idx != idx || L.members[k].ver != h.ver) {
         patch = false;
+        if (!L.relayout) L.why = "membership";
         continue;
       }
       LaidMember& lm = L.members[k];
@@ -561,6 +568,7 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
         for (size_t f = 0; fits && f < nf; ++f) fits = scratch_len_[f] <= fl[f].width;
         if (!fits) {
           patch = false;
+          L.why = "outgrown";
           continue;
         }
         for (size_t f = 0; f < nf; ++f) {
@@ -586,6 +594,8 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
       continue;
     }
     if (!patch || k != L.members.size()) {
+      if (!L.valid) L.why = "appeared";
+      else if (patch) L.why = "membership";
       L.relayout = true;
       rebuild = true;
     }

@@ -174,6 +174,7 @@ class SeriesTable {
   struct Layout {
     bool valid = false;
     bool relayout = false;
+    const char* why = "";  // why it is laid out again (GPUEXP_DEBUG_RELAYOUT logs it)
     std::vector<LaidMember> members;  // one array: the per-tick pass streams through it
     TmplSegment seg;
   };
@@ -225,6 +226,7 @@ class SeriesTable {
   size_t last_relayouts_ = 0;
   uint64_t compiled_gen_ = 0;  // generation of the last render_compiled
   bool parse_check_ = true;    // segments were laid out since their parses were last checked
+  bool debug_relayout_ = false;  // GPUEXP_DEBUG_RELAYOUT: log every family laid out again (stderr)
   uint64_t rebuild_gen_ = 0;   // generation of the last layout change
   size_t last_copied_ = 0;
   uint64_t library_gzips_ = 0; // gzip members made by the library compressor (layout not settled)
