@@ -919,8 +919,8 @@ def main() -> int:
             # gzip copies made by the sampler (scrape expected before the next tick) and by the
             # HTTP worker for off-schedule requests (each adds one compression to that scrape)
             "gzip_compressions": gz_where or None,
-            # compiled exposition over the run: families laid out again, gzip members from the library
-            # compressor while the layout settled, Huffman code builds
+            # compiled exposition over the run: families laid out again, segments encoded without
+            # matches while the layout settled, Huffman code builds
             "exposition_events": {lab.get("event"): int(v) for _, lab, v in
                                   promtext.samples(fams, "gpuexp_exposition_events_total")} or None,
             # KFD process scans over the run: directory listings vs tracked-only reads, and how

@@ -408,8 +408,8 @@ void Engine::define_families() {
   f_self_render_bytes_ = add("gpuexp_render_bytes", "Size of the last rendered exposition", G, {});
   f_self_expo_ = add("gpuexp_exposition_events_total",
                      "Compiled exposition: families laid out again (a series appeared or went, a value outgrew "
-                     "its field), gzip members made by the library compressor while the layout settled, and "
-                     "Huffman code builds (0 per tick in steady state)", C, {"event"});
+                     "its field), segments encoded without matches while the layout settled, and Huffman code "
+                     "builds (0 per tick in steady state)", C, {"event"});
   f_self_series_ = add("gpuexp_series", "Series in the last rendered exposition", G, {});
   f_self_dev_errors_ = add("gpuexp_device_errors_total", "Failed telemetry reads per GPU", C, {"gpu"});
   f_self_overruns_ = add("gpuexp_tick_overruns_total", "Ticks skipped because a tick ran past its deadline", C, {});
@@ -1622,9 +1622,11 @@ void Engine::emit_self(uint64_t gen) {
   for (int k = 0; k < kDevParts; ++k)
     cput(dev_part_refs_[k], f_self_dev_part_, dev_part_total_s_[k], gen,
          [&] { return std::vector<std::string>{dev_part_name(k)}; });
-  // histograms: accumulated every tick, published at most once a second (see engine.h)
+  // histograms: accumulated every tick, published every tick at <= 10 Hz (or manual ticks) and at
+  // most once a second above that (see engine.h)
   const uint64_t hnow = last_tick_now_;
-  const bool publish_hist = !self_hist_pub_ns_ || hnow < self_hist_pub_ns_ || hnow - self_hist_pub_ns_ >= 1000000000ull;
+  const bool publish_hist = cfg_.interval_s <= 0 || cfg_.interval_s >= 0.1 || !self_hist_pub_ns_ ||
+                            hnow < self_hist_pub_ns_ || hnow - self_hist_pub_ns_ >= 1000000000ull;
   if (publish_hist) self_hist_pub_ns_ = hnow;
   const std::vector<double>& sb = stage_bounds();
   for (int k = 0; k < kStages; ++k) {
@@ -1704,8 +1706,8 @@ void Engine::emit_self(uint64_t gen) {
     cput(self_refs_[20], f_driver_, 1, gen, [&] { return std::vector<std::string>{driver_version_, kernel_release_}; });
   if (compiled_) {
     cput(expo_refs_[0], f_self_expo_, double(expo_relayouts_), gen, [] { return std::vector<std::string>{"relayout"}; });
-    cput(expo_refs_[1], f_self_expo_, double(table_.library_gzips()), gen,
-         [] { return std::vector<std::string>{"library_gzip"}; });
+    cput(expo_refs_[1], f_self_expo_, double(table_.literal_parses()), gen,
+         [] { return std::vector<std::string>{"literal_segment"}; });
     cput(expo_refs_[2], f_self_expo_, double(table_.code_builds()), gen,
          [] { return std::vector<std::string>{"code_build"}; });
   }

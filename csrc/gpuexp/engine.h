@@ -386,8 +386,9 @@ class Engine {
   SeriesRef self_refs_[21];
   SeriesRef expo_refs_[3];
   // The self-observability histograms (per-stage tick time, scrape latency) accumulate every
-  // tick here and are published into the table at most once a second: re-rendering and
-  // re-splicing ~120 bucket lines per tick was most of a 100 Hz tick's exposition work.
+  // tick here; above 10 Hz they are published into the table at most once a second:
+  // re-rendering and re-splicing ~120 bucket lines per tick was most of a 100 Hz tick's
+  // exposition work.
   std::vector<uint64_t> stage_hist_[8];
   double stage_hist_sum_[8] = {};
   uint64_t stage_hist_n_[8] = {};

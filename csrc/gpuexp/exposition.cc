@@ -1,7 +1,5 @@
 #include "gpuexp/exposition.h"
 
-#include "gpuexp/snapshot.h"  // gzip_compress
-
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -466,14 +464,16 @@ void SeriesTable::layout_family(int fid, uint64_t gen, std::string* body) {
     for (size_t f = 0; f < nf; ++f) {
       body->append(hist ? s.hlines[f] : s.line);
       const uint8_t len = scratch_len_[f];
-      // Room to grow, so the body settles within a few ticks: a field that outgrew its width (and
-      // a counter's or histogram's from the start: they only grow) gets two more digits if it is
-      // an integer, the typical longest shortest-round-trip form (20) if it is a fraction.
-      const bool grows = s.widths[f] ? len > s.widths[f] : fam.def.type != MetricType::kGauge;
-      if (grows) {
+      // Room to grow, so the body settles within a few ticks (on silicon the first ~10 ticks laid
+      // out ~100 families again: sentinel latencies, activity percentages): a fraction gets the
+      // typical longest shortest-round-trip form (20) from the start; an integer one more digit
+      // (a gauge) or two (a counter or histogram count: they only grow), and two more whenever
+      // it outgrows its field.
+      if (!s.widths[f] || len > s.widths[f]) {
         const char* t = &scratch_[32 * f];
         const bool frac = std::memchr(t, '.', len) || std::memchr(t, 'e', len);
-        s.widths[f] = uint8_t(std::min<int>(32, frac ? std::max<int>(len, 20) : len + 2));
+        const int room = s.widths[f] || fam.def.type != MetricType::kGauge ? 2 : 1;
+        s.widths[f] = uint8_t(std::min<int>(32, frac ? std::max<int>(len, 20) : len + room));
       }
       s.widths[f] = std::max(s.widths[f], len);
       L.seg.fields.push_back({uint32_t(body->size() - base), s.widths[f]});
@@ -612,7 +612,6 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
         layout_family(fid, gen, &cbody_next_);
         ++last_relayouts_;
         ++last_rebuilt_;
-        relaid_bytes_ += L.seg.len;
       } else {
         const size_t nb = cbody_next_.size();
         cbody_next_.append(cbody_, L.seg.base, L.seg.len);
@@ -647,33 +646,40 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
     last_copied_ = cbody_.size();
   }
   if (!gz) return;
-  // While the layout still moves (warm-up: values reaching their widths; a process appearing)
-  // the whole body goes through the library compressor: a parse costs more than one
-  // compression, and would be thrown away by the next layout change.  After kStableRenders
-  // renders without a layout change the changed segments are parsed once.
-  if (parse_check_ && gen - rebuild_gen_ < kStableRenders) {
-    if (!gzip_compress(cbody_, gz, 1)) gz->clear();
-    ++library_gzips_;
-    return;
-  }
-  // (re-)parse laid-out segments and those whose matches reached into a segment laid out
-  // since; consecutive ones as one run (only after a rebuild: otherwise every parse stands)
-  for (size_t i = 0; parse_check_ && i < csegs_.size();) {
-    if (TemplateDeflate::parse_valid(csegs_, i)) {
-      ++i;
-      continue;
+  // A segment laid out again (and any whose matches reached into it) is first encoded without
+  // matches -- static bytes as literals under the current code, O(bytes) -- while the layout still
+  // moves (warm-up: values reaching their widths; a process appearing); once it held for
+  // kStableRenders renders, those segments get one real parse (consecutive ones as one run).
+  if (parse_check_) {
+    const bool stable = gen - rebuild_gen_ >= kStableRenders;
+    for (size_t i = 0; i < csegs_.size();) {
+      TmplSegment* seg = csegs_[i];
+      const bool valid = TemplateDeflate::parse_valid(csegs_, i);
+      if (!stable) {
+        if (!valid) {
+          TemplateDeflate::parse_literal(seg);
+          ++literal_parses_;
+        }
+        ++i;
+        continue;
+      }
+      if (valid && !seg->literal_only) {
+        ++i;
+        continue;
+      }
+      size_t j = i;
+      for (; j < csegs_.size() && (!TemplateDeflate::parse_valid(csegs_, j) || csegs_[j]->literal_only); ++j)
+        relaid_bytes_ += csegs_[j]->len;
+      TemplateDeflate::parse(cbody_.data(), csegs_, i, j);
+      i = j;
     }
-    size_t j = i;
-    for (; j < csegs_.size() && !TemplateDeflate::parse_valid(csegs_, j); ++j)
-      if (csegs_[j]->parsed) relaid_bytes_ += csegs_[j]->len;  // a dependant: its bits change too
-    TemplateDeflate::parse(cbody_.data(), csegs_, i, j);
-    i = j;
+    if (stable) parse_check_ = false;
   }
-  parse_check_ = false;
-  // The code is complete (any segment encodes under it); it is rebuilt for compression once as
-  // many bytes as the body holds were laid out or re-parsed since the last build (a build
-  // re-encodes every segment: ~0.7 ms for an 8-GPU body).
-  if (!deflate_.have_code() || relaid_bytes_ > cbody_.size()) {
+  // The code is complete (any segment encodes under it); it is rebuilt for compression once half
+  // as many bytes as the body holds were (re-)parsed since the last build (a build re-encodes
+  // every segment: ~0.7 ms for an 8-GPU body) -- so the first real parse of the whole body, after
+  // the warm-up's literal encodes, gets a code of its own.
+  if (!deflate_.have_code() || 2 * relaid_bytes_ > cbody_.size()) {
     deflate_.build_code(cbody_.data(), csegs_);
     relaid_bytes_ = 0;
     ++code_builds_;

@@ -96,7 +96,8 @@ class SeriesTable {
   size_t last_relayouts() const { return last_relayouts_; }
   size_t last_skipped() const { return last_skipped_; }
   size_t last_walked() const { return last_walked_; }
-  uint64_t library_gzips() const { return library_gzips_; }
+  // Segments encoded without matches while the layout settled (cumulative).
+  uint64_t literal_parses() const { return literal_parses_; }
   // Bytes copied into `out` by the last render_compiled (the whole body, or the changed fields).
   size_t last_copied() const { return last_copied_; }
   uint64_t code_builds() const { return code_builds_; }
@@ -229,12 +230,12 @@ class SeriesTable {
   bool debug_relayout_ = false;  // GPUEXP_DEBUG_RELAYOUT: log every family laid out again (stderr)
   uint64_t rebuild_gen_ = 0;   // generation of the last layout change
   size_t last_copied_ = 0;
-  uint64_t library_gzips_ = 0; // gzip members made by the library compressor (layout not settled)
-  static constexpr uint64_t kStableRenders = 4;
+  uint64_t literal_parses_ = 0;  // segments encoded literal-only while the layout settled
+  static constexpr uint64_t kStableRenders = 8;
   size_t last_skipped_ = 0;    // families passed over unchanged by the last render_compiled
   size_t last_walked_ = 0;     // families whose members the last render_compiled walked
   uint64_t code_builds_ = 0;
-  size_t relaid_bytes_ = 0;  // bytes laid out again since the code was last built
+  size_t relaid_bytes_ = 0;  // bytes (re-)parsed since the code was last built
   std::vector<char> scratch_;  // field_texts output, 32 bytes per field
   std::vector<uint8_t> scratch_len_;
 };

