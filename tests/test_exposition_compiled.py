@@ -237,3 +237,38 @@ def test_engine_gzip_scrape_inflates_to_the_identity_body(mock_engine):
         _, ident = get("identity")
         assert gzip.decompress(gz) == ident == e.snapshot_text().encode()
     assert e.stats()["gzip_eager"] >= 4
+
+
+def test_compiled_randomized_layouts(native):
+    """Property check (hypothesis): any family set, label values (escapes, unicode), value
+    sequence and liveness pattern renders through the compiled path to exactly the classic
+    renderer's samples, and its gzip member inflates to its text."""
+    hypothesis = pytest.importorskip("hypothesis")
+    st = hypothesis.strategies
+    label = st.text(alphabet=st.characters(blacklist_categories=("Cs",)), max_size=12)
+    value = st.one_of(st.floats(allow_nan=True, allow_infinity=True), st.integers(-10**15, 10**15).map(float))
+
+    @hypothesis.settings(max_examples=40, deadline=None)
+    @hypothesis.given(nfam=st.integers(1, 5), labels=st.lists(label, min_size=1, max_size=6, unique=True),
+                      ticks=st.lists(st.lists(st.one_of(st.none(), value), min_size=30, max_size=30),
+                                     min_size=2, max_size=16))
+    def check(nfam, labels, ticks):
+        a, b = native.SeriesTable(), native.SeriesTable()
+        fa = [a.add_family(f"f{i}_x", f"help {i}", native.MetricType.gauge, ["l"]) for i in range(nfam)]
+        fb = [b.add_family(f"f{i}_x", f"help {i}", native.MetricType.gauge, ["l"]) for i in range(nfam)]
+        for gen, vals in enumerate(ticks, start=1):
+            k = 0
+            for i in range(nfam):
+                for lab in labels:
+                    v = vals[k % len(vals)]
+                    k += 1
+                    if v is None:
+                        continue  # not set this tick
+                    a.put(fa[i], [lab], v, gen)
+                    b.put(fb[i], [lab], v, gen)
+            ref = a.render(gen, 1)
+            txt, gz = b.render_compiled(gen, 1, True)
+            _same(promtext.parse(ref), promtext.parse(txt))
+            assert zlib.decompress(gz, 31) == txt.encode()
+
+    check()
