@@ -221,6 +221,7 @@ void TemplateDeflate::parse_literal(TmplSegment* seg) {
   if (seg->len > p) seg->toks.push_back({0, uint32_t(seg->len) - p, p});
   seg->parsed = true;
   seg->literal_only = true;
+  seg->capped = false;
 }
 
 void TemplateDeflate::parse(const char* body, const std::vector<TmplSegment*>& segs, size_t i0, size_t i1,
@@ -292,6 +293,7 @@ void TemplateDeflate::parse(const char* body, const std::vector<TmplSegment*>& s
     seg->code_epoch = 0;
     seg->splice_valid = false;
     seg->literal_only = false;
+    seg->capped = false;
     const uint32_t start = uint32_t(seg->base - w0);
     const uint32_t seg_end = start + uint32_t(seg->len);
     uint32_t min_src = start;

@@ -35,6 +35,7 @@ struct TmplSegment {
   std::vector<TmplField> fields;  // ascending, non-overlapping, inside [0, len)
 
   uint64_t layout_ver = 0;  // bumped by the owner on every layout change of this segment
+  uint64_t changed_gen = 0; // the owner's generation of that change (how long it has held)
 
   // Compiled (owned by TemplateDeflate).
   struct Tok {
@@ -58,6 +59,7 @@ struct TmplSegment {
   bool splice_valid = false;
   bool parsed = false;
   bool literal_only = false;  // parsed without matches (parse_literal): valid, but worth a real parse
+  bool capped = false;        // parsed with a short lookback (owner's policy): worth a re-parse later
   // Matches may reach back into preceding segments' static bytes: the parse is valid while the
   // same segments, at the same layout versions, precede this one (nearest first).
   std::vector<std::pair<const TmplSegment*, uint64_t>> deps;

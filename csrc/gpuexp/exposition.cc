@@ -487,6 +487,7 @@ void SeriesTable::layout_family(int fid, uint64_t gen, std::string* body) {
   L.seg.parsed = false;
   L.seg.code_epoch = 0;
   L.seg.splice_valid = false;
+  L.seg.changed_gen = gen;
   L.seg.layout_ver += 1;
   L.valid = true;
   L.relayout = false;
@@ -651,29 +652,57 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
   // moves (warm-up: values reaching their widths; a process appearing); once it held for
   // kStableRenders renders, those segments get one real parse (consecutive ones as one run).
   if (parse_check_) {
-    const bool stable = gen - rebuild_gen_ >= kStableRenders;
+    // Per segment: one laid out within the last kStableRenders renders is still settling.  A run
+    // of settled segments that need a parse gets one, its matches reaching back no further than
+    // the nearest settling segment (so a neighbour that moves again cannot invalidate it).
+    // A segment parsed with its lookback cut short by a settling neighbour is parsed again once
+    // no segment within its window settles any more.
+    auto settling = [&](size_t k) { return gen - csegs_[k]->changed_gen < kStableRenders; };
+    auto blocked = [&](size_t k) {  // a settling segment within kLookback before segs[k]
+      for (size_t m = k; m > 0 && csegs_[k]->base - (csegs_[m - 1]->base + csegs_[m - 1]->len) < kLookback; --m)
+        if (settling(m - 1)) return true;
+      return false;
+    };
+    bool pending = false;
+    auto needs = [&](size_t k) {
+      const TmplSegment* s = csegs_[k];
+      if (!TemplateDeflate::parse_valid(csegs_, k) || s->literal_only) return true;
+      if (!s->capped) return false;
+      if (!blocked(k)) return true;
+      pending = true;
+      return false;
+    };
     for (size_t i = 0; i < csegs_.size();) {
-      TmplSegment* seg = csegs_[i];
-      const bool valid = TemplateDeflate::parse_valid(csegs_, i);
-      if (!stable) {
-        if (!valid) {
-          TemplateDeflate::parse_literal(seg);
-          ++literal_parses_;
-        }
+      if (!needs(i)) {
         ++i;
         continue;
       }
-      if (valid && !seg->literal_only) {
+      if (settling(i)) {
+        if (!TemplateDeflate::parse_valid(csegs_, i)) {
+          TemplateDeflate::parse_literal(csegs_[i]);
+          ++literal_parses_;
+        }
+        pending = true;
         ++i;
         continue;
       }
       size_t j = i;
-      for (; j < csegs_.size() && (!TemplateDeflate::parse_valid(csegs_, j) || csegs_[j]->literal_only); ++j)
-        relaid_bytes_ += csegs_[j]->len;
-      TemplateDeflate::parse(cbody_.data(), csegs_, i, j);
+      for (; j < csegs_.size() && needs(j) && !settling(j); ++j) relaid_bytes_ += csegs_[j]->len;
+      size_t lookback = kLookback;
+      for (size_t k = i; k > 0; --k) {  // back to the nearest settling segment, at most kLookback
+        if (csegs_[i]->base - csegs_[k - 1]->base > kLookback) break;
+        if (settling(k - 1)) {
+          lookback = csegs_[i]->base - (csegs_[k - 1]->base + csegs_[k - 1]->len);
+          break;
+        }
+      }
+      TemplateDeflate::parse(cbody_.data(), csegs_, i, j, lookback);
+      if (lookback < kLookback && csegs_[i]->base > lookback)
+        for (size_t k = i; k < j && csegs_[k]->base - csegs_[i]->base + lookback < kLookback; ++k)
+          csegs_[k]->capped = true;
       i = j;
     }
-    if (stable) parse_check_ = false;
+    parse_check_ = pending;
   }
   // The code is complete (any segment encodes under it); it is rebuilt for compression once half
   // as many bytes as the body holds were (re-)parsed since the last build (a build re-encodes

@@ -232,6 +232,7 @@ class SeriesTable {
   size_t last_copied_ = 0;
   uint64_t literal_parses_ = 0;  // segments encoded literal-only while the layout settled
   static constexpr uint64_t kStableRenders = 8;
+  static constexpr size_t kLookback = 8192;  // how far a segment's matches may reach back
   size_t last_skipped_ = 0;    // families passed over unchanged by the last render_compiled
   size_t last_walked_ = 0;     // families whose members the last render_compiled walked
   uint64_t code_builds_ = 0;

@@ -272,3 +272,27 @@ def test_compiled_randomized_layouts(native):
             assert zlib.decompress(gz, 31) == txt.encode()
 
     check()
+
+
+def test_settling_is_per_family(native):
+    """One family laid out again every few ticks (a value outgrowing, a process coming) must not
+    keep the rest of the body in literal-only encoding: each family gets its real parse once it
+    has held for 8 renders, whatever the others do (on silicon, an owner-label change re-laid 70
+    families at once while a few kept moving, profiles/r05/session6)."""
+    (t, ids, h), _ = _tables(native, 12)
+    sizes = []
+    for gen in range(1, 60):
+        owner = "pod-a" if gen < 14 else "pod-b"  # every series renamed at 14 (a new owner label)
+        for i, f in enumerate(ids):
+            v = float(10 ** (gen // 5)) if i == 5 else 1.0  # family 5 outgrows its field every 5 ticks
+            for g in range(4):
+                t.put(f, [str(g), owner], v, gen)
+        txt, gz = t.render_compiled(gen, 1, True)
+        assert gzip.decompress(gz) == txt.encode()
+        sizes.append(len(gz))
+    settled_before, all_literal = sizes[12], sizes[14]
+    # family 5 (field room: one extra digit) is laid out again at 25 and 40; only it encodes
+    # literal-only meanwhile, and everything else -- including the segments whose matches had to
+    # stop short of it -- gets its full parse back once it settles (gens 33..39)
+    assert max(sizes[24:32]) < 0.5 * all_literal, (all_literal, sizes[24:32])
+    assert max(sizes[32:39]) < 1.05 * settled_before, (settled_before, sizes[32:39])

@@ -246,8 +246,8 @@ def test_eight_agents_inline_and_thread_machines_at_once(native):
             assert x["uncollected"] <= (1 if i in (3, 6) else 0), (inline, i, x)
             if i != 6:
                 assert x["bad_windows"] == 0, (inline, i, x)
-        for i in (0, 1, 7):  # (GPU 1's 3 ms reads outlast the sync: a few merged windows)
-            assert g[i]["windows"] >= r["ticks"] - (12 if i == 1 else 5), (inline, i, g[i])
+        for i in (0, 1, 7):  # (GPU 1's 3 ms reads outlast the sync: merged windows, more under CPU load)
+            assert g[i]["windows"] >= r["ticks"] - (20 if i == 1 else 5), (inline, i, g[i])
         assert (g[2]["resets"], g[2]["rearms"], g[2]["arms"]) == (1, 1, 1)
         assert (g[3]["rescues"], g[3]["releases"]) == (1, 1) and g[3]["stalls"] >= 3
         assert (g[4]["rearms"], g[4]["conflicts"]) == (1, 3)
