@@ -451,6 +451,13 @@ void SeriesTable::layout_family(int fid, uint64_t gen, std::string* body) {
   const size_t base = body->size();
   body->append(fam.header);
   const bool hist = fam.def.type == MetricType::kHistogram;
+  const std::string& nm = fam.def.name;
+  auto ends = [&](const char* suf) {
+    const size_t n = std::strlen(suf);
+    return nm.size() >= n && nm.compare(nm.size() - n, n, suf) == 0;
+  };
+  const bool frac_unit = ends("_seconds") || ends("_seconds_total") || ends("_percent") || ends("_ratio") ||
+                         ends("_per_second");
   for (uint32_t idx : fam.members) {
     Hot& h = hot_[idx];
     if (h.gen != gen) continue;
@@ -469,11 +476,15 @@ void SeriesTable::layout_family(int fid, uint64_t gen, std::string* body) {
       // typical longest shortest-round-trip form (20) from the start; an integer one more digit
       // (a gauge) or two (a counter or histogram count: they only grow), and two more whenever
       // it outgrows its field.
+      // A fraction may later print as any shortest round-trip form, up to 24 characters
+      // ("-1.2345678901234567e-308"), so it gets all of them once it outgrows its first 20; so
+      // does a value of a fractional unit still integral (a latency of 0 before its first sample).
       if (!s.widths[f] || len > s.widths[f]) {
         const char* t = &scratch_[32 * f];
-        const bool frac = std::memchr(t, '.', len) || std::memchr(t, 'e', len);
+        const bool frac = std::memchr(t, '.', len) || std::memchr(t, 'e', len) ||
+                          (frac_unit && (!hist || f == s.bounds.size() + 1));
         const int room = s.widths[f] || fam.def.type != MetricType::kGauge ? 2 : 1;
-        s.widths[f] = uint8_t(std::min<int>(32, frac ? std::max<int>(len, 20) : len + room));
+        s.widths[f] = uint8_t(frac ? std::max<int>(len, s.widths[f] ? 24 : 20) : std::min<int>(32, len + room));
       }
       s.widths[f] = std::max(s.widths[f], len);
       L.seg.fields.push_back({uint32_t(body->size() - base), s.widths[f]});

@@ -158,13 +158,13 @@ def test_outgrown_field_relayouts_only_its_family(native):
     assert t.last_relayouts() == 1
     assert gzip.decompress(gz) == txt.encode()
     # back to a short value: the field keeps its width (blank-padded; an outgrown fraction
-    # field gets the room of a typical longest round-trip form, 20), no new layout
+    # field gets the room of the longest round-trip form, 24), no new layout
     for f in ids:
         t.put(f, ["0", "a"], 5.0, 5)
     txt, gz = t.render_compiled(5, 1, True)
     assert t.last_relayouts() == 0
     line = [ln for ln in txt.splitlines() if ln.startswith("m03_")][0]
-    assert line.endswith("5" + " " * 19)
+    assert line.endswith("5" + " " * 23)
     # an outgrown integer field keeps two more digits of room
     for f in ids:
         t.put(f, ["0", "a"], 5.0, 6)
