@@ -572,7 +572,7 @@ PYBIND11_MODULE(_gpuexp, m) {
          "render_compiled into a kept buffer (slot): (text, gzip, bytes copied into the buffer)")
       .def("last_relayouts", &SeriesTable::last_relayouts)
       .def("last_skipped", &SeriesTable::last_skipped)
-      .def("literal_parses", &SeriesTable::literal_parses)
+      .def("provisional_parses", &SeriesTable::provisional_parses)
       .def("code_builds", &SeriesTable::code_builds)
       .def("set_histogram", [](SeriesTable& t, int fid, std::vector<std::string> labels, std::vector<double> bounds,
                                std::vector<uint64_t> counts, double sum, uint64_t count, uint64_t gen) {

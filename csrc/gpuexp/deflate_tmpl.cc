@@ -204,26 +204,6 @@ bool TemplateDeflate::parse_valid(const std::vector<TmplSegment*>& segs, size_t 
   return true;
 }
 
-void TemplateDeflate::parse_literal(TmplSegment* seg) {
-  seg->toks.clear();
-  seg->words.clear();
-  seg->piece_bits.clear();
-  seg->deps.clear();
-  seg->code_epoch = 0;
-  seg->splice_valid = false;
-  uint32_t p = 0;
-  for (size_t fi = 0; fi < seg->fields.size(); ++fi) {
-    const TmplField& f = seg->fields[fi];
-    if (f.off > p) seg->toks.push_back({0, f.off - p, p});
-    seg->toks.push_back({2, 0, uint32_t(fi)});
-    p = f.off + f.width;
-  }
-  if (seg->len > p) seg->toks.push_back({0, uint32_t(seg->len) - p, p});
-  seg->parsed = true;
-  seg->literal_only = true;
-  seg->capped = false;
-}
-
 void TemplateDeflate::parse(const char* body, const std::vector<TmplSegment*>& segs, size_t i0, size_t i1,
                             size_t lookback) {
   if (i1 <= i0) return;
@@ -292,7 +272,7 @@ void TemplateDeflate::parse(const char* body, const std::vector<TmplSegment*>& s
     seg->deps.clear();
     seg->code_epoch = 0;
     seg->splice_valid = false;
-    seg->literal_only = false;
+    seg->provisional = false;
     seg->capped = false;
     const uint32_t start = uint32_t(seg->base - w0);
     const uint32_t seg_end = start + uint32_t(seg->len);

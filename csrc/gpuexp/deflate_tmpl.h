@@ -58,7 +58,7 @@ struct TmplSegment {
   size_t spliced_bits = 0;
   bool splice_valid = false;
   bool parsed = false;
-  bool literal_only = false;  // parsed without matches (parse_literal): valid, but worth a real parse
+  bool provisional = false;   // parsed on its own (lookback 0, owner's policy): valid, but worth a real parse
   bool capped = false;        // parsed with a short lookback (owner's policy): worth a re-parse later
   // Matches may reach back into preceding segments' static bytes: the parse is valid while the
   // same segments, at the same layout versions, precede this one (nearest first).
@@ -72,9 +72,6 @@ class TemplateDeflate {
   // static bytes only); segs tile `body`.  A run of consecutive segments shares one hash state.
   static void parse(const char* body, const std::vector<TmplSegment*>& segs, size_t i0, size_t i1,
                     size_t lookback = 8192);
-  // Tokens without LZ77 matches (static bytes as literals), in O(len): a segment laid out again
-  // encodes this way until the layout settles and a real parse pays off.
-  static void parse_literal(TmplSegment* seg);
   // Whether segs[i]'s parse still holds (its cross-segment references point at the same bytes).
   static bool parse_valid(const std::vector<TmplSegment*>& segs, size_t i);
 

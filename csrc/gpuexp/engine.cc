@@ -1706,8 +1706,8 @@ void Engine::emit_self(uint64_t gen) {
     cput(self_refs_[20], f_driver_, 1, gen, [&] { return std::vector<std::string>{driver_version_, kernel_release_}; });
   if (compiled_) {
     cput(expo_refs_[0], f_self_expo_, double(expo_relayouts_), gen, [] { return std::vector<std::string>{"relayout"}; });
-    cput(expo_refs_[1], f_self_expo_, double(table_.literal_parses()), gen,
-         [] { return std::vector<std::string>{"literal_segment"}; });
+    cput(expo_refs_[1], f_self_expo_, double(table_.provisional_parses()), gen,
+         [] { return std::vector<std::string>{"provisional_parse"}; });
     cput(expo_refs_[2], f_self_expo_, double(table_.code_builds()), gen,
          [] { return std::vector<std::string>{"code_build"}; });
   }

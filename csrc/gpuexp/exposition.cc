@@ -658,10 +658,11 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
     last_copied_ = cbody_.size();
   }
   if (!gz) return;
-  // A segment laid out again (and any whose matches reached into it) is first encoded without
-  // matches -- static bytes as literals under the current code, O(bytes) -- while the layout still
-  // moves (warm-up: values reaching their widths; a process appearing); once it held for
-  // kStableRenders renders, those segments get one real parse (consecutive ones as one run).
+  // A segment laid out again (and any whose matches reached into it) is first parsed on its own
+  // -- matches within its own bytes only, so no other segment's moves can invalidate it and it
+  // invalidates none -- while its layout still moves (warm-up: values reaching their widths; a
+  // process appearing); once it held for kStableRenders renders it gets one real parse, reaching
+  // back into the segments before it (consecutive ones as one run).
   if (parse_check_) {
     // Per segment: one laid out within the last kStableRenders renders is still settling.  A run
     // of settled segments that need a parse gets one, its matches reaching back no further than
@@ -677,7 +678,7 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
     bool pending = false;
     auto needs = [&](size_t k) {
       const TmplSegment* s = csegs_[k];
-      if (!TemplateDeflate::parse_valid(csegs_, k) || s->literal_only) return true;
+      if (!TemplateDeflate::parse_valid(csegs_, k) || s->provisional) return true;
       if (!s->capped) return false;
       if (!blocked(k)) return true;
       pending = true;
@@ -690,8 +691,9 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
       }
       if (settling(i)) {
         if (!TemplateDeflate::parse_valid(csegs_, i)) {
-          TemplateDeflate::parse_literal(csegs_[i]);
-          ++literal_parses_;
+          TemplateDeflate::parse(cbody_.data(), csegs_, i, i + 1, 0);
+          csegs_[i]->provisional = true;
+          ++provisional_parses_;
         }
         pending = true;
         ++i;
@@ -718,7 +720,7 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
   // The code is complete (any segment encodes under it); it is rebuilt for compression once half
   // as many bytes as the body holds were (re-)parsed since the last build (a build re-encodes
   // every segment: ~0.7 ms for an 8-GPU body) -- so the first real parse of the whole body, after
-  // the warm-up's literal encodes, gets a code of its own.
+  // the warm-up's provisional parses, gets a code of its own.
   if (!deflate_.have_code() || 2 * relaid_bytes_ > cbody_.size()) {
     deflate_.build_code(cbody_.data(), csegs_);
     relaid_bytes_ = 0;

@@ -97,7 +97,7 @@ class SeriesTable {
   size_t last_skipped() const { return last_skipped_; }
   size_t last_walked() const { return last_walked_; }
   // Segments encoded without matches while the layout settled (cumulative).
-  uint64_t literal_parses() const { return literal_parses_; }
+  uint64_t provisional_parses() const { return provisional_parses_; }
   // Bytes copied into `out` by the last render_compiled (the whole body, or the changed fields).
   size_t last_copied() const { return last_copied_; }
   uint64_t code_builds() const { return code_builds_; }
@@ -230,7 +230,7 @@ class SeriesTable {
   bool debug_relayout_ = false;  // GPUEXP_DEBUG_RELAYOUT: log every family laid out again (stderr)
   uint64_t rebuild_gen_ = 0;   // generation of the last layout change
   size_t last_copied_ = 0;
-  uint64_t literal_parses_ = 0;  // segments encoded literal-only while the layout settled
+  uint64_t provisional_parses_ = 0;  // segments parsed on their own while their layout settled
   static constexpr uint64_t kStableRenders = 8;
   static constexpr size_t kLookback = 8192;  // how far a segment's matches may reach back
   size_t last_skipped_ = 0;    // families passed over unchanged by the last render_compiled
