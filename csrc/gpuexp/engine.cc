@@ -408,7 +408,7 @@ void Engine::define_families() {
   f_self_render_bytes_ = add("gpuexp_render_bytes", "Size of the last rendered exposition", G, {});
   f_self_expo_ = add("gpuexp_exposition_events_total",
                      "Compiled exposition: families laid out again (a series appeared or went, a value outgrew "
-                     "its field), segments encoded without matches while the layout settled, and Huffman code "
+                     "its field), segments parsed on their own while their layout settled, and Huffman code "
                      "builds (0 per tick in steady state)", C, {"event"});
   f_self_series_ = add("gpuexp_series", "Series in the last rendered exposition", G, {});
   f_self_dev_errors_ = add("gpuexp_device_errors_total", "Failed telemetry reads per GPU", C, {"gpu"});
