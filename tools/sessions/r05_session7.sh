@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-5 GPU session 7: per-segment settling (each segment on its own clock, capped parses redone),
-# 24-character fraction fields:
+# provisional self-contained parses while a family settles, 24-character fraction fields:
+# the whole GPU tier, smoke, the driver's command x3 (one with the relayout log), config 5 x2.
 # the whole GPU tier, smoke, the driver's command x3 (one with the relayout log), config 5 x2.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/r05s7
