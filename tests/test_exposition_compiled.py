@@ -298,3 +298,54 @@ def test_settling_is_per_family(native):
     # stop short of it -- gets its full parse back once it settles (gens 33..39)
     assert max(sizes[24:32]) < 0.6 * all_provisional, (all_provisional, sizes[24:32])
     assert max(sizes[32:39]) < 1.05 * settled_before, (settled_before, sizes[32:39])
+
+
+def test_compiled_randomized_settling(native):
+    """Property check (hypothesis) of the settling policy: families disturbed on a random schedule
+    (a value outgrowing its field, a series gone for a tick, every series renamed), gzip asked for
+    on random ticks only.  Every gzip member inflates to its text, every text parses to the
+    classic renderer's samples, and once the body has been quiet for 10 renders its gzip is as
+    small as a fresh table's settled one: no segment is left provisional or cut short."""
+    hypothesis = pytest.importorskip("hypothesis")
+    st = hypothesis.strategies
+    event = st.tuples(st.integers(1, 30), st.integers(0, 7), st.sampled_from(["outgrow", "drop", "rename"]))
+
+    def state(nfam, evs, gen):
+        """{(family, label): value} at `gen` under the events so far."""
+        out = {}
+        for i in range(nfam):
+            mine = [(t, k) for t, f, k in evs if f % nfam == i and t <= gen]
+            grow = sum(1 for t, k in mine if k == "outgrow")
+            owner = "own-%d" % sum(1 for t, k in mine if k == "rename")
+            gone = any(t == gen and k == "drop" for t, k in mine)
+            for g in range(3):
+                if not (gone and g == 1):
+                    out[(i, (str(g), owner))] = float(10 ** (2 * grow)) + g
+        return out
+
+    @hypothesis.settings(max_examples=30, deadline=None)
+    @hypothesis.given(nfam=st.integers(2, 8), evs=st.lists(event, max_size=12),
+                      want=st.lists(st.booleans(), min_size=45, max_size=45))
+    def check(nfam, evs, want):
+        a, b, c = native.SeriesTable(), native.SeriesTable(), native.SeriesTable()
+        fams = [[t.add_family(f"f{i}_metric_seconds", f"help of {i}", native.MetricType.gauge, ["gpu", "pod"])
+                 for i in range(nfam)] for t in (a, b, c)]
+        last = None
+        for gen in range(1, 46):
+            for (i, labs), v in state(nfam, evs, gen).items():
+                a.put(fams[0][i], list(labs), v, gen)
+                b.put(fams[1][i], list(labs), v, gen)
+            ref = a.render(gen, 1)
+            txt, gz = b.render_compiled(gen, 1, want[gen - 1] or gen > 40)
+            _same(promtext.parse(ref), promtext.parse(txt))
+            if gz:
+                assert zlib.decompress(gz, 31) == txt.encode(), gen
+                last = gz
+        # a fresh table given the final state from the start, settled the same way
+        for gen in range(1, 12):
+            for (i, labs), v in state(nfam, evs, 45).items():
+                c.put(fams[2][i], list(labs), v, gen)
+            _, fresh = c.render_compiled(gen, 1, True)
+        assert len(last) <= 1.1 * len(fresh) + 16, (len(last), len(fresh))
+
+    check()
