@@ -472,19 +472,19 @@ void SeriesTable::layout_family(int fid, uint64_t gen, std::string* body) {
       body->append(hist ? s.hlines[f] : s.line);
       const uint8_t len = scratch_len_[f];
       // Room to grow, so the body settles within a few ticks (on silicon the first ~10 ticks laid
-      // out ~100 families again: sentinel latencies, activity percentages): a fraction gets the
-      // typical longest shortest-round-trip form (20) from the start; an integer one more digit
-      // (a gauge) or two (a counter or histogram count: they only grow), and two more whenever
-      // it outgrows its field.
-      // A fraction may later print as any shortest round-trip form, up to 24 characters
-      // ("-1.2345678901234567e-308"), so it gets all of them once it outgrows its first 20; so
-      // does a value of a fractional unit still integral (a latency of 0 before its first sample).
+      // out ~100 families again: sentinel latencies, activity percentages).  A fraction may later
+      // print as any shortest round-trip form, up to 24 characters ("-1.2345678901234567e-308"),
+      // so it gets all 24 from the start (with 20, each GPU's CPU-seconds counter on a fake 8-GPU
+      // node outgrew its field at its own tick, one relayout each); so does a value of a
+      // fractional unit still integral (a latency of 0 before its first sample).  An integer gets
+      // one more digit (a gauge) or two (a counter or histogram count: they only grow), and two
+      // more whenever it outgrows its field.
       if (!s.widths[f] || len > s.widths[f]) {
         const char* t = &scratch_[32 * f];
         const bool frac = std::memchr(t, '.', len) || std::memchr(t, 'e', len) ||
                           (frac_unit && (!hist || f == s.bounds.size() + 1));
         const int room = s.widths[f] || fam.def.type != MetricType::kGauge ? 2 : 1;
-        s.widths[f] = uint8_t(frac ? std::max<int>(len, s.widths[f] ? 24 : 20) : std::min<int>(32, len + room));
+        s.widths[f] = uint8_t(frac ? std::max<int>(len, 24) : std::min<int>(32, len + room));
       }
       s.widths[f] = std::max(s.widths[f], len);
       L.seg.fields.push_back({uint32_t(body->size() - base), s.widths[f]});
@@ -700,7 +700,11 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
         continue;
       }
       size_t j = i;
-      for (; j < csegs_.size() && needs(j) && !settling(j); ++j) relaid_bytes_ += csegs_[j]->len;
+      for (; j < csegs_.size() && needs(j) && !settling(j); ++j) {
+        const TmplSegment* s = csegs_[j];
+        // (a capped segment parsed again with its full lookback barely moves the code's statistics)
+        if (!s->capped || s->provisional || !TemplateDeflate::parse_valid(csegs_, j)) relaid_bytes_ += s->len;
+      }
       size_t lookback = kLookback;
       for (size_t k = i; k > 0; --k) {  // back to the nearest settling segment, at most kLookback
         if (csegs_[i]->base - csegs_[k - 1]->base > kLookback) break;

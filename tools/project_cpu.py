@@ -40,7 +40,11 @@ while True:
 
 
 def measure(native, n_gpus: int, hz: float, fetch_us: int, policy: str, budget: float, seconds: float,
-            scrape: str = "none", exposition: str = "compiled") -> dict:
+            scrape: str = "none", exposition: str = "compiled", warmup: float = -1.0) -> dict:
+    # warm-up: long enough for the exposition to settle (a family's real parse comes 8 renders after
+    # its last layout; the scraper's first gzip ask starts the gzip copies): 20 ticks, at least 1 s
+    if warmup < 0:
+        warmup = max(1.0, 20.0 / hz)
     import subprocess
     import test_fakehost as tf
     root = tempfile.mkdtemp(prefix="gpuexp-proj-")
@@ -67,7 +71,7 @@ def measure(native, n_gpus: int, hz: float, fetch_us: int, policy: str, budget: 
     if scrape != "none":  # another process, so its CPU is not the exporter's
         scraper = subprocess.Popen([sys.executable, "-c", SCRAPER, PKG_ROOT, str(e.http_port), str(hz), scrape])
     try:
-        time.sleep(1.0)
+        time.sleep(warmup)
         r0, t0, s0 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter(), e.stats()
         time.sleep(seconds)
         r1, t1, s1 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter(), e.stats()
@@ -100,6 +104,7 @@ def main() -> int:
     ap.add_argument("--gpus", default="1,2,4,8")
     ap.add_argument("--budget", type=float, default=1.5)
     ap.add_argument("--seconds", type=float, default=4.0)
+    ap.add_argument("--warmup", type=float, default=-1.0, help="seconds before measuring (default: 20 ticks, >= 1 s)")
     ap.add_argument("--policies", default="auto,every")
     ap.add_argument("--scrape", default="none", help="none | gzip | identity: a scraper process at the tick rate")
     ap.add_argument("--exposition", default="compiled", help="compiled | classic (comma list to compare)")
@@ -116,7 +121,7 @@ def main() -> int:
             for n in (int(x) for x in args.gpus.split(",")):
                 for policy in args.policies.split(","):
                   for expo in args.exposition.split(","):
-                    r = measure(native, n, hz, fetch, policy, args.budget, args.seconds, args.scrape, expo)
+                    r = measure(native, n, hz, fetch, policy, args.budget, args.seconds, args.scrape, expo, args.warmup)
                     print(f"{r['gpus']:>4} {r['hz']:>5g} {r['fetch_us']:>8} {r['policy']:>6} "
                           f"{r['process_cpu_pct']:>7.2f} {r['sampler_us_per_tick']:>15.1f}  "
                           f"{expo} scrape={args.scrape}", flush=True)
