@@ -1752,6 +1752,11 @@ void Engine::tick_locked(uint64_t now) {
   double dt_s = last_tick_now_ && now > last_tick_now_ ? double(now - last_tick_now_) * 1e-9 : 0.0;
   last_tick_now_ = now;
   uint64_t ts[kStages + 1], cs[kStages + 1];  // stage boundaries: wall, sampler-thread CPU
+  // The per-stage CPU split is sampled on one tick in kStageCpuEvery (a thread CPU clock read is
+  // a system call: 7 of them per tick were ~1 % of an 8-GPU node's tick at 10 Hz); the whole
+  // tick's CPU is read every tick.
+  const bool split_cpu = gen % kStageCpuEvery == 0;
+  auto cpu_mark = [split_cpu]() { return split_cpu ? thread_cpu_ns() : 0; };
   ts[0] = mono_ns();
   cs[0] = cpu0;
   if (!startup_ns_ && start_mono_ns_ && ts[0] > start_mono_ns_) startup_ns_ = ts[0] - start_mono_ns_;
@@ -1873,7 +1878,7 @@ void Engine::tick_locked(uint64_t now) {
     part[0] = mono_ns() - k0;
   }
   ts[1] = mono_ns();
-  cs[1] = thread_cpu_ns();
+  cs[1] = cpu_mark();
   for (int k = 0; k < kDevParts; ++k) dev_part_total_s_[k] += double(part[k]) * 1e-9;
 
   // 1: processes
@@ -1895,7 +1900,7 @@ void Engine::tick_locked(uint64_t now) {
     }
   }
   ts[2] = mono_ns();
-  cs[2] = thread_cpu_ns();
+  cs[2] = cpu_mark();
 
   // 2: device ownership (device plugin map first, then single-pod inference).
   for (size_t i = 0; i < devices_.size(); ++i) {
@@ -1934,17 +1939,17 @@ void Engine::tick_locked(uint64_t now) {
     st.owner = own;
   }
   ts[3] = mono_ns();
-  cs[3] = thread_cpu_ns();
+  cs[3] = cpu_mark();
 
   // 3: sentinel (drain previous run, launch next; never blocks on the GPU)
   if (sentinel_) sentinel_->tick(now);
   if (kfd_events_) count_kfd_events();
   ts[4] = mono_ns();
-  cs[4] = thread_cpu_ns();
+  cs[4] = cpu_mark();
   // 4: counters: wait (bounded) for this tick's read round; sampled in collect_device
   if (counters_ && !counters_->sync(cfg_.counters_sync_us)) counters_late_ += 1;
   ts[5] = mono_ns();
-  cs[5] = thread_cpu_ns();
+  cs[5] = cpu_mark();
 
   // 5: series
   for (size_t i = 0; i < devices_.size(); ++i) {
@@ -1954,7 +1959,7 @@ void Engine::tick_locked(uint64_t now) {
   if (kfd_events_) emit_kfd_events(gen);
   emit_self(gen);
   ts[6] = mono_ns();
-  cs[6] = thread_cpu_ns();
+  cs[6] = cpu_mark();
 
   // 6: render into a free snapshot slot
   int slot = store_.begin_write();
@@ -1976,7 +1981,7 @@ void Engine::tick_locked(uint64_t now) {
     nseries = table_.live_series(gen);
     snap->series = nseries;
     ts[7] = mono_ns();
-    cs[7] = thread_cpu_ns();
+    cs[7] = cpu_mark();
     // 7: gzip (classic; compiled emitted it with the body) + publish
     snap->pb.clear();
     snap->pb_gz.clear();
@@ -1992,7 +1997,7 @@ void Engine::tick_locked(uint64_t now) {
     if (http_) http_->set_ready(true);
   } else {
     ts[7] = mono_ns();
-    cs[7] = thread_cpu_ns();
+    cs[7] = cpu_mark();
   }
   if (counters_ && kick_end) counters_->kick();  // next tick's read, completing while we sleep
   uint64_t tend = mono_ns();
@@ -2022,13 +2027,14 @@ void Engine::tick_locked(uint64_t now) {
     stats_.device_errors += errs;
     for (int k = 0; k < kStages; ++k) {
       stats_.stage_ns[k] = double(stage_dur[k]);
-      stats_.stage_cpu_ns[k] += cs[k + 1] - cs[k];  // the sampler thread's own CPU per stage
+      if (split_cpu)  // the sampler thread's own CPU per stage, scaled up from the sampled ticks
+        stats_.stage_cpu_ns[k] += kStageCpuEvery * (cs[k + 1] - cs[k]);
     }
     // every thread that worked for this tick: the sampler, the per-GPU read pool, and the
     // counter plugin's thread (its PM4 read rounds since the last tick)
     // The sampler thread charges its whole clock since the last tick (timerfd wake-ups
     // included); a manual tick_now() from another thread charges the tick itself.
-    const uint64_t own = thread_cpu_ns();
+    const uint64_t own = cs[kStages];
     uint64_t cpu = own - cpu0;
     if (tl_sampler_thread) {
       if (sampler_cpu_seen_ && own >= sampler_cpu_seen_) cpu = own - sampler_cpu_seen_;

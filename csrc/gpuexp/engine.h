@@ -208,6 +208,7 @@ class Engine {
 
   static const char* stage_name(int i);
   static constexpr int kStages = 8;
+  static constexpr uint64_t kStageCpuEvery = 4;  // ticks per sampled per-stage CPU split
   // The devices stage split (gpuexp_device_read_seconds_total{part}): PMC read kick,
   // control-plane apply, gpu_metrics (SMU fetch or cached decode), VRAM-used file, RAS/AER
   // files, GTT file.  Per-GPU parts are summed over GPUs (wall time on whichever thread).
