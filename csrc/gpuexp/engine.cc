@@ -1754,8 +1754,9 @@ void Engine::tick_locked(uint64_t now) {
   uint64_t ts[kStages + 1], cs[kStages + 1];  // stage boundaries: wall, sampler-thread CPU
   // The per-stage CPU split is sampled on one tick in kStageCpuEvery (a thread CPU clock read is
   // a system call: 7 of them per tick were ~1 % of an 8-GPU node's tick at 10 Hz); the whole
-  // tick's CPU is read every tick.
-  const bool split_cpu = gen % kStageCpuEvery == 0;
+  // tick's CPU is read every tick.  Which ticks: a hash of the generation, so a periodic stage
+  // (a gpu_metrics fetch every 2nd or 4th tick) is not always in or always out of the sample.
+  const bool split_cpu = ((gen * 0x9E3779B97F4A7C15ull) >> 61) % kStageCpuEvery == 0;
   auto cpu_mark = [split_cpu]() { return split_cpu ? thread_cpu_ns() : 0; };
   ts[0] = mono_ns();
   cs[0] = cpu0;
