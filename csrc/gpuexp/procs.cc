@@ -435,9 +435,11 @@ void PidResolver::clear_overrides() {
 }
 
 void PidResolver::gc(const std::vector<int>& live_pids) {
-  std::unordered_set<int> live(live_pids.begin(), live_pids.end());
+  // (every tick: a sorted scratch vector, no hash set built and freed each time)
+  gc_live_.assign(live_pids.begin(), live_pids.end());
+  std::sort(gc_live_.begin(), gc_live_.end());
   for (auto it = cache_.begin(); it != cache_.end();)
-    it = live.count(it->first) ? std::next(it) : cache_.erase(it);
+    it = std::binary_search(gc_live_.begin(), gc_live_.end(), it->first) ? std::next(it) : cache_.erase(it);
 }
 
 }  // namespace gpuexp

@@ -134,6 +134,7 @@ class PidResolver {
   uint64_t epoch_ = 1, now_ns_ = 0;
   std::string root_;
   std::unordered_map<int, Entry> cache_;
+  std::vector<int> gc_live_;  // gc() scratch
   std::unordered_map<int, std::string> overrides_;
 };
 
