@@ -235,13 +235,17 @@ void TemplateDeflate::parse(const char* body, const std::vector<TmplSegment*>& s
     }
     for (; p < n; ++p) static_end[p] = n;
   }
+  // hash table sized to the window (a settling family parsed on its own is a few hundred bytes:
+  // clearing 2^13 heads for each of ~100 such parses at start-up cost more than the parses)
+  int hb = 8;
+  while (hb < kHashBits && (uint32_t(1) << hb) < n) ++hb;
   thread_local std::vector<int32_t> head, prev;
-  head.assign(size_t(1) << kHashBits, -1);
+  head.assign(size_t(1) << hb, -1);
   prev.resize(n);
   auto hash = [&](uint32_t p) {
     uint32_t v;
     std::memcpy(&v, s + p, 4);
-    return (v * 2654435761u) >> (32 - kHashBits);
+    return (v * 2654435761u) >> (32 - hb);
   };
   auto insert = [&](uint32_t p) {
     if (p + kMinMatch > static_end[p]) return;  // fewer than 4 static bytes: never a source
