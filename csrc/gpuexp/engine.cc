@@ -1230,7 +1230,8 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
 void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSample>>& per_dev) {
   // pid -> attribution, resolved once per tick (and kept while KFD vouches for the process)
   unresolved_.clear();
-  std::vector<int> live;
+  std::vector<int>& live = live_scratch_;
+  live.clear();
   for (auto& lst : per_dev)
     for (auto& p : lst) {
       ProcAttr& a = attr_cache_[p.pid];
@@ -1883,7 +1884,10 @@ void Engine::tick_locked(uint64_t now) {
   for (int k = 0; k < kDevParts; ++k) dev_part_total_s_[k] += double(part[k]) * 1e-9;
 
   // 1: processes
-  std::vector<std::vector<ProcSample>> per_dev(devices_.size());
+  // (reused across ticks: the lists keep their capacity, no allocation per tick)
+  std::vector<std::vector<ProcSample>>& per_dev = per_dev_;
+  per_dev.resize(devices_.size());
+  for (auto& l : per_dev) l.clear();
   if (cfg_.process_source != "none") {
     bool from_backend = cfg_.process_source != "kfd";
     if (from_backend)

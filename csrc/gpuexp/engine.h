@@ -369,6 +369,8 @@ class Engine {
   std::unordered_map<std::string, std::string> container_names_;  // cid -> name
   std::unordered_map<std::string, DeviceOwner> owners_;           // lower(device id) -> owner
   std::set<std::string> unresolved_;                               // pod UIDs without metadata (last tick)
+  std::vector<std::vector<ProcSample>> per_dev_;  // tick scratch: processes per device
+  std::vector<int> live_scratch_;                 // tick scratch: PIDs seen this tick
   std::unordered_map<uint64_t, ProcRefs> proc_refs_;               // (device << 32 | pid) -> handles
   std::unordered_map<uint64_t, ProcRefs> legacy_refs_;             // pid -> legacy handles (pod, vram, gfx=perc)
   std::map<std::pair<std::string, std::string>, PodRefs> pod_refs_;  // (ns, pod) -> handles

@@ -41,6 +41,7 @@ bool wait_until(std::condition_variable& cv, std::unique_lock<std::mutex>& lk, C
 constexpr double kMaxTimeUncFrac = 0.05;  // a window is published when its ends are this well-timed
 constexpr double kAnchorUncS = 250e-6;     // a read timed this well can start a window
 constexpr std::chrono::microseconds kPromptRead{300};  // a read not held up completes within this
+constexpr std::chrono::microseconds kSlowRead{1000};   // a read seen pending and done only later than this was held
 
 struct RoundMachine::Slot {
   ReadPort* port = nullptr;
@@ -270,9 +271,12 @@ void RoundMachine::round_done(Slot& s, int dev, Clock::time_point now) {
   // post, not from how late the look came (a look delayed by scheduling would otherwise move the
   // window's end by half the delay).
   // (A look within kPromptRead of the post that finds it pending says nothing more: it is still
-  // a prompt read.  Held reads are those still pending later than that.)
+  // a prompt read.  Held reads are those still pending later than that, and those seen pending
+  // and then done only more than kSlowRead after the post: the read may have run anywhere since
+  // the pending look.  A sampler descheduled between two looks, on a loaded host, otherwise
+  // took a read that ran milliseconds late for a prompt one and published a wrong rate.)
   const auto since = now - s.t_checked;
-  const bool held = s.seen_pending && s.t_checked - s.t_post > kPromptRead;
+  const bool held = s.seen_pending && (s.t_checked - s.t_post > kPromptRead || now - s.t_post > kSlowRead);
   const auto t = held ? s.t_checked + since / 2 : s.t_checked + std::min<Clock::duration>(since, kPromptRead) / 2;
   const double unc = held ? std::chrono::duration<double>(since).count() / 2 : 0.0;
   Sample smp;

@@ -24,7 +24,8 @@ KfdProcReader::~KfdProcReader() {
 
 void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
                          std::vector<std::vector<ProcSample>>* per_dev, uint64_t now_ns) {
-  per_dev->assign(devs.size(), {});
+  per_dev->resize(devs.size());
+  for (auto& l : *per_dev) l.clear();
   ++scan_no_;
   const std::string base = root_ + "/sys/class/kfd/kfd/proc";
   // The directory listing is the scan's most expensive step (a cold getdents: ~20 us on
