@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-5 GPU session 8: the final exposition (24-character fractions, capped re-parses not
-# counted toward a code build, LZ77 hash sized to the window), listed KFD process directories, sampled stage CPU:
+# counted toward a code build, LZ77 hash sized to the window), listed KFD process directories, sampled stage CPU,
+# PMC reads done late after a pending look timed as held:
 # the whole GPU tier, smoke, the driver's command x2 (one with the relayout log), config 5 x2.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/r05s8
