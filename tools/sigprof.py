@@ -5,7 +5,8 @@ Drives Engine.tick() in this thread over a fake /sys + /proc tree (utils/fakehos
 full profile, 4 GPU processes per GPU) under tools/sigprof.cc's ITIMER_PROF sampler and
 prints self and inclusive sample shares per function.  The SMU fetch is not simulated
 (fake_metrics_cost_us 0): this profiles everything else a tick does.
-Usage: python tools/sigprof.py [--gpus 8] [--ticks 20000] [--top 40] [--gzip]
+Usage: python tools/sigprof.py [--gpus 8] [--ticks 20000] [--top 40] [--gzip] [--backend amdsmi]
+(--backend amdsmi: GPU 0 of a GPU box, sentinel and PMC counters on, the SMU fetch real)
 """
 import argparse
 import bisect
@@ -139,16 +140,29 @@ def main() -> int:
     ap.add_argument("--gzip", action="store_true", help="serve HTTP with a 100 Hz gzip scraper (another process)")
     ap.add_argument("--exposition", default="compiled")
     ap.add_argument("--lines", default="", help="also print the source lines of leaf samples in this function")
+    ap.add_argument("--backend", default="sysfs",
+                    help="sysfs: the fake node; amdsmi: GPU 0 of this host, with sentinel and PMC counters "
+                         "(a GPU box; the SMU fetch is then real)")
     args = ap.parse_args()
     lib = ctypes.CDLL(build_lib())
-    import test_fakehost as tf
     from kubernetes_gpu_exporter_amd._native import load
     native = load()
-    root = tempfile.mkdtemp(prefix="gpuexp-prof-")
-    tf._loaded_node(root, args.gpus)
     c = native.EngineConfig()
-    c.backend = "sysfs"
-    c.host_root = root
+    real = args.backend == "amdsmi"
+    if real:
+        from kubernetes_gpu_exporter_amd._native import rocprof_plugin_path
+        c.backend = "amdsmi"
+        c.device_filter = [0]
+        c.enable_sentinel = True
+        c.enable_counters = True
+        c.counters_plugin = rocprof_plugin_path("aqlpmc")
+        args.gpus = 1
+    else:
+        import test_fakehost as tf
+        root = tempfile.mkdtemp(prefix="gpuexp-prof-")
+        tf._loaded_node(root, args.gpus)
+        c.backend = "sysfs"
+        c.host_root = root
     c.interval_s = 0
     c.serve_http = args.gzip
     if args.gzip:
@@ -158,7 +172,8 @@ def main() -> int:
         c.http = h
     c.series_profile = "full"
     c.exposition = args.exposition
-    c.fake_metrics_cost_us = 0
+    if not real:
+        c.fake_metrics_cost_us = 0
     e = native.Engine(c)
     e.start()
     scraper = None
@@ -167,15 +182,21 @@ def main() -> int:
         scraper = subprocess.Popen([sys.executable, "-c", project_cpu.SCRAPER, ROOT, str(e.http_port), "100", "gzip"])
         time.sleep(1.0)
     now = 1_000_000_000
-    for _ in range(200):
+
+    def tick():  # a real device ticks on the real clock (the sentinel's and counters' domain)
+        nonlocal now
         now += 10_000_000
-        e.tick(now)
+        e.tick() if real else e.tick(now)
+
+    for _ in range(200 if not real else 20):
+        tick()
+        if real:
+            time.sleep(args.sleep_ms / 1e3)
     trace = os.path.join(tempfile.gettempdir(), "gpuexp_sigprof.txt")
     lib.sigprof_start(args.hz)
     t0 = time.process_time()
     for _ in range(args.ticks):
-        now += 10_000_000
-        e.tick(now)
+        tick()
         if args.sleep_ms:
             time.sleep(args.sleep_ms / 1e3)
     cpu = time.process_time() - t0
