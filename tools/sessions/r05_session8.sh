@@ -2,7 +2,8 @@
 # Round-5 GPU session 8: the final exposition (24-character fractions, capped re-parses not
 # counted toward a code build, LZ77 hash sized to the window), listed KFD process directories, sampled stage CPU,
 # PMC reads done late after a pending look timed as held:
-# the whole GPU tier, smoke, the driver's command x2 (one with the relayout log), config 5 x2.
+# the whole GPU tier, smoke, the driver's command x2 (one with the relayout log), config 5 x2,
+# and a sampling profile of the tick on silicon at 10 Hz spacing.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/r05s8
 mkdir -p $O
@@ -13,4 +14,5 @@ bash tools/gpu_session.sh \
   "150::GPUEXP_DEBUG_RELAYOUT=1 python -u bench.py --gpus 1 --steps 20 --warmup 5 --out $O/driver.1.json; cp gpurun_out/bench_exporter.log $O/exporter_relayout.log" \
   "150::python -u bench.py --gpus 1 --steps 20 --warmup 5 --out $O/driver.2.json" \
   "200::$C5 --out $O/c5.1.json" \
-  "200::$C5 --out $O/c5.2.json"
+  "200::$C5 --out $O/c5.2.json" \
+  "150::python -u tools/sigprof.py --backend amdsmi --ticks 600 --sleep-ms 100 --top 50 > $O/sigprof_silicon.txt 2>&1; tail -3 $O/sigprof_silicon.txt"
