@@ -1582,13 +1582,27 @@ void Engine::emit_processes(uint64_t gen, const std::vector<std::vector<ProcSamp
           }
         }
       }
-      std::vector<std::string> L = {a.ns, a.pod, std::to_string(t.pid), t.op};
-      table_.put(f_rccl_calls_, L, double(t.calls), gen);
-      table_.put(f_rccl_bytes_, L, double(t.bytes), gen);
+      // handles cached per (PID, op) while the labels stay the same (no label vector per tick)
+      RcclRefs& r = rccl_refs_[{t.pid, t.op}];
+      if (r.ns != a.ns || r.pod != a.pod || r.rank != t.rank || r.nranks != t.nranks) {
+        r = RcclRefs();
+        r.ns = a.ns;
+        r.pod = a.pod;
+        r.rank = t.rank;
+        r.nranks = t.nranks;
+      }
+      r.gen = gen;
+      auto L = [&] { return std::vector<std::string>{a.ns, a.pod, std::to_string(t.pid), t.op}; };
+      cput(r.calls, f_rccl_calls_, double(t.calls), gen, L);
+      cput(r.bytes, f_rccl_bytes_, double(t.bytes), gen, L);
       if (t.nranks > 0 && t.rank >= 0)
-        table_.put(f_rccl_comm_, {a.ns, a.pod, std::to_string(t.pid), std::to_string(t.rank),
-                                  std::to_string(t.nranks)}, 1, gen);
+        cput(r.comm, f_rccl_comm_, 1, gen, [&] {
+          return std::vector<std::string>{a.ns, a.pod, std::to_string(t.pid), std::to_string(t.rank),
+                                          std::to_string(t.nranks)};
+        });
     }
+    for (auto it = rccl_refs_.begin(); it != rccl_refs_.end();)
+      it = it->second.gen != gen ? rccl_refs_.erase(it) : std::next(it);
   }
 }
 

@@ -371,6 +371,13 @@ class Engine {
   std::set<std::string> unresolved_;                               // pod UIDs without metadata (last tick)
   std::vector<std::vector<ProcSample>> per_dev_;  // tick scratch: processes per device
   std::vector<int> live_scratch_;                 // tick scratch: PIDs seen this tick
+  struct RcclRefs {  // an RCCL (PID, op)'s series handles and the label values they were made for
+    std::string ns, pod;
+    int rank = -2, nranks = -2;
+    SeriesRef calls, bytes, comm;
+    uint64_t gen = 0;
+  };
+  std::map<std::pair<int, std::string>, RcclRefs> rccl_refs_;
   std::unordered_map<uint64_t, ProcRefs> proc_refs_;               // (device << 32 | pid) -> handles
   std::unordered_map<uint64_t, ProcRefs> legacy_refs_;             // pid -> legacy handles (pod, vram, gfx=perc)
   std::map<std::pair<std::string, std::string>, PodRefs> pod_refs_;  // (ns, pod) -> handles
