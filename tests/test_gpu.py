@@ -1237,6 +1237,10 @@ def test_compiled_exposition_on_silicon(native):
     try:
         gz = native.ScrapeClient("127.0.0.1", e.http_port, "/metrics", True, 5000)
         ident = native.ScrapeClient("127.0.0.1", e.http_port, "/metrics", False, 5000)
+        t_ready = time.time() + 10.0  # 503 until the first tick published (device open, first reads)
+        while ident.scrape() <= 0 or ident.last_status != 200:
+            assert time.time() < t_ready, ident.last_status
+            time.sleep(0.05)
         t_end = time.time() + 3.0
         while time.time() < t_end:  # 20 Hz gzip asks, as Prometheus would at this rate
             assert gz.scrape() > 0 and gz.last_status == 200
