@@ -231,7 +231,7 @@ class SeriesTable {
   uint64_t rebuild_gen_ = 0;   // generation of the last layout change
   size_t last_copied_ = 0;
   uint64_t provisional_parses_ = 0;  // segments parsed on their own while their layout settled
-  static constexpr uint64_t kStableRenders = 8;
+  static constexpr uint64_t kStableRenders = 3;
   static constexpr size_t kLookback = 8192;  // how far a segment's matches may reach back
   size_t last_skipped_ = 0;    // families passed over unchanged by the last render_compiled
   size_t last_walked_ = 0;     // families whose members the last render_compiled walked

@@ -126,7 +126,7 @@ def test_unchanged_families_are_passed_over(native):
 def test_provisional_parses_while_the_layout_settles(native):
     """A family laid out again is parsed on its own (matches within its own bytes only) while the
     layout still moves; the real parse, reaching back into the families before it, comes once the
-    layout held for 8 renders, and the gzip member is valid and equal to the text throughout."""
+    layout held for 3 renders, and the gzip member is valid and equal to the text throughout."""
     (t, ids, h), _ = _tables(native, 4)
     gen = 0
     lit, sizes = [], []
@@ -141,7 +141,7 @@ def test_provisional_parses_while_the_layout_settles(native):
         assert gzip.decompress(gz) == txt.encode()
     # first layout: every family provisional; the outgrown field at 11: its family provisional again
     assert lit[0] == len(ids) and sum(lit[1:10]) == 0 and lit[10] >= 1 and sum(lit[11:]) == 0, lit
-    assert sizes[9] < sizes[0]        # the real parse after the first 8 renders compresses better
+    assert sizes[9] < sizes[0]        # the real parse after the first 3 renders compresses better
     assert sizes[-1] <= sizes[10]     # ... and again after the outgrown field settled
 
 
@@ -189,7 +189,7 @@ def test_compiled_gzip_is_close_to_zlib(native):
                         native.MetricType.gauge, ["gpu", "xcc"])
            for n in ("xcc_busy_percent", "xcc_clock_hz", "xcc_mfma_busy_percent", "xcc_temperature_celsius",
                      "xcc_power_watts", "xcc_util_percent", "xcc_waves", "xcc_lds_bytes")]
-    for gen in range(1, 13):  # (the real parse comes after 8 renders of a settled layout)
+    for gen in range(1, 13):  # (the real parse comes after 3 renders of a settled layout)
         for f in ids:
             for g in range(8):
                 for x in range(8):
@@ -277,7 +277,7 @@ def test_compiled_randomized_layouts(native):
 def test_settling_is_per_family(native):
     """One family laid out again every few ticks (a value outgrowing, a process coming) must not
     keep the rest of the body in provisional parses: each family gets its real parse once it
-    has held for 8 renders, whatever the others do (on silicon, an owner-label change re-laid 70
+    has held for 3 renders, whatever the others do (on silicon, an owner-label change re-laid 70
     families at once while a few kept moving, profiles/r05/session6)."""
     (t, ids, h), _ = _tables(native, 12)
     sizes = []
