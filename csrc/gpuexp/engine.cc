@@ -1933,9 +1933,23 @@ void Engine::tick_locked(uint64_t now) {
     if (it != owners_.end()) {
       own = it->second;
     } else if (cfg_.pod_attribution && cfg_.infer_device_owner) {
+      // the same processes (KFD identities, order-free) under the same control plane infer the
+      // same owner: reuse it instead of resolving and building sets of label strings every tick
+      uint64_t sig = 0x9E3779B97F4A7C15ull ^ ctl_epoch_;
+      bool cacheable = true;
+      for (auto& p : per_dev[i]) {
+        cacheable = cacheable && p.kfd_id != 0;
+        sig += (p.kfd_id ^ (uint64_t(uint32_t(p.pid)) << 32)) * 0xBF58476D1CE4E5B9ull;
+      }
+      sig = cacheable ? (sig | 1) : 0;
+      if (sig && sig == st.owner_sig) {
+        st.owner = st.owner_inferred;
+        continue;
+      }
       std::set<std::tuple<std::string, std::string, std::string>> seen;
       for (auto& p : per_dev[i]) {
         const CgroupInfo* ci = resolver_->resolve(p.pid, p.kfd_id);
+        if (!ci) sig = 0;  // unreadable /proc/<pid>: ask again next tick
         if (!ci || !ci->kube) continue;
         auto pit = pods_by_uid_.find(ci->pod_uid);
         if (pit == pods_by_uid_.end()) {
@@ -1954,6 +1968,8 @@ void Engine::tick_locked(uint64_t now) {
         own.pod = podset.begin()->second;
         if (seen.size() == 1) own.container = std::get<2>(*seen.begin());
       }
+      st.owner_sig = sig;
+      st.owner_inferred = own;
     }
     st.owner = own;
   }

@@ -219,6 +219,10 @@ class Engine {
   struct DevState {
     DeviceSample cur, prev;
     bool have_prev = false;
+    // single-pod owner inference, kept while the GPU's processes (by KFD identity) and the
+    // control plane stay the same (0: recompute)
+    uint64_t owner_sig = 0;
+    DeviceOwner owner_inferred;
     double xgmi_rd_rate[kMaxXgmiLinks] = {};
     double xgmi_wr_rate[kMaxXgmiLinks] = {};
     bool rates_valid = false;
