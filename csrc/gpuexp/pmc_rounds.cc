@@ -41,7 +41,7 @@ bool wait_until(std::condition_variable& cv, std::unique_lock<std::mutex>& lk, C
 constexpr double kMaxTimeUncFrac = 0.05;  // a window is published when its ends are this well-timed
 constexpr double kAnchorUncS = 250e-6;     // a read timed this well can start a window
 constexpr std::chrono::microseconds kPromptRead{300};  // a read not held up completes within this
-constexpr std::chrono::microseconds kSlowRead{1000};   // a read seen pending and done only later than this was held
+constexpr std::chrono::microseconds kSlowRead{1000};   // on a slow queue: a read done later than this was held
 
 struct RoundMachine::Slot {
   ReadPort* port = nullptr;
@@ -55,6 +55,7 @@ struct RoundMachine::Slot {
   bool seen_pending = false;      // ... by a look after it was posted (its execution time is then
                                   // known only to within [t_checked, the look that saw it done])
   Clock::time_point t_post{};     // when the pending packet was posted
+  double pending_seen_s = 0;      // EWMA of how long after its post a read was last seen pending
   double cum[kNumCtr] = {}, cum_xm[kMaxXcc] = {}, cum_xg[kMaxXcc] = {};
   bool have_cum = false;
   Clock::time_point t_last{};  // when the last read executed (the start of the next window)
@@ -271,12 +272,18 @@ void RoundMachine::round_done(Slot& s, int dev, Clock::time_point now) {
   // post, not from how late the look came (a look delayed by scheduling would otherwise move the
   // window's end by half the delay).
   // (A look within kPromptRead of the post that finds it pending says nothing more: it is still
-  // a prompt read.  Held reads are those still pending later than that, and those seen pending
-  // and then done only more than kSlowRead after the post: the read may have run anywhere since
-  // the pending look.  A sampler descheduled between two looks, on a loaded host, otherwise
-  // took a read that ran milliseconds late for a prompt one and published a wrong rate.)
+  // a prompt read.  Held reads are those still pending later than that.  A queue whose reads
+  // are still pending that late as a rule -- its EWMA says so -- is slow: there, a read first
+  // seen done more than kSlowRead after its post may have run anywhere since the last look that
+  // found it pending (or since its post), and is held too.  Without that, a sampler descheduled
+  // between two looks on a loaded host took a slow queue's read for a prompt one and published
+  // a wrong rate; on a prompt queue the same gap says nothing about the read, which ran within
+  // its usual time.)
   const auto since = now - s.t_checked;
-  const bool held = s.seen_pending && (s.t_checked - s.t_post > kPromptRead || now - s.t_post > kSlowRead);
+  const bool slow_queue = s.pending_seen_s > std::chrono::duration<double>(kPromptRead).count();
+  const bool held = (s.seen_pending && s.t_checked - s.t_post > kPromptRead) || (slow_queue && now - s.t_post > kSlowRead);
+  if (s.seen_pending)
+    s.pending_seen_s = 0.8 * s.pending_seen_s + 0.2 * std::chrono::duration<double>(s.t_checked - s.t_post).count();
   const auto t = held ? s.t_checked + since / 2 : s.t_checked + std::min<Clock::duration>(since, kPromptRead) / 2;
   const double unc = held ? std::chrono::duration<double>(since).count() / 2 : 0.0;
   Sample smp;
