@@ -42,6 +42,8 @@ constexpr double kMaxTimeUncFrac = 0.05;  // a window is published when its ends
 constexpr double kAnchorUncS = 250e-6;     // a read timed this well can start a window
 constexpr std::chrono::microseconds kPromptRead{300};  // a read not held up completes within this
 constexpr std::chrono::microseconds kSlowRead{1000};   // on a slow queue: a read done later than this was held
+constexpr std::chrono::microseconds kSlowQueue{800};   // reads seen pending this long after their post, as a rule
+                                                       // (prompt reads take 50-600 us on MI355X)
 
 struct RoundMachine::Slot {
   ReadPort* port = nullptr;
@@ -56,6 +58,7 @@ struct RoundMachine::Slot {
                                   // known only to within [t_checked, the look that saw it done])
   Clock::time_point t_post{};     // when the pending packet was posted
   double pending_seen_s = 0;      // EWMA of how long after its post a read was last seen pending
+  uint64_t pending_seen_n = 0;    // reads in that average
   double cum[kNumCtr] = {}, cum_xm[kMaxXcc] = {}, cum_xg[kMaxXcc] = {};
   bool have_cum = false;
   Clock::time_point t_last{};  // when the last read executed (the start of the next window)
@@ -273,17 +276,19 @@ void RoundMachine::round_done(Slot& s, int dev, Clock::time_point now) {
   // window's end by half the delay).
   // (A look within kPromptRead of the post that finds it pending says nothing more: it is still
   // a prompt read.  Held reads are those still pending later than that.  A queue whose reads
-  // are still pending that late as a rule -- its EWMA says so -- is slow: there, a read first
+  // are still pending kSlowQueue after their post as a rule -- its EWMA says so -- is slow: a read first
   // seen done more than kSlowRead after its post may have run anywhere since the last look that
   // found it pending (or since its post), and is held too.  Without that, a sampler descheduled
   // between two looks on a loaded host took a slow queue's read for a prompt one and published
   // a wrong rate; on a prompt queue the same gap says nothing about the read, which ran within
   // its usual time.)
   const auto since = now - s.t_checked;
-  const bool slow_queue = s.pending_seen_s > std::chrono::duration<double>(kPromptRead).count();
+  const bool slow_queue = s.pending_seen_s > std::chrono::duration<double>(kSlowQueue).count();
   const bool held = (s.seen_pending && s.t_checked - s.t_post > kPromptRead) || (slow_queue && now - s.t_post > kSlowRead);
-  if (s.seen_pending)
-    s.pending_seen_s = 0.8 * s.pending_seen_s + 0.2 * std::chrono::duration<double>(s.t_checked - s.t_post).count();
+  if (s.seen_pending) {  // (the first observation seeds the average: a slow queue is slow from its first reads)
+    const double v = std::chrono::duration<double>(s.t_checked - s.t_post).count();
+    s.pending_seen_s = s.pending_seen_n++ ? 0.8 * s.pending_seen_s + 0.2 * v : v;
+  }
   const auto t = held ? s.t_checked + since / 2 : s.t_checked + std::min<Clock::duration>(since, kPromptRead) / 2;
   const double unc = held ? std::chrono::duration<double>(since).count() / 2 : 0.0;
   Sample smp;

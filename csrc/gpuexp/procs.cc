@@ -115,13 +115,18 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
       if (read_small_file(root_ + "/proc/" + name + "/comm", &comm, 64)) it->second.comm = trim(comm);
     }
     if (!fresh && it->second.devs.size() < devs.size() &&
-        (!now_ns || now_ns < it->second.probe_ns || now_ns - it->second.probe_ns >= kReprobeNs)) {
+        (!now_ns || now_ns < it->second.probe_ns || now_ns - it->second.probe_ns >= it->second.probe_every_ns)) {
       // KFD adds a process's vram_<gpu_id> when it first uses that GPU, which can be after its
       // directory appeared (or after the listing that found it, mid-creation): look for the
       // GPUs it had no files for at a listing every kReprobeNs, or it would never show on them
       // (one listing of its directory per look).
+      // (a process on 1 of 8 GPUs stays there, as a rule: the look backs off to every kReprobeMaxNs
+      // while it finds nothing, and is back to every kReprobeNs once it found a GPU)
       it->second.probe_ns = now_ns;
+      const size_t had = it->second.devs.size();
       probe_devs(pdir, &it->second);
+      it->second.probe_every_ns =
+          it->second.devs.size() > had ? kReprobeNs : std::min(kReprobeMaxNs, 2 * it->second.probe_every_ns);
     }
     if (emit(it->second, pid, per_dev, now_ns) == 0 && !fresh && !it->second.devs.empty()) {
       // Cached fds of a PID whose KFD directory was removed and re-created between two

@@ -52,11 +52,13 @@ class KfdProcReader {
     std::string comm;
     int comm_tries = 0;  // re-reads of an empty comm at later listings
     uint64_t probe_ns = 0;  // last look for GPUs it had no files for
+    uint64_t probe_every_ns = kReprobeNs;  // doubles (to kReprobeMaxNs) while looks find nothing
     uint64_t seen = 0;
     uint64_t id = 0;        // ProcSample::kfd_id
   };
   static constexpr int kCommTries = 3;
   static constexpr uint64_t kReprobeNs = 1000000000ull;
+  static constexpr uint64_t kReprobeMaxNs = 8000000000ull;
   // Appends the entry's per-GPU samples; returns how many vram reads succeeded.
   int emit(Entry& e, int pid, std::vector<std::vector<ProcSample>>* per_dev, uint64_t now_ns);
   std::string root_;
