@@ -207,6 +207,29 @@ def test_device_owner_explicit_and_inferred(mock_engine):
     assert up["1"]["pod"] == "" and up["0"]["pod"] == ""
 
 
+def test_inferred_owner_follows_control_plane_changes(mock_engine):
+    """The single-pod owner inference is reused while the GPU's processes and the control plane
+    stay the same: a pod renamed in the pod list, or a PID's cgroup overridden into another
+    pod, relabels the GPU at the next tick."""
+    e = mock_engine(1, http=False)
+    uid2 = "22345678-1234-1234-1234-123456789abc"
+    cg2 = CG.replace(UID.replace("-", "_"), uid2.replace("-", "_"))
+    e.set_pods([dict(uid=UID, namespace="ml", name="trainer-0", containers={CID: "main"}),
+                dict(uid=uid2, namespace="ml", name="other-0", containers={})])
+    e.mock_set_processes(0, [dict(pid=5, vram_bytes=1.0)])
+    e.set_pid_cgroup(5, CG)
+    t = ticks(e, 3)
+    owner = lambda: parse(e)["amd_gpu_up"].samples[0][1]["pod"]
+    assert owner() == "trainer-0"
+    e.set_pods([dict(uid=UID, namespace="ml", name="trainer-1", containers={CID: "main"}),
+                dict(uid=uid2, namespace="ml", name="other-0", containers={})])
+    t = ticks(e, 2, t)
+    assert owner() == "trainer-1"
+    e.set_pid_cgroup(5, cg2)
+    ticks(e, 2, t)
+    assert owner() == "other-0"
+
+
 def test_shared_gpu_has_no_owner(mock_engine):
     e = mock_engine(1, http=False)
     uid2 = "22345678-1234-1234-1234-123456789abc"

@@ -92,6 +92,39 @@ def _engine(native, root, **kw):
     return e
 
 
+def test_inferred_owner_follows_control_plane_changes(native, tmp_path):
+    """The single-pod owner inference is reused while the GPU's processes (by KFD identity) and
+    the control plane stay the same: a pod renamed in the pod list, or a PID's cgroup overridden
+    into another pod, relabels the GPU at the next tick; a new process on it too."""
+    h = mi355x_node(tmp_path, 1)
+    (g0,) = h.gpus
+    uid2 = "bbbbbbbb-bbbb-cccc-dddd-eeeeeeeeeeee"
+    h.add_process(4242, kubepods_cgroup(UID, CID), gpus={g0.gpu_id: (1000, 10)})
+    e = _engine(native, tmp_path)
+    owner = lambda: promtext.parse(e.snapshot_text())["amd_gpu_up"].samples[0][1]["pod"]
+    try:
+        e.set_pods([dict(uid=UID, namespace="ml", name="trainer-0", containers={CID: "main"}),
+                    dict(uid=uid2, namespace="ml", name="other-0", containers={})])
+        for k in range(3):
+            e.tick(S + k * S // 10)
+        assert owner() == "trainer-0"
+        e.set_pods([dict(uid=UID, namespace="ml", name="trainer-1", containers={CID: "main"}),
+                    dict(uid=uid2, namespace="ml", name="other-0", containers={})])
+        e.tick(S + 3 * S // 10)
+        e.tick(S + 4 * S // 10)
+        assert owner() == "trainer-1"
+        e.set_pid_cgroup(4242, kubepods_cgroup(uid2, CID))
+        e.tick(S + 5 * S // 10)
+        e.tick(S + 6 * S // 10)
+        assert owner() == "other-0"
+        h.add_process(4343, kubepods_cgroup(UID, CID), gpus={g0.gpu_id: (1000, 10)})  # a second pod
+        e.tick(2 * S)  # (the next listing finds it)
+        e.tick(2 * S + S // 10)
+        assert owner() == ""
+    finally:
+        e.stop()
+
+
 def test_end_to_end_attribution(native, tmp_path):
     """KFD host PID -> /proc/<pid>/cgroup -> pod UID -> (namespace, name, container)."""
     h = mi355x_node(tmp_path, 2)
