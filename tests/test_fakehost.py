@@ -510,6 +510,38 @@ def test_process_found_on_a_gpu_it_starts_using_later(native, tmp_path):
     e.stop()
 
 
+def test_late_gpu_found_within_the_reprobe_cap(native, tmp_path):
+    """A process that stays on one of its node's GPUs is looked for on the others less and less
+    often (1, 2, 4, 8 s: one listing of its directory each), so a GPU it starts using much later
+    shows within the 8 s cap plus one listing."""
+    h = mi355x_node(tmp_path, 2)
+    g0, g1 = h.gpus
+    h.add_process(4242, kubepods_cgroup(UID, CID), gpus={g0.gpu_id: (1000, 10)})
+    e = _engine(native, tmp_path, kfd_rescan_interval_s=0.5)
+
+    def gpus_of_4242():
+        f = promtext.parse(e.snapshot_text())
+        return sorted(lab["gpu"] for _, lab, _ in promtext.samples(f, "amd_gpu_process_vram_bytes")
+                      if lab["pid"] == "4242")
+
+    try:
+        t = S
+        for _ in range(200):  # 20 s on one GPU: the look backs off to its cap
+            e.tick(t)
+            t += S // 10
+        h.set_process_gpu(4242, g1.gpu_id, vram=2000, cu=5)
+        found = None
+        for k in range(100):
+            e.tick(t)
+            t += S // 10
+            if gpus_of_4242() == ["0", "1"]:
+                found = k
+                break
+        assert found is not None and found <= 86, found  # 8 s cap + one 0.5 s listing
+    finally:
+        e.stop()
+
+
 def test_unreadable_pid_is_not_looked_up_every_tick(native, tmp_path):
     """A GPU process whose /proc/<pid> the exporter cannot read (a host PID seen from inside
     a PID namespace, hidepid, a process on its way out) is looked up again at most once a
