@@ -965,8 +965,8 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
   const DeviceInfo& d = devices_[size_t(i)];
   const DeviceSample& c = st.cur;
   // Owner change -> rebuild every cached handle with the new pod labels.
-  std::string okey = st.owner.ns + "/" + st.owner.pod + "/" + st.owner.container;
-  if (okey != st.owner_key) {
+  if (!st.owner_built_set || st.owner.ns != st.owner_built.ns || st.owner.pod != st.owner_built.pod ||
+      st.owner.container != st.owner_built.container) {
     DeviceOwner keep = st.owner;
     DevState fresh;
     fresh.cur = st.cur;
@@ -985,7 +985,8 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
     fresh.metrics_fresh_ns = st.metrics_fresh_ns;
     std::copy(std::begin(st.kfd_events), std::end(st.kfd_events), std::begin(fresh.kfd_events));
     fresh.owner = keep;
-    fresh.owner_key = okey;
+    fresh.owner_built = keep;
+    fresh.owner_built_set = true;
     st = fresh;
   }
 

@@ -234,7 +234,8 @@ class Engine {
     double mfma_last = kNaN;  // this tick's amd_gpu_mfma_busy_percent (NaN: no counter window)
     double flops_last[2] = {kNaN, kNaN};  // this tick's bf16 / fp8 MFMA FLOP/s (NaN: not device-wide)
     DeviceOwner owner;
-    std::string owner_key;  // ns/pod/container the refs were built for
+    DeviceOwner owner_built;  // ns/pod/container the refs were built for
+    bool owner_built_set = false;
     // cached series handles (re-upserted on owner change or GC)
     SeriesRef info, up, gfx, umc, xcc[kMaxXcc], vram_used, vram_total, hbm_bw, power, power_cap,
         energy, temp[9], clk[3], xrd[kMaxXgmiLinks], xwr[kMaxXgmiLinks], xrd_rate, xwr_rate,
