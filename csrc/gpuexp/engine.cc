@@ -1730,11 +1730,11 @@ void Engine::emit_self(uint64_t gen) {
   if (rccl_) {
     int a = 0, u = 0, x = 0;
     rccl_->file_states(&a, &u, &x);
-    table_.put(f_self_rccl_files_, {"active"}, a, gen);
-    table_.put(f_self_rccl_files_, {"unverified"}, u, gen);
-    table_.put(f_self_rccl_files_, {"exited"}, x, gen);
-    table_.put(f_self_rccl_files_, {"ignored"}, rccl_->ignored(), gen);
-    table_.put(f_self_rccl_scans_, {}, double(rccl_->scans()), gen);
+    static const char* const kStates[4] = {"active", "unverified", "exited", "ignored"};
+    const double v[4] = {double(a), double(u), double(x), double(rccl_->ignored())};
+    for (int k = 0; k < 4; ++k)
+      cput(rccl_self_refs_[k], f_self_rccl_files_, v[k], gen, [&] { return std::vector<std::string>{kStates[k]}; });
+    cput(rccl_self_refs_[4], f_self_rccl_scans_, double(rccl_->scans()), gen, none);
   }
 }
 

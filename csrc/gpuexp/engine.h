@@ -383,6 +383,7 @@ class Engine {
     uint64_t gen = 0;
   };
   std::map<std::pair<int, std::string>, RcclRefs> rccl_refs_;
+  SeriesRef rccl_self_refs_[5];  // tracer file states (4) and scans
   std::unordered_map<uint64_t, ProcRefs> proc_refs_;               // (device << 32 | pid) -> handles
   std::unordered_map<uint64_t, ProcRefs> legacy_refs_;             // pid -> legacy handles (pod, vram, gfx=perc)
   std::map<std::pair<std::string, std::string>, PodRefs> pod_refs_;  // (ns, pod) -> handles
