@@ -167,8 +167,11 @@ def run_problems(result: dict, n_gpus: int, attribution_ok: bool, rccl_on: bool)
     if got != n_gpus:
         probs.append(f"series_per_gpu covers {got} GPUs, not {n_gpus}: {sorted(result['series_per_gpu'])}")
     want = {f"gemm-pod-{r}" for r in range(n_gpus)}
-    if not attribution_ok or set(result["attributed_pods"]) != want:
+    if set(result["attributed_pods"]) != want:
         probs.append(f"attributed pods {result['attributed_pods']} != {sorted(want)}")
+    elif not attribution_ok:
+        probs.append("attributed pods: not all ranks (or their RCCL communicators) were attributed within the "
+                     "untimed 20 s wait before the warm-up")
     if rccl_on:
         ranks = result.get("rccl_rank_per_pod") or {}
         bad = {p: rn for p, rn in ranks.items() if rn[1] != n_gpus}
