@@ -157,9 +157,14 @@ int main(int argc, char** argv) {
     report(ok ? "code object loaded + frozen (no queue yet)" : "code object load FAILED");
   }
   std::vector<hsa_queue_t*> qs;
+  // GPUEXP_PROBE_SEG=0: queues asking for no private / group segment (the exporter's packets need
+  // none: PM4 reads and a scratch-free sentinel) instead of the maximum
+  const char* seg_env = std::getenv("GPUEXP_PROBE_SEG");
+  const uint32_t seg = seg_env && std::strcmp(seg_env, "0") == 0 ? 0 : UINT32_MAX;
+  std::printf("== queue private/group segment size: %s\n", seg ? "UINT32_MAX" : "0");
   for (int i = 0; i < nq; ++i) {
     hsa_queue_t* q = nullptr;
-    if (hsa_queue_create(gpu, 64, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &q) !=
+    if (hsa_queue_create(gpu, 64, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr, seg, seg, &q) !=
         HSA_STATUS_SUCCESS)
       return 2;
     qs.push_back(q);
