@@ -201,3 +201,37 @@ def test_memory_limits_cover_the_read_rescue_worst_case():
     for n in range(1, 9):
         limit = 100 + n * v["memoryPerQueueGpuMi"] + n * v["memoryPerRescueQueueMi"] + v["resources"]["memoryLimitHeadroomMi"]
         assert limit >= worst(n), (n, limit, worst(n))
+
+
+def test_helm_args_accepted_by_the_cli():
+    """The Helm DaemonSet's exporter args, rendered with the chart's default values (a minimal
+    stand-in for `helm template`: `{{ .Values.x }}` and `{{ join "," .Values.x }}`), parse with
+    the exporter's own CLI parser and give the chart's settings."""
+    chart = os.path.join(ROOT, "deploy", "helm", "gpuexp")
+    with open(os.path.join(chart, "values.yaml")) as fh:
+        values = yaml.safe_load(fh)
+
+    def value(path):
+        node = values
+        for part in path.split("."):
+            node = node[part]
+        return node
+
+    def render(line):
+        line = re.sub(r'\{\{\s*join\s+"([^"]*)"\s+\.Values\.([A-Za-z0-9_.]+)\s*\}\}',
+                      lambda m: m.group(1).join(str(x) for x in value(m.group(2))), line)
+        return re.sub(r"\{\{\s*\.Values\.([A-Za-z0-9_.]+)\s*\}\}",
+                      lambda m: str(value(m.group(1))).lower() if isinstance(value(m.group(1)), bool)
+                      else str(value(m.group(1))), line)
+
+    with open(os.path.join(chart, "templates", "daemonset.yaml")) as fh:
+        text = fh.read()
+    args = [render(m.group(1)) for m in re.finditer(r"^\s+- (--[a-z-]+=.*)$", text, re.M)
+            if "{{ if" not in m.group(1) and "{{- " not in m.group(1)]
+    args = [a for a in args if "{{" not in a]  # (conditional args stay out of this check)
+    assert any(a.startswith("--exposition=") for a in args), args
+    cfg = load_config(args, env={"NODE_NAME": "n1"})
+    assert cfg.exposition == values["exposition"]
+    assert str(cfg.metrics_min_interval) == str(values["metricsMinInterval"])
+    assert cfg.metrics_cpu_budget == values["metricsCpuBudget"]
+    assert cfg.series_profile == values["seriesProfile"] and cfg.enable_counters == values["counters"]
