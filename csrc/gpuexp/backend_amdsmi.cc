@@ -366,13 +366,13 @@ class AmdsmiBackend : public Backend {
       from_amdsmi_metrics(m, out, d.xcp, d.nxcc);
     }
     uint64_t used = 0;
-    const uint64_t v0 = mono_ns();
+    const uint64_t v0 = out->time_parts ? mono_ns() : 0;
     if (d.vram_used_file.read_u64(&used)) {
       out->vram_used = double(used);
     } else if (amdsmi_get_gpu_memory_usage(d.h, AMDSMI_MEM_TYPE_VRAM, &used) == AMDSMI_STATUS_SUCCESS) {
       out->vram_used = double(used);
     }
-    out->vram_wall_ns = mono_ns() - v0;
+    if (out->time_parts) out->vram_wall_ns = mono_ns() - v0;
     out->vram_total = double(dev.vram_total);
     out->power_cap_w = d.power_cap_w;
     out->ok = true;

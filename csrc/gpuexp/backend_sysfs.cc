@@ -313,7 +313,7 @@ void SysfsBackend::sample(const DeviceInfo& dev, DeviceSample* out) {
   }
   if (!any) sample_fallback(d, out);
   uint64_t used = 0;
-  const uint64_t v0 = mono_ns();
+  const uint64_t v0 = out->time_parts ? mono_ns() : 0;
   if (d.vram_used.read_u64(&used)) {
     out->vram_used = double(used);
     any = true;
@@ -321,7 +321,7 @@ void SysfsBackend::sample(const DeviceInfo& dev, DeviceSample* out) {
     out->vram_used = double(used);
     any = true;
   }
-  out->vram_wall_ns = mono_ns() - v0;
+  if (out->time_parts) out->vram_wall_ns = mono_ns() - v0;
   out->vram_total = double(dev.vram_total);
   out->power_cap_w = d.power_cap_w;
   out->ok = any || !std::isnan(out->gfx_activity) || !std::isnan(out->power_w);

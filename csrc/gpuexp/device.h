@@ -88,6 +88,7 @@ struct DeviceSample {
   // gpuexp_device_read_seconds_total): gpu_metrics wall + thread CPU (a fresh read is an
   // SMU round trip the kernel busy-waits on; ~0 when coalesced), the VRAM-used file, wall.
   uint64_t metrics_wall_ns = 0, metrics_cpu_ns = 0, vram_wall_ns = 0;
+  bool time_parts = true;  // set by the engine: time the VRAM read (vram_wall_ns) on this tick
 
   double gfx_activity = kNaN;  // %
   double umc_activity = kNaN;  // %

@@ -1829,7 +1829,9 @@ void Engine::tick_locked(uint64_t now) {
   // 0: device telemetry (per-GPU reads fan out over the pool; each touches only its own
   // DevState and its own backend device slot)
   uint64_t errs = 0;
-  auto sample_one = [this, now](int i) {
+  // (the VRAM / RAS / GTT read times are sampled on the same ticks as the stage CPU split: two
+  // clock reads each per GPU per tick otherwise, for a diagnostic)
+  auto sample_one = [this, now, split_cpu](int i) {
     DevState& st = dstate_[size_t(i)];
     if (st.cur.ok) {
       st.prev = st.cur;
@@ -1837,12 +1839,13 @@ void Engine::tick_locked(uint64_t now) {
     }
     st.cur = DeviceSample();
     st.cur.host_ns = now;
+    st.cur.time_parts = split_cpu;
     backend_->sample(devices_[size_t(i)], &st.cur);
     (st.cur.metrics_coalesced ? metrics_coalesced_ : metrics_fresh_)[size_t(i)] += 1;
     if (st.cur.ok && !st.cur.metrics_coalesced) st.metrics_fresh_ns = now;
     st.ras_ns = st.gtt_ns = 0;
     if (!ras_.empty()) {
-      const uint64_t r0 = mono_ns();
+      const uint64_t r0 = split_cpu ? mono_ns() : 0;
       if (now >= ras_next_ns_[size_t(i)]) {
         ras_[size_t(i)].read(&ras_cache_[size_t(i)]);
         ras_next_ns_[size_t(i)] = now + uint64_t(cfg_.ras_interval_s * 1e9);
@@ -1857,14 +1860,14 @@ void Engine::tick_locked(uint64_t now) {
       st.cur.pages_retired = r.pages_retired;
       st.cur.pages_pending = r.pages_pending;
       st.cur.pages_unreservable = r.pages_unreservable;
-      st.ras_ns = mono_ns() - r0;
+      if (split_cpu) st.ras_ns = mono_ns() - r0;
     }
     if (!gtt_used_f_.empty()) {
-      const uint64_t g0 = mono_ns();
+      const uint64_t g0 = split_cpu ? mono_ns() : 0;
       uint64_t v = 0;
       if (gtt_used_f_[size_t(i)].read_u64(&v)) st.cur.gtt_used = double(v);
       st.cur.gtt_total = gtt_total_[size_t(i)];
-      st.gtt_ns = mono_ns() - g0;
+      if (split_cpu) st.gtt_ns = mono_ns() - g0;
     }
   };
   if (pool_) {
@@ -1878,9 +1881,9 @@ void Engine::tick_locked(uint64_t now) {
       errs += 1;
     }
     part[2] += st.cur.metrics_wall_ns;
-    part[3] += st.cur.vram_wall_ns;
-    part[4] += st.ras_ns;
-    part[5] += st.gtt_ns;
+    part[3] += kStageCpuEvery * st.cur.vram_wall_ns;  // (0 off the sampled ticks)
+    part[4] += kStageCpuEvery * st.ras_ns;
+    part[5] += kStageCpuEvery * st.gtt_ns;
     if (!st.cur.metrics_coalesced && st.cur.metrics_cpu_ns) {
       st.fetch_cpu_s += double(st.cur.metrics_cpu_ns) * 1e-9;
       // EWMA over fresh reads (a few outliers, e.g. a preempted read, barely move it)

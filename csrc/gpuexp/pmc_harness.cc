@@ -101,8 +101,10 @@ HarnessOutcome run_pmc_harness(const HarnessConfig& cfg, double rate_tolerance) 
     const size_t p = d.find("windows=");
     out.gpus[size_t(i)].windows = p == std::string::npos ? 0 : std::strtoull(d.c_str() + p + 8, nullptr, 10);
   }
-  // reads that completed before the machine stopped must all have been collected
-  const int64_t end = ports.empty() ? 0 : ports[0]->now();
+  // reads that completed before the machine stopped must all have been collected (those that
+  // completed within the last two ticks may still have been waiting for a look: a counting
+  // thread descheduled on a loaded host looks late, and stop() does not wait for it)
+  const int64_t end = (ports.empty() ? 0 : ports[0]->now()) - 2 * int64_t(cfg.tick_us);
   m.stop();
   for (int i = 0; i < cfg.gpus; ++i) {
     GpuOutcome& g = out.gpus[size_t(i)];

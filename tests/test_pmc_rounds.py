@@ -127,7 +127,7 @@ def test_leftover_reads_are_collected_exactly_once(native):
     assert r["late_syncs"] >= r["ticks"] // 2  # (a sync that starts late, OS jitter, finds it done)
     g1 = r["gpus"][1]
     assert g1["double_collected"] == 0 and g1["uncollected"] == 0
-    assert g1["reads_completed"] >= r["ticks"]
+    assert g1["reads_completed"] >= r["ticks"] - 2  # (counted up to two ticks before the stop)
     # (a read collected after the sync is timed only to within the counting thread's look: the
     # few whose look came late are merged into the next window rather than published mistimed)
     assert g1["windows"] >= r["ticks"] - 12 and g1["bad_windows"] == 0
