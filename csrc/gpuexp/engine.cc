@@ -372,7 +372,7 @@ void Engine::define_families() {
   f_self_dev_part_ = add("gpuexp_device_read_seconds_total",
                          "The devices stage split: time in each part (counters_kick: PMC read submitted; "
                          "control: control-plane apply; gpu_metrics: SMU fetch or cached decode; vram; ras; "
-                         "gtt), summed over GPUs", C, {"part"});
+                         "gtt; these three timed on one tick in four and scaled), summed over GPUs", C, {"part"});
   f_self_fetch_cpu_ = add("gpuexp_gpu_metrics_fetch_cpu_seconds_total",
                           "Thread CPU of fresh gpu_metrics reads (each one an SMU round trip the kernel "
                           "busy-waits on)", C, {"gpu"});
