@@ -84,6 +84,10 @@ def start_exporter(args, n_gpus: int, backend: str, port: int, pod_map: str, log
         # fills in once it knows every rank's PID (real KFD-reader and attribution path).
         cmd += ["--mock-devices", str(n_gpus), "--enable-sentinel", "true", "--enable-counters", "true",
                 "--host-root", args.fake_root]
+    if getattr(args, "runtime_file", ""):
+        cmd += ["--runtime-file", args.runtime_file]
+        if args.prewake_ab:  # the A/B's first arm from the start (warm-up included)
+            cmd += ["--http-prewake", args.prewake_ab.split(",")[0]]
     env = dict(os.environ)
     env.pop("ROCP_TOOL_LIBRARIES", None)  # the exporter itself issues no collectives
     env["GPUEXP_POD_MAP_FILE"] = pod_map
@@ -289,6 +293,13 @@ def main() -> int:
     ap.add_argument("--xgmi-patterns", type=int, default=1,
                     help="N > 1: after the timed phases (untimed), drive a ring (CP) and an all-to-all (EP) "
                          "pattern and report each rank's xGMI bytes per peer from the exporter's link counters")
+    ap.add_argument("--prewake-ab", default="",
+                    help="comma-separated HTTP pre-wake modes (off,slices,spin): the timed scrapes alternate "
+                         "between them every --ab-block scrapes inside the one exporter process (switched at "
+                         "run time: runtime file + SIGUSR1); per-arm table + block-bootstrap CIs in "
+                         "result['prewake_ab'] (utils/abtest.py)")
+    ap.add_argument("--ab-block", type=int, default=10, help="timed scrapes per A/B block")
+    ap.add_argument("--ab-seed", type=int, default=6, help="seed of the A/B block order")
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="self-launch (--gpus N > 1 without torchrun): stop the ranks after this many seconds")
     argv = sys.argv[1:]
@@ -337,6 +348,7 @@ def main() -> int:
     tmpdir = tempfile.mkdtemp(prefix="gpuexp-bench-")
     pod_map = os.path.join(tmpdir, "podmap.json")
     args.fake_root = os.path.join(tmpdir, "host")
+    args.runtime_file = os.path.join(tmpdir, "runtime.yaml") if args.prewake_ab else ""
     os.makedirs(os.path.join(args.fake_root, "sys/class/kfd/kfd/proc"), exist_ok=True)
     port = 0
     exporter = None
@@ -502,6 +514,32 @@ def main() -> int:
 
     splits: list = []
     prewoken: list = []  # per timed headline scrape: 1 pre-woken worker, 0 not, -1 unknown
+    # --prewake-ab: the arm of each block of timed scrapes, the blocks measured so far, and the
+    # arm to switch the exporter to right after the next scrape (its ~100 ms idle gap follows)
+    from kubernetes_gpu_exporter_amd.utils import abtest
+    ab_arms = [a.strip() for a in args.prewake_ab.split(",") if a.strip()]
+    ab_blocks: list = []
+    ab_state = {"next": None, "cur": None, "t0": 0.0, "http0": 0, "proc0": 0}
+
+    def ab_boundary():
+        """Closes the current A/B block (wall and CPU since it began) and switches the
+        exporter to ab_state['next'] (runtime file + SIGUSR1)."""
+        th = thread_cpu_ns_by_name(exporter.pid)
+        now = time.perf_counter()
+        http_ns, proc_ns = sum(v for k, v in th.items() if k.startswith("gpuexp-http")), sum(th.values())
+        if ab_state["cur"] is not None and ab_blocks:
+            b = ab_blocks[-1]
+            b.wall_s, b.http_cpu_ns, b.proc_cpu_ns = now - ab_state["t0"], http_ns - ab_state["http0"], \
+                proc_ns - ab_state["proc0"]
+        nxt = ab_state["next"]
+        ab_state.update(next=None, cur=nxt, t0=now, http0=http_ns, proc0=proc_ns)
+        if nxt is not None:
+            with open(args.runtime_file, "w") as fh:
+                fh.write(f"http_prewake: {nxt}\n")
+            exporter.send_signal(signal.SIGUSR1)
+            ab_blocks.append(abtest.Block(nxt))
+            if len(ab_blocks) % 10 == 1:  # progress (a long A/B must not look hung)
+                print(f"[bench] A/B block {len(ab_blocks)}/{len(ab_sched)}: {nxt}", file=sys.stderr, flush=True)
 
     def step(cl, lat: list | None):
         t_start = time.perf_counter()
@@ -516,11 +554,21 @@ def main() -> int:
                     pw = cl.last_prewoken()
                     rx = cl.last_server_rx()  # kernel receive time of the request on the server socket
                     prewoken.append(pw)
+                    rec = {"total": ns / 1e3, "pw": pw}
                     if t_parse and t_send <= t_parse <= t_write <= t_done:
                         rx_ok = bool(rx) and t_send <= rx <= t_parse
                         splits.append(((t_parse - t_send) / 1e3, (t_write - t_parse) / 1e3, (t_done - t_write) / 1e3,
                                        pw, (rx - t_send) / 1e3 if rx_ok else None,
                                        (t_parse - rx) / 1e3 if rx_ok else None))
+                        rec["req"] = (t_parse - t_send) / 1e3
+                        rec["sq"] = (t_parse - rx) / 1e3 if rx_ok else None
+                    if ab_arms and ab_blocks and ab_state["cur"] is not None:
+                        ab_blocks[-1].scrapes.append(rec)
+            if ab_arms and cl is client and (ab_state["next"] is not None or ab_state["cur"] is not None):
+                if ab_state["next"] is not None or (ab_blocks and len(ab_blocks[-1].scrapes) >= args.ab_block):
+                    if ab_state["next"] is None:  # block full: the next arm of the schedule
+                        ab_state["next"] = ab_sched[len(ab_blocks)] if len(ab_blocks) < len(ab_sched) else None
+                    ab_boundary()
         if dist is not None:
             dist.all_reduce(grad)
         sync()
@@ -636,7 +684,9 @@ def main() -> int:
     def phase(proc, cl, native_exporter: bool = False):
         """W untimed + K timed steps (barrier + synchronize on both sides); returns the
         latencies, exporter CPU% over the timed window and max-over-ranks ms/step."""
-        for _ in range(args.warmup):
+        for w in range(args.warmup):
+            if ab_arms and native_exporter and rank == 0 and w == args.warmup - 1:
+                ab_state["next"] = ab_sched[0]  # the first block's arm, switched after this scrape
             step(cl, None)
         x0 = None
         if native_exporter and rank == 0 and use_gpu:
@@ -711,9 +761,17 @@ def main() -> int:
         except subprocess.TimeoutExpired:
             proc.kill()
 
+    ab_sched = abtest.block_schedule(ab_arms, (args.steps + args.ab_block - 1) // args.ab_block, args.ab_seed) \
+        if ab_arms else []
+    if ab_arms and args.warmup < 1:
+        print("[bench] --prewake-ab needs --warmup >= 1 (the first arm is switched after the last warm-up scrape)",
+              file=sys.stderr)
+        return 2
     lat, cpu_pct, ms_per_step = phase(exporter, client if rank == 0 else None, native_exporter=True)
+    if ab_arms and rank == 0 and ab_state["cur"] is not None:
+        ab_boundary()  # closes the last block
     lat_id = cpu_id = None
-    if args.identity_phase and args.gzip:
+    if args.identity_phase and args.gzip and not ab_arms:
         # Same workload, same exporter, plain-text (identity) responses: the bytes on the
         # wire grow with the GPU count here, gzip'd ones barely do.
         id_client = n.ScrapeClient("127.0.0.1", port, "/metrics", False, 5000,
@@ -939,6 +997,9 @@ def main() -> int:
                                  "rccl_trace": bool(rccl_dir),
                                  "degraded_reason": degraded},
             "xgmi_patterns": None,
+            # --prewake-ab: per-arm latency / hit-rate / CPU table, block-bootstrap CIs against
+            # the first arm, and the default the data supports (utils/abtest.py)
+            "prewake_ab": abtest.analyse(ab_blocks, baseline=ab_arms[0]) if ab_arms and ab_blocks else None,
         }
     if args.xgmi_patterns and world > 1:
         patterns = xgmi_patterns(client, [b for _, _, b in pids])
@@ -981,8 +1042,9 @@ def main() -> int:
     if rank == 0 and not problems:
         print(json.dumps(result), file=result_out, flush=True)
     if rank == 0 and args.out:
+        extra = {"prewake_ab_blocks": abtest.blocks_to_json(ab_blocks)} if ab_blocks else {}
         with open(args.out, "w") as fh:
-            json.dump(dict(result, problems=problems), fh, indent=1)
+            json.dump(dict(result, problems=problems, **extra), fh, indent=1)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -514,6 +514,23 @@ PYBIND11_MODULE(_gpuexp, m) {
     return learnt_scrape_period_ns(newest_first.data(), int(std::min<size_t>(newest_first.size(), 4)));
   }, py::arg("intervals_newest_first"), "The scrape period the HTTP pre-wake learns from request intervals (ns)");
 
+  m.def("spin_windows", [](std::vector<uint64_t> arrivals, uint64_t max_ns, uint64_t margin) {
+    // replays arrivals through the spin pre-wake's predictor: for each arrival after the
+    // first, the window it would have been polled in (from, until, predictor) -- 0s = none
+    ArrivalPredictor p;
+    py::list out;
+    for (size_t i = 0; i < arrivals.size(); ++i) {
+      if (i) {
+        uint64_t f = 0, u = 0;
+        const int which = p.window(max_ns, margin, &f, &u);
+        out.append(py::make_tuple(f, u, which));
+      }
+      p.observe(arrivals[i], true);
+    }
+    return out;
+  }, py::arg("arrivals_ns"), py::arg("max_ns") = 300000, py::arg("margin_ns") = 15000,
+     "Spin pre-wake windows (ArrivalPredictor, http.h) for a sequence of request arrivals");
+
   py::class_<ScrapeClient>(m, "ScrapeClient")
       .def(py::init<std::string, int, std::string, bool, int, std::string, bool>(), py::arg("host"),
            py::arg("port"), py::arg("path") = "/metrics", py::arg("gzip") = false, py::arg("timeout_ms") = 5000,
@@ -593,7 +610,17 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("gzip_unsteady_hold_ns", &HttpConfig::gzip_unsteady_hold_ns)
       .def_readwrite("socket_sndbuf", &HttpConfig::socket_sndbuf)
       .def_readwrite("stale_after_ns", &HttpConfig::stale_after_ns)
-      .def_readwrite("prewake", &HttpConfig::prewake)
+      // legacy boolean: True = the timer-slice mode, False = off
+      .def_property("prewake", [](const HttpConfig& h) { return h.prewake_mode != kPrewakeOff; },
+                    [](HttpConfig& h, bool on) { h.prewake_mode = on ? kPrewakeSlices : kPrewakeOff; })
+      .def_property("prewake_mode", [](const HttpConfig& h) { return std::string(prewake_mode_name(h.prewake_mode)); },
+                    [](HttpConfig& h, const std::string& m) {
+                      const int v = parse_prewake_mode(m);
+                      if (v < 0) throw py::value_error("prewake_mode must be off|slices|spin, got " + m);
+                      h.prewake_mode = v;
+                    })
+      .def_readwrite("prewake_spin_max_ns", &HttpConfig::prewake_spin_max_ns)
+      .def_readwrite("prewake_spin_margin_ns", &HttpConfig::prewake_spin_margin_ns)
       .def_readwrite("follow_rx_cpu", &HttpConfig::follow_rx_cpu)
       .def_readwrite("prewake_lead_ns", &HttpConfig::prewake_lead_ns)
       .def_readwrite("prewake_step_ns", &HttpConfig::prewake_step_ns)
@@ -728,6 +755,10 @@ PYBIND11_MODULE(_gpuexp, m) {
           d["http_prewake_timer_wakeups"] = hs->prewake_timer_wakeups.load();
           d["http_prewake_hits"] = hs->prewake_hits.load();
           d["http_prewake_hits_narrow"] = hs->prewake_hits_narrow.load();
+          d["http_prewake_spins"] = hs->prewake_spins.load();
+          d["http_prewake_spin_hits"] = hs->prewake_spin_hits.load();
+          d["http_prewake_spin_timeouts"] = hs->prewake_spin_timeouts.load();
+          d["http_prewake_spin_ns"] = hs->prewake_spin_ns.load();
           d["http_writev_ns"] = hs->writev_ns.load();
           d["http_partial_writes"] = hs->partial_writes.load();
           d["http_scrape_ns"] = hs->lat_sum_ns.load();
@@ -735,6 +766,12 @@ PYBIND11_MODULE(_gpuexp, m) {
         }
         return d;
       })
+      .def("set_prewake_mode", [](Engine& e, const std::string& m) {
+        const int v = parse_prewake_mode(m);
+        if (v < 0) throw py::value_error("prewake mode must be off|slices|spin, got " + m);
+        return e.set_prewake_mode(v);
+      }, py::arg("mode"), "switch the HTTP workers' scrape pre-wake at run time (off|slices|spin)")
+      .def_property_readonly("prewake_mode", [](const Engine& e) { return std::string(prewake_mode_name(e.prewake_mode())); })
       .def("source_status", &Engine::source_status)
       .def("set_pods", [](Engine& e, py::list pods, bool complete) {
         std::vector<PodMeta> v;

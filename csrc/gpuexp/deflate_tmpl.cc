@@ -361,9 +361,9 @@ void TemplateDeflate::build_code(const char* body, const std::vector<TmplSegment
         df[dist_sym(t.a)] += 1;
       } else {
         const TmplField& f = seg->fields[t.a];
-        uint32_t k = 0;
-        while (k < f.width && s[f.off + k] != ' ') lf[s[f.off + k++]] += 1;
-        const uint32_t pad = f.width - k;
+        uint32_t pad = 0;  // leading blanks (values are right-aligned), then the value
+        while (pad < f.width && s[f.off + pad] == ' ') ++pad;
+        for (uint32_t k = pad; k < f.width; ++k) lf[s[f.off + k]] += 1;
         if (pad >= 4) {
           lf[' '] += 1;
           lf[len_sym(int(std::min<uint32_t>(pad - 1, kMaxMatch)))] += 1;
@@ -526,12 +526,9 @@ void TemplateDeflate::splice(const char* body, TmplSegment* seg) const {
     if (i == seg->fields.size()) break;
     const TmplField& f = seg->fields[i];
     const unsigned char* fp = s + f.off;
-    uint32_t k = 0;
-    for (; k < f.width && fp[k] != ' '; ++k) {
-      const Code& c = lit_[fp[k]];
-      bw.put(c.code, c.len);
-    }
-    uint32_t pad = f.width - k;
+    uint32_t lead = 0;  // right-aligned: the blank run first, then the value's bytes
+    while (lead < f.width && fp[lead] == ' ') ++lead;
+    uint32_t pad = lead;
     while (pad > 64) {  // only for absurd widths
       bw.put(pad_bits_[64] & 0xffffffffu, std::min<unsigned>(32, pad_len_[64]));
       if (pad_len_[64] > 32) bw.put(pad_bits_[64] >> 32, pad_len_[64] - 32u);
@@ -545,6 +542,10 @@ void TemplateDeflate::splice(const char* body, TmplSegment* seg) const {
       } else {
         bw.put(pad_bits_[pad], pl);
       }
+    }
+    for (uint32_t k = lead; k < f.width; ++k) {
+      const Code& c = lit_[fp[k]];
+      bw.put(c.code, c.len);
     }
   }
   seg->spliced_bits = size_t(bw.p - start) * 8 + bw.n;

@@ -5,8 +5,9 @@
 // afford that (libdeflate level 1: ~86 us for the 47 KB 1-GPU body on MI355X hosts, ~190 us for
 // 8 GPUs, every tick).  Here the body is a set of segments (one per metric family) whose static
 // bytes -- HELP/TYPE lines, `name{labels} ` prefixes -- stay put between layouts because every
-// value lives in a fixed-width, blank-padded field (Prometheus' text parsers skip blanks after a
-// value).  So the LZ77 parse of the static bytes (matches never read or cover a field byte) is
+// value lives in a fixed-width field, right-aligned behind leading blanks (every text parser
+// skips blanks between the labels and the value; client_golang's expfmt would read blanks after
+// a value as a timestamp separator).  So the LZ77 parse of the static bytes (matches never read or cover a field byte) is
 // computed once per layout, and so is the Huffman code and the static bits it encodes to.  A tick
 // then only splices pre-encoded static bit strings with the field bytes coded as literals (one
 // table lookup per character; a padding run is one literal plus one distance-1 match).
@@ -25,7 +26,7 @@ namespace gpuexp {
 
 struct TmplField {
   uint32_t off = 0;    // relative to the segment start
-  uint16_t width = 0;  // value bytes + trailing blanks
+  uint16_t width = 0;  // leading blanks + value bytes (right-aligned)
 };
 
 struct TmplSegment {

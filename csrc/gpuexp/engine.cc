@@ -397,6 +397,12 @@ void Engine::define_families() {
   f_self_prewake_hits_narrow_ = add("gpuexp_http_prewake_hits_narrow_total",
                                     "Pre-woken scrapes under round 3's narrower window (timer fired within the "
                                     "minimum lead + one slice before the request)", C, {});
+  f_self_prewake_spins_ = add("gpuexp_http_prewake_spins_total",
+                              "Spin pre-wake windows the HTTP worker polled in, by how they ended: a /metrics "
+                              "request arrived (hit) or the window ran out (timeout)", C, {"outcome"});
+  f_self_prewake_spin_s_ = add("gpuexp_http_prewake_spin_seconds_total",
+                               "Wall time the HTTP worker spent polling in spin pre-wake windows (the CPU the "
+                               "spin mode costs)", C, {});
   f_self_rx_moves_ = add("gpuexp_http_rx_cpu_moves_total",
                          "Times an HTTP worker moved to the CPU a steady scraper's requests arrive on "
                          "(http follow_rx_cpu; 0 when off)",
@@ -486,6 +492,8 @@ bool Engine::start(std::string* err) {
     // experiment knobs (A/B on a box): pre-wake slice and minimum lead, microseconds
     if (const char* e = std::getenv("GPUEXP_HTTP_PREWAKE_STEP_US")) hc.prewake_step_ns = uint64_t(std::atoll(e)) * 1000;
     if (const char* e = std::getenv("GPUEXP_HTTP_PREWAKE_LEAD_US")) hc.prewake_lead_ns = uint64_t(std::atoll(e)) * 1000;
+    if (const char* e = std::getenv("GPUEXP_HTTP_PREWAKE_SPIN_MAX_US"))
+      hc.prewake_spin_max_ns = uint64_t(std::atoll(e)) * 1000;
     http_ = std::make_unique<HttpServer>(&store_, hc);
     if (!http_->start(err)) {
       http_.reset();
@@ -1672,14 +1680,20 @@ void Engine::emit_self(uint64_t gen) {
     }
     cput(self_refs_[9], f_self_scrapes_, double(hs.metrics_requests.load(std::memory_order_relaxed)), gen, none);
     cput(self_refs_[10], f_self_http_bytes_, double(hs.bytes_sent.load(std::memory_order_relaxed)), gen, none);
-    if (cfg_.http.prewake) {
-      cput(self_refs_[11], f_self_prewake_, double(hs.prewake_timer_wakeups.load(std::memory_order_relaxed)), gen,
-           none);
-      cput(prewake_hits_ref_, f_self_prewake_hits_, double(hs.prewake_hits.load(std::memory_order_relaxed)), gen,
-           none);
-      cput(prewake_hits_narrow_ref_, f_self_prewake_hits_narrow_,
-           double(hs.prewake_hits_narrow.load(std::memory_order_relaxed)), gen, none);
-    }
+    // every mode: the mode is switched at run time (set_prewake_mode)
+    cput(self_refs_[11], f_self_prewake_, double(hs.prewake_timer_wakeups.load(std::memory_order_relaxed)), gen,
+         none);
+    cput(prewake_hits_ref_, f_self_prewake_hits_, double(hs.prewake_hits.load(std::memory_order_relaxed)), gen,
+         none);
+    cput(prewake_hits_narrow_ref_, f_self_prewake_hits_narrow_,
+         double(hs.prewake_hits_narrow.load(std::memory_order_relaxed)), gen, none);
+    cput(prewake_spin_refs_[0], f_self_prewake_spins_, double(hs.prewake_spin_hits.load(std::memory_order_relaxed)),
+         gen, [] { return std::vector<std::string>{"hit"}; });
+    cput(prewake_spin_refs_[1], f_self_prewake_spins_,
+         double(hs.prewake_spin_timeouts.load(std::memory_order_relaxed)), gen,
+         [] { return std::vector<std::string>{"timeout"}; });
+    cput(prewake_spin_refs_[2], f_self_prewake_spin_s_,
+         double(hs.prewake_spin_ns.load(std::memory_order_relaxed)) * 1e-9, gen, none);
     cput(rx_moves_ref_, f_self_rx_moves_, double(hs.rx_cpu_moves.load(std::memory_order_relaxed)), gen, none);
     if (cfg_.http.enable_gzip) {
       cput(self_refs_[16], f_self_gzip_, double(gzip_eager_), gen,

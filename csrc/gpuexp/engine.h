@@ -195,6 +195,13 @@ class Engine {
   MockBackend* mock() { return mock_; }
   EngineStats stats();
   const HttpStats* http_stats() const { return http_ ? &http_->stats() : nullptr; }
+  // Runtime pre-wake switch of the HTTP workers (PrewakeMode); false without an HTTP server.
+  bool set_prewake_mode(int mode) {
+    if (!http_ || mode < kPrewakeOff || mode > kPrewakeSpin) return false;
+    http_->set_prewake_mode(mode);
+    return true;
+  }
+  int prewake_mode() const { return http_ ? http_->prewake_mode() : cfg_.http.prewake_mode; }
   std::string source_status();
 
   // Control-plane inputs (any thread; applied at the next tick).
@@ -442,7 +449,8 @@ class Engine {
       f_self_overruns_, f_self_cpu_, f_self_source_up_, f_self_ctr_scope_, f_self_metrics_reads_, f_self_metrics_period_, f_self_prewake_, f_self_gzip_,
       f_self_rccl_files_, f_self_unresolved_, f_self_ctr_late_ = -1, f_self_rccl_scans_ = -1, f_self_prewake_hits_ = -1, f_self_startup_ = -1;
   SeriesRef prewake_hits_ref_, prewake_hits_narrow_ref_, startup_ref_;
-  int f_self_prewake_hits_narrow_ = -1;
+  int f_self_prewake_hits_narrow_ = -1, f_self_prewake_spins_ = -1, f_self_prewake_spin_s_ = -1;
+  SeriesRef prewake_spin_refs_[3];
   SeriesRef self_stage_refs_[kStages];
   uint64_t last_stage_ns_[kStages] = {};
   SeriesRef dev_part_refs_[kDevParts];

@@ -488,8 +488,10 @@ void SeriesTable::layout_family(int fid, uint64_t gen, std::string* body) {
       }
       s.widths[f] = std::max(s.widths[f], len);
       L.seg.fields.push_back({uint32_t(body->size() - base), s.widths[f]});
-      body->append(&scratch_[32 * f], len);
+      // right-aligned: the blanks sit between "} " and the value, where every text parser
+      // skips them (client_golang's expfmt reads a blank AFTER a value as a timestamp separator)
       body->append(size_t(s.widths[f] - len), ' ');
+      body->append(&scratch_[32 * f], len);
       body->push_back('\n');
     }
   }
@@ -585,8 +587,9 @@ void SeriesTable::render_compiled(std::string* out, std::string* gz, uint64_t ge
         }
         for (size_t f = 0; f < nf; ++f) {
           char* dst = &cbody_[L.seg.base + fl[f].off];
-          std::memcpy(dst, &scratch_[32 * f], scratch_len_[f]);
-          std::memset(dst + scratch_len_[f], ' ', fl[f].width - scratch_len_[f]);
+          const size_t pad = fl[f].width - scratch_len_[f];
+          std::memset(dst, ' ', pad);
+          std::memcpy(dst + pad, &scratch_[32 * f], scratch_len_[f]);
         }
         lm.stamp = h.stamp;
         lm.change_gen = gen;

@@ -81,8 +81,8 @@ class SeriesTable {
   // encoding=delimited`).  Call after render() of the same generation (GC + ordering).
   void render_proto(std::string* out, uint64_t gen) const;
 
-  // Fixed-layout rendering: the samples render() gives, with every value in a blank-padded
-  // field whose width only grows (per series), so the body keeps its layout from tick to tick.
+  // Fixed-layout rendering: the samples render() gives, with every value right-aligned in a
+  // blank-led field whose width only grows (per series), so the body keeps its layout from tick to tick.
   // Between layout changes (a series appears or goes, a value outgrows its field) a tick only
   // patches the fields whose values changed, and -- with `gz` -- emits the gzip member from the
   // pre-encoded static bits plus the field bytes (TemplateDeflate).  Do not mix with render()

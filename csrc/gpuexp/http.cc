@@ -12,9 +12,11 @@
 #include <sys/socket.h>
 #include <sys/uio.h>
 #include <unistd.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <cerrno>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <unordered_map>
@@ -22,6 +24,74 @@
 #include "gpuexp/common.h"
 
 namespace gpuexp {
+
+uint64_t ArrivalPredictor::period() const {
+  if (n_iv < 4) return 0;
+  uint64_t v[16];
+  std::copy(iv, iv + n_iv, v);
+  std::nth_element(v, v + n_iv / 2, v + n_iv);
+  return v[n_iv / 2];
+}
+
+void ArrivalPredictor::observe(uint64_t arrival, bool steady) {
+  if (!steady || !last || arrival <= last) {  // (re)start: no schedule to predict from
+    if (!steady) n = n_iv = 0;
+    phase = last = arrival;
+    return;
+  }
+  const uint64_t p = period();
+  if (p) {
+    const uint64_t e_rel = last + p, e_abs = phase + p;
+    err_rel[pos] = int64_t(arrival) - int64_t(e_rel);
+    err_abs[pos] = int64_t(arrival) - int64_t(e_abs);
+    pos = (pos + 1) & 15;
+    if (n < 16) ++n;
+    const int64_t d = err_abs[(pos + 15) & 15];
+    // follow the schedule a quarter of each error; a jump beyond 1/8 period re-anchors it
+    phase = (d > int64_t(p / 8) || -d > int64_t(p / 8)) ? arrival : uint64_t(int64_t(e_abs) + d / 4);
+  } else {
+    phase = arrival;
+  }
+  iv[iv_pos] = arrival - last;
+  iv_pos = (iv_pos + 1) & 15;
+  if (n_iv < 16) ++n_iv;
+  last = arrival;
+}
+
+static int64_t spread_of(const int64_t* e, int n, int64_t* sorted) {
+  std::copy(e, e + n, sorted);
+  std::sort(sorted, sorted + n);
+  return sorted[n - 2] - sorted[1];  // one outlier each side ignored
+}
+
+int ArrivalPredictor::window(uint64_t max_ns, uint64_t margin, uint64_t* from, uint64_t* until) const {
+  const uint64_t p = period();
+  if (!p || !last) return 0;
+  if (n < 8) {  // too few errors: max_ns centred on the relative prediction
+    *from = last + p - max_ns / 2;
+    *until = last + p + max_ns / 2;
+    return 1;
+  }
+  int64_t vr[16], va[16];
+  const int64_t sr = spread_of(err_rel, n, vr), sa = spread_of(err_abs, n, va);
+  const bool abs_wins = sa < sr;
+  const int64_t* v = abs_wins ? va : vr;
+  const uint64_t e = (abs_wins ? phase : last) + p;
+  const int64_t lo = v[1] - int64_t(margin), hi = v[n - 2] + int64_t(margin);
+  const int64_t med = v[n / 2];
+  int64_t a = lo, b = hi;
+  if (b - a > int64_t(max_ns)) {  // keep max_ns around the median arrival
+    a = std::max(lo, med - int64_t(max_ns) / 2);
+    b = a + int64_t(max_ns);
+    if (b > hi) {
+      b = hi;
+      a = b - int64_t(max_ns);
+    }
+  }
+  *from = uint64_t(int64_t(e) + a);
+  *until = uint64_t(int64_t(e) + b);
+  return abs_wins ? 2 : 1;
+}
 
 uint64_t learnt_scrape_period_ns(const uint64_t* newest_first, int n) {
   for (int k = 0; k < n; ++k) {
@@ -41,6 +111,23 @@ uint64_t learnt_scrape_period_ns(const uint64_t* newest_first, int n) {
     if (agree) return sum / uint64_t(agree + 1);
   }
   return 0;
+}
+
+const char* prewake_mode_name(int mode) {
+  switch (mode) {
+    case kPrewakeSlices: return "slices";
+    case kPrewakeSpin: return "spin";
+    default: return "off";
+  }
+}
+
+int parse_prewake_mode(const std::string& s) {
+  std::string v;
+  for (char ch : s) v.push_back(char(::tolower(static_cast<unsigned char>(ch))));
+  if (v == "off" || v == "false" || v == "0" || v == "no" || v.empty()) return kPrewakeOff;
+  if (v == "slices" || v == "true" || v == "on" || v == "1" || v == "yes") return kPrewakeSlices;
+  if (v == "spin") return kPrewakeSpin;
+  return -1;
 }
 
 const std::vector<double>& scrape_latency_bounds() {
@@ -79,10 +166,10 @@ struct Conn {
   bool gzip_client = false;  // its last /metrics request accepted gzip
   uint64_t last_active_ns = 0;
   uint64_t req_start_ns = 0;
-  // Benchmark diagnostics: once a request asked for X-Gpuexp-Timing, the socket carries
-  // kernel receive timestamps (SO_TIMESTAMPNS) and rx_mono_ns is when the kernel queued
-  // the last bytes read (CLOCK_MONOTONIC), splitting "request sent -> parsed" into loopback
-  // delivery and this server's wake-up + read.
+  // Every socket carries kernel receive timestamps (SO_TIMESTAMPNS): rx_mono_ns is when the
+  // kernel queued the last bytes read (CLOCK_MONOTONIC) -- the request's arrival for the
+  // learnt scrape schedule, and (X-Gpuexp-Timing) the split of "request sent -> parsed" into
+  // loopback delivery and this server's wake-up + read.
   bool rx_ts = false;
   uint64_t rx_mono_ns = 0;
   // arrival times of this connection's /metrics requests: the scrape period, learnt
@@ -123,6 +210,7 @@ struct Conn {
     }
     return std::clamp<uint64_t>(2 * dev, min_lead, max_lead);
   }
+  ArrivalPredictor pred;  // spin pre-wake: where the next request lands
 };
 
 bool ieq_prefix(const char* a, size_t alen, const char* b) {
@@ -181,6 +269,8 @@ struct HttpServer::Worker {
   int epfd = -1;
   int stopfd = -1;
   int timerfd = -1;  // scrape pre-wake
+  int kickfd = -1;   // set_prewake_mode: re-arm now
+  uint64_t armed_at = 0;  // absolute expiry the timer is armed for (0 = disarmed)
   std::thread th;
   std::unordered_map<int, Conn> conns;
   int pinned_cpu = -1;  // follow_rx_cpu: the CPU this worker is pinned to (-1: its own mask)
@@ -275,15 +365,20 @@ bool HttpServer::start(std::string* err) {
     ::epoll_ctl(w->epfd, EPOLL_CTL_ADD, w->listen_fd, &ev);
     ev.data.fd = w->stopfd;
     ::epoll_ctl(w->epfd, EPOLL_CTL_ADD, w->stopfd, &ev);
-    if (cfg_.prewake) {
-      w->timerfd = ::timerfd_create(CLOCK_MONOTONIC, TFD_NONBLOCK | TFD_CLOEXEC);
-      if (w->timerfd >= 0) {
-        ev.data.fd = w->timerfd;
-        ::epoll_ctl(w->epfd, EPOLL_CTL_ADD, w->timerfd, &ev);
-      }
+    // the pre-wake timer and the kick exist in every mode: the mode is switched at run time
+    w->timerfd = ::timerfd_create(CLOCK_MONOTONIC, TFD_NONBLOCK | TFD_CLOEXEC);
+    if (w->timerfd >= 0) {
+      ev.data.fd = w->timerfd;
+      ::epoll_ctl(w->epfd, EPOLL_CTL_ADD, w->timerfd, &ev);
+    }
+    w->kickfd = ::eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    if (w->kickfd >= 0) {
+      ev.data.fd = w->kickfd;
+      ::epoll_ctl(w->epfd, EPOLL_CTL_ADD, w->kickfd, &ev);
     }
     workers_.push_back(std::move(w));
   }
+  prewake_mode_.store(cfg_.prewake_mode, std::memory_order_relaxed);
   running_.store(true);
   for (auto& w : workers_) {
     Worker* wp = w.get();
@@ -308,9 +403,21 @@ void HttpServer::stop() {
     if (w->epfd >= 0) ::close(w->epfd);
     if (w->stopfd >= 0) ::close(w->stopfd);
     if (w->timerfd >= 0) ::close(w->timerfd);
+    if (w->kickfd >= 0) ::close(w->kickfd);
   }
   workers_.clear();
   running_.store(false);
+}
+
+void HttpServer::set_prewake_mode(int mode) {
+  if (mode < kPrewakeOff || mode > kPrewakeSpin) return;
+  prewake_mode_.store(mode, std::memory_order_relaxed);
+  for (auto& w : workers_) {
+    if (w->kickfd < 0) continue;
+    uint64_t one = 1;
+    ssize_t r = ::write(w->kickfd, &one, sizeof(one));
+    (void)r;
+  }
 }
 
 bool HttpServer::gzip_due(uint64_t now_ns, uint64_t horizon_ns) const {
@@ -367,6 +474,9 @@ void HttpServer::run(Worker* w) {
   char rbuf[16384];
   uint64_t last_sweep = mono_ns();
   uint64_t last_prewake_ns = 0;  // this worker's last pre-wake timer expiry
+  bool spin_poll = false;        // the events being handled came from a spin poll
+  uint64_t spin_until = 0, spin_started = 0;  // spin mode: the window being polled (0 = none)
+  bool metrics_seen = false;     // a /metrics request was parsed in this batch of events
 
   bool refollow = false;  // follow_rx_cpu: a connection closed, re-check the pinning
   auto close_conn = [&](int fd) {
@@ -510,17 +620,27 @@ void HttpServer::run(Worker* w) {
         respond_simple(c, 405, "Method Not Allowed", "text/plain", "method not allowed\n", false);
       } else if (path == cfg_.metrics_path) {
         stats_.metrics_requests.fetch_add(1, std::memory_order_relaxed);
-        const bool prewoken = last_prewake_ns && t0 >= last_prewake_ns &&
-                              t0 - last_prewake_ns <= cfg_.prewake_max_lead_ns + cfg_.prewake_step_ns;
+        // pre-woken: picked up by a spin poll, or (slices) its timer fired shortly before
+        const bool timer_woken = last_prewake_ns && t0 >= last_prewake_ns &&
+                                 t0 - last_prewake_ns <= cfg_.prewake_max_lead_ns + cfg_.prewake_step_ns;
+        const bool prewoken = spin_poll || (timer_woken && prewake_mode_.load(std::memory_order_relaxed) !=
+                                                               kPrewakeOff);
         if (prewoken) stats_.prewake_hits.fetch_add(1, std::memory_order_relaxed);
-        if (prewoken && t0 - last_prewake_ns <= cfg_.prewake_lead_ns + cfg_.prewake_step_ns)
+        if (prewoken && (spin_poll || t0 - last_prewake_ns <= cfg_.prewake_lead_ns + cfg_.prewake_step_ns))
           stats_.prewake_hits_narrow.fetch_add(1, std::memory_order_relaxed);
-        if (c.last_metrics_ns && t0 > c.last_metrics_ns) {
-          c.intervals[c.iv_pos] = t0 - c.last_metrics_ns;
+        metrics_seen = true;
+        // The scrape schedule is learnt from ARRIVAL times (the kernel's receive timestamp):
+        // parse times would carry this worker's own wake-up delay, which differs per mode and
+        // would bias the spin window late, where it then misses and stays biased.
+        const uint64_t arrival = c.rx_ts && c.rx_mono_ns && c.rx_mono_ns <= t0 && t0 - c.rx_mono_ns < 100000000ull
+                                     ? c.rx_mono_ns : t0;
+        c.pred.observe(arrival, c.n_intervals < 2 || c.period_ns() != 0);
+        if (c.last_metrics_ns && arrival > c.last_metrics_ns) {
+          c.intervals[c.iv_pos] = arrival - c.last_metrics_ns;
           c.iv_pos = (c.iv_pos + 1) & 3;
           if (c.n_intervals < 4) ++c.n_intervals;
         }
-        c.last_metrics_ns = t0;
+        c.last_metrics_ns = arrival;
         c.gzip_client = want_gzip && cfg_.enable_gzip;
         if (c.gzip_client && !c.expected_next()) gzip_unsteady_ns_.store(t0, std::memory_order_relaxed);
         SnapshotStore::Pin pin = store_->acquire();
@@ -566,10 +686,6 @@ void HttpServer::run(Worker* w) {
             c.head.append(prewoken ? " 1 " : " 0 ");
             c.head.append(std::to_string(c.rx_ts ? c.rx_mono_ns : 0));
             c.head.append("\r\n");
-            if (!c.rx_ts) {
-              int one = 1;
-              c.rx_ts = ::setsockopt(c.fd, SOL_SOCKET, SO_TIMESTAMPNS, &one, sizeof(one)) == 0;
-            }
           }
           c.head.append("Content-Length: ");
           c.head.append(std::to_string(b.size()));
@@ -612,13 +728,35 @@ void HttpServer::run(Worker* w) {
     return true;
   };
 
-  if (w->timerfd >= 0) ::prctl(PR_SET_TIMERSLACK, 10000UL, 0, 0, 0);  // 10 us: pre-wake slices stay short
-  // Arms the pre-wake timer for the earliest expected scrape (see HttpConfig::prewake).
+  ::prctl(PR_SET_TIMERSLACK, 10000UL, 0, 0, 0);  // 10 us: pre-wake timers stay punctual
+  // spin mode state: the window being polled (0 = not spinning), when it began, and how late
+  // the pre-wake timer fires on this host (EWMA; the timer is armed that much early)
+  uint64_t timer_late_ns = 30000;
+  auto set_timer = [&](uint64_t at) {
+    if (w->timerfd < 0 || at == w->armed_at) return;
+    itimerspec its{};
+    its.it_value.tv_sec = time_t(at / 1000000000ull);
+    its.it_value.tv_nsec = long(at % 1000000000ull);
+    ::timerfd_settime(w->timerfd, TFD_TIMER_ABSTIME, &its, nullptr);  // zero disarms
+    w->armed_at = at;
+  };
+  // Arms the pre-wake for the earliest expected scrape (see HttpConfig::prewake_mode); in
+  // spin mode, starts spinning when its window is (about to be) open.
   auto arm_prewake = [&]() {
     const uint64_t now = mono_ns();
+    const int mode = prewake_mode_.load(std::memory_order_relaxed);
     uint64_t next = 0, gz_next = 0, lead = cfg_.prewake_lead_ns;
+    uint64_t sp_from = 0, sp_until = 0;
     for (auto& kv : w->conns) {
       const uint64_t e = kv.second.expected_next();
+      uint64_t f, u;
+      if (e && mode == kPrewakeSpin &&
+          kv.second.pred.window(cfg_.prewake_spin_max_ns, cfg_.prewake_spin_margin_ns, &f, &u)) {
+        if (u > now && (!sp_from || f < sp_from)) {
+          sp_from = f;
+          sp_until = u;
+        }
+      }
       if (e && e + cfg_.prewake_window_ns > now && (!next || e < next)) {
         next = e;
         lead = kv.second.jitter_lead(cfg_.prewake_lead_ns, cfg_.prewake_max_lead_ns);
@@ -627,30 +765,68 @@ void HttpServer::run(Worker* w) {
       if (e && kv.second.gzip_client && e + 60000000000ull > now && (!gz_next || e < gz_next)) gz_next = e;
     }
     gzip_next_ns_[w->index].store(gz_next, std::memory_order_relaxed);
-    if (w->timerfd < 0) return;
-    itimerspec its{};
-    if (next) {
+    uint64_t at = 0;
+    if ((mode == kPrewakeSlices || mode == kPrewakeSpin) && next) {
       // before the lead: one timer at (expected - lead); inside the window: short slices
-      const uint64_t at = now + lead < next ? next - lead : now + cfg_.prewake_step_ns;
-      its.it_value.tv_sec = time_t(at / 1000000000ull);
-      its.it_value.tv_nsec = long(at % 1000000000ull);
+      at = now + lead < next ? next - lead : now + cfg_.prewake_step_ns;
     }
-    ::timerfd_settime(w->timerfd, TFD_TIMER_ABSTIME, &its, nullptr);  // zero disarms
+    if (mode == kPrewakeSpin && sp_from) {
+      // spin = slices + polling inside the predicted arrival window: a request before the
+      // window or after it still finds a shallow-idle worker (the slices), one inside it an
+      // on-CPU worker
+      if (now + timer_late_ns >= sp_from) {  // the window is open (or opens before a timer could fire)
+        spin_until = sp_until;
+        spin_started = now;
+        stats_.prewake_spins.fetch_add(1, std::memory_order_relaxed);
+        at = 0;
+      } else if (!at || sp_from - timer_late_ns < at) {
+        at = sp_from - timer_late_ns;
+      }
+    }
+    set_timer(at);
+  };
+  auto end_spin = [&](bool hit) {
+    stats_.prewake_spin_ns.fetch_add(mono_ns() - spin_started, std::memory_order_relaxed);
+    (hit ? stats_.prewake_spin_hits : stats_.prewake_spin_timeouts).fetch_add(1, std::memory_order_relaxed);
+    spin_until = 0;
   };
 
   for (;;) {
-    if (refollow) {  // the steady scraper may be gone: unpin (or follow the one left)
-      refollow = false;
-      follow_steady();
+    int timeout_ms = 1000;
+    if (spin_until) {
+      if (mono_ns() >= spin_until || prewake_mode_.load(std::memory_order_relaxed) != kPrewakeSpin) {
+        end_spin(false);
+        continue;
+      }
+      timeout_ms = 0;  // poll: the request finds this thread on-CPU
+    } else {
+      if (refollow) {  // the steady scraper may be gone: unpin (or follow the one left)
+        refollow = false;
+        follow_steady();
+      }
+      arm_prewake();
+      if (spin_until) continue;
     }
-    arm_prewake();
-    int n = ::epoll_wait(w->epfd, events, kMaxEvents, 1000);
+    int n = ::epoll_wait(w->epfd, events, kMaxEvents, timeout_ms);
     if (n < 0 && errno != EINTR) break;
+    if (n <= 0 && spin_until) {
+      for (int k = 0; k < 32; ++k) _mm_pause();
+      continue;
+    }
+    spin_poll = spin_until != 0;
+    metrics_seen = false;
     bool stopping = false;
     for (int i = 0; i < n; ++i) {
       int fd = events[i].data.fd;
       if (fd == w->stopfd) {
         stopping = true;
+        continue;
+      }
+      if (fd == w->kickfd) {  // mode switched: the loop re-arms
+        uint64_t v = 0;
+        ssize_t r = ::read(w->kickfd, &v, sizeof(v));
+        (void)r;
+        set_timer(0);
         continue;
       }
       if (fd == w->timerfd) {
@@ -659,6 +835,12 @@ void HttpServer::run(Worker* w) {
         (void)r;
         stats_.prewake_timer_wakeups.fetch_add(1, std::memory_order_relaxed);
         last_prewake_ns = mono_ns();
+        if (w->armed_at && prewake_mode_.load(std::memory_order_relaxed) == kPrewakeSpin) {
+          const uint64_t late = last_prewake_ns > w->armed_at ? last_prewake_ns - w->armed_at : 0;
+          timer_late_ns = std::clamp<uint64_t>((timer_late_ns * 7 + std::min<uint64_t>(late, 200000)) / 8,
+                                               2000, 100000);
+        }
+        w->armed_at = 0;  // fired: a re-arm to the same time must reach the kernel
         continue;
       }
       if (fd == w->listen_fd) {
@@ -676,6 +858,9 @@ void HttpServer::run(Worker* w) {
             ::setsockopt(cfd, SOL_SOCKET, SO_SNDBUF, &cfg_.socket_sndbuf, sizeof(cfg_.socket_sndbuf));
           Conn& c = w->conns[cfd];
           c.fd = cfd;
+          // kernel receive timestamps on every connection: request arrival times for the
+          // scrape schedule (pre-wake) and the benchmark's latency split
+          c.rx_ts = ::setsockopt(cfd, SOL_SOCKET, SO_TIMESTAMPNS, &one, sizeof(one)) == 0;
           c.last_active_ns = mono_ns();
           epoll_event ev{};
           ev.events = EPOLLIN;
@@ -701,7 +886,7 @@ void HttpServer::run(Worker* w) {
       if (ok && (events[i].events & EPOLLIN)) {
         for (;;) {
           ssize_t r;
-          if (c.rx_ts) {  // recvmsg for the receive timestamp (benchmark connections only)
+          if (c.rx_ts) {  // recvmsg for the receive timestamp
             iovec iov{rbuf, sizeof(rbuf)};
             alignas(cmsghdr) char cbuf[CMSG_SPACE(sizeof(timespec))];
             msghdr mh{};
@@ -739,6 +924,8 @@ void HttpServer::run(Worker* w) {
       }
       if (!ok) close_conn(fd);
     }
+    if (spin_until && metrics_seen) end_spin(true);
+    spin_poll = false;
     if (stopping) break;
     uint64_t now = mono_ns();
     if (now - last_sweep > 1000000000ull) {

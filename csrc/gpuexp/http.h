@@ -18,6 +18,10 @@
 
 namespace gpuexp {
 
+enum PrewakeMode : int { kPrewakeOff = 0, kPrewakeSlices = 1, kPrewakeSpin = 2 };
+const char* prewake_mode_name(int mode);
+int parse_prewake_mode(const std::string& s);  // off|slices|spin (true/on = slices); -1 = invalid
+
 struct HttpConfig {
   std::string host;  // "" = every interface, dual-stack (see make_listener)
   int port = 8000;                     // main.go:71 ":8000"; 0 = ephemeral
@@ -40,19 +44,33 @@ struct HttpConfig {
   // out of the Service instead of Prometheus ingesting frozen values as current.  0 = off.
   uint64_t stale_after_ns = 0;
   // Scrape-phase pre-wake.  Prometheus scrapes a target at a fixed interval, so once a
-  // connection's /metrics requests arrive at a steady period (>= 20 ms), the worker arms a
-  // timer for prewake_lead_ns before the next expected request and then sleeps in
-  // prewake_step_ns slices until it arrives (at most prewake_window_ns past the expected
-  // time).  Short sleeps keep the worker's core in a shallow idle state, so the request
-  // does not pay a deep-idle exit on the critical path: a few timer wake-ups per scrape
-  // instead of one long sleep, no spinning.  Off by default from round 5: five interleaved
-  // on/off pairs at the driver's command did not beat the pair-wise drift in p50 while costing
-  // the HTTP thread ~2x the CPU per scrape (profiles/r05/prewake_ab.txt).
-  bool prewake = false;
-  uint64_t prewake_lead_ns = 400000;       // ... at least; twice the connection's period jitter,
+  // connection's /metrics requests arrive at a steady period (>= 20 ms) the worker can be
+  // awake when the next one lands instead of paying a wake-up from an idle epoll_wait on the
+  // critical path (the `socket_queue_to_parsed` part of a scrape).  Modes (runtime-switchable,
+  // HttpServer::set_prewake_mode):
+  //   off     block in epoll_wait until the request arrives;
+  //   slices  arm a timer prewake_lead_ns before the expected request, then sleep in
+  //           prewake_step_ns slices until it arrives (at most prewake_window_ns late):
+  //           shallow idle, but each request still pays a timer-to-epoll wake-up;
+  //   spin    slices, plus: from each connection's recent arrival errors (ArrivalPredictor)
+  //           a window [expected + lo - margin, expected + hi + margin] no longer than
+  //           prewake_spin_max_ns, entered by a timer just before it (the timer's own measured
+  //           lateness ahead), in which the worker polls the epoll set with a zero timeout +
+  //           pause until the request arrives or the window ends.  A request inside the window
+  //           finds the worker on-CPU (no wake-up at all); one before or after it still finds
+  //           the slices' shallow-idle worker.  CPU cost = the window actually spun (the
+  //           arrival jitter) + the slices' few timer wake-ups.
+  //           Round 6 A/B (profiles/r06/): spin alone (no slices around the window) reached
+  //           86 % hits; slices 98.8 %.
+  // The default is chosen by an interleaved in-process A/B (bench.py --prewake-ab,
+  // profiles/r06/prewake_ab*).
+  int prewake_mode = 0;  // PrewakeMode
+  uint64_t prewake_lead_ns = 400000;       // slices: at least; twice the connection's period jitter,
   uint64_t prewake_max_lead_ns = 1500000;  // ... at most
   uint64_t prewake_step_ns = 150000;
   uint64_t prewake_window_ns = 3000000;
+  uint64_t prewake_spin_max_ns = 300000;    // spin: longest window (and the window before 4 errors are known)
+  uint64_t prewake_spin_margin_ns = 15000;  // spin: slack on both sides of the observed error range
   // Serve a steady scraper from the CPU its requests arrive on (SO_INCOMING_CPU: where the
   // kernel ran the receive path, the NIC queue's CPU, or the client's own for loopback): the
   // worker is pinned there while exactly one steady /metrics connection is open, so the
@@ -64,6 +82,30 @@ struct HttpConfig {
 // intervals, newest first: the newest interval that another one agrees with within 12 % (and
 // >= 20 ms), averaged with its partners; 0 = no steady period.
 uint64_t learnt_scrape_period_ns(const uint64_t* newest_first, int n);
+
+// Where a steady scraper's next request will arrive (spin pre-wake), predicted two ways from
+// the median of the last 16 arrival intervals (one late scrape does not skew it, as it does a
+// mean): relative -- the last arrival + the period (a scraper that sleeps a period after each
+// scrape, like bench.py) -- and phase-locked -- a schedule phase that follows a quarter of each
+// error, + the period (a ticker, like Prometheus' scrape loop, whose late scrape is followed by
+// an early one).  Each keeps its last 16 errors (arrival - prediction); the window follows the
+// predictor whose errors spread less.
+struct ArrivalPredictor {
+  int64_t err_rel[16] = {}, err_abs[16] = {};
+  int n = 0, pos = 0;
+  uint64_t iv[16] = {};
+  int n_iv = 0, iv_pos = 0;
+  uint64_t phase = 0;  // phase-locked estimate of the last arrival
+  uint64_t last = 0;   // last arrival
+  // `steady` = the connection's scrape period is steady (else the history restarts)
+  void observe(uint64_t arrival, bool steady);
+  uint64_t period() const;  // median interval (0 before 4 intervals)
+  // [from, until] for the next request: [e + lo - margin, e + hi + margin] with lo / hi the
+  // 2nd smallest / largest error of the last 16, trimmed to max_ns around the median; before
+  // 8 errors, max_ns centred on the relative prediction.  Returns 0 = no window, 1 = relative,
+  // 2 = phase-locked.
+  int window(uint64_t max_ns, uint64_t margin, uint64_t* from, uint64_t* until) const;
+};
 
 // Fixed latency buckets (seconds) for gpuexp_scrape_duration_seconds.
 const std::vector<double>& scrape_latency_bounds();
@@ -95,6 +137,12 @@ struct HttpStats {
   // gzip scrape was expected before the next tick (see HttpServer::gzip_due)
   std::atomic<uint64_t> gzip_on_demand{0};
   std::atomic<uint64_t> rx_cpu_moves{0};  // follow_rx_cpu: worker re-pinned to a new CPU
+  // spin pre-wake: windows entered, of which a /metrics request ended them (hit) or the window
+  // ran out (timeout), and the wall time spent polling in them (= the CPU the mode costs)
+  std::atomic<uint64_t> prewake_spins{0};
+  std::atomic<uint64_t> prewake_spin_hits{0};
+  std::atomic<uint64_t> prewake_spin_timeouts{0};
+  std::atomic<uint64_t> prewake_spin_ns{0};
   std::atomic<uint64_t> lat_buckets[kBuckets + 1]{};  // +Inf last, non-cumulative
   std::atomic<uint64_t> lat_sum_ns{0};
   std::atomic<uint64_t> lat_count{0};
@@ -126,6 +174,9 @@ class HttpServer {
   // Last time a scraper negotiated the protobuf exposition (the sampler renders it then).
   uint64_t proto_wanted_ns() const { return proto_wanted_ns_.load(std::memory_order_relaxed); }
   const HttpStats& stats() const { return stats_; }
+  // Switches the pre-wake mode of a running server (PrewakeMode); every worker re-arms at once.
+  void set_prewake_mode(int mode);
+  int prewake_mode() const { return prewake_mode_.load(std::memory_order_relaxed); }
 
  private:
   struct Worker;
@@ -136,6 +187,7 @@ class HttpServer {
   int bound_port_ = -1;
   std::atomic<bool> running_{false};
   std::atomic<bool> ready_{false};
+  std::atomic<int> prewake_mode_{0};
   std::atomic<uint64_t> gzip_wanted_ns_{0};
   std::atomic<uint64_t> proto_wanted_ns_{0};
   // last gzip /metrics request from a connection without a steady period

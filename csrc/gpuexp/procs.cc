@@ -59,6 +59,18 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
   relist_ = false;
   last_list_ns_ = now_ns;
   ++lists_;
+  // A full listing also checks that dir_fd_ is still the directory at `base`: after a KFD
+  // reload the kept fd names the dead node, whose mtime never moves again.  st_nlink == 0 (above)
+  // catches that on tmpfs, never on sysfs (kernfs reports a directory's nlink as subdirs + 2),
+  // so compare identities: one stat per listing (at most every rescan_ns on a quiet node).
+  struct stat ps {};
+  if (::stat(base.c_str(), &ps) == 0 &&
+      (dir_fd_ < 0 || !have_mtime || ps.st_ino != sb.st_ino || ps.st_dev != sb.st_dev)) {
+    if (dir_fd_ >= 0) ::close(dir_fd_);
+    dir_fd_ = ::open(base.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+    if (dir_fd_ >= 0 && ::fstat(dir_fd_, &sb) == 0) mtime_ = sb.st_mtim;
+    ++dir_reopens_;
+  }
   // Opens device `di`'s files of a process directory; false if it has no context there (yet).
   auto open_dev = [&](const std::string& pdir, size_t di, PerDev* pd) {
     const DeviceInfo& d = devs[di];

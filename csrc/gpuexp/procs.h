@@ -37,6 +37,7 @@ class KfdProcReader {
             uint64_t now_ns = 0);
   size_t tracked() const { return pids_.size(); }
   uint64_t lists() const { return lists_; }    // scans that listed the directory
+  uint64_t dir_reopens() const { return dir_reopens_; }  // the proc directory was replaced (KFD reload)
   uint64_t scans() const { return scan_no_; }  // all scans
 
  private:
@@ -71,7 +72,7 @@ class KfdProcReader {
   bool relist_ = false;          // a tracked process vanished: list at the next scan
   timespec mtime_{};             // the directory's mtime at the last look
   int dir_fd_ = -1;              // the KFD proc directory, kept open: fstat per scan, no path walk
-  uint64_t scan_no_ = 0, lists_ = 0, next_id_ = 0;
+  uint64_t scan_no_ = 0, lists_ = 0, next_id_ = 0, dir_reopens_ = 0;
   std::unordered_map<int, Entry> pids_;
 };
 

@@ -23,8 +23,10 @@ class Config:
     path: str = "/metrics"                 # main.go:70
     http_threads: int = 1
     gzip: bool = True
-    http_prewake: bool = False             # wake shortly before a steady scraper's next request (off: no
-                                           # p50 gain beyond run-to-run drift, profiles/r05/prewake_ab.txt)
+    http_prewake: str = "off"              # off | slices | spin (true = slices): have the HTTP worker awake
+                                           # when a steady scraper's next request lands (HttpConfig, http.h);
+                                           # default chosen by bench.py --prewake-ab (profiles/r06/)
+    runtime_file: str = ""                 # YAML/JSON of run-time overrides, re-read on SIGUSR1 (http_prewake)
     stale_after: float = -1.0              # /readyz 503 when the newest sample is older (s); -1 = auto
                                            # (max(5 s, 10 intervals)), 0 = never
     # sampling
@@ -143,7 +145,7 @@ class Config:
         hc.metrics_path = self.path
         hc.threads = int(self.http_threads)
         hc.enable_gzip = bool(self.gzip)
-        hc.prewake = bool(self.http_prewake)
+        hc.prewake_mode = self.prewake_mode()
         hc.follow_rx_cpu = bool(self.http_follow_rx_cpu)
         stale = float(self.stale_after)
         if stale < 0:
@@ -195,6 +197,22 @@ class Config:
         return ec
 
 
+    def prewake_mode(self) -> str:
+        return normalize_prewake(self.http_prewake)
+
+
+def normalize_prewake(v: Any) -> str:
+    """off | slices | spin; booleans keep their round-5 meaning (true = the timer slices)."""
+    s = str(v).strip().lower()
+    if s in ("", "off", "false", "0", "no"):
+        return "off"
+    if s in ("slices", "true", "on", "1", "yes"):
+        return "slices"
+    if s == "spin":
+        return "spin"
+    raise ValueError(f"http_prewake must be off|slices|spin, got {v!r}")
+
+
 _BOOL_TRUE = {"1", "true", "yes", "on"}
 _BOOL_FALSE = {"0", "false", "no", "off"}
 
@@ -219,6 +237,10 @@ def _coerce(f: dataclasses.Field, raw: Any) -> Any:
             return list(raw)
         return [x for x in str(raw).split(",") if x != ""]
     return str(raw)
+
+
+# options that also work as a bare flag (`--http-prewake` = the round-5 "on")
+_FLAG_CONST = {"http_prewake": "slices"}
 
 
 def from_yaml(path: str) -> dict:
@@ -247,9 +269,9 @@ def build_arg_parser() -> argparse.ArgumentParser:
     for f in fields(Config):
         flag = "--" + f.name.replace("_", "-")
         default = f.default if f.default is not dataclasses.MISSING else None
-        if isinstance(default, bool):
-            ap.add_argument(flag, dest=f.name, default=None, nargs="?", const="true",
-                            help=f"bool (default {default})")
+        if isinstance(default, bool) or f.name in _FLAG_CONST:
+            ap.add_argument(flag, dest=f.name, default=None, nargs="?", const=_FLAG_CONST.get(f.name, "true"),
+                            help=f"bool (default {default})" if isinstance(default, bool) else f"(default {default!r})")
         else:
             ap.add_argument(flag, dest=f.name, default=None, help=f"(default {default!r})")
     return ap
@@ -295,6 +317,7 @@ def validate(cfg: Config) -> None:
         raise ValueError(f"metrics_min_interval must be 'auto' or seconds >= 0, got {cfg.metrics_min_interval!r}")
     if not (0 <= cfg.metrics_cpu_budget <= 100):
         raise ValueError("metrics_cpu_budget must be a percentage of one core, 0-100 (0 = no cap under auto)")
+    normalize_prewake(cfg.http_prewake)
     if cfg.exposition not in ("compiled", "classic"):
         raise ValueError(f"exposition must be compiled|classic, got {cfg.exposition}")
     if cfg.counters_kick not in ("auto", "start", "after_devices", "end"):

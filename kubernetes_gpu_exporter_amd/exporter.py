@@ -76,6 +76,29 @@ class Exporter:
     def stats(self) -> dict:
         return self.engine.stats()
 
+    def apply_runtime(self, path: Optional[str] = None) -> dict:
+        """Applies the run-time overrides file (config `runtime_file`, re-read on SIGUSR1):
+        a YAML/JSON mapping; supported key: `http_prewake` (off|slices|spin).  Returns what
+        was applied; a bad file is logged and changes nothing."""
+        path = path or self.cfg.runtime_file
+        if not path:
+            return {}
+        from .config import from_yaml, normalize_prewake
+        try:
+            data = from_yaml(path)
+            applied = {}
+            if "http_prewake" in data:
+                mode = normalize_prewake(data["http_prewake"])
+                if self.engine.set_prewake_mode(mode):
+                    applied["http_prewake"] = mode
+            unknown = sorted(set(data) - {"http_prewake"})
+            if unknown:
+                log.warning("runtime file %s: ignored keys %s", path, unknown)
+            return applied
+        except (OSError, ValueError) as ex:
+            log.warning("runtime file %s not applied: %s", path, ex)
+            return {}
+
     def run_forever(self) -> int:
         def _handler(signum, frame):
             log.info("signal %s: shutting down", signum)
@@ -88,6 +111,7 @@ class Exporter:
         signal.signal(signal.SIGTERM, _handler)
         signal.signal(signal.SIGINT, _handler)
         signal.signal(signal.SIGHUP, _refresh)  # re-read pod metadata now
+        signal.signal(signal.SIGUSR1, lambda signum, frame: self.apply_runtime())  # run-time overrides
         self.start()
         log.info("serving %s on %s (%s)", self.cfg.path, self.cfg.listen, self.engine.source_status())
         # no timeout: lock waits are interrupted by signals, the handler sets the event, and

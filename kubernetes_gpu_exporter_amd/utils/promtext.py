@@ -130,7 +130,10 @@ def parse(text: str) -> dict[str, Family]:
             labels, pos = _parse_labels(line, pos, line)
         if pos >= len(line) or line[pos] != " ":
             raise ParseError(f"expected space before value: {line}")
-        toks = line[pos + 1:].split(" ")
+        # any run of blanks around the value (the compiled exposition right-aligns values)
+        toks = line[pos + 1:].split()
+        if not toks or len(toks) > 2:
+            raise ParseError(f"expected value [timestamp]: {line}")
         value = _parse_value(toks[0])
         base = sname
         for suf in ("_bucket", "_sum", "_count"):

@@ -227,3 +227,24 @@ def test_json_log_format_from_both_halves(capfd, native):
     assert core["msg"] == 'gpu "0" \\ read\x01failed retrying'
     assert py["component"] == "control" and py["msg"] == 'source "x" failed'
     assert abs(core["ts"] - py["ts"]) < 60
+
+
+def test_round6_prewake_modes(native):
+    """http_prewake is a mode (off|slices|spin); booleans keep their round-5 meaning and the
+    bare flag is the timer-slice mode.  The engine's HttpConfig carries it as prewake_mode."""
+    from kubernetes_gpu_exporter_amd.config import normalize_prewake
+    assert normalize_prewake(True) == "slices" and normalize_prewake(False) == "off"
+    assert normalize_prewake("SPIN") == "spin"
+    with pytest.raises(ValueError):
+        make_config({"http_prewake": "busy"})
+    for argv, want in ((["--http-prewake"], "slices"), (["--http-prewake", "spin"], "spin"),
+                       (["--http-prewake", "false"], "off")):
+        ec = load_config(argv, env={}).to_engine_config(native)
+        assert ec.http.prewake_mode == want, argv
+    ec = make_config({"http_prewake": "spin"}).to_engine_config(native)
+    assert ec.http.prewake is True  # the legacy boolean view: any mode but off
+    c = native.HttpConfig()
+    c.prewake = True
+    assert c.prewake_mode == "slices"
+    with pytest.raises(ValueError):
+        c.prewake_mode = "nope"

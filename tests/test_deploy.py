@@ -5,6 +5,7 @@ template exists in values.yaml."""
 import os
 import re
 
+import pytest
 import yaml
 
 from kubernetes_gpu_exporter_amd.config import load_config
@@ -234,4 +235,12 @@ def test_helm_args_accepted_by_the_cli():
     assert cfg.exposition == values["exposition"]
     assert str(cfg.metrics_min_interval) == str(values["metricsMinInterval"])
     assert cfg.metrics_cpu_budget == values["metricsCpuBudget"]
+    # the option is a percent of one core: the chart must give the engine the same fraction as
+    # the exporter's own default (round 5 shipped 0.015 = 0.015 %, 100x too small, which pinned
+    # every Helm install's gpu_metrics refresh at metrics_max_interval)
+    from kubernetes_gpu_exporter_amd._native import load
+    from kubernetes_gpu_exporter_amd.config import Config
+    n = load()
+    assert cfg.to_engine_config(n).metrics_cpu_budget == pytest.approx(Config().to_engine_config(n).metrics_cpu_budget)
+    assert Config().to_engine_config(n).metrics_cpu_budget == pytest.approx(0.015)
     assert cfg.series_profile == values["seriesProfile"] and cfg.enable_counters == values["counters"]

@@ -1,0 +1,27 @@
+"""The engine's exposition on a deterministic mock 8-GPU node (tests/golden_engine.py), full
+profile, both expositions, compared byte for byte with checked-in goldens (clock-driven values
+masked).  Pins the output across refactors of the engine (round 6: engine.cc split by source,
+table-driven families).  Regenerate deliberately with GPUEXP_REGEN_GOLDEN=1."""
+import os
+
+import pytest
+
+import golden_engine
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.mark.parametrize("exposition", ["classic", "compiled"])
+def test_engine_exposition_matches_golden(native, exposition):
+    got = golden_engine.mask(golden_engine.run(native, exposition))
+    path = os.path.join(HERE, "golden", f"engine_8gpu_full_{exposition}.txt")
+    if os.environ.get("GPUEXP_REGEN_GOLDEN") == "1":
+        with open(path, "w") as fh:
+            fh.write(got)
+    with open(path) as fh:
+        want = fh.read()
+    if got != want:
+        import difflib
+        diff = "\n".join(list(difflib.unified_diff(want.split("\n"), got.split("\n"), "golden", "now",
+                                                   lineterm=""))[:60])
+        pytest.fail("exposition differs from the golden:\n" + diff)

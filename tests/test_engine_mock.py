@@ -70,14 +70,15 @@ def test_legacy_families_exact_contract(mock_engine, exposition):
     e.set_pods([dict(uid=UID, namespace="ml", name="trainer-0", containers={CID: "main"})])
     ticks(e, 2)
     text = e.snapshot_text()
-    pad = "" if exposition == "classic" else " *"
+    pad = "" if exposition == "classic" else " *"  # compiled: the value right-aligned behind blanks
     assert re.search(re.escape("# HELP docker_gpu_memory_perc_usage GPU memory in percentage used by pod\n"
                                "# TYPE docker_gpu_memory_perc_usage gauge\n"
-                               'docker_gpu_memory_perc_usage{pid="4242",pod="trainer-0"} 10') + pad + "\n", text)
+                               'docker_gpu_memory_perc_usage{pid="4242",pod="trainer-0"} ') + pad +
+                     re.escape("10\n"), text)
     assert re.search(re.escape("# HELP pod_gpu_memory_usage GPU memory used by Kubernetes Pod\n"
                                "# TYPE pod_gpu_memory_usage gauge\n"
-                               'pod_gpu_memory_usage{pid="4242",pod="trainer-0"} 30922086809.6') + pad + "\n",
-                     text)
+                               'pod_gpu_memory_usage{pid="4242",pod="trainer-0"} ') + pad +
+                     re.escape("30922086809.6\n"), text)
     # docker_ sorts before pod_ (client_golang Gather order)
     assert text.index("docker_gpu_memory_perc_usage") < text.index("pod_gpu_memory_usage")
 

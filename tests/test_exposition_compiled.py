@@ -157,14 +157,14 @@ def test_outgrown_field_relayouts_only_its_family(native):
     txt, gz = t.render_compiled(4, 1, True)
     assert t.last_relayouts() == 1
     assert gzip.decompress(gz) == txt.encode()
-    # back to a short value: the field keeps its width (blank-padded; an outgrown fraction
-    # field gets the room of the longest round-trip form, 24), no new layout
+    # back to a short value: the field keeps its width (right-aligned behind blanks; an
+    # outgrown fraction field gets the room of the longest round-trip form, 24), no new layout
     for f in ids:
         t.put(f, ["0", "a"], 5.0, 5)
     txt, gz = t.render_compiled(5, 1, True)
     assert t.last_relayouts() == 0
     line = [ln for ln in txt.splitlines() if ln.startswith("m03_")][0]
-    assert line.endswith("5" + " " * 23)
+    assert line.endswith("} " + " " * 23 + "5")
     # an outgrown integer field keeps two more digits of room
     for f in ids:
         t.put(f, ["0", "a"], 5.0, 6)
@@ -349,3 +349,55 @@ def test_compiled_randomized_settling(native):
         assert len(last) <= 1.1 * len(fresh) + 16, (len(last), len(fresh))
 
     check()
+
+
+@pytest.mark.parametrize("gc_after", [1, 3])
+def test_rotating_slots_take_only_the_changed_fields(native, gc_after):
+    """The engine renders into rotating snapshot slots (render_compiled with out_gen): a slot
+    that holds this layout's body as of an older generation gets only the fields changed
+    since then copied in.  With 3 slots, skipped generations (a publish that did not happen),
+    relayouts (a value outgrowing its field, series coming and going), families passed over
+    unchanged and gc_after > 1, every slot's text must equal a fresh render of a twin table
+    with the same history, and its gzip must inflate to it (a stale field left in
+    a rotating slot would publish wrong values under a valid gzip)."""
+    rng = random.Random(11 + gc_after)
+    a, b = native.SeriesTable(), native.SeriesTable()
+    nfam = 7
+    fa = [a.add_family(f"s{i}_metric", f"help {i}", native.MetricType.gauge, ["gpu", "k"]) for i in range(nfam)]
+    fb = [b.add_family(f"s{i}_metric", f"help {i}", native.MetricType.gauge, ["gpu", "k"]) for i in range(nfam)]
+    vals = {}
+    gen = 0
+    copied_less = 0
+    for step in range(160):
+        gen += 2 if rng.random() < 0.15 else 1  # a skipped generation now and then
+        for i in range(nfam):
+            if i == 0 and step:
+                # family 0: the same series every tick, values changed every 3rd (else passed over)
+                for (fi, g, k), v in [(k, v) for k, v in vals.items() if k[0] == 0]:
+                    v = float(rng.randint(0, 99)) if step % 3 == 0 else v
+                    vals[(fi, g, k)] = v
+                    a.put(fa[fi], [g, k], v, gen)
+                    b.put(fb[fi], [g, k], v, gen)
+                continue
+            churn = step % 12 == 0  # layout changes come in bursts, steady ticks in between
+            for g in range(3):
+                if churn and rng.random() < 0.2:
+                    continue  # series absent this tick (GC'd after gc_after generations)
+                key = (i, str(g), "y" if churn and rng.random() < 0.2 else "x")  # sometimes a new series
+                r = rng.random()
+                if r < 0.6 and key in vals:
+                    v = vals[key]  # unchanged
+                elif r < 0.97 or not churn:
+                    v = float(rng.randint(0, 99))
+                else:
+                    v = float(rng.randint(0, 10 ** rng.randint(3, 12)))  # may outgrow its field
+                vals[key] = v
+                a.put(fa[i], [key[1], key[2]], v, gen)
+                b.put(fb[i], [key[1], key[2]], v, gen)
+        txt, gz, copied = a.render_compiled_slot(gen, gen % 3, gc_after)
+        ref, _ = b.render_compiled(gen, gc_after, False)
+        assert txt == ref, (step, gen)
+        assert zlib.decompress(gz, 31) == txt.encode()
+        if copied < len(txt):
+            copied_less += 1
+    assert copied_less > 40  # the delta path really ran (not only full copies)

@@ -957,3 +957,33 @@ def test_vm_fault_of_an_exited_process_keeps_its_pod(native, mock_engine, tmp_pa
     pod = {(s[1]["pod"], s[1]["event"]): s[2] for s in promtext.samples(fams, "amd_pod_gpu_kfd_events_total")}
     assert pod == {("trainer-0", "vm_fault"): 1}
     assert 'pid="4242"' not in e.snapshot_text()  # its process series are gone all the same
+
+
+def test_replaced_kfd_proc_directory_is_reopened(native, tmp_path):
+    """A KFD reload replaces /sys/class/kfd/kfd/proc.  On sysfs the old directory's nlink never
+    reaches 0 (kernfs reports subdirs + 2), so the reader cannot rely on it to notice that its
+    kept directory fd names a dead node whose mtime never moves again.  Here the old directory
+    survives under another name (nlink stays > 0, as on sysfs): the next full listing (the
+    rescan) compares identities and reopens, so a process added afterwards is found by the
+    directory's mtime at the next tick, not one rescan interval later."""
+    h = mi355x_node(tmp_path, 1)
+    (g,) = h.gpus
+    h.add_process(4242, kubepods_cgroup(UID, CID), gpus={g.gpu_id: (1000, 10)})
+    e = _engine(native, tmp_path, kfd_rescan_interval_s=10.0)
+
+    def pids():
+        f = promtext.parse(e.snapshot_text())
+        return sorted(lab["pid"] for _, lab, _ in promtext.samples(f, "amd_gpu_process_vram_bytes"))
+
+    e.tick(1 * S)
+    assert pids() == ["4242"]
+    kfd = tmp_path / "sys/class/kfd/kfd"
+    (kfd / "proc").rename(kfd / "proc.old")      # the old node lives on (nlink > 0) ...
+    (kfd / "proc").mkdir()                        # ... and a new directory takes its path
+    h.add_process(4242, kubepods_cgroup(UID, CID), gpus={g.gpu_id: (1000, 10)})
+    e.tick(12 * S)                                # the rescan: a full listing, identity checked
+    assert pids() == ["4242"]
+    h.add_process(5151, kubepods_cgroup(UID, CID), gpus={g.gpu_id: (3000, 10)})
+    e.tick(12 * S + 100_000_000)                  # mtime of the NEW directory moved: listed now
+    assert pids() == ["4242", "5151"]
+    e.stop()

@@ -593,3 +593,96 @@ def test_gzip_copy_follows_the_scrape_schedule(native):
         assert on_demand <= 3, on_demand
     finally:
         e.stop()
+
+
+def _window_hits(native, arrivals, **kw):
+    w = native.spin_windows(arrivals, **kw)
+    inside = [bool(k) and f <= a <= u for (f, u, k), a in zip(w, arrivals[1:])]
+    return w, inside
+
+
+def test_spin_predictor_follows_a_relative_scraper(native):
+    """A scraper that sleeps one period after each scrape (bench.py's step pacing): each
+    interval is the period plus a sleep overshoot, so the next arrival is the last one plus
+    the (median) period.  After 8 errors the spin window is the observed error range plus a
+    margin -- far shorter than the 300 us cap on a steady client -- and holds the arrival."""
+    import random
+    rng = random.Random(7)
+    t, arr = 10 ** 12, []
+    for _ in range(120):
+        t += 100_000_000 + rng.randint(40_000, 60_000)
+        arr.append(t + int(rng.gauss(0, 5_000)))
+    w, inside = _window_hits(native, arr)
+    late = inside[20:]
+    assert sum(late) / len(late) >= 0.9, sum(late) / len(late)
+    assert all(k == 1 for *_, k in w[20:]) or sum(1 for *_, k in w[20:] if k == 2) < len(w[20:])
+    widths = [u - f for f, u, k in w[20:]]
+    assert max(widths) <= 300_000 and sorted(widths)[len(widths) // 2] < 120_000, widths[:5]
+
+
+def test_spin_predictor_locks_to_a_ticker_phase(native):
+    """A ticker scraper (Prometheus' scrape loop) on a busy host: scrapes land on a fixed
+    grid k * period, but one in four is delayed 300 us and the next comes back on the grid.
+    The relative prediction (last + period) is then off by 300 us after every late one; the
+    phase-locked one is not, and wins on error spread."""
+    import random
+    rng = random.Random(3)
+    arr = [10 ** 12 + k * 100_000_000 + (300_000 if k % 4 == 3 else 0) + int(rng.gauss(0, 5_000))
+           for k in range(120)]
+    w, inside = _window_hits(native, arr)
+    assert sum(1 for *_, k in w[30:] if k == 2) >= 0.9 * len(w[30:])  # phase-locked chosen
+    on_grid = [h for h, a in zip(inside[30:], range(31, 120)) if a % 4 != 3]
+    assert sum(on_grid) / len(on_grid) >= 0.9, sum(on_grid) / len(on_grid)
+    assert native.spin_windows([]) == [] and native.spin_windows([5]) == []
+    # no period yet: no window
+    assert native.spin_windows([10 ** 12, 10 ** 12 + 10 ** 8])[0][2] == 0
+
+
+def test_prewake_mode_switches_at_run_time(native):
+    """set_prewake_mode on a running engine (what SIGUSR1 + the runtime file do in the
+    exporter): spin windows are entered only in spin mode, the timer stays quiet when off,
+    and the spin counters reach the exposition."""
+    c = native.EngineConfig()
+    c.backend = "mock"
+    c.interval_s = 0
+    c.http.host = "127.0.0.1"
+    c.http.port = 0
+    e = native.Engine(c)
+    e.start()
+    try:
+        assert e.prewake_mode == "off"
+        e.tick(1_000_000_000)
+        cl = native.ScrapeClient("127.0.0.1", e.http_port, "/metrics")
+        t = time.monotonic()
+
+        def scrape_n(k):
+            nonlocal t
+            for _ in range(k):
+                t += 0.030
+                time.sleep(max(0.0, t - time.monotonic()))
+                assert cl.scrape() > 0
+
+        scrape_n(12)
+        s0 = e.stats()
+        assert s0["http_prewake_timer_wakeups"] == 0 and s0["http_prewake_spins"] == 0
+        assert e.set_prewake_mode("spin") and e.prewake_mode == "spin"
+        scrape_n(20)
+        s1 = e.stats()
+        assert s1["http_prewake_spins"] >= 5, s1
+        assert s1["http_prewake_spin_hits"] + s1["http_prewake_spin_timeouts"] <= s1["http_prewake_spins"]
+        # a window is at most prewake_spin_max_ns (+ the poll's own granularity) long
+        assert s1["http_prewake_spin_ns"] <= s1["http_prewake_spins"] * 400_000
+        e.set_prewake_mode("off")
+        scrape_n(3)
+        s2 = e.stats()
+        scrape_n(10)
+        s3 = e.stats()
+        assert s3["http_prewake_spins"] == s2["http_prewake_spins"]
+        with pytest.raises(ValueError):
+            e.set_prewake_mode("fast")
+        e.tick(2_000_000_000)
+        fams = promtext.parse(e.snapshot_text())
+        assert promtext.value(fams, "gpuexp_http_prewake_spins_total", outcome="hit") == s3["http_prewake_spin_hits"]
+        assert "gpuexp_http_prewake_spin_seconds_total" in fams
+    finally:
+        e.stop()

@@ -132,7 +132,7 @@ def test_control_plane_isolates_failures_and_pushes_on_change(mock_engine):
     assert "boom" in cp.errors
     e.mock_set_processes(0, [dict(pid=42, vram_bytes=7.0)])
     e.tick(1_000_000_000)
-    assert 'pod_gpu_memory_usage{pid="42",pod="p"} 7' in e.snapshot_text()
+    assert promtext.value(promtext.parse(e.snapshot_text()), "pod_gpu_memory_usage", pid="42", pod="p") == 7
     # unchanged metadata is not re-pushed
     fp = cp._last_fp
     cp.refresh_once()
