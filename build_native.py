@@ -32,7 +32,9 @@ ARCH = os.environ.get("GPUEXP_OFFLOAD_ARCH", "gfx950")
 CORE_CC = [
     "gpuexp/common.cc", "gpuexp/exposition.cc", "gpuexp/deflate_tmpl.cc", "gpuexp/gzip.cc", "gpuexp/http.cc",
     "gpuexp/gpu_metrics.cc", "gpuexp/backend_mock.cc", "gpuexp/backend_sysfs.cc",
-    "gpuexp/backend_amdsmi.cc", "gpuexp/procs.cc", "gpuexp/ras.cc", "gpuexp/kfd_events.cc", "gpuexp/engine.cc",
+    "gpuexp/backend_amdsmi.cc", "gpuexp/procs.cc", "gpuexp/ras.cc", "gpuexp/kfd_events.cc", "gpuexp/engine.cc", "gpuexp/engine_device.cc", "gpuexp/engine_procs.cc",
+    "gpuexp/engine_pods.cc", "gpuexp/engine_rccl.cc", "gpuexp/engine_kfd_events.cc", "gpuexp/engine_self.cc",
+    "gpuexp/engine_state.cc", "gpuexp/fake_sources.cc",
     "gpuexp/optional_sources.cc", "gpuexp/client.cc", "gpuexp/pmc_rounds.cc", "gpuexp/pmc_harness.cc",
     "bindings.cc",
 ]

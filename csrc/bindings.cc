@@ -673,6 +673,10 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("kfd_rescan_interval_s", &EngineConfig::kfd_rescan_interval_s)
       .def_readwrite("metrics_max_interval_s", &EngineConfig::metrics_max_interval_s)
       .def_readwrite("fake_metrics_cost_us", &EngineConfig::fake_metrics_cost_us)
+      .def_readwrite("fake_pmc_cost_us", &EngineConfig::fake_pmc_cost_us)
+      .def_readwrite("fake_sentinel_cost_us", &EngineConfig::fake_sentinel_cost_us)
+      .def_readwrite("sentinel_min_interval_s", &EngineConfig::sentinel_min_interval_s)
+      .def_readwrite("counters_min_interval_s", &EngineConfig::counters_min_interval_s)
       .def_readwrite("queue_devices", &EngineConfig::queue_devices)
       .def_readwrite("queue_devices_bdf", &EngineConfig::queue_devices_bdf)
       .def_readwrite("force_amdsmi_metrics", &EngineConfig::force_amdsmi_metrics)
@@ -727,6 +731,7 @@ PYBIND11_MODULE(_gpuexp, m) {
         d["publish_skipped"] = s.publish_skipped;
         d["last_tick_ns"] = s.last_tick_ns;
         d["max_tick_ns"] = s.max_tick_ns;
+        d["tick_ns_total"] = s.tick_ns_total;
         d["render_bytes"] = s.render_bytes;
         d["series"] = s.series;
         d["device_errors"] = s.device_errors;
@@ -772,6 +777,7 @@ PYBIND11_MODULE(_gpuexp, m) {
         return e.set_prewake_mode(v);
       }, py::arg("mode"), "switch the HTTP workers' scrape pre-wake at run time (off|slices|spin)")
       .def_property_readonly("prewake_mode", [](const Engine& e) { return std::string(prewake_mode_name(e.prewake_mode())); })
+      .def("reset_tick_max", &Engine::reset_tick_max, "restart stats()['max_tick_ns'] (a measurement window)")
       .def("source_status", &Engine::source_status)
       .def("set_pods", [](Engine& e, py::list pods, bool complete) {
         std::vector<PodMeta> v;

@@ -408,8 +408,9 @@ class AmdsmiBackend : public Backend {
     return double(devs_.at(size_t(dev.index)).gm.period_ns()) * 1e-9;
   }
 
-  void update_metrics_min_interval(const DeviceInfo& dev, uint64_t ns) override {
+  void update_metrics_min_interval(const DeviceInfo& dev, uint64_t ns, uint64_t not_before_ns = 0) override {
     devs_.at(size_t(dev.index)).gm.set_min_fresh_interval(ns);
+    devs_.at(size_t(dev.index)).gm.defer_fresh_until(not_before_ns);
   }
 
   std::string describe(const DeviceInfo& dev) override {

@@ -219,9 +219,11 @@ class Backend {
   void set_fake_metrics_cost(uint64_t ns) { fake_metrics_cost_ns_ = ns; }
   // Per-GPU cap on fresh gpu_metrics reads, changed while running (the engine's "auto"
   // policy, EngineConfig::metrics_min_interval_s < 0).  Sampler thread only.
-  virtual void update_metrics_min_interval(const DeviceInfo& dev, uint64_t ns) {
+  // not_before_ns: no fresh read before then (0 = none): the GPU's phase within the cap.
+  virtual void update_metrics_min_interval(const DeviceInfo& dev, uint64_t ns, uint64_t not_before_ns = 0) {
     (void)dev;
     (void)ns;
+    (void)not_before_ns;
   }
   virtual const char* name() const = 0;
   // Enumerates devices once.  Returns false (with *err) if the backend cannot run.

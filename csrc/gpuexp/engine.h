@@ -26,6 +26,7 @@
 #include "gpuexp/backends.h"
 #include "gpuexp/device.h"
 #include "gpuexp/exposition.h"
+#include "gpuexp/engine_families.h"
 #include "gpuexp/http.h"
 #include "gpuexp/kfd_events.h"
 #include "gpuexp/procs.h"
@@ -79,9 +80,16 @@ struct EngineConfig {
   // metrics_cpu_budget of one core (between fetches the cached table is re-decoded; the
   // per-tick activity signals come from the PMC counters, read every tick).
   double metrics_min_interval_s = -1;
-  double metrics_cpu_budget = 0.015;   // auto: fraction of one core for SMU fetches (all GPUs)
+  // auto: fraction of one core for SMU fetches (all GPUs).  0.75 %: 8 GPUs under load (~380 us of
+  // kernel busy-wait per fetch) fetch every 5th tick at 10 Hz, one GPU every tick
+  // (profiles/r06/cpu_projection.txt)
+  double metrics_cpu_budget = 0.0075;
   double metrics_max_interval_s = 1.0;  // auto: never staler than this
   uint64_t fake_metrics_cost_us = 0;   // tests only: thread CPU burnt per fresh gpu_metrics read
+  // tests / tools/project_cpu.py only (fake_sources.cc): >= 0 runs the real PMC read machine on
+  // scripted fake GPUs (counters) or a fake sentinel, burning this much CPU per GPU per read / run
+  int fake_pmc_cost_us = -1;
+  int fake_sentinel_cost_us = -1;
   bool legacy_families = true;         // pod_gpu_memory_usage / docker_gpu_memory_perc_usage
   bool pod_attribution = true;
   bool infer_device_owner = true;      // single-pod GPU -> device series carry the pod
@@ -99,6 +107,10 @@ struct EngineConfig {
   std::string sentinel_impl = "auto";  // auto (PMC queue if the aqlprofile counters run, else HIP) | hip | queue
   int sentinel_ring = 64;
   int sentinel_spin = 500;  // ~15 us window (rocprofv3: spin 2000 ran 61 us/launch)
+  // The sentinel runs at most this often (its SCLK / dispatch / memory-latency probes do not need
+  // a 100 Hz tick; each run is a dispatch + ring drain per GPU on the sampler).  Manual-tick
+  // engines (interval_s = 0) run it every tick.
+  double sentinel_min_interval_s = 0.5;
   bool enable_counters = false;
   std::string counters_plugin;         // path to _gpuexp_aqlpmc.so / _gpuexp_rocprof.so
   // continuous: counting never pauses and is read once per tick (aqlprofile plugin);
@@ -107,6 +119,9 @@ struct EngineConfig {
   int counters_window_ms = 20;         // duty: counting window...
   int counters_interval_ms = 1000;     // ...once per interval (see rocprof_plugin.cc)
   int counters_sync_us = 2000;         // continuous: longest a tick waits for its own counter read
+  // continuous: a PMC read round at most this often (0 = every tick).  Each round costs host CPU
+  // per GPU (packet + output reduction); above 20 Hz a tick exports the last window again.
+  double counters_min_interval_s = 0.05;
   // continuous: when a tick's PMC read goes out.  "start": before the device reads;
   // "after_devices": once the gpu_metrics SMU fetches are done (a PM4 read in flight while
   // the SMU serves the metrics table slows the fetch, profiles/r04/devices_split.txt).
@@ -162,7 +177,8 @@ struct EngineStats {
   uint64_t overruns = 0;
   uint64_t publish_skipped = 0;
   uint64_t last_tick_ns = 0;
-  uint64_t max_tick_ns = 0;
+  uint64_t max_tick_ns = 0;   // since start or the last reset_tick_max()
+  uint64_t tick_ns_total = 0;  // wall time of every tick so far (mean = tick_ns_total / ticks)
   uint64_t render_bytes = 0;
   uint64_t series = 0;
   uint64_t device_errors = 0;
@@ -194,6 +210,10 @@ class Engine {
   const std::vector<DeviceInfo>& devices() const { return devices_; }
   MockBackend* mock() { return mock_; }
   EngineStats stats();
+  void reset_tick_max() {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    stats_.max_tick_ns = 0;
+  }
   const HttpStats* http_stats() const { return http_ ? &http_->stats() : nullptr; }
   // Runtime pre-wake switch of the HTTP workers (PrewakeMode); false without an HTTP server.
   bool set_prewake_mode(int mode) {
@@ -243,36 +263,57 @@ class Engine {
     DeviceOwner owner;
     DeviceOwner owner_built;  // ns/pod/container the refs were built for
     bool owner_built_set = false;
-    // cached series handles (re-upserted on owner change or GC)
-    SeriesRef info, up, gfx, umc, xcc[kMaxXcc], vram_used, vram_total, hbm_bw, power, power_cap,
-        energy, temp[9], clk[3], xrd[kMaxXgmiLinks], xwr[kMaxXgmiLinks], xrd_rate, xwr_rate,
-        links_up, pcie_bw, pcie_replay, pcie_speed, pcie_width, thr[5], nprocs, cu_occ, ctr[10],
-        sen[4], ecc[3], aer[3], nak[2], recov, xgmi_w, xgmi_s, xclk[kMaxXcc], sen_xlat[kMaxXcc], sen_mem, sen_xmem[kMaxXcc],
-        kev[std::size(kKfdSubscribed)], pages[3], gtt_used, gtt_total, board, mfma_util, xmfma[kMaxXcc], sen_pend, mflops[2],
-        disp_stall, occ_lim[4], ctr_health[6];
+    // cached series handles of every per-GPU family (RefScope::kGpu), addressed by dref();
+    // rebuilt on an owner change (new pod labels) or GC
+    std::vector<SeriesRef> refs;
     std::vector<SeriesRef> fw;  // amd_gpu_firmware_info, one per component
     uint64_t kfd_events[kKfdEventIds] = {};  // KFD SMI events seen on this GPU, by id
     uint64_t errors = 0;
-    SeriesRef err_ref;
-    SeriesRef self_reads[4];  // gpu_metrics reads fresh / coalesced, refresh period, counter scope
-    SeriesRef fetch_cpu, fetch_cap;  // SMU-fetch CPU so far; current fetch cap (auto policy)
-    uint64_t ras_ns = 0, gtt_ns = 0;  // this tick's RAS / GTT read time (sample_one)
+    uint64_t ras_ns = 0, gtt_ns = 0;  // this tick's RAS / GTT read time (sample_devices)
     double fetch_cost_ns = 0;        // EWMA thread CPU of a fresh gpu_metrics read (0 = none yet)
     double fetch_cpu_s = 0;          // thread CPU of every fresh gpu_metrics read so far
     uint64_t fetch_cap_ns = 0;       // cap currently set on the backend's reader
     uint64_t metrics_fresh_ns = 0;   // tick time of the last fresh gpu_metrics read (0 = none yet)
-    SeriesRef metrics_age;
   };
-  // Cached series handles of a (GPU, PID) or a pod, valid while their label values are the
-  // ones recorded here: the per-tick path then sets values without building label vectors.
+  // Cached series handles of a (GPU, PID) (and of a PID's legacy series) or a pod, valid while
+  // their label values are the ones recorded here: the per-tick path then sets values without
+  // building label vectors.  Indexed by family: pref()/podref().
   struct ProcRefs {
     std::string comm, ns, pod, container;
-    SeriesRef vram, cu, sdma, evicted, gfx;
+    SeriesRef ref[kFamProcEnd - kFamProcVram];
     uint64_t gen = 0;
   };
   struct PodRefs {
-    SeriesRef ref[12];
+    SeriesRef ref[kFamPodEnd - kFamPodVram + 1];  // (+1: the fp8 series of amd_pod_gpu_mfma_flops)
     uint64_t gen = 0;
+  };
+  static SeriesRef& pref(ProcRefs& r, Fam f) { return r.ref[f - kFamProcVram]; }
+  static SeriesRef& podref(PodRefs& r, Fam f, int k = 0) {
+    return r.ref[f == kFamPodFlops && k ? kFamPodEnd - kFamPodVram : f - kFamPodVram];
+  }
+  // A GPU's gfx activity split over its processes by their share of the occupied CUs.  KFD
+  // compute contexts report no per-process engine time (fdinfo drm-engine-* stays empty,
+  // profiles/r01/kfd_read_costs.txt); a sole process gets all of it, and with no waves resident
+  // at the CU sample the split is even (engine_procs.cc).
+  struct CuSplit {
+    explicit CuSplit(const std::vector<ProcSample>& procs);
+    double frac(const ProcSample& p) const;  // the process's fraction of the GPU (NaN: unknown)
+    size_t n = 0;
+    bool any = false;  // some process has a CU occupancy
+    double sum = 0;    // CUs occupied by all processes
+  };
+  // A pod's aggregates over one tick (engine_pods.cc)
+  struct PodAgg {
+    double vram = 0;
+    std::set<int> pids;
+    int gpus = 0;
+    double xrd = 0, xwr = 0, power = 0, gfx = 0, gfx_share = 0;
+    double energy_j = 0;          // this tick
+    double xrd_b = 0, xwr_b = 0;  // xGMI bytes this tick (owned GPUs whole, shared GPUs by share)
+    double mfma = 0, hbm = 0, flops[2] = {0, 0};
+    int gfx_n = 0, mfma_n = 0, hbm_n = 0, flops_n = 0;
+    double alloc_s = 0, busy_s = 0;  // GPU-seconds this tick
+    bool share_known = false;
   };
   struct ProcAttr {
     std::string ns, pod, container, uid;
@@ -284,20 +325,45 @@ class Engine {
   uint64_t ctl_epoch_ = 1;
 
   void define_families();
+  void register_families(const std::vector<FamilySpec>& specs);
+  int counters_interval_ms() const;
   void run_sampler();
   void tick_locked(uint64_t now_ns);
+  // engine_device.cc
+  uint64_t sample_devices(uint64_t now, bool split_cpu, uint64_t* part);  // returns failed reads
+  void update_fetch_policy(uint64_t now);
   void collect_device(int i, uint64_t gen, double dt_s);
+  void collect_counters(int i, uint64_t gen, double dt_s);
+  void collect_sentinel(int i, uint64_t gen);
+  // engine_procs.cc
   void emit_processes(uint64_t gen, const std::vector<std::vector<ProcSample>>& per_dev);
-  void emit_self(uint64_t gen);
-  void update_fetch_policy();
+  // engine_pods.cc
+  void infer_owners(const std::vector<std::vector<ProcSample>>& per_dev);
+  void emit_pods(uint64_t gen, const std::vector<std::vector<ProcSample>>& per_dev);
+  void emit_pod_totals(uint64_t gen);
+  // engine_rccl.cc
+  void emit_rccl(uint64_t gen);
+  void emit_rccl_self(uint64_t gen);
+  // engine_kfd_events.cc
   void count_kfd_events();
+  void emit_device_kfd_events(int dev, uint64_t gen);
   void emit_kfd_events(uint64_t gen);
+  // engine_self.cc
+  void emit_self(uint64_t gen);
+  void emit_http_self(uint64_t gen, bool publish_hist);
   std::string device_key(size_t i) const;  // "<bdf>/<partition>": stable across restarts
   void load_state();
   bool save_state();
   void trace_event(const char* name, uint64_t start_ns, uint64_t dur_ns);
-  void dput(DevState& st, int dev, SeriesRef& r, int fid, std::initializer_list<const char*> extra,
-            double v, uint64_t gen);
+  // Sets `v` on slot `k` of per-GPU family `f` (labels: the device's, then `extra`).
+  void dput(DevState& st, int dev, Fam f, int k, std::initializer_list<const char*> extra, double v, uint64_t gen);
+  SeriesRef& dref(DevState& st, Fam f, int k = 0) { return st.refs[size_t(fam_off_[f] + k)]; }
+  SeriesRef& gref(Fam f, int k = 0) { return grefs_[size_t(fam_off_[f] + k)]; }
+  // Sets `v` on slot `k` of global family `f`; labels() only when the handle is stale.
+  template <class F>
+  void gput(Fam f, int k, double v, uint64_t gen, F&& labels) {
+    cput(gref(f, k), fam_ids_[f], v, gen, std::forward<F>(labels));
+  }
   // Sets `v` through the cached handle `r`; builds the label values (labels()) and
   // re-interns only when the handle is stale.
   template <class F>
@@ -353,7 +419,10 @@ class Engine {
   uint64_t start_mono_ns_ = 0, startup_ns_ = 0;  // start() entry; start() -> first tick
   // thread clocks already charged to gpuexp_sampler_cpu_seconds_total (sampler thread only)
   uint64_t counters_cpu_seen_ = 0, pool_cpu_seen_ = 0, sampler_cpu_seen_ = 0;  // ticks whose counter read missed counters_sync_us (sampler thread)
-  std::string counters_kick_mode_ = "start";  // cfg_.counters_kick with "auto" resolved
+  std::string counters_kick_mode_ = "start";
+  uint64_t sentinel_last_ns_ = 0;  // tick time of the last sentinel run (sentinel_min_interval_s)
+  uint64_t counters_kick_ns_ = 0;  // tick time the last PMC read round was for (counters_min_interval_s)
+  bool counters_round_next_ = false;  // "end" kick: the next tick has a round to sync  // cfg_.counters_kick with "auto" resolved
   std::string sentinel_status_ = "disabled", counters_status_ = "disabled";
 
   SeriesTable table_;
@@ -390,7 +459,6 @@ class Engine {
     uint64_t gen = 0;
   };
   std::map<std::pair<int, std::string>, RcclRefs> rccl_refs_;
-  SeriesRef rccl_self_refs_[5];  // tracer file states (4) and scans
   std::unordered_map<uint64_t, ProcRefs> proc_refs_;               // (device << 32 | pid) -> handles
   std::unordered_map<uint64_t, ProcRefs> legacy_refs_;             // pid -> legacy handles (pod, vram, gfx=perc)
   std::map<std::pair<std::string, std::string>, PodRefs> pod_refs_;  // (ns, pod) -> handles
@@ -401,13 +469,6 @@ class Engine {
   std::map<std::pair<std::string, std::string>, std::pair<double, double>> pod_gpu_s_;
   // (ns, pod) -> last time an applied pod list had it (GC of per-pod totals under partial lists)
   std::map<std::pair<std::string, std::string>, uint64_t> pod_last_known_ns_;
-  SeriesRef pods_complete_ref_;
-  SeriesRef kfd_scan_refs_[3];
-  SeriesRef rx_moves_ref_;
-  int f_self_rx_moves_ = -1;
-  int f_self_pods_complete_ = -1, f_self_kfd_scans_ = -1, f_self_kfd_tracked_ = -1;
-  SeriesRef self_refs_[21];
-  SeriesRef expo_refs_[3];
   // The self-observability histograms (per-stage tick time, scrape latency) accumulate every
   // tick here; above 10 Hz they are published into the table at most once a second:
   // re-rendering and re-splicing ~120 bucket lines per tick was most of a 100 Hz tick's
@@ -416,8 +477,8 @@ class Engine {
   double stage_hist_sum_[8] = {};
   uint64_t stage_hist_n_[8] = {};
   uint64_t self_hist_pub_ns_ = 0;
-  int f_self_expo_ = -1;
   uint64_t expo_relayouts_ = 0;  // sampler thread
+  std::map<std::pair<std::string, std::string>, PodAgg> pod_agg_;  // tick scratch (engine_pods.cc)
 
   // stats (guarded by stats_mu_)
   std::mutex stats_mu_;
@@ -428,34 +489,15 @@ class Engine {
   size_t trace_events_ = 0;
   uint64_t trace_t0_ = 0;
 
-  // family ids
-  int f_info_, f_up_, f_gfx_, f_umc_, f_xcc_, f_vram_used_, f_vram_total_, f_hbm_bw_, f_power_,
-      f_power_cap_, f_energy_, f_temp_, f_clk_, f_xrd_, f_xwr_, f_xrd_rate_, f_xwr_rate_,
-      f_links_up_, f_pcie_bw_, f_pcie_replay_, f_pcie_speed_, f_pcie_width_, f_thr_, f_nprocs_,
-      f_cu_occ_, f_ecc_, f_aer_, f_pcie_nak_, f_pcie_recov_, f_xgmi_width_, f_xgmi_speed_, f_mfma_, f_sq_busy_, f_gui_, f_waves_, f_lds_, f_lds_conf_, f_hbm_rd_, f_remote_rd_, f_remote_wr_,
-      f_hbm_wr_, f_sen_sclk_, f_sen_lat_, f_sen_xcc_, f_sen_runs_, f_xcc_clk_, f_sen_xlat_, f_sen_mem_, f_sen_xmem_, f_mfma_util_, f_xcc_mfma_, f_sen_pend_, f_mfma_flops_ = -1;
-  int f_proc_vram_, f_proc_cu_, f_proc_sdma_, f_proc_evicted_, f_proc_gfx_;
-  int f_legacy_mem_ = -1, f_legacy_perc_ = -1;
-  int f_pod_mfma_ = -1, f_pod_hbm_ = -1, f_pod_flops_ = -1;
-  int f_disp_stall_ = -1, f_occ_lim_ = -1, f_self_ctr_events_ = -1, f_self_ctr_rescue_ = -1;
-  int f_pod_vram_, f_pod_procs_, f_pod_gpus_, f_pod_xrd_, f_pod_xwr_, f_pod_power_, f_pod_gfx_, f_pod_gfx_share_,
-      f_pod_energy_ = -1, f_pod_xrd_total_ = -1, f_pod_xwr_total_ = -1, f_pod_alloc_s_ = -1, f_pod_busy_s_ = -1;
-  int f_rccl_calls_, f_rccl_bytes_, f_rccl_comm_;
-  int f_kfd_ev_ = -1, f_pod_kfd_ev_ = -1, f_pages_ = -1, f_gtt_used_ = -1, f_gtt_total_ = -1;
-  int f_board_ = -1, f_fw_ = -1, f_driver_ = -1;
+  // family ids (table-driven, engine_families.h): SeriesTable id of each Fam (-1: not
+  // registered), and the first handle slot of a per-GPU (DevState::refs) or global (grefs_) family
+  int fam_ids_[kFamCount];
+  int fam_off_[kFamCount];
+  int gpu_slots_ = 0;
+  std::vector<SeriesRef> grefs_;
   std::string driver_version_, kernel_release_;
-  int f_self_build_, f_self_ticks_, f_self_last_, f_self_stage_, f_self_scrape_, f_self_scrapes_,
-      f_self_http_bytes_, f_self_render_bytes_, f_self_series_, f_self_dev_errors_,
-      f_self_overruns_, f_self_cpu_, f_self_source_up_, f_self_ctr_scope_, f_self_metrics_reads_, f_self_metrics_period_, f_self_prewake_, f_self_gzip_,
-      f_self_rccl_files_, f_self_unresolved_, f_self_ctr_late_ = -1, f_self_rccl_scans_ = -1, f_self_prewake_hits_ = -1, f_self_startup_ = -1;
-  SeriesRef prewake_hits_ref_, prewake_hits_narrow_ref_, startup_ref_;
-  int f_self_prewake_hits_narrow_ = -1, f_self_prewake_spins_ = -1, f_self_prewake_spin_s_ = -1;
-  SeriesRef prewake_spin_refs_[3];
-  SeriesRef self_stage_refs_[kStages];
   uint64_t last_stage_ns_[kStages] = {};
-  SeriesRef dev_part_refs_[kDevParts];
   double dev_part_total_s_[kDevParts] = {};  // sampler thread
-  int f_self_dev_part_ = -1, f_self_fetch_cpu_ = -1, f_self_fetch_cap_ = -1, f_self_metrics_age_ = -1;
 };
 
 }  // namespace gpuexp

@@ -94,6 +94,7 @@ GpuMetricsReader& GpuMetricsReader::operator=(GpuMetricsReader&& o) noexcept {
   content_ = o.content_;
   coalesce_ = o.coalesce_;
   min_fresh_ns_ = o.min_fresh_ns_;
+  not_before_ns_ = o.not_before_ns_;
   fake_cost_ns_ = o.fake_cost_ns_;
   xcp_ = o.xcp_;
   nxcc_ = o.nxcc_;
@@ -154,8 +155,9 @@ bool GpuMetricsReader::read(DeviceSample* out, uint64_t now_ns) {
     out->metrics_coalesced = true;
     return decode_gpu_metrics_v1_8(buf_, size_t(last_n_), out, xcp_, nxcc_);
   }
-  if (min_fresh_ns_ && now_ns && last_n_ > 0 && last_read_ns_ && now_ns > last_read_ns_ &&
-      now_ns - last_read_ns_ < min_fresh_ns_) {
+  if ((min_fresh_ns_ && now_ns && last_n_ > 0 && last_read_ns_ && now_ns > last_read_ns_ &&
+       now_ns - last_read_ns_ < min_fresh_ns_) ||
+      (not_before_ns_ && now_ns && last_n_ > 0 && now_ns < not_before_ns_)) {
     coalesced_reads_ += 1;
     last_was_fresh_ = false;
     out->metrics_coalesced = true;

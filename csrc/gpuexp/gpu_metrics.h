@@ -127,6 +127,9 @@ class GpuMetricsReader {
   // Fresh reads at most every `ns` (0 = as often as the PMFW refreshes): caps the kernel
   // CPU of the SMU fetches (120-420 us each) when many GPUs are sampled at a high rate.
   void set_min_fresh_interval(uint64_t ns) { min_fresh_ns_ = ns; }
+  // No fresh read before `ns` (0 = none): the engine gives each GPU's fetch its own phase of the
+  // cap, so a node's GPUs do not all fetch on the same tick.
+  void defer_fresh_until(uint64_t ns) { not_before_ns_ = ns; }
   uint64_t min_fresh_interval() const { return min_fresh_ns_; }
   // Tests only: thread CPU burnt per fresh read (models the SMU round trip on a fake host).
   void set_fake_cost(uint64_t ns) { fake_cost_ns_ = ns; }
@@ -146,6 +149,7 @@ class GpuMetricsReader {
   uint8_t fmt_ = 0, content_ = 0;
   bool coalesce_ = true;
   uint64_t min_fresh_ns_ = 0;
+  uint64_t not_before_ns_ = 0;
   uint64_t fake_cost_ns_ = 0;
   int xcp_ = 0, nxcc_ = 0;
   long last_n_ = 0;

@@ -40,6 +40,32 @@ using rp_sample_xcc_fn = int (*)(int, double*, int);
 using rp_sync_fn = int (*)(int timeout_us);
 using rp_health_fn = int (*)(int dev, uint64_t* out, int n);
 
+}  // namespace
+
+void fill_counter_reading(const double* v, CounterReading* out) {
+  out->ok = true;
+  out->mfma_busy_pct = v[0];
+  out->mfma_util_pct = v[10];
+  out->sq_busy_pct = v[1];
+  out->gui_active_pct = v[2];
+  out->waves_per_s = v[3];
+  out->lds_active_pct = v[4];
+  out->lds_bank_conflict_pct = v[5];
+  out->hbm_read_bps = v[6];
+  out->hbm_write_bps = v[7];
+  out->remote_read_bps = v[8];
+  out->remote_write_bps = v[9];
+  out->mfma_bf16_flops = v[11];
+  out->mfma_fp8_flops = v[12];
+  out->dispatch_stall_pct = v[13];
+  out->lds_limited_pct = v[14];
+  out->wave_limited_pct = v[15];
+  out->vgpr_limited_pct = v[16];
+  out->sgpr_limited_pct = v[17];
+}
+
+namespace {
+
 class PluginCounters : public CounterSource {
  public:
   PluginCounters(std::string path, int window_ms, int interval_ms, bool continuous, bool inline_rounds)
@@ -103,25 +129,7 @@ class PluginCounters : public CounterSource {
     if (!started_) return false;
     double v[kCounterOutputs];
     if (sample_(dev, dt_s, v) != 0) return false;
-    out->ok = true;
-    out->mfma_busy_pct = v[0];
-    out->mfma_util_pct = v[10];
-    out->sq_busy_pct = v[1];
-    out->gui_active_pct = v[2];
-    out->waves_per_s = v[3];
-    out->lds_active_pct = v[4];
-    out->lds_bank_conflict_pct = v[5];
-    out->hbm_read_bps = v[6];
-    out->hbm_write_bps = v[7];
-    out->remote_read_bps = v[8];
-    out->remote_write_bps = v[9];
-    out->mfma_bf16_flops = v[11];
-    out->mfma_fp8_flops = v[12];
-    out->dispatch_stall_pct = v[13];
-    out->lds_limited_pct = v[14];
-    out->wave_limited_pct = v[15];
-    out->vgpr_limited_pct = v[16];
-    out->sgpr_limited_pct = v[17];
+    fill_counter_reading(v, out);
     out->nxcc = sample_xcc_ ? std::max(0, sample_xcc_(dev, out->xcc_mfma_busy_pct, kMaxXcc)) : 0;
     return true;
   }

@@ -33,6 +33,8 @@ std::string default_rocprof_plugin();
 
 // Derived values a counter plugin's gpuexp_rp_sample fills, in CounterReading order.
 constexpr int kCounterOutputs = 18;
+// CounterReading from those kCounterOutputs values (ok = true; nxcc left to the caller).
+void fill_counter_reading(const double* v, CounterReading* out);
 
 // Health of a GPU's counter reads (continuous mode), cumulative: reads found still queued,
 // windows dropped because the counters went backwards, re-arms after another profiler reset
@@ -81,6 +83,11 @@ class CounterSource {
 std::unique_ptr<CounterSource> make_rocprof_counters(const std::string& plugin_path, int window_ms,
                                                      int interval_ms, bool continuous = false,
                                                      bool inline_rounds = false);
+
+// Tests / tools/project_cpu.py (fake_sources.cc): the real PMC read machine over scripted fake
+// GPUs, and a sentinel, each burning `cost_us` of host CPU per GPU per read / run.
+std::unique_ptr<CounterSource> make_fake_counters(uint64_t cost_us, int interval_ms, bool inline_rounds);
+std::unique_ptr<SentinelSource> make_fake_sentinel(uint64_t cost_us);
 
 // One collective call record written by the RCCL tracer tool into a per-process ring.
 struct RcclTotals {

@@ -37,7 +37,8 @@ class Config:
     metrics_min_interval: str = "auto"     # at most one gpu_metrics SMU fetch per GPU per this many s
                                            # (0 = every PMFW refresh; auto = as often as metrics_cpu_budget
                                            # allows at the measured fetch cost): bounds sampler CPU at 8 GPUs
-    metrics_cpu_budget: float = 1.5        # auto: % of one core all GPUs' SMU fetches may use together
+    metrics_cpu_budget: float = 0.75       # auto: % of one core all GPUs' SMU fetches may use together
+                                           # (8 loaded GPUs at 10 Hz: a fetch every 5th tick; 1 GPU: every tick)
     mock_devices: int = 1
     host_root: str = ""                    # prefix for /sys and /proc (DaemonSet: /host)
     devices: list = field(default_factory=list)  # GPU indices and/or PCI BDFs to export (empty = all)
@@ -55,6 +56,7 @@ class Config:
     # optional sources
     enable_sentinel: bool = False
     sentinel_spin: int = 500
+    sentinel_interval: float = 0.5         # the sentinel kernel runs at most this often (s; manual ticks: every tick)
     sentinel_impl: str = "auto"            # auto (on the PMC counters' queue when they run, else HIP) | hip | queue
     enable_counters: bool = False
     counters_plugin: str = "aqlpmc"        # aqlpmc | rocprof | /path/to/plugin.so
@@ -63,6 +65,7 @@ class Config:
     counters_interval_ms: int = 1000       # ... per interval (the rocprof plugin's spin is duty-cycled)
     counters_kick: str = "auto"            # continuous: a tick's PMC read goes out at its start | after_devices |
                                            # end of the previous tick | auto (end below 50 ms ticks, else start)
+    counters_min_interval: float = 0.05    # continuous counters: a PMC read round at most this often (s)
     counters_inline: bool = True           # continuous: the sampler posts/collects each tick's PMC read itself
     http_follow_rx_cpu: bool = False       # pin the HTTP worker to the CPU a steady scraper's requests arrive on
     queue_devices: list = field(default_factory=list)  # GPUs (indices / BDFs) that get the exporter's
@@ -165,6 +168,7 @@ class Config:
         ec.enable_sentinel = bool(self.enable_sentinel)
         ec.sentinel_spin = int(self.sentinel_spin)
         ec.sentinel_impl = str(self.sentinel_impl)
+        ec.sentinel_min_interval_s = float(self.sentinel_interval)
         ec.enable_counters = bool(self.enable_counters)
         if self.counters_plugin in ("", "aqlpmc", "rocprof"):
             from ._native import rocprof_plugin_path
@@ -176,6 +180,7 @@ class Config:
         ec.counters_interval_ms = int(self.counters_interval_ms)
         ec.counters_kick = str(self.counters_kick)
         ec.counters_inline = bool(self.counters_inline)
+        ec.counters_min_interval_s = float(self.counters_min_interval)
         ec.enable_rccl = bool(self.enable_rccl)
         ec.rccl_dir = self.rccl_dir
         ec.rccl_verify = bool(self.rccl_verify)

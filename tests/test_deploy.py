@@ -242,5 +242,6 @@ def test_helm_args_accepted_by_the_cli():
     from kubernetes_gpu_exporter_amd.config import Config
     n = load()
     assert cfg.to_engine_config(n).metrics_cpu_budget == pytest.approx(Config().to_engine_config(n).metrics_cpu_budget)
-    assert Config().to_engine_config(n).metrics_cpu_budget == pytest.approx(0.015)
+    assert Config().to_engine_config(n).metrics_cpu_budget == pytest.approx(0.0075)
+    assert n.EngineConfig().metrics_cpu_budget == pytest.approx(0.0075)  # the engine's own default agrees
     assert cfg.series_profile == values["seriesProfile"] and cfg.enable_counters == values["counters"]

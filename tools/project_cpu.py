@@ -10,6 +10,9 @@ gpu_metrics read (--fetch-us, from tools/probe_fetch_cost.py on MI355X).  Whole-
 (metrics_min_interval auto, --budget % of one core for all GPUs' fetches) and, for
 comparison, with every tick fetching (metrics_min_interval 0).  A projection of the
 per-GPU costs, not a measurement of an 8-GPU node (the driver's SCALE run is that).
+Round 6: the GPU-side sources are in the projection too -- the real PMC read machine on fake
+GPUs at --pmc-us of CPU per GPU per round and a sentinel at --sentinel-us per GPU per run
+(fake_sources.cc) -- so its counters and sentinel stages scale with the GPU count.
 Usage: python tools/project_cpu.py [--fetch-us 206,450] [--hz 10,100] [--seconds 4]
 """
 import argparse
@@ -40,7 +43,8 @@ while True:
 
 
 def measure(native, n_gpus: int, hz: float, fetch_us: int, policy: str, budget: float, seconds: float,
-            scrape: str = "none", exposition: str = "compiled", warmup: float = -1.0) -> dict:
+            scrape: str = "none", exposition: str = "compiled", warmup: float = -1.0, pmc_us: int = -1,
+            sentinel_us: int = -1) -> dict:
     # warm-up: long enough for the exposition to settle (a family's real parse comes 8 renders after
     # its last layout; the scraper's first gzip ask starts the gzip copies): 20 ticks, at least 1 s
     if warmup < 0:
@@ -63,6 +67,12 @@ def measure(native, n_gpus: int, hz: float, fetch_us: int, policy: str, budget: 
     if hasattr(c, "exposition"):  # (an older tree, --root, has only the classic one)
         c.exposition = exposition
     c.fake_metrics_cost_us = fetch_us
+    if pmc_us >= 0 and hasattr(c, "fake_pmc_cost_us"):  # the real PMC read machine on fake GPUs
+        c.enable_counters = True
+        c.fake_pmc_cost_us = pmc_us
+    if sentinel_us >= 0 and hasattr(c, "fake_sentinel_cost_us"):
+        c.enable_sentinel = True
+        c.fake_sentinel_cost_us = sentinel_us
     c.metrics_min_interval_s = -1.0 if policy == "auto" else 0.0
     c.metrics_cpu_budget = budget / 100.0
     e = native.Engine(c)
@@ -72,6 +82,8 @@ def measure(native, n_gpus: int, hz: float, fetch_us: int, policy: str, budget: 
         scraper = subprocess.Popen([sys.executable, "-c", SCRAPER, PKG_ROOT, str(e.http_port), str(hz), scrape])
     try:
         time.sleep(warmup)
+        if hasattr(e, "reset_tick_max"):
+            e.reset_tick_max()
         r0, t0, s0 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter(), e.stats()
         time.sleep(seconds)
         r1, t1, s1 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter(), e.stats()
@@ -89,7 +101,9 @@ def measure(native, n_gpus: int, hz: float, fetch_us: int, policy: str, budget: 
             "sampler_us_per_tick": round((s1["sampler_cpu_ns"] - s0["sampler_cpu_ns"]) / ticks / 1e3, 1),
             "stage_us_per_tick": stages,
             "relayouts_per_tick": round((s1.get("relayouts", 0) - s0.get("relayouts", 0)) / ticks, 3),
-            "code_builds": s1.get("code_builds", 0) - s0.get("code_builds", 0)}
+            "code_builds": s1.get("code_builds", 0) - s0.get("code_builds", 0),
+            "tick_wall_mean_us": round((s1.get("tick_ns_total", 0) - s0.get("tick_ns_total", 0)) / ticks / 1e3, 1),
+            "tick_wall_max_us": round(s1.get("max_tick_ns", 0) / 1e3, 1)}
 
 
 PKG_ROOT = ROOT
@@ -102,7 +116,10 @@ def main() -> int:
     ap.add_argument("--fetch-us", default="206,450")
     ap.add_argument("--hz", default="10,100")
     ap.add_argument("--gpus", default="1,2,4,8")
-    ap.add_argument("--budget", type=float, default=1.5)
+    ap.add_argument("--budget", type=float, default=0.75)
+    ap.add_argument("--pmc-us", type=int, default=14,
+                    help="CPU per GPU per PMC read round (fake GPUs under the real read machine; -1 = no counters)")
+    ap.add_argument("--sentinel-us", type=int, default=4, help="CPU per GPU per sentinel run (-1 = no sentinel)")
     ap.add_argument("--seconds", type=float, default=4.0)
     ap.add_argument("--warmup", type=float, default=-1.0, help="seconds before measuring (default: 20 ticks, >= 1 s)")
     ap.add_argument("--policies", default="auto,every")
@@ -114,16 +131,20 @@ def main() -> int:
     sys.path.insert(0, PKG_ROOT)
     from kubernetes_gpu_exporter_amd._native import load
     native = load()
-    print(f"# fake-host projection, full profile, 4 processes/GPU, budget {args.budget} % (auto policy)")
-    print(f"{'gpus':>4} {'hz':>5} {'fetch_us':>8} {'policy':>6} {'cpu_%':>7} {'sampler_us/tick':>15}  exposition")
+    print(f"# fake-host projection, full profile, 4 processes/GPU, budget {args.budget} % (auto policy), "
+          f"PMC {args.pmc_us} us + sentinel {args.sentinel_us} us CPU per GPU per round / run")
+    print(f"{'gpus':>4} {'hz':>5} {'fetch_us':>8} {'policy':>6} {'cpu_%':>7} {'sampler_us/tick':>15} "
+          f"{'tick_mean_us':>12} {'tick_max_us':>11}  exposition")
     for fetch in (int(x) for x in args.fetch_us.split(",")):
         for hz in (float(x) for x in args.hz.split(",")):
             for n in (int(x) for x in args.gpus.split(",")):
                 for policy in args.policies.split(","):
                   for expo in args.exposition.split(","):
-                    r = measure(native, n, hz, fetch, policy, args.budget, args.seconds, args.scrape, expo, args.warmup)
+                    r = measure(native, n, hz, fetch, policy, args.budget, args.seconds, args.scrape, expo, args.warmup,
+                                args.pmc_us, args.sentinel_us)
                     print(f"{r['gpus']:>4} {r['hz']:>5g} {r['fetch_us']:>8} {r['policy']:>6} "
-                          f"{r['process_cpu_pct']:>7.2f} {r['sampler_us_per_tick']:>15.1f}  "
+                          f"{r['process_cpu_pct']:>7.2f} {r['sampler_us_per_tick']:>15.1f} "
+                          f"{r['tick_wall_mean_us']:>12.1f} {r['tick_wall_max_us']:>11.1f}  "
                           f"{expo} scrape={args.scrape}", flush=True)
                     if args.stages:
                         print("      stage us/tick: " + " ".join(f"{k}={v}" for k, v in r["stage_us_per_tick"].items())
