@@ -84,6 +84,8 @@ def start_exporter(args, n_gpus: int, backend: str, port: int, pod_map: str, log
         # fills in once it knows every rank's PID (real KFD-reader and attribution path).
         cmd += ["--mock-devices", str(n_gpus), "--enable-sentinel", "true", "--enable-counters", "true",
                 "--host-root", args.fake_root]
+    if backend == "mock" and getattr(args, "mock_xgmi_file", ""):
+        cmd += ["--mock-xgmi-file", args.mock_xgmi_file]
     if getattr(args, "runtime_file", ""):
         cmd += ["--runtime-file", args.runtime_file]
         if args.prewake_ab:  # the A/B's first arm from the start (warm-up included)
@@ -189,6 +191,39 @@ def run_problems(result: dict, n_gpus: int, attribution_ok: bool, rccl_on: bool)
         probs.append(f"exporter start-up {result['exporter_startup_s']} s > budget {result['exporter_startup_budget_s']} s")
     result["problems"] = probs or None
     return probs
+
+
+def xgmi_checks(patterns: dict | None, window: dict | None, world: int) -> dict | None:
+    """Per-peer sanity of the exporter's xGMI attribution at N > 1 (a SCALE record
+    with wrong per-peer attribution must not look as valid as a right one).  Values plus a
+    pass flag each; None where the run has no such data (N = 1, pattern phase off):
+      cp  every rank's ring_neighbour_share >= 0.9 (a ring uses its two neighbour links);
+      ep  every rank's per-peer shares within 20 % of uniform 1 / (N - 1) (all-to-all);
+      dp  measured / expected xGMI write of the timed all-reduce within 0.8 .. 1.25."""
+    if world <= 1:
+        return None
+    out: dict = {}
+    cp = (patterns or {}).get("cp")
+    if cp:
+        shares = [r.get("ring_neighbour_share") for r in cp["per_rank"].values()]
+        ok = bool(shares) and all(s is not None and s >= 0.9 for s in shares)
+        out["cp_ring_neighbour_share_min"] = min((s for s in shares if s is not None), default=None)
+        out["cp_ok"] = ok
+    ep = (patterns or {}).get("ep")
+    if ep:
+        uni = 1.0 / (world - 1)
+        devs = []
+        for r, v in ep["per_rank"].items():
+            sh = {p: x for p, x in v.get("per_peer_share", {}).items() if p != r}
+            devs.append(max((abs(x / uni - 1.0) for x in sh.values()), default=1.0) if len(sh) == world - 1 else 1.0)
+        out["ep_max_deviation_from_uniform"] = round(max(devs), 3) if devs else None
+        out["ep_ok"] = bool(devs) and max(devs) <= 0.2
+    moe = (window or {}).get("measured_over_expected_write")
+    out["dp_measured_over_expected_write"] = moe
+    out["dp_ok"] = None if moe is None else 0.8 <= moe <= 1.25
+    flags = [v for k, v in out.items() if k.endswith("_ok") and v is not None]
+    out["ok"] = all(flags) if flags else None
+    return out
 
 
 def launch_ranks(args, argv: list) -> int:
@@ -349,6 +384,31 @@ def main() -> int:
     pod_map = os.path.join(tmpdir, "podmap.json")
     args.fake_root = os.path.join(tmpdir, "host")
     args.runtime_file = os.path.join(tmpdir, "runtime.yaml") if args.prewake_ab else ""
+    # mock backend, N > 1: the ranks' pattern traffic per peer goes into an N x N matrix file
+    # the exporter's mock GPUs turn into per-link xGMI bytes (MockBackend::set_traffic_file),
+    # so the per-peer checks of the pattern phase run on CPU rehearsals too
+    args.mock_xgmi_file = ""
+    if backend == "mock" and world > 1:
+        run_id = "-".join(v for v in (os.environ.get("TORCHELASTIC_RUN_ID"), os.environ.get("MASTER_PORT")) if v) \
+            or str(os.getpid())
+        args.mock_xgmi_file = os.path.join(tempfile.gettempdir(), f"gpuexp-bench-xgmi-{run_id}.bin")
+        if rank == 0:
+            with open(args.mock_xgmi_file, "wb") as fh:
+                fh.write(b"\0" * (8 * world * world))
+    mock_sent: dict = {}  # this rank's pattern bytes per peer so far (mock rehearsal)
+
+    def record_mock_traffic(st) -> None:
+        if not args.mock_xgmi_file:
+            return
+        import struct
+        for p, b in st.peer_bytes.items():
+            mock_sent[p] = mock_sent.get(p, 0) + b
+        row = struct.pack(f"<{world}Q", *(int(mock_sent.get(p, 0)) for p in range(world)))
+        fd = os.open(args.mock_xgmi_file, os.O_WRONLY)
+        try:
+            os.pwrite(fd, row, 8 * world * rank)  # this rank's row only: no other writer
+        finally:
+            os.close(fd)
     os.makedirs(os.path.join(args.fake_root, "sys/class/kfd/kfd/proc"), exist_ok=True)
     port = 0
     exporter = None
@@ -625,10 +685,10 @@ def main() -> int:
         for pattern in ("cp", "ep"):
             # check=False throughout: a rank that raised here would leave the others in a
             # collective (the generators' results are verified by the tests instead)
-            run_pattern(pattern, steps=1, nbytes=nb, device=dev, check=False)  # warm the transport
+            record_mock_traffic(run_pattern(pattern, steps=1, nbytes=nb, device=dev, check=False))  # warm-up
             sync()
             t = time.perf_counter()
-            run_pattern(pattern, steps=1, nbytes=nb, device=dev, check=False)
+            record_mock_traffic(run_pattern(pattern, steps=1, nbytes=nb, device=dev, check=False))
             sync()
             steps = torch.tensor([max(1, int(target_s / max(1e-4, time.perf_counter() - t)))], device=dev)
             dist.all_reduce(steps, op=dist.ReduceOp.MAX)  # every rank runs the same step count
@@ -641,6 +701,7 @@ def main() -> int:
             t0 = time.perf_counter()
             st = run_pattern(pattern, steps=int(steps.item()), nbytes=nb, device=dev, check=False)
             sync()
+            record_mock_traffic(st)
             dist.barrier()
             if rank != 0:
                 continue
@@ -1006,6 +1067,9 @@ def main() -> int:
         if rank == 0:
             result["xgmi_patterns"] = patterns
     if rank == 0:
+        # per-peer sanity of the exporter's xGMI attribution, reported, never failing the run
+        result["xgmi_checks"] = xgmi_checks(result.get("xgmi_patterns"), result.get("xgmi_timed_window"), world)
+    if rank == 0:
         stop_proc(exporter)
 
     if args.exporter == "both":
@@ -1048,6 +1112,11 @@ def main() -> int:
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    if rank == 0 and args.mock_xgmi_file:
+        try:
+            os.unlink(args.mock_xgmi_file)
+        except OSError:
+            pass
     if problems:
         # a degraded N-GPU run must not pass for a measurement: no result line, exit 1
         for p in problems:

@@ -36,7 +36,7 @@ CORE_CC = [
     "gpuexp/engine_pods.cc", "gpuexp/engine_rccl.cc", "gpuexp/engine_kfd_events.cc", "gpuexp/engine_self.cc",
     "gpuexp/engine_state.cc", "gpuexp/fake_sources.cc",
     "gpuexp/optional_sources.cc", "gpuexp/client.cc", "gpuexp/pmc_rounds.cc", "gpuexp/pmc_harness.cc",
-    "bindings.cc",
+    "gpuexp/pmc_agents.cc", "bindings.cc",
 ]
 SENTINEL_HIP = ["gpuexp/sentinel.hip"]
 SENTINEL_HSACO = "gpuexp/sentinel_hsaco.hip"  # device-only code object for raw AQL dispatch
@@ -160,7 +160,8 @@ def build(force: bool = False, jobs: int = 8, sanitize: str | None = None, verbo
         outputs["rocprof_plugin"] = str(link_plain([objs[ROCPROF_CC[0]]], PKG / "_gpuexp_rocprof.so",
                                                    ["-lrocprofiler-sdk", "-lhsa-runtime64", "-lpthread"]))
     if (CSRC / AQLPMC_CC[0]).exists():
-        outputs["aqlpmc_plugin"] = str(link_plain([objs[AQLPMC_CC[0]], objs["gpuexp/pmc_rounds.cc"]],
+        outputs["aqlpmc_plugin"] = str(link_plain([objs[AQLPMC_CC[0]], objs["gpuexp/pmc_rounds.cc"],
+                                                   objs["gpuexp/pmc_agents.cc"]],
                                                   PKG / "_gpuexp_aqlpmc.so",
                                                   ["-lhsa-runtime64", "-lpthread"]))
         outputs["sentinel_hsaco"] = str(build_hsaco(SENTINEL_HSACO, PKG / "gpuexp_sentinel.hsaco", hdr, force))

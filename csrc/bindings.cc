@@ -14,6 +14,7 @@
 #include "gpuexp/kfd_events.h"
 #include "gpuexp/exposition.h"
 #include "gpuexp/gpu_metrics.h"
+#include "gpuexp/pmc_agents.h"
 #include "gpuexp/pmc_fake.h"
 #include "gpuexp/procs.h"
 #include "gpuexp/ras.h"
@@ -321,6 +322,34 @@ PYBIND11_MODULE(_gpuexp, m) {
      py::arg("calm_ms") = 300000.0);
   // The PMC read machine (pmc_rounds.h) on scripted fake GPUs (pmc_fake.h): see
   // tests/test_pmc_rounds.py.  Runs for ticks x tick_us with the GIL released.
+  m.def("pmc_agent_lifecycle", [](int gpus, int failing, int starved, int broken, int ticks) {
+    gpuexp_pmc::LifecycleOutcome o;
+    {
+      py::gil_scoped_release nogil;
+      o = gpuexp_pmc::run_agent_lifecycle(gpus, failing, starved, broken, ticks);
+    }
+    py::dict d;
+    d["devices"] = o.devices;
+    d["matched"] = o.matched;
+    d["usable"] = o.usable;
+    d["armed"] = o.armed;
+    d["queues_created"] = o.queues_created;
+    d["queues_live"] = o.queues_live;
+    d["signals_created"] = o.signals_created;
+    d["signals_live"] = o.signals_live;
+    d["buffers_allocated"] = o.buffers_allocated;
+    d["buffers_live"] = o.buffers_live;
+    d["buffers_left_by_design"] = o.buffers_left_by_design;
+    d["double_release"] = o.double_release;
+    d["foreign_release"] = o.foreign_release;
+    d["rescues_opened"] = o.rescues_opened;
+    d["rescues_closed"] = o.rescues_closed;
+    d["windows_on_failed_gpu"] = o.windows_on_failed_gpu;
+    d["windows"] = o.windows;
+    return d;
+  }, py::arg("gpus") = 8, py::arg("failing_gpu") = 3, py::arg("starved_gpu") = 5, py::arg("broken_gpu") = 6,
+     py::arg("ticks") = 40, "the PMC plugin's multi-agent lifecycle (pmc_agents.h) on stub GPUs");
+
   m.def("pmc_harness", [](const py::dict& d) {
     using namespace gpuexp_pmc;
     HarnessConfig c;
@@ -631,6 +660,7 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("backend", &EngineConfig::backend)
       .def_readwrite("device_threads", &EngineConfig::device_threads)
       .def_readwrite("mock_devices", &EngineConfig::mock_devices)
+      .def_readwrite("mock_xgmi_file", &EngineConfig::mock_xgmi_file)
       .def_readwrite("host_root", &EngineConfig::host_root)
       .def_readwrite("interval_s", &EngineConfig::interval_s)
       .def_readwrite("serve_http", &EngineConfig::serve_http)

@@ -53,6 +53,7 @@
 #include <unistd.h>
 
 #include "gpuexp/counter_model.h"
+#include "gpuexp/pmc_agents.h"
 #include "gpuexp/pmc_rounds.h"
 #include "kernels/probe_args.h"
 #include "gpuexp/sentinel_common.h"
@@ -88,19 +89,17 @@ const EventDef kGfx950[] = {
 // One GPU: its HSA queue(s), signals and aqlprofile programs.  The read machine
 // (pmc_rounds.cc) drives it through the ReadPort interface; init, the duty-cycled windows and
 // the sentinel / calibration dispatches use it directly.
-struct Agent : public gpuexp_pmc::ReadPort {
+// Its queue, signal and buffers (and the rescue queue's) are AgentResources (pmc_agents.h), created
+// and released through HsaOps by the same code the stub-GPU lifecycle test runs.
+struct Agent : public gpuexp_pmc::ReadPort, gpuexp_pmc::AgentResources<hsa_queue_t*, hsa_signal_t> {
   int dev = -1;
   hsa_agent_t gpu{};
   std::string bdf, gfx;
-  hsa_queue_t* queue = nullptr;
-  hsa_signal_t sig{};
   std::vector<hsa_ven_amd_aqlprofile_event_t> events;
   std::vector<int> event_ctr;  // events[i] -> Ctr
   hsa_ven_amd_aqlprofile_profile_t profile{};
   hsa_ext_amd_aql_pm4_packet_t start_pkt{}, read_pkt{}, stop_pkt{};
   uint32_t out_size = 0, cmd_size = 0;
-  void* cmd_buf = nullptr;
-  void* out_buf = nullptr;
   bool ready = false;
   std::atomic<bool> queue_error{false};
   // The queue has two producers: the read machine / init (PM4 programs) and the sampler
@@ -110,12 +109,8 @@ struct Agent : public gpuexp_pmc::ReadPort {
   Derived model;                 // SIMD / CU counts, privilege (the machine's derivations)
   // Read rescue (pmc_rounds.cc): a second queue that only ever carries read packets, with its
   // own profile, command and output buffers; exists between open_rescue and close_rescue.
-  hsa_queue_t* rq = nullptr;
-  hsa_signal_t rsig{};
   hsa_ven_amd_aqlprofile_profile_t rprofile{};
   hsa_ext_amd_aql_pm4_packet_t rstart_pkt{}, rread_pkt{};
-  void* rcmd_buf = nullptr;
-  void* rout_buf = nullptr;
   // debug (GPUEXP_AQLPMC_DEBUG): aqlprofile's coordinates of the first MFMA sample and the last
   // read's MFMA / GRBM samples
   std::mutex dbg_mu;
@@ -253,6 +248,32 @@ void* sys_alloc(size_t bytes, hsa_agent_t gpu) {
   std::memset(p, 0, bytes);
   return p;
 }
+
+// The HSA calls behind pmc_agents.h's lifecycle helpers, for one agent.
+struct HsaOps {
+  Agent* a;
+  bool create_queue(hsa_queue_t** q) {
+    if (hsa_queue_create(a->gpu, 64, HSA_QUEUE_TYPE_MULTI, queue_error_cb, a, UINT32_MAX, UINT32_MAX, q) !=
+        HSA_STATUS_SUCCESS) {
+      *q = nullptr;
+      return false;
+    }
+    // experiment knob (profiles/r03/mfma_calibration.txt): low | normal | high
+    const char* pr = std::getenv("GPUEXP_PMC_QUEUE_PRIORITY");
+    const std::string p = pr ? pr : "low";
+    hsa_amd_queue_set_priority(*q, p == "high"     ? HSA_AMD_QUEUE_PRIORITY_HIGH
+                                   : p == "normal" ? HSA_AMD_QUEUE_PRIORITY_NORMAL
+                                                   : HSA_AMD_QUEUE_PRIORITY_LOW);
+    return true;
+  }
+  void destroy_queue(hsa_queue_t* q) { hsa_queue_destroy(q); }
+  bool valid(hsa_queue_t* q) const { return q != nullptr; }
+  bool create_signal(hsa_signal_t* s) { return hsa_signal_create(1, 0, nullptr, s) == HSA_STATUS_SUCCESS; }
+  void destroy_signal(hsa_signal_t s) { hsa_signal_destroy(s); }
+  bool valid(hsa_signal_t s) const { return s.handle != 0; }
+  void* alloc(size_t bytes) { return sys_alloc(bytes, a->gpu); }
+  void release(void* p) { hsa_amd_memory_pool_free(p); }
+};
 
 // Writes one vendor-specific AQL packet and rings the doorbell.  At most one PM4 packet and
 // one sentinel dispatch are ever in flight on the 64-slot queue, so it never fills.
@@ -458,8 +479,9 @@ bool setup_agent(Agent& a, std::string* why) {
   // hsa_ven_amd_aqlprofile_start), so both buffers are over-provisioned.
   cmd_size = std::max<uint32_t>(cmd_size * 16, 256u << 10);
   out_size = std::max<uint32_t>(out_size * 16, 64u << 10);
-  a.cmd_buf = sys_alloc(cmd_size, a.gpu);
-  a.out_buf = sys_alloc(out_size, a.gpu);
+  HsaOps ops{&a};
+  a.cmd_buf = ops.alloc(cmd_size);
+  a.out_buf = ops.alloc(out_size);
   if (!a.cmd_buf || !a.out_buf) {
     *why = "system memory pool allocation failed";
     return false;
@@ -501,21 +523,12 @@ bool setup_agent(Agent& a, std::string* why) {
   }
   a.out_size = out_size;
   a.cmd_size = cmd_size;
-  if (hsa_queue_create(a.gpu, 64, HSA_QUEUE_TYPE_MULTI, queue_error_cb, &a, UINT32_MAX, UINT32_MAX, &a.queue) !=
-      HSA_STATUS_SUCCESS) {
+  if (!ops.create_queue(&a.queue)) {
     *why = "hsa_queue_create failed";
     return false;
   }
   crumb("queue created");
-  {
-    // experiment knob (profiles/r03/mfma_calibration.txt): low | normal | high
-    const char* pr = std::getenv("GPUEXP_PMC_QUEUE_PRIORITY");
-    const std::string p = pr ? pr : "low";
-    hsa_amd_queue_set_priority(a.queue, p == "high"     ? HSA_AMD_QUEUE_PRIORITY_HIGH
-                                        : p == "normal" ? HSA_AMD_QUEUE_PRIORITY_NORMAL
-                                                        : HSA_AMD_QUEUE_PRIORITY_LOW);
-  }
-  if (hsa_signal_create(1, 0, nullptr, &a.sig) != HSA_STATUS_SUCCESS) {
+  if (!ops.create_signal(&a.sig)) {
     *why = "hsa_signal_create failed";
     return false;
   }
@@ -627,35 +640,23 @@ bool Agent::collect(int q, gpuexp_pmc::Sample* out) {
 // drains 0.8 s after a 6 s starvation, profiles/r03/sentinel_starvation.txt).
 // GPUEXP_PMC_READ_RESCUE=0 disables.
 bool Agent::open_rescue() {
+  HsaOps ops{this};
   rprofile = profile;
-  rcmd_buf = sys_alloc(cmd_size, gpu);
-  rout_buf = sys_alloc(out_size, gpu);
-  bool ok = rcmd_buf && rout_buf;
-  if (ok) {
+  const bool ok = gpuexp_pmc::open_rescue(ops, *this, cmd_size, out_size, [this] {
     rprofile.command_buffer = {rcmd_buf, cmd_size};
     rprofile.output_buffer = {rout_buf, out_size};
     // the start program is generated (the read program is built after it) but never run:
     // it would re-program and reset the running counters
-    ok = g_aql.hsa_ven_amd_aqlprofile_start(&rprofile, &rstart_pkt) == HSA_STATUS_SUCCESS &&
-         g_aql.hsa_ven_amd_aqlprofile_read(&rprofile, &rread_pkt) == HSA_STATUS_SUCCESS;
-  }
-  ok = ok && hsa_queue_create(gpu, 64, HSA_QUEUE_TYPE_MULTI, queue_error_cb, this, UINT32_MAX, UINT32_MAX, &rq) ==
-                 HSA_STATUS_SUCCESS;
-  if (ok) hsa_amd_queue_set_priority(rq, HSA_AMD_QUEUE_PRIORITY_LOW);
-  ok = ok && hsa_signal_create(1, 0, nullptr, &rsig) == HSA_STATUS_SUCCESS;
-  if (!ok) close_rescue();
+    return g_aql.hsa_ven_amd_aqlprofile_start(&rprofile, &rstart_pkt) == HSA_STATUS_SUCCESS &&
+           g_aql.hsa_ven_amd_aqlprofile_read(&rprofile, &rread_pkt) == HSA_STATUS_SUCCESS;
+  });
   return ok;
 }
 
 // Releases the rescue queue (its context-save area), its signal and buffers.
 void Agent::close_rescue() {
-  if (rq) hsa_queue_destroy(rq);
-  if (rsig.handle) hsa_signal_destroy(rsig);
-  if (rcmd_buf) hsa_amd_memory_pool_free(rcmd_buf);
-  if (rout_buf) hsa_amd_memory_pool_free(rout_buf);
-  rq = nullptr;
-  rsig = hsa_signal_t{};
-  rcmd_buf = rout_buf = nullptr;
+  HsaOps ops{this};
+  gpuexp_pmc::close_rescue(ops, *this);
 }
 
 // Duty-cycled windows: start, sleep(window), read, stop on every GPU, one window per interval.
@@ -738,18 +739,10 @@ void duty_loop(gpuexp_pmc::RoundMachine* m) {
 void teardown_locked() {
   for (Agent* a : g_agents) {
     if (!a) continue;
-    if (a->queue) hsa_queue_destroy(a->queue);
-    if (a->sig.handle) hsa_signal_destroy(a->sig);
     // A timed-out (or still queued, or abandoned and never run) packet may still write the
-    // buffers: the read machine marks such a GPU broken at its stop, and they are leaked.
-    if (!a->broken) {
-      a->close_rescue();
-      if (a->cmd_buf) hsa_amd_memory_pool_free(a->cmd_buf);
-      if (a->out_buf) hsa_amd_memory_pool_free(a->out_buf);
-    } else {
-      if (a->rq) hsa_queue_destroy(a->rq);
-      if (a->rsig.handle) hsa_signal_destroy(a->rsig);
-    }
+    // buffers: the read machine marks such a GPU broken at its stop, and they are left.
+    HsaOps ops{a};
+    gpuexp_pmc::release_agent(ops, *a, a->broken.load());
     delete a;
   }
   g_agents.clear();
@@ -1093,28 +1086,21 @@ extern "C" __attribute__((visibility("default"))) int gpuexp_rp_init(int ndev, c
   int ok = 0;
   std::string why;
   // Partitioned sockets (CPX/DPX/QPX) expose several agents with one BDF, in partition
-  // order, as do the exporter's devices: match the k-th device to the k-th free agent.
-  std::vector<bool> taken(f.gpus.size(), false);
-  int disabled = 0;
+  // order, as do the exporter's devices: the k-th device gets the k-th free agent
+  // (pmc_agents.h match_agents).  A GPU whose setup fails keeps its slot, unusable.
+  std::vector<std::string> gpu_bdfs;
+  for (const auto& g : f.gpus) gpu_bdfs.push_back(g.second);
+  const gpuexp_pmc::AgentMatch match = gpuexp_pmc::match_agents(ndev, bdfs, gpu_bdfs);
+  const int disabled = match.n_reserved;
   for (int d = 0; d < ndev; ++d) {
-    const bool off = bdfs[d][0] == '-';  // reserve the agent, no queue (queue_devices)
-    const std::string want = lower(bdfs[d] + (off ? 1 : 0));
-    for (size_t gi = 0; gi < f.gpus.size(); ++gi) {
-      const auto& g = f.gpus[gi];
-      if (taken[gi] || want != g.second) continue;
-      taken[gi] = true;
-      if (off) {
-        ++disabled;
-        break;
-      }
-      auto* a = new Agent;
-      a->dev = d;
-      a->gpu = g.first;
-      a->bdf = g.second;
-      g_agents[size_t(d)] = a;
-      if (setup_agent(*a, &why)) ++ok;
-      break;
-    }
+    const int gi = match.gpu_of[size_t(d)];
+    if (gi < 0) continue;
+    auto* a = new Agent;
+    a->dev = d;
+    a->gpu = f.gpus[size_t(gi)].first;
+    a->bdf = f.gpus[size_t(gi)].second;
+    g_agents[size_t(d)] = a;
+    if (setup_agent(*a, &why)) ++ok;
   }
   if (!ok) {
     teardown_locked();

@@ -1,9 +1,13 @@
 // Mock GPU backend (BASELINE config 1: "mock-GPU backend on CPU, 1 fake device").
 // Values are smooth deterministic functions of the injected sample time, so tests can
 // assert exact rates; every field can be pinned and faults injected from Python.
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 
 #include "gpuexp/backends.h"
 
@@ -108,10 +112,11 @@ void MockBackend::sample(const DeviceInfo& dev, DeviceSample* out) {
   out->gtt_used = get(s, "gtt_used", 2.0 * (1ull << 30));
   out->vram_max_bw_gbs = 8192;
 
-  // Integrate accumulators with the scripted rates.
+  // Integrate accumulators with the scripted rates (none on a traffic-file rehearsal).
   s.energy_units += out->power_w * dt / 15.259e-6;
-  double rd_rate = get(s, "xgmi_read_rate_kbps", 1000.0);   // per link
-  double wr_rate = get(s, "xgmi_write_rate_kbps", 1000.0);
+  const bool traffic = !traffic_path_.empty();
+  double rd_rate = traffic ? 0.0 : get(s, "xgmi_read_rate_kbps", 1000.0);   // per link
+  double wr_rate = traffic ? 0.0 : get(s, "xgmi_write_rate_kbps", 1000.0);
   for (int l = 1; l < kMaxXgmiLinks; ++l) {
     double r = s.xgmi_frac[0][l] + rd_rate * dt, w = s.xgmi_frac[1][l] + wr_rate * dt;
     s.xgmi_rd_kb[l] += uint64_t(r);
@@ -139,9 +144,16 @@ void MockBackend::sample(const DeviceInfo& dev, DeviceSample* out) {
   out->num_xgmi_links = kMaxXgmiLinks;
   out->xgmi_valid = true;
   out->xgmi_link_up[0] = kNaN;
+  std::vector<uint64_t> m;
+  const bool have_m = traffic && read_traffic(&m);
   for (int l = 1; l < kMaxXgmiLinks; ++l) {
     out->xgmi_read_kb[l] = s.xgmi_rd_kb[l];
     out->xgmi_write_kb[l] = s.xgmi_wr_kb[l];
+    const int peer = (dev.index + l) % 8;  // the mesh of init()
+    if (have_m && peer < n_) {
+      out->xgmi_write_kb[l] += m[size_t(dev.index) * size_t(n_) + size_t(peer)] / 1024;
+      out->xgmi_read_kb[l] += m[size_t(peer) * size_t(n_) + size_t(dev.index)] / 1024;
+    }
     out->xgmi_link_up[l] = 1;
   }
   out->residency_valid = true;
@@ -248,6 +260,24 @@ void MockBackend::set_fault(int dev, const std::string& fault) {
   std::lock_guard<std::mutex> lk(mu_);
   if (dev < 0 || dev >= n_) return;
   scripts_[size_t(dev)].fault = fault;
+}
+
+void MockBackend::set_traffic_file(const std::string& path) {
+  std::lock_guard<std::mutex> lk(mu_);
+  traffic_path_ = path;
+}
+
+bool MockBackend::read_traffic(std::vector<uint64_t>* m) const {
+  const size_t n = size_t(n_) * size_t(n_);
+  m->assign(n, 0);
+  const int fd = ::open(traffic_path_.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return false;
+  const ssize_t r = ::pread(fd, m->data(), n * sizeof(uint64_t), 0);
+  ::close(fd);
+  if (r < 0) return false;
+  if (size_t(r) < n * sizeof(uint64_t))  // a short file: the rest has not been written yet
+    std::memset(reinterpret_cast<char*>(m->data()) + r, 0, n * sizeof(uint64_t) - size_t(r));
+  return true;
 }
 
 }  // namespace gpuexp

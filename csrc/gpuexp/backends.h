@@ -62,6 +62,11 @@ class MockBackend : public Backend {
   // Fault injection: "none", "error" (sample fails), "vanish" (device gone),
   // "counter_reset" (accumulators restart from 0 once), "wrap" (xGMI acc near 2^64).
   void set_fault(int dev, const std::string& fault);
+  // Rehearsals of per-peer xGMI attribution on CPU ranks (bench.py --backend mock): `path` holds
+  // an N x N little-endian uint64 matrix, bytes rank/GPU i sent to GPU j so far, written by the
+  // traffic generators; each mock link's write (read) accumulator then carries exactly what its
+  // GPU sent to (received from) the link's peer, and the synthetic per-link rates are off.
+  void set_traffic_file(const std::string& path);
 
  private:
   struct Script {
@@ -84,6 +89,8 @@ class MockBackend : public Backend {
   double get(const Script& s, const char* field, double dflt) const;
   int n_;
   uint32_t kfd_base_;
+  std::string traffic_path_;
+  bool read_traffic(std::vector<uint64_t>* m) const;  // the N x N matrix (false: unreadable)
   mutable std::mutex mu_;
   std::vector<Script> scripts_;
 };

@@ -202,6 +202,7 @@ bool Engine::start(std::string* err) {
   } undo{this, &ok};
   if (cfg_.backend == "mock") {
     auto m = std::make_unique<MockBackend>(cfg_.mock_devices);
+    if (!cfg_.mock_xgmi_file.empty()) m->set_traffic_file(cfg_.mock_xgmi_file);
     mock_ = m.get();
     backend_ = std::move(m);
   } else if (cfg_.backend == "sysfs") {

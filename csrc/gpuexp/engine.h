@@ -68,6 +68,7 @@ struct EngineConfig {
   std::string backend = "mock";        // mock | sysfs | amdsmi
   int device_threads = 0;              // 0 = auto (serial), N > 1 = a pool of N reader threads
   int mock_devices = 1;
+  std::string mock_xgmi_file;          // mock only: per-peer traffic matrix (MockBackend::set_traffic_file)
   std::string host_root;               // "" == "/"
   double interval_s = 1.0;             // 0 = manual ticks only (tests)
   bool serve_http = true;

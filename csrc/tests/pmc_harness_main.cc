@@ -12,6 +12,7 @@
 #include <string>
 #include <thread>
 
+#include "gpuexp/pmc_agents.h"
 #include "gpuexp/pmc_fake.h"
 
 using namespace gpuexp_pmc;
@@ -84,7 +85,29 @@ int main(int argc, char** argv) {
   std::thread tt([&] { b = run_pmc_harness(combined(false, scale), 0.3); });
   ti.join();
   tt.join();
-  const int bad = check("inline", a) + check("thread", b);
+  int bad = check("inline", a) + check("thread", b);
+  // the HSA port's multi-agent bookkeeping (pmc_agents.h) on 8 stub GPUs + one reserved:
+  // GPU 3's setup fails, GPU 5 starves into a rescue queue, GPU 6 is broken at teardown
+  const LifecycleOutcome l = run_agent_lifecycle(8, 3, 5, 6, 40 * scale);
+  auto lfail = [&](const char* what, long long got, long long want) {
+    if (got == want) return;
+    std::printf("lifecycle: %s = %lld, want %lld\n", what, got, want);
+    bad += 1;
+  };
+  lfail("matched", l.matched, 8);
+  lfail("usable", l.usable, 7);
+  lfail("armed", l.armed, 7);
+  lfail("queues live", l.queues_live, 0);
+  lfail("signals live", l.signals_live, 0);
+  lfail("double / foreign releases", l.double_release + l.foreign_release, 0);
+  lfail("buffers left but the broken GPU's", l.buffers_live - l.buffers_left_by_design, 0);
+  lfail("windows on the failed GPU", l.windows_on_failed_gpu, 0);
+  lfail("rescues closed", l.rescues_closed, l.rescues_opened);
+  if (l.rescues_opened < 1) lfail("rescues opened >= 1", l.rescues_opened, 1);
+  std::printf("lifecycle: devices %d matched %d usable %d armed %d queues %d/%d live signals %d/%d live buffers %d "
+              "(%d left by design) rescues %d/%d\n",
+              l.devices, l.matched, l.usable, l.armed, l.queues_created, l.queues_live, l.signals_created,
+              l.signals_live, l.buffers_allocated, l.buffers_left_by_design, l.rescues_opened, l.rescues_closed);
   for (auto* o : {&a, &b})
     std::printf("%s: ticks %d late_syncs %d max_sync_us %lld reader_calls %llu\n", o == &a ? "inline" : "thread",
                 o->ticks, o->late_syncs, (long long)o->max_sync_us, (unsigned long long)o->reader_calls);

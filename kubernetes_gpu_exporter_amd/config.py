@@ -40,6 +40,7 @@ class Config:
     metrics_cpu_budget: float = 0.75       # auto: % of one core all GPUs' SMU fetches may use together
                                            # (8 loaded GPUs at 10 Hz: a fetch every 5th tick; 1 GPU: every tick)
     mock_devices: int = 1
+    mock_xgmi_file: str = ""               # mock backend: per-peer traffic matrix of a CPU rehearsal (bench.py)
     host_root: str = ""                    # prefix for /sys and /proc (DaemonSet: /host)
     devices: list = field(default_factory=list)  # GPU indices and/or PCI BDFs to export (empty = all)
     series_profile: str = "full"           # full | standard (64/GPU BASELINE load) | compact | legacy
@@ -135,6 +136,7 @@ class Config:
         ec = native.EngineConfig()
         ec.backend = self.resolved_backend()
         ec.mock_devices = int(self.mock_devices)
+        ec.mock_xgmi_file = str(self.mock_xgmi_file)
         ec.device_threads = int(self.device_threads)
         ec.metrics_coalesce = bool(self.metrics_coalesce)
         ec.metrics_min_interval_s = self.metrics_min_interval_s()

@@ -33,10 +33,16 @@ class TrafficStats:
     calls: dict = field(default_factory=dict)   # op -> calls per rank
     bytes: dict = field(default_factory=dict)   # op -> payload bytes per rank (tracer accounting)
     seconds: float = 0.0
+    # peer rank -> payload bytes this rank sent it directly (point-to-point and all-to-all
+    # patterns, whose peers the pattern fixes; a collective's per-peer split is RCCL's choice)
+    peer_bytes: dict = field(default_factory=dict)
 
     def add(self, op: str, nbytes: int, n: int = 1) -> None:
         self.calls[op] = self.calls.get(op, 0) + n
         self.bytes[op] = self.bytes.get(op, 0) + nbytes * n
+
+    def add_peer(self, peer: int, nbytes: int) -> None:
+        self.peer_bytes[peer] = self.peer_bytes.get(peer, 0) + nbytes
 
 
 def _elems(nbytes: int, world: int, esize: int) -> int:
@@ -98,6 +104,9 @@ def run(strategy: str, steps: int = 1, nbytes: int = 1 << 20, device=None, dtype
                 y = torch.empty_like(x)
                 dist.all_to_all_single(y, x)
                 st.add("alltoall", (n // world) * esize * world)
+                for p in range(world):
+                    if p != rank:
+                        st.add_peer(p, (n // world) * esize)
                 if check:
                     assert float(y[(world - 1) * (n // world)]) == world - 1
         elif strategy == "pp":
@@ -113,6 +122,7 @@ def run(strategy: str, steps: int = 1, nbytes: int = 1 << 20, device=None, dtype
                     r.wait()
                 if rank + 1 < world:
                     st.add("send", n * esize)
+                    st.add_peer(rank + 1, n * esize)
                 if rank > 0:
                     st.add("recv", n * esize)
                     if check:
@@ -139,6 +149,7 @@ def run(strategy: str, steps: int = 1, nbytes: int = 1 << 20, device=None, dtype
                         r.wait()
                     st.add("send", n * esize)
                     st.add("recv", n * esize)
+                    st.add_peer((rank + 1) % world, n * esize)
                     kv = recv
                 if check:
                     assert float(kv[0]) == (rank + 1) % world  # after world-1 hops

@@ -115,11 +115,15 @@ def test_bench_torchrun_two_ranks():
 def test_bench_eight_ranks_every_check_holds():
     """The driver's 8-GPU shape, rehearsed on CPU (8 gloo ranks, 8 mock GPUs): one line,
     every GPU exported, every rank's pod attributed, and the run's own validity checks
-    (bench.run_problems) empty; the timed scrapes are each accounted pre-woken or not."""
+    (bench.run_problems) empty; the timed scrapes are each accounted pre-woken or not.  The
+    xGMI pattern phase runs too: the ranks' ring (CP) and all-to-all (EP) traffic per peer
+    reaches the mock GPUs' links (MockBackend::set_traffic_file), and the exporter's per-peer
+    attribution must show it: every rank's ring-neighbour share >= 0.9, every all-to-all
+    peer share within 20 % of uniform (result['xgmi_checks'])."""
     env = dict(os.environ, OMP_NUM_THREADS="1")
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "8", "--backend", "mock", "--steps", "4", "--warmup",
-                        "1", "--xgmi-patterns", "0"], cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+                        "1"], cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     (d,) = _json_lines(r.stdout)
     _check(d, 8, 4, 1)
@@ -129,6 +133,13 @@ def test_bench_eight_ranks_every_check_holds():
     pw = d["prewake"]
     assert pw["timed_scrapes"] == 4 and pw["prewoken"] + pw["not_prewoken"] + pw["unknown"] == 4, pw
     assert pw["unknown"] == 0, pw  # the server echoes the pre-wake state of every timed scrape
+    chk = d["xgmi_checks"]
+    assert chk["cp_ok"] and chk["cp_ring_neighbour_share_min"] >= 0.9, (chk, d["xgmi_patterns"]["cp"])
+    assert chk["ep_ok"] and chk["ep_max_deviation_from_uniform"] <= 0.2, (chk, d["xgmi_patterns"]["ep"])
+    assert chk["dp_ok"] is None  # the DP all-reduce's per-peer split is RCCL's: nothing injected on mock links
+    for r_, v in d["xgmi_patterns"]["cp"]["per_rank"].items():
+        nbr = {str((int(r_) + 1) % 8), str((int(r_) - 1) % 8)}
+        assert set(k for k, x in v["per_peer_share"].items() if x > 0.01) <= nbr, (r_, v)
 
 
 def test_bench_unattributed_rank_fails_loudly():

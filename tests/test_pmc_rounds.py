@@ -254,3 +254,27 @@ def test_eight_agents_inline_and_thread_machines_at_once(native):
         assert (g[5]["resets"], g[5]["rearms"]) == (1, 1)
         assert g[6]["broken"]
         assert r["reader_calls"] > 1000
+
+
+def test_hsa_port_multi_agent_lifecycle_on_stub_gpus(native):
+    """The aqlprofile plugin's multi-agent bookkeeping (pmc_agents.h: BDF matching with a
+    reserved agent, per-GPU setup, arm, the rescue queue's ownership, teardown) on 8 stub GPUs
+    plus one the engine reserves without a queue, through the same templates aql_pmc.cc uses
+    on HSA (the port had only ever run with one agent).  GPU 3's queue creation
+    fails: the other 7 are armed and read; GPU 5's first queue stalls behind a sentinel run and
+    its reads move to a rescue queue and back; GPU 6 is broken at teardown, so its buffers are
+    left to the runtime's shutdown.  No queue or signal outlives teardown, nothing is released
+    twice, and only the broken GPU's buffers are left (the sanitizer presets run the same
+    lifecycle: csrc/tests/pmc_harness_main.cc)."""
+    o = native.pmc_agent_lifecycle(8, 3, 5, 6, 40)
+    assert o["devices"] == 9 and o["matched"] == 8, o
+    assert o["usable"] == 7 and o["armed"] == 7, o
+    assert o["queues_created"] == 8 and o["signals_created"] == 8, o  # 7 setups + the rescue; GPU 3 got none
+    assert o["queues_live"] == 0 and o["signals_live"] == 0, o
+    assert o["double_release"] == 0 and o["foreign_release"] == 0, o
+    assert o["buffers_left_by_design"] == 2 and o["buffers_live"] == 2, o  # GPU 6's command + output buffers
+    assert o["rescues_opened"] >= 1 and o["rescues_closed"] == o["rescues_opened"], o
+    assert o["windows_on_failed_gpu"] == 0, o
+    w = o["windows"]
+    assert w[0] == 0  # the reserved device (listed first: the engine's order is reversed)
+    assert sum(1 for x in w if x >= 30) == 7, w  # every usable GPU read on (nearly) every tick
