@@ -40,3 +40,59 @@ def test_stress_under_sanitizer(preset, env):
     assert r.returncode == 0 and out.rstrip().endswith("OK"), out[-5000:]
     assert "WARNING: ThreadSanitizer" not in out and "ERROR: AddressSanitizer" not in out
     assert "runtime error" not in out
+
+
+CLANG = "/opt/rocm/lib/llvm/bin/clang++"
+FUZZ_SEEDS = os.path.join(ROOT, "tests", "fuzz_corpus", "deflate_tmpl")
+
+
+def test_deflate_template_fuzz(tmp_path):
+    """VERDICT r05 Next #4: the compiled exposition's gzip writer (deflate_tmpl.cc) under
+    libFuzzer + ASan + UBSan for 60 s from the checked-in seed corpus, every encode inflated
+    with zlib and compared with the body (csrc/tests/fuzz_deflate_tmpl.cc).  ROCm 7.2 clang's
+    coverage instrumentation (inline-8bit-counters / trace-pc-guard) leaves ASan-instrumented
+    globals misaligned -- reported at start-up as an ODR violation on deflate_tmpl.cc's constant
+    tables -- so the libFuzzer build runs with -asan-globals=0, and everything it kept is then
+    replayed through a g++ ASan + UBSan build with global redzones (fuzz_replay_main.cc)."""
+    if not os.path.exists(CLANG) or not shutil.which("g++"):
+        pytest.skip("ROCm clang++ / g++ not available")
+    seeds = sorted(os.listdir(FUZZ_SEEDS))
+    assert len(seeds) >= 12, seeds
+    src = os.path.join(ROOT, "csrc", "tests", "fuzz_deflate_tmpl.cc")
+    inc = os.path.join(ROOT, "csrc")
+    fuzzer = str(tmp_path / "fuzz_deflate")
+    b = subprocess.run([CLANG, "-g", "-O1", "-std=c++17", "-fsanitize=fuzzer,address,undefined",
+                        "-fno-sanitize-recover=undefined", "-mllvm", "-asan-globals=0", "-I", inc, src,
+                        "-lz", "-o", fuzzer], capture_output=True, text=True, timeout=300)
+    if b.returncode != 0 and "libclang_rt.fuzzer" in b.stderr:
+        pytest.skip("libFuzzer runtime not available")
+    assert b.returncode == 0, b.stderr[-3000:]
+    corpus = tmp_path / "corpus"
+    corpus.mkdir()
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    r = subprocess.run([fuzzer, "-max_total_time=60", "-rss_limit_mb=2048", "-timeout=20",
+                        f"-artifact_prefix={tmp_path}/", str(corpus), FUZZ_SEEDS],
+                       env=env, capture_output=True, text=True, timeout=240)
+    out = r.stdout + r.stderr
+    print(out[-1500:])
+    assert r.returncode == 0, out[-5000:]
+    assert "ERROR: AddressSanitizer" not in out and "runtime error" not in out
+    assert "ERROR: libFuzzer" not in out
+    runs = [int(line.split()[1]) for line in out.splitlines() if line.startswith("Done ")]
+    assert runs and runs[0] > 1000, out[-2000:]
+    kept = os.listdir(corpus)
+    assert kept, "the fuzzer found no new coverage over the seeds"
+    # everything found, plus the seeds, through a build with ASan's global checks on
+    replay = str(tmp_path / "fuzz_replay")
+    b = subprocess.run(["g++", "-g", "-O1", "-std=c++17", "-fsanitize=address,undefined",
+                        "-fno-sanitize-recover=undefined", "-I", inc, src,
+                        os.path.join(ROOT, "csrc", "tests", "fuzz_replay_main.cc"), "-lz", "-o", replay],
+                       capture_output=True, text=True, timeout=300)
+    assert b.returncode == 0, b.stderr[-3000:]
+    r = subprocess.run([replay, str(corpus), FUZZ_SEEDS], env=env, capture_output=True, text=True,
+                       timeout=600)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-5000:]
+    assert f"replayed {len(kept) + len(seeds)} inputs" in out, out[-2000:]
+    assert "ERROR: AddressSanitizer" not in out and "runtime error" not in out
