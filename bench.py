@@ -100,7 +100,7 @@ def start_exporter(args, n_gpus: int, backend: str, port: int, pod_map: str, log
     if os.environ.get("GPUEXP_BENCH_FAIL_EXPORTER_WITH_COUNTERS") == "1" and args.counters:
         raise RuntimeError("exporter start failed on request (GPUEXP_BENCH_FAIL_EXPORTER_WITH_COUNTERS)")  # test hook
     t_start = time.perf_counter()
-    # A/B hook: start the exporter of another checkout (tools/devices_ab.sh runs an older
+    # A/B hook: start the exporter of another checkout (profiles/provenance/tools/devices_ab.sh ran an older
     # round's exporter under this bench's workload); never set in a measurement of this tree
     exp_root = os.environ.get("GPUEXP_BENCH_EXPORTER_ROOT") or ROOT
     proc = subprocess.Popen(cmd, env=env, stdout=logf, stderr=subprocess.STDOUT, cwd=exp_root)

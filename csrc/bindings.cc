@@ -762,6 +762,8 @@ PYBIND11_MODULE(_gpuexp, m) {
         d["last_tick_ns"] = s.last_tick_ns;
         d["max_tick_ns"] = s.max_tick_ns;
         d["tick_ns_total"] = s.tick_ns_total;
+        d["max_tick_cpu_ns"] = s.max_tick_cpu_ns;
+        d["tick_cpu_ns_total"] = s.tick_cpu_ns_total;
         d["render_bytes"] = s.render_bytes;
         d["series"] = s.series;
         d["device_errors"] = s.device_errors;
@@ -807,7 +809,7 @@ PYBIND11_MODULE(_gpuexp, m) {
         return e.set_prewake_mode(v);
       }, py::arg("mode"), "switch the HTTP workers' scrape pre-wake at run time (off|slices|spin)")
       .def_property_readonly("prewake_mode", [](const Engine& e) { return std::string(prewake_mode_name(e.prewake_mode())); })
-      .def("reset_tick_max", &Engine::reset_tick_max, "restart stats()['max_tick_ns'] (a measurement window)")
+      .def("reset_tick_max", &Engine::reset_tick_max, "restart stats()['max_tick_ns'] and ['max_tick_cpu_ns'] (a measurement window)")
       .def("source_status", &Engine::source_status)
       .def("set_pods", [](Engine& e, py::list pods, bool complete) {
         std::vector<PodMeta> v;

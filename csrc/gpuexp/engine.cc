@@ -708,6 +708,8 @@ void Engine::tick_locked(uint64_t now) {
     stats_.last_tick_ns = tend - ts[0];
     stats_.max_tick_ns = std::max(stats_.max_tick_ns, stats_.last_tick_ns);
     stats_.tick_ns_total += stats_.last_tick_ns;
+    stats_.max_tick_cpu_ns = std::max(stats_.max_tick_cpu_ns, cs[kStages] - cpu0);
+    stats_.tick_cpu_ns_total += cs[kStages] - cpu0;
     if (slot >= 0) {
       stats_.render_bytes = rbytes;
       stats_.series = nseries;

@@ -180,6 +180,9 @@ struct EngineStats {
   uint64_t last_tick_ns = 0;
   uint64_t max_tick_ns = 0;   // since start or the last reset_tick_max()
   uint64_t tick_ns_total = 0;  // wall time of every tick so far (mean = tick_ns_total / ticks)
+  // the sampler thread's own CPU per tick: the work a tick carries, whatever preempts it
+  uint64_t max_tick_cpu_ns = 0;   // since start or the last reset_tick_max()
+  uint64_t tick_cpu_ns_total = 0;
   uint64_t render_bytes = 0;
   uint64_t series = 0;
   uint64_t device_errors = 0;
@@ -214,6 +217,7 @@ class Engine {
   void reset_tick_max() {
     std::lock_guard<std::mutex> lk(stats_mu_);
     stats_.max_tick_ns = 0;
+    stats_.max_tick_cpu_ns = 0;
   }
   const HttpStats* http_stats() const { return http_ ? &http_->stats() : nullptr; }
   // Runtime pre-wake switch of the HTTP workers (PrewakeMode); false without an HTTP server.

@@ -13,7 +13,7 @@ def pytest_configure(config):
     # process ends up with one HIP runtime (see csrc/gpuexp/sentinel.hip factory comment).
     # Also initialise that runtime first when a GPU is present: measured on the box, HIP
     # initialised by our sentinel before torch (with amdsmi in the same process) makes
-    # the interpreter hang at exit; torch-first is clean (tools/probe_order.sh, D vs E).
+    # the interpreter hang at exit; torch-first is clean (profiles/provenance/tools/probe_order.sh, D vs E).
     try:
         import torch
         if torch.cuda.is_available():

@@ -891,8 +891,10 @@ def test_whole_process_cpu_8_gpus(native, tmp_path, hz, scrape, budget_pct):
     core (8 GPUs fetch every 5th tick at 10 Hz, each GPU at its own phase), PMC rounds at most
     every 50 ms, the sentinel at most every 0.5 s.  Targets: <= 1.3 % at 10 Hz and <= 4.0 % at
     100 Hz without a scraper; a Prometheus-style gzip scraper (another process, at the tick rate)
-    adds the HTTP worker and the spliced gzip copy.  At 10 Hz the longest tick is also at most
-    1.5x the mean (each GPU fetches at its own phase, so no tick carries all 8 fetches).
+    adds the HTTP worker and the spliced gzip copy.  At 10 Hz the heaviest tick is also at most
+    1.5x the mean (each GPU fetches at its own phase, so no tick carries all 8 fetches): the
+    sampler thread's CPU per tick, since a preempted tick's wall time measures the host, not the
+    work (one 383 us fake fetch took 4.4 ms of wall on a loaded 8-CPU container).
     profiles/r06/cpu_projection.txt.  A measurement over its budget is taken once more (a 4 s
     window on a shared host), and the better of the two counts."""
     import resource
@@ -932,10 +934,12 @@ def test_whole_process_cpu_8_gpus(native, tmp_path, hz, scrape, budget_pct):
         pct = 100.0 * cpu / (t1 - t0)
         ticks = st["ticks"] - s0["ticks"]
         mean_ns = (st["tick_ns_total"] - s0["tick_ns_total"]) / max(1, ticks)
+        mean_cpu_ns = (st["tick_cpu_ns_total"] - s0["tick_cpu_ns_total"]) / max(1, ticks)
         print(f"8 GPUs at {hz} Hz, scraper {scrape}: process CPU {pct:.2f} % of a core ({ticks} ticks, "
               f"{st['sampler_cpu_ns'] / max(1, st['ticks']) / 1e3:.0f} us sampler CPU per tick; tick wall "
-              f"mean {mean_ns / 1e3:.0f} us, max {st['max_tick_ns'] / 1e3:.0f} us)")
-        return pct, st["max_tick_ns"] / mean_ns
+              f"mean {mean_ns / 1e3:.0f} us, max {st['max_tick_ns'] / 1e3:.0f} us; tick CPU mean "
+              f"{mean_cpu_ns / 1e3:.0f} us, max {st['max_tick_cpu_ns'] / 1e3:.0f} us)")
+        return pct, st["max_tick_cpu_ns"] / mean_cpu_ns
 
     pct, lump = measure()
     if pct >= budget_pct or (hz == 10 and not scrape and lump > 1.5):

@@ -559,7 +559,7 @@ def test_pcie_bandwidth_under_host_to_device_copy(native):
     child streams pinned host memory to the GPU at a measured payload rate: link traffic is
     the payload plus protocol overhead and the reverse direction's requests (measured
     1.15-1.22x), so between 1.0x and 1.4x.  (Read as the kernel header's GB/s it was
-    ~9700x too high; tools/probe_pcie_units.py.)"""
+    ~9700x too high; profiles/provenance/tools/probe_pcie_units.py.)"""
     import json
     child = subprocess.Popen([sys.executable, "-c", _H2D], stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                              text=True)
