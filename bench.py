@@ -151,6 +151,9 @@ def prewake_summary(lat: list, prewoken: list, splits: list) -> dict | None:
     for name, flag in (("request_to_server_p50_us_prewoken", 1), ("request_to_server_p50_us_not_prewoken", 0)):
         v = [x[0] for x in splits if x[3] == flag]
         out[name] = round(statistics.median(v), 2) if v else None
+    if len(lat) <= 200:  # the driver's short runs: which scrapes, in order (1 pre-woken, 0 not, ? unknown)
+        out["sequence"] = "".join("1" if p == 1 else "0" if p == 0 else "?" for p in prewoken)
+        out["timed_scrape_us"] = [round(x, 1) for x in lat]
     return out
 
 

@@ -62,9 +62,11 @@ struct HttpConfig {
   //           arrival jitter) + the slices' few timer wake-ups.
   //           Round 6 A/B (profiles/r06/): spin alone (no slices around the window) reached
   //           86 % hits; slices 98.8 %.
-  // The default is chosen by an interleaved in-process A/B (bench.py --prewake-ab,
-  // profiles/r06/prewake_ab*).
-  int prewake_mode = 0;  // PrewakeMode
+  // The default, slices, is what an interleaved in-process A/B chose (bench.py --prewake-ab,
+  // 400 scrapes per arm, block bootstrap; profiles/r06/prewake_ab.md): socket_queue_to_parsed
+  // p50 20.1 -> 5.8 us at +0.023 pt exporter CPU, 98.8 % of scrapes pre-woken; spin's p50 was
+  // no better than slices' (CI of the difference spans 0) at twice the extra CPU.
+  int prewake_mode = 1;  // PrewakeMode (kPrewakeSlices)
   uint64_t prewake_lead_ns = 400000;       // slices: at least; twice the connection's period jitter,
   uint64_t prewake_max_lead_ns = 1500000;  // ... at most
   uint64_t prewake_step_ns = 150000;
@@ -187,7 +189,7 @@ class HttpServer {
   int bound_port_ = -1;
   std::atomic<bool> running_{false};
   std::atomic<bool> ready_{false};
-  std::atomic<int> prewake_mode_{0};
+  std::atomic<int> prewake_mode_{1};
   std::atomic<uint64_t> gzip_wanted_ns_{0};
   std::atomic<uint64_t> proto_wanted_ns_{0};
   // last gzip /metrics request from a connection without a steady period

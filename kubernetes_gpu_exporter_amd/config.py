@@ -23,9 +23,9 @@ class Config:
     path: str = "/metrics"                 # main.go:70
     http_threads: int = 1
     gzip: bool = True
-    http_prewake: str = "off"              # off | slices | spin (true = slices): have the HTTP worker awake
+    http_prewake: str = "slices"           # off | slices | spin (true = slices): have the HTTP worker awake
                                            # when a steady scraper's next request lands (HttpConfig, http.h);
-                                           # default chosen by bench.py --prewake-ab (profiles/r06/)
+                                           # default chosen by bench.py --prewake-ab (profiles/r06/prewake_ab.md)
     runtime_file: str = ""                 # YAML/JSON of run-time overrides, re-read on SIGUSR1 (http_prewake)
     stale_after: float = -1.0              # /readyz 503 when the newest sample is older (s); -1 = auto
                                            # (max(5 s, 10 intervals)), 0 = never

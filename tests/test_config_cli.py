@@ -156,7 +156,10 @@ def test_round4_keys_reach_the_engine(native):
 
 def test_round5_keys_reach_the_engine(native):
     ec = make_config({}).to_engine_config(native)
-    assert ec.exposition == "compiled" and ec.http.prewake is False  # profiles/r05/prewake_ab.txt
+    # pre-wake on (slices) since round 6's in-process A/B (profiles/r06/prewake_ab.md)
+    assert ec.exposition == "compiled" and ec.http.prewake is True and ec.http.prewake_mode == "slices"
+    c = load_config(["--http-prewake", "false"], env={"GPUEXP_EXPOSITION": "classic"})
+    assert c.to_engine_config(native).http.prewake is False
     c = load_config(["--http-prewake"], env={"GPUEXP_EXPOSITION": "classic"})
     ec = c.to_engine_config(native)
     assert ec.exposition == "classic" and ec.http.prewake is True

@@ -1127,10 +1127,14 @@ def test_gemm_pod_model_on_gpu(native):
 
 def test_raw_metrics_path_and_pmfw_coalescing(native):
     """The amdsmi backend reads gpu_metrics raw (no silent library fallback) and, at
-    100 Hz, learns the ~20 ms PMFW refresh and skips the SMU fetch in between."""
+    100 Hz, learns the ~20 ms PMFW refresh and skips the SMU fetch in between.  The CPU cap of
+    the auto fetch policy is off here (metrics_min_interval_s = 0): at round 6's 0.75 % budget
+    it alone would fetch every 4th 10 ms tick, and the refresh period is only learnt from
+    fresh reads on consecutive ticks (it read 0.0 in profiles/r06/session2/pytest_gpu.log)."""
     c = native.EngineConfig()
     c.backend = "amdsmi"
     c.interval_s = 0.01
+    c.metrics_min_interval_s = 0
     c.serve_http = False
     c.device_filter = [0]
     e = native.Engine(c)

@@ -457,7 +457,7 @@ def test_prewake_survives_one_late_scrape(native):
     c.interval_s = 0
     c.http.host = "127.0.0.1"
     c.http.port = 0
-    c.http.prewake = True  # (off by default)
+    c.http.prewake = True  # (the default since round 6: slices)
     e = native.Engine(c)
     e.start()
     try:
@@ -647,6 +647,8 @@ def test_prewake_mode_switches_at_run_time(native):
     c.interval_s = 0
     c.http.host = "127.0.0.1"
     c.http.port = 0
+    assert c.http.prewake_mode == "slices"  # the default (profiles/r06/prewake_ab.md)
+    c.http.prewake_mode = "off"
     e = native.Engine(c)
     e.start()
     try:

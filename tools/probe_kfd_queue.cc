@@ -145,8 +145,24 @@ int main() {
     std::printf("ring map failed\n");
     return 1;
   }
-  report("ring allocated + mapped");
+  // the queue's read / write dispatch ids and error-reason payload: inputs for an AQL queue
+  // (as ROCr passes its amd_queue_t fields), in a second GPU-mapped host page
+  void* ctl = nullptr;
+  if (hsaKmtAllocMemory(0, 4096, fl, &ctl) != HSAKMT_STATUS_SUCCESS || !ctl) {
+    std::printf("control page alloc failed\n");
+    return 1;
+  }
+  std::memset(ctl, 0, 4096);
+  HSAuint64 cva = 0;
+  if (hsaKmtMapMemoryToGPU(ctl, 4096, &cva) != HSAKMT_STATUS_SUCCESS) {
+    std::printf("control page map failed\n");
+    return 1;
+  }
+  report("ring + control page allocated + mapped");
   HsaQueueResource res{};
+  res.Queue_read_ptr_aql = static_cast<HSAuint64*>(ctl);
+  res.Queue_write_ptr_aql = static_cast<HSAuint64*>(ctl) + 8;  // own 64-byte line
+  res.ErrorReason = reinterpret_cast<volatile HSAint64*>(static_cast<HSAuint64*>(ctl) + 16);
   const HSAKMT_STATUS st = hsaKmtCreateQueue(HSAuint32(node), HSA_QUEUE_COMPUTE_AQL, 100, HSA_QUEUE_PRIORITY_NORMAL,
                                              ring, ring_bytes, nullptr, &res);
   std::printf("== hsaKmtCreateQueue: status %d\n", int(st));
@@ -155,6 +171,8 @@ int main() {
     hsaKmtDestroyQueue(res.QueueId);
     report("queue destroyed");
   }
+  hsaKmtUnmapMemoryToGPU(ctl);
+  hsaKmtFreeMemory(ctl, 4096);
   hsaKmtUnmapMemoryToGPU(ring);
   hsaKmtFreeMemory(ring, 4096);
   hsaKmtReleaseSystemProperties();
