@@ -103,7 +103,10 @@ def measure(native, n_gpus: int, hz: float, fetch_us: int, policy: str, budget: 
             "relayouts_per_tick": round((s1.get("relayouts", 0) - s0.get("relayouts", 0)) / ticks, 3),
             "code_builds": s1.get("code_builds", 0) - s0.get("code_builds", 0),
             "tick_wall_mean_us": round((s1.get("tick_ns_total", 0) - s0.get("tick_ns_total", 0)) / ticks / 1e3, 1),
-            "tick_wall_max_us": round(s1.get("max_tick_ns", 0) / 1e3, 1)}
+            "tick_wall_max_us": round(s1.get("max_tick_ns", 0) / 1e3, 1),
+            # the sampler thread's CPU per tick: the work a tick carries, whatever preempts it
+            "tick_cpu_mean_us": round((s1.get("tick_cpu_ns_total", 0) - s0.get("tick_cpu_ns_total", 0)) / ticks / 1e3, 1),
+            "tick_cpu_max_us": round(s1.get("max_tick_cpu_ns", 0) / 1e3, 1)}
 
 
 PKG_ROOT = ROOT
@@ -134,7 +137,7 @@ def main() -> int:
     print(f"# fake-host projection, full profile, 4 processes/GPU, budget {args.budget} % (auto policy), "
           f"PMC {args.pmc_us} us + sentinel {args.sentinel_us} us CPU per GPU per round / run")
     print(f"{'gpus':>4} {'hz':>5} {'fetch_us':>8} {'policy':>6} {'cpu_%':>7} {'sampler_us/tick':>15} "
-          f"{'tick_mean_us':>12} {'tick_max_us':>11}  exposition")
+          f"{'tick_mean_us':>12} {'tick_max_us':>11} {'cpu_mean_us':>11} {'cpu_max_us':>10}  exposition")
     for fetch in (int(x) for x in args.fetch_us.split(",")):
         for hz in (float(x) for x in args.hz.split(",")):
             for n in (int(x) for x in args.gpus.split(",")):
@@ -144,7 +147,8 @@ def main() -> int:
                                 args.pmc_us, args.sentinel_us)
                     print(f"{r['gpus']:>4} {r['hz']:>5g} {r['fetch_us']:>8} {r['policy']:>6} "
                           f"{r['process_cpu_pct']:>7.2f} {r['sampler_us_per_tick']:>15.1f} "
-                          f"{r['tick_wall_mean_us']:>12.1f} {r['tick_wall_max_us']:>11.1f}  "
+                          f"{r['tick_wall_mean_us']:>12.1f} {r['tick_wall_max_us']:>11.1f} "
+                          f"{r['tick_cpu_mean_us']:>11.1f} {r['tick_cpu_max_us']:>10.1f}  "
                           f"{expo} scrape={args.scrape}", flush=True)
                     if args.stages:
                         print("      stage us/tick: " + " ".join(f"{k}={v}" for k, v in r["stage_us_per_tick"].items())
