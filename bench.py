@@ -604,7 +604,7 @@ def main() -> int:
             if len(ab_blocks) % 10 == 1:  # progress (a long A/B must not look hung)
                 print(f"[bench] A/B block {len(ab_blocks)}/{len(ab_sched)}: {nxt}", file=sys.stderr, flush=True)
 
-    def step(cl, lat: list | None):
+    def step(cl, lat: list | None, after_scrape=None):
         t_start = time.perf_counter()
         if use_gpu:
             gemm_burst(iters)
@@ -632,6 +632,8 @@ def main() -> int:
                     if ab_state["next"] is None:  # block full: the next arm of the schedule
                         ab_state["next"] = ab_sched[len(ab_blocks)] if len(ab_blocks) < len(ab_sched) else None
                     ab_boundary()
+            if after_scrape is not None:
+                after_scrape()
         if dist is not None:
             dist.all_reduce(grad)
         sync()
@@ -748,15 +750,17 @@ def main() -> int:
     def phase(proc, cl, native_exporter: bool = False):
         """W untimed + K timed steps (barrier + synchronize on both sides); returns the
         latencies, exporter CPU% over the timed window and max-over-ranks ms/step."""
-        for w in range(args.warmup):
-            if ab_arms and native_exporter and rank == 0 and w == args.warmup - 1:
-                ab_state["next"] = ab_sched[0]  # the first block's arm, switched after this scrape
-            step(cl, None)
         x0 = None
-        if native_exporter and rank == 0 and use_gpu:
-            # xGMI accumulators at the start of the window (untimed), on a connection of its
-            # own: an extra request on the timed connection would break the steady scrape
-            # period the server learns per connection (pre-wake), as Prometheus never does
+
+        def window_start():
+            """xGMI accumulators and self counters at the start of the window (untimed), on a
+            connection of its own: an extra request on the timed connection would break the
+            steady scrape period the server learns per connection (pre-wake), as Prometheus
+            never does.  Runs inside the last warm-up step, right after its scrape, so its
+            time comes out of that step's idle rest: run between the steps it made the first
+            timed scrape late by the side scrape + parse, past the pre-wake window
+            (profiles/r06/session4: "0111...")."""
+            nonlocal x0
             side = n.ScrapeClient("127.0.0.1", port, "/metrics", args.gzip, 5000,
                                   promproto.ACCEPT if args.proto else "")
             side.scrape()
@@ -769,6 +773,14 @@ def main() -> int:
                 v = [x for _, _, x in promtext.samples(f0, name)]
                 if v:
                     counters0[name] = v[0]
+
+        capture = native_exporter and rank == 0  # (mock backends too: the CPU tests run this path)
+        for w in range(args.warmup):
+            if ab_arms and native_exporter and rank == 0 and w == args.warmup - 1:
+                ab_state["next"] = ab_sched[0]  # the first block's arm, switched after this scrape
+            step(cl, None, window_start if capture and w == args.warmup - 1 else None)
+        if capture and x0 is None:  # no warm-up
+            window_start()
         if dist is not None:
             dist.barrier()
         sync()
@@ -796,7 +808,7 @@ def main() -> int:
                                           if l.startswith("VmRSS:")][0].split()[1])
             except (OSError, IndexError, ValueError):
                 pass
-        if x0 is not None:
+        if x0 is not None and use_gpu:  # (mock links carry no all-reduce bytes)
             # xGMI bytes the hardware counted over the window vs what the DP all-reduce must
             # move: 2(N-1)/N x buffer per GPU per step for any bandwidth-optimal algorithm
             # (ring or direct); counters lag by <= one sample period (100 ms at 10 Hz).
