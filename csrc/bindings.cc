@@ -141,6 +141,14 @@ PYBIND11_MODULE(_gpuexp, m) {
   m.doc() = "MI355X per-pod GPU exporter: native telemetry core";
 
   m.def("mono_ns", &mono_ns);
+  m.def("timer_wakeup_cost", [](double hz, int n) {
+    uint64_t cpu = 0, late = 0;
+    {
+      py::gil_scoped_release rel;
+      timer_wakeup_cost(uint64_t(1e9 / hz), n, &cpu, &late);
+    }
+    return py::make_tuple(cpu, late);
+  }, py::arg("hz"), py::arg("n"), "(thread CPU ns per wake-up, mean lateness ns) of the sampler's timer wait");
   m.def("set_log_level", [](int lvl) { set_log_level(static_cast<LogLevel>(lvl)); });
   m.def("set_log_json", [](bool json) { set_log_json(json); });
   m.def("log", [](int lvl, const std::string& component, const std::string& msg) {
@@ -705,6 +713,8 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("fake_metrics_cost_us", &EngineConfig::fake_metrics_cost_us)
       .def_readwrite("fake_pmc_cost_us", &EngineConfig::fake_pmc_cost_us)
       .def_readwrite("fake_sentinel_cost_us", &EngineConfig::fake_sentinel_cost_us)
+      .def_readwrite("sampler_thread", &EngineConfig::sampler_thread)
+      .def_readwrite("process_min_interval_s", &EngineConfig::process_min_interval_s)
       .def_readwrite("sentinel_min_interval_s", &EngineConfig::sentinel_min_interval_s)
       .def_readwrite("counters_min_interval_s", &EngineConfig::counters_min_interval_s)
       .def_readwrite("queue_devices", &EngineConfig::queue_devices)

@@ -367,7 +367,8 @@ class AmdsmiBackend : public Backend {
     }
     uint64_t used = 0;
     const uint64_t v0 = out->time_parts ? mono_ns() : 0;
-    if (d.vram_used_file.read_u64(&used)) {
+    if (!out->read_memory) {
+    } else if (d.vram_used_file.read_u64(&used)) {
       out->vram_used = double(used);
     } else if (amdsmi_get_gpu_memory_usage(d.h, AMDSMI_MEM_TYPE_VRAM, &used) == AMDSMI_STATUS_SUCCESS) {
       out->vram_used = double(used);

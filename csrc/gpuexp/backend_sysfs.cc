@@ -314,7 +314,9 @@ void SysfsBackend::sample(const DeviceInfo& dev, DeviceSample* out) {
   if (!any) sample_fallback(d, out);
   uint64_t used = 0;
   const uint64_t v0 = out->time_parts ? mono_ns() : 0;
-  if (d.vram_used.read_u64(&used)) {
+  if (!out->read_memory) {
+    any = any || d.vram_used.is_open();
+  } else if (d.vram_used.read_u64(&used)) {
     out->vram_used = double(used);
     any = true;
   } else if (d.vram_used.open(d.dev_dir + "/mem_info_vram_used") && d.vram_used.read_u64(&used)) {

@@ -89,6 +89,7 @@ struct DeviceSample {
   // SMU round trip the kernel busy-waits on; ~0 when coalesced), the VRAM-used file, wall.
   uint64_t metrics_wall_ns = 0, metrics_cpu_ns = 0, vram_wall_ns = 0;
   bool time_parts = true;  // set by the engine: time the VRAM read (vram_wall_ns) on this tick
+  bool read_memory = true;  // set by the engine: read VRAM used on this tick (else left NaN)
 
   double gfx_activity = kNaN;  // %
   double umc_activity = kNaN;  // %

@@ -395,7 +395,7 @@ bool Engine::start(std::string* err) {
   }
   ok = true;
   running_.store(true);
-  if (cfg_.interval_s > 0) {
+  if (cfg_.interval_s > 0 && cfg_.sampler_thread) {
     stop_fd_ = ::eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
     sampler_ = std::thread([this] { run_sampler(); });
   }
@@ -455,6 +455,34 @@ void Engine::run_sampler() {
       tick_locked(mono_ns());
     }
   }
+  ::close(tfd);
+}
+
+void timer_wakeup_cost(uint64_t period_ns, int n, uint64_t* cpu_ns, uint64_t* late_ns) {
+  *cpu_ns = *late_ns = 0;
+  int tfd = ::timerfd_create(CLOCK_MONOTONIC, TFD_CLOEXEC);
+  if (tfd < 0 || n <= 0) {
+    if (tfd >= 0) ::close(tfd);
+    return;
+  }
+  itimerspec its{};
+  its.it_interval.tv_sec = time_t(period_ns / 1000000000ull);
+  its.it_interval.tv_nsec = long(period_ns % 1000000000ull);
+  its.it_value = its.it_interval;
+  uint64_t due = mono_ns() + period_ns;
+  ::timerfd_settime(tfd, 0, &its, nullptr);
+  pollfd fd{tfd, POLLIN, 0};
+  const uint64_t c0 = thread_cpu_ns();
+  for (int i = 0; i < n; ++i) {  // the sampler's own wait (run_sampler), with no tick in between
+    if (::poll(&fd, 1, -1) < 0) continue;
+    uint64_t exp = 0;
+    if (::read(tfd, &exp, sizeof(exp)) != sizeof(exp)) continue;
+    const uint64_t t = mono_ns();
+    *late_ns += t > due ? t - due : 0;
+    due += (exp ? exp : 1) * period_ns;
+  }
+  *cpu_ns = (thread_cpu_ns() - c0) / uint64_t(n);
+  *late_ns /= uint64_t(n);
   ::close(tfd);
 }
 
@@ -573,8 +601,14 @@ void Engine::tick_locked(uint64_t now) {
   }
   part[1] = mono_ns() - c0;
 
+  // The memory reads -- per-process VRAM (KFD / amdsmi list) and each GPU's VRAM / GTT used --
+  // run at most every process_min_interval_s; a tick in between exports the last values again.
+  const bool procs_due = !period_ns || !procs_read_ns_ || now < procs_read_ns_ || per_dev_.size() != devices_.size() ||
+                         now - procs_read_ns_ + period_ns / 2 >= uint64_t(cfg_.process_min_interval_s * 1e9);
+  if (procs_due) procs_read_ns_ = now;
+
   // 0: device telemetry (engine_device.cc)
-  const uint64_t errs = sample_devices(now, split_cpu, part);
+  const uint64_t errs = sample_devices(now, split_cpu, procs_due, part);
   if (counters_ && kick_late && counters_due(now)) {
     counters_kick_ns_ = now;
     round = true;
@@ -589,9 +623,11 @@ void Engine::tick_locked(uint64_t now) {
   // 1: processes
   // (reused across ticks: the lists keep their capacity, no allocation per tick)
   std::vector<std::vector<ProcSample>>& per_dev = per_dev_;
-  per_dev.resize(devices_.size());
-  for (auto& l : per_dev) l.clear();
-  if (cfg_.process_source != "none") {
+  if (procs_due) {
+    per_dev.resize(devices_.size());
+    for (auto& l : per_dev) l.clear();
+  }
+  if (procs_due && cfg_.process_source != "none") {
     bool from_backend = cfg_.process_source != "kfd";
     if (from_backend)
       for (size_t i = 0; i < devices_.size(); ++i)

@@ -64,6 +64,11 @@ class ForkJoinPool {
   bool quit_ = false;
 };
 
+// Thread CPU (ns) the host charges for one timer wake-up of the sampler's own wait (timerfd +
+// poll, no work in between), and the mean lateness of the wake-ups: n periods of period_ns.  A
+// host property, not the exporter's: tests/test_fakehost.py charges an MI355X host's figure.
+void timer_wakeup_cost(uint64_t period_ns, int n, uint64_t* cpu_ns, uint64_t* late_ns);
+
 struct EngineConfig {
   std::string backend = "mock";        // mock | sysfs | amdsmi
   int device_threads = 0;              // 0 = auto (serial), N > 1 = a pool of N reader threads
@@ -71,6 +76,9 @@ struct EngineConfig {
   std::string mock_xgmi_file;          // mock only: per-peer traffic matrix (MockBackend::set_traffic_file)
   std::string host_root;               // "" == "/"
   double interval_s = 1.0;             // 0 = manual ticks only (tests)
+  // false: no sampler thread although interval_s > 0 -- the caller ticks (tick_now) on its own
+  // clock, with every interval-derived policy as the sampler would have it (tools/tickbench.py)
+  bool sampler_thread = true;
   bool serve_http = true;
   HttpConfig http;
   std::string series_profile = "standard";  // standard | full | compact | legacy
@@ -103,6 +111,11 @@ struct EngineConfig {
   // KFD proc directory listed at least this often (and on its mtime moving, or a tracked
   // process vanishing); tracked processes' VRAM is read every tick either way (0 = list every tick)
   double kfd_rescan_interval_s = 0.5;
+  // The per-process reads (KFD VRAM per process and GPU, or amdsmi's process list) run at most
+  // this often; a tick in between exports the last lists again (0 = every tick).  Per-process
+  // VRAM does not need a 100 Hz tick, and at 8 GPUs x 4 processes these reads were the
+  // sampler's largest stage after the SMU fetch (tools/tickbench.py).  At <= 20 Hz: every tick.
+  double process_min_interval_s = 0.05;
   bool exclude_self = true;
   bool enable_sentinel = false;
   std::string sentinel_impl = "auto";  // auto (PMC queue if the aqlprofile counters run, else HIP) | hip | queue
@@ -261,6 +274,7 @@ class Engine {
     // Last residency-derived values: the PMFW accumulates them at its own rate (slower
     // than a 100 Hz tick), so a tick without a new accumulation re-exports these instead
     // of dropping the series.
+    double vram_last = kNaN, gtt_last = kNaN;  // the last VRAM / GTT used read (process_min_interval_s)
     double thr_last[5] = {kNaN, kNaN, kNaN, kNaN, kNaN};
     double xcc_last[kMaxXcc] = {kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN, kNaN};
     double mfma_last = kNaN;  // this tick's amd_gpu_mfma_busy_percent (NaN: no counter window)
@@ -335,7 +349,7 @@ class Engine {
   void run_sampler();
   void tick_locked(uint64_t now_ns);
   // engine_device.cc
-  uint64_t sample_devices(uint64_t now, bool split_cpu, uint64_t* part);  // returns failed reads
+  uint64_t sample_devices(uint64_t now, bool split_cpu, bool memory_due, uint64_t* part);  // returns failed reads
   void update_fetch_policy(uint64_t now);
   void collect_device(int i, uint64_t gen, double dt_s);
   void collect_counters(int i, uint64_t gen, double dt_s);
@@ -426,6 +440,7 @@ class Engine {
   uint64_t counters_cpu_seen_ = 0, pool_cpu_seen_ = 0, sampler_cpu_seen_ = 0;  // ticks whose counter read missed counters_sync_us (sampler thread)
   std::string counters_kick_mode_ = "start";
   uint64_t sentinel_last_ns_ = 0;  // tick time of the last sentinel run (sentinel_min_interval_s)
+  uint64_t procs_read_ns_ = 0;  // tick time of the last per-process read (process_min_interval_s)
   uint64_t counters_kick_ns_ = 0;  // tick time the last PMC read round was for (counters_min_interval_s)
   bool counters_round_next_ = false;  // "end" kick: the next tick has a round to sync  // cfg_.counters_kick with "auto" resolved
   std::string sentinel_status_ = "disabled", counters_status_ = "disabled";

@@ -180,8 +180,8 @@ void Engine::dput(DevState& st, int dev, Fam f, int k, std::initializer_list<con
 // Stage 0 of a tick: every GPU's telemetry read (fanned out over the pool when there is one;
 // each read touches only its own DevState and backend device slot), then the fetch policy.
 // part[2..5]: gpu_metrics / VRAM / RAS / GTT time (the last three sampled with split_cpu).
-uint64_t Engine::sample_devices(uint64_t now, bool split_cpu, uint64_t* part) {
-  auto sample_one = [this, now, split_cpu](int i) {
+uint64_t Engine::sample_devices(uint64_t now, bool split_cpu, bool memory_due, uint64_t* part) {
+  auto sample_one = [this, now, split_cpu, memory_due](int i) {
     DevState& st = dstate_[size_t(i)];
     if (st.cur.ok) {
       st.prev = st.cur;
@@ -190,7 +190,10 @@ uint64_t Engine::sample_devices(uint64_t now, bool split_cpu, uint64_t* part) {
     st.cur = DeviceSample();
     st.cur.host_ns = now;
     st.cur.time_parts = split_cpu;
+    st.cur.read_memory = memory_due || std::isnan(st.vram_last);
     backend_->sample(devices_[size_t(i)], &st.cur);
+    if (st.cur.read_memory) st.vram_last = st.cur.vram_used;
+    else st.cur.vram_used = st.vram_last;  // (between process_min_interval_s reads: the last one)
     (st.cur.metrics_coalesced ? metrics_coalesced_ : metrics_fresh_)[size_t(i)] += 1;
     if (st.cur.ok && !st.cur.metrics_coalesced) st.metrics_fresh_ns = now;
     st.ras_ns = st.gtt_ns = 0;
@@ -215,7 +218,8 @@ uint64_t Engine::sample_devices(uint64_t now, bool split_cpu, uint64_t* part) {
     if (!gtt_used_f_.empty()) {
       const uint64_t g0 = split_cpu ? mono_ns() : 0;
       uint64_t v = 0;
-      if (gtt_used_f_[size_t(i)].read_u64(&v)) st.cur.gtt_used = double(v);
+      if (!st.cur.read_memory) st.cur.gtt_used = st.gtt_last;
+      else if (gtt_used_f_[size_t(i)].read_u64(&v)) st.cur.gtt_used = st.gtt_last = double(v);
       st.cur.gtt_total = gtt_total_[size_t(i)];
       if (split_cpu) st.gtt_ns = mono_ns() - g0;
     }

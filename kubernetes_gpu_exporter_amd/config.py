@@ -51,6 +51,8 @@ class Config:
     kfd_sdma_activity: bool = False        # KFD sdma_<id> per process: not SDMA time on MI355X (profiles/r04)
     kfd_detail_interval: float = 1.0       # seconds between cu_occupancy / sdma re-reads (0 = every tick)
     kfd_rescan_interval: float = 0.5       # KFD proc directory listed at least this often (also on change)
+    process_min_interval: float = 0.05     # per-process reads (KFD VRAM / amdsmi list) at most this often (s;
+                                           # 0 = every tick): a 100 Hz tick re-exports the last lists in between
     gc_after: int = 1
     exposition: str = "compiled"           # compiled (fixed-layout body, values patched in place, gzip from
                                            # pre-encoded static bits) | classic (re-render + compress)
@@ -167,6 +169,7 @@ class Config:
         ec.kfd_sdma = bool(self.kfd_sdma_activity)
         ec.kfd_detail_interval_s = float(self.kfd_detail_interval)
         ec.kfd_rescan_interval_s = float(self.kfd_rescan_interval)
+        ec.process_min_interval_s = float(self.process_min_interval)
         ec.enable_sentinel = bool(self.enable_sentinel)
         ec.sentinel_spin = int(self.sentinel_spin)
         ec.sentinel_impl = str(self.sentinel_impl)
@@ -333,6 +336,8 @@ def validate(cfg: Config) -> None:
         raise ValueError("state_interval must be > 0")
     if cfg.pod_totals_ttl <= 0:
         raise ValueError("pod_totals_ttl must be > 0")
+    if cfg.process_min_interval < 0:
+        raise ValueError("process_min_interval must be >= 0 seconds")
     if cfg.ras_interval <= 0:
         raise ValueError("ras_interval must be > 0")
     if cfg.process_source not in ("auto", "kfd", "amdsmi", "none"):

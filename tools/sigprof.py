@@ -140,6 +140,10 @@ def main() -> int:
     ap.add_argument("--gzip", action="store_true", help="serve HTTP with a 100 Hz gzip scraper (another process)")
     ap.add_argument("--exposition", default="compiled")
     ap.add_argument("--lines", default="", help="also print the source lines of leaf samples in this function")
+    ap.add_argument("--tick-hz", type=float, default=0,
+                    help="fake node: run the engine's interval policies for this tick rate (no sampler "
+                         "thread; the SMU fetch, PMC reads and sentinel burn their silicon CPU, as in "
+                         "tools/tickbench.py); 0 = every source every tick, no fetch cost")
     ap.add_argument("--backend", default="sysfs",
                     help="sysfs: the fake node; amdsmi: GPU 0 of this host, with sentinel and PMC counters "
                          "(a GPU box; the SMU fetch is then real)")
@@ -164,6 +168,12 @@ def main() -> int:
         c.backend = "sysfs"
         c.host_root = root
     c.interval_s = 0
+    if args.tick_hz and not real:
+        c.interval_s = 1.0 / args.tick_hz
+        c.sampler_thread = False
+        c.enable_counters = c.enable_sentinel = True
+        c.fake_pmc_cost_us = tf.PMC_READ_CPU_US
+        c.fake_sentinel_cost_us = tf.SENTINEL_RUN_CPU_US
     c.serve_http = args.gzip
     if args.gzip:
         h = c.http
@@ -173,7 +183,7 @@ def main() -> int:
     c.series_profile = "full"
     c.exposition = args.exposition
     if not real:
-        c.fake_metrics_cost_us = 0
+        c.fake_metrics_cost_us = tf.SMU_FETCH_CPU_US if args.tick_hz else 0
     e = native.Engine(c)
     e.start()
     scraper = None
@@ -183,9 +193,11 @@ def main() -> int:
         time.sleep(1.0)
     now = 1_000_000_000
 
+    step = int(1e9 / args.tick_hz) if args.tick_hz else 10_000_000
+
     def tick():  # a real device ticks on the real clock (the sentinel's and counters' domain)
         nonlocal now
-        now += 10_000_000
+        now += step
         e.tick() if real else e.tick(now)
 
     for _ in range(200 if not real else 20):
