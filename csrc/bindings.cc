@@ -774,6 +774,7 @@ PYBIND11_MODULE(_gpuexp, m) {
         d["tick_ns_total"] = s.tick_ns_total;
         d["max_tick_cpu_ns"] = s.max_tick_cpu_ns;
         d["tick_cpu_ns_total"] = s.tick_cpu_ns_total;
+        d["fake_cpu_burnt_ns"] = fake_cpu_burnt_ns().load();  // (process-wide: the fake sources' stand-ins)
         d["render_bytes"] = s.render_bytes;
         d["series"] = s.series;
         d["device_errors"] = s.device_errors;

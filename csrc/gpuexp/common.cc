@@ -14,6 +14,11 @@ namespace gpuexp {
 
 void set_thread_name(const char* name) { ::prctl(PR_SET_NAME, name, 0, 0, 0); }
 
+std::atomic<uint64_t>& fake_cpu_burnt_ns() {
+  static std::atomic<uint64_t> total{0};
+  return total;
+}
+
 static std::atomic<int> g_log_level{static_cast<int>(LogLevel::kWarn)};
 static std::atomic<bool> g_log_json{false};
 static std::mutex g_log_mu;

@@ -12,6 +12,7 @@
 #include <ctime>
 #include <limits>
 #include <string>
+#include <atomic>
 #include <vector>
 
 namespace gpuexp {
@@ -29,6 +30,11 @@ inline uint64_t thread_cpu_ns() {
   clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
   return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
 }
+
+// Tests / projections only: thread CPU burnt so far by the fake sources' stand-ins for silicon
+// costs (a fresh SMU fetch, a PMC read round, a sentinel run; fake_metrics_cost_us and
+// fake_{pmc,sentinel}_cost_us), so a projection can tell the exporter's own work from them.
+std::atomic<uint64_t>& fake_cpu_burnt_ns();
 
 // Names the calling thread (/proc/<pid>/task/<tid>/comm, 15 chars): the exporter's threads
 // are gpuexp-sampler, gpuexp-dev (per-GPU read pool), gpuexp-http, gpuexp-pmc, so their CPU

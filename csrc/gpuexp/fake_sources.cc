@@ -17,8 +17,10 @@ namespace {
 void burn_cpu_us(uint64_t us) {
   if (!us) return;
   const uint64_t c0 = thread_cpu_ns();
-  while (thread_cpu_ns() - c0 < us * 1000) {
+  uint64_t c = c0;
+  while ((c = thread_cpu_ns()) - c0 < us * 1000) {
   }
+  fake_cpu_burnt_ns().fetch_add(c - c0, std::memory_order_relaxed);
 }
 
 // A fake GPU's read path that costs host CPU like an HSA queue's: writing the AQL packet and

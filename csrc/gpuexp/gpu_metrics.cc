@@ -165,9 +165,12 @@ bool GpuMetricsReader::read(DeviceSample* out, uint64_t now_ns) {
   }
   const uint64_t w0 = mono_ns(), c0 = thread_cpu_ns();
   long n = pread_once(fd_, reinterpret_cast<char*>(buf_), sizeof(buf_));
-  if (fake_cost_ns_)
-    while (thread_cpu_ns() - c0 < fake_cost_ns_) {
+  if (fake_cost_ns_) {
+    uint64_t c = c0;
+    while ((c = thread_cpu_ns()) - c0 < fake_cost_ns_) {
     }
+    fake_cpu_burnt_ns().fetch_add(c - c0, std::memory_order_relaxed);
+  }
   out->metrics_cpu_ns = thread_cpu_ns() - c0;
   out->metrics_wall_ns = mono_ns() - w0;
   if (n <= 0) {

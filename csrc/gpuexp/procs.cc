@@ -175,7 +175,13 @@ int KfdProcReader::emit(Entry& e, int pid, std::vector<std::vector<ProcSample>>*
         if (pd.evicted.is_open() && (n = pd.evicted.read(buf, sizeof(buf) - 1)) > 0 &&
             parse_u64(buf, size_t(n), &v))
           pd.evicted_last = double(v);
-        pd.detail_ns = now_ns;
+        // After the first read, each (process, GPU) keeps its own phase of detail_every_ns_:
+        // processes found by one listing would otherwise read their details on the same tick
+        // forever (64 more reads every 10th tick at 8 GPUs x 4 processes and 10 Hz).
+        const uint64_t phase = pd.detail_read || !now_ns || detail_every_ns_ == 0
+                                   ? 0
+                                   : ((e.id * 0x9E3779B97F4A7C15ull + uint64_t(pd.dev)) >> 20) % detail_every_ns_;
+        pd.detail_ns = now_ns >= phase ? now_ns - phase : now_ns;
         pd.detail_read = true;
       }
       ps.cu_occupancy = pd.cu_last;
