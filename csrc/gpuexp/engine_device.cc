@@ -201,7 +201,11 @@ uint64_t Engine::sample_devices(uint64_t now, bool split_cpu, bool memory_due, u
       const uint64_t r0 = split_cpu ? mono_ns() : 0;
       if (now >= ras_next_ns_[size_t(i)]) {
         ras_[size_t(i)].read(&ras_cache_[size_t(i)]);
-        ras_next_ns_[size_t(i)] = now + uint64_t(cfg_.ras_interval_s * 1e9);
+        // every GPU reads at the first tick; after that each keeps its own phase of the interval,
+        // so no later tick carries all GPUs' RAS / AER / bad-page files
+        const uint64_t iv = uint64_t(cfg_.ras_interval_s * 1e9);
+        const uint64_t phase = ras_next_ns_[size_t(i)] == 0 ? iv * uint64_t(i) / devices_.size() : 0;
+        ras_next_ns_[size_t(i)] = now + iv + phase;
       }
       const RasTotals& r = ras_cache_[size_t(i)];
       st.cur.ecc_ce = r.ecc_ce;

@@ -34,7 +34,18 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
   // keeps attributes), at least every rescan_ns, and whenever a tracked process vanished;
   // in between, read the tracked processes' files only (an exited process's reads fail).
   struct stat sb {};
-  if (dir_fd_ < 0) dir_fd_ = ::open(base.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+  if (dir_fd_ < 0) {
+    // no KFD proc directory (a node without the driver, the mock): a failed open is retried at
+    // the rescan interval, not every tick
+    if (open_tried_ns_ && now_ns && rescan_ns_ && now_ns >= open_tried_ns_ && now_ns - open_tried_ns_ < rescan_ns_)
+      return;
+    dir_fd_ = ::open(base.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+    open_tried_ns_ = dir_fd_ < 0 ? now_ns : 0;
+    if (dir_fd_ < 0 && now_ns && rescan_ns_) {
+      pids_.clear();  // (the directory went away: nothing tracked is readable)
+      return;
+    }
+  }
   bool have_mtime = dir_fd_ >= 0 && ::fstat(dir_fd_, &sb) == 0;
   if (have_mtime && sb.st_nlink == 0) {  // the directory itself was removed (KFD reloaded): reopen
     ::close(dir_fd_);

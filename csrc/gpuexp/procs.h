@@ -72,6 +72,7 @@ class KfdProcReader {
   bool relist_ = false;          // a tracked process vanished: list at the next scan
   timespec mtime_{};             // the directory's mtime at the last look
   int dir_fd_ = -1;              // the KFD proc directory, kept open: fstat per scan, no path walk
+  uint64_t open_tried_ns_ = 0;   // last failed open of it (no KFD): retried at the rescan interval
   uint64_t scan_no_ = 0, lists_ = 0, next_id_ = 0, dir_reopens_ = 0;
   std::unordered_map<int, Entry> pids_;
 };

@@ -880,13 +880,24 @@ def test_sampler_cpu_account_matches_thread_clocks(native, tmp_path):
 
 
 # The CPU one timer wake-up costs a thread on an MI355X host (AMD EPYC 9575F, bare metal):
-# 5.5 us at 100 Hz, 9.9 us at 10 Hz (tools/wakecost.py, profiles/r06/session5/wakecost.txt).
+# 5.5 us at 100 Hz, 9.9 us at 10 Hz (tools/wakecost.py, profiles/r06/session5/wakecost.txt);
+# 16-47 us on a busier box (session6/).
 # A host that charges far more than that (this repo's build container, an overcommitted VM:
 # 60-110 us per wake-up, 160-450 us late, and 3x slower on the exporter's own code,
 # profiles/r06/host_cpu.md) measures the VM, not the exporter, against the node budgets below.
 MI355X_HOST_WAKE_US = 9.9
-BUDGET_HOST_MAX_WAKE_US = 20.0
+BUDGET_HOST_MAX_WAKE_US = 50.0  # (the most an MI355X box has charged: 47 us, profiles/r06/session6/wakecost.txt)
 CPU_BUDGETS_8_GPUS = [(10, None, 1.3), (100, None, 4.0), (10, "gzip", 1.5), (100, "gzip", 5.5)]
+
+
+def _under_hypervisor() -> bool:
+    """The CPU flags say this kernel runs in a VM (an MI355X node is bare metal; the build
+    container is a VM whose CPU accounting charges the hypervisor's work to the guest's threads)."""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            return any(l.startswith("flags") and " hypervisor" in l for l in fh)
+    except OSError:
+        return False
 
 
 def _whole_process_cpu_8_gpus(native, tmp_path, hz, scrape):
@@ -962,9 +973,9 @@ def test_whole_process_cpu_8_gpus(native, tmp_path, hz, scrape, budget_pct):
     wall time measures the host, not the work.  A measurement over its budget is taken once more
     (a 4 s window on a shared host), and the better of the two counts.
 
-    The budgets are MI355X-node CPU, so they are asserted where the host's own cost of a timer
-    wake-up is an MI355X host's (<= BUDGET_HOST_MAX_WAKE_US; measured first, with the sampler's
-    own timerfd wait).  The gpu tier runs the same check on the MI355X host's CPU unconditionally
+    The budgets are MI355X-node CPU, so they are asserted on a bare-metal host whose own cost of
+    a timer wake-up is an MI355X host's (<= BUDGET_HOST_MAX_WAKE_US; measured first, with the
+    sampler's own timerfd wait).  The gpu tier runs the same check on the MI355X host's CPU unconditionally
     (test_whole_process_cpu_8_gpus_mi355x_host), and profiles/r06/session5/cpu_projection.txt
     is that host's projection: 1.04 % at 10 Hz, 1.43 % at 100 Hz.  The 10 Hz heaviest-tick ratio
     is host-independent and asserted everywhere."""
@@ -972,10 +983,11 @@ def test_whole_process_cpu_8_gpus(native, tmp_path, hz, scrape, budget_pct):
     pct, lump = _check_cpu_budget_8_gpus(native, tmp_path, hz, scrape, budget_pct)
     if hz == 10 and not scrape:
         assert lump <= 1.5, lump
-    if wake_ns / 1e3 > BUDGET_HOST_MAX_WAKE_US:
-        pytest.skip(f"this host charges {wake_ns / 1e3:.0f} us of thread CPU per timer wake-up ({late_ns / 1e3:.0f} us "
-                    f"late; an MI355X host: {MI355X_HOST_WAKE_US} us): {pct:.2f} % here is not MI355X-node CPU; the "
-                    f"gpu tier asserts the {budget_pct} % budget on the MI355X host")
+    if wake_ns / 1e3 > BUDGET_HOST_MAX_WAKE_US or _under_hypervisor():
+        pytest.skip(f"this host {'runs under a hypervisor and ' if _under_hypervisor() else ''}charges "
+                    f"{wake_ns / 1e3:.0f} us of thread CPU per timer wake-up ({late_ns / 1e3:.0f} us late; an MI355X "
+                    f"host: {MI355X_HOST_WAKE_US} us): {pct:.2f} % here is not MI355X-node CPU; the gpu tier asserts "
+                    f"the {budget_pct} % budget on the MI355X host")
     assert pct < budget_pct, pct
 
 

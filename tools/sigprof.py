@@ -145,7 +145,8 @@ def main() -> int:
                          "thread; the SMU fetch, PMC reads and sentinel burn their silicon CPU, as in "
                          "tools/tickbench.py); 0 = every source every tick, no fetch cost")
     ap.add_argument("--backend", default="sysfs",
-                    help="sysfs: the fake node; amdsmi: GPU 0 of this host, with sentinel and PMC counters "
+                    help="sysfs: the fake node; mock: simulated devices whose values change every tick; amdsmi: GPU 0 "
+                         "of this host, with sentinel and PMC counters "
                          "(a GPU box; the SMU fetch is then real)")
     args = ap.parse_args()
     lib = ctypes.CDLL(build_lib())
@@ -161,6 +162,10 @@ def main() -> int:
         c.enable_counters = True
         c.counters_plugin = rocprof_plugin_path("aqlpmc")
         args.gpus = 1
+    elif args.backend == "mock":  # simulated telemetry that changes every tick (the fake node's is static)
+        import test_fakehost as tf
+        c.backend = "mock"
+        c.mock_devices = args.gpus
     else:
         import test_fakehost as tf
         root = tempfile.mkdtemp(prefix="gpuexp-prof-")
