@@ -122,8 +122,12 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
       probe_devs(pdir, &e);
       std::string comm;
       if (read_small_file(root_ + "/proc/" + name + "/comm", &comm, 64)) e.comm = trim(comm);
-      e.probe_ns = now_ns;
       e.id = ++next_id_;
+      // each process at its own phase of the re-probe period: processes one listing found
+      // would otherwise list their directories on the same tick every few seconds (32 listings
+      // on one tick at 8 GPUs x 4 processes, the heaviest tick of a 10 Hz sampler)
+      const uint64_t phase = (e.id * 0x9E3779B97F4A7C15ull >> 24) % kReprobeNs;
+      e.probe_ns = now_ns > phase ? now_ns - phase : now_ns;
       return pids_.insert_or_assign(pid, std::move(e)).first;
     };
     auto it = pids_.find(pid);
