@@ -775,6 +775,11 @@ PYBIND11_MODULE(_gpuexp, m) {
         d["max_tick_cpu_ns"] = s.max_tick_cpu_ns;
         d["tick_cpu_ns_total"] = s.tick_cpu_ns_total;
         d["fake_cpu_burnt_ns"] = fake_cpu_burnt_ns().load();  // (process-wide: the fake sources' stand-ins)
+        d["fresh_reads"] = s.fresh_reads;
+        d["last_tick_fresh"] = s.last_tick_fresh;
+        d["sentinel_runs"] = s.sentinel_runs;
+        d["kfd_lists"] = s.kfd_lists;
+        d["leveled_ticks"] = s.leveled_ticks;
         d["render_bytes"] = s.render_bytes;
         d["series"] = s.series;
         d["device_errors"] = s.device_errors;

@@ -609,6 +609,16 @@ void Engine::tick_locked(uint64_t now) {
 
   // 0: device telemetry (engine_device.cc)
   const uint64_t errs = sample_devices(now, split_cpu, procs_due, part);
+  // Tick leveling: with the SMU fetches phased over k ticks (update_fetch_policy), a tick that
+  // carries two or more of them defers the periodic extras whose timers came due -- the
+  // sentinel run and the KFD rescan listing -- to a lighter tick (at most to twice their
+  // interval).  Once run there they stay there: their timers count from the actual run.  At
+  // 8 GPUs and 10 Hz the fetches come 2,2,1,2,1 per tick and these extras had a 0.5 s period
+  // too, so without it they kept landing on a two-fetch tick (the heaviest tick ~1.5x the mean).
+  int fresh_now = 0;
+  for (const DevState& st : dstate_) fresh_now += st.cur.ok && !st.cur.metrics_coalesced;
+  leveled_ = false;
+  const bool heavy_tick = fresh_now >= 2 && fresh_now < int(dstate_.size());  // (all fresh: no lighter tick)
   if (counters_ && kick_late && counters_due(now)) {
     counters_kick_ns_ = now;
     round = true;
@@ -636,7 +646,9 @@ void Engine::tick_locked(uint64_t now) {
           break;
         }
     if (!from_backend) {
-      kfd_->scan(devices_, &per_dev, now);
+      const uint64_t lists0 = kfd_->lists();
+      kfd_->scan(devices_, &per_dev, now, heavy_tick);
+      if (heavy_tick && kfd_->lists() == lists0 && kfd_->listing_deferred()) leveled_ = true;
     } else if (cfg_.exclude_self) {
       for (auto& l : per_dev)
         l.erase(std::remove_if(l.begin(), l.end(), [this](const ProcSample& p) { return p.pid == self_pid_; }),
@@ -652,11 +664,15 @@ void Engine::tick_locked(uint64_t now) {
   cs[3] = cpu_mark();
 
   // 3: sentinel (drain previous run, launch next; never blocks on the GPU)
+  const uint64_t sen_iv = uint64_t(cfg_.sentinel_min_interval_s * 1e9);
   if (sentinel_ && (cfg_.interval_s <= 0 || !sentinel_last_ns_ || now < sentinel_last_ns_ ||
-                    now - sentinel_last_ns_ + uint64_t(cfg_.interval_s * 5e8) >=
-                        uint64_t(cfg_.sentinel_min_interval_s * 1e9))) {
+                    (now - sentinel_last_ns_ + uint64_t(cfg_.interval_s * 5e8) >= sen_iv &&
+                     !(heavy_tick && now - sentinel_last_ns_ < 2 * sen_iv)))) {
     sentinel_->tick(now);  // at most every sentinel_min_interval_s (half a tick of slack)
     sentinel_last_ns_ = now;
+    ++sentinel_runs_;
+  } else if (sentinel_ && heavy_tick && now - sentinel_last_ns_ + uint64_t(cfg_.interval_s * 5e8) >= sen_iv) {
+    leveled_ = true;
   }
   if (kfd_events_) count_kfd_events();
   ts[4] = mono_ns();
@@ -740,6 +756,11 @@ void Engine::tick_locked(uint64_t now) {
   {
     std::lock_guard<std::mutex> lk(stats_mu_);
     stats_.ticks += 1;
+    stats_.fresh_reads += uint64_t(fresh_now);
+    stats_.last_tick_fresh = uint64_t(fresh_now);
+    stats_.sentinel_runs = sentinel_runs_;
+    stats_.kfd_lists = kfd_ ? kfd_->lists() : 0;
+    stats_.leveled_ticks += leveled_ ? 1 : 0;
     if (slot < 0) stats_.publish_skipped += 1;
     stats_.last_tick_ns = tend - ts[0];
     stats_.max_tick_ns = std::max(stats_.max_tick_ns, stats_.last_tick_ns);

@@ -207,6 +207,10 @@ struct EngineStats {
   uint64_t code_builds = 0; // compiled exposition: Huffman code builds
   uint64_t families_skipped = 0;  // compiled exposition: families passed over unchanged (cumulative)
   uint64_t families_rendered = 0; // ... and families walked (cumulative)
+  // tick leveling (engine.cc): fresh gpu_metrics reads, sentinel runs and KFD listings so far,
+  // and ticks that deferred one of the last two because they carried >= 2 SMU fetches
+  uint64_t fresh_reads = 0, sentinel_runs = 0, kfd_lists = 0, leveled_ticks = 0;
+  uint64_t last_tick_fresh = 0;  // SMU fetches the last tick carried
 };
 
 class Engine {
@@ -440,6 +444,8 @@ class Engine {
   uint64_t counters_cpu_seen_ = 0, pool_cpu_seen_ = 0, sampler_cpu_seen_ = 0;  // ticks whose counter read missed counters_sync_us (sampler thread)
   std::string counters_kick_mode_ = "start";
   uint64_t sentinel_last_ns_ = 0;  // tick time of the last sentinel run (sentinel_min_interval_s)
+  uint64_t sentinel_runs_ = 0;  // ticks that ran the sentinel
+  bool leveled_ = false;        // this tick deferred the sentinel or a KFD listing (tick leveling)
   uint64_t procs_read_ns_ = 0;  // tick time of the last per-process read (process_min_interval_s)
   uint64_t counters_kick_ns_ = 0;  // tick time the last PMC read round was for (counters_min_interval_s)
   bool counters_round_next_ = false;  // "end" kick: the next tick has a round to sync  // cfg_.counters_kick with "auto" resolved

@@ -23,7 +23,7 @@ KfdProcReader::~KfdProcReader() {
 }
 
 void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
-                         std::vector<std::vector<ProcSample>>* per_dev, uint64_t now_ns) {
+                         std::vector<std::vector<ProcSample>>* per_dev, uint64_t now_ns, bool defer_listing) {
   per_dev->resize(devs.size());
   for (auto& l : *per_dev) l.clear();
   ++scan_no_;
@@ -54,8 +54,12 @@ void KfdProcReader::scan(const std::vector<DeviceInfo>& devs,
   }
   const bool moved = have_mtime && (sb.st_mtim.tv_sec != mtime_.tv_sec || sb.st_mtim.tv_nsec != mtime_.tv_nsec);
   if (have_mtime) mtime_ = sb.st_mtim;
-  const bool list = !now_ns || !rescan_ns_ || moved || relist_ || now_ns - last_list_ns_ >= rescan_ns_ ||
-                    now_ns < last_list_ns_;
+  // (a rescan-timer listing may wait while the engine levels a heavy tick, at most to twice the
+  // interval; a moved mtime or a vanished process lists at once)
+  const bool timer_due = now_ns - last_list_ns_ >= rescan_ns_ &&
+                         !(defer_listing && now_ns - last_list_ns_ < 2 * rescan_ns_);
+  const bool list = !now_ns || !rescan_ns_ || moved || relist_ || timer_due || now_ns < last_list_ns_;
+  deferred_ = !list && defer_listing && now_ns - last_list_ns_ >= rescan_ns_;
   if (!list) {
     for (auto it = pids_.begin(); it != pids_.end();) {
       if (emit(it->second, it->first, per_dev, now_ns) == 0 && !it->second.devs.empty()) {

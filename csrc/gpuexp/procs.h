@@ -33,10 +33,13 @@ class KfdProcReader {
   KfdProcReader(const KfdProcReader&) = delete;
   KfdProcReader& operator=(const KfdProcReader&) = delete;
   // Fills per_dev[d] with the processes that have a KFD context on device d.
+  // `defer_listing`: a listing due only to the rescan timer waits for a later scan (a tick that
+  // already carries more SMU fetches than most; the engine's tick leveling, engine.cc).
   void scan(const std::vector<DeviceInfo>& devs, std::vector<std::vector<ProcSample>>* per_dev,
-            uint64_t now_ns = 0);
+            uint64_t now_ns = 0, bool defer_listing = false);
   size_t tracked() const { return pids_.size(); }
   uint64_t lists() const { return lists_; }    // scans that listed the directory
+  bool listing_deferred() const { return deferred_; }  // the last scan put off a due listing
   uint64_t dir_reopens() const { return dir_reopens_; }  // the proc directory was replaced (KFD reload)
   uint64_t scans() const { return scan_no_; }  // all scans
 
@@ -69,6 +72,7 @@ class KfdProcReader {
   uint64_t detail_every_ns_;
   uint64_t rescan_ns_ = 0;       // list the KFD proc directory at least this often (0: every scan)
   uint64_t last_list_ns_ = 0;
+  bool deferred_ = false;
   bool relist_ = false;          // a tracked process vanished: list at the next scan
   timespec mtime_{};             // the directory's mtime at the last look
   int dir_fd_ = -1;              // the KFD proc directory, kept open: fstat per scan, no path walk

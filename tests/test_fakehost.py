@@ -1134,3 +1134,49 @@ def test_memory_reads_at_process_min_interval(native, tmp_path):
         assert values(e.snapshot_text()) == (float(2 << 30), float(7 << 30))  # the very next tick
     finally:
         e.stop()
+
+
+def test_tick_leveling_moves_extras_off_two_fetch_ticks(native, tmp_path):
+    """8 GPUs at 10 Hz: the auto fetch cap phases the SMU fetches 2,2,1,2,1 per tick, and the
+    sentinel (0.5 s) and the KFD rescan listing (0.5 s) have the same 5-tick period.  A tick
+    with >= 2 fetches defers those two to a lighter tick (once moved, they stay there), so after
+    start-up neither runs on a two-fetch tick and neither runs late by more than one interval.
+    On the simulated clock: every tick's fetches, sentinel runs and listings are counted."""
+    import time
+    _loaded_node(tmp_path, 8)
+    c = native.EngineConfig()
+    c.backend = "sysfs"
+    c.host_root = str(tmp_path)
+    c.interval_s = 0.1
+    c.sampler_thread = False
+    c.serve_http = False
+    c.series_profile = "full"
+    c.fake_metrics_cost_us = SMU_FETCH_CPU_US
+    c.enable_counters = c.enable_sentinel = True
+    c.fake_pmc_cost_us = 1  # (the cost does not matter here; the SMU fetch's sets the cap)
+    c.fake_sentinel_cost_us = 1
+    e = native.Engine(c)
+    e.start()
+    try:
+        now = time.monotonic_ns()
+        rows = []
+        s0 = e.stats()
+        for i in range(120):
+            now += 100_000_000
+            e.tick(now)
+            s1 = e.stats()
+            rows.append((s1["last_tick_fresh"], s1["sentinel_runs"] - s0["sentinel_runs"],
+                         s1["kfd_lists"] - s0["kfd_lists"], s1["leveled_ticks"] - s0["leveled_ticks"]))
+            s0 = s1
+    finally:
+        e.stop()
+    steady = rows[40:]  # past the cap's measurement and the first re-phasing
+    fresh = [r[0] for r in steady]
+    assert max(fresh) == 2 and min(fresh) == 1, fresh  # the 2,2,1,2,1 phasing
+    sen = [i for i, r in enumerate(steady) if r[1]]
+    lst = [i for i, r in enumerate(steady) if r[2]]
+    assert sen and lst, (sen, lst)
+    assert all(steady[i][0] < 2 for i in sen), [(i, steady[i]) for i in sen]
+    assert all(steady[i][0] < 2 for i in lst), [(i, steady[i]) for i in lst]
+    assert max(b - a for a, b in zip(sen, sen[1:])) <= 10, sen  # never more than one interval late
+    assert max(b - a for a, b in zip(lst, lst[1:])) <= 10, lst
