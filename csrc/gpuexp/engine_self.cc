@@ -177,12 +177,15 @@ void Engine::emit_self(uint64_t gen) {
   gput(kFamSelfCpu, 0, double(s.sampler_cpu_ns) * 1e-9, gen, none);
   for (int k = 0; k < kDevParts; ++k)
     gput(kFamSelfDevPart, k, dev_part_total_s_[k], gen, [&] { return std::vector<std::string>{dev_part_name(k)}; });
-  // histograms: accumulated every tick, published every tick at <= 10 Hz (or manual ticks) and at
-  // most once a second above that (see engine.h)
+  // histograms: accumulated every tick, published at most once a second (every tick at <= 1 Hz
+  // or manual ticks; see engine.h)
   const uint64_t hnow = last_tick_now_;
-  const bool publish_hist = cfg_.interval_s <= 0 || cfg_.interval_s >= 0.1 || !self_hist_pub_ns_ ||
+  const bool publish_hist = cfg_.interval_s <= 0 || cfg_.interval_s >= 1.0 || !self_hist_pub_ns_ ||
                             hnow < self_hist_pub_ns_ || hnow - self_hist_pub_ns_ >= 1000000000ull;
   if (publish_hist) self_hist_pub_ns_ = hnow;
+  // the scrape-latency histogram changes only with scrapes: every tick at <= 10 Hz, so a
+  // scraper reads its own previous scrapes counted (above 10 Hz with the others, once a second)
+  const bool publish_http_hist = publish_hist || cfg_.interval_s >= 0.1;
   const std::vector<double>& sb = stage_bounds();
   for (int k = 0; k < kStages; ++k) {
     SeriesRef& r = gref(kFamSelfStage, k);
@@ -197,7 +200,7 @@ void Engine::emit_self(uint64_t gen) {
     }
     if (!publish_hist || !table_.set_histogram(r, sb, h, stage_hist_sum_[k], stage_hist_n_[k], gen)) table_.touch(r, gen);
   }
-  if (http_) emit_http_self(gen, publish_hist);
+  if (http_) emit_http_self(gen, publish_http_hist);
   if (!mock_)
     for (size_t i = 0; i < devices_.size(); ++i) {
       DevState& st = dstate_[i];
