@@ -714,6 +714,7 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("fake_pmc_cost_us", &EngineConfig::fake_pmc_cost_us)
       .def_readwrite("fake_sentinel_cost_us", &EngineConfig::fake_sentinel_cost_us)
       .def_readwrite("sampler_thread", &EngineConfig::sampler_thread)
+      .def_readwrite("render_when_due", &EngineConfig::render_when_due)
       .def_readwrite("process_min_interval_s", &EngineConfig::process_min_interval_s)
       .def_readwrite("sentinel_min_interval_s", &EngineConfig::sentinel_min_interval_s)
       .def_readwrite("counters_min_interval_s", &EngineConfig::counters_min_interval_s)
@@ -780,6 +781,7 @@ PYBIND11_MODULE(_gpuexp, m) {
         d["sentinel_runs"] = s.sentinel_runs;
         d["kfd_lists"] = s.kfd_lists;
         d["leveled_ticks"] = s.leveled_ticks;
+        d["renders_skipped"] = s.renders_skipped;
         d["render_bytes"] = s.render_bytes;
         d["series"] = s.series;
         d["device_errors"] = s.device_errors;

@@ -696,10 +696,20 @@ void Engine::tick_locked(uint64_t now) {
   ts[6] = mono_ns();
   cs[6] = cpu_mark();
 
-  // 6: render into a free snapshot slot
-  int slot = store_.begin_write();
+  // 6: render into a free snapshot slot -- when a scrape will read it (render_when_due): with
+  // only steady scrapers known and none due before the tick after next, the tick publishes
+  // nothing (at least one render a second; the series stage above ran all the same)
+  bool render_now = true;
+  if (http_ && cfg_.render_when_due && period_ns) {
+    const uint64_t tn = mono_ns();
+    render_now = !last_render_mono_ || tn < last_render_mono_ || tn - last_render_mono_ >= 1000000000ull ||
+                 http_->render_due(tn, 2 * period_ns + 5000000ull);
+    if (!render_now) ++renders_skipped_;
+  }
+  int slot = render_now ? store_.begin_write() : -1;
   uint64_t rbytes = 0, nseries = 0;
   if (slot >= 0) {
+    last_render_mono_ = mono_ns();
     Snapshot* snap = store_.slot(slot);
     // gzip copy only when a gzip scrape is expected before the tick after next (or its
     // schedule is unknown): a 15 s Prometheus scrape costs one compression, not 150
@@ -728,12 +738,12 @@ void Engine::tick_locked(uint64_t now) {
     }
     snap->published_mono_ns = mono_ns();
     store_.publish(slot);
-    if (!cfg_.state_file.empty() && tnow - state_saved_ns_ >= uint64_t(cfg_.state_interval_s * 1e9)) save_state();
     if (http_) http_->set_ready(true);
   } else {
     ts[7] = mono_ns();
     cs[7] = cpu_mark();
   }
+  if (!cfg_.state_file.empty() && ts[7] - state_saved_ns_ >= uint64_t(cfg_.state_interval_s * 1e9)) save_state();
   if (counters_ && kick_end && counters_due(now + period_ns)) {  // next tick's read, completing while we sleep
     counters_->kick();
     counters_kick_ns_ = now + period_ns;
@@ -761,7 +771,8 @@ void Engine::tick_locked(uint64_t now) {
     stats_.sentinel_runs = sentinel_runs_;
     stats_.kfd_lists = kfd_ ? kfd_->lists() : 0;
     stats_.leveled_ticks += leveled_ ? 1 : 0;
-    if (slot < 0) stats_.publish_skipped += 1;
+    if (slot < 0 && render_now) stats_.publish_skipped += 1;
+    stats_.renders_skipped = renders_skipped_;
     stats_.last_tick_ns = tend - ts[0];
     stats_.max_tick_ns = std::max(stats_.max_tick_ns, stats_.last_tick_ns);
     stats_.tick_ns_total += stats_.last_tick_ns;

@@ -107,9 +107,10 @@ const std::vector<FamilySpec>& self_family_specs() {
       {kFamSelfRenderBytes, "gpuexp_render_bytes", "Size of the last rendered exposition", G, N, {}, kGlobal, 1},
       {kFamSelfExpo, "gpuexp_exposition_events_total",
        "Compiled exposition: families laid out again (a series appeared or went, a value outgrew "
-       "its field), segments parsed on their own while their layout settled, and Huffman code "
-       "builds (0 per tick in steady state)",
-       C, N, {"event"}, kGlobal, 3},
+       "its field), segments parsed on their own while their layout settled, Huffman code "
+       "builds (0 per tick in steady state), and ticks that rendered nothing because no "
+       "steady scraper was due (render_when_due)",
+       C, N, {"event"}, kGlobal, 4},
       {kFamSelfSeries, "gpuexp_series", "Series in the last rendered exposition", G, N, {}, kGlobal, 1},
       {kFamSelfDevErrors, "gpuexp_device_errors_total", "Failed telemetry reads per GPU", C, N, {"gpu"}, kGpu, 1},
       {kFamSelfOverruns, "gpuexp_tick_overruns_total", "Ticks skipped because a tick ran past its deadline", C, N, {},
@@ -237,6 +238,7 @@ void Engine::emit_self(uint64_t gen) {
     gput(kFamSelfExpo, 1, double(table_.provisional_parses()), gen,
          [] { return std::vector<std::string>{"provisional_parse"}; });
     gput(kFamSelfExpo, 2, double(table_.code_builds()), gen, [] { return std::vector<std::string>{"code_build"}; });
+    gput(kFamSelfExpo, 3, double(renders_skipped_), gen, [] { return std::vector<std::string>{"render_skipped"}; });
   }
   emit_rccl_self(gen);
 }

@@ -434,6 +434,20 @@ bool HttpServer::gzip_due(uint64_t now_ns, uint64_t horizon_ns) const {
   return false;
 }
 
+bool HttpServer::render_due(uint64_t now_ns, uint64_t horizon_ns) const {
+  if (!metrics_seen_ns_.load(std::memory_order_relaxed)) return true;
+  const uint64_t u = unsteady_ns_.load(std::memory_order_relaxed);
+  if (u && now_ns < u + cfg_.gzip_unsteady_hold_ns) return true;
+  bool steady = false;
+  for (const auto& g : scrape_next_ns_) {
+    const uint64_t e = g.load(std::memory_order_relaxed);
+    if (!e) continue;
+    steady = true;
+    if (e <= now_ns + horizon_ns) return true;
+  }
+  return !steady;
+}
+
 void HttpServer::run(Worker* w) {
   set_thread_name("gpuexp-http");
   if (cfg_.follow_rx_cpu) {
@@ -647,6 +661,8 @@ void HttpServer::run(Worker* w) {
         c.last_metrics_ns = arrival;
         c.gzip_client = want_gzip && cfg_.enable_gzip;
         if (c.gzip_client && !c.expected_next()) gzip_unsteady_ns_.store(t0, std::memory_order_relaxed);
+        metrics_seen_ns_.store(t0, std::memory_order_relaxed);
+        if (!c.expected_next()) unsteady_ns_.store(t0, std::memory_order_relaxed);
         SnapshotStore::Pin pin = store_->acquire();
         if (!pin) {
           respond_simple(c, 503, "Service Unavailable", "text/plain", "no sample yet\n", is_head);
@@ -749,7 +765,7 @@ void HttpServer::run(Worker* w) {
   auto arm_prewake = [&]() {
     const uint64_t now = mono_ns();
     const int mode = prewake_mode_.load(std::memory_order_relaxed);
-    uint64_t next = 0, gz_next = 0, lead = cfg_.prewake_lead_ns;
+    uint64_t next = 0, gz_next = 0, any_next = 0, lead = cfg_.prewake_lead_ns;
     uint64_t sp_from = 0, sp_until = 0;
     for (auto& kv : w->conns) {
       const uint64_t e = kv.second.expected_next();
@@ -767,8 +783,10 @@ void HttpServer::run(Worker* w) {
       }
       // a steady gzip scraper gone quiet for a minute no longer holds the sampler to it
       if (e && kv.second.gzip_client && e + 60000000000ull > now && (!gz_next || e < gz_next)) gz_next = e;
+      if (e && e + 60000000000ull > now && (!any_next || e < any_next)) any_next = e;
     }
     gzip_next_ns_[w->index].store(gz_next, std::memory_order_relaxed);
+    scrape_next_ns_[w->index].store(any_next, std::memory_order_relaxed);
     uint64_t at = 0;
     if ((mode == kPrewakeSlices || mode == kPrewakeSpin) && next) {
       // before the lead: one timer at (expected - lead); inside the window: short slices

@@ -173,6 +173,12 @@ class HttpServer {
   // scraping every 15 s against a 10 Hz sampler thus costs one compression per scrape,
   // not 150; a request that arrives off schedule is compressed by the worker itself.
   bool gzip_due(uint64_t now_ns, uint64_t horizon_ns) const;
+  // Whether a snapshot published at `now_ns` will be read: false only while every /metrics
+  // scraper of the last unsteady_hold is steady and none is expected within `horizon_ns` (nor
+  // overdue).  A process never scraped, an irregular scraper, or one that went quiet: true.
+  // Prometheus scraping every 15 s against a 10 Hz sampler thus needs a render per scrape, not
+  // 150 (the engine still renders at least once a second: EngineConfig::render_when_due).
+  bool render_due(uint64_t now_ns, uint64_t horizon_ns) const;
   // Last time a scraper negotiated the protobuf exposition (the sampler renders it then).
   uint64_t proto_wanted_ns() const { return proto_wanted_ns_.load(std::memory_order_relaxed); }
   const HttpStats& stats() const { return stats_; }
@@ -197,6 +203,10 @@ class HttpServer {
   // per worker: earliest expected request of its steady gzip connections (0 = none)
   static constexpr int kMaxWorkers = 64;
   std::atomic<uint64_t> gzip_next_ns_[kMaxWorkers]{};
+  // the same for every steady /metrics connection, any encoding (render_due)
+  std::atomic<uint64_t> scrape_next_ns_[kMaxWorkers]{};
+  std::atomic<uint64_t> metrics_seen_ns_{0};  // last /metrics request (0 = never scraped)
+  std::atomic<uint64_t> unsteady_ns_{0};      // last /metrics request from a connection without a steady period
   HttpStats stats_;
   std::vector<std::unique_ptr<Worker>> workers_;
 };

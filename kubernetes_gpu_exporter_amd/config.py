@@ -54,6 +54,8 @@ class Config:
     process_min_interval: float = 0.05     # per-process reads (KFD VRAM / amdsmi list) at most this often (s;
                                            # 0 = every tick): a 100 Hz tick re-exports the last lists in between
     gc_after: int = 1
+    render_when_due: bool = True           # publish a snapshot only when a steady scraper's request is due
+                                           # (and >= 1/s): 15 s scrapes of a 10 Hz sampler render ~1.1/s
     exposition: str = "compiled"           # compiled (fixed-layout body, values patched in place, gzip from
                                            # pre-encoded static bits) | classic (re-render + compress)
     # optional sources
@@ -196,6 +198,7 @@ class Config:
         ec.pod_totals_ttl_s = float(self.pod_totals_ttl)
         ec.kfd_path = self.kfd_path
         ec.gc_after = int(self.gc_after)
+        ec.render_when_due = bool(self.render_when_due)
         ec.exposition = str(self.exposition)
         ec.device_filter = [int(d) for d in self.devices if ":" not in str(d)]
         ec.device_filter_bdf = [str(d) for d in self.devices if ":" in str(d)]

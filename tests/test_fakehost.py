@@ -977,18 +977,21 @@ def test_whole_process_cpu_8_gpus(native, tmp_path, hz, scrape, budget_pct):
     a timer wake-up is an MI355X host's (<= BUDGET_HOST_MAX_WAKE_US; measured first, with the
     sampler's own timerfd wait).  The gpu tier runs the same check on the MI355X host's CPU unconditionally
     (test_whole_process_cpu_8_gpus_mi355x_host), and profiles/r06/session5/cpu_projection.txt
-    is that host's projection: 1.04 % at 10 Hz, 1.43 % at 100 Hz.  The 10 Hz heaviest-tick ratio
-    is host-independent and asserted everywhere."""
+    is that host's projection: 1.04 % at 10 Hz, 1.43 % at 100 Hz.  The heaviest-tick ratio is
+    a maximum over 40 ticks, which a VM's steal time charged to the sampler thread can double:
+    it is asserted with the budgets; its structure (fetch phasing, extras off two-fetch ticks,
+    per-tick stand-in CPU) is pinned on a simulated clock everywhere
+    (test_tick_leveling_moves_extras_off_two_fetch_ticks)."""
     wake_ns, late_ns = native.timer_wakeup_cost(hz, int(max(20, hz)))
     pct, lump = _check_cpu_budget_8_gpus(native, tmp_path, hz, scrape, budget_pct)
-    if hz == 10 and not scrape:
-        assert lump <= 1.5, lump
     if wake_ns / 1e3 > BUDGET_HOST_MAX_WAKE_US or _under_hypervisor():
         pytest.skip(f"this host {'runs under a hypervisor and ' if _under_hypervisor() else ''}charges "
                     f"{wake_ns / 1e3:.0f} us of thread CPU per timer wake-up ({late_ns / 1e3:.0f} us late; an MI355X "
                     f"host: {MI355X_HOST_WAKE_US} us): {pct:.2f} % here is not MI355X-node CPU; the gpu tier asserts "
                     f"the {budget_pct} % budget on the MI355X host")
     assert pct < budget_pct, pct
+    if hz == 10 and not scrape:
+        assert lump <= 1.5, lump
 
 
 @pytest.mark.gpu
@@ -1153,8 +1156,8 @@ def test_tick_leveling_moves_extras_off_two_fetch_ticks(native, tmp_path):
     c.series_profile = "full"
     c.fake_metrics_cost_us = SMU_FETCH_CPU_US
     c.enable_counters = c.enable_sentinel = True
-    c.fake_pmc_cost_us = 1  # (the cost does not matter here; the SMU fetch's sets the cap)
-    c.fake_sentinel_cost_us = 1
+    c.fake_pmc_cost_us = PMC_READ_CPU_US
+    c.fake_sentinel_cost_us = SENTINEL_RUN_CPU_US
     e = native.Engine(c)
     e.start()
     try:
@@ -1166,7 +1169,8 @@ def test_tick_leveling_moves_extras_off_two_fetch_ticks(native, tmp_path):
             e.tick(now)
             s1 = e.stats()
             rows.append((s1["last_tick_fresh"], s1["sentinel_runs"] - s0["sentinel_runs"],
-                         s1["kfd_lists"] - s0["kfd_lists"], s1["leveled_ticks"] - s0["leveled_ticks"]))
+                         s1["kfd_lists"] - s0["kfd_lists"], s1["leveled_ticks"] - s0["leveled_ticks"],
+                         s1["fake_cpu_burnt_ns"] - s0["fake_cpu_burnt_ns"]))
             s0 = s1
     finally:
         e.stop()
@@ -1180,3 +1184,7 @@ def test_tick_leveling_moves_extras_off_two_fetch_ticks(native, tmp_path):
     assert all(steady[i][0] < 2 for i in lst), [(i, steady[i]) for i in lst]
     assert max(b - a for a, b in zip(sen, sen[1:])) <= 10, sen  # never more than one interval late
     assert max(b - a for a, b in zip(lst, lst[1:])) <= 10, lst
+    # the silicon-cost stand-ins a tick carries (SMU fetches, PMC round, sentinel run): the
+    # heaviest tick at most 1.35x the mean (two fetches against 1.6 on average)
+    burnt = [r[4] for r in steady]
+    assert max(burnt) <= 1.35 * sum(burnt) / len(burnt), (max(burnt), sum(burnt) / len(burnt))

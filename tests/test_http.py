@@ -730,3 +730,55 @@ def test_prewake_mode_switches_at_run_time(native):
         assert "gpuexp_http_prewake_spin_seconds_total" in fams
     finally:
         e.stop()
+
+
+def _ticks_in(body: bytes) -> float:
+    for line in body.decode().splitlines():
+        if line.startswith("gpuexp_ticks_total"):
+            return float(line.split()[-1])
+    raise AssertionError("no gpuexp_ticks_total")
+
+
+@pytest.mark.parametrize("when_due", [True, False])
+def test_render_when_due_skips_unread_ticks_and_serves_fresh(native, when_due):
+    """A steady scraper at 4 Hz against a 100 Hz sampler: with render_when_due the ticks no
+    scrape will read publish nothing (most of them), yet every scrape after the period is learnt
+    reads a snapshot at most 3 ticks old; without it every tick renders."""
+    c = native.EngineConfig()
+    c.backend = "mock"
+    c.interval_s = 0.01
+    c.series_profile = "standard"
+    c.render_when_due = when_due
+    h = c.http
+    h.host = "127.0.0.1"
+    h.port = 0
+    h.gzip_unsteady_hold_ns = 300_000_000  # (60 s by default: the first, unlearnt scrapes hold it)
+    c.http = h
+    e = native.Engine(c)
+    e.start()
+    try:
+        time.sleep(0.3)
+        cl = native.ScrapeClient("127.0.0.1", e.http_port, "/metrics", True, 5000, "", False)
+        lags = []
+        t = time.perf_counter()
+        s0 = None
+        for i in range(16):
+            assert cl.scrape(), cl.last_status
+            ticks_now = e.stats()["ticks"]
+            if i >= 6:
+                lags.append(ticks_now - _ticks_in(gzip.decompress(cl.last_body())))
+            if i == 5:
+                s0 = e.stats()
+            t += 0.25
+            time.sleep(max(0.0, t - time.perf_counter()))
+        s1 = e.stats()
+    finally:
+        e.stop()
+    skipped = s1["renders_skipped"] - s0["renders_skipped"]
+    ticks = s1["ticks"] - s0["ticks"]
+    print(f"render_when_due={when_due}: {skipped} of {ticks} ticks not rendered; lag in ticks {lags}")
+    assert max(lags) <= 3, lags  # (the tick counter in the body is the render's own tick)
+    if when_due:
+        assert skipped > 0.6 * ticks, (skipped, ticks)
+    else:
+        assert skipped == 0
