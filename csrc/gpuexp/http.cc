@@ -436,8 +436,10 @@ bool HttpServer::gzip_due(uint64_t now_ns, uint64_t horizon_ns) const {
 
 bool HttpServer::render_due(uint64_t now_ns, uint64_t horizon_ns) const {
   if (!metrics_seen_ns_.load(std::memory_order_relaxed)) return true;
-  const uint64_t u = unsteady_ns_.load(std::memory_order_relaxed);
-  if (u && now_ns < u + cfg_.gzip_unsteady_hold_ns) return true;
+  for (const auto& a : unsteady_ns_) {
+    const uint64_t u = a.load(std::memory_order_relaxed);
+    if (u && now_ns < u + cfg_.gzip_unsteady_hold_ns) return true;
+  }
   bool steady = false;
   for (const auto& g : scrape_next_ns_) {
     const uint64_t e = g.load(std::memory_order_relaxed);
@@ -662,7 +664,7 @@ void HttpServer::run(Worker* w) {
         c.gzip_client = want_gzip && cfg_.enable_gzip;
         if (c.gzip_client && !c.expected_next()) gzip_unsteady_ns_.store(t0, std::memory_order_relaxed);
         metrics_seen_ns_.store(t0, std::memory_order_relaxed);
-        if (!c.expected_next()) unsteady_ns_.store(t0, std::memory_order_relaxed);
+        if (!c.expected_next()) unsteady_ns_[w->index].store(t0, std::memory_order_relaxed);  // (at once)
         SnapshotStore::Pin pin = store_->acquire();
         if (!pin) {
           respond_simple(c, 503, "Service Unavailable", "text/plain", "no sample yet\n", is_head);
@@ -765,7 +767,7 @@ void HttpServer::run(Worker* w) {
   auto arm_prewake = [&]() {
     const uint64_t now = mono_ns();
     const int mode = prewake_mode_.load(std::memory_order_relaxed);
-    uint64_t next = 0, gz_next = 0, any_next = 0, lead = cfg_.prewake_lead_ns;
+    uint64_t next = 0, gz_next = 0, any_next = 0, unsteady = 0, lead = cfg_.prewake_lead_ns;
     uint64_t sp_from = 0, sp_until = 0;
     for (auto& kv : w->conns) {
       const uint64_t e = kv.second.expected_next();
@@ -784,7 +786,9 @@ void HttpServer::run(Worker* w) {
       // a steady gzip scraper gone quiet for a minute no longer holds the sampler to it
       if (e && kv.second.gzip_client && e + 60000000000ull > now && (!gz_next || e < gz_next)) gz_next = e;
       if (e && e + 60000000000ull > now && (!any_next || e < any_next)) any_next = e;
+      if (!e && kv.second.last_metrics_ns) unsteady = std::max(unsteady, kv.second.last_metrics_ns);
     }
+    unsteady_ns_[w->index].store(unsteady, std::memory_order_relaxed);
     gzip_next_ns_[w->index].store(gz_next, std::memory_order_relaxed);
     scrape_next_ns_[w->index].store(any_next, std::memory_order_relaxed);
     uint64_t at = 0;

@@ -173,9 +173,10 @@ class HttpServer {
   // scraping every 15 s against a 10 Hz sampler thus costs one compression per scrape,
   // not 150; a request that arrives off schedule is compressed by the worker itself.
   bool gzip_due(uint64_t now_ns, uint64_t horizon_ns) const;
-  // Whether a snapshot published at `now_ns` will be read: false only while every /metrics
-  // scraper of the last unsteady_hold is steady and none is expected within `horizon_ns` (nor
-  // overdue).  A process never scraped, an irregular scraper, or one that went quiet: true.
+  // Whether a snapshot published at `now_ns` will be read: false only while every open /metrics
+  // connection that scraped within gzip_unsteady_hold is steady and none is expected within
+  // `horizon_ns` (nor overdue).  A process never scraped, an irregular scraper (until its period
+  // is learnt), or one that went quiet: true.
   // Prometheus scraping every 15 s against a 10 Hz sampler thus needs a render per scrape, not
   // 150 (the engine still renders at least once a second: EngineConfig::render_when_due).
   bool render_due(uint64_t now_ns, uint64_t horizon_ns) const;
@@ -206,7 +207,9 @@ class HttpServer {
   // the same for every steady /metrics connection, any encoding (render_due)
   std::atomic<uint64_t> scrape_next_ns_[kMaxWorkers]{};
   std::atomic<uint64_t> metrics_seen_ns_{0};  // last /metrics request (0 = never scraped)
-  std::atomic<uint64_t> unsteady_ns_{0};      // last /metrics request from a connection without a steady period
+  // per worker: newest /metrics request of its open connections that have no steady period yet
+  // (a connection that became steady, or closed, no longer holds renders to every tick)
+  std::atomic<uint64_t> unsteady_ns_[kMaxWorkers]{};
   HttpStats stats_;
   std::vector<std::unique_ptr<Worker>> workers_;
 };

@@ -752,7 +752,6 @@ def test_render_when_due_skips_unread_ticks_and_serves_fresh(native, when_due):
     h = c.http
     h.host = "127.0.0.1"
     h.port = 0
-    h.gzip_unsteady_hold_ns = 300_000_000  # (60 s by default: the first, unlearnt scrapes hold it)
     c.http = h
     e = native.Engine(c)
     e.start()

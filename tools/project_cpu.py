@@ -44,7 +44,7 @@ while True:
 
 def measure(native, n_gpus: int, hz: float, fetch_us: int, policy: str, budget: float, seconds: float,
             scrape: str = "none", exposition: str = "compiled", warmup: float = -1.0, pmc_us: int = -1,
-            sentinel_us: int = -1) -> dict:
+            sentinel_us: int = -1, scrape_hz: float = 0.0, render_when_due: bool = True) -> dict:
     # warm-up: long enough for the exposition to settle (a family's real parse comes 8 renders after
     # its last layout; the scraper's first gzip ask starts the gzip copies): 20 ticks, at least 1 s
     if warmup < 0:
@@ -74,12 +74,15 @@ def measure(native, n_gpus: int, hz: float, fetch_us: int, policy: str, budget: 
         c.enable_sentinel = True
         c.fake_sentinel_cost_us = sentinel_us
     c.metrics_min_interval_s = -1.0 if policy == "auto" else 0.0
+    if hasattr(c, "render_when_due"):
+        c.render_when_due = render_when_due
     c.metrics_cpu_budget = budget / 100.0
     e = native.Engine(c)
     e.start()
     scraper = None
     if scrape != "none":  # another process, so its CPU is not the exporter's
-        scraper = subprocess.Popen([sys.executable, "-c", SCRAPER, PKG_ROOT, str(e.http_port), str(hz), scrape])
+        scraper = subprocess.Popen([sys.executable, "-c", SCRAPER, PKG_ROOT, str(e.http_port), str(scrape_hz or hz),
+                                    scrape])
     try:
         time.sleep(warmup)
         if hasattr(e, "reset_tick_max"):
@@ -127,6 +130,8 @@ def main() -> int:
     ap.add_argument("--warmup", type=float, default=-1.0, help="seconds before measuring (default: 20 ticks, >= 1 s)")
     ap.add_argument("--policies", default="auto,every")
     ap.add_argument("--scrape", default="none", help="none | gzip | identity: a scraper process at the tick rate")
+    ap.add_argument("--scrape-hz", type=float, default=0.0, help="the scraper's rate (default: the tick rate)")
+    ap.add_argument("--render-when-due", default="1", help="1 | 0 | 1,0 (compare)")
     ap.add_argument("--exposition", default="compiled", help="compiled | classic (comma list to compare)")
     ap.add_argument("--stages", action="store_true", help="also print the sampler thread's CPU per stage")
     args = ap.parse_args()
@@ -143,13 +148,16 @@ def main() -> int:
             for n in (int(x) for x in args.gpus.split(",")):
                 for policy in args.policies.split(","):
                   for expo in args.exposition.split(","):
+                   for rwd in args.render_when_due.split(","):
                     r = measure(native, n, hz, fetch, policy, args.budget, args.seconds, args.scrape, expo, args.warmup,
-                                args.pmc_us, args.sentinel_us)
+                                args.pmc_us, args.sentinel_us, args.scrape_hz, rwd == "1")
                     print(f"{r['gpus']:>4} {r['hz']:>5g} {r['fetch_us']:>8} {r['policy']:>6} "
                           f"{r['process_cpu_pct']:>7.2f} {r['sampler_us_per_tick']:>15.1f} "
                           f"{r['tick_wall_mean_us']:>12.1f} {r['tick_wall_max_us']:>11.1f} "
                           f"{r['tick_cpu_mean_us']:>11.1f} {r['tick_cpu_max_us']:>10.1f}  "
-                          f"{expo} scrape={args.scrape}", flush=True)
+                          f"{expo} scrape={args.scrape}"
+                          + (f"@{args.scrape_hz:g}Hz" if args.scrape_hz else "")
+                          + ("" if rwd == "1" else " render_when_due=0"), flush=True)
                     if args.stages:
                         print("      stage us/tick: " + " ".join(f"{k}={v}" for k, v in r["stage_us_per_tick"].items())
                               + f"  relayouts/tick={r['relayouts_per_tick']} code_builds={r['code_builds']}"
