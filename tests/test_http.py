@@ -781,3 +781,83 @@ def test_render_when_due_skips_unread_ticks_and_serves_fresh(native, when_due):
         assert skipped > 0.6 * ticks, (skipped, ticks)
     else:
         assert skipped == 0
+
+
+def test_render_when_due_resumes_for_an_irregular_scraper_and_a_quiet_one(native):
+    """render_when_due keeps every tick rendered (1) while an open connection without a learnt
+    period has scraped, even next to a steady scraper, and (2) once the steady scraper is overdue;
+    right after a steady scraper's request most ticks until its next one are skipped."""
+    c = native.EngineConfig()
+    c.backend = "mock"
+    c.interval_s = 0.01
+    c.series_profile = "compact"
+    h = c.http
+    h.host = "127.0.0.1"
+    h.port = 0
+    c.http = h
+    e = native.Engine(c)
+    e.start()
+    try:
+        time.sleep(0.2)
+        steady = native.ScrapeClient("127.0.0.1", e.http_port, "/metrics", False, 5000, "", False)
+        t = time.perf_counter()
+        for i in range(6):  # a 3 Hz scraper: learnt after its third request
+            if i:
+                t += 0.33
+                time.sleep(max(0.0, t - time.perf_counter()))
+            assert steady.scrape()
+
+        def skipped_over(seconds):
+            s0 = e.stats()
+            time.sleep(seconds)
+            s1 = e.stats()
+            return s1["renders_skipped"] - s0["renders_skipped"], s1["ticks"] - s0["ticks"]
+
+        # the steady case, right after its scrape: until the next is due most ticks are skipped
+        sk, n = skipped_over(0.2)
+        assert 0.5 * n < sk, (sk, n)
+        # (1) an irregular second connection: one request, kept open -> every tick renders
+        odd = native.ScrapeClient("127.0.0.1", e.http_port, "/metrics", False, 5000, "", False)
+        assert odd.scrape() and steady.scrape()
+        sk, n = skipped_over(0.5)
+        assert sk == 0, (sk, n)
+        del odd  # closes it: the steady scraper alone again
+        time.sleep(0.05)
+        assert steady.scrape()
+        # (2) the steady scraper stops: overdue after ~one period -> every tick renders
+        time.sleep(0.8)
+        sk, n = skipped_over(0.5)
+        assert sk == 0, (sk, n)
+    finally:
+        e.stop()
+
+
+def test_render_when_due_still_renders_once_a_second(native):
+    """A steady scraper every 1.5 s: between its requests the engine still renders at least
+    once a second (the snapshot an unexpected request reads is never older than that)."""
+    c = native.EngineConfig()
+    c.backend = "mock"
+    c.interval_s = 0.02
+    c.series_profile = "compact"
+    h = c.http
+    h.host = "127.0.0.1"
+    h.port = 0
+    c.http = h
+    e = native.Engine(c)
+    e.start()
+    try:
+        time.sleep(0.2)
+        cl = native.ScrapeClient("127.0.0.1", e.http_port, "/metrics", False, 5000, "", False)
+        t = time.perf_counter()
+        for i in range(4):
+            if i:
+                t += 1.5
+                time.sleep(max(0.0, t - time.perf_counter()))
+            assert cl.scrape()
+        s0 = e.stats()
+        time.sleep(1.3)  # before the next request is due (1.5 s - two ticks)
+        s1 = e.stats()
+    finally:
+        e.stop()
+    rendered = (s1["ticks"] - s0["ticks"]) - (s1["renders_skipped"] - s0["renders_skipped"])
+    assert 1 <= rendered <= 3, (rendered, s1["ticks"] - s0["ticks"])
