@@ -682,6 +682,19 @@ void Engine::tick_locked(uint64_t now) {
   ts[5] = mono_ns();
   cs[5] = cpu_mark();
 
+  // 6 (decided here): does this tick render -- when a scrape will read it (render_when_due):
+  // with only steady scrapers known and none due before the tick after next, the tick neither
+  // writes the series table nor renders (at least one render a second); the series stage's
+  // computations run all the same
+  bool render_now = true;
+  if (http_ && cfg_.render_when_due && period_ns) {
+    const uint64_t tn = mono_ns();
+    render_now = !last_render_mono_ || tn < last_render_mono_ || tn - last_render_mono_ >= 1000000000ull ||
+                 http_->render_due(tn, 2 * period_ns + 5000000ull);
+    if (!render_now) ++renders_skipped_;
+  }
+  emit_ = render_now;
+
   // 5: series
   for (size_t i = 0; i < devices_.size(); ++i) {
     if (cfg_.series_profile != "legacy") collect_device(int(i), gen, dt_s);
@@ -696,16 +709,8 @@ void Engine::tick_locked(uint64_t now) {
   ts[6] = mono_ns();
   cs[6] = cpu_mark();
 
-  // 6: render into a free snapshot slot -- when a scrape will read it (render_when_due): with
-  // only steady scrapers known and none due before the tick after next, the tick publishes
-  // nothing (at least one render a second; the series stage above ran all the same)
-  bool render_now = true;
-  if (http_ && cfg_.render_when_due && period_ns) {
-    const uint64_t tn = mono_ns();
-    render_now = !last_render_mono_ || tn < last_render_mono_ || tn - last_render_mono_ >= 1000000000ull ||
-                 http_->render_due(tn, 2 * period_ns + 5000000ull);
-    if (!render_now) ++renders_skipped_;
-  }
+  // 6: render into a free snapshot slot (render_now: decided before the series stage)
+  emit_ = true;
   int slot = render_now ? store_.begin_write() : -1;
   uint64_t rbytes = 0, nseries = 0;
   if (slot >= 0) {

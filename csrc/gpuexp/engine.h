@@ -397,6 +397,7 @@ class Engine {
   // re-interns only when the handle is stale.
   template <class F>
   void cput(SeriesRef& r, int fid, double v, uint64_t gen, F&& labels) {
+    if (!emit_) return;
     if (table_.set(r, v, gen)) return;
     r = table_.upsert(fid, labels());
     table_.set(r, v, gen);
@@ -452,6 +453,12 @@ class Engine {
   uint64_t sentinel_last_ns_ = 0;  // tick time of the last sentinel run (sentinel_min_interval_s)
   uint64_t sentinel_runs_ = 0;  // ticks that ran the sentinel
   uint64_t last_render_mono_ = 0, renders_skipped_ = 0;  // render_when_due
+  // This tick writes the series table (render_when_due: only a tick that renders does; every
+  // computation of the series stage -- rates, per-pod integration, event totals, histograms --
+  // runs on every tick, only the table writes are skipped).  The write sites: dput / cput /
+  // gput and the few direct table_ calls (engine_device / engine_pods / engine_kfd_events /
+  // engine_self).
+  bool emit_ = true;
   bool leveled_ = false;        // this tick deferred the sentinel or a KFD listing (tick leveling)
   uint64_t procs_read_ns_ = 0;  // tick time of the last per-process read (process_min_interval_s)
   uint64_t counters_kick_ns_ = 0;  // tick time the last PMC read round was for (counters_min_interval_s)

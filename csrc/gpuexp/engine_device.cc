@@ -167,7 +167,7 @@ const std::vector<FamilySpec>& device_family_specs() {
 
 void Engine::dput(DevState& st, int dev, Fam f, int k, std::initializer_list<const char*> extra, double v,
                   uint64_t gen) {
-  if (std::isnan(v)) return;
+  if (!emit_ || std::isnan(v)) return;
   SeriesRef& r = dref(st, f, k);
   if (table_.set(r, v, gen)) return;  // the per-tick path: no allocation, no hashing
   const DeviceInfo& d = devices_[size_t(dev)];
@@ -302,7 +302,7 @@ void Engine::collect_device(int i, uint64_t gen, double dt_s) {
     st.owner_built_set = true;
   }
 
-  if (!table_.set(dref(st, kFamInfo), 1, gen)) {
+  if (emit_ && !table_.set(dref(st, kFamInfo), 1, gen)) {
     dref(st, kFamInfo) = table_.upsert(
         fam_ids_[kFamInfo], {std::to_string(d.index), d.bdf, d.uuid, d.name, std::to_string(d.kfd_gpu_id),
                              d.render_minor >= 0 ? "renderD" + std::to_string(d.render_minor) : "",

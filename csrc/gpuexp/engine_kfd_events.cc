@@ -75,8 +75,9 @@ void Engine::emit_kfd_events(uint64_t gen) {
       it = pod_kfd_events_.erase(it);
       continue;
     }
-    table_.put(fam_ids_[kFamPodKfdEv], {std::get<0>(k), std::get<1>(k), kfd_event_name(std::get<2>(k))},
-               double(it->second), gen);
+    if (emit_)
+      table_.put(fam_ids_[kFamPodKfdEv], {std::get<0>(k), std::get<1>(k), kfd_event_name(std::get<2>(k))},
+                 double(it->second), gen);
     ++it;
   }
 }

@@ -297,7 +297,7 @@ void Engine::emit_pod_totals(uint64_t gen) {
       it = pod_energy_j_.erase(it);
       continue;
     }
-    table_.put(fam_ids_[kFamPodEnergy], {it->first.first, it->first.second}, it->second, gen);
+    if (emit_) table_.put(fam_ids_[kFamPodEnergy], {it->first.first, it->first.second}, it->second, gen);
     ++it;
   }
   for (auto it = pod_xgmi_.begin(); it != pod_xgmi_.end();) {
@@ -305,8 +305,8 @@ void Engine::emit_pod_totals(uint64_t gen) {
       it = pod_xgmi_.erase(it);
       continue;
     }
-    table_.put(fam_ids_[kFamPodXrdTotal], {it->first.first, it->first.second}, it->second.first, gen);
-    table_.put(fam_ids_[kFamPodXwrTotal], {it->first.first, it->first.second}, it->second.second, gen);
+    if (emit_) table_.put(fam_ids_[kFamPodXrdTotal], {it->first.first, it->first.second}, it->second.first, gen);
+    if (emit_) table_.put(fam_ids_[kFamPodXwrTotal], {it->first.first, it->first.second}, it->second.second, gen);
     ++it;
   }
   for (auto it = pod_gpu_s_.begin(); it != pod_gpu_s_.end();) {
@@ -314,8 +314,8 @@ void Engine::emit_pod_totals(uint64_t gen) {
       it = pod_gpu_s_.erase(it);
       continue;
     }
-    table_.put(fam_ids_[kFamPodAllocS], {it->first.first, it->first.second}, it->second.first, gen);
-    table_.put(fam_ids_[kFamPodBusyS], {it->first.first, it->first.second}, it->second.second, gen);
+    if (emit_) table_.put(fam_ids_[kFamPodAllocS], {it->first.first, it->first.second}, it->second.first, gen);
+    if (emit_) table_.put(fam_ids_[kFamPodBusyS], {it->first.first, it->first.second}, it->second.second, gen);
     ++it;
   }
   // a pod's stamp lives while any of its totals does (KFD event counts included: they expire

@@ -181,16 +181,16 @@ void Engine::emit_self(uint64_t gen) {
   // histograms: accumulated every tick, published at most once a second (every tick at <= 1 Hz
   // or manual ticks; see engine.h)
   const uint64_t hnow = last_tick_now_;
-  const bool publish_hist = cfg_.interval_s <= 0 || cfg_.interval_s >= 1.0 || !self_hist_pub_ns_ ||
-                            hnow < self_hist_pub_ns_ || hnow - self_hist_pub_ns_ >= 1000000000ull;
+  const bool publish_hist = emit_ && (cfg_.interval_s <= 0 || cfg_.interval_s >= 1.0 || !self_hist_pub_ns_ ||
+                                      hnow < self_hist_pub_ns_ || hnow - self_hist_pub_ns_ >= 1000000000ull);
   if (publish_hist) self_hist_pub_ns_ = hnow;
   // the scrape-latency histogram changes only with scrapes: every tick at <= 10 Hz, so a
   // scraper reads its own previous scrapes counted (above 10 Hz with the others, once a second)
-  const bool publish_http_hist = publish_hist || cfg_.interval_s >= 0.1;
+  const bool publish_http_hist = publish_hist || (emit_ && cfg_.interval_s >= 0.1);
   const std::vector<double>& sb = stage_bounds();
   for (int k = 0; k < kStages; ++k) {
     SeriesRef& r = gref(kFamSelfStage, k);
-    if (!r.valid()) r = table_.upsert(fam_ids_[kFamSelfStage], {stage_name(k)});
+    if (!r.valid() && emit_) r = table_.upsert(fam_ids_[kFamSelfStage], {stage_name(k)});
     std::vector<uint64_t>& h = stage_hist_[k];
     if (h.size() != sb.size() + 1) h.assign(sb.size() + 1, 0);
     if (s.ticks) {
@@ -199,7 +199,8 @@ void Engine::emit_self(uint64_t gen) {
       stage_hist_sum_[k] += v;
       stage_hist_n_[k] += 1;
     }
-    if (!publish_hist || !table_.set_histogram(r, sb, h, stage_hist_sum_[k], stage_hist_n_[k], gen)) table_.touch(r, gen);
+    if (emit_ && (!publish_hist || !table_.set_histogram(r, sb, h, stage_hist_sum_[k], stage_hist_n_[k], gen)))
+      table_.touch(r, gen);
   }
   if (http_) emit_http_self(gen, publish_http_hist);
   if (!mock_)
@@ -248,7 +249,7 @@ void Engine::emit_http_self(uint64_t gen, bool publish_hist) {
   const HttpStats& hs = http_->stats();
   auto ld = [](const std::atomic<uint64_t>& a) { return double(a.load(std::memory_order_relaxed)); };
   SeriesRef& sr = gref(kFamSelfScrape);
-  if (publish_hist || !table_.touch(sr, gen)) {
+  if (emit_ && (publish_hist || !table_.touch(sr, gen))) {
     std::vector<uint64_t> counts(HttpStats::kBuckets + 1);
     for (int b = 0; b <= HttpStats::kBuckets; ++b) counts[size_t(b)] = hs.lat_buckets[b].load(std::memory_order_relaxed);
     const uint64_t cnt = hs.lat_count.load(std::memory_order_relaxed);
