@@ -715,6 +715,7 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("fake_sentinel_cost_us", &EngineConfig::fake_sentinel_cost_us)
       .def_readwrite("sampler_thread", &EngineConfig::sampler_thread)
       .def_readwrite("render_when_due", &EngineConfig::render_when_due)
+      .def_readwrite("render_every_ticks", &EngineConfig::render_every_ticks)
       .def_readwrite("process_min_interval_s", &EngineConfig::process_min_interval_s)
       .def_readwrite("sentinel_min_interval_s", &EngineConfig::sentinel_min_interval_s)
       .def_readwrite("counters_min_interval_s", &EngineConfig::counters_min_interval_s)

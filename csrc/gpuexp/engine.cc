@@ -693,6 +693,11 @@ void Engine::tick_locked(uint64_t now) {
                  http_->render_due(tn, 2 * period_ns + 5000000ull);
     if (!render_now) ++renders_skipped_;
   }
+  ++tick_index_;
+  if (cfg_.render_every_ticks > 0) {  // (tests: a scrape schedule without an HTTP server)
+    render_now = tick_index_ % uint64_t(cfg_.render_every_ticks) == 0;
+    if (!render_now) ++renders_skipped_;
+  }
   emit_ = render_now;
 
   // 5: series

@@ -84,6 +84,7 @@ struct EngineConfig {
   // = skip), and at least once a second.  Prometheus at 15 s against a 10 Hz sampler: ~1.1
   // renders a second instead of 10.  A scraper at the tick rate (the bench) reads every tick.
   bool render_when_due = true;
+  int render_every_ticks = 0;  // tests only: > 0 renders (and writes the table) on every N-th tick only
   bool serve_http = true;
   HttpConfig http;
   std::string series_profile = "standard";  // standard | full | compact | legacy
@@ -459,6 +460,7 @@ class Engine {
   // gput and the few direct table_ calls (engine_device / engine_pods / engine_kfd_events /
   // engine_self).
   bool emit_ = true;
+  uint64_t tick_index_ = 0;  // ticks so far (render_every_ticks)
   bool leveled_ = false;        // this tick deferred the sentinel or a KFD listing (tick leveling)
   uint64_t procs_read_ns_ = 0;  // tick time of the last per-process read (process_min_interval_s)
   uint64_t counters_kick_ns_ = 0;  // tick time the last PMC read round was for (counters_min_interval_s)

@@ -24,8 +24,9 @@ def cgroup(uid: str, cid: str) -> str:
             ".slice/cri-containerd-" + cid + ".scope")
 
 
-def run(native, exposition: str, ticks: int = 6) -> str:
+def run(native, exposition: str, ticks: int = 6, render_every: int = 0) -> str:
     c = native.EngineConfig()
+    c.render_every_ticks = render_every
     c.backend = "mock"
     c.mock_devices = 8
     c.interval_s = 0

@@ -25,3 +25,21 @@ def test_engine_exposition_matches_golden(native, exposition):
         diff = "\n".join(list(difflib.unified_diff(want.split("\n"), got.split("\n"), "golden", "now",
                                                    lineterm=""))[:60])
         pytest.fail("exposition differs from the golden:\n" + diff)
+
+
+@pytest.mark.parametrize("exposition", ["classic", "compiled"])
+def test_skipped_ticks_render_the_same_exposition(native, exposition):
+    """render_when_due's skipped ticks write nothing to the series table but run every
+    computation (rates, per-pod integration of energy / busy time / xGMI bytes, KFD event
+    totals, histograms): rendering only every 3rd tick gives, on the ticks it renders, the
+    exposition an every-tick engine gives (only the render counters themselves differ)."""
+    import re
+    every = golden_engine.mask(golden_engine.run(native, exposition, ticks=6))
+    third = golden_engine.mask(golden_engine.run(native, exposition, ticks=6, render_every=3))
+
+    def samples(t):  # (the compiled body's field widths follow its own layout history: compare values)
+        t = "\n".join(" ".join(l.split()) for l in t.split("\n")
+                      if not re.match(r"gpuexp_exposition_events_total\{", l))
+        return t
+    assert samples(every) == samples(third)
+    assert 'gpuexp_exposition_events_total{event="render_skipped"}' in third or exposition == "classic"
