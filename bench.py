@@ -929,6 +929,8 @@ def main() -> int:
         prewake = [v for _, _, v in promtext.samples(fams, "gpuexp_http_prewake_wakeups_total")]
         scrapes_total = [v for _, _, v in promtext.samples(fams, "gpuexp_scrapes_total")]
         gz_where = {lab.get("where"): int(v) for _, lab, v in promtext.samples(fams, "gpuexp_gzip_compressions_total")}
+        # render_when_due: ticks that rendered nothing because no steady scraper was due (whole run)
+        expo_events = {lab.get("event"): int(v) for _, lab, v in promtext.samples(fams, "gpuexp_exposition_events_total")}
         rccl = {}
         for sname, lab, v in promtext.samples(fams, "amd_rccl_collective_bytes_total"):
             rccl.setdefault(lab.get("pod") or lab.get("pid"), {}).setdefault(lab["op"], {})["bytes"] = v
@@ -1056,6 +1058,8 @@ def main() -> int:
             # gzip copies made by the sampler (scrape expected before the next tick) and by the
             # HTTP worker for off-schedule requests (each adds one compression to that scrape)
             "gzip_compressions": gz_where or None,
+            "renders_skipped_fraction": (round(expo_events.get("render_skipped", 0) / ticks[0], 3)
+                                         if ticks and ticks[0] else None),
             # compiled exposition over the run: families laid out again, segments encoded without
             # matches while the layout settled, Huffman code builds
             "exposition_events": {lab.get("event"): int(v) for _, lab, v in
