@@ -687,17 +687,15 @@ void Engine::tick_locked(uint64_t now) {
   // writes the series table nor renders (at least one render a second); the series stage's
   // computations run all the same
   bool render_now = true;
-  if (http_ && cfg_.render_when_due && period_ns) {
-    const uint64_t tn = mono_ns();
-    render_now = !last_render_mono_ || tn < last_render_mono_ || tn - last_render_mono_ >= 1000000000ull ||
-                 http_->render_due(tn, 2 * period_ns + 5000000ull);
-    if (!render_now) ++renders_skipped_;
-  }
   ++tick_index_;
   if (cfg_.render_every_ticks > 0) {  // (tests: a scrape schedule without an HTTP server)
     render_now = tick_index_ % uint64_t(cfg_.render_every_ticks) == 0;
-    if (!render_now) ++renders_skipped_;
+  } else if (http_ && cfg_.render_when_due && period_ns) {
+    const uint64_t tn = mono_ns();
+    render_now = !last_render_mono_ || tn < last_render_mono_ || tn - last_render_mono_ >= 1000000000ull ||
+                 http_->render_due(tn, 2 * period_ns + 5000000ull);
   }
+  if (!render_now) ++renders_skipped_;
   emit_ = render_now;
 
   // 5: series
