@@ -257,6 +257,7 @@ class AmdsmiBackend : public Backend {
       *err = "amdsmi found no AMD GPUs";
       return false;
     }
+    share_socket_fetches(devices, [this](size_t i) { return devs_[i].fast_ok ? &devs_[i].gm : nullptr; });
     return true;
   }
 

@@ -256,6 +256,7 @@ bool SysfsBackend::init(std::vector<DeviceInfo>* devices, std::string* err) {
     *err = "no KFD GPU nodes under " + nodes_dir;
     return false;
   }
+  share_socket_fetches(devices, [this](size_t i) { return devs_[i]->gm_ok ? &devs_[i]->gm : nullptr; });
   return true;
 }
 

@@ -39,6 +39,9 @@ struct DeviceInfo {
   // socket-level telemetry (power, temperatures, xGMI, PCIe) is shared by all of them.
   std::string compute_partition, memory_partition;
   int partition_id = 0;        // XCP index of this logical GPU within its socket
+  // Logical GPUs of one partitioned socket (same BDF) share one gpu_metrics fetch per tick and
+  // one phase of the fetch cap (share_socket_fetches); -1 = a whole GPU, its own fetches.
+  int socket_group = -1;
   // The sysfs device behind the render node: the PCI BDF for a whole GPU and for partition
   // 0 of a partitioned socket, "amdgpu_xcp.<n>" for its other partitions (platform
   // devices).  What device plugins name a logical GPU by; unique per logical GPU where the
@@ -84,6 +87,7 @@ struct DeviceSample {
   uint64_t host_ns = 0;        // CLOCK_MONOTONIC at read
   uint64_t fw_ts_10ns = 0;     // PMFW timestamp (10 ns units), 0 = n/a
   bool metrics_coalesced = false;  // decoded from the cached gpu_metrics table (no SMU fetch)
+  bool metrics_shared = false;     // a fresh table another partition of the socket fetched this tick
   // What this sample's reads cost (filled by the backend; the engine's devices-stage split,
   // gpuexp_device_read_seconds_total): gpu_metrics wall + thread CPU (a fresh read is an
   // SMU round trip the kernel busy-waits on; ~0 when coalesced), the VRAM-used file, wall.

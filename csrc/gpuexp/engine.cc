@@ -243,6 +243,18 @@ bool Engine::start(std::string* err) {
     return d.queue_enabled;
   });
   dstate_.assign(devices_.size(), DevState());
+  {  // SMU fetch groups: a whole GPU, or the partitions of one socket (share_socket_fetches)
+    std::vector<int> sockets;
+    fetch_groups_ = 0;
+    for (const DeviceInfo& d : devices_) {
+      if (d.socket_group < 0) {
+        ++fetch_groups_;
+      } else if (std::find(sockets.begin(), sockets.end(), d.socket_group) == sockets.end()) {
+        sockets.push_back(d.socket_group);
+        ++fetch_groups_;
+      }
+    }
+  }
   for (DevState& st : dstate_) st.refs.assign(size_t(gpu_slots_), SeriesRef());
   owner_keys_.clear();
   for (const DeviceInfo& d : devices_) owner_keys_.push_back(device_owner_keys(d));
@@ -616,9 +628,9 @@ void Engine::tick_locked(uint64_t now) {
   // 8 GPUs and 10 Hz the fetches come 2,2,1,2,1 per tick and these extras had a 0.5 s period
   // too, so without it they kept landing on a two-fetch tick (the heaviest tick ~1.5x the mean).
   int fresh_now = 0;
-  for (const DevState& st : dstate_) fresh_now += st.cur.ok && !st.cur.metrics_coalesced;
+  for (const DevState& st : dstate_) fresh_now += st.cur.ok && !st.cur.metrics_coalesced && !st.cur.metrics_shared;
   leveled_ = false;
-  const bool heavy_tick = fresh_now >= 2 && fresh_now < int(dstate_.size());  // (all fresh: no lighter tick)
+  const bool heavy_tick = fresh_now >= 2 && fresh_now < fetch_groups_;  // (every group fetched: no lighter tick)
   if (counters_ && kick_late && counters_due(now)) {
     counters_kick_ns_ = now;
     round = true;

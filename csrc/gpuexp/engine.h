@@ -461,6 +461,7 @@ class Engine {
   // engine_self).
   bool emit_ = true;
   uint64_t tick_index_ = 0;  // ticks so far (render_every_ticks)
+  int fetch_groups_ = 0;     // GPUs fetching gpu_metrics on their own (a partitioned socket counts once)
   bool leveled_ = false;        // this tick deferred the sentinel or a KFD listing (tick leveling)
   uint64_t procs_read_ns_ = 0;  // tick time of the last per-process read (process_min_interval_s)
   uint64_t counters_kick_ns_ = 0;  // tick time the last PMC read round was for (counters_min_interval_s)

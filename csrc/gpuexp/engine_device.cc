@@ -271,15 +271,32 @@ void Engine::update_fetch_policy(uint64_t now) {
   const double period = cfg_.interval_s > 0 ? cfg_.interval_s * 1e9 : 0;
   double cap = std::min(sum_ns / cfg_.metrics_cpu_budget, cfg_.metrics_max_interval_s * 1e9);
   if (period > 0) cap = cap <= period ? 0 : (std::ceil(cap / period) - 0.5) * period;
-  const size_t n = dstate_.size();
+  // Phases go per fetch group: a whole GPU is its own; the partitions of one socket share one
+  // SMU fetch per tick (share_socket_fetches), so they keep one phase and fetch together.
+  std::vector<int> group(dstate_.size());
+  int n_groups = 0;
+  {
+    std::vector<int> seen;  // socket_group -> fetch group
+    for (size_t i = 0; i < dstate_.size(); ++i) {
+      const int sg = devices_[i].socket_group;
+      if (sg < 0) {
+        group[i] = n_groups++;
+        continue;
+      }
+      if (size_t(sg) >= seen.size()) seen.resize(size_t(sg) + 1, -1);
+      if (seen[size_t(sg)] < 0) seen[size_t(sg)] = n_groups++;
+      group[i] = seen[size_t(sg)];
+    }
+  }
+  const size_t n = size_t(std::max(1, n_groups));
   const int k = period > 0 && cap > 0 ? int(std::lround(cap / period + 0.5)) : 0;  // ticks per fetch
-  for (size_t i = 0; i < n; ++i) {
+  for (size_t i = 0; i < dstate_.size(); ++i) {
     DevState& st = dstate_[i];
     const double prev = double(st.fetch_cap_ns);
     // re-set only on a 5 % change (the EWMA moves a little every fresh read)
     if (std::fabs(cap - prev) <= 0.05 * std::max(cap, prev) && !(cap == 0 && prev != 0)) continue;
     st.fetch_cap_ns = uint64_t(cap);
-    const uint64_t phase = k > 1 ? uint64_t(i * size_t(k) / n) : 0;  // whole ticks
+    const uint64_t phase = k > 1 ? uint64_t(size_t(group[i]) * size_t(k) / n) : 0;  // whole ticks
     // (the cap counts from the GPU's last fresh read, this tick's or an earlier one: the phase
     // goes on top of a whole cap)
     const uint64_t not_before = phase ? now + uint64_t((double(k + phase) - 0.5) * period) : 0;

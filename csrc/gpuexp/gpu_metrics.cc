@@ -4,6 +4,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <map>
 #include <cstring>
 #include <utility>
 
@@ -78,6 +79,22 @@ bool decode_gpu_metrics_v1_8(const void* blob, size_t len, DeviceSample* out, in
   return true;
 }
 
+void share_socket_fetches(std::vector<DeviceInfo>* devs, const std::function<GpuMetricsReader*(size_t)>& reader) {
+  std::map<std::string, std::vector<size_t>> by_bdf;
+  for (size_t i = 0; i < devs->size(); ++i)
+    if (!(*devs)[i].bdf.empty()) by_bdf[(*devs)[i].bdf].push_back(i);
+  int group = 0;
+  for (const auto& kv : by_bdf) {
+    if (kv.second.size() < 2) continue;  // a whole GPU
+    auto shared = std::make_shared<GpuMetricsShared>();
+    for (size_t i : kv.second) {
+      (*devs)[i].socket_group = group;
+      if (GpuMetricsReader* r = reader(i)) r->set_shared(shared);
+    }
+    ++group;
+  }
+}
+
 GpuMetricsReader::~GpuMetricsReader() {
   if (fd_ >= 0) ::close(fd_);
 }
@@ -107,6 +124,7 @@ GpuMetricsReader& GpuMetricsReader::operator=(GpuMetricsReader&& o) noexcept {
   std::copy(o.steps_, o.steps_ + kSteps, steps_);
   nsteps_ = o.nsteps_;
   fresh_reads_ = o.fresh_reads_;
+  shared_ = std::move(o.shared_);
   coalesced_reads_ = o.coalesced_reads_;
   std::memcpy(buf_, o.buf_, sizeof(buf_));
   return *this;
@@ -163,16 +181,29 @@ bool GpuMetricsReader::read(DeviceSample* out, uint64_t now_ns) {
     out->metrics_coalesced = true;
     return decode_gpu_metrics_v1_8(buf_, size_t(last_n_), out, xcp_, nxcc_);
   }
-  const uint64_t w0 = mono_ns(), c0 = thread_cpu_ns();
-  long n = pread_once(fd_, reinterpret_cast<char*>(buf_), sizeof(buf_));
-  if (fake_cost_ns_) {
-    uint64_t c = c0;
-    while ((c = thread_cpu_ns()) - c0 < fake_cost_ns_) {
+  long n = 0;
+  if (shared_ && now_ns && shared_->tick_ns == now_ns && shared_->n > 0) {
+    // another partition of this socket fetched at this tick: the same table, no SMU round trip
+    n = shared_->n;
+    std::memcpy(buf_, shared_->buf, size_t(n));
+    out->metrics_shared = true;
+  } else {
+    const uint64_t w0 = mono_ns(), c0 = thread_cpu_ns();
+    n = pread_once(fd_, reinterpret_cast<char*>(buf_), sizeof(buf_));
+    if (fake_cost_ns_) {
+      uint64_t c = c0;
+      while ((c = thread_cpu_ns()) - c0 < fake_cost_ns_) {
+      }
+      fake_cpu_burnt_ns().fetch_add(c - c0, std::memory_order_relaxed);
     }
-    fake_cpu_burnt_ns().fetch_add(c - c0, std::memory_order_relaxed);
+    out->metrics_cpu_ns = thread_cpu_ns() - c0;
+    out->metrics_wall_ns = mono_ns() - w0;
+    if (shared_ && n > 0) {
+      std::memcpy(shared_->buf, buf_, size_t(n));
+      shared_->n = n;
+      shared_->tick_ns = now_ns;
+    }
   }
-  out->metrics_cpu_ns = thread_cpu_ns() - c0;
-  out->metrics_wall_ns = mono_ns() - w0;
   if (n <= 0) {
     last_n_ = 0;
     out->error = "gpu_metrics read failed";

@@ -14,7 +14,10 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <functional>
+#include <memory>
 #include <string>
+#include <vector>
 
 #include "gpuexp/device.h"
 
@@ -106,6 +109,15 @@ bool decode_gpu_metrics_v1_8(const void* blob, size_t len, DeviceSample* out, in
 // the reader learns the refresh period from firmware_timestamp steps and, until the next
 // expected refresh, decodes its cached copy instead of re-reading — no information is
 // lost, the kernel-side cost drops to the PMFW rate.
+// One fetched table, shared by the readers of the compute partitions of one socket (CPX:
+// eight logical GPUs, one SMU): the first partition to read fresh at a tick fetches, the others
+// decode the same blob for their own XCDs at that tick instead of asking the SMU again.
+struct GpuMetricsShared {
+  uint64_t tick_ns = 0;  // the tick (now_ns) it was fetched at (0 = never)
+  long n = 0;
+  alignas(8) unsigned char buf[8192];
+};
+
 class GpuMetricsReader {
  public:
   GpuMetricsReader() = default;
@@ -137,6 +149,8 @@ class GpuMetricsReader {
     xcp_ = xcp;
     nxcc_ = nxcc;
   }
+  // Partitions of one socket share their fetches (see GpuMetricsShared; nullptr = own fetches).
+  void set_shared(std::shared_ptr<GpuMetricsShared> s) { shared_ = std::move(s); }
   // Never reuse a table for longer than this, whatever the learnt period.
   static constexpr uint64_t kMaxCoalesceNs = 50000000;
   uint64_t period_ns() const { return period_ns_; }
@@ -164,7 +178,14 @@ class GpuMetricsReader {
   uint64_t steps_[kSteps] = {};
   int nsteps_ = 0;
   uint64_t fresh_reads_ = 0, coalesced_reads_ = 0;
+  std::shared_ptr<GpuMetricsShared> shared_;
   alignas(8) unsigned char buf_[8192];
 };
+
+// Gives the logical GPUs of each partitioned socket (the DeviceInfo entries that share a PCI
+// BDF) one GpuMetricsShared, so one SMU fetch per tick serves all of them, and a common
+// DeviceInfo::socket_group (the engine phases the fetch cap per socket).  `reader(i)` is device
+// i's reader (nullptr: none).  Whole GPUs are left alone.
+void share_socket_fetches(std::vector<DeviceInfo>* devs, const std::function<GpuMetricsReader*(size_t)>& reader);
 
 }  // namespace gpuexp

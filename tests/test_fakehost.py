@@ -1188,3 +1188,43 @@ def test_tick_leveling_moves_extras_off_two_fetch_ticks(native, tmp_path):
     # heaviest tick at most 1.35x the mean (two fetches against 1.6 on average)
     burnt = [r[4] for r in steady]
     assert max(burnt) <= 1.35 * sum(burnt) / len(burnt), (max(burnt), sum(burnt) / len(burnt))
+
+
+def test_cpx_partitions_share_one_smu_fetch_per_tick(native, tmp_path):
+    """The 8 logical GPUs of a CPX socket read one gpu_metrics table: one SMU fetch per tick
+    serves all of them (each decodes its own XCD's slice), instead of eight -- at 382 us of
+    kernel CPU a fetch, 3 ms per tick at 10 Hz.  The fetch cap counts the socket once, and every
+    partition still gets a fresh table each tick it is due."""
+    import time
+    from kubernetes_gpu_exporter_amd.utils.fakehost import mi355x_cpx_socket
+    h = mi355x_cpx_socket(tmp_path)
+    for g in h.gpus:
+        h.set_metrics(g, gfx=50, accum=1000, num_partition=8)
+    c = native.EngineConfig()
+    c.backend = "sysfs"
+    c.host_root = str(tmp_path)
+    c.interval_s = 0.1
+    c.sampler_thread = False
+    c.serve_http = False
+    c.series_profile = "full"
+    c.fake_metrics_cost_us = SMU_FETCH_CPU_US
+    e = native.Engine(c)
+    e.start()
+    try:
+        now = time.monotonic_ns()
+        burnt, fresh = [], []
+        for _ in range(20):
+            now += 100_000_000
+            s0 = e.stats()
+            e.tick(now)
+            s1 = e.stats()
+            burnt.append((s1["fake_cpu_burnt_ns"] - s0["fake_cpu_burnt_ns"]) / 1e3)
+            fresh.append(s1["last_tick_fresh"])
+        fams = promtext.parse(e.snapshot_text())
+    finally:
+        e.stop()
+    assert max(fresh) == 1, fresh  # one real fetch per tick for the whole socket
+    assert max(burnt) < 1.5 * SMU_FETCH_CPU_US, burnt  # not 8 x 382 us
+    reads = {(s[1]["gpu"], s[1]["kind"]): s[2] for s in fams["gpuexp_gpu_metrics_reads_total"].samples}
+    fresh_per_gpu = {reads[(str(k), "fresh")] for k in range(8)}
+    assert len(fresh_per_gpu) == 1 and fresh_per_gpu.pop() >= 18, reads  # every partition fresh every tick
