@@ -175,6 +175,18 @@ PYBIND11_MODULE(_gpuexp, m) {
     if (!gpuexp::parse_bad_pages(body, &t)) return py::none();
     return py::make_tuple(int(t.pages_retired), int(t.pages_pending), int(t.pages_unreservable));
   }, "Parses ras/gpu_vram_bad_pages: (retired, pending, unreservable) or None");
+  m.def("kfd_events_drain_fds", [](std::vector<int> fds, int rounds) {
+    // drains non-blocking fds (pipes standing in for KFD's SMI event fds) `rounds` times
+    KfdEventSource src;
+    src.adopt_fds(fds);
+    std::vector<std::tuple<int, int, int>> all;
+    for (int r = 0; r < rounds; ++r) {
+      std::vector<KfdEvent> evs;
+      src.drain(&evs);
+      for (const KfdEvent& e : evs) all.emplace_back(e.dev, e.event, e.pid);
+    }
+    return all;
+  });
   m.def("parse_kfd_event", [](py::bytes b) -> py::object {
     std::string s(b);
     int ev = 0, pid = -1;

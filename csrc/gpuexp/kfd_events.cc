@@ -2,6 +2,7 @@
 
 #include <fcntl.h>
 #include <linux/kfd_ioctl.h>
+#include <poll.h>
 #include <sys/ioctl.h>
 #include <unistd.h>
 
@@ -141,9 +142,17 @@ int KfdEventSource::open(const std::vector<DeviceInfo>& devs, const std::string&
 }
 
 void KfdEventSource::drain(std::vector<KfdEvent>* out) {
+  // one poll over every GPU's event fd per tick (a quiet node: one system call, not one read
+  // per GPU); only the readable ones are read
+  pfds_.clear();
+  for (size_t i = 0; i < fds_.size(); ++i)
+    if (fds_[i] >= 0) pfds_.push_back({fds_[i], POLLIN, 0});
+  if (pfds_.empty() || ::poll(pfds_.data(), nfds_t(pfds_.size()), 0) <= 0) return;
   char buf[4096];
+  size_t p = 0;
   for (size_t i = 0; i < fds_.size(); ++i) {
     if (fds_[i] < 0) continue;
+    if (!(pfds_[p++].revents & (POLLIN | POLLERR | POLLHUP))) continue;
     for (int rounds = 0; rounds < 16; ++rounds) {  // the kernel FIFO is small: a few reads empty it
       const ssize_t r = ::read(fds_[i], buf, sizeof(buf));
       if (r <= 0) break;  // EAGAIN: empty

@@ -17,6 +17,8 @@
 #include <string>
 #include <vector>
 
+#include <poll.h>
+
 #include "gpuexp/device.h"
 
 namespace gpuexp {
@@ -73,6 +75,11 @@ class KfdEventSource {
   void close_all();
   size_t devices() const { return partial_.size(); }
   void set_devices(size_t n) { partial_.assign(n, std::string()); fds_.assign(n, -1); }
+  // Tests: drain() these (non-blocking) fds as devices 0..n-1 instead of KFD's (owned: closed).
+  void adopt_fds(const std::vector<int>& fds) {
+    set_devices(fds.size());
+    fds_ = fds;
+  }
   // CAP_SYS_ADMIN was effective at open: every process's per-process events are delivered.
   bool all_processes() const { return all_processes_; }
   uint64_t malformed() const { return malformed_; }
@@ -80,6 +87,7 @@ class KfdEventSource {
  private:
   int kfd_fd_ = -1;
   std::vector<int> fds_;
+  std::vector<struct pollfd> pfds_;  // drain()'s poll set (reused)
   std::vector<std::string> partial_;
   bool all_processes_ = false;
   uint64_t malformed_ = 0;

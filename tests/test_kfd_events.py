@@ -107,3 +107,20 @@ def test_pod_kfd_event_totals_expire_under_partial_pod_lists(native, mock_engine
     fams = promtext.parse(e.snapshot_text())
     assert not promtext.samples(fams, "amd_pod_gpu_energy_joules_total")
     assert pod(fams) == {}
+
+
+def test_drain_polls_every_gpu_fd_and_reads_only_the_ready_ones(native):
+    """KfdEventSource.drain: one poll over all GPUs' event fds, then reads of the readable ones
+    (pipes stand in for KFD's SMI event fds): events of two GPUs among four, a trailing partial
+    line kept back, and a second drain with every fd quiet."""
+    import os
+    pipes = [os.pipe() for _ in range(4)]
+    for r, _ in pipes:
+        os.set_blocking(r, False)
+    os.write(pipes[1][1], b"1 1092:python3\n")              # GPU 1: a VM fault of pid 0x1092
+    os.write(pipes[3][1], b"9 100 -4242 0 2\n2 0:")         # GPU 3: an eviction of 4242 + half a line
+    # two drains: the second finds every fd quiet (the poll returns 0, nothing is read)
+    got = native.kfd_events_drain_fds([r for r, _ in pipes], 2)  # (the source owns and closes the read ends)
+    assert sorted(got) == [(1, 1, 0x1092), (3, 9, 4242)], got
+    for _, w in pipes:
+        os.close(w)
