@@ -918,7 +918,12 @@ class QueueSentinel : public gpuexp::SentinelSource {
 
   bool read(int dev, gpuexp::SentinelReading* out) override {
     if (dev < 0 || size_t(dev) >= per_.size() || !per_[size_t(dev)].ready) return false;
-    return gpuexp::sentinel_fill(per_[size_t(dev)].run, out);
+    Per& p = per_[size_t(dev)];
+    // every tick (the sampler's thread, like tick()): a completed run is folded in and the
+    // outstanding one's pending time is current -- the launches alone run at most every
+    // sentinel_min_interval, and a pending time sampled only then read in 0.5 s steps
+    if (!p.a->broken && !p.a->queue_error.load()) gpuexp::sentinel_drain(p.run, nslots_, sys_ns_per_tick_);
+    return gpuexp::sentinel_fill(p.run, out);
   }
 
   void stop() override {

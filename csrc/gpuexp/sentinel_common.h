@@ -68,8 +68,8 @@ struct SentinelRun {
   hsa_agent_t agent{};
   bool have_agent = false;
   uint64_t launched = 0, completed = 0, stalled = 0, errors = 0;
-  // at the last drain (the start of a tick, before its launch): age of the oldest run still
-  // outstanding, 0 when every earlier launch had finished
+  // at the last drain (every tick's read, and each launch tick before its launch): age of the
+  // oldest run still outstanding, 0 when every earlier launch had finished
   double pending_s = 0;
   SentinelReading last;
 };
