@@ -913,6 +913,7 @@ class QueueSentinel : public gpuexp::SentinelSource {
       std::memcpy(ka, &args, sizeof(args));
       dispatch(*p.a, p.run_k, ka, uint32_t(p.run.waves), hsa_signal_t{0});
       p.run.launched = seq;
+      p.run.fresh_seq = seq;
     }
   }
 
@@ -922,8 +923,8 @@ class QueueSentinel : public gpuexp::SentinelSource {
     // every tick (the sampler's thread, like tick()): a completed run is folded in and the
     // outstanding one's pending time is current -- the launches alone run at most every
     // sentinel_min_interval, and a pending time sampled only then read in 0.5 s steps
-    if (!p.a->broken && !p.a->queue_error.load()) gpuexp::sentinel_drain(p.run, nslots_, sys_ns_per_tick_);
-    return gpuexp::sentinel_fill(p.run, out);
+    if (p.a->broken || p.a->queue_error.load()) return gpuexp::sentinel_fill(p.run, out);
+    return gpuexp::sentinel_read(p.run, nslots_, sys_ns_per_tick_, out);
   }
 
   void stop() override {

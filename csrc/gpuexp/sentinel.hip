@@ -197,6 +197,7 @@ class HipSentinel : public SentinelSource {
         continue;
       }
       p.run.launched = seq;
+      p.run.fresh_seq = seq;
     }
   }
 
@@ -204,8 +205,7 @@ class HipSentinel : public SentinelSource {
     if (dev < 0 || size_t(dev) >= per_.size() || !per_[size_t(dev)].ready) return false;
     // every tick: completions folded in and the pending time current (launches run at most
     // every sentinel_min_interval)
-    sentinel_drain(per_[size_t(dev)].run, nslots_, sys_ns_per_tick_);
-    return sentinel_fill(per_[size_t(dev)].run, out);
+    return sentinel_read(per_[size_t(dev)].run, nslots_, sys_ns_per_tick_, out);
   }
 
   void stop() override {

@@ -71,6 +71,9 @@ struct SentinelRun {
   // at the last drain (every tick's read, and each launch tick before its launch): age of the
   // oldest run still outstanding, 0 when every earlier launch had finished
   double pending_s = 0;
+  // the run launched at this tick (0: none): it is not "waiting" when the same tick reads it
+  // microseconds later (sentinel_read)
+  uint64_t fresh_seq = 0;
   SentinelReading last;
 };
 
@@ -144,6 +147,16 @@ inline bool sentinel_fill(const SentinelRun& p, SentinelReading* out) {
   out->runs = p.completed;
   out->pending_s = p.pending_s;
   return true;
+}
+
+// A sampler tick's read of GPU `p`: folds in completed runs and brings pending_s up to date
+// (every tick, although launches run at most every sentinel_min_interval); a run launched by
+// this same tick counts as not pending yet.
+inline bool sentinel_read(SentinelRun& p, int nslots, double sys_ns_per_tick, SentinelReading* out) {
+  sentinel_drain(p, nslots, sys_ns_per_tick);
+  if (p.fresh_seq && p.completed + 1 == p.fresh_seq) p.pending_s = 0;
+  p.fresh_seq = 0;
+  return sentinel_fill(p, out);
 }
 
 // Marks run `seq`'s slots unpublished and returns the slot it uses.
