@@ -369,7 +369,14 @@ def main() -> int:
     # ranks of one launch share the directory the exporter watches.
     rccl_dir = ""
     tracer = os.path.join(ROOT, "kubernetes_gpu_exporter_amd", "libgpuexp_rccl_tracer.so")
-    if args.rccl_trace and args.backend != "mock" and os.path.exists(tracer) and os.path.exists("/dev/kfd"):
+    # under rocprofv3 (its preloaded rocprofiler-sdk tool owns the tool slot, so the tracer would
+    # never attach and every pod would miss its communicator): no RCCL tracing in that run
+    under_rocprof = "rocprofiler-sdk" in os.environ.get("LD_PRELOAD", "") or \
+        any(k.startswith("ROCPROF_") for k in os.environ)
+    if args.rccl_trace and under_rocprof and rank == 0:
+        print("[bench] under rocprofv3: RCCL tracing off for this run", file=sys.stderr, flush=True)
+    if args.rccl_trace and not under_rocprof and args.backend != "mock" and os.path.exists(tracer) and \
+            os.path.exists("/dev/kfd"):
         # one directory per launch, shared by its ranks (torchrun's static rendezvous names
         # every run "none", so the port tells back-to-back launches apart)
         run_id = "-".join(v for v in (os.environ.get("TORCHELASTIC_RUN_ID"), os.environ.get("MASTER_PORT")) if v) \
