@@ -5,9 +5,14 @@
 //   - a control-plane thread swapping pods / cgroup overrides / process lists / faults
 //   - an RCCL-tracer stand-in that rewrites, truncates and replaces its counters file
 //     (the exporter's writer proof maps the file itself, see optional_sources.cc)
+//   - then a steady phase: one scraper at a fixed 40 ms period alone, so the sampler skips the
+//     ticks no scrape reads (render_when_due: no table writes, no render) while the
+//     control-plane and tracer threads keep going
 // Every response must be a complete exposition whose tick counter never goes backwards.
 // SURVEY.md §5 "Race detection / sanitizers": sampler vs HTTP vs attribution updates.
+#include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -99,19 +104,19 @@ int main(int argc, char** argv) {
     return 2;
   }
   int port = e.http_port();
-  std::atomic<bool> stop{false};
+  std::atomic<bool> stop{false}, stop_busy{false};
   std::atomic<long> scrapes{0}, bad{0}, rccl_seen{0};
 
-  std::vector<std::thread> th;
+  std::vector<std::thread> th, busy;
   for (int s = 0; s < scrapers; ++s) {
-    th.emplace_back([&, s] {
+    busy.emplace_back([&, s] {
       // scraper 0: gzip; scraper 1: protobuf exposition; the rest: plain text
       ScrapeClient c("127.0.0.1", port, "/metrics", s == 0, 2000,
                      s == 1 ? "application/vnd.google.protobuf;proto=io.prometheus.client.MetricFamily;"
                               "encoding=delimited"
                             : "");
       double last = -1;
-      while (!stop.load()) {
+      while (!stop_busy.load()) {
         double ns = c.scrape();
         if (ns < 0 || c.last_status() == 503) continue;
         scrapes.fetch_add(1);
@@ -204,6 +209,30 @@ int main(int argc, char** argv) {
     });
   }
   std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
+  stop_busy.store(true);
+  for (auto& t : busy) t.join();
+  // steady phase: one keep-alive scraper at a fixed period, everything else still churning
+  long steady_scrapes = 0;
+  const uint64_t skipped0 = e.stats().renders_skipped;
+  {
+    ScrapeClient c("127.0.0.1", port, "/metrics", true, 2000, "");
+    double last = -1;
+    auto next = std::chrono::steady_clock::now();
+    const auto end = next + std::chrono::duration<double>(std::max(1.0, seconds / 2));
+    while (next < end) {
+      double ns = c.scrape();
+      std::string inflated;
+      if (ns >= 0 && c.last_status() == 200) {
+        ++steady_scrapes;
+        const double t = gunzip(c.last_body(), &inflated) ? ticks_in(inflated) : -2;
+        if (t < last) bad.fetch_add(1);  // (a skipped tick serves the last render: never older than it)
+        last = t;
+      }
+      next += std::chrono::milliseconds(40);
+      std::this_thread::sleep_until(next);
+    }
+  }
+  const uint64_t skipped = e.stats().renders_skipped - skipped0;
   stop.store(true);
   for (auto& t : th) t.join();
   EngineStats st = e.stats();
@@ -213,9 +242,10 @@ int main(int argc, char** argv) {
     ::unlink(rccl_path.c_str());
     ::rmdir(rccl_dir.c_str());
   }
-  std::printf("ticks=%llu scrapes=%ld bad=%ld series=%llu render_bytes=%llu rccl_scrapes=%ld\n",
+  std::printf("ticks=%llu scrapes=%ld bad=%ld series=%llu render_bytes=%llu rccl_scrapes=%ld steady_scrapes=%ld "
+              "renders_skipped=%llu\n",
               (unsigned long long)st.ticks, scrapes.load(), bad.load(), (unsigned long long)st.series,
-              (unsigned long long)st.render_bytes, rccl_seen.load());
+              (unsigned long long)st.render_bytes, rccl_seen.load(), steady_scrapes, (unsigned long long)skipped);
   // (a sanitizer build on a loaded host ticks slowly: the point is the races, not the rate)
   return (bad.load() == 0 && scrapes.load() > 100 && st.ticks >= 5) ? 0 : 1;
 }
