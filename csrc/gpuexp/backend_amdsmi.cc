@@ -114,6 +114,7 @@ class AmdsmiBackend : public Backend {
     int validated_fields = 0;
     uint64_t raw_failures = 0;  // __atomic_* access: sampler writes, describe() reads
     CachedFile vram_used_file;
+    uint32_t socket = 0;  // index of its amdsmi socket handle (the partitions of one GPU share it)
     double power_cap_w = kNaN;
     int xcp = 0, nxcc = 0;  // compute partition of this logical GPU (see DeviceInfo)
     std::vector<amdsmi_proc_info_t> procbuf = std::vector<amdsmi_proc_info_t>(64);
@@ -159,6 +160,7 @@ class AmdsmiBackend : public Backend {
           continue;
         Dev d;
         d.h = ph[p];
+        d.socket = s;
         DeviceInfo info;
         amdsmi_bdf_t bdf{};
         if (amdsmi_get_gpu_device_bdf(d.h, &bdf) == AMDSMI_STATUS_SUCCESS) {
@@ -257,7 +259,9 @@ class AmdsmiBackend : public Backend {
       *err = "amdsmi found no AMD GPUs";
       return false;
     }
-    share_socket_fetches(devices, [this](size_t i) { return devs_[i].fast_ok ? &devs_[i].gm : nullptr; });
+    // (the partitions of a socket are the GPU processors of one amdsmi socket handle)
+    share_socket_fetches(devices, [this](size_t i) { return devs_[i].fast_ok ? &devs_[i].gm : nullptr; },
+                         [this](size_t i) { return std::to_string(devs_[i].socket); });
     return true;
   }
 

@@ -79,10 +79,13 @@ bool decode_gpu_metrics_v1_8(const void* blob, size_t len, DeviceSample* out, in
   return true;
 }
 
-void share_socket_fetches(std::vector<DeviceInfo>* devs, const std::function<GpuMetricsReader*(size_t)>& reader) {
+void share_socket_fetches(std::vector<DeviceInfo>* devs, const std::function<GpuMetricsReader*(size_t)>& reader,
+                          const std::function<std::string(size_t)>& socket) {
   std::map<std::string, std::vector<size_t>> by_bdf;
-  for (size_t i = 0; i < devs->size(); ++i)
-    if (!(*devs)[i].bdf.empty()) by_bdf[(*devs)[i].bdf].push_back(i);
+  for (size_t i = 0; i < devs->size(); ++i) {
+    const std::string key = socket ? socket(i) : (*devs)[i].bdf;
+    if (!key.empty()) by_bdf[key].push_back(i);
+  }
   int group = 0;
   for (const auto& kv : by_bdf) {
     if (kv.second.size() < 2) continue;  // a whole GPU

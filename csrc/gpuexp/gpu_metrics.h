@@ -182,10 +182,12 @@ class GpuMetricsReader {
   alignas(8) unsigned char buf_[8192];
 };
 
-// Gives the logical GPUs of each partitioned socket (the DeviceInfo entries that share a PCI
-// BDF) one GpuMetricsShared, so one SMU fetch per tick serves all of them, and a common
-// DeviceInfo::socket_group (the engine phases the fetch cap per socket).  `reader(i)` is device
-// i's reader (nullptr: none).  Whole GPUs are left alone.
-void share_socket_fetches(std::vector<DeviceInfo>* devs, const std::function<GpuMetricsReader*(size_t)>& reader);
+// Gives the logical GPUs of each partitioned socket one GpuMetricsShared, so one SMU fetch per
+// tick serves all of them, and a common DeviceInfo::socket_group (the engine phases the fetch
+// cap per socket).  The socket of device i is `socket(i)` (default: its PCI BDF, which KFD
+// gives every partition of a socket; amdsmi: its socket handle).  `reader(i)` is device i's
+// reader (nullptr: none).  Whole GPUs (alone on their socket) are left alone.
+void share_socket_fetches(std::vector<DeviceInfo>* devs, const std::function<GpuMetricsReader*(size_t)>& reader,
+                          const std::function<std::string(size_t)>& socket = nullptr);
 
 }  // namespace gpuexp
