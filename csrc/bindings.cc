@@ -731,6 +731,7 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("process_min_interval_s", &EngineConfig::process_min_interval_s)
       .def_readwrite("sentinel_min_interval_s", &EngineConfig::sentinel_min_interval_s)
       .def_readwrite("counters_min_interval_s", &EngineConfig::counters_min_interval_s)
+      .def_readwrite("counters_cpu_budget", &EngineConfig::counters_cpu_budget)
       .def_readwrite("queue_devices", &EngineConfig::queue_devices)
       .def_readwrite("queue_devices_bdf", &EngineConfig::queue_devices_bdf)
       .def_readwrite("force_amdsmi_metrics", &EngineConfig::force_amdsmi_metrics)
@@ -795,6 +796,9 @@ PYBIND11_MODULE(_gpuexp, m) {
         d["kfd_lists"] = s.kfd_lists;
         d["leveled_ticks"] = s.leveled_ticks;
         d["renders_skipped"] = s.renders_skipped;
+        d["counter_rounds"] = s.counter_rounds;
+        d["counters_round_cpu_ns"] = s.counters_round_cpu_ns;
+        d["counters_round_interval_s"] = s.counters_round_interval_s;
         d["render_bytes"] = s.render_bytes;
         d["series"] = s.series;
         d["device_errors"] = s.device_errors;

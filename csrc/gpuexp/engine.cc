@@ -122,6 +122,36 @@ int Engine::counters_interval_ms() const {
   return std::max(10, int(std::max(cfg_.interval_s, cfg_.counters_min_interval_s) * 2000));
 }
 
+// counters_cpu_budget: a finished read round's CPU (this thread's kick + sync, and the plugin
+// thread's since the last round) goes into a per-round EWMA; the rounds' minimum interval becomes
+// EWMA / budget when that is longer than both counters_min_interval_s and a tick, rounded up to
+// whole ticks and at most 2 x max(counters_min_interval_s, tick) -- the plugin's fallback interval
+// (counters_interval_ms) is twice that, so a window is never taken for stale.  8 MI355X GPUs at
+// ~15 us per read: 120 us per round -> 16 ms, no change; a CPX node's 64 partitions at that cost:
+// ~0.9 ms per round -> 120 ms, a round every 2nd tick at 10 Hz, every 10th at 100 Hz.
+void Engine::counters_round_done() {
+  uint64_t c = counters_round_acc_ns_;
+  counters_round_acc_ns_ = 0;
+  const uint64_t p = counters_->cpu_ns();
+  const bool first = counter_rounds_++ == 0;  // (the first round carries the plugin's start-up)
+  if (p >= counters_round_plugin_seen_) c += p - counters_round_plugin_seen_;
+  counters_round_plugin_seen_ = p;
+  if (first) return;
+  counters_round_cpu_ns_ = counters_round_cpu_ns_ > 0 ? 0.9 * counters_round_cpu_ns_ + 0.1 * double(c) : double(c);
+  const double period = cfg_.interval_s * 1e9, base = cfg_.counters_min_interval_s * 1e9;
+  double iv = 0;
+  if (cfg_.counters_cpu_budget > 0 && period > 0) {
+    const double want = std::min(counters_round_cpu_ns_ / cfg_.counters_cpu_budget, 2 * std::max(base, period));
+    if (want > base && want > period) iv = std::max(base, std::ceil(want / period - 1e-6) * period);
+  }
+  counters_round_iv_ns_ = iv;
+}
+
+double Engine::counters_round_interval_s() const {
+  if (!counters_) return 0;
+  return (counters_round_iv_ns_ > 0 ? counters_round_iv_ns_ : cfg_.counters_min_interval_s * 1e9) * 1e-9;
+}
+
 // Registers a source's family table: SeriesTable ids, and handle slots per GPU or global.
 void Engine::register_families(const std::vector<FamilySpec>& specs) {
   for (const FamilySpec& f : specs) {
@@ -565,16 +595,24 @@ void Engine::tick_locked(uint64_t now) {
   const std::string& kick_mode = counters_kick_mode_;
   const bool kick_late = kick_mode == "after_devices";
   const bool kick_end = kick_mode == "end";
-  // (rounds at most every counters_min_interval_s: above that rate a tick exports the last window)
+  // (rounds at most every counters_min_interval_s, or longer under counters_cpu_budget: in
+  // between a tick exports the last window)
   const uint64_t period_ns = cfg_.interval_s > 0 ? uint64_t(cfg_.interval_s * 1e9) : 0;
+  const uint64_t ctr_iv = counters_round_iv_ns_ > 0 ? uint64_t(counters_round_iv_ns_)
+                                                    : uint64_t(cfg_.counters_min_interval_s * 1e9);
   auto counters_due = [&](uint64_t t) {
-    return !period_ns || !counters_kick_ns_ || t < counters_kick_ns_ ||
-           t - counters_kick_ns_ + period_ns / 2 >= uint64_t(cfg_.counters_min_interval_s * 1e9);
+    return !period_ns || !counters_kick_ns_ || t < counters_kick_ns_ || t - counters_kick_ns_ + period_ns / 2 >= ctr_iv;
+  };
+  // a round's CPU on this thread (kick + sync), for counters_cpu_budget
+  auto kick_counters = [&] {
+    const uint64_t k0 = thread_cpu_ns();
+    counters_->kick();
+    counters_round_acc_ns_ += thread_cpu_ns() - k0;
   };
   bool round = kick_end && counters_round_next_;  // kicked at the end of the previous tick
   counters_round_next_ = false;
   if (counters_ && !kick_late && !kick_end && counters_due(now)) {
-    counters_->kick();
+    kick_counters();
     counters_kick_ns_ = now;
     round = true;
     part[0] = mono_ns() - ts[0];
@@ -635,7 +673,7 @@ void Engine::tick_locked(uint64_t now) {
     counters_kick_ns_ = now;
     round = true;
     const uint64_t k0 = mono_ns();
-    counters_->kick();
+    kick_counters();
     part[0] = mono_ns() - k0;
   }
   ts[1] = mono_ns();
@@ -690,7 +728,12 @@ void Engine::tick_locked(uint64_t now) {
   ts[4] = mono_ns();
   cs[4] = cpu_mark();
   // 4: counters: wait (bounded) for this tick's read round; sampled in collect_device
-  if (counters_ && round && !counters_->sync(cfg_.counters_sync_us)) counters_late_ += 1;
+  if (counters_ && round) {
+    const uint64_t s0 = thread_cpu_ns();
+    if (!counters_->sync(cfg_.counters_sync_us)) counters_late_ += 1;
+    counters_round_acc_ns_ += thread_cpu_ns() - s0;
+    counters_round_done();
+  }
   ts[5] = mono_ns();
   cs[5] = cpu_mark();
 
@@ -765,7 +808,7 @@ void Engine::tick_locked(uint64_t now) {
   }
   if (!cfg_.state_file.empty() && ts[7] - state_saved_ns_ >= uint64_t(cfg_.state_interval_s * 1e9)) save_state();
   if (counters_ && kick_end && counters_due(now + period_ns)) {  // next tick's read, completing while we sleep
-    counters_->kick();
+    kick_counters();
     counters_kick_ns_ = now + period_ns;
     counters_round_next_ = true;
   }
@@ -793,6 +836,9 @@ void Engine::tick_locked(uint64_t now) {
     stats_.leveled_ticks += leveled_ ? 1 : 0;
     if (slot < 0 && render_now) stats_.publish_skipped += 1;
     stats_.renders_skipped = renders_skipped_;
+    stats_.counter_rounds = counter_rounds_;
+    stats_.counters_round_cpu_ns = counters_round_cpu_ns_;
+    stats_.counters_round_interval_s = counters_round_interval_s();
     stats_.last_tick_ns = tend - ts[0];
     stats_.max_tick_ns = std::max(stats_.max_tick_ns, stats_.last_tick_ns);
     stats_.tick_ns_total += stats_.last_tick_ns;

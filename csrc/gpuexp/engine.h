@@ -142,6 +142,11 @@ struct EngineConfig {
   // continuous: a PMC read round at most this often (0 = every tick).  Each round costs host CPU
   // per GPU (packet + output reduction); above 20 Hz a tick exports the last window again.
   double counters_min_interval_s = 0.05;
+  // continuous + periodic ticks: the read rounds together may use this share of one core (0 = no
+  // cap).  A round's CPU grows with the logical GPUs (a CPX node has 64 PMC reads per round); when
+  // the measured round CPU / this share exceeds counters_min_interval_s, rounds come that much less
+  // often, at most half as often (a window never gets older than two round intervals + a tick).
+  double counters_cpu_budget = 0.0075;
   // continuous: when a tick's PMC read goes out.  "start": before the device reads;
   // "after_devices": once the gpu_metrics SMU fetches are done (a PM4 read in flight while
   // the SMU serves the metrics table slows the fetch, profiles/r04/devices_split.txt).
@@ -218,6 +223,11 @@ struct EngineStats {
   uint64_t fresh_reads = 0, sentinel_runs = 0, kfd_lists = 0, leveled_ticks = 0;
   uint64_t last_tick_fresh = 0;  // SMU fetches the last tick carried
   uint64_t renders_skipped = 0;  // ticks that published nothing: no scrape due (render_when_due)
+  // continuous counters: read rounds so far, their CPU (EWMA per round, the sampler's kick + sync
+  // and the plugin thread's), and the current minimum round interval (counters_min_interval_s, or
+  // longer under counters_cpu_budget)
+  uint64_t counter_rounds = 0;
+  double counters_round_cpu_ns = 0, counters_round_interval_s = 0;
 };
 
 class Engine {
@@ -465,7 +475,12 @@ class Engine {
   bool leveled_ = false;        // this tick deferred the sentinel or a KFD listing (tick leveling)
   uint64_t procs_read_ns_ = 0;  // tick time of the last per-process read (process_min_interval_s)
   uint64_t counters_kick_ns_ = 0;  // tick time the last PMC read round was for (counters_min_interval_s)
-  bool counters_round_next_ = false;  // "end" kick: the next tick has a round to sync  // cfg_.counters_kick with "auto" resolved
+  bool counters_round_next_ = false;  // "end" kick: the next tick has a round to sync
+  // counters_cpu_budget: CPU of the round in flight so far, EWMA per round, current interval
+  uint64_t counters_round_acc_ns_ = 0, counter_rounds_ = 0, counters_round_plugin_seen_ = 0;
+  double counters_round_cpu_ns_ = 0, counters_round_iv_ns_ = 0;
+  void counters_round_done();
+  double counters_round_interval_s() const;  // cfg_.counters_kick with "auto" resolved
   std::string sentinel_status_ = "disabled", counters_status_ = "disabled";
 
   SeriesTable table_;

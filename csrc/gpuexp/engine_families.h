@@ -59,7 +59,7 @@ enum Fam : int {
   kFamSelfPrewakeHitsNarrow, kFamSelfPrewakeSpins, kFamSelfPrewakeSpinS, kFamSelfRxMoves, kFamSelfGzip,
   kFamSelfRenderBytes, kFamSelfExpo, kFamSelfSeries, kFamSelfDevErrors, kFamSelfOverruns, kFamSelfCpu,
   kFamSelfSourceUp, kFamSelfMetricsReads, kFamSelfMetricsPeriod, kFamSelfUnresolved, kFamSelfCtrLate,
-  kFamSelfCtrEvents, kFamSelfCtrRescue, kFamSelfCtrScope,
+  kFamSelfCtrEvents, kFamSelfCtrRescue, kFamSelfCtrScope, kFamSelfCtrInterval,
   kFamCount
 };
 

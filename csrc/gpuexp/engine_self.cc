@@ -134,6 +134,11 @@ const std::vector<FamilySpec>& self_family_specs() {
        "Ticks that exported the previous counter window because this tick's PMC read had not "
        "completed within counters_sync_us (continuous counters)",
        C, N, {}, kGlobal, 1},
+      {kFamSelfCtrInterval, "gpuexp_counters_round_interval_seconds",
+       "Current minimum interval between PMC read rounds (continuous counters): "
+       "counters_min_interval, or longer when the measured round CPU / counters_cpu_budget is "
+       "(many logical GPUs, e.g. a CPX node); between rounds a tick exports the last window",
+       G, N, {}, kGlobal, 1},
       {kFamSelfCtrEvents, "gpuexp_counters_events_total",
        "PMC read health per GPU: read_stall (a read still queued at the round's end), "
        "reset (a window dropped: counters went backwards), rearm (counting restarted after "
@@ -229,7 +234,10 @@ void Engine::emit_self(uint64_t gen) {
   gput(kFamSelfSourceUp, 2, (counters_ || (cfg_.enable_counters && mock_)) ? 1 : 0, gen,
        [] { return std::vector<std::string>{"counters"}; });
   gput(kFamSelfSourceUp, 3, rccl_ ? 1 : 0, gen, [] { return std::vector<std::string>{"rccl"}; });
-  if (counters_ && cfg_.counters_mode == "continuous") gput(kFamSelfCtrLate, 0, double(counters_late_), gen, none);
+  if (counters_ && cfg_.counters_mode == "continuous") {
+    gput(kFamSelfCtrLate, 0, double(counters_late_), gen, none);
+    if (cfg_.interval_s > 0) gput(kFamSelfCtrInterval, 0, counters_round_interval_s(), gen, none);
+  }
   if (cfg_.enable_kfd_events && cfg_.series_profile == "full")
     gput(kFamSelfSourceUp, 4, kfd_events_ ? 1 : 0, gen, [] { return std::vector<std::string>{"kfd_events"}; });
   if (cfg_.series_profile == "full")

@@ -71,6 +71,7 @@ class Config:
     counters_kick: str = "auto"            # continuous: a tick's PMC read goes out at its start | after_devices |
                                            # end of the previous tick | auto (end below 50 ms ticks, else start)
     counters_min_interval: float = 0.05    # continuous counters: a PMC read round at most this often (s)
+    counters_cpu_budget: float = 0.75      # continuous counters: % of one core the read rounds may use (0 = no cap)
     counters_inline: bool = True           # continuous: the sampler posts/collects each tick's PMC read itself
     http_follow_rx_cpu: bool = False       # pin the HTTP worker to the CPU a steady scraper's requests arrive on
     queue_devices: list = field(default_factory=list)  # GPUs (indices / BDFs) that get the exporter's
@@ -188,6 +189,7 @@ class Config:
         ec.counters_kick = str(self.counters_kick)
         ec.counters_inline = bool(self.counters_inline)
         ec.counters_min_interval_s = float(self.counters_min_interval)
+        ec.counters_cpu_budget = float(self.counters_cpu_budget) / 100.0
         ec.enable_rccl = bool(self.enable_rccl)
         ec.rccl_dir = self.rccl_dir
         ec.rccl_verify = bool(self.rccl_verify)
@@ -330,6 +332,8 @@ def validate(cfg: Config) -> None:
         raise ValueError(f"metrics_min_interval must be 'auto' or seconds >= 0, got {cfg.metrics_min_interval!r}")
     if not (0 <= cfg.metrics_cpu_budget <= 100):
         raise ValueError("metrics_cpu_budget must be a percentage of one core, 0-100 (0 = no cap under auto)")
+    if not (0 <= cfg.counters_cpu_budget <= 100):
+        raise ValueError("counters_cpu_budget must be a percentage of one core, 0-100 (0 = no cap)")
     normalize_prewake(cfg.http_prewake)
     if cfg.exposition not in ("compiled", "classic"):
         raise ValueError(f"exposition must be compiled|classic, got {cfg.exposition}")

@@ -280,6 +280,26 @@ def mi355x_cpx_socket(root, bus: int = 0x72, partitions: int = 8, xcp_files: boo
     return h
 
 
+def mi355x_cpx_node(root, sockets: int = 8, partitions: int = 8) -> FakeHost:
+    """An MI355X node with every socket in CPX (or DPX/QPX) mode: sockets x partitions logical
+    GPUs (64 for 8 sockets in CPX), laid out as mi355x_cpx_socket lays out one socket, with
+    node-wide KFD node ids, gpu_ids, render minors and amdgpu_xcp.<n> platform devices."""
+    h = FakeHost(root)
+    h.add_cpu_node(0)
+    buses = [0x72, 0x5A, 0x23, 0xD9, 0xF1, 0xA4, 0x8B, 0x0A]
+    mode = "CPX" if partitions == 8 else {2: "DPX", 4: "QPX"}.get(partitions, "SPX")
+    for s in range(sockets):
+        bus = buses[s % len(buses)] + (s // len(buses))
+        bdf = f"0000:{bus:02x}:00.0"
+        for k in range(partitions):
+            n = s * partitions + k
+            h.add_gpu(1 + n, FakeGpu(gpu_id=41000 + 13 * n, location_id=bus << 8, render_minor=128 + n,
+                                     num_xcc=8 // partitions, compute_partition=mode, memory_partition="NPS4",
+                                     vram_total=309220868096 // 4, unique_id=0xE296A367FEF9A1BE + s,
+                                     dev_node=bdf if k == 0 else f"amdgpu_xcp.{n}"))
+    return h
+
+
 def mi355x_node(root, n_gpus: int = 8) -> FakeHost:
     """An 8-GPU MI355X node (gpu_ids/BDFs shaped like the probe's real values)."""
     h = FakeHost(root)

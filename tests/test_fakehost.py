@@ -1195,6 +1195,56 @@ def test_tick_leveling_moves_extras_off_two_fetch_ticks(native, tmp_path):
     assert max(burnt) <= 1.35 * sum(burnt) / len(burnt), (max(burnt), sum(burnt) / len(burnt))
 
 
+@pytest.mark.parametrize("hz,read_us,want_s,every", [
+    (10, PMC_READ_CPU_US, 0.05, 1),  # 8 x 14 us a round: 15 ms at 0.75 %, no stretch (every tick)
+    (10, 150, 0.2, 2),               # 8 x 150 us: 160 ms -> whole ticks, 200 ms
+    (100, 150, 0.1, 10),             # capped at 2 x counters_min_interval (the windows stay current)
+])
+def test_counter_rounds_follow_cpu_budget(native, tmp_path, hz, read_us, want_s, every):
+    """counters_cpu_budget: a PMC read round costs host CPU per logical GPU (a CPX node has 64),
+    so when the measured round CPU / budget exceeds counters_min_interval the rounds come less
+    often -- in whole ticks, at most half as often -- and the ticks between export the last
+    window.  One CPX socket (8 logical GPUs) on the simulated clock with the PMC read stand-in
+    at its silicon cost and at ~10x that."""
+    import time
+    from kubernetes_gpu_exporter_amd.utils.fakehost import mi355x_cpx_socket
+    h = mi355x_cpx_socket(tmp_path)
+    for g in h.gpus:
+        h.set_metrics(g, gfx=50, accum=1000, num_partition=8)
+    c = native.EngineConfig()
+    c.backend = "sysfs"
+    c.host_root = str(tmp_path)
+    c.interval_s = 1.0 / hz
+    c.sampler_thread = False
+    c.serve_http = False
+    c.series_profile = "full"
+    c.enable_counters = True
+    c.fake_pmc_cost_us = read_us
+    assert c.counters_cpu_budget == pytest.approx(0.0075)
+    e = native.Engine(c)
+    e.start()
+    try:
+        now, per = time.monotonic_ns(), int(1e9 / hz)
+        for _ in range(40):  # the round CPU's EWMA settles
+            now += per
+            e.tick(now)
+        s0 = e.stats()
+        for _ in range(40):
+            now += per
+            e.tick(now)
+        s1 = e.stats()
+        fams = promtext.parse(e.snapshot_text())
+    finally:
+        e.stop()
+    assert s1["counters_round_interval_s"] == pytest.approx(want_s), s1["counters_round_interval_s"]
+    assert s1["counter_rounds"] - s0["counter_rounds"] == 40 // every
+    assert s1["counters_round_cpu_ns"] > 8 * read_us * 1e3 * 0.8
+    assert fams["gpuexp_counters_round_interval_seconds"].samples[0][2] == pytest.approx(want_s)
+    # every partition still exports a current window (the ticks between rounds repeat it)
+    busy = {sm[1]["gpu"] for sm in fams["amd_gpu_mfma_busy_percent"].samples}
+    assert busy == {str(k) for k in range(8)}, busy
+
+
 def test_cpx_partitions_share_one_smu_fetch_per_tick(native, tmp_path):
     """The 8 logical GPUs of a CPX socket read one gpu_metrics table: one SMU fetch per tick
     serves all of them (each decodes its own XCD's slice), instead of eight -- at 382 us of
