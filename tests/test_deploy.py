@@ -244,4 +244,6 @@ def test_helm_args_accepted_by_the_cli():
     assert cfg.to_engine_config(n).metrics_cpu_budget == pytest.approx(Config().to_engine_config(n).metrics_cpu_budget)
     assert Config().to_engine_config(n).metrics_cpu_budget == pytest.approx(0.0075)
     assert n.EngineConfig().metrics_cpu_budget == pytest.approx(0.0075)  # the engine's own default agrees
+    assert cfg.counters_cpu_budget == values["countersCpuBudget"]
+    assert cfg.to_engine_config(n).counters_cpu_budget == pytest.approx(n.EngineConfig().counters_cpu_budget)
     assert cfg.series_profile == values["seriesProfile"] and cfg.enable_counters == values["counters"]
