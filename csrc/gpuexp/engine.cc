@@ -129,15 +129,20 @@ int Engine::counters_interval_ms() const {
 // (counters_interval_ms) is twice that, so a window is never taken for stale.  8 MI355X GPUs at
 // ~15 us per read: 120 us per round -> 16 ms, no change; a CPX node's 64 partitions at that cost:
 // ~0.9 ms per round -> 120 ms, a round every 2nd tick at 10 Hz, every 10th at 100 Hz.
-void Engine::counters_round_done() {
+// The EWMA follows the steady cost, not a stall: a late round (its sync ran out: the wait polls,
+// up to counters_sync_us of CPU) is left out, and a round counts at most 2x the EWMA -- a GPU
+// whose reads queue behind a starved sentinel run for a second must not halve its round rate
+// (MI355X: 8 stalled rounds took the EWMA past 750 us and the windows to 200 ms, session 10).
+void Engine::counters_round_done(bool late) {
   uint64_t c = counters_round_acc_ns_;
   counters_round_acc_ns_ = 0;
   const uint64_t p = counters_->cpu_ns();
   const bool first = counter_rounds_++ == 0;  // (the first round carries the plugin's start-up)
   if (p >= counters_round_plugin_seen_) c += p - counters_round_plugin_seen_;
   counters_round_plugin_seen_ = p;
-  if (first) return;
-  counters_round_cpu_ns_ = counters_round_cpu_ns_ > 0 ? 0.9 * counters_round_cpu_ns_ + 0.1 * double(c) : double(c);
+  if (first || late) return;
+  const double x = counters_round_cpu_ns_ > 0 ? std::min(double(c), 2 * counters_round_cpu_ns_) : double(c);
+  counters_round_cpu_ns_ = counters_round_cpu_ns_ > 0 ? 0.9 * counters_round_cpu_ns_ + 0.1 * x : x;
   const double period = cfg_.interval_s * 1e9, base = cfg_.counters_min_interval_s * 1e9;
   double iv = 0;
   if (cfg_.counters_cpu_budget > 0 && period > 0) {
@@ -730,9 +735,10 @@ void Engine::tick_locked(uint64_t now) {
   // 4: counters: wait (bounded) for this tick's read round; sampled in collect_device
   if (counters_ && round) {
     const uint64_t s0 = thread_cpu_ns();
-    if (!counters_->sync(cfg_.counters_sync_us)) counters_late_ += 1;
+    const bool late = !counters_->sync(cfg_.counters_sync_us);
+    counters_late_ += late;
     counters_round_acc_ns_ += thread_cpu_ns() - s0;
-    counters_round_done();
+    counters_round_done(late);
   }
   ts[5] = mono_ns();
   cs[5] = cpu_mark();

@@ -479,7 +479,7 @@ class Engine {
   // counters_cpu_budget: CPU of the round in flight so far, EWMA per round, current interval
   uint64_t counters_round_acc_ns_ = 0, counter_rounds_ = 0, counters_round_plugin_seen_ = 0;
   double counters_round_cpu_ns_ = 0, counters_round_iv_ns_ = 0;
-  void counters_round_done();
+  void counters_round_done(bool late);
   double counters_round_interval_s() const;  // cfg_.counters_kick with "auto" resolved
   std::string sentinel_status_ = "disabled", counters_status_ = "disabled";
 
