@@ -746,7 +746,19 @@ def main() -> int:
     xgmi_window: dict = {}
     fresh0: dict = {}  # per-GPU fresh gpu_metrics reads at the start of the timed window
     counters0: dict = {}  # exporter self counters at the start of the timed window
+    expo0: dict = {}  # compiled-exposition events (relayouts, ...) and ticks at the window's start
     window_s = [0.0]
+
+    stage0: dict = {}  # per-stage (sum, count) of the tick-time histogram at the window's start
+
+    def stage_sums(fams) -> dict:
+        out: dict = {}
+        for sname, lab, v in fams.get("gpuexp_sample_stage_duration_seconds", promtext.Family("x")).samples:
+            if sname.endswith("_sum"):
+                out.setdefault(lab["stage"], [0.0, 0.0])[0] = v
+            elif sname.endswith("_count"):
+                out.setdefault(lab["stage"], [0.0, 0.0])[1] = v
+        return out
 
     def fresh_reads(fams) -> dict:
         return {lab["gpu"]: v for _, lab, v in promtext.samples(fams, "gpuexp_gpu_metrics_reads_total")
@@ -775,6 +787,11 @@ def main() -> int:
             f0 = last_fams(side)
             fresh0.clear()
             fresh0.update(fresh_reads(f0))
+            stage0.clear()
+            stage0.update(stage_sums(f0))
+            expo0.clear()
+            expo0.update({lab.get("event"): v for _, lab, v in promtext.samples(f0, "gpuexp_exposition_events_total")})
+            expo0.update({"ticks": v for _, _, v in promtext.samples(f0, "gpuexp_ticks_total")})
             for name in ("gpuexp_http_prewake_hits_total", "gpuexp_http_prewake_hits_narrow_total",
                          "gpuexp_scrapes_total"):
                 v = [x for _, _, x in promtext.samples(f0, name)]
@@ -892,13 +909,15 @@ def main() -> int:
         fam_gpu0 = {name: sum(1 for _, lab, _ in fam.samples if lab.get("gpu") == "0")
                     for name, fam in fams.items() if name.startswith("amd_gpu_")
                     and not name.startswith("amd_gpu_process_")}
-        stage_us = {}
-        for sname, lab, v in fams.get("gpuexp_sample_stage_duration_seconds", promtext.Family("x")).samples:
-            if sname.endswith("_sum"):
-                stage_us.setdefault(lab["stage"], [0.0, 0.0])[0] = v
-            elif sname.endswith("_count"):
-                stage_us.setdefault(lab["stage"], [0.0, 0.0])[1] = v
-        stage_us = {k: round(a / c * 1e6, 2) for k, (a, c) in stage_us.items() if c}
+        stage_raw = stage_sums(fams)
+        stage_us = {k: round(a / c * 1e6, 2) for k, (a, c) in stage_raw.items() if c}
+        # the same between the histogram publications around the timed window (published at most
+        # once a second; sum and count come from the same publication): start-up's first renders
+        # (every family laid out) dominate a short run's whole-run mean
+        stage_us_window = {k: round((a - stage0[k][0]) / (c - stage0[k][1]) * 1e6, 2)
+                           for k, (a, c) in stage_raw.items()
+                           if k in stage0 and stage0[k][1] > 0 and c > stage0[k][1]} or None  # (None: not
+        # published before the window -- a warm-up under a second)
         # p50 per stage from the cumulative histogram buckets (upper bound of the median bucket)
         buckets: dict = {}
         for sname, lab, v in fams.get("gpuexp_sample_stage_duration_seconds", promtext.Family("x")).samples:
@@ -1047,6 +1066,7 @@ def main() -> int:
             "xgmi_timed_window": dict({"measured_over_expected_write": None}, **xgmi_window),
             "families_gpu0": {k: v for k, v in sorted(fam_gpu0.items()) if v},
             "sample_stage_mean_us": stage_us,
+            "sample_stage_mean_us_timed_window": stage_us_window,
             "sample_stage_p50_le_us": stage_p50_us,
             "gpu_metrics_reads_gpu0": metrics_reads,
             "device_read_mean_us_per_tick": {k: round(v / ticks[0] * 1e6, 2) for k, v in sorted(dev_parts.items())}
@@ -1071,6 +1091,10 @@ def main() -> int:
             # matches while the layout settled, Huffman code builds
             "exposition_events": {lab.get("event"): int(v) for _, lab, v in
                                   promtext.samples(fams, "gpuexp_exposition_events_total")} or None,
+            # the same over the timed window only (steady state: relayouts should be ~0 a tick)
+            "exposition_events_timed_window": ({k: int(v - expo0[k]) for k, v in
+                                                list(expo_events.items()) + [("ticks", ticks[0] if ticks else 0)]
+                                                if k in expo0} if expo0 else None),
             # KFD process scans over the run: directory listings vs tracked-only reads, and how
             # many processes the node's KFD proc directory holds (other GPUs' included)
             "kfd_proc_scans": {lab.get("kind"): v for _, lab, v in promtext.samples(fams, "gpuexp_kfd_proc_scans_total")}
