@@ -391,6 +391,13 @@ def main() -> int:
     have_gpu = os.path.exists("/dev/kfd") and torch.cuda.device_count() > 0
     backend = args.backend if args.backend != "auto" else ("amdsmi" if have_gpu else "mock")
     tmpdir = tempfile.mkdtemp(prefix="gpuexp-bench-")
+    import atexit
+    import shutil
+    # (at exit: after the exporter child is stopped; back-to-back launches leave nothing behind)
+    atexit.register(shutil.rmtree, tmpdir, True)
+    if rank == 0 and os.environ.get("GPUEXP_RCCL_DIR", "").startswith(
+            os.path.join(tempfile.gettempdir(), "gpuexp-bench-rccl-")):
+        atexit.register(shutil.rmtree, os.environ["GPUEXP_RCCL_DIR"], True)
     pod_map = os.path.join(tmpdir, "podmap.json")
     args.fake_root = os.path.join(tmpdir, "host")
     args.runtime_file = os.path.join(tmpdir, "runtime.yaml") if args.prewake_ab else ""
@@ -405,6 +412,7 @@ def main() -> int:
         if rank == 0:
             with open(args.mock_xgmi_file, "wb") as fh:
                 fh.write(b"\0" * (8 * world * world))
+            atexit.register(lambda f=args.mock_xgmi_file: os.path.exists(f) and os.unlink(f))
     mock_sent: dict = {}  # this rank's pattern bytes per peer so far (mock rehearsal)
 
     def record_mock_traffic(st) -> None:
