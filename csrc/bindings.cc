@@ -724,6 +724,7 @@ PYBIND11_MODULE(_gpuexp, m) {
       .def_readwrite("metrics_max_interval_s", &EngineConfig::metrics_max_interval_s)
       .def_readwrite("fake_metrics_cost_us", &EngineConfig::fake_metrics_cost_us)
       .def_readwrite("fake_pmc_cost_us", &EngineConfig::fake_pmc_cost_us)
+      .def_readwrite("fake_pmc_stalls_us", &EngineConfig::fake_pmc_stalls_us)
       .def_readwrite("fake_sentinel_cost_us", &EngineConfig::fake_sentinel_cost_us)
       .def_readwrite("sampler_thread", &EngineConfig::sampler_thread)
       .def_readwrite("render_when_due", &EngineConfig::render_when_due)

@@ -339,7 +339,8 @@ bool Engine::start(std::string* err) {
   // which the sentinel's first HIP call does.
   if (cfg_.enable_counters && cfg_.fake_pmc_cost_us >= 0 && cfg_.backend != "amdsmi") {
     const bool inline_rounds = cfg_.interval_s > 0 && cfg_.counters_inline;
-    counters_ = make_fake_counters(uint64_t(cfg_.fake_pmc_cost_us), counters_interval_ms(), inline_rounds);
+    counters_ = make_fake_counters(uint64_t(cfg_.fake_pmc_cost_us), counters_interval_ms(), inline_rounds,
+                                   cfg_.fake_pmc_stalls_us);
     std::string e;
     if (!counters_->start(devices_, &e)) {
       counters_status_ = "unavailable: " + e;

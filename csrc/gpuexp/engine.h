@@ -104,6 +104,8 @@ struct EngineConfig {
   // tests / tools/project_cpu.py only (fake_sources.cc): >= 0 runs the real PMC read machine on
   // scripted fake GPUs (counters) or a fake sentinel, burning this much CPU per GPU per read / run
   int fake_pmc_cost_us = -1;
+  // tests only: every fake GPU's PMC queue stands still over these [a, b) windows (us since start)
+  std::vector<std::pair<int64_t, int64_t>> fake_pmc_stalls_us;
   int fake_sentinel_cost_us = -1;
   bool legacy_families = true;         // pod_gpu_memory_usage / docker_gpu_memory_perc_usage
   bool pod_attribution = true;

@@ -53,7 +53,9 @@ class CostPort : public gpuexp_pmc::ReadPort {
 
 class FakeCounters : public CounterSource {
  public:
-  FakeCounters(uint64_t cost_us, int interval_ms, bool inline_rounds) : cost_us_(cost_us) {
+  FakeCounters(uint64_t cost_us, int interval_ms, bool inline_rounds,
+               std::vector<std::pair<int64_t, int64_t>> stalls_us)
+      : cost_us_(cost_us), stalls_us_(std::move(stalls_us)) {
     mc_.interval_ms = interval_ms;
     mc_.inline_rounds = inline_rounds;
     mc_.log = false;
@@ -70,6 +72,7 @@ class FakeCounters : public CounterSource {
     for (size_t i = 0; i < devs.size(); ++i) {
       gpuexp_pmc::FakeScript s;
       s.latency_us = 20;  // a PM4 counter read on MI355X: tens of microseconds
+      s.stalls = stalls_us_;
       ports_.push_back(std::make_unique<CostPort>(std::make_unique<gpuexp_pmc::FakePort>(s, t0, int(i)), cost_us_));
       m_->add(devs[i].queue_enabled ? ports_.back().get() : nullptr, model);
     }
@@ -116,6 +119,7 @@ class FakeCounters : public CounterSource {
 
  private:
   uint64_t cost_us_;
+  std::vector<std::pair<int64_t, int64_t>> stalls_us_;
   gpuexp_pmc::MachineConfig mc_;
   std::unique_ptr<gpuexp_pmc::RoundMachine> m_;
   std::vector<std::unique_ptr<CostPort>> ports_;
@@ -164,8 +168,9 @@ class FakeSentinel : public SentinelSource {
 
 }  // namespace
 
-std::unique_ptr<CounterSource> make_fake_counters(uint64_t cost_us, int interval_ms, bool inline_rounds) {
-  return std::make_unique<FakeCounters>(cost_us, interval_ms, inline_rounds);
+std::unique_ptr<CounterSource> make_fake_counters(uint64_t cost_us, int interval_ms, bool inline_rounds,
+                                                  const std::vector<std::pair<int64_t, int64_t>>& stalls_us) {
+  return std::make_unique<FakeCounters>(cost_us, interval_ms, inline_rounds, stalls_us);
 }
 
 std::unique_ptr<SentinelSource> make_fake_sentinel(uint64_t cost_us) {

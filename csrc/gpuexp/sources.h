@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "gpuexp/device.h"
@@ -86,7 +87,8 @@ std::unique_ptr<CounterSource> make_rocprof_counters(const std::string& plugin_p
 
 // Tests / tools/project_cpu.py (fake_sources.cc): the real PMC read machine over scripted fake
 // GPUs, and a sentinel, each burning `cost_us` of host CPU per GPU per read / run.
-std::unique_ptr<CounterSource> make_fake_counters(uint64_t cost_us, int interval_ms, bool inline_rounds);
+std::unique_ptr<CounterSource> make_fake_counters(uint64_t cost_us, int interval_ms, bool inline_rounds,
+                                                  const std::vector<std::pair<int64_t, int64_t>>& stalls_us = {});
 std::unique_ptr<SentinelSource> make_fake_sentinel(uint64_t cost_us);
 
 // One collective call record written by the RCCL tracer tool into a per-process ring.

@@ -1245,6 +1245,46 @@ def test_counter_rounds_follow_cpu_budget(native, tmp_path, hz, read_us, want_s,
     assert busy == {str(k) for k in range(8)}, busy
 
 
+def test_counter_round_budget_ignores_stalled_reads(native, tmp_path):
+    """A stall is not a cost: a round whose reads are stuck (sync runs out) stays out of the
+    round-CPU average, and no round counts more than twice it.  One CPX socket at the silicon
+    read cost, every fake queue standing still for 0.4 s of real time.  (The fake's ticks come
+    ms apart, so the reads' follow-up polling stays cheap here; the silicon regression -- 8
+    stalled rounds behind a starved sentinel run had halved the round rate -- is
+    tests/test_gpu.py::test_xcc_mfma_busy_calibration's starvation phase.)"""
+    import time
+    from kubernetes_gpu_exporter_amd.utils.fakehost import mi355x_cpx_socket
+    h = mi355x_cpx_socket(tmp_path)
+    for g in h.gpus:
+        h.set_metrics(g, gfx=50, accum=1000, num_partition=8)
+    c = native.EngineConfig()
+    c.backend = "sysfs"
+    c.host_root = str(tmp_path)
+    c.interval_s = 0.1
+    c.sampler_thread = False
+    c.serve_http = False
+    c.series_profile = "full"
+    c.enable_counters = True
+    c.fake_pmc_cost_us = PMC_READ_CPU_US
+    c.fake_pmc_stalls_us = [(300_000, 700_000)]
+    e = native.Engine(c)
+    e.start()
+    t0 = time.monotonic()
+    try:
+        now, ivs = time.monotonic_ns(), []
+        while time.monotonic() - t0 < 1.0:  # through the stall on the real clock (the fake queues')
+            now += 100_000_000
+            e.tick(now)
+            ivs.append(e.stats()["counters_round_interval_s"])
+            time.sleep(0.002)
+        fams = promtext.parse(e.snapshot_text())
+    finally:
+        e.stop()
+    late = fams["gpuexp_counters_late_ticks_total"].samples[0][2]
+    assert late >= 1, late  # the stall made a round late (its reads then move to a rescue queue)
+    assert max(ivs) == pytest.approx(0.05), sorted(set(ivs))  # and the round rate never dropped
+
+
 def test_cpx_partitions_share_one_smu_fetch_per_tick(native, tmp_path):
     """The 8 logical GPUs of a CPX socket read one gpu_metrics table: one SMU fetch per tick
     serves all of them (each decodes its own XCD's slice), instead of eight -- at 382 us of
