@@ -59,9 +59,12 @@ def main() -> int:
                 now += per
                 e.tick(now)
             s0, c0, k = e.stats(), time.thread_time_ns(), int(args.seconds * hz)
+            per_tick = []
             for _ in range(k):
                 now += per
+                t = time.thread_time_ns()
                 e.tick(now)
+                per_tick.append(time.thread_time_ns() - t)
             cpu = (time.thread_time_ns() - c0) / k / 1e3
             s1 = e.stats()
         finally:
@@ -72,7 +75,7 @@ def main() -> int:
         print(f"{hz:g} Hz: tick {cpu:.0f} us ({cpu * hz / 1e4:.2f} % of a core), of which silicon stand-ins "
               f"{fake:.0f} us; SMU fetches per tick {(s1['fresh_reads'] - s0['fresh_reads']) / k:.2f}; "
               f"PMC rounds every {s1['counters_round_interval_s'] * 1e3:.0f} ms "
-              f"({s1['counters_round_cpu_ns'] / 1e3:.0f} us each); {s1['series']} series, {s1['render_bytes']} B body\n    stage us/tick: {stages}", flush=True)
+              f"({s1['counters_round_cpu_ns'] / 1e3:.0f} us each); heaviest tick {max(per_tick) / (sum(per_tick) / k):.2f}x the mean; {s1['series']} series, {s1['render_bytes']} B body\n    stage us/tick: {stages}", flush=True)
     return 0
 
 
