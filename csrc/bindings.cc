@@ -149,6 +149,18 @@ PYBIND11_MODULE(_gpuexp, m) {
     }
     return py::make_tuple(cpu, late);
   }, py::arg("hz"), py::arg("n"), "(thread CPU ns per wake-up, mean lateness ns) of the sampler's timer wait");
+  m.def("counters_round_policy", [](const std::vector<std::pair<double, bool>>& rounds, double budget, double base_s,
+                                     double period_s) {
+    // (round CPU ns, late) per finished round -> (EWMA ns, minimum interval s) after each
+    double ewma = 0, iv = 0;
+    std::vector<std::pair<double, double>> out;
+    for (const auto& r : rounds) {
+      counters_round_policy(r.first, r.second, budget, base_s * 1e9, period_s * 1e9, &ewma, &iv);
+      out.emplace_back(ewma, (iv > 0 ? iv : base_s * 1e9) * 1e-9);
+    }
+    return out;
+  }, py::arg("rounds"), py::arg("budget"), py::arg("base_s"), py::arg("period_s"),
+     "counters_cpu_budget's policy over a sequence of (round CPU ns, late) rounds");
   m.def("set_log_level", [](int lvl) { set_log_level(static_cast<LogLevel>(lvl)); });
   m.def("set_log_json", [](bool json) { set_log_json(json); });
   m.def("log", [](int lvl, const std::string& component, const std::string& msg) {

@@ -133,6 +133,19 @@ int Engine::counters_interval_ms() const {
 // up to counters_sync_us of CPU) is left out, and a round counts at most 2x the EWMA -- a GPU
 // whose reads queue behind a starved sentinel run for a second must not halve its round rate
 // (MI355X: 8 stalled rounds took the EWMA past 750 us and the windows to 200 ms, session 10).
+void counters_round_policy(double round_cpu_ns, bool late, double budget, double base_ns, double period_ns,
+                           double* ewma_ns, double* iv_ns) {
+  if (late) return;
+  const double x = *ewma_ns > 0 ? std::min(round_cpu_ns, 2 * *ewma_ns) : round_cpu_ns;
+  *ewma_ns = *ewma_ns > 0 ? 0.9 * *ewma_ns + 0.1 * x : x;
+  double iv = 0;
+  if (budget > 0 && period_ns > 0) {
+    const double want = std::min(*ewma_ns / budget, 2 * std::max(base_ns, period_ns));
+    if (want > base_ns && want > period_ns) iv = std::max(base_ns, std::ceil(want / period_ns - 1e-6) * period_ns);
+  }
+  *iv_ns = iv;
+}
+
 void Engine::counters_round_done(bool late) {
   uint64_t c = counters_round_acc_ns_;
   counters_round_acc_ns_ = 0;
@@ -140,16 +153,9 @@ void Engine::counters_round_done(bool late) {
   const bool first = counter_rounds_++ == 0;  // (the first round carries the plugin's start-up)
   if (p >= counters_round_plugin_seen_) c += p - counters_round_plugin_seen_;
   counters_round_plugin_seen_ = p;
-  if (first || late) return;
-  const double x = counters_round_cpu_ns_ > 0 ? std::min(double(c), 2 * counters_round_cpu_ns_) : double(c);
-  counters_round_cpu_ns_ = counters_round_cpu_ns_ > 0 ? 0.9 * counters_round_cpu_ns_ + 0.1 * x : x;
-  const double period = cfg_.interval_s * 1e9, base = cfg_.counters_min_interval_s * 1e9;
-  double iv = 0;
-  if (cfg_.counters_cpu_budget > 0 && period > 0) {
-    const double want = std::min(counters_round_cpu_ns_ / cfg_.counters_cpu_budget, 2 * std::max(base, period));
-    if (want > base && want > period) iv = std::max(base, std::ceil(want / period - 1e-6) * period);
-  }
-  counters_round_iv_ns_ = iv;
+  if (first) return;
+  counters_round_policy(double(c), late, cfg_.counters_cpu_budget, cfg_.counters_min_interval_s * 1e9,
+                        cfg_.interval_s * 1e9, &counters_round_cpu_ns_, &counters_round_iv_ns_);
 }
 
 double Engine::counters_round_interval_s() const {

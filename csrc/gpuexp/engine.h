@@ -69,6 +69,12 @@ class ForkJoinPool {
 // host property, not the exporter's: tests/test_fakehost.py charges an MI355X host's figure.
 void timer_wakeup_cost(uint64_t period_ns, int n, uint64_t* cpu_ns, uint64_t* late_ns);
 
+// counters_cpu_budget's policy (engine.cc): one finished read round of `round_cpu_ns` moves the
+// per-round CPU EWMA and sets the rounds' minimum interval (0 = counters_min_interval); a late
+// round leaves both as they are.
+void counters_round_policy(double round_cpu_ns, bool late, double budget, double base_ns, double period_ns,
+                           double* ewma_ns, double* iv_ns);
+
 struct EngineConfig {
   std::string backend = "mock";        // mock | sysfs | amdsmi
   int device_threads = 0;              // 0 = auto (serial), N > 1 = a pool of N reader threads

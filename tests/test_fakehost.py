@@ -1245,6 +1245,33 @@ def test_counter_rounds_follow_cpu_budget(native, tmp_path, hz, read_us, want_s,
     assert busy == {str(k) for k in range(8)}, busy
 
 
+def test_counter_round_policy_follows_steady_cost_not_stalls(native):
+    """counters_cpu_budget's policy on synthetic round costs (10 Hz, base 50 ms, 0.75 %):
+    - 8 whole GPUs at ~120 us a round: no stretch;
+    - a CPX node's 64 partitions at ~0.9 ms a round: every 2nd tick (200 ms, the 2x cap);
+    - the MI355X starvation pattern (session 10): 8 late rounds, then rounds carrying the
+      read follow-up's polling (5 ms each) -- the late ones are left out and each of the
+      others counts at most 2x the average, so the 120 us node keeps its 50 ms rounds;
+    - without those two guards the same sequence would have stretched it."""
+    pol = native.counters_round_policy
+    steady = [(120e3, False)] * 40
+    assert pol(steady, 0.0075, 0.05, 0.1)[-1][1] == pytest.approx(0.05)
+    assert pol([(900e3, False)] * 40, 0.0075, 0.05, 0.1)[-1][1] == pytest.approx(0.2)
+    starve = steady + [(2.5e6, True)] * 8 + [(5e6, False)] * 4 + steady
+    out = pol(starve, 0.0075, 0.05, 0.1)
+    assert max(iv for _, iv in out) == pytest.approx(0.05), out
+    assert max(e for e, _ in out) < 2.0 * 120e3
+    # the unguarded EWMA of the same sequence (what round 6's first cut did) crosses the budget
+    e, peak = 0.0, 0.0
+    for c, _ in starve:
+        e = c if e == 0 else 0.9 * e + 0.1 * c
+        peak = max(peak, e)
+    assert peak / 0.0075 > 0.1  # -> rounds every 200 ms in the middle of the starvation
+    # a real rise is followed, only at most 2x per round: 0.9 ms rounds after 120 us ones
+    rise = pol(steady + [(900e3, False)] * 60, 0.0075, 0.05, 0.1)
+    assert rise[-1][1] == pytest.approx(0.2)
+
+
 def test_counter_round_budget_ignores_stalled_reads(native, tmp_path):
     """A stall is not a cost: a round whose reads are stuck (sync runs out) stays out of the
     round-CPU average, and no round counts more than twice it.  One CPX socket at the silicon
