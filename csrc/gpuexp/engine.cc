@@ -612,8 +612,26 @@ void Engine::tick_locked(uint64_t now) {
   const uint64_t period_ns = cfg_.interval_s > 0 ? uint64_t(cfg_.interval_s * 1e9) : 0;
   const uint64_t ctr_iv = counters_round_iv_ns_ > 0 ? uint64_t(counters_round_iv_ns_)
                                                     : uint64_t(cfg_.counters_min_interval_s * 1e9);
-  auto counters_due = [&](uint64_t t) {
-    return !period_ns || !counters_kick_ns_ || t < counters_kick_ns_ || t - counters_kick_ns_ + period_ns / 2 >= ctr_iv;
+  // Leveling: a round stretched over several ticks (counters_cpu_budget, e.g. a CPX node) is put
+  // off by one tick when that tick is due two or more SMU fetches -- predicted from the tick one
+  // fetch pattern (fetch_ticks_) earlier, since the read goes out before the tick's fetches.  A
+  // put-off round runs on the next tick whatever it carries; windows stay < 2 fallback intervals.
+  auto heavy_ahead = [&](uint64_t tick) {  // `tick`: a tick_index_ value
+    const uint64_t k = uint64_t(fetch_ticks_);
+    if (k < 2 || k >= uint64_t(kFreshHist) || tick <= k) return false;
+    const int f = fresh_hist_[(tick - k) % kFreshHist];
+    return f >= 2 && f < fetch_groups_;
+  };
+  auto counters_due = [&](uint64_t t, uint64_t tick) {
+    if (!period_ns || !counters_kick_ns_ || t < counters_kick_ns_) return true;
+    if (t - counters_kick_ns_ + period_ns / 2 < ctr_iv) return false;
+    if (counters_round_iv_ns_ > 0 && !counters_deferred_ && heavy_ahead(tick)) {
+      counters_deferred_ = true;
+      leveled_ = true;
+      return false;
+    }
+    counters_deferred_ = false;
+    return true;
   };
   // a round's CPU on this thread (kick + sync), for counters_cpu_budget
   auto kick_counters = [&] {
@@ -623,7 +641,8 @@ void Engine::tick_locked(uint64_t now) {
   };
   bool round = kick_end && counters_round_next_;  // kicked at the end of the previous tick
   counters_round_next_ = false;
-  if (counters_ && !kick_late && !kick_end && counters_due(now)) {
+  leveled_ = false;
+  if (counters_ && !kick_late && !kick_end && counters_due(now, tick_index_ + 1)) {
     kick_counters();
     counters_kick_ns_ = now;
     round = true;
@@ -679,9 +698,18 @@ void Engine::tick_locked(uint64_t now) {
   // too, so without it they kept landing on a two-fetch tick (the heaviest tick ~1.5x the mean).
   int fresh_now = 0;
   for (const DevState& st : dstate_) fresh_now += st.cur.ok && !st.cur.metrics_coalesced && !st.cur.metrics_shared;
-  leveled_ = false;
-  const bool heavy_tick = fresh_now >= 2 && fresh_now < fetch_groups_;  // (every group fetched: no lighter tick)
-  if (counters_ && kick_late && counters_due(now)) {
+  // (with the fetches phased over k ticks, "heavy" is relative to the lightest of the last k: a
+  // stretched PMC round -- a CPX node's 64 reads -- weighs as two fetches, so the extras do not
+  // pile onto the one-fetch ticks the rounds were leveled to)
+  const int load_now = fresh_now + (round && counters_round_iv_ns_ > 0 ? 2 : 0);
+  bool heavy_tick = fresh_now >= 2 && fresh_now < fetch_groups_;
+  if (counters_round_iv_ns_ > 0 && fetch_ticks_ >= 2 && fetch_ticks_ < kFreshHist &&
+      tick_index_ >= uint64_t(fetch_ticks_)) {
+    int lo = 255;
+    for (int j = 1; j <= fetch_ticks_; ++j) lo = std::min<int>(lo, load_hist_[(tick_index_ + 1 - uint64_t(j)) % kFreshHist]);
+    heavy_tick = load_now >= 2 && load_now > lo;
+  }  // (every group fetched: no lighter tick)
+  if (counters_ && kick_late && counters_due(now, tick_index_ + 1)) {
     counters_kick_ns_ = now;
     round = true;
     const uint64_t k0 = mono_ns();
@@ -820,7 +848,9 @@ void Engine::tick_locked(uint64_t now) {
     cs[7] = cpu_mark();
   }
   if (!cfg_.state_file.empty() && ts[7] - state_saved_ns_ >= uint64_t(cfg_.state_interval_s * 1e9)) save_state();
-  if (counters_ && kick_end && counters_due(now + period_ns)) {  // next tick's read, completing while we sleep
+  fresh_hist_[tick_index_ % kFreshHist] = uint8_t(std::min(fresh_now, 255));
+  load_hist_[tick_index_ % kFreshHist] = uint8_t(std::min(load_now, 255));
+  if (counters_ && kick_end && counters_due(now + period_ns, tick_index_ + 1)) {  // next tick's read, completing while we sleep
     kick_counters();
     counters_kick_ns_ = now + period_ns;
     counters_round_next_ = true;

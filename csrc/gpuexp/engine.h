@@ -480,6 +480,13 @@ class Engine {
   bool emit_ = true;
   uint64_t tick_index_ = 0;  // ticks so far (render_every_ticks)
   int fetch_groups_ = 0;     // GPUs fetching gpu_metrics on their own (a partitioned socket counts once)
+  // PMC round leveling: the auto fetch policy's ticks per fetch (0: every tick), and each recent
+  // tick's fresh SMU fetches by tick_index_ (the fetch pattern repeats every fetch_ticks_ ticks)
+  int fetch_ticks_ = 0;
+  static constexpr int kFreshHist = 32;
+  uint8_t fresh_hist_[kFreshHist] = {};
+  uint8_t load_hist_[kFreshHist] = {};  // ... and its load: fetches, + 2 for a stretched PMC round
+  bool counters_deferred_ = false;  // the due round was put off by one tick (leveling)
   bool leveled_ = false;        // this tick deferred the sentinel or a KFD listing (tick leveling)
   uint64_t procs_read_ns_ = 0;  // tick time of the last per-process read (process_min_interval_s)
   uint64_t counters_kick_ns_ = 0;  // tick time the last PMC read round was for (counters_min_interval_s)

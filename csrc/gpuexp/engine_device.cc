@@ -290,6 +290,7 @@ void Engine::update_fetch_policy(uint64_t now) {
   }
   const size_t n = size_t(std::max(1, n_groups));
   const int k = period > 0 && cap > 0 ? int(std::lround(cap / period + 0.5)) : 0;  // ticks per fetch
+  fetch_ticks_ = k;
   for (size_t i = 0; i < dstate_.size(); ++i) {
     DevState& st = dstate_[i];
     const double prev = double(st.fetch_cap_ns);

@@ -1312,6 +1312,57 @@ def test_counter_round_budget_ignores_stalled_reads(native, tmp_path):
     assert max(ivs) == pytest.approx(0.05), sorted(set(ivs))  # and the round rate never dropped
 
 
+def test_cpx_node_pmc_rounds_avoid_two_fetch_ticks(native, tmp_path):
+    """A CPX node (8 sockets x 8 partitions) at 10 Hz: the socket fetches come 2,2,1,2,1 per tick
+    and the PMC rounds, stretched by counters_cpu_budget to every 2nd tick, would land on a
+    two-fetch tick every other round (~1.7 ms of stand-ins on one tick).  Leveled, a round due
+    on a tick predicted to carry two fetches goes one tick later: in steady state no tick carries
+    both, and no round is more than one tick late (3 ticks apart at most).  The sentinel run
+    (0.5 s) and the KFD listing then stay off the rounds' ticks too (a stretched round weighs as
+    two fetches), so the heaviest tick's stand-ins are <= 1.45x the mean (1.56x unleveled, with
+    the round on two-fetch ticks).  Simulated clock."""
+    import time
+    from kubernetes_gpu_exporter_amd.utils.fakehost import mi355x_cpx_node
+    h = mi355x_cpx_node(tmp_path, 8, 8)
+    for g in h.gpus:
+        h.set_metrics(g, gfx=50, accum=1000, num_partition=8)
+    c = native.EngineConfig()
+    c.backend = "sysfs"
+    c.host_root = str(tmp_path)
+    c.interval_s = 0.1
+    c.sampler_thread = False
+    c.serve_http = False
+    c.series_profile = "full"
+    c.fake_metrics_cost_us = SMU_FETCH_CPU_US
+    c.enable_counters = True
+    c.fake_pmc_cost_us = PMC_READ_CPU_US
+    c.enable_sentinel = True
+    c.fake_sentinel_cost_us = SENTINEL_RUN_CPU_US
+    e = native.Engine(c)
+    e.start()
+    try:
+        now, rows = time.monotonic_ns(), []
+        s0 = e.stats()
+        for _ in range(60):
+            now += 100_000_000
+            e.tick(now)
+            s1 = e.stats()
+            rows.append((s1["last_tick_fresh"], s1["counter_rounds"] - s0["counter_rounds"],
+                         s1["fake_cpu_burnt_ns"] - s0["fake_cpu_burnt_ns"]))
+            s0 = s1
+        iv = s1["counters_round_interval_s"]
+    finally:
+        e.stop()
+    assert iv == pytest.approx(0.2), iv  # stretched: 64 reads a round
+    steady = rows[30:]
+    assert max(r[0] for r in steady) == 2 and min(r[0] for r in steady) == 1, steady  # 2,2,1,2,1
+    assert not [r for r in steady if r[0] >= 2 and r[1]], steady  # no tick with 2 fetches + a round
+    ticks = [i for i, r in enumerate(steady) if r[1]]
+    assert max(b - a for a, b in zip(ticks, ticks[1:])) <= 3, ticks
+    burnt = [r[2] for r in steady]
+    assert max(burnt) <= 1.45 * sum(burnt) / len(burnt), (max(burnt), sum(burnt) / len(burnt))
+
+
 def test_cpx_partitions_share_one_smu_fetch_per_tick(native, tmp_path):
     """The 8 logical GPUs of a CPX socket read one gpu_metrics table: one SMU fetch per tick
     serves all of them (each decodes its own XCD's slice), instead of eight -- at 382 us of
