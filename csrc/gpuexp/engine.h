@@ -153,7 +153,8 @@ struct EngineConfig {
   // continuous + periodic ticks: the read rounds together may use this share of one core (0 = no
   // cap).  A round's CPU grows with the logical GPUs (a CPX node has 64 PMC reads per round); when
   // the measured round CPU / this share exceeds counters_min_interval_s, rounds come that much less
-  // often, at most half as often (a window never gets older than two round intervals + a tick).
+  // often, at most half as often, and a stretched round may go one tick later to stay off a tick
+  // with two SMU fetches (a window never gets older than the plugin's two fallback intervals).
   double counters_cpu_budget = 0.0075;
   // continuous: when a tick's PMC read goes out.  "start": before the device reads;
   // "after_devices": once the gpu_metrics SMU fetches are done (a PM4 read in flight while
